@@ -1,0 +1,235 @@
+#!/usr/bin/env python
+"""Headline benchmark: Mrows/s of demean + solve at 50M rows x 2 HDFE.
+
+Workload (BASELINE.json configs[2]): synthetic counter-based panel
+(leanfe_amd/synth.py, seed 12345), N = 5e7 rows per GPU, k = 10 regressors,
+FEs with 1e5 and 1e3 levels, vcov = HC1.  One "step" = one full regression on
+device-resident inputs exactly as ``leanfe_hip`` runs it after the data
+hand-off: singleton drop -> alternating projections to convergence
+(tol 1e-6, max_iter 50, check from it=3) -> Gram (MFMA) -> host Cholesky ->
+residual + HC1 meat -> SEs.
+
+Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): one process per
+GPU, rows sharded (rank r generates rows [r*N, (r+1)*N) of the same panel,
+weak scaling), every per-group partial sum / Gram / meat all-reduced with RCCL
+inside the engine.  Timing: W warm-up steps, then barrier + device sync, K
+timed steps, device sync + barrier; the max over ranks is reported.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from leanfe_amd import inference, synth  # noqa: E402
+from leanfe_amd._lib import Engine  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rows", type=int, default=50_000_000, help="rows per GPU")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--levels", type=str, default="100000,1000")
+    ap.add_argument("--vcov", type=str, default="HC1")
+    ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--cpu-rows", type=int, default=2_000_000, help="CPU baseline sample (prefix rows)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def bcast_bytes(self, b: bytes | None) -> bytes:
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def max(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def device_sync(eng: Engine):
+    eng.sync()
+    torch = sys.modules.get("torch")  # only when already imported (multi-GPU runs)
+    if torch is not None and torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def solve_step(eng: Engine, vcov: str):
+    """One regression on device-resident data (the hip backend's hot path)."""
+    n_obs, dims, card = eng.drop_singletons()
+    order = sorted(range(len(card)), key=lambda i: card[i])
+    iterations, _ = eng.demean(order, 1e-6, 50, check_from=3)
+    G = eng.gram()
+    XtX, Xty = inference.split_gram(G)
+    beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
+    k = XtX.shape[0] - 1
+    df_resid = n_obs - (k + 1) - (sum(dims) - len(dims))
+    stats, meat = eng.resid(beta_full, hc1=vcov.lower() == "hc1")
+    if vcov.lower() == "hc1":
+        se = inference.se_hc1(XtX_inv[1:, 1:], meat, n_obs, df_resid)
+    else:
+        se = inference.se_iid(XtX_inv[1:, 1:], stats[0], df_resid)
+    return dict(n_obs=n_obs, iterations=iterations, beta=beta_full[1:], se=se, df_resid=df_resid)
+
+
+def algorithmic_bytes(n: int, p: int, F: int, T: int, hc1: bool) -> dict:
+    """Bytes the engine's passes must move, per kernel and total."""
+    b = {
+        "count_pre": 4 * n * F,
+        "keep": 4 * n * F + n,                       # codes + keep mask write
+        "group_sums": n * (8 * p + 4 * F + 1),       # columns + codes + mask
+        "cross_sums": n * (4 * F + 1),               # per projection: codes + mask
+        "check_sums": n * (8 + 4 * F + 1),           # y + codes + mask
+        "gram_design": n * (8 * p + 4 * F + 1),
+        "gram_resid": n * (8 * p + 4 * F + 1),
+    }
+    return b
+
+
+def cpu_baseline(args, levels):
+    """Oracle (NumPy restatement of polars_impl.py alt_proj) on a prefix sample, 1 thread."""
+    from threadpoolctl import threadpool_limits
+    from oracle import altproj
+    n = args.cpu_rows
+    data = synth.panel(n, args.k, levels, seed=args.seed)
+    xs = [f"x{j + 1}" for j in range(args.k)]
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        r = altproj.fit(data, "y", xs, fes, vcov=args.vcov)
+        dt = time.perf_counter() - t0
+    return dict(value=n / dt / 1e6, unit="Mrows/s", cores=1, kind="port",
+                sample=f"first {n:_} rows of the same panel (k={args.k}, levels={levels}, vcov={args.vcov}), "
+                       f"oracle/altproj.py NumPy, 1 thread, {dt:.2f} s, iterations={r['iterations']}",
+                iterations=int(r["iterations"]), seconds=dt)
+
+
+def main():
+    args = parse()
+    levels = [int(x) for x in args.levels.split(",")]
+    d = Dist()
+    eng = Engine(d.local)
+    if d.world > 1:
+        uid = Engine.unique_id() if d.rank == 0 else None
+        uid = d.bcast_bytes(uid)
+        eng.set_comm(uid, d.rank, d.world)
+    beta = synth.betas(args.k)
+    t0 = time.perf_counter()
+    eng.synth_load(args.rows, args.k, levels, beta, seed=args.seed, row_offset=d.rank * args.rows)
+    gen_s = time.perf_counter() - t0
+
+    for _ in range(args.warmup):
+        solve_step(eng, args.vcov)
+
+    d.barrier()
+    device_sync(eng)
+    eng.profile(True)
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = solve_step(eng, args.vcov)
+    device_sync(eng)
+    t1 = time.perf_counter()
+    d.barrier()
+    elapsed = d.max(t1 - t0)
+    kstats = eng.kernel_stats()
+    eng.profile(False)
+
+    total_rows = args.rows * d.world
+    value = total_rows * args.steps / elapsed / 1e6
+    p = args.k + 1
+    F = len(levels)
+    T = res["iterations"]
+    ab = algorithmic_bytes(args.rows, p, F, T, args.vcov.lower() == "hc1")
+    # dominant kernel = most device time in the timed region
+    dom = max(kstats.items(), key=lambda kv: kv[1][0]) if kstats else ("none", (0.0, 1))
+    dom_name, (dom_ms, dom_launches) = dom
+    per_launch_s = dom_ms / 1e3 / max(dom_launches, 1)
+    dom_bytes = ab.get(dom_name)
+    roofline = None
+    if dom_bytes:
+        achieved = dom_bytes / per_launch_s / 1e9
+        roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                    "bytes_per_launch": dom_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4)}
+    cpu = None
+    if d.rank == 0 and d.world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, levels)
+    if d.rank == 0:
+        line = {
+            "metric": "Mrows/sec demean+solve, 50M x 2-HDFE (1e5/1e3 levels), k=10, HC1",
+            "value": round(value, 2),
+            "unit": "Mrows/s",
+            "n_gpus": d.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (counter-based splitmix64 panel generated on device, seed 12345)",
+            "config": {"workload": "configs[2]: 50M rows/GPU, 2 FE (1e5, 1e3 levels), k=10, HC1 SE",
+                       "rows_per_gpu": args.rows, "total_rows": total_rows, "k": args.k, "levels": levels,
+                       "vcov": args.vcov, "iterations": T, "parallelism": f"row-shard dp{d.world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels_ms": {k: [round(v[0] / args.steps, 4), v[1] // args.steps] for k, v in kstats.items()},
+            "gen_s": round(gen_s, 3),
+        }
+        if args.verbose:
+            line["beta"] = [float(x) for x in res["beta"]]
+            line["se"] = [float(x) for x in res["se"]]
+        print(json.dumps(line))
+    eng.close()
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

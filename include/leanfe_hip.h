@@ -1,0 +1,136 @@
+/* leanfe_hip.h — C ABI of the MI355X (gfx950) fixed-effects demean + solve engine.
+ *
+ * This is the drop-in boundary for leanfe's `strategy='alt_proj'` / `'demean'`
+ * hot path.  The reference has no FFI: its only seam is the backend string
+ * dispatch in `leanfe()` (python/leanfe/leanfe.py:138-184).  Each entry point
+ * below replaces one block of the reference's Polars backend, cited as
+ * (reference file:line).  Python binds it with ctypes (leanfe_amd/_lib.py),
+ * which releases the GIL for every call.
+ *
+ * Conventions
+ *   - return 0 on success, a negative LFE_E* code on failure; lfe_last_error()
+ *     (thread-local) describes the last failure.
+ *   - all host buffers are caller-owned; outputs go to caller-provided buffers.
+ *   - device memory is owned by the context and reused across calls.
+ *   - one context is not thread-safe; use one per host thread.
+ *   - non-convergence is not an error: *iterations_out == max_iter, as in the
+ *     reference (polars_impl.py:526).
+ */
+#ifndef LEANFE_HIP_H
+#define LEANFE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lfe_ctx lfe_ctx;
+
+enum {
+  LFE_OK = 0,
+  LFE_EINVAL = -1, /* bad argument (maps to ValueError) */
+  LFE_EHIP = -2,   /* HIP runtime failure (RuntimeError) */
+  LFE_ERCCL = -3,  /* RCCL failure (RuntimeError) */
+  LFE_ENOMEM = -4, /* device allocation failure (MemoryError) */
+  LFE_ESTATE = -5  /* call out of order (RuntimeError) */
+};
+
+enum { LFE_HOST = 0, LFE_DEVICE = 1 };
+
+/* Context on one GPU (`device` = HIP ordinal).  Owns one HIP stream. */
+int lfe_ctx_create(lfe_ctx** out, int device);
+void lfe_ctx_destroy(lfe_ctx* ctx);
+
+/* Multi-GPU: join an RCCL communicator (one process per GPU).  `unique_id` is
+ * the 128-byte id from lfe_comm_unique_id() on rank 0, broadcast by the caller.
+ * Every reduction below (counts, per-group partial sums, Gram, SE partials)
+ * is then summed over the ranks' row shards. */
+int lfe_comm_unique_id(void* out128);
+int lfe_ctx_set_comm(lfe_ctx* ctx, const void* unique_id128, int rank, int world);
+
+/* Upload one row shard.  cols[0] = y, cols[1..p-1] = x (then instruments),
+ * f64; fe_codes[f] = dense int32 codes in [0, n_levels[f]) (global across
+ * shards); weights may be NULL.  `where` = LFE_HOST or LFE_DEVICE for the
+ * source pointers.  Replaces the data handoff of polars_impl.py:324-356. */
+int lfe_load(lfe_ctx* ctx, int64_t n, int p, const double* const* cols, int F,
+             const int32_t* const* fe_codes, const int32_t* n_levels,
+             const double* weights, int where);
+
+/* Fill the context with rows [row_offset, row_offset+n) of the counter-based
+ * synthetic panel (leanfe_amd/synth.py) directly on the device: p = 1 + k
+ * columns, F = n_fe FE code arrays with n_levels[f] levels. */
+int lfe_synth_load(lfe_ctx* ctx, int64_t n, int k, int n_fe, const int32_t* n_levels,
+                   const double* beta, uint64_t seed, int64_t row_offset);
+
+/* Cluster code arrays for SEs, in the same row order as lfe_load (dense int32
+ * codes, n_levels[j] each).  Subsets/intersections are passed as separate
+ * arrays (std_errors.py:396-408). */
+int lfe_load_clusters(lfe_ctx* ctx, int m, const int32_t* const* cl_codes,
+                      const int32_t* cl_levels, int where);
+
+/* Single-pass singleton drop (polars_impl.py:477-482; :433-435 for 'demean'):
+ * keep a row iff every FE's pre-filter group count is > 1.  Outputs the kept
+ * row count (global over ranks), per-FE distinct levels among kept rows
+ * (fe_dims, :531-534) and pre-filter cardinality (fe_card, :373).  Either
+ * output pointer may be NULL. */
+int lfe_drop_singletons(lfe_ctx* ctx, int64_t* n_kept, int32_t* fe_dims_out,
+                        int32_t* fe_card_out);
+
+/* Alternating projections (polars_impl.py:490-526): for it = 1..max_iter,
+ * project every FE in `fe_order`; from it >= check_from stop when
+ * max_f max_g |mean_g(y)| < tol (y only, unweighted).  check_from <= 0 means
+ * a single projection pass ('demean', polars_impl.py:437-465). */
+int lfe_demean(lfe_ctx* ctx, const int* fe_order, double tol, int max_iter, int check_from,
+               int* iterations_out, double* last_check_out);
+
+/* Gram of [1, y~, x~] (with sqrt(w) row scaling when weighted), p+1 columns,
+ * row-major (p+1)x(p+1), column 0 = intercept, column 1 = y.  Replaces
+ * XtX = X'X, Xty = X'Y of polars_impl.py:165-209. */
+int lfe_gram(lfe_ctx* ctx, double* gram_out);
+
+/* With beta_full = [intercept, beta_1..beta_k] (host Cholesky solve of the
+ * Gram, polars_impl.py:212-225): residual r = y~ - [1, x~] beta_full
+ * (:229) and stats_out[0..3] = {sum w r^2, sum r^2, sum y~, sum y~^2}
+ * (std_errors.py:196-207, polars_impl.py:281-282).  If hc1_meat is non-NULL it
+ * receives the k x k meat sum (w) r^2 x~ x~' (std_errors.py:240-264).
+ * If keep_scores != 0 the per-row scores x~ r (w) are kept on the device for
+ * lfe_cluster_meat. */
+int lfe_resid(lfe_ctx* ctx, const double* beta_full, double* stats_out, double* hc1_meat,
+              int keep_scores);
+
+/* For each loaded cluster array j: S_c = sum_{i in c} x~_i r_i (w_i);
+ * meats_out[j] = S'S (k x k), G_out[j] = number of clusters present among the
+ * kept rows (std_errors.py:317-336, compress.py:929-942 — the W_C'(X.e) SpMM). */
+int lfe_cluster_meat(lfe_ctx* ctx, double* meats_out, int64_t* G_out);
+
+/* Debug/fixtures: copy the demeaned columns (kept rows, device order) to host. */
+int lfe_copy_demeaned(lfe_ctx* ctx, double* const* cols_out, int64_t* n_out);
+
+/* Debug/fixtures: copy the loaded inputs (p columns, F code arrays; input row
+ * order) back to host buffers. */
+int lfe_copy_inputs(lfe_ctx* ctx, double* const* cols_out, int32_t* const* codes_out);
+
+/* Wait for all work queued on the context's stream. */
+int lfe_sync(lfe_ctx* ctx);
+
+/* Per-phase device times (ms) of the last lfe_* calls, measured with HIP
+ * events on the context's stream: [prep, demean, gram, resid, cluster, last_kernel]. */
+int lfe_timings(lfe_ctx* ctx, double* out6);
+
+/* Per-kernel HIP-event timing on the context's stream.  lfe_profile(ctx, 1)
+ * resets and enables it (each launch is bracketed by an event pair; adds no
+ * synchronisation); lfe_kernel_stats() synchronises, folds every pending
+ * pair and returns, per kernel name, total milliseconds and launch count.
+ * `names` receives n_out NUL-terminated names of at most 32 bytes each. */
+int lfe_profile(lfe_ctx* ctx, int enable);
+int lfe_kernel_stats(lfe_ctx* ctx, int max, char* names, double* total_ms, int64_t* launches, int* n_out);
+
+const char* lfe_last_error(void);
+const char* lfe_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LEANFE_HIP_H */

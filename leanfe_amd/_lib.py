@@ -1,0 +1,253 @@
+"""ctypes binding of ``liblfe_hip.so`` (C ABI declared in ``include/leanfe_hip.h``).
+
+ctypes releases the GIL for every foreign call.  The engine is the only
+compute path of the ``hip`` backend: if the shared library is missing or no
+GPU is visible, every entry point raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LEANFE_HIP_LIB") or os.path.join(_HERE, "liblfe_hip.so")
+
+LFE_OK, LFE_EINVAL, LFE_EHIP, LFE_ERCCL, LFE_ENOMEM, LFE_ESTATE = 0, -1, -2, -3, -4, -5
+LFE_HOST, LFE_DEVICE = 0, 1
+
+_i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
+_dp = C.POINTER(C.c_double)
+_vp = C.c_void_p
+
+# name -> (restype, argtypes); must match include/leanfe_hip.h
+SIGNATURES = {
+    "lfe_ctx_create": (C.c_int, [C.POINTER(_vp), C.c_int]),
+    "lfe_ctx_destroy": (None, [_vp]),
+    "lfe_comm_unique_id": (C.c_int, [_vp]),
+    "lfe_ctx_set_comm": (C.c_int, [_vp, _vp, C.c_int, C.c_int]),
+    "lfe_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.POINTER(_vp), C.c_int, C.POINTER(_vp), _i32p, _vp, C.c_int]),
+    "lfe_synth_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, _dp, C.c_uint64, C.c_int64]),
+    "lfe_load_clusters": (C.c_int, [_vp, C.c_int, C.POINTER(_vp), _i32p, C.c_int]),
+    "lfe_drop_singletons": (C.c_int, [_vp, _i64p, _i32p, _i32p]),
+    "lfe_demean": (C.c_int, [_vp, _i32p, C.c_double, C.c_int, C.c_int, _i32p, _dp]),
+    "lfe_gram": (C.c_int, [_vp, _dp]),
+    "lfe_resid": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int]),
+    "lfe_cluster_meat": (C.c_int, [_vp, _dp, _i64p]),
+    "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
+    "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
+    "lfe_sync": (C.c_int, [_vp]),
+    "lfe_timings": (C.c_int, [_vp, _dp]),
+    "lfe_profile": (C.c_int, [_vp, C.c_int]),
+    "lfe_kernel_stats": (C.c_int, [_vp, C.c_int, C.c_char_p, _dp, _i64p, _i32p]),
+    "lfe_last_error": (C.c_char_p, []),
+    "lfe_version": (C.c_char_p, []),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load (once) and type the engine library; raises ImportError if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise ImportError(
+                f"leanfe_amd HIP engine not found at {p}; build it with `python -m leanfe_amd.build`")
+        lib = C.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def _check(rc: int) -> None:
+    if rc == LFE_OK:
+        return
+    msg = (load_library().lfe_last_error() or b"").decode(errors="replace")
+    if rc == LFE_EINVAL:
+        raise ValueError(msg)
+    if rc == LFE_ENOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(f"leanfe HIP engine error {rc}: {msg}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class Engine:
+    """One engine context on one GPU (one HIP stream, optional RCCL comm)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        h = _vp()
+        _check(self._lib.lfe_ctx_create(C.byref(h), int(device)))
+        self._h = h
+        self.device = device
+        self.p = 0
+        self.F = 0
+        self._keep = []  # host arrays that must outlive async copies
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.lfe_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- distributed -------------------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_char * 128)()
+        _check(load_library().lfe_comm_unique_id(C.cast(buf, _vp)))
+        return bytes(buf)
+
+    def set_comm(self, unique_id: bytes | None, rank: int, world: int) -> None:
+        if world > 1:
+            buf = (C.c_char * 128).from_buffer_copy(unique_id)
+            _check(self._lib.lfe_ctx_set_comm(self._h, C.cast(buf, _vp), rank, world))
+        else:
+            _check(self._lib.lfe_ctx_set_comm(self._h, None, 0, 1))
+
+    # -- data --------------------------------------------------------------
+    def load(self, cols: list[np.ndarray], codes: list[np.ndarray], levels: list[int],
+             weights: np.ndarray | None = None) -> None:
+        cols = [np.ascontiguousarray(c, dtype=np.float64) for c in cols]
+        codes = [np.ascontiguousarray(c, dtype=np.int32) for c in codes]
+        n = cols[0].size if cols else 0
+        for a in cols + codes:
+            if a.size != n:
+                raise ValueError("all columns must have the same length")
+        w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
+        cp = (_vp * len(cols))(*[_ptr(c) for c in cols])
+        kp = (_vp * max(len(codes), 1))(*[_ptr(c) for c in codes])
+        lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
+        _check(self._lib.lfe_load(self._h, n, len(cols), cp, len(codes), kp, lv,
+                                  None if w is None else _ptr(w), LFE_HOST))
+        self.p, self.F = len(cols), len(codes)
+
+    def synth_load(self, n: int, k: int, levels: list[int], beta: np.ndarray, seed: int = 12345,
+                   row_offset: int = 0) -> None:
+        lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
+        b = np.ascontiguousarray(beta, dtype=np.float64)
+        if b.size < max(k, 1):
+            b = np.concatenate([b, np.zeros(max(k, 1) - b.size)])
+        _check(self._lib.lfe_synth_load(self._h, int(n), int(k), len(levels), lv,
+                                        b.ctypes.data_as(_dp), C.c_uint64(seed), int(row_offset)))
+        self.p, self.F = k + 1, len(levels)
+
+    def load_clusters(self, codes: list[np.ndarray], levels: list[int]) -> None:
+        codes = [np.ascontiguousarray(c, dtype=np.int32) for c in codes]
+        kp = (_vp * max(len(codes), 1))(*[_ptr(c) for c in codes])
+        lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
+        _check(self._lib.lfe_load_clusters(self._h, len(codes), kp, lv, LFE_HOST))
+        self._ncl = len(codes)
+
+    # -- hot path ----------------------------------------------------------
+    def drop_singletons(self) -> tuple[int, tuple, tuple]:
+        n = C.c_int64()
+        dims = (C.c_int32 * max(self.F, 1))()
+        card = (C.c_int32 * max(self.F, 1))()
+        _check(self._lib.lfe_drop_singletons(self._h, C.byref(n), dims, card))
+        return int(n.value), tuple(int(d) for d in dims[:self.F]), tuple(int(c) for c in card[:self.F])
+
+    def demean(self, order: list[int], tol: float = 1e-6, max_iter: int = 50,
+               check_from: int = 3) -> tuple[int, float]:
+        o = (C.c_int32 * max(len(order), 1))(*order)
+        it = C.c_int32()
+        last = C.c_double()
+        _check(self._lib.lfe_demean(self._h, o, float(tol), int(max_iter), int(check_from),
+                                    C.byref(it), C.byref(last)))
+        return int(it.value), float(last.value)
+
+    def gram(self) -> np.ndarray:
+        m = self.p + 1
+        out = np.zeros((m, m))
+        _check(self._lib.lfe_gram(self._h, out.ctypes.data_as(_dp)))
+        return out
+
+    def resid(self, beta_full: np.ndarray, hc1: bool = False, keep_scores: bool = False):
+        b = np.ascontiguousarray(beta_full, dtype=np.float64)
+        stats = np.zeros(4)
+        k = self.p - 1
+        meat = np.zeros((max(k, 1), max(k, 1))) if hc1 else None
+        _check(self._lib.lfe_resid(self._h, b.ctypes.data_as(_dp), stats.ctypes.data_as(_dp),
+                                   None if meat is None else meat.ctypes.data_as(_dp),
+                                   1 if keep_scores else 0))
+        return stats, (meat[:k, :k] if meat is not None else None)
+
+    def cluster_meat(self) -> tuple[np.ndarray, np.ndarray]:
+        k = self.p - 1
+        m = self._ncl
+        meats = np.zeros(max(m * k * k, 1))
+        G = np.zeros(max(m, 1), dtype=np.int64)
+        _check(self._lib.lfe_cluster_meat(self._h, meats.ctypes.data_as(_dp), G.ctypes.data_as(_i64p)))
+        return meats[:m * k * k].reshape(m, k, k), G[:m]
+
+    def copy_demeaned(self, n: int) -> np.ndarray:
+        out = np.zeros((self.p, n))
+        ptrs = (_vp * self.p)(*[out[j].ctypes.data for j in range(self.p)])
+        nn = C.c_int64()
+        _check(self._lib.lfe_copy_demeaned(self._h, ptrs, C.byref(nn)))
+        return out
+
+    def copy_inputs(self, n: int) -> tuple[np.ndarray, np.ndarray]:
+        cols = np.zeros((self.p, n))
+        codes = np.zeros((max(self.F, 1), n), dtype=np.int32)
+        cp = (_vp * self.p)(*[cols[j].ctypes.data for j in range(self.p)])
+        kp = (_vp * max(self.F, 1))(*[codes[f].ctypes.data for f in range(max(self.F, 1))])
+        _check(self._lib.lfe_copy_inputs(self._h, cp, kp))
+        return cols, codes[:self.F]
+
+    def sync(self) -> None:
+        _check(self._lib.lfe_sync(self._h))
+
+    def profile(self, enable: bool = True) -> None:
+        _check(self._lib.lfe_profile(self._h, 1 if enable else 0))
+
+    def kernel_stats(self) -> dict:
+        """{kernel name: (total ms, launches)} since the last profile(True)."""
+        cap = 64
+        names = C.create_string_buffer(32 * cap)
+        ms = np.zeros(cap)
+        cnt = np.zeros(cap, dtype=np.int64)
+        n = C.c_int32()
+        _check(self._lib.lfe_kernel_stats(self._h, cap, names, ms.ctypes.data_as(_dp),
+                                          cnt.ctypes.data_as(_i64p), C.byref(n)))
+        raw = names.raw
+        out = {}
+        for j in range(n.value):
+            nm = raw[32 * j:32 * j + 32].split(b"\0", 1)[0].decode()
+            out[nm] = (float(ms[j]), int(cnt[j]))
+        return out
+
+    def timings(self) -> dict:
+        t = np.zeros(6)
+        _check(self._lib.lfe_timings(self._h, t.ctypes.data_as(_dp)))
+        return dict(zip(["prep", "demean", "gram", "resid", "cluster", "last"], t.tolist()))
+
+
+def version() -> str:
+    return load_library().lfe_version().decode()

@@ -1,0 +1,576 @@
+// leanfe HIP engine — C ABI (include/leanfe_hip.h), context management, RCCL.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lfe_internal.h"
+
+namespace lfe {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string& msg) { g_err = msg; }
+
+static int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+#define LFE_NCCL(expr)                                                                  \
+  do {                                                                                  \
+    ncclResult_t _r = (expr);                                                           \
+    if (_r != ncclSuccess) return fail(LFE_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+template <typename T>
+static int dalloc(T** p, size_t elems) {
+  *p = nullptr;
+  if (elems == 0) elems = 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * elems);
+  if (e != hipSuccess) {
+    set_error(std::string("hipMalloc(") + std::to_string(sizeof(T) * elems) + " B): " + hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? LFE_ENOMEM : LFE_EHIP;
+  }
+  return LFE_OK;
+}
+
+template <typename T>
+static void dfree(T*& p) {
+  if (p) hipFree(p);
+  p = nullptr;
+}
+
+int ensure_scratch(lfe_ctx* c, size_t elems) {
+  if (c->scratch_elems >= elems) return LFE_OK;
+  dfree(c->scratch);
+  c->scratch_elems = 0;
+  LFE_TRY(dalloc(&c->scratch, elems));
+  c->scratch_elems = elems;
+  return LFE_OK;
+}
+
+int ensure_dred(lfe_ctx* c, size_t elems) {
+  if (c->dred_elems >= elems) return LFE_OK;
+  dfree(c->dred);
+  c->dred_elems = 0;
+  LFE_TRY(dalloc(&c->dred, elems));
+  c->dred_elems = elems;
+  return LFE_OK;
+}
+
+int ensure_iscratch(lfe_ctx* c, size_t elems) {
+  if (c->iscratch_elems >= elems) return LFE_OK;
+  dfree(c->iscratch);
+  c->iscratch_elems = 0;
+  LFE_TRY(dalloc(&c->iscratch, elems));
+  c->iscratch_elems = elems;
+  return LFE_OK;
+}
+
+int ensure_pinned(lfe_ctx* c, size_t elems) {
+  if (c->hpinned_elems >= elems) return LFE_OK;
+  if (c->hpinned) hipHostFree(c->hpinned);
+  c->hpinned = nullptr;
+  c->hpinned_elems = 0;
+  LFE_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hpinned), sizeof(double) * elems, hipHostMallocDefault));
+  c->hpinned_elems = elems;
+  return LFE_OK;
+}
+
+int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count) {
+  if (c->world <= 1 || count == 0) return LFE_OK;
+  LFE_NCCL(ncclAllReduce(dev, dev, count, ncclFloat64, ncclSum, c->comm, c->stream));
+  return LFE_OK;
+}
+
+int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count) {
+  if (c->world <= 1 || count == 0) return LFE_OK;
+  LFE_NCCL(ncclAllReduce(dev, dev, count, ncclInt32, ncclSum, c->comm, c->stream));
+  return LFE_OK;
+}
+
+int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count) {
+  if (c->world <= 1 || count == 0) return LFE_OK;
+  LFE_NCCL(ncclAllReduce(dev, dev, count, ncclFloat64, ncclMax, c->comm, c->stream));
+  return LFE_OK;
+}
+
+FeArgs fe_args(const lfe_ctx* c) {
+  FeArgs a{};
+  a.F = c->F;
+  a.p = c->p;
+  for (int f = 0; f < c->F; ++f) {
+    a.code[f] = c->fe[f].code;
+    a.alpha[f] = c->fe[f].alpha;
+  }
+  return a;
+}
+
+const char* const kKernelNames[K_NUM_KERNELS] = {
+    "count_pre", "keep", "group_sums", "cross_sums", "finalize", "check_sums", "check_max", "gram_design",
+    "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "count_nonzero", "synth"};
+
+static hipEvent_t prof_event(lfe_ctx* c) {
+  if (!c->prof.pool.empty()) {
+    hipEvent_t e = c->prof.pool.back();
+    c->prof.pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+void prof_begin(lfe_ctx* c, int kid) {
+  if (!c->prof.on) return;
+  hipEvent_t e = prof_event(c);
+  if (!e) return;
+  hipEventRecord(e, c->stream);
+  c->prof.open_ev = e;
+  c->prof.open_id = kid;
+}
+
+void prof_end(lfe_ctx* c) {
+  if (!c->prof.on || !c->prof.open_ev) return;
+  hipEvent_t e = prof_event(c);
+  if (!e) return;
+  hipEventRecord(e, c->stream);
+  c->prof.pending.push_back({c->prof.open_id, {c->prof.open_ev, e}});
+  c->prof.open_ev = nullptr;
+  if (c->prof.pending.size() > 4096) prof_fold(c);
+}
+
+int prof_fold(lfe_ctx* c) {
+  if (c->prof.pending.empty()) return LFE_OK;
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  for (auto& r : c->prof.pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.second.first, r.second.second) == hipSuccess) {
+      c->prof.total_ms[r.first] += ms;
+      c->prof.count[r.first] += 1;
+    }
+    c->prof.pool.push_back(r.second.first);
+    c->prof.pool.push_back(r.second.second);
+  }
+  c->prof.pending.clear();
+  return LFE_OK;
+}
+
+static void free_data(lfe_ctx* c) {
+  dfree(c->X);
+  dfree(c->w);
+  dfree(c->keep);
+  dfree(c->scores);
+  for (auto& fe : c->fe) {
+    dfree(fe.code);
+    dfree(fe.cnt_pre);
+    dfree(fe.cnt);
+    dfree(fe.W);
+    dfree(fe.S);
+    dfree(fe.T);
+    dfree(fe.alpha);
+    dfree(fe.R);
+  }
+  c->fe.clear();
+  for (auto& p : c->cl) dfree(p);
+  c->cl.clear();
+  c->cl_levels.clear();
+  c->loaded = c->prepared = c->demeaned = c->scores_valid = false;
+  c->n = c->ld = 0;
+  c->p = c->F = 0;
+}
+
+// allocate all per-shard buffers for (n, p, F, levels)
+static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_levels, bool weighted) {
+  free_data(c);
+  if (p < 1 || p > kMaxCols) return fail(LFE_EINVAL, "p must be in [1, 63] (y plus up to 62 regressors)");
+  if (F < 0 || F > kMaxFE) return fail(LFE_EINVAL, "number of fixed effects must be in [0, 8]");
+  if (n < 0) return fail(LFE_EINVAL, "n must be >= 0");
+  c->n = n;
+  c->ld = (n + 63) / 64 * 64;
+  if (c->ld == 0) c->ld = 64;
+  c->p = p;
+  c->F = F;
+  LFE_TRY(dalloc(&c->X, (size_t)p * c->ld));
+  if (weighted) LFE_TRY(dalloc(&c->w, (size_t)c->ld));
+  LFE_TRY(dalloc(&c->keep, (size_t)c->ld));
+  c->fe.resize(F);
+  for (int f = 0; f < F; ++f) {
+    auto& fe = c->fe[f];
+    if (n_levels[f] < 1) return fail(LFE_EINVAL, "n_levels must be >= 1");
+    fe.G = n_levels[f];
+    LFE_TRY(dalloc(&fe.code, (size_t)c->ld));
+    LFE_TRY(dalloc(&fe.cnt_pre, (size_t)fe.G));
+    LFE_TRY(dalloc(&fe.cnt, (size_t)fe.G));
+    LFE_TRY(dalloc(&fe.W, (size_t)fe.G));
+    LFE_TRY(dalloc(&fe.S, (size_t)fe.G * p));
+    LFE_TRY(dalloc(&fe.T, (size_t)fe.G * p));
+    LFE_TRY(dalloc(&fe.alpha, (size_t)fe.G * p));
+    LFE_TRY(dalloc(&fe.R, (size_t)fe.G));
+  }
+  return LFE_OK;
+}
+
+struct PhaseTimer {
+  lfe_ctx* c;
+  double* slot;
+  PhaseTimer(lfe_ctx* c_, double* s) : c(c_), slot(s) { hipEventRecord(c->ev0, c->stream); }
+  ~PhaseTimer() {
+    hipEventRecord(c->ev1, c->stream);
+    if (hipEventSynchronize(c->ev1) == hipSuccess) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, c->ev0, c->ev1);
+      *slot = ms;
+      c->tm.last = ms;
+    }
+  }
+};
+
+#define LFE_CTX(c)                                                        \
+  do {                                                                    \
+    if (!(c)) return fail(LFE_EINVAL, "null context");                    \
+    LFE_HIP(hipSetDevice((c)->device));                                   \
+  } while (0)
+
+}  // namespace lfe
+
+using namespace lfe;
+
+extern "C" {
+
+const char* lfe_last_error(void) { return g_err.c_str(); }
+
+const char* lfe_version(void) { return "leanfe_amd-hip 0.1.0 (gfx950)"; }
+
+int lfe_ctx_create(lfe_ctx** out, int device) {
+  if (!out) return fail(LFE_EINVAL, "out is null");
+  *out = nullptr;
+  int ndev = 0;
+  LFE_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(LFE_EINVAL, "device ordinal out of range");
+  LFE_HIP(hipSetDevice(device));
+  lfe_ctx* c = new lfe_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess) {
+    delete c;
+    return fail(LFE_EHIP, "stream/event/buffer creation failed");
+  }
+  *out = c;
+  return LFE_OK;
+}
+
+void lfe_ctx_destroy(lfe_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  free_data(c);
+  dfree(c->scratch);
+  dfree(c->dred);
+  dfree(c->iscratch);
+  dfree(c->dbeta);
+  if (c->hpinned) hipHostFree(c->hpinned);
+  if (c->comm) ncclCommDestroy(c->comm);
+  for (auto& r : c->prof.pending) {
+    hipEventDestroy(r.second.first);
+    hipEventDestroy(r.second.second);
+  }
+  for (auto e : c->prof.pool) hipEventDestroy(e);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int lfe_comm_unique_id(void* out128) {
+  if (!out128) return fail(LFE_EINVAL, "out is null");
+  static_assert(sizeof(ncclUniqueId) == 128, "unique id size");
+  ncclUniqueId id;
+  LFE_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(out128, &id, sizeof(id));
+  return LFE_OK;
+}
+
+int lfe_ctx_set_comm(lfe_ctx* c, const void* unique_id128, int rank, int world) {
+  LFE_CTX(c);
+  if (world < 1 || rank < 0 || rank >= world) return fail(LFE_EINVAL, "bad rank/world");
+  if (c->comm) {
+    ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  c->rank = rank;
+  c->world = world;
+  if (world == 1) return LFE_OK;
+  if (!unique_id128) return fail(LFE_EINVAL, "unique id is null");
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id128, sizeof(id));
+  LFE_NCCL(ncclCommInitRank(&c->comm, world, id, rank));
+  return LFE_OK;
+}
+
+int lfe_load(lfe_ctx* c, int64_t n, int p, const double* const* cols, int F, const int32_t* const* fe_codes,
+             const int32_t* n_levels, const double* weights, int where) {
+  LFE_CTX(c);
+  if (where != LFE_HOST && where != LFE_DEVICE) return fail(LFE_EINVAL, "where must be LFE_HOST or LFE_DEVICE");
+  if (n > 0 && (!cols || (F > 0 && (!fe_codes || !n_levels)))) return fail(LFE_EINVAL, "null input pointer");
+  LFE_TRY(alloc_data(c, n, p, F, n_levels, weights != nullptr));
+  const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  for (int j = 0; j < p && n > 0; ++j)
+    LFE_HIP(hipMemcpyAsync(c->X + (size_t)j * c->ld, cols[j], sizeof(double) * n, kind, c->stream));
+  if (weights && n > 0) LFE_HIP(hipMemcpyAsync(c->w, weights, sizeof(double) * n, kind, c->stream));
+  LFE_TRY(ensure_iscratch(c, 16));
+  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
+  for (int f = 0; f < F && n > 0; ++f) {
+    LFE_HIP(hipMemcpyAsync(c->fe[f].code, fe_codes[f], sizeof(int32_t) * n, kind, c->stream));
+    LFE_TRY(launch_validate_codes(c->fe[f].code, n, c->fe[f].G, c->iscratch, c->stream));
+  }
+  int32_t bad = 0;
+  LFE_HIP(hipMemcpyAsync(&bad, c->iscratch, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  if (bad) {
+    free_data(c);
+    return fail(LFE_EINVAL, "FE codes must be dense int32 in [0, n_levels)");
+  }
+  c->loaded = true;
+  return LFE_OK;
+}
+
+int lfe_synth_load(lfe_ctx* c, int64_t n, int k, int n_fe, const int32_t* n_levels, const double* beta,
+                   uint64_t seed, int64_t row_offset) {
+  LFE_CTX(c);
+  if (k < 0 || k + 1 > kMaxCols) return fail(LFE_EINVAL, "k out of range");
+  if (n_fe > 0 && !n_levels) return fail(LFE_EINVAL, "n_levels is null");
+  LFE_TRY(alloc_data(c, n, k + 1, n_fe, n_levels, false));
+  LFE_TRY(launch_synth(c, k, n_levels, beta, seed, row_offset));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  c->loaded = true;
+  return LFE_OK;
+}
+
+int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const int32_t* cl_levels, int where) {
+  LFE_CTX(c);
+  if (!c->loaded) return fail(LFE_ESTATE, "lfe_load must precede lfe_load_clusters");
+  if (m < 0 || (m > 0 && (!cl_codes || !cl_levels))) return fail(LFE_EINVAL, "bad cluster arrays");
+  for (auto& p : c->cl) dfree(p);
+  c->cl.assign(m, nullptr);
+  c->cl_levels.assign(cl_levels, cl_levels + m);
+  const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  LFE_TRY(ensure_iscratch(c, 16));
+  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
+  for (int j = 0; j < m; ++j) {
+    if (cl_levels[j] < 1) return fail(LFE_EINVAL, "cluster n_levels must be >= 1");
+    LFE_TRY(dalloc(&c->cl[j], (size_t)c->ld));
+    if (c->n > 0) {
+      LFE_HIP(hipMemcpyAsync(c->cl[j], cl_codes[j], sizeof(int32_t) * c->n, kind, c->stream));
+      LFE_TRY(launch_validate_codes(c->cl[j], c->n, cl_levels[j], c->iscratch, c->stream));
+    }
+  }
+  int32_t bad = 0;
+  LFE_HIP(hipMemcpyAsync(&bad, c->iscratch, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  if (bad) return fail(LFE_EINVAL, "cluster codes must be dense int32 in [0, n_levels)");
+  return LFE_OK;
+}
+
+int lfe_drop_singletons(lfe_ctx* c, int64_t* n_kept, int32_t* fe_dims_out, int32_t* fe_card_out) {
+  LFE_CTX(c);
+  if (!c->loaded) return fail(LFE_ESTATE, "lfe_load first");
+  {
+    PhaseTimer t(c, &c->tm.prep);
+    LFE_TRY(launch_count_pre(c));
+    for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt_pre, c->fe[f].G));
+    LFE_TRY(launch_keep(c));
+    for (int f = 0; f < c->F; ++f) {
+      LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt, c->fe[f].G));
+      LFE_TRY(allreduce_sum_f64(c, c->fe[f].W, c->fe[f].G));
+    }
+    int32_t dims[kMaxFE] = {0}, card[kMaxFE] = {0};
+    if (c->F) LFE_TRY(launch_count_dims(c, dims, card));
+    for (int f = 0; f < c->F; ++f) {
+      c->fe[f].dims = dims[f];
+      c->fe[f].card = card[f];
+      if (fe_dims_out) fe_dims_out[f] = dims[f];
+      if (fe_card_out) fe_card_out[f] = card[f];
+    }
+    // kept rows (global): for F == 0 every row is kept; else sum of counts of FE 0
+    int64_t kept = 0;
+    if (c->F == 0) {
+      kept = c->n;
+      if (c->world > 1) {
+        LFE_TRY(ensure_dred(c, 1));
+        double v = (double)kept;
+        LFE_HIP(hipMemcpyAsync(c->dred, &v, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        LFE_TRY(allreduce_sum_f64(c, c->dred, 1));
+        LFE_HIP(hipMemcpyAsync(&v, c->dred, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        LFE_HIP(hipStreamSynchronize(c->stream));
+        kept = (int64_t)v;
+      }
+    } else {
+      std::vector<int32_t> h(c->fe[0].G);
+      LFE_HIP(hipMemcpyAsync(h.data(), c->fe[0].cnt, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, c->stream));
+      LFE_HIP(hipStreamSynchronize(c->stream));
+      for (int32_t v : h) kept += v;
+    }
+    c->n_kept = kept;
+    if (n_kept) *n_kept = kept;
+  }
+  if (c->F == 0) LFE_HIP(hipMemsetAsync(c->keep, 1, (size_t)c->ld, c->stream));
+  c->prepared = true;
+  c->demeaned = false;
+  return LFE_OK;
+}
+
+int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int check_from, int* iterations_out,
+               double* last_check_out) {
+  LFE_CTX(c);
+  if (!c->prepared) return fail(LFE_ESTATE, "lfe_drop_singletons first");
+  std::vector<int> order(c->F);
+  for (int f = 0; f < c->F; ++f) order[f] = fe_order ? fe_order[f] : f;
+  {
+    std::vector<int> chk(order);
+    std::sort(chk.begin(), chk.end());
+    for (int f = 0; f < c->F; ++f)
+      if (chk[f] != f) return fail(LFE_EINVAL, "fe_order must be a permutation of 0..F-1");
+  }
+  int iterations = 0;
+  double last = -1.0;
+  {
+    PhaseTimer t(c, &c->tm.demean);
+    for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
+    if (c->F > 0) {
+      LFE_TRY(launch_group_sums(c));
+      if (check_from <= 0) {
+        // single within-transform pass ('demean' strategy, polars_impl.py:437-465)
+        for (int f : order) {
+          LFE_TRY(launch_cross_sums(c, f));
+          LFE_TRY(launch_finalize(c, f));
+        }
+        iterations = 1;
+      } else {
+        if (max_iter < 1) return fail(LFE_EINVAL, "max_iter must be >= 1");
+        for (int it = 1; it <= max_iter; ++it) {
+          for (int f : order) {
+            LFE_TRY(launch_cross_sums(c, f));
+            LFE_TRY(launch_finalize(c, f));
+          }
+          iterations = it;
+          if (it >= check_from) {
+            LFE_TRY(launch_check(c, &last));
+            if (last < tol) break;
+          }
+        }
+      }
+    }
+  }
+  if (iterations_out) *iterations_out = iterations;
+  if (last_check_out) *last_check_out = last;
+  c->demeaned = true;
+  return LFE_OK;
+}
+
+int lfe_gram(lfe_ctx* c, double* gram_out) {
+  LFE_CTX(c);
+  if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
+  if (!gram_out) return fail(LFE_EINVAL, "gram_out is null");
+  PhaseTimer t(c, &c->tm.gram);
+  return launch_gram(c, gram_out);
+}
+
+int lfe_resid(lfe_ctx* c, const double* beta_full, double* stats_out, double* hc1_meat, int keep_scores) {
+  LFE_CTX(c);
+  if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
+  if (!beta_full || !stats_out) return fail(LFE_EINVAL, "null pointer");
+  if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)(c->p - 1) * c->ld));
+  PhaseTimer t(c, &c->tm.resid);
+  return launch_resid(c, beta_full, stats_out, hc1_meat, keep_scores);
+}
+
+int lfe_cluster_meat(lfe_ctx* c, double* meats_out, int64_t* G_out) {
+  LFE_CTX(c);
+  if (!c->scores_valid) return fail(LFE_ESTATE, "lfe_resid(keep_scores=1) first");
+  if (!meats_out || !G_out) return fail(LFE_EINVAL, "null pointer");
+  PhaseTimer t(c, &c->tm.cluster);
+  return launch_cluster(c, meats_out, G_out);
+}
+
+int lfe_copy_demeaned(lfe_ctx* c, double* const* cols_out, int64_t* n_out) {
+  LFE_CTX(c);
+  if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
+  double* d = nullptr;
+  LFE_TRY(dalloc(&d, (size_t)c->p * std::max<int64_t>(c->n, 1)));
+  int rc = launch_copy_demeaned(c, d);
+  if (rc == LFE_OK) {
+    for (int j = 0; j < c->p && c->n > 0; ++j)
+      if (hipMemcpyAsync(cols_out[j], d + (size_t)j * c->n, sizeof(double) * c->n, hipMemcpyDeviceToHost,
+                         c->stream) != hipSuccess)
+        rc = fail(LFE_EHIP, "copy out failed");
+    hipStreamSynchronize(c->stream);
+  }
+  dfree(d);
+  if (n_out) *n_out = c->n;
+  return rc;
+}
+
+int lfe_copy_inputs(lfe_ctx* c, double* const* cols_out, int32_t* const* codes_out) {
+  LFE_CTX(c);
+  if (!c->loaded) return fail(LFE_ESTATE, "nothing loaded");
+  for (int j = 0; j < c->p && c->n > 0 && cols_out; ++j)
+    LFE_HIP(hipMemcpyAsync(cols_out[j], c->X + (size_t)j * c->ld, sizeof(double) * c->n, hipMemcpyDeviceToHost,
+                           c->stream));
+  for (int f = 0; f < c->F && c->n > 0 && codes_out; ++f)
+    LFE_HIP(hipMemcpyAsync(codes_out[f], c->fe[f].code, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  return LFE_OK;
+}
+
+int lfe_sync(lfe_ctx* c) {
+  LFE_CTX(c);
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  return LFE_OK;
+}
+
+int lfe_profile(lfe_ctx* c, int enable) {
+  LFE_CTX(c);
+  LFE_TRY(prof_fold(c));
+  for (int k = 0; k < K_NUM_KERNELS; ++k) {
+    c->prof.total_ms[k] = 0;
+    c->prof.count[k] = 0;
+  }
+  c->prof.on = enable != 0;
+  return LFE_OK;
+}
+
+int lfe_kernel_stats(lfe_ctx* c, int max, char* names, double* total_ms, int64_t* launches, int* n_out) {
+  LFE_CTX(c);
+  LFE_TRY(prof_fold(c));
+  int n = 0;
+  for (int k = 0; k < K_NUM_KERNELS && n < max; ++k) {
+    if (c->prof.count[k] == 0) continue;
+    if (names) {
+      std::strncpy(names + 32 * n, kKernelNames[k], 31);
+      names[32 * n + 31] = 0;
+    }
+    if (total_ms) total_ms[n] = c->prof.total_ms[k];
+    if (launches) launches[n] = c->prof.count[k];
+    ++n;
+  }
+  if (n_out) *n_out = n;
+  return LFE_OK;
+}
+
+int lfe_timings(lfe_ctx* c, double* out6) {
+  if (!c || !out6) return fail(LFE_EINVAL, "null pointer");
+  out6[0] = c->tm.prep;
+  out6[1] = c->tm.demean;
+  out6[2] = c->tm.gram;
+  out6[3] = c->tm.resid;
+  out6[4] = c->tm.cluster;
+  out6[5] = c->tm.last;
+  return LFE_OK;
+}
+
+}  // extern "C"

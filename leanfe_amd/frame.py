@@ -1,0 +1,147 @@
+"""Host-side data preparation for the HIP backend.
+
+Replaces the Polars data handling in front of the reference's hot path:
+column selection (polars_impl.py:324-347), categorical -> integer codes
+(``_cats_to_int``, :118-139), factor/interaction expansion (:27-115) and the
+hand-off of NumPy columns to the engine.  Accepted inputs: a mapping of
+array-likes, a pandas DataFrame, a pyarrow Table, a Parquet path, or a Polars
+DataFrame/LazyFrame when ``polars`` is importable.
+"""
+from __future__ import annotations
+
+from collections.abc import Mapping
+
+import numpy as np
+
+
+def get_columns(data, names: list[str]) -> dict[str, np.ndarray]:
+    names = list(dict.fromkeys(names))
+    if isinstance(data, str):
+        import pyarrow.parquet as pq
+        t = pq.read_table(data, columns=names)
+        return {c: _arrow_to_numpy(t.column(c)) for c in names}
+    mod = type(data).__module__
+    if mod.startswith("polars"):
+        df = data.select(names)
+        if hasattr(df, "collect"):
+            df = df.collect()
+        return {c: _polars_to_numpy(df[c]) for c in names}
+    if mod.startswith("pyarrow"):
+        return {c: _arrow_to_numpy(data.column(c)) for c in names}
+    if mod.startswith("pandas"):
+        out = {}
+        for c in names:
+            s = data[c]
+            if str(s.dtype) == "category":
+                out[c] = np.asarray(s.cat.codes.to_numpy(), dtype=np.int64)
+            else:
+                out[c] = s.to_numpy()
+        return out
+    if isinstance(data, Mapping) or hasattr(data, "__getitem__"):
+        missing = [c for c in names if c not in data]
+        if missing:
+            raise ValueError(f"columns not found in data: {missing}")
+        return {c: np.asarray(data[c]) for c in names}
+    raise TypeError(f"unsupported data type: {type(data)!r}")
+
+
+def _arrow_to_numpy(col) -> np.ndarray:
+    import pyarrow as pa
+    if pa.types.is_dictionary(col.type):
+        col = col.combine_chunks()
+        return np.asarray(col.indices.to_numpy(zero_copy_only=False), dtype=np.int64)
+    return col.to_numpy()
+
+
+def _polars_to_numpy(s) -> np.ndarray:
+    if str(s.dtype) in ("Categorical", "Enum"):
+        return s.to_physical().to_numpy()
+    return s.to_numpy()
+
+
+def factorize(values) -> tuple[np.ndarray, int]:
+    """Dense int32 group codes and the number of code values.
+
+    Non-negative integer columns whose maximum is below max(4n, 2^20) are used
+    as codes directly (O(n); unused code values are empty groups, which every
+    kernel ignores).  Anything else (strings, floats, sparse ids) goes through
+    a sorted unique.  Only group membership matters for the estimator."""
+    v = np.asarray(values)
+    n = v.size
+    if n == 0:
+        return np.zeros(0, dtype=np.int32), 1
+    if np.issubdtype(v.dtype, np.integer) or v.dtype == np.bool_:
+        vmin, vmax = int(v.min()), int(v.max())
+        if vmin >= 0 and vmax < max(4 * n, 1 << 20) and vmax < 2 ** 31 - 1:
+            return v.astype(np.int32, copy=False), vmax + 1
+    uniq, inv = np.unique(v, return_inverse=True)
+    return inv.astype(np.int32).ravel(), int(uniq.size)
+
+
+def intersect(codes: list[np.ndarray], levels: list[int]) -> tuple[np.ndarray, int]:
+    """Composite-key codes for ``group_by([c1, c2, ...])`` (std_errors.py:399-408)."""
+    if len(codes) == 1:
+        return codes[0], levels[0]
+    key = codes[0].astype(np.int64)
+    span = levels[0]
+    for c, g in zip(codes[1:], levels[1:]):
+        if span * g < 2 ** 62:
+            key = key * g + c
+            span = span * g
+        else:
+            key, span = _dense(key)
+            key = key.astype(np.int64) * g + c
+            span = span * g
+    if span < max(4 * key.size, 1 << 20):
+        return key.astype(np.int32), int(span)
+    return _dense(key)
+
+
+def _dense(key: np.ndarray) -> tuple[np.ndarray, int]:
+    uniq, inv = np.unique(key, return_inverse=True)
+    return inv.astype(np.int32).ravel(), int(uniq.size)
+
+
+def _coerce_ref(ref, categories):
+    if ref is None:
+        return categories[0]
+    if len(categories) and not isinstance(categories[0], type(ref)):
+        try:
+            return type(categories[0])(ref)
+        except (ValueError, TypeError):
+            return ref
+    return ref
+
+
+def expand_interactions(cols: dict[str, np.ndarray], interactions) -> list[str]:
+    """``var:i(factor)`` -> var * (factor == cat) for cat != ref (polars_impl.py:72-115)."""
+    names = []
+    for var, factor, ref in interactions:
+        cats = np.unique(cols[factor])
+        ref_cat = _coerce_ref(ref, cats)
+        if ref_cat not in cats:
+            raise ValueError(f"Reference category '{ref}' not found in {factor}. Available: {list(cats)}")
+        for cat in cats:
+            if cat == ref_cat:
+                continue
+            name = f"{var}_{cat}"
+            cols[name] = np.asarray(cols[var], dtype=np.float64) * (cols[factor] == cat)
+            names.append(name)
+    return names
+
+
+def expand_factors(cols: dict[str, np.ndarray], factor_vars) -> list[str]:
+    """``i(var)`` -> dummies (var == cat) for cat != ref (polars_impl.py:27-69)."""
+    names = []
+    for var, ref in factor_vars:
+        cats = np.unique(cols[var])
+        ref_cat = _coerce_ref(ref, cats)
+        if ref_cat not in cats:
+            raise ValueError(f"Reference category '{ref}' not found in {var}. Available: {list(cats)}")
+        for cat in cats:
+            if cat == ref_cat:
+                continue
+            name = f"{var}_{cat}"
+            cols[name] = (cols[var] == cat).astype(np.float64)
+            names.append(name)
+    return names

@@ -1,0 +1,193 @@
+"""``backend="hip"``: the reference's ``leanfe_polars`` control flow
+(python/leanfe/polars_impl.py:287-579) driving the gfx950 engine.
+
+Host side: formula parsing, column selection, categorical -> int32 codes,
+factor/interaction expansion and strategy choice (all cheap, O(n) or less).
+Device side (``liblfe_hip.so`` through ctypes): singleton drop, alternating
+projections to convergence, Gram, residuals and SE reductions.  Host again:
+the (k+1)^2 Cholesky solve and k x k sandwich products (leanfe_amd.inference).
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+
+from . import frame, inference
+from ._lib import Engine
+from .formula import parse_formula
+from .result import LeanFEResult
+from .strategy import DEFAULT_MAX_FE_LEVELS, determine_strategy, estimate_compression_ratio
+
+MAX_FE_LEVELS = DEFAULT_MAX_FE_LEVELS  # polars_impl.py:24
+_VERBOSE = os.environ.get("LEANFE_HIP_VERBOSE", "0") not in ("", "0")
+
+
+def _default_device() -> int:
+    return int(os.environ.get("LOCAL_RANK", os.environ.get("LEANFE_HIP_DEVICE", "0")))
+
+
+def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols: list[str] | None = None,
+               fe_cols: list[str] | None = None, formula: str | None = None, strategy: str = "auto",
+               weights: str | None = None, max_iter: int = 50, vcov: str = "iid",
+               cluster_cols: list[str] | None = None, ssc: bool = True, sample_frac: float | None = None,
+               device: int | None = None, engine: Engine | None = None, quiet: bool = False) -> LeanFEResult:
+    """Fixed-effects OLS on the MI355X engine; arguments as ``leanfe_polars``.
+
+    ``vcov`` accepts 'iid', 'HC1' (or 'hc1') and 'cluster'.  ``engine`` lets a
+    caller reuse an ``Engine`` (e.g. one joined to an RCCL communicator with
+    ``leanfe_amd.dist.attach``: every rank then passes its own row shard and
+    gets the global fit; FE/cluster columns must then be global int codes)."""
+    t_start = time.perf_counter()
+    say = (lambda *a: None) if quiet else print
+    if formula is not None:
+        y_col, x_cols, fe_cols, factor_vars, interactions, instruments = parse_formula(formula)
+    elif y_col is None or x_cols is None or fe_cols is None:
+        raise ValueError("Must provide either 'formula' or (y_col, x_cols, fe_cols)")
+    else:
+        factor_vars, interactions, instruments = [], [], []
+    if instruments:
+        raise NotImplementedError("IV/2SLS is not on the hip backend's hot path (SURVEY.md §8f)")
+    x_cols = list(x_cols)
+    fe_cols = list(fe_cols) if fe_cols is not None else []
+    v = vcov.lower()
+    if v not in ("iid", "hc1", "cluster"):
+        raise ValueError(f"Unknown vcov type: {vcov}")
+    if v == "cluster" and cluster_cols is None:
+        raise ValueError("cluster_cols required for vcov='cluster'")
+
+    needed = [y_col] + x_cols + fe_cols
+    for var, _ in factor_vars:
+        needed.append(var)
+    for var, fac, _ in interactions:
+        needed += [var, fac]
+    if cluster_cols is not None:
+        needed += list(cluster_cols)
+    if weights is not None:
+        needed.append(weights)
+    cols = frame.get_columns(data, needed)
+
+    if interactions:
+        x_cols = x_cols + frame.expand_interactions(cols, interactions)
+    if sample_frac is not None:
+        n0 = len(cols[y_col])
+        idx = np.sort(np.random.default_rng(42).choice(n0, size=int(round(n0 * sample_frac)), replace=False))
+        cols = {c: np.asarray(a)[idx] for c, a in cols.items()}
+    if factor_vars:
+        x_cols = x_cols + frame.expand_factors(cols, factor_vars)
+
+    codes, levels = [], []
+    for fe in fe_cols:
+        c, g = frame.factorize(cols[fe])
+        codes.append(c)
+        levels.append(g)
+    Y = np.asarray(cols[y_col], dtype=np.float64)
+    Xc = [np.asarray(cols[c], dtype=np.float64) for c in x_cols]
+    w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
+
+    own_engine = engine is None
+    eng = engine if engine is not None else Engine(_default_device() if device is None else device)
+    try:
+        t0 = time.perf_counter()
+        eng.load([Y] + Xc, codes, levels, w)
+        t_load = time.perf_counter() - t0
+        n_obs, fe_dims, fe_card = eng.drop_singletons()
+        fe_cardinality = dict(zip(fe_cols, fe_card))
+
+        est_comp_ratio = None
+        if strategy == "auto":
+            est_comp_ratio = estimate_compression_ratio([cols[c] for c in x_cols + fe_cols])
+            n_initial = Y.size
+            if not fe_cols:
+                inferred = "ols"
+            elif len(fe_cols) == 1:
+                inferred = "demean"
+            else:
+                inferred = determine_strategy(vcov, False, fe_cardinality, max_fe_levels=MAX_FE_LEVELS,
+                                              n_obs=n_initial, n_x_cols=len(x_cols),
+                                              estimated_compression_ratio=est_comp_ratio)
+            say(f"Auto selection: Inferring {inferred} strategy. N = {n_initial:_}, "
+                f"est. compression ratio: {est_comp_ratio}")
+            strategy = inferred
+        if strategy == "compress":
+            if not fe_cols:
+                strategy = "ols"
+            else:
+                say("hip backend: 'compress' (YOCO) is not on the device path; "
+                    "running alternating projections for the same estimator")
+                strategy = "alt_proj" if len(fe_cols) > 1 else "demean"
+
+        if strategy == "demean":
+            if len(fe_cols) != 1:
+                raise ValueError("Strategy 'demean' requires exactly one FE column.")
+            say("Using simple within-transform (demean) strategy for single FE...")
+            iterations, _ = eng.demean([0], demean_tol, max_iter, check_from=0)
+            absorbed_df = fe_dims[0] - 1
+        elif strategy == "alt_proj":
+            if not fe_cols:
+                raise ValueError("Strategy 'alt_proj' requires FE-cols. "
+                                 "Use strategy='ols' instead for OLS without FE.")
+            say("Using FWL/alternating projections strategy...")
+            order = sorted(range(len(fe_cols)), key=lambda i: fe_card[i])  # polars_impl.py:485
+            iterations, _ = eng.demean(order, demean_tol, max_iter, check_from=3)
+            absorbed_df = sum(fe_dims) - len(fe_cols)
+        elif strategy == "ols":
+            if fe_cols:
+                raise ValueError("Strategy 'ols' takes no fixed effects")
+            say("Using simple OLS strategy (no fixed effects)...")
+            iterations, _ = eng.demean([], demean_tol, max_iter, check_from=0)
+            iterations, absorbed_df, fe_dims = 0, 0, None
+        else:
+            raise ValueError(f"Unknown strategy: {strategy}")
+
+        k = len(x_cols)
+        G = eng.gram()
+        XtX, Xty = inference.split_gram(G)
+        beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
+        beta = beta_full[1:]
+        df_resid = n_obs - (k + 1) - absorbed_df
+        Vb = XtX_inv[1:, 1:]
+        stats, meat = eng.resid(beta_full, hc1=(v == "hc1"), keep_scores=(v == "cluster"))
+        rss_w, rss, sum_y, sum_y2 = stats
+        n_clusters = None
+        if v == "iid":
+            se = inference.se_iid(Vb, rss_w, df_resid)
+        elif v == "hc1":
+            se = inference.se_hc1(Vb, meat, n_obs, df_resid)
+        else:
+            cl_codes, cl_levels = [], []
+            for c in cluster_cols:
+                cc, gg = frame.factorize(cols[c])
+                cl_codes.append(cc)
+                cl_levels.append(gg)
+            if len(cluster_cols) == 1:
+                eng.load_clusters(cl_codes, cl_levels)
+                meats, Gs = eng.cluster_meat()
+                se, n_clusters = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, ssc)
+            else:
+                subsets = inference.cluster_subsets(len(cluster_cols))
+                arrs, lv = [], []
+                for s in subsets:
+                    a, g = frame.intersect([cl_codes[j] for j in s], [cl_levels[j] for j in s])
+                    arrs.append(a)
+                    lv.append(g)
+                eng.load_clusters(arrs, lv)
+                meats, Gs = eng.cluster_meat()
+                se, n_clusters = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets,
+                                                               n_obs, df_resid, ssc)
+        tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
+        r_squared = 1 - rss / tss if tss > 0 else None
+        timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
+        if _VERBOSE:
+            print(f"[leanfe_amd] iterations={iterations} device ms: {timings}")
+    finally:
+        if own_engine:
+            eng.close()
+
+    return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta))),
+                        std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
+                        iterations=iterations, vcov_type=vcov, is_iv=False, n_instruments=None,
+                        n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
+                        fe_dims=fe_dims, r_squared=r_squared, compression_ratio=est_comp_ratio,
+                        rss=rss, tss=tss, backend="hip", timings=timings)

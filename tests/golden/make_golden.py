@@ -1,0 +1,260 @@
+"""Generate the golden fixtures in tests/golden/*.npz — run in the build container only.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What is pinned and how
+----------------------
+The reference's Polars hot path (polars_impl.py:468-537) cannot run here: the
+``polars`` wheel is absent (an ordinary ModuleNotFoundError, not a permission
+denial).  Its NumPy/SciPy-only modules CAN run when ``polars`` / ``duckdb`` are
+replaced by name-only stub modules, because they only use those names in type
+annotations and ``isinstance`` checks.  This script loads, read-only and with
+bytecode writing disabled, ``result.py``, ``common.py``, ``compress.py`` and
+``std_errors.py`` from /root/reference/python/leanfe and uses:
+
+* ``compress.build_design_matrix`` + ``compress.solve_wls`` on the UNcompressed
+  rows (one "group" per row, weight 1): the exact least-squares-dummy-variable
+  (LSDV) solution that alternating projections converge to.  Golden ``beta``.
+* ``compress.compute_rss_grouped`` + ``compress.CompressionContext`` +
+  ``compress.compute_se_compress``: IID, HC1 and one/multi-way clustered SEs of
+  that LSDV fit (for the x block, equal to the FWL sandwich).  Golden ``se``.
+
+``df_resid`` and ``n_obs`` are passed in following polars_impl.py:532-537
+(n - (k+1) - absorbed_df after the single-pass singleton drop), which is what
+the alt_proj path reports.
+
+The oracle (oracle/altproj.py) is then run (a) at a tight tolerance, where it
+must agree with the golden LSDV beta/SE to 1e-9, and (b) at the reference's
+default tolerance (1e-6, max_iter 50), whose outputs (iterations, beta, SE) are
+stored as ``oracle_*`` for the GPU parity tests.  Inputs and outputs only —
+no reference source — go into the .npz files.
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_PKG = "/root/reference/python/leanfe"
+sys.path.insert(0, REPO)
+
+from oracle import altproj  # noqa: E402
+from leanfe_amd import synth  # noqa: E402
+
+
+def load_reference():
+    """Import the reference's NumPy-only modules behind name-only stubs."""
+    pl = types.ModuleType("polars")
+
+    class _Frame:  # only used in isinstance checks / annotations
+        pass
+
+    pl.DataFrame = type("DataFrame", (_Frame,), {})
+    pl.LazyFrame = type("LazyFrame", (_Frame,), {})
+    pl.Config = type("Config", (), {"set_engine_affinity": staticmethod(lambda *a, **k: None)})
+    sel = types.ModuleType("polars.selectors")
+    pl.selectors = sel
+    duck = types.ModuleType("duckdb")
+    duck.DuckDBPyConnection = type("DuckDBPyConnection", (), {})
+    sys.modules.update({"polars": pl, "polars.selectors": sel, "duckdb": duck})
+    pkg = types.ModuleType("leanfe")
+    pkg.__path__ = [REF_PKG]
+    sys.modules["leanfe"] = pkg
+    compress = importlib.import_module("leanfe.compress")
+    std_errors = importlib.import_module("leanfe.std_errors")
+    return compress, std_errors
+
+
+def lsdv_reference(compress, data, y, xs, fes, keep, vcov, cluster_cols, ssc, n_obs, df_resid):
+    """Exact LSDV fit + SEs computed by the reference's own functions."""
+    sel = lambda a: np.asarray(a)[keep]
+    cols = {c: sel(data[c]).astype(np.float64) for c in xs}
+    for f in fes:
+        cols[f] = sel(data[f])
+    yv = sel(data[y]).astype(np.float64)
+    n = yv.size
+    cols["_mean_y"] = yv
+    cols["_wts"] = np.ones(n)
+    cols["_n"] = np.ones(n)
+    cols["_sum_y"] = yv
+    cols["_sum_y_sq"] = yv ** 2
+    res = compress.DuckDBResult(cols)
+    design, Y, wts, all_cols, _ = compress.build_design_matrix(res, xs, fes, use_sparse=True)
+    beta, XtX_inv = compress.solve_wls(design, Y, wts)
+    rss_total, rss_per_group = compress.compute_rss_grouped(res, design, beta, backend="duckdb")
+    cl_ids, resid_sums = None, None
+    if vcov == "cluster":
+        cl = [sel(data[c]) for c in cluster_cols]
+        cl_ids = cl[0] if len(cl) == 1 else np.stack(cl, axis=1)
+        fitted = np.asarray(design @ beta).ravel()
+        resid_sums = yv - fitted
+    k_x = len(xs) + 1
+    ctx = compress.CompressionContext(
+        XtX_inv=XtX_inv, rss_total=rss_total, rss_per_group=rss_per_group,
+        n_obs=n_obs, df_resid=df_resid, vcov=vcov, design_matrix=design,
+        x_cols=all_cols[:k_x], cluster_ids=cl_ids, residual_sums_per_group=resid_sums,
+        apply_small_sample_correction=ssc)
+    se, ncl = compress.compute_se_compress(ctx)
+    return np.asarray(beta[1:k_x]), np.asarray(se[1:]), ncl
+
+
+# ---------------------------------------------------------------------------
+# fixture recipes
+# ---------------------------------------------------------------------------
+
+def fx_xlang():
+    """tests/test_cross_language_equivalence.py:19-48 (seed 12345, n=1000)."""
+    np.random.seed(12345)
+    n = 1000
+    return {
+        "y": np.random.normal(10, 2, n),
+        "x1": np.random.normal(0, 1, n),
+        "x2": np.random.normal(5, 2, n),
+        "treatment": np.random.binomial(1, 0.5, n),
+        "fe1": np.repeat(np.arange(100), 10),
+        "fe2": np.tile(np.arange(50), 20),
+        "cluster": np.repeat(np.arange(50), 20),
+        "weight": np.random.uniform(0.5, 2.0, n),
+    }
+
+
+def fx_multitreat():
+    """python/tests/test_multiple_treatments.py:10-38 (seed 42, n=10000)."""
+    np.random.seed(42)
+    n = 10000
+    d = {
+        "customer_id": np.repeat(np.arange(1000), 10),
+        "product_id": np.tile(np.arange(100), 100),
+        "region": np.random.choice([0, 1, 2], n),
+        "treatment_A": np.random.binomial(1, 0.3, n),
+        "treatment_B": np.random.binomial(1, 0.4, n),
+        "treatment_C": np.random.choice([0, 1, 2], n),
+    }
+    d["revenue"] = (10.0 + 0.5 * d["treatment_A"] + 0.8 * d["treatment_B"] + 1.2 * d["treatment_C"]
+                    + d["customer_id"] * 0.01 + d["product_id"] * 0.02 + np.random.normal(0, 1, n))
+    return d
+
+
+def fx_panel(seed=7, n=20000, L=(400, 30), k=3, singletons=25, weights=False, clusters=True):
+    """Unbalanced random panel with FE-correlated regressors and injected singletons."""
+    rng = np.random.default_rng(seed)
+    codes = [rng.integers(0, G, n) for G in L]
+    # injected singletons: fresh fe1 levels used once (dropped by the single-pass rule)
+    codes[0][:singletons] = L[0] + np.arange(singletons)
+    eff = [rng.normal(0, 1.0 / (f + 1), G + singletons) for f, G in enumerate(L)]
+    d = {}
+    y = rng.normal(0, 1, n)
+    for j in range(k):
+        x = rng.normal(0, 1, n) + 0.7 * eff[0][codes[0]] - 0.3 * eff[-1][codes[-1]]
+        d[f"x{j + 1}"] = x
+        y = y + (1.0 - 0.3 * j) * x
+    for f in range(len(L)):
+        y = y + eff[f][codes[f]]
+        d[f"fe{f + 1}"] = codes[f]
+    d["y"] = y
+    if weights:
+        d["w"] = rng.uniform(0.5, 2.0, n)
+    if clusters:
+        d["cl1"] = rng.integers(0, 60, n)
+        d["cl2"] = rng.integers(0, 45, n)
+    return d
+
+
+def fx_synth(n=20000, k=4, L=(500, 40)):
+    return synth.panel(n, k, list(L), seed=12345)
+
+
+CASES = [
+    # name, recipe, y, xs, fes, strategy, weights, vcov, cluster_cols
+    ("xlang_iid", fx_xlang, "y", ["x1", "x2", "treatment"], ["fe1", "fe2"], "alt_proj", None, "iid", None),
+    ("xlang_hc1", fx_xlang, "y", ["x1", "x2", "treatment"], ["fe1", "fe2"], "alt_proj", None, "HC1", None),
+    ("xlang_cl1", fx_xlang, "y", ["x1", "x2", "treatment"], ["fe1", "fe2"], "alt_proj", None, "cluster", ["cluster"]),
+    ("xlang_cl2", fx_xlang, "y", ["x1", "x2", "treatment"], ["fe1", "fe2"], "alt_proj", None, "cluster", ["cluster", "fe2"]),
+    ("xlang_demean", fx_xlang, "y", ["x1", "x2", "treatment"], ["fe1"], "demean", None, "iid", None),
+    ("multitreat_iid", fx_multitreat, "revenue", ["treatment_A", "treatment_B", "treatment_C"],
+     ["customer_id", "product_id"], "alt_proj", None, "iid", None),
+    ("multitreat_cl1", fx_multitreat, "revenue", ["treatment_A", "treatment_B"],
+     ["customer_id", "product_id"], "alt_proj", None, "cluster", ["customer_id"]),
+    ("panel_iid", fx_panel, "y", ["x1", "x2", "x3"], ["fe1", "fe2"], "alt_proj", None, "iid", None),
+    ("panel_hc1", fx_panel, "y", ["x1", "x2", "x3"], ["fe1", "fe2"], "alt_proj", None, "HC1", None),
+    ("panel_cl1", fx_panel, "y", ["x1", "x2", "x3"], ["fe1", "fe2"], "alt_proj", None, "cluster", ["cl1"]),
+    ("panel_cl2", fx_panel, "y", ["x1", "x2", "x3"], ["fe1", "fe2"], "alt_proj", None, "cluster", ["cl1", "cl2"]),
+    ("panel3_cl2", lambda: fx_panel(seed=11, n=20000, L=(300, 60, 12), k=3), "y", ["x1", "x2", "x3"],
+     ["fe1", "fe2", "fe3"], "alt_proj", None, "cluster", ["fe2", "fe3"]),
+    ("panel_demean_hc1", lambda: fx_panel(seed=5, n=15000, L=(700,), k=2), "y", ["x1", "x2"], ["fe1"],
+     "demean", None, "HC1", None),
+    ("synth_iid", fx_synth, "y", ["x1", "x2", "x3", "x4"], ["fe1", "fe2"], "alt_proj", None, "iid", None),
+    ("synth_hc1", fx_synth, "y", ["x1", "x2", "x3", "x4"], ["fe1", "fe2"], "alt_proj", None, "HC1", None),
+]
+
+# weighted fits: the reference's LSDV helpers take weights only as sqrt(group
+# size), so weighted goldens are pinned to the oracle restatement of
+# polars_impl.py:493-500 + :201-206 (no independent reference vector exists).
+WEIGHTED = [
+    ("xlang_w_iid", fx_xlang, "y", ["x1", "x2", "treatment"], ["fe1", "fe2"], "alt_proj", "weight", "iid", None),
+    ("panel_w_cl1", lambda: fx_panel(seed=9, weights=True), "y", ["x1", "x2", "x3"], ["fe1", "fe2"],
+     "alt_proj", "w", "cluster", ["cl1"]),
+]
+
+
+def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight):
+    arrays = {f"in_{c}": np.asarray(v) for c, v in data.items()}
+    meta = dict(name=name, y=y, xs=xs, fes=fes, strategy=strategy, weights=weights, vcov=vcov,
+                cluster_cols=cl, demean_tol=1e-6, max_iter=50, ssc=True,
+                oracle_n_clusters=orc["n_clusters"], ref_n_clusters=ref[2] if ref else None,
+                pinned="reference-lsdv" if ref else "oracle-only")
+    arrays.update(
+        oracle_beta=orc["beta"], oracle_se=orc["se"], oracle_iterations=np.int64(orc["iterations"]),
+        oracle_n_obs=np.int64(orc["n_obs"]), oracle_df_resid=np.int64(orc["df_resid"]),
+        oracle_fe_dims=np.asarray(orc["fe_dims"], dtype=np.int64),
+        oracle_r2=np.float64(orc["r_squared"] if orc["r_squared"] is not None else np.nan),
+        tight_beta=tight["beta"], tight_se=tight["se"],
+        meta=np.frombuffer(json.dumps(meta, default=lambda o: list(o) if isinstance(o, tuple) else o)
+                           .encode(), dtype=np.uint8))
+    if ref:
+        arrays.update(ref_beta=ref[0], ref_se=ref[1])
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+
+
+def _json_ncl(v):
+    return list(v) if isinstance(v, tuple) else v
+
+
+def main():
+    compress, _ = load_reference()
+    worst = 0.0
+    for name, recipe, y, xs, fes, strategy, weights, vcov, cl in CASES + WEIGHTED:
+        data = recipe()
+        orc = altproj.fit(data, y, xs, fes, strategy=strategy, weights=weights, vcov=vcov,
+                          cluster_cols=cl)
+        tight = altproj.fit(data, y, xs, fes, strategy=strategy, weights=weights, vcov=vcov,
+                            cluster_cols=cl, demean_tol=1e-14, max_iter=100000)
+        ref = None
+        if weights is None:
+            ref = lsdv_reference(compress, data, y, xs, fes, orc["keep"], vcov, cl, True,
+                                 orc["n_obs"], orc["df_resid"])
+            rb = np.max(np.abs(tight["beta"] - ref[0]) / np.maximum(np.abs(ref[0]), 1e-300))
+            rs = np.max(np.abs(tight["se"] - ref[1]) / np.maximum(np.abs(ref[1]), 1e-300))
+            db = np.max(np.abs(orc["beta"] - ref[0]) / np.maximum(np.abs(ref[0]), 1e-300))
+            assert rb < 1e-9 and rs < 1e-9, (name, rb, rs)
+            assert _json_ncl(ref[2]) == _json_ncl(orc["n_clusters"]), (name, ref[2], orc["n_clusters"])
+            worst = max(worst, rb, rs)
+            print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} df={orc['df_resid']:6d} "
+                  f"tight-vs-ref beta {rb:.1e} se {rs:.1e} | default-tol beta dev {db:.1e}")
+        else:
+            print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} (oracle-pinned, weighted)")
+        _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight)
+    print(f"worst tight-oracle vs reference-LSDV relative deviation: {worst:.2e}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,103 @@
+"""GPU parity: the HIP engine (through the C ABI) against the oracle and the golden fixtures.
+
+Tolerances: coefficients and SEs within 1e-10 relative (BASELINE.json
+north_star); integer outputs (n_obs, iterations, fe_dims, df_resid,
+n_clusters) bit-exact.  Synthetic-panel generation is bit-exact host vs device.
+"""
+import numpy as np
+import pytest
+
+from golden_util import load, names, ncl
+from leanfe_amd import synth
+from oracle import altproj
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-10
+
+
+def _hip_fit(meta, data, **kw):
+    from leanfe_amd import leanfe_hip
+    return leanfe_hip(data, y_col=meta["y"], x_cols=meta["xs"], fe_cols=meta["fes"], strategy=meta["strategy"],
+                      weights=meta["weights"], vcov=meta["vcov"], cluster_cols=meta["cluster_cols"],
+                      ssc=meta["ssc"], quiet=True, **kw)
+
+
+def _assert_same(r, beta, se, n_obs, iterations, df_resid, fe_dims, n_clusters, xs, rtol=RTOL):
+    b = np.array([r.coefs[x] for x in xs])
+    s = np.array([r.std_errors[x] for x in xs])
+    assert r.n_obs == n_obs
+    assert r.iterations == iterations
+    assert r.df_resid == df_resid
+    assert tuple(r.fe_dims or ()) == tuple(fe_dims)
+    assert ncl(r.n_clusters) == ncl(n_clusters)
+    np.testing.assert_allclose(b, beta, rtol=rtol, atol=0)
+    np.testing.assert_allclose(s, se, rtol=rtol, atol=0)
+
+
+@pytest.mark.parametrize("name", names())
+def test_golden_fixture(name):
+    meta, data, exp = load(name)
+    r = _hip_fit(meta, data, demean_tol=meta["demean_tol"], max_iter=meta["max_iter"])
+    _assert_same(r, exp["oracle_beta"], exp["oracle_se"], int(exp["oracle_n_obs"]), int(exp["oracle_iterations"]),
+                 int(exp["oracle_df_resid"]), exp["oracle_fe_dims"].tolist(), meta["oracle_n_clusters"], meta["xs"])
+    if "ref_beta" in exp:  # the reference's exact LSDV values, up to alt-proj convergence error
+        b = np.array([r.coefs[x] for x in meta["xs"]])
+        np.testing.assert_allclose(b, exp["ref_beta"], rtol=1e-7, atol=0)
+
+
+def test_synth_device_equals_host_bit_exact():
+    from leanfe_amd._lib import Engine
+    n, k, L = 5000, 3, [300, 20]
+    host = synth.panel(n, k, L, seed=12345, row_offset=777)
+    with Engine(0) as eng:
+        eng.synth_load(n, k, L, synth.betas(k), seed=12345, row_offset=777)
+        cols, codes = eng.copy_inputs(n)
+    np.testing.assert_array_equal(cols[0], host["y"])
+    for j in range(k):
+        np.testing.assert_array_equal(cols[1 + j], host[f"x{j + 1}"])
+    for f in range(len(L)):
+        np.testing.assert_array_equal(codes[f], host[f"fe{f + 1}"])
+
+
+@pytest.mark.parametrize("seed,n,L,k,vcov", [
+    (1, 200_000, (5000, 300), 5, "iid"),
+    (2, 300_000, (20000, 500), 3, "HC1"),
+    (3, 150_000, (3000, 40, 7), 4, "cluster"),
+])
+def test_random_panels_vs_oracle(seed, n, L, k, vcov):
+    data = synth.panel(n, k, list(L), seed=seed)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(L))]
+    cl = ["fe2", "fe3"] if vcov == "cluster" else None
+    o = altproj.fit(data, "y", xs, fes, vcov=vcov, cluster_cols=cl)
+    from leanfe_amd import leanfe_hip
+    r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov=vcov, cluster_cols=cl,
+                   quiet=True)
+    _assert_same(r, o["beta"], o["se"], o["n_obs"], o["iterations"], o["df_resid"], o["fe_dims"],
+                 o["n_clusters"], xs)
+
+
+def test_ols_no_fe_and_single_fe_demean():
+    data = synth.panel(20000, 2, [400], seed=4)
+    from leanfe_amd import leanfe_hip
+    r = leanfe_hip(data, formula="y ~ x1 + x2 | fe1", quiet=True)
+    o = altproj.fit(data, "y", ["x1", "x2"], ["fe1"], strategy="demean")
+    _assert_same(r, o["beta"], o["se"], o["n_obs"], 1, o["df_resid"], o["fe_dims"], None, ["x1", "x2"])
+    r = leanfe_hip(data, formula="y ~ x1 + x2", quiet=True)
+    X = np.column_stack([np.ones(20000), data["x1"], data["x2"]])
+    b = np.linalg.lstsq(X, data["y"], rcond=None)[0]
+    np.testing.assert_allclose([r.coefs["x1"], r.coefs["x2"]], b[1:], rtol=1e-10)
+
+
+def test_all_rows_singletons_raises_or_empty():
+    data = {"y": np.arange(5.0), "x": np.arange(5.0) ** 2, "a": np.arange(5), "b": np.arange(5)}
+    from leanfe_amd import leanfe_hip
+    with pytest.raises(Exception):
+        leanfe_hip(data, formula="y ~ x | a + b", strategy="alt_proj", quiet=True)
+
+
+def test_bad_codes_rejected():
+    from leanfe_amd._lib import Engine
+    with Engine(0) as eng:
+        with pytest.raises(ValueError):
+            eng.load([np.zeros(4)], [np.array([0, 1, 5, 0], dtype=np.int32)], [3])

@@ -1,0 +1,178 @@
+"""CPU: host-side logic of the hip backend (no GPU calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from leanfe_amd import frame, inference, synth
+from leanfe_amd.formula import parse_formula
+from leanfe_amd.result import LeanFEResult
+from leanfe_amd.strategy import determine_strategy, estimate_compression_ratio
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---------------------------------------------------------------- formula
+# cases mirror the grammar of common.py:51-181
+
+
+def test_formula_basic():
+    f = parse_formula("y ~ x1 + x2 | fe1 + fe2")
+    assert f.y_col == "y" and f.x_cols == ["x1", "x2"] and f.fe_cols == ["fe1", "fe2"]
+    assert f.factor_vars == [] and f.interactions == [] and f.instruments == []
+
+
+def test_formula_no_fe_and_iv():
+    assert parse_formula("y ~ x").fe_cols == []
+    f = parse_formula("y ~ x1 | fe | z1 + z2")
+    assert f.instruments == ["z1", "z2"]
+
+
+def test_formula_factor_and_interaction():
+    f = parse_formula("y ~ x + i(region, ref=R1) + treat:i(region) + i(year) | fe")
+    assert f.x_cols == ["x"]
+    assert f.factor_vars == [("region", "R1"), ("year", None)]
+    assert f.interactions == [("treat", "region", None)]
+    f = parse_formula('y ~ treat:i(region, ref="R2") | fe')
+    assert f.interactions == [("treat", "region", "R2")]
+
+
+def test_formula_errors():
+    with pytest.raises(ValueError):
+        parse_formula("y ~ x | a | b | c")
+    with pytest.raises(ValueError):
+        parse_formula("y x")
+    with pytest.raises(ValueError):
+        parse_formula("y ~ i(1bad-) | fe")
+
+
+# ---------------------------------------------------------------- result
+
+
+def test_result_dict_interface_and_pvalues():
+    r = LeanFEResult(coefs={"x": 2.0, "z": 0.0}, std_errors={"x": 0.5, "z": 0.0}, n_obs=1000,
+                     vcov_type="iid", df_resid=990, iterations=4, fe_cols=["a", "b"], fe_dims=(10, 5))
+    assert r["coefs"]["x"] == 2.0 and r["iterations"] == 4
+    assert repr(r["n_obs"]) == "1_000"
+    from scipy import stats
+    assert np.isclose(r.p_values["x"], 2 * (1 - stats.t.cdf(4.0, 990)))
+    assert np.isnan(r.t_stats["z"])
+    lo, hi = r.confint()["x"]
+    assert lo < 2.0 < hi
+    s = str(r)
+    assert "FE Dimensions: 10 × 5" in s and "Variable" in s
+    assert set(r.keys()) >= {"coefs", "std_errors", "n_obs", "iterations", "df_resid", "n_clusters"}
+
+
+# ---------------------------------------------------------------- strategy (compress.py:96-184)
+
+
+def test_determine_strategy_rules():
+    assert determine_strategy("iid", True, {"a": 5}) == "alt_proj"
+    assert determine_strategy("iid", False, {"a": 10_001, "b": 3}) == "alt_proj"
+    assert determine_strategy("iid", False, {"a": 9_000, "b": 12_000}) == "alt_proj"
+    assert determine_strategy("iid", False, {"a": 50, "b": 20}) == "compress"
+    assert determine_strategy("iid", False, {"a": 5000, "b": 5000}, n_obs=1000,
+                              estimated_compression_ratio=1.0) == "alt_proj"
+    assert determine_strategy("weird", False, {"a": 5}) == "alt_proj"
+
+
+def test_compression_ratio_exact_small():
+    x = np.array([1, 1, 2, 2, 2.0])
+    fe = np.array([1, 1, 2, 3, 3])
+    assert estimate_compression_ratio([x, fe]) == pytest.approx(3 / 5)
+
+
+# ---------------------------------------------------------------- frame
+
+
+def test_factorize_fast_path_and_unique():
+    c, g = frame.factorize(np.array([3, 0, 3, 7]))
+    assert c.dtype == np.int32 and g == 8 and c.tolist() == [3, 0, 3, 7]
+    c, g = frame.factorize(np.array(["b", "a", "b"]))
+    assert g == 2 and c.tolist() == [1, 0, 1]
+    c, g = frame.factorize(np.array([-5, 10, -5]))
+    assert g == 2 and c.tolist() == [0, 1, 0]
+
+
+def test_intersect_membership():
+    a = np.array([0, 0, 1, 1, 0], dtype=np.int32)
+    b = np.array([0, 1, 0, 1, 0], dtype=np.int32)
+    c, g = frame.intersect([a, b], [2, 2])
+    assert c[0] == c[4] and len(set(c.tolist())) == 4 and g >= 4
+
+
+def test_expand_factors_and_interactions():
+    cols = {"r": np.array(["A", "B", "C", "A"]), "t": np.array([1.0, 2.0, 3.0, 4.0])}
+    names = frame.expand_factors(cols, [("r", None)])
+    assert names == ["r_B", "r_C"] and cols["r_B"].tolist() == [0, 1, 0, 0]
+    names = frame.expand_interactions(cols, [("t", "r", "B")])
+    assert names == ["t_A", "t_C"] and cols["t_C"].tolist() == [0, 0, 3.0, 0]
+    with pytest.raises(ValueError):
+        frame.expand_factors(cols, [("r", "Z")])
+
+
+def test_get_columns_pandas_and_dict():
+    import pandas as pd
+    df = pd.DataFrame({"a": [1.0, 2.0], "c": pd.Categorical(["x", "y"])})
+    out = frame.get_columns(df, ["a", "c"])
+    assert out["c"].tolist() == [0, 1]
+    with pytest.raises(ValueError):
+        frame.get_columns({"a": [1]}, ["a", "b"])
+
+
+# ---------------------------------------------------------------- inference
+
+
+def test_split_gram_and_solve():
+    rng = np.random.default_rng(0)
+    X = np.column_stack([np.ones(50), rng.normal(size=(50, 3))])
+    y = X @ np.array([1.0, 2.0, -1.0, 0.5]) + rng.normal(size=50) * 0.1
+    Z = np.column_stack([np.ones(50), y, X[:, 1:]])
+    XtX, Xty = inference.split_gram(Z.T @ Z)
+    b, inv = inference.solve_normal(XtX, Xty)
+    np.testing.assert_allclose(b, np.linalg.lstsq(X, y, rcond=None)[0], rtol=1e-10)
+    np.testing.assert_allclose(inv @ XtX, np.eye(4), atol=1e-10)
+
+
+def test_multiway_subsets_order():
+    assert inference.cluster_subsets(3) == [(0,), (1,), (2,), (0, 1), (0, 2), (1, 2), (0, 1, 2)]
+
+
+# ---------------------------------------------------------------- synthetic panel
+
+
+def test_synth_counter_based_and_shardable():
+    full = synth.panel(1000, 3, [50, 7], seed=12345)
+    part = synth.panel(400, 3, [50, 7], seed=12345, row_offset=600)
+    for k in full:
+        np.testing.assert_array_equal(full[k][600:], part[k])
+    assert full["fe1"].max() < 50 and full["fe2"].min() >= 0
+    assert abs(float(np.mean(synth.normal(np.arange(20000, dtype=np.uint64), 5, 1)))) < 0.05
+
+
+# ---------------------------------------------------------------- C ABI surface
+
+
+def _declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "leanfe_hip.h")).read()
+    return sorted(set(re.findall(r"\b(lfe_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_header_matches_binding_table():
+    from leanfe_amd._lib import SIGNATURES
+    assert sorted(SIGNATURES) == _declared_symbols()
+
+
+def test_library_loads_and_exports_every_symbol():
+    path = os.path.join(ROOT, "leanfe_amd", "liblfe_hip.so")
+    if not os.path.exists(path):
+        from leanfe_amd.build import build
+        build(verbose=False)
+    lib = ctypes.CDLL(path)
+    for name in _declared_symbols():
+        assert hasattr(lib, name), name
+    lib.lfe_version.restype = ctypes.c_char_p
+    assert b"gfx950" in lib.lfe_version()
