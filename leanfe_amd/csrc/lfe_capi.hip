@@ -19,12 +19,15 @@ static int fail(int code, const std::string& msg) {
   return code;
 }
 
-#define LFE_NCCL(expr)                                                                  \
-  do {                                                                                  \
-    ncclResult_t _r = (expr);                                                           \
+#define LFE_NCCL(expr)                                                                                  \
+  do {                                                                                                  \
+    ncclResult_t _r = (expr);                                                                           \
     if (_r != ncclSuccess) return fail(LFE_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
   } while (0)
 
+// Device allocations are plain hipMalloc: the stream-ordered allocator is not
+// used anywhere in the engine (a hipMallocAsync'd table raced with later
+// hipMalloc/hipFree in an early version).
 template <typename T>
 static int dalloc(T** p, size_t elems) {
   *p = nullptr;
@@ -39,45 +42,33 @@ static int dalloc(T** p, size_t elems) {
 
 template <typename T>
 static void dfree(T*& p) {
-  if (p) hipFree(p);
+  if (p) (void)hipFree(p);
   p = nullptr;
 }
 
-int ensure_scratch(lfe_ctx* c, size_t elems) {
-  if (c->scratch_elems >= elems) return LFE_OK;
-  dfree(c->scratch);
-  c->scratch_elems = 0;
-  LFE_TRY(dalloc(&c->scratch, elems));
-  c->scratch_elems = elems;
+template <typename T>
+static int ensure(T*& p, size_t& have, size_t want) {
+  if (have >= want) return LFE_OK;
+  dfree(p);
+  have = 0;
+  LFE_TRY(dalloc(&p, want));
+  have = want;
   return LFE_OK;
 }
 
-int ensure_dred(lfe_ctx* c, size_t elems) {
-  if (c->dred_elems >= elems) return LFE_OK;
-  dfree(c->dred);
-  c->dred_elems = 0;
-  LFE_TRY(dalloc(&c->dred, elems));
-  c->dred_elems = elems;
-  return LFE_OK;
+int ensure_scratch(lfe_ctx* c, size_t elems) { return ensure(c->scratch, c->scratch_elems, elems); }
+int ensure_dred(lfe_ctx* c, size_t elems) { return ensure(c->dred, c->dred_elems, elems); }
+int ensure_iscratch(lfe_ctx* c, size_t elems) { return ensure(c->iscratch, c->iscratch_elems, elems); }
+int ensure_items(lfe_ctx* c, size_t n_items) { return ensure(c->items_d, c->items_cap, 4 * n_items); }
+
+int ensure_pcounts(lfe_ctx* c, size_t elems, size_t sums) {
+  LFE_TRY(ensure(c->pcounts, c->pcounts_elems, elems));
+  return ensure(c->psums, c->psums_elems, sums);
 }
 
-int ensure_iscratch(lfe_ctx* c, size_t elems) {
-  if (c->iscratch_elems >= elems) return LFE_OK;
-  dfree(c->iscratch);
-  c->iscratch_elems = 0;
-  LFE_TRY(dalloc(&c->iscratch, elems));
-  c->iscratch_elems = elems;
-  return LFE_OK;
-}
-
-int ensure_pinned(lfe_ctx* c, size_t elems) {
-  if (c->hpinned_elems >= elems) return LFE_OK;
-  if (c->hpinned) hipHostFree(c->hpinned);
-  c->hpinned = nullptr;
-  c->hpinned_elems = 0;
-  LFE_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hpinned), sizeof(double) * elems, hipHostMallocDefault));
-  c->hpinned_elems = elems;
-  return LFE_OK;
+int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems) {
+  LFE_TRY(ensure(c->clS, c->clS_elems, table_elems));
+  return ensure(c->clP, c->clP_elems, flag_elems);
 }
 
 int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count) {
@@ -98,20 +89,13 @@ int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count) {
   return LFE_OK;
 }
 
-FeArgs fe_args(const lfe_ctx* c) {
-  FeArgs a{};
-  a.F = c->F;
-  a.p = c->p;
-  for (int f = 0; f < c->F; ++f) {
-    a.code[f] = c->fe[f].code;
-    a.alpha[f] = c->fe[f].alpha;
-  }
-  return a;
-}
+// ---------------------------------------------------------------------------
+// per-kernel event profiling
+// ---------------------------------------------------------------------------
 
 const char* const kKernelNames[K_NUM_KERNELS] = {
-    "count_pre", "keep", "group_sums", "cross_sums", "finalize", "check_sums", "check_max", "gram_design",
-    "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "count_nonzero", "synth"};
+    "part_hist", "scan", "part_scatter", "count", "mark", "group_sums", "cross", "check", "finalize",
+    "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth"};
 
 static hipEvent_t prof_event(lfe_ctx* c) {
   if (!c->prof.pool.empty()) {
@@ -128,7 +112,7 @@ void prof_begin(lfe_ctx* c, int kid) {
   if (!c->prof.on) return;
   hipEvent_t e = prof_event(c);
   if (!e) return;
-  hipEventRecord(e, c->stream);
+  (void)hipEventRecord(e, c->stream);
   c->prof.open_ev = e;
   c->prof.open_id = kid;
 }
@@ -137,10 +121,10 @@ void prof_end(lfe_ctx* c) {
   if (!c->prof.on || !c->prof.open_ev) return;
   hipEvent_t e = prof_event(c);
   if (!e) return;
-  hipEventRecord(e, c->stream);
+  (void)hipEventRecord(e, c->stream);
   c->prof.pending.push_back({c->prof.open_id, {c->prof.open_ev, e}});
   c->prof.open_ev = nullptr;
-  if (c->prof.pending.size() > 4096) prof_fold(c);
+  if (c->prof.pending.size() > 4096) (void)prof_fold(c);
 }
 
 int prof_fold(lfe_ctx* c) {
@@ -159,17 +143,26 @@ int prof_fold(lfe_ctx* c) {
   return LFE_OK;
 }
 
+// ---------------------------------------------------------------------------
+// data buffers
+// ---------------------------------------------------------------------------
+
 static void free_data(lfe_ctx* c) {
   dfree(c->X);
   dfree(c->w);
-  dfree(c->keep);
+  dfree(c->Xp);
+  dfree(c->wp);
+  dfree(c->codes_p);
+  dfree(c->origp);
   dfree(c->scores);
   for (auto& fe : c->fe) {
     dfree(fe.code);
     dfree(fe.cnt_pre);
+    dfree(fe.drops);
     dfree(fe.cnt);
     dfree(fe.W);
     dfree(fe.S);
+    dfree(fe.Sy);
     dfree(fe.T);
     dfree(fe.alpha);
     dfree(fe.R);
@@ -178,6 +171,7 @@ static void free_data(lfe_ctx* c) {
   for (auto& p : c->cl) dfree(p);
   c->cl.clear();
   c->cl_levels.clear();
+  c->L = Layout();
   c->loaded = c->prepared = c->demeaned = c->scores_valid = false;
   c->n = c->ld = 0;
   c->p = c->F = 0;
@@ -188,28 +182,39 @@ static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_leve
   free_data(c);
   if (p < 1 || p > kMaxCols) return fail(LFE_EINVAL, "p must be in [1, 63] (y plus up to 62 regressors)");
   if (F < 0 || F > kMaxFE) return fail(LFE_EINVAL, "number of fixed effects must be in [0, 8]");
-  if (n < 0) return fail(LFE_EINVAL, "n must be >= 0");
+  if (n < 0 || n >= (int64_t)INT32_MAX) return fail(LFE_EINVAL, "rows per shard must be in [0, 2^31 - 1)");
+  for (int f = 0; f < F; ++f)
+    if (n_levels[f] < 1) return fail(LFE_EINVAL, "n_levels must be >= 1");
   c->n = n;
-  c->ld = (n + 63) / 64 * 64;
-  if (c->ld == 0) c->ld = 64;
+  c->ld = std::max<int64_t>((n + 63) / 64 * 64, 64);
   c->p = p;
   c->F = F;
   LFE_TRY(dalloc(&c->X, (size_t)p * c->ld));
   if (weighted) LFE_TRY(dalloc(&c->w, (size_t)c->ld));
-  LFE_TRY(dalloc(&c->keep, (size_t)c->ld));
+  if (F > 0) LFE_TRY(dalloc(&c->codes_p, (size_t)F * c->ld));
   c->fe.resize(F);
+  bool need_perm = false;
   for (int f = 0; f < F; ++f) {
     auto& fe = c->fe[f];
-    if (n_levels[f] < 1) return fail(LFE_EINVAL, "n_levels must be >= 1");
     fe.G = n_levels[f];
+    need_perm = need_perm || fe.G > 256;
     LFE_TRY(dalloc(&fe.code, (size_t)c->ld));
     LFE_TRY(dalloc(&fe.cnt_pre, (size_t)fe.G));
+    LFE_TRY(dalloc(&fe.drops, (size_t)fe.G));
     LFE_TRY(dalloc(&fe.cnt, (size_t)fe.G));
-    LFE_TRY(dalloc(&fe.W, (size_t)fe.G));
     LFE_TRY(dalloc(&fe.S, (size_t)fe.G * p));
     LFE_TRY(dalloc(&fe.T, (size_t)fe.G * p));
     LFE_TRY(dalloc(&fe.alpha, (size_t)fe.G * p));
     LFE_TRY(dalloc(&fe.R, (size_t)fe.G));
+    if (weighted) {
+      LFE_TRY(dalloc(&fe.W, (size_t)fe.G));
+      LFE_TRY(dalloc(&fe.Sy, (size_t)fe.G));
+    }
+  }
+  if (need_perm) {  // bucketed layout storage (rows regrouped by the primary FE)
+    LFE_TRY(dalloc(&c->Xp, (size_t)p * c->ld));
+    if (weighted) LFE_TRY(dalloc(&c->wp, (size_t)c->ld));
+    LFE_TRY(dalloc(&c->origp, (size_t)c->ld));
   }
   return LFE_OK;
 }
@@ -217,23 +222,38 @@ static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_leve
 struct PhaseTimer {
   lfe_ctx* c;
   double* slot;
-  PhaseTimer(lfe_ctx* c_, double* s) : c(c_), slot(s) { hipEventRecord(c->ev0, c->stream); }
+  PhaseTimer(lfe_ctx* c_, double* s) : c(c_), slot(s) { (void)hipEventRecord(c->ev0, c->stream); }
   ~PhaseTimer() {
-    hipEventRecord(c->ev1, c->stream);
+    (void)hipEventRecord(c->ev1, c->stream);
     if (hipEventSynchronize(c->ev1) == hipSuccess) {
       float ms = 0.f;
-      hipEventElapsedTime(&ms, c->ev0, c->ev1);
+      (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
       *slot = ms;
       c->tm.last = ms;
     }
   }
 };
 
-#define LFE_CTX(c)                                                        \
-  do {                                                                    \
-    if (!(c)) return fail(LFE_EINVAL, "null context");                    \
-    LFE_HIP(hipSetDevice((c)->device));                                   \
+#define LFE_CTX(c)                                     \
+  do {                                                 \
+    if (!(c)) return fail(LFE_EINVAL, "null context"); \
+    LFE_HIP(hipSetDevice((c)->device));                \
   } while (0)
+
+static int validate_all(lfe_ctx* c) {
+  LFE_TRY(ensure_iscratch(c, 16));
+  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
+  for (int f = 0; f < c->F && c->n > 0; ++f)
+    LFE_TRY(launch_validate_codes(c->fe[f].code, c->n, c->fe[f].G, c->iscratch, c->stream));
+  int32_t bad = 0;
+  LFE_HIP(hipMemcpyAsync(&bad, c->iscratch, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  if (bad) {
+    free_data(c);
+    return fail(LFE_EINVAL, "FE codes must be dense int32 in [0, n_levels)");
+  }
+  return LFE_OK;
+}
 
 }  // namespace lfe
 
@@ -243,7 +263,7 @@ extern "C" {
 
 const char* lfe_last_error(void) { return g_err.c_str(); }
 
-const char* lfe_version(void) { return "leanfe_amd-hip 0.1.0 (gfx950)"; }
+const char* lfe_version(void) { return "leanfe_amd-hip 0.2.0 (gfx950)"; }
 
 int lfe_ctx_create(lfe_ctx** out, int device) {
   if (!out) return fail(LFE_EINVAL, "out is null");
@@ -266,23 +286,27 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
 
 void lfe_ctx_destroy(lfe_ctx* c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_data(c);
   dfree(c->scratch);
   dfree(c->dred);
   dfree(c->iscratch);
+  dfree(c->pcounts);
+  dfree(c->psums);
+  dfree(c->items_d);
   dfree(c->dbeta);
-  if (c->hpinned) hipHostFree(c->hpinned);
+  dfree(c->clS);
+  dfree(c->clP);
   if (c->comm) ncclCommDestroy(c->comm);
   for (auto& r : c->prof.pending) {
-    hipEventDestroy(r.second.first);
-    hipEventDestroy(r.second.second);
+    (void)hipEventDestroy(r.second.first);
+    (void)hipEventDestroy(r.second.second);
   }
-  for (auto e : c->prof.pool) hipEventDestroy(e);
-  if (c->ev0) hipEventDestroy(c->ev0);
-  if (c->ev1) hipEventDestroy(c->ev1);
-  if (c->stream) hipStreamDestroy(c->stream);
+  for (auto e : c->prof.pool) (void)hipEventDestroy(e);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -317,24 +341,15 @@ int lfe_load(lfe_ctx* c, int64_t n, int p, const double* const* cols, int F, con
   LFE_CTX(c);
   if (where != LFE_HOST && where != LFE_DEVICE) return fail(LFE_EINVAL, "where must be LFE_HOST or LFE_DEVICE");
   if (n > 0 && (!cols || (F > 0 && (!fe_codes || !n_levels)))) return fail(LFE_EINVAL, "null input pointer");
+  if (F > 0 && !n_levels) return fail(LFE_EINVAL, "n_levels is null");
   LFE_TRY(alloc_data(c, n, p, F, n_levels, weights != nullptr));
   const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
   for (int j = 0; j < p && n > 0; ++j)
     LFE_HIP(hipMemcpyAsync(c->X + (size_t)j * c->ld, cols[j], sizeof(double) * n, kind, c->stream));
   if (weights && n > 0) LFE_HIP(hipMemcpyAsync(c->w, weights, sizeof(double) * n, kind, c->stream));
-  LFE_TRY(ensure_iscratch(c, 16));
-  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
-  for (int f = 0; f < F && n > 0; ++f) {
+  for (int f = 0; f < F && n > 0; ++f)
     LFE_HIP(hipMemcpyAsync(c->fe[f].code, fe_codes[f], sizeof(int32_t) * n, kind, c->stream));
-    LFE_TRY(launch_validate_codes(c->fe[f].code, n, c->fe[f].G, c->iscratch, c->stream));
-  }
-  int32_t bad = 0;
-  LFE_HIP(hipMemcpyAsync(&bad, c->iscratch, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  LFE_HIP(hipStreamSynchronize(c->stream));
-  if (bad) {
-    free_data(c);
-    return fail(LFE_EINVAL, "FE codes must be dense int32 in [0, n_levels)");
-  }
+  LFE_TRY(validate_all(c));
   c->loaded = true;
   return LFE_OK;
 }
@@ -381,46 +396,16 @@ int lfe_drop_singletons(lfe_ctx* c, int64_t* n_kept, int32_t* fe_dims_out, int32
   if (!c->loaded) return fail(LFE_ESTATE, "lfe_load first");
   {
     PhaseTimer t(c, &c->tm.prep);
-    LFE_TRY(launch_count_pre(c));
-    for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt_pre, c->fe[f].G));
-    LFE_TRY(launch_keep(c));
-    for (int f = 0; f < c->F; ++f) {
-      LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt, c->fe[f].G));
-      LFE_TRY(allreduce_sum_f64(c, c->fe[f].W, c->fe[f].G));
-    }
-    int32_t dims[kMaxFE] = {0}, card[kMaxFE] = {0};
-    if (c->F) LFE_TRY(launch_count_dims(c, dims, card));
-    for (int f = 0; f < c->F; ++f) {
-      c->fe[f].dims = dims[f];
-      c->fe[f].card = card[f];
-      if (fe_dims_out) fe_dims_out[f] = dims[f];
-      if (fe_card_out) fe_card_out[f] = card[f];
-    }
-    // kept rows (global): for F == 0 every row is kept; else sum of counts of FE 0
-    int64_t kept = 0;
-    if (c->F == 0) {
-      kept = c->n;
-      if (c->world > 1) {
-        LFE_TRY(ensure_dred(c, 1));
-        double v = (double)kept;
-        LFE_HIP(hipMemcpyAsync(c->dred, &v, sizeof(double), hipMemcpyHostToDevice, c->stream));
-        LFE_TRY(allreduce_sum_f64(c, c->dred, 1));
-        LFE_HIP(hipMemcpyAsync(&v, c->dred, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-        LFE_HIP(hipStreamSynchronize(c->stream));
-        kept = (int64_t)v;
-      }
-    } else {
-      std::vector<int32_t> h(c->fe[0].G);
-      LFE_HIP(hipMemcpyAsync(h.data(), c->fe[0].cnt, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, c->stream));
-      LFE_HIP(hipStreamSynchronize(c->stream));
-      for (int32_t v : h) kept += v;
-    }
-    c->n_kept = kept;
-    if (n_kept) *n_kept = kept;
+    LFE_TRY(prepare_layout(c));
   }
-  if (c->F == 0) LFE_HIP(hipMemsetAsync(c->keep, 1, (size_t)c->ld, c->stream));
+  for (int f = 0; f < c->F; ++f) {
+    if (fe_dims_out) fe_dims_out[f] = c->fe[f].dims;
+    if (fe_card_out) fe_card_out[f] = c->fe[f].card;
+  }
+  if (n_kept) *n_kept = c->n_kept;
   c->prepared = true;
   c->demeaned = false;
+  c->scores_valid = false;
   return LFE_OK;
 }
 
@@ -436,30 +421,24 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
     for (int f = 0; f < c->F; ++f)
       if (chk[f] != f) return fail(LFE_EINVAL, "fe_order must be a permutation of 0..F-1");
   }
+  if (check_from > 0 && max_iter < 1) return fail(LFE_EINVAL, "max_iter must be >= 1");
   int iterations = 0;
   double last = -1.0;
   {
     PhaseTimer t(c, &c->tm.demean);
     for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
     if (c->F > 0) {
-      LFE_TRY(launch_group_sums(c));
+      LFE_TRY(sweep_group_sums(c));
       if (check_from <= 0) {
         // single within-transform pass ('demean' strategy, polars_impl.py:437-465)
-        for (int f : order) {
-          LFE_TRY(launch_cross_sums(c, f));
-          LFE_TRY(launch_finalize(c, f));
-        }
+        for (int f : order) LFE_TRY(sweep_project(c, f));
         iterations = 1;
       } else {
-        if (max_iter < 1) return fail(LFE_EINVAL, "max_iter must be >= 1");
         for (int it = 1; it <= max_iter; ++it) {
-          for (int f : order) {
-            LFE_TRY(launch_cross_sums(c, f));
-            LFE_TRY(launch_finalize(c, f));
-          }
+          for (int f : order) LFE_TRY(sweep_project(c, f));
           iterations = it;
           if (it >= check_from) {
-            LFE_TRY(launch_check(c, &last));
+            LFE_TRY(sweep_check(c, &last));
             if (last < tol) break;
           }
         }
@@ -508,7 +487,7 @@ int lfe_copy_demeaned(lfe_ctx* c, double* const* cols_out, int64_t* n_out) {
       if (hipMemcpyAsync(cols_out[j], d + (size_t)j * c->n, sizeof(double) * c->n, hipMemcpyDeviceToHost,
                          c->stream) != hipSuccess)
         rc = fail(LFE_EHIP, "copy out failed");
-    hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream);
   }
   dfree(d);
   if (n_out) *n_out = c->n;

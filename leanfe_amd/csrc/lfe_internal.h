@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/leanfe_hip.h"
@@ -15,7 +16,12 @@ namespace lfe {
 
 constexpr int kMaxFE = 8;        // FE dimensions supported per regression
 constexpr int kMaxCols = 63;     // p = 1 + k (+ instruments) <= 63 -> Gram width <= 64
-constexpr int kBlock = 256;      // threads per workgroup for streaming kernels (4 waves)
+constexpr int kBlock = 256;      // threads per workgroup for simple streaming kernels
+constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
+constexpr int kMaxGroupCols = 16;    // columns per column group in a sweep
+constexpr int kLdsBudget = 64 * 1024;  // bytes of LDS tables per sweep workgroup (2 WG per CU)
+constexpr int kItemRows = 65536;     // rows per work item (a bucket is split into items)
+constexpr int kLdsHistMax = 16384;   // int32 counters in an LDS histogram
 
 void set_error(const std::string& msg);
 
@@ -37,36 +43,31 @@ void set_error(const std::string& msg);
 // Per-FE device state.  Group tables are row-major [G][p] so that the p values
 // of one group are contiguous (one 8*p-byte gather per row and FE).
 struct FeState {
-  int32_t G = 0;             // n_levels
-  int32_t* code = nullptr;   // [ld] int32 codes (context-owned)
+  int32_t G = 0;               // n_levels
+  int32_t* code = nullptr;     // [ld] input codes (context-owned copy, input row order)
   int32_t* cnt_pre = nullptr;  // [G] pre-filter counts
+  int32_t* drops = nullptr;    // [G] dropped-row counts (singleton filter)
   int32_t* cnt = nullptr;      // [G] kept counts
-  double* W = nullptr;         // [G] sum of weights (or counts) over kept rows
-  double* S = nullptr;         // [G*p] sum_{i in g} w_i x_i  (constant)
+  double* W = nullptr;         // [G] sum of weights over kept rows (weighted fits only)
+  double* S = nullptr;         // [G*p] sum_{i in g} w_i x_i  (constant per solve)
+  double* Sy = nullptr;        // [G] unweighted sum of y (weighted fits; the check is unweighted)
   double* T = nullptr;         // [G*p] cross term of the current projection
-  double* alpha = nullptr;     // [G*p] accumulated group effect (the "subtracted mean")
-  double* R = nullptr;         // [G] check sums (unweighted y residual)
+  double* alpha = nullptr;     // [G*p] group effect subtracted so far
+  double* R = nullptr;         // [G] check cross term (y column, unweighted)
   int32_t dims = 0, card = 0;
-};
-
-// Kernel-argument bundle (passed by value) describing all FEs.
-struct FeArgs {
-  int F;
-  int p;
-  const int32_t* code[kMaxFE];
-  const double* alpha[kMaxFE];
 };
 
 // kernel ids for per-launch event timing (lfe_profile / lfe_kernel_stats)
 enum KernelId {
-  K_COUNT_PRE = 0, K_KEEP, K_GROUP_SUMS, K_CROSS_SUMS, K_FINALIZE, K_CHECK_SUMS, K_CHECK_MAX, K_GRAM_DESIGN,
-  K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_COUNT_NONZERO, K_SYNTH, K_NUM_KERNELS
+  K_PART_HIST = 0, K_SCAN, K_PART_SCATTER, K_COUNT, K_MARK, K_GROUP_SUMS, K_CROSS, K_CHECK, K_FINALIZE,
+  K_CHECK_MAX, K_GRAM_DESIGN, K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_MISC, K_SYNTH,
+  K_NUM_KERNELS
 };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 
 struct Prof {
   bool on = false;
-  std::vector<hipEvent_t> pool;        // free events
+  std::vector<hipEvent_t> pool;  // free events
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   double total_ms[K_NUM_KERNELS] = {0};
   int64_t count[K_NUM_KERNELS] = {0};
@@ -78,25 +79,49 @@ struct Timings {
   double prep = 0, demean = 0, gram = 0, resid = 0, cluster = 0, last = 0;
 };
 
+// Row layout used by every pass after the singleton drop: rows grouped by
+// buckets of the primary (highest-cardinality) FE, bucket b holding codes
+// [b << s, (b+1) << s).  Work item = contiguous row range inside one bucket.
+struct Layout {
+  int P = -1;          // primary FE (-1: no FE)
+  int s = 0;           // bucket shift
+  int nb = 1;          // buckets
+  bool permuted = false;
+  double* X = nullptr;          // [p][ld] (aliases input when !permuted)
+  double* w = nullptr;          // [ld] or nullptr
+  int32_t* code[kMaxFE] = {};   // per FE, bucket order; code[P][i] = -1 marks a dropped row
+  int32_t* orig = nullptr;      // [ld] input row index of each layout row (nullptr = identity)
+  int n_items = 0;
+  std::vector<int32_t> hitems;  // host copy of the work items
+  std::vector<int32_t> bstart;  // host [nb + 1]
+};
+
 }  // namespace lfe
 
 struct lfe_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // data (row shard)
+  // data (row shard, input order)
   int64_t n = 0;      // rows in this shard
   int64_t ld = 0;     // leading dimension of column storage (n rounded up)
   int p = 0;          // columns: y + x (+ instruments)
   int F = 0;
   double* X = nullptr;       // [p][ld]
   double* w = nullptr;       // [ld] or nullptr
-  uint8_t* keep = nullptr;   // [ld]
   std::vector<lfe::FeState> fe;
-  // clusters
+  // layout (bucket order) storage
+  lfe::Layout L;
+  double* Xp = nullptr;          // [p][ld] permuted columns
+  double* wp = nullptr;          // [ld] permuted weights
+  int32_t* codes_p = nullptr;    // [F][ld] permuted / working codes
+  int32_t* origp = nullptr;      // [ld]
+  int32_t* items_d = nullptr;    // device work items [n_items][4]
+  size_t items_cap = 0;
+  // clusters (input row order)
   std::vector<int32_t*> cl;
   std::vector<int32_t> cl_levels;
-  double* scores = nullptr;  // [k][ld] x~ r (w)
+  double* scores = nullptr;  // [k][ld] x~ r (w), layout order
   double* dbeta = nullptr;   // [64] beta_full staging
   bool scores_valid = false;
   // scratch
@@ -104,10 +129,16 @@ struct lfe_ctx {
   size_t scratch_elems = 0;
   double* dred = nullptr;        // device reduced output (small)
   size_t dred_elems = 0;
-  double* hpinned = nullptr;     // pinned host staging
-  size_t hpinned_elems = 0;
   int32_t* iscratch = nullptr;   // device int scratch
   size_t iscratch_elems = 0;
+  int32_t* pcounts = nullptr;    // partition histogram matrix / scan
+  size_t pcounts_elems = 0;
+  int32_t* psums = nullptr;      // scan block sums
+  size_t psums_elems = 0;
+  double* clS = nullptr;         // cluster score table [C][k]
+  size_t clS_elems = 0;
+  int32_t* clP = nullptr;        // cluster presence flags [C] + counter
+  size_t clP_elems = 0;
   // state
   int64_t n_kept = 0;
   bool loaded = false, prepared = false, demeaned = false;
@@ -120,19 +151,20 @@ struct lfe_ctx {
 
 namespace lfe {
 
-// --- launchers (lfe_kernels.hip) ---
-int launch_count_pre(lfe_ctx* c);
-int launch_keep(lfe_ctx* c);
-int launch_group_sums(lfe_ctx* c);
-int launch_cross_sums(lfe_ctx* c, int f);
-int launch_finalize(lfe_ctx* c, int f);
-int launch_check(lfe_ctx* c, double* host_max);
+// --- prep / partition (lfe_prep.hip) ---
+int prepare_layout(lfe_ctx* c);   // partition + counts + singleton marks
+
+// --- sweeps (lfe_sweep.hip) ---
+int sweep_group_sums(lfe_ctx* c);
+int sweep_project(lfe_ctx* c, int f);
+int sweep_check(lfe_ctx* c, double* host_max);
+
+// --- Gram / residual / clusters (lfe_gram.hip) ---
 int launch_gram(lfe_ctx* c, double* host_gram);
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores);
 int launch_cluster(lfe_ctx* c, double* meats, int64_t* G_out);
-int launch_count_dims(lfe_ctx* c, int32_t* dims, int32_t* card);
-int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* flag, hipStream_t s);
 int launch_copy_demeaned(lfe_ctx* c, double* dev_out);
+int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* flag, hipStream_t s);
 
 // --- synthetic panel (lfe_synth.hip) ---
 int launch_synth(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed,
@@ -141,12 +173,13 @@ int launch_synth(lfe_ctx* c, int k, const int32_t* levels, const double* beta, u
 // --- helpers (lfe_capi.hip) ---
 int ensure_scratch(lfe_ctx* c, size_t elems);
 int ensure_dred(lfe_ctx* c, size_t elems);
-int ensure_pinned(lfe_ctx* c, size_t elems);
 int ensure_iscratch(lfe_ctx* c, size_t elems);
+int ensure_pcounts(lfe_ctx* c, size_t elems, size_t sums);
+int ensure_items(lfe_ctx* c, size_t n_items);
+int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems);
 int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count);
 int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count);
 int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count);
-FeArgs fe_args(const lfe_ctx* c);
 void prof_begin(lfe_ctx* c, int kid);
 void prof_end(lfe_ctx* c);
 int prof_fold(lfe_ctx* c);
@@ -164,5 +197,16 @@ inline int grid_for(int64_t n, int block = kBlock, int cap = 256 * 8) {
   if (g > cap) g = cap;
   return (int)g;
 }
+
+// What every sweep / Gram kernel needs to evaluate x~_i = x_i - sum_f alpha_f[g_f(i)]
+// on the layout: codes in layout order, alpha tables, primary FE bucket geometry.
+struct LayoutArgs {
+  int F, p, P, s;
+  const int32_t* code[kMaxFE];
+  const double* alpha[kMaxFE];
+  const int4* items;
+  int n_items;
+};
+LayoutArgs layout_args(const lfe_ctx* c);
 
 }  // namespace lfe

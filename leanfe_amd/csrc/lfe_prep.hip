@@ -1,0 +1,430 @@
+// leanfe HIP engine — row layout + singleton drop (polars_impl.py:477-482).
+//
+// Every later pass runs on a bucketed row layout: rows are grouped by
+// buckets of the primary (highest-cardinality) FE P, bucket b holding the
+// codes [b << s, (b+1) << s).  A group table slice of one bucket (2^s groups x
+// a few columns) then fits in LDS, so group sums over P become LDS-privatised
+// reductions instead of global atomics over a G_P x p table.
+//
+// Partition = stable counting sort by bucket, one wavefront per row chunk:
+//   k_part_hist    per-wave bucket histogram -> counts[bucket][wave]
+//   scan           exclusive scan of counts (bucket-major) -> destinations
+//   k_part_scatter per-wave LDS cursors; rows written to their bucket slot
+// Within one wave instruction same-bucket lanes are ranked by an LDS atomic,
+// so the layout does not depend on inter-wave timing.
+#include "lfe_internal.h"
+
+#include <algorithm>
+
+namespace lfe {
+
+#define GRID_STRIDE(i, n)                                                      \
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n);   \
+       i += (int64_t)gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------------------
+// histograms
+// ---------------------------------------------------------------------------
+
+// LDS-privatised histogram for G <= kLdsHistMax; flush of non-zero bins
+__global__ __launch_bounds__(256) void k_hist_lds(const int32_t* __restrict__ code, int64_t n, int32_t G,
+                                                  int32_t* __restrict__ cnt) {
+  extern __shared__ int32_t h[];
+  for (int g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
+  __syncthreads();
+  GRID_STRIDE(i, n) atomicAdd(&h[code[i]], 1);
+  __syncthreads();
+  for (int g = threadIdx.x; g < G; g += blockDim.x)
+    if (h[g]) atomicAdd(&cnt[g], h[g]);
+}
+
+__global__ void k_hist_global(const int32_t* __restrict__ code, int64_t n, int32_t* __restrict__ cnt) {
+  GRID_STRIDE(i, n) atomicAdd(&cnt[code[i]], 1);
+}
+
+// per-wave bucket histogram; one wavefront per block, rows [w*cw, (w+1)*cw)
+__global__ __launch_bounds__(64) void k_part_hist(const int32_t* __restrict__ code, int64_t n, int s, int nb,
+                                                  int64_t cw, int nw, int32_t* __restrict__ counts) {
+  extern __shared__ int32_t h[];
+  const int w = blockIdx.x, lane = threadIdx.x;
+  for (int b = lane; b < nb; b += 64) h[b] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)w * cw, r1 = min(n, r0 + cw);
+  for (int64_t i = r0 + lane; i < r1; i += 64) atomicAdd(&h[code[i] >> s], 1);
+  __syncthreads();
+  for (int b = lane; b < nb; b += 64) counts[(int64_t)b * nw + w] = h[b];
+}
+
+// ---------------------------------------------------------------------------
+// exclusive scan of int32 (3 kernels: block scan, scan of block sums, add)
+// ---------------------------------------------------------------------------
+
+constexpr int kScanPer = 8;                 // elements per thread
+constexpr int kScanBlock = 256 * kScanPer;  // elements per block
+
+__device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t* tmp, int32_t* total) {
+  // wave inclusive scan
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int32_t x = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    int32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) tmp[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t acc = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+      int32_t t = tmp[k];
+      tmp[k] = acc;
+      acc += t;
+    }
+    *total = acc;
+  }
+  __syncthreads();
+  return x - v + tmp[wave];
+}
+
+__global__ __launch_bounds__(256) void k_scan_blocks(int32_t* __restrict__ a, int64_t m, int32_t* __restrict__ sums) {
+  __shared__ int32_t tmp[8];
+  __shared__ int32_t total;
+  const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+  int32_t v[kScanPer];
+  int32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    v[k] = (base + k < m) ? a[base + k] : 0;
+    s += v[k];
+  }
+  int32_t off = block_excl_scan(s, tmp, &total);
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (base + k < m) a[base + k] = off;
+    off += v[k];
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_top(int32_t* __restrict__ sums, int nblocks) {
+  __shared__ int32_t tmp[16];
+  __shared__ int32_t total;
+  int32_t carry = 0;
+  for (int base = 0; base < nblocks; base += blockDim.x) {
+    const int i = base + threadIdx.x;
+    const int32_t v = i < nblocks ? sums[i] : 0;
+    const int32_t ex = block_excl_scan(v, tmp, &total);
+    if (i < nblocks) sums[i] = ex + carry;
+    __syncthreads();
+    carry += total;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(int32_t* __restrict__ a, int64_t m, const int32_t* __restrict__ sums) {
+  const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+  const int32_t add = sums[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k)
+    if (base + k < m) a[base + k] += add;
+}
+
+static int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) {
+  const int64_t nblocks = (m + kScanBlock - 1) / kScanBlock;
+  LFE_TRY(ensure_pcounts(c, 0, (size_t)nblocks + 1));
+  ProfScope _ps(c, K_SCAN);
+  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nblocks), dim3(256), 0, c->stream, a, m, c->psums);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, c->psums, (int)nblocks);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nblocks), dim3(256), 0, c->stream, a, m, c->psums);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// partition scatter
+// ---------------------------------------------------------------------------
+
+struct ScatterArgs {
+  int p, F, P, s, nb, nw;
+  int64_t cw, n, ld;
+  const double* X;
+  const double* w;
+  const int32_t* code[kMaxFE];
+  double* Xo;
+  double* wo;
+  int32_t* codeo[kMaxFE];
+  int32_t* orig;
+  const int32_t* scanned;  // [nb][nw] exclusive destinations
+};
+
+__global__ __launch_bounds__(64) void k_part_scatter(ScatterArgs a) {
+  extern __shared__ int32_t cur[];
+  const int w = blockIdx.x, lane = threadIdx.x;
+  for (int b = lane; b < a.nb; b += 64) cur[b] = a.scanned[(int64_t)b * a.nw + w];
+  __syncthreads();
+  const int64_t r0 = (int64_t)w * a.cw, r1 = min(a.n, r0 + a.cw);
+  for (int64_t i0 = r0; i0 < r1; i0 += 64) {
+    const int64_t i = i0 + lane;
+    if (i < r1) {
+      const int32_t b = a.code[a.P][i] >> a.s;
+      const int64_t pos = atomicAdd(&cur[b], 1);
+      for (int c = 0; c < a.p; ++c) a.Xo[(int64_t)c * a.ld + pos] = a.X[(int64_t)c * a.ld + i];
+      if (a.w) a.wo[pos] = a.w[i];
+      for (int f = 0; f < a.F; ++f) a.codeo[f][pos] = a.code[f][i];
+      a.orig[pos] = (int32_t)i;
+    }
+  }
+}
+
+__global__ void k_gather_bstart(const int32_t* __restrict__ scanned, int nb, int nw, int32_t* __restrict__ out) {
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x)
+    out[b] = scanned[(int64_t)b * nw];
+}
+
+// ---------------------------------------------------------------------------
+// counts on the layout + singleton marks
+// ---------------------------------------------------------------------------
+
+// primary-FE counts: per work item an LDS slice of 2^s bins
+__global__ __launch_bounds__(256) void k_count_items(const int4* __restrict__ items, const int32_t* __restrict__ code,
+                                                     int s, int32_t G, int32_t* __restrict__ cnt) {
+  extern __shared__ int32_t h[];
+  const int4 it = items[blockIdx.x];
+  const int B = 1 << s;
+  for (int j = threadIdx.x; j < B; j += blockDim.x) h[j] = 0;
+  __syncthreads();
+  const int32_t lo = it.x << s;
+  for (int64_t i = it.y + threadIdx.x; i < it.z; i += blockDim.x) atomicAdd(&h[code[i] - lo], 1);
+  __syncthreads();
+  for (int j = threadIdx.x; j < B; j += blockDim.x)
+    if (h[j] && lo + j < G) atomicAdd(&cnt[lo + j], h[j]);
+}
+
+struct MarkArgs {
+  int F, P;
+  int32_t* code[kMaxFE];
+  const int32_t* cnt_pre[kMaxFE];
+  int32_t* drops[kMaxFE];
+  int32_t* ndropped;
+};
+
+__global__ void k_mark(MarkArgs a, int64_t n) {
+  GRID_STRIDE(i, n) {
+    bool ok = true;
+    int32_t g[kMaxFE];
+    for (int f = 0; f < a.F; ++f) {
+      g[f] = a.code[f][i];
+      ok = ok && (a.cnt_pre[f][g[f]] > 1);
+    }
+    if (!ok) {
+      for (int f = 0; f < a.F; ++f) atomicAdd(&a.drops[f][g[f]], 1);
+      a.code[a.P][i] = -1;
+      atomicAdd(a.ndropped, 1);
+    }
+  }
+}
+
+__global__ void k_sub_counts(const int32_t* __restrict__ pre, const int32_t* __restrict__ drops, int32_t G,
+                             int32_t* __restrict__ cnt) {
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) cnt[g] = pre[g] - drops[g];
+}
+
+__global__ void k_count_nonzero2(const int32_t* __restrict__ a, const int32_t* __restrict__ b, int32_t G,
+                                 int32_t* __restrict__ out) {
+  int la = 0, lb = 0;
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+    la += a[g] > 0;
+    lb += b[g] > 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    la += __shfl_down(la, off, 64);
+    lb += __shfl_down(lb, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (la) atomicAdd(&out[0], la);
+    if (lb) atomicAdd(&out[1], lb);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// driver
+// ---------------------------------------------------------------------------
+
+static int choose_shift(int32_t G) {
+  int s = 0;
+  while ((1ll << s) < G && s < 8) ++s;       // small FE: one bucket
+  if ((1ll << s) >= G) return s;
+  s = 8;                                       // 256 groups per bucket slice
+  while (((int64_t)G + (1ll << s) - 1) >> s > 8192) ++s;  // <= 8192 buckets
+  return s;
+}
+
+static int build_items(lfe_ctx* c) {
+  auto& L = c->L;
+  L.hitems.clear();
+  for (int b = 0; b < L.nb; ++b) {
+    const int32_t lo = L.bstart[b], hi = L.bstart[b + 1];
+    const int32_t len = hi - lo;
+    if (len <= 0) continue;
+    const int32_t k = (len + kItemRows - 1) / kItemRows;
+    for (int32_t q = 0; q < k; ++q) {
+      const int32_t r0 = lo + (int32_t)((int64_t)len * q / k), r1 = lo + (int32_t)((int64_t)len * (q + 1) / k);
+      L.hitems.insert(L.hitems.end(), {b, r0, r1, 0});
+    }
+  }
+  if (L.hitems.empty()) L.hitems.insert(L.hitems.end(), {0, 0, 0, 0});
+  L.n_items = (int)(L.hitems.size() / 4);
+  LFE_TRY(ensure_items(c, L.n_items));
+  LFE_HIP(hipMemcpyAsync(c->items_d, L.hitems.data(), sizeof(int32_t) * L.hitems.size(), hipMemcpyHostToDevice,
+                         c->stream));
+  return LFE_OK;
+}
+
+int prepare_layout(lfe_ctx* c) {
+  auto& L = c->L;
+  const int64_t n = c->n;
+  // primary FE: most levels (ties -> first)
+  L.P = -1;
+  for (int f = 0; f < c->F; ++f)
+    if (L.P < 0 || c->fe[f].G > c->fe[L.P].G) L.P = f;
+  L.s = L.P >= 0 ? choose_shift(c->fe[L.P].G) : 0;
+  L.nb = L.P >= 0 ? (int)(((int64_t)c->fe[L.P].G + (1ll << L.s) - 1) >> L.s) : 1;
+  L.permuted = L.nb > 1 && n > 0;
+
+  // pre-filter counts of every FE (on input codes, except P when bucketed)
+  for (int f = 0; f < c->F; ++f) {
+    auto& fe = c->fe[f];
+    LFE_HIP(hipMemsetAsync(fe.cnt_pre, 0, sizeof(int32_t) * fe.G, c->stream));
+    if (n == 0 || (f == L.P && L.permuted)) continue;
+    ProfScope _ps(c, K_COUNT);
+    if (fe.G <= kLdsHistMax)
+      hipLaunchKernelGGL(k_hist_lds, dim3(grid_for(n, 256, 512)), dim3(256), sizeof(int32_t) * fe.G, c->stream,
+                         fe.code, n, fe.G, fe.cnt_pre);
+    else
+      hipLaunchKernelGGL(k_hist_global, dim3(grid_for(n)), dim3(kBlock), 0, c->stream, fe.code, n, fe.cnt_pre);
+    LFE_HIP(hipGetLastError());
+  }
+
+  if (L.permuted) {
+    // ---- partition by bucket of P ----
+    const int nb = L.nb;
+    int64_t cw = 4096;
+    while ((int64_t)nb * ((n + cw - 1) / cw) > (16ll << 20)) cw *= 2;
+    const int nw = (int)((n + cw - 1) / cw);
+    const int64_t m = (int64_t)nb * nw;
+    LFE_TRY(ensure_pcounts(c, (size_t)m + nb + 1, 0));
+    {
+      ProfScope _ps(c, K_PART_HIST);
+      hipLaunchKernelGGL(k_part_hist, dim3(nw), dim3(64), sizeof(int32_t) * nb, c->stream, c->fe[L.P].code, n, L.s,
+                         nb, cw, nw, c->pcounts);
+    }
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(exclusive_scan(c, c->pcounts, m));
+    ScatterArgs a{};
+    a.p = c->p;
+    a.F = c->F;
+    a.P = L.P;
+    a.s = L.s;
+    a.nb = nb;
+    a.nw = nw;
+    a.cw = cw;
+    a.n = n;
+    a.ld = c->ld;
+    a.X = c->X;
+    a.w = c->w;
+    a.Xo = c->Xp;
+    a.wo = c->wp;
+    for (int f = 0; f < c->F; ++f) {
+      a.code[f] = c->fe[f].code;
+      a.codeo[f] = c->codes_p + (size_t)f * c->ld;
+    }
+    a.orig = c->origp;
+    a.scanned = c->pcounts;
+    {
+      ProfScope _ps(c, K_PART_SCATTER);
+      hipLaunchKernelGGL(k_part_scatter, dim3(nw), dim3(64), sizeof(int32_t) * nb, c->stream, a);
+    }
+    LFE_HIP(hipGetLastError());
+    int32_t* dbstart = c->pcounts + m;
+    hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(nb)), dim3(kBlock), 0, c->stream, c->pcounts, nb, nw, dbstart);
+    LFE_HIP(hipGetLastError());
+    L.bstart.assign(nb + 1, 0);
+    LFE_HIP(hipMemcpyAsync(L.bstart.data(), dbstart, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->stream));
+    LFE_HIP(hipStreamSynchronize(c->stream));
+    L.bstart[nb] = (int32_t)n;
+    L.X = c->Xp;
+    L.w = c->w ? c->wp : nullptr;
+    for (int f = 0; f < c->F; ++f) L.code[f] = c->codes_p + (size_t)f * c->ld;
+    L.orig = c->origp;
+  } else {
+    L.bstart = {0, (int32_t)n};
+    L.X = c->X;
+    L.w = c->w;
+    for (int f = 0; f < c->F; ++f) {
+      L.code[f] = c->codes_p + (size_t)f * c->ld;
+      if (n) LFE_HIP(hipMemcpyAsync(L.code[f], c->fe[f].code, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, c->stream));
+    }
+    L.orig = nullptr;
+  }
+  LFE_TRY(build_items(c));
+
+  if (L.permuted) {
+    ProfScope _ps(c, K_COUNT);
+    auto& fe = c->fe[L.P];
+    hipLaunchKernelGGL(k_count_items, dim3(L.n_items), dim3(256), sizeof(int32_t) << L.s, c->stream,
+                       reinterpret_cast<const int4*>(c->items_d), L.code[L.P], L.s, fe.G, fe.cnt_pre);
+    LFE_HIP(hipGetLastError());
+  }
+  for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt_pre, c->fe[f].G));
+
+  // ---- single-pass singleton drop: mark, then kept counts = pre - drops ----
+  LFE_TRY(ensure_iscratch(c, 2 * kMaxFE + 8));
+  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t) * (2 * kMaxFE + 8), c->stream));
+  int32_t* ndropped = c->iscratch + 2 * kMaxFE;
+  if (c->F > 0) {
+    MarkArgs a{};
+    a.F = c->F;
+    a.P = L.P;
+    for (int f = 0; f < c->F; ++f) {
+      auto& fe = c->fe[f];
+      LFE_HIP(hipMemsetAsync(fe.drops, 0, sizeof(int32_t) * fe.G, c->stream));
+      a.code[f] = L.code[f];
+      a.cnt_pre[f] = fe.cnt_pre;
+      a.drops[f] = fe.drops;
+    }
+    a.ndropped = ndropped;
+    if (n) {
+      ProfScope _ps(c, K_MARK);
+      hipLaunchKernelGGL(k_mark, dim3(grid_for(n)), dim3(kBlock), 0, c->stream, a, n);
+    }
+    LFE_HIP(hipGetLastError());
+    for (int f = 0; f < c->F; ++f) {
+      auto& fe = c->fe[f];
+      LFE_TRY(allreduce_sum_i32(c, fe.drops, fe.G));
+      hipLaunchKernelGGL(k_sub_counts, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, fe.cnt_pre, fe.drops, fe.G,
+                         fe.cnt);
+      hipLaunchKernelGGL(k_count_nonzero2, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, fe.cnt, fe.cnt_pre,
+                         fe.G, c->iscratch + 2 * f);
+      LFE_HIP(hipGetLastError());
+    }
+  }
+  int32_t h[2 * kMaxFE + 8];
+  LFE_HIP(hipMemcpyAsync(h, c->iscratch, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  for (int f = 0; f < c->F; ++f) {
+    c->fe[f].dims = h[2 * f];
+    c->fe[f].card = h[2 * f + 1];
+  }
+  // kept rows over all ranks
+  double kept = (double)(n - h[2 * kMaxFE]);
+  if (c->world > 1) {
+    LFE_TRY(ensure_dred(c, 1));
+    LFE_HIP(hipMemcpyAsync(c->dred, &kept, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    LFE_TRY(allreduce_sum_f64(c, c->dred, 1));
+    LFE_HIP(hipMemcpyAsync(&kept, c->dred, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    LFE_HIP(hipStreamSynchronize(c->stream));
+  }
+  c->n_kept = (int64_t)kept;
+  return LFE_OK;
+}
+
+}  // namespace lfe

@@ -78,7 +78,7 @@ int launch_synth(lfe_ctx* c, int k, const int32_t* levels, const double* beta, u
   for (int f = 0; f < c->F; ++f) {
     a.L[f] = levels[f];
     a.code[f] = c->fe[f].code;
-    LFE_HIP(hipMallocAsync(&eff[f], sizeof(double) * (size_t)levels[f], c->stream));
+    LFE_HIP(hipMalloc(&eff[f], sizeof(double) * (size_t)levels[f]));
     hipLaunchKernelGGL(k_synth_effects, dim3(grid_for(levels[f])), dim3(kBlock), 0, c->stream, eff[f], levels[f],
                        f, scale, seed);
     LFE_HIP(hipGetLastError());
@@ -90,7 +90,8 @@ int launch_synth(lfe_ctx* c, int k, const int32_t* levels, const double* beta, u
     hipLaunchKernelGGL(k_synth_rows, dim3(grid_for(c->n, kBlock, 256 * 16)), dim3(kBlock), 0, c->stream, a, c->X,
                        c->ld, c->n, seed, row_offset);
   LFE_HIP(hipGetLastError());
-  for (int f = 0; f < c->F; ++f) LFE_HIP(hipFreeAsync(eff[f], c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  for (int f = 0; f < c->F; ++f) LFE_HIP(hipFree(eff[f]));
   return LFE_OK;
 }
 
