@@ -285,6 +285,9 @@ static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
   const size_t dyn = a.stage ? sbytes : 0;
   {
     ProfScope _ps(c, MODE == GRAM_DESIGN ? K_GRAM_DESIGN : (MODE == GRAM_RESID ? K_GRAM_RESID : K_GRAM_TABLE));
+    if (dyn > 0)  // dynamic LDS above 64 KB must be opted in
+      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gram<MODE, NT>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
     hipLaunchKernelGGL((k_gram<MODE, NT>), dim3(nblocks), dim3(kTR), dyn, c->stream, a, c->scratch, pstride);
   }
   LFE_HIP(hipGetLastError());

@@ -42,17 +42,17 @@ __global__ void k_hist_global(const int32_t* __restrict__ code, int64_t n, int32
   GRID_STRIDE(i, n) atomicAdd(&cnt[code[i]], 1);
 }
 
-// per-wave bucket histogram; one wavefront per block, rows [w*cw, (w+1)*cw)
-__global__ __launch_bounds__(64) void k_part_hist(const int32_t* __restrict__ code, int64_t n, int s, int nb,
-                                                  int64_t cw, int nw, int32_t* __restrict__ counts) {
+// per-chunk bucket histogram, chunk = rows [w*cw, (w+1)*cw) -> counts[bucket][chunk]
+__global__ __launch_bounds__(256) void k_part_hist(const int32_t* __restrict__ code, int64_t n, int s, int nb,
+                                                   int64_t cw, int nw, int32_t* __restrict__ counts) {
   extern __shared__ int32_t h[];
-  const int w = blockIdx.x, lane = threadIdx.x;
-  for (int b = lane; b < nb; b += 64) h[b] = 0;
+  const int w = blockIdx.x;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)w * cw, r1 = min(n, r0 + cw);
-  for (int64_t i = r0 + lane; i < r1; i += 64) atomicAdd(&h[code[i] >> s], 1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) atomicAdd(&h[code[i] >> s], 1);
   __syncthreads();
-  for (int b = lane; b < nb; b += 64) counts[(int64_t)b * nw + w] = h[b];
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) counts[(int64_t)b * nw + w] = h[b];
 }
 
 // ---------------------------------------------------------------------------
@@ -143,9 +143,19 @@ static int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) {
 // partition scatter
 // ---------------------------------------------------------------------------
 
+// LDS-staged scatter.  A workgroup owns a chunk of kPartThreads*PER rows
+// (wave w: PER*64 consecutive rows).  It ranks its rows by bucket in LDS
+// (per-wave cursors: an LDS atomic ranks same-bucket lanes of one wave
+// instruction; waves own disjoint cursor ranges, so ranks do not depend on
+// wave timing), then moves every column through an LDS stage in bucket order,
+// so consecutive threads write consecutive addresses of one bucket run
+// (~chunk/nb rows per run) instead of 8-byte scatters.
+constexpr int kPartThreads = 512;
+constexpr int kPartWaves = kPartThreads / 64;
+
 struct ScatterArgs {
-  int p, F, P, s, nb, nw;
-  int64_t cw, n, ld;
+  int p, F, P, s, nb, nchunks;
+  int64_t n, ld;
   const double* X;
   const double* w;
   const int32_t* code[kMaxFE];
@@ -153,25 +163,116 @@ struct ScatterArgs {
   double* wo;
   int32_t* codeo[kMaxFE];
   int32_t* orig;
-  const int32_t* scanned;  // [nb][nw] exclusive destinations
+  const int32_t* scanned;  // [nb][nchunks] exclusive destinations
 };
 
-__global__ __launch_bounds__(64) void k_part_scatter(ScatterArgs a) {
-  extern __shared__ int32_t cur[];
-  const int w = blockIdx.x, lane = threadIdx.x;
-  for (int b = lane; b < a.nb; b += 64) cur[b] = a.scanned[(int64_t)b * a.nw + w];
+template <int PER>
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
+  constexpr int R = kPartThreads * PER;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* stage = smem;                                        // [R] (doubles or int32)
+  int32_t* sb = reinterpret_cast<int32_t*>(stage + R);         // [R] bucket of sorted slot
+  int32_t* cur = sb + R;                                       // [waves][nb] cursors
+  int32_t* delta = cur + kPartWaves * a.nb;                    // [nb]
+  int32_t* tot = delta + a.nb;                                 // [nb + 1]
+  __shared__ int32_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int chunk = blockIdx.x;
+  const int64_t r0 = (int64_t)chunk * R, r1 = min(a.n, r0 + R);
+  const int64_t wbase = r0 + (int64_t)wave * PER * 64;
+  for (int j = tid; j < kPartWaves * a.nb; j += kPartThreads) cur[j] = 0;
   __syncthreads();
-  const int64_t r0 = (int64_t)w * a.cw, r1 = min(a.n, r0 + a.cw);
-  for (int64_t i0 = r0; i0 < r1; i0 += 64) {
-    const int64_t i = i0 + lane;
-    if (i < r1) {
-      const int32_t b = a.code[a.P][i] >> a.s;
-      const int64_t pos = atomicAdd(&cur[b], 1);
-      for (int c = 0; c < a.p; ++c) a.Xo[(int64_t)c * a.ld + pos] = a.X[(int64_t)c * a.ld + i];
-      if (a.w) a.wo[pos] = a.w[i];
-      for (int f = 0; f < a.F; ++f) a.codeo[f][pos] = a.code[f][i];
-      a.orig[pos] = (int32_t)i;
+  int32_t bk[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int64_t i = wbase + k * 64 + lane;
+    bk[k] = i < r1 ? (a.code[a.P][i] >> a.s) : -1;
+    if (bk[k] >= 0) atomicAdd(&cur[wave * a.nb + bk[k]], 1);
+  }
+  __syncthreads();
+  // per bucket: exclusive scan over waves, total
+  for (int b = tid; b < a.nb; b += kPartThreads) {
+    int32_t t = 0;
+    for (int w2 = 0; w2 < kPartWaves; ++w2) {
+      const int32_t h = cur[w2 * a.nb + b];
+      cur[w2 * a.nb + b] = t;
+      t += h;
     }
+    tot[b] = t;
+  }
+  __syncthreads();
+  // exclusive scan of tot over buckets (one thread per PERB buckets, then waves)
+  {
+    const int per = (a.nb + kPartThreads - 1) / kPartThreads;
+    const int b0 = tid * per;
+    int32_t s = 0;
+    for (int q = 0; q < per; ++q)
+      if (b0 + q < a.nb) s += tot[b0 + q];
+    int32_t x = s;  // wave inclusive scan
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int32_t wofs = 0;
+    for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[w2];
+    int32_t run = x - s + wofs;
+    __syncthreads();
+    for (int q = 0; q < per; ++q)
+      if (b0 + q < a.nb) {
+        const int32_t t = tot[b0 + q];
+        tot[b0 + q] = run;  // now: local offset of bucket
+        run += t;
+      }
+  }
+  __syncthreads();
+  for (int b = tid; b < a.nb; b += kPartThreads) {
+    const int32_t boff = tot[b];
+    delta[b] = a.scanned[(int64_t)b * a.nchunks + chunk] - boff;
+    for (int w2 = 0; w2 < kPartWaves; ++w2) cur[w2 * a.nb + b] += boff;
+  }
+  __syncthreads();
+  int32_t pos[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    pos[k] = -1;
+    if (bk[k] >= 0) {
+      pos[k] = atomicAdd(&cur[wave * a.nb + bk[k]], 1);
+      sb[pos[k]] = bk[k];
+    }
+  }
+  __syncthreads();
+  const int len = (int)(r1 - r0);
+  // ---- move columns through the stage: gather in row order, store in bucket order ----
+  const int ncol = a.p + (a.w ? 1 : 0);
+  for (int c = 0; c < ncol; ++c) {
+    const double* src = c < a.p ? a.X + (int64_t)c * a.ld : a.w;
+    double* dst = c < a.p ? a.Xo + (int64_t)c * a.ld : a.wo;
+    double v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int64_t i = wbase + k * 64 + lane;
+      v[k] = pos[k] >= 0 ? src[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (pos[k] >= 0) stage[pos[k]] = v[k];
+    __syncthreads();
+    for (int j = tid; j < len; j += kPartThreads) dst[delta[sb[j]] + j] = stage[j];
+    __syncthreads();
+  }
+  int32_t* istage = reinterpret_cast<int32_t*>(stage);
+  for (int c = 0; c <= a.F; ++c) {  // F code arrays, then the input row index
+    int32_t* dst = c < a.F ? a.codeo[c] : a.orig;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int64_t i = wbase + k * 64 + lane;
+      if (pos[k] >= 0) istage[pos[k]] = c < a.F ? a.code[c][i] : (int32_t)i;
+    }
+    __syncthreads();
+    for (int j = tid; j < len; j += kPartThreads) dst[delta[sb[j]] + j] = istage[j];
+    __syncthreads();
   }
 }
 
@@ -254,7 +355,7 @@ static int choose_shift(int32_t G) {
   while ((1ll << s) < G && s < 8) ++s;       // small FE: one bucket
   if ((1ll << s) >= G) return s;
   s = 8;                                       // 256 groups per bucket slice
-  while (((int64_t)G + (1ll << s) - 1) >> s > 8192) ++s;  // <= 8192 buckets
+  while (((int64_t)G + (1ll << s) - 1) >> s > 2048) ++s;  // <= 2048 buckets (LDS cursors of the scatter)
   return s;
 }
 
@@ -307,14 +408,14 @@ int prepare_layout(lfe_ctx* c) {
   if (L.permuted) {
     // ---- partition by bucket of P ----
     const int nb = L.nb;
-    int64_t cw = 4096;
-    while ((int64_t)nb * ((n + cw - 1) / cw) > (16ll << 20)) cw *= 2;
+    const int per = nb <= 512 ? 16 : 8;  // rows per thread of the staged scatter
+    const int64_t cw = (int64_t)kPartThreads * per;
     const int nw = (int)((n + cw - 1) / cw);
     const int64_t m = (int64_t)nb * nw;
     LFE_TRY(ensure_pcounts(c, (size_t)m + nb + 1, 0));
     {
       ProfScope _ps(c, K_PART_HIST);
-      hipLaunchKernelGGL(k_part_hist, dim3(nw), dim3(64), sizeof(int32_t) * nb, c->stream, c->fe[L.P].code, n, L.s,
+      hipLaunchKernelGGL(k_part_hist, dim3(nw), dim3(256), sizeof(int32_t) * nb, c->stream, c->fe[L.P].code, n, L.s,
                          nb, cw, nw, c->pcounts);
     }
     LFE_HIP(hipGetLastError());
@@ -325,8 +426,7 @@ int prepare_layout(lfe_ctx* c) {
     a.P = L.P;
     a.s = L.s;
     a.nb = nb;
-    a.nw = nw;
-    a.cw = cw;
+    a.nchunks = nw;
     a.n = n;
     a.ld = c->ld;
     a.X = c->X;
@@ -340,8 +440,16 @@ int prepare_layout(lfe_ctx* c) {
     a.orig = c->origp;
     a.scanned = c->pcounts;
     {
+      const size_t lds = sizeof(double) * cw + sizeof(int32_t) * (cw + (size_t)kPartWaves * nb + 2 * (size_t)nb + 1);
+      // dynamic LDS above 64 KB must be opted in (static LDS + dynamic <= 160 KB)
+      const void* fn = per == 16 ? reinterpret_cast<const void*>(&k_part_scatter<16>)
+                                 : reinterpret_cast<const void*>(&k_part_scatter<8>);
+      LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       ProfScope _ps(c, K_PART_SCATTER);
-      hipLaunchKernelGGL(k_part_scatter, dim3(nw), dim3(64), sizeof(int32_t) * nb, c->stream, a);
+      if (per == 16)
+        hipLaunchKernelGGL(k_part_scatter<16>, dim3(nw), dim3(kPartThreads), lds, c->stream, a);
+      else
+        hipLaunchKernelGGL(k_part_scatter<8>, dim3(nw), dim3(kPartThreads), lds, c->stream, a);
     }
     LFE_HIP(hipGetLastError());
     int32_t* dbstart = c->pcounts + m;
