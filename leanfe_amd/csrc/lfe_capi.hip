@@ -60,6 +60,8 @@ int ensure_scratch(lfe_ctx* c, size_t elems) { return ensure(c->scratch, c->scra
 int ensure_dred(lfe_ctx* c, size_t elems) { return ensure(c->dred, c->dred_elems, elems); }
 int ensure_iscratch(lfe_ctx* c, size_t elems) { return ensure(c->iscratch, c->iscratch_elems, elems); }
 int ensure_items(lfe_ctx* c, size_t n_items) { return ensure(c->items_d, c->items_cap, 4 * n_items); }
+int ensure_i32(lfe_ctx*, int32_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
+int ensure_f64(lfe_ctx*, double*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 
 int ensure_pcounts(lfe_ctx* c, size_t elems, size_t sums) {
   LFE_TRY(ensure(c->pcounts, c->pcounts_elems, elems));
@@ -295,6 +297,12 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   dfree(c->pcounts);
   dfree(c->psums);
   dfree(c->items_d);
+  dfree(c->bitems_d);
+  dfree(c->seg_off);
+  dfree(c->seg_q);
+  dfree(c->seg_aux);
+  dfree(c->seg_units);
+  dfree(c->alpha_spare);
   dfree(c->dbeta);
   dfree(c->clS);
   dfree(c->clP);
@@ -429,7 +437,10 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
     for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
     if (c->F > 0) {
       LFE_TRY(sweep_group_sums(c));
-      if (check_from <= 0) {
+      if (check_from > 0 && fast_path_ok(c, order)) {
+        // two FEs, unweighted: segment layout + one fused codes-only kernel per sweep
+        LFE_TRY(demean_fast(c, tol, max_iter, check_from, &iterations, &last));
+      } else if (check_from <= 0) {
         // single within-transform pass ('demean' strategy, polars_impl.py:437-465)
         for (int f : order) LFE_TRY(sweep_project(c, f));
         iterations = 1;

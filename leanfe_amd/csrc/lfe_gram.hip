@@ -6,16 +6,16 @@
 //   scores S_c = sum_{i in c} x~_i r_i (w_i) and meat S'S: the one-hot SpMM
 //          W_C'(X.e)                           (std_errors.py:317-336, compress.py:929-942)
 //
-// Every row pass is thread-per-row: a thread loads its row's p columns
-// (coalesced: consecutive threads, consecutive rows), subtracts the group
-// effects (eq. 1 of lfe_sweep.hip; the primary FE's alpha slice for the item's
-// bucket is staged in LDS, other FEs' tables are read through L2) and writes
-// the row into a column-major LDS tile Z[16*NT][kTR + 2].  Each wave then
-// multiplies 64 tile rows into NT(NT+1)/2 16x16 f64 accumulators with
-// v_mfma_f64_16x16x4_f64: lane l supplies A[i=l&15][k=l>>4] = B[k][j=l&15]
-// = Z[16*I + (l&15)][row0 + (l>>4)], result D[(l>>4) + 4r][l&15].
-// The tile stride kTR + 2 doubles keeps both the row-wise writes and the
-// 16-column MFMA operand reads bank-conflict free.
+// "MFMA-native" lane layout.  v_mfma_f64_16x16x4_f64 takes lane l's operand
+// as A[i = l&15][k = l>>4] = B[k][j = l&15]; for a Gram G = Z'Z over 4 rows
+// that is Z[row_k][col], so lane (k = l>>4, c = l&15) owns column c (plus
+// 16*I for wider designs) of rows 16g + 4k + s, s = 0..3 of a 16-row group g.
+// A lane therefore loads its 4 consecutive rows of a column as one 32-byte
+// vector (a 16-row group of a column is one full 128-byte line), gathers the
+// group effects of its column for 4 rows (16 lanes = 16 consecutive doubles
+// of an alpha row), and feeds step s of the MFMA straight from registers: no
+// LDS tile, no barrier per tile, waves run independently.  Only the primary
+// FE's alpha slice for the item's bucket is staged in LDS (once per item).
 #include "lfe_internal.h"
 
 #include <algorithm>
@@ -26,8 +26,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 enum { GRAM_DESIGN = 0, GRAM_RESID = 1, GRAM_TABLE = 2 };
 
-constexpr int kTR = 256;          // tile rows (= threads per workgroup)
-constexpr int kZST = kTR + 2;     // column stride of the LDS tile (doubles)
+constexpr int kGramThreads = 256;  // 4 independent waves
 
 struct GramArgs {
   LayoutArgs la;
@@ -42,39 +41,58 @@ struct GramArgs {
   int B;                // 1 << s
   int G_P;
   int stage;            // 1: the primary FE's alpha slice is staged in LDS per item
+  int nq;               // number of non-primary FEs
+  int qf[kMaxFE];       // their FE indices
 };
 
 template <int NT>
 struct GramShape {
-  static constexpr int ZW = 16 * NT;
   static constexpr int NP = NT * (NT + 1) / 2;
   static constexpr int LEN = NP * 256;
 };
 
-// MFMA over one staged tile: wave w owns tile rows [64w, 64w + 64)
+__device__ __forceinline__ d4 ld4(const double* p) { return *reinterpret_cast<const d4*>(p); }
+__device__ __forceinline__ void st4(double* p, d4 v) { *reinterpret_cast<d4*>(p) = v; }
+
+// one 64-bit DPP lane move (two 32-bit halves)
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// sum over the 16 lanes of a DPP row (quad xor 1, xor 2, half mirror, mirror); all lanes get it
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dppd<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dppd<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dppd<0x141>(v);  // row_half_mirror
+  v += dppd<0x140>(v);  // row_mirror
+  return v;
+}
+
+// z[s][I] -> acc (4 MFMA steps per pair)
 template <int NT>
-__device__ __forceinline__ void tile_mfma(const double* Z, d4* acc, int wave, int lane) {
+__device__ __forceinline__ void mfma_rows(const double (&z)[4][NT], d4* acc) {
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) {
-    const int row = wave * 64 + kk * 4 + (lane >> 4);
-    double av[NT];
-#pragma unroll
-    for (int I = 0; I < NT; ++I) av[I] = Z[(I * 16 + (lane & 15)) * kZST + row];
+  for (int s = 0; s < 4; ++s) {
     int q = 0;
 #pragma unroll
     for (int I = 0; I < NT; ++I)
 #pragma unroll
-      for (int J = I; J < NT; ++J, ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], av[J], acc[q], 0, 0, 0);
+      for (int J = I; J < NT; ++J, ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(z[s][I], z[s][J], acc[q], 0, 0, 0);
   }
 }
 
-template <int MODE, int NT>
-__global__ __launch_bounds__(kTR) void k_gram(GramArgs a, double* __restrict__ partial, int64_t pstride) {
+// MODE: design / resid / table; NT: 16-column slots per lane; FQ: max non-primary FEs;
+// GU: 16-row groups a wave loads before it uses any of them (memory-level parallelism)
+template <int MODE, int NT, int FQ, int GU>
+__global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __restrict__ partial, int64_t pstride) {
   using Sh = GramShape<NT>;
-  __shared__ __attribute__((aligned(16))) double Z[Sh::ZW * kZST];
+  __shared__ double red[Sh::LEN];
   __shared__ double stat_red[4][4];
   extern __shared__ __attribute__((aligned(16))) double slice[];  // [B][p] alpha_P slice of the item's bucket
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kq = lane >> 4, c = lane & 15;
   const int p = a.la.p, P = a.la.P;
 
   d4 acc[Sh::NP];
@@ -83,116 +101,182 @@ __global__ __launch_bounds__(kTR) void k_gram(GramArgs a, double* __restrict__ p
   double st[4] = {0.0, 0.0, 0.0, 0.0};  // sum w r^2, sum r^2, sum y~, sum y~^2
 
   if (MODE == GRAM_TABLE) {
-    const int64_t ntiles = (a.rows + kTR - 1) / kTR;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-      const int64_t i = tile * kTR + tid;
-      const bool valid = i < a.rows;
+    const int64_t ngroups = (a.rows + 15) / 16;
+    for (int64_t gi = (int64_t)blockIdx.x * 4 + wave; gi < ngroups; gi += (int64_t)gridDim.x * 4) {
+      double z[4][NT];
 #pragma unroll
-      for (int c = 0; c < Sh::ZW; ++c) Z[c * kZST + tid] = (valid && c < a.tcols) ? a.table[i * a.tcols + c] : 0.0;
-      __syncthreads();
-      tile_mfma<NT>(Z, acc, wave, lane);
-      __syncthreads();
+      for (int s = 0; s < 4; ++s) {
+        const int64_t r = gi * 16 + kq * 4 + s;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+          const int col = 16 * I + c;
+          z[s][I] = (r < a.rows && col < a.tcols) ? a.table[r * a.tcols + col] : 0.0;
+        }
+      }
+      mfma_rows<NT>(z, acc);
     }
   } else {
-    const int nitems = a.la.n_items;
-    for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    // columns held by this lane: design column col = 16I + c -> data column xc
+    int xc[NT];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+      const int col = 16 * I + c;
+      xc[I] = (MODE == GRAM_DESIGN) ? col - 1 : col;  // DESIGN: col 0 = intercept, col 1 = y
+      if (xc[I] >= p) xc[I] = -2;                       // padding column
+    }
+    // RESID: the 16 lanes of a row quad sum term = y~ (column 0) - beta_j x~_j (columns j >= 1)
+    double coef[NT];
+    if (MODE == GRAM_RESID) {
+#pragma unroll
+      for (int I = 0; I < NT; ++I) coef[I] = xc[I] == 0 ? 1.0 : (xc[I] >= 1 ? -a.beta[xc[I]] : 0.0);
+    }
+    const double beta0 = (MODE == GRAM_RESID) ? a.beta[0] : 0.0;
+    const int nq = a.nq < FQ ? a.nq : FQ;
+    for (int item = blockIdx.x; item < a.la.n_items; item += gridDim.x) {
       const int4 it = a.la.items[item];
       const int lo = it.x << a.la.s;
-      __syncthreads();
-      if (P >= 0 && a.stage)
-        for (int j = tid; j < a.B * p; j += kTR) {
+      if (a.stage) {
+        __syncthreads();
+        for (int j = tid; j < a.B * p; j += kGramThreads) {
           const int g = lo + j / p;
           slice[j] = g < a.G_P ? a.la.alpha[P][(int64_t)g * p + (j % p)] : 0.0;
         }
-      __syncthreads();
-      for (int64_t r0 = it.y; r0 < it.z; r0 += kTR) {
-        const int64_t i = r0 + tid;
-        int32_t hP = 0;
-        bool valid = i < it.z;
-        if (valid && P >= 0) {
-          hP = a.la.code[P][i];
-          valid = hP >= 0;  // singleton-dropped rows contribute nothing
+        __syncthreads();
+      }
+      const int64_t g0 = it.y >> 4, g1 = ((int64_t)it.z + 15) >> 4;
+      for (int64_t gb = g0 + (int64_t)wave * GU; gb < g1; gb += 4 * GU) {
+        // ---- phase 1: issue every load of GU row groups ----
+        int4 hq[GU], cq[GU][FQ];
+        d4 xv[GU][NT], wv[GU];
+        int64_t rb[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+          const int64_t gi = gb + u;
+          rb[u] = gi * 16 + kq * 4;
+          const bool live = gi < g1;
+          hq[u] = (P >= 0 && live) ? *reinterpret_cast<const int4*>(a.la.code[P] + rb[u]) : int4{-1, -1, -1, -1};
+          if (P < 0 && live) hq[u] = int4{0, 0, 0, 0};
+#pragma unroll
+          for (int q = 0; q < FQ; ++q)
+            cq[u][q] = (q < nq && live) ? *reinterpret_cast<const int4*>(a.la.code[a.qf[q]] + rb[u]) : int4{0, 0, 0, 0};
+#pragma unroll
+          for (int I = 0; I < NT; ++I)
+            xv[u][I] = (xc[I] >= 0 && live) ? ld4(a.X + (int64_t)xc[I] * a.ld + rb[u]) : d4{0.0, 0.0, 0.0, 0.0};
+          wv[u] = (a.w && live) ? ld4(a.w + rb[u]) : d4{1.0, 1.0, 1.0, 1.0};
         }
-        double xt[Sh::ZW];
+        // ---- phase 2: gather the group effects of every row ----
 #pragma unroll
-        for (int c = 0; c < Sh::ZW; ++c) xt[c] = 0.0;
-        if (valid) {
+        for (int u = 0; u < GU; ++u) {
+          const int hv[4] = {hq[u].x, hq[u].y, hq[u].z, hq[u].w};
+          bool valid[4];
 #pragma unroll
-          for (int c = 0; c < Sh::ZW; ++c)
-            if (c < p) xt[c] = a.X[(int64_t)c * a.ld + i];
+          for (int s = 0; s < 4; ++s) valid[s] = rb[u] + s >= it.y && rb[u] + s < it.z && hv[s] >= 0;
+          double xt[4][NT];
+#pragma unroll
+          for (int I = 0; I < NT; ++I)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) xt[s][I] = xv[u][I][s];
+#pragma unroll
+          for (int q = 0; q < FQ; ++q) {
+            if (q >= nq) continue;
+            const double* aq = a.la.alpha[a.qf[q]];
+            const int gq[4] = {cq[u][q].x, cq[u][q].y, cq[u][q].z, cq[u][q].w};
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+              for (int I = 0; I < NT; ++I)
+                if (valid[s] && xc[I] >= 0) xt[s][I] -= aq[(int64_t)gq[s] * p + xc[I]];
+          }
           if (P >= 0) {
-            const double* sl = a.stage ? &slice[(hP - lo) * p] : &a.la.alpha[P][(int64_t)hP * p];
+            // separate LDS / global paths: a generic pointer over both address
+            // spaces trips a gfx950 codegen error (flat address-space check)
+            if (a.stage) {
 #pragma unroll
-            for (int c = 0; c < Sh::ZW; ++c)
-              if (c < p) xt[c] -= sl[c];
-          }
-          for (int f = 0; f < a.la.F; ++f) {
-            if (f == P) continue;
-            const double* al = &a.la.alpha[f][(int64_t)a.la.code[f][i] * p];
+              for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int c = 0; c < Sh::ZW; ++c)
-              if (c < p) xt[c] -= al[c];
-          }
-        }
-        if (MODE == GRAM_DESIGN) {
-          // Z = sqrt(w) [1, y~, x~]   (X_w = X * sqrt(w), polars_impl.py:202-203)
-          const double sw = (valid && a.w) ? sqrt(a.w[i]) : 1.0;
-          Z[tid] = valid ? sw : 0.0;
+                for (int I = 0; I < NT; ++I)
+                  if (valid[s] && xc[I] >= 0) xt[s][I] -= slice[(hv[s] - lo) * p + xc[I]];
+            } else {
 #pragma unroll
-          for (int c = 1; c < Sh::ZW; ++c) Z[c * kZST + tid] = (valid && c - 1 < p) ? (a.w ? xt[c - 1] * sw : xt[c - 1]) : 0.0;
-        } else {
-          // r = y~ - beta0 - sum_j beta_j x~_j  (unweighted residual, polars_impl.py:229)
-          double scale = 0.0;
-          if (valid) {
-            double fit = a.beta[0];
+              for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int c = 1; c < Sh::ZW; ++c)
-              if (c < p) fit += xt[c] * a.beta[c];
-            const double res = xt[0] - fit;
-            const double wi = a.w ? a.w[i] : 1.0;
-            st[0] += wi * res * res;
-            st[1] += res * res;
-            st[2] += xt[0];
-            st[3] += xt[0] * xt[0];
-            scale = a.w ? res * sqrt(wi) : res;
-            if (a.scores) {
-              const double sc = a.w ? res * wi : res;
-#pragma unroll
-              for (int c = 1; c < Sh::ZW; ++c)
-                if (c < p) a.scores[(int64_t)(c - 1) * a.ld + i] = xt[c] * sc;
+                for (int I = 0; I < NT; ++I)
+                  if (valid[s] && xc[I] >= 0) xt[s][I] -= a.la.alpha[P][(int64_t)hv[s] * p + xc[I]];
             }
-          } else if (a.scores && i < it.z) {
-#pragma unroll
-            for (int c = 1; c < Sh::ZW; ++c)
-              if (c < p) a.scores[(int64_t)(c - 1) * a.ld + i] = 0.0;
           }
-          // HC1 meat rows: r sqrt(w) x~_j over the k = p-1 regressors
+          double z[4][NT];
+          if (MODE == GRAM_DESIGN) {
+            // Z = sqrt(w) [1, y~, x~]   (X_w = X * sqrt(w), polars_impl.py:202-203)
 #pragma unroll
-          for (int c = 0; c < Sh::ZW; ++c) Z[c * kZST + tid] = (c + 1 < p && c + 1 < Sh::ZW) ? xt[c + 1] * scale : 0.0;
+            for (int s = 0; s < 4; ++s) {
+              const double sw = a.w ? sqrt(wv[u][s]) : 1.0;
+#pragma unroll
+              for (int I = 0; I < NT; ++I) {
+                double v = (xc[I] == -1) ? 1.0 : (xc[I] >= 0 ? xt[s][I] : 0.0);
+                if (a.w) v *= sw;
+                z[s][I] = valid[s] ? v : 0.0;
+              }
+            }
+          } else {
+            // r = y~ - beta0 - sum_j beta_j x~_j (unweighted residual, polars_impl.py:229)
+            double sc[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              double t = 0.0;
+#pragma unroll
+              for (int I = 0; I < NT; ++I) t += coef[I] * xt[s][I];
+              const double res = row16_sum(t) - beta0;
+              const double wi = wv[u][s];
+              if (c == 0 && valid[s]) {  // lane c = 0 holds y~ (column 0)
+                st[0] += a.w ? wi * res * res : res * res;
+                st[1] += res * res;
+                st[2] += xt[s][0];
+                st[3] += xt[s][0] * xt[s][0];
+              }
+              sc[s] = a.w ? res * wi : res;
+              const double m = a.w ? res * sqrt(wi) : res;
+#pragma unroll
+              for (int I = 0; I < NT; ++I) z[s][I] = (valid[s] && xc[I] >= 1) ? xt[s][I] * m : 0.0;
+            }
+            if (a.scores) {
+#pragma unroll
+              for (int I = 0; I < NT; ++I) {
+                if (xc[I] < 1) continue;
+                double* dst = a.scores + (int64_t)(xc[I] - 1) * a.ld + rb[u];
+                const d4 v = d4{valid[0] ? xt[0][I] * sc[0] : 0.0, valid[1] ? xt[1][I] * sc[1] : 0.0,
+                                valid[2] ? xt[2][I] * sc[2] : 0.0, valid[3] ? xt[3][I] * sc[3] : 0.0};
+                if (rb[u] >= it.y && rb[u] + 3 < it.z) {
+                  st4(dst, v);
+                } else {
+#pragma unroll
+                  for (int s = 0; s < 4; ++s)
+                    if (rb[u] + s >= it.y && rb[u] + s < it.z) dst[s] = v[s];
+                }
+              }
+            }
+          }
+          mfma_rows<NT>(z, acc);
         }
-        __syncthreads();
-        tile_mfma<NT>(Z, acc, wave, lane);
-        __syncthreads();
       }
     }
   }
 
-  // ---- reduce the 4 waves' accumulators through LDS (reuse Z) ----
-  static_assert(Sh::LEN <= Sh::ZW * kZST, "LDS reuse");
+  // ---- reduce the 4 waves' accumulators through LDS ----
   for (int wv = 0; wv < 4; ++wv) {
+    __syncthreads();
     if (wave == wv) {
 #pragma unroll
       for (int q = 0; q < Sh::NP; ++q)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int e = q * 256 + ((lane >> 4) + 4 * rr) * 16 + (lane & 15);
-          Z[e] = (wv == 0) ? acc[q][rr] : Z[e] + acc[q][rr];
+          red[e] = (wv == 0) ? acc[q][rr] : red[e] + acc[q][rr];
         }
     }
-    __syncthreads();
   }
+  __syncthreads();
   double* out = partial + (int64_t)blockIdx.x * pstride;
-  for (int e = tid; e < Sh::LEN; e += kTR) out[e] = Z[e];
+  for (int e = tid; e < Sh::LEN; e += kGramThreads) out[e] = red[e];
   if (MODE == GRAM_RESID) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -204,14 +288,20 @@ __global__ __launch_bounds__(kTR) void k_gram(GramArgs a, double* __restrict__ p
   }
 }
 
-// fixed-order sum of per-block partials (deterministic for a fixed grid)
-__global__ void k_reduce_partials(const double* __restrict__ partial, int nblocks, int64_t pstride, int len,
-                                  double* __restrict__ out) {
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < len; e += gridDim.x * blockDim.x) {
-    double s = 0.0;
-    for (int b = 0; b < nblocks; ++b) s += partial[(int64_t)b * pstride + e];
-    out[e] = s;
+// fixed-order tree sum of per-block partials: one workgroup per output entry
+__global__ __launch_bounds__(256) void k_reduce_partials(const double* __restrict__ partial, int nblocks,
+                                                         int64_t pstride, double* __restrict__ out) {
+  __shared__ double red[256];
+  const int e = blockIdx.x;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += 256) s += partial[(int64_t)b * pstride + e];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) out[e] = red[0];
 }
 
 // cluster scores on the layout: S[cl[orig(i)]] += scores_i
@@ -220,9 +310,9 @@ __global__ void k_cluster_scatter(const int32_t* __restrict__ cl, const int32_t*
                                   int64_t n, int k, double* __restrict__ S, int32_t* __restrict__ present) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (codeP && codeP[i] < 0) continue;
-    const int64_t c = cl[orig ? orig[i] : i];
-    present[c] = 1;
-    for (int j = 0; j < k; ++j) atomicAdd(&S[c * k + j], U[(int64_t)j * ld + i]);
+    const int64_t cc = cl[orig ? orig[i] : i];
+    present[cc] = 1;
+    for (int j = 0; j < k; ++j) atomicAdd(&S[cc * k + j], U[(int64_t)j * ld + i]);
   }
 }
 
@@ -270,32 +360,40 @@ static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
   using Sh = GramShape<NT>;
   int nblocks;
   if (MODE == GRAM_TABLE) {
-    const int64_t ntiles = (a.rows + kTR - 1) / kTR;
-    nblocks = (int)std::min<int64_t>(std::max<int64_t>(ntiles, 1), 1024);
+    const int64_t ngroups = (a.rows + 15) / 16;
+    nblocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + 3) / 4, 1), 2048);
   } else {
-    nblocks = std::max(1, std::min(c->L.n_items, 1024));
+    nblocks = std::max(1, std::min(c->L.n_items, 2048));
   }
   const int64_t pstride = Sh::LEN + 4;
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
   LFE_TRY(ensure_dred(c, (size_t)pstride));
-  // stage the alpha_P slice in LDS when it fits beside the tile (<= 160 KB per CU, 1+ workgroups)
-  const size_t zbytes = sizeof(double) * Sh::ZW * kZST + 128;
   const size_t sbytes = sizeof(double) * (size_t)a.B * a.la.p;
-  a.stage = (MODE != GRAM_TABLE && a.la.P >= 0 && zbytes + sbytes <= 150 * 1024) ? 1 : 0;
+  a.stage = (MODE != GRAM_TABLE && a.la.P >= 0 && sbytes <= 96 * 1024) ? 1 : 0;
   const size_t dyn = a.stage ? sbytes : 0;
+  a.nq = 0;
+  for (int f = 0; f < a.la.F; ++f)
+    if (f != a.la.P) a.qf[a.nq++] = f;
+  // lean instantiation for <= 1 non-primary FE (the 2-FE case), general one otherwise
+  constexpr int GU = NT == 1 ? 4 : 2;
+  const void* fn = a.nq <= 1 ? reinterpret_cast<const void*>(&k_gram<MODE, NT, 1, GU>)
+                             : reinterpret_cast<const void*>(&k_gram<MODE, NT, kMaxFE - 1, 1>);
   {
     ProfScope _ps(c, MODE == GRAM_DESIGN ? K_GRAM_DESIGN : (MODE == GRAM_RESID ? K_GRAM_RESID : K_GRAM_TABLE));
-    if (dyn > 0)  // dynamic LDS above 64 KB must be opted in
-      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gram<MODE, NT>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-    hipLaunchKernelGGL((k_gram<MODE, NT>), dim3(nblocks), dim3(kTR), dyn, c->stream, a, c->scratch, pstride);
+    if (dyn > 64 * 1024)  // dynamic LDS above 64 KB must be opted in
+      LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+    if (a.nq <= 1)
+      hipLaunchKernelGGL((k_gram<MODE, NT, 1, GU>), dim3(nblocks), dim3(kGramThreads), dyn, c->stream, a, c->scratch,
+                         pstride);
+    else
+      hipLaunchKernelGGL((k_gram<MODE, NT, kMaxFE - 1, 1>), dim3(nblocks), dim3(kGramThreads), dyn, c->stream, a,
+                         c->scratch, pstride);
   }
   LFE_HIP(hipGetLastError());
   const int len = Sh::LEN + extra;
   {
     ProfScope _ps(c, K_REDUCE);
-    hipLaunchKernelGGL(k_reduce_partials, dim3((len + 255) / 256), dim3(256), 0, c->stream, c->scratch, nblocks,
-                       pstride, len, c->dred);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(len), dim3(256), 0, c->stream, c->scratch, nblocks, pstride, c->dred);
   }
   LFE_HIP(hipGetLastError());
   LFE_TRY(allreduce_sum_f64(c, c->dred, len));
@@ -320,11 +418,11 @@ static void unpack_tiles(const double* tiles, int NT, int ncols, double* out) {
         }
 }
 
-// ncols = Gram width; tile_cols = columns a row staging needs (>= ncols)
+// gram of `tile_cols` staged columns; the dense output keeps columns [off, off + ncols)
 template <int MODE>
-static int gram_dispatch(lfe_ctx* c, GramArgs a, int ncols, int tile_cols, double* dense_out, double* extra_out,
-                         int extra) {
-  const int NT = (std::max(std::max(ncols, tile_cols), 1) + 15) / 16;
+static int gram_dispatch(lfe_ctx* c, GramArgs a, int tile_cols, int off, int ncols, double* dense_out,
+                         double* extra_out, int extra) {
+  const int NT = (std::max(tile_cols, 1) + 15) / 16;
   std::vector<double> h((size_t)10 * 256 + 4);
   int rc;
   switch (NT) {
@@ -335,7 +433,12 @@ static int gram_dispatch(lfe_ctx* c, GramArgs a, int ncols, int tile_cols, doubl
     default: set_error("too many columns for the Gram kernel (max 64)"); return LFE_EINVAL;
   }
   if (rc) return rc;
-  if (dense_out) unpack_tiles(h.data(), NT, ncols, dense_out);
+  if (dense_out) {
+    std::vector<double> full((size_t)tile_cols * tile_cols);
+    unpack_tiles(h.data(), NT, tile_cols, full.data());
+    for (int i = 0; i < ncols; ++i)
+      for (int j = 0; j < ncols; ++j) dense_out[i * ncols + j] = full[(size_t)(i + off) * tile_cols + (j + off)];
+  }
   if (extra_out) {
     const int len = NT * (NT + 1) / 2 * 256;
     for (int s = 0; s < extra; ++s) extra_out[s] = h[len + s];
@@ -356,7 +459,7 @@ static GramArgs base_args(lfe_ctx* c) {
 
 int launch_gram(lfe_ctx* c, double* host_gram) {
   GramArgs a = base_args(c);
-  return gram_dispatch<GRAM_DESIGN>(c, a, c->p + 1, c->p + 1, host_gram, nullptr, 0);
+  return gram_dispatch<GRAM_DESIGN>(c, a, c->p + 1, 0, c->p + 1, host_gram, nullptr, 0);
 }
 
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores) {
@@ -366,7 +469,8 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
   a.scores = keep_scores ? c->scores : nullptr;
   const int k = c->p - 1;
   std::vector<double> meat((size_t)std::max(k, 1) * std::max(k, 1));
-  const int rc = gram_dispatch<GRAM_RESID>(c, a, k, c->p, meat.data(), stats, 4);
+  // staged columns 0..p-1 (col 0 = y, zeroed in the meat); meat = columns 1..p-1
+  const int rc = gram_dispatch<GRAM_RESID>(c, a, c->p, 1, k, meat.data(), stats, 4);
   if (rc) return rc;
   if (hc1)
     for (int e = 0; e < k * k; ++e) hc1[e] = meat[e];
@@ -409,7 +513,7 @@ int launch_cluster(lfe_ctx* c, double* meats, int64_t* G_out) {
       // is reduced locally only (no second all-reduce)
       const int world = c->world;
       c->world = 1;
-      const int rc = gram_dispatch<GRAM_TABLE>(c, a, k, k, meats + j * (size_t)k * k, nullptr, 0);
+      const int rc = gram_dispatch<GRAM_TABLE>(c, a, k, 0, k, meats + j * (size_t)k * k, nullptr, 0);
       c->world = world;
       if (rc) return rc;
     }

@@ -118,6 +118,20 @@ struct lfe_ctx {
   int32_t* origp = nullptr;      // [ld]
   int32_t* items_d = nullptr;    // device work items [n_items][4]
   size_t items_cap = 0;
+  int32_t* bitems_d = nullptr;   // device [nb + 1]: first work item of each bucket
+  size_t bitems_cap = 0;
+  // segment layout (fast path, F == 2): kept rows sorted by the primary code
+  int32_t* seg_off = nullptr;    // [G_P + 1] local row offsets of each primary group
+  size_t seg_off_cap = 0;
+  int32_t* seg_q = nullptr;      // [ld] secondary codes in segment order
+  size_t seg_q_cap = 0;
+  int32_t* seg_aux = nullptr;    // [n_items * B] per-item counts -> bases
+  size_t seg_aux_cap = 0;
+  int32_t* seg_units = nullptr;  // [n_units + 1] first primary group of each work unit
+  size_t seg_units_cap = 0;
+  int n_units = 0;
+  double* alpha_spare = nullptr; // [G_Q * p] double buffer for the secondary alpha
+  size_t alpha_spare_cap = 0;
   // clusters (input row order)
   std::vector<int32_t*> cl;
   std::vector<int32_t> cl_levels;
@@ -154,6 +168,11 @@ namespace lfe {
 // --- prep / partition (lfe_prep.hip) ---
 int prepare_layout(lfe_ctx* c);   // partition + counts + singleton marks
 
+// --- fast paths (lfe_fast.hip) ---
+int sums4(lfe_ctx* c);
+bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order);
+int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out);
+
 // --- sweeps (lfe_sweep.hip) ---
 int sweep_group_sums(lfe_ctx* c);
 int sweep_project(lfe_ctx* c, int f);
@@ -176,6 +195,9 @@ int ensure_dred(lfe_ctx* c, size_t elems);
 int ensure_iscratch(lfe_ctx* c, size_t elems);
 int ensure_pcounts(lfe_ctx* c, size_t elems, size_t sums);
 int ensure_items(lfe_ctx* c, size_t n_items);
+int ensure_i32(lfe_ctx* c, int32_t*& p, size_t& cap, size_t elems);
+int ensure_f64(lfe_ctx* c, double*& p, size_t& cap, size_t elems);
+int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
 int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems);
 int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count);
 int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count);

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void k_scan_add(int32_t* __restrict__ a, int64
     if (base + k < m) a[base + k] += add;
 }
 
-static int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) {
+int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) {
   const int64_t nblocks = (m + kScanBlock - 1) / kScanBlock;
   LFE_TRY(ensure_pcounts(c, 0, (size_t)nblocks + 1));
   ProfScope _ps(c, K_SCAN);
@@ -362,9 +362,11 @@ static int choose_shift(int32_t G) {
 static int build_items(lfe_ctx* c) {
   auto& L = c->L;
   L.hitems.clear();
+  std::vector<int32_t> bfirst(L.nb + 1, 0);
   for (int b = 0; b < L.nb; ++b) {
     const int32_t lo = L.bstart[b], hi = L.bstart[b + 1];
     const int32_t len = hi - lo;
+    bfirst[b] = (int32_t)(L.hitems.size() / 4);
     if (len <= 0) continue;
     const int32_t k = (len + kItemRows - 1) / kItemRows;
     for (int32_t q = 0; q < k; ++q) {
@@ -372,11 +374,16 @@ static int build_items(lfe_ctx* c) {
       L.hitems.insert(L.hitems.end(), {b, r0, r1, 0});
     }
   }
+  bfirst[L.nb] = (int32_t)(L.hitems.size() / 4);
   if (L.hitems.empty()) L.hitems.insert(L.hitems.end(), {0, 0, 0, 0});
   L.n_items = (int)(L.hitems.size() / 4);
   LFE_TRY(ensure_items(c, L.n_items));
   LFE_HIP(hipMemcpyAsync(c->items_d, L.hitems.data(), sizeof(int32_t) * L.hitems.size(), hipMemcpyHostToDevice,
                          c->stream));
+  LFE_TRY(ensure_i32(c, c->bitems_d, c->bitems_cap, bfirst.size()));
+  LFE_HIP(hipMemcpyAsync(c->bitems_d, bfirst.data(), sizeof(int32_t) * bfirst.size(), hipMemcpyHostToDevice,
+                         c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));  // host vectors are pageable and local
   return LFE_OK;
 }
 

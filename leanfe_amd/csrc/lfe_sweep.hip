@@ -299,15 +299,8 @@ int sweep_group_sums(lfe_ctx* c) {
   bool target[kMaxFE];
   for (int f = 0; f < c->F; ++f) target[f] = true;
   SweepArgs a = sweep_base(c);
-  // S_f: all p columns (weighted by w)
-  for (int f = 0; f < c->F; ++f) {
-    LFE_HIP(hipMemsetAsync(c->fe[f].S, 0, sizeof(double) * (size_t)c->fe[f].G * c->p, c->stream));
-    a.out[f] = c->fe[f].S;
-  }
-  a.src = SRC_X;
-  a.ostride = c->p;
-  LFE_TRY(run_sweep<SW_SUMS>(c, a, c->p, target, false, K_GROUP_SUMS));
-  for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_f64(c, c->fe[f].S, (size_t)c->fe[f].G * c->p));
+  // S_f: all p columns (weighted by w), lane-layout kernel (lfe_fast.hip)
+  LFE_TRY(sums4(c));
   if (c->L.w) {
     // W_f = sum w and Sy_f = unweighted sum of y (the stop test is unweighted)
     for (int f = 0; f < c->F; ++f) {
