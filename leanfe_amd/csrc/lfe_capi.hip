@@ -59,6 +59,13 @@ static int ensure(T*& p, size_t& have, size_t want) {
 int ensure_scratch(lfe_ctx* c, size_t elems) { return ensure(c->scratch, c->scratch_elems, elems); }
 int ensure_dred(lfe_ctx* c, size_t elems) { return ensure(c->dred, c->dred_elems, elems); }
 int ensure_iscratch(lfe_ctx* c, size_t elems) { return ensure(c->iscratch, c->iscratch_elems, elems); }
+int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, dyn_lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  return per_cu * c->n_cu;
+}
+
 int ensure_items(lfe_ctx* c, size_t n_items) { return ensure(c->items_d, c->items_cap, 4 * n_items); }
 int ensure_i32(lfe_ctx*, int32_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 int ensure_f64(lfe_ctx*, double*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
@@ -276,6 +283,8 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
   LFE_HIP(hipSetDevice(device));
   lfe_ctx* c = new lfe_ctx();
   c->device = device;
+  (void)hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
+  if (c->n_cu <= 0) c->n_cu = 256;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess) {

@@ -64,13 +64,31 @@ __global__ __launch_bounds__(kSumThreads) void k_sums4(Sums4Args a) {
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
       for (int j = tid; j < a.G[f] * p; j += kSumThreads) lds[a.tab_off[f] + j] = 0.0;
-  for (int item = blockIdx.x; item < a.la.n_items; item += gridDim.x) {
+  // primary slice [B][p] of the current bucket: flushed to S_P (and zeroed) on a
+  // bucket change; a block owns a contiguous range of items
+  auto flush = [&](int b) {
+    const int lo = b << a.la.s;
+    for (int j = tid; j < a.B * p; j += kSumThreads) {
+      const double val = lds[j];
+      const int g = lo + j / p;
+      if (val != 0.0 && g < a.G_P) atomicAdd(&a.S[P][(int64_t)g * p + (j % p)], val);
+      lds[j] = 0.0;
+    }
+  };
+  if (a.slice)
+    for (int j = tid; j < a.B * p; j += kSumThreads) lds[j] = 0.0;
+  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
+  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  int cur = -1;
+  for (int item = i0; item < i1; ++item) {
     const int4 it = a.la.items[item];
     const int lo = it.x << a.la.s;
-    __syncthreads();
-    if (a.slice)
-      for (int j = tid; j < a.B * p; j += kSumThreads) lds[j] = 0.0;
-    __syncthreads();
+    if (a.slice && it.x != cur) {
+      __syncthreads();
+      if (cur >= 0) flush(cur);
+      __syncthreads();
+      cur = it.x;
+    }
     const int64_t g0 = it.y >> 4, g1 = ((int64_t)it.z + 15) >> 4;
     for (int64_t gb = g0 + (int64_t)wave * GU; gb < g1; gb += nwv * GU) {
       int4 hq[GU], cq[GU][FQ];
@@ -122,15 +140,9 @@ __global__ __launch_bounds__(kSumThreads) void k_sums4(Sums4Args a) {
         }
       }
     }
-    __syncthreads();
-    if (a.slice)
-      for (int j = tid; j < a.B * p; j += kSumThreads) {
-        const double val = lds[j];
-        const int g = lo + j / p;
-        if (val != 0.0 && g < a.G_P) atomicAdd(&a.S[P][(int64_t)g * p + (j % p)], val);
-      }
   }
   __syncthreads();
+  if (a.slice && cur >= 0) flush(cur);
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
       for (int j = tid; j < a.G[f] * p; j += kSumThreads) {
@@ -166,8 +178,6 @@ int sums4(lfe_ctx* c) {
   for (int f = 0; f < c->F; ++f)
     if (f != P) a.qf[a.nq++] = f;
   const size_t lds = off * 8;
-  const int per_cu = lds <= 75 * 1024 ? 2 : 1;
-  const int nblocks = std::max(1, std::min(c->L.n_items, 256 * per_cu));
   const int NT = (p + 15) / 16;
   const void* fn = nullptr;
 #define SUMS4_FN(FQ, GU, NT_) reinterpret_cast<const void*>(&k_sums4<FQ, GU, NT_>)
@@ -177,6 +187,7 @@ int sums4(lfe_ctx* c) {
     fn = NT == 1 ? SUMS4_FN(7, 1, 1) : NT == 2 ? SUMS4_FN(7, 1, 2) : NT == 3 ? SUMS4_FN(7, 1, 3) : SUMS4_FN(7, 1, 4);
 #undef SUMS4_FN
   LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 1)));
+  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kSumThreads, lds)));
   {
     ProfScope _ps(c, K_GROUP_SUMS);
     void* args[] = {&a};

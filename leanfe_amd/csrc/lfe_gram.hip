@@ -83,185 +83,11 @@ __device__ __forceinline__ void mfma_rows(const double (&z)[4][NT], d4* acc) {
   }
 }
 
-// MODE: design / resid / table; NT: 16-column slots per lane; FQ: max non-primary FEs;
-// GU: 16-row groups a wave loads before it uses any of them (memory-level parallelism)
-template <int MODE, int NT, int FQ, int GU>
-__global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __restrict__ partial, int64_t pstride) {
+// LDS reduction of the 4 waves' accumulators -> partial[blockIdx.x]
+template <int NT>
+__device__ __forceinline__ void block_reduce_store(const d4* acc, double* red, double* out, int tid) {
   using Sh = GramShape<NT>;
-  __shared__ double red[Sh::LEN];
-  __shared__ double stat_red[4][4];
-  extern __shared__ __attribute__((aligned(16))) double slice[];  // [B][p] alpha_P slice of the item's bucket
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kq = lane >> 4, c = lane & 15;
-  const int p = a.la.p, P = a.la.P;
-
-  d4 acc[Sh::NP];
-#pragma unroll
-  for (int q = 0; q < Sh::NP; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
-  double st[4] = {0.0, 0.0, 0.0, 0.0};  // sum w r^2, sum r^2, sum y~, sum y~^2
-
-  if (MODE == GRAM_TABLE) {
-    const int64_t ngroups = (a.rows + 15) / 16;
-    for (int64_t gi = (int64_t)blockIdx.x * 4 + wave; gi < ngroups; gi += (int64_t)gridDim.x * 4) {
-      double z[4][NT];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int64_t r = gi * 16 + kq * 4 + s;
-#pragma unroll
-        for (int I = 0; I < NT; ++I) {
-          const int col = 16 * I + c;
-          z[s][I] = (r < a.rows && col < a.tcols) ? a.table[r * a.tcols + col] : 0.0;
-        }
-      }
-      mfma_rows<NT>(z, acc);
-    }
-  } else {
-    // columns held by this lane: design column col = 16I + c -> data column xc
-    int xc[NT];
-#pragma unroll
-    for (int I = 0; I < NT; ++I) {
-      const int col = 16 * I + c;
-      xc[I] = (MODE == GRAM_DESIGN) ? col - 1 : col;  // DESIGN: col 0 = intercept, col 1 = y
-      if (xc[I] >= p) xc[I] = -2;                       // padding column
-    }
-    // RESID: the 16 lanes of a row quad sum term = y~ (column 0) - beta_j x~_j (columns j >= 1)
-    double coef[NT];
-    if (MODE == GRAM_RESID) {
-#pragma unroll
-      for (int I = 0; I < NT; ++I) coef[I] = xc[I] == 0 ? 1.0 : (xc[I] >= 1 ? -a.beta[xc[I]] : 0.0);
-    }
-    const double beta0 = (MODE == GRAM_RESID) ? a.beta[0] : 0.0;
-    const int nq = a.nq < FQ ? a.nq : FQ;
-    for (int item = blockIdx.x; item < a.la.n_items; item += gridDim.x) {
-      const int4 it = a.la.items[item];
-      const int lo = it.x << a.la.s;
-      if (a.stage) {
-        __syncthreads();
-        for (int j = tid; j < a.B * p; j += kGramThreads) {
-          const int g = lo + j / p;
-          slice[j] = g < a.G_P ? a.la.alpha[P][(int64_t)g * p + (j % p)] : 0.0;
-        }
-        __syncthreads();
-      }
-      const int64_t g0 = it.y >> 4, g1 = ((int64_t)it.z + 15) >> 4;
-      for (int64_t gb = g0 + (int64_t)wave * GU; gb < g1; gb += 4 * GU) {
-        // ---- phase 1: issue every load of GU row groups ----
-        int4 hq[GU], cq[GU][FQ];
-        d4 xv[GU][NT], wv[GU];
-        int64_t rb[GU];
-#pragma unroll
-        for (int u = 0; u < GU; ++u) {
-          const int64_t gi = gb + u;
-          rb[u] = gi * 16 + kq * 4;
-          const bool live = gi < g1;
-          hq[u] = (P >= 0 && live) ? *reinterpret_cast<const int4*>(a.la.code[P] + rb[u]) : int4{-1, -1, -1, -1};
-          if (P < 0 && live) hq[u] = int4{0, 0, 0, 0};
-#pragma unroll
-          for (int q = 0; q < FQ; ++q)
-            cq[u][q] = (q < nq && live) ? *reinterpret_cast<const int4*>(a.la.code[a.qf[q]] + rb[u]) : int4{0, 0, 0, 0};
-#pragma unroll
-          for (int I = 0; I < NT; ++I)
-            xv[u][I] = (xc[I] >= 0 && live) ? ld4(a.X + (int64_t)xc[I] * a.ld + rb[u]) : d4{0.0, 0.0, 0.0, 0.0};
-          wv[u] = (a.w && live) ? ld4(a.w + rb[u]) : d4{1.0, 1.0, 1.0, 1.0};
-        }
-        // ---- phase 2: gather the group effects of every row ----
-#pragma unroll
-        for (int u = 0; u < GU; ++u) {
-          const int hv[4] = {hq[u].x, hq[u].y, hq[u].z, hq[u].w};
-          bool valid[4];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) valid[s] = rb[u] + s >= it.y && rb[u] + s < it.z && hv[s] >= 0;
-          double xt[4][NT];
-#pragma unroll
-          for (int I = 0; I < NT; ++I)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) xt[s][I] = xv[u][I][s];
-#pragma unroll
-          for (int q = 0; q < FQ; ++q) {
-            if (q >= nq) continue;
-            const double* aq = a.la.alpha[a.qf[q]];
-            const int gq[4] = {cq[u][q].x, cq[u][q].y, cq[u][q].z, cq[u][q].w};
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-              for (int I = 0; I < NT; ++I)
-                if (valid[s] && xc[I] >= 0) xt[s][I] -= aq[(int64_t)gq[s] * p + xc[I]];
-          }
-          if (P >= 0) {
-            // separate LDS / global paths: a generic pointer over both address
-            // spaces trips a gfx950 codegen error (flat address-space check)
-            if (a.stage) {
-#pragma unroll
-              for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int I = 0; I < NT; ++I)
-                  if (valid[s] && xc[I] >= 0) xt[s][I] -= slice[(hv[s] - lo) * p + xc[I]];
-            } else {
-#pragma unroll
-              for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int I = 0; I < NT; ++I)
-                  if (valid[s] && xc[I] >= 0) xt[s][I] -= a.la.alpha[P][(int64_t)hv[s] * p + xc[I]];
-            }
-          }
-          double z[4][NT];
-          if (MODE == GRAM_DESIGN) {
-            // Z = sqrt(w) [1, y~, x~]   (X_w = X * sqrt(w), polars_impl.py:202-203)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              const double sw = a.w ? sqrt(wv[u][s]) : 1.0;
-#pragma unroll
-              for (int I = 0; I < NT; ++I) {
-                double v = (xc[I] == -1) ? 1.0 : (xc[I] >= 0 ? xt[s][I] : 0.0);
-                if (a.w) v *= sw;
-                z[s][I] = valid[s] ? v : 0.0;
-              }
-            }
-          } else {
-            // r = y~ - beta0 - sum_j beta_j x~_j (unweighted residual, polars_impl.py:229)
-            double sc[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              double t = 0.0;
-#pragma unroll
-              for (int I = 0; I < NT; ++I) t += coef[I] * xt[s][I];
-              const double res = row16_sum(t) - beta0;
-              const double wi = wv[u][s];
-              if (c == 0 && valid[s]) {  // lane c = 0 holds y~ (column 0)
-                st[0] += a.w ? wi * res * res : res * res;
-                st[1] += res * res;
-                st[2] += xt[s][0];
-                st[3] += xt[s][0] * xt[s][0];
-              }
-              sc[s] = a.w ? res * wi : res;
-              const double m = a.w ? res * sqrt(wi) : res;
-#pragma unroll
-              for (int I = 0; I < NT; ++I) z[s][I] = (valid[s] && xc[I] >= 1) ? xt[s][I] * m : 0.0;
-            }
-            if (a.scores) {
-#pragma unroll
-              for (int I = 0; I < NT; ++I) {
-                if (xc[I] < 1) continue;
-                double* dst = a.scores + (int64_t)(xc[I] - 1) * a.ld + rb[u];
-                const d4 v = d4{valid[0] ? xt[0][I] * sc[0] : 0.0, valid[1] ? xt[1][I] * sc[1] : 0.0,
-                                valid[2] ? xt[2][I] * sc[2] : 0.0, valid[3] ? xt[3][I] * sc[3] : 0.0};
-                if (rb[u] >= it.y && rb[u] + 3 < it.z) {
-                  st4(dst, v);
-                } else {
-#pragma unroll
-                  for (int s = 0; s < 4; ++s)
-                    if (rb[u] + s >= it.y && rb[u] + s < it.z) dst[s] = v[s];
-                }
-              }
-            }
-          }
-          mfma_rows<NT>(z, acc);
-        }
-      }
-    }
-  }
-
-  // ---- reduce the 4 waves' accumulators through LDS ----
+  const int lane = tid & 63, wave = tid >> 6;
   for (int wv = 0; wv < 4; ++wv) {
     __syncthreads();
     if (wave == wv) {
@@ -275,8 +101,265 @@ __global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __res
     }
   }
   __syncthreads();
-  double* out = partial + (int64_t)blockIdx.x * pstride;
   for (int e = tid; e < Sh::LEN; e += kGramThreads) out[e] = red[e];
+}
+
+// Gram of a small row-major table (cluster score sums): Z = table[rows][tcols]
+template <int NT>
+__global__ __launch_bounds__(kGramThreads) void k_gram_table(GramArgs a, double* __restrict__ partial, int64_t pstride) {
+  using Sh = GramShape<NT>;
+  __shared__ double red[Sh::LEN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kq = lane >> 4, c = lane & 15;
+  d4 acc[Sh::NP];
+#pragma unroll
+  for (int q = 0; q < Sh::NP; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  const int64_t ngroups = (a.rows + 15) / 16;
+  for (int64_t gi = (int64_t)blockIdx.x * 4 + wave; gi < ngroups; gi += (int64_t)gridDim.x * 4) {
+    double z[4][NT];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int64_t r = gi * 16 + kq * 4 + s;
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+        const int col = 16 * I + c;
+        z[s][I] = (r < a.rows && col < a.tcols) ? a.table[r * a.tcols + col] : 0.0;
+      }
+    }
+    mfma_rows<NT>(z, acc);
+  }
+  block_reduce_store<NT>(acc, red, partial + (int64_t)blockIdx.x * pstride, tid);
+}
+
+// Design Gram / residual pass over the bucket layout.
+// MODE: design / resid; NT: 16-column slots per lane; FQ: max non-primary FEs;
+// GU: 16-row groups per wave iteration; WT: weighted fit.
+// Every load address is valid for every lane: lanes without a data column read
+// column 0 and rows outside the item get primary code -1, so nothing is
+// predicated and each row's validity is the single test h >= 0.
+template <int MODE, int NT, int FQ, int GU, bool WT>
+__global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __restrict__ partial, int64_t pstride) {
+  using Sh = GramShape<NT>;
+  __shared__ double red[Sh::LEN];
+  __shared__ double stat_red[4][4];
+  extern __shared__ __attribute__((aligned(16))) double slice[];  // [B][p] alpha_P slice of the item's bucket
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kq = lane >> 4, c = lane & 15;
+  const int p = a.la.p, P = a.la.P;
+
+  d4 acc[Sh::NP];
+#pragma unroll
+  for (int q = 0; q < Sh::NP; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  double st[4] = {0.0, 0.0, 0.0, 0.0};  // sum w r^2, sum r^2, sum y~, sum y~^2
+
+  // columns held by this lane: design column col = 16I + c -> data column xc
+  int xl[NT];          // data column loaded (0 for lanes without one)
+  bool dat[NT];        // lane holds a data column
+  double fill[NT];     // DESIGN: value of a non-data column (1 for the intercept)
+  double coef[NT];     // RESID: row term y~ - sum_j beta_j x~_j
+  const double* xb[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) {
+    const int col = 16 * I + c;
+    int xc = (MODE == GRAM_DESIGN) ? col - 1 : col;  // DESIGN: col 0 = intercept, col 1 = y
+    if (xc >= p) xc = -2;
+    dat[I] = xc >= 0;
+    xl[I] = xc >= 0 ? xc : 0;
+    fill[I] = xc == -1 ? 1.0 : 0.0;
+    coef[I] = (MODE == GRAM_RESID) ? (xc == 0 ? 1.0 : (xc >= 1 ? -a.beta[xc] : 0.0)) : 0.0;
+    if (MODE == GRAM_RESID) dat[I] = xc >= 1;  // meat columns
+    xb[I] = a.X + (int64_t)xl[I] * a.ld;
+  }
+  const double beta0 = (MODE == GRAM_RESID) ? a.beta[0] : 0.0;
+  const int nq = a.nq < FQ ? a.nq : FQ;
+
+  // a contiguous range of items per block (all blocks co-resident): the
+  // primary slice is staged again only when the bucket changes
+  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
+  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  int staged = -1;
+  for (int item = i0; item < i1; ++item) {
+    const int4 it = a.la.items[item];
+    const int lo = it.x << a.la.s;
+    if (a.stage && it.x != staged) {
+      __syncthreads();
+      for (int j = tid; j < a.B * p; j += kGramThreads) {
+        const int g = lo + j / p;
+        slice[j] = g < a.G_P ? a.la.alpha[P][(int64_t)g * p + (j % p)] : 0.0;
+      }
+      __syncthreads();
+      staged = it.x;
+    }
+    const int g0 = it.y >> 4, g1 = (it.z + 15) >> 4;
+    constexpr int step = 4 * GU;
+    // software pipeline: the codes of a batch are loaded one iteration ahead,
+    // so X loads, every group's alpha gathers and the next codes are in flight together
+    int hq[GU][4], cq[GU][FQ][4];
+    auto load_codes = [&](int gb) {
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int gi = gb + u;
+        const int r = gi * 16 + kq * 4;
+        int4 h = int4{-1, -1, -1, -1};
+        if (gi < g1) h = P >= 0 ? *reinterpret_cast<const int4*>(a.la.code[P] + r) : int4{0, 0, 0, 0};
+        hq[u][0] = h.x; hq[u][1] = h.y; hq[u][2] = h.z; hq[u][3] = h.w;
+#pragma unroll
+        for (int q = 0; q < FQ; ++q) {
+          int4 v = int4{0, 0, 0, 0};
+          if (q < nq && gi < g1) v = *reinterpret_cast<const int4*>(a.la.code[a.qf[q]] + r);
+          cq[u][q][0] = v.x; cq[u][q][1] = v.y; cq[u][q][2] = v.z; cq[u][q][3] = v.w;
+        }
+        // a group straddling the item edge (wave-uniform test): rows outside the
+        // item are marked dropped and their other codes zeroed (rows past n hold
+        // uninitialised codes, and the gathers below are not predicated)
+        if (gi < g1 && (gi * 16 < it.y || gi * 16 + 16 > it.z)) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            if (r + s < it.y || r + s >= it.z) {
+              hq[u][s] = -1;
+#pragma unroll
+              for (int q = 0; q < FQ; ++q) cq[u][q][s] = 0;
+            }
+        }
+      }
+    };
+    load_codes(g0 + wave * GU);
+    for (int gb = g0 + wave * GU; gb < g1; gb += step) {
+      d4 xv[GU][NT], wv[GU];
+      bool valid[GU][4];
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int gi = gb + u;
+        const int r = gi * 16 + kq * 4;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) xv[u][I] = gi < g1 ? ld4(xb[I] + r) : d4{0.0, 0.0, 0.0, 0.0};
+        if (WT) wv[u] = gi < g1 ? ld4(a.w + r) : d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) valid[u][s] = hq[u][s] >= 0;
+      }
+      // group effects: non-primary FEs gathered from global (L2-resident tables)
+      double ga[GU][4][NT];
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int I = 0; I < NT; ++I) ga[u][s][I] = 0.0;
+#pragma unroll
+      for (int q = 0; q < FQ; ++q) {
+        if (q >= nq) continue;
+        const double* aq = a.la.alpha[a.qf[q]];
+#pragma unroll
+        for (int u = 0; u < GU; ++u)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const uint32_t ro = (uint32_t)cq[u][q][s] * (uint32_t)p;
+#pragma unroll
+            for (int I = 0; I < NT; ++I) {
+              const double v = aq[ro + (uint32_t)xl[I]];
+              ga[u][s][I] = (q == 0) ? v : ga[u][s][I] + v;
+            }
+          }
+      }
+      int hv[GU][4];
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) hv[u][s] = hq[u][s];
+      load_codes(gb + step);  // next batch
+      if (P >= 0) {
+        // separate LDS / global paths: a generic pointer over both address
+        // spaces trips a gfx950 codegen error (flat address-space check)
+        if (a.stage) {
+#pragma unroll
+          for (int u = 0; u < GU; ++u)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const uint32_t ro = (uint32_t)(valid[u][s] ? hv[u][s] - lo : 0) * (uint32_t)p;
+#pragma unroll
+              for (int I = 0; I < NT; ++I) ga[u][s][I] += slice[ro + (uint32_t)xl[I]];
+            }
+        } else {
+          const double* ap = a.la.alpha[P];
+#pragma unroll
+          for (int u = 0; u < GU; ++u)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const uint32_t ro = (uint32_t)(valid[u][s] ? hv[u][s] : 0) * (uint32_t)p;
+#pragma unroll
+              for (int I = 0; I < NT; ++I) ga[u][s][I] += ap[ro + (uint32_t)xl[I]];
+            }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        double xt[4][NT];
+#pragma unroll
+        for (int I = 0; I < NT; ++I)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) xt[s][I] = xv[u][I][s] - ga[u][s][I];
+        double z[4][NT];
+        if (MODE == GRAM_DESIGN) {
+          // Z = sqrt(w) [1, y~, x~]   (X_w = X * sqrt(w), polars_impl.py:202-203)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const double sw = WT ? sqrt(wv[u][s]) : 1.0;
+#pragma unroll
+            for (int I = 0; I < NT; ++I) {
+              double v = dat[I] ? xt[s][I] : fill[I];
+              if (WT) v *= sw;
+              z[s][I] = valid[u][s] ? v : 0.0;
+            }
+          }
+        } else {
+          // r = y~ - beta0 - sum_j beta_j x~_j (unweighted residual, polars_impl.py:229)
+          double sc[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            double t = coef[0] * xt[s][0];
+#pragma unroll
+            for (int I = 1; I < NT; ++I) t += coef[I] * xt[s][I];
+            const double res = row16_sum(t) - beta0;
+            if (c == 0 && valid[u][s]) {  // lane c = 0 holds y~ (column 0)
+              const double rr = res * res;
+              st[0] += WT ? wv[u][s] * rr : rr;
+              st[1] += rr;
+              st[2] += xt[s][0];
+              st[3] += xt[s][0] * xt[s][0];
+            }
+            sc[s] = WT ? res * wv[u][s] : res;
+            const double m = WT ? res * sqrt(wv[u][s]) : res;
+#pragma unroll
+            for (int I = 0; I < NT; ++I) z[s][I] = (valid[u][s] && dat[I]) ? xt[s][I] * m : 0.0;
+          }
+          if (a.scores) {
+            const int gi = gb + u;
+            const int r = gi * 16 + kq * 4;
+            const bool full = gi * 16 >= it.y && gi * 16 + 16 <= it.z;
+#pragma unroll
+            for (int I = 0; I < NT; ++I) {
+              if (!dat[I]) continue;
+              double* dst = a.scores + (int64_t)(xl[I] - 1) * a.ld + r;
+              const d4 v = d4{valid[u][0] ? xt[0][I] * sc[0] : 0.0, valid[u][1] ? xt[1][I] * sc[1] : 0.0,
+                              valid[u][2] ? xt[2][I] * sc[2] : 0.0, valid[u][3] ? xt[3][I] * sc[3] : 0.0};
+              if (full) {
+                st4(dst, v);
+              } else if (gi < g1) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                  if (valid[u][s]) dst[s] = v[s];
+              }
+            }
+          }
+        }
+        mfma_rows<NT>(z, acc);
+      }
+    }
+  }
+
+  double* out = partial + (int64_t)blockIdx.x * pstride;
+  block_reduce_store<NT>(acc, red, out, tid);
   if (MODE == GRAM_RESID) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -356,38 +439,46 @@ int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* fl
 }
 
 template <int MODE, int NT>
+static const void* gram_kernel(bool general, bool weighted) {
+  constexpr int GU = NT == 1 ? 4 : 2;
+  if (MODE == GRAM_TABLE) return reinterpret_cast<const void*>(&k_gram_table<NT>);
+  constexpr int M = MODE == GRAM_TABLE ? GRAM_DESIGN : MODE;
+  if (!general)
+    return weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, true>)
+                    : reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, false>);
+  return weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, true>)
+                  : reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, false>);
+}
+
+template <int MODE, int NT>
 static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
   using Sh = GramShape<NT>;
   int nblocks;
-  if (MODE == GRAM_TABLE) {
-    const int64_t ngroups = (a.rows + 15) / 16;
-    nblocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + 3) / 4, 1), 2048);
-  } else {
-    nblocks = std::max(1, std::min(c->L.n_items, 2048));
-  }
-  const int64_t pstride = Sh::LEN + 4;
-  LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
-  LFE_TRY(ensure_dred(c, (size_t)pstride));
-  const size_t sbytes = sizeof(double) * (size_t)a.B * a.la.p;
-  a.stage = (MODE != GRAM_TABLE && a.la.P >= 0 && sbytes <= 96 * 1024) ? 1 : 0;
-  const size_t dyn = a.stage ? sbytes : 0;
+  size_t dyn = 0;
   a.nq = 0;
   for (int f = 0; f < a.la.F; ++f)
     if (f != a.la.P) a.qf[a.nq++] = f;
   // lean instantiation for <= 1 non-primary FE (the 2-FE case), general one otherwise
-  constexpr int GU = NT == 1 ? 4 : 2;
-  const void* fn = a.nq <= 1 ? reinterpret_cast<const void*>(&k_gram<MODE, NT, 1, GU>)
-                             : reinterpret_cast<const void*>(&k_gram<MODE, NT, kMaxFE - 1, 1>);
-  {
-    ProfScope _ps(c, MODE == GRAM_DESIGN ? K_GRAM_DESIGN : (MODE == GRAM_RESID ? K_GRAM_RESID : K_GRAM_TABLE));
+  const void* fn = gram_kernel<MODE, NT>(a.nq > 1, a.w != nullptr);
+  if (MODE == GRAM_TABLE) {
+    const int64_t ngroups = (a.rows + 15) / 16;
+    nblocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + 3) / 4, 1), 2048);
+  } else {
+    const size_t sbytes = sizeof(double) * (size_t)a.B * a.la.p;
+    a.stage = (a.la.P >= 0 && sbytes <= 96 * 1024) ? 1 : 0;
+    dyn = a.stage ? sbytes : 0;
     if (dyn > 64 * 1024)  // dynamic LDS above 64 KB must be opted in
       LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-    if (a.nq <= 1)
-      hipLaunchKernelGGL((k_gram<MODE, NT, 1, GU>), dim3(nblocks), dim3(kGramThreads), dyn, c->stream, a, c->scratch,
-                         pstride);
-    else
-      hipLaunchKernelGGL((k_gram<MODE, NT, kMaxFE - 1, 1>), dim3(nblocks), dim3(kGramThreads), dyn, c->stream, a,
-                         c->scratch, pstride);
+    nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kGramThreads, dyn)));
+  }
+  const int64_t pstride = Sh::LEN + 4;
+  LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
+  LFE_TRY(ensure_dred(c, (size_t)pstride));
+  {
+    ProfScope _ps(c, MODE == GRAM_DESIGN ? K_GRAM_DESIGN : (MODE == GRAM_RESID ? K_GRAM_RESID : K_GRAM_TABLE));
+    double* part = c->scratch;
+    void* args[] = {&a, &part, const_cast<int64_t*>(&pstride)};
+    LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(kGramThreads), args, dyn, c->stream));
   }
   LFE_HIP(hipGetLastError());
   const int len = Sh::LEN + extra;

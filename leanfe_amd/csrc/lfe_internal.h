@@ -20,7 +20,7 @@ constexpr int kBlock = 256;      // threads per workgroup for simple streaming k
 constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
 constexpr int kMaxGroupCols = 16;    // columns per column group in a sweep
 constexpr int kLdsBudget = 64 * 1024;  // bytes of LDS tables per sweep workgroup (2 WG per CU)
-constexpr int kItemRows = 65536;     // rows per work item (a bucket is split into items)
+constexpr int kItemRows = 8192;      // rows per work item (a bucket is split into items)
 constexpr int kLdsHistMax = 16384;   // int32 counters in an LDS histogram
 
 void set_error(const std::string& msg);
@@ -100,6 +100,7 @@ struct Layout {
 
 struct lfe_ctx {
   int device = 0;
+  int n_cu = 256;        // compute units of the device
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // data (row shard, input order)
@@ -198,6 +199,8 @@ int ensure_items(lfe_ctx* c, size_t n_items);
 int ensure_i32(lfe_ctx* c, int32_t*& p, size_t& cap, size_t elems);
 int ensure_f64(lfe_ctx* c, double*& p, size_t& cap, size_t elems);
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
+// blocks of `fn` that fit on the whole device at once (occupancy API x CUs)
+int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds);
 int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems);
 int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count);
 int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count);

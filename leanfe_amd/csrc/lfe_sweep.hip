@@ -258,7 +258,6 @@ static int plan_lds(const lfe_ctx* c, const bool* target, int stage_rows, int nc
 
 template <int MODE>
 static int run_sweep(lfe_ctx* c, SweepArgs a, int ncols, const bool* target, bool stage_alphaP, int kid) {
-  const int P = c->L.P;
   const int B = 1 << c->L.s;
   int lds_off[kMaxFE], lds_doubles = 0, W = 1;
   const int stage_rows = (MODE == SW_CROSS && stage_alphaP) ? B : 0;

@@ -60,9 +60,9 @@ def test_synth_device_equals_host_bit_exact():
 
 
 @pytest.mark.parametrize("seed,n,L,k,vcov", [
-    (1, 200_000, (5000, 300), 5, "iid"),
+    (1, 200_003, (5000, 300), 5, "iid"),            # n % 16 != 0: partial last row group
     (2, 300_000, (20000, 500), 3, "HC1"),
-    (3, 150_000, (3000, 40, 7), 4, "cluster"),
+    (3, 150_005, (3000, 40, 7), 4, "cluster"),
     (12345, 2_000_000, (100000, 1000), 10, "HC1"),   # headline geometry (1e5 / 1e3 levels, k = 10)
     (6, 400_000, (700_000, 50), 2, "iid"),           # more levels than rows: many singletons, nb > 512
 ])
