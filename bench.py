@@ -119,17 +119,21 @@ def solve_step(eng: Engine, vcov: str):
 
 
 def algorithmic_bytes(n: int, p: int, F: int, T: int, hc1: bool) -> dict:
-    """Bytes the engine's passes must move, per kernel and total."""
-    b = {
-        "count_pre": 4 * n * F,
-        "keep": 4 * n * F + n,                       # codes + keep mask write
-        "group_sums": n * (8 * p + 4 * F + 1),       # columns + codes + mask
-        "cross_sums": n * (4 * F + 1),               # per projection: codes + mask
-        "check_sums": n * (8 + 4 * F + 1),           # y + codes + mask
-        "gram_design": n * (8 * p + 4 * F + 1),
-        "gram_resid": n * (8 * p + 4 * F + 1),
+    """HBM bytes each kernel must move per launch (DESIGN.md "Kernels and their rooflines").
+
+    n rows/GPU, p = 1 + k data columns (f64), F fixed effects (int32 codes).  The
+    layout passes scan every row of the shard (dropped rows included).
+    """
+    return {
+        "part_hist": 4 * n,                              # primary codes
+        "part_scatter": n * (2 * 8 * p + 2 * 4 * F + 4),  # read + write X and codes, write orig
+        "count": 4 * n,                                  # one code column per launch
+        "mark": 4 * n * F,                               # every code column (+ sparse writes)
+        "group_sums": n * (8 * p + 4 * F),               # X + codes
+        "cross": 4 * n,                                  # secondary codes in segment order
+        "gram_design": n * (8 * p + 4 * F),              # X + codes
+        "gram_resid": n * (8 * p + 4 * F),               # X + codes (HC1: no score write)
     }
-    return b
 
 
 def cpu_baseline(args, levels):

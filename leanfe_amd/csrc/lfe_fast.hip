@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace lfe {
 
@@ -181,8 +182,14 @@ int sums4(lfe_ctx* c) {
   const int NT = (p + 15) / 16;
   const void* fn = nullptr;
 #define SUMS4_FN(FQ, GU, NT_) reinterpret_cast<const void*>(&k_sums4<FQ, GU, NT_>)
-  if (a.nq <= 1)
-    fn = NT == 1 ? SUMS4_FN(1, 4, 1) : NT == 2 ? SUMS4_FN(1, 2, 2) : NT == 3 ? SUMS4_FN(1, 2, 3) : SUMS4_FN(1, 2, 4);
+  static const int gu_env = [] {
+    const char* e = getenv("LFE_SUMS_GU");  // tuning override
+    return e ? atoi(e) : 0;
+  }();
+  if (a.nq <= 1 && NT == 1)
+    fn = gu_env == 1 ? SUMS4_FN(1, 1, 1) : gu_env == 2 ? SUMS4_FN(1, 2, 1) : SUMS4_FN(1, 4, 1);
+  else if (a.nq <= 1)
+    fn = NT == 2 ? SUMS4_FN(1, 2, 2) : NT == 3 ? SUMS4_FN(1, 2, 3) : SUMS4_FN(1, 2, 4);
   else
     fn = NT == 1 ? SUMS4_FN(7, 1, 1) : NT == 2 ? SUMS4_FN(7, 1, 2) : NT == 3 ? SUMS4_FN(7, 1, 3) : SUMS4_FN(7, 1, 4);
 #undef SUMS4_FN
@@ -412,6 +419,8 @@ int build_segments(lfe_ctx* c, int Q) {
 
 constexpr int kIterThreads = 1024;
 constexpr int kIterMaxW = 8;
+constexpr int kIterK = 12;  // secondary codes per lane held in registers (segments <= 768 rows)
+constexpr int kIterLds = 150 * 1024;  // LDS bytes for the two secondary tables
 
 enum { IT_FUSED = 0, IT_REDUCE = 1, IT_SCATTER = 2 };
 
@@ -433,27 +442,61 @@ struct IterArgs {
 __global__ __launch_bounds__(kIterThreads) void k_iter(IterArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int W = a.W;
-  double* aQ = lds;                       // [G_Q][W] staged alpha_Q columns
-  double* tQ = lds + (int64_t)a.G_Q * W;  // [G_Q][W] T_Q accumulation
+  // rows of the LDS tables are padded to an odd number of doubles (WS): with an
+  // even stride the random secondary codes of a wavefront would fall on a few
+  // banks only (a stride of 8 doubles: 16-way conflicts)
+  const int WS = W | 1;
+  double* aQ = lds;                        // [G_Q][WS] staged alpha_Q columns
+  double* tQ = lds + (int64_t)a.G_Q * WS;  // [G_Q][WS] T_Q accumulation
   const int tid = threadIdx.x, lane = tid & 63;
   if (a.mode != IT_SCATTER)
-    for (int j = tid; j < a.G_Q * W; j += kIterThreads) aQ[j] = a.alphaQ[(int64_t)(j / W) * a.p + a.c0 + (j % W)];
+    for (int j = tid; j < a.G_Q * W; j += kIterThreads)
+      aQ[(j / W) * WS + (j % W)] = a.alphaQ[(int64_t)(j / W) * a.p + a.c0 + (j % W)];
   if (a.mode != IT_REDUCE)
-    for (int j = tid; j < a.G_Q * W; j += kIterThreads) tQ[j] = 0.0;
+    for (int j = tid; j < a.G_Q * WS; j += kIterThreads) tQ[j] = 0.0;
   __syncthreads();
   const int nwaves = gridDim.x * (kIterThreads / 64);
+  // The secondary codes of a segment are held in registers (kIterK per lane:
+  // segments up to 64 kIterK rows; longer ones finish in a plain loop) and the
+  // next segment's codes are loaded while this one runs on LDS, so a segment
+  // costs one exposed global latency at most.
+  int qn[kIterK];
+  int nr0 = 0, nr1 = 0;
+  auto load_seg = [&](int h) {
+    nr0 = a.seg_off[h];
+    nr1 = a.seg_off[h + 1];
+#pragma unroll
+    for (int k = 0; k < kIterK; ++k) {
+      const int32_t r = nr0 + lane + 64 * k;
+      qn[k] = r < nr1 ? a.seg_q[r] : -1;
+    }
+  };
   for (int u = blockIdx.x * (kIterThreads / 64) + (tid >> 6); u < a.n_units; u += nwaves) {
     const int h0 = a.units[u], h1 = a.units[u + 1];
+    if (h0 < h1) load_seg(h0);
     for (int h = h0; h < h1; ++h) {
-      const int32_t r0 = a.seg_off[h], r1 = a.seg_off[h + 1];
+      int qc[kIterK];
+#pragma unroll
+      for (int k = 0; k < kIterK; ++k) qc[k] = qn[k];
+      const int32_t r0 = nr0, r1 = nr1;
       const int32_t n = r1 - r0;
+      if (h + 1 < h1) load_seg(h + 1);
+      const int32_t rtail = r0 + 64 * kIterK + lane;  // rows beyond the register window
       double ap[kIterMaxW];
       if (a.mode != IT_SCATTER) {
         double acc[kIterMaxW];
 #pragma unroll
         for (int cc = 0; cc < kIterMaxW; ++cc) acc[cc] = 0.0;
-        for (int32_t r = r0 + lane; r < r1; r += 64) {
-          const double* src = &aQ[a.seg_q[r] * W];
+#pragma unroll
+        for (int k = 0; k < kIterK; ++k) {
+          if (qc[k] < 0) continue;
+          const double* src = &aQ[qc[k] * WS];
+#pragma unroll
+          for (int cc = 0; cc < kIterMaxW; ++cc)
+            if (cc < W) acc[cc] += src[cc];
+        }
+        for (int32_t r = rtail; r < r1; r += 64) {
+          const double* src = &aQ[a.seg_q[r] * WS];
 #pragma unroll
           for (int cc = 0; cc < kIterMaxW; ++cc)
             if (cc < W) acc[cc] += src[cc];
@@ -478,8 +521,16 @@ __global__ __launch_bounds__(kIterThreads) void k_iter(IterArgs a) {
 #pragma unroll
         for (int cc = 0; cc < kIterMaxW; ++cc) ap[cc] = cc < W ? a.alphaP[(int64_t)h * a.p + a.c0 + cc] : 0.0;
       }
-      for (int32_t r = r0 + lane; r < r1; r += 64) {
-        double* dst = &tQ[a.seg_q[r] * W];
+#pragma unroll
+      for (int k = 0; k < kIterK; ++k) {
+        if (qc[k] < 0) continue;
+        double* dst = &tQ[qc[k] * WS];
+#pragma unroll
+        for (int cc = 0; cc < kIterMaxW; ++cc)
+          if (cc < W) atomicAdd(&dst[cc], ap[cc]);
+      }
+      for (int32_t r = rtail; r < r1; r += 64) {
+        double* dst = &tQ[a.seg_q[r] * WS];
 #pragma unroll
         for (int cc = 0; cc < kIterMaxW; ++cc)
           if (cc < W) atomicAdd(&dst[cc], ap[cc]);
@@ -489,7 +540,7 @@ __global__ __launch_bounds__(kIterThreads) void k_iter(IterArgs a) {
   if (a.mode == IT_REDUCE) return;
   __syncthreads();
   for (int j = tid; j < a.G_Q * W; j += kIterThreads) {
-    const double v = tQ[j];
+    const double v = tQ[(j / W) * WS + (j % W)];
     if (v != 0.0) atomicAdd(&a.T_Q[(int64_t)(j / W) * a.p + a.c0 + (j % W)], v);
   }
 }
@@ -532,7 +583,7 @@ bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order) {
   if (c->F != 2 || c->L.w || c->L.P < 0 || !c->L.permuted) return false;
   if (order.back() != c->L.P) return false;
   const int Q = 1 - c->L.P;
-  return (int64_t)c->fe[Q].G * 2 * 8 <= 128 * 1024;  // W >= 1 columns of alpha_Q and T_Q in LDS
+  return (int64_t)c->fe[Q].G * 2 * 8 <= kIterLds;  // W >= 1 columns of alpha_Q and T_Q in LDS
 }
 
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out) {
@@ -542,12 +593,14 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   LFE_TRY(build_segments(c, Q));
   LFE_TRY(ensure_f64(c, c->alpha_spare, c->alpha_spare_cap, (size_t)fq.G * p));
   LFE_TRY(ensure_dred(c, 1));
-  // column groups: 2 * G_Q * W doubles of LDS
-  int W = (int)std::min<int64_t>(kIterMaxW, (128 * 1024 / 16) / std::max<int32_t>(fq.G, 1));
+  // column groups: 2 * G_Q * (W | 1) doubles of LDS (odd row stride, see k_iter)
+  const int64_t wmax = (kIterLds / 16) / std::max<int32_t>(fq.G, 1);  // max odd-padded stride
+  int W = (int)std::min<int64_t>(kIterMaxW, wmax);
+  if ((W | 1) > wmax) --W;
   W = std::max(1, std::min(W, p));
   const int ng = (p + W - 1) / W;
   W = (p + ng - 1) / ng;
-  const size_t lds = sizeof(double) * 2 * (size_t)fq.G * W;
+  const size_t lds = sizeof(double) * 2 * (size_t)fq.G * (W | 1);
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iter), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)std::max<size_t>(lds, 1)));
   const int nblocks = std::max(1, std::min(256, (c->n_units + 15) / 16));

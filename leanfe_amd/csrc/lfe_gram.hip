@@ -19,6 +19,7 @@
 #include "lfe_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace lfe {
 
@@ -43,6 +44,7 @@ struct GramArgs {
   int stage;            // 1: the primary FE's alpha slice is staged in LDS per item
   int nq;               // number of non-primary FEs
   int qf[kMaxFE];       // their FE indices
+  int G_Q;              // levels of qf[0] (its alpha table staged in LDS when it fits)
 };
 
 template <int NT>
@@ -84,11 +86,11 @@ __device__ __forceinline__ void mfma_rows(const double (&z)[4][NT], d4* acc) {
 }
 
 // LDS reduction of the 4 waves' accumulators -> partial[blockIdx.x]
-template <int NT>
+template <int NT, int TH>
 __device__ __forceinline__ void block_reduce_store(const d4* acc, double* red, double* out, int tid) {
   using Sh = GramShape<NT>;
   const int lane = tid & 63, wave = tid >> 6;
-  for (int wv = 0; wv < 4; ++wv) {
+  for (int wv = 0; wv < TH / 64; ++wv) {
     __syncthreads();
     if (wave == wv) {
 #pragma unroll
@@ -101,7 +103,7 @@ __device__ __forceinline__ void block_reduce_store(const d4* acc, double* red, d
     }
   }
   __syncthreads();
-  for (int e = tid; e < Sh::LEN; e += kGramThreads) out[e] = red[e];
+  for (int e = tid; e < Sh::LEN; e += TH) out[e] = red[e];
 }
 
 // Gram of a small row-major table (cluster score sums): Z = table[rows][tcols]
@@ -128,21 +130,27 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_table(GramArgs a, double*
     }
     mfma_rows<NT>(z, acc);
   }
-  block_reduce_store<NT>(acc, red, partial + (int64_t)blockIdx.x * pstride, tid);
+  block_reduce_store<NT, kGramThreads>(acc, red, partial + (int64_t)blockIdx.x * pstride, tid);
 }
 
 // Design Gram / residual pass over the bucket layout.
 // MODE: design / resid; NT: 16-column slots per lane; FQ: max non-primary FEs;
-// GU: 16-row groups per wave iteration; WT: weighted fit.
+// GU: 16-row groups per wave iteration; WT: weighted fit; QL: the (single)
+// non-primary FE's alpha table is staged in LDS (an L2 gather of 88-byte rows
+// costs half the bandwidth of the pass, tools/ubench_gram.hip); TH: threads.
 // Every load address is valid for every lane: lanes without a data column read
 // column 0 and rows outside the item get primary code -1, so nothing is
 // predicated and each row's validity is the single test h >= 0.
-template <int MODE, int NT, int FQ, int GU, bool WT>
-__global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __restrict__ partial, int64_t pstride) {
+template <int MODE, int NT, int FQ, int GU, bool WT, bool QL, int TH>
+__global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ partial, int64_t pstride) {
   using Sh = GramShape<NT>;
+  constexpr int NW = TH / 64;
   __shared__ double red[Sh::LEN];
-  __shared__ double stat_red[4][4];
-  extern __shared__ __attribute__((aligned(16))) double slice[];  // [B][p] alpha_P slice of the item's bucket
+  __shared__ double stat_red[NW][4];
+  extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
+  // dynamic LDS: [B][p] alpha_P slice of the item's bucket, then (QL) [G_Q][p] alpha_Q
+  double* slice = dyn_lds;
+  double* aqL = dyn_lds + (QL ? a.B * a.la.p : 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kq = lane >> 4, c = lane & 15;
@@ -173,6 +181,11 @@ __global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __res
   }
   const double beta0 = (MODE == GRAM_RESID) ? a.beta[0] : 0.0;
   const int nq = a.nq < FQ ? a.nq : FQ;
+  if (QL) {
+    const double* src = a.la.alpha[a.qf[0]];
+    for (int j = tid; j < a.G_Q * p; j += TH) aqL[j] = src[j];
+    __syncthreads();
+  }
 
   // a contiguous range of items per block (all blocks co-resident): the
   // primary slice is staged again only when the bucket changes
@@ -184,7 +197,7 @@ __global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __res
     const int lo = it.x << a.la.s;
     if (a.stage && it.x != staged) {
       __syncthreads();
-      for (int j = tid; j < a.B * p; j += kGramThreads) {
+      for (int j = tid; j < a.B * p; j += TH) {
         const int g = lo + j / p;
         slice[j] = g < a.G_P ? a.la.alpha[P][(int64_t)g * p + (j % p)] : 0.0;
       }
@@ -192,7 +205,7 @@ __global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __res
       staged = it.x;
     }
     const int g0 = it.y >> 4, g1 = (it.z + 15) >> 4;
-    constexpr int step = 4 * GU;
+    constexpr int step = NW * GU;
     // software pipeline: the codes of a batch are loaded one iteration ahead,
     // so X loads, every group's alpha gathers and the next codes are in flight together
     int hq[GU][4], cq[GU][FQ][4];
@@ -257,7 +270,7 @@ __global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __res
             const uint32_t ro = (uint32_t)cq[u][q][s] * (uint32_t)p;
 #pragma unroll
             for (int I = 0; I < NT; ++I) {
-              const double v = aq[ro + (uint32_t)xl[I]];
+              const double v = QL ? aqL[ro + (uint32_t)xl[I]] : aq[ro + (uint32_t)xl[I]];
               ga[u][s][I] = (q == 0) ? v : ga[u][s][I] + v;
             }
           }
@@ -359,7 +372,7 @@ __global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __res
   }
 
   double* out = partial + (int64_t)blockIdx.x * pstride;
-  block_reduce_store<NT>(acc, red, out, tid);
+  block_reduce_store<NT, TH>(acc, red, out, tid);
   if (MODE == GRAM_RESID) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -367,7 +380,11 @@ __global__ __launch_bounds__(kGramThreads) void k_gram(GramArgs a, double* __res
     if (lane == 0)
       for (int s = 0; s < 4; ++s) stat_red[wave][s] = st[s];
     __syncthreads();
-    if (tid < 4) out[Sh::LEN + tid] = stat_red[0][tid] + stat_red[1][tid] + stat_red[2][tid] + stat_red[3][tid];
+    if (tid < 4) {
+      double t = 0.0;
+      for (int w = 0; w < NW; ++w) t += stat_red[w][tid];
+      out[Sh::LEN + tid] = t;
+    }
   }
 }
 
@@ -438,16 +455,35 @@ int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* fl
   return LFE_OK;
 }
 
+// row groups per wave iteration for the 2-FE kernels (LFE_GRAM_GU overrides, for tuning)
+static int gram_gu(int /*NT*/) {
+  static const int env = [] {
+    const char* e = getenv("LFE_GRAM_GU");
+    return e ? atoi(e) : 0;
+  }();
+  if (env == 1 || env == 2 || env == 4) return env;
+  return 2;  // measured: GU 2 beats 1 and 4 at NT = 1 (occupancy 4 vs 2 waves/SIMD)
+}
+
+constexpr int kGramThreadsQL = 1024;  // alpha_Q in LDS: one 110 KB workgroup per CU, 16 waves
+
 template <int MODE, int NT>
-static const void* gram_kernel(bool general, bool weighted) {
-  constexpr int GU = NT == 1 ? 4 : 2;
+static const void* gram_kernel(bool general, bool weighted, bool ql) {
   if (MODE == GRAM_TABLE) return reinterpret_cast<const void*>(&k_gram_table<NT>);
   constexpr int M = MODE == GRAM_TABLE ? GRAM_DESIGN : MODE;
-  if (!general)
-    return weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, true>)
-                    : reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, false>);
-  return weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, true>)
-                  : reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, false>);
+  if (general)
+    return weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, true, false, kGramThreads>)
+                    : reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, false, false, kGramThreads>);
+  const int gu = gram_gu(NT);
+  if (ql && NT == 1) {
+    // 16 waves per CU need <= 128 VGPRs: GU 2
+    return weighted ? reinterpret_cast<const void*>(&k_gram<M, 1, 1, 2, true, true, kGramThreadsQL>)
+                    : reinterpret_cast<const void*>(&k_gram<M, 1, 1, 2, false, true, kGramThreadsQL>);
+  }
+#define GRAM_FN(GU) (weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, true, false, kGramThreads>) \
+                              : reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, false, false, kGramThreads>))
+  return gu == 1 ? GRAM_FN(1) : gu == 2 ? GRAM_FN(2) : GRAM_FN(4);
+#undef GRAM_FN
 }
 
 template <int MODE, int NT>
@@ -455,21 +491,31 @@ static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
   using Sh = GramShape<NT>;
   int nblocks;
   size_t dyn = 0;
+  int threads = kGramThreads;
   a.nq = 0;
   for (int f = 0; f < a.la.F; ++f)
     if (f != a.la.P) a.qf[a.nq++] = f;
-  // lean instantiation for <= 1 non-primary FE (the 2-FE case), general one otherwise
-  const void* fn = gram_kernel<MODE, NT>(a.nq > 1, a.w != nullptr);
+  a.G_Q = a.nq > 0 ? c->fe[a.qf[0]].G : 0;
+  const void* fn = nullptr;
   if (MODE == GRAM_TABLE) {
+    fn = gram_kernel<MODE, NT>(false, false, false);
     const int64_t ngroups = (a.rows + 15) / 16;
     nblocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + 3) / 4, 1), 2048);
   } else {
     const size_t sbytes = sizeof(double) * (size_t)a.B * a.la.p;
     a.stage = (a.la.P >= 0 && sbytes <= 96 * 1024) ? 1 : 0;
     dyn = a.stage ? sbytes : 0;
+    // one non-primary FE whose alpha table fits next to the slice: stage it in LDS
+    const size_t qbytes = sizeof(double) * (size_t)a.G_Q * a.la.p;
+    const bool ql = NT == 1 && a.nq == 1 && a.stage && dyn + qbytes <= 150 * 1024;
+    if (ql) {
+      dyn += qbytes;
+      threads = kGramThreadsQL;
+    }
+    fn = gram_kernel<MODE, NT>(a.nq > 1, a.w != nullptr, ql);
     if (dyn > 64 * 1024)  // dynamic LDS above 64 KB must be opted in
       LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-    nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kGramThreads, dyn)));
+    nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, threads, dyn)));
   }
   const int64_t pstride = Sh::LEN + 4;
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
@@ -478,7 +524,7 @@ static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
     ProfScope _ps(c, MODE == GRAM_DESIGN ? K_GRAM_DESIGN : (MODE == GRAM_RESID ? K_GRAM_RESID : K_GRAM_TABLE));
     double* part = c->scratch;
     void* args[] = {&a, &part, const_cast<int64_t*>(&pstride)};
-    LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(kGramThreads), args, dyn, c->stream));
+    LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, dyn, c->stream));
   }
   LFE_HIP(hipGetLastError());
   const int len = Sh::LEN + extra;

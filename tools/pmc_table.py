@@ -30,8 +30,11 @@ for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
 
 want = ["ms", "FETCH_GB", "WRITE_GB", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
         "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "L2hit"]
+if len(sys.argv) > 2:
+    want = ["ms"] + sys.argv[2].split(",")
 print("%-28s" % "kernel" + "".join("%14s" % w[-14:] for w in want))
-for k in sorted(vals, key=lambda k: -sum(dur.get(k, [0])) / max(len(dur.get(k, [1])), 1)):
+n_show = 14
+for k in sorted(vals, key=lambda k: -sum(dur.get(k, [0])) / max(len(dur.get(k, [1])), 1))[:n_show]:
     cs = vals[k]
     avg = lambda c: sum(cs[c]) / len(cs[c]) if cs.get(c) else float("nan")
     row = {
@@ -39,8 +42,10 @@ for k in sorted(vals, key=lambda k: -sum(dur.get(k, [0])) / max(len(dur.get(k, [
         "FETCH_GB": 2 * avg("FETCH_SIZE") * 1024 / 1e9,
         "WRITE_GB": avg("WRITE_SIZE") * 1024 / 1e9,
     }
-    for c in want[3:-1]:
-        row[c] = avg(c)
+    for c in want:
+        if c not in row and c != "L2hit":
+            row[c] = avg(c)
     h, m = avg("TCC_HIT_sum"), avg("TCC_MISS_sum")
-    row["L2hit"] = h / (h + m) if h + m else float("nan")
+    if "L2hit" in want:
+        row["L2hit"] = h / (h + m) if h + m else float("nan")
     print("%-28s" % k[:28] + "".join("%14.4g" % row[w] for w in want))
