@@ -53,23 +53,23 @@ struct Sums4Args {
 };
 
 // FQ: max non-primary FEs held in registers; GU: 16-row groups loaded before use;
-// NT: 16-column slots per lane (p <= 16 NT)
-template <int FQ, int GU, int NT>
-__global__ __launch_bounds__(kSumThreads) void k_sums4(Sums4Args a) {
+// NT: 16-column slots per lane (p <= 16 NT); TH: threads per workgroup
+template <int FQ, int GU, int NT, int TH>
+__global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int nwv = kSumThreads / 64;
+  constexpr int nwv = TH / 64;
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.la.p, P = a.la.P, F = a.la.F;
   const int nq = a.nq < FQ ? a.nq : FQ;
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
-      for (int j = tid; j < a.G[f] * p; j += kSumThreads) lds[a.tab_off[f] + j] = 0.0;
+      for (int j = tid; j < a.G[f] * p; j += TH) lds[a.tab_off[f] + j] = 0.0;
   // primary slice [B][p] of the current bucket: flushed to S_P (and zeroed) on a
   // bucket change; a block owns a contiguous range of items
   auto flush = [&](int b) {
     const int lo = b << a.la.s;
-    for (int j = tid; j < a.B * p; j += kSumThreads) {
+    for (int j = tid; j < a.B * p; j += TH) {
       const double val = lds[j];
       const int g = lo + j / p;
       if (val != 0.0 && g < a.G_P) atomicAdd(&a.S[P][(int64_t)g * p + (j % p)], val);
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kSumThreads) void k_sums4(Sums4Args a) {
     }
   };
   if (a.slice)
-    for (int j = tid; j < a.B * p; j += kSumThreads) lds[j] = 0.0;
+    for (int j = tid; j < a.B * p; j += TH) lds[j] = 0.0;
   const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
   const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
   int cur = -1;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kSumThreads) void k_sums4(Sums4Args a) {
   if (a.slice && cur >= 0) flush(cur);
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
-      for (int j = tid; j < a.G[f] * p; j += kSumThreads) {
+      for (int j = tid; j < a.G[f] * p; j += TH) {
         const double val = lds[a.tab_off[f] + j];
         if (val != 0.0) atomicAdd(&a.S[f][j], val);
       }
@@ -181,24 +181,32 @@ int sums4(lfe_ctx* c) {
   const size_t lds = off * 8;
   const int NT = (p + 15) / 16;
   const void* fn = nullptr;
-#define SUMS4_FN(FQ, GU, NT_) reinterpret_cast<const void*>(&k_sums4<FQ, GU, NT_>)
+#define SUMS4_FN(FQ, GU, NT_, TH_) reinterpret_cast<const void*>(&k_sums4<FQ, GU, NT_, TH_>)
   static const int gu_env = [] {
     const char* e = getenv("LFE_SUMS_GU");  // tuning override
     return e ? atoi(e) : 0;
   }();
-  if (a.nq <= 1 && NT == 1)
-    fn = gu_env == 1 ? SUMS4_FN(1, 1, 1) : gu_env == 2 ? SUMS4_FN(1, 2, 1) : SUMS4_FN(1, 4, 1);
-  else if (a.nq <= 1)
-    fn = NT == 2 ? SUMS4_FN(1, 2, 2) : NT == 3 ? SUMS4_FN(1, 2, 3) : SUMS4_FN(1, 2, 4);
-  else
-    fn = NT == 1 ? SUMS4_FN(7, 1, 1) : NT == 2 ? SUMS4_FN(7, 1, 2) : NT == 3 ? SUMS4_FN(7, 1, 3) : SUMS4_FN(7, 1, 4);
+  int threads = kSumThreads;
+  if (a.nq <= 1 && NT == 1) {
+    // the 2-FE case: one workgroup per CU (LDS), so 16 waves of <= 128 VGPRs (GU 2)
+    threads = gu_env == 4 ? kSumThreads : 1024;
+    fn = gu_env == 4 ? SUMS4_FN(1, 4, 1, kSumThreads) : SUMS4_FN(1, 2, 1, 1024);
+  } else if (a.nq <= 1) {
+    fn = NT == 2 ? SUMS4_FN(1, 2, 2, kSumThreads) : NT == 3 ? SUMS4_FN(1, 2, 3, kSumThreads)
+                                                    : SUMS4_FN(1, 2, 4, kSumThreads);
+  } else {
+    fn = NT == 1   ? SUMS4_FN(7, 1, 1, kSumThreads)
+         : NT == 2 ? SUMS4_FN(7, 1, 2, kSumThreads)
+         : NT == 3 ? SUMS4_FN(7, 1, 3, kSumThreads)
+                   : SUMS4_FN(7, 1, 4, kSumThreads);
+  }
 #undef SUMS4_FN
   LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 1)));
-  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kSumThreads, lds)));
+  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, threads, lds)));
   {
     ProfScope _ps(c, K_GROUP_SUMS);
     void* args[] = {&a};
-    LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(kSumThreads), args, lds, c->stream));
+    LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, lds, c->stream));
   }
   LFE_HIP(hipGetLastError());
   for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_f64(c, c->fe[f].S, (size_t)c->fe[f].G * p));

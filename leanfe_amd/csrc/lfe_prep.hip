@@ -415,7 +415,11 @@ int prepare_layout(lfe_ctx* c) {
   if (L.permuted) {
     // ---- partition by bucket of P ----
     const int nb = L.nb;
-    const int per = nb <= 512 ? 16 : 8;  // rows per thread of the staged scatter
+    // rows per thread of the staged scatter.  Measured at 50M rows x 391 buckets: one
+    // 8192-row chunk per workgroup with consecutive chunks in flight together is the
+    // fastest form (4096-row chunks, several chunks per workgroup, a software-pipelined
+    // column loop and register scatter without the LDS stage were all 20-60 % slower)
+    const int per = nb <= 512 ? 16 : 8;
     const int64_t cw = (int64_t)kPartThreads * per;
     const int nw = (int)((n + cw - 1) / cw);
     const int64_t m = (int64_t)nb * nw;
