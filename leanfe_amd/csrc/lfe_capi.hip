@@ -69,6 +69,7 @@ int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds) {
 int ensure_items(lfe_ctx* c, size_t n_items) { return ensure(c->items_d, c->items_cap, 4 * n_items); }
 int ensure_i32(lfe_ctx*, int32_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 int ensure_f64(lfe_ctx*, double*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
+int ensure_u16(lfe_ctx*, uint16_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 
 int ensure_pcounts(lfe_ctx* c, size_t elems, size_t sums) {
   LFE_TRY(ensure(c->pcounts, c->pcounts_elems, elems));
@@ -104,7 +105,8 @@ int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count) {
 
 const char* const kKernelNames[K_NUM_KERNELS] = {
     "part_hist", "scan", "part_scatter", "count", "mark", "group_sums", "cross", "check", "finalize",
-    "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth"};
+    "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth",
+    "tp", "tq"};
 
 static hipEvent_t prof_event(lfe_ctx* c) {
   if (!c->prof.pool.empty()) {
@@ -311,6 +313,8 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   dfree(c->seg_q);
   dfree(c->seg_aux);
   dfree(c->seg_units);
+  dfree(c->run_off);
+  dfree(c->run_h);
   dfree(c->alpha_spare);
   dfree(c->dbeta);
   dfree(c->clS);

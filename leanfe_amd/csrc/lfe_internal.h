@@ -61,7 +61,7 @@ struct FeState {
 enum KernelId {
   K_PART_HIST = 0, K_SCAN, K_PART_SCATTER, K_COUNT, K_MARK, K_GROUP_SUMS, K_CROSS, K_CHECK, K_FINALIZE,
   K_CHECK_MAX, K_GRAM_DESIGN, K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_MISC, K_SYNTH,
-  K_NUM_KERNELS
+  K_TP, K_TQ, K_NUM_KERNELS
 };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 
@@ -122,7 +122,7 @@ struct lfe_ctx {
   int32_t* bitems_d = nullptr;   // device [nb + 1]: first work item of each bucket
   size_t bitems_cap = 0;
   // segment layout (fast path, F == 2): kept rows sorted by the primary code
-  int32_t* seg_off = nullptr;    // [G_P + 1] local row offsets of each primary group
+  int32_t* seg_off = nullptr;    // [nb * B + 1] local row offsets of each primary group
   size_t seg_off_cap = 0;
   int32_t* seg_q = nullptr;      // [ld] secondary codes in segment order
   size_t seg_q_cap = 0;
@@ -130,6 +130,11 @@ struct lfe_ctx {
   size_t seg_aux_cap = 0;
   int32_t* seg_units = nullptr;  // [n_units + 1] first primary group of each work unit
   size_t seg_units_cap = 0;
+  // run layout (fast path): kept rows of each bucket sorted by the secondary code
+  int32_t* run_off = nullptr;    // [nb * G_Q + 1] offsets of the (bucket, q) runs
+  size_t run_off_cap = 0;
+  uint16_t* run_h = nullptr;     // [ld] primary code - bucket base, run order
+  size_t run_h_cap = 0;
   int n_units = 0;
   double* alpha_spare = nullptr; // [G_Q * p] double buffer for the secondary alpha
   size_t alpha_spare_cap = 0;
@@ -169,8 +174,9 @@ namespace lfe {
 // --- prep / partition (lfe_prep.hip) ---
 int prepare_layout(lfe_ctx* c);   // partition + counts + singleton marks
 
-// --- fast paths (lfe_fast.hip) ---
+// --- group sums (lfe_fast.hip) ---
 int sums4(lfe_ctx* c);
+// --- two-FE sweeps (lfe_iter.hip) ---
 bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order);
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out);
 
@@ -198,6 +204,7 @@ int ensure_pcounts(lfe_ctx* c, size_t elems, size_t sums);
 int ensure_items(lfe_ctx* c, size_t n_items);
 int ensure_i32(lfe_ctx* c, int32_t*& p, size_t& cap, size_t elems);
 int ensure_f64(lfe_ctx* c, double*& p, size_t& cap, size_t elems);
+int ensure_u16(lfe_ctx* c, uint16_t*& p, size_t& cap, size_t elems);
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
 // blocks of `fn` that fit on the whole device at once (occupancy API x CUs)
 int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds);

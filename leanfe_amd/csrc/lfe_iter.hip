@@ -1,0 +1,747 @@
+// leanfe HIP engine — alternating projections for two fixed effects, the
+// headline case (polars_impl.py:490-526, strategy 'alt_proj', unweighted).
+//
+// alpha-form sweep, order [Q, P] (ascending cardinality, polars_impl.py:476-480):
+//     T_P[h]   = sum_{i in h} alpha_Q[q_i]            (K1)
+//     alpha_P  = (S_P - T_P) / n_P                     projection of P
+//     T_Q'[q]  = sum_{i in q} alpha_P[h_i]            (K2)
+//     alpha_Q' = (S_Q - T_Q') / n_Q                    next sweep's Q projection
+// The stop test after a sweep (max_g |mean_g(y~)|, y only, polars_impl.py:511-521)
+// is exactly |alpha_Q' - alpha_Q| on the y column (0 for the just-projected P),
+// so it costs nothing extra.
+//
+// Both cross terms are segmented sums over a codes-only row layout, so neither
+// pass needs a per-row atomic (per-row LDS f64 atomics bound the earlier
+// version at ~2.7 lane-ops/clk/CU):
+//   segment layout: kept rows of each bucket sorted by the primary code h;
+//                   per row the secondary code q (int32).  K1: per segment,
+//                   gather alpha_Q[q] rows from an LDS copy of alpha_Q.
+//   run layout:     kept rows of each bucket sorted by q; per row h - lo
+//                   (uint16).  K2: per (bucket, q) run, gather alpha_P rows
+//                   from the bucket's LDS slice; one global atomic add per run
+//                   and column (nb * G_Q runs, ~1/128 of the rows here).
+// Both passes use the MFMA lane layout of the Gram kernels (lane = row quad x
+// column): a 16-row group is one aligned int4 / ushort4 load per lane and four
+// conflict-free LDS row gathers; rows outside the current segment/run index a
+// zero row of the LDS table, so nothing is predicated.  Codes are loaded a
+// batch of groups ahead.  Multi-GPU: T_P (when P's projection needs the
+// all-reduce) and T_Q are reduced over ranks between the passes.
+#include "lfe_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <type_traits>
+
+namespace lfe {
+
+// ===========================================================================
+// 1. bucket-local counting sort (segment and run layouts)
+// ===========================================================================
+// Key of a kept row: KEYQ ? its secondary code : its primary code - lo (the
+// offset in its bucket); value stored: the other one.  Stable and
+// deterministic (per-wave cursors ranked by LDS atomics in lane order, as in
+// the partition scatter of lfe_prep.hip).
+
+template <bool KEYQ>
+__global__ __launch_bounds__(256) void k_ls_hist(const int4* __restrict__ items, const int32_t* __restrict__ codeP,
+                                                 const int32_t* __restrict__ codeQ, int s, int K,
+                                                 int32_t* __restrict__ itemcnt) {
+  extern __shared__ int32_t h[];
+  const int4 it = items[blockIdx.x];
+  const int lo = it.x << s;
+  for (int j = threadIdx.x; j < K; j += blockDim.x) h[j] = 0;
+  __syncthreads();
+  for (int32_t i = it.y + threadIdx.x; i < it.z; i += blockDim.x) {
+    const int32_t g = codeP[i];
+    if (g >= 0) atomicAdd(&h[KEYQ ? codeQ[i] : g - lo], 1);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < K; j += blockDim.x) itemcnt[(int64_t)blockIdx.x * K + j] = h[j];
+}
+
+// per (bucket, key): exclusive scan over the bucket's items -> item bases; total -> off[b K + key]
+__global__ void k_ls_base(const int32_t* __restrict__ bitems, int nb, int K, int32_t* __restrict__ itemcnt,
+                          int32_t* __restrict__ off) {
+  const int64_t total = (int64_t)nb * K;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / K), j = (int)(e % K);
+    int32_t run = 0;
+    for (int i = bitems[b]; i < bitems[b + 1]; ++i) {
+      const int32_t t = itemcnt[(int64_t)i * K + j];
+      itemcnt[(int64_t)i * K + j] = run;
+      run += t;
+    }
+    off[e] = run;
+  }
+}
+
+constexpr int kLsThreads = 512;
+constexpr int kLsWaves = kLsThreads / 64;
+constexpr int kLsPer = 8;
+constexpr int kLsRows = kLsThreads * kLsPer;
+
+static size_t ls_scatter_lds(int K, int ncur) {
+  return sizeof(int32_t) * ((size_t)ncur * K + 3 * (size_t)K + 2 * (size_t)kLsRows);
+}
+
+// NCUR: cursor sets (kLsWaves: one per wave, stable; 1: shared, unstable)
+template <bool KEYQ, typename VT, int NCUR>
+__global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restrict__ items,
+                                                           const int32_t* __restrict__ codeP,
+                                                           const int32_t* __restrict__ codeQ, int s, int K,
+                                                           const int32_t* __restrict__ off,
+                                                           const int32_t* __restrict__ itembase,
+                                                           VT* __restrict__ out) {
+  extern __shared__ int32_t sm[];
+  int32_t* cur = sm;              // [NCUR][K]
+  int32_t* run = cur + NCUR * K;  // [K] next free slot of each key
+  int32_t* tot = run + K;             // [K]
+  int32_t* delta = tot + K;           // [K]
+  int32_t* stage = delta + K;         // [kLsRows]
+  int32_t* sb = stage + kLsRows;      // [kLsRows]
+  __shared__ int32_t wsum[kLsWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int4 it = items[blockIdx.x];
+  const int lo = it.x << s;
+  for (int j = tid; j < K; j += kLsThreads)
+    run[j] = off[(int64_t)it.x * K + j] + itembase[(int64_t)blockIdx.x * K + j];
+  for (int32_t r0 = it.y; r0 < it.z; r0 += kLsRows) {
+    const int32_t r1 = min(it.z, r0 + kLsRows);
+    const int32_t wbase = r0 + wave * kLsPer * 64;
+    __syncthreads();
+    for (int j = tid; j < NCUR * K; j += kLsThreads) cur[j] = 0;
+    __syncthreads();
+    int32_t key[kLsPer], val[kLsPer];
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k) {
+      const int32_t i = wbase + k * 64 + lane;
+      key[k] = -1;
+      if (i < r1) {
+        const int32_t g = codeP[i];
+        if (g >= 0) {
+          const int32_t q = codeQ[i];
+          key[k] = KEYQ ? q : g - lo;
+          val[k] = KEYQ ? g - lo : q;
+          atomicAdd(&cur[(NCUR > 1 ? wave : 0) * K + key[k]], 1);
+        }
+      }
+    }
+    __syncthreads();
+    for (int j = tid; j < K; j += kLsThreads) {  // per key: exclusive scan over waves
+      int32_t t = 0;
+      for (int w2 = 0; w2 < NCUR; ++w2) {
+        const int32_t hh = cur[w2 * K + j];
+        cur[w2 * K + j] = t;
+        t += hh;
+      }
+      tot[j] = t;
+    }
+    __syncthreads();
+    {  // exclusive scan of tot over keys
+      const int per = (K + kLsThreads - 1) / kLsThreads;
+      const int b0 = tid * per;
+      int32_t sum = 0;
+      for (int k = 0; k < per; ++k)
+        if (b0 + k < K) sum += tot[b0 + k];
+      int32_t x = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) wsum[wave] = x;
+      __syncthreads();
+      int32_t wofs = 0;
+      for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[w2];
+      int32_t acc = x - sum + wofs;
+      __syncthreads();
+      for (int k = 0; k < per; ++k)
+        if (b0 + k < K) {
+          const int32_t t = tot[b0 + k];
+          tot[b0 + k] = acc;
+          acc += t;
+        }
+    }
+    __syncthreads();
+    for (int j = tid; j < K; j += kLsThreads) {
+      const int32_t boff = tot[j];
+      delta[j] = run[j] - boff;
+      for (int w2 = 0; w2 < NCUR; ++w2) cur[w2 * K + j] += boff;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k)
+      if (key[k] >= 0) {
+        const int32_t pos = atomicAdd(&cur[(NCUR > 1 ? wave : 0) * K + key[k]], 1);
+        stage[pos] = val[k];
+        sb[pos] = key[k];
+      }
+    __syncthreads();
+    const int32_t nk = cur[(NCUR - 1) * K + (K - 1)];  // kept rows of this sub-chunk
+    for (int j = tid; j < nk; j += kLsThreads) out[delta[sb[j]] + j] = (VT)stage[j];
+    __syncthreads();
+    for (int j = tid; j < K; j += kLsThreads) run[j] = delta[j] + cur[(NCUR - 1) * K + j];
+  }
+}
+
+// first segment (primary group) of each work unit of ~U kept rows
+__global__ void k_unit_bounds(const int32_t* __restrict__ seg_off, int32_t H, int64_t U, int n_units,
+                              int32_t* __restrict__ units) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k <= n_units; k += gridDim.x * blockDim.x) {
+    if (k == n_units) {
+      units[k] = H;
+      continue;
+    }
+    const int64_t target = (int64_t)k * U;
+    int lo = 0, hi = H;  // first h with seg_off[h] >= target
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (seg_off[mid] < target) lo = mid + 1;
+      else hi = mid;
+    }
+    units[k] = lo;
+  }
+}
+
+// bucket-local counting sort of the kept rows; off = [nb K + 1] exclusive offsets
+template <bool KEYQ, typename VT>
+static int local_sort(lfe_ctx* c, int Q, int K, int32_t*& off, size_t& off_cap, VT* out) {
+  auto& L = c->L;
+  const int P = L.P;
+  const size_t m = (size_t)L.nb * K;
+  LFE_TRY(ensure_i32(c, c->seg_aux, c->seg_aux_cap, (size_t)L.n_items * K));
+  LFE_TRY(ensure_i32(c, off, off_cap, m + 1));
+  const int4* items = reinterpret_cast<const int4*>(c->items_d);
+  LFE_HIP(hipMemsetAsync(off, 0, sizeof(int32_t) * (m + 1), c->stream));
+  {
+    ProfScope _ps(c, K_MISC);
+    hipLaunchKernelGGL(k_ls_hist<KEYQ>, dim3(L.n_items), dim3(256), sizeof(int32_t) * K, c->stream, items,
+                       L.code[P], L.code[Q], L.s, K, c->seg_aux);
+  }
+  {
+    ProfScope _ps(c, K_MISC);
+    hipLaunchKernelGGL(k_ls_base, dim3(grid_for((int64_t)m)), dim3(kBlock), 0, c->stream, c->bitems_d, L.nb, K,
+                       c->seg_aux, off);
+  }
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(exclusive_scan(c, off, (int64_t)m + 1));
+  // the run layout ranks with one shared cursor set (unstable inside a run: that
+  // order only sets K2's summation order, which the cross-workgroup atomics into
+  // T_Q leave unordered anyway); per-wave cursors cost O(K x waves) LDS work per
+  // sub-chunk, 3x the whole kernel at K = 1000
+  constexpr int NCUR = KEYQ ? 1 : kLsWaves;
+  const size_t lds = ls_scatter_lds(K, NCUR);
+  const void* fn = reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, NCUR>);
+  if (lds > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  {
+    ProfScope _ps(c, K_MISC);
+    hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR>), dim3(L.n_items), dim3(kLsThreads), lds, c->stream, items,
+                       L.code[P], L.code[Q], L.s, K, off, c->seg_aux, out);
+  }
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+static int build_layouts(lfe_ctx* c, int Q) {
+  auto& L = c->L;
+  const int B = 1 << L.s;
+  const int32_t G_Q = c->fe[Q].G;
+  LFE_TRY(ensure_i32(c, c->seg_q, c->seg_q_cap, (size_t)c->ld));
+  LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_off, c->seg_off_cap, c->seg_q)));
+  LFE_TRY(ensure_u16(c, c->run_h, c->run_h_cap, (size_t)c->ld));
+  LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->run_off, c->run_off_cap, c->run_h)));
+  // work units of ~2048 kept rows (whole segments) for K1
+  const int64_t U = 2048;
+  const int32_t H = L.nb * B;
+  c->n_units = (int)std::max<int64_t>(1, (c->n + U - 1) / U);
+  LFE_TRY(ensure_i32(c, c->seg_units, c->seg_units_cap, (size_t)c->n_units + 1));
+  {
+    ProfScope _ps(c, K_MISC);
+    hipLaunchKernelGGL(k_unit_bounds, dim3(grid_for(c->n_units + 1)), dim3(kBlock), 0, c->stream, c->seg_off, H, U,
+                       c->n_units, c->seg_units);
+  }
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+// ===========================================================================
+// 2. the two cross-term passes
+// ===========================================================================
+
+constexpr int kTpThreads = 1024;  // K1: one workgroup per CU (alpha_Q in LDS)
+constexpr int kTqThreads = 512;   // K2: kTqSplit workgroups per bucket
+constexpr int kTqSplit = 2;
+constexpr int kIterLds = 150 * 1024;
+
+// reduce over the 4 row quads of the lane layout (lanes 16 and 32 apart)
+__device__ __forceinline__ double quad_sum(double v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// DPP row_newbcast:D (gfx90a+): every lane of a 16-lane row receives lane D of
+// that row (checked on the device by tools/dpp_check.hip)
+template <int D>
+__device__ __forceinline__ int rowbc(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + D, 0xF, 0xF, false);
+}
+template <int D>
+__device__ __forceinline__ int4 rowbc4(const int4& v) {
+  return int4{rowbc<D>(v.x), rowbc<D>(v.y), rowbc<D>(v.z), rowbc<D>(v.w)};
+}
+// compile-time loop D = B, B + 4, ..., < E
+template <int B, int E, typename Fn>
+__device__ __forceinline__ void static_for4(Fn&& fn) {
+  if constexpr (B < E) {
+    fn(std::integral_constant<int, B>{});
+    static_for4<B + 4, E>(fn);
+  }
+}
+
+// Codes of 16 consecutive 16-row groups [gb, gb + 16) are one load per lane:
+// lane (kq, c) holds quad kq of group gb + c; group gb + d's codes reach the
+// lanes of row kq by row_newbcast:d.  Two such batches are in flight (ping-pong).
+constexpr int kBatch = 16;
+
+struct TpArgs {
+  const int32_t* seg_off;  // [H + 1] segment offsets (h = bucket * B + offset)
+  const int32_t* seg_q;    // secondary code of each kept row, segment order
+  const int32_t* units;    // [n_units + 1] first segment of each work unit
+  int n_units;
+  int G_Q, G_P, p;
+  const double* alphaQ;  // [G_Q][p]
+  const double* S_P;     // [G_P][p]
+  const int32_t* cntP;   // [G_P] kept counts (all ranks)
+  double* out;           // fused: alpha_P [G_P][p]; else T_P [G_P][p]
+  int fused;
+};
+
+// K1: T_P[h] = sum_{i in h} alpha_Q[q_i]; fused: alpha_P[h] = (S_P[h] - T_P[h]) / n_h
+template <int NT>
+__global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double aq[];  // [G_Q + 1][p], row G_Q = 0
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kq = lane >> 4, c = lane & 15;
+  const int p = a.p, G_Q = a.G_Q;
+  for (int j = tid; j < G_Q * p; j += kTpThreads) aq[j] = a.alphaQ[j];
+  for (int j = tid; j < p; j += kTpThreads) aq[G_Q * p + j] = 0.0;
+  __syncthreads();
+  int cl[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) cl[I] = 16 * I + c < p ? 16 * I + c : 0;
+  const int nwaves = gridDim.x * (kTpThreads / 64);
+  for (int u = blockIdx.x * (kTpThreads / 64) + wave; u < a.n_units; u += nwaves) {
+    int h = a.units[u];
+    const int h1 = a.units[u + 1];
+    if (h >= h1) continue;
+    int r0 = a.seg_off[h], r1 = a.seg_off[h + 1];
+    const int g0 = r0 >> 4, g1 = (a.seg_off[h1] + 15) >> 4;
+    double acc[NT];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) acc[I] = 0.0;
+    auto finalize = [&]() {  // segment h complete
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+        const double t = quad_sum(acc[I]);
+        const int col = 16 * I + c;
+        if (kq == 0 && col < p && h < a.G_P) {
+          const int64_t e = (int64_t)h * p + col;
+          if (a.fused) {
+            const int32_t n = a.cntP[h];
+            a.out[e] = n > 0 ? (a.S_P[e] - t) / (double)n : 0.0;
+          } else {
+            a.out[e] = t;
+          }
+        }
+        acc[I] = 0.0;
+      }
+    };
+    bool done = false;
+    // one 16-row group: lane rows g*16 + 4 kq + s
+    auto group = [&](int g, const int4& q4) {
+      const int gs = g * 16, rb = gs + 4 * kq;
+      const int qv[4] = {q4.x, q4.y, q4.z, q4.w};
+      if (gs >= r0 && gs + 16 <= r1) {  // inside segment h (wave-uniform): no masks
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t ro = (uint32_t)qv[s] * (uint32_t)p;
+#pragma unroll
+          for (int I = 0; I < NT; ++I) acc[I] += aq[ro + (uint32_t)cl[I]];
+        }
+        if (gs + 16 < r1) return;
+        finalize();
+        if (++h >= h1) {
+          done = true;
+          return;
+        }
+        r0 = r1;
+        r1 = a.seg_off[h + 1];
+        return;
+      }
+      while (true) {  // the group holds a segment boundary
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = rb + s;
+          const uint32_t ro = (uint32_t)(row >= r0 && row < r1 ? qv[s] : G_Q) * (uint32_t)p;
+#pragma unroll
+          for (int I = 0; I < NT; ++I) acc[I] += aq[ro + (uint32_t)cl[I]];
+        }
+        if (r1 > gs + 16) return;  // segment h continues in the next group
+        finalize();
+        if (++h >= h1) {
+          done = true;
+          return;
+        }
+        r0 = r1;
+        r1 = a.seg_off[h + 1];
+      }
+    };
+    auto load = [&](int gb) -> int4 {
+      const int g = gb + c;
+      return g < g1 ? *reinterpret_cast<const int4*>(a.seg_q + g * 16 + 4 * kq) : int4{0, 0, 0, 0};
+    };
+    auto batch = [&](const int4& v, int gb) {
+      static_for4<0, kBatch>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if (gb + d >= g1 || done) return;
+        const int4 q[4] = {rowbc4<d>(v), rowbc4<d + 1>(v), rowbc4<d + 2>(v), rowbc4<d + 3>(v)};
+        const int gs = (gb + d) * 16;
+        if (gs >= r0 && gs + 64 < r1) {  // 4 groups inside segment h, which continues after them
+          double t[4][NT];
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int I = 0; I < NT; ++I) t[s][I] = 0.0;
+#pragma unroll
+          for (int dd = 0; dd < 4; ++dd) {
+            const int qv[4] = {q[dd].x, q[dd].y, q[dd].z, q[dd].w};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const uint32_t ro = (uint32_t)qv[s] * (uint32_t)p;
+#pragma unroll
+              for (int I = 0; I < NT; ++I) t[s][I] += aq[ro + (uint32_t)cl[I]];
+            }
+          }
+#pragma unroll
+          for (int I = 0; I < NT; ++I) acc[I] += (t[0][I] + t[1][I]) + (t[2][I] + t[3][I]);
+          return;
+        }
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+          if (gb + d + dd >= g1 || done) return;
+          group(gb + d + dd, q[dd]);
+        }
+      });
+    };
+    int4 va = load(g0), vb;
+    for (int gb = g0; gb < g1 && !done;) {
+      vb = load(gb + kBatch);
+      batch(va, gb);
+      gb += kBatch;
+      if (gb >= g1 || done) break;
+      va = load(gb + kBatch);
+      batch(vb, gb);
+      gb += kBatch;
+    }
+  }
+}
+
+struct TqArgs {
+  const int32_t* run_off;  // [nb * G_Q + 1] run offsets
+  const uint16_t* run_h;   // primary code - lo of each kept row, run order
+  int nb, s, G_Q, G_P, p;
+  const double* alphaP;  // [G_P][p]
+  double* T_Q;           // [G_Q][p], accumulated
+};
+
+// K2: T_Q[q] += sum over the (bucket, q) runs of alpha_P[h_i]
+template <int NT>
+__global__ __launch_bounds__(kTqThreads) void k_tq(TqArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sl[];  // [B + 1][p], row B = 0
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NW = kTqThreads / 64;
+  const int kq = lane >> 4, c = lane & 15;
+  const int p = a.p, G_Q = a.G_Q, B = 1 << a.s;
+  int cl[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) cl[I] = 16 * I + c < p ? 16 * I + c : 0;
+  for (int bs = blockIdx.x; bs < a.nb * kTqSplit; bs += gridDim.x) {
+    const int b = bs / kTqSplit, part = bs % kTqSplit;
+    const int lo = b << a.s;
+    __syncthreads();
+    for (int j = tid; j < B * p; j += kTqThreads) {
+      const int g = lo + j / p;
+      sl[j] = g < a.G_P ? a.alphaP[(int64_t)g * p + (j % p)] : 0.0;
+    }
+    for (int j = tid; j < p; j += kTqThreads) sl[B * p + j] = 0.0;
+    __syncthreads();
+    // wave: runs q in [q, q1) of bucket b
+    const int slot = part * NW + wave;
+    int q = slot * G_Q / (NW * kTqSplit);
+    const int q1 = (slot + 1) * G_Q / (NW * kTqSplit);
+    if (q >= q1) continue;
+    const int32_t* off = a.run_off + (int64_t)b * G_Q;
+    int r0 = off[q], r1 = off[q + 1];
+    const int g0 = r0 >> 4, g1 = (off[q1] + 15) >> 4;
+    if (g0 >= g1) continue;
+    double acc[NT];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) acc[I] = 0.0;
+    typedef unsigned short us4 __attribute__((ext_vector_type(4)));
+    auto finalize = [&]() {  // run q complete
+      if (r1 > r0) {
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+          const double t = quad_sum(acc[I]);
+          const int col = 16 * I + c;
+          if (kq == 0 && col < p) atomicAdd(&a.T_Q[(int64_t)q * p + col], t);
+        }
+      }
+#pragma unroll
+      for (int I = 0; I < NT; ++I) acc[I] = 0.0;
+    };
+    bool done = false;
+    auto group = [&](int g, const us4& h4) {
+      const int gs = g * 16, rb = gs + 4 * kq;
+      if (gs >= r0 && gs + 16 <= r1) {  // inside run q (wave-uniform): no masks
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t ro = (uint32_t)h4[s] * (uint32_t)p;
+#pragma unroll
+          for (int I = 0; I < NT; ++I) acc[I] += sl[ro + (uint32_t)cl[I]];
+        }
+        if (gs + 16 < r1) return;
+        finalize();
+        if (++q >= q1) {
+          done = true;
+          return;
+        }
+        r0 = r1;
+        r1 = off[q + 1];
+        return;
+      }
+      while (true) {  // the group holds a run boundary
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = rb + s;
+          const uint32_t ro = (uint32_t)(row >= r0 && row < r1 ? (int)h4[s] : B) * (uint32_t)p;
+#pragma unroll
+          for (int I = 0; I < NT; ++I) acc[I] += sl[ro + (uint32_t)cl[I]];
+        }
+        if (r1 > gs + 16) return;  // run continues in the next group
+        finalize();
+        if (++q >= q1) {
+          done = true;
+          return;
+        }
+        r0 = r1;
+        r1 = off[q + 1];
+      }
+    };
+    // ushort4 of codes = 2 dwords per lane; broadcast dword-wise
+    auto load = [&](int gb) -> int2 {
+      const int g = gb + c;
+      return g < g1 ? *reinterpret_cast<const int2*>(a.run_h + g * 16 + 4 * kq) : int2{0, 0};
+    };
+    auto unpack = [](int lo32, int hi32) {
+      return us4{(unsigned short)(lo32 & 0xFFFF), (unsigned short)((unsigned)lo32 >> 16),
+                 (unsigned short)(hi32 & 0xFFFF), (unsigned short)((unsigned)hi32 >> 16)};
+    };
+    auto batch = [&](const int2& v, int gb) {
+      static_for4<0, kBatch>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if (gb + d >= g1 || done) return;
+        const us4 hh[4] = {unpack(rowbc<d>(v.x), rowbc<d>(v.y)), unpack(rowbc<d + 1>(v.x), rowbc<d + 1>(v.y)),
+                           unpack(rowbc<d + 2>(v.x), rowbc<d + 2>(v.y)), unpack(rowbc<d + 3>(v.x), rowbc<d + 3>(v.y))};
+        const int gs = (gb + d) * 16;
+        if (gs >= r0 && gs + 64 < r1) {  // 4 groups inside run q, which continues after them
+          double t[4][NT];
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int I = 0; I < NT; ++I) t[s][I] = 0.0;
+#pragma unroll
+          for (int dd = 0; dd < 4; ++dd)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const uint32_t ro = (uint32_t)hh[dd][s] * (uint32_t)p;
+#pragma unroll
+              for (int I = 0; I < NT; ++I) t[s][I] += sl[ro + (uint32_t)cl[I]];
+            }
+#pragma unroll
+          for (int I = 0; I < NT; ++I) acc[I] += (t[0][I] + t[1][I]) + (t[2][I] + t[3][I]);
+          return;
+        }
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+          if (gb + d + dd >= g1 || done) return;
+          group(gb + d + dd, hh[dd]);
+        }
+      });
+    };
+    int2 va = load(g0), vb;
+    for (int gb = g0; gb < g1 && !done;) {
+      vb = load(gb + kBatch);
+      batch(va, gb);
+      gb += kBatch;
+      if (gb >= g1 || done) break;
+      va = load(gb + kBatch);
+      batch(vb, gb);
+      gb += kBatch;
+    }
+  }
+}
+
+// alpha_new = (S - T) / cnt; check = max_g |alpha_new[g][0] - alpha_cur[g][0]| over groups present
+// (= |mean_g(y~)| after the sweep); NaN propagates (a NaN panel never converges).
+__global__ void k_fin_check(const double* __restrict__ S, const double* __restrict__ T,
+                            const int32_t* __restrict__ cnt, int32_t G, int p, const double* __restrict__ cur,
+                            double* __restrict__ out, unsigned long long* __restrict__ check) {
+  double m = 0.0;
+  const int64_t total = (int64_t)G * p;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = e / p;
+    const int32_t n = cnt[g];
+    const double v = n > 0 ? (S[e] - (T ? T[e] : 0.0)) / (double)n : 0.0;
+    out[e] = v;
+    if (check && n > 0 && e % p == 0) {
+      const double d = fabs(v - cur[e]);
+      m = (isnan(d) || isnan(m)) ? __builtin_nan("") : fmax(m, d);
+    }
+  }
+  if (!check) return;
+  for (int off = 32; off > 0; off >>= 1) {
+    const double o = __shfl_down(m, off, 64);
+    m = (isnan(o) || isnan(m)) ? __builtin_nan("") : fmax(m, o);
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(check, (unsigned long long)__double_as_longlong(fabs(m)));
+}
+
+static int fin_check(lfe_ctx* c, int f, const double* T, const double* cur, double* out, bool check) {
+  auto& fe = c->fe[f];
+  ProfScope _ps(c, K_FINALIZE);
+  hipLaunchKernelGGL(k_fin_check, dim3(grid_for((int64_t)fe.G * c->p)), dim3(kBlock), 0, c->stream, fe.S, T, fe.cnt,
+                     fe.G, c->p, cur, out, check ? reinterpret_cast<unsigned long long*>(c->dred) : nullptr);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order) {
+  if (c->F != 2 || c->L.w || c->L.P < 0 || !c->L.permuted) return false;
+  if (order.back() != c->L.P) return false;
+  const int Q = 1 - c->L.P, p = c->p;
+  const int64_t G_Q = c->fe[Q].G, B = 1ll << c->L.s;
+  return (G_Q + 1) * p * 8 <= kIterLds                 // K1: alpha_Q in LDS
+         && (B + 1) * p * 8 <= 96 * 1024               // K2: primary slice in LDS
+         && ls_scatter_lds((int)G_Q, 1) <= 150 * 1024  // run layout sort
+         && B <= 65536;                                // uint16 offsets
+}
+
+template <int NT>
+static void launch_tp(lfe_ctx* c, const TpArgs& a, size_t lds) {
+  hipLaunchKernelGGL(k_tp<NT>, dim3(c->n_cu), dim3(kTpThreads), lds, c->stream, a);
+}
+template <int NT>
+static void launch_tq(lfe_ctx* c, const TqArgs& a, size_t lds) {
+  hipLaunchKernelGGL(k_tq<NT>, dim3(a.nb * kTqSplit), dim3(kTqThreads), lds, c->stream, a);
+}
+
+int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out) {
+  const int P = c->L.P, Q = 1 - P, p = c->p;
+  auto& fp = c->fe[P];
+  auto& fq = c->fe[Q];
+  const int NT = (p + 15) / 16;
+  LFE_TRY(build_layouts(c, Q));
+  LFE_TRY(ensure_f64(c, c->alpha_spare, c->alpha_spare_cap, (size_t)fq.G * p));
+  LFE_TRY(ensure_dred(c, 1));
+  const size_t lds_tp = sizeof(double) * ((size_t)fq.G + 1) * p;
+  const size_t lds_tq = sizeof(double) * (((size_t)1 << c->L.s) + 1) * p;
+  const void* ftp = NT == 1 ? reinterpret_cast<const void*>(&k_tp<1>)
+                    : NT == 2 ? reinterpret_cast<const void*>(&k_tp<2>)
+                    : NT == 3 ? reinterpret_cast<const void*>(&k_tp<3>)
+                              : reinterpret_cast<const void*>(&k_tp<4>);
+  const void* ftq = NT == 1 ? reinterpret_cast<const void*>(&k_tq<1>)
+                    : NT == 2 ? reinterpret_cast<const void*>(&k_tq<2>)
+                    : NT == 3 ? reinterpret_cast<const void*>(&k_tq<3>)
+                              : reinterpret_cast<const void*>(&k_tq<4>);
+  LFE_HIP(hipFuncSetAttribute(ftp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds_tp, 1)));
+  LFE_HIP(hipFuncSetAttribute(ftq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds_tq, 1)));
+  TpArgs tp{};
+  tp.seg_off = c->seg_off;
+  tp.seg_q = c->seg_q;
+  tp.units = c->seg_units;
+  tp.n_units = c->n_units;
+  tp.G_Q = fq.G;
+  tp.G_P = fp.G;
+  tp.p = p;
+  tp.S_P = fp.S;
+  tp.cntP = fp.cnt;
+  tp.fused = c->world == 1;
+  tp.out = tp.fused ? fp.alpha : fp.T;
+  TqArgs tq{};
+  tq.run_off = c->run_off;
+  tq.run_h = c->run_h;
+  tq.nb = c->L.nb;
+  tq.s = c->L.s;
+  tq.G_Q = fq.G;
+  tq.G_P = fp.G;
+  tq.p = p;
+  tq.alphaP = fp.alpha;
+  tq.T_Q = fq.T;
+  // sweep 1's Q projection: alpha_P = 0 -> alpha_Q = S_Q / n_Q
+  LFE_HIP(hipMemsetAsync(fp.alpha, 0, sizeof(double) * (size_t)fp.G * p, c->stream));
+  LFE_TRY(fin_check(c, Q, nullptr, nullptr, fq.alpha, false));
+  int iterations = 0;
+  double last = -1.0;
+  for (int it = 1; it <= max_iter; ++it) {
+    tp.alphaQ = fq.alpha;
+    // T_P partials: segments with no local rows are not written by K1
+    if (!tp.fused) LFE_HIP(hipMemsetAsync(fp.T, 0, sizeof(double) * (size_t)fp.G * p, c->stream));
+    {
+      ProfScope _ps(c, K_TP);
+      switch (NT) {
+        case 1: launch_tp<1>(c, tp, lds_tp); break;
+        case 2: launch_tp<2>(c, tp, lds_tp); break;
+        case 3: launch_tp<3>(c, tp, lds_tp); break;
+        default: launch_tp<4>(c, tp, lds_tp); break;
+      }
+    }
+    LFE_HIP(hipGetLastError());
+    if (!tp.fused) {
+      LFE_TRY(allreduce_sum_f64(c, fp.T, (size_t)fp.G * p));
+      LFE_TRY(fin_check(c, P, fp.T, nullptr, fp.alpha, false));
+    }
+    LFE_HIP(hipMemsetAsync(fq.T, 0, sizeof(double) * (size_t)fq.G * p, c->stream));
+    {
+      ProfScope _ps(c, K_TQ);
+      switch (NT) {
+        case 1: launch_tq<1>(c, tq, lds_tq); break;
+        case 2: launch_tq<2>(c, tq, lds_tq); break;
+        case 3: launch_tq<3>(c, tq, lds_tq); break;
+        default: launch_tq<4>(c, tq, lds_tq); break;
+      }
+    }
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(allreduce_sum_f64(c, fq.T, (size_t)fq.G * p));
+    iterations = it;
+    const bool check = it >= check_from;
+    if (!check && it == max_iter) break;
+    if (check) LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double), c->stream));
+    LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check));
+    if (check) {
+      LFE_HIP(hipMemcpyAsync(&last, c->dred, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      LFE_HIP(hipStreamSynchronize(c->stream));
+      if (last < tol) break;  // converged after sweep `it`: keep alpha_Q of this sweep
+    }
+    if (it == max_iter) break;
+    std::swap(fq.alpha, c->alpha_spare);
+  }
+  *iterations_out = iterations;
+  *last_out = last;
+  return LFE_OK;
+}
+
+}  // namespace lfe
