@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 from leanfe_amd import inference, synth  # noqa: E402
 from leanfe_amd._lib import Engine  # noqa: E402
+from leanfe_amd.dist import HostGroup  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -48,49 +49,6 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
-
-
-class Dist:
-    def __init__(self):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.init_process_group("gloo")
-            self.dist = dist
-
-    def barrier(self):
-        if self.world > 1:
-            self.dist.barrier()
-
-    def bcast_bytes(self, b: bytes | None) -> bytes:
-        if self.world == 1:
-            return b
-        obj = [b]
-        self.dist.broadcast_object_list(obj, src=0)
-        return obj[0]
-
-    def max(self, v: float) -> float:
-        if self.world == 1:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum(self, v: float) -> float:
-        if self.world == 1:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.dist.all_reduce(t)
-        return float(t.item())
-
-    def close(self):
-        if self.world > 1:
-            self.dist.destroy_process_group()
 
 
 def device_sync(eng: Engine):
@@ -157,7 +115,7 @@ def cpu_baseline(args, levels):
 def main():
     args = parse()
     levels = [int(x) for x in args.levels.split(",")]
-    d = Dist()
+    d = HostGroup()
     eng = Engine(d.local)
     if d.world > 1:
         uid = Engine.unique_id() if d.rank == 0 else None

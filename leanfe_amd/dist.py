@@ -1,0 +1,96 @@
+"""Multi-GPU plumbing: one process per GPU, rows sharded, RCCL inside the engine.
+
+The engine (``liblfe_hip.so``) owns its RCCL communicator and issues every
+collective on its own stream (include/leanfe_hip.h: ``lfe_ctx_set_comm``).
+torch.distributed is only used here to ship the RCCL unique id from rank 0 to
+the other ranks and for host-side barriers / reductions around timed regions
+(any backend; ``gloo`` is enough, no GPU tensors are involved).
+
+Data-parallel contract: each rank loads a contiguous block of
+rows; FE and cluster codes are *global* (the same level ids on every rank, e.g.
+factorized before sharding); every result (counts, fe_dims, iterations, beta,
+SE) is the global one and identical on all ranks.
+"""
+from __future__ import annotations
+
+import os
+
+
+def env_world() -> tuple[int, int, int]:
+    """(rank, world, local_rank) from the torchrun environment (1 process: 0, 1, 0)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous row block [lo, hi) of rank ``rank`` (sizes differ by at most one)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    q, r = divmod(int(n), world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def attach(engine, group=None) -> None:
+    """Join ``engine`` to an RCCL communicator spanning the ranks of ``group``.
+
+    Rank 0 creates the unique id (``lfe_comm_unique_id``), torch.distributed
+    broadcasts it, every rank calls ``lfe_ctx_set_comm(uid, rank, world)``.
+    A 1-rank group detaches (world 1: no collectives)."""
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        raise RuntimeError("torch.distributed is not initialized")
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if world == 1:
+        engine.set_comm(None, 0, 1)
+        return
+    obj = [type(engine).unique_id() if rank == 0 else None]
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast_object_list(obj, src=src, group=group)
+    engine.set_comm(obj[0], rank, world)
+
+
+class HostGroup:
+    """Host-side helpers for a timed multi-rank run (barrier, max / sum over ranks,
+    byte broadcast) on top of torch.distributed; no-ops for a single process."""
+
+    def __init__(self, backend: str = "gloo"):
+        self.rank, self.world, self.local = env_world()
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            if not dist.is_initialized():
+                dist.init_process_group(backend)
+            self.dist = dist
+
+    def barrier(self) -> None:
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def bcast_bytes(self, b: bytes | None) -> bytes | None:
+        if self.dist is None:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def _reduce(self, v: float, op) -> float:
+        import torch
+
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def max(self, v: float) -> float:
+        return v if self.dist is None else self._reduce(v, self.dist.ReduceOp.MAX)
+
+    def sum(self, v: float) -> float:
+        return v if self.dist is None else self._reduce(v, self.dist.ReduceOp.SUM)
+
+    def close(self) -> None:
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+            self.dist = None
