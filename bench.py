@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--levels", type=str, default="100000,1000")
     ap.add_argument("--vcov", type=str, default="HC1")
     ap.add_argument("--seed", type=int, default=12345)
-    ap.add_argument("--cpu-rows", type=int, default=2_000_000, help="CPU baseline sample (prefix rows)")
+    ap.add_argument("--cpu-rows", type=int, default=50_000_000, help="CPU baseline sample (prefix rows)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
@@ -94,22 +94,42 @@ def algorithmic_bytes(n: int, p: int, F: int, T: int, hc1: bool) -> dict:
     }
 
 
-def cpu_baseline(args, levels):
-    """Oracle (NumPy restatement of polars_impl.py alt_proj) on a prefix sample, 1 thread."""
-    from threadpoolctl import threadpool_limits
-    from oracle import altproj
-    n = args.cpu_rows
-    data = synth.panel(n, args.k, levels, seed=args.seed)
-    xs = [f"x{j + 1}" for j in range(args.k)]
-    fes = [f"fe{f + 1}" for f in range(len(levels))]
-    with threadpool_limits(limits=1):
-        t0 = time.perf_counter()
-        r = altproj.fit(data, "y", xs, fes, vcov=args.vcov)
-        dt = time.perf_counter() - t0
-    return dict(value=n / dt / 1e6, unit="Mrows/s", cores=1, kind="port",
-                sample=f"first {n:_} rows of the same panel (k={args.k}, levels={levels}, vcov={args.vcov}), "
-                       f"oracle/altproj.py NumPy, 1 thread, {dt:.2f} s, iterations={r['iterations']}",
-                iterations=int(r["iterations"]), seconds=dt)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+
+
+def pmc_traffic(kernel: str, args, levels) -> float | None:
+    """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters
+    (tools/pmc.sh + tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+    correction of MI355X_MICROARCH.md) for this exact configuration, else None."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    cfg = {"rows": args.rows, "k": args.k, "levels": list(levels), "vcov": args.vcov}
+    if t.get("config") != cfg or kernel not in t.get("kernels", {}):
+        return None
+    return float(t["kernels"][kernel]["bytes_per_launch"])
+
+
+def cpu_baseline(args, levels, eng: Engine) -> dict:
+    """CPU baseline: the C restatement of the reference alt_proj path (oracle/altproj_c.c,
+    OpenMP over columns) on the host cores, over the first ``--cpu-rows`` rows of the very
+    panel the GPU solved (copied back from the device)."""
+    from oracle.altproj_c import fit_c
+
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1, 16))
+    cols, codes = eng.copy_inputs()
+    n = min(args.cpu_rows, cols.shape[1])
+    t0 = time.perf_counter()
+    r = fit_c([c[:n] for c in cols], [c[:n] for c in codes], levels, vcov=args.vcov, threads=threads)
+    dt = time.perf_counter() - t0
+    whole = "the whole" if n == cols.shape[1] else f"the first {n:_} rows of the"
+    return dict(value=n / dt / 1e6, unit="Mrows/s", cores=threads, kind="port",
+                sample=f"{whole} {cols.shape[1]:_}-row panel (k={args.k}, levels={levels}, vcov={args.vcov}); "
+                       f"oracle/altproj_c.c (C restatement of polars_impl.py alt_proj), {threads} OpenMP threads, "
+                       f"{dt:.2f} s, iterations={r['iterations']}",
+                iterations=int(r["iterations"]), seconds=round(dt, 3))
 
 
 def main():
@@ -158,11 +178,14 @@ def main():
     if dom_bytes:
         achieved = dom_bytes / per_launch_s / 1e9
         roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                    "traffic": pmc_traffic(dom_name, args, levels),
                     "bytes_per_launch": dom_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4)}
+        if roofline["traffic"] is not None:
+            roofline["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) + " (rocprofv3 PMC, same config)"
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, levels)
+        cpu = cpu_baseline(args, levels, eng)
     if d.rank == 0:
         line = {
             "metric": "Mrows/sec demean+solve, 50M x 2-HDFE (1e5/1e3 levels), k=10, HC1",

@@ -97,6 +97,7 @@ class Engine:
         self.device = device
         self.p = 0
         self.F = 0
+        self.n = 0  # rows of the loaded shard
         self._keep = []  # host arrays that must outlive async copies
 
     # -- lifecycle ---------------------------------------------------------
@@ -146,7 +147,7 @@ class Engine:
         lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
         _check(self._lib.lfe_load(self._h, n, len(cols), cp, len(codes), kp, lv,
                                   None if w is None else _ptr(w), LFE_HOST))
-        self.p, self.F = len(cols), len(codes)
+        self.p, self.F, self.n = len(cols), len(codes), n
 
     def synth_load(self, n: int, k: int, levels: list[int], beta: np.ndarray, seed: int = 12345,
                    row_offset: int = 0) -> None:
@@ -156,7 +157,7 @@ class Engine:
             b = np.concatenate([b, np.zeros(max(k, 1) - b.size)])
         _check(self._lib.lfe_synth_load(self._h, int(n), int(k), len(levels), lv,
                                         b.ctypes.data_as(_dp), C.c_uint64(seed), int(row_offset)))
-        self.p, self.F = k + 1, len(levels)
+        self.p, self.F, self.n = k + 1, len(levels), int(n)
 
     def load_clusters(self, codes: list[np.ndarray], levels: list[int]) -> None:
         codes = [np.ascontiguousarray(c, dtype=np.int32) for c in codes]
@@ -206,14 +207,22 @@ class Engine:
         _check(self._lib.lfe_cluster_meat(self._h, meats.ctypes.data_as(_dp), G.ctypes.data_as(_i64p)))
         return meats[:m * k * k].reshape(m, k, k), G[:m]
 
-    def copy_demeaned(self, n: int) -> np.ndarray:
+    def _rows(self, n: int | None) -> int:
+        # the engine always copies every row of the loaded shard
+        if n is not None and int(n) != self.n:
+            raise ValueError(f"n={n} but the loaded shard has {self.n} rows")
+        return self.n
+
+    def copy_demeaned(self, n: int | None = None) -> np.ndarray:
+        n = self._rows(n)
         out = np.zeros((self.p, n))
         ptrs = (_vp * self.p)(*[out[j].ctypes.data for j in range(self.p)])
         nn = C.c_int64()
         _check(self._lib.lfe_copy_demeaned(self._h, ptrs, C.byref(nn)))
         return out
 
-    def copy_inputs(self, n: int) -> tuple[np.ndarray, np.ndarray]:
+    def copy_inputs(self, n: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+        n = self._rows(n)
         cols = np.zeros((self.p, n))
         codes = np.zeros((max(self.F, 1), n), dtype=np.int32)
         cp = (_vp * self.p)(*[cols[j].ctypes.data for j in range(self.p)])
