@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--cpu-rows", type=int, default=50_000_000, help="CPU baseline sample (prefix rows)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-prof", action="store_true", help="diagnostic: no per-kernel events (no roofline)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -151,7 +152,7 @@ def main():
 
     d.barrier()
     device_sync(eng)
-    eng.profile(True)
+    eng.profile(not args.no_prof)
     t0 = time.perf_counter()
     res = None
     for _ in range(args.steps):

@@ -59,6 +59,48 @@ static int ensure(T*& p, size_t& have, size_t want) {
 int ensure_scratch(lfe_ctx* c, size_t elems) { return ensure(c->scratch, c->scratch_elems, elems); }
 int ensure_dred(lfe_ctx* c, size_t elems) { return ensure(c->dred, c->dred_elems, elems); }
 int ensure_iscratch(lfe_ctx* c, size_t elems) { return ensure(c->iscratch, c->iscratch_elems, elems); }
+int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes) {
+  if (bytes == 0) return LFE_OK;
+  if (bytes > kPinD2H) {
+    LFE_HIP(hipMemcpyAsync(dst, src_dev, bytes, hipMemcpyDeviceToHost, c->stream));
+    LFE_HIP(hipStreamSynchronize(c->stream));
+    return LFE_OK;
+  }
+  LFE_HIP(hipMemcpyAsync(c->hpin, src_dev, bytes, hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  memcpy(dst, c->hpin, bytes);
+  return LFE_OK;
+}
+
+int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes) {
+  if (bytes == 0) return LFE_OK;
+  if (bytes > kPinSmall - kPinD2H) {
+    LFE_HIP(hipMemcpyAsync(dst_dev, src, bytes, hipMemcpyHostToDevice, c->stream));
+    LFE_HIP(hipStreamSynchronize(c->stream));
+    return LFE_OK;
+  }
+  LFE_HIP(hipEventSynchronize(c->hpin_ev));  // the previous upload from the region has been read
+  char* stage = c->hpin + kPinD2H;
+  memcpy(stage, src, bytes);
+  LFE_HIP(hipMemcpyAsync(dst_dev, stage, bytes, hipMemcpyHostToDevice, c->stream));
+  LFE_HIP(hipEventRecord(c->hpin_ev, c->stream));
+  return LFE_OK;
+}
+
+int ensure_pinned_items(lfe_ctx* c, size_t bytes) {
+  if (c->hpin_items_cap >= bytes) return LFE_OK;
+  if (c->hpin_items) {
+    LFE_HIP(hipStreamSynchronize(c->stream));  // no upload from the old buffer in flight
+    (void)hipHostFree(c->hpin_items);
+    c->hpin_items = nullptr;
+    c->hpin_items_cap = 0;
+  }
+  const size_t cap = std::max<size_t>(bytes, 1 << 20);
+  LFE_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hpin_items), cap, hipHostMallocDefault));
+  c->hpin_items_cap = cap;
+  return LFE_OK;
+}
+
 int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, dyn_lds) != hipSuccess || per_cu < 1)
@@ -289,6 +331,8 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
   if (c->n_cu <= 0) c->n_cu = 256;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreateWithFlags(&c->hpin_ev, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->hpin), kPinSmall, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess) {
     delete c;
     return fail(LFE_EHIP, "stream/event/buffer creation failed");
@@ -317,6 +361,9 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   dfree(c->run_h);
   dfree(c->alpha_spare);
   dfree(c->dbeta);
+  if (c->hpin) (void)hipHostFree(c->hpin);
+  if (c->hpin_items) (void)hipHostFree(c->hpin_items);
+  if (c->hpin_ev) (void)hipEventDestroy(c->hpin_ev);
   dfree(c->clS);
   dfree(c->clP);
   if (c->comm) ncclCommDestroy(c->comm);

@@ -534,8 +534,7 @@ static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
   }
   LFE_HIP(hipGetLastError());
   LFE_TRY(allreduce_sum_f64(c, c->dred, len));
-  LFE_HIP(hipMemcpyAsync(host_out, c->dred, sizeof(double) * len, hipMemcpyDeviceToHost, c->stream));
-  LFE_HIP(hipStreamSynchronize(c->stream));
+  LFE_TRY(d2h_sync(c, host_out, c->dred, sizeof(double) * len));
   return LFE_OK;
 }
 
@@ -601,7 +600,7 @@ int launch_gram(lfe_ctx* c, double* host_gram) {
 
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores) {
   GramArgs a = base_args(c);
-  LFE_HIP(hipMemcpyAsync(c->dbeta, beta_full, sizeof(double) * c->p, hipMemcpyHostToDevice, c->stream));
+  LFE_TRY(h2d_small(c, c->dbeta, beta_full, sizeof(double) * c->p));
   a.beta = c->dbeta;
   a.scores = keep_scores ? c->scores : nullptr;
   const int k = c->p - 1;
@@ -638,8 +637,7 @@ int launch_cluster(lfe_ctx* c, double* meats, int64_t* G_out) {
     hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(C)), dim3(kBlock), 0, c->stream, present, C, cntG);
     LFE_HIP(hipGetLastError());
     int32_t hG = 0;
-    LFE_HIP(hipMemcpyAsync(&hG, cntG, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    LFE_HIP(hipStreamSynchronize(c->stream));
+    LFE_TRY(d2h_sync(c, &hG, cntG, sizeof(int32_t)));
     G_out[j] = hG;
     if (k > 0) {
       GramArgs a{};

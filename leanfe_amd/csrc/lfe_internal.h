@@ -22,6 +22,8 @@ constexpr int kMaxGroupCols = 16;    // columns per column group in a sweep
 constexpr int kLdsBudget = 64 * 1024;  // bytes of LDS tables per sweep workgroup (2 WG per CU)
 constexpr int kItemRows = 8192;      // rows per work item (a bucket is split into items)
 constexpr int kLdsHistMax = 16384;   // int32 counters in an LDS histogram
+constexpr size_t kPinD2H = 128 * 1024;   // pinned staging: device -> host results
+constexpr size_t kPinSmall = 192 * 1024; // pinned staging total (D2H + small H2D)
 
 void set_error(const std::string& msg);
 
@@ -141,6 +143,11 @@ struct lfe_ctx {
   // clusters (input row order)
   std::vector<int32_t*> cl;
   std::vector<int32_t> cl_levels;
+  // pinned host staging (small transfers avoid the runtime's pageable path)
+  char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
+  hipEvent_t hpin_ev = nullptr;    // last H2D from the staging region
+  char* hpin_items = nullptr;      // work-item upload staging
+  size_t hpin_items_cap = 0;
   double* scores = nullptr;  // [k][ld] x~ r (w), layout order
   double* dbeta = nullptr;   // [64] beta_full staging
   bool scores_valid = false;
@@ -206,6 +213,12 @@ int ensure_i32(lfe_ctx* c, int32_t*& p, size_t& cap, size_t elems);
 int ensure_f64(lfe_ctx* c, double*& p, size_t& cap, size_t elems);
 int ensure_u16(lfe_ctx* c, uint16_t*& p, size_t& cap, size_t elems);
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
+// device -> host copy of a small result through pinned staging, synchronizing the stream
+int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes);
+// host -> device copy of a small argument through pinned staging (asynchronous)
+int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes);
+// pinned upload buffer of at least `bytes` (work items)
+int ensure_pinned_items(lfe_ctx* c, size_t bytes);
 // blocks of `fn` that fit on the whole device at once (occupancy API x CUs)
 int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds);
 int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems);

@@ -732,8 +732,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     if (check) LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double), c->stream));
     LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check));
     if (check) {
-      LFE_HIP(hipMemcpyAsync(&last, c->dred, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      LFE_HIP(hipStreamSynchronize(c->stream));
+      LFE_TRY(d2h_sync(c, &last, c->dred, sizeof(double)));
       if (last < tol) break;  // converged after sweep `it`: keep alpha_Q of this sweep
     }
     if (it == max_iter) break;

@@ -15,6 +15,7 @@
 #include "lfe_internal.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace lfe {
 
@@ -386,12 +387,15 @@ static int build_items(lfe_ctx* c) {
   if (L.hitems.empty()) L.hitems.insert(L.hitems.end(), {0, 0, 0, 0});
   L.n_items = (int)(L.hitems.size() / 4);
   LFE_TRY(ensure_items(c, L.n_items));
-  LFE_HIP(hipMemcpyAsync(c->items_d, L.hitems.data(), sizeof(int32_t) * L.hitems.size(), hipMemcpyHostToDevice,
-                         c->stream));
   LFE_TRY(ensure_i32(c, c->bitems_d, c->bitems_cap, bfirst.size()));
-  LFE_HIP(hipMemcpyAsync(c->bitems_d, bfirst.data(), sizeof(int32_t) * bfirst.size(), hipMemcpyHostToDevice,
-                         c->stream));
-  LFE_HIP(hipStreamSynchronize(c->stream));  // host vectors are pageable and local
+  // upload through pinned staging, asynchronously (the staging buffer is next written
+  // only after later stream synchronizations)
+  const size_t ib = sizeof(int32_t) * L.hitems.size(), bb = sizeof(int32_t) * bfirst.size();
+  LFE_TRY(ensure_pinned_items(c, ib + bb));
+  memcpy(c->hpin_items, L.hitems.data(), ib);
+  memcpy(c->hpin_items + ib, bfirst.data(), bb);
+  LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib, hipMemcpyHostToDevice, c->stream));
+  LFE_HIP(hipMemcpyAsync(c->bitems_d, c->hpin_items + ib, bb, hipMemcpyHostToDevice, c->stream));
   return LFE_OK;
 }
 
@@ -477,8 +481,7 @@ int prepare_layout(lfe_ctx* c) {
     hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(nb)), dim3(kBlock), 0, c->stream, c->pcounts, nb, nw, dbstart);
     LFE_HIP(hipGetLastError());
     L.bstart.assign(nb + 1, 0);
-    LFE_HIP(hipMemcpyAsync(L.bstart.data(), dbstart, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->stream));
-    LFE_HIP(hipStreamSynchronize(c->stream));
+    LFE_TRY(d2h_sync(c, L.bstart.data(), dbstart, sizeof(int32_t) * nb));
     L.bstart[nb] = (int32_t)n;
     L.X = c->Xp;
     L.w = c->w ? c->wp : nullptr;
@@ -537,8 +540,7 @@ int prepare_layout(lfe_ctx* c) {
     }
   }
   int32_t h[2 * kMaxFE + 8];
-  LFE_HIP(hipMemcpyAsync(h, c->iscratch, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-  LFE_HIP(hipStreamSynchronize(c->stream));
+  LFE_TRY(d2h_sync(c, h, c->iscratch, sizeof(h)));
   for (int f = 0; f < c->F; ++f) {
     c->fe[f].dims = h[2 * f];
     c->fe[f].card = h[2 * f + 1];
@@ -547,10 +549,9 @@ int prepare_layout(lfe_ctx* c) {
   double kept = (double)(n - h[2 * kMaxFE]);
   if (c->world > 1) {
     LFE_TRY(ensure_dred(c, 1));
-    LFE_HIP(hipMemcpyAsync(c->dred, &kept, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    LFE_TRY(h2d_small(c, c->dred, &kept, sizeof(double)));
     LFE_TRY(allreduce_sum_f64(c, c->dred, 1));
-    LFE_HIP(hipMemcpyAsync(&kept, c->dred, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    LFE_HIP(hipStreamSynchronize(c->stream));
+    LFE_TRY(d2h_sync(c, &kept, c->dred, sizeof(double)));
   }
   c->n_kept = (int64_t)kept;
   return LFE_OK;

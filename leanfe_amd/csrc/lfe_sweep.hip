@@ -370,8 +370,7 @@ int sweep_check(lfe_ctx* c, double* host_max) {
                        reinterpret_cast<unsigned long long*>(c->dred));
   }
   LFE_HIP(hipGetLastError());
-  LFE_HIP(hipMemcpyAsync(host_max, c->dred, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  LFE_HIP(hipStreamSynchronize(c->stream));
+  LFE_TRY(d2h_sync(c, host_max, c->dred, sizeof(double)));
   return LFE_OK;
 }
 
