@@ -388,6 +388,246 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
   }
 }
 
+// Residual pass, row per lane (two FEs, unweighted, p <= PM <= 16).  The lane
+// layout above needs a 16-lane DPP reduction for every row's residual (~6 VALU
+// per row); here each lane owns whole rows: it loads the row's p columns
+// (coalesced across the wave), gathers the two alpha rows from LDS (tables padded
+// to PM doubles per row so a row is PM/2 16-byte reads), forms the residual with
+// a lane-local dot product and accumulates the HC1 meat (upper triangle, VALU
+// f64 FMAs) and the residual statistics.  Output: the same [16][16] tile + 4
+// statistics per block as k_gram<RESID>.
+constexpr int kResThreads = 512;
+
+template <int PM, int UR>
+__global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* __restrict__ partial, int64_t pstride) {
+  constexpr int KM = PM - 1;              // regressor columns held
+  constexpr int NM = KM * (KM + 1) / 2;   // meat upper triangle
+  constexpr int NW = kResThreads / 64;
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* slice = lds;                    // [B][PM] alpha_P slice of the current bucket
+  double* aqL = lds + a.B * PM;           // [G_Q][PM] alpha_Q
+  __shared__ double red[NW][NM + 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p = a.la.p, P = a.la.P;
+  const int Q = a.qf[0];
+  const double* aQg = a.la.alpha[Q];
+  for (int j = tid; j < a.G_Q * PM; j += kResThreads) {
+    const int g = j / PM, cc = j % PM;
+    aqL[j] = cc < p ? aQg[(int64_t)g * p + cc] : 0.0;
+  }
+  double beta[PM];
+#pragma unroll
+  for (int cc = 0; cc < PM; ++cc) beta[cc] = cc < p ? a.beta[cc] : 0.0;
+  double m[NM];
+#pragma unroll
+  for (int e = 0; e < NM; ++e) m[e] = 0.0;
+  double st[4] = {0.0, 0.0, 0.0, 0.0};  // sum r^2 (w = 1), sum r^2, sum y~, sum y~^2
+  const int32_t* codeP = a.la.code[P];
+  const int32_t* codeQ = a.la.code[Q];
+  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
+  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  int staged = -1;
+  for (int item = i0; item < i1; ++item) {
+    const int4 it = a.la.items[item];
+    const int lo = it.x << a.la.s;
+    if (it.x != staged) {
+      __syncthreads();
+      for (int j = tid; j < a.B * PM; j += kResThreads) {
+        const int g = lo + j / PM, cc = j % PM;
+        slice[j] = (g < a.G_P && cc < p) ? a.la.alpha[P][(int64_t)g * p + cc] : 0.0;
+      }
+      __syncthreads();
+      staged = it.x;
+    }
+    for (int rb = it.y + wave * 64 * UR; rb < it.z; rb += NW * 64 * UR) {
+      int hq[UR], qq[UR];
+      double x[UR][PM];
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        const int r = rb + u * 64 + lane;
+        const bool in = r < it.z;
+        hq[u] = in ? codeP[r] : -1;
+        qq[u] = in ? codeQ[r] : 0;
+#pragma unroll
+        for (int cc = 0; cc < PM; ++cc) x[u][cc] = (in && cc < p) ? a.X[(int64_t)cc * a.ld + r] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        const bool valid = hq[u] >= 0;
+        const d2* sp = reinterpret_cast<const d2*>(slice + (valid ? hq[u] - lo : 0) * PM);
+        const d2* qp = reinterpret_cast<const d2*>(aqL + qq[u] * PM);
+        double xt[PM];
+#pragma unroll
+        for (int c2 = 0; c2 < PM / 2; ++c2) {
+          const d2 s2 = sp[c2], q2 = qp[c2];
+          xt[2 * c2] = x[u][2 * c2] - s2.x - q2.x;
+          xt[2 * c2 + 1] = x[u][2 * c2 + 1] - s2.y - q2.y;
+        }
+        // r = y~ - beta0 - sum_j beta_j x~_j (polars_impl.py:229)
+        double res = xt[0] - beta[0];
+#pragma unroll
+        for (int cc = 1; cc < PM; ++cc) res -= beta[cc] * xt[cc];
+        if (!valid) continue;
+        const double rr = res * res;
+        st[0] += rr;
+        st[1] += rr;
+        st[2] += xt[0];
+        st[3] += xt[0] * xt[0];
+        double wv[KM];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) wv[j] = xt[j + 1] * res;
+        int e = 0;
+#pragma unroll
+        for (int i = 0; i < KM; ++i)
+#pragma unroll
+          for (int j = i; j < KM; ++j, ++e) m[e] += wv[i] * wv[j];
+        if (a.scores) {
+          const int r = rb + u * 64 + lane;
+#pragma unroll
+          for (int j = 0; j < KM; ++j)
+            if (j + 1 < p) a.scores[(int64_t)j * a.ld + r] = wv[j];
+        }
+      }
+    }
+  }
+  // block reduction: wave sums (xor shuffles), then the NW wave rows in LDS
+#pragma unroll
+  for (int e = 0; e < NM; ++e) {
+    double v = m[e];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[wave][e] = v;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    double v = st[e];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[wave][NM + e] = v;
+  }
+  __syncthreads();
+  double* out = partial + (int64_t)blockIdx.x * pstride;
+  for (int t = tid; t < 256 + 4; t += kResThreads) {
+    double v = 0.0;
+    if (t < 256) {
+      const int i = t / 16 - 1, j = t % 16 - 1;  // tile (1 + i, 1 + j) = meat (i, j)
+      if (i >= 0 && j >= 0 && i < KM && j < KM) {
+        const int lo2 = i < j ? i : j, hi2 = i < j ? j : i;
+        const int e = lo2 * KM - lo2 * (lo2 - 1) / 2 + (hi2 - lo2);
+        for (int w = 0; w < NW; ++w) v += red[w][e];
+      }
+    } else {
+      for (int w = 0; w < NW; ++w) v += red[w][NM + (t - 256)];
+    }
+    out[t] = v;
+  }
+}
+
+// Design Gram, row per lane (same conditions as k_resid_rows).  Accumulates, for
+// the data columns d = [y~, x~_1..x~_k] (PM >= p slots), the row count, the column
+// sums (intercept row of [1, d]'[1, d]) and the upper triangle of d'd, on VALU f64
+// FMAs; output in the [16][16] tile order of k_gram<DESIGN> (column 0 = intercept).
+template <int PM, int UR>
+__global__ __launch_bounds__(kResThreads) void k_design_rows(GramArgs a, double* __restrict__ partial,
+                                                             int64_t pstride) {
+  constexpr int PS = (PM + 1) & ~1;      // LDS row stride (even: 16-byte pair reads)
+  constexpr int NG = PM * (PM + 1) / 2;  // upper triangle of d'd
+  constexpr int NA = NG + PM + 1;        // + column sums + count
+  constexpr int NW = kResThreads / 64;
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* slice = lds;           // [B][PS]
+  double* aqL = lds + a.B * PS;  // [G_Q][PS]
+  __shared__ double red[NW][NA];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p = a.la.p, P = a.la.P;
+  const int Q = a.qf[0];
+  const double* aQg = a.la.alpha[Q];
+  for (int j = tid; j < a.G_Q * PS; j += kResThreads) {
+    const int g = j / PS, cc = j % PS;
+    aqL[j] = cc < p ? aQg[(int64_t)g * p + cc] : 0.0;
+  }
+  double acc[NA];
+#pragma unroll
+  for (int e = 0; e < NA; ++e) acc[e] = 0.0;
+  const int32_t* codeP = a.la.code[P];
+  const int32_t* codeQ = a.la.code[Q];
+  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
+  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  int staged = -1;
+  for (int item = i0; item < i1; ++item) {
+    const int4 it = a.la.items[item];
+    const int lo = it.x << a.la.s;
+    if (it.x != staged) {
+      __syncthreads();
+      for (int j = tid; j < a.B * PS; j += kResThreads) {
+        const int g = lo + j / PS, cc = j % PS;
+        slice[j] = (g < a.G_P && cc < p) ? a.la.alpha[P][(int64_t)g * p + cc] : 0.0;
+      }
+      __syncthreads();
+      staged = it.x;
+    }
+    for (int rb = it.y + wave * 64 * UR; rb < it.z; rb += NW * 64 * UR) {
+      int hq[UR], qq[UR];
+      double x[UR][PS];
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        const int r = rb + u * 64 + lane;
+        const bool in = r < it.z;
+        hq[u] = in ? codeP[r] : -1;
+        qq[u] = in ? codeQ[r] : 0;
+#pragma unroll
+        for (int cc = 0; cc < PS; ++cc) x[u][cc] = (in && cc < p) ? a.X[(int64_t)cc * a.ld + r] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        if (hq[u] < 0) continue;
+        const d2* sp = reinterpret_cast<const d2*>(slice + (hq[u] - lo) * PS);
+        const d2* qp = reinterpret_cast<const d2*>(aqL + qq[u] * PS);
+        double d[PS];
+#pragma unroll
+        for (int c2 = 0; c2 < PS / 2; ++c2) {
+          const d2 s2 = sp[c2], q2 = qp[c2];
+          d[2 * c2] = x[u][2 * c2] - s2.x - q2.x;
+          d[2 * c2 + 1] = x[u][2 * c2 + 1] - s2.y - q2.y;
+        }
+        int e = 0;
+#pragma unroll
+        for (int i = 0; i < PM; ++i)
+#pragma unroll
+          for (int j = i; j < PM; ++j, ++e) acc[e] += d[i] * d[j];
+#pragma unroll
+        for (int i = 0; i < PM; ++i) acc[NG + i] += d[i];
+        acc[NG + PM] += 1.0;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < NA; ++e) {
+    double v = acc[e];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[wave][e] = v;
+  }
+  __syncthreads();
+  double* out = partial + (int64_t)blockIdx.x * pstride;
+  for (int t = tid; t < 256; t += kResThreads) {
+    const int i = t / 16, j = t % 16;  // design column 0 = intercept, 1 + c = data column c
+    int e = -1;
+    if (i == 0 && j == 0) e = NG + PM;
+    else if (i == 0 && j - 1 < PM) e = NG + (j - 1);
+    else if (j == 0 && i - 1 < PM) e = NG + (i - 1);
+    else if (i >= 1 && j >= 1 && i - 1 < PM && j - 1 < PM) {
+      const int lo2 = (i < j ? i : j) - 1, hi2 = (i < j ? j : i) - 1;
+      e = lo2 * PM - lo2 * (lo2 - 1) / 2 + (hi2 - lo2);
+    }
+    double v = 0.0;
+    if (e >= 0)
+      for (int w = 0; w < NW; ++w) v += red[w][e];
+    out[t] = v;
+  }
+}
+
 // fixed-order tree sum of per-block partials: one workgroup per output entry
 __global__ __launch_bounds__(256) void k_reduce_partials(const double* __restrict__ partial, int nblocks,
                                                          int64_t pstride, double* __restrict__ out) {
@@ -593,10 +833,100 @@ static GramArgs base_args(lfe_ctx* c) {
   return a;
 }
 
+static bool resid_rows_ok(const lfe_ctx* c, const GramArgs& a) {
+  static const int off = [] {
+    const char* e = getenv("LFE_RESID_LANES");  // tuning: 1 = lane-layout kernel
+    return e ? atoi(e) : 0;
+  }();
+  if (off == 1) return false;
+  // p <= 12: the meat's upper triangle stays in registers (p = 16 would spill)
+  const int PM = c->p <= 4 ? 4 : c->p <= 8 ? 8 : 12;
+  return c->F == 2 && c->p <= 12 && c->p >= 2 && !a.w && a.la.P >= 0 && c->L.permuted &&
+         ((size_t)a.B + c->fe[1 - a.la.P].G) * PM * 8 <= 150 * 1024;
+}
+
 int launch_gram(lfe_ctx* c, double* host_gram) {
   GramArgs a = base_args(c);
+  static const int lanes = [] {
+    const char* e = getenv("LFE_DESIGN_LANES");  // tuning: 1 = lane-layout MFMA kernel
+    return e ? atoi(e) : 0;
+  }();
+  if (lanes != 1 && resid_rows_ok(c, a) && c->p <= 11) {
+    // row-per-lane design Gram: [16][16] tile, column 0 = intercept, 1 + c = data column c
+    a.nq = 1;
+    a.qf[0] = 1 - a.la.P;
+    a.G_Q = c->fe[a.qf[0]].G;
+    const int p = c->p;
+    const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 11;
+    const size_t dyn = sizeof(double) * ((size_t)a.B + a.G_Q) * ((PM + 1) & ~1);
+    const void* fn = PM == 4   ? reinterpret_cast<const void*>(&k_design_rows<4, 2>)
+                     : PM == 8 ? reinterpret_cast<const void*>(&k_design_rows<8, 2>)
+                               : reinterpret_cast<const void*>(&k_design_rows<11, 1>);
+    if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+    const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kResThreads, dyn)));
+    const int64_t pstride = 256 + 4;
+    LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
+    LFE_TRY(ensure_dred(c, (size_t)pstride));
+    {
+      ProfScope _ps(c, K_GRAM_DESIGN);
+      double* part = c->scratch;
+      void* args[] = {&a, &part, const_cast<int64_t*>(&pstride)};
+      LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(kResThreads), args, dyn, c->stream));
+    }
+    LFE_HIP(hipGetLastError());
+    {
+      ProfScope _ps(c, K_REDUCE);
+      hipLaunchKernelGGL(k_reduce_partials, dim3(256), dim3(256), 0, c->stream, c->scratch, nblocks, pstride,
+                         c->dred);
+    }
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(allreduce_sum_f64(c, c->dred, 256));
+    std::vector<double> h(256);
+    LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 256));
+    const int D = p + 1;
+    for (int i = 0; i < D; ++i)
+      for (int j = 0; j < D; ++j) host_gram[i * D + j] = h[(size_t)i * 16 + j];
+    return LFE_OK;
+  }
   return gram_dispatch<GRAM_DESIGN>(c, a, c->p + 1, 0, c->p + 1, host_gram, nullptr, 0);
 }
+
+// row-per-lane residual pass (k_resid_rows): two FEs, unweighted, p <= 16, both
+// alpha tables (padded to PM doubles per row) in LDS
+static int resid_rows(lfe_ctx* c, GramArgs a, double* meat, double* stats) {
+  const int p = c->p, k = p - 1;
+  const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
+  const size_t dyn = sizeof(double) * ((size_t)a.B + a.G_Q) * PM;
+  const void* fn = PM == 4   ? reinterpret_cast<const void*>(&k_resid_rows<4, 2>)
+                   : PM == 8 ? reinterpret_cast<const void*>(&k_resid_rows<8, 2>)
+                             : reinterpret_cast<const void*>(&k_resid_rows<12, 2>);
+  if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kResThreads, dyn)));
+  const int64_t pstride = 256 + 4;
+  LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
+  LFE_TRY(ensure_dred(c, (size_t)pstride));
+  {
+    ProfScope _ps(c, K_GRAM_RESID);
+    double* part = c->scratch;
+    void* args[] = {&a, &part, const_cast<int64_t*>(&pstride)};
+    LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(kResThreads), args, dyn, c->stream));
+  }
+  LFE_HIP(hipGetLastError());
+  {
+    ProfScope _ps(c, K_REDUCE);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(pstride), dim3(256), 0, c->stream, c->scratch, nblocks, pstride,
+                       c->dred);
+  }
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(allreduce_sum_f64(c, c->dred, (size_t)pstride));
+  std::vector<double> h((size_t)pstride);
+  LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * pstride));
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) meat[i * k + j] = h[(size_t)(1 + i) * 16 + (1 + j)];
+  for (int e = 0; e < 4; ++e) stats[e] = h[256 + e];
+  return LFE_OK;
+}
+
 
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores) {
   GramArgs a = base_args(c);
@@ -605,6 +935,16 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
   a.scores = keep_scores ? c->scores : nullptr;
   const int k = c->p - 1;
   std::vector<double> meat((size_t)std::max(k, 1) * std::max(k, 1));
+  if (resid_rows_ok(c, a)) {
+    a.nq = 1;
+    a.qf[0] = 1 - a.la.P;
+    a.G_Q = c->fe[a.qf[0]].G;
+    LFE_TRY(resid_rows(c, a, meat.data(), stats));
+    if (hc1)
+      for (int e = 0; e < k * k; ++e) hc1[e] = meat[e];
+    c->scores_valid = keep_scores != 0;
+    return LFE_OK;
+  }
   // staged columns 0..p-1 (col 0 = y, zeroed in the meat); meat = columns 1..p-1
   const int rc = gram_dispatch<GRAM_RESID>(c, a, c->p, 1, k, meat.data(), stats, 4);
   if (rc) return rc;
