@@ -38,8 +38,8 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10, help="untimed steps (GPU clocks settle within ~0.1 s)")
     ap.add_argument("--rows", type=int, default=50_000_000, help="rows per GPU")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--levels", type=str, default="100000,1000")

@@ -43,21 +43,28 @@ namespace lfe {
 // deterministic (per-wave cursors ranked by LDS atomics in lane order, as in
 // the partition scatter of lfe_prep.hip).
 
-template <bool KEYQ>
-__global__ __launch_bounds__(256) void k_ls_hist(const int4* __restrict__ items, const int32_t* __restrict__ codeP,
-                                                 const int32_t* __restrict__ codeQ, int s, int K,
-                                                 int32_t* __restrict__ itemcnt) {
+// both layouts' per-item histograms in one pass over the codes: itemcnt1[item][h - lo]
+// (K1 = 2^s keys) and itemcnt2[item][q] (K2 = G_Q keys)
+__global__ __launch_bounds__(256) void k_ls_hist2(const int4* __restrict__ items, const int32_t* __restrict__ codeP,
+                                                  const int32_t* __restrict__ codeQ, int s, int K1, int K2,
+                                                  int32_t* __restrict__ cnt1, int32_t* __restrict__ cnt2) {
   extern __shared__ int32_t h[];
+  int32_t* h1 = h;
+  int32_t* h2 = h + K1;
   const int4 it = items[blockIdx.x];
   const int lo = it.x << s;
-  for (int j = threadIdx.x; j < K; j += blockDim.x) h[j] = 0;
+  for (int j = threadIdx.x; j < K1 + K2; j += blockDim.x) h[j] = 0;
   __syncthreads();
   for (int32_t i = it.y + threadIdx.x; i < it.z; i += blockDim.x) {
     const int32_t g = codeP[i];
-    if (g >= 0) atomicAdd(&h[KEYQ ? codeQ[i] : g - lo], 1);
+    if (g >= 0) {
+      atomicAdd(&h1[g - lo], 1);
+      atomicAdd(&h2[codeQ[i]], 1);
+    }
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < K; j += blockDim.x) itemcnt[(int64_t)blockIdx.x * K + j] = h[j];
+  for (int j = threadIdx.x; j < K1; j += blockDim.x) cnt1[(int64_t)blockIdx.x * K1 + j] = h1[j];
+  for (int j = threadIdx.x; j < K2; j += blockDim.x) cnt2[(int64_t)blockIdx.x * K2 + j] = h2[j];
 }
 
 // per (bucket, key): exclusive scan over the bucket's items -> item bases; total -> off[b K + key]
@@ -78,7 +85,7 @@ __global__ void k_ls_base(const int32_t* __restrict__ bitems, int nb, int K, int
 
 constexpr int kLsThreads = 512;
 constexpr int kLsWaves = kLsThreads / 64;
-constexpr int kLsPer = 8;
+constexpr int kLsPer = 16;
 constexpr int kLsRows = kLsThreads * kLsPer;
 
 static size_t ls_scatter_lds(int K, int ncur) {
@@ -92,6 +99,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
                                                            const int32_t* __restrict__ codeQ, int s, int K,
                                                            const int32_t* __restrict__ off,
                                                            const int32_t* __restrict__ itembase,
+                                                           const int32_t* __restrict__ xitems,
                                                            VT* __restrict__ out) {
   extern __shared__ int32_t sm[];
   int32_t* cur = sm;              // [NCUR][K]
@@ -102,10 +110,12 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
   int32_t* sb = stage + kLsRows;      // [kLsRows]
   __shared__ int32_t wsum[kLsWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int4 it = items[blockIdx.x];
+  const int item = xitems[blockIdx.x];  // XCD-grouped order (build_items)
+  if (item < 0) return;
+  const int4 it = items[item];
   const int lo = it.x << s;
   for (int j = tid; j < K; j += kLsThreads)
-    run[j] = off[(int64_t)it.x * K + j] + itembase[(int64_t)blockIdx.x * K + j];
+    run[j] = off[(int64_t)it.x * K + j] + itembase[(int64_t)item * K + j];
   for (int32_t r0 = it.y; r0 < it.z; r0 += kLsRows) {
     const int32_t r1 = min(it.z, r0 + kLsRows);
     const int32_t wbase = r0 + wave * kLsPer * 64;
@@ -203,40 +213,35 @@ __global__ void k_unit_bounds(const int32_t* __restrict__ seg_off, int32_t H, in
   }
 }
 
-// bucket-local counting sort of the kept rows; off = [nb K + 1] exclusive offsets
+// bucket-local counting sort of the kept rows given the per-item histograms
+// itemcnt [n_items][K] (k_ls_hist2); off = [nb K + 1] exclusive offsets.  Both
+// layouts rank rows with one shared LDS cursor set (unstable inside a segment or
+// run): the order there only sets the summation order of K1 / K2, and the sweeps
+// are not bit-reproducible anyway (K2's cross-workgroup atomics into T_Q); the
+// stable per-wave ranking costs O(K x waves) LDS work per sub-chunk.
 template <bool KEYQ, typename VT>
-static int local_sort(lfe_ctx* c, int Q, int K, int32_t*& off, size_t& off_cap, VT* out) {
+static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off, size_t& off_cap, VT* out) {
   auto& L = c->L;
   const int P = L.P;
   const size_t m = (size_t)L.nb * K;
-  LFE_TRY(ensure_i32(c, c->seg_aux, c->seg_aux_cap, (size_t)L.n_items * K));
   LFE_TRY(ensure_i32(c, off, off_cap, m + 1));
   const int4* items = reinterpret_cast<const int4*>(c->items_d);
   LFE_HIP(hipMemsetAsync(off, 0, sizeof(int32_t) * (m + 1), c->stream));
   {
     ProfScope _ps(c, K_MISC);
-    hipLaunchKernelGGL(k_ls_hist<KEYQ>, dim3(L.n_items), dim3(256), sizeof(int32_t) * K, c->stream, items,
-                       L.code[P], L.code[Q], L.s, K, c->seg_aux);
-  }
-  {
-    ProfScope _ps(c, K_MISC);
     hipLaunchKernelGGL(k_ls_base, dim3(grid_for((int64_t)m)), dim3(kBlock), 0, c->stream, c->bitems_d, L.nb, K,
-                       c->seg_aux, off);
+                       itemcnt, off);
   }
   LFE_HIP(hipGetLastError());
   LFE_TRY(exclusive_scan(c, off, (int64_t)m + 1));
-  // the run layout ranks with one shared cursor set (unstable inside a run: that
-  // order only sets K2's summation order, which the cross-workgroup atomics into
-  // T_Q leave unordered anyway); per-wave cursors cost O(K x waves) LDS work per
-  // sub-chunk, 3x the whole kernel at K = 1000
-  constexpr int NCUR = KEYQ ? 1 : kLsWaves;
+  constexpr int NCUR = 1;
   const size_t lds = ls_scatter_lds(K, NCUR);
   const void* fn = reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, NCUR>);
   if (lds > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   {
     ProfScope _ps(c, K_MISC);
-    hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR>), dim3(L.n_items), dim3(kLsThreads), lds, c->stream, items,
-                       L.code[P], L.code[Q], L.s, K, off, c->seg_aux, out);
+    hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream, items,
+                       L.code[P], L.code[Q], L.s, K, off, itemcnt, c->xitems_d, out);
   }
   LFE_HIP(hipGetLastError());
   return LFE_OK;
@@ -246,10 +251,21 @@ static int build_layouts(lfe_ctx* c, int Q) {
   auto& L = c->L;
   const int B = 1 << L.s;
   const int32_t G_Q = c->fe[Q].G;
+  const int P = L.P;
+  // per-item histograms of both keys in one pass (seg_aux = [n_items][B] ++ [n_items][G_Q])
+  const size_t n1 = (size_t)L.n_items * B;
+  LFE_TRY(ensure_i32(c, c->seg_aux, c->seg_aux_cap, n1 + (size_t)L.n_items * G_Q));
+  {
+    ProfScope _ps(c, K_MISC);
+    hipLaunchKernelGGL(k_ls_hist2, dim3(L.n_items), dim3(256), sizeof(int32_t) * ((size_t)B + G_Q), c->stream,
+                       reinterpret_cast<const int4*>(c->items_d), L.code[P], L.code[Q], L.s, B, (int)G_Q,
+                       c->seg_aux, c->seg_aux + n1);
+  }
+  LFE_HIP(hipGetLastError());
   LFE_TRY(ensure_i32(c, c->seg_q, c->seg_q_cap, (size_t)c->ld));
-  LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_off, c->seg_off_cap, c->seg_q)));
+  LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, c->seg_q)));
   LFE_TRY(ensure_u16(c, c->run_h, c->run_h_cap, (size_t)c->ld));
-  LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->run_off, c->run_off_cap, c->run_h)));
+  LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, c->run_h)));
   // work units of ~2048 kept rows (whole segments) for K1
   const int64_t U = 2048;
   const int32_t H = L.nb * B;
@@ -637,6 +653,7 @@ bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order) {
   return (G_Q + 1) * p * 8 <= kIterLds                 // K1: alpha_Q in LDS
          && (B + 1) * p * 8 <= 96 * 1024               // K2: primary slice in LDS
          && ls_scatter_lds((int)G_Q, 1) <= 150 * 1024  // run layout sort
+         && (B + G_Q) * 4 <= 64 * 1024                 // both histograms in LDS
          && B <= 65536;                                // uint16 offsets
 }
 

@@ -15,6 +15,7 @@
 #include "lfe_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace lfe {
@@ -165,7 +166,15 @@ struct ScatterArgs {
   int32_t* codeo[kMaxFE];
   int32_t* orig;
   const int32_t* scanned;  // [nb][nchunks] exclusive destinations
+  int xcd_map;             // 1: XCD-contiguous chunk order
 };
+
+// block i -> chunk: XCD x = i % 8 walks its contiguous eighth of the chunks
+__device__ __forceinline__ int xcd_chunk(int i, int nw) {
+  const int x = i & 7, r = i >> 3;
+  const int per = (nw + 7) >> 3;          // chunks per XCD (the last XCD may have fewer)
+  return x * per + r;                      // may be >= nw: the caller's r0 >= n then
+}
 
 template <int PER>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
@@ -178,8 +187,12 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
   int32_t* tot = delta + a.nb;                                 // [nb + 1]
   __shared__ int32_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int chunk = blockIdx.x;
+  // XCD-contiguous chunks: workgroups go round-robin to the 8 XCDs (block i on XCD
+  // i % 8); XCD x takes chunks [x nw / 8, (x + 1) nw / 8) in order, so the adjacent
+  // runs that consecutive chunks write into every bucket region meet in one L2
+  const int chunk = a.xcd_map ? xcd_chunk(blockIdx.x, a.nchunks) : (int)blockIdx.x;
   const int64_t r0 = (int64_t)chunk * R, r1 = min(a.n, r0 + R);
+  if (chunk >= a.nchunks) return;
   const int64_t wbase = r0 + (int64_t)wave * PER * 64;
   for (int j = tid; j < kPartWaves * a.nb; j += kPartThreads) cur[j] = 0;
   __syncthreads();
@@ -386,16 +399,39 @@ static int build_items(lfe_ctx* c) {
   bfirst[L.nb] = (int32_t)(L.hitems.size() / 4);
   if (L.hitems.empty()) L.hitems.insert(L.hitems.end(), {0, 0, 0, 0});
   L.n_items = (int)(L.hitems.size() / 4);
+  // XCD-grouped block order: workgroups are dispatched round-robin over the 8 XCDs
+  // (block i on XCD i % 8), so block r * 8 + x takes the r-th item of the buckets
+  // b with b % 8 == x.  All items of a bucket then share one L2, where the short
+  // per-item pieces they write into the bucket's key regions merge into full
+  // lines.  Speed only: any mapping is correct.
+  std::vector<int32_t> xg;
+  {
+    constexpr int kX = 8;
+    std::vector<std::vector<int32_t>> per(kX);
+    for (int b = 0; b < L.nb; ++b)
+      for (int i = bfirst[b]; i < bfirst[b + 1]; ++i) per[b % kX].push_back(i);
+    size_t rounds = 0;
+    for (auto& v : per) rounds = std::max(rounds, v.size());
+    xg.assign(rounds * kX, -1);
+    for (int x = 0; x < kX; ++x)
+      for (size_t r = 0; r < per[x].size(); ++r) xg[r * kX + x] = per[x][r];
+    if (xg.empty()) xg.push_back(0);
+    c->n_xgrid = (int)xg.size();
+  }
   LFE_TRY(ensure_items(c, L.n_items));
   LFE_TRY(ensure_i32(c, c->bitems_d, c->bitems_cap, bfirst.size()));
+  LFE_TRY(ensure_i32(c, c->xitems_d, c->xitems_cap, xg.size()));
   // upload through pinned staging, asynchronously (the staging buffer is next written
   // only after later stream synchronizations)
   const size_t ib = sizeof(int32_t) * L.hitems.size(), bb = sizeof(int32_t) * bfirst.size();
-  LFE_TRY(ensure_pinned_items(c, ib + bb));
+  const size_t xb = sizeof(int32_t) * xg.size();
+  LFE_TRY(ensure_pinned_items(c, ib + bb + xb));
   memcpy(c->hpin_items, L.hitems.data(), ib);
   memcpy(c->hpin_items + ib, bfirst.data(), bb);
+  memcpy(c->hpin_items + ib + bb, xg.data(), xb);
   LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib, hipMemcpyHostToDevice, c->stream));
   LFE_HIP(hipMemcpyAsync(c->bitems_d, c->hpin_items + ib, bb, hipMemcpyHostToDevice, c->stream));
+  LFE_HIP(hipMemcpyAsync(c->xitems_d, c->hpin_items + ib + bb, xb, hipMemcpyHostToDevice, c->stream));
   return LFE_OK;
 }
 
@@ -464,6 +500,12 @@ int prepare_layout(lfe_ctx* c) {
     }
     a.orig = c->origp;
     a.scanned = c->pcounts;
+    static const int xmap_env = [] {
+      const char* e = getenv("LFE_PART_XCD");  // tuning: 0 = plain chunk order
+      return e ? atoi(e) : 1;
+    }();
+    a.xcd_map = xmap_env;
+    const int pgrid = a.xcd_map ? ((nw + 7) / 8) * 8 : nw;
     {
       const size_t lds = sizeof(double) * cw + sizeof(int32_t) * (cw + (size_t)kPartWaves * nb + 2 * (size_t)nb + 1);
       // dynamic LDS above 64 KB must be opted in (static LDS + dynamic <= 160 KB)
@@ -472,9 +514,9 @@ int prepare_layout(lfe_ctx* c) {
       LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       ProfScope _ps(c, K_PART_SCATTER);
       if (per == 16)
-        hipLaunchKernelGGL(k_part_scatter<16>, dim3(nw), dim3(kPartThreads), lds, c->stream, a);
+        hipLaunchKernelGGL(k_part_scatter<16>, dim3(pgrid), dim3(kPartThreads), lds, c->stream, a);
       else
-        hipLaunchKernelGGL(k_part_scatter<8>, dim3(nw), dim3(kPartThreads), lds, c->stream, a);
+        hipLaunchKernelGGL(k_part_scatter<8>, dim3(pgrid), dim3(kPartThreads), lds, c->stream, a);
     }
     LFE_HIP(hipGetLastError());
     int32_t* dbstart = c->pcounts + m;
