@@ -34,7 +34,19 @@ __global__ __launch_bounds__(256) void k_hist_lds(const int32_t* __restrict__ co
   extern __shared__ int32_t h[];
   for (int g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
   __syncthreads();
-  GRID_STRIDE(i, n) atomicAdd(&h[code[i]], 1);
+  // 4 rows per thread per trip (one 16-byte load); the tail n % 4 rows one by one
+  const int64_t n4 = n >> 2;
+  const int4* c4 = reinterpret_cast<const int4*>(code);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int4 v = c4[i];
+    atomicAdd(&h[v.x], 1);
+    atomicAdd(&h[v.y], 1);
+    atomicAdd(&h[v.z], 1);
+    atomicAdd(&h[v.w], 1);
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&h[code[i]], 1);
   __syncthreads();
   for (int g = threadIdx.x; g < G; g += blockDim.x)
     if (h[g]) atomicAdd(&cnt[g], h[g]);
@@ -322,17 +334,31 @@ struct MarkArgs {
   int32_t* ndropped;
 };
 
-__global__ void k_mark(MarkArgs a, int64_t n) {
-  GRID_STRIDE(i, n) {
-    bool ok = true;
-    int32_t g[kMaxFE];
-    for (int f = 0; f < a.F; ++f) {
-      g[f] = a.code[f][i];
-      ok = ok && (a.cnt_pre[f][g[f]] > 1);
+// single-pass singleton marks (polars_impl.py:477-482): a row is dropped when any
+// of its FE groups has a pre-filter count of 1.  F is a template parameter and a
+// thread handles 4 consecutive rows (16-byte code loads; the layout is padded to ld).
+template <int F>
+__global__ __launch_bounds__(256) void k_mark(MarkArgs a, int64_t n) {
+  const int64_t n4 = (n + 3) >> 2;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i0 = t << 2;
+    int4 g[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) g[f] = reinterpret_cast<const int4*>(a.code[f])[t];
+    bool ok[4] = {true, true, true, true};
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const int gv[4] = {g[f].x, g[f].y, g[f].z, g[f].w};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (i0 + s < n) ok[s] = ok[s] && a.cnt_pre[f][gv[s]] > 1;
     }
-    if (!ok) {
-      for (int f = 0; f < a.F; ++f) atomicAdd(&a.drops[f][g[f]], 1);
-      a.code[a.P][i] = -1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (ok[s] || i0 + s >= n) continue;
+#pragma unroll
+      for (int f = 0; f < F; ++f) atomicAdd(&a.drops[f][(&g[f].x)[s]], 1);
+      a.code[a.P][i0 + s] = -1;
       atomicAdd(a.ndropped, 1);
     }
   }
@@ -455,7 +481,7 @@ int prepare_layout(lfe_ctx* c) {
     if (n == 0 || (f == L.P && L.permuted)) continue;
     ProfScope _ps(c, K_COUNT);
     if (fe.G <= kLdsHistMax)
-      hipLaunchKernelGGL(k_hist_lds, dim3(grid_for(n, 256, 512)), dim3(256), sizeof(int32_t) * fe.G, c->stream,
+      hipLaunchKernelGGL(k_hist_lds, dim3(grid_for((n + 3) / 4, 256, 2048)), dim3(256), sizeof(int32_t) * fe.G, c->stream,
                          fe.code, n, fe.G, fe.cnt_pre);
     else
       hipLaunchKernelGGL(k_hist_global, dim3(grid_for(n)), dim3(kBlock), 0, c->stream, fe.code, n, fe.cnt_pre);
@@ -568,7 +594,14 @@ int prepare_layout(lfe_ctx* c) {
     a.ndropped = ndropped;
     if (n) {
       ProfScope _ps(c, K_MARK);
-      hipLaunchKernelGGL(k_mark, dim3(grid_for(n)), dim3(kBlock), 0, c->stream, a, n);
+      const int grid = grid_for((n + 3) / 4, kBlock, 8192);
+      switch (c->F) {
+#define MARK_CASE(FF) \
+  case FF: hipLaunchKernelGGL(k_mark<FF>, dim3(grid), dim3(kBlock), 0, c->stream, a, n); break;
+        MARK_CASE(1) MARK_CASE(2) MARK_CASE(3) MARK_CASE(4) MARK_CASE(5) MARK_CASE(6) MARK_CASE(7) MARK_CASE(8)
+#undef MARK_CASE
+        default: break;
+      }
     }
     LFE_HIP(hipGetLastError());
     for (int f = 0; f < c->F; ++f) {
