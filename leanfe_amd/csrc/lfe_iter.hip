@@ -285,7 +285,9 @@ static int build_layouts(lfe_ctx* c, int Q) {
 // ===========================================================================
 
 constexpr int kTpThreads = 1024;  // K1: one workgroup per CU (alpha_Q in LDS)
-constexpr int kTqThreads = 512;   // K2: kTqSplit workgroups per bucket
+// K2 workgroup size: 16 waves while the columns fit two 16-lane slots (<= 128 VGPRs)
+template <int NT>
+constexpr int tq_threads() { return NT <= 2 ? 1024 : 512; }
 constexpr int kTqSplit = 2;
 constexpr int kIterLds = 150 * 1024;
 
@@ -474,7 +476,8 @@ struct TqArgs {
 
 // K2: T_Q[q] += sum over the (bucket, q) runs of alpha_P[h_i]
 template <int NT>
-__global__ __launch_bounds__(kTqThreads) void k_tq(TqArgs a) {
+__global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
+  constexpr int kTqThreads = tq_threads<NT>();
   extern __shared__ __attribute__((aligned(16))) double sl[];  // [B + 1][p], row B = 0
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -663,7 +666,7 @@ static void launch_tp(lfe_ctx* c, const TpArgs& a, size_t lds) {
 }
 template <int NT>
 static void launch_tq(lfe_ctx* c, const TqArgs& a, size_t lds) {
-  hipLaunchKernelGGL(k_tq<NT>, dim3(a.nb * kTqSplit), dim3(kTqThreads), lds, c->stream, a);
+  hipLaunchKernelGGL(k_tq<NT>, dim3(a.nb * kTqSplit), dim3(tq_threads<NT>()), lds, c->stream, a);
 }
 
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out) {

@@ -179,6 +179,7 @@ struct ScatterArgs {
   int32_t* orig;
   const int32_t* scanned;  // [nb][nchunks] exclusive destinations
   int xcd_map;             // 1: XCD-contiguous chunk order
+  int pipe;                // 1: load column c + 1 during column c's write-out
 };
 
 // block i -> chunk: XCD x = i % 8 walks its contiguous eighth of the chunks
@@ -272,21 +273,26 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
   const int len = (int)(r1 - r0);
   // ---- move columns through the stage: gather in row order, store in bucket order ----
   const int ncol = a.p + (a.w ? 1 : 0);
-  for (int c = 0; c < ncol; ++c) {
+  double v[PER];
+  auto load_col = [&](int c) {
     const double* src = c < a.p ? a.X + (int64_t)c * a.ld : a.w;
-    double* dst = c < a.p ? a.Xo + (int64_t)c * a.ld : a.wo;
-    double v[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int64_t i = wbase + k * 64 + lane;
       v[k] = pos[k] >= 0 ? src[i] : 0.0;
     }
+  };
+  load_col(0);
+  for (int c = 0; c < ncol; ++c) {
+    double* dst = c < a.p ? a.Xo + (int64_t)c * a.ld : a.wo;
 #pragma unroll
     for (int k = 0; k < PER; ++k)
       if (pos[k] >= 0) stage[pos[k]] = v[k];
+    if (a.pipe && c + 1 < ncol) load_col(c + 1);  // next column in flight during the write-out
     __syncthreads();
     for (int j = tid; j < len; j += kPartThreads) dst[delta[sb[j]] + j] = stage[j];
     __syncthreads();
+    if (!a.pipe && c + 1 < ncol) load_col(c + 1);
   }
   int32_t* istage = reinterpret_cast<int32_t*>(stage);
   for (int c = 0; c <= a.F; ++c) {  // F code arrays, then the input row index
@@ -531,6 +537,11 @@ int prepare_layout(lfe_ctx* c) {
       return e ? atoi(e) : 1;
     }();
     a.xcd_map = xmap_env;
+    static const int pipe_env = [] {
+      const char* e = getenv("LFE_PART_PIPE");  // tuning (measured: 1 is 0.5 % faster)
+      return e ? atoi(e) : 1;
+    }();
+    a.pipe = pipe_env;
     const int pgrid = a.xcd_map ? ((nw + 7) / 8) * 8 : nw;
     {
       const size_t lds = sizeof(double) * cw + sizeof(int32_t) * (cw + (size_t)kPartWaves * nb + 2 * (size_t)nb + 1);
