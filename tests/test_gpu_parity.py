@@ -65,6 +65,8 @@ def test_synth_device_equals_host_bit_exact():
     (3, 150_005, (3000, 40, 7), 4, "cluster"),
     (12345, 2_000_000, (100000, 1000), 10, "HC1"),   # headline geometry (1e5 / 1e3 levels, k = 10)
     (6, 400_000, (700_000, 50), 2, "iid"),           # more levels than rows: many singletons, nb > 512
+    (7, 300_000, (20000, 300), 20, "HC1"),           # p = 21: two 16-column slots (NT = 2) in every kernel
+    (8, 120_000, (4000, 150), 40, "iid"),            # p = 41: NT = 3
 ])
 def test_random_panels_vs_oracle(seed, n, L, k, vcov):
     data = synth.panel(n, k, list(L), seed=seed)
