@@ -64,12 +64,14 @@ def solve_step(eng: Engine, vcov: str):
     n_obs, dims, card = eng.drop_singletons()
     order = sorted(range(len(card)), key=lambda i: card[i])
     iterations, _ = eng.demean(order, 1e-6, 50, check_from=3)
-    G = eng.gram()
+    hc1 = vcov.lower() == "hc1"
+    fused = eng.gram_resid(hc1=hc1)  # Gram + device solve + residual pass, one round trip
+    G = fused[0] if fused is not None else eng.gram()
     XtX, Xty = inference.split_gram(G)
     beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
     k = XtX.shape[0] - 1
     df_resid = n_obs - (k + 1) - (sum(dims) - len(dims))
-    stats, meat = eng.resid(beta_full, hc1=vcov.lower() == "hc1")
+    stats, meat = (fused[2], fused[3]) if fused is not None else eng.resid(beta_full, hc1=hc1)
     if vcov.lower() == "hc1":
         se = inference.se_hc1(XtX_inv[1:, 1:], meat, n_obs, df_resid)
     else:

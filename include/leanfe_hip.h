@@ -99,6 +99,15 @@ int lfe_gram(lfe_ctx* ctx, double* gram_out);
 int lfe_resid(lfe_ctx* ctx, const double* beta_full, double* stats_out, double* hc1_meat,
               int keep_scores);
 
+/* lfe_gram + solve + lfe_resid with one host round trip: the (p+1)^2 Gram as
+ * lfe_gram, the beta_full[p] a one-thread device Cholesky solved from it (used
+ * for the residuals; equal to the host's polars_impl.py:212-226 solve up to
+ * rounding), then stats/HC1 meat/scores as lfe_resid.  Returns 1 and computes
+ * nothing usable when the fused path does not apply (F != 2, weights, p > 11,
+ * or X'X not positive definite): call lfe_gram and lfe_resid instead. */
+int lfe_gram_resid(lfe_ctx* ctx, double* gram_out, double* beta_full_out, double* stats_out, double* hc1_meat,
+                   int keep_scores);
+
 /* For each loaded cluster array j: S_c = sum_{i in c} x~_i r_i (w_i);
  * meats_out[j] = S'S (k x k), G_out[j] = number of clusters present among the
  * kept rows (std_errors.py:317-336, compress.py:929-942 — the W_C'(X.e) SpMM). */

@@ -36,6 +36,7 @@ SIGNATURES = {
     "lfe_demean": (C.c_int, [_vp, _i32p, C.c_double, C.c_int, C.c_int, _i32p, _dp]),
     "lfe_gram": (C.c_int, [_vp, _dp]),
     "lfe_resid": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int]),
+    "lfe_gram_resid": (C.c_int, [_vp, _dp, _dp, _dp, _dp, C.c_int]),
     "lfe_cluster_meat": (C.c_int, [_vp, _dp, _i64p]),
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
@@ -198,6 +199,23 @@ class Engine:
                                    None if meat is None else meat.ctypes.data_as(_dp),
                                    1 if keep_scores else 0))
         return stats, (meat[:k, :k] if meat is not None else None)
+
+    def gram_resid(self, hc1: bool = False, keep_scores: bool = False):
+        """Gram + device solve + residual pass in one call (lfe_gram_resid).  Returns
+        (gram, beta_full_device, stats, meat) or None when the fused path does not apply."""
+        D = self.p + 1
+        G = np.zeros((D, D))
+        b = np.zeros(self.p)
+        stats = np.zeros(4)
+        k = self.p - 1
+        meat = np.zeros((max(k, 1), max(k, 1))) if hc1 else None
+        rc = self._lib.lfe_gram_resid(self._h, G.ctypes.data_as(_dp), b.ctypes.data_as(_dp),
+                                      stats.ctypes.data_as(_dp), None if meat is None else meat.ctypes.data_as(_dp),
+                                      int(keep_scores))
+        if rc == 1:
+            return None
+        _check(rc)
+        return G, b, stats, (meat[:k, :k] if hc1 else None)
 
     def cluster_meat(self) -> tuple[np.ndarray, np.ndarray]:
         k = self.p - 1

@@ -72,6 +72,19 @@ int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes) {
   return LFE_OK;
 }
 
+int d2h_async(lfe_ctx* c, const void* src_dev, size_t bytes) {
+  if (bytes > kPinD2H) return fail(LFE_EINVAL, "d2h_async: transfer too large");
+  LFE_HIP(hipMemcpyAsync(c->hpin, src_dev, bytes, hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipEventRecord(c->aux_ev, c->stream));
+  return LFE_OK;
+}
+
+int d2h_wait(lfe_ctx* c, void* dst, size_t bytes) {
+  LFE_HIP(hipEventSynchronize(c->aux_ev));  // work enqueued after the copy keeps running
+  memcpy(dst, c->hpin, bytes);
+  return LFE_OK;
+}
+
 int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes) {
   if (bytes == 0) return LFE_OK;
   if (bytes > kPinSmall - kPinD2H) {
@@ -332,6 +345,7 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreateWithFlags(&c->hpin_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->hpin), kPinSmall, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess) {
     delete c;
@@ -365,6 +379,7 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   if (c->hpin) (void)hipHostFree(c->hpin);
   if (c->hpin_items) (void)hipHostFree(c->hpin_items);
   if (c->hpin_ev) (void)hipEventDestroy(c->hpin_ev);
+  if (c->aux_ev) (void)hipEventDestroy(c->aux_ev);
   dfree(c->clS);
   dfree(c->clP);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -497,7 +512,7 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
     PhaseTimer t(c, &c->tm.demean);
     for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
     if (c->F > 0) {
-      LFE_TRY(sweep_group_sums(c));
+      if (!c->sums_ready) LFE_TRY(sweep_group_sums(c));
       if (check_from > 0 && fast_path_ok(c, order)) {
         // two FEs, unweighted: segment layout + one fused codes-only kernel per sweep
         LFE_TRY(demean_fast(c, tol, max_iter, check_from, &iterations, &last));
@@ -538,6 +553,16 @@ int lfe_resid(lfe_ctx* c, const double* beta_full, double* stats_out, double* hc
   if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)(c->p - 1) * c->ld));
   PhaseTimer t(c, &c->tm.resid);
   return launch_resid(c, beta_full, stats_out, hc1_meat, keep_scores);
+}
+
+int lfe_gram_resid(lfe_ctx* c, double* gram_out, double* beta_full_out, double* stats_out, double* hc1_meat,
+                   int keep_scores) {
+  LFE_CTX(c);
+  if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
+  if (!gram_out || !beta_full_out || !stats_out) return fail(LFE_EINVAL, "null pointer");
+  if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)(c->p - 1) * c->ld));
+  PhaseTimer t(c, &c->tm.resid);
+  return launch_gram_resid(c, gram_out, beta_full_out, stats_out, hc1_meat, keep_scores);
 }
 
 int lfe_cluster_meat(lfe_ctx* c, double* meats_out, int64_t* G_out) {

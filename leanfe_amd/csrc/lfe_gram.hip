@@ -845,6 +845,75 @@ static bool resid_rows_ok(const lfe_ctx* c, const GramArgs& a) {
          ((size_t)a.B + c->fe[1 - a.la.P].G) * PM * 8 <= 150 * 1024;
 }
 
+// row-per-lane design Gram (k_design_rows): the reduced [16][16] tile (column 0 =
+// intercept, 1 + c = data column c; all ranks) is left in out_dev
+static int design_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
+  a.nq = 1;
+  a.qf[0] = 1 - a.la.P;
+  a.G_Q = c->fe[a.qf[0]].G;
+  const int p = c->p;
+  const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 11;
+  const size_t dyn = sizeof(double) * ((size_t)a.B + a.G_Q) * ((PM + 1) & ~1);
+  const void* fn = PM == 4   ? reinterpret_cast<const void*>(&k_design_rows<4, 2>)
+                   : PM == 8 ? reinterpret_cast<const void*>(&k_design_rows<8, 2>)
+                             : reinterpret_cast<const void*>(&k_design_rows<11, 1>);
+  if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kResThreads, dyn)));
+  const int64_t pstride = 256 + 4;
+  LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
+  {
+    ProfScope _ps(c, K_GRAM_DESIGN);
+    double* part = c->scratch;
+    void* args[] = {&a, &part, const_cast<int64_t*>(&pstride)};
+    LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(kResThreads), args, dyn, c->stream));
+  }
+  LFE_HIP(hipGetLastError());
+  {
+    ProfScope _ps(c, K_REDUCE);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(256), dim3(256), 0, c->stream, c->scratch, nblocks, pstride, out_dev);
+  }
+  LFE_HIP(hipGetLastError());
+  return allreduce_sum_f64(c, out_dev, 256);
+}
+
+// beta_full of X = [1, x] from the reduced design tile (column 0 intercept, 1 y, 2.. x):
+// Cholesky of X'X and two triangular solves, one thread (m <= 12).  ok = 0 when X'X is
+// not positive definite (the host then solves as polars_impl.py:217-220 does).
+__global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __restrict__ beta,
+                             double* __restrict__ beta_copy, double* __restrict__ ok) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int m = p;  // intercept + k regressors
+  double L[12][12], b[12], y[12];
+  auto idx = [](int i) { return i == 0 ? 0 : i + 1; };
+  for (int i = 0; i < m; ++i) b[i] = tile[idx(i) * 16 + 1];
+  for (int j = 0; j < m; ++j) {
+    double d = tile[idx(j) * 16 + idx(j)];
+    for (int t = 0; t < j; ++t) d -= L[j][t] * L[j][t];
+    if (!(d > 0.0)) {
+      *ok = 0.0;
+      return;
+    }
+    L[j][j] = sqrt(d);
+    for (int i = j + 1; i < m; ++i) {
+      double v = tile[idx(i) * 16 + idx(j)];
+      for (int t = 0; t < j; ++t) v -= L[i][t] * L[j][t];
+      L[i][j] = v / L[j][j];
+    }
+  }
+  for (int i = 0; i < m; ++i) {
+    double v = b[i];
+    for (int t = 0; t < i; ++t) v -= L[i][t] * y[t];
+    y[i] = v / L[i][i];
+  }
+  for (int i = m - 1; i >= 0; --i) {
+    double v = y[i];
+    for (int t = i + 1; t < m; ++t) v -= L[t][i] * b[t];
+    b[i] = v / L[i][i];
+  }
+  for (int i = 0; i < m; ++i) beta[i] = beta_copy[i] = b[i];
+  *ok = 1.0;
+}
+
 int launch_gram(lfe_ctx* c, double* host_gram) {
   GramArgs a = base_args(c);
   static const int lanes = [] {
@@ -852,38 +921,11 @@ int launch_gram(lfe_ctx* c, double* host_gram) {
     return e ? atoi(e) : 0;
   }();
   if (lanes != 1 && resid_rows_ok(c, a) && c->p <= 11) {
-    // row-per-lane design Gram: [16][16] tile, column 0 = intercept, 1 + c = data column c
-    a.nq = 1;
-    a.qf[0] = 1 - a.la.P;
-    a.G_Q = c->fe[a.qf[0]].G;
-    const int p = c->p;
-    const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 11;
-    const size_t dyn = sizeof(double) * ((size_t)a.B + a.G_Q) * ((PM + 1) & ~1);
-    const void* fn = PM == 4   ? reinterpret_cast<const void*>(&k_design_rows<4, 2>)
-                     : PM == 8 ? reinterpret_cast<const void*>(&k_design_rows<8, 2>)
-                               : reinterpret_cast<const void*>(&k_design_rows<11, 1>);
-    if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-    const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kResThreads, dyn)));
-    const int64_t pstride = 256 + 4;
-    LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
-    LFE_TRY(ensure_dred(c, (size_t)pstride));
-    {
-      ProfScope _ps(c, K_GRAM_DESIGN);
-      double* part = c->scratch;
-      void* args[] = {&a, &part, const_cast<int64_t*>(&pstride)};
-      LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(kResThreads), args, dyn, c->stream));
-    }
-    LFE_HIP(hipGetLastError());
-    {
-      ProfScope _ps(c, K_REDUCE);
-      hipLaunchKernelGGL(k_reduce_partials, dim3(256), dim3(256), 0, c->stream, c->scratch, nblocks, pstride,
-                         c->dred);
-    }
-    LFE_HIP(hipGetLastError());
-    LFE_TRY(allreduce_sum_f64(c, c->dred, 256));
+    LFE_TRY(ensure_dred(c, 256));
+    LFE_TRY(design_rows_enqueue(c, a, c->dred));
     std::vector<double> h(256);
     LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 256));
-    const int D = p + 1;
+    const int D = c->p + 1;
     for (int i = 0; i < D; ++i)
       for (int j = 0; j < D; ++j) host_gram[i * D + j] = h[(size_t)i * 16 + j];
     return LFE_OK;
@@ -891,10 +933,11 @@ int launch_gram(lfe_ctx* c, double* host_gram) {
   return gram_dispatch<GRAM_DESIGN>(c, a, c->p + 1, 0, c->p + 1, host_gram, nullptr, 0);
 }
 
-// row-per-lane residual pass (k_resid_rows): two FEs, unweighted, p <= 16, both
-// alpha tables (padded to PM doubles per row) in LDS
-static int resid_rows(lfe_ctx* c, GramArgs a, double* meat, double* stats) {
-  const int p = c->p, k = p - 1;
+// row-per-lane residual pass (k_resid_rows): two FEs, unweighted, p <= 12, both
+// alpha tables (padded to PM doubles per row) in LDS; leaves the reduced [16][16]
+// tile + 4 statistics (260 doubles, all ranks) in out_dev
+static int resid_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
+  const int p = c->p;
   const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
   const size_t dyn = sizeof(double) * ((size_t)a.B + a.G_Q) * PM;
   const void* fn = PM == 4   ? reinterpret_cast<const void*>(&k_resid_rows<4, 2>)
@@ -904,7 +947,6 @@ static int resid_rows(lfe_ctx* c, GramArgs a, double* meat, double* stats) {
   const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kResThreads, dyn)));
   const int64_t pstride = 256 + 4;
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
-  LFE_TRY(ensure_dred(c, (size_t)pstride));
   {
     ProfScope _ps(c, K_GRAM_RESID);
     double* part = c->scratch;
@@ -915,18 +957,58 @@ static int resid_rows(lfe_ctx* c, GramArgs a, double* meat, double* stats) {
   {
     ProfScope _ps(c, K_REDUCE);
     hipLaunchKernelGGL(k_reduce_partials, dim3(pstride), dim3(256), 0, c->stream, c->scratch, nblocks, pstride,
-                       c->dred);
+                       out_dev);
   }
   LFE_HIP(hipGetLastError());
-  LFE_TRY(allreduce_sum_f64(c, c->dred, (size_t)pstride));
-  std::vector<double> h((size_t)pstride);
-  LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * pstride));
+  return allreduce_sum_f64(c, out_dev, (size_t)pstride);
+}
+
+static void unpack_resid(const double* h, int k, double* meat, double* stats) {
   for (int i = 0; i < k; ++i)
     for (int j = 0; j < k; ++j) meat[i * k + j] = h[(size_t)(1 + i) * 16 + (1 + j)];
   for (int e = 0; e < 4; ++e) stats[e] = h[256 + e];
+}
+
+static int resid_rows(lfe_ctx* c, GramArgs a, double* meat, double* stats) {
+  LFE_TRY(ensure_dred(c, 260));
+  LFE_TRY(resid_rows_enqueue(c, a, c->dred));
+  std::vector<double> h(260);
+  LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 260));
+  unpack_resid(h.data(), c->p - 1, meat, stats);
   return LFE_OK;
 }
 
+// Gram, device solve and residual pass with one host round trip (row-kernel case:
+// two FEs, unweighted, p <= 11).  Returns 1 (nothing done) when unavailable.
+int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores) {
+  GramArgs a = base_args(c);
+  if (!(resid_rows_ok(c, a) && c->p <= 11)) return 1;
+  const int p = c->p, k = p - 1;
+  // dred: [0, 256) design tile | [256, 516) residual tile + stats | 516 ok | [520, 532) beta
+  LFE_TRY(ensure_dred(c, 544));
+  LFE_TRY(design_rows_enqueue(c, a, c->dred));
+  hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dred, p, c->dbeta, c->dred + 520, c->dred + 516);
+  LFE_HIP(hipGetLastError());
+  a.nq = 1;
+  a.qf[0] = 1 - a.la.P;
+  a.G_Q = c->fe[a.qf[0]].G;
+  a.beta = c->dbeta;
+  a.scores = keep_scores ? c->scores : nullptr;
+  LFE_TRY(resid_rows_enqueue(c, a, c->dred + 256));
+  std::vector<double> h(532);
+  LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 532));
+  if (h[516] != 1.0) return 1;  // not positive definite: the caller takes the two-call path
+  const int D = p + 1;
+  for (int i = 0; i < D; ++i)
+    for (int j = 0; j < D; ++j) host_gram[i * D + j] = h[(size_t)i * 16 + j];
+  for (int i = 0; i < p; ++i) beta_full[i] = h[520 + i];
+  std::vector<double> meat((size_t)std::max(k, 1) * std::max(k, 1));
+  unpack_resid(h.data() + 256, k, meat.data(), stats);
+  if (hc1)
+    for (int e = 0; e < k * k; ++e) hc1[e] = meat[e];
+  c->scores_valid = keep_scores != 0;
+  return LFE_OK;
+}
 
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores) {
   GramArgs a = base_args(c);

@@ -149,6 +149,7 @@ struct lfe_ctx {
   // pinned host staging (small transfers avoid the runtime's pageable path)
   char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
   hipEvent_t hpin_ev = nullptr;    // last H2D from the staging region
+  hipEvent_t aux_ev = nullptr;     // completion of an asynchronous D2H into the staging region
   char* hpin_items = nullptr;      // work-item upload staging
   size_t hpin_items_cap = 0;
   double* scores = nullptr;  // [k][ld] x~ r (w), layout order
@@ -172,6 +173,7 @@ struct lfe_ctx {
   // state
   int64_t n_kept = 0;
   bool loaded = false, prepared = false, demeaned = false;
+  bool sums_ready = false;  // S (and W, Sy) already enqueued by lfe_drop_singletons
   // distributed
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
@@ -198,6 +200,7 @@ int sweep_check(lfe_ctx* c, double* host_max);
 // --- Gram / residual / clusters (lfe_gram.hip) ---
 int launch_gram(lfe_ctx* c, double* host_gram);
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores);
+int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores);
 int launch_cluster(lfe_ctx* c, double* meats, int64_t* G_out);
 int launch_copy_demeaned(lfe_ctx* c, double* dev_out);
 int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* flag, hipStream_t s);
@@ -218,6 +221,9 @@ int ensure_u16(lfe_ctx* c, uint16_t*& p, size_t& cap, size_t elems);
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
 // device -> host copy of a small result through pinned staging, synchronizing the stream
 int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes);
+// device -> host copy into the pinned staging region without waiting; d2h_wait finishes it
+int d2h_async(lfe_ctx* c, const void* src_dev, size_t bytes);
+int d2h_wait(lfe_ctx* c, void* dst, size_t bytes);
 // host -> device copy of a small argument through pinned staging (asynchronous)
 int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes);
 // pinned upload buffer of at least `bytes` (work items)

@@ -470,6 +470,7 @@ static int build_items(lfe_ctx* c) {
 int prepare_layout(lfe_ctx* c) {
   auto& L = c->L;
   const int64_t n = c->n;
+  c->sums_ready = false;
   // primary FE: most levels (ties -> first)
   L.P = -1;
   for (int f = 0; f < c->F; ++f)
@@ -513,6 +514,12 @@ int prepare_layout(lfe_ctx* c) {
     }
     LFE_HIP(hipGetLastError());
     LFE_TRY(exclusive_scan(c, c->pcounts, m));
+    // bucket starts depend on the scan only: fetch them now and build the work items
+    // on the host while the GPU runs the scatter
+    int32_t* dbstart = c->pcounts + m;
+    hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(nb)), dim3(kBlock), 0, c->stream, c->pcounts, nb, nw, dbstart);
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(d2h_async(c, dbstart, sizeof(int32_t) * nb));
     ScatterArgs a{};
     a.p = c->p;
     a.F = c->F;
@@ -556,11 +563,8 @@ int prepare_layout(lfe_ctx* c) {
         hipLaunchKernelGGL(k_part_scatter<8>, dim3(pgrid), dim3(kPartThreads), lds, c->stream, a);
     }
     LFE_HIP(hipGetLastError());
-    int32_t* dbstart = c->pcounts + m;
-    hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(nb)), dim3(kBlock), 0, c->stream, c->pcounts, nb, nw, dbstart);
-    LFE_HIP(hipGetLastError());
     L.bstart.assign(nb + 1, 0);
-    LFE_TRY(d2h_sync(c, L.bstart.data(), dbstart, sizeof(int32_t) * nb));
+    LFE_TRY(d2h_wait(c, L.bstart.data(), sizeof(int32_t) * nb));
     L.bstart[nb] = (int32_t)n;
     L.X = c->Xp;
     L.w = c->w ? c->wp : nullptr;
@@ -626,7 +630,14 @@ int prepare_layout(lfe_ctx* c) {
     }
   }
   int32_t h[2 * kMaxFE + 8];
-  LFE_TRY(d2h_sync(c, h, c->iscratch, sizeof(h)));
+  LFE_TRY(d2h_async(c, c->iscratch, sizeof(h)));
+  // the constant group sums S_f do not depend on the FE order: enqueue them now so the
+  // GPU keeps working while the host reads the counts and returns (lfe_demean skips them)
+  if (c->F > 0 && c->n > 0) {
+    LFE_TRY(sweep_group_sums(c));
+    c->sums_ready = true;
+  }
+  LFE_TRY(d2h_wait(c, h, sizeof(h)));
   for (int f = 0; f < c->F; ++f) {
     c->fe[f].dims = h[2 * f];
     c->fe[f].card = h[2 * f + 1];

@@ -142,13 +142,19 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             raise ValueError(f"Unknown strategy: {strategy}")
 
         k = len(x_cols)
-        G = eng.gram()
+        # Gram + solve + residual pass; one host round trip when the fused path applies
+        # (the residuals then use the device's Cholesky solve of the same Gram)
+        fused = eng.gram_resid(hc1=(v == "hc1"), keep_scores=(v == "cluster"))
+        G = fused[0] if fused is not None else eng.gram()
         XtX, Xty = inference.split_gram(G)
-        beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
+        beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # polars_impl.py:212-226, host
         beta = beta_full[1:]
         df_resid = n_obs - (k + 1) - absorbed_df
         Vb = XtX_inv[1:, 1:]
-        stats, meat = eng.resid(beta_full, hc1=(v == "hc1"), keep_scores=(v == "cluster"))
+        if fused is not None:
+            stats, meat = fused[2], fused[3]
+        else:
+            stats, meat = eng.resid(beta_full, hc1=(v == "hc1"), keep_scores=(v == "cluster"))
         rss_w, rss, sum_y, sum_y2 = stats
         n_clusters = None
         if v == "iid":
