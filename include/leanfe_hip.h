@@ -49,6 +49,14 @@ void lfe_ctx_destroy(lfe_ctx* ctx);
 int lfe_comm_unique_id(void* out128);
 int lfe_ctx_set_comm(lfe_ctx* ctx, const void* unique_id128, int rank, int world);
 
+/* Testing the multi-rank paths on one GPU: an in-process emulated group of `world`
+ * contexts (each driven by its own host thread) whose all-reduces go through host
+ * memory behind a barrier, in the same order as with RCCL. */
+typedef struct lfe_emu lfe_emu;
+int lfe_emu_create(int world, lfe_emu** out);
+void lfe_emu_destroy(lfe_emu* emu);
+int lfe_ctx_set_emu(lfe_ctx* ctx, lfe_emu* emu, int rank);
+
 /* Upload one row shard.  cols[0] = y, cols[1..p-1] = x (then instruments),
  * f64; fe_codes[f] = dense int32 codes in [0, n_levels[f]) (global across
  * shards); weights may be NULL.  `where` = LFE_HOST or LFE_DEVICE for the

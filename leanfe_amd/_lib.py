@@ -29,6 +29,9 @@ SIGNATURES = {
     "lfe_ctx_destroy": (None, [_vp]),
     "lfe_comm_unique_id": (C.c_int, [_vp]),
     "lfe_ctx_set_comm": (C.c_int, [_vp, _vp, C.c_int, C.c_int]),
+    "lfe_emu_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "lfe_emu_destroy": (None, [_vp]),
+    "lfe_ctx_set_emu": (C.c_int, [_vp, _vp, C.c_int]),
     "lfe_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.POINTER(_vp), C.c_int, C.POINTER(_vp), _i32p, _vp, C.c_int]),
     "lfe_synth_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, _dp, C.c_uint64, C.c_int64]),
     "lfe_load_clusters": (C.c_int, [_vp, C.c_int, C.POINTER(_vp), _i32p, C.c_int]),
@@ -132,6 +135,11 @@ class Engine:
             _check(self._lib.lfe_ctx_set_comm(self._h, C.cast(buf, _vp), rank, world))
         else:
             _check(self._lib.lfe_ctx_set_comm(self._h, None, 0, 1))
+
+    def set_emu(self, group: "EmuGroup", rank: int) -> None:
+        """Join an in-process emulated group (tests of the multi-rank paths on one GPU)."""
+        _check(self._lib.lfe_ctx_set_emu(self._h, group.handle, int(rank)))
+        self._emu = group  # keep the group alive while this context uses it
 
     # -- data --------------------------------------------------------------
     def load(self, cols: list[np.ndarray], codes: list[np.ndarray], levels: list[int],
@@ -278,3 +286,21 @@ class Engine:
 
 def version() -> str:
     return load_library().lfe_version().decode()
+
+
+class EmuGroup:
+    """In-process emulated communicator of `world` contexts (lfe_emu_create): each
+    context must be driven by its own thread; all-reduces meet at a host barrier."""
+
+    def __init__(self, world: int):
+        self._lib = load_library()
+        h = _vp()
+        _check(self._lib.lfe_emu_create(int(world), C.byref(h)))
+        self.handle = h
+        self.world = world
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            self._lib.lfe_emu_destroy(h)
+            self.handle = None

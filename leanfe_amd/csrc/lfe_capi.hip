@@ -2,7 +2,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -136,20 +138,81 @@ int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems) {
   return ensure(c->clP, c->clP_elems, flag_elems);
 }
 
+}  // namespace lfe
+
+// In-process emulated communicator (tests only): `world` contexts of one process,
+// each driven by its own host thread, exchange all-reduce buffers through host
+// memory behind a barrier.  It exercises the engine's multi-rank code paths (the
+// same collective calls, in the same order, as with RCCL) on a single GPU.
+struct lfe_emu {
+  int world = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  int64_t generation = 0;
+  std::vector<std::vector<char>> slots;
+  std::vector<char> result;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    const int64_t gen = generation;
+    if (++arrived == world) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != gen; });
+    }
+  }
+};
+
+namespace lfe {
+
+enum EmuOp { EMU_SUM_F64, EMU_SUM_I32, EMU_MAX_F64 };
+
+static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
+  lfe_emu* e = c->emu;
+  const size_t esz = op == EMU_SUM_I32 ? sizeof(int32_t) : sizeof(double);
+  const size_t bytes = count * esz;
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  e->slots[c->rank].resize(bytes);
+  LFE_HIP(hipMemcpy(e->slots[c->rank].data(), dev, bytes, hipMemcpyDeviceToHost));
+  e->barrier();
+  if (c->rank == 0) {  // fixed rank order: deterministic
+    e->result = e->slots[0];
+    for (int r = 1; r < e->world; ++r)
+      for (size_t i = 0; i < count; ++i) {
+        if (op == EMU_SUM_I32) {
+          reinterpret_cast<int32_t*>(e->result.data())[i] += reinterpret_cast<const int32_t*>(e->slots[r].data())[i];
+        } else {
+          double& acc = reinterpret_cast<double*>(e->result.data())[i];
+          const double v = reinterpret_cast<const double*>(e->slots[r].data())[i];
+          acc = op == EMU_SUM_F64 ? acc + v : std::max(acc, v);
+        }
+      }
+  }
+  e->barrier();
+  LFE_HIP(hipMemcpy(dev, e->result.data(), bytes, hipMemcpyHostToDevice));
+  e->barrier();  // every rank has its copy before the result buffer is reused
+  return LFE_OK;
+}
+
 int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count) {
   if (c->world <= 1 || count == 0) return LFE_OK;
+  if (c->emu) return emu_allreduce(c, dev, count, EMU_SUM_F64);
   LFE_NCCL(ncclAllReduce(dev, dev, count, ncclFloat64, ncclSum, c->comm, c->stream));
   return LFE_OK;
 }
 
 int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count) {
   if (c->world <= 1 || count == 0) return LFE_OK;
+  if (c->emu) return emu_allreduce(c, dev, count, EMU_SUM_I32);
   LFE_NCCL(ncclAllReduce(dev, dev, count, ncclInt32, ncclSum, c->comm, c->stream));
   return LFE_OK;
 }
 
 int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count) {
   if (c->world <= 1 || count == 0) return LFE_OK;
+  if (c->emu) return emu_allreduce(c, dev, count, EMU_MAX_F64);
   LFE_NCCL(ncclAllReduce(dev, dev, count, ncclFloat64, ncclMax, c->comm, c->stream));
   return LFE_OK;
 }
@@ -403,6 +466,30 @@ int lfe_comm_unique_id(void* out128) {
   return LFE_OK;
 }
 
+int lfe_emu_create(int world, lfe_emu** out) {
+  if (!out || world < 1) return fail(LFE_EINVAL, "bad arguments");
+  lfe_emu* e = new lfe_emu();
+  e->world = world;
+  e->slots.resize(world);
+  *out = e;
+  return LFE_OK;
+}
+
+void lfe_emu_destroy(lfe_emu* e) { delete e; }
+
+int lfe_ctx_set_emu(lfe_ctx* c, lfe_emu* e, int rank) {
+  LFE_CTX(c);
+  if (!e || rank < 0 || rank >= e->world) return fail(LFE_EINVAL, "bad emulated group / rank");
+  if (c->comm) {
+    ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  c->emu = e;
+  c->rank = rank;
+  c->world = e->world;
+  return LFE_OK;
+}
+
 int lfe_ctx_set_comm(lfe_ctx* c, const void* unique_id128, int rank, int world) {
   LFE_CTX(c);
   if (world < 1 || rank < 0 || rank >= world) return fail(LFE_EINVAL, "bad rank/world");
@@ -410,6 +497,7 @@ int lfe_ctx_set_comm(lfe_ctx* c, const void* unique_id128, int rank, int world) 
     ncclCommDestroy(c->comm);
     c->comm = nullptr;
   }
+  c->emu = nullptr;
   c->rank = rank;
   c->world = world;
   if (world == 1) return LFE_OK;

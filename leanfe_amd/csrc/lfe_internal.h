@@ -174,8 +174,9 @@ struct lfe_ctx {
   int64_t n_kept = 0;
   bool loaded = false, prepared = false, demeaned = false;
   bool sums_ready = false;  // S (and W, Sy) already enqueued by lfe_drop_singletons
-  // distributed
+  // distributed: an RCCL communicator, or (tests) an in-process emulated group
   ncclComm_t comm = nullptr;
+  struct lfe_emu* emu = nullptr;
   int rank = 0, world = 1;
   lfe::Timings tm;
   lfe::Prof prof;

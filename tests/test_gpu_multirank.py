@@ -1,0 +1,115 @@
+"""The engine's multi-rank code paths on one GPU.
+
+``world`` engine contexts, each driven by its own host thread and joined in an
+in-process emulated group (``lfe_ctx_set_emu``: the same collective calls, in the
+same order, as with RCCL, reduced through host memory), solve contiguous row
+shards of one panel (global FE codes).  Every rank must return the single-process
+oracle's fit on the whole panel, and all ranks must agree bit for bit.
+
+This runs what world > 1 changes inside the engine:
+- the all-reduced counts and the kept-row total;
+- T_P partials with the P projection after the all-reduce (fast path);
+- the all-reduced T_Q and the convergence test;
+- the Gram and the device solve on every rank;
+- the residual statistics and the cluster score tables.
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import pytest
+
+from leanfe_amd import inference, synth
+from leanfe_amd.dist import shard_range
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(eng, vcov, cl_levels, n_obs_expected=None):
+    n_obs, dims, card = eng.drop_singletons()
+    order = sorted(range(len(card)), key=lambda i: card[i])
+    iterations, _ = eng.demean(order, 1e-6, 50, check_from=3)
+    v = vcov.lower()
+    fused = eng.gram_resid(hc1=v == "hc1", keep_scores=v == "cluster")
+    G = fused[0] if fused is not None else eng.gram()
+    XtX, Xty = inference.split_gram(G)
+    beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
+    if fused is not None:
+        stats, meat = fused[2], fused[3]
+    else:
+        stats, meat = eng.resid(beta_full, hc1=v == "hc1", keep_scores=v == "cluster")
+    k = XtX.shape[0] - 1
+    df = n_obs - (k + 1) - (sum(dims) - len(dims))
+    Vb = XtX_inv[1:, 1:]
+    ncl = None
+    if v == "iid":
+        se = inference.se_iid(Vb, stats[0], df)
+    elif v == "hc1":
+        se = inference.se_hc1(Vb, meat, n_obs, df)
+    else:
+        meats, Gs = eng.cluster_meat()
+        se, ncl = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df, True)
+    return dict(beta=beta_full[1:], se=se, iterations=iterations, n_obs=n_obs, df_resid=df, fe_dims=list(dims),
+                n_clusters=ncl, fused=fused is not None)
+
+
+def _run_group(world, n, k, levels, vcov, cluster_fe, seed):
+    from leanfe_amd._lib import EmuGroup, Engine
+
+    group = EmuGroup(world)
+    out, errs = {}, {}
+
+    def worker(rank):
+        try:
+            lo, hi = shard_range(n, rank, world)
+            eng = Engine(0)
+            eng.set_emu(group, rank)
+            eng.synth_load(hi - lo, k, levels, synth.betas(k), seed=seed, row_offset=lo)
+            cl_levels = None
+            if cluster_fe is not None:
+                _, codes = eng.copy_inputs()
+                eng.load_clusters([np.ascontiguousarray(codes[cluster_fe])], [levels[cluster_fe]])
+                cl_levels = [levels[cluster_fe]]
+            out[rank] = _solve(eng, vcov, cl_levels)
+            eng.close()
+        except BaseException as e:  # noqa: BLE001
+            errs[rank] = e
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+    if errs:
+        raise next(iter(errs.values()))
+    return out
+
+
+@pytest.mark.parametrize("world,n,k,levels,vcov,cluster_fe", [
+    (2, 400_003, 10, (20000, 500), "HC1", None),       # fast path (REDUCE mode), fused Gram/solve/resid
+    (3, 300_000, 4, (8000, 300), "iid", None),
+    (2, 200_000, 3, (3000, 200, 9), "cluster", 1),      # generic sweeps (F = 3) + cluster score tables
+])
+def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe):
+    from oracle import altproj
+
+    seed = 11
+    out = _run_group(world, n, k, list(levels), vcov, cluster_fe, seed)
+    full = synth.panel(n, k, list(levels), seed=seed)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    cl = [fes[cluster_fe]] if cluster_fe is not None else None
+    o = altproj.fit(full, "y", xs, fes, vcov=vcov, cluster_cols=cl)
+    for r in range(world):
+        res = out[r]
+        assert res["iterations"] == o["iterations"]
+        assert res["n_obs"] == o["n_obs"] and res["df_resid"] == o["df_resid"]
+        assert res["fe_dims"] == list(o["fe_dims"])
+        np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=0)
+        np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
+        if cluster_fe is not None:
+            assert res["n_clusters"] == o["n_clusters"]
+        np.testing.assert_array_equal(res["beta"], out[0]["beta"])  # identical on every rank
+        np.testing.assert_array_equal(res["se"], out[0]["se"])
