@@ -224,7 +224,7 @@ int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count) {
 const char* const kKernelNames[K_NUM_KERNELS] = {
     "part_hist", "scan", "part_scatter", "count", "mark", "group_sums", "cross", "check", "finalize",
     "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth",
-    "tp", "tq"};
+    "tp", "tq", "seg_build"};
 
 static hipEvent_t prof_event(lfe_ctx* c) {
   if (!c->prof.pool.empty()) {
@@ -295,13 +295,18 @@ static void free_data(lfe_ctx* c) {
     dfree(fe.T);
     dfree(fe.alpha);
     dfree(fe.R);
+    dfree(fe.seg_off);
+    dfree(fe.seg_cur);
+    dfree(fe.oc);
+    dfree(fe.ws);
+    dfree(fe.ufirst);
   }
   c->fe.clear();
   for (auto& p : c->cl) dfree(p);
   c->cl.clear();
   c->cl_levels.clear();
   c->L = Layout();
-  c->loaded = c->prepared = c->demeaned = c->scores_valid = false;
+  c->loaded = c->prepared = c->demeaned = c->scores_valid = c->seg_ready = false;
   c->n = c->ld = 0;
   c->p = c->F = 0;
 }
@@ -604,19 +609,8 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
       if (check_from > 0 && fast_path_ok(c, order)) {
         // two FEs, unweighted: segment layout + one fused codes-only kernel per sweep
         LFE_TRY(demean_fast(c, tol, max_iter, check_from, &iterations, &last));
-      } else if (check_from <= 0) {
-        // single within-transform pass ('demean' strategy, polars_impl.py:437-465)
-        for (int f : order) LFE_TRY(sweep_project(c, f));
-        iterations = 1;
       } else {
-        for (int it = 1; it <= max_iter; ++it) {
-          for (int f : order) LFE_TRY(sweep_project(c, f));
-          iterations = it;
-          if (it >= check_from) {
-            LFE_TRY(sweep_check(c, &last));
-            if (last < tol) break;
-          }
-        }
+        LFE_TRY(demean_generic(c, order, tol, max_iter, check_from, &iterations, &last));
       }
     }
   }

@@ -18,7 +18,6 @@ constexpr int kMaxFE = 8;        // FE dimensions supported per regression
 constexpr int kMaxCols = 63;     // p = 1 + k (+ instruments) <= 63 -> Gram width <= 64
 constexpr int kBlock = 256;      // threads per workgroup for simple streaming kernels
 constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
-constexpr int kMaxGroupCols = 16;    // columns per column group in a sweep
 constexpr int kLdsBudget = 64 * 1024;  // bytes of LDS tables per sweep workgroup (2 WG per CU)
 constexpr int kItemRows = 8192;      // rows per work item (a bucket is split into items)
 constexpr int kLdsHistMax = 16384;   // int32 counters in an LDS histogram
@@ -56,6 +55,17 @@ struct FeState {
   double* T = nullptr;         // [G*p] cross term of the current projection
   double* alpha = nullptr;     // [G*p] group effect subtracted so far
   double* R = nullptr;         // [G] check cross term (y column, unweighted)
+  // segment layout (general sweeps, lfe_seg.hip): kept rows sorted by this FE's code
+  int32_t* seg_off = nullptr;  // [G + 1]
+  size_t seg_off_cap = 0;
+  int32_t* seg_cur = nullptr;  // [G] scatter cursors
+  size_t seg_cur_cap = 0;
+  int32_t* oc = nullptr;       // [F - 1][ld] the other FEs' codes, segment order
+  size_t oc_cap = 0;
+  double* ws = nullptr;        // [ld] weights, segment order (weighted fits)
+  size_t ws_cap = 0;
+  int32_t* ufirst = nullptr;   // [units] segment holding each work unit's first row
+  size_t ufirst_cap = 0;
   int32_t dims = 0, card = 0;
 };
 
@@ -63,7 +73,7 @@ struct FeState {
 enum KernelId {
   K_PART_HIST = 0, K_SCAN, K_PART_SCATTER, K_COUNT, K_MARK, K_GROUP_SUMS, K_CROSS, K_CHECK, K_FINALIZE,
   K_CHECK_MAX, K_GRAM_DESIGN, K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_MISC, K_SYNTH,
-  K_TP, K_TQ, K_NUM_KERNELS
+  K_TP, K_TQ, K_SEG_BUILD, K_NUM_KERNELS
 };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 
@@ -174,6 +184,7 @@ struct lfe_ctx {
   int64_t n_kept = 0;
   bool loaded = false, prepared = false, demeaned = false;
   bool sums_ready = false;  // S (and W, Sy) already enqueued by lfe_drop_singletons
+  bool seg_ready = false;   // segment layouts built for the current drop_singletons
   // distributed: an RCCL communicator, or (tests) an in-process emulated group
   ncclComm_t comm = nullptr;
   struct lfe_emu* emu = nullptr;
@@ -193,10 +204,12 @@ int sums4(lfe_ctx* c);
 bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order);
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out);
 
-// --- sweeps (lfe_sweep.hip) ---
+// --- constant sums (lfe_sweep.hip) ---
 int sweep_group_sums(lfe_ctx* c);
-int sweep_project(lfe_ctx* c, int f);
-int sweep_check(lfe_ctx* c, double* host_max);
+// --- general sweeps (lfe_seg.hip) ---
+int seg_build(lfe_ctx* c);
+int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int max_iter, int check_from,
+                   int* iterations_out, double* last_out);
 
 // --- Gram / residual / clusters (lfe_gram.hip) ---
 int launch_gram(lfe_ctx* c, double* host_gram);

@@ -471,6 +471,7 @@ int prepare_layout(lfe_ctx* c) {
   auto& L = c->L;
   const int64_t n = c->n;
   c->sums_ready = false;
+  c->seg_ready = false;
   // primary FE: most levels (ties -> first)
   L.P = -1;
   for (int f = 0; f < c->F; ++f)

@@ -1,0 +1,451 @@
+// leanfe HIP engine — alternating projections, general case (polars_impl.py:490-526):
+// three or more FEs, weighted fits, and two-FE fits whose secondary table does not
+// fit in LDS (the unweighted two-FE case with a small secondary FE runs lfe_iter.hip).
+//
+// alpha form (see lfe_sweep.hip): projecting FE f sets
+//     alpha_f[g] = (S_f[g] - T_f[g]) / W_f[g]
+//     T_f[g]     = sum_{i in g} w_i sum_{f' != f} alpha_f'[g_f'(i)]
+// so a projection reads FE codes and gathers alpha rows; it never touches X.
+//
+// Segment layouts.  For every FE f the kept rows are counting-sorted by g_f
+// (seg_off_f[g] .. seg_off_f[g+1]) and, in that order, the codes of the other
+// FEs (and w) are stored.  T_f is then a segmented sum of gathered alpha rows:
+// no atomics, except where a segment crosses a work-unit boundary (2048-row
+// units, so one huge group cannot serialize a wave).  The gathers hit the
+// alpha tables in L2 / MALL (88 MB for 1e6 levels at p = 11).
+//
+// Lane layout as in lfe_iter.hip: lane = row quad kq (4 rows) x column c (16
+// columns per slot, NT slots), a wave walks its unit in 16-row groups.
+//
+// Stop test (polars_impl.py:511-521): after sweep `it`, max_f max_g |mean_g(y~)|.
+//   - last FE in the order: mean_g(y~) = (Sy - n alpha - T)/n with the T it was
+//     just projected with;
+//   - first FE: the same with T' = the next sweep's first cross term (computed
+//     now, reused as that projection when the loop continues);
+//   - middle FEs: one y-only cross pass each.
+// Weighted fits check with unweighted sums (polars_impl.py:513), so they run
+// y-only passes for every FE.
+#include "lfe_internal.h"
+
+#include <algorithm>
+
+namespace lfe {
+
+constexpr int kSegUnit = 2048;   // rows per work unit (multiple of 16)
+constexpr int kSegThreads = 256;
+
+// ---------------------------------------------------------------------------
+// layout build
+// ---------------------------------------------------------------------------
+
+// local kept counts (multi-rank; world == 1 copies the kept counts instead)
+__global__ __launch_bounds__(256) void k_seg_hist(const int32_t* __restrict__ keep, const int32_t* __restrict__ code,
+                                                  int64_t n, int32_t* __restrict__ hist) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (keep[i] >= 0) atomicAdd(&hist[code[i]], 1);
+}
+
+struct SegScatterArgs {
+  int F;
+  int64_t n, ld;
+  const int32_t* keep;          // layout codes of P (-1: dropped row)
+  const int32_t* code[kMaxFE];  // layout order
+  const double* w;              // layout order, or null
+  int32_t* cur[kMaxFE];         // per FE cursor (starts at seg_off)
+  int32_t* oc[kMaxFE];          // per FE: F-1 arrays of other codes, stride ld
+  double* ws[kMaxFE];           // per FE weights in segment order (null: unweighted)
+};
+
+// every kept row goes to one slot of every FE's layout (unstable: the order
+// within a segment follows the cursor atomics; sums are order-independent up to
+// rounding, as with the reduction trees elsewhere)
+__global__ __launch_bounds__(256) void k_seg_scatter(SegScatterArgs a) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (a.keep[i] < 0) continue;
+    int32_t g[kMaxFE];
+    for (int f = 0; f < a.F; ++f) g[f] = a.code[f][i];
+    const double wi = a.w ? a.w[i] : 0.0;
+    for (int f = 0; f < a.F; ++f) {
+      const int64_t pos = atomicAdd(&a.cur[f][g[f]], 1);
+      int j = 0;
+      for (int f2 = 0; f2 < a.F; ++f2)
+        if (f2 != f) a.oc[f][(int64_t)(j++) * a.ld + pos] = g[f2];
+      if (a.ws[f]) a.ws[f][pos] = wi;
+    }
+  }
+}
+
+// ufirst[u] = the segment holding row u * kSegUnit
+__global__ void k_seg_units(const int32_t* __restrict__ seg_off, int32_t G, int32_t* __restrict__ ufirst) {
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+    const int32_t a = seg_off[g], b = seg_off[g + 1];
+    for (int32_t u = (a + kSegUnit - 1) / kSegUnit; (int64_t)u * kSegUnit < b; ++u) ufirst[u] = g;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// cross term
+// ---------------------------------------------------------------------------
+
+struct SegCrossArgs {
+  const int32_t* seg_off;            // [G + 1]
+  const int32_t* ufirst;             // [n_units]
+  int n_units;
+  const int32_t* oc[kMaxFE - 1];     // other FEs' codes, segment order
+  const double* alpha[kMaxFE - 1];   // their tables [G'][p]
+  const double* ws;                  // weights in segment order (WT)
+  int p;                             // alpha row stride
+  int pc;                            // columns computed: p, or 1 (y only)
+  int G;
+  double* T;                         // [G][pc], zeroed before the launch
+};
+
+__device__ __forceinline__ double seg_quad_sum(double v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// groups gathered per step (register budget: codes UNR*NO int4, values UNR*4*NT f64)
+template <int NT, int NO>
+constexpr int seg_unroll() {
+  return NT >= 3 ? 1 : (NT == 2 ? (NO <= 2 ? 2 : 1) : (NO <= 2 ? 4 : (NO <= 4 ? 2 : 1)));
+}
+
+template <int NT, int NO, bool WT>
+__global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
+  constexpr int UNR = seg_unroll<NT, NO>();
+  const int lane = threadIdx.x & 63;
+  const int kq = lane >> 4, c = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSegThreads / 64) + (threadIdx.x >> 6)));
+  const int nwaves = gridDim.x * (kSegThreads / 64);
+  const int p = a.p, pc = a.pc, G = a.G;
+  int cl[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) cl[I] = 16 * I + c < pc ? 16 * I + c : 0;
+  const int32_t kept = a.seg_off[G];
+  for (int u = wv; u < a.n_units; u += nwaves) {
+    const int lo = u * kSegUnit;
+    if (lo >= kept) break;
+    const int hi = min(lo + kSegUnit, kept);
+    int h = a.ufirst[u];
+    int r0 = a.seg_off[h], r1 = a.seg_off[h + 1];
+    bool part = r0 < lo;  // segment h began in an earlier unit
+    bool done = false;
+    double acc[NT];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) acc[I] = 0.0;
+    auto finalize = [&](bool atomic) {
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+        const double t = seg_quad_sum(acc[I]);
+        const int col = 16 * I + c;
+        if (kq == 0 && col < pc) {
+          double* d = a.T + (int64_t)h * pc + col;
+          if (atomic) atomicAdd(d, t);
+          else *d = t;
+        }
+        acc[I] = 0.0;
+      }
+    };
+    for (int gs0 = lo; gs0 < hi && !done; gs0 += 16 * UNR) {
+      // codes of UNR 16-row groups, then all their gathers
+      int cd[UNR][NO][4];
+#pragma unroll
+      for (int U = 0; U < UNR; ++U) {
+        const int rb = gs0 + 16 * U + 4 * kq;
+#pragma unroll
+        for (int j = 0; j < NO; ++j) {
+          int4 v = int4{0, 0, 0, 0};
+          if (gs0 + 16 * U < hi) v = *reinterpret_cast<const int4*>(a.oc[j] + rb);
+          cd[U][j][0] = rb + 0 < hi ? v.x : 0;
+          cd[U][j][1] = rb + 1 < hi ? v.y : 0;
+          cd[U][j][2] = rb + 2 < hi ? v.z : 0;
+          cd[U][j][3] = rb + 3 < hi ? v.w : 0;
+        }
+      }
+      double val[UNR][4][NT];
+#pragma unroll
+      for (int U = 0; U < UNR; ++U)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int I = 0; I < NT; ++I) val[U][s][I] = 0.0;
+#pragma unroll
+          for (int j = 0; j < NO; ++j) {
+            const double* al = a.alpha[j] + (uint32_t)cd[U][j][s] * (uint32_t)p;
+#pragma unroll
+            for (int I = 0; I < NT; ++I) val[U][s][I] += al[cl[I]];
+          }
+        }
+#pragma unroll
+      for (int U = 0; U < UNR; ++U) {
+        const int gs = gs0 + 16 * U, ge = gs + 16;
+        if (gs >= hi || done) break;
+        const int rb = gs + 4 * kq;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          double ws = rb + s < hi ? 1.0 : 0.0;
+          if (WT) ws = rb + s < hi ? a.ws[rb + s] : 0.0;
+#pragma unroll
+          for (int I = 0; I < NT; ++I) val[U][s][I] *= ws;
+        }
+        while (true) {
+          if (r0 <= gs && r1 >= ge) {  // the whole group lies in segment h
+#pragma unroll
+            for (int I = 0; I < NT; ++I)
+              acc[I] += (val[U][0][I] + val[U][1][I]) + (val[U][2][I] + val[U][3][I]);
+          } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const int row = rb + s;
+              const bool in = row >= r0 && row < r1;
+#pragma unroll
+              for (int I = 0; I < NT; ++I) acc[I] += in ? val[U][s][I] : 0.0;
+            }
+          }
+          if (r1 > ge) break;  // segment h continues in the next group
+          finalize(part);      // r1 <= ge <= hi: segment h ends in this unit
+          part = false;
+          do {  // next non-empty segment
+            ++h;
+            r0 = r1;
+            if (h >= G) break;
+            r1 = a.seg_off[h + 1];
+          } while (r1 == r0);
+          if (h >= G || r0 >= hi) {
+            done = true;
+            break;
+          }
+          if (r0 >= ge) break;
+        }
+      }
+    }
+    // segment h continues past the unit: partial sum
+    if (!done && h < G && r0 < hi && r1 > hi) finalize(true);
+  }
+}
+
+// alpha_f = (S_f - T_f) / W_f   (weighted: W = sum w; else W = kept count)
+__global__ void k_finalize(const double* __restrict__ S, const double* __restrict__ T, const double* __restrict__ Wsum,
+                           const int32_t* __restrict__ cnt, int32_t G, int p, double* __restrict__ alpha) {
+  const int64_t total = (int64_t)G * p;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = e / p;
+    const double den = Wsum ? Wsum[g] : (double)cnt[g];
+    alpha[e] = den > 0.0 ? (S[e] - (T ? T[e] : 0.0)) / den : 0.0;
+  }
+}
+
+// stop test (polars_impl.py:512-521): for every group present,
+//   mean_g(y~) = (Sy[g] - cnt[g] alpha[g][0] - R[g]) / cnt[g]
+// max |.| -> out (non-negative doubles order like their bit patterns)
+__global__ void k_check_max(const double* __restrict__ Sy, int sy_stride, const double* __restrict__ R, int r_stride,
+                            const double* __restrict__ alpha, int p, const int32_t* __restrict__ cnt, int32_t G,
+                            unsigned long long* __restrict__ out) {
+  double m = 0.0;
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+    const int32_t n = cnt[g];
+    if (n > 0) {
+      const double r =
+          Sy[(int64_t)g * sy_stride] - (double)n * alpha[(int64_t)g * p] - (R ? R[(int64_t)g * r_stride] : 0.0);
+      m = fmax(m, fabs(r / (double)n));
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+
+using CrossFn = void (*)(SegCrossArgs);
+
+template <int NT, int NO>
+static CrossFn cross_fn_nt(bool wt) {
+  return wt ? &k_seg_cross<NT, NO, true> : &k_seg_cross<NT, NO, false>;
+}
+template <int NO>
+static CrossFn cross_fn_no(int nt, bool wt) {
+  switch (nt) {
+    case 1: return cross_fn_nt<1, NO>(wt);
+    case 2: return cross_fn_nt<2, NO>(wt);
+    case 3: return cross_fn_nt<3, NO>(wt);
+    default: return cross_fn_nt<4, NO>(wt);
+  }
+}
+static CrossFn cross_fn(int nt, int no, bool wt) {
+  switch (no) {
+    case 1: return cross_fn_no<1>(nt, wt);
+    case 2: return cross_fn_no<2>(nt, wt);
+    case 3: return cross_fn_no<3>(nt, wt);
+    case 4: return cross_fn_no<4>(nt, wt);
+    case 5: return cross_fn_no<5>(nt, wt);
+    case 6: return cross_fn_no<6>(nt, wt);
+    default: return cross_fn_no<7>(nt, wt);
+  }
+}
+
+static int n_units_of(const lfe_ctx* c) { return (int)((c->n + kSegUnit - 1) / kSegUnit); }
+
+int seg_build(lfe_ctx* c) {
+  if (c->seg_ready || c->F < 2) return LFE_OK;
+  const auto& L = c->L;
+  const int64_t n = c->n;
+  const bool weighted = L.w != nullptr;
+  const int nu = std::max(n_units_of(c), 1);
+  SegScatterArgs a{};
+  a.F = c->F;
+  a.n = n;
+  a.ld = c->ld;
+  a.keep = L.code[L.P];
+  a.w = L.w;
+  for (int f = 0; f < c->F; ++f) {
+    auto& fe = c->fe[f];
+    LFE_TRY(ensure_i32(c, fe.seg_off, fe.seg_off_cap, (size_t)fe.G + 1));
+    LFE_TRY(ensure_i32(c, fe.seg_cur, fe.seg_cur_cap, (size_t)fe.G));
+    LFE_TRY(ensure_i32(c, fe.oc, fe.oc_cap, (size_t)(c->F - 1) * c->ld));
+    LFE_TRY(ensure_i32(c, fe.ufirst, fe.ufirst_cap, (size_t)nu));
+    if (weighted) LFE_TRY(ensure_f64(c, fe.ws, fe.ws_cap, (size_t)c->ld));
+    ProfScope _ps(c, K_SEG_BUILD);
+    LFE_HIP(hipMemsetAsync(fe.seg_off + fe.G, 0, sizeof(int32_t), c->stream));
+    if (c->world == 1) {
+      LFE_HIP(hipMemcpyAsync(fe.seg_off, fe.cnt, sizeof(int32_t) * fe.G, hipMemcpyDeviceToDevice, c->stream));
+    } else {
+      LFE_HIP(hipMemsetAsync(fe.seg_off, 0, sizeof(int32_t) * fe.G, c->stream));
+      if (n > 0)
+        hipLaunchKernelGGL(k_seg_hist, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, a.keep, L.code[f], n,
+                           fe.seg_off);
+      LFE_HIP(hipGetLastError());
+    }
+    LFE_TRY(exclusive_scan(c, fe.seg_off, (int64_t)fe.G + 1));
+    LFE_HIP(hipMemcpyAsync(fe.seg_cur, fe.seg_off, sizeof(int32_t) * fe.G, hipMemcpyDeviceToDevice, c->stream));
+    a.code[f] = L.code[f];
+    a.cur[f] = fe.seg_cur;
+    a.oc[f] = fe.oc;
+    a.ws[f] = weighted ? fe.ws : nullptr;
+  }
+  {
+    ProfScope _ps(c, K_SEG_BUILD);
+    if (n > 0) hipLaunchKernelGGL(k_seg_scatter, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, a);
+    LFE_HIP(hipGetLastError());
+    for (int f = 0; f < c->F; ++f) {
+      auto& fe = c->fe[f];
+      hipLaunchKernelGGL(k_seg_units, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, fe.seg_off, fe.G, fe.ufirst);
+    }
+    LFE_HIP(hipGetLastError());
+  }
+  c->seg_ready = true;
+  return LFE_OK;
+}
+
+// T (all columns, weighted as the fit) or R (y only, unweighted) of FE f, summed over ranks
+static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
+  auto& fe = c->fe[f];
+  const int pc = y_only ? 1 : c->p;
+  double* out = y_only ? fe.R : fe.T;
+  LFE_HIP(hipMemsetAsync(out, 0, sizeof(double) * (size_t)fe.G * pc, c->stream));
+  SegCrossArgs a{};
+  a.seg_off = fe.seg_off;
+  a.ufirst = fe.ufirst;
+  a.n_units = n_units_of(c);
+  int j = 0;
+  for (int f2 = 0; f2 < c->F; ++f2)
+    if (f2 != f) {
+      a.oc[j] = fe.oc + (size_t)j * c->ld;
+      a.alpha[j] = c->fe[f2].alpha;
+      ++j;
+    }
+  const bool wt = !y_only && c->L.w != nullptr;
+  a.ws = wt ? fe.ws : nullptr;
+  a.p = c->p;
+  a.pc = pc;
+  a.G = fe.G;
+  a.T = out;
+  if (a.n_units > 0) {
+    const int nt = (pc + 15) / 16;
+    CrossFn fn = cross_fn(nt, c->F - 1, wt);
+    const int waves_per_block = kSegThreads / 64;
+    const int grid = (a.n_units + waves_per_block - 1) / waves_per_block;
+    ProfScope _ps(c, kid);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kSegThreads), 0, c->stream, a);
+  }
+  LFE_HIP(hipGetLastError());
+  return allreduce_sum_f64(c, out, (size_t)fe.G * pc);
+}
+
+static int seg_finalize(lfe_ctx* c, int f) {
+  auto& fe = c->fe[f];
+  const bool cross = c->F > 1;
+  ProfScope _ps(c, K_FINALIZE);
+  hipLaunchKernelGGL(k_finalize, dim3(grid_for((int64_t)fe.G * c->p)), dim3(kBlock), 0, c->stream, fe.S,
+                     cross ? fe.T : nullptr, c->L.w ? fe.W : nullptr, fe.cnt, fe.G, c->p, fe.alpha);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+// max_g |mean_g(y~)| of FE f given its check cross term R (stride r_stride, null: none)
+static int seg_check_max(lfe_ctx* c, int f, const double* R, int r_stride) {
+  auto& fe = c->fe[f];
+  ProfScope _ps(c, K_CHECK_MAX);
+  const double* Sy = c->L.w ? fe.Sy : fe.S;
+  hipLaunchKernelGGL(k_check_max, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, Sy, c->L.w ? 1 : c->p, R,
+                     r_stride, fe.alpha, c->p, fe.cnt, fe.G, reinterpret_cast<unsigned long long*>(c->dred));
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int max_iter, int check_from,
+                   int* iterations_out, double* last_out) {
+  const int F = c->F;
+  const bool cross = F > 1;
+  if (cross) LFE_TRY(seg_build(c));
+  const bool reuse = cross && c->L.w == nullptr;  // T of the first FE doubles as its check term
+  auto project = [&](int f) -> int {
+    if (cross) LFE_TRY(seg_cross(c, f, false, K_CROSS));
+    return seg_finalize(c, f);
+  };
+  int iterations = 0;
+  double last = -1.0;
+  if (check_from <= 0) {
+    // single within-transform pass ('demean' strategy, polars_impl.py:437-465)
+    for (int f : order) LFE_TRY(project(f));
+    iterations = 1;
+  } else {
+    bool first_ready = false;  // T of order[0] already holds the next projection's cross term
+    for (int it = 1; it <= max_iter; ++it) {
+      for (size_t k = 0; k < order.size(); ++k) {
+        if (k == 0 && first_ready) LFE_TRY(seg_finalize(c, order[0]));
+        else LFE_TRY(project(order[k]));
+      }
+      first_ready = false;
+      iterations = it;
+      if (it < check_from) continue;
+      LFE_TRY(ensure_dred(c, 1));
+      LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double), c->stream));
+      for (size_t k = 0; k < order.size(); ++k) {
+        const int f = order[k];
+        if (!cross) {
+          LFE_TRY(seg_check_max(c, f, nullptr, 1));
+        } else if (reuse && k == order.size() - 1) {
+          LFE_TRY(seg_check_max(c, f, c->fe[f].T, c->p));
+        } else if (reuse && k == 0) {
+          LFE_TRY(seg_cross(c, f, false, K_CROSS));
+          LFE_TRY(seg_check_max(c, f, c->fe[f].T, c->p));
+          first_ready = true;
+        } else {
+          LFE_TRY(seg_cross(c, f, true, K_CHECK));
+          LFE_TRY(seg_check_max(c, f, c->fe[f].R, 1));
+        }
+      }
+      LFE_TRY(d2h_sync(c, &last, c->dred, sizeof(double)));
+      if (last < tol) break;
+    }
+  }
+  *iterations_out = iterations;
+  *last_out = last;
+  return LFE_OK;
+}
+
+}  // namespace lfe
