@@ -121,6 +121,16 @@ int lfe_gram_resid(lfe_ctx* ctx, double* gram_out, double* beta_full_out, double
  * kept rows (std_errors.py:317-336, compress.py:929-942 — the W_C'(X.e) SpMM). */
 int lfe_cluster_meat(lfe_ctx* ctx, double* meats_out, int64_t* G_out);
 
+/* Multi-way CGM subsets on the device (std_errors.py:354-441).  subset_masks[s]
+ * selects loaded cluster columns (bit j = column j); its clusters are the distinct
+ * tuples of those columns' codes among kept rows (the group_by of the intersection,
+ * std_errors.py:399-408), formed and grouped on the device (mixed-radix key, radix
+ * sort; no host factorization).  meats_out[s] = S'S, G_out[s] = number of clusters.
+ * The product of the selected n_levels must be < 2^62 (and < 2^31 with a
+ * communicator); otherwise LFE_EINVAL. */
+int lfe_cluster_meat_subsets(lfe_ctx* ctx, int n_subsets, const int32_t* subset_masks, double* meats_out,
+                             int64_t* G_out);
+
 /* Debug/fixtures: copy the demeaned columns (kept rows, device order) to host. */
 int lfe_copy_demeaned(lfe_ctx* ctx, double* const* cols_out, int64_t* n_out);
 

@@ -41,6 +41,7 @@ SIGNATURES = {
     "lfe_resid": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int]),
     "lfe_gram_resid": (C.c_int, [_vp, _dp, _dp, _dp, _dp, C.c_int]),
     "lfe_cluster_meat": (C.c_int, [_vp, _dp, _i64p]),
+    "lfe_cluster_meat_subsets": (C.c_int, [_vp, C.c_int, _vp, _dp, _i64p]),
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_sync": (C.c_int, [_vp]),
@@ -231,6 +232,17 @@ class Engine:
         meats = np.zeros(max(m * k * k, 1))
         G = np.zeros(max(m, 1), dtype=np.int64)
         _check(self._lib.lfe_cluster_meat(self._h, meats.ctypes.data_as(_dp), G.ctypes.data_as(_i64p)))
+        return meats[:m * k * k].reshape(m, k, k), G[:m]
+
+    def cluster_meat_subsets(self, subsets) -> tuple[np.ndarray, np.ndarray]:
+        """CGM subsets (tuples of loaded cluster column indices) grouped on the device."""
+        k = self.p - 1
+        masks = np.array([sum(1 << j for j in s) for s in subsets], dtype=np.int32)
+        m = len(masks)
+        meats = np.zeros(max(m * k * k, 1))
+        G = np.zeros(max(m, 1), dtype=np.int64)
+        _check(self._lib.lfe_cluster_meat_subsets(self._h, m, masks.ctypes.data_as(_vp),
+                                                  meats.ctypes.data_as(_dp), G.ctypes.data_as(_i64p)))
         return meats[:m * k * k].reshape(m, k, k), G[:m]
 
     def _rows(self, n: int | None) -> int:

@@ -127,6 +127,7 @@ int ensure_items(lfe_ctx* c, size_t n_items) { return ensure(c->items_d, c->item
 int ensure_i32(lfe_ctx*, int32_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 int ensure_f64(lfe_ctx*, double*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 int ensure_u16(lfe_ctx*, uint16_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
+int ensure_u64(lfe_ctx*, uint64_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 
 int ensure_pcounts(lfe_ctx* c, size_t elems, size_t sums) {
   LFE_TRY(ensure(c->pcounts, c->pcounts_elems, elems));
@@ -224,7 +225,7 @@ int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count) {
 const char* const kKernelNames[K_NUM_KERNELS] = {
     "part_hist", "scan", "part_scatter", "count", "mark", "group_sums", "cross", "check", "finalize",
     "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth",
-    "tp", "tq", "seg_build"};
+    "tp", "tq", "seg_build", "cluster_sort"};
 
 static hipEvent_t prof_event(lfe_ctx* c) {
   if (!c->prof.pool.empty()) {
@@ -305,6 +306,7 @@ static void free_data(lfe_ctx* c) {
   for (auto& p : c->cl) dfree(p);
   c->cl.clear();
   c->cl_levels.clear();
+  free_cluster_ws(c);
   c->L = Layout();
   c->loaded = c->prepared = c->demeaned = c->scores_valid = c->seg_ready = false;
   c->n = c->ld = 0;
@@ -547,7 +549,9 @@ int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const i
   LFE_CTX(c);
   if (!c->loaded) return fail(LFE_ESTATE, "lfe_load must precede lfe_load_clusters");
   if (m < 0 || (m > 0 && (!cl_codes || !cl_levels))) return fail(LFE_EINVAL, "bad cluster arrays");
+  if (m > 30) return fail(LFE_EINVAL, "at most 30 cluster columns");
   for (auto& p : c->cl) dfree(p);
+  free_cluster_ws(c);
   c->cl.assign(m, nullptr);
   c->cl_levels.assign(cl_levels, cl_levels + m);
   const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
@@ -652,7 +656,17 @@ int lfe_cluster_meat(lfe_ctx* c, double* meats_out, int64_t* G_out) {
   if (!c->scores_valid) return fail(LFE_ESTATE, "lfe_resid(keep_scores=1) first");
   if (!meats_out || !G_out) return fail(LFE_EINVAL, "null pointer");
   PhaseTimer t(c, &c->tm.cluster);
-  return launch_cluster(c, meats_out, G_out);
+  std::vector<int32_t> masks(c->cl.size());
+  for (size_t j = 0; j < masks.size(); ++j) masks[j] = 1 << j;
+  return launch_cluster_subsets(c, (int)masks.size(), masks.data(), meats_out, G_out);
+}
+
+int lfe_cluster_meat_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, double* meats_out, int64_t* G_out) {
+  LFE_CTX(c);
+  if (!c->scores_valid) return fail(LFE_ESTATE, "lfe_resid(keep_scores=1) first");
+  if (n_subsets < 0 || (n_subsets > 0 && (!masks || !meats_out || !G_out))) return fail(LFE_EINVAL, "null pointer");
+  PhaseTimer t(c, &c->tm.cluster);
+  return launch_cluster_subsets(c, n_subsets, masks, meats_out, G_out);
 }
 
 int lfe_copy_demeaned(lfe_ctx* c, double* const* cols_out, int64_t* n_out) {

@@ -1,0 +1,436 @@
+// leanfe HIP engine — cluster scores and the CGM meats (std_errors.py:289-441,
+// compress.py:817-851: the one-hot SpMM W_C'(X (.) e)).
+//
+// For a cluster subset s (bit j = loaded cluster column j) the clusters are the
+// distinct tuples of the selected columns' codes among kept rows
+// (std_errors.py:399-408 groups by the intersection).  On the device:
+//   1. key_i = mixed-radix code of the tuple (span = prod of levels < 2^62);
+//      dropped rows get key = span, which sorts last;
+//   2. stable LSD radix sort of (key, row) pairs, 8-bit digits: per-block digit
+//      histograms, one exclusive scan, a scatter ranked by wave ballots;
+//   3. segments = runs of equal keys (flags + scan), G = their number;
+//   4. S_c = segmented gather-sum of the row-major score rows x~_i r_i (w_i)
+//      (seg_gather_sum, the general-sweep kernel of lfe_seg.hip);
+//   5. meat = S'S (table Gram, lfe_gram.hip).
+// No hash table and no f64 atomics, whatever the number of clusters (config 4:
+// fe2 x fe3 has 48.8M clusters for 50M rows).
+//
+// Multi-rank: clusters span row shards.  The key space is global (codes are
+// global), so for span < 2^31 the S table is indexed by key directly, summed
+// with f64 atomics and all-reduced; larger spans across ranks are rejected.
+#include "lfe_internal.h"
+
+#include <algorithm>
+
+namespace lfe {
+
+static int fail(int code, const char* msg) {
+  set_error(msg);
+  return code;
+}
+
+constexpr int kRsThreads = 256;
+constexpr int kRsWaves = kRsThreads / 64;
+constexpr int kRsPer = 16;                       // items per thread
+constexpr int kRsItems = kRsThreads * kRsPer;    // items per block
+constexpr int kRsBits = 8;
+constexpr int kRsBins = 1 << kRsBits;
+static_assert(kRsBins == kRsThreads, "one digit per thread in the wave prefix");
+
+// cluster code of every layout row (input-order array gathered through orig)
+__global__ void k_cl_layout(const int32_t* __restrict__ cl, const int32_t* __restrict__ orig, int64_t n,
+                            int32_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = cl[orig ? orig[i] : i];
+}
+
+struct KeyArgs {
+  int m;
+  const int32_t* code[kMaxCl];  // layout order
+  uint64_t mult[kMaxCl];
+  const int32_t* keep;          // layout codes of P (-1: dropped), or null
+  int64_t n;
+  uint64_t drop;                // key of dropped rows (= span)
+  uint64_t* keys;
+  int32_t* rows;
+};
+
+__global__ void k_cl_keys(KeyArgs a) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t key = 0;
+    for (int j = 0; j < a.m; ++j) key += (uint64_t)(uint32_t)a.code[j][i] * a.mult[j];
+    a.keys[i] = (a.keep && a.keep[i] < 0) ? a.drop : key;
+    a.rows[i] = (int32_t)i;
+  }
+}
+
+// digit counts of block b: counts[d * nblk + b]
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
+                                                        int nblk, int32_t* __restrict__ counts) {
+  __shared__ int32_t h[kRsBins];
+  const int tid = threadIdx.x;
+  h[tid] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRsItems;
+#pragma unroll 4
+  for (int s = 0; s < kRsPer; ++s) {
+    const int64_t i = base + s * kRsThreads + tid;
+    if (i < n) atomicAdd(&h[(int)((keys[i] >> shift) & (kRsBins - 1))], 1);
+  }
+  __syncthreads();
+  counts[(int64_t)tid * nblk + blockIdx.x] = h[tid];
+}
+
+// Stable scatter.  Wave w of block b owns items [b*4096 + w*1024, +1024) in 16
+// steps of 64; within a step, lanes with equal digits are matched by 8 ballots
+// and ranked by lane; per-wave running counts in LDS carry the rank across
+// steps; a prefix over waves and the scanned global counts give the position.
+__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint64_t* __restrict__ kin,
+                                                           const int32_t* __restrict__ vin,
+                                                           uint64_t* __restrict__ kout, int32_t* __restrict__ vout,
+                                                           int64_t n, int shift, int nblk,
+                                                           const int32_t* __restrict__ scanned) {
+  __shared__ int32_t cnt[kRsWaves][kRsBins];
+  __shared__ int32_t base_d[kRsBins];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int j = tid; j < kRsWaves * kRsBins; j += kRsThreads) (&cnt[0][0])[j] = 0;
+  base_d[tid] = scanned[(int64_t)tid * nblk + blockIdx.x];
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * kRsItems + (int64_t)w * (kRsItems / kRsWaves);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint64_t key[kRsPer];
+  int32_t val[kRsPer];
+  int rank[kRsPer];
+#pragma unroll
+  for (int s = 0; s < kRsPer; ++s) {
+    const int64_t i = b0 + s * 64 + lane;
+    const bool valid = i < n;
+    key[s] = valid ? kin[i] : 0ull;
+    val[s] = valid ? vin[i] : 0;
+  }
+#pragma unroll
+  for (int s = 0; s < kRsPer; ++s) {
+    const bool valid = b0 + s * 64 + lane < n;
+    const int d = (int)((key[s] >> shift) & (kRsBins - 1));
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kRsBits; ++b) {
+      const bool bit = (d >> b) & 1;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const int before = __popcll(m & lt);
+    rank[s] = cnt[w][d] + before;  // every lane reads before the leader below writes
+    if (valid && before == 0) cnt[w][d] += __popcll(m);
+  }
+  __syncthreads();
+  {
+    int run = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < kRsWaves; ++w2) {
+      const int t = cnt[w2][tid];
+      cnt[w2][tid] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < kRsPer; ++s) {
+    if (b0 + s * 64 + lane >= n) continue;
+    const int d = (int)((key[s] >> shift) & (kRsBins - 1));
+    const int64_t pos = (int64_t)base_d[d] + cnt[w][d] + rank[s];
+    kout[pos] = key[s];
+    vout[pos] = val[s];
+  }
+}
+
+__device__ __forceinline__ bool cl_head(const uint64_t* K, int64_t i, uint64_t drop) {
+  return K[i] != drop && (i == 0 || K[i] != K[i - 1]);
+}
+
+__global__ void k_cl_heads(const uint64_t* __restrict__ K, int64_t n, uint64_t drop, int32_t* __restrict__ flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    flag[i] = cl_head(K, i, drop) ? 1 : 0;
+}
+
+// seg_off[segment index] = first position; seg_off[G] = number of kept positions
+__global__ void k_cl_segoff(const uint64_t* __restrict__ K, const int32_t* __restrict__ scan, int64_t n,
+                            uint64_t drop, int32_t* __restrict__ seg_off) {
+  const int32_t G = scan[n];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (cl_head(K, i, drop)) seg_off[scan[i]] = (int32_t)i;
+    if (K[i] != drop && (i + 1 == n || K[i + 1] == drop)) seg_off[G] = (int32_t)(i + 1);
+  }
+}
+
+// Short segments (a few rows per cluster): one sorted position per lane, its
+// score row gathered into registers, a segmented inclusive scan across the
+// wave (segment ids are non-decreasing), and the last lane of each segment
+// stores S[h]; segments cut by a wave edge add their part atomically (S zeroed).
+template <int KM>
+__global__ __launch_bounds__(256) void k_seg_rows(const uint64_t* __restrict__ K, const int32_t* __restrict__ scan,
+                                                  const int32_t* __restrict__ R, int64_t nv, uint64_t drop,
+                                                  const double* __restrict__ U, int k, double* __restrict__ S) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t wb = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64; wb < nv; wb += nwaves * 64) {
+    const int64_t q = wb + lane;
+    const bool in = q < nv;
+    int32_t h = 0x7fffffff;
+    double v[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) v[j] = 0.0;
+    if (in) {
+      const bool head = q == 0 || K[q] != K[q - 1];
+      h = scan[q] + (head ? 0 : -1);
+      const double* u = U + (int64_t)R[q] * k;
+#pragma unroll
+      for (int j = 0; j < KM; ++j)
+        if (j < k) v[j] = u[j];
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t oh = __shfl_up(h, off, 64);
+      const bool add = lane >= off && oh == h;
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        const double o = __shfl_up(v[j], off, 64);
+        if (add) v[j] += o;
+      }
+    }
+    const int32_t nh = __shfl_down(h, 1, 64);
+    const int32_t h0 = __shfl(h, 0, 64);
+    const bool last = in && (lane == 63 || q + 1 == nv || nh != h);
+    if (!last) continue;
+    // complete inside this wave: starts after lane 0's segment, or lane 0 opens it
+    const bool starts_here = h != h0 || wb == 0 || K[wb] != K[wb - 1];
+    const bool ends_here = lane < 63 || q + 1 == nv || K[q + 1] != K[q];
+    double* dst = S + (int64_t)h * k;
+    if (starts_here && ends_here) {
+#pragma unroll
+      for (int j = 0; j < KM; ++j)
+        if (j < k) dst[j] = v[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < KM; ++j)
+        if (j < k) atomicAdd(&dst[j], v[j]);
+    }
+  }
+}
+
+// multi-rank dense form: S[key] += scores_i (span < 2^31)
+__global__ void k_cl_dense_scatter(const uint64_t* __restrict__ keys, int64_t n, uint64_t drop,
+                                   const double* __restrict__ U, int k, double* __restrict__ S,
+                                   int32_t* __restrict__ present) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    if (key == drop) continue;
+    present[key] = 1;
+    for (int j = 0; j < k; ++j) atomicAdd(&S[key * k + j], U[i * k + j]);
+  }
+}
+
+__global__ void k_count_nonzero(const int32_t* __restrict__ cnt, int32_t G, int32_t* __restrict__ out) {
+  int local = 0;
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) local += cnt[g] > 0;
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(out, local);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+
+static int bit_length(uint64_t v) {
+  int b = 0;
+  while (v) {
+    ++b;
+    v >>= 1;
+  }
+  return b;
+}
+
+// sort (keys, rows) [0, n) by the low `bits` bits; returns the buffer index (0/1) holding the result
+static int radix_sort(lfe_ctx* c, int64_t n, int bits, int* out_buf) {
+  auto& W = c->clw;
+  const int nblk = (int)((n + kRsItems - 1) / kRsItems);
+  LFE_TRY(ensure_i32(c, W.counts, W.counts_cap, (size_t)kRsBins * nblk));
+  int cur = 0;
+  for (int shift = 0; shift < bits; shift += kRsBits) {
+    {
+      ProfScope _ps(c, K_CLUSTER_SORT);
+      hipLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], n, shift, nblk,
+                         W.counts);
+    }
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(exclusive_scan(c, W.counts, (int64_t)kRsBins * nblk));
+    {
+      ProfScope _ps(c, K_CLUSTER_SORT);
+      hipLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], W.rows[cur],
+                         W.keys[1 - cur], W.rows[1 - cur], n, shift, nblk, W.counts);
+    }
+    LFE_HIP(hipGetLastError());
+    cur = 1 - cur;
+  }
+  *out_buf = cur;
+  return LFE_OK;
+}
+
+// meat and cluster count of one subset (mask over the loaded cluster columns)
+static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
+  const int k = c->p - 1;
+  const int64_t n = c->n;
+  auto& W = c->clw;
+  KeyArgs ka{};
+  uint64_t span = 1;
+  for (int j = 0; j < (int)c->cl.size(); ++j) {
+    if (!(mask >> j & 1)) continue;
+    const uint64_t g = (uint64_t)c->cl_levels[j];
+    if (span > ((1ull << 62) / g)) return fail(LFE_EINVAL, "cluster intersection span exceeds 2^62");
+    ka.code[ka.m] = W.lay[j];
+    ka.mult[ka.m] = span;  // key = c_0 + G_0 (c_1 + G_1 (...)): any injective mixed radix groups the same rows
+    ++ka.m;
+    span *= g;
+  }
+  ka.keep = c->L.P >= 0 ? c->L.code[c->L.P] : nullptr;
+  ka.n = n;
+  ka.drop = span;
+  ka.keys = W.keys[0];
+  ka.rows = W.rows[0];
+  if (n > 0) hipLaunchKernelGGL(k_cl_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka);
+  LFE_HIP(hipGetLastError());
+
+  if (c->world > 1) {
+    // global key space indexed directly, partial tables all-reduced
+    if (span >= (1ull << 31)) return fail(LFE_EINVAL, "multi-rank cluster intersection needs span < 2^31");
+    const int32_t C = (int32_t)span;
+    LFE_TRY(ensure_cluster_ws(c, (size_t)C * std::max(k, 1), (size_t)C + 4));
+    double* S = c->clS;
+    int32_t* present = c->clP;
+    int32_t* cntG = present + C;
+    LFE_HIP(hipMemsetAsync(S, 0, sizeof(double) * (size_t)C * std::max(k, 1), c->stream));
+    LFE_HIP(hipMemsetAsync(present, 0, sizeof(int32_t) * ((size_t)C + 4), c->stream));
+    if (n > 0 && k > 0) {
+      ProfScope _ps(c, K_CLUSTER_SCATTER);
+      hipLaunchKernelGGL(k_cl_dense_scatter, dim3(grid_for(n)), dim3(kBlock), 0, c->stream, W.keys[0], n, span,
+                         c->scores, k, S, present);
+    }
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(allreduce_sum_f64(c, S, (size_t)C * k));
+    LFE_TRY(allreduce_sum_i32(c, present, C));
+    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(C)), dim3(kBlock), 0, c->stream, present, C, cntG);
+    LFE_HIP(hipGetLastError());
+    int32_t hG = 0;
+    LFE_TRY(d2h_sync(c, &hG, cntG, sizeof(int32_t)));
+    *G_out = hG;
+    if (k > 0) {
+      const int world = c->world;  // S is replicated after the all-reduce: reduce its Gram locally
+      c->world = 1;
+      const int rc = launch_table_gram(c, S, C, k, meat);
+      c->world = world;
+      if (rc) return rc;
+    }
+    return LFE_OK;
+  }
+
+  int buf = 0;
+  if (n > 0) LFE_TRY(radix_sort(c, n, bit_length(span), &buf));
+  const uint64_t* K = W.keys[buf];
+  const int32_t* R = W.rows[buf];
+  int32_t G = 0;
+  LFE_HIP(hipMemsetAsync(W.flag + n, 0, sizeof(int32_t), c->stream));
+  LFE_HIP(hipMemsetAsync(W.seg_off, 0, sizeof(int32_t), c->stream));
+  if (n > 0) {
+    ProfScope _ps(c, K_CLUSTER_SORT);
+    hipLaunchKernelGGL(k_cl_heads, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, n, span, W.flag);
+  }
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(exclusive_scan(c, W.flag, n + 1));
+  if (n > 0) {
+    ProfScope _ps(c, K_CLUSTER_SORT);
+    hipLaunchKernelGGL(k_cl_segoff, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, W.flag, n, span,
+                       W.seg_off);
+  }
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(d2h_sync(c, &G, W.flag + n, sizeof(int32_t)));
+  *G_out = G;
+  if (k == 0) return LFE_OK;
+  LFE_TRY(ensure_cluster_ws(c, (size_t)std::max(G, 1) * k, 4));
+  // kept positions = n minus the dropped rows (sorted last): G clusters over them
+  int32_t nv = 0;
+  LFE_TRY(d2h_sync(c, &nv, W.seg_off + G, sizeof(int32_t)));
+  if (k <= 16 && G > 0 && (int64_t)nv < 8 * (int64_t)G) {
+    // short clusters (mean < 8 rows): row-per-lane segmented scan
+    LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)G * k, c->stream));
+    const int grid = grid_for(((int64_t)nv + 63) / 64 * 64, 256, 8192);
+    ProfScope _ps(c, K_CLUSTER_SCATTER);
+    if (k <= 4)
+      hipLaunchKernelGGL(k_seg_rows<4>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, span,
+                         c->scores, k, c->clS);
+    else if (k <= 8)
+      hipLaunchKernelGGL(k_seg_rows<8>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, span,
+                         c->scores, k, c->clS);
+    else if (k <= 12)
+      hipLaunchKernelGGL(k_seg_rows<12>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, span,
+                         c->scores, k, c->clS);
+    else
+      hipLaunchKernelGGL(k_seg_rows<16>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, span,
+                         c->scores, k, c->clS);
+  } else {
+    LFE_TRY(seg_gather_sum(c, W.seg_off, G, W.ufirst, n, R, c->scores, k, k, c->clS, K_CLUSTER_SCATTER));
+  }
+  LFE_HIP(hipGetLastError());
+  return launch_table_gram(c, c->clS, G, k, meat);
+}
+
+int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, double* meats, int64_t* G_out) {
+  const int k = c->p - 1;
+  const int64_t n = c->n;
+  const int m = (int)c->cl.size();
+  for (int s = 0; s < n_subsets; ++s)
+    if (masks[s] <= 0 || masks[s] >= (1 << m)) return fail(LFE_EINVAL, "subset mask must select loaded cluster columns");
+  auto& W = c->clw;
+  const size_t ld = (size_t)c->ld;
+  for (int b = 0; b < 2; ++b) {
+    LFE_TRY(ensure_u64(c, W.keys[b], W.keys_cap[b], ld));
+    LFE_TRY(ensure_i32(c, W.rows[b], W.rows_cap[b], ld));
+  }
+  LFE_TRY(ensure_i32(c, W.flag, W.flag_cap, ld + 1));
+  LFE_TRY(ensure_i32(c, W.seg_off, W.seg_off_cap, ld + 1));
+  LFE_TRY(ensure_i32(c, W.ufirst, W.ufirst_cap, (size_t)seg_units_needed(c->ld)));
+  if (!W.lay_valid) {
+    W.lay.resize(m, nullptr);
+    W.lay_cap.resize(m, 0);
+    for (int j = 0; j < m; ++j) {
+      LFE_TRY(ensure_i32(c, W.lay[j], W.lay_cap[j], ld));
+      if (n > 0)
+        hipLaunchKernelGGL(k_cl_layout, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, c->cl[j],
+                           c->L.orig, n, W.lay[j]);
+      LFE_HIP(hipGetLastError());
+    }
+    W.lay_valid = true;
+  }
+  for (int s = 0; s < n_subsets; ++s)
+    LFE_TRY(subset_meat(c, masks[s], meats + (size_t)s * k * k, G_out + s));
+  return LFE_OK;
+}
+
+void free_cluster_ws(lfe_ctx* c) {
+  auto& W = c->clw;
+  for (int b = 0; b < 2; ++b) {
+    dfree_any(W.keys[b]);
+    dfree_any(W.rows[b]);
+    W.keys_cap[b] = W.rows_cap[b] = 0;
+  }
+  dfree_any(W.counts);
+  dfree_any(W.flag);
+  dfree_any(W.seg_off);
+  dfree_any(W.ufirst);
+  W.counts_cap = W.flag_cap = W.seg_off_cap = W.ufirst_cap = 0;
+  for (auto& p : W.lay) dfree_any(p);
+  W.lay.clear();
+  W.lay_cap.clear();
+  W.lay_valid = false;
+}
+
+}  // namespace lfe

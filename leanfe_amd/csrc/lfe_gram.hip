@@ -35,7 +35,7 @@ struct GramArgs {
   int64_t ld;
   const double* w;
   const double* beta;   // GRAM_RESID: beta_full [p] = {intercept, b_1..b_{p-1}}
-  double* scores;       // GRAM_RESID: optional [p-1][ld] output x~ r (w)
+  double* scores;       // GRAM_RESID: optional row-major [ld][p-1] output x~ r (w)
   const double* table;  // GRAM_TABLE: row-major [rows][tcols]
   int64_t rows;         // GRAM_TABLE
   int tcols;
@@ -353,15 +353,18 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
 #pragma unroll
             for (int I = 0; I < NT; ++I) {
               if (!dat[I]) continue;
-              double* dst = a.scores + (int64_t)(xl[I] - 1) * a.ld + r;
+              // row-major [row][k]: the 16 column lanes of a row quad write one contiguous row
+              const int64_t ks = a.la.p - 1;
+              double* dst = a.scores + (int64_t)r * ks + (xl[I] - 1);
               const d4 v = d4{valid[u][0] ? xt[0][I] * sc[0] : 0.0, valid[u][1] ? xt[1][I] * sc[1] : 0.0,
                               valid[u][2] ? xt[2][I] * sc[2] : 0.0, valid[u][3] ? xt[3][I] * sc[3] : 0.0};
               if (full) {
-                st4(dst, v);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) dst[s * ks] = v[s];
               } else if (gi < g1) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
-                  if (valid[u][s]) dst[s] = v[s];
+                  if (valid[u][s]) dst[s * ks] = v[s];
               }
             }
           }
@@ -487,7 +490,7 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
           const int r = rb + u * 64 + lane;
 #pragma unroll
           for (int j = 0; j < KM; ++j)
-            if (j + 1 < p) a.scores[(int64_t)j * a.ld + r] = wv[j];
+            if (j + 1 < p) a.scores[(int64_t)r * (p - 1) + j] = wv[j];
         }
       }
     }
@@ -642,25 +645,6 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const double* __restric
     __syncthreads();
   }
   if (threadIdx.x == 0) out[e] = red[0];
-}
-
-// cluster scores on the layout: S[cl[orig(i)]] += scores_i
-__global__ void k_cluster_scatter(const int32_t* __restrict__ cl, const int32_t* __restrict__ orig,
-                                  const int32_t* __restrict__ codeP, const double* __restrict__ U, int64_t ld,
-                                  int64_t n, int k, double* __restrict__ S, int32_t* __restrict__ present) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (codeP && codeP[i] < 0) continue;
-    const int64_t cc = cl[orig ? orig[i] : i];
-    present[cc] = 1;
-    for (int j = 0; j < k; ++j) atomicAdd(&S[cc * k + j], U[(int64_t)j * ld + i]);
-  }
-}
-
-__global__ void k_count_nonzero(const int32_t* __restrict__ cnt, int32_t G, int32_t* __restrict__ out) {
-  int local = 0;
-  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) local += cnt[g] > 0;
-  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
-  if ((threadIdx.x & 63) == 0 && local) atomicAdd(out, local);
 }
 
 __global__ void k_validate(const int32_t* __restrict__ code, int64_t n, int32_t G, int32_t* __restrict__ flag) {
@@ -1036,46 +1020,14 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
   return LFE_OK;
 }
 
-int launch_cluster(lfe_ctx* c, double* meats, int64_t* G_out) {
-  const int k = c->p - 1;
-  const int32_t* codeP = c->L.P >= 0 ? c->L.code[c->L.P] : nullptr;
-  for (size_t j = 0; j < c->cl.size(); ++j) {
-    const int32_t C = c->cl_levels[j];
-    const size_t tab = (size_t)C * std::max(k, 1);
-    LFE_TRY(ensure_cluster_ws(c, tab, (size_t)C + 4));
-    double* S = c->clS;
-    int32_t* present = c->clP;
-    int32_t* cntG = present + C;
-    LFE_HIP(hipMemsetAsync(S, 0, sizeof(double) * tab, c->stream));
-    LFE_HIP(hipMemsetAsync(present, 0, sizeof(int32_t) * ((size_t)C + 4), c->stream));
-    if (c->n && k > 0) {
-      ProfScope _ps(c, K_CLUSTER_SCATTER);
-      hipLaunchKernelGGL(k_cluster_scatter, dim3(grid_for(c->n)), dim3(kBlock), 0, c->stream, c->cl[j], c->L.orig,
-                         codeP, c->scores, c->ld, c->n, k, S, present);
-    }
-    LFE_HIP(hipGetLastError());
-    LFE_TRY(allreduce_sum_f64(c, S, (size_t)C * k));
-    LFE_TRY(allreduce_sum_i32(c, present, C));
-    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(C)), dim3(kBlock), 0, c->stream, present, C, cntG);
-    LFE_HIP(hipGetLastError());
-    int32_t hG = 0;
-    LFE_TRY(d2h_sync(c, &hG, cntG, sizeof(int32_t)));
-    G_out[j] = hG;
-    if (k > 0) {
-      GramArgs a{};
-      a.table = S;
-      a.rows = C;
-      a.tcols = k;
-      // the S table is replicated on every rank after the all-reduce: its Gram
-      // is reduced locally only (no second all-reduce)
-      const int world = c->world;
-      c->world = 1;
-      const int rc = gram_dispatch<GRAM_TABLE>(c, a, k, 0, k, meats + j * (size_t)k * k, nullptr, 0);
-      c->world = world;
-      if (rc) return rc;
-    }
-  }
-  return LFE_OK;
+// meat = table' table of a row-major [rows][k] score table (summed over ranks
+// unless the caller sets world = 1 for a replicated table)
+int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat) {
+  GramArgs a{};
+  a.table = table;
+  a.rows = rows;
+  a.tcols = k;
+  return gram_dispatch<GRAM_TABLE>(c, a, k, 0, k, meat, nullptr, 0);
 }
 
 int launch_copy_demeaned(lfe_ctx* c, double* dev_out) {

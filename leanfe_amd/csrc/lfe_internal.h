@@ -15,6 +15,7 @@
 namespace lfe {
 
 constexpr int kMaxFE = 8;        // FE dimensions supported per regression
+constexpr int kMaxCl = 16;       // cluster columns per CGM subset
 constexpr int kMaxCols = 63;     // p = 1 + k (+ instruments) <= 63 -> Gram width <= 64
 constexpr int kBlock = 256;      // threads per workgroup for simple streaming kernels
 constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
@@ -73,7 +74,7 @@ struct FeState {
 enum KernelId {
   K_PART_HIST = 0, K_SCAN, K_PART_SCATTER, K_COUNT, K_MARK, K_GROUP_SUMS, K_CROSS, K_CHECK, K_FINALIZE,
   K_CHECK_MAX, K_GRAM_DESIGN, K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_MISC, K_SYNTH,
-  K_TP, K_TQ, K_SEG_BUILD, K_NUM_KERNELS
+  K_TP, K_TQ, K_SEG_BUILD, K_CLUSTER_SORT, K_NUM_KERNELS
 };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 
@@ -85,6 +86,25 @@ struct Prof {
   int64_t count[K_NUM_KERNELS] = {0};
   hipEvent_t open_ev = nullptr;
   int open_id = -1;
+};
+
+// cluster workspace (lfe_cluster.hip)
+struct ClusterWS {
+  uint64_t* keys[2] = {nullptr, nullptr};  // radix sort ping-pong
+  size_t keys_cap[2] = {0, 0};
+  int32_t* rows[2] = {nullptr, nullptr};
+  size_t rows_cap[2] = {0, 0};
+  int32_t* counts = nullptr;    // [bins][blocks] digit counts
+  size_t counts_cap = 0;
+  int32_t* flag = nullptr;      // [ld + 1] segment heads -> indices
+  size_t flag_cap = 0;
+  int32_t* seg_off = nullptr;   // [ld + 1]
+  size_t seg_off_cap = 0;
+  int32_t* ufirst = nullptr;
+  size_t ufirst_cap = 0;
+  std::vector<int32_t*> lay;    // loaded cluster columns in layout order
+  std::vector<size_t> lay_cap;
+  bool lay_valid = false;
 };
 
 struct Timings {
@@ -156,6 +176,7 @@ struct lfe_ctx {
   // clusters (input row order)
   std::vector<int32_t*> cl;
   std::vector<int32_t> cl_levels;
+  lfe::ClusterWS clw;
   // pinned host staging (small transfers avoid the runtime's pageable path)
   char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
   hipEvent_t hpin_ev = nullptr;    // last H2D from the staging region
@@ -215,7 +236,14 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
 int launch_gram(lfe_ctx* c, double* host_gram);
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores);
 int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores);
-int launch_cluster(lfe_ctx* c, double* meats, int64_t* G_out);
+int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
+// --- clusters (lfe_cluster.hip) ---
+int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, double* meats, int64_t* G_out);
+void free_cluster_ws(lfe_ctx* c);
+// --- segmented gather-sums (lfe_seg.hip) ---
+int seg_gather_sum(lfe_ctx* c, const int32_t* seg_off, int32_t G, int32_t* ufirst, int64_t n_pos,
+                   const int32_t* rows, const double* table, int stride, int cols, double* out, int kid);
+int seg_units_needed(int64_t n_pos);
 int launch_copy_demeaned(lfe_ctx* c, double* dev_out);
 int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* flag, hipStream_t s);
 
@@ -232,6 +260,12 @@ int ensure_items(lfe_ctx* c, size_t n_items);
 int ensure_i32(lfe_ctx* c, int32_t*& p, size_t& cap, size_t elems);
 int ensure_f64(lfe_ctx* c, double*& p, size_t& cap, size_t elems);
 int ensure_u16(lfe_ctx* c, uint16_t*& p, size_t& cap, size_t elems);
+int ensure_u64(lfe_ctx* c, uint64_t*& p, size_t& cap, size_t elems);
+template <typename T>
+inline void dfree_any(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
 // device -> host copy of a small result through pinned staging, synchronizing the stream
 int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes);

@@ -472,6 +472,7 @@ int prepare_layout(lfe_ctx* c) {
   const int64_t n = c->n;
   c->sums_ready = false;
   c->seg_ready = false;
+  c->clw.lay_valid = false;  // cluster columns follow the new layout
   // primary FE: most levels (ties -> first)
   L.P = -1;
   for (int f = 0; f < c->F; ++f)

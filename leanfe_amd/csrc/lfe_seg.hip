@@ -173,7 +173,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
           for (int I = 0; I < NT; ++I) val[U][s][I] = 0.0;
 #pragma unroll
           for (int j = 0; j < NO; ++j) {
-            const double* al = a.alpha[j] + (uint32_t)cd[U][j][s] * (uint32_t)p;
+            const double* al = a.alpha[j] + (uint64_t)(uint32_t)cd[U][j][s] * (uint32_t)p;
 #pragma unroll
             for (int I = 0; I < NT; ++I) val[U][s][I] += al[cl[I]];
           }
@@ -308,15 +308,16 @@ int seg_build(lfe_ctx* c) {
     LFE_TRY(ensure_i32(c, fe.oc, fe.oc_cap, (size_t)(c->F - 1) * c->ld));
     LFE_TRY(ensure_i32(c, fe.ufirst, fe.ufirst_cap, (size_t)nu));
     if (weighted) LFE_TRY(ensure_f64(c, fe.ws, fe.ws_cap, (size_t)c->ld));
-    ProfScope _ps(c, K_SEG_BUILD);
     LFE_HIP(hipMemsetAsync(fe.seg_off + fe.G, 0, sizeof(int32_t), c->stream));
     if (c->world == 1) {
       LFE_HIP(hipMemcpyAsync(fe.seg_off, fe.cnt, sizeof(int32_t) * fe.G, hipMemcpyDeviceToDevice, c->stream));
     } else {
       LFE_HIP(hipMemsetAsync(fe.seg_off, 0, sizeof(int32_t) * fe.G, c->stream));
-      if (n > 0)
+      if (n > 0) {
+        ProfScope _ps(c, K_SEG_BUILD);
         hipLaunchKernelGGL(k_seg_hist, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, a.keep, L.code[f], n,
                            fe.seg_off);
+      }
       LFE_HIP(hipGetLastError());
     }
     LFE_TRY(exclusive_scan(c, fe.seg_off, (int64_t)fe.G + 1));
@@ -374,6 +375,38 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
   LFE_HIP(hipGetLastError());
   return allreduce_sum_f64(c, out, (size_t)fe.G * pc);
 }
+
+// out[h][0, cols) = sum over positions q in [seg_off[h], seg_off[h + 1]) of
+// table[rows[q]][0, cols) (row stride `stride`); positions [0, seg_off[G]), at
+// most n_pos.  `ufirst` holds ceil(n_pos / kSegUnit) ints.  The cluster score
+// sums (lfe_cluster.hip) are this with rows = the cluster-sorted row indices.
+int seg_gather_sum(lfe_ctx* c, const int32_t* seg_off, int32_t G, int32_t* ufirst, int64_t n_pos,
+                   const int32_t* rows, const double* table, int stride, int cols, double* out, int kid) {
+  LFE_HIP(hipMemsetAsync(out, 0, sizeof(double) * (size_t)G * cols, c->stream));
+  const int n_units = (int)((n_pos + kSegUnit - 1) / kSegUnit);
+  if (G == 0 || n_units == 0 || cols < 1) return LFE_OK;
+  hipLaunchKernelGGL(k_seg_units, dim3(grid_for(G)), dim3(kBlock), 0, c->stream, seg_off, G, ufirst);
+  SegCrossArgs a{};
+  a.seg_off = seg_off;
+  a.ufirst = ufirst;
+  a.n_units = n_units;
+  a.oc[0] = rows;
+  a.alpha[0] = table;
+  a.p = stride;
+  a.pc = cols;
+  a.G = G;
+  a.T = out;
+  CrossFn fn = cross_fn((cols + 15) / 16, 1, false);
+  const int grid = (n_units + kSegThreads / 64 - 1) / (kSegThreads / 64);
+  {
+    ProfScope _ps(c, kid);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kSegThreads), 0, c->stream, a);
+  }
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+int seg_units_needed(int64_t n_pos) { return (int)std::max<int64_t>((n_pos + kSegUnit - 1) / kSegUnit, 1); }
 
 static int seg_finalize(lfe_ctx* c, int f) {
   auto& fe = c->fe[f];

@@ -45,11 +45,34 @@ def attach(engine, group=None) -> None:
     rank = dist.get_rank(group)
     if world == 1:
         engine.set_comm(None, 0, 1)
+        engine.dist_group = None
         return
     obj = [type(engine).unique_id() if rank == 0 else None]
     src = dist.get_global_rank(group, 0) if group is not None else 0
     dist.broadcast_object_list(obj, src=src, group=group)
     engine.set_comm(obj[0], rank, world)
+    engine.dist_group = (group,)
+
+
+def is_sharded(engine) -> bool:
+    """True when ``engine`` was joined to a multi-rank group by ``attach``."""
+    return getattr(engine, "dist_group", None) is not None
+
+
+def agree_levels(engine, levels: list[int]) -> list[int]:
+    """Level counts every rank uses: the max over the ranks of ``engine``'s group.
+
+    Codes are global, but a shard may not contain a group's largest code; the
+    engine's group tables (and their all-reduces) must have the same size on
+    every rank."""
+    if not is_sharded(engine) or not levels:
+        return list(levels)
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([int(g) for g in levels], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=engine.dist_group[0])
+    return [int(g) for g in t.tolist()]
 
 
 class HostGroup:

@@ -59,15 +59,28 @@ def _polars_to_numpy(s) -> np.ndarray:
     return s.to_numpy()
 
 
-def factorize(values) -> tuple[np.ndarray, int]:
+def factorize(values, global_codes: bool = False) -> tuple[np.ndarray, int]:
     """Dense int32 group codes and the number of code values.
 
     Non-negative integer columns whose maximum is below max(4n, 2^20) are used
     as codes directly (O(n); unused code values are empty groups, which every
     kernel ignores).  Anything else (strings, floats, sparse ids) goes through
-    a sorted unique.  Only group membership matters for the estimator."""
+    a sorted unique.  Only group membership matters for the estimator.
+
+    ``global_codes`` (row shards of one fit): the values must already be global
+    non-negative integer codes and are used as they are, since a per-shard
+    unique would number the groups differently on every rank."""
     v = np.asarray(values)
     n = v.size
+    if global_codes:
+        if n == 0:
+            return np.zeros(0, dtype=np.int32), 1
+        if not (np.issubdtype(v.dtype, np.integer) or v.dtype == np.bool_):
+            raise ValueError("sharded fits need global non-negative integer FE / cluster codes")
+        vmin, vmax = int(v.min()), int(v.max())
+        if vmin < 0 or vmax >= 2 ** 31 - 1:
+            raise ValueError("sharded fits need global integer codes in [0, 2^31 - 1)")
+        return v.astype(np.int32, copy=False), vmax + 1
     if n == 0:
         return np.zeros(0, dtype=np.int32), 1
     if np.issubdtype(v.dtype, np.integer) or v.dtype == np.bool_:

@@ -14,7 +14,7 @@ import time
 
 import numpy as np
 
-from . import frame, inference
+from . import dist, frame, inference
 from ._lib import Engine
 from .formula import parse_formula
 from .result import LeanFEResult
@@ -77,17 +77,19 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     if factor_vars:
         x_cols = x_cols + frame.expand_factors(cols, factor_vars)
 
+    own_engine = engine is None
+    sharded = engine is not None and dist.is_sharded(engine)
     codes, levels = [], []
     for fe in fe_cols:
-        c, g = frame.factorize(cols[fe])
+        c, g = frame.factorize(cols[fe], global_codes=sharded)
         codes.append(c)
         levels.append(g)
     Y = np.asarray(cols[y_col], dtype=np.float64)
     Xc = [np.asarray(cols[c], dtype=np.float64) for c in x_cols]
     w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
 
-    own_engine = engine is None
     eng = engine if engine is not None else Engine(_default_device() if device is None else device)
+    levels = dist.agree_levels(eng, levels)
     try:
         t0 = time.perf_counter()
         eng.load([Y] + Xc, codes, levels, w)
@@ -164,22 +166,19 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         else:
             cl_codes, cl_levels = [], []
             for c in cluster_cols:
-                cc, gg = frame.factorize(cols[c])
+                cc, gg = frame.factorize(cols[c], global_codes=sharded)
                 cl_codes.append(cc)
                 cl_levels.append(gg)
+            cl_levels = dist.agree_levels(eng, cl_levels)
             if len(cluster_cols) == 1:
                 eng.load_clusters(cl_codes, cl_levels)
                 meats, Gs = eng.cluster_meat()
                 se, n_clusters = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, ssc)
             else:
+                # intersections are formed and grouped on the device (std_errors.py:399-408)
                 subsets = inference.cluster_subsets(len(cluster_cols))
-                arrs, lv = [], []
-                for s in subsets:
-                    a, g = frame.intersect([cl_codes[j] for j in s], [cl_levels[j] for j in s])
-                    arrs.append(a)
-                    lv.append(g)
-                eng.load_clusters(arrs, lv)
-                meats, Gs = eng.cluster_meat()
+                eng.load_clusters(cl_codes, cl_levels)
+                meats, Gs = eng.cluster_meat_subsets(subsets)
                 se, n_clusters = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets,
                                                                n_obs, df_resid, ssc)
         tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0

@@ -121,6 +121,32 @@ def test_hostgroup_and_attach_gloo():
 # the engine's data-parallel schedule, restated on two shards
 # ---------------------------------------------------------------------------
 
+def _levels(rank):
+    from leanfe_amd import frame
+    from leanfe_amd.dist import agree_levels, is_sharded
+
+    eng = _FakeEngine()
+    attach(eng)
+    # global codes of one FE: this shard happens not to hold the largest code
+    shard = np.array([0, 3, 3, 1] if rank == 0 else [2, 7, 5], dtype=np.int64)
+    codes, g = frame.factorize(shard, global_codes=True)
+    try:
+        frame.factorize(np.array(["a", "b"]), global_codes=True)
+        strings_rejected = False
+    except ValueError:
+        strings_rejected = True
+    return dict(sharded=is_sharded(eng), local=g, agreed=agree_levels(eng, [g, 10 + rank]),
+                same_codes=bool(np.array_equal(codes, shard)), strings_rejected=strings_rejected)
+
+
+def test_sharded_levels_agree_gloo():
+    """Every rank sizes its group tables by the max code over all shards (dist.agree_levels)."""
+    out = _run(_levels)
+    assert out[0]["local"] == 4 and out[1]["local"] == 8
+    assert out[0]["agreed"] == out[1]["agreed"] == [8, 11]
+    assert all(out[r]["sharded"] and out[r]["same_codes"] and out[r]["strings_rejected"] for r in range(WORLD))
+
+
 def _allreduce(a: np.ndarray) -> np.ndarray:
     t = torch.from_numpy(np.ascontiguousarray(a).copy())
     dist.all_reduce(t)

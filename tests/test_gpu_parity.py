@@ -81,6 +81,27 @@ def test_random_panels_vs_oracle(seed, n, L, k, vcov):
                  o["n_clusters"], xs)
 
 
+@pytest.mark.parametrize("weighted", [False, True])
+def test_three_way_cgm_on_device(weighted):
+    """Three cluster columns: 7 CGM subsets whose intersections are keyed and grouped on
+    the device (the fe1 x fe2 x fe3 subset is almost all singleton clusters), with
+    singleton FE rows dropped (fe1 has ~5 rows per level) and optional weights."""
+    n, L, k = 150_000, [30_000, 200, 13], 3
+    data = synth.panel(n, k, L, seed=21)
+    if weighted:
+        data["w"] = 0.5 + np.random.default_rng(3).random(n)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = ["fe1", "fe2", "fe3"]
+    w = "w" if weighted else None
+    o = altproj.fit(data, "y", xs, fes, vcov="cluster", cluster_cols=fes, weights=w)
+    from leanfe_amd import leanfe_hip
+    r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov="cluster", cluster_cols=fes,
+                   weights=w, quiet=True)
+    assert o["n_obs"] < n  # singletons were dropped
+    _assert_same(r, o["beta"], o["se"], o["n_obs"], o["iterations"], o["df_resid"], o["fe_dims"],
+                 o["n_clusters"], xs)
+
+
 def test_ols_no_fe_and_single_fe_demean():
     data = synth.panel(20000, 2, [400], seed=4)
     from leanfe_amd import leanfe_hip

@@ -19,7 +19,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from leanfe_amd import frame, inference, synth  # noqa: E402
+from leanfe_amd import inference, synth  # noqa: E402
 from leanfe_amd._lib import Engine  # noqa: E402
 from oracle.altproj_c import fit_c  # noqa: E402
 
@@ -41,8 +41,8 @@ def solve(eng, vcov, cl_levels=None):
     elif v == "iid":
         out["se"] = inference.se_iid(XtX_inv[1:, 1:], stats[0], df)
     else:
-        meats, Gs = eng.cluster_meat()
         subsets = inference.cluster_subsets(len(cl_levels))
+        meats, Gs = eng.cluster_meat_subsets(subsets)  # intersections formed on the device
         out["se"], _ = inference.se_cluster_multiway(XtX_inv[1:, 1:], list(meats), [int(g) for g in Gs], subsets,
                                                      n_obs, df, True)
         out["G"] = [int(g) for g in Gs]
@@ -56,15 +56,9 @@ def run(cfg, n, k, levels, vcov, cluster_fes=None, threads=16):
     cl_levels = None
     if cluster_fes:
         cols, codes = eng.copy_inputs()
-        # CGM subsets: each cluster column, then intersections (std_errors.py:399-408)
-        subsets = inference.cluster_subsets(len(cluster_fes))
-        cc, cl_levels_all = [], []
-        for s in subsets:
-            key, G = frame.intersect([codes[cluster_fes[j]] for j in s], [levels[cluster_fes[j]] for j in s])
-            cc.append(np.ascontiguousarray(key, dtype=np.int32))
-            cl_levels_all.append(int(G))
-        eng.load_clusters(cc, cl_levels_all)
+        # first-order cluster columns; the CGM intersections are formed on the device
         cl_levels = [levels[f] for f in cluster_fes]
+        eng.load_clusters([np.ascontiguousarray(codes[f]) for f in cluster_fes], cl_levels)
     solve(eng, vcov, cl_levels)  # warm-up
     eng.profile(True)
     r = solve(eng, vcov, cl_levels)
