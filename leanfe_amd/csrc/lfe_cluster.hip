@@ -230,11 +230,18 @@ __global__ void k_cl_dense_scatter(const uint64_t* __restrict__ keys, int64_t n,
   }
 }
 
-__global__ void k_count_nonzero(const int32_t* __restrict__ cnt, int32_t G, int32_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_count_nonzero(const int32_t* __restrict__ cnt, int32_t G,
+                                                       int32_t* __restrict__ out) {
+  __shared__ int32_t ws[4];
   int local = 0;
   for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) local += cnt[g] > 0;
   for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
-  if ((threadIdx.x & 63) == 0 && local) atomicAdd(out, local);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = ws[0] + ws[1] + ws[2] + ws[3];
+    if (t) atomicAdd(out, t);  // one add per block
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -318,7 +325,7 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
     LFE_HIP(hipGetLastError());
     LFE_TRY(allreduce_sum_f64(c, S, (size_t)C * k));
     LFE_TRY(allreduce_sum_i32(c, present, C));
-    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(C)), dim3(kBlock), 0, c->stream, present, C, cntG);
+    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(C, 256, 1024)), dim3(256), 0, c->stream, present, C, cntG);
     LFE_HIP(hipGetLastError());
     int32_t hG = 0;
     LFE_TRY(d2h_sync(c, &hG, cntG, sizeof(int32_t)));

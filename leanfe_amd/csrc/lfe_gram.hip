@@ -863,38 +863,65 @@ static int design_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
 // beta_full of X = [1, x] from the reduced design tile (column 0 intercept, 1 y, 2.. x):
 // Cholesky of X'X and two triangular solves, one thread (m <= 12).  ok = 0 when X'X is
 // not positive definite (the host then solves as polars_impl.py:217-220 does).
+// beta_full from the Gram tile by Cholesky (p <= 12).  Fixed loop bounds with
+// guards unroll completely, so L stays in registers (a runtime-bounded version
+// indexed a scratch array and took ~70 us).
 __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __restrict__ beta,
                              double* __restrict__ beta_copy, double* __restrict__ ok) {
+  constexpr int M = 12;
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int m = p;  // intercept + k regressors
-  double L[12][12], b[12], y[12];
+  double L[M][M], b[M], y[M];
   auto idx = [](int i) { return i == 0 ? 0 : i + 1; };
-  for (int i = 0; i < m; ++i) b[i] = tile[idx(i) * 16 + 1];
-  for (int j = 0; j < m; ++j) {
-    double d = tile[idx(j) * 16 + idx(j)];
-    for (int t = 0; t < j; ++t) d -= L[j][t] * L[j][t];
-    if (!(d > 0.0)) {
-      *ok = 0.0;
-      return;
-    }
-    L[j][j] = sqrt(d);
-    for (int i = j + 1; i < m; ++i) {
-      double v = tile[idx(i) * 16 + idx(j)];
-      for (int t = 0; t < j; ++t) v -= L[i][t] * L[j][t];
-      L[i][j] = v / L[j][j];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    b[i] = i < m ? tile[idx(i) * 16 + 1] : 0.0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) L[i][j] = (i < m && j <= i) ? tile[idx(i) * 16 + idx(j)] : 0.0;
+  }
+  bool pd = true;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    if (j < m) {
+      double d = L[j][j];
+#pragma unroll
+      for (int t = 0; t < j; ++t) d -= L[j][t] * L[j][t];
+      pd = pd && d > 0.0;
+      const double ljj = sqrt(d > 0.0 ? d : 1.0);
+      L[j][j] = ljj;
+#pragma unroll
+      for (int i = j + 1; i < M; ++i) {
+        double v = L[i][j];
+#pragma unroll
+        for (int t = 0; t < j; ++t) v -= L[i][t] * L[j][t];
+        L[i][j] = v / ljj;
+      }
     }
   }
-  for (int i = 0; i < m; ++i) {
+  if (!pd) {
+    *ok = 0.0;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
     double v = b[i];
+#pragma unroll
     for (int t = 0; t < i; ++t) v -= L[i][t] * y[t];
-    y[i] = v / L[i][i];
+    y[i] = i < m ? v / L[i][i] : 0.0;
   }
-  for (int i = m - 1; i >= 0; --i) {
-    double v = y[i];
-    for (int t = i + 1; t < m; ++t) v -= L[t][i] * b[t];
-    b[i] = v / L[i][i];
+#pragma unroll
+  for (int i = M - 1; i >= 0; --i) {
+    if (i < m) {
+      double v = y[i];
+#pragma unroll
+      for (int t = i + 1; t < M; ++t)
+        if (t < m) v -= L[t][i] * b[t];
+      b[i] = v / L[i][i];
+    }
   }
-  for (int i = 0; i < m; ++i) beta[i] = beta_copy[i] = b[i];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+    if (i < m) beta[i] = beta_copy[i] = b[i];
   *ok = 1.0;
 }
 

@@ -89,7 +89,7 @@ constexpr int kLsPer = 16;
 constexpr int kLsRows = kLsThreads * kLsPer;
 
 static size_t ls_scatter_lds(int K, int ncur) {
-  return sizeof(int32_t) * ((size_t)ncur * K + 3 * (size_t)K + 2 * (size_t)kLsRows);
+  return sizeof(int32_t) * ((size_t)ncur * K + 3 * (size_t)K + (size_t)kLsRows);
 }
 
 // NCUR: cursor sets (kLsWaves: one per wave, stable; 1: shared, unstable)
@@ -106,8 +106,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
   int32_t* run = cur + NCUR * K;  // [K] next free slot of each key
   int32_t* tot = run + K;             // [K]
   int32_t* delta = tot + K;           // [K]
-  int32_t* stage = delta + K;         // [kLsRows]
-  int32_t* sb = stage + kLsRows;      // [kLsRows]
+  int32_t* stage = delta + K;         // [kLsRows] slot keys, then slot values
   __shared__ int32_t wsum[kLsWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int item = xitems[blockIdx.x];  // XCD-grouped order (build_items)
@@ -179,16 +178,30 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
       for (int w2 = 0; w2 < NCUR; ++w2) cur[w2 * K + j] += boff;
     }
     __syncthreads();
+    int32_t pos[kLsPer];
 #pragma unroll
     for (int k = 0; k < kLsPer; ++k)
       if (key[k] >= 0) {
-        const int32_t pos = atomicAdd(&cur[(NCUR > 1 ? wave : 0) * K + key[k]], 1);
-        stage[pos] = val[k];
-        sb[pos] = key[k];
+        pos[k] = atomicAdd(&cur[(NCUR > 1 ? wave : 0) * K + key[k]], 1);
+        stage[pos[k]] = key[k];
       }
     __syncthreads();
+    // each thread keeps the destinations of the slots it writes out (j = tid + k * threads)
     const int32_t nk = cur[(NCUR - 1) * K + (K - 1)];  // kept rows of this sub-chunk
-    for (int j = tid; j < nk; j += kLsThreads) out[delta[sb[j]] + j] = (VT)stage[j];
+    int32_t dd[kLsPer];
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k) {
+      const int j = tid + k * kLsThreads;
+      dd[k] = j < nk ? delta[stage[j]] + j : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k)
+      if (key[k] >= 0) stage[pos[k]] = val[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k)
+      if (dd[k] >= 0) out[dd[k]] = (VT)stage[tid + k * kLsThreads];
     __syncthreads();
     for (int j = tid; j < K; j += kLsThreads) run[j] = delta[j] + cur[(NCUR - 1) * K + j];
   }

@@ -164,8 +164,6 @@ int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) {
 // wave timing), then moves every column through an LDS stage in bucket order,
 // so consecutive threads write consecutive addresses of one bucket run
 // (~chunk/nb rows per run) instead of 8-byte scatters.
-constexpr int kPartThreads = 512;
-constexpr int kPartWaves = kPartThreads / 64;
 
 struct ScatterArgs {
   int p, F, P, s, nb, nchunks;
@@ -189,13 +187,14 @@ __device__ __forceinline__ int xcd_chunk(int i, int nw) {
   return x * per + r;                      // may be >= nw: the caller's r0 >= n then
 }
 
-template <int PER>
-__global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
+template <int PER, int NTH>
+__global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
+  constexpr int kPartThreads = NTH;
+  constexpr int kPartWaves = NTH / 64;
   constexpr int R = kPartThreads * PER;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* stage = smem;                                        // [R] (doubles or int32)
-  int32_t* sb = reinterpret_cast<int32_t*>(stage + R);         // [R] bucket of sorted slot
-  int32_t* cur = sb + R;                                       // [waves][nb] cursors
+  int32_t* cur = reinterpret_cast<int32_t*>(stage + R);        // [waves][nb] cursors
   int32_t* delta = cur + kPartWaves * a.nb;                    // [nb]
   int32_t* tot = delta + a.nb;                                 // [nb + 1]
   __shared__ int32_t wsum[16];
@@ -260,6 +259,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
     for (int w2 = 0; w2 < kPartWaves; ++w2) cur[w2 * a.nb + b] += boff;
   }
   __syncthreads();
+  // slot -> bucket through the (not yet used) stage, then every thread keeps the
+  // global destination of the slots it writes out (j = tid + k * NTH) in registers
+  int32_t* sb = reinterpret_cast<int32_t*>(stage);
   int32_t pos[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -271,6 +273,13 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
   }
   __syncthreads();
   const int len = (int)(r1 - r0);
+  int32_t dd[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int j = tid + k * kPartThreads;
+    dd[k] = j < len ? delta[sb[j]] + j : -1;
+  }
+  __syncthreads();
   // ---- move columns through the stage: gather in row order, store in bucket order ----
   const int ncol = a.p + (a.w ? 1 : 0);
   double v[PER];
@@ -290,7 +299,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
       if (pos[k] >= 0) stage[pos[k]] = v[k];
     if (a.pipe && c + 1 < ncol) load_col(c + 1);  // next column in flight during the write-out
     __syncthreads();
-    for (int j = tid; j < len; j += kPartThreads) dst[delta[sb[j]] + j] = stage[j];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (dd[k] >= 0) dst[dd[k]] = stage[tid + k * kPartThreads];
     __syncthreads();
     if (!a.pipe && c + 1 < ncol) load_col(c + 1);
   }
@@ -303,7 +314,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(ScatterArgs a) {
       if (pos[k] >= 0) istage[pos[k]] = c < a.F ? a.code[c][i] : (int32_t)i;
     }
     __syncthreads();
-    for (int j = tid; j < len; j += kPartThreads) dst[delta[sb[j]] + j] = istage[j];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (dd[k] >= 0) dst[dd[k]] = istage[tid + k * kPartThreads];
     __syncthreads();
   }
 }
@@ -500,12 +513,32 @@ int prepare_layout(lfe_ctx* c) {
   if (L.permuted) {
     // ---- partition by bucket of P ----
     const int nb = L.nb;
-    // rows per thread of the staged scatter.  Measured at 50M rows x 391 buckets: one
-    // 8192-row chunk per workgroup with consecutive chunks in flight together is the
-    // fastest form (4096-row chunks, several chunks per workgroup, a software-pipelined
-    // column loop and register scatter without the LDS stage were all 20-60 % slower)
-    const int per = nb <= 512 ? 16 : 8;
-    const int64_t cw = (int64_t)kPartThreads * per;
+    // Chunk geometry, measured at 50M rows x 196 buckets (s = 9): 16384-row chunks on
+    // 1024-thread workgroups (16 rows per thread), one workgroup per CU, 2.06 ms; 8192-row
+    // chunks on 512 threads 2.28 ms.  Earlier: 4096-row chunks, several chunks per
+    // workgroup and register scatter without the LDS stage were all slower.
+    static const int nth_env = [] {
+      const char* e = getenv("LFE_PART_T");  // tuning: 512 or 1024 threads per chunk
+      return e && atoi(e) == 512 ? 512 : 1024;
+    }();
+    // one 16-wave workgroup per CU: with two per CU (32 waves) twice as many chunks write into
+    // every bucket region at once and the scatter ran 13 % slower (measured); pad the LDS request
+    static const size_t lds_min = [] {
+      const char* e = getenv("LFE_PART_LDS_MIN");  // tuning: LDS floor in bytes
+      return e ? (size_t)atol(e) : (size_t)(82 * 1024);
+    }();
+    static const int64_t cw_env = [] {
+      const char* e = getenv("LFE_PART_CW");  // tuning: rows per chunk (8192 or 16384)
+      return e ? (int64_t)atol(e) : (int64_t)16384;  // 16K: ~84-row runs per bucket at s = 9
+    }();
+    int64_t cw = nb <= 512 ? cw_env : 4096;
+    auto part_lds = [&](int nth) {
+      return sizeof(double) * cw + sizeof(int32_t) * ((size_t)(nth / 64) * nb + 2 * (size_t)nb + 1);
+    };
+    // 16 waves per chunk when their per-wave bucket cursors fit (nb <= ~1500)
+    const int nth = nth_env == 1024 && part_lds(1024) <= 150 * 1024 ? 1024 : 512;
+    if (cw == 16384 && (nth != 1024 || part_lds(1024) > 150 * 1024)) cw = 8192;
+    const int per = (int)(cw / nth);
     const int nw = (int)((n + cw - 1) / cw);
     const int64_t m = (int64_t)nb * nw;
     LFE_TRY(ensure_pcounts(c, (size_t)m + nb + 1, 0));
@@ -553,16 +586,16 @@ int prepare_layout(lfe_ctx* c) {
     a.pipe = pipe_env;
     const int pgrid = a.xcd_map ? ((nw + 7) / 8) * 8 : nw;
     {
-      const size_t lds = sizeof(double) * cw + sizeof(int32_t) * (cw + (size_t)kPartWaves * nb + 2 * (size_t)nb + 1);
+      const size_t lds = std::min<size_t>(std::max(part_lds(nth), lds_min), 160 * 1024);
       // dynamic LDS above 64 KB must be opted in (static LDS + dynamic <= 160 KB)
-      const void* fn = per == 16 ? reinterpret_cast<const void*>(&k_part_scatter<16>)
-                                 : reinterpret_cast<const void*>(&k_part_scatter<8>);
-      LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      using Fn = void (*)(ScatterArgs);
+      Fn fn = nth == 1024 ? (per == 16 ? &k_part_scatter<16, 1024>
+                             : per == 8 ? &k_part_scatter<8, 1024> : &k_part_scatter<4, 1024>)
+                          : (per == 16 ? &k_part_scatter<16, 512> : &k_part_scatter<8, 512>);
+      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
       ProfScope _ps(c, K_PART_SCATTER);
-      if (per == 16)
-        hipLaunchKernelGGL(k_part_scatter<16>, dim3(pgrid), dim3(kPartThreads), lds, c->stream, a);
-      else
-        hipLaunchKernelGGL(k_part_scatter<8>, dim3(pgrid), dim3(kPartThreads), lds, c->stream, a);
+      hipLaunchKernelGGL(fn, dim3(pgrid), dim3(nth), lds, c->stream, a);
     }
     LFE_HIP(hipGetLastError());
     L.bstart.assign(nb + 1, 0);
@@ -626,7 +659,8 @@ int prepare_layout(lfe_ctx* c) {
       LFE_TRY(allreduce_sum_i32(c, fe.drops, fe.G));
       hipLaunchKernelGGL(k_sub_counts, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, fe.cnt_pre, fe.drops, fe.G,
                          fe.cnt);
-      hipLaunchKernelGGL(k_count_nonzero2, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, fe.cnt, fe.cnt_pre,
+      // few blocks: one atomic per wave into two counters (thousands of same-address adds serialize)
+      hipLaunchKernelGGL(k_count_nonzero2, dim3(grid_for(fe.G, kBlock, 32)), dim3(kBlock), 0, c->stream, fe.cnt, fe.cnt_pre,
                          fe.G, c->iscratch + 2 * f);
       LFE_HIP(hipGetLastError());
     }
