@@ -131,6 +131,17 @@ int lfe_cluster_meat(lfe_ctx* ctx, double* meats_out, int64_t* G_out);
 int lfe_cluster_meat_subsets(lfe_ctx* ctx, int n_subsets, const int32_t* subset_masks, double* meats_out,
                              int64_t* G_out);
 
+/* Host prep on the device.
+ * Dense int32 codes of an integer id column in sorted-unique order (np.unique's
+ * inverse; polars_impl.py:118-139 only needs group membership): n host int64 ids in,
+ * n host codes out, *n_levels_out = number of distinct ids.  Needs no loaded data. */
+int lfe_factorize_ids(lfe_ctx* ctx, int64_t n, const int64_t* ids, int32_t* codes_out, int32_t* n_levels_out);
+
+/* Exact number of distinct rows over the loaded regressors (columns 1..p-1, not y)
+ * and FE codes, all loaded rows: the numerator of estimate_compression_ratio
+ * (compress.py:187-253).  -0.0 == 0.0 and NaNs compare equal.  One process only. */
+int lfe_count_distinct_rows(lfe_ctx* ctx, int64_t* n_distinct_out);
+
 /* Debug/fixtures: copy the demeaned columns (kept rows, device order) to host. */
 int lfe_copy_demeaned(lfe_ctx* ctx, double* const* cols_out, int64_t* n_out);
 

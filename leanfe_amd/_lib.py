@@ -42,6 +42,8 @@ SIGNATURES = {
     "lfe_gram_resid": (C.c_int, [_vp, _dp, _dp, _dp, _dp, C.c_int]),
     "lfe_cluster_meat": (C.c_int, [_vp, _dp, _i64p]),
     "lfe_cluster_meat_subsets": (C.c_int, [_vp, C.c_int, _vp, _dp, _i64p]),
+    "lfe_factorize_ids": (C.c_int, [_vp, C.c_int64, _vp, _vp, C.POINTER(C.c_int32)]),
+    "lfe_count_distinct_rows": (C.c_int, [_vp, _i64p]),
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_sync": (C.c_int, [_vp]),
@@ -175,6 +177,22 @@ class Engine:
         lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
         _check(self._lib.lfe_load_clusters(self._h, len(codes), kp, lv, LFE_HOST))
         self._ncl = len(codes)
+
+    # -- host prep on the device --------------------
+    def factorize_ids(self, ids: np.ndarray) -> tuple[np.ndarray, int]:
+        """Dense int32 codes of an integer id column, sorted-unique order (np.unique's inverse)."""
+        a = np.ascontiguousarray(ids, dtype=np.int64)
+        codes = np.empty(a.size, dtype=np.int32)
+        g = C.c_int32()
+        _check(self._lib.lfe_factorize_ids(self._h, a.size, _ptr(a) if a.size else None,
+                                           _ptr(codes) if a.size else None, C.byref(g)))
+        return codes, int(g.value)
+
+    def count_distinct_rows(self) -> int:
+        """Distinct (x, FE) rows of the loaded data (estimate_compression_ratio's numerator)."""
+        out = C.c_int64()
+        _check(self._lib.lfe_count_distinct_rows(self._h, C.byref(out)))
+        return int(out.value)
 
     # -- hot path ----------------------------------------------------------
     def drop_singletons(self) -> tuple[int, tuple, tuple]:

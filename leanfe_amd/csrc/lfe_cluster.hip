@@ -6,8 +6,7 @@
 // (std_errors.py:399-408 groups by the intersection).  On the device:
 //   1. key_i = mixed-radix code of the tuple (span = prod of levels < 2^62);
 //      dropped rows get key = span, which sorts last;
-//   2. stable LSD radix sort of (key, row) pairs, 8-bit digits: per-block digit
-//      histograms, one exclusive scan, a scatter ranked by wave ballots;
+//   2. stable LSD radix sort of (key, row) pairs (lfe_keys.hip);
 //   3. segments = runs of equal keys (flags + scan), G = their number;
 //   4. S_c = segmented gather-sum of the row-major score rows x~_i r_i (w_i)
 //      (seg_gather_sum, the general-sweep kernel of lfe_seg.hip);
@@ -28,14 +27,6 @@ static int fail(int code, const char* msg) {
   set_error(msg);
   return code;
 }
-
-constexpr int kRsThreads = 256;
-constexpr int kRsWaves = kRsThreads / 64;
-constexpr int kRsPer = 16;                       // items per thread
-constexpr int kRsItems = kRsThreads * kRsPer;    // items per block
-constexpr int kRsBits = 8;
-constexpr int kRsBins = 1 << kRsBits;
-static_assert(kRsBins == kRsThreads, "one digit per thread in the wave prefix");
 
 // cluster code of every layout row (input-order array gathered through orig)
 __global__ void k_cl_layout(const int32_t* __restrict__ cl, const int32_t* __restrict__ orig, int64_t n,
@@ -61,86 +52,6 @@ __global__ void k_cl_keys(KeyArgs a) {
     for (int j = 0; j < a.m; ++j) key += (uint64_t)(uint32_t)a.code[j][i] * a.mult[j];
     a.keys[i] = (a.keep && a.keep[i] < 0) ? a.drop : key;
     a.rows[i] = (int32_t)i;
-  }
-}
-
-// digit counts of block b: counts[d * nblk + b]
-__global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
-                                                        int nblk, int32_t* __restrict__ counts) {
-  __shared__ int32_t h[kRsBins];
-  const int tid = threadIdx.x;
-  h[tid] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kRsItems;
-#pragma unroll 4
-  for (int s = 0; s < kRsPer; ++s) {
-    const int64_t i = base + s * kRsThreads + tid;
-    if (i < n) atomicAdd(&h[(int)((keys[i] >> shift) & (kRsBins - 1))], 1);
-  }
-  __syncthreads();
-  counts[(int64_t)tid * nblk + blockIdx.x] = h[tid];
-}
-
-// Stable scatter.  Wave w of block b owns items [b*4096 + w*1024, +1024) in 16
-// steps of 64; within a step, lanes with equal digits are matched by 8 ballots
-// and ranked by lane; per-wave running counts in LDS carry the rank across
-// steps; a prefix over waves and the scanned global counts give the position.
-__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint64_t* __restrict__ kin,
-                                                           const int32_t* __restrict__ vin,
-                                                           uint64_t* __restrict__ kout, int32_t* __restrict__ vout,
-                                                           int64_t n, int shift, int nblk,
-                                                           const int32_t* __restrict__ scanned) {
-  __shared__ int32_t cnt[kRsWaves][kRsBins];
-  __shared__ int32_t base_d[kRsBins];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int j = tid; j < kRsWaves * kRsBins; j += kRsThreads) (&cnt[0][0])[j] = 0;
-  base_d[tid] = scanned[(int64_t)tid * nblk + blockIdx.x];
-  __syncthreads();
-  const int64_t b0 = (int64_t)blockIdx.x * kRsItems + (int64_t)w * (kRsItems / kRsWaves);
-  const uint64_t lt = (1ull << lane) - 1ull;
-  uint64_t key[kRsPer];
-  int32_t val[kRsPer];
-  int rank[kRsPer];
-#pragma unroll
-  for (int s = 0; s < kRsPer; ++s) {
-    const int64_t i = b0 + s * 64 + lane;
-    const bool valid = i < n;
-    key[s] = valid ? kin[i] : 0ull;
-    val[s] = valid ? vin[i] : 0;
-  }
-#pragma unroll
-  for (int s = 0; s < kRsPer; ++s) {
-    const bool valid = b0 + s * 64 + lane < n;
-    const int d = (int)((key[s] >> shift) & (kRsBins - 1));
-    uint64_t m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < kRsBits; ++b) {
-      const bool bit = (d >> b) & 1;
-      const uint64_t bb = __ballot(bit);
-      m &= bit ? bb : ~bb;
-    }
-    const int before = __popcll(m & lt);
-    rank[s] = cnt[w][d] + before;  // every lane reads before the leader below writes
-    if (valid && before == 0) cnt[w][d] += __popcll(m);
-  }
-  __syncthreads();
-  {
-    int run = 0;
-#pragma unroll
-    for (int w2 = 0; w2 < kRsWaves; ++w2) {
-      const int t = cnt[w2][tid];
-      cnt[w2][tid] = run;
-      run += t;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < kRsPer; ++s) {
-    if (b0 + s * 64 + lane >= n) continue;
-    const int d = (int)((key[s] >> shift) & (kRsBins - 1));
-    const int64_t pos = (int64_t)base_d[d] + cnt[w][d] + rank[s];
-    kout[pos] = key[s];
-    vout[pos] = val[s];
   }
 }
 
@@ -248,40 +159,6 @@ __global__ __launch_bounds__(256) void k_count_nonzero(const int32_t* __restrict
 // host side
 // ---------------------------------------------------------------------------
 
-static int bit_length(uint64_t v) {
-  int b = 0;
-  while (v) {
-    ++b;
-    v >>= 1;
-  }
-  return b;
-}
-
-// sort (keys, rows) [0, n) by the low `bits` bits; returns the buffer index (0/1) holding the result
-static int radix_sort(lfe_ctx* c, int64_t n, int bits, int* out_buf) {
-  auto& W = c->clw;
-  const int nblk = (int)((n + kRsItems - 1) / kRsItems);
-  LFE_TRY(ensure_i32(c, W.counts, W.counts_cap, (size_t)kRsBins * nblk));
-  int cur = 0;
-  for (int shift = 0; shift < bits; shift += kRsBits) {
-    {
-      ProfScope _ps(c, K_CLUSTER_SORT);
-      hipLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], n, shift, nblk,
-                         W.counts);
-    }
-    LFE_HIP(hipGetLastError());
-    LFE_TRY(exclusive_scan(c, W.counts, (int64_t)kRsBins * nblk));
-    {
-      ProfScope _ps(c, K_CLUSTER_SORT);
-      hipLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], W.rows[cur],
-                         W.keys[1 - cur], W.rows[1 - cur], n, shift, nblk, W.counts);
-    }
-    LFE_HIP(hipGetLastError());
-    cur = 1 - cur;
-  }
-  *out_buf = cur;
-  return LFE_OK;
-}
 
 // meat and cluster count of one subset (mask over the loaded cluster columns)
 static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
@@ -398,11 +275,7 @@ int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, doub
     if (masks[s] <= 0 || masks[s] >= (1 << m)) return fail(LFE_EINVAL, "subset mask must select loaded cluster columns");
   auto& W = c->clw;
   const size_t ld = (size_t)c->ld;
-  for (int b = 0; b < 2; ++b) {
-    LFE_TRY(ensure_u64(c, W.keys[b], W.keys_cap[b], ld));
-    LFE_TRY(ensure_i32(c, W.rows[b], W.rows_cap[b], ld));
-  }
-  LFE_TRY(ensure_i32(c, W.flag, W.flag_cap, ld + 1));
+  LFE_TRY(ensure_sort_ws(c, ld));
   LFE_TRY(ensure_i32(c, W.seg_off, W.seg_off_cap, ld + 1));
   LFE_TRY(ensure_i32(c, W.ufirst, W.ufirst_cap, (size_t)seg_units_needed(c->ld)));
   if (!W.lay_valid) {

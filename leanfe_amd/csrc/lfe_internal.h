@@ -237,6 +237,10 @@ int launch_gram(lfe_ctx* c, double* host_gram);
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores);
 int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
+// --- device keys (lfe_keys.hip) ---
+int bit_length(uint64_t v);
+int ensure_sort_ws(lfe_ctx* c, size_t n);
+int radix_sort(lfe_ctx* c, int64_t n, int bits, int* out_buf);
 // --- clusters (lfe_cluster.hip) ---
 int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, double* meats, int64_t* G_out);
 void free_cluster_ws(lfe_ctx* c);

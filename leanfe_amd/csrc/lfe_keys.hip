@@ -1,0 +1,381 @@
+// leanfe HIP engine — device keys: a stable LSD radix sort of (u64 key, int32 row)
+// pairs, and the two host-prep steps built on it:
+//   - lfe_factorize_ids: integer id column -> dense codes in sorted-unique order,
+//     i.e. np.unique(..., return_inverse=True) (the code values do not affect any
+//     result, polars_impl.py:118-139; only group membership does);
+//   - lfe_count_distinct_rows: the exact number of distinct (x, FE) rows,
+//     estimate_compression_ratio's numerator (compress.py:187-253, the
+//     `lf.select(key_cols).unique()` count), over all loaded rows.
+// Distinct rows: 64-bit row hashes are sorted; equal rows have equal hashes, so a
+// new row starts at every hash change.  Neighbours with equal hashes are compared
+// value by value; if two different rows ever share a hash (about 1e-4 odds per 50M
+// rows) the affected runs are recounted exactly, so the count is exact.
+// Float values compare as in a group-by: -0.0 == 0.0 and every NaN equal.
+#include "lfe_internal.h"
+
+#include <algorithm>
+
+namespace lfe {
+
+static int fail(int code, const char* msg) {
+  set_error(msg);
+  return code;
+}
+
+constexpr int kRsThreads = 256;
+constexpr int kRsWaves = kRsThreads / 64;
+constexpr int kRsPer = 16;                       // items per thread
+constexpr int kRsItems = kRsThreads * kRsPer;    // items per block
+constexpr int kRsBits = 8;
+constexpr int kRsBins = 1 << kRsBits;
+static_assert(kRsBins == kRsThreads, "one digit per thread in the wave prefix");
+
+// digit counts of block b: counts[d * nblk + b]
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
+                                                        int nblk, int32_t* __restrict__ counts) {
+  __shared__ int32_t h[kRsBins];
+  const int tid = threadIdx.x;
+  h[tid] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRsItems;
+#pragma unroll 4
+  for (int s = 0; s < kRsPer; ++s) {
+    const int64_t i = base + s * kRsThreads + tid;
+    if (i < n) atomicAdd(&h[(int)((keys[i] >> shift) & (kRsBins - 1))], 1);
+  }
+  __syncthreads();
+  counts[(int64_t)tid * nblk + blockIdx.x] = h[tid];
+}
+
+// Stable scatter.  Wave w of block b owns items [b*4096 + w*1024, +1024) in 16
+// steps of 64; within a step, lanes with equal digits are matched by 8 ballots
+// and ranked by lane; per-wave running counts in LDS carry the rank across
+// steps; a prefix over waves and the scanned global counts give the position.
+__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint64_t* __restrict__ kin,
+                                                           const int32_t* __restrict__ vin,
+                                                           uint64_t* __restrict__ kout, int32_t* __restrict__ vout,
+                                                           int64_t n, int shift, int nblk,
+                                                           const int32_t* __restrict__ scanned) {
+  __shared__ int32_t cnt[kRsWaves][kRsBins];
+  __shared__ int32_t base_d[kRsBins];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int j = tid; j < kRsWaves * kRsBins; j += kRsThreads) (&cnt[0][0])[j] = 0;
+  base_d[tid] = scanned[(int64_t)tid * nblk + blockIdx.x];
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * kRsItems + (int64_t)w * (kRsItems / kRsWaves);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint64_t key[kRsPer];
+  int32_t val[kRsPer];
+  int rank[kRsPer];
+#pragma unroll
+  for (int s = 0; s < kRsPer; ++s) {
+    const int64_t i = b0 + s * 64 + lane;
+    const bool valid = i < n;
+    key[s] = valid ? kin[i] : 0ull;
+    val[s] = valid ? vin[i] : 0;
+  }
+#pragma unroll
+  for (int s = 0; s < kRsPer; ++s) {
+    const bool valid = b0 + s * 64 + lane < n;
+    const int d = (int)((key[s] >> shift) & (kRsBins - 1));
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kRsBits; ++b) {
+      const bool bit = (d >> b) & 1;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const int before = __popcll(m & lt);
+    rank[s] = cnt[w][d] + before;  // every lane reads before the leader below writes
+    if (valid && before == 0) cnt[w][d] += __popcll(m);
+  }
+  __syncthreads();
+  {
+    int run = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < kRsWaves; ++w2) {
+      const int t = cnt[w2][tid];
+      cnt[w2][tid] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < kRsPer; ++s) {
+    if (b0 + s * 64 + lane >= n) continue;
+    const int d = (int)((key[s] >> shift) & (kRsBins - 1));
+    const int64_t pos = (int64_t)base_d[d] + cnt[w][d] + rank[s];
+    kout[pos] = key[s];
+    vout[pos] = val[s];
+  }
+}
+
+
+int bit_length(uint64_t v) {
+  int b = 0;
+  while (v) {
+    ++b;
+    v >>= 1;
+  }
+  return b;
+}
+
+int ensure_sort_ws(lfe_ctx* c, size_t n) {
+  auto& W = c->clw;
+  for (int b = 0; b < 2; ++b) {
+    LFE_TRY(ensure_u64(c, W.keys[b], W.keys_cap[b], std::max<size_t>(n, 1)));
+    LFE_TRY(ensure_i32(c, W.rows[b], W.rows_cap[b], std::max<size_t>(n, 1)));
+  }
+  LFE_TRY(ensure_i32(c, W.flag, W.flag_cap, n + 1));
+  return LFE_OK;
+}
+
+// sort (keys, rows) [0, n) of the workspace by the low `bits` bits; *out_buf = the
+// buffer (0/1) holding the result
+int radix_sort(lfe_ctx* c, int64_t n, int bits, int* out_buf) {
+  auto& W = c->clw;
+  const int nblk = (int)((n + kRsItems - 1) / kRsItems);
+  LFE_TRY(ensure_i32(c, W.counts, W.counts_cap, (size_t)kRsBins * std::max(nblk, 1)));
+  int cur = 0;
+  for (int shift = 0; shift < bits && n > 0; shift += kRsBits) {
+    {
+      ProfScope _ps(c, K_CLUSTER_SORT);
+      hipLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], n, shift, nblk,
+                         W.counts);
+    }
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(exclusive_scan(c, W.counts, (int64_t)kRsBins * nblk));
+    {
+      ProfScope _ps(c, K_CLUSTER_SORT);
+      hipLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], W.rows[cur],
+                         W.keys[1 - cur], W.rows[1 - cur], n, shift, nblk, W.counts);
+    }
+    LFE_HIP(hipGetLastError());
+    cur = 1 - cur;
+  }
+  *out_buf = cur;
+  return LFE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// factorization of integer ids
+// ---------------------------------------------------------------------------
+
+__global__ void k_minmax_i64(const int64_t* __restrict__ v, int64_t n, unsigned long long* __restrict__ out) {
+  // out[0] = min, out[1] = max, as order-preserving unsigned (sign bit flipped)
+  unsigned long long lo = ~0ull, hi = 0ull;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long u = (unsigned long long)v[i] ^ (1ull << 63);
+    lo = u < lo ? u : lo;
+    hi = u > hi ? u : hi;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long a = __shfl_down(lo, off, 64), b = __shfl_down(hi, off, 64);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&out[0], lo);
+    atomicMax(&out[1], hi);
+  }
+}
+
+__global__ void k_fz_keys(const int64_t* __restrict__ ids, int64_t n, unsigned long long lo_biased,
+                          uint64_t* __restrict__ keys, int32_t* __restrict__ rows) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    keys[i] = ((unsigned long long)ids[i] ^ (1ull << 63)) - lo_biased;
+    rows[i] = (int32_t)i;
+  }
+}
+
+__global__ void k_key_heads(const uint64_t* __restrict__ K, int64_t n, int32_t* __restrict__ flag) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+    flag[q] = (q == 0 || K[q] != K[q - 1]) ? 1 : 0;
+}
+
+// code of row R[q] = rank of its key among the distinct keys
+__global__ void k_fz_codes(const uint64_t* __restrict__ K, const int32_t* __restrict__ scan,
+                           const int32_t* __restrict__ R, int64_t n, int32_t* __restrict__ codes) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+    const bool head = q == 0 || K[q] != K[q - 1];
+    codes[R[q]] = scan[q] + (head ? 0 : -1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// distinct rows
+// ---------------------------------------------------------------------------
+
+struct RowArgs {
+  const double* X;   // [p][ld]; columns 1..p-1 are the regressors
+  int64_t ld, n;
+  int p, F;
+  const int32_t* code[kMaxFE];
+  int hash_bits;     // 64; fewer only to exercise the collision path in tests
+};
+
+__device__ __forceinline__ uint64_t canon_bits(double v) {
+  if (v != v) return 0x7ff8000000000000ull;  // every NaN alike
+  if (v == 0.0) return 0ull;                 // -0.0 == 0.0
+  return (uint64_t)__double_as_longlong(v);
+}
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 33;
+  return h;
+}
+
+__global__ void k_row_hash(RowArgs a, uint64_t* __restrict__ keys, int32_t* __restrict__ rows) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (int c = 1; c < a.p; ++c) h = fmix64(h ^ canon_bits(a.X[(int64_t)c * a.ld + i]));
+    for (int f = 0; f < a.F; ++f) h = fmix64(h ^ (uint64_t)(uint32_t)a.code[f][i] ^ 0x5bd1e995ull);
+    keys[i] = a.hash_bits >= 64 ? h : (h & ((1ull << a.hash_bits) - 1));
+    rows[i] = (int32_t)i;
+  }
+}
+
+__device__ __forceinline__ bool rows_equal(const RowArgs& a, int64_t i, int64_t j) {
+  for (int c = 1; c < a.p; ++c)
+    if (canon_bits(a.X[(int64_t)c * a.ld + i]) != canon_bits(a.X[(int64_t)c * a.ld + j])) return false;
+  for (int f = 0; f < a.F; ++f)
+    if (a.code[f][i] != a.code[f][j]) return false;
+  return true;
+}
+
+// flag[q] = hash change; count neighbours with equal hashes but different rows
+__global__ void k_dr_heads(RowArgs a, const uint64_t* __restrict__ K, const int32_t* __restrict__ R,
+                           int32_t* __restrict__ flag, int32_t* __restrict__ nmismatch) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += (int64_t)gridDim.x * blockDim.x) {
+    const bool head = q == 0 || K[q] != K[q - 1];
+    flag[q] = head ? 1 : 0;
+    if (!head && !rows_equal(a, R[q], R[q - 1])) atomicAdd(nmismatch, 1);
+  }
+}
+
+// exact recount of hash runs holding different rows: one thread per run head;
+// a run with mismatching neighbours counts its distinct rows by pairwise
+// comparison and adds (distinct - 1) (the run was counted once)
+__global__ void k_dr_exact(RowArgs a, const uint64_t* __restrict__ K, const int32_t* __restrict__ R,
+                           unsigned long long* __restrict__ extra) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += (int64_t)gridDim.x * blockDim.x) {
+    if (!(q == 0 || K[q] != K[q - 1])) continue;
+    int64_t e = q + 1;
+    bool mixed = false;
+    while (e < a.n && K[e] == K[q]) {
+      mixed = mixed || !rows_equal(a, R[e], R[e - 1]);
+      ++e;
+    }
+    if (!mixed) continue;
+    unsigned long long distinct = 0;
+    for (int64_t i = q; i < e; ++i) {
+      bool seen = false;
+      for (int64_t j = q; j < i && !seen; ++j) seen = rows_equal(a, R[i], R[j]);
+      distinct += seen ? 0 : 1;
+    }
+    atomicAdd(extra, distinct - 1);
+  }
+}
+
+}  // namespace lfe
+
+using namespace lfe;
+
+int lfe_factorize_ids(lfe_ctx* c, int64_t n, const int64_t* ids, int32_t* codes_out, int32_t* n_levels_out) {
+  if (!c) return fail(LFE_EINVAL, "null context");
+  if (n < 0 || n >= (int64_t)INT32_MAX || (n > 0 && (!ids || !codes_out)) || !n_levels_out)
+    return fail(LFE_EINVAL, "bad arguments");
+  if (n == 0) {
+    *n_levels_out = 0;
+    return LFE_OK;
+  }
+  LFE_HIP(hipSetDevice(c->device));
+  LFE_TRY(ensure_sort_ws(c, (size_t)n));
+  auto& W = c->clw;
+  int64_t* dids = reinterpret_cast<int64_t*>(W.keys[1]);  // raw ids staged in the second key buffer
+  LFE_HIP(hipMemcpyAsync(dids, ids, sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream));
+  LFE_TRY(ensure_dred(c, 2));
+  unsigned long long* mm = reinterpret_cast<unsigned long long*>(c->dred);
+  const unsigned long long init[2] = {~0ull, 0ull};
+  LFE_TRY(h2d_small(c, mm, init, sizeof(init)));
+  hipLaunchKernelGGL(k_minmax_i64, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, c->stream, dids, n, mm);
+  LFE_HIP(hipGetLastError());
+  unsigned long long h[2];
+  LFE_TRY(d2h_sync(c, h, mm, sizeof(h)));
+  hipLaunchKernelGGL(k_fz_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, dids, n, h[0], W.keys[0],
+                     W.rows[0]);
+  LFE_HIP(hipGetLastError());
+  int buf = 0;
+  LFE_TRY(radix_sort(c, n, bit_length(h[1] - h[0]), &buf));
+  const uint64_t* K = W.keys[buf];
+  const int32_t* R = W.rows[buf];
+  LFE_HIP(hipMemsetAsync(W.flag + n, 0, sizeof(int32_t), c->stream));
+  hipLaunchKernelGGL(k_key_heads, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, n, W.flag);
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(exclusive_scan(c, W.flag, n + 1));
+  // codes go to the other row buffer (free now), then to the host
+  int32_t* dcodes = W.rows[1 - buf];
+  hipLaunchKernelGGL(k_fz_codes, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, W.flag, R, n, dcodes);
+  LFE_HIP(hipGetLastError());
+  LFE_HIP(hipMemcpyAsync(codes_out, dcodes, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  int32_t G = 0;
+  LFE_TRY(d2h_sync(c, &G, W.flag + n, sizeof(int32_t)));
+  *n_levels_out = G;
+  return LFE_OK;
+}
+
+int lfe_count_distinct_rows(lfe_ctx* c, int64_t* n_distinct_out) {
+  if (!c) return fail(LFE_EINVAL, "null context");
+  if (!n_distinct_out) return fail(LFE_EINVAL, "null pointer");
+  if (!c->loaded) return fail(LFE_ESTATE, "lfe_load first");
+  if (c->world > 1) return fail(LFE_EINVAL, "lfe_count_distinct_rows counts one process's rows only");
+  LFE_HIP(hipSetDevice(c->device));
+  const int64_t n = c->n;
+  if (n == 0) {
+    *n_distinct_out = 0;
+    return LFE_OK;
+  }
+  LFE_TRY(ensure_sort_ws(c, (size_t)n));
+  auto& W = c->clw;
+  RowArgs a{};
+  a.X = c->X;
+  a.ld = c->ld;
+  a.n = n;
+  a.p = c->p;
+  a.F = c->F;
+  for (int f = 0; f < c->F; ++f) a.code[f] = c->fe[f].code;
+  const char* hb_env = getenv("LFE_ROW_HASH_BITS");  // tests: a short hash forces collisions
+  const int hb = hb_env ? atoi(hb_env) : 64;
+  a.hash_bits = hb >= 4 && hb <= 64 ? hb : 64;
+  hipLaunchKernelGGL(k_row_hash, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, W.keys[0], W.rows[0]);
+  LFE_HIP(hipGetLastError());
+  int buf = 0;
+  LFE_TRY(radix_sort(c, n, a.hash_bits, &buf));
+  const uint64_t* K = W.keys[buf];
+  const int32_t* R = W.rows[buf];
+  LFE_TRY(ensure_dred(c, 2));
+  LFE_HIP(hipMemsetAsync(c->dred, 0, 2 * sizeof(double), c->stream));
+  int32_t* nmis = reinterpret_cast<int32_t*>(c->dred);
+  LFE_HIP(hipMemsetAsync(W.flag + n, 0, sizeof(int32_t), c->stream));
+  hipLaunchKernelGGL(k_dr_heads, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, K, R, W.flag, nmis);
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(exclusive_scan(c, W.flag, n + 1));
+  int32_t hres[2] = {0, 0};
+  LFE_TRY(d2h_sync(c, &hres[0], nmis, sizeof(int32_t)));
+  LFE_TRY(d2h_sync(c, &hres[1], W.flag + n, sizeof(int32_t)));
+  int64_t distinct = hres[1];
+  if (hres[0] > 0) {
+    unsigned long long* extra = reinterpret_cast<unsigned long long*>(c->dred) + 1;
+    hipLaunchKernelGGL(k_dr_exact, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, K, R, extra);
+    LFE_HIP(hipGetLastError());
+    unsigned long long ex = 0;
+    LFE_TRY(d2h_sync(c, &ex, extra, sizeof(ex)));
+    distinct += (int64_t)ex;
+  }
+  *n_distinct_out = distinct;
+  return LFE_OK;
+}

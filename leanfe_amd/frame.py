@@ -59,7 +59,7 @@ def _polars_to_numpy(s) -> np.ndarray:
     return s.to_numpy()
 
 
-def factorize(values, global_codes: bool = False) -> tuple[np.ndarray, int]:
+def factorize(values, global_codes: bool = False, device=None) -> tuple[np.ndarray, int]:
     """Dense int32 group codes and the number of code values.
 
     Non-negative integer columns whose maximum is below max(4n, 2^20) are used
@@ -69,7 +69,10 @@ def factorize(values, global_codes: bool = False) -> tuple[np.ndarray, int]:
 
     ``global_codes`` (row shards of one fit): the values must already be global
     non-negative integer codes and are used as they are, since a per-shard
-    unique would number the groups differently on every rank."""
+    unique would number the groups differently on every rank.
+
+    ``device`` (an ``Engine``): sparse integer ids are factorized on the GPU
+    (``Engine.factorize_ids``, a radix sort; same codes as the sorted unique)."""
     v = np.asarray(values)
     n = v.size
     if global_codes:
@@ -87,6 +90,8 @@ def factorize(values, global_codes: bool = False) -> tuple[np.ndarray, int]:
         vmin, vmax = int(v.min()), int(v.max())
         if vmin >= 0 and vmax < max(4 * n, 1 << 20) and vmax < 2 ** 31 - 1:
             return v.astype(np.int32, copy=False), vmax + 1
+        if device is not None and n < 2 ** 31 - 1 and (v.dtype != np.uint64 or vmax < 2 ** 63):
+            return device.factorize_ids(v.astype(np.int64, copy=False))
     uniq, inv = np.unique(v, return_inverse=True)
     return inv.astype(np.int32).ravel(), int(uniq.size)
 

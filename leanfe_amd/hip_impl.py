@@ -18,7 +18,7 @@ from . import dist, frame, inference
 from ._lib import Engine
 from .formula import parse_formula
 from .result import LeanFEResult
-from .strategy import DEFAULT_MAX_FE_LEVELS, determine_strategy, estimate_compression_ratio
+from .strategy import DEFAULT_MAX_FE_LEVELS, determine_strategy
 
 MAX_FE_LEVELS = DEFAULT_MAX_FE_LEVELS  # polars_impl.py:24
 _VERBOSE = os.environ.get("LEANFE_HIP_VERBOSE", "0") not in ("", "0")
@@ -79,18 +79,19 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
 
     own_engine = engine is None
     sharded = engine is not None and dist.is_sharded(engine)
-    codes, levels = [], []
-    for fe in fe_cols:
-        c, g = frame.factorize(cols[fe], global_codes=sharded)
-        codes.append(c)
-        levels.append(g)
-    Y = np.asarray(cols[y_col], dtype=np.float64)
-    Xc = [np.asarray(cols[c], dtype=np.float64) for c in x_cols]
-    w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
-
     eng = engine if engine is not None else Engine(_default_device() if device is None else device)
-    levels = dist.agree_levels(eng, levels)
     try:
+        # FE codes (polars_impl.py:118-139); sparse integer ids are factorized on the GPU
+        codes, levels = [], []
+        for fe in fe_cols:
+            c, g = frame.factorize(cols[fe], global_codes=sharded, device=None if sharded else eng)
+            codes.append(c)
+            levels.append(g)
+        levels = dist.agree_levels(eng, levels)
+        Y = np.asarray(cols[y_col], dtype=np.float64)
+        Xc = [np.asarray(cols[c], dtype=np.float64) for c in x_cols]
+        w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
+
         t0 = time.perf_counter()
         eng.load([Y] + Xc, codes, levels, w)
         t_load = time.perf_counter() - t0
@@ -99,10 +100,16 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
 
         est_comp_ratio = None
         if strategy == "auto":
-            est_comp_ratio = estimate_compression_ratio([cols[c] for c in x_cols + fe_cols])
+            # distinct (x, FE) rows / n over all loaded rows, exact (compress.py:187-253), on the
+            # GPU; a row shard cannot see the other shards' rows, so sharded fits skip it
             n_initial = Y.size
+            if not sharded and n_initial:
+                est_comp_ratio = eng.count_distinct_rows() / n_initial
+            elif not sharded:
+                est_comp_ratio = 1.0
             if not fe_cols:
-                inferred = "ols"
+                # polars_impl.py:385-390 ('compress' without FEs runs OLS here, the same estimates)
+                inferred = "ols" if est_comp_ratio is None or est_comp_ratio >= 0.8 else "compress"
             elif len(fe_cols) == 1:
                 inferred = "demean"
             else:

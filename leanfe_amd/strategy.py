@@ -50,7 +50,9 @@ def _mix64(h: np.ndarray, v: np.ndarray) -> np.ndarray:
 
 
 def estimate_compression_ratio(columns: list[np.ndarray]) -> float | None:
-    """Unique rows over (x, FE) columns / n (compress.py:187-253).  Exact
+    """Unique rows over (x, FE) columns / n (compress.py:187-253), on the host.
+    The hip backend counts exactly on the device (``Engine.count_distinct_rows``);
+    this restatement is kept for host-only callers and as a test reference.  Exact
     (``np.unique`` over stacked rows) for small n; for n up to
     COMPRESSION_RATIO_MAX_ROWS a 64-bit row hash stands in for the row (a
     collision only lowers the estimate by a negligible amount); above that the

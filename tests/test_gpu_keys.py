@@ -1,0 +1,94 @@
+"""Host prep on the device: integer id factorization and the
+exact distinct-row count behind estimate_compression_ratio (compress.py:187-253).
+References: np.unique (sorted-unique codes, as polars_impl.py:118-139 needs only
+group membership) and a host count over canonicalized row bytes."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from leanfe_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from leanfe_amd._lib import Engine
+    with Engine(0) as e:
+        yield e
+
+
+@pytest.mark.parametrize("case", ["random", "negative_wide", "extremes", "constant", "single"])
+def test_factorize_ids_matches_np_unique(eng, case):
+    rng = np.random.default_rng(5)
+    if case == "random":
+        ids = rng.integers(0, 10**12, 1_000_003)
+        ids[::7] = ids[3]  # duplicates
+    elif case == "negative_wide":
+        ids = rng.integers(-(2**62), 2**62, 300_000)
+        ids[100:5000] = ids[:4900]
+    elif case == "extremes":
+        ids = np.array([np.iinfo(np.int64).max, np.iinfo(np.int64).min, 0, -1, 1, np.iinfo(np.int64).max] * 1000)
+    elif case == "constant":
+        ids = np.full(70_000, 123456789012)
+    else:
+        ids = np.array([42])
+    codes, G = eng.factorize_ids(ids)
+    uniq, inv = np.unique(ids, return_inverse=True)
+    assert G == uniq.size
+    np.testing.assert_array_equal(codes, inv.ravel())
+
+
+def _host_distinct(cols, codes):
+    canon = []
+    for c in cols:
+        v = np.asarray(c, dtype=np.float64).copy()
+        v[v == 0.0] = 0.0
+        bits = v.view(np.uint64).copy()
+        bits[np.isnan(v)] = np.uint64(0x7FF8000000000000)
+        canon.append(bits)
+    for k in codes:
+        canon.append(np.asarray(k, dtype=np.uint64))
+    return np.unique(np.stack(canon, axis=1), axis=0).shape[0]
+
+
+@pytest.mark.parametrize("hash_bits", [64, 10])
+def test_count_distinct_rows_exact(eng, hash_bits):
+    rng = np.random.default_rng(9)
+    n = 400_000
+    y = rng.standard_normal(n)                     # y is not part of the key
+    x1 = rng.integers(0, 3, n).astype(np.float64)
+    x2 = rng.choice(np.array([-0.0, 0.0, 1.5, np.nan, -np.nan]), n)
+    x3 = np.where(rng.random(n) < 0.5, 2.0, rng.integers(0, 50, n).astype(np.float64))
+    fe1 = rng.integers(0, 40, n).astype(np.int32)
+    fe2 = rng.integers(0, 7, n).astype(np.int32)
+    eng.load([y, x1, x2, x3], [fe1, fe2], [40, 7])
+    os.environ["LFE_ROW_HASH_BITS"] = str(hash_bits)  # 10 bits: thousands of collisions -> exact recount
+    try:
+        got = eng.count_distinct_rows()
+    finally:
+        os.environ.pop("LFE_ROW_HASH_BITS", None)
+    assert got == _host_distinct([x1, x2, x3], [fe1, fe2])
+
+
+def test_auto_strategy_ratio_and_device_factorized_ids():
+    """strategy='auto' reports the exact ratio; sparse int64 FE ids (factorized on the
+    device) give the same fit as their dense codes."""
+    from leanfe_amd import leanfe_hip
+    from leanfe_amd.strategy import estimate_compression_ratio
+    n, L = 120_000, [3000, 40]
+    data = synth.panel(n, 2, L, seed=17)
+    data["x1"] = np.round(data["x1"], 1)  # some repeated rows
+    ref = leanfe_hip(data, formula="y ~ x1 + x2 | fe1 + fe2", vcov="HC1", quiet=True)
+    sparse = dict(data)
+    sparse["fe1"] = data["fe1"].astype(np.int64) * 1_000_003_000_017 - 5  # ids far beyond 4n
+    r = leanfe_hip(sparse, formula="y ~ x1 + x2 | fe1 + fe2", vcov="HC1", quiet=True)
+    assert r.compression_ratio == pytest.approx(estimate_compression_ratio(
+        [data["x1"], data["x2"], data["fe1"], data["fe2"]]), rel=0, abs=0)
+    assert r.fe_dims == ref.fe_dims and r.iterations == ref.iterations and r.n_obs == ref.n_obs
+    for x in ("x1", "x2"):
+        assert r.coefs[x] == pytest.approx(ref.coefs[x], rel=1e-12)
+        assert r.std_errors[x] == pytest.approx(ref.std_errors[x], rel=1e-12)
