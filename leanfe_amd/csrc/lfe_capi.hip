@@ -153,6 +153,9 @@ struct lfe_emu {
   int64_t generation = 0;
   std::vector<std::vector<char>> slots;
   std::vector<char> result;
+  // all-to-all: every rank publishes its device send buffer and per-peer blocks
+  std::vector<const char*> a2a_send;
+  std::vector<std::vector<size_t>> a2a_off, a2a_bytes;
   void barrier() {
     std::unique_lock<std::mutex> lk(m);
     const int64_t gen = generation;
@@ -194,6 +197,52 @@ static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
   e->barrier();
   LFE_HIP(hipMemcpy(dev, e->result.data(), bytes, hipMemcpyHostToDevice));
   e->barrier();  // every rank has its copy before the result buffer is reused
+  return LFE_OK;
+}
+
+// peer r receives this rank's block [send_off[r], + send_bytes[r]); this rank
+// receives peer r's block for it at recv_off[r] (recv_bytes[r] bytes)
+int alltoallv_bytes(lfe_ctx* c, const char* send, const size_t* send_off, const size_t* send_bytes, char* recv,
+                    const size_t* recv_off, const size_t* recv_bytes) {
+  const int W = c->world;
+  if (W <= 1) {
+    if (send_bytes[0])
+      LFE_HIP(hipMemcpyAsync(recv + recv_off[0], send + send_off[0], send_bytes[0], hipMemcpyDeviceToDevice,
+                             c->stream));
+    return LFE_OK;
+  }
+  if (c->emu) {  // all contexts of an emulated group share one device: peer copies are D2D
+    lfe_emu* e = c->emu;
+    LFE_HIP(hipStreamSynchronize(c->stream));
+    {
+      std::lock_guard<std::mutex> lk(e->m);
+      e->a2a_send.resize(W);
+      e->a2a_off.resize(W);
+      e->a2a_bytes.resize(W);
+      e->a2a_send[c->rank] = send;
+      e->a2a_off[c->rank].assign(send_off, send_off + W);
+      e->a2a_bytes[c->rank].assign(send_bytes, send_bytes + W);
+    }
+    e->barrier();
+    for (int q = 0; q < W; ++q) {
+      const size_t b = e->a2a_bytes[q][c->rank];
+      if (b != recv_bytes[q]) return fail(LFE_EINVAL, "alltoallv: peer block size mismatch");
+      if (b) LFE_HIP(hipMemcpy(recv + recv_off[q], e->a2a_send[q] + e->a2a_off[q][c->rank], b,
+                               hipMemcpyDeviceToDevice));
+    }
+    e->barrier();  // every peer has read this rank's buffer
+    return LFE_OK;
+  }
+  LFE_NCCL(ncclGroupStart());
+  for (int r = 0; r < W; ++r) {
+    if (r == c->rank) continue;
+    if (send_bytes[r]) LFE_NCCL(ncclSend(send + send_off[r], send_bytes[r], ncclUint8, r, c->comm, c->stream));
+    if (recv_bytes[r]) LFE_NCCL(ncclRecv(recv + recv_off[r], recv_bytes[r], ncclUint8, r, c->comm, c->stream));
+  }
+  LFE_NCCL(ncclGroupEnd());
+  if (send_bytes[c->rank])
+    LFE_HIP(hipMemcpyAsync(recv + recv_off[c->rank], send + send_off[c->rank], send_bytes[c->rank],
+                           hipMemcpyDeviceToDevice, c->stream));
   return LFE_OK;
 }
 

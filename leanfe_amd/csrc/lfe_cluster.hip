@@ -14,9 +14,11 @@
 // No hash table and no f64 atomics, whatever the number of clusters (config 4:
 // fe2 x fe3 has 48.8M clusters for 50M rows).
 //
-// Multi-rank: clusters span row shards.  The key space is global (codes are
-// global), so for span < 2^31 the S table is indexed by key directly, summed
-// with f64 atomics and all-reduced; larger spans across ranks are rejected.
+// Multi-rank: clusters span row shards; keys are global (codes are global).  Few
+// clusters (key table <= 64 MB): a key-indexed S table, f64 atomics, all-reduce.
+// Otherwise owner-partitioned (owner_meat): local sums per cluster are sent to
+// the rank owner(key) by an all-to-all, merged there, and only the k x k meats
+// and the cluster counts are all-reduced.
 #include "lfe_internal.h"
 
 #include <algorithm>
@@ -160,6 +162,178 @@ __global__ __launch_bounds__(256) void k_count_nonzero(const int32_t* __restrict
 // ---------------------------------------------------------------------------
 
 
+// Clusters of sorted (key, row) pairs [0, n) (dropped rows carry key = drop and sort
+// last): segment offsets in W.seg_off, S[h] = sum of the rows' records (row-major
+// [.][k] `table`) in c->clS; *G_out clusters.
+static int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R,
+                        const double* table, int k, int32_t* G_out) {
+  auto& W = c->clw;
+  LFE_TRY(ensure_i32(c, W.seg_off, W.seg_off_cap, (size_t)n + 1));
+  LFE_TRY(ensure_i32(c, W.ufirst, W.ufirst_cap, (size_t)seg_units_needed(n)));
+  int32_t G = 0;
+  LFE_HIP(hipMemsetAsync(W.flag + n, 0, sizeof(int32_t), c->stream));
+  LFE_HIP(hipMemsetAsync(W.seg_off, 0, sizeof(int32_t), c->stream));
+  if (n > 0) {
+    ProfScope _ps(c, K_CLUSTER_SORT);
+    hipLaunchKernelGGL(k_cl_heads, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, n, drop, W.flag);
+  }
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(exclusive_scan(c, W.flag, n + 1));
+  if (n > 0) {
+    ProfScope _ps(c, K_CLUSTER_SORT);
+    hipLaunchKernelGGL(k_cl_segoff, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, W.flag, n, drop,
+                       W.seg_off);
+  }
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(d2h_sync(c, &G, W.flag + n, sizeof(int32_t)));
+  *G_out = G;
+  if (k == 0) return LFE_OK;
+  LFE_TRY(ensure_cluster_ws(c, (size_t)std::max(G, 1) * k, 4));
+  // kept positions = n minus the dropped rows (sorted last): G clusters over them
+  int32_t nv = 0;
+  LFE_TRY(d2h_sync(c, &nv, W.seg_off + G, sizeof(int32_t)));
+  if (k <= 16 && G > 0 && (int64_t)nv < 8 * (int64_t)G) {
+    // short clusters (mean < 8 rows): row-per-lane segmented scan
+    LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)G * k, c->stream));
+    const int grid = grid_for(((int64_t)nv + 63) / 64 * 64, 256, 8192);
+    ProfScope _ps(c, K_CLUSTER_SCATTER);
+    if (k <= 4)
+      hipLaunchKernelGGL(k_seg_rows<4>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, drop, table,
+                         k, c->clS);
+    else if (k <= 8)
+      hipLaunchKernelGGL(k_seg_rows<8>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, drop, table,
+                         k, c->clS);
+    else if (k <= 12)
+      hipLaunchKernelGGL(k_seg_rows<12>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, drop,
+                         table, k, c->clS);
+    else
+      hipLaunchKernelGGL(k_seg_rows<16>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, drop,
+                         table, k, c->clS);
+  } else {
+    LFE_TRY(seg_gather_sum(c, W.seg_off, G, W.ufirst, n, R, table, k, k, c->clS, K_CLUSTER_SCATTER));
+  }
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+__device__ __forceinline__ int cl_owner(uint64_t key, int world) {
+  key ^= key >> 33;
+  key *= 0xff51afd7ed558ccdull;
+  key ^= key >> 33;
+  return (int)(key % (uint64_t)world);
+}
+
+__global__ void k_cl_owner_count(const uint64_t* __restrict__ K, const int32_t* __restrict__ seg_off, int32_t G,
+                                 int world, int32_t* __restrict__ cnt) {
+  for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < G; h += gridDim.x * blockDim.x)
+    atomicAdd(&cnt[cl_owner(K[seg_off[h]], world)], 1);
+}
+
+// send record of cluster h: its key and S[h][0, k), grouped by owner rank
+__global__ void k_cl_owner_scatter(const uint64_t* __restrict__ K, const int32_t* __restrict__ seg_off,
+                                   const double* __restrict__ S, int32_t G, int k, int world,
+                                   int32_t* __restrict__ cursor, uint64_t* __restrict__ skey,
+                                   double* __restrict__ srec) {
+  for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < G; h += gridDim.x * blockDim.x) {
+    const uint64_t key = K[seg_off[h]];
+    const int32_t pos = atomicAdd(&cursor[cl_owner(key, world)], 1);
+    skey[pos] = key;
+    for (int j = 0; j < k; ++j) srec[(int64_t)pos * k + j] = S[(int64_t)h * k + j];
+  }
+}
+
+__global__ void k_iota_pairs(const uint64_t* __restrict__ kin, int64_t n, uint64_t* __restrict__ keys,
+                             int32_t* __restrict__ rows) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    keys[i] = kin[i];
+    rows[i] = (int32_t)i;
+  }
+}
+
+// Owner-partitioned reduction of the local cluster sums: cluster h's
+// record goes to rank owner(key); every owner merges what it received by key, forms
+// S'S of its clusters, and only the k x k meats and cluster counts are all-reduced.
+static int owner_meat(lfe_ctx* c, const uint64_t* K, int32_t G, int k, uint64_t span, double* meat,
+                      int64_t* G_out) {
+  auto& W = c->clw;
+  const int world = c->world, rank = c->rank;
+  LFE_TRY(ensure_u64(c, W.skey, W.skey_cap, (size_t)std::max(G, 1)));
+  LFE_TRY(ensure_f64(c, W.srec, W.srec_cap, (size_t)std::max(G, 1) * k));
+  LFE_TRY(ensure_i32(c, W.ocnt, W.ocnt_cap, (size_t)world * world + 2 * world));
+  int32_t* cnt = W.ocnt;               // [world] my records per owner, then cursors
+  int32_t* cur = W.ocnt + world;       // [world]
+  int32_t* mat = W.ocnt + 2 * world;   // [world][world] records from rank r to rank q
+  LFE_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * world, c->stream));
+  if (G > 0)
+    hipLaunchKernelGGL(k_cl_owner_count, dim3(grid_for(G)), dim3(kBlock), 0, c->stream, K, W.seg_off, G, world, cnt);
+  LFE_HIP(hipGetLastError());
+  std::vector<int32_t> mine(world), offs(world);
+  LFE_TRY(d2h_sync(c, mine.data(), cnt, sizeof(int32_t) * world));
+  for (int q = 0, run = 0; q < world; ++q) {
+    offs[q] = run;
+    run += mine[q];
+  }
+  LFE_TRY(h2d_small(c, cur, offs.data(), sizeof(int32_t) * world));
+  if (G > 0)
+    hipLaunchKernelGGL(k_cl_owner_scatter, dim3(grid_for(G)), dim3(kBlock), 0, c->stream, K, W.seg_off, c->clS, G, k,
+                       world, cur, W.skey, W.srec);
+  LFE_HIP(hipGetLastError());
+  // who sends how much to whom
+  std::vector<int32_t> hm((size_t)world * world, 0);
+  for (int q = 0; q < world; ++q) hm[(size_t)rank * world + q] = mine[q];
+  LFE_HIP(hipMemsetAsync(mat, 0, sizeof(int32_t) * world * world, c->stream));
+  LFE_TRY(h2d_small(c, mat + (size_t)rank * world, mine.data(), sizeof(int32_t) * world));
+  LFE_TRY(allreduce_sum_i32(c, mat, (size_t)world * world));
+  LFE_TRY(d2h_sync(c, hm.data(), mat, sizeof(int32_t) * world * world));
+  std::vector<size_t> so(world), sb(world), ro(world), rb(world), so8(world), sb8(world), ro8(world), rb8(world);
+  int64_t R = 0;
+  for (int q = 0; q < world; ++q) {
+    const int64_t from_q = hm[(size_t)q * world + rank];
+    so[q] = (size_t)offs[q] * k * sizeof(double);
+    sb[q] = (size_t)mine[q] * k * sizeof(double);
+    so8[q] = (size_t)offs[q] * sizeof(uint64_t);
+    sb8[q] = (size_t)mine[q] * sizeof(uint64_t);
+    ro[q] = (size_t)R * k * sizeof(double);
+    rb[q] = (size_t)from_q * k * sizeof(double);
+    ro8[q] = (size_t)R * sizeof(uint64_t);
+    rb8[q] = (size_t)from_q * sizeof(uint64_t);
+    R += from_q;
+  }
+  LFE_TRY(ensure_u64(c, W.rkey, W.rkey_cap, (size_t)std::max<int64_t>(R, 1)));
+  LFE_TRY(ensure_f64(c, W.rrec, W.rrec_cap, (size_t)std::max<int64_t>(R, 1) * k));
+  LFE_TRY(alltoallv_bytes(c, reinterpret_cast<const char*>(W.skey), so8.data(), sb8.data(),
+                          reinterpret_cast<char*>(W.rkey), ro8.data(), rb8.data()));
+  LFE_TRY(alltoallv_bytes(c, reinterpret_cast<const char*>(W.srec), so.data(), sb.data(),
+                          reinterpret_cast<char*>(W.rrec), ro.data(), rb.data()));
+  // merge the received partial sums of this rank's clusters
+  LFE_TRY(ensure_sort_ws(c, (size_t)R));
+  if (R > 0)
+    hipLaunchKernelGGL(k_iota_pairs, dim3(grid_for(R, kBlock, 8192)), dim3(kBlock), 0, c->stream, W.rkey, R,
+                       W.keys[0], W.rows[0]);
+  LFE_HIP(hipGetLastError());
+  int buf = 0;
+  if (R > 0) LFE_TRY(radix_sort(c, R, bit_length(span), &buf));
+  int32_t Gown = 0;
+  LFE_TRY(group_sorted(c, R, span, W.keys[buf], W.rows[buf], W.rrec, k, &Gown));
+  // this rank's clusters only: the table Gram is reduced locally, then the meats summed
+  std::vector<double> part((size_t)k * k, 0.0);
+  if (Gown > 0) {
+    c->world = 1;
+    const int rc = launch_table_gram(c, c->clS, Gown, k, part.data());
+    c->world = world;
+    if (rc) return rc;
+  }
+  LFE_TRY(ensure_dred(c, (size_t)k * k + 1));
+  std::vector<double> packed(part);
+  packed.push_back((double)Gown);
+  LFE_TRY(h2d_small(c, c->dred, packed.data(), sizeof(double) * packed.size()));
+  LFE_TRY(allreduce_sum_f64(c, c->dred, packed.size()));
+  LFE_TRY(d2h_sync(c, packed.data(), c->dred, sizeof(double) * packed.size()));
+  for (int e = 0; e < k * k; ++e) meat[e] = packed[e];
+  *G_out = (int64_t)packed[(size_t)k * k];
+  return LFE_OK;
+}
+
 // meat and cluster count of one subset (mask over the loaded cluster columns)
 static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   const int k = c->p - 1;
@@ -169,6 +343,7 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   uint64_t span = 1;
   for (int j = 0; j < (int)c->cl.size(); ++j) {
     if (!(mask >> j & 1)) continue;
+    if (ka.m == kMaxCl) return fail(LFE_EINVAL, "too many cluster columns in one subset");
     const uint64_t g = (uint64_t)c->cl_levels[j];
     if (span > ((1ull << 62) / g)) return fail(LFE_EINVAL, "cluster intersection span exceeds 2^62");
     ka.code[ka.m] = W.lay[j];
@@ -184,9 +359,10 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   if (n > 0) hipLaunchKernelGGL(k_cl_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka);
   LFE_HIP(hipGetLastError());
 
-  if (c->world > 1) {
-    // global key space indexed directly, partial tables all-reduced
-    if (span >= (1ull << 31)) return fail(LFE_EINVAL, "multi-rank cluster intersection needs span < 2^31");
+  // multi-rank, few clusters: a key-indexed table, all-reduced (smaller than the exchange)
+  const char* own_env = getenv("LFE_CL_OWNER_MIN_SPAN");  // tests: force the owner-partitioned form
+  const uint64_t owner_min = own_env ? (uint64_t)atoll(own_env) : ((64ull << 20) / (8ull * std::max(k, 1)));
+  if (c->world > 1 && span < owner_min && span < (1ull << 31)) {
     const int32_t C = (int32_t)span;
     LFE_TRY(ensure_cluster_ws(c, (size_t)C * std::max(k, 1), (size_t)C + 4));
     double* S = c->clS;
@@ -219,51 +395,11 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
 
   int buf = 0;
   if (n > 0) LFE_TRY(radix_sort(c, n, bit_length(span), &buf));
-  const uint64_t* K = W.keys[buf];
-  const int32_t* R = W.rows[buf];
   int32_t G = 0;
-  LFE_HIP(hipMemsetAsync(W.flag + n, 0, sizeof(int32_t), c->stream));
-  LFE_HIP(hipMemsetAsync(W.seg_off, 0, sizeof(int32_t), c->stream));
-  if (n > 0) {
-    ProfScope _ps(c, K_CLUSTER_SORT);
-    hipLaunchKernelGGL(k_cl_heads, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, n, span, W.flag);
-  }
-  LFE_HIP(hipGetLastError());
-  LFE_TRY(exclusive_scan(c, W.flag, n + 1));
-  if (n > 0) {
-    ProfScope _ps(c, K_CLUSTER_SORT);
-    hipLaunchKernelGGL(k_cl_segoff, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, W.flag, n, span,
-                       W.seg_off);
-  }
-  LFE_HIP(hipGetLastError());
-  LFE_TRY(d2h_sync(c, &G, W.flag + n, sizeof(int32_t)));
+  LFE_TRY(group_sorted(c, n, span, W.keys[buf], W.rows[buf], c->scores, k, &G));
+  if (c->world > 1) return owner_meat(c, W.keys[buf], G, k, span, meat, G_out);
   *G_out = G;
   if (k == 0) return LFE_OK;
-  LFE_TRY(ensure_cluster_ws(c, (size_t)std::max(G, 1) * k, 4));
-  // kept positions = n minus the dropped rows (sorted last): G clusters over them
-  int32_t nv = 0;
-  LFE_TRY(d2h_sync(c, &nv, W.seg_off + G, sizeof(int32_t)));
-  if (k <= 16 && G > 0 && (int64_t)nv < 8 * (int64_t)G) {
-    // short clusters (mean < 8 rows): row-per-lane segmented scan
-    LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)G * k, c->stream));
-    const int grid = grid_for(((int64_t)nv + 63) / 64 * 64, 256, 8192);
-    ProfScope _ps(c, K_CLUSTER_SCATTER);
-    if (k <= 4)
-      hipLaunchKernelGGL(k_seg_rows<4>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, span,
-                         c->scores, k, c->clS);
-    else if (k <= 8)
-      hipLaunchKernelGGL(k_seg_rows<8>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, span,
-                         c->scores, k, c->clS);
-    else if (k <= 12)
-      hipLaunchKernelGGL(k_seg_rows<12>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, span,
-                         c->scores, k, c->clS);
-    else
-      hipLaunchKernelGGL(k_seg_rows<16>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, span,
-                         c->scores, k, c->clS);
-  } else {
-    LFE_TRY(seg_gather_sum(c, W.seg_off, G, W.ufirst, n, R, c->scores, k, k, c->clS, K_CLUSTER_SCATTER));
-  }
-  LFE_HIP(hipGetLastError());
   return launch_table_gram(c, c->clS, G, k, meat);
 }
 

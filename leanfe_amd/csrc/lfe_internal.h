@@ -102,6 +102,17 @@ struct ClusterWS {
   size_t seg_off_cap = 0;
   int32_t* ufirst = nullptr;
   size_t ufirst_cap = 0;
+  // owner-partitioned exchange (multi-rank, many clusters)
+  uint64_t* skey = nullptr;     // [G_local] segment keys -> send order
+  size_t skey_cap = 0;
+  double* srec = nullptr;       // [G_local][k] send records
+  size_t srec_cap = 0;
+  uint64_t* rkey = nullptr;     // received keys
+  size_t rkey_cap = 0;
+  double* rrec = nullptr;       // received records
+  size_t rrec_cap = 0;
+  int32_t* ocnt = nullptr;      // [world] owner counts + cursors, [world * world] count matrix
+  size_t ocnt_cap = 0;
   std::vector<int32_t*> lay;    // loaded cluster columns in layout order
   std::vector<size_t> lay_cap;
   bool lay_valid = false;
@@ -286,6 +297,8 @@ int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems);
 int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count);
 int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count);
 int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count);
+int alltoallv_bytes(lfe_ctx* c, const char* send, const size_t* send_off, const size_t* send_bytes, char* recv,
+                    const size_t* recv_off, const size_t* recv_bytes);
 void prof_begin(lfe_ctx* c, int kid);
 void prof_end(lfe_ctx* c);
 int prof_fold(lfe_ctx* c);

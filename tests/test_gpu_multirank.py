@@ -47,9 +47,13 @@ def _solve(eng, vcov, cl_levels, n_obs_expected=None):
         se = inference.se_iid(Vb, stats[0], df)
     elif v == "hc1":
         se = inference.se_hc1(Vb, meat, n_obs, df)
-    else:
+    elif len(cl_levels) == 1:
         meats, Gs = eng.cluster_meat()
         se, ncl = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df, True)
+    else:
+        subsets = inference.cluster_subsets(len(cl_levels))
+        meats, Gs = eng.cluster_meat_subsets(subsets)
+        se, ncl = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets, n_obs, df, True)
     return dict(beta=beta_full[1:], se=se, iterations=iterations, n_obs=n_obs, df_resid=df, fe_dims=list(dims),
                 n_clusters=ncl, fused=fused is not None)
 
@@ -68,9 +72,10 @@ def _run_group(world, n, k, levels, vcov, cluster_fe, seed):
             eng.synth_load(hi - lo, k, levels, synth.betas(k), seed=seed, row_offset=lo)
             cl_levels = None
             if cluster_fe is not None:
+                fes = [cluster_fe] if isinstance(cluster_fe, int) else list(cluster_fe)
                 _, codes = eng.copy_inputs()
-                eng.load_clusters([np.ascontiguousarray(codes[cluster_fe])], [levels[cluster_fe]])
-                cl_levels = [levels[cluster_fe]]
+                cl_levels = [levels[f] for f in fes]
+                eng.load_clusters([np.ascontiguousarray(codes[f]) for f in fes], cl_levels)
             out[rank] = _solve(eng, vcov, cl_levels)
             eng.close()
         except BaseException as e:  # noqa: BLE001
@@ -87,20 +92,29 @@ def _run_group(world, n, k, levels, vcov, cluster_fe, seed):
     return out
 
 
-@pytest.mark.parametrize("world,n,k,levels,vcov,cluster_fe", [
-    (2, 400_003, 10, (20000, 500), "HC1", None),       # fast path (REDUCE mode), fused Gram/solve/resid
-    (3, 300_000, 4, (8000, 300), "iid", None),
-    (2, 200_000, 3, (3000, 200, 9), "cluster", 1),      # generic sweeps (F = 3) + cluster score tables
+@pytest.mark.parametrize("world,n,k,levels,vcov,cluster_fe,owner", [
+    (2, 400_003, 10, (20000, 500), "HC1", None, False),       # fast path (REDUCE mode), fused Gram/solve/resid
+    (3, 300_000, 4, (8000, 300), "iid", None, False),
+    (2, 200_000, 3, (3000, 200, 9), "cluster", 1, False),      # generic sweeps (F = 3) + key-indexed score table
+    (2, 200_000, 3, (3000, 200, 9), "cluster", (0, 1), True),  # two-way CGM, owner-partitioned exchange
+    (3, 250_001, 5, (30000, 120), "cluster", (0, 1), True),    # 3 ranks; fe1 x fe2: ~1.4 rows per cluster
+    (3, 250_001, 5, (30000, 120), "cluster", (0, 1), False),   # same through the key-indexed table
 ])
-def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe):
+def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe, owner, monkeypatch):
     from oracle import altproj
 
+    if owner:
+        monkeypatch.setenv("LFE_CL_OWNER_MIN_SPAN", "0")
+    else:
+        monkeypatch.setenv("LFE_CL_OWNER_MIN_SPAN", str(1 << 40))
     seed = 11
     out = _run_group(world, n, k, list(levels), vcov, cluster_fe, seed)
     full = synth.panel(n, k, list(levels), seed=seed)
     xs = [f"x{j + 1}" for j in range(k)]
     fes = [f"fe{f + 1}" for f in range(len(levels))]
-    cl = [fes[cluster_fe]] if cluster_fe is not None else None
+    cl = None
+    if cluster_fe is not None:
+        cl = [fes[cluster_fe]] if isinstance(cluster_fe, int) else [fes[f] for f in cluster_fe]
     o = altproj.fit(full, "y", xs, fes, vcov=vcov, cluster_cols=cl)
     for r in range(world):
         res = out[r]
@@ -110,6 +124,8 @@ def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe):
         np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=0)
         np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
         if cluster_fe is not None:
-            assert res["n_clusters"] == o["n_clusters"]
+            ncl = o["n_clusters"]
+            assert (tuple(res["n_clusters"]) if isinstance(res["n_clusters"], (tuple, list)) else res["n_clusters"]) == (
+                tuple(ncl) if isinstance(ncl, (tuple, list)) else ncl)
         np.testing.assert_array_equal(res["beta"], out[0]["beta"])  # identical on every rank
         np.testing.assert_array_equal(res["se"], out[0]["se"])
