@@ -85,15 +85,22 @@ __global__ void k_ls_base(const int32_t* __restrict__ bitems, int nb, int K, int
 
 constexpr int kLsThreads = 512;
 constexpr int kLsWaves = kLsThreads / 64;
-constexpr int kLsPer = 16;
-constexpr int kLsRows = kLsThreads * kLsPer;
+// rows per thread of the local sort (LFE_LS_PER: 16 or 8; fewer rows, fewer registers, more
+// resident workgroups)
+static int ls_per() {
+  static const int v = [] {
+    const char* e = getenv("LFE_LS_PER");
+    return e && atoi(e) == 16 ? 16 : 8;
+  }();
+  return v;
+}
 
-static size_t ls_scatter_lds(int K, int ncur) {
-  return sizeof(int32_t) * ((size_t)ncur * K + 3 * (size_t)K + (size_t)kLsRows);
+static size_t ls_scatter_lds(int K, int ncur, int per = 16) {
+  return sizeof(int32_t) * ((size_t)ncur * K + 3 * (size_t)K + (size_t)kLsThreads * per);
 }
 
 // NCUR: cursor sets (kLsWaves: one per wave, stable; 1: shared, unstable)
-template <bool KEYQ, typename VT, int NCUR>
+template <bool KEYQ, typename VT, int NCUR, int kLsPer>
 __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restrict__ items,
                                                            const int32_t* __restrict__ codeP,
                                                            const int32_t* __restrict__ codeQ, int s, int K,
@@ -101,6 +108,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
                                                            const int32_t* __restrict__ itembase,
                                                            const int32_t* __restrict__ xitems,
                                                            VT* __restrict__ out) {
+  constexpr int kLsRows = kLsThreads * kLsPer;
   extern __shared__ int32_t sm[];
   int32_t* cur = sm;              // [NCUR][K]
   int32_t* run = cur + NCUR * K;  // [K] next free slot of each key
@@ -248,13 +256,19 @@ static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off,
   LFE_HIP(hipGetLastError());
   LFE_TRY(exclusive_scan(c, off, (int64_t)m + 1));
   constexpr int NCUR = 1;
-  const size_t lds = ls_scatter_lds(K, NCUR);
-  const void* fn = reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, NCUR>);
+  const int per = ls_per();
+  const size_t lds = ls_scatter_lds(K, NCUR, per);
+  const void* fn = per == 16 ? reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, NCUR, 16>)
+                             : reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, NCUR, 8>);
   if (lds > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   {
     ProfScope _ps(c, K_MISC);
-    hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream, items,
-                       L.code[P], L.code[Q], L.s, K, off, itemcnt, c->xitems_d, out);
+    if (per == 16)
+      hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR, 16>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream,
+                         items, L.code[P], L.code[Q], L.s, K, off, itemcnt, c->xitems_d, out);
+    else
+      hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR, 8>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream,
+                         items, L.code[P], L.code[Q], L.s, K, off, itemcnt, c->xitems_d, out);
   }
   LFE_HIP(hipGetLastError());
   return LFE_OK;
