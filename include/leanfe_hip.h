@@ -107,6 +107,15 @@ int lfe_gram(lfe_ctx* ctx, double* gram_out);
 int lfe_resid(lfe_ctx* ctx, const double* beta_full, double* stats_out, double* hc1_meat,
               int keep_scores);
 
+/* IV/2SLS residual pass (polars_impl.py:176-200, 229 with instruments loaded as the
+ * columns after x; std_errors.py:448-602).  coef[p] = {c_0, c_1..c_{p-1}} over
+ * u = [1, col_1..col_{p-1}] (the host's first stage folded into the second:
+ * X_hat beta = Z (gamma beta), zero on the x columns); r = y~ - coef . u, stats_out
+ * as lfe_resid; meat_out (p x p, may be NULL) = sum (w) r^2 u u' — the intercept
+ * in slot 0, so X_hat' diag(r^2) X_hat = gamma' meat[Z, Z] gamma on the host.
+ * keep_scores != 0 keeps u r (w), p wide, for lfe_cluster_meat*. */
+int lfe_resid_iv(lfe_ctx* ctx, const double* coef, double* stats_out, double* meat_out, int keep_scores);
+
 /* lfe_gram + solve + lfe_resid with one host round trip: the (p+1)^2 Gram as
  * lfe_gram, the beta_full[p] a one-thread device Cholesky solved from it (used
  * for the residuals; equal to the host's polars_impl.py:212-226 solve up to
@@ -116,9 +125,12 @@ int lfe_resid(lfe_ctx* ctx, const double* beta_full, double* stats_out, double* 
 int lfe_gram_resid(lfe_ctx* ctx, double* gram_out, double* beta_full_out, double* stats_out, double* hc1_meat,
                    int keep_scores);
 
-/* For each loaded cluster array j: S_c = sum_{i in c} x~_i r_i (w_i);
+/* For each loaded cluster array j: S_c = sum_{i in c} u_i r_i (w_i);
  * meats_out[j] = S'S (k x k), G_out[j] = number of clusters present among the
- * kept rows (std_errors.py:317-336, compress.py:929-942 — the W_C'(X.e) SpMM). */
+ * kept rows (std_errors.py:317-336, compress.py:929-942 — the W_C'(X.e) SpMM).
+ * u and k are those of the last residual pass that kept scores: u = x~, k = p-1
+ * (lfe_resid, lfe_gram_resid), or u = [1, x~, z~], k = p (lfe_resid_iv,
+ * std_errors.py:473-602). */
 int lfe_cluster_meat(lfe_ctx* ctx, double* meats_out, int64_t* G_out);
 
 /* Multi-way CGM subsets on the device (std_errors.py:354-441).  subset_masks[s]

@@ -39,6 +39,7 @@ SIGNATURES = {
     "lfe_demean": (C.c_int, [_vp, _i32p, C.c_double, C.c_int, C.c_int, _i32p, _dp]),
     "lfe_gram": (C.c_int, [_vp, _dp]),
     "lfe_resid": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int]),
+    "lfe_resid_iv": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int]),
     "lfe_gram_resid": (C.c_int, [_vp, _dp, _dp, _dp, _dp, C.c_int]),
     "lfe_cluster_meat": (C.c_int, [_vp, _dp, _i64p]),
     "lfe_cluster_meat_subsets": (C.c_int, [_vp, C.c_int, _vp, _dp, _i64p]),
@@ -225,7 +226,23 @@ class Engine:
         _check(self._lib.lfe_resid(self._h, b.ctypes.data_as(_dp), stats.ctypes.data_as(_dp),
                                    None if meat is None else meat.ctypes.data_as(_dp),
                                    1 if keep_scores else 0))
+        if keep_scores:
+            self._score_k = k
         return stats, (meat[:k, :k] if meat is not None else None)
+
+    def resid_iv(self, coef: np.ndarray, meat: bool = False, keep_scores: bool = False):
+        """IV residual pass (lfe_resid_iv): r = y~ - coef . [1, cols 1..p-1]; returns
+        (stats, p x p meat over u = [1, cols 1..p-1] or None)."""
+        c = np.ascontiguousarray(coef, dtype=np.float64)
+        if c.shape != (self.p,):
+            raise ValueError(f"coef must have p = {self.p} entries")
+        stats = np.zeros(4)
+        M = np.zeros((self.p, self.p)) if meat else None
+        _check(self._lib.lfe_resid_iv(self._h, c.ctypes.data_as(_dp), stats.ctypes.data_as(_dp),
+                                      None if M is None else M.ctypes.data_as(_dp), 1 if keep_scores else 0))
+        if keep_scores:
+            self._score_k = self.p
+        return stats, M
 
     def gram_resid(self, hc1: bool = False, keep_scores: bool = False):
         """Gram + device solve + residual pass in one call (lfe_gram_resid).  Returns
@@ -242,10 +259,12 @@ class Engine:
         if rc == 1:
             return None
         _check(rc)
+        if keep_scores:
+            self._score_k = k
         return G, b, stats, (meat[:k, :k] if hc1 else None)
 
     def cluster_meat(self) -> tuple[np.ndarray, np.ndarray]:
-        k = self.p - 1
+        k = getattr(self, "_score_k", self.p - 1)
         m = self._ncl
         meats = np.zeros(max(m * k * k, 1))
         G = np.zeros(max(m, 1), dtype=np.int64)
@@ -254,7 +273,7 @@ class Engine:
 
     def cluster_meat_subsets(self, subsets) -> tuple[np.ndarray, np.ndarray]:
         """CGM subsets (tuples of loaded cluster column indices) grouped on the device."""
-        k = self.p - 1
+        k = getattr(self, "_score_k", self.p - 1)
         masks = np.array([sum(1 << j for j in s) for s in subsets], dtype=np.int32)
         m = len(masks)
         meats = np.zeros(max(m * k * k, 1))

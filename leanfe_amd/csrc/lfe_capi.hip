@@ -685,9 +685,18 @@ int lfe_resid(lfe_ctx* c, const double* beta_full, double* stats_out, double* hc
   LFE_CTX(c);
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!beta_full || !stats_out) return fail(LFE_EINVAL, "null pointer");
-  if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)(c->p - 1) * c->ld));
+  if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
   PhaseTimer t(c, &c->tm.resid);
-  return launch_resid(c, beta_full, stats_out, hc1_meat, keep_scores);
+  return launch_resid(c, beta_full, stats_out, hc1_meat, keep_scores, 0);
+}
+
+int lfe_resid_iv(lfe_ctx* c, const double* coef, double* stats_out, double* meat_out, int keep_scores) {
+  LFE_CTX(c);
+  if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
+  if (!coef || !stats_out) return fail(LFE_EINVAL, "null pointer");
+  if (keep_scores && !c->scores) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
+  PhaseTimer t(c, &c->tm.resid);
+  return launch_resid(c, coef, stats_out, meat_out, keep_scores, 1);
 }
 
 int lfe_gram_resid(lfe_ctx* c, double* gram_out, double* beta_full_out, double* stats_out, double* hc1_meat,
@@ -695,7 +704,7 @@ int lfe_gram_resid(lfe_ctx* c, double* gram_out, double* beta_full_out, double* 
   LFE_CTX(c);
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!gram_out || !beta_full_out || !stats_out) return fail(LFE_EINVAL, "null pointer");
-  if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)(c->p - 1) * c->ld));
+  if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
   PhaseTimer t(c, &c->tm.resid);
   return launch_gram_resid(c, gram_out, beta_full_out, stats_out, hc1_meat, keep_scores);
 }

@@ -336,7 +336,7 @@ static int owner_meat(lfe_ctx* c, const uint64_t* K, int32_t G, int k, uint64_t 
 
 // meat and cluster count of one subset (mask over the loaded cluster columns)
 static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
-  const int k = c->p - 1;
+  const int k = c->score_k;
   const int64_t n = c->n;
   auto& W = c->clw;
   KeyArgs ka{};
@@ -404,7 +404,7 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
 }
 
 int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, double* meats, int64_t* G_out) {
-  const int k = c->p - 1;
+  const int k = c->score_k;
   const int64_t n = c->n;
   const int m = (int)c->cl.size();
   for (int s = 0; s < n_subsets; ++s)

@@ -35,7 +35,8 @@ struct GramArgs {
   int64_t ld;
   const double* w;
   const double* beta;   // GRAM_RESID: beta_full [p] = {intercept, b_1..b_{p-1}}
-  double* scores;       // GRAM_RESID: optional row-major [ld][p-1] output x~ r (w)
+  double* scores;       // GRAM_RESID: optional row-major [ld][p-1+icpt] output u r (w)
+  int icpt;             // GRAM_RESID: the intercept takes y's slot in the meat / scores (u = [1, x~])
   const double* table;  // GRAM_TABLE: row-major [rows][tcols]
   int64_t rows;         // GRAM_TABLE
   int tcols;
@@ -166,6 +167,7 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
   bool dat[NT];        // lane holds a data column
   double fill[NT];     // DESIGN: value of a non-data column (1 for the intercept)
   double coef[NT];     // RESID: row term y~ - sum_j beta_j x~_j
+  bool one[NT];        // RESID with icpt: this slot is the intercept (value 1 in the meat / scores)
   const double* xb[NT];
 #pragma unroll
   for (int I = 0; I < NT; ++I) {
@@ -176,7 +178,8 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
     xl[I] = xc >= 0 ? xc : 0;
     fill[I] = xc == -1 ? 1.0 : 0.0;
     coef[I] = (MODE == GRAM_RESID) ? (xc == 0 ? 1.0 : (xc >= 1 ? -a.beta[xc] : 0.0)) : 0.0;
-    if (MODE == GRAM_RESID) dat[I] = xc >= 1;  // meat columns
+    one[I] = MODE == GRAM_RESID && a.icpt && xc == 0;
+    if (MODE == GRAM_RESID) dat[I] = xc >= 1 || one[I];  // meat columns
     xb[I] = a.X + (int64_t)xl[I] * a.ld;
   }
   const double beta0 = (MODE == GRAM_RESID) ? a.beta[0] : 0.0;
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
             sc[s] = WT ? res * wv[u][s] : res;
             const double m = WT ? res * sqrt(wv[u][s]) : res;
 #pragma unroll
-            for (int I = 0; I < NT; ++I) z[s][I] = (valid[u][s] && dat[I]) ? xt[s][I] * m : 0.0;
+            for (int I = 0; I < NT; ++I) z[s][I] = (valid[u][s] && dat[I]) ? (one[I] ? 1.0 : xt[s][I]) * m : 0.0;
           }
           if (a.scores) {
             const int gi = gb + u;
@@ -354,10 +357,11 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
             for (int I = 0; I < NT; ++I) {
               if (!dat[I]) continue;
               // row-major [row][k]: the 16 column lanes of a row quad write one contiguous row
-              const int64_t ks = a.la.p - 1;
-              double* dst = a.scores + (int64_t)r * ks + (xl[I] - 1);
-              const d4 v = d4{valid[u][0] ? xt[0][I] * sc[0] : 0.0, valid[u][1] ? xt[1][I] * sc[1] : 0.0,
-                              valid[u][2] ? xt[2][I] * sc[2] : 0.0, valid[u][3] ? xt[3][I] * sc[3] : 0.0};
+              const int64_t ks = a.la.p - 1 + a.icpt;
+              double* dst = a.scores + (int64_t)r * ks + (xl[I] - 1 + a.icpt);
+              d4 v;
+#pragma unroll
+              for (int s = 0; s < 4; ++s) v[s] = valid[u][s] ? (one[I] ? 1.0 : xt[s][I]) * sc[s] : 0.0;
               if (full) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) dst[s * ks] = v[s];
@@ -1018,17 +1022,20 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
   if (hc1)
     for (int e = 0; e < k * k; ++e) hc1[e] = meat[e];
   c->scores_valid = keep_scores != 0;
+  c->score_k = k;
   return LFE_OK;
 }
 
-int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores) {
+int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores, int icpt) {
   GramArgs a = base_args(c);
   LFE_TRY(h2d_small(c, c->dbeta, beta_full, sizeof(double) * c->p));
   a.beta = c->dbeta;
   a.scores = keep_scores ? c->scores : nullptr;
-  const int k = c->p - 1;
+  a.icpt = icpt ? 1 : 0;
+  const int k = c->p - 1 + a.icpt;  // meat / score width
+  c->score_k = k;
   std::vector<double> meat((size_t)std::max(k, 1) * std::max(k, 1));
-  if (resid_rows_ok(c, a)) {
+  if (!icpt && resid_rows_ok(c, a)) {
     a.nq = 1;
     a.qf[0] = 1 - a.la.P;
     a.G_Q = c->fe[a.qf[0]].G;
@@ -1038,8 +1045,9 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
     c->scores_valid = keep_scores != 0;
     return LFE_OK;
   }
-  // staged columns 0..p-1 (col 0 = y, zeroed in the meat); meat = columns 1..p-1
-  const int rc = gram_dispatch<GRAM_RESID>(c, a, c->p, 1, k, meat.data(), stats, 4);
+  // staged columns 0..p-1 (col 0 = y, zeroed in the meat, or the intercept with icpt);
+  // meat = columns 1..p-1, or 0..p-1 with icpt
+  const int rc = gram_dispatch<GRAM_RESID>(c, a, c->p, 1 - a.icpt, k, meat.data(), stats, 4);
   if (rc) return rc;
   if (hc1)
     for (int e = 0; e < k * k; ++e) hc1[e] = meat[e];

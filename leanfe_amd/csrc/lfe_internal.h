@@ -194,9 +194,10 @@ struct lfe_ctx {
   hipEvent_t aux_ev = nullptr;     // completion of an asynchronous D2H into the staging region
   char* hpin_items = nullptr;      // work-item upload staging
   size_t hpin_items_cap = 0;
-  double* scores = nullptr;  // [k][ld] x~ r (w), layout order
+  double* scores = nullptr;  // row-major [ld][score_k] score rows u r (w), layout order (p * ld allocated)
   double* dbeta = nullptr;   // [64] beta_full staging
   bool scores_valid = false;
+  int score_k = 0;           // score width: p - 1 (u = x~), or p with the intercept (IV, u = [1, x~, z~])
   // scratch
   double* scratch = nullptr;     // device partials
   size_t scratch_elems = 0;
@@ -245,7 +246,7 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
 
 // --- Gram / residual / clusters (lfe_gram.hip) ---
 int launch_gram(lfe_ctx* c, double* host_gram);
-int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores);
+int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores, int icpt);
 int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
 // --- device keys (lfe_keys.hip) ---

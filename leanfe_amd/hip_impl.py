@@ -47,8 +47,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         raise ValueError("Must provide either 'formula' or (y_col, x_cols, fe_cols)")
     else:
         factor_vars, interactions, instruments = [], [], []
-    if instruments:
-        raise NotImplementedError("IV/2SLS is not on the hip backend's hot path (SURVEY.md §8f)")
+    instruments = list(instruments or [])
     x_cols = list(x_cols)
     fe_cols = list(fe_cols) if fe_cols is not None else []
     v = vcov.lower()
@@ -57,7 +56,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     if v == "cluster" and cluster_cols is None:
         raise ValueError("cluster_cols required for vcov='cluster'")
 
-    needed = [y_col] + x_cols + fe_cols
+    needed = [y_col] + x_cols + fe_cols + instruments
     for var, _ in factor_vars:
         needed.append(var)
     for var, fac, _ in interactions:
@@ -89,7 +88,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             levels.append(g)
         levels = dist.agree_levels(eng, levels)
         Y = np.asarray(cols[y_col], dtype=np.float64)
-        Xc = [np.asarray(cols[c], dtype=np.float64) for c in x_cols]
+        Xc = [np.asarray(cols[c], dtype=np.float64) for c in x_cols + instruments]  # polars_impl.py:486
         w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
 
         t0 = time.perf_counter()
@@ -113,7 +112,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             elif len(fe_cols) == 1:
                 inferred = "demean"
             else:
-                inferred = determine_strategy(vcov, False, fe_cardinality, max_fe_levels=MAX_FE_LEVELS,
+                inferred = determine_strategy(vcov, bool(instruments), fe_cardinality, max_fe_levels=MAX_FE_LEVELS,
                                               n_obs=n_initial, n_x_cols=len(x_cols),
                                               estimated_compression_ratio=est_comp_ratio)
             say(f"Auto selection: Inferring {inferred} strategy. N = {n_initial:_}, "
@@ -151,6 +150,18 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             raise ValueError(f"Unknown strategy: {strategy}")
 
         k = len(x_cols)
+        df_resid = n_obs - (k + 1) - absorbed_df
+        if instruments:
+            beta, se, n_clusters, rss, stats = _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, fe_cols,
+                                                       sharded, n_obs, df_resid, ssc)
+            timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
+            return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta))),
+                                std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
+                                iterations=iterations, vcov_type=vcov, is_iv=True,
+                                n_instruments=len(instruments), n_clusters=n_clusters, df_resid=df_resid,
+                                formula=formula, fe_cols=fe_cols, fe_dims=fe_dims, r_squared=None,
+                                compression_ratio=est_comp_ratio, rss=rss, tss=None, backend="hip",
+                                timings=timings)
         # Gram + solve + residual pass; one host round trip when the fused path applies
         # (the residuals then use the device's Cholesky solve of the same Gram)
         fused = eng.gram_resid(hc1=(v == "hc1"), keep_scores=(v == "cluster"))
@@ -158,7 +169,6 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         XtX, Xty = inference.split_gram(G)
         beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # polars_impl.py:212-226, host
         beta = beta_full[1:]
-        df_resid = n_obs - (k + 1) - absorbed_df
         Vb = XtX_inv[1:, 1:]
         if fused is not None:
             stats, meat = fused[2], fused[3]
@@ -171,23 +181,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         elif v == "hc1":
             se = inference.se_hc1(Vb, meat, n_obs, df_resid)
         else:
-            cl_codes, cl_levels = [], []
-            for c in cluster_cols:
-                cc, gg = frame.factorize(cols[c], global_codes=sharded)
-                cl_codes.append(cc)
-                cl_levels.append(gg)
-            cl_levels = dist.agree_levels(eng, cl_levels)
-            if len(cluster_cols) == 1:
-                eng.load_clusters(cl_codes, cl_levels)
-                meats, Gs = eng.cluster_meat()
-                se, n_clusters = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, ssc)
-            else:
-                # intersections are formed and grouped on the device (std_errors.py:399-408)
-                subsets = inference.cluster_subsets(len(cluster_cols))
-                eng.load_clusters(cl_codes, cl_levels)
-                meats, Gs = eng.cluster_meat_subsets(subsets)
-                se, n_clusters = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets,
-                                                               n_obs, df_resid, ssc)
+            se, n_clusters = _cluster_se(eng, cols, cluster_cols, sharded, Vb, lambda M: M, n_obs, df_resid, ssc)
         tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
         r_squared = 1 - rss / tss if tss > 0 else None
         timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
@@ -203,3 +197,51 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                         n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
                         fe_dims=fe_dims, r_squared=r_squared, compression_ratio=est_comp_ratio,
                         rss=rss, tss=tss, backend="hip", timings=timings)
+
+
+def _cluster_se(eng, cols, cluster_cols, sharded, Vb, to_meat, n_obs, df_resid, ssc):
+    """One-way (std_errors.py:289-347) or CGM multi-way (:354-441) SEs from the device's
+    score meats; ``to_meat`` maps a device meat to the estimator's space (identity for
+    OLS, gamma' M_Z gamma for IV, :473-602)."""
+    cl_codes, cl_levels = [], []
+    for c in cluster_cols:
+        cc, gg = frame.factorize(cols[c], global_codes=sharded)
+        cl_codes.append(cc)
+        cl_levels.append(gg)
+    cl_levels = dist.agree_levels(eng, cl_levels)
+    eng.load_clusters(cl_codes, cl_levels)
+    if len(cluster_cols) == 1:
+        meats, Gs = eng.cluster_meat()
+        return inference.se_cluster_oneway(Vb, to_meat(meats[0]), int(Gs[0]), n_obs, df_resid, ssc)
+    # intersections are formed and grouped on the device (std_errors.py:399-408)
+    subsets = inference.cluster_subsets(len(cluster_cols))
+    meats, Gs = eng.cluster_meat_subsets(subsets)
+    return inference.se_cluster_multiway(Vb, [to_meat(M) for M in meats], [int(g) for g in Gs], subsets,
+                                         n_obs, df_resid, ssc)
+
+
+def _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, fe_cols, sharded, n_obs, df_resid, ssc):
+    """IV/2SLS branch of ``_run_regression`` (polars_impl.py:176-200, 229, 254-270):
+    the device Gram of [1, y~, x~, z~] -> host 2SLS (inference.IVSystem) -> one device
+    residual pass r = y~ - X_hat beta_full with u = [1, x~, z~] meats / scores -> the
+    reference's IV SEs (std_errors.py:448-602), intercept stripped."""
+    k, m = len(x_cols), len(instruments)
+    G = eng.gram()
+    # polars_impl.py:180: a Z column of all ones stops the intercept from being added.
+    # Demeaned instruments cannot be all ones; without FEs they are the raw columns.
+    z_has_ones = not fe_cols and any(np.allclose(np.asarray(cols[z], dtype=np.float64), 1.0)
+                                     for z in instruments)
+    iv = inference.IVSystem(G, k, m, z_has_ones=z_has_ones)
+    stats, meat_u = eng.resid_iv(iv.coef, meat=(v == "hc1"), keep_scores=(v == "cluster"))
+    n_clusters = None
+    XtX_inv = iv.XtX_inv
+    if v == "iid":
+        se = inference.se_iid(XtX_inv, stats[0], df_resid)
+    elif v == "hc1":
+        se = inference.se_hc1(XtX_inv, iv.xhat_meat(meat_u), n_obs, df_resid)
+    else:
+        se, n_clusters = _cluster_se(eng, cols, cluster_cols, sharded, XtX_inv, iv.xhat_meat, n_obs, df_resid, ssc)
+    strip = len(iv.beta_full) == k + 1
+    beta = iv.beta_full[1:] if strip else iv.beta_full
+    se = se[1:] if strip else se
+    return beta, se, n_clusters, float(stats[1]), stats

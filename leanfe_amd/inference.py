@@ -10,6 +10,9 @@ keeps them call-for-call identical to the reference.
 * HC1 .......... std_errors.py:275-282
 * one-way ...... std_errors.py:335-347
 * multi-way .... std_errors.py:395-441 (Cameron-Gelbach-Miller, G_min rule)
+* IV / 2SLS .... polars_impl.py:176-198 + common.py:188-287 (first and second
+                 stage from the device Gram of [1, y, x, z]), std_errors.py:448-602
+                 (the X_hat meats as gamma' M_Z gamma of the device's Z-space meats)
 """
 from __future__ import annotations
 
@@ -76,3 +79,49 @@ def se_cluster_multiway(XtX_inv_b, meats: list[np.ndarray], Gs: list[int], subse
     if ssc:
         V *= (n_obs - 1) / df_resid
     return np.sqrt(np.maximum(np.diag(V), 0.0)), tuple(first)
+
+
+class IVSystem:
+    """2SLS from the (p+1)^2 device Gram of [1, y~, x~_1..x~_k, z~_1..z~_m]
+    (sqrt(w) rows when weighted), as ``_run_regression`` + ``iv_2sls`` do it with the
+    n-row matrices (polars_impl.py:176-198, common.py:188-287):
+
+        Z = [1, z~] when X = [1, x~] is wider than z~ and no z column is all ones
+            (polars_impl.py:179-181; ``z_has_ones`` is that test, done by the caller)
+        gamma = (Z'Z)^-1 Z'X,  X_hat = Z gamma,  beta_full = (X_hat'X_hat)^-1 X_hat'y
+        XtX_inv = (X_hat'X_hat)^-1 by Cholesky (:185-198)
+
+    Every X_hat-space product is gamma' (Z-space product) gamma, so the device only
+    ever forms Z-space sums.  ``coef`` is X_hat beta_full = Z (gamma beta_full) as a
+    coefficient vector over u = [1, col_1..col_{p-1}] for ``lfe_resid_iv``.
+    """
+
+    def __init__(self, G: np.ndarray, k: int, m: int, z_has_ones: bool = False):
+        x_idx = [0] + list(range(2, 2 + k))
+        z_idx = list(range(2 + k, 2 + k + m))
+        if len(x_idx) > len(z_idx) and not z_has_ones:
+            z_idx = [0] + z_idx
+        if len(z_idx) < len(x_idx):
+            raise ValueError(f"Under-identified: {len(z_idx)} instruments for {len(x_idx)} endogenous variables")
+        self.k, self.m = k, m
+        ZtZ = G[np.ix_(z_idx, z_idx)]
+        ZtX = G[np.ix_(z_idx, x_idx)]
+        Zty = G[z_idx, 1]
+        self.gamma = np.linalg.solve(ZtZ, ZtX)                  # common.py:264-266
+        XhtXh = self.gamma.T @ ZtZ @ self.gamma
+        self.beta_full = np.linalg.solve(XhtXh, self.gamma.T @ Zty)  # :269-272
+        try:                                                     # polars_impl.py:192-198
+            L = np.linalg.cholesky(XhtXh)
+            self.XtX_inv = np.linalg.solve(L.T, np.linalg.solve(L, np.eye(L.shape[0])))
+        except np.linalg.LinAlgError:
+            self.XtX_inv = np.linalg.inv(XhtXh)
+        # Z columns as positions in u = [1, col_1..col_{p-1}] (Gram index - 1; intercept 0)
+        self.z_u = [0 if j == 0 else j - 1 for j in z_idx]
+        p = 1 + k + m
+        self.coef = np.zeros(p)
+        self.coef[self.z_u] = self.gamma @ self.beta_full
+
+    def xhat_meat(self, meat_u: np.ndarray) -> np.ndarray:
+        """X_hat' D X_hat from the device's u-space meat u' D u (or S'S of u-scores)."""
+        Mz = meat_u[np.ix_(self.z_u, self.z_u)]
+        return self.gamma.T @ Mz @ self.gamma

@@ -23,6 +23,8 @@ reference repo ``jorgenhost/leanfe``):
 * HC1 ....................... std_errors.py:217-282
 * one-way cluster ........... std_errors.py:289-347
 * multi-way CGM ............. std_errors.py:354-441
+* IV / 2SLS ................. polars_impl.py:176-200, 229, 234-270; common.py:188-287;
+                              std_errors.py:448-602 (HC1 / one-way / multi-way on X_hat)
 
 Pinning: ``tests/golden/make_golden.py`` checks this restatement against the
 reference's own importable NumPy/SciPy functions (exact LSDV solve in
@@ -246,12 +248,77 @@ def run_regression(Y, Xdm, w, vcov, cl_cols, ssc, n_obs, absorbed_df):
                 n_clusters=ncl, r_squared=r2, XtX=XtX, Xty=Xty, XtX_inv=XtX_inv, rss=rss, tss=tss)
 
 
+def iv_2sls(Y, X, Z, w):
+    """common.py:188-287: first stage X = Z gamma (weighted normal equations with
+    sqrt(w) rows, X_hat = Z gamma unweighted), second stage on X_hat."""
+    if Z.shape[1] < X.shape[1]:
+        raise ValueError(f"Under-identified: {Z.shape[1]} instruments for {X.shape[1]} endogenous variables")
+    if w is not None:
+        sw = np.sqrt(w)
+        Zw, Xw, Yw = Z * sw[:, None], X * sw[:, None], Y * sw
+    else:
+        Zw, Xw, Yw = Z, X, Y
+    gamma = np.linalg.solve(Zw.T @ Zw, Zw.T @ Xw)
+    X_hat = Z @ gamma
+    Xhw = X_hat * sw[:, None] if w is not None else X_hat
+    beta = np.linalg.solve(Xhw.T @ Xhw, Xhw.T @ Yw)
+    return beta, X_hat
+
+
+def run_regression_iv(Y, Xdm, Zdm, w, vcov, cl_cols, ssc, n_obs, absorbed_df):
+    """``_run_regression`` IV branch, polars_impl.py:176-200 (intercept added to Z
+    when X is wider and no Z column is all ones, :179-181), residual on X_hat
+    (:229, as the reference computes it), SEs on X_hat with the full XtX_inv
+    (:254-270 -> std_errors.py:86-141, 448-602), intercept stripped."""
+    n, k = Xdm.shape
+    X = np.hstack([np.ones((n, 1)), Xdm]) if k > 0 else np.ones((n, 1))
+    Z = Zdm
+    if X.shape[1] > Z.shape[1] and not any(np.allclose(col, 1.0) for col in Z.T):
+        Z = np.column_stack([np.ones(n), Z])
+    beta_full, X_hat = iv_2sls(Y, X, Z, w)
+    if w is not None:
+        Xhw = X_hat * np.sqrt(w)[:, None]
+        XtX = Xhw.T @ Xhw
+    else:
+        XtX = X_hat.T @ X_hat
+    try:
+        L = np.linalg.cholesky(XtX)
+        XtX_inv = np.linalg.solve(L.T, np.linalg.solve(L, np.eye(L.shape[0])))
+    except np.linalg.LinAlgError:
+        XtX_inv = np.linalg.inv(XtX)
+    resid = Y - X_hat @ beta_full
+    df_resid = n_obs - (k + 1) - absorbed_df
+    v = vcov.lower()
+    if v == "iid":
+        se, ncl = se_iid(XtX_inv, resid, w, df_resid)
+    elif v == "hc1":
+        se, ncl = se_hc1(X_hat, XtX_inv, resid, w, n_obs, df_resid)
+    elif v == "cluster":
+        if cl_cols is None:
+            raise ValueError("cluster_cols required for vcov='cluster'")
+        if len(cl_cols) == 1:
+            se, ncl = se_cluster_oneway(X_hat, XtX_inv, resid, w, factorize(cl_cols[0])[0],
+                                        n_obs, df_resid, ssc)
+        else:
+            se, ncl = se_cluster_multiway(X_hat, XtX_inv, resid, w, cl_cols, n_obs, df_resid, ssc)
+    else:
+        raise ValueError(f"Unknown vcov type: {vcov}")
+    strip = X.shape[1] == k + 1
+    return dict(beta=beta_full[1:] if strip else beta_full, beta_full=beta_full,
+                se=se[1:] if strip else se, resid=resid, df_resid=df_resid, n_clusters=ncl,
+                r_squared=None, XtX=XtX, XtX_inv=XtX_inv, Z_cols=Z.shape[1],
+                rss=float(np.sum(resid ** 2)), tss=None)
+
+
 def fit(data: dict, y: str, xs: list[str], fes: list[str], *, strategy: str = "alt_proj",
         weights: str | None = None, demean_tol: float = 1e-6, max_iter: int = 50,
         vcov: str = "iid", cluster_cols: list[str] | None = None, ssc: bool = True,
-        trace: list | None = None) -> dict:
+        instruments: list[str] | None = None, trace: list | None = None) -> dict:
     """The alt_proj / demean branch of ``leanfe_polars`` (polars_impl.py:424-579)
-    on a dict of NumPy columns.  Returns a plain dict of results."""
+    on a dict of NumPy columns.  Returns a plain dict of results.  With
+    ``instruments`` the columns ``[y] + xs + instruments`` are demeaned
+    (:431, :486) and the IV branch of ``_run_regression`` runs."""
+    instruments = list(instruments or [])
     if strategy not in ("alt_proj", "demean"):
         raise ValueError(f"oracle supports alt_proj/demean, got {strategy}")
     if strategy == "demean" and len(fes) != 1:
@@ -263,7 +330,7 @@ def fit(data: dict, y: str, xs: list[str], fes: list[str], *, strategy: str = "a
     card = [G for _, G in fac]  # fe_cardinality, polars_impl.py:373 (pre-filter)
     keep = singleton_keep(codes, card)
     sel = lambda a: np.asarray(a)[keep]
-    cols = np.stack([sel(data[c]).astype(np.float64) for c in [y] + xs])
+    cols = np.stack([sel(data[c]).astype(np.float64) for c in [y] + xs + instruments])
     codes_k = [c[keep] for c in codes]
     w = sel(data[weights]).astype(np.float64) if weights else None
     if strategy == "demean":
@@ -277,7 +344,12 @@ def fit(data: dict, y: str, xs: list[str], fes: list[str], *, strategy: str = "a
     absorbed_df = sum(fe_dims) - len(fes)                        # :535 (demean: G-1, :463)
     n_obs = int(keep.sum())
     cl = [sel(data[c]) for c in cluster_cols] if cluster_cols else None
-    reg = run_regression(cols[0], cols[1:].T.copy(), w, vcov, cl, ssc, n_obs, absorbed_df)
+    k = len(xs)
+    if instruments:
+        reg = run_regression_iv(cols[0], cols[1:1 + k].T.copy(), cols[1 + k:].T.copy(), w, vcov, cl, ssc,
+                                n_obs, absorbed_df)
+    else:
+        reg = run_regression(cols[0], cols[1:].T.copy(), w, vcov, cl, ssc, n_obs, absorbed_df)
     reg.update(n_obs=n_obs, iterations=iterations, fe_dims=fe_dims,
                absorbed_df=absorbed_df, keep=keep, demeaned=cols)
     return reg

@@ -71,7 +71,8 @@ def load_reference():
     sys.modules["leanfe"] = pkg
     compress = importlib.import_module("leanfe.compress")
     std_errors = importlib.import_module("leanfe.std_errors")
-    return compress, std_errors
+    common = importlib.import_module("leanfe.common")
+    return compress, std_errors, common
 
 
 def lsdv_reference(compress, data, y, xs, fes, keep, vcov, cluster_cols, ssc, n_obs, df_resid):
@@ -169,6 +170,27 @@ def fx_panel(seed=7, n=20000, L=(400, 30), k=3, singletons=25, weights=False, cl
     return d
 
 
+def fx_iv(seed=21, n=20000, L=(400, 30), weights=False):
+    """IV panel: x1 endogenous (shares the shock u with y), z1 its instrument,
+    x2 exogenous (its own instrument, as the reference's Z holds only the listed
+    instruments, polars_impl.py:178)."""
+    rng = np.random.default_rng(seed)
+    codes = [rng.integers(0, G, n) for G in L]
+    codes[0][:20] = L[0] + np.arange(20)  # singletons
+    eff = [rng.normal(0, 1.0, G + 20) for G in L]
+    u = rng.normal(0, 1, n)
+    z1 = rng.normal(0, 1, n) + 0.5 * eff[0][codes[0]]
+    x2 = rng.normal(0, 1, n) - 0.3 * eff[-1][codes[-1]]
+    x1 = 0.9 * z1 + 0.3 * x2 + 0.7 * u + 0.4 * eff[-1][codes[-1]] + rng.normal(0, 0.5, n)
+    y = 1.5 * x1 - 0.5 * x2 + u + sum(e[c] for e, c in zip(eff, codes))
+    d = {"y": y, "x1": x1, "x2": x2, "z1": z1, "cl1": rng.integers(0, 60, n), "cl2": rng.integers(0, 45, n)}
+    for f, c in enumerate(codes):
+        d[f"fe{f + 1}"] = c
+    if weights:
+        d["w"] = rng.uniform(0.5, 2.0, n)
+    return d
+
+
 def fx_synth(n=20000, k=4, L=(500, 40)):
     return synth.panel(n, k, list(L), seed=12345)
 
@@ -206,12 +228,67 @@ WEIGHTED = [
 ]
 
 
-def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight):
+# IV/2SLS (polars_impl.py:176-270): just-identified designs (instruments = x count,
+# so an intercept joins Z, :179-181).  The 2SLS algebra and the IV SEs are pinned by
+# the reference's own common.iv_2sls and std_errors._compute_se_*_iv run on the
+# oracle's demeaned columns; the demeaning itself is pinned by the LSDV cases above.
+IV = [
+    # name, recipe, y, xs, fes, strategy, weights, vcov, cluster_cols, instruments
+    ("iv_iid", fx_iv, "y", ["x1", "x2"], ["fe1", "fe2"], "alt_proj", None, "iid", None, ["z1", "x2"]),
+    ("iv_hc1", fx_iv, "y", ["x1", "x2"], ["fe1", "fe2"], "alt_proj", None, "HC1", None, ["z1", "x2"]),
+    ("iv_cl1", fx_iv, "y", ["x1", "x2"], ["fe1", "fe2"], "alt_proj", None, "cluster", ["cl1"], ["z1", "x2"]),
+    ("iv_cl2", fx_iv, "y", ["x1", "x2"], ["fe1", "fe2"], "alt_proj", None, "cluster", ["cl1", "cl2"],
+     ["z1", "x2"]),
+    ("iv_w_hc1", lambda: fx_iv(seed=23, weights=True), "y", ["x1", "x2"], ["fe1", "fe2"], "alt_proj", "w",
+     "HC1", None, ["z1", "x2"]),
+    ("iv_demean_cl1", lambda: fx_iv(seed=25, L=(500,)), "y", ["x1"], ["fe1"], "demean", None, "cluster",
+     ["cl1"], ["z1"]),
+]
+
+
+def iv_reference(std_errors, common, orc, data, weights, vcov, cl, ssc=True):
+    """2SLS + SEs of the oracle's demeaned columns by the reference's own functions
+    (common.iv_2sls, std_errors._compute_se_hc1_iv / _cluster_oneway_iv /
+    _cluster_multiway_iv); XtX_inv as polars_impl.py:185-198, IID as std_errors.py:196-210."""
+    keep = orc["keep"]
+    cols = orc["demeaned"]
+    k = len(orc["beta"])
+    n = cols.shape[1]
+    Y = cols[0]
+    X = np.hstack([np.ones((n, 1)), cols[1:1 + k].T])
+    Z = cols[1 + k:].T
+    if X.shape[1] > Z.shape[1] and not any(np.allclose(c, 1.0) for c in Z.T):
+        Z = np.column_stack([np.ones(n), Z])
+    w = np.asarray(data[weights])[keep].astype(np.float64) if weights else None
+    beta_full, X_hat = common.iv_2sls(Y, X, Z, w)
+    Xh = X_hat * np.sqrt(w)[:, None] if w is not None else X_hat
+    L = np.linalg.cholesky(Xh.T @ Xh)
+    XtX_inv = np.linalg.solve(L.T, np.linalg.solve(L, np.eye(L.shape[0])))
+    resid = Y - X_hat @ beta_full
+    n_obs, df_resid = orc["n_obs"], orc["df_resid"]
+    v = vcov.lower()
+    ncl = None
+    if v == "iid":
+        s2 = float(np.sum((w if w is not None else 1.0) * resid ** 2)) / df_resid
+        se = np.sqrt(np.maximum(s2 * np.diag(XtX_inv), 0.0))
+    elif v == "hc1":
+        se, _ = std_errors._compute_se_hc1_iv(XtX_inv, resid, X_hat, w, n_obs, df_resid)
+    elif len(cl) == 1:
+        ids = np.asarray(data[cl[0]])[keep]
+        se, ncl = std_errors._compute_se_cluster_oneway_iv(XtX_inv, resid, X_hat, w, ids, n_obs, df_resid, ssc)
+    else:
+        ids = np.stack([np.asarray(data[c])[keep] for c in cl], axis=1)
+        se, ncl = std_errors._compute_se_cluster_multiway_iv(XtX_inv, resid, X_hat, w, ids, n_obs, df_resid, ssc)
+    return np.asarray(beta_full[1:]), np.asarray(se[1:]), ncl
+
+
+def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=None):
     arrays = {f"in_{c}": np.asarray(v) for c, v in data.items()}
     meta = dict(name=name, y=y, xs=xs, fes=fes, strategy=strategy, weights=weights, vcov=vcov,
+                instruments=instruments or [],
                 cluster_cols=cl, demean_tol=1e-6, max_iter=50, ssc=True,
                 oracle_n_clusters=orc["n_clusters"], ref_n_clusters=ref[2] if ref else None,
-                pinned="reference-lsdv" if ref else "oracle-only")
+                pinned=("reference-iv" if instruments else "reference-lsdv") if ref else "oracle-only")
     arrays.update(
         oracle_beta=orc["beta"], oracle_se=orc["se"], oracle_iterations=np.int64(orc["iterations"]),
         oracle_n_obs=np.int64(orc["n_obs"]), oracle_df_resid=np.int64(orc["df_resid"]),
@@ -230,7 +307,7 @@ def _json_ncl(v):
 
 
 def main():
-    compress, _ = load_reference()
+    compress, std_errors, common = load_reference()
     worst = 0.0
     for name, recipe, y, xs, fes, strategy, weights, vcov, cl in CASES + WEIGHTED:
         data = recipe()
@@ -254,6 +331,23 @@ def main():
             print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} (oracle-pinned, weighted)")
         _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight)
     print(f"worst tight-oracle vs reference-LSDV relative deviation: {worst:.2e}")
+    worst = 0.0
+    for name, recipe, y, xs, fes, strategy, weights, vcov, cl, inst in IV:
+        data = recipe()
+        orc = altproj.fit(data, y, xs, fes, strategy=strategy, weights=weights, vcov=vcov,
+                          cluster_cols=cl, instruments=inst)
+        tight = altproj.fit(data, y, xs, fes, strategy=strategy, weights=weights, vcov=vcov,
+                            cluster_cols=cl, instruments=inst, demean_tol=1e-14, max_iter=100000)
+        ref = iv_reference(std_errors, common, orc, data, weights, vcov, cl)
+        rb = np.max(np.abs(orc["beta"] - ref[0]) / np.abs(ref[0]))
+        rs = np.max(np.abs(orc["se"] - ref[1]) / np.abs(ref[1]))
+        assert rb < 1e-11 and rs < 1e-11, (name, rb, rs)
+        assert _json_ncl(ref[2]) == _json_ncl(orc["n_clusters"]), (name, ref[2], orc["n_clusters"])
+        worst = max(worst, rb, rs)
+        print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} df={orc['df_resid']:6d} "
+              f"oracle-vs-ref IV beta {rb:.1e} se {rs:.1e}")
+        _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=inst)
+    print(f"worst oracle vs reference IV relative deviation: {worst:.2e}")
 
 
 if __name__ == "__main__":

@@ -15,8 +15,16 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-10
 
 
+def _formula(y, xs, fes, inst):
+    return f"{y} ~ {' + '.join(xs)} | {' + '.join(fes)} | {' + '.join(inst)}"
+
+
 def _hip_fit(meta, data, **kw):
     from leanfe_amd import leanfe_hip
+    if meta.get("instruments"):  # IV enters through the formula only, as in leanfe_polars (:311-319)
+        return leanfe_hip(data, formula=_formula(meta["y"], meta["xs"], meta["fes"], meta["instruments"]),
+                          strategy=meta["strategy"], weights=meta["weights"], vcov=meta["vcov"],
+                          cluster_cols=meta["cluster_cols"], ssc=meta["ssc"], quiet=True, **kw)
     return leanfe_hip(data, y_col=meta["y"], x_cols=meta["xs"], fe_cols=meta["fes"], strategy=meta["strategy"],
                       weights=meta["weights"], vcov=meta["vcov"], cluster_cols=meta["cluster_cols"],
                       ssc=meta["ssc"], quiet=True, **kw)
@@ -40,7 +48,10 @@ def test_golden_fixture(name):
     r = _hip_fit(meta, data, demean_tol=meta["demean_tol"], max_iter=meta["max_iter"])
     _assert_same(r, exp["oracle_beta"], exp["oracle_se"], int(exp["oracle_n_obs"]), int(exp["oracle_iterations"]),
                  int(exp["oracle_df_resid"]), exp["oracle_fe_dims"].tolist(), meta["oracle_n_clusters"], meta["xs"])
-    if "ref_beta" in exp:  # the reference's exact LSDV values, up to alt-proj convergence error
+    if meta.get("instruments"):  # the reference's own 2SLS / IV SE functions on the same demeaned columns
+        assert r.is_iv and r.n_instruments == len(meta["instruments"]) and r.r_squared is None
+        np.testing.assert_allclose([r.std_errors[x] for x in meta["xs"]], exp["ref_se"], rtol=RTOL, atol=0)
+    elif "ref_beta" in exp:  # the reference's exact LSDV values, up to alt-proj convergence error
         b = np.array([r.coefs[x] for x in meta["xs"]])
         np.testing.assert_allclose(b, exp["ref_beta"], rtol=1e-7, atol=0)
 
@@ -126,3 +137,68 @@ def test_bad_codes_rejected():
     with Engine(0) as eng:
         with pytest.raises(ValueError):
             eng.load([np.zeros(4)], [np.array([0, 1, 5, 0], dtype=np.int32)], [3])
+
+
+def _iv_panel(seed, n, L, k, m, weights=False):
+    """k regressors (x1 endogenous), m >= k - 1 instruments (z1 plus the exogenous x2..xk)."""
+    data = synth.panel(n, k, list(L), seed=seed)
+    rng = np.random.default_rng(seed)
+    u = rng.normal(0, 1, n)
+    data["z1"] = rng.normal(0, 1, n) + 0.3 * data["x2"]
+    data["x1"] = data["x1"] + 0.8 * data["z1"] + 0.6 * u
+    data["y"] = data["y"] + 0.6 * data["x1"] + u
+    if weights:
+        data["w"] = rng.uniform(0.5, 2.0, n)
+    data["cl1"] = rng.integers(0, 97, n)
+    inst = ["z1"] + [f"x{j + 1}" for j in range(1, k)]
+    return data, inst[:m]
+
+
+@pytest.mark.parametrize("seed,n,L,k,vcov,weights", [
+    (31, 300_000, (20000, 300), 3, "HC1", False),      # two-FE IV, general Gram + IV residual pass
+    (32, 200_001, (5000, 200, 30), 4, "cluster", False),  # three FEs, one-way cluster on u = [1, x, z] scores
+    (33, 150_000, (3000, 60), 2, "iid", True),          # weighted first and second stage
+    (34, 250_000, (8000, 90), 3, "cluster", True),      # two-way CGM, weighted scores
+])
+def test_iv_panels_vs_oracle(seed, n, L, k, vcov, weights):
+    data, inst = _iv_panel(seed, n, L, k, k)
+    if weights:
+        data["w"] = np.random.default_rng(seed + 1).uniform(0.5, 2.0, n)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(L))]
+    cl = (["cl1"] if seed != 34 else ["cl1", "fe2"]) if vcov == "cluster" else None
+    w = "w" if weights else None
+    o = altproj.fit(data, "y", xs, fes, vcov=vcov, cluster_cols=cl, weights=w, instruments=inst)
+    from leanfe_amd import leanfe_hip
+    r = leanfe_hip(data, formula=_formula("y", xs, fes, inst), strategy="alt_proj", vcov=vcov, cluster_cols=cl,
+                   weights=w, quiet=True)
+    assert r.is_iv
+    _assert_same(r, o["beta"], o["se"], o["n_obs"], o["iterations"], o["df_resid"], o["fe_dims"],
+                 o["n_clusters"], xs)
+
+
+def test_iv_without_fixed_effects():
+    """IV with no FE part: strategy 'ols', the raw columns (polars_impl.py:176-198 on
+    undemeaned data); an all-ones instrument column suppresses the added intercept."""
+    from leanfe_amd import leanfe_hip
+    data, inst = _iv_panel(35, 50_000, (100, 10), 2, 2)
+    r = leanfe_hip(data, formula="y ~ x1 + x2 | | z1 + x2", strategy="ols", vcov="HC1", quiet=True)
+    Y = data["y"]
+    X = np.column_stack([np.ones(Y.size), data["x1"], data["x2"]])
+    Z = np.column_stack([np.ones(Y.size), data["z1"], data["x2"]])
+    o = altproj.run_regression_iv(Y, X[:, 1:], Z[:, 1:], None, "HC1", None, True, Y.size, 0)
+    np.testing.assert_allclose([r.coefs["x1"], r.coefs["x2"]], o["beta"], rtol=RTOL, atol=0)
+    np.testing.assert_allclose([r.std_errors["x1"], r.std_errors["x2"]], o["se"], rtol=RTOL, atol=0)
+    data["one"] = np.ones(Y.size)
+    r1 = leanfe_hip(data, formula="y ~ x1 + x2 | | one + z1 + x2", strategy="ols", vcov="iid", quiet=True)
+    o1 = altproj.run_regression_iv(Y, X[:, 1:], Z, None, "iid", None, True, Y.size, 0)
+    assert o1["Z_cols"] == 3  # no second intercept
+    np.testing.assert_allclose([r1.coefs["x1"], r1.coefs["x2"]], o1["beta"], rtol=RTOL, atol=0)
+    np.testing.assert_allclose([r1.std_errors["x1"], r1.std_errors["x2"]], o1["se"], rtol=RTOL, atol=0)
+
+
+def test_iv_under_identified_raises():
+    from leanfe_amd import leanfe_hip
+    data, _ = _iv_panel(36, 20_000, (100, 10), 3, 1)
+    with pytest.raises(ValueError, match="Under-identified"):
+        leanfe_hip(data, formula="y ~ x1 + x2 + x3 | fe1 + fe2 | z1", strategy="alt_proj", quiet=True)

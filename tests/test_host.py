@@ -176,3 +176,34 @@ def test_library_loads_and_exports_every_symbol():
         assert hasattr(lib, name), name
     lib.lfe_version.restype = ctypes.c_char_p
     assert b"gfx950" in lib.lfe_version()
+
+
+@pytest.mark.parametrize("weighted,z_ones", [(False, False), (True, False), (False, True)])
+def test_iv_system_matches_oracle_2sls(weighted, z_ones):
+    """inference.IVSystem (2SLS from the (p+1)^2 Gram of [1, y, x, z] plus the u-space
+    meat transform) == the oracle's restatement of polars_impl.py:176-198 +
+    common.py:188-287 + std_errors.py:448-470 on the same columns."""
+    from leanfe_amd import inference
+    from oracle import altproj
+    rng = np.random.default_rng(5)
+    n, k, m = 4000, 2, 2
+    X = rng.normal(size=(n, k))
+    Z = np.column_stack([X[:, 1], rng.normal(size=n) + 0.5 * X[:, 0]])
+    if z_ones:
+        Z = np.column_stack([np.ones(n), Z])
+        m = 3
+    y = X @ np.array([1.0, -0.5]) + rng.normal(size=n)
+    w = rng.uniform(0.5, 2.0, n) if weighted else None
+    o = altproj.run_regression_iv(y, X, Z, w, "HC1", None, True, n, 0)
+    D = np.column_stack([np.ones(n), y, X, Z])
+    Dw = D * np.sqrt(w)[:, None] if weighted else D
+    iv = inference.IVSystem(Dw.T @ Dw, k, m, z_has_ones=z_ones)
+    np.testing.assert_allclose(iv.beta_full, o["beta_full"], rtol=1e-12)
+    np.testing.assert_allclose(iv.XtX_inv, o["XtX_inv"], rtol=1e-10)
+    u = np.column_stack([np.ones(n), X, Z])
+    r = y - u @ iv.coef
+    np.testing.assert_allclose(r, o["resid"], rtol=1e-10, atol=1e-12)
+    s = r ** 2 * (w if weighted else 1.0)
+    meat_u = u.T @ (u * s[:, None])
+    se = inference.se_hc1(iv.XtX_inv, iv.xhat_meat(meat_u), n, n - (k + 1))
+    np.testing.assert_allclose(se[1:], o["se"], rtol=1e-10)

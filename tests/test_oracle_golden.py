@@ -16,7 +16,7 @@ CASES = names()
 def _fit(meta, data, **kw):
     return altproj.fit(data, meta["y"], meta["xs"], meta["fes"], strategy=meta["strategy"],
                        weights=meta["weights"], vcov=meta["vcov"], cluster_cols=meta["cluster_cols"],
-                       ssc=meta["ssc"], **kw)
+                       ssc=meta["ssc"], instruments=meta.get("instruments"), **kw)
 
 
 def test_fixture_count():
@@ -53,6 +53,18 @@ def test_default_tolerance_close_to_reference(name):
     meta, data, exp = load(name)
     np.testing.assert_allclose(exp["oracle_beta"], exp["ref_beta"], rtol=1e-7, atol=0)
     np.testing.assert_allclose(exp["oracle_se"], exp["ref_se"], rtol=1e-7, atol=0)
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if load(n)[0]["pinned"] == "reference-iv"])
+def test_oracle_iv_matches_reference_functions(name):
+    """IV/2SLS: the oracle's 2SLS and IV SEs == the reference's own common.iv_2sls and
+    std_errors._compute_se_*_iv evaluated on the same demeaned columns."""
+    meta, data, exp = load(name)
+    assert meta["instruments"]
+    r = _fit(meta, data, demean_tol=meta["demean_tol"], max_iter=meta["max_iter"])
+    np.testing.assert_allclose(r["beta"], exp["ref_beta"], rtol=1e-11, atol=0)
+    np.testing.assert_allclose(r["se"], exp["ref_se"], rtol=1e-11, atol=0)
+    assert ncl(r["n_clusters"]) == ncl(meta["ref_n_clusters"])
 
 
 def test_singleton_rule_is_single_pass():
