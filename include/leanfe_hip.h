@@ -77,6 +77,25 @@ int lfe_synth_load(lfe_ctx* ctx, int64_t n, int k, int n_fe, const int32_t* n_le
 int lfe_load_clusters(lfe_ctx* ctx, int m, const int32_t* const* cl_codes,
                       const int32_t* cl_levels, int where);
 
+/* YOCO compression (compress.py:282-358): group the loaded rows
+ * by every regressor (columns 1..p-1, exact f64 values; -0.0 == 0.0, NaNs alike), FE
+ * code and loaded cluster column, and replace them in the context by one record per
+ * group: column 0 = _mean_y = _sum_y / _n, the key columns, weight _n = count (or
+ * sum w), and the record's _sum_y / _sum_y_sq kept on the device.  *n_records_out =
+ * number of records (n_compressed).  The context is then in records mode:
+ *   - lfe_drop_singletons keeps every record (compress has no singleton drop);
+ *     fe_card = fe_dims = levels present;
+ *   - lfe_demean runs weighted projections and stops when the weighted group means of
+ *     y~ are below tol or no longer decrease (20 checks without a new minimum): the
+ *     FWL form of the exact LSDV solve (build_design_matrix + solve_wls, :503-747);
+ *   - lfe_resid returns stats_out[0] = sum_g rss_g with rss_g = _sum_y_sq -
+ *     2 fit_g _sum_y + _n fit_g^2 (compute_rss_grouped, :754-811), the HC1 meat
+ *     sum_g rss_g x~_g x~_g' (:907-919) and scores x~_g e_g, e_g = _sum_y - _n fit_g
+ *     (:1118-1124), fit_g = _mean_y - r_g; lfe_resid_iv likewise with u = [1, x]
+ *     (records without FEs: the reference's meat spans the intercept, :907-919).
+ * One process only. */
+int lfe_compress(lfe_ctx* ctx, int64_t* n_records_out);
+
 /* Single-pass singleton drop (polars_impl.py:477-482; :433-435 for 'demean'):
  * keep a row iff every FE's pre-filter group count is > 1.  Outputs the kept
  * row count (global over ranks), per-FE distinct levels among kept rows

@@ -45,6 +45,7 @@ SIGNATURES = {
     "lfe_cluster_meat_subsets": (C.c_int, [_vp, C.c_int, _vp, _dp, _i64p]),
     "lfe_factorize_ids": (C.c_int, [_vp, C.c_int64, _vp, _vp, C.POINTER(C.c_int32)]),
     "lfe_count_distinct_rows": (C.c_int, [_vp, _i64p]),
+    "lfe_compress": (C.c_int, [_vp, _i64p]),
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_sync": (C.c_int, [_vp]),
@@ -229,6 +230,14 @@ class Engine:
         if keep_scores:
             self._score_k = k
         return stats, (meat[:k, :k] if meat is not None else None)
+
+    def compress(self) -> int:
+        """YOCO: replace the loaded rows (and cluster columns) by their compressed
+        records (lfe_compress); returns the number of records."""
+        n = C.c_int64()
+        _check(self._lib.lfe_compress(self._h, C.byref(n)))
+        self.n = int(n.value)
+        return self.n
 
     def resid_iv(self, coef: np.ndarray, meat: bool = False, keep_scores: bool = False):
         """IV residual pass (lfe_resid_iv): r = y~ - coef . [1, cols 1..p-1]; returns

@@ -356,6 +356,12 @@ static void free_data(lfe_ctx* c) {
   c->cl.clear();
   c->cl_levels.clear();
   free_cluster_ws(c);
+  dfree(c->rec_sy);
+  dfree(c->rec_syy);
+  dfree(c->rec_lay);
+  c->rec_sy_cap = c->rec_syy_cap = c->rec_lay_cap = 0;
+  c->records = false;
+  c->rows_in = 0;
   c->L = Layout();
   c->loaded = c->prepared = c->demeaned = c->scores_valid = c->seg_ready = false;
   c->n = c->ld = 0;

@@ -37,6 +37,9 @@ struct GramArgs {
   const double* beta;   // GRAM_RESID: beta_full [p] = {intercept, b_1..b_{p-1}}
   double* scores;       // GRAM_RESID: optional row-major [ld][p-1+icpt] output u r (w)
   int icpt;             // GRAM_RESID: the intercept takes y's slot in the meat / scores (u = [1, x~])
+  int yoco;             // GRAM_RESID on YOCO records: sufficient-statistic residuals (compress.py:754-811)
+  const double* rsy;    // yoco: [ld] _sum_y, layout order
+  const double* rsyy;   // yoco: [ld] _sum_y_sq, layout order
   const double* table;  // GRAM_TABLE: row-major [rows][tcols]
   int64_t rows;         // GRAM_TABLE
   int tcols;
@@ -242,7 +245,7 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
     };
     load_codes(g0 + wave * GU);
     for (int gb = g0 + wave * GU; gb < g1; gb += step) {
-      d4 xv[GU][NT], wv[GU];
+      d4 xv[GU][NT], wv[GU], yr[GU], s1[GU], s2[GU];
       bool valid[GU][4];
 #pragma unroll
       for (int u = 0; u < GU; ++u) {
@@ -251,6 +254,11 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
 #pragma unroll
         for (int I = 0; I < NT; ++I) xv[u][I] = gi < g1 ? ld4(xb[I] + r) : d4{0.0, 0.0, 0.0, 0.0};
         if (WT) wv[u] = gi < g1 ? ld4(a.w + r) : d4{0.0, 0.0, 0.0, 0.0};
+        if (MODE == GRAM_RESID && WT && a.yoco) {  // record mean of y (raw column 0), _sum_y, _sum_y_sq
+          yr[u] = gi < g1 ? ld4(a.X + r) : d4{0.0, 0.0, 0.0, 0.0};
+          s1[u] = gi < g1 ? ld4(a.rsy + r) : d4{0.0, 0.0, 0.0, 0.0};
+          s2[u] = gi < g1 ? ld4(a.rsyy + r) : d4{0.0, 0.0, 0.0, 0.0};
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) valid[u][s] = hq[u][s] >= 0;
       }
@@ -337,15 +345,32 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
 #pragma unroll
             for (int I = 1; I < NT; ++I) t += coef[I] * xt[s][I];
             const double res = row16_sum(t) - beta0;
-            if (c == 0 && valid[u][s]) {  // lane c = 0 holds y~ (column 0)
-              const double rr = res * res;
-              st[0] += WT ? wv[u][s] * rr : rr;
-              st[1] += rr;
-              st[2] += xt[s][0];
-              st[3] += xt[s][0] * xt[s][0];
+            double m;
+            if (WT && a.yoco) {
+              // record g: LSDV fitted value = mean_y - r; rss_g = sum_y_sq - 2 fit sum_y + n fit^2
+              // (compress.py:803-808); residual sum e_g = sum_y - n fit (:1118-1124).  The HC1
+              // meat is sum_g rss_g x~ x~' (:907-919): rss_g >= 0 up to rounding, clamped for the sqrt
+              const double fit = yr[u][s] - res;
+              const double rss = s2[u][s] - 2.0 * fit * s1[u][s] + wv[u][s] * fit * fit;
+              if (c == 0 && valid[u][s]) {
+                st[0] += rss;
+                st[1] += wv[u][s] * res * res;
+                st[2] += xt[s][0];
+                st[3] += xt[s][0] * xt[s][0];
+              }
+              sc[s] = s1[u][s] - wv[u][s] * fit;
+              m = sqrt(fmax(rss, 0.0));
+            } else {
+              if (c == 0 && valid[u][s]) {  // lane c = 0 holds y~ (column 0)
+                const double rr = res * res;
+                st[0] += WT ? wv[u][s] * rr : rr;
+                st[1] += rr;
+                st[2] += xt[s][0];
+                st[3] += xt[s][0] * xt[s][0];
+              }
+              sc[s] = WT ? res * wv[u][s] : res;
+              m = WT ? res * sqrt(wv[u][s]) : res;
             }
-            sc[s] = WT ? res * wv[u][s] : res;
-            const double m = WT ? res * sqrt(wv[u][s]) : res;
 #pragma unroll
             for (int I = 0; I < NT; ++I) z[s][I] = (valid[u][s] && dat[I]) ? (one[I] ? 1.0 : xt[s][I]) * m : 0.0;
           }
@@ -1032,10 +1057,16 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
   a.beta = c->dbeta;
   a.scores = keep_scores ? c->scores : nullptr;
   a.icpt = icpt ? 1 : 0;
+  if (c->records) {
+    LFE_TRY(records_layout(c));
+    a.yoco = 1;
+    a.rsy = c->rec_lay;
+    a.rsyy = c->rec_lay + c->ld;
+  }
   const int k = c->p - 1 + a.icpt;  // meat / score width
   c->score_k = k;
   std::vector<double> meat((size_t)std::max(k, 1) * std::max(k, 1));
-  if (!icpt && resid_rows_ok(c, a)) {
+  if (!icpt && !a.yoco && resid_rows_ok(c, a)) {
     a.nq = 1;
     a.qf[0] = 1 - a.la.P;
     a.G_Q = c->fe[a.qf[0]].G;

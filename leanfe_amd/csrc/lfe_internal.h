@@ -198,6 +198,14 @@ struct lfe_ctx {
   double* dbeta = nullptr;   // [64] beta_full staging
   bool scores_valid = false;
   int score_k = 0;           // score width: p - 1 (u = x~), or p with the intercept (IV, u = [1, x~, z~])
+  // YOCO records (lfe_compress): the loaded rows are compressed records, weight = n_g (or sum w);
+  // no singleton drop, weighted convergence check, lfe_resid_yoco's sufficient-statistic residuals
+  bool records = false;
+  int64_t rows_in = 0;           // rows before compression
+  double* rec_sy = nullptr;      // [ld] sum (w) y per record, input (record) order
+  double* rec_syy = nullptr;     // [ld] sum (w) y^2 per record
+  double* rec_lay = nullptr;     // [2][ld] the two above in layout order
+  size_t rec_sy_cap = 0, rec_syy_cap = 0, rec_lay_cap = 0;
   // scratch
   double* scratch = nullptr;     // device partials
   size_t scratch_elems = 0;
@@ -249,6 +257,8 @@ int launch_gram(lfe_ctx* c, double* host_gram);
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores, int icpt);
 int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
+// --- YOCO records (lfe_compress.hip) ---
+int records_layout(lfe_ctx* c);   // rec_sy / rec_syy in layout order -> rec_lay
 // --- device keys (lfe_keys.hip) ---
 int bit_length(uint64_t v);
 int ensure_sort_ws(lfe_ctx* c, size_t n);
@@ -316,6 +326,23 @@ inline int grid_for(int64_t n, int block = kBlock, int cap = 256 * 8) {
   if (g < 1) g = 1;
   if (g > cap) g = cap;
   return (int)g;
+}
+
+// group-by equality of f64 values (keys of distinct rows and YOCO records):
+// -0.0 == 0.0 and every NaN alike
+__device__ __forceinline__ uint64_t canon_bits(double v) {
+  if (v != v) return 0x7ff8000000000000ull;
+  if (v == 0.0) return 0ull;
+  return (uint64_t)__double_as_longlong(v);
+}
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 33;
+  return h;
 }
 
 // What every sweep / Gram kernel needs to evaluate x~_i = x_i - sum_f alpha_f[g_f(i)]

@@ -214,21 +214,6 @@ struct RowArgs {
   int hash_bits;     // 64; fewer only to exercise the collision path in tests
 };
 
-__device__ __forceinline__ uint64_t canon_bits(double v) {
-  if (v != v) return 0x7ff8000000000000ull;  // every NaN alike
-  if (v == 0.0) return 0ull;                 // -0.0 == 0.0
-  return (uint64_t)__double_as_longlong(v);
-}
-
-__device__ __forceinline__ uint64_t fmix64(uint64_t h) {
-  h ^= h >> 33;
-  h *= 0xff51afd7ed558ccdull;
-  h ^= h >> 33;
-  h *= 0xc4ceb9fe1a85ec53ull;
-  h ^= h >> 33;
-  return h;
-}
-
 __global__ void k_row_hash(RowArgs a, uint64_t* __restrict__ keys, int32_t* __restrict__ rows) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t h = 0x9e3779b97f4a7c15ull;

@@ -642,7 +642,9 @@ int prepare_layout(lfe_ctx* c) {
       a.drops[f] = fe.drops;
     }
     a.ndropped = ndropped;
-    if (n) {
+    // YOCO records keep every record: compress has no singleton drop (compress.py:1049-1175);
+    // a record alone in its level is fitted exactly by its own dummy
+    if (n && !c->records) {
       ProfScope _ps(c, K_MARK);
       const int grid = grid_for((n + 3) / 4, kBlock, 8192);
       switch (c->F) {

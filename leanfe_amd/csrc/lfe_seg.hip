@@ -240,16 +240,18 @@ __global__ void k_finalize(const double* __restrict__ S, const double* __restric
 // stop test (polars_impl.py:512-521): for every group present,
 //   mean_g(y~) = (Sy[g] - cnt[g] alpha[g][0] - R[g]) / cnt[g]
 // max |.| -> out (non-negative doubles order like their bit patterns)
+// YOCO records (Wsum != null): the weighted mean, (S_y - W alpha - R) / W
 __global__ void k_check_max(const double* __restrict__ Sy, int sy_stride, const double* __restrict__ R, int r_stride,
-                            const double* __restrict__ alpha, int p, const int32_t* __restrict__ cnt, int32_t G,
-                            unsigned long long* __restrict__ out) {
+                            const double* __restrict__ alpha, int p, const int32_t* __restrict__ cnt,
+                            const double* __restrict__ Wsum, int32_t G, unsigned long long* __restrict__ out) {
   double m = 0.0;
   for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
     const int32_t n = cnt[g];
     if (n > 0) {
+      const double den = Wsum ? Wsum[g] : (double)n;
       const double r =
-          Sy[(int64_t)g * sy_stride] - (double)n * alpha[(int64_t)g * p] - (R ? R[(int64_t)g * r_stride] : 0.0);
-      m = fmax(m, fabs(r / (double)n));
+          Sy[(int64_t)g * sy_stride] - den * alpha[(int64_t)g * p] - (R ? R[(int64_t)g * r_stride] : 0.0);
+      if (den > 0.0) m = fmax(m, fabs(r / den));
     }
   }
   for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
@@ -358,7 +360,7 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
       a.alpha[j] = c->fe[f2].alpha;
       ++j;
     }
-  const bool wt = !y_only && c->L.w != nullptr;
+  const bool wt = (!y_only || c->records) && c->L.w != nullptr;  // the check is unweighted, except for records
   a.ws = wt ? fe.ws : nullptr;
   a.p = c->p;
   a.pc = pc;
@@ -422,9 +424,11 @@ static int seg_finalize(lfe_ctx* c, int f) {
 static int seg_check_max(lfe_ctx* c, int f, const double* R, int r_stride) {
   auto& fe = c->fe[f];
   ProfScope _ps(c, K_CHECK_MAX);
-  const double* Sy = c->L.w ? fe.Sy : fe.S;
-  hipLaunchKernelGGL(k_check_max, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, Sy, c->L.w ? 1 : c->p, R,
-                     r_stride, fe.alpha, c->p, fe.cnt, fe.G, reinterpret_cast<unsigned long long*>(c->dred));
+  const bool unw = c->L.w && !c->records;  // weighted fit, unweighted check (polars_impl.py:513)
+  const double* Sy = unw ? fe.Sy : fe.S;
+  hipLaunchKernelGGL(k_check_max, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, Sy, unw ? 1 : c->p, R,
+                     r_stride, fe.alpha, c->p, fe.cnt, (c->L.w && c->records) ? fe.W : nullptr, fe.G,
+                     reinterpret_cast<unsigned long long*>(c->dred));
   LFE_HIP(hipGetLastError());
   return LFE_OK;
 }
@@ -434,7 +438,8 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
   const int F = c->F;
   const bool cross = F > 1;
   if (cross) LFE_TRY(seg_build(c));
-  const bool reuse = cross && c->L.w == nullptr;  // T of the first FE doubles as its check term
+  // T of the first FE doubles as its check term (unweighted fits, and YOCO records whose check is weighted)
+  const bool reuse = cross && (c->L.w == nullptr || c->records);
   auto project = [&](int f) -> int {
     if (cross) LFE_TRY(seg_cross(c, f, false, K_CROSS));
     return seg_finalize(c, f);
@@ -447,6 +452,9 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
     iterations = 1;
   } else {
     bool first_ready = false;  // T of order[0] already holds the next projection's cross term
+    constexpr int kStall = 20;
+    double best = 1e300;
+    int stall = 0;
     for (int it = 1; it <= max_iter; ++it) {
       for (size_t k = 0; k < order.size(); ++k) {
         if (k == 0 && first_ready) LFE_TRY(seg_finalize(c, order[0]));
@@ -474,6 +482,16 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
       }
       LFE_TRY(d2h_sync(c, &last, c->dred, sizeof(double)));
       if (last < tol) break;
+      if (c->records) {
+        // records are solved to machine precision: stop once the check has not reached a
+        // new minimum for kStall checks (it only moves at rounding level from there)
+        if (last < best) {
+          best = last;
+          stall = 0;
+        } else if (++stall >= kStall) {
+          break;
+        }
+      }
     }
   }
   *iterations_out = iterations;

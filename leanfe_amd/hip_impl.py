@@ -119,12 +119,11 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                 f"est. compression ratio: {est_comp_ratio}")
             strategy = inferred
         if strategy == "compress":
-            if not fe_cols:
-                strategy = "ols"
-            else:
-                say("hip backend: 'compress' (YOCO) is not on the device path; "
-                    "running alternating projections for the same estimator")
-                strategy = "alt_proj" if len(fe_cols) > 1 else "demean"
+            if sharded:
+                raise ValueError("strategy='compress' groups one process's rows; use alt_proj with a sharded engine")
+            say("Using compresssion strategy...")
+            return _compress_fit(eng, cols, x_cols, fe_cols, fe_card, cluster_cols, v, vcov, ssc, formula, t_start,
+                                 t_load)
 
         if strategy == "demean":
             if len(fe_cols) != 1:
@@ -245,3 +244,69 @@ def _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, fe_cols, sharded, n
     beta = iv.beta_full[1:] if strip else iv.beta_full
     se = se[1:] if strip else se
     return beta, se, n_clusters, float(stats[1]), stats
+
+
+def _compress_fit(eng, cols, x_cols, fe_cols, fe_card, cluster_cols, v, vcov, ssc, formula, t_start, t_load):
+    """YOCO ``strategy='compress'`` (leanfe_compress_polars, compress.py:1049-1175) on the device.
+
+    lfe_compress groups the loaded rows by (x, FE, cluster) into records (compress.py:282-358);
+    the exact LSDV fit of the records (build_design_matrix + solve_wls, :503-747) is computed in
+    its FWL form: weighted alternating projections of the records run to machine precision
+    (stopping when the weighted group means no longer decrease), then the weighted Gram and the
+    host solve give beta and the x block of the LSDV (X'WX)^-1.  The residual pass forms the
+    grouped RSS (:754-811), the HC1 meat sum_g rss_g x~ x~' (:907-919) and the cluster scores
+    x~_g e_g (:922-1042), whose x rows equal the reference's [X'WX]^-1 X' rows.
+    """
+    cl_codes = None
+    if cluster_cols is not None:
+        # polars_impl.py:407-416 passes cluster_cols whatever vcov is: they join the group key
+        cl_codes, cl_levels = [], []
+        for c in cluster_cols:
+            cc, gg = frame.factorize(cols[c])
+            cl_codes.append(cc)
+            cl_levels.append(gg)
+        eng.load_clusters(cl_codes, cl_levels)
+    n_obs = eng.n
+    n_compressed = eng.compress()
+    _, _, card = eng.drop_singletons()  # records mode: every record kept
+    order = sorted(range(len(fe_cols)), key=lambda i: card[i])
+    eng.demean(order, 0.0, 100_000, check_from=1)  # to the rounding floor (stall stop in the engine)
+    k = len(x_cols)
+    G = eng.gram()
+    XtX, Xty = inference.split_gram(G)
+    beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
+    Vb = XtX_inv[1:, 1:]
+    fe_dims = tuple(int(c) for c in card) if fe_cols else None
+    P = 1 + k + sum(int(c) - 1 for c in card)  # [1, x, dummies of every level but the first]
+    df_resid = n_obs - P
+    if fe_cols:
+        stats, meat = eng.resid(beta_full, hc1=(v == "hc1"), keep_scores=(v == "cluster"))
+    else:
+        # no FE: x is not demeaned, so the reference's sandwich spans the intercept
+        # (the full design's XtX_inv and meat, compress.py:907-919): u = [1, x] meats / scores
+        stats, meat = eng.resid_iv(beta_full, meat=(v == "hc1"), keep_scores=(v == "cluster"))
+        Vb = XtX_inv
+    rss = float(stats[0])
+    n_clusters = None
+    if v == "iid":
+        se = inference.se_iid(Vb, rss, df_resid)
+    elif v == "hc1":
+        se = inference.se_hc1(Vb, meat, n_obs, df_resid)
+    else:
+        if len(cluster_cols) == 1:
+            meats, Gs = eng.cluster_meat()
+            se, n_clusters = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, ssc)
+        else:
+            subsets = inference.cluster_subsets(len(cluster_cols))
+            meats, Gs = eng.cluster_meat_subsets(subsets)
+            se, n_clusters = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets, n_obs,
+                                                           df_resid, ssc)
+    beta = beta_full[1:]
+    if not fe_cols:
+        se = se[1:]
+    timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
+    return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta))),
+                        std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
+                        n_compressed=n_compressed, vcov_type=vcov, df_resid=df_resid, rss=rss,
+                        n_clusters=n_clusters, fe_dims=fe_dims, formula=formula, fe_cols=fe_cols, backend="hip",
+                        timings=timings)

@@ -47,7 +47,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 REF_PKG = "/root/reference/python/leanfe"
 sys.path.insert(0, REPO)
 
-from oracle import altproj  # noqa: E402
+from oracle import altproj, yoco  # noqa: E402
 from leanfe_amd import synth  # noqa: E402
 
 
@@ -282,6 +282,62 @@ def iv_reference(std_errors, common, orc, data, weights, vcov, cl, ssc=True):
     return np.asarray(beta_full[1:]), np.asarray(se[1:]), ncl
 
 
+def fx_yoco(seed=41, n=20000, L=(50, 20), weights=False):
+    """Discrete regressors on low-cardinality FEs (the YOCO use case): a binary
+    treatment and a 5-level dose, so (x, FE) cells repeat and records compress."""
+    rng = np.random.default_rng(seed)
+    codes = [rng.integers(0, G, n) for G in L]
+    eff = [rng.normal(0, 1.0, G) for G in L]
+    d = {"treat": rng.integers(0, 2, n).astype(np.float64), "dose": rng.integers(0, 5, n).astype(np.float64)}
+    d["y"] = 0.8 * d["treat"] - 0.3 * d["dose"] + rng.normal(0, 1, n) + sum(e[c] for e, c in zip(eff, codes))
+    for f, c in enumerate(codes):
+        d[f"fe{f + 1}"] = c
+    d["state"] = codes[0] // 5
+    if weights:
+        d["w"] = rng.uniform(0.5, 2.0, n)
+    return d
+
+
+# YOCO strategy='compress' (compress.py:282-1175): outputs of the reference's own
+# build_design_matrix / solve_wls / compute_rss_grouped / compute_se_compress on the
+# records of oracle/yoco.compress (the Polars group_by restated in NumPy)
+YOCO = [
+    # name, recipe, y, xs, fes, weights, vcov, cluster_cols
+    ("yoco_iid", fx_yoco, "y", ["treat", "dose"], ["fe1", "fe2"], None, "iid", None),
+    ("yoco_hc1", fx_yoco, "y", ["treat", "dose"], ["fe1", "fe2"], None, "HC1", None),
+    ("yoco_cl1", fx_yoco, "y", ["treat", "dose"], ["fe1", "fe2"], None, "cluster", ["state"]),
+    ("yoco_cl2", fx_yoco, "y", ["treat", "dose"], ["fe1", "fe2"], None, "cluster", ["state", "fe2"]),
+    ("yoco_w_hc1", lambda: fx_yoco(seed=43, weights=True), "y", ["treat", "dose"], ["fe1", "fe2"], "w", "HC1",
+     None),
+    ("yoco_1fe_cl1", lambda: fx_yoco(seed=45, L=(80,)), "y", ["treat", "dose"], ["fe1"], None, "cluster",
+     ["state"]),
+    ("yoco_nofe_hc1", lambda: fx_yoco(seed=47, L=(3,)), "y", ["treat", "dose"], [], None, "HC1", None),
+]
+
+
+def yoco_reference(compress, orc, xs, fes, vcov, cl, ssc=True):
+    """leanfe_compress_polars (compress.py:1049-1175) after the group_by, by the
+    reference's own functions."""
+    rec = orc["records"]
+    res = compress.DuckDBResult({c: np.asarray(v) for c, v in rec.items()})
+    design, Y, wts, all_cols, _ = compress.build_design_matrix(res, list(xs), list(fes), use_sparse=True)
+    beta, XtX_inv = compress.solve_wls(design, Y, wts)
+    rss_total, rss_per_group = compress.compute_rss_grouped(res, design, beta, backend="duckdb")
+    df_resid = orc["n_obs"] - len(all_cols)
+    cl_ids, resid_sums = None, None
+    if vcov.lower() == "cluster":
+        cl_ids = rec[cl[0]] if len(cl) == 1 else np.stack([rec[c] for c in cl], axis=1)
+        fitted = np.asarray(design @ beta).ravel()
+        resid_sums = rec["_sum_y"] - rec["_n"] * fitted
+    k_x = len(xs) + 1
+    ctx = compress.CompressionContext(
+        XtX_inv=XtX_inv, rss_total=rss_total, rss_per_group=rss_per_group, n_obs=orc["n_obs"],
+        df_resid=df_resid, vcov=vcov, design_matrix=design, x_cols=all_cols[:k_x], cluster_ids=cl_ids,
+        residual_sums_per_group=resid_sums, apply_small_sample_correction=ssc)
+    se, ncl = compress.compute_se_compress(ctx)
+    return np.asarray(beta[1:k_x]), np.asarray(se[1:]), ncl, df_resid, float(rss_total)
+
+
 def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=None):
     arrays = {f"in_{c}": np.asarray(v) for c, v in data.items()}
     meta = dict(name=name, y=y, xs=xs, fes=fes, strategy=strategy, weights=weights, vcov=vcov,
@@ -348,6 +404,31 @@ def main():
               f"oracle-vs-ref IV beta {rb:.1e} se {rs:.1e}")
         _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=inst)
     print(f"worst oracle vs reference IV relative deviation: {worst:.2e}")
+    worst = 0.0
+    for name, recipe, y, xs, fes, weights, vcov, cl in YOCO:
+        data = recipe()
+        orc = yoco.fit(data, y, xs, fes, weights=weights, vcov=vcov, cluster_cols=cl)
+        rb_, rs_, rncl, rdf, rrss = yoco_reference(compress, orc, xs, fes, vcov, cl)
+        rb = np.max(np.abs(orc["beta"] - rb_) / np.abs(rb_))
+        rs = np.max(np.abs(orc["se"] - rs_) / np.abs(rs_))
+        assert rb < 1e-11 and rs < 1e-11 and rdf == orc["df_resid"], (name, rb, rs, rdf, orc["df_resid"])
+        assert _json_ncl(rncl) == _json_ncl(orc["n_clusters"]), (name, rncl, orc["n_clusters"])
+        worst = max(worst, rb, rs)
+        print(f"{name:18s} records={orc['n_compressed']:6d} n={orc['n_obs']:6d} df={orc['df_resid']:6d} "
+              f"oracle-vs-ref YOCO beta {rb:.1e} se {rs:.1e}")
+        arrays = {f"in_{c}": np.asarray(v) for c, v in data.items()}
+        meta = dict(name=name, y=y, xs=xs, fes=fes, strategy="compress", weights=weights, vcov=vcov,
+                    cluster_cols=cl, instruments=[], demean_tol=1e-6, max_iter=50, ssc=True,
+                    oracle_n_clusters=orc["n_clusters"], ref_n_clusters=rncl, pinned="reference-yoco")
+        arrays.update(
+            oracle_beta=orc["beta"], oracle_se=orc["se"], oracle_n_obs=np.int64(orc["n_obs"]),
+            oracle_df_resid=np.int64(orc["df_resid"]), oracle_n_compressed=np.int64(orc["n_compressed"]),
+            oracle_fe_dims=np.asarray(orc["fe_dims"] or (), dtype=np.int64), oracle_rss=np.float64(orc["rss"]),
+            ref_beta=rb_, ref_se=rs_, ref_rss=np.float64(rrss),
+            meta=np.frombuffer(json.dumps(meta, default=lambda o: list(o) if isinstance(o, tuple) else o)
+                               .encode(), dtype=np.uint8))
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+    print(f"worst oracle vs reference YOCO relative deviation: {worst:.2e}")
 
 
 if __name__ == "__main__":

@@ -9,7 +9,7 @@ import pytest
 
 from golden_util import load, names, ncl
 from leanfe_amd import synth
-from oracle import altproj
+from oracle import altproj, yoco
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-10
@@ -42,7 +42,10 @@ def _assert_same(r, beta, se, n_obs, iterations, df_resid, fe_dims, n_clusters, 
     np.testing.assert_allclose(s, se, rtol=rtol, atol=0)
 
 
-@pytest.mark.parametrize("name", names())
+YOCO_NAMES = [n for n in names() if load(n)[0]["pinned"] == "reference-yoco"]
+
+
+@pytest.mark.parametrize("name", [n for n in names() if n not in YOCO_NAMES])
 def test_golden_fixture(name):
     meta, data, exp = load(name)
     r = _hip_fit(meta, data, demean_tol=meta["demean_tol"], max_iter=meta["max_iter"])
@@ -202,3 +205,79 @@ def test_iv_under_identified_raises():
     data, _ = _iv_panel(36, 20_000, (100, 10), 3, 1)
     with pytest.raises(ValueError, match="Under-identified"):
         leanfe_hip(data, formula="y ~ x1 + x2 + x3 | fe1 + fe2 | z1", strategy="alt_proj", quiet=True)
+
+
+def _assert_yoco(r, o, xs, rtol=RTOL):
+    assert r.n_obs == o["n_obs"] and r.df_resid == o["df_resid"]
+    assert r.n_compressed == o["n_compressed"]
+    assert tuple(r.fe_dims or ()) == tuple(o["fe_dims"] or ())
+    assert ncl(r.n_clusters) == ncl(o["n_clusters"])
+    np.testing.assert_allclose([r.coefs[x] for x in xs], o["beta"], rtol=rtol, atol=0)
+    np.testing.assert_allclose([r.std_errors[x] for x in xs], o["se"], rtol=rtol, atol=0)
+    np.testing.assert_allclose(r.rss, o["rss"], rtol=rtol)
+
+
+@pytest.mark.parametrize("name", YOCO_NAMES)
+def test_yoco_fixture(name):
+    """strategy='compress' on the device (lfe_compress + records-mode solve) against the
+    reference's own LSDV WLS / grouped-RSS SE functions (tests/golden/make_golden.py)."""
+    meta, data, exp = load(name)
+    r = _hip_fit(meta, data)
+    assert r.n_obs == int(exp["oracle_n_obs"]) and r.df_resid == int(exp["oracle_df_resid"])
+    assert r.n_compressed == int(exp["oracle_n_compressed"])
+    assert tuple(r.fe_dims or ()) == tuple(exp["oracle_fe_dims"].tolist())
+    assert ncl(r.n_clusters) == ncl(meta["ref_n_clusters"])
+    np.testing.assert_allclose([r.coefs[x] for x in meta["xs"]], exp["ref_beta"], rtol=RTOL, atol=0)
+    np.testing.assert_allclose([r.std_errors[x] for x in meta["xs"]], exp["ref_se"], rtol=RTOL, atol=0)
+    np.testing.assert_allclose(r.rss, float(exp["ref_rss"]), rtol=RTOL)
+
+
+def _yoco_panel(seed, n, L, k, weights=False):
+    rng = np.random.default_rng(seed)
+    codes = [rng.integers(0, G, n) for G in L]
+    d = {f"x{j + 1}": rng.integers(0, 3 + j, n).astype(np.float64) for j in range(k)}
+    d["y"] = sum((1.0 - 0.2 * j) * d[f"x{j + 1}"] for j in range(k)) + rng.normal(0, 1, n)
+    for f, c in enumerate(codes):
+        d[f"fe{f + 1}"] = c
+        d["y"] = d["y"] + rng.normal(0, 1, L[f])[c]
+    d["cl1"] = codes[0] // 4
+    if weights:
+        d["w"] = rng.uniform(0.5, 2.0, n)
+    return d
+
+
+@pytest.mark.parametrize("seed,n,L,k,vcov,weights", [
+    (51, 2_000_000, (200, 50), 3, "HC1", False),        # ~50% of cells filled: 1M+ records, 2 FEs
+    (52, 1_000_000, (120, 30, 8), 2, "cluster", False),  # three FEs, one-way cluster on the records
+    (53, 600_000, (150, 40), 2, "iid", True),            # weighted: _n = sum w
+    (54, 800_000, (100, 25), 2, "cluster", False),       # two-way CGM (cl1 x fe2) on the records
+])
+def test_yoco_panels_vs_oracle(seed, n, L, k, vcov, weights):
+    from leanfe_amd import leanfe_hip
+    d = _yoco_panel(seed, n, L, k, weights)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(L))]
+    cl = (["cl1"] if seed != 54 else ["cl1", "fe2"]) if vcov == "cluster" else None
+    w = "w" if weights else None
+    o = yoco.fit(d, "y", xs, fes, weights=w, vcov=vcov, cluster_cols=cl)
+    r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="compress", vcov=vcov, cluster_cols=cl,
+                   weights=w, quiet=True)
+    _assert_yoco(r, o, xs)
+
+
+def test_yoco_auto_selects_compress_and_hash_collisions_are_exact(monkeypatch):
+    """strategy='auto' picks 'compress' for low-cardinality FEs with discrete x
+    (compress.py:96-184), and an 8-bit row hash (forced collisions) still groups exactly."""
+    from leanfe_amd import leanfe_hip
+    d = _yoco_panel(55, 200_000, (60, 20), 2)
+    xs, fes = ["x1", "x2"], ["fe1", "fe2"]
+    o = yoco.fit(d, "y", xs, fes, vcov="HC1")
+    r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="auto", vcov="HC1", quiet=True)
+    assert r.n_compressed == o["n_compressed"]
+    _assert_yoco(r, o, xs)
+    monkeypatch.setenv("LFE_ROW_HASH_BITS", "8")
+    d = _yoco_panel(56, 20_000, (30, 10), 2)
+    o = yoco.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=["cl1"])
+    r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="compress", vcov="cluster", cluster_cols=["cl1"],
+                   quiet=True)
+    _assert_yoco(r, o, xs)

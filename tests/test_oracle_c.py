@@ -12,7 +12,7 @@ from golden_util import load, names
 
 pytestmark = pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not available")
 
-CASES = [n for n in names() if n.endswith(("_iid", "_hc1")) and "_w_" not in n and load(n)[0]["strategy"] != "demean"
+CASES = [n for n in names() if n.endswith(("_iid", "_hc1")) and "_w_" not in n and load(n)[0]["strategy"] not in ("demean", "compress")
          and not load(n)[0].get("instruments")]  # the C port is the OLS baseline only
 
 

@@ -8,9 +8,10 @@ import numpy as np
 import pytest
 
 from golden_util import load, names, ncl
-from oracle import altproj
+from oracle import altproj, yoco
 
-CASES = names()
+YOCO_CASES = [n for n in names() if load(n)[0]["pinned"] == "reference-yoco"]
+CASES = [n for n in names() if n not in YOCO_CASES]
 
 
 def _fit(meta, data, **kw):
@@ -20,7 +21,23 @@ def _fit(meta, data, **kw):
 
 
 def test_fixture_count():
-    assert len(CASES) >= 15
+    assert len(CASES) >= 15 and len(YOCO_CASES) >= 7
+
+
+@pytest.mark.parametrize("name", YOCO_CASES)
+def test_yoco_oracle_matches_reference_functions(name):
+    """strategy='compress': the oracle's group-by + LSDV WLS + grouped-RSS SEs == the
+    reference's own build_design_matrix / solve_wls / compute_rss_grouped /
+    compute_se_compress on the same records (tests/golden/make_golden.py)."""
+    meta, data, exp = load(name)
+    r = yoco.fit(data, meta["y"], meta["xs"], meta["fes"], weights=meta["weights"], vcov=meta["vcov"],
+                 cluster_cols=meta["cluster_cols"], ssc=meta["ssc"])
+    assert r["n_obs"] == int(exp["oracle_n_obs"]) and r["df_resid"] == int(exp["oracle_df_resid"])
+    assert r["n_compressed"] == int(exp["oracle_n_compressed"])
+    np.testing.assert_allclose(r["beta"], exp["ref_beta"], rtol=1e-11, atol=0)
+    np.testing.assert_allclose(r["se"], exp["ref_se"], rtol=1e-11, atol=0)
+    np.testing.assert_allclose(r["rss"], exp["ref_rss"], rtol=1e-11)
+    assert ncl(r["n_clusters"]) == ncl(meta["ref_n_clusters"])
 
 
 @pytest.mark.parametrize("name", CASES)
