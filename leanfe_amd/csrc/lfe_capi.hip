@@ -274,7 +274,7 @@ int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count) {
 const char* const kKernelNames[K_NUM_KERNELS] = {
     "part_hist", "scan", "part_scatter", "count", "mark", "group_sums", "cross", "check", "finalize",
     "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth",
-    "tp", "tq", "seg_build", "cluster_sort"};
+    "tp", "tq", "seg_build", "cluster_sort", "gram_tables"};
 
 static hipEvent_t prof_event(lfe_ctx* c) {
   if (!c->prof.pool.empty()) {
@@ -360,6 +360,10 @@ static void free_data(lfe_ctx* c) {
   dfree(c->rec_syy);
   dfree(c->rec_lay);
   c->rec_sy_cap = c->rec_syy_cap = c->rec_lay_cap = 0;
+  dfree(c->raw_part);
+  dfree(c->raw_tile);
+  c->raw_part_cap = c->raw_tile_cap = 0;
+  c->raw_ready = c->tq_final = false;
   c->records = false;
   c->rows_in = 0;
   c->L = Layout();
@@ -660,6 +664,7 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
   if (check_from > 0 && max_iter < 1) return fail(LFE_EINVAL, "max_iter must be >= 1");
   int iterations = 0;
   double last = -1.0;
+  c->tq_final = false;
   {
     PhaseTimer t(c, &c->tm.demean);
     for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));

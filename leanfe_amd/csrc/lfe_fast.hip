@@ -37,11 +37,15 @@ struct Sums4Args {
   int slice;            // 1: primary slice accumulated in LDS at offset 0
   int nq;               // number of non-primary FEs and their indices
   int qf[kMaxFE];
+  double* raw_part;     // RAW: [blocks][256] raw Gram tiles
 };
 
 // FQ: max non-primary FEs held in registers; GU: 16-row groups loaded before use;
-// NT: 16-column slots per lane (p <= 16 NT); TH: threads per workgroup
-template <int FQ, int GU, int NT, int TH>
+// NT: 16-column slots per lane (p <= 16 NT); TH: threads per workgroup.
+// RAW (NT = 1, p <= 15, unweighted): the same loads also feed one MFMA per 16-row
+// group that accumulates the raw Gram of the kept rows' data columns, shifted by the
+// first layout row (slot 15 = intercept), for the Gram-from-tables path (lfe_gram.hip).
+template <int FQ, int GU, int NT, int TH, bool RAW>
 __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -49,6 +53,10 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.la.p, P = a.la.P, F = a.la.F;
   const int nq = a.nq < FQ ? a.nq : FQ;
+  d4 racc[4];  // one per row of the quad: independent MFMA chains (issue never waits on the previous one)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) racc[s] = d4{0.0, 0.0, 0.0, 0.0};
+  const double shift = (RAW && c < p) ? a.X[(int64_t)c * a.ld] : 0.0;
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
       for (int j = tid; j < a.G[f] * p; j += TH) lds[a.tab_off[f] + j] = 0.0;
@@ -103,6 +111,13 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
         bool valid[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) valid[s] = rb[u] + s >= it.y && rb[u] + s < it.z && hv[s] >= 0;
+        if (RAW) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const double z = !valid[s] ? 0.0 : (c == 15 ? 1.0 : (c < p ? xv[u][0][s] - shift : 0.0));
+            racc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[s], 0, 0, 0);
+          }
+        }
 #pragma unroll
         for (int I = 0; I < NT; ++I) {
           const int col = 16 * I + c;
@@ -137,6 +152,22 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
         const double val = lds[a.tab_off[f] + j];
         if (val != 0.0) atomicAdd(&a.S[f][j], val);
       }
+  if (RAW) {
+    // waves' raw tiles summed in LDS (lane (kq, c) holds rows kq + 4 rr of column c)
+    __shared__ double rred[256];
+    for (int wv = 0; wv < nwv; ++wv) {
+      __syncthreads();
+      if (wave == wv)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int e = (kq + 4 * rr) * 16 + c;
+          const double v = (racc[0][rr] + racc[1][rr]) + (racc[2][rr] + racc[3][rr]);
+          rred[e] = (wv == 0) ? v : rred[e] + v;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < 256; e += TH) a.raw_part[(int64_t)blockIdx.x * 256 + e] = rred[e];
+  }
 }
 
 int sums4(lfe_ctx* c) {
@@ -168,16 +199,25 @@ int sums4(lfe_ctx* c) {
   const size_t lds = off * 8;
   const int NT = (p + 15) / 16;
   const void* fn = nullptr;
-#define SUMS4_FN(FQ, GU, NT_, TH_) reinterpret_cast<const void*>(&k_sums4<FQ, GU, NT_, TH_>)
+#define SUMS4_FN(FQ, GU, NT_, TH_) reinterpret_cast<const void*>(&k_sums4<FQ, GU, NT_, TH_, false>)
   static const int gu_env = [] {
     const char* e = getenv("LFE_SUMS_GU");  // tuning override
     return e ? atoi(e) : 0;
   }();
+  static const int raw_env = [] {
+    const char* e = getenv("LFE_TABLE_GRAM");  // 0: no Gram from tables (explicit design pass)
+    return e ? atoi(e) : 1;
+  }();
+  const bool raw = raw_env != 0 && c->F == 2 && P >= 0 && a.nq == 1 && p <= 15 && !a.w && c->world == 1 &&
+                   gu_env != 4;
+  c->raw_ready = false;
   int threads = kSumThreads;
   if (a.nq <= 1 && NT == 1) {
     // the 2-FE case: one workgroup per CU (LDS), so 16 waves of <= 128 VGPRs (GU 2)
     threads = gu_env == 4 ? kSumThreads : 1024;
-    fn = gu_env == 4 ? SUMS4_FN(1, 4, 1, kSumThreads) : SUMS4_FN(1, 2, 1, 1024);
+    fn = gu_env == 4 ? SUMS4_FN(1, 4, 1, kSumThreads)
+         : raw       ? reinterpret_cast<const void*>(&k_sums4<1, 2, 1, 1024, true>)
+                     : SUMS4_FN(1, 2, 1, 1024);
   } else if (a.nq <= 1) {
     fn = NT == 2 ? SUMS4_FN(1, 2, 2, kSumThreads) : NT == 3 ? SUMS4_FN(1, 2, 3, kSumThreads)
                                                     : SUMS4_FN(1, 2, 4, kSumThreads);
@@ -190,12 +230,22 @@ int sums4(lfe_ctx* c) {
 #undef SUMS4_FN
   LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 1)));
   const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, threads, lds)));
+  if (raw) {
+    LFE_TRY(ensure_f64(c, c->raw_part, c->raw_part_cap, (size_t)nblocks * 256));
+    LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
+    a.raw_part = c->raw_part;
+  }
   {
     ProfScope _ps(c, K_GROUP_SUMS);
     void* args[] = {&a};
     LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, lds, c->stream));
   }
   LFE_HIP(hipGetLastError());
+  if (raw) {
+    reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
+    LFE_HIP(hipGetLastError());
+    c->raw_ready = true;
+  }
   for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_f64(c, c->fe[f].S, (size_t)c->fe[f].G * p));
   return LFE_OK;
 }

@@ -889,6 +889,172 @@ static int design_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
   return allreduce_sum_f64(c, out_dev, 256);
 }
 
+// ---------------------------------------------------------------------------
+// Gram from group tables (two FEs after demean_fast, unweighted, one process).
+// With d~ = d - a_h - b_q (a = alpha_P, b = alpha_Q) and every data column shifted
+// by its first layout row c (a shift the FEs absorb: d - c - a - (b - c) = d~):
+//   sum d~ d~' = R + sum_h [n a a' - S a' - a S'] + sum_q [n b' b'' - V b'' - b' V']
+//   sum d~     = C - sum_h n a - sum_q n b'
+// with R, C the raw Gram / column sums of d - c over kept rows (k_sums4<RAW>),
+// S the group sums, b' = b - c, V = S_Q - n c - T_Q and T_Q = sum_{i in q} a_{h_i}
+// (the last sweep's cross term, formed from the final a).  Per group the bracket is
+// n a_i a_j - V_i a_j - a_i V_j: symmetric, so only the upper triangle is summed.
+// The group tables replace the design pass over X (8p + 4F bytes per row).
+// Cancellation guard: the assembled diagonal must keep > 1/kTabKappa of R's.
+// ---------------------------------------------------------------------------
+constexpr double kTabKappa = 1e4;
+
+struct TabArgs {
+  const double* alpha[2];  // [G][p]: P, Q
+  const double* S[2];
+  const double* TQ;        // [G_Q][p]
+  const int32_t* cnt[2];
+  int G[2];
+  int p;
+  const double* X;         // layout X: the shift is row 0
+  int64_t ld;
+};
+
+template <int PM>
+__global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restrict__ partial) {
+  constexpr int NG = PM * (PM + 1) / 2;
+  constexpr int NA = NG + PM;
+  __shared__ double red[4][NA];
+  const int p = t.p;
+  double sh[PM];
+#pragma unroll
+  for (int j = 0; j < PM; ++j) sh[j] = j < p ? t.X[(int64_t)j * t.ld] : 0.0;
+  double acc[NA];
+#pragma unroll
+  for (int e = 0; e < NA; ++e) acc[e] = 0.0;
+  const int total = t.G[0] + t.G[1];
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
+    const int f = g < t.G[0] ? 0 : 1;
+    const int gg = f ? g - t.G[0] : g;
+    const double n = (double)t.cnt[f][gg];
+    if (n == 0.0) continue;
+    const double* al = t.alpha[f] + (int64_t)gg * p;
+    const double* Sg = t.S[f] + (int64_t)gg * p;
+    const double* Tg = t.TQ + (int64_t)gg * p;
+    double av[PM], V[PM];
+#pragma unroll
+    for (int j = 0; j < PM; ++j) {
+      if (j < p) {
+        av[j] = f ? al[j] - sh[j] : al[j];
+        V[j] = Sg[j] - n * sh[j] - (f ? Tg[j] : 0.0);
+      } else {
+        av[j] = V[j] = 0.0;
+      }
+    }
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < PM; ++i)
+#pragma unroll
+      for (int j = i; j < PM; ++j, ++e) acc[e] += (n * av[i] - V[i]) * av[j] - av[i] * V[j];
+#pragma unroll
+    for (int i = 0; i < PM; ++i) acc[NG + i] += n * av[i];
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < NA; ++e) {
+    double v = acc[e];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[wave][e] = v;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NA; e += blockDim.x)
+    partial[(int64_t)blockIdx.x * NA + e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+}
+
+// one block: the design tile [16][16] (column 0 = intercept, 1 + j = data column j)
+// from the raw tile + table partials; *flag = 1 when the cancellation guard holds
+template <int PM>
+__global__ __launch_bounds__(256) void k_tables_final(const double* __restrict__ partial, int nblk,
+                                                      const double* __restrict__ raw, int p,
+                                                      double* __restrict__ tile, double* __restrict__ flag) {
+  constexpr int NG = PM * (PM + 1) / 2;
+  constexpr int NA = NG + PM;
+  __shared__ double m[NA];
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  for (int e = threadIdx.x; e < NA; e += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < nblk; ++b) s += partial[(int64_t)b * NA + e];
+    m[e] = s;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 256; t += blockDim.x) {
+    const int i = t / 16 - 1, j = t % 16 - 1;  // design indices -> data columns
+    double v = 0.0;
+    if (i < p && j < p) {
+      if (i < 0 && j < 0) {
+        v = raw[15 * 16 + 15];
+      } else if (i < 0 || j < 0) {
+        const int d = i < 0 ? j : i;
+        v = raw[15 * 16 + d] - m[NG + d];
+      } else {
+        const int lo = i < j ? i : j, hi = i < j ? j : i;
+        v = raw[i * 16 + j] + m[lo * PM - lo * (lo - 1) / 2 + (hi - lo)];
+        if (i == j && !(v > 0.0 && raw[i * 16 + i] <= kTabKappa * v)) atomicAdd(&bad, 1);
+      }
+    }
+    tile[t] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = bad ? 0.0 : 1.0;
+}
+
+static bool tables_gram_ok(const lfe_ctx* c) {
+  return c->raw_ready && c->tq_final && c->F == 2 && c->world == 1 && c->p <= 12 && c->L.P >= 0 && !c->L.w;
+}
+
+// design tile into out_dev[0, 256) and the guard flag into *flag_dev, from the group tables
+static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev) {
+  const int P = c->L.P, Q = 1 - P, p = c->p;
+  TabArgs t{};
+  t.alpha[0] = c->fe[P].alpha;
+  t.alpha[1] = c->fe[Q].alpha;
+  t.S[0] = c->fe[P].S;
+  t.S[1] = c->fe[Q].S;
+  t.TQ = c->fe[Q].T;
+  t.cnt[0] = c->fe[P].cnt;
+  t.cnt[1] = c->fe[Q].cnt;
+  t.G[0] = c->fe[P].G;
+  t.G[1] = c->fe[Q].G;
+  t.p = p;
+  t.X = c->L.X;
+  t.ld = c->ld;
+  const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
+  const int NA = PM * (PM + 1) / 2 + PM;
+  const int nblk = grid_for((int64_t)t.G[0] + t.G[1], 256, 64);  // few partials: the final sum is serial
+  LFE_TRY(ensure_scratch(c, (size_t)nblk * NA));
+  ProfScope _ps(c, K_GRAM_TABLES);
+  double* part = c->scratch;
+  switch (PM) {
+    case 4:
+      hipLaunchKernelGGL(k_tables_gram<4>, dim3(nblk), dim3(256), 0, c->stream, t, part);
+      hipLaunchKernelGGL(k_tables_final<4>, dim3(1), dim3(256), 0, c->stream, part, nblk, c->raw_tile, p, out_dev,
+                         flag_dev);
+      break;
+    case 8:
+      hipLaunchKernelGGL(k_tables_gram<8>, dim3(nblk), dim3(256), 0, c->stream, t, part);
+      hipLaunchKernelGGL(k_tables_final<8>, dim3(1), dim3(256), 0, c->stream, part, nblk, c->raw_tile, p, out_dev,
+                         flag_dev);
+      break;
+    default:
+      hipLaunchKernelGGL(k_tables_gram<12>, dim3(nblk), dim3(256), 0, c->stream, t, part);
+      hipLaunchKernelGGL(k_tables_final<12>, dim3(1), dim3(256), 0, c->stream, part, nblk, c->raw_tile, p, out_dev,
+                         flag_dev);
+      break;
+  }
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out) {
+  hipLaunchKernelGGL(k_reduce_partials, dim3(256), dim3(256), 0, c->stream, part, nblocks, (int64_t)256, out);
+}
+
 // beta_full of X = [1, x] from the reduced design tile (column 0 intercept, 1 y, 2.. x):
 // Cholesky of X'X and two triangular solves, one thread (m <= 12).  ok = 0 when X'X is
 // not positive definite (the host then solves as polars_impl.py:217-220 does).
@@ -1024,19 +1190,25 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
   GramArgs a = base_args(c);
   if (!(resid_rows_ok(c, a) && c->p <= 11)) return 1;
   const int p = c->p, k = p - 1;
-  // dred: [0, 256) design tile | [256, 516) residual tile + stats | 516 ok | [520, 532) beta
+  // dred: [0, 256) design tile | [256, 516) residual tile + stats | 516 ok | [520, 532) beta | 532 tables guard
   LFE_TRY(ensure_dred(c, 544));
-  LFE_TRY(design_rows_enqueue(c, a, c->dred));
-  hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dred, p, c->dbeta, c->dred + 520, c->dred + 516);
-  LFE_HIP(hipGetLastError());
-  a.nq = 1;
-  a.qf[0] = 1 - a.la.P;
-  a.G_Q = c->fe[a.qf[0]].G;
-  a.beta = c->dbeta;
-  a.scores = keep_scores ? c->scores : nullptr;
-  LFE_TRY(resid_rows_enqueue(c, a, c->dred + 256));
-  std::vector<double> h(532);
-  LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 532));
+  std::vector<double> h(533);
+  for (int pass = tables_gram_ok(c) ? 0 : 1; pass < 2; ++pass) {
+    if (pass == 0) LFE_TRY(tables_gram_enqueue(c, c->dred, c->dred + 532));
+    else LFE_TRY(design_rows_enqueue(c, a, c->dred));
+    hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dred, p, c->dbeta, c->dred + 520,
+                       c->dred + 516);
+    LFE_HIP(hipGetLastError());
+    GramArgs ar = a;
+    ar.nq = 1;
+    ar.qf[0] = 1 - a.la.P;
+    ar.G_Q = c->fe[ar.qf[0]].G;
+    ar.beta = c->dbeta;
+    ar.scores = keep_scores ? c->scores : nullptr;
+    LFE_TRY(resid_rows_enqueue(c, ar, c->dred + 256));
+    LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 533));
+    if (pass == 1 || h[532] == 1.0) break;  // guard failed: the explicit design pass
+  }
   if (h[516] != 1.0) return 1;  // not positive definite: the caller takes the two-call path
   const int D = p + 1;
   for (int i = 0; i < D; ++i)

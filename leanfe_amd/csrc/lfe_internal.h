@@ -74,7 +74,7 @@ struct FeState {
 enum KernelId {
   K_PART_HIST = 0, K_SCAN, K_PART_SCATTER, K_COUNT, K_MARK, K_GROUP_SUMS, K_CROSS, K_CHECK, K_FINALIZE,
   K_CHECK_MAX, K_GRAM_DESIGN, K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_MISC, K_SYNTH,
-  K_TP, K_TQ, K_SEG_BUILD, K_CLUSTER_SORT, K_NUM_KERNELS
+  K_TP, K_TQ, K_SEG_BUILD, K_CLUSTER_SORT, K_GRAM_TABLES, K_NUM_KERNELS
 };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 
@@ -206,6 +206,14 @@ struct lfe_ctx {
   double* rec_syy = nullptr;     // [ld] sum (w) y^2 per record
   double* rec_lay = nullptr;     // [2][ld] the two above in layout order
   size_t rec_sy_cap = 0, rec_syy_cap = 0, rec_lay_cap = 0;
+  // Gram from group tables (two FEs, unweighted, one process): the group-sum pass also forms
+  // the raw Gram of the shifted data columns, so lfe_gram_resid needs no design pass
+  double* raw_part = nullptr;    // [blocks][256] per-block raw tiles
+  size_t raw_part_cap = 0;
+  double* raw_tile = nullptr;    // [256] raw tile: slots 0..p-1 data (shifted by row 0), slot 15 intercept
+  size_t raw_tile_cap = 0;
+  bool raw_ready = false;        // raw_tile holds this layout's kept rows
+  bool tq_final = false;         // fe[Q].T = sum over q of the final alpha_P (demean_fast)
   // scratch
   double* scratch = nullptr;     // device partials
   size_t scratch_elems = 0;
@@ -257,6 +265,7 @@ int launch_gram(lfe_ctx* c, double* host_gram);
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores, int icpt);
 int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
+void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out);  // sum of [nblocks][256] tiles
 // --- YOCO records (lfe_compress.hip) ---
 int records_layout(lfe_ctx* c);   // rec_sy / rec_syy in layout order -> rec_lay
 // --- device keys (lfe_keys.hip) ---

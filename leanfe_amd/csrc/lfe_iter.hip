@@ -787,6 +787,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   }
   *iterations_out = iterations;
   *last_out = last;
+  c->tq_final = true;  // fq.T was formed from the final alpha_P (the Gram-from-tables cross term)
   return LFE_OK;
 }
 

@@ -281,3 +281,26 @@ def test_yoco_auto_selects_compress_and_hash_collisions_are_exact(monkeypatch):
     r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="compress", vcov="cluster", cluster_cols=["cl1"],
                    quiet=True)
     _assert_yoco(r, o, xs)
+
+
+def test_gram_from_tables_guard_falls_back_to_the_design_pass():
+    """Two-FE fits form the Gram from the group tables (R + table terms); when the FE part
+    explains almost all of a column's variance that sum cancels, the device guard trips and
+    the explicit design pass runs instead.  Both regimes must match the oracle."""
+    from leanfe_amd import leanfe_hip
+    n, L = 400_000, [20_000, 300]
+    for scale in (0.5, 1e3):  # kappa ~ 1 (tables) and ~1e6 (> 1e4: design pass)
+        d = synth.panel(n, 3, L, seed=61)
+        eff = np.random.default_rng(61).normal(0, 1, L[0])
+        d["x1"] = d["x1"] + scale * eff[d["fe1"]]
+        xs, fes = ["x1", "x2", "x3"], ["fe1", "fe2"]
+        o = altproj.fit(d, "y", xs, fes, vcov="HC1")
+        from leanfe_amd._lib import Engine
+        with Engine(0) as eng:
+            eng.profile(True)
+            r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov="HC1", quiet=True,
+                           engine=eng)
+            ks = eng.kernel_stats()
+        assert "gram_tables" in ks
+        assert ("gram_design" in ks) == (scale > 1.0), sorted(ks)
+        _assert_same(r, o["beta"], o["se"], o["n_obs"], o["iterations"], o["df_resid"], o["fe_dims"], None, xs)
