@@ -65,13 +65,16 @@ def solve_step(eng: Engine, vcov: str):
     order = sorted(range(len(card)), key=lambda i: card[i])
     iterations, _ = eng.demean(order, 1e-6, 50, check_from=3)
     hc1 = vcov.lower() == "hc1"
-    fused = eng.gram_resid(hc1=hc1)  # Gram + device solve + residual pass, one round trip
+    # HC1: Gram + device solve + residual pass, one round trip; IID: the Gram alone
+    fused = eng.gram_resid(hc1=hc1) if hc1 else None
     G = fused[0] if fused is not None else eng.gram()
     XtX, Xty = inference.split_gram(G)
     beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
     k = XtX.shape[0] - 1
     df_resid = n_obs - (k + 1) - (sum(dims) - len(dims))
-    stats, meat = (fused[2], fused[3]) if fused is not None else eng.resid(beta_full, hc1=hc1)
+    stats, meat = (fused[2], fused[3]) if fused is not None else (inference.stats_from_gram(G, beta_full), None)
+    if stats is None:
+        stats, meat = eng.resid(beta_full, hc1=hc1)
     if vcov.lower() == "hc1":
         se = inference.se_hc1(XtX_inv[1:, 1:], meat, n_obs, df_resid)
     else:

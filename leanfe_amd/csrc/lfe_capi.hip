@@ -362,7 +362,8 @@ static void free_data(lfe_ctx* c) {
   c->rec_sy_cap = c->rec_syy_cap = c->rec_lay_cap = 0;
   dfree(c->raw_part);
   dfree(c->raw_tile);
-  c->raw_part_cap = c->raw_tile_cap = 0;
+  dfree(c->raw_shift);
+  c->raw_part_cap = c->raw_tile_cap = c->raw_shift_cap = 0;
   c->raw_ready = c->tq_final = false;
   c->records = false;
   c->rows_in = 0;

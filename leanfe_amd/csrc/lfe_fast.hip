@@ -56,7 +56,7 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   d4 racc[4];  // one per row of the quad: independent MFMA chains (issue never waits on the previous one)
 #pragma unroll
   for (int s = 0; s < 4; ++s) racc[s] = d4{0.0, 0.0, 0.0, 0.0};
-  const double shift = (RAW && c < p) ? a.X[(int64_t)c * a.ld] : 0.0;
+  const double shift = (RAW && c < p && a.la.n_items > 0) ? a.X[(int64_t)c * a.ld] : 0.0;
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
       for (int j = tid; j < a.G[f] * p; j += TH) lds[a.tab_off[f] + j] = 0.0;
@@ -170,6 +170,37 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   }
 }
 
+// raw_shift[16 + j] = this rank's shift (first layout row; 0 for an empty shard);
+// raw_shift[j] = rank 0's (summed over ranks afterwards)
+__global__ void k_raw_shift(const double* __restrict__ X, int64_t ld, int p, int has_rows, int rank,
+                            double* __restrict__ sh) {
+  const int j = threadIdx.x;
+  if (j >= 16) return;
+  const double own = (j < p && has_rows) ? X[(int64_t)j * ld] : 0.0;
+  sh[16 + j] = own;
+  sh[j] = rank == 0 ? own : 0.0;
+}
+
+// re-centre this rank's raw tile from its own shift c_r to the common shift c*:
+// sum (d - c*)(d - c*)' = R + dl C' + C dl' + n dl dl',  sum (d - c*) = C + n dl,  dl = c_r - c*
+__global__ void k_raw_recenter(double* __restrict__ R, const double* __restrict__ sh, int p) {
+  __shared__ double C[16], dl[16];
+  const int t = threadIdx.x;
+  if (t < 16) {
+    C[t] = R[15 * 16 + t];
+    dl[t] = t < p ? sh[16 + t] - sh[t] : 0.0;
+  }
+  __syncthreads();
+  const double n = R[15 * 16 + 15];
+  const int i = t / 16, j = t % 16;
+  double v = R[t];
+  if (i < p && j < p) v += dl[i] * C[j] + C[i] * dl[j] + n * dl[i] * dl[j];
+  else if (i == 15 && j < p) v += n * dl[j];
+  else if (j == 15 && i < p) v += n * dl[i];
+  __syncthreads();
+  R[t] = v;
+}
+
 int sums4(lfe_ctx* c) {
   Sums4Args a{};
   a.la = layout_args(c);
@@ -208,8 +239,7 @@ int sums4(lfe_ctx* c) {
     const char* e = getenv("LFE_TABLE_GRAM");  // 0: no Gram from tables (explicit design pass)
     return e ? atoi(e) : 1;
   }();
-  const bool raw = raw_env != 0 && c->F == 2 && P >= 0 && a.nq == 1 && p <= 15 && !a.w && c->world == 1 &&
-                   gu_env != 4;
+  const bool raw = raw_env != 0 && c->F == 2 && P >= 0 && a.nq == 1 && p <= 15 && !a.w && gu_env != 4;
   c->raw_ready = false;
   int threads = kSumThreads;
   if (a.nq <= 1 && NT == 1) {
@@ -243,7 +273,17 @@ int sums4(lfe_ctx* c) {
   LFE_HIP(hipGetLastError());
   if (raw) {
     reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
+    LFE_TRY(ensure_f64(c, c->raw_shift, c->raw_shift_cap, 32));
+    hipLaunchKernelGGL(k_raw_shift, dim3(1), dim3(64), 0, c->stream, c->L.X, c->ld, p, c->L.n_items > 0 ? 1 : 0,
+                       c->rank, c->raw_shift);
     LFE_HIP(hipGetLastError());
+    if (c->world > 1) {
+      // every rank's tile re-centred on rank 0's shift, then summed: the global raw Gram
+      LFE_TRY(allreduce_sum_f64(c, c->raw_shift, 16));
+      hipLaunchKernelGGL(k_raw_recenter, dim3(1), dim3(256), 0, c->stream, c->raw_tile, c->raw_shift, p);
+      LFE_HIP(hipGetLastError());
+      LFE_TRY(allreduce_sum_f64(c, c->raw_tile, 256));
+    }
     c->raw_ready = true;
   }
   for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_f64(c, c->fe[f].S, (size_t)c->fe[f].G * p));

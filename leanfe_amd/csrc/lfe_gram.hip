@@ -911,8 +911,7 @@ struct TabArgs {
   const int32_t* cnt[2];
   int G[2];
   int p;
-  const double* X;         // layout X: the shift is row 0
-  int64_t ld;
+  const double* shift;     // [16] the raw tile's shift c
 };
 
 template <int PM>
@@ -923,7 +922,7 @@ __global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restri
   const int p = t.p;
   double sh[PM];
 #pragma unroll
-  for (int j = 0; j < PM; ++j) sh[j] = j < p ? t.X[(int64_t)j * t.ld] : 0.0;
+  for (int j = 0; j < PM; ++j) sh[j] = j < p ? t.shift[j] : 0.0;
   double acc[NA];
 #pragma unroll
   for (int e = 0; e < NA; ++e) acc[e] = 0.0;
@@ -1005,7 +1004,7 @@ __global__ __launch_bounds__(256) void k_tables_final(const double* __restrict__
 }
 
 static bool tables_gram_ok(const lfe_ctx* c) {
-  return c->raw_ready && c->tq_final && c->F == 2 && c->world == 1 && c->p <= 12 && c->L.P >= 0 && !c->L.w;
+  return c->raw_ready && c->tq_final && c->F == 2 && c->p <= 12 && c->L.P >= 0 && !c->L.w;
 }
 
 // design tile into out_dev[0, 256) and the guard flag into *flag_dev, from the group tables
@@ -1022,8 +1021,7 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev) {
   t.G[0] = c->fe[P].G;
   t.G[1] = c->fe[Q].G;
   t.p = p;
-  t.X = c->L.X;
-  t.ld = c->ld;
+  t.shift = c->raw_shift;
   const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
   const int NA = PM * (PM + 1) / 2 + PM;
   const int nblk = grid_for((int64_t)t.G[0] + t.G[1], 256, 64);  // few partials: the final sum is serial
@@ -1127,10 +1125,18 @@ int launch_gram(lfe_ctx* c, double* host_gram) {
     return e ? atoi(e) : 0;
   }();
   if (lanes != 1 && resid_rows_ok(c, a) && c->p <= 11) {
-    LFE_TRY(ensure_dred(c, 256));
-    LFE_TRY(design_rows_enqueue(c, a, c->dred));
-    std::vector<double> h(256);
-    LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 256));
+    LFE_TRY(ensure_dred(c, 260));
+    std::vector<double> h(257);
+    bool done = false;
+    if (tables_gram_ok(c)) {  // the Gram from the group tables, unless its guard trips
+      LFE_TRY(tables_gram_enqueue(c, c->dred, c->dred + 256));
+      LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 257));
+      done = h[256] == 1.0;
+    }
+    if (!done) {
+      LFE_TRY(design_rows_enqueue(c, a, c->dred));
+      LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 256));
+    }
     const int D = c->p + 1;
     for (int i = 0; i < D; ++i)
       for (int j = 0; j < D; ++j) host_gram[i * D + j] = h[(size_t)i * 16 + j];

@@ -210,8 +210,10 @@ struct lfe_ctx {
   // the raw Gram of the shifted data columns, so lfe_gram_resid needs no design pass
   double* raw_part = nullptr;    // [blocks][256] per-block raw tiles
   size_t raw_part_cap = 0;
-  double* raw_tile = nullptr;    // [256] raw tile: slots 0..p-1 data (shifted by row 0), slot 15 intercept
+  double* raw_tile = nullptr;    // [256] raw tile: slots 0..p-1 data (shifted by raw_shift), slot 15 intercept
   size_t raw_tile_cap = 0;
+  double* raw_shift = nullptr;   // [32]: [0, 16) the shift of raw_tile (rank 0's first row on every rank),
+  size_t raw_shift_cap = 0;      //       [16, 32) this rank's own first row
   bool raw_ready = false;        // raw_tile holds this layout's kept rows
   bool tq_final = false;         // fe[Q].T = sum over q of the final alpha_P (demean_fast)
   // scratch

@@ -161,15 +161,21 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                                 formula=formula, fe_cols=fe_cols, fe_dims=fe_dims, r_squared=None,
                                 compression_ratio=est_comp_ratio, rss=rss, tss=None, backend="hip",
                                 timings=timings)
+        # IID without weights: the residual statistics follow from the Gram (no residual pass)
+        gram_only = v == "iid" and weights is None
         # Gram + solve + residual pass; one host round trip when the fused path applies
         # (the residuals then use the device's Cholesky solve of the same Gram)
-        fused = eng.gram_resid(hc1=(v == "hc1"), keep_scores=(v == "cluster"))
+        fused = None if gram_only else eng.gram_resid(hc1=(v == "hc1"), keep_scores=(v == "cluster"))
         G = fused[0] if fused is not None else eng.gram()
         XtX, Xty = inference.split_gram(G)
         beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # polars_impl.py:212-226, host
         beta = beta_full[1:]
         Vb = XtX_inv[1:, 1:]
-        if fused is not None:
+        stats = inference.stats_from_gram(G, beta_full) if gram_only else None
+        meat = None
+        if stats is not None:
+            pass
+        elif fused is not None:
             stats, meat = fused[2], fused[3]
         else:
             stats, meat = eng.resid(beta_full, hc1=(v == "hc1"), keep_scores=(v == "cluster"))

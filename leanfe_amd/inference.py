@@ -40,6 +40,23 @@ def split_gram(G: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
     return G[np.ix_(idx, idx)].copy(), G[idx, 1].copy()
 
 
+# rss from the Gram cancels as R^2 -> 1: below this share of sum y~^2 the residual pass runs
+RSS_FROM_GRAM_MIN = 1e-4
+
+
+def stats_from_gram(G: np.ndarray, beta_full: np.ndarray):
+    """Residual statistics {sum r^2, sum r^2, sum y~, sum y~^2} of an unweighted fit from
+    the Gram of [1, y~, x~] alone: r'r = y'y - 2 b'X'y + b'X'X b (polars_impl.py:229,
+    281-282 without the residual pass).  None when r'r < RSS_FROM_GRAM_MIN * y'y."""
+    idx = [0] + list(range(2, G.shape[0]))
+    yy = G[1, 1]
+    Xy = G[idx, 1]
+    rss = yy - 2.0 * beta_full @ Xy + beta_full @ G[np.ix_(idx, idx)] @ beta_full
+    if not (rss > RSS_FROM_GRAM_MIN * yy):
+        return None
+    return np.array([rss, rss, G[0, 1], yy])
+
+
 def se_iid(XtX_inv_b: np.ndarray, rss_w: float, df_resid: int) -> np.ndarray:
     sigma2 = rss_w / df_resid
     return np.sqrt(np.maximum(sigma2 * np.diag(XtX_inv_b), 0.0))

@@ -51,6 +51,8 @@ def test_golden_fixture(name):
     r = _hip_fit(meta, data, demean_tol=meta["demean_tol"], max_iter=meta["max_iter"])
     _assert_same(r, exp["oracle_beta"], exp["oracle_se"], int(exp["oracle_n_obs"]), int(exp["oracle_iterations"]),
                  int(exp["oracle_df_resid"]), exp["oracle_fe_dims"].tolist(), meta["oracle_n_clusters"], meta["xs"])
+    if np.isfinite(exp["oracle_r2"]) and not meta.get("instruments"):  # R^2 (IID: from the Gram alone)
+        np.testing.assert_allclose(r.r_squared, float(exp["oracle_r2"]), rtol=1e-10)
     if meta.get("instruments"):  # the reference's own 2SLS / IV SE functions on the same demeaned columns
         assert r.is_iv and r.n_instruments == len(meta["instruments"]) and r.r_squared is None
         np.testing.assert_allclose([r.std_errors[x] for x in meta["xs"]], exp["ref_se"], rtol=RTOL, atol=0)
