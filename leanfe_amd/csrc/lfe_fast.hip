@@ -112,11 +112,23 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) valid[s] = rb[u] + s >= it.y && rb[u] + s < it.z && hv[s] >= 0;
         if (RAW) {
+          // one MFMA per row of the quad, each followed by that row's LDS atomics, so the
+          // matrix core works while the wave keeps issuing (NT = 1, unweighted, one FE besides P)
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             const double z = !valid[s] ? 0.0 : (c == 15 ? 1.0 : (c < p ? xv[u][0][s] - shift : 0.0));
             racc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[s], 0, 0, 0);
+            if (c < p && valid[s]) {
+              const double v = xv[u][0][s];
+              if (a.slice) atomicAdd(&lds[(hv[s] - lo) * p + c], v);
+              else atomicAdd(&a.S[P][(int64_t)hv[s] * p + c], v);
+              const int f = a.qf[0];
+              const int g = (&cq[u][0].x)[s];
+              if (a.tab_off[f] >= 0) atomicAdd(&lds[a.tab_off[f] + g * p + c], v);
+              else atomicAdd(&a.S[f][(int64_t)g * p + c], v);
+            }
           }
+          continue;
         }
 #pragma unroll
         for (int I = 0; I < NT; ++I) {
