@@ -21,9 +21,10 @@ from collections import defaultdict
 
 # engine kernel id -> demangled kernel name prefix
 KERNELS = {
-    "part_hist": "k_part_hist", "part_scatter": "k_part_scatter", "mark": "k_mark",
-    "group_sums": "k_sums4", "tp": "k_tp", "tq": "k_tq",
-    "gram_design": "k_gram<0,", "gram_resid": "k_gram<1,",
+    "part_hist": ("k_part_hist",), "part_scatter": ("k_part_scatter",), "mark": ("k_mark",),
+    "group_sums": ("k_sums4",), "tp": ("k_tp",), "tq": ("k_tq",),
+    "gram_design": ("k_design_rows", "k_gram<0,"), "gram_resid": ("k_resid_rows", "k_gram<1,"),
+    "gram_tables": ("k_tables_gram",), "layout_sort": ("k_ls_scatter",),
 }
 
 ap = argparse.ArgumentParser()
@@ -57,7 +58,7 @@ out = {"config": {"rows": a.rows, "k": a.k, "levels": [int(x) for x in a.levels.
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes); bytes = 2*FETCH + WRITE",
        "kernels": {}}
 for kid, prefix in KERNELS.items():
-    fk = [n for n in fetch if n.startswith(prefix.replace(" ", ""))]
+    fk = [n for n in fetch if any(n.startswith(px.replace(" ", "")) for px in prefix)]
     if not fk:
         continue
     fv = [v for n in fk for v in fetch[n]]
