@@ -1061,60 +1061,54 @@ void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out) {
 // indexed a scratch array and took ~70 us).
 __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __restrict__ beta,
                              double* __restrict__ beta_copy, double* __restrict__ ok) {
+  // one wave: right-looking Cholesky in LDS (a column step is a sqrt, a scaled column and a
+  // trailing update spread over the lanes), then the two triangular solves on lane 0
   constexpr int M = 12;
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  __shared__ double L[M][M + 1];
+  __shared__ double b[M];
+  __shared__ int bad;
+  const int t = threadIdx.x;
   const int m = p;  // intercept + k regressors
-  double L[M][M], b[M], y[M];
   auto idx = [](int i) { return i == 0 ? 0 : i + 1; };
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    b[i] = i < m ? tile[idx(i) * 16 + 1] : 0.0;
-#pragma unroll
-    for (int j = 0; j < M; ++j) L[i][j] = (i < m && j <= i) ? tile[idx(i) * 16 + idx(j)] : 0.0;
+  for (int e = t; e < M * M; e += blockDim.x) {
+    const int i = e / M, j = e % M;
+    L[i][j] = (i < m && j < m) ? tile[idx(i) * 16 + idx(j)] : 0.0;
   }
-  bool pd = true;
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    if (j < m) {
-      double d = L[j][j];
-#pragma unroll
-      for (int t = 0; t < j; ++t) d -= L[j][t] * L[j][t];
-      pd = pd && d > 0.0;
-      const double ljj = sqrt(d > 0.0 ? d : 1.0);
-      L[j][j] = ljj;
-#pragma unroll
-      for (int i = j + 1; i < M; ++i) {
-        double v = L[i][j];
-#pragma unroll
-        for (int t = 0; t < j; ++t) v -= L[i][t] * L[j][t];
-        L[i][j] = v / ljj;
-      }
+  if (t < M) b[t] = t < m ? tile[idx(t) * 16 + 1] : 0.0;
+  if (t == 0) bad = 0;
+  __syncthreads();
+  for (int j = 0; j < m; ++j) {
+    if (t == 0) {
+      const double d = L[j][j];
+      if (!(d > 0.0)) bad = 1;
+      L[j][j] = sqrt(d > 0.0 ? d : 1.0);
     }
+    __syncthreads();
+    if (t > j && t < m) L[t][j] /= L[j][j];
+    __syncthreads();
+    for (int e = t; e < M * M; e += blockDim.x) {
+      const int i = e / M, k = e % M;
+      if (i > j && k > j && k <= i && i < m) L[i][k] -= L[i][j] * L[k][j];
+    }
+    __syncthreads();
   }
-  if (!pd) {
+  if (t != 0) return;
+  if (bad) {
     *ok = 0.0;
     return;
   }
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
+  // in place on the LDS right-hand side (a dynamically indexed private array would live in scratch)
+  for (int i = 0; i < m; ++i) {
     double v = b[i];
-#pragma unroll
-    for (int t = 0; t < i; ++t) v -= L[i][t] * y[t];
-    y[i] = i < m ? v / L[i][i] : 0.0;
+    for (int k = 0; k < i; ++k) v -= L[i][k] * b[k];
+    b[i] = v / L[i][i];
   }
-#pragma unroll
-  for (int i = M - 1; i >= 0; --i) {
-    if (i < m) {
-      double v = y[i];
-#pragma unroll
-      for (int t = i + 1; t < M; ++t)
-        if (t < m) v -= L[t][i] * b[t];
-      b[i] = v / L[i][i];
-    }
+  for (int i = m - 1; i >= 0; --i) {
+    double v = b[i];
+    for (int k = i + 1; k < m; ++k) v -= L[k][i] * b[k];
+    b[i] = v / L[i][i];
   }
-#pragma unroll
-  for (int i = 0; i < M; ++i)
-    if (i < m) beta[i] = beta_copy[i] = b[i];
+  for (int i = 0; i < m; ++i) beta[i] = beta_copy[i] = b[i];
   *ok = 1.0;
 }
 
