@@ -65,6 +65,19 @@ int lfe_load(lfe_ctx* ctx, int64_t n, int p, const double* const* cols, int F,
              const int32_t* const* fe_codes, const int32_t* n_levels,
              const double* weights, int where);
 
+/* Chunked upload for streaming ingest (the reference streams
+ * Parquet with pl.scan_parquet, polars_impl.py:341-343).  lfe_load_begin sizes the shard
+ * (n rows, p columns, F FEs with n_levels, weighted or not); lfe_load_rows copies rows
+ * [row0, row0 + rows) of every column (and code array, and weights) from host memory
+ * asynchronously, returning once the copies issued two calls earlier have completed, so
+ * the caller keeps the host arrays of its last two calls alive and decodes the next chunk
+ * while this one crosses PCIe; lfe_load_finish waits, validates the codes (as lfe_load)
+ * and marks the shard loaded.  The calls must cover every row exactly once. */
+int lfe_load_begin(lfe_ctx* ctx, int64_t n, int p, int F, const int32_t* n_levels, int weighted);
+int lfe_load_rows(lfe_ctx* ctx, int64_t row0, int64_t rows, const double* const* cols,
+                  const int32_t* const* fe_codes, const double* weights);
+int lfe_load_finish(lfe_ctx* ctx);
+
 /* Fill the context with rows [row_offset, row_offset+n) of the counter-based
  * synthetic panel (leanfe_amd/synth.py) directly on the device: p = 1 + k
  * columns, F = n_fe FE code arrays with n_levels[f] levels. */

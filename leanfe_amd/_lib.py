@@ -33,6 +33,9 @@ SIGNATURES = {
     "lfe_emu_destroy": (None, [_vp]),
     "lfe_ctx_set_emu": (C.c_int, [_vp, _vp, C.c_int]),
     "lfe_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.POINTER(_vp), C.c_int, C.POINTER(_vp), _i32p, _vp, C.c_int]),
+    "lfe_load_begin": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, C.c_int]),
+    "lfe_load_rows": (C.c_int, [_vp, C.c_int64, C.c_int64, C.POINTER(_vp), C.POINTER(_vp), _vp]),
+    "lfe_load_finish": (C.c_int, [_vp]),
     "lfe_synth_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, _dp, C.c_uint64, C.c_int64]),
     "lfe_load_clusters": (C.c_int, [_vp, C.c_int, C.POINTER(_vp), _i32p, C.c_int]),
     "lfe_drop_singletons": (C.c_int, [_vp, _i64p, _i32p, _i32p]),
@@ -162,6 +165,32 @@ class Engine:
         _check(self._lib.lfe_load(self._h, n, len(cols), cp, len(codes), kp, lv,
                                   None if w is None else _ptr(w), LFE_HOST))
         self.p, self.F, self.n = len(cols), len(codes), n
+
+    # -- chunked upload (streaming ingest) --------------------------------
+    def load_begin(self, n: int, p: int, levels: list[int], weighted: bool = False) -> None:
+        lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
+        _check(self._lib.lfe_load_begin(self._h, int(n), int(p), len(levels), lv, 1 if weighted else 0))
+        self.p, self.F, self.n = int(p), len(levels), int(n)
+        self._inflight = []
+
+    def load_rows(self, row0: int, cols: list[np.ndarray], codes: list[np.ndarray],
+                  weights: np.ndarray | None = None) -> None:
+        """Rows [row0, row0 + len) of every column; asynchronous (the engine returns once the
+        copies of two calls ago are done, so the arrays of the last two calls are kept here)."""
+        cols = [np.ascontiguousarray(c, dtype=np.float64) for c in cols]
+        codes = [np.ascontiguousarray(c, dtype=np.int32) for c in codes]
+        rows = cols[0].size if cols else 0
+        if len(cols) != self.p or len(codes) != self.F or any(a.size != rows for a in cols + codes):
+            raise ValueError("load_rows: p columns and F code arrays of equal length expected")
+        w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
+        cp = (_vp * len(cols))(*[_ptr(c) for c in cols])
+        kp = (_vp * max(len(codes), 1))(*[_ptr(c) for c in codes])
+        _check(self._lib.lfe_load_rows(self._h, int(row0), rows, cp, kp, None if w is None else _ptr(w)))
+        self._inflight = (self._inflight + [(cols, codes, w)])[-2:]
+
+    def load_finish(self) -> None:
+        _check(self._lib.lfe_load_finish(self._h))
+        self._inflight = []
 
     def synth_load(self, n: int, k: int, levels: list[int], beta: np.ndarray, seed: int = 12345,
                    row_offset: int = 0) -> None:

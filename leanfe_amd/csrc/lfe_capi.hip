@@ -367,6 +367,7 @@ static void free_data(lfe_ctx* c) {
   c->raw_ready = c->tq_final = false;
   c->records = false;
   c->rows_in = 0;
+  c->loading = false;
   c->L = Layout();
   c->loaded = c->prepared = c->demeaned = c->scores_valid = c->seg_ready = false;
   c->n = c->ld = 0;
@@ -509,6 +510,8 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   if (c->hpin) (void)hipHostFree(c->hpin);
   if (c->hpin_items) (void)hipHostFree(c->hpin_items);
   if (c->hpin_ev) (void)hipEventDestroy(c->hpin_ev);
+  for (auto& e : c->load_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->aux_ev) (void)hipEventDestroy(c->aux_ev);
   dfree(c->clS);
   dfree(c->clP);
@@ -588,6 +591,53 @@ int lfe_load(lfe_ctx* c, int64_t n, int p, const double* const* cols, int F, con
   if (weights && n > 0) LFE_HIP(hipMemcpyAsync(c->w, weights, sizeof(double) * n, kind, c->stream));
   for (int f = 0; f < F && n > 0; ++f)
     LFE_HIP(hipMemcpyAsync(c->fe[f].code, fe_codes[f], sizeof(int32_t) * n, kind, c->stream));
+  LFE_TRY(validate_all(c));
+  c->loaded = true;
+  return LFE_OK;
+}
+
+int lfe_load_begin(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_levels, int weighted) {
+  LFE_CTX(c);
+  if (F > 0 && !n_levels) return fail(LFE_EINVAL, "n_levels is null");
+  LFE_TRY(alloc_data(c, n, p, F, n_levels, weighted != 0));
+  for (auto& e : c->load_ev)
+    if (!e) LFE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  c->load_calls = 0;
+  c->load_rows_done = 0;
+  c->loading = true;
+  return LFE_OK;
+}
+
+int lfe_load_rows(lfe_ctx* c, int64_t row0, int64_t rows, const double* const* cols, const int32_t* const* fe_codes,
+                  const double* weights) {
+  LFE_CTX(c);
+  if (!c->loading) return fail(LFE_ESTATE, "lfe_load_begin first");
+  if (row0 < 0 || rows < 0 || row0 + rows > c->n) return fail(LFE_EINVAL, "rows outside the shard");
+  if (rows > 0 && (!cols || (c->F > 0 && !fe_codes) || ((c->w != nullptr) != (weights != nullptr))))
+    return fail(LFE_EINVAL, "null input pointer (or weights given to an unweighted shard)");
+  // the copies issued two calls ago have finished: the caller may release those host arrays
+  const int slot = (int)(c->load_calls & 1);
+  LFE_HIP(hipEventSynchronize(c->load_ev[slot]));
+  for (int j = 0; j < c->p && rows > 0; ++j)
+    LFE_HIP(hipMemcpyAsync(c->X + (size_t)j * c->ld + row0, cols[j], sizeof(double) * rows, hipMemcpyHostToDevice,
+                           c->stream));
+  if (c->w && rows > 0)
+    LFE_HIP(hipMemcpyAsync(c->w + row0, weights, sizeof(double) * rows, hipMemcpyHostToDevice, c->stream));
+  for (int f = 0; f < c->F && rows > 0; ++f)
+    LFE_HIP(hipMemcpyAsync(c->fe[f].code + row0, fe_codes[f], sizeof(int32_t) * rows, hipMemcpyHostToDevice,
+                           c->stream));
+  LFE_HIP(hipEventRecord(c->load_ev[slot], c->stream));
+  ++c->load_calls;
+  c->load_rows_done += rows;
+  return LFE_OK;
+}
+
+int lfe_load_finish(lfe_ctx* c) {
+  LFE_CTX(c);
+  if (!c->loading) return fail(LFE_ESTATE, "lfe_load_begin first");
+  c->loading = false;
+  if (c->load_rows_done != c->n) return fail(LFE_EINVAL, "lfe_load_rows did not cover the shard's rows");
+  LFE_HIP(hipStreamSynchronize(c->stream));
   LFE_TRY(validate_all(c));
   c->loaded = true;
   return LFE_OK;

@@ -231,6 +231,10 @@ struct lfe_ctx {
   size_t clS_elems = 0;
   int32_t* clP = nullptr;        // cluster presence flags [C] + counter
   size_t clP_elems = 0;
+  // chunked upload (lfe_load_begin / lfe_load_rows / lfe_load_finish)
+  hipEvent_t load_ev[2] = {nullptr, nullptr};
+  int64_t load_calls = 0, load_rows_done = 0;
+  bool loading = false;
   // state
   int64_t n_kept = 0;
   bool loaded = false, prepared = false, demeaned = false;

@@ -45,6 +45,23 @@ def get_columns(data, names: list[str]) -> dict[str, np.ndarray]:
     raise TypeError(f"unsupported data type: {type(data)!r}")
 
 
+def parquet_rows(path: str) -> int:
+    import pyarrow.parquet as pq
+    return int(pq.ParquetFile(path).metadata.num_rows)
+
+
+def stream_parquet(path: str, names: list[str], batch_rows: int = 1 << 22):
+    """Yield (row0, {name: ndarray}) batches of a Parquet file's columns, in file order
+    (the streaming counterpart of ``pl.scan_parquet``, polars_impl.py:341-343): one
+    batch is decoded while the previous one is uploaded."""
+    import pyarrow.parquet as pq
+    row0 = 0
+    for rb in pq.ParquetFile(path).iter_batches(batch_size=int(batch_rows), columns=list(names)):
+        out = {c: _arrow_to_numpy(rb.column(c)) for c in names}
+        yield row0, out
+        row0 += rb.num_rows
+
+
 def _arrow_to_numpy(col) -> np.ndarray:
     import pyarrow as pa
     if pa.types.is_dictionary(col.type):

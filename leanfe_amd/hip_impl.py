@@ -65,7 +65,18 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         needed += list(cluster_cols)
     if weights is not None:
         needed.append(weights)
-    cols = frame.get_columns(data, needed)
+    # a Parquet path streams: the FE / cluster / weight columns are read first (for the codes),
+    # then [y] + x + instruments are decoded batch by batch while earlier batches upload
+    # (pl.scan_parquet's role, polars_impl.py:341-343)
+    stream = (isinstance(data, str) and not factor_vars and not interactions and sample_frac is None
+              and os.environ.get("LEANFE_HIP_STREAM", "1") != "0")
+    num_cols = [y_col] + x_cols + instruments  # the columns leanfe demeans (polars_impl.py:486)
+    if stream:
+        small = list(dict.fromkeys(fe_cols + list(cluster_cols or []) + ([weights] if weights else [])))
+        cols = frame.get_columns(data, small) if small else {}
+        n_rows = frame.parquet_rows(data)
+    else:
+        cols = frame.get_columns(data, needed)
 
     if interactions:
         x_cols = x_cols + frame.expand_interactions(cols, interactions)
@@ -87,12 +98,28 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             codes.append(c)
             levels.append(g)
         levels = dist.agree_levels(eng, levels)
-        Y = np.asarray(cols[y_col], dtype=np.float64)
-        Xc = [np.asarray(cols[c], dtype=np.float64) for c in x_cols + instruments]  # polars_impl.py:486
         w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
-
+        # polars_impl.py:180: an all-ones instrument stops 2SLS from adding an intercept to Z.
+        # Demeaned instruments cannot be all ones; without FEs they are the raw columns.
+        z_ones = {z: not fe_cols for z in instruments}
         t0 = time.perf_counter()
-        eng.load([Y] + Xc, codes, levels, w)
+        if stream:
+            eng.load_begin(n_rows, len(num_cols), levels, weighted=w is not None)
+            batch = int(os.environ.get("LEANFE_HIP_STREAM_BATCH", 1 << 22))
+            for row0, b in frame.stream_parquet(data, num_cols, batch_rows=batch):
+                sl = slice(row0, row0 + len(b[y_col]))
+                eng.load_rows(row0, [b[c] for c in num_cols], [c[sl] for c in codes], None if w is None else w[sl])
+                for z in instruments:
+                    z_ones[z] = z_ones[z] and bool(np.allclose(np.asarray(b[z], dtype=np.float64), 1.0))
+            eng.load_finish()
+            n_initial = n_rows
+        else:
+            Y = np.asarray(cols[y_col], dtype=np.float64)
+            Xc = [np.asarray(cols[c], dtype=np.float64) for c in num_cols[1:]]
+            for z in instruments:
+                z_ones[z] = z_ones[z] and bool(np.allclose(np.asarray(cols[z], dtype=np.float64), 1.0))
+            eng.load([Y] + Xc, codes, levels, w)
+            n_initial = Y.size
         t_load = time.perf_counter() - t0
         n_obs, fe_dims, fe_card = eng.drop_singletons()
         fe_cardinality = dict(zip(fe_cols, fe_card))
@@ -101,7 +128,6 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         if strategy == "auto":
             # distinct (x, FE) rows / n over all loaded rows, exact (compress.py:187-253), on the
             # GPU; a row shard cannot see the other shards' rows, so sharded fits skip it
-            n_initial = Y.size
             if not sharded and n_initial:
                 est_comp_ratio = eng.count_distinct_rows() / n_initial
             elif not sharded:
@@ -151,8 +177,8 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         k = len(x_cols)
         df_resid = n_obs - (k + 1) - absorbed_df
         if instruments:
-            beta, se, n_clusters, rss, stats = _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, fe_cols,
-                                                       sharded, n_obs, df_resid, ssc)
+            beta, se, n_clusters, rss, stats = _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v,
+                                                       any(z_ones.values()), sharded, n_obs, df_resid, ssc)
             timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
             return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta))),
                                 std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
@@ -225,17 +251,13 @@ def _cluster_se(eng, cols, cluster_cols, sharded, Vb, to_meat, n_obs, df_resid, 
                                          n_obs, df_resid, ssc)
 
 
-def _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, fe_cols, sharded, n_obs, df_resid, ssc):
+def _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, z_has_ones, sharded, n_obs, df_resid, ssc):
     """IV/2SLS branch of ``_run_regression`` (polars_impl.py:176-200, 229, 254-270):
     the device Gram of [1, y~, x~, z~] -> host 2SLS (inference.IVSystem) -> one device
     residual pass r = y~ - X_hat beta_full with u = [1, x~, z~] meats / scores -> the
     reference's IV SEs (std_errors.py:448-602), intercept stripped."""
     k, m = len(x_cols), len(instruments)
     G = eng.gram()
-    # polars_impl.py:180: a Z column of all ones stops the intercept from being added.
-    # Demeaned instruments cannot be all ones; without FEs they are the raw columns.
-    z_has_ones = not fe_cols and any(np.allclose(np.asarray(cols[z], dtype=np.float64), 1.0)
-                                     for z in instruments)
     iv = inference.IVSystem(G, k, m, z_has_ones=z_has_ones)
     stats, meat_u = eng.resid_iv(iv.coef, meat=(v == "hc1"), keep_scores=(v == "cluster"))
     n_clusters = None

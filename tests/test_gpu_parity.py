@@ -306,3 +306,29 @@ def test_gram_from_tables_guard_falls_back_to_the_design_pass():
         assert "gram_tables" in ks
         assert ("gram_design" in ks) == (scale > 1.0), sorted(ks)
         _assert_same(r, o["beta"], o["se"], o["n_obs"], o["iterations"], o["df_resid"], o["fe_dims"], None, xs)
+
+
+@pytest.mark.parametrize("vcov,weights,inst", [("HC1", False, False), ("cluster", True, False), ("iid", False, True)])
+def test_parquet_path_streams_and_matches_in_memory(tmp_path, monkeypatch, vcov, weights, inst):
+    """A Parquet path streams (FE / cluster / weight columns first, then [y] + x (+ z) in
+    batches through lfe_load_rows): the fit equals the in-memory one (to the last bits the
+    atomic group sums leave free; the integer outputs exactly)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from leanfe_amd import leanfe_hip
+    d = synth.panel(300_001, 3, [5000, 80], seed=71)
+    rng = np.random.default_rng(71)
+    d["w"] = rng.uniform(0.5, 2.0, d["y"].size)
+    d["cl"] = rng.integers(0, 400, d["y"].size)
+    d["z1"] = d["x1"] + rng.normal(0, 1, d["y"].size)
+    path = str(tmp_path / "panel.parquet")
+    pq.write_table(pa.table(d), path, row_group_size=70_000)
+    monkeypatch.setenv("LEANFE_HIP_STREAM_BATCH", "65536")
+    formula = "y ~ x1 + x2 + x3 | fe1 + fe2" + (" | z1 + x2 + x3" if inst else "")
+    kw = dict(formula=formula, strategy="alt_proj", vcov=vcov, cluster_cols=["cl"] if vcov == "cluster" else None,
+              weights="w" if weights else None, quiet=True)
+    a = leanfe_hip(path, **kw)
+    b = leanfe_hip(d, **kw)
+    for x in ("x1", "x2", "x3"):
+        np.testing.assert_allclose([a.coefs[x], a.std_errors[x]], [b.coefs[x], b.std_errors[x]], rtol=1e-13, atol=0)
+    assert a.n_obs == b.n_obs and a.iterations == b.iterations and a.n_clusters == b.n_clusters

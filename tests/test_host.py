@@ -207,3 +207,22 @@ def test_iv_system_matches_oracle_2sls(weighted, z_ones):
     meat_u = u.T @ (u * s[:, None])
     se = inference.se_hc1(iv.XtX_inv, iv.xhat_meat(meat_u), n, n - (k + 1))
     np.testing.assert_allclose(se[1:], o["se"], rtol=1e-10)
+
+
+def test_stream_parquet_batches_cover_rows_in_order(tmp_path):
+    """frame.stream_parquet (the streaming ingest of a Parquet path) yields every row once,
+    in file order, with the requested columns only."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    n = 10_007
+    d = {"y": np.arange(n, dtype=np.float64), "x": np.arange(n, dtype=np.float64) * 2, "fe": np.arange(n) % 7}
+    path = str(tmp_path / "p.parquet")
+    pq.write_table(pa.table(d), path, row_group_size=3000)
+    assert frame.parquet_rows(path) == n
+    seen = []
+    for row0, b in frame.stream_parquet(path, ["y", "x"], batch_rows=1024):
+        assert set(b) == {"y", "x"}
+        assert b["y"][0] == row0 and np.array_equal(b["x"], 2 * b["y"])
+        seen.append((row0, len(b["y"])))
+    assert seen[0][0] == 0 and sum(m for _, m in seen) == n
+    assert all(r + m == r2 for (r, m), (r2, _) in zip(seen, seen[1:]))

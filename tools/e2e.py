@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--vcov", default="HC1")
     ap.add_argument("--sparse-ids", action="store_true", help="FE ids as sparse int64 (device factorization)")
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--parquet", default=None, help="also time leanfe(<this Parquet path>): streamed and read whole")
     a = ap.parse_args()
     levels = [int(x) for x in a.levels.split(",")]
     t0 = time.perf_counter()
@@ -49,6 +50,23 @@ def main():
                           wall_s=[round(t, 3) for t in out], gen_s=round(t_gen, 2), iterations=r.iterations,
                           compression_ratio=r.compression_ratio,
                           timings={k: round(v, 4) for k, v in r.timings.items()})), flush=True)
+    if a.parquet:
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+        t0 = time.perf_counter()
+        pq.write_table(pa.table(data), a.parquet, row_group_size=1 << 20)
+        t_write = time.perf_counter() - t0
+        del data
+        for mode in ("1", "0"):  # streamed (lfe_load_rows per batch) / read whole, then lfe_load
+            os.environ["LEANFE_HIP_STREAM"] = mode
+            walls = []
+            for _ in range(a.repeat):
+                t0 = time.perf_counter()
+                r = leanfe_hip(a.parquet, formula=formula, vcov=a.vcov, strategy="alt_proj", quiet=True)
+                walls.append(time.perf_counter() - t0)
+            print(json.dumps(dict(rows=a.rows, parquet=True, streamed=mode == "1", write_s=round(t_write, 2),
+                                  wall_s=[round(t, 3) for t in walls], mrows_s=round(a.rows / min(walls) / 1e6, 1),
+                                  load_s=round(r.timings["load_s"], 3), iterations=r.iterations)), flush=True)
 
 
 if __name__ == "__main__":
