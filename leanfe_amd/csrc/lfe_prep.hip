@@ -351,13 +351,25 @@ struct MarkArgs {
   const int32_t* cnt_pre[kMaxFE];
   int32_t* drops[kMaxFE];
   int32_t* ndropped;
+  const int32_t* any;   // number of singleton groups (k_any_singleton); 0: nothing to mark
+  int G[kMaxFE];
 };
+
+// singleton groups over every FE (pre-filter counts of 1): k_mark returns at once without any
+__global__ void k_any_singleton(MarkArgs a, int32_t* __restrict__ out) {
+  int found = 0;
+  for (int f = 0; f < a.F; ++f)
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G[f]; g += gridDim.x * blockDim.x)
+      found |= a.cnt_pre[f][g] == 1;
+  if (__any(found) && (threadIdx.x & 63) == 0) atomicAdd(out, 1);
+}
 
 // single-pass singleton marks (polars_impl.py:477-482): a row is dropped when any
 // of its FE groups has a pre-filter count of 1.  F is a template parameter and a
 // thread handles 4 consecutive rows (16-byte code loads; the layout is padded to ld).
 template <int F>
 __global__ __launch_bounds__(256) void k_mark(MarkArgs a, int64_t n) {
+  if (*a.any == 0) return;  // no group has a single row: nothing is dropped
   const int64_t n4 = (n + 3) >> 2;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i0 = t << 2;
@@ -642,6 +654,15 @@ int prepare_layout(lfe_ctx* c) {
       a.drops[f] = fe.drops;
     }
     a.ndropped = ndropped;
+    a.any = ndropped + 1;
+    int gmax = 1;
+    for (int f = 0; f < c->F; ++f) {
+      a.G[f] = c->fe[f].G;
+      gmax = std::max(gmax, c->fe[f].G);
+    }
+    hipLaunchKernelGGL(k_any_singleton, dim3(grid_for(gmax, kBlock, 256)), dim3(kBlock), 0, c->stream, a,
+                       ndropped + 1);
+    LFE_HIP(hipGetLastError());
     // YOCO records keep every record: compress has no singleton drop (compress.py:1049-1175);
     // a record alone in its level is fitted exactly by its own dummy
     if (n && !c->records) {
