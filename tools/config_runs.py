@@ -29,12 +29,16 @@ def solve(eng, vcov, cl_levels=None):
     n_obs, dims, card = eng.drop_singletons()
     order = sorted(range(len(card)), key=lambda i: card[i])
     iterations, _ = eng.demean(order, 1e-6, 50, check_from=3)
-    XtX, Xty = inference.split_gram(eng.gram())
+    G = eng.gram()
+    XtX, Xty = inference.split_gram(G)
     beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
     k = XtX.shape[0] - 1
     df = n_obs - (k + 1) - (sum(dims) - len(dims))
     v = vcov.lower()
-    stats, meat = eng.resid(beta_full, hc1=v == "hc1", keep_scores=v == "cluster")
+    stats = inference.stats_from_gram(G, beta_full) if v == "iid" else None  # as leanfe_hip: no residual pass
+    meat = None
+    if stats is None:
+        stats, meat = eng.resid(beta_full, hc1=v == "hc1", keep_scores=v == "cluster")
     out = dict(n_obs=n_obs, iterations=iterations, beta=beta_full[1:], df_resid=df, fe_dims=list(dims))
     if v == "hc1":
         out["se"] = inference.se_hc1(XtX_inv[1:, 1:], meat, n_obs, df)
