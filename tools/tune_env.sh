@@ -1,18 +1,18 @@
 #!/bin/bash
-# time bench.py under each of several environment settings: VARIANTS="A=1 B=2;A=2" (';'-separated)
+# Tuning sweep on one box: bench.py once per value of an engine tuning variable.
+#   VAR=LFE_TQ_SPLIT VALUES="1 2 4" KEYS="tq,tp" bash tools/tune_env.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-python -m leanfe_amd.build > gpurun_out/build.log 2>&1 || exit 1
-i=0
-IFS=';' read -ra VS <<< "${VARIANTS:-}"
-for v in "${VS[@]}"; do
-  i=$((i+1))
-  env $v timeout -k 10 300 python bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu > gpurun_out/tune_$i.log 2>&1
-  rc=$?; [ $rc -eq 0 ] || { echo "[$v] rc=$rc"; exit $rc; }
-  python - "$i" "$v" <<'PY'
+for v in ${VALUES}; do
+  env ${VAR}=${v} timeout -k 10 120 python bench.py --no-cpu --steps ${STEPS:-10} --warmup 5 > gpurun_out/tune_${v}.log 2>&1
+  rc=$?
+  [ $rc -eq 0 ] || { echo "${VAR}=${v} rc=$rc"; tail -3 gpurun_out/tune_${v}.log; exit $rc; }
+  python - "$v" "${KEYS:-}" <<'PY'
 import json, sys
-l = json.loads(open(f"gpurun_out/tune_{sys.argv[1]}.log").read().strip().splitlines()[-1])
-print(f"[{sys.argv[2]}] value {l['value']} ms/step {l['ms_per_step']}", {n: v[0] for n, v in l["kernels_ms"].items() if v[0] > 0.1})
+v, keys = sys.argv[1], [k for k in sys.argv[2].split(",") if k]
+d = json.loads([l for l in open(f"gpurun_out/tune_{v}.log") if l.startswith("{")][-1])
+ks = d["kernels_ms"]
+print(f"{v:>8}: {d['ms_per_step']:.3f} ms/step  " + "  ".join(f"{k}={ks[k][0]:.4f}" for k in keys if k in ks))
 PY
 done
