@@ -216,6 +216,7 @@ struct lfe_ctx {
   size_t raw_shift_cap = 0;      //       [16, 32) this rank's own first row
   bool raw_ready = false;        // raw_tile holds this layout's kept rows
   bool tq_final = false;         // fe[Q].T = sum over q of the final alpha_P (demean_fast)
+  bool hists_kept = false;       // seg_aux holds the kept rows' per-item histograms (no row dropped)
   // scratch
   double* scratch = nullptr;     // device partials
   size_t scratch_elems = 0;
@@ -257,6 +258,8 @@ int prepare_layout(lfe_ctx* c);   // partition + counts + singleton marks
 int sums4(lfe_ctx* c);
 // --- two-FE sweeps (lfe_iter.hip) ---
 bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order);
+bool fast_layout_ok(const lfe_ctx* c);            // the two-FE layouts fit (any FE order)
+int layout_hists(lfe_ctx* c, int Q);              // per-item histograms of both codes -> seg_aux
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out);
 
 // --- constant sums (lfe_sweep.hip) ---

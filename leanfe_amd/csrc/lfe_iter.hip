@@ -274,21 +274,31 @@ static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off,
   return LFE_OK;
 }
 
+// per-item histograms of both keys in one pass (seg_aux = [n_items][B] ++ [n_items][G_Q]) over
+// the rows whose primary code is >= 0 (before the singleton marks: every row)
+int layout_hists(lfe_ctx* c, int Q) {
+  auto& L = c->L;
+  const int B = 1 << L.s;
+  const int32_t G_Q = c->fe[Q].G;
+  const size_t n1 = (size_t)L.n_items * B;
+  LFE_TRY(ensure_i32(c, c->seg_aux, c->seg_aux_cap, n1 + (size_t)L.n_items * G_Q));
+  ProfScope _ps(c, K_MISC);
+  hipLaunchKernelGGL(k_ls_hist2, dim3(L.n_items), dim3(256), sizeof(int32_t) * ((size_t)B + G_Q), c->stream,
+                     reinterpret_cast<const int4*>(c->items_d), L.code[L.P], L.code[Q], L.s, B, (int)G_Q, c->seg_aux,
+                     c->seg_aux + n1);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
 static int build_layouts(lfe_ctx* c, int Q) {
   auto& L = c->L;
   const int B = 1 << L.s;
   const int32_t G_Q = c->fe[Q].G;
-  const int P = L.P;
-  // per-item histograms of both keys in one pass (seg_aux = [n_items][B] ++ [n_items][G_Q])
   const size_t n1 = (size_t)L.n_items * B;
-  LFE_TRY(ensure_i32(c, c->seg_aux, c->seg_aux_cap, n1 + (size_t)L.n_items * G_Q));
-  {
-    ProfScope _ps(c, K_MISC);
-    hipLaunchKernelGGL(k_ls_hist2, dim3(L.n_items), dim3(256), sizeof(int32_t) * ((size_t)B + G_Q), c->stream,
-                       reinterpret_cast<const int4*>(c->items_d), L.code[P], L.code[Q], L.s, B, (int)G_Q,
-                       c->seg_aux, c->seg_aux + n1);
-  }
-  LFE_HIP(hipGetLastError());
+  // the pre-filter histograms of prepare_layout are the kept rows' when nothing was dropped
+  // (used once: the local sorts below turn them into item bases)
+  if (!c->hists_kept) LFE_TRY(layout_hists(c, Q));
+  c->hists_kept = false;
   LFE_TRY(ensure_i32(c, c->seg_q, c->seg_q_cap, (size_t)c->ld));
   LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, c->seg_q)));
   LFE_TRY(ensure_u16(c, c->run_h, c->run_h_cap, (size_t)c->ld));
@@ -678,8 +688,11 @@ static int fin_check(lfe_ctx* c, int f, const double* T, const double* cur, doub
 }
 
 bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order) {
+  return order.back() == c->L.P && fast_layout_ok(c);
+}
+
+bool fast_layout_ok(const lfe_ctx* c) {
   if (c->F != 2 || c->L.w || c->L.P < 0 || !c->L.permuted) return false;
-  if (order.back() != c->L.P) return false;
   const int Q = 1 - c->L.P, p = c->p;
   const int64_t G_Q = c->fe[Q].G, B = 1ll << c->L.s;
   return (G_Q + 1) * p * 8 <= kIterLds                 // K1: alpha_Q in LDS

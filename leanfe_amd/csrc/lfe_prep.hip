@@ -330,6 +330,29 @@ __global__ void k_gather_bstart(const int32_t* __restrict__ scanned, int nb, int
 // counts on the layout + singleton marks
 // ---------------------------------------------------------------------------
 
+// pre-filter counts from the per-item histograms of the two-FE layouts: primary group h sums
+// its bucket's items (cnt1[item][h - lo]); secondary level q sums a 1/64 slice of all items
+__global__ void k_cnt_from_items_p(const int32_t* __restrict__ cnt1, const int32_t* __restrict__ bitems, int s,
+                                   int32_t G, int32_t* __restrict__ cnt) {
+  const int B = 1 << s;
+  for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < G; h += gridDim.x * blockDim.x) {
+    const int b = h >> s, j = h & (B - 1);
+    int32_t t = 0;
+    for (int i = bitems[b]; i < bitems[b + 1]; ++i) t += cnt1[(int64_t)i * B + j];
+    cnt[h] = t;
+  }
+}
+
+__global__ void k_cnt_from_items_q(const int32_t* __restrict__ cnt2, int n_items, int32_t G,
+                                   int32_t* __restrict__ cnt) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= G) return;
+  const int i0 = (int)((int64_t)blockIdx.y * n_items / gridDim.y), i1 = (int)((int64_t)(blockIdx.y + 1) * n_items / gridDim.y);
+  int32_t t = 0;
+  for (int i = i0; i < i1; ++i) t += cnt2[(int64_t)i * G + q];
+  if (t) atomicAdd(&cnt[q], t);
+}
+
 // primary-FE counts: per work item an LDS slice of 2^s bins
 __global__ __launch_bounds__(256) void k_count_items(const int4* __restrict__ items, const int32_t* __restrict__ code,
                                                      int s, int32_t G, int32_t* __restrict__ cnt) {
@@ -508,11 +531,16 @@ int prepare_layout(lfe_ctx* c) {
   L.nb = L.P >= 0 ? (int)(((int64_t)c->fe[L.P].G + (1ll << L.s) - 1) >> L.s) : 1;
   L.permuted = L.nb > 1 && n > 0;
 
+  // two-FE fast layouts: both FEs' pre-filter counts come from the layouts' per-item
+  // histograms (formed after the partition, reused by build_layouts when nothing is dropped)
+  c->hists_kept = false;
+  L.w = c->w;  // fast_layout_ok reads it before the layout pointers are set below
+  const bool item_counts = L.permuted && fast_layout_ok(c);
   // pre-filter counts of every FE (on input codes, except P when bucketed)
   for (int f = 0; f < c->F; ++f) {
     auto& fe = c->fe[f];
     LFE_HIP(hipMemsetAsync(fe.cnt_pre, 0, sizeof(int32_t) * fe.G, c->stream));
-    if (n == 0 || (f == L.P && L.permuted)) continue;
+    if (n == 0 || (f == L.P && L.permuted) || item_counts) continue;
     ProfScope _ps(c, K_COUNT);
     if (fe.G <= kLdsHistMax)
       hipLaunchKernelGGL(k_hist_lds, dim3(grid_for((n + 3) / 4, 256, 2048)), dim3(256), sizeof(int32_t) * fe.G, c->stream,
@@ -629,7 +657,18 @@ int prepare_layout(lfe_ctx* c) {
   }
   LFE_TRY(build_items(c));
 
-  if (L.permuted) {
+  if (item_counts) {
+    const int Q = 1 - L.P, B = 1 << L.s;
+    LFE_TRY(layout_hists(c, Q));
+    ProfScope _ps(c, K_COUNT);
+    const int32_t* c1 = c->seg_aux;
+    const int32_t* c2 = c->seg_aux + (size_t)L.n_items * B;
+    hipLaunchKernelGGL(k_cnt_from_items_p, dim3(grid_for(c->fe[L.P].G)), dim3(kBlock), 0, c->stream, c1, c->bitems_d,
+                       L.s, c->fe[L.P].G, c->fe[L.P].cnt_pre);
+    hipLaunchKernelGGL(k_cnt_from_items_q, dim3((c->fe[Q].G + 255) / 256, 64), dim3(256), 0, c->stream, c2,
+                       L.n_items, c->fe[Q].G, c->fe[Q].cnt_pre);
+    LFE_HIP(hipGetLastError());
+  } else if (L.permuted) {
     ProfScope _ps(c, K_COUNT);
     auto& fe = c->fe[L.P];
     hipLaunchKernelGGL(k_count_items, dim3(L.n_items), dim3(256), sizeof(int32_t) << L.s, c->stream,
@@ -701,6 +740,7 @@ int prepare_layout(lfe_ctx* c) {
     c->fe[f].dims = h[2 * f];
     c->fe[f].card = h[2 * f + 1];
   }
+  c->hists_kept = item_counts && h[2 * kMaxFE] == 0;
   // kept rows over all ranks
   double kept = (double)(n - h[2 * kMaxFE]);
   if (c->world > 1) {
