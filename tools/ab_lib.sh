@@ -1,0 +1,19 @@
+#!/bin/bash
+# Same-box A/B of two engine builds: tools/ab_old.so (baseline) vs the in-tree library.
+#   KEYS="part_scatter" ROUNDS=3 bash tools/ab_lib.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+for r in $(seq 1 ${ROUNDS:-3}); do
+  for lib in tools/ab_old.so leanfe_amd/liblfe_hip.so; do
+    LEANFE_HIP_LIB=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu --steps ${STEPS:-10} --warmup 5 > gpurun_out/ab.log 2>&1
+    rc=$?; [ $rc -eq 0 ] || { echo "$lib rc=$rc"; tail -3 gpurun_out/ab.log; exit $rc; }
+    python - "$lib" "${KEYS:-}" <<'PY'
+import json, sys
+lib, keys = sys.argv[1], [k for k in sys.argv[2].split(",") if k]
+d = json.loads([l for l in open("gpurun_out/ab.log") if l.startswith("{")][-1])
+ks = d["kernels_ms"]
+print(f"{lib:>28}: {d['ms_per_step']:.3f} ms/step  " + "  ".join(f"{k}={ks[k][0]:.4f}" for k in keys if k in ks))
+PY
+  done
+done
