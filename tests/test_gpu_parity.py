@@ -332,3 +332,24 @@ def test_parquet_path_streams_and_matches_in_memory(tmp_path, monkeypatch, vcov,
     for x in ("x1", "x2", "x3"):
         np.testing.assert_allclose([a.coefs[x], a.std_errors[x]], [b.coefs[x], b.std_errors[x]], rtol=1e-13, atol=0)
     assert a.n_obs == b.n_obs and a.iterations == b.iterations and a.n_clusters == b.n_clusters
+
+
+def test_nan_input_gives_nan_estimates_without_faulting():
+    """The Polars path filters no NULLs (polars_impl.py:468-537), so a NaN in y spreads through the
+    projections and the estimates are NaN.  How many sweeps the reference then runs depends on
+    Polars' NaN-ignoring max over partly-NaN group means and is not pinned by any reference test or
+    fixture; only the NaN estimates and a clean return are checked here."""
+    from leanfe_amd import leanfe_hip
+    d = synth.panel(30_000, 2, [600, 40], seed=81)
+    d["y"] = d["y"].copy()
+    d["y"][123] = np.nan
+    r = leanfe_hip(d, formula="y ~ x1 + x2 | fe1 + fe2", strategy="alt_proj", vcov="iid", quiet=True)
+    assert 3 <= r.iterations <= 50
+    assert all(np.isnan(r.coefs[x]) for x in ("x1", "x2"))
+
+
+def test_empty_input_raises():
+    from leanfe_amd import leanfe_hip
+    d = {"y": np.zeros(0), "x": np.zeros(0), "a": np.zeros(0, dtype=np.int64), "b": np.zeros(0, dtype=np.int64)}
+    with pytest.raises(Exception):
+        leanfe_hip(d, formula="y ~ x | a + b", strategy="alt_proj", quiet=True)

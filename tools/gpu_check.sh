@@ -7,7 +7,8 @@ mkdir -p gpurun_out
 python -m leanfe_amd.build > gpurun_out/build.log 2>&1 || { echo build failed; exit 1; }
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 if [ "${RUN_TESTS:-1}" = 1 ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-500} python -m pytest tests -m gpu -q -x -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/pytest.log 2>&1
+  eval "set -- ${PYTEST_ARGS:-}"  # shell-quoted extra arguments, e.g. PYTEST_ARGS="-k 'a or b'"
+  timeout -k 10 ${TEST_TIMEOUT:-500} python -m pytest tests -m gpu -q -x -p no:cacheprovider "$@" > gpurun_out/pytest.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest.log
   ok $rc || exit $rc
 fi
