@@ -64,7 +64,16 @@ __global__ __launch_bounds__(256) void k_part_hist(const int32_t* __restrict__ c
   for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)w * cw, r1 = min(n, r0 + cw);
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) atomicAdd(&h[code[i] >> s], 1);
+  // 16-byte code loads (chunk starts are multiples of 4 rows; the shard's tail is scalar)
+  const int64_t v1 = r0 + ((r1 - r0) & ~(int64_t)3);
+  for (int64_t i = r0 + 4 * (int64_t)threadIdx.x; i < v1; i += 4 * (int64_t)blockDim.x) {
+    const int4 g = *reinterpret_cast<const int4*>(code + i);
+    atomicAdd(&h[g.x >> s], 1);
+    atomicAdd(&h[g.y >> s], 1);
+    atomicAdd(&h[g.z >> s], 1);
+    atomicAdd(&h[g.w >> s], 1);
+  }
+  for (int64_t i = v1 + threadIdx.x; i < r1; i += blockDim.x) atomicAdd(&h[code[i] >> s], 1);
   __syncthreads();
   for (int b = threadIdx.x; b < nb; b += blockDim.x) counts[(int64_t)b * nw + w] = h[b];
 }
