@@ -55,13 +55,24 @@ __global__ __launch_bounds__(256) void k_ls_hist2(const int4* __restrict__ items
   const int lo = it.x << s;
   for (int j = threadIdx.x; j < K1 + K2; j += blockDim.x) h[j] = 0;
   __syncthreads();
-  for (int32_t i = it.y + threadIdx.x; i < it.z; i += blockDim.x) {
-    const int32_t g = codeP[i];
+  // 16-byte code loads over the 4-aligned middle of the item, scalar at its two ends
+  const int32_t a0 = min(it.z, (it.y + 3) & ~3), a1 = max(a0, it.z & ~3);
+  auto one = [&](int32_t g, int32_t q) {
     if (g >= 0) {
       atomicAdd(&h1[g - lo], 1);
-      atomicAdd(&h2[codeQ[i]], 1);
+      atomicAdd(&h2[q], 1);
     }
+  };
+  for (int32_t i = it.y + threadIdx.x; i < a0; i += blockDim.x) one(codeP[i], codeQ[i]);
+  for (int32_t i = a0 + 4 * threadIdx.x; i < a1; i += 4 * blockDim.x) {
+    const int4 g = *reinterpret_cast<const int4*>(codeP + i);
+    const int4 q = *reinterpret_cast<const int4*>(codeQ + i);
+    one(g.x, q.x);
+    one(g.y, q.y);
+    one(g.z, q.z);
+    one(g.w, q.w);
   }
+  for (int32_t i = a1 + threadIdx.x; i < it.z; i += blockDim.x) one(codeP[i], codeQ[i]);
   __syncthreads();
   for (int j = threadIdx.x; j < K1; j += blockDim.x) cnt1[(int64_t)blockIdx.x * K1 + j] = h1[j];
   for (int j = threadIdx.x; j < K2; j += blockDim.x) cnt2[(int64_t)blockIdx.x * K2 + j] = h2[j];
@@ -123,7 +134,11 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
   const int lo = it.x << s;
   for (int j = tid; j < K; j += kLsThreads)
     run[j] = off[(int64_t)it.x * K + j] + itembase[(int64_t)item * K + j];
-  for (int32_t r0 = it.y; r0 < it.z; r0 += kLsRows) {
+  // sub-chunks start at multiples of 4 rows and slots k .. k + 3 of a lane are 4 consecutive
+  // rows, so the codes come in 16-byte loads (rows before it.y are masked; the shared cursor
+  // set makes the order within a key free anyway)
+  static_assert(kLsPer % 4 == 0, "rows per thread in fours");
+  for (int32_t r0 = it.y & ~3; r0 < it.z; r0 += kLsRows) {
     const int32_t r1 = min(it.z, r0 + kLsRows);
     const int32_t wbase = r0 + wave * kLsPer * 64;
     __syncthreads();
@@ -131,16 +146,22 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
     __syncthreads();
     int32_t key[kLsPer], val[kLsPer];
 #pragma unroll
-    for (int k = 0; k < kLsPer; ++k) {
-      const int32_t i = wbase + k * 64 + lane;
-      key[k] = -1;
-      if (i < r1) {
-        const int32_t g = codeP[i];
-        if (g >= 0) {
-          const int32_t q = codeQ[i];
-          key[k] = KEYQ ? q : g - lo;
-          val[k] = KEYQ ? g - lo : q;
-          atomicAdd(&cur[(NCUR > 1 ? wave : 0) * K + key[k]], 1);
+    for (int k = 0; k < kLsPer; k += 4) {
+      const int32_t i0 = wbase + (k >> 2) * 256 + 4 * lane;
+      int4 g4 = int4{-1, -1, -1, -1}, q4 = int4{0, 0, 0, 0};
+      if (i0 < r1) {
+        g4 = *reinterpret_cast<const int4*>(codeP + i0);
+        q4 = *reinterpret_cast<const int4*>(codeQ + i0);
+      }
+      const int32_t gv[4] = {g4.x, g4.y, g4.z, g4.w}, qv[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int32_t i = i0 + t;
+        key[k + t] = -1;
+        if (i >= it.y && i < r1 && gv[t] >= 0) {
+          key[k + t] = KEYQ ? qv[t] : gv[t] - lo;
+          val[k + t] = KEYQ ? gv[t] - lo : qv[t];
+          atomicAdd(&cur[(NCUR > 1 ? wave : 0) * K + key[k + t]], 1);
         }
       }
     }
