@@ -473,17 +473,29 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
       __syncthreads();
       staged = it.x;
     }
-    for (int rb = it.y + wave * 64 * UR; rb < it.z; rb += NW * 64 * UR) {
+    // a lane takes UR = 2 consecutive rows (from an even base; rows before it.y are masked), so
+    // columns come in 16-byte loads and the two code arrays in 8-byte loads
+    static_assert(UR == 2, "row pairs");
+    for (int rb = (it.y & ~1) + wave * 64 * UR; rb < it.z; rb += NW * 64 * UR) {
       int hq[UR], qq[UR];
       double x[UR][PM];
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      const int r0 = rb + 2 * lane;
+      const bool in0 = r0 < it.z;  // r0 + 1 <= ld - 1: r0 is even and ld a multiple of 64
+      {
+        const int2 h2 = in0 ? *reinterpret_cast<const int2*>(codeP + r0) : int2{-1, -1};
+        const int2 q2 = in0 ? *reinterpret_cast<const int2*>(codeQ + r0) : int2{0, 0};
+        const bool lo_in = in0 && r0 >= it.y, hi_in = in0 && r0 + 1 < it.z;
+        hq[0] = lo_in ? h2.x : -1;
+        hq[1] = hi_in ? h2.y : -1;
+        qq[0] = lo_in ? q2.x : 0;
+        qq[1] = hi_in ? q2.y : 0;
 #pragma unroll
-      for (int u = 0; u < UR; ++u) {
-        const int r = rb + u * 64 + lane;
-        const bool in = r < it.z;
-        hq[u] = in ? codeP[r] : -1;
-        qq[u] = in ? codeQ[r] : 0;
-#pragma unroll
-        for (int cc = 0; cc < PM; ++cc) x[u][cc] = (in && cc < p) ? a.X[(int64_t)cc * a.ld + r] : 0.0;
+        for (int cc = 0; cc < PM; ++cc) {
+          const d2 v = (in0 && cc < p) ? *reinterpret_cast<const d2*>(a.X + (int64_t)cc * a.ld + r0) : d2{0.0, 0.0};
+          x[0][cc] = v.x;
+          x[1][cc] = v.y;
+        }
       }
 #pragma unroll
       for (int u = 0; u < UR; ++u) {
@@ -516,7 +528,7 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
 #pragma unroll
           for (int j = i; j < KM; ++j, ++e) m[e] += wv[i] * wv[j];
         if (a.scores) {
-          const int r = rb + u * 64 + lane;
+          const int r = rb + 2 * lane + u;
 #pragma unroll
           for (int j = 0; j < KM; ++j)
             if (j + 1 < p) a.scores[(int64_t)r * (p - 1) + j] = wv[j];
