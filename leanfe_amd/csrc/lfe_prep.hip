@@ -223,11 +223,15 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   __syncthreads();
   int32_t bk[PER];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int64_t i = row_of(k);
-    bk[k] = i < r1 ? (a.code[a.P][i] >> a.s) : -1;
-    if (bk[k] >= 0) atomicAdd(&cur[wave * a.nb + bk[k]], 1);
+  for (int k = 0; k < PER; k += 2) {
+    const int64_t i = row_of(k);  // even: an 8-byte code pair (i + 1 < ld)
+    const int2 g = i < r1 ? *reinterpret_cast<const int2*>(a.code[a.P] + i) : int2{0, 0};
+    bk[k] = i < r1 ? (g.x >> a.s) : -1;
+    bk[k + 1] = i + 1 < r1 ? (g.y >> a.s) : -1;
   }
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (bk[k] >= 0) atomicAdd(&cur[wave * a.nb + bk[k]], 1);
   __syncthreads();
   // per bucket: exclusive scan over waves, total
   for (int b = tid; b < a.nb; b += kPartThreads) {
@@ -338,9 +342,12 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   for (int c = 0; c <= a.F; ++c) {  // F code arrays, then the input row index
     int32_t* dst = c < a.F ? a.codeo[c] : a.orig;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
+    for (int k = 0; k < PER; k += 2) {
       const int64_t i = row_of(k);
-      if (pos[k] >= 0) istage[pos[k]] = c < a.F ? a.code[c][i] : (int32_t)i;
+      int2 g = int2{(int32_t)i, (int32_t)i + 1};
+      if (c < a.F && pos[k] >= 0) g = *reinterpret_cast<const int2*>(a.code[c] + i);
+      if (pos[k] >= 0) istage[pos[k]] = g.x;
+      if (pos[k + 1] >= 0) istage[pos[k + 1]] = g.y;
     }
     __syncthreads();
 #pragma unroll
