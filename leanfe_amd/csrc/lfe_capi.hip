@@ -129,6 +129,37 @@ int ensure_f64(lfe_ctx*, double*& p, size_t& cap, size_t elems) { return ensure(
 int ensure_u16(lfe_ctx*, uint16_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 int ensure_u64(lfe_ctx*, uint64_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 
+struct ZeroArgs {
+  uint32_t* p[32];
+  int64_t end[32];  // running word offsets: range j covers [end[j - 1], end[j])
+  int n;
+};
+
+__global__ void k_zero_ranges(ZeroArgs a) {
+  const int64_t total = a.end[a.n - 1];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int j = 0;
+    while (e >= a.end[j]) ++j;
+    a.p[j][e - (j ? a.end[j - 1] : 0)] = 0u;
+  }
+}
+
+int zero_ranges(lfe_ctx* c, const std::vector<std::pair<void*, size_t>>& ranges) {
+  ZeroArgs a{};
+  int64_t off = 0;
+  for (const auto& r : ranges) {
+    if (!r.first || r.second == 0) continue;
+    if (a.n == 32) return fail(LFE_EINVAL, "zero_ranges: at most 32 ranges");
+    a.p[a.n] = static_cast<uint32_t*>(r.first);
+    off += (int64_t)(r.second / 4);
+    a.end[a.n++] = off;
+  }
+  if (a.n == 0) return LFE_OK;
+  hipLaunchKernelGGL(k_zero_ranges, dim3(grid_for(off, 256, 1024)), dim3(256), 0, c->stream, a);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
 int ensure_pcounts(lfe_ctx* c, size_t elems, size_t sums) {
   LFE_TRY(ensure(c->pcounts, c->pcounts_elems, elems));
   return ensure(c->psums, c->psums_elems, sums);
@@ -718,10 +749,12 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
   c->tq_final = false;
   {
     PhaseTimer t(c, &c->tm.demean);
-    for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
+    const bool fast = c->F > 0 && check_from > 0 && fast_path_ok(c, order);
+    if (!fast)  // the two-FE sweeps write every alpha entry before reading any
+      for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
     if (c->F > 0) {
       if (!c->sums_ready) LFE_TRY(sweep_group_sums(c));
-      if (check_from > 0 && fast_path_ok(c, order)) {
+      if (fast) {
         // two FEs, unweighted: segment layout + one fused codes-only kernel per sweep
         LFE_TRY(demean_fast(c, tol, max_iter, check_from, &iterations, &last));
       } else {

@@ -234,11 +234,12 @@ int sums4(lfe_ctx* c) {
       a.tab_off[f] = (int)off;
       off += (size_t)c->fe[f].G * p;
     }
-    LFE_HIP(hipMemsetAsync(c->fe[f].S, 0, sizeof(double) * (size_t)c->fe[f].G * p, c->stream));
+    if (!c->sums_zeroed) LFE_HIP(hipMemsetAsync(c->fe[f].S, 0, sizeof(double) * (size_t)c->fe[f].G * p, c->stream));
   }
   a.nq = 0;
   for (int f = 0; f < c->F; ++f)
     if (f != P) a.qf[a.nq++] = f;
+  c->sums_zeroed = false;
   const size_t lds = off * 8;
   const int NT = (p + 15) / 16;
   const void* fn = nullptr;

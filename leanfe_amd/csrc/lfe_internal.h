@@ -217,6 +217,7 @@ struct lfe_ctx {
   bool raw_ready = false;        // raw_tile holds this layout's kept rows
   bool tq_final = false;         // fe[Q].T = sum over q of the final alpha_P (demean_fast)
   bool hists_kept = false;       // seg_aux holds the kept rows' per-item histograms (no row dropped)
+  bool sums_zeroed = false;      // prepare_layout zeroed the S tables (sums4 skips its memsets)
   // scratch
   double* scratch = nullptr;     // device partials
   size_t scratch_elems = 0;
@@ -311,6 +312,8 @@ inline void dfree_any(T*& p) {
   p = nullptr;
 }
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
+// zero up to 32 device ranges (byte counts multiples of 4) in one launch instead of a memset each
+int zero_ranges(lfe_ctx* c, const std::vector<std::pair<void*, size_t>>& ranges);
 // device -> host copy of a small result through pinned staging, synchronizing the stream
 int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes);
 // device -> host copy into the pinned staging region without waiting; d2h_wait finishes it

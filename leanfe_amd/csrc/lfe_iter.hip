@@ -782,8 +782,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   // tail: 196 buckets -> 5 per bucket (tq 0.61 -> 0.49 ms per step at 50M rows, measured)
   tq.split = split_env > 0 ? split_env
                            : std::max(kTqSplitDefault / 2, (int)std::lround(4.0 * c->n_cu / std::max(c->L.nb, 1)));
-  // sweep 1's Q projection: alpha_P = 0 -> alpha_Q = S_Q / n_Q
-  LFE_HIP(hipMemsetAsync(fp.alpha, 0, sizeof(double) * (size_t)fp.G * p, c->stream));
+  // sweep 1's Q projection: alpha_P = 0 -> alpha_Q = S_Q / n_Q (alpha_P is first written by K1,
+  // which covers every primary group)
   LFE_TRY(fin_check(c, Q, nullptr, nullptr, fq.alpha, false));
   int iterations = 0;
   double last = -1.0;

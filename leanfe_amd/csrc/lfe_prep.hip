@@ -572,10 +572,23 @@ int prepare_layout(lfe_ctx* c) {
   c->hists_kept = false;
   L.w = c->w;  // fast_layout_ok reads it before the layout pointers are set below
   const bool item_counts = L.permuted && fast_layout_ok(c);
+  // every count / drop / group-sum table and the scratch counters zeroed in one launch
+  LFE_TRY(ensure_iscratch(c, 2 * kMaxFE + 8));
+  {
+    std::vector<std::pair<void*, size_t>> z;
+    for (int f = 0; f < c->F; ++f) {
+      auto& fe = c->fe[f];
+      z.push_back({fe.cnt_pre, sizeof(int32_t) * fe.G});
+      z.push_back({fe.drops, sizeof(int32_t) * fe.G});
+      z.push_back({fe.S, sizeof(double) * (size_t)fe.G * c->p});
+    }
+    z.push_back({c->iscratch, sizeof(int32_t) * (2 * kMaxFE + 8)});
+    LFE_TRY(zero_ranges(c, z));
+    c->sums_zeroed = true;
+  }
   // pre-filter counts of every FE (on input codes, except P when bucketed)
   for (int f = 0; f < c->F; ++f) {
     auto& fe = c->fe[f];
-    LFE_HIP(hipMemsetAsync(fe.cnt_pre, 0, sizeof(int32_t) * fe.G, c->stream));
     if (n == 0 || (f == L.P && L.permuted) || item_counts) continue;
     ProfScope _ps(c, K_COUNT);
     if (fe.G <= kLdsHistMax)
@@ -721,8 +734,6 @@ int prepare_layout(lfe_ctx* c) {
   for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt_pre, c->fe[f].G));
 
   // ---- single-pass singleton drop: mark, then kept counts = pre - drops ----
-  LFE_TRY(ensure_iscratch(c, 2 * kMaxFE + 8));
-  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t) * (2 * kMaxFE + 8), c->stream));
   int32_t* ndropped = c->iscratch + 2 * kMaxFE;
   if (c->F > 0) {
     MarkArgs a{};
@@ -730,7 +741,6 @@ int prepare_layout(lfe_ctx* c) {
     a.P = L.P;
     for (int f = 0; f < c->F; ++f) {
       auto& fe = c->fe[f];
-      LFE_HIP(hipMemsetAsync(fe.drops, 0, sizeof(int32_t) * fe.G, c->stream));
       a.code[f] = L.code[f];
       a.cnt_pre[f] = fe.cnt_pre;
       a.drops[f] = fe.drops;
