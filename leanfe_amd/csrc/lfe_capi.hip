@@ -447,18 +447,16 @@ static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_leve
   return LFE_OK;
 }
 
+enum { PH_PREP, PH_DEMEAN, PH_GRAM, PH_RESID, PH_CLUSTER };
+
 struct PhaseTimer {
   lfe_ctx* c;
-  double* slot;
-  PhaseTimer(lfe_ctx* c_, double* s) : c(c_), slot(s) { (void)hipEventRecord(c->ev0, c->stream); }
+  int ph;
+  PhaseTimer(lfe_ctx* c_, int ph_) : c(c_), ph(ph_) { (void)hipEventRecord(c->tm.ev[ph][0], c->stream); }
   ~PhaseTimer() {
-    (void)hipEventRecord(c->ev1, c->stream);
-    if (hipEventSynchronize(c->ev1) == hipSuccess) {
-      float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
-      *slot = ms;
-      c->tm.last = ms;
-    }
+    (void)hipEventRecord(c->tm.ev[ph][1], c->stream);
+    c->tm.pending |= 1u << ph;
+    c->tm.last_phase = ph;
   }
 };
 
@@ -505,7 +503,6 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
   (void)hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (c->n_cu <= 0) c->n_cu = 256;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreateWithFlags(&c->hpin_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->hpin), kPinSmall, hipHostMallocDefault) != hipSuccess ||
@@ -513,6 +510,13 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
     delete c;
     return fail(LFE_EHIP, "stream/event/buffer creation failed");
   }
+  for (auto& pair : c->tm.ev)
+    for (auto& e : pair)
+      if (hipEventCreate(&e) != hipSuccess) {
+        e = nullptr;
+        lfe_ctx_destroy(c);
+        return fail(LFE_EHIP, "event creation failed");
+      }
   *out = c;
   return LFE_OK;
 }
@@ -552,8 +556,9 @@ void lfe_ctx_destroy(lfe_ctx* c) {
     (void)hipEventDestroy(r.second.second);
   }
   for (auto e : c->prof.pool) (void)hipEventDestroy(e);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (auto& pair : c->tm.ev)
+    for (auto e : pair)
+      if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -717,7 +722,7 @@ int lfe_drop_singletons(lfe_ctx* c, int64_t* n_kept, int32_t* fe_dims_out, int32
   LFE_CTX(c);
   if (!c->loaded) return fail(LFE_ESTATE, "lfe_load first");
   {
-    PhaseTimer t(c, &c->tm.prep);
+    PhaseTimer t(c, PH_PREP);
     LFE_TRY(prepare_layout(c));
   }
   for (int f = 0; f < c->F; ++f) {
@@ -748,7 +753,7 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
   double last = -1.0;
   c->tq_final = false;
   {
-    PhaseTimer t(c, &c->tm.demean);
+    PhaseTimer t(c, PH_DEMEAN);
     const bool fast = c->F > 0 && check_from > 0 && fast_path_ok(c, order);
     if (!fast)  // the two-FE sweeps write every alpha entry before reading any
       for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
@@ -772,7 +777,7 @@ int lfe_gram(lfe_ctx* c, double* gram_out) {
   LFE_CTX(c);
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!gram_out) return fail(LFE_EINVAL, "gram_out is null");
-  PhaseTimer t(c, &c->tm.gram);
+  PhaseTimer t(c, PH_GRAM);
   return launch_gram(c, gram_out);
 }
 
@@ -781,7 +786,7 @@ int lfe_resid(lfe_ctx* c, const double* beta_full, double* stats_out, double* hc
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!beta_full || !stats_out) return fail(LFE_EINVAL, "null pointer");
   if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
-  PhaseTimer t(c, &c->tm.resid);
+  PhaseTimer t(c, PH_RESID);
   return launch_resid(c, beta_full, stats_out, hc1_meat, keep_scores, 0);
 }
 
@@ -790,7 +795,7 @@ int lfe_resid_iv(lfe_ctx* c, const double* coef, double* stats_out, double* meat
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!coef || !stats_out) return fail(LFE_EINVAL, "null pointer");
   if (keep_scores && !c->scores) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
-  PhaseTimer t(c, &c->tm.resid);
+  PhaseTimer t(c, PH_RESID);
   return launch_resid(c, coef, stats_out, meat_out, keep_scores, 1);
 }
 
@@ -800,7 +805,7 @@ int lfe_gram_resid(lfe_ctx* c, double* gram_out, double* beta_full_out, double* 
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!gram_out || !beta_full_out || !stats_out) return fail(LFE_EINVAL, "null pointer");
   if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
-  PhaseTimer t(c, &c->tm.resid);
+  PhaseTimer t(c, PH_RESID);
   return launch_gram_resid(c, gram_out, beta_full_out, stats_out, hc1_meat, keep_scores);
 }
 
@@ -808,7 +813,7 @@ int lfe_cluster_meat(lfe_ctx* c, double* meats_out, int64_t* G_out) {
   LFE_CTX(c);
   if (!c->scores_valid) return fail(LFE_ESTATE, "lfe_resid(keep_scores=1) first");
   if (!meats_out || !G_out) return fail(LFE_EINVAL, "null pointer");
-  PhaseTimer t(c, &c->tm.cluster);
+  PhaseTimer t(c, PH_CLUSTER);
   std::vector<int32_t> masks(c->cl.size());
   for (size_t j = 0; j < masks.size(); ++j) masks[j] = 1 << j;
   return launch_cluster_subsets(c, (int)masks.size(), masks.data(), meats_out, G_out);
@@ -818,7 +823,7 @@ int lfe_cluster_meat_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, do
   LFE_CTX(c);
   if (!c->scores_valid) return fail(LFE_ESTATE, "lfe_resid(keep_scores=1) first");
   if (n_subsets < 0 || (n_subsets > 0 && (!masks || !meats_out || !G_out))) return fail(LFE_EINVAL, "null pointer");
-  PhaseTimer t(c, &c->tm.cluster);
+  PhaseTimer t(c, PH_CLUSTER);
   return launch_cluster_subsets(c, n_subsets, masks, meats_out, G_out);
 }
 
@@ -889,11 +894,16 @@ int lfe_kernel_stats(lfe_ctx* c, int max, char* names, double* total_ms, int64_t
 
 int lfe_timings(lfe_ctx* c, double* out6) {
   if (!c || !out6) return fail(LFE_EINVAL, "null pointer");
-  out6[0] = c->tm.prep;
-  out6[1] = c->tm.demean;
-  out6[2] = c->tm.gram;
-  out6[3] = c->tm.resid;
-  out6[4] = c->tm.cluster;
+  for (int ph = 0; ph < 5; ++ph) {
+    if (!(c->tm.pending & (1u << ph))) continue;
+    float ms = 0.f;
+    if (hipEventSynchronize(c->tm.ev[ph][1]) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->tm.ev[ph][0], c->tm.ev[ph][1]) == hipSuccess)
+      c->tm.ms[ph] = ms;
+  }
+  c->tm.pending = 0;
+  if (c->tm.last_phase >= 0) c->tm.last = c->tm.ms[c->tm.last_phase];
+  for (int ph = 0; ph < 5; ++ph) out6[ph] = c->tm.ms[ph];
   out6[5] = c->tm.last;
   return LFE_OK;
 }

@@ -182,6 +182,143 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   }
 }
 
+// The two-FE Gram-from-tables case of k_sums4 (RAW, unweighted, p <= 15, primary slice and
+// secondary table both in LDS) with the per-row work cut to what the data needs: a row's
+// only test is its primary code's sign (item edges are masked once per 16-row group), LDS
+// byte offsets are one multiply-add per table, every pointer is hoisted out of the loop, and
+// the next group pair's loads are issued before the current pair is consumed.
+template <int TH, int NACC, int GU>
+__global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int nwv = TH / 64, step = nwv * GU;
+  const int kq = lane >> 4, c = lane & 15;
+  const int p = a.la.p, P = a.la.P, Q = a.qf[0], s = a.la.s;
+  const int p8 = p * 8;
+  const bool col = c < p;
+  // z = x - shift on the data lanes, 1 on lane 15 (intercept), 0 elsewhere: z = x * cm + zc
+  // (lanes c >= p load column 0 so that every load is unconditional)
+  const double cm = col ? 1.0 : 0.0;
+  const double zc = (c == 15 ? 1.0 : 0.0) - ((col && a.la.n_items > 0) ? a.X[(int64_t)c * a.ld] : 0.0);
+  const int32_t* __restrict__ hP = a.la.code[P];
+  const int32_t* __restrict__ hQ = a.la.code[Q];
+  const double* __restrict__ xc = a.X + (int64_t)(col ? c : 0) * a.ld;
+  char* lb = reinterpret_cast<char*>(lds);
+  const int qoff = a.tab_off[Q];
+  const uint32_t qbase = (uint32_t)(qoff * 8 + c * 8);
+  d4 racc[NACC];  // independent MFMA chains
+#pragma unroll
+  for (int r = 0; r < NACC; ++r) racc[r] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int j = tid; j < a.G[Q] * p; j += TH) lds[qoff + j] = 0.0;
+  for (int j = tid; j < a.B * p; j += TH) lds[j] = 0.0;
+  auto flush = [&](int b) {
+    const int lo = b << s;
+    for (int j = tid; j < a.B * p; j += TH) {
+      const double val = lds[j];
+      const int g = lo + j / p;
+      if (val != 0.0 && g < a.G_P) atomicAdd(&a.S[P][(int64_t)g * p + (j % p)], val);
+      lds[j] = 0.0;
+    }
+  };
+  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
+  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  int cur = -1;
+  for (int item = i0; item < i1; ++item) {
+    const int4 it = a.la.items[item];
+    if (it.x != cur) {
+      __syncthreads();
+      if (cur >= 0) flush(cur);
+      __syncthreads();
+      cur = it.x;
+    }
+    // slice byte offset of code h: h * p8 + sbase (unsigned wrap-around cancels the bucket base)
+    const uint32_t sbase = (uint32_t)(c * 8) - (uint32_t)((it.x << s) * p8);
+    const int g0 = it.y >> 4, g1 = (it.z + 15) >> 4;
+    int4 h0[GU], q0[GU];
+    d4 x0[GU];
+    // loads of groups gb, gb + 1, unconditional so that the pair in flight never forces a
+    // wait for the next one (clamped into the item: a dead group is reloaded, not used)
+    auto load = [&](int gb, int4 (&h)[GU], int4 (&q)[GU], d4 (&x)[GU]) {
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int gi = min(gb + u, g1 - 1);
+        const int rb = gi * 16 + kq * 4;
+        h[u] = *reinterpret_cast<const int4*>(hP + rb);
+        q[u] = *reinterpret_cast<const int4*>(hQ + rb);
+        x[u] = ld4(xc + rb);
+      }
+    };
+    auto consume = [&](int gb, const int4 (&h)[GU], const int4 (&q)[GU], const d4 (&x)[GU]) {
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int gi = gb + u;
+        if (gi >= g1) continue;  // wave-uniform
+        int hv[4] = {h[u].x, h[u].y, h[u].z, h[u].w};
+        const int gq[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+        if (gi * 16 < it.y || gi * 16 + 16 > it.z) {  // an item edge cuts this group
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = gi * 16 + kq * 4 + r;
+            if (row < it.y || row >= it.z) hv[r] = -1;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool v = hv[r] >= 0;
+          const double xv = x[u][r];
+          const double z = v ? __builtin_fma(xv, cm, zc) : 0.0;
+          racc[r % NACC] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[r % NACC], 0, 0, 0);
+          if (v && col) {
+            atomicAdd(reinterpret_cast<double*>(lb + ((uint32_t)hv[r] * (uint32_t)p8 + sbase)), xv);
+            atomicAdd(reinterpret_cast<double*>(lb + ((uint32_t)gq[r] * (uint32_t)p8 + qbase)), xv);
+          }
+        }
+      }
+      // every register of the set is read here (a no-op), so no path leaves one of its loads
+      // pending: the set's next loads then never wait for the other set's loads in flight
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+        asm volatile("" ::"v"(h[u].x), "v"(h[u].y), "v"(h[u].z), "v"(h[u].w), "v"(q[u].x), "v"(q[u].y),
+                     "v"(q[u].z), "v"(q[u].w), "v"(x[u][0]), "v"(x[u][1]), "v"(x[u][2]), "v"(x[u][3]));
+    };
+    // ping-pong register sets (no copies, which would wait for the loads in flight)
+    int4 h1[GU], q1[GU];
+    d4 x1[GU];
+    int gb = g0 + wave * GU;
+    load(gb, h0, q0, x0);
+    while (gb < g1) {
+      load(gb + step, h1, q1, x1);
+      consume(gb, h0, q0, x0);
+      gb += step;
+      if (gb >= g1) break;
+      load(gb + step, h0, q0, x0);
+      consume(gb, h1, q1, x1);
+      gb += step;
+    }
+  }
+  __syncthreads();
+  if (cur >= 0) flush(cur);
+  for (int j = tid; j < a.G[Q] * p; j += TH) {
+    const double val = lds[qoff + j];
+    if (val != 0.0) atomicAdd(&a.S[Q][j], val);
+  }
+  __shared__ double rred[256];
+  for (int wv = 0; wv < nwv; ++wv) {
+    __syncthreads();
+    if (wave == wv)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int e = (kq + 4 * rr) * 16 + c;
+        double v = racc[0][rr];
+#pragma unroll
+        for (int r = 1; r < NACC; ++r) v += racc[r][rr];
+        rred[e] = (wv == 0) ? v : rred[e] + v;
+      }
+  }
+  __syncthreads();
+  for (int e = tid; e < 256; e += TH) a.raw_part[(int64_t)blockIdx.x * 256 + e] = rred[e];
+}
+
 // raw_shift[16 + j] = this rank's shift (first layout row; 0 for an empty shard);
 // raw_shift[j] = rank 0's (summed over ranks afterwards)
 __global__ void k_raw_shift(const double* __restrict__ X, int64_t ld, int p, int has_rows, int rank,
@@ -254,11 +391,22 @@ int sums4(lfe_ctx* c) {
   }();
   const bool raw = raw_env != 0 && c->F == 2 && P >= 0 && a.nq == 1 && p <= 15 && !a.w && gu_env != 4;
   c->raw_ready = false;
+  static const int sums2_env = [] {
+    // tuning: 0 = k_sums4 for the two-FE Gram case; MFMA chains x groups per load: 1 = 4 x 2,
+    // 2 = 2 x 2, 3 = 4 x 1, 4 = 2 x 1
+    const char* e = getenv("LFE_SUMS2");
+    return e ? atoi(e) : 1;
+  }();
   int threads = kSumThreads;
   if (a.nq <= 1 && NT == 1) {
     // the 2-FE case: one workgroup per CU (LDS), so 16 waves of <= 128 VGPRs (GU 2)
     threads = gu_env == 4 ? kSumThreads : 1024;
+    const bool two = raw && sums2_env && a.slice && a.tab_off[a.qf[0]] >= 0;
     fn = gu_env == 4 ? SUMS4_FN(1, 4, 1, kSumThreads)
+         : two       ? (sums2_env == 2   ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 2, 2>)
+                        : sums2_env == 3 ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1>)
+                        : sums2_env == 4 ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 2, 1>)
+                                         : reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 2>))
          : raw       ? reinterpret_cast<const void*>(&k_sums4<1, 2, 1, 1024, true>)
                      : SUMS4_FN(1, 2, 1, 1024);
   } else if (a.nq <= 1) {

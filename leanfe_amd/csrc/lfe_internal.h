@@ -118,8 +118,14 @@ struct ClusterWS {
   bool lay_valid = false;
 };
 
+// per-phase device time of the latest call (prep, demean, gram, resid, cluster): begin/end
+// events recorded on the stream, read only when lfe_timings asks (no host wait per phase)
 struct Timings {
-  double prep = 0, demean = 0, gram = 0, resid = 0, cluster = 0, last = 0;
+  double ms[5] = {0, 0, 0, 0, 0};
+  double last = 0;
+  hipEvent_t ev[5][2] = {};
+  unsigned pending = 0;  // phases whose events are not read yet
+  int last_phase = -1;
 };
 
 // Row layout used by every pass after the singleton drop: rows grouped by
@@ -145,7 +151,6 @@ struct lfe_ctx {
   int device = 0;
   int n_cu = 256;        // compute units of the device
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // data (row shard, input order)
   int64_t n = 0;      // rows in this shard
   int64_t ld = 0;     // leading dimension of column storage (n rounded up)
