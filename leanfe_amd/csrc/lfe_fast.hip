@@ -194,7 +194,7 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   constexpr int nwv = TH / 64, step = nwv * GU;
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.la.p, P = a.la.P, Q = a.qf[0], s = a.la.s;
-  const int p8 = p * 8;
+  const uint32_t p8 = p * 8, c8 = c * 8;
   const bool col = c < p;
   // z = x - shift on the data lanes, 1 on lane 15 (intercept), 0 elsewhere: z = x * cm + zc
   // (lanes c >= p load column 0 so that every load is unconditional)
@@ -203,9 +203,8 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   const int32_t* __restrict__ hP = a.la.code[P];
   const int32_t* __restrict__ hQ = a.la.code[Q];
   const double* __restrict__ xc = a.X + (int64_t)(col ? c : 0) * a.ld;
-  char* lb = reinterpret_cast<char*>(lds);
   const int qoff = a.tab_off[Q];
-  const uint32_t qbase = (uint32_t)(qoff * 8 + c * 8);
+  double* const qtab = lds + qoff;
   d4 racc[NACC];  // independent MFMA chains
 #pragma unroll
   for (int r = 0; r < NACC; ++r) racc[r] = d4{0.0, 0.0, 0.0, 0.0};
@@ -231,8 +230,7 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
       __syncthreads();
       cur = it.x;
     }
-    // slice byte offset of code h: h * p8 + sbase (unsigned wrap-around cancels the bucket base)
-    const uint32_t sbase = (uint32_t)(c * 8) - (uint32_t)((it.x << s) * p8);
+    const int lo = it.x << s;
     const int g0 = it.y >> 4, g1 = (it.z + 15) >> 4;
     int4 h0[GU], q0[GU];
     d4 x0[GU];
@@ -269,8 +267,8 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
           const double z = v ? __builtin_fma(xv, cm, zc) : 0.0;
           racc[r % NACC] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[r % NACC], 0, 0, 0);
           if (v && col) {
-            atomicAdd(reinterpret_cast<double*>(lb + ((uint32_t)hv[r] * (uint32_t)p8 + sbase)), xv);
-            atomicAdd(reinterpret_cast<double*>(lb + ((uint32_t)gq[r] * (uint32_t)p8 + qbase)), xv);
+            atomicAdd(lds_row_ptr(lds, hv[r] - lo, p8, c8), xv);
+            atomicAdd(lds_row_ptr(qtab, gq[r], p8, c8), xv);
           }
         }
       }

@@ -362,6 +362,16 @@ __device__ __forceinline__ uint64_t canon_bits(double v) {
   return (uint64_t)__double_as_longlong(v);
 }
 
+// Element (row, col) of a row-major [rows][p] f64 table in LDS, addressed with one 24-bit
+// multiply-add on byte offsets (v_mad_u32_u24; a 32-bit v_mul_lo_u32 issues at quarter rate).
+// row < 2^24 and p8 = 8 p, col8 = 8 col.
+__device__ __forceinline__ double lds_row(const double* t, uint32_t row, uint32_t p8, uint32_t col8) {
+  return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(t) + (__umul24(row, p8) + col8));
+}
+__device__ __forceinline__ double* lds_row_ptr(double* t, uint32_t row, uint32_t p8, uint32_t col8) {
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(t) + (__umul24(row, p8) + col8));
+}
+
 __device__ __forceinline__ uint64_t fmix64(uint64_t h) {
   h ^= h >> 33;
   h *= 0xff51afd7ed558ccdull;

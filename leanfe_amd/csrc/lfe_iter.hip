@@ -404,9 +404,10 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
   for (int j = tid; j < G_Q * p; j += kTpThreads) aq[j] = a.alphaQ[j];
   for (int j = tid; j < p; j += kTpThreads) aq[G_Q * p + j] = 0.0;
   __syncthreads();
-  int cl[NT];
+  uint32_t cl8[NT];  // byte offset of the lane's column (dead lanes read column 0)
 #pragma unroll
-  for (int I = 0; I < NT; ++I) cl[I] = 16 * I + c < p ? 16 * I + c : 0;
+  for (int I = 0; I < NT; ++I) cl8[I] = 8 * (16 * I + c < p ? 16 * I + c : 0);
+  const uint32_t p8 = 8 * p;
   const int nwaves = gridDim.x * (kTpThreads / 64);
   for (int u = blockIdx.x * (kTpThreads / 64) + wave; u < a.n_units; u += nwaves) {
     int h = a.units[u];
@@ -442,9 +443,8 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
       if (gs >= r0 && gs + 16 <= r1) {  // inside segment h (wave-uniform): no masks
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const uint32_t ro = (uint32_t)qv[s] * (uint32_t)p;
 #pragma unroll
-          for (int I = 0; I < NT; ++I) acc[I] += aq[ro + (uint32_t)cl[I]];
+          for (int I = 0; I < NT; ++I) acc[I] += lds_row(aq, qv[s], p8, cl8[I]);
         }
         if (gs + 16 < r1) return;
         finalize();
@@ -460,9 +460,9 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int row = rb + s;
-          const uint32_t ro = (uint32_t)(row >= r0 && row < r1 ? qv[s] : G_Q) * (uint32_t)p;
+          const uint32_t ro = row >= r0 && row < r1 ? qv[s] : G_Q;
 #pragma unroll
-          for (int I = 0; I < NT; ++I) acc[I] += aq[ro + (uint32_t)cl[I]];
+          for (int I = 0; I < NT; ++I) acc[I] += lds_row(aq, ro, p8, cl8[I]);
         }
         if (r1 > gs + 16) return;  // segment h continues in the next group
         finalize();
@@ -487,17 +487,15 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
         if (gs >= r0 && gs + 64 < r1) {  // 4 groups inside segment h, which continues after them
           double t[4][NT];
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int I = 0; I < NT; ++I) t[s][I] = 0.0;
-#pragma unroll
           for (int dd = 0; dd < 4; ++dd) {
             const int qv[4] = {q[dd].x, q[dd].y, q[dd].z, q[dd].w};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-              const uint32_t ro = (uint32_t)qv[s] * (uint32_t)p;
 #pragma unroll
-              for (int I = 0; I < NT; ++I) t[s][I] += aq[ro + (uint32_t)cl[I]];
+              for (int I = 0; I < NT; ++I) {
+                const double v = lds_row(aq, qv[s], p8, cl8[I]);
+                t[s][I] = dd == 0 ? v : t[s][I] + v;
+              }
             }
           }
 #pragma unroll
@@ -543,9 +541,10 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
   constexpr int NW = kTqThreads / 64;
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.p, G_Q = a.G_Q, B = 1 << a.s;
-  int cl[NT];
+  uint32_t cl8[NT];  // byte offset of the lane's column (dead lanes read column 0)
 #pragma unroll
-  for (int I = 0; I < NT; ++I) cl[I] = 16 * I + c < p ? 16 * I + c : 0;
+  for (int I = 0; I < NT; ++I) cl8[I] = 8 * (16 * I + c < p ? 16 * I + c : 0);
+  const uint32_t p8 = 8 * p;
   const int kTqSplit = a.split;
   for (int bs = blockIdx.x; bs < a.nb * kTqSplit; bs += gridDim.x) {
     const int b = bs / kTqSplit, part = bs % kTqSplit;
@@ -588,9 +587,8 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
       if (gs >= r0 && gs + 16 <= r1) {  // inside run q (wave-uniform): no masks
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const uint32_t ro = (uint32_t)h4[s] * (uint32_t)p;
 #pragma unroll
-          for (int I = 0; I < NT; ++I) acc[I] += sl[ro + (uint32_t)cl[I]];
+          for (int I = 0; I < NT; ++I) acc[I] += lds_row(sl, h4[s], p8, cl8[I]);
         }
         if (gs + 16 < r1) return;
         finalize();
@@ -606,9 +604,9 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int row = rb + s;
-          const uint32_t ro = (uint32_t)(row >= r0 && row < r1 ? (int)h4[s] : B) * (uint32_t)p;
+          const uint32_t ro = row >= r0 && row < r1 ? (uint32_t)h4[s] : (uint32_t)B;
 #pragma unroll
-          for (int I = 0; I < NT; ++I) acc[I] += sl[ro + (uint32_t)cl[I]];
+          for (int I = 0; I < NT; ++I) acc[I] += lds_row(sl, ro, p8, cl8[I]);
         }
         if (r1 > gs + 16) return;  // run continues in the next group
         finalize();
@@ -639,16 +637,14 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
         if (gs >= r0 && gs + 64 < r1) {  // 4 groups inside run q, which continues after them
           double t[4][NT];
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int I = 0; I < NT; ++I) t[s][I] = 0.0;
-#pragma unroll
           for (int dd = 0; dd < 4; ++dd)
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-              const uint32_t ro = (uint32_t)hh[dd][s] * (uint32_t)p;
 #pragma unroll
-              for (int I = 0; I < NT; ++I) t[s][I] += sl[ro + (uint32_t)cl[I]];
+              for (int I = 0; I < NT; ++I) {
+                const double v = lds_row(sl, hh[dd][s], p8, cl8[I]);
+                t[s][I] = dd == 0 ? v : t[s][I] + v;
+              }
             }
 #pragma unroll
           for (int I = 0; I < NT; ++I) acc[I] += (t[0][I] + t[1][I]) + (t[2][I] + t[3][I]);
