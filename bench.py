@@ -90,7 +90,7 @@ def algorithmic_bytes(n: int, p: int, F: int, T: int, hc1: bool) -> dict:
     """
     return {
         "part_hist": 4 * n,                              # primary codes
-        "part_scatter": n * (2 * 8 * p + 2 * 4 * F + 4),  # read + write X and codes, write orig
+        "part_scatter": n * (2 * 8 * p + 2 * 4 * F),      # read + write X and codes
         "count": 4 * n,                                  # one code column per launch
         "mark": 4 * n * F,                               # every code column (+ sparse writes)
         "group_sums": n * (8 * p + 4 * F),               # X + codes

@@ -415,6 +415,7 @@ int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, doub
   LFE_TRY(ensure_i32(c, W.seg_off, W.seg_off_cap, ld + 1));
   LFE_TRY(ensure_i32(c, W.ufirst, W.ufirst_cap, (size_t)seg_units_needed(c->ld)));
   if (!W.lay_valid) {
+    LFE_TRY(ensure_layout_orig(c));
     W.lay.resize(m, nullptr);
     W.lay_cap.resize(m, 0);
     for (int j = 0; j < m; ++j) {

@@ -185,6 +185,7 @@ __global__ void k_gather_lay(const double* __restrict__ src, const int32_t* __re
 int records_layout(lfe_ctx* c) {
   const int64_t n = c->n;
   LFE_TRY(ensure_f64(c, c->rec_lay, c->rec_lay_cap, 2 * (size_t)c->ld));
+  LFE_TRY(ensure_layout_orig(c));
   if (n > 0) {
     hipLaunchKernelGGL(k_gather_lay, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, c->rec_sy,
                        c->L.orig, n, c->rec_lay);

@@ -1281,6 +1281,7 @@ int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, doub
 }
 
 int launch_copy_demeaned(lfe_ctx* c, double* dev_out) {
+  LFE_TRY(ensure_layout_orig(c));
   if (c->n)
     hipLaunchKernelGGL(k_copy_demeaned, dim3(grid_for(c->n)), dim3(kBlock), 0, c->stream, layout_args(c), c->L.X,
                        c->ld, c->n, c->L.orig, dev_out);

@@ -131,6 +131,11 @@ struct Timings {
 // Row layout used by every pass after the singleton drop: rows grouped by
 // buckets of the primary (highest-cardinality) FE, bucket b holding codes
 // [b << s, (b+1) << s).  Work item = contiguous row range inside one bucket.
+struct PartGeom {  // partition scatter launch geometry (lfe_prep.hip)
+  int nth = 0, per = 0, nw = 0;
+  size_t lds = 0;
+};
+
 struct Layout {
   int P = -1;          // primary FE (-1: no FE)
   int s = 0;           // bucket shift
@@ -140,6 +145,8 @@ struct Layout {
   double* w = nullptr;          // [ld] or nullptr
   int32_t* code[kMaxFE] = {};   // per FE, bucket order; code[P][i] = -1 marks a dropped row
   int32_t* orig = nullptr;      // [ld] input row index of each layout row (nullptr = identity)
+  bool orig_pending = false;    // orig not written yet (ensure_layout_orig)
+  PartGeom part;
   int n_items = 0;
   std::vector<int32_t> hitems;  // host copy of the work items
   std::vector<int32_t> bstart;  // host [nb + 1]
@@ -259,6 +266,7 @@ namespace lfe {
 
 // --- prep / partition (lfe_prep.hip) ---
 int prepare_layout(lfe_ctx* c);   // partition + counts + singleton marks
+int ensure_layout_orig(lfe_ctx* c);  // L.orig written (deferred by prepare_layout)
 
 // --- group sums (lfe_fast.hip) ---
 int sums4(lfe_ctx* c);

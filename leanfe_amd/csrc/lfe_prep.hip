@@ -188,6 +188,8 @@ struct ScatterArgs {
   int xcd_map;             // 1: XCD-contiguous chunk order
   int pipe;                // 1: load column c + 1 during column c's write-out
   int nt;                  // bit 0: non-temporal stores, bit 1: non-temporal column loads
+  int cols;                // move the X / w columns and the codes
+  int want_orig;           // write the input row index of each layout row
 };
 
 // block i -> chunk: XCD x = i % 8 walks its contiguous eighth of the chunks
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   }
   __syncthreads();
   // ---- move columns through the stage: gather in row order, store in bucket order ----
-  const int ncol = a.p + (a.w ? 1 : 0);
+  const int ncol = a.cols ? a.p + (a.w ? 1 : 0) : 0;
   double v[PER];
   typedef double d2v __attribute__((ext_vector_type(2)));
   auto load_col = [&](int c) {
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
       }
     }
   };
-  load_col(0);
+  if (ncol > 0) load_col(0);
   for (int c = 0; c < ncol; ++c) {
     double* dst = c < a.p ? a.Xo + (int64_t)c * a.ld : a.wo;
 #pragma unroll
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
     if (!a.pipe && c + 1 < ncol) load_col(c + 1);
   }
   int32_t* istage = reinterpret_cast<int32_t*>(stage);
-  for (int c = 0; c <= a.F; ++c) {  // F code arrays, then the input row index
+  for (int c = a.cols ? 0 : a.F; c < a.F + a.want_orig; ++c) {  // F code arrays, then the input row index
     int32_t* dst = c < a.F ? a.codeo[c] : a.orig;
 #pragma unroll
     for (int k = 0; k < PER; k += 2) {
@@ -551,6 +553,74 @@ static int build_items(lfe_ctx* c) {
   return LFE_OK;
 }
 
+// Partition scatter of the current layout geometry (L.part, the scanned destinations in
+// c->pcounts): cols = X / w columns and codes, orig = the input row index of each layout row.
+// The ranking is deterministic, so an orig-only launch later reproduces the same layout.
+static int launch_part_scatter(lfe_ctx* c, int cols, int orig) {
+  auto& L = c->L;
+  const PartGeom& g = L.part;
+  ScatterArgs a{};
+  a.p = c->p;
+  a.F = c->F;
+  a.P = L.P;
+  a.s = L.s;
+  a.nb = L.nb;
+  a.nchunks = g.nw;
+  a.n = c->n;
+  a.ld = c->ld;
+  a.X = c->X;
+  a.w = c->w;
+  a.Xo = c->Xp;
+  a.wo = c->wp;
+  for (int f = 0; f < c->F; ++f) {
+    a.code[f] = c->fe[f].code;
+    a.codeo[f] = c->codes_p + (size_t)f * c->ld;
+  }
+  a.orig = c->origp;
+  a.scanned = c->pcounts;
+  a.cols = cols;
+  a.want_orig = orig;
+  static const int xmap_env = [] {
+    const char* e = getenv("LFE_PART_XCD");  // tuning: 0 = plain chunk order
+    return e ? atoi(e) : 1;
+  }();
+  a.xcd_map = xmap_env;
+  static const int pipe_env = [] {
+    const char* e = getenv("LFE_PART_PIPE");  // tuning (measured: 1 is 0.5 % faster)
+    return e ? atoi(e) : 1;
+  }();
+  a.pipe = pipe_env;
+  static const int nt_env = [] {
+    // tuning: non-temporal stores (1), loads (2); measured at 50M rows: stores 2.23 -> 2.74 ms,
+    // loads no change, so both stay off
+    const char* e = getenv("LFE_PART_NT");
+    return e ? atoi(e) : 0;
+  }();
+  a.nt = nt_env;
+  const int pgrid = a.xcd_map ? ((g.nw + 7) / 8) * 8 : g.nw;
+  // dynamic LDS above 64 KB must be opted in (static LDS + dynamic <= 160 KB)
+  using Fn = void (*)(ScatterArgs);
+  Fn fn = g.nth == 1024 ? (g.per == 16 ? &k_part_scatter<16, 1024>
+                           : g.per == 8 ? &k_part_scatter<8, 1024> : &k_part_scatter<4, 1024>)
+                        : (g.per == 16 ? &k_part_scatter<16, 512> : &k_part_scatter<8, 512>);
+  LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)g.lds));
+  {
+    ProfScope _ps(c, cols ? K_PART_SCATTER : K_MISC);
+    hipLaunchKernelGGL(fn, dim3(pgrid), dim3(g.nth), g.lds, c->stream, a);
+  }
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+int ensure_layout_orig(lfe_ctx* c) {
+  if (!c->L.orig_pending) return LFE_OK;
+  LFE_TRY(launch_part_scatter(c, /*cols=*/0, /*orig=*/1));
+  c->L.orig = c->origp;
+  c->L.orig_pending = false;
+  return LFE_OK;
+}
+
 int prepare_layout(lfe_ctx* c) {
   auto& L = c->L;
   const int64_t n = c->n;
@@ -644,55 +714,12 @@ int prepare_layout(lfe_ctx* c) {
     hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(nb)), dim3(kBlock), 0, c->stream, c->pcounts, nb, nw, dbstart);
     LFE_HIP(hipGetLastError());
     LFE_TRY(d2h_async(c, dbstart, sizeof(int32_t) * nb));
-    ScatterArgs a{};
-    a.p = c->p;
-    a.F = c->F;
-    a.P = L.P;
-    a.s = L.s;
-    a.nb = nb;
-    a.nchunks = nw;
-    a.n = n;
-    a.ld = c->ld;
-    a.X = c->X;
-    a.w = c->w;
-    a.Xo = c->Xp;
-    a.wo = c->wp;
-    for (int f = 0; f < c->F; ++f) {
-      a.code[f] = c->fe[f].code;
-      a.codeo[f] = c->codes_p + (size_t)f * c->ld;
-    }
-    a.orig = c->origp;
-    a.scanned = c->pcounts;
-    static const int xmap_env = [] {
-      const char* e = getenv("LFE_PART_XCD");  // tuning: 0 = plain chunk order
-      return e ? atoi(e) : 1;
-    }();
-    a.xcd_map = xmap_env;
-    static const int pipe_env = [] {
-      const char* e = getenv("LFE_PART_PIPE");  // tuning (measured: 1 is 0.5 % faster)
-      return e ? atoi(e) : 1;
-    }();
-    a.pipe = pipe_env;
-    static const int nt_env = [] {
-      // tuning: non-temporal stores (1), loads (2); measured at 50M rows: stores 2.23 -> 2.74 ms,
-      // loads no change, so both stay off
-      const char* e = getenv("LFE_PART_NT");
-      return e ? atoi(e) : 0;
-    }();
-    a.nt = nt_env;
-    const int pgrid = a.xcd_map ? ((nw + 7) / 8) * 8 : nw;
-    {
-      const size_t lds = std::min<size_t>(std::max(part_lds(nth), lds_min), 160 * 1024);
-      // dynamic LDS above 64 KB must be opted in (static LDS + dynamic <= 160 KB)
-      using Fn = void (*)(ScatterArgs);
-      Fn fn = nth == 1024 ? (per == 16 ? &k_part_scatter<16, 1024>
-                             : per == 8 ? &k_part_scatter<8, 1024> : &k_part_scatter<4, 1024>)
-                          : (per == 16 ? &k_part_scatter<16, 512> : &k_part_scatter<8, 512>);
-      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
-      ProfScope _ps(c, K_PART_SCATTER);
-      hipLaunchKernelGGL(fn, dim3(pgrid), dim3(nth), lds, c->stream, a);
-    }
+    const size_t lds = std::min<size_t>(std::max(part_lds(nth), lds_min), 160 * 1024);
+    L.part = PartGeom{nth, per, nw, lds};
+    // the input row index of each layout row is written only when a caller needs it
+    // (ensure_layout_orig: cluster, records and demeaned-column export paths)
+    LFE_TRY(launch_part_scatter(c, /*cols=*/1, /*orig=*/0));
+    L.orig_pending = true;
     LFE_HIP(hipGetLastError());
     L.bstart.assign(nb + 1, 0);
     LFE_TRY(d2h_wait(c, L.bstart.data(), sizeof(int32_t) * nb));
@@ -700,8 +727,9 @@ int prepare_layout(lfe_ctx* c) {
     L.X = c->Xp;
     L.w = c->w ? c->wp : nullptr;
     for (int f = 0; f < c->F; ++f) L.code[f] = c->codes_p + (size_t)f * c->ld;
-    L.orig = c->origp;
+    L.orig = nullptr;
   } else {
+    L.orig_pending = false;
     L.bstart = {0, (int32_t)n};
     L.X = c->X;
     L.w = c->w;
