@@ -22,7 +22,7 @@ from collections import defaultdict
 # engine kernel id -> demangled kernel name prefix
 KERNELS = {
     "part_hist": ("k_part_hist",), "part_scatter": ("k_part_scatter",), "mark": ("k_mark",),
-    "group_sums": ("k_sums4",), "tp": ("k_tp",), "tq": ("k_tq",),
+    "group_sums": ("k_sums4", "k_sums2_raw"), "tp": ("k_tp",), "tq": ("k_tq",),
     "gram_design": ("k_design_rows", "k_gram<0,"), "gram_resid": ("k_resid_rows", "k_gram<1,"),
     "gram_tables": ("k_tables_gram",), "layout_sort": ("k_ls_scatter",),
 }
