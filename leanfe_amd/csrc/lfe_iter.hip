@@ -236,6 +236,163 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
   }
 }
 
+// Both layouts in one pass over the codes: the segment layout (key h - lo, value q -> seg_q)
+// and the run layout (key q, value h - lo -> run_h) of the same sub-chunk are ranked together
+// (shared cursors, as k_ls_scatter<.., 1, ..>), so the two code columns are read once.
+struct Ls2Args {
+  const int4* items;
+  const int32_t* codeP;
+  const int32_t* codeQ;
+  int s, K1, K2;
+  const int32_t* off1;   // [nb K1 + 1]
+  const int32_t* off2;   // [nb K2 + 1]
+  const int32_t* base1;  // [n_items][K1] item bases
+  const int32_t* base2;  // [n_items][K2]
+  const int32_t* xitems;
+  int32_t* seg_q;
+  uint16_t* run_h;
+};
+
+static size_t ls2_lds(int K1, int K2, int per) {
+  return sizeof(int32_t) * (4 * ((size_t)K1 + K2) + 2 * (size_t)kLsThreads * per);
+}
+
+template <int kLsPer>
+__global__ __launch_bounds__(kLsThreads) void k_ls_scatter2(Ls2Args a) {
+  constexpr int kLsRows = kLsThreads * kLsPer;
+  extern __shared__ int32_t sm[];
+  const int K1 = a.K1, K2 = a.K2;
+  int32_t* cur1 = sm;           // [K1]
+  int32_t* cur2 = cur1 + K1;    // [K2]
+  int32_t* run1 = cur2 + K2;    // [K1] next free slot of each key
+  int32_t* run2 = run1 + K1;    // [K2]
+  int32_t* tot1 = run2 + K2;    // [K1] (then the keys' local offsets)
+  int32_t* tot2 = tot1 + K1;    // [K2]
+  int32_t* del1 = tot2 + K2;    // [K1]
+  int32_t* del2 = del1 + K1;    // [K2]
+  int32_t* st1 = del2 + K2;     // [kLsRows]
+  int32_t* st2 = st1 + kLsRows; // [kLsRows]
+  __shared__ int32_t wsum[kLsWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int item = a.xitems[blockIdx.x];  // XCD-grouped order (build_items)
+  if (item < 0) return;
+  const int4 it = a.items[item];
+  const int lo = it.x << a.s;
+  for (int j = tid; j < K1; j += kLsThreads)
+    run1[j] = a.off1[(int64_t)it.x * K1 + j] + a.base1[(int64_t)item * K1 + j];
+  for (int j = tid; j < K2; j += kLsThreads)
+    run2[j] = a.off2[(int64_t)it.x * K2 + j] + a.base2[(int64_t)item * K2 + j];
+  // exclusive scan of tot[0, K) in place (one thread per `per` keys, then the waves)
+  auto scan_keys = [&](int32_t* tot, int K) {
+    const int per = (K + kLsThreads - 1) / kLsThreads;
+    const int b0 = tid * per;
+    int32_t sum = 0;
+    for (int k = 0; k < per; ++k)
+      if (b0 + k < K) sum += tot[b0 + k];
+    int32_t x = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int32_t wofs = 0;
+    for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[w2];
+    int32_t acc = x - sum + wofs;
+    __syncthreads();
+    for (int k = 0; k < per; ++k)
+      if (b0 + k < K) {
+        const int32_t t = tot[b0 + k];
+        tot[b0 + k] = acc;
+        acc += t;
+      }
+  };
+  static_assert(kLsPer % 4 == 0, "rows per thread in fours");
+  for (int32_t r0 = it.y & ~3; r0 < it.z; r0 += kLsRows) {
+    const int32_t r1 = min(it.z, r0 + kLsRows);
+    const int32_t wbase = r0 + wave * kLsPer * 64;
+    __syncthreads();
+    for (int j = tid; j < K1; j += kLsThreads) cur1[j] = 0;
+    for (int j = tid; j < K2; j += kLsThreads) cur2[j] = 0;
+    __syncthreads();
+    int32_t hk[kLsPer], qk[kLsPer];  // h - lo (key of layout 1) and q (key of layout 2); -1: not kept
+#pragma unroll
+    for (int k = 0; k < kLsPer; k += 4) {
+      const int32_t i0 = wbase + (k >> 2) * 256 + 4 * lane;
+      int4 g4 = int4{-1, -1, -1, -1}, q4 = int4{0, 0, 0, 0};
+      if (i0 < r1) {
+        g4 = *reinterpret_cast<const int4*>(a.codeP + i0);
+        q4 = *reinterpret_cast<const int4*>(a.codeQ + i0);
+      }
+      const int32_t gv[4] = {g4.x, g4.y, g4.z, g4.w}, qv[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int32_t i = i0 + t;
+        hk[k + t] = -1;
+        qk[k + t] = 0;
+        if (i >= it.y && i < r1 && gv[t] >= 0) {
+          hk[k + t] = gv[t] - lo;
+          qk[k + t] = qv[t];
+          atomicAdd(&cur1[hk[k + t]], 1);
+          atomicAdd(&cur2[qk[k + t]], 1);
+        }
+      }
+    }
+    __syncthreads();
+    for (int j = tid; j < K1; j += kLsThreads) tot1[j] = cur1[j];
+    for (int j = tid; j < K2; j += kLsThreads) tot2[j] = cur2[j];
+    __syncthreads();
+    scan_keys(tot1, K1);
+    __syncthreads();
+    scan_keys(tot2, K2);
+    __syncthreads();
+    for (int j = tid; j < K1; j += kLsThreads) {
+      del1[j] = run1[j] - tot1[j];
+      cur1[j] = tot1[j];
+    }
+    for (int j = tid; j < K2; j += kLsThreads) {
+      del2[j] = run2[j] - tot2[j];
+      cur2[j] = tot2[j];
+    }
+    __syncthreads();
+    int32_t p1[kLsPer], p2[kLsPer];
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k)
+      if (hk[k] >= 0) {
+        p1[k] = atomicAdd(&cur1[hk[k]], 1);
+        p2[k] = atomicAdd(&cur2[qk[k]], 1);
+        st1[p1[k]] = hk[k];
+        st2[p2[k]] = qk[k];
+      }
+    __syncthreads();
+    // kept rows of this sub-chunk = the last key's end
+    const int32_t nk = cur1[K1 - 1];
+    int32_t d1[kLsPer], d2[kLsPer];
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k) {
+      const int j = tid + k * kLsThreads;
+      d1[k] = j < nk ? del1[st1[j]] + j : -1;
+      d2[k] = j < nk ? del2[st2[j]] + j : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k)
+      if (hk[k] >= 0) {
+        st1[p1[k]] = qk[k];
+        st2[p2[k]] = hk[k];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kLsPer; ++k) {
+      if (d1[k] >= 0) a.seg_q[d1[k]] = st1[tid + k * kLsThreads];
+      if (d2[k] >= 0) a.run_h[d2[k]] = (uint16_t)st2[tid + k * kLsThreads];
+    }
+    __syncthreads();
+    for (int j = tid; j < K1; j += kLsThreads) run1[j] = del1[j] + cur1[j];
+    for (int j = tid; j < K2; j += kLsThreads) run2[j] = del2[j] + cur2[j];
+  }
+}
+
 // first segment (primary group) of each work unit of ~U kept rows
 __global__ void k_unit_bounds(const int32_t* __restrict__ seg_off, int32_t H, int64_t U, int n_units,
                               int32_t* __restrict__ units) {
@@ -276,6 +433,7 @@ static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off,
   }
   LFE_HIP(hipGetLastError());
   LFE_TRY(exclusive_scan(c, off, (int64_t)m + 1));
+  if (!out) return LFE_OK;  // offsets and item bases only (the fused two-layout sort)
   constexpr int NCUR = 1;
   const int per = ls_per();
   const size_t lds = ls_scatter_lds(K, NCUR, per);
@@ -321,9 +479,43 @@ static int build_layouts(lfe_ctx* c, int Q) {
   if (!c->hists_kept) LFE_TRY(layout_hists(c, Q));
   c->hists_kept = false;
   LFE_TRY(ensure_i32(c, c->seg_q, c->seg_q_cap, (size_t)c->ld));
-  LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, c->seg_q)));
   LFE_TRY(ensure_u16(c, c->run_h, c->run_h_cap, (size_t)c->ld));
-  LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, c->run_h)));
+  static const int fused_env = [] {
+    const char* e = getenv("LFE_LS_FUSED");  // tuning: 0 = one local sort per layout
+    return e ? atoi(e) : 1;
+  }();
+  const int per = ls_per();
+  const size_t lds2 = ls2_lds(B, G_Q, per);
+  if (fused_env && lds2 <= 150 * 1024) {
+    LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, nullptr)));
+    LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, nullptr)));
+    Ls2Args a{};
+    a.items = reinterpret_cast<const int4*>(c->items_d);
+    a.codeP = L.code[L.P];
+    a.codeQ = L.code[Q];
+    a.s = L.s;
+    a.K1 = B;
+    a.K2 = G_Q;
+    a.off1 = c->seg_off;
+    a.off2 = c->run_off;
+    a.base1 = c->seg_aux;
+    a.base2 = c->seg_aux + n1;
+    a.xitems = c->xitems_d;
+    a.seg_q = c->seg_q;
+    a.run_h = c->run_h;
+    const void* fn = per == 16 ? reinterpret_cast<const void*>(&k_ls_scatter2<16>)
+                               : reinterpret_cast<const void*>(&k_ls_scatter2<8>);
+    if (lds2 > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+    {
+      ProfScope _ps(c, K_MISC);
+      void* args[] = {&a};
+      LFE_HIP(hipLaunchKernel(fn, dim3(c->n_xgrid), dim3(kLsThreads), args, lds2, c->stream));
+    }
+    LFE_HIP(hipGetLastError());
+  } else {
+    LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, c->seg_q)));
+    LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, c->run_h)));
+  }
   // work units of ~2048 kept rows (whole segments) for K1
   const int64_t U = 2048;
   const int32_t H = L.nb * B;
