@@ -325,6 +325,8 @@ inline void dfree_any(T*& p) {
   p = nullptr;
 }
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
+// two independent exclusive scans in one set of launches (a2 may be null)
+int exclusive_scan2(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2);
 // zero up to 32 device ranges (byte counts multiples of 4) in one launch instead of a memset each
 int zero_ranges(lfe_ctx* c, const std::vector<std::pair<void*, size_t>>& ranges);
 // device -> host copy of a small result through pinned staging, synchronizing the stream

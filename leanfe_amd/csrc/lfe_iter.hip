@@ -82,7 +82,11 @@ __global__ __launch_bounds__(256) void k_ls_hist2(const int4* __restrict__ items
 __global__ void k_ls_base(const int32_t* __restrict__ bitems, int nb, int K, int32_t* __restrict__ itemcnt,
                           int32_t* __restrict__ off) {
   const int64_t total = (int64_t)nb * K;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e <= total; e += (int64_t)gridDim.x * blockDim.x) {
+    if (e == total) {  // the scan's trailing element (the total after the exclusive scan)
+      off[e] = 0;
+      continue;
+    }
     const int b = (int)(e / K), j = (int)(e % K);
     int32_t run = 0;
     for (int i = bitems[b]; i < bitems[b + 1]; ++i) {
@@ -425,15 +429,14 @@ static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off,
   const size_t m = (size_t)L.nb * K;
   LFE_TRY(ensure_i32(c, off, off_cap, m + 1));
   const int4* items = reinterpret_cast<const int4*>(c->items_d);
-  LFE_HIP(hipMemsetAsync(off, 0, sizeof(int32_t) * (m + 1), c->stream));
   {
     ProfScope _ps(c, K_MISC);
-    hipLaunchKernelGGL(k_ls_base, dim3(grid_for((int64_t)m)), dim3(kBlock), 0, c->stream, c->bitems_d, L.nb, K,
+    hipLaunchKernelGGL(k_ls_base, dim3(grid_for((int64_t)m + 1)), dim3(kBlock), 0, c->stream, c->bitems_d, L.nb, K,
                        itemcnt, off);
   }
   LFE_HIP(hipGetLastError());
+  if (!out) return LFE_OK;  // per-key totals and item bases only (the fused sort scans both)
   LFE_TRY(exclusive_scan(c, off, (int64_t)m + 1));
-  if (!out) return LFE_OK;  // offsets and item bases only (the fused two-layout sort)
   constexpr int NCUR = 1;
   const int per = ls_per();
   const size_t lds = ls_scatter_lds(K, NCUR, per);
@@ -489,6 +492,7 @@ static int build_layouts(lfe_ctx* c, int Q) {
   if (fused_env && lds2 <= 150 * 1024) {
     LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, nullptr)));
     LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, nullptr)));
+    LFE_TRY(exclusive_scan2(c, c->seg_off, (int64_t)L.nb * B + 1, c->run_off, (int64_t)L.nb * G_Q + 1));
     Ls2Args a{};
     a.items = reinterpret_cast<const int4*>(c->items_d);
     a.codeP = L.code[L.P];
@@ -583,6 +587,9 @@ struct TpArgs {
   const int32_t* cntP;   // [G_P] kept counts (all ranks)
   double* out;           // fused: alpha_P [G_P][p]; else T_P [G_P][p]
   int fused;
+  double* zeroT;         // T_Q [zero_n], zeroed for the K2 pass that follows (saves a fill launch)
+  int64_t zero_n;
+  double* zero_check;    // the stop test's max, zeroed for the check after K2 (or null)
 };
 
 // K1: T_P[h] = sum_{i in h} alpha_Q[q_i]; fused: alpha_P[h] = (S_P[h] - T_P[h]) / n_h
@@ -595,6 +602,9 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
   const int p = a.p, G_Q = a.G_Q;
   for (int j = tid; j < G_Q * p; j += kTpThreads) aq[j] = a.alphaQ[j];
   for (int j = tid; j < p; j += kTpThreads) aq[G_Q * p + j] = 0.0;
+  for (int64_t j = (int64_t)blockIdx.x * kTpThreads + tid; j < a.zero_n; j += (int64_t)gridDim.x * kTpThreads)
+    a.zeroT[j] = 0.0;
+  if (a.zero_check && blockIdx.x == 0 && tid == 0) *a.zero_check = 0.0;
   __syncthreads();
   uint32_t cl8[NT];  // byte offset of the lane's column (dead lanes read column 0)
 #pragma unroll
@@ -977,6 +987,9 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   double last = -1.0;
   for (int it = 1; it <= max_iter; ++it) {
     tp.alphaQ = fq.alpha;
+    tp.zeroT = fq.T;
+    tp.zero_n = (int64_t)fq.G * p;
+    tp.zero_check = it >= check_from ? c->dred : nullptr;
     // T_P partials: segments with no local rows are not written by K1
     if (!tp.fused) LFE_HIP(hipMemsetAsync(fp.T, 0, sizeof(double) * (size_t)fp.G * p, c->stream));
     {
@@ -993,8 +1006,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       LFE_TRY(allreduce_sum_f64(c, fp.T, (size_t)fp.G * p));
       LFE_TRY(fin_check(c, P, fp.T, nullptr, fp.alpha, false));
     }
-    LFE_HIP(hipMemsetAsync(fq.T, 0, sizeof(double) * (size_t)fq.G * p, c->stream));
-    {
+    {  // fq.T (and the check's max) were zeroed by K1
       ProfScope _ps(c, K_TQ);
       switch (NT) {
         case 1: launch_tq<1>(c, tq, lds_tq); break;
@@ -1008,7 +1020,6 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     iterations = it;
     const bool check = it >= check_from;
     if (!check && it == max_iter) break;
-    if (check) LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double), c->stream));
     LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check));
     if (check) {
       LFE_TRY(d2h_sync(c, &last, c->dred, sizeof(double)));

@@ -108,10 +108,30 @@ __device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t* tmp, int3
   return x - v + tmp[wave];
 }
 
-__global__ __launch_bounds__(256) void k_scan_blocks(int32_t* __restrict__ a, int64_t m, int32_t* __restrict__ sums) {
+// Up to two independent arrays per launch: blocks [0, nb1) scan a1[0, m1), the rest a2[0, m2).
+struct ScanPair {
+  int32_t* a1;
+  int64_t m1;
+  int64_t nb1;
+  int32_t* a2;
+  int64_t m2;
+  __device__ __forceinline__ int32_t* arr(int64_t& blk, int64_t& m) const {
+    if (blk < nb1) {
+      m = m1;
+      return a1;
+    }
+    blk -= nb1;
+    m = m2;
+    return a2;
+  }
+};
+
+__global__ __launch_bounds__(256) void k_scan_blocks(ScanPair sp, int32_t* __restrict__ sums) {
   __shared__ int32_t tmp[8];
   __shared__ int32_t total;
-  const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+  int64_t blk = blockIdx.x, m;
+  int32_t* __restrict__ a = sp.arr(blk, m);
+  const int64_t base = blk * kScanBlock + (int64_t)threadIdx.x * kScanPer;
   int32_t v[kScanPer];
   int32_t s = 0;
 #pragma unroll
@@ -128,39 +148,51 @@ __global__ __launch_bounds__(256) void k_scan_blocks(int32_t* __restrict__ a, in
   if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(1024) void k_scan_top(int32_t* __restrict__ sums, int nblocks) {
+// block sums of both arrays: [0, nb1) and [nb1, nb1 + nb2), each scanned from 0
+__global__ __launch_bounds__(1024) void k_scan_top(int32_t* __restrict__ sums, int nb1, int nb2) {
   __shared__ int32_t tmp[16];
   __shared__ int32_t total;
-  int32_t carry = 0;
-  for (int base = 0; base < nblocks; base += blockDim.x) {
-    const int i = base + threadIdx.x;
-    const int32_t v = i < nblocks ? sums[i] : 0;
-    const int32_t ex = block_excl_scan(v, tmp, &total);
-    if (i < nblocks) sums[i] = ex + carry;
-    __syncthreads();
-    carry += total;
-    __syncthreads();
+  for (int seg = 0; seg < 2; ++seg) {
+    int32_t* sg = sums + (seg ? nb1 : 0);
+    const int nblocks = seg ? nb2 : nb1;
+    int32_t carry = 0;
+    for (int base = 0; base < nblocks; base += blockDim.x) {
+      const int i = base + threadIdx.x;
+      const int32_t v = i < nblocks ? sg[i] : 0;
+      const int32_t ex = block_excl_scan(v, tmp, &total);
+      if (i < nblocks) sg[i] = ex + carry;
+      __syncthreads();
+      carry += total;
+      __syncthreads();
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void k_scan_add(int32_t* __restrict__ a, int64_t m, const int32_t* __restrict__ sums) {
-  const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+__global__ __launch_bounds__(256) void k_scan_add(ScanPair sp, const int32_t* __restrict__ sums) {
+  int64_t blk = blockIdx.x, m;
+  int32_t* __restrict__ a = sp.arr(blk, m);
+  const int64_t base = blk * kScanBlock + (int64_t)threadIdx.x * kScanPer;
   const int32_t add = sums[blockIdx.x];
 #pragma unroll
   for (int k = 0; k < kScanPer; ++k)
     if (base + k < m) a[base + k] += add;
 }
 
-int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) {
-  const int64_t nblocks = (m + kScanBlock - 1) / kScanBlock;
+int exclusive_scan2(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2) {
+  const int64_t nb1 = (m1 + kScanBlock - 1) / kScanBlock, nb2 = a2 ? (m2 + kScanBlock - 1) / kScanBlock : 0;
+  const int64_t nblocks = nb1 + nb2;
+  if (nblocks == 0) return LFE_OK;
   LFE_TRY(ensure_pcounts(c, 0, (size_t)nblocks + 1));
+  const ScanPair sp{a1, m1, nb1, a2, m2};
   ProfScope _ps(c, K_SCAN);
-  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nblocks), dim3(256), 0, c->stream, a, m, c->psums);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, c->psums, (int)nblocks);
-  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nblocks), dim3(256), 0, c->stream, a, m, c->psums);
+  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, c->psums, (int)nb1, (int)nb2);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
 }
+
+int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) { return exclusive_scan2(c, a, m, nullptr, 0); }
 
 // ---------------------------------------------------------------------------
 // partition scatter
@@ -456,25 +488,33 @@ __global__ __launch_bounds__(256) void k_mark(MarkArgs a, int64_t n) {
   }
 }
 
-__global__ void k_sub_counts(const int32_t* __restrict__ pre, const int32_t* __restrict__ drops, int32_t G,
-                             int32_t* __restrict__ cnt) {
-  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) cnt[g] = pre[g] - drops[g];
-}
+// every FE at once (blockIdx.y = f): cnt = pre - drops, and the number of levels present
+// before and after the drop (one atomic per wave into two counters per FE)
+struct FinishCountsArgs {
+  const int32_t* pre[kMaxFE];
+  const int32_t* drops[kMaxFE];
+  int32_t* cnt[kMaxFE];
+  int32_t G[kMaxFE];
+  int32_t* out;  // [2 F]: (levels kept, levels present) per FE
+};
 
-__global__ void k_count_nonzero2(const int32_t* __restrict__ a, const int32_t* __restrict__ b, int32_t G,
-                                 int32_t* __restrict__ out) {
+__global__ void k_finish_counts(FinishCountsArgs a) {
+  const int f = blockIdx.y;
+  const int32_t G = a.G[f];
   int la = 0, lb = 0;
   for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
-    la += a[g] > 0;
-    lb += b[g] > 0;
+    const int32_t pre = a.pre[f][g], c = pre - a.drops[f][g];
+    a.cnt[f][g] = c;
+    la += c > 0;
+    lb += pre > 0;
   }
   for (int off = 32; off > 0; off >>= 1) {
     la += __shfl_down(la, off, 64);
     lb += __shfl_down(lb, off, 64);
   }
   if ((threadIdx.x & 63) == 0) {
-    if (la) atomicAdd(&out[0], la);
-    if (lb) atomicAdd(&out[1], lb);
+    if (la) atomicAdd(&a.out[2 * f], la);
+    if (lb) atomicAdd(&a.out[2 * f + 1], lb);
   }
 }
 
@@ -797,14 +837,19 @@ int prepare_layout(lfe_ctx* c) {
       }
     }
     LFE_HIP(hipGetLastError());
+    FinishCountsArgs fa{};
     for (int f = 0; f < c->F; ++f) {
       auto& fe = c->fe[f];
       LFE_TRY(allreduce_sum_i32(c, fe.drops, fe.G));
-      hipLaunchKernelGGL(k_sub_counts, dim3(grid_for(fe.G)), dim3(kBlock), 0, c->stream, fe.cnt_pre, fe.drops, fe.G,
-                         fe.cnt);
-      // few blocks: one atomic per wave into two counters (thousands of same-address adds serialize)
-      hipLaunchKernelGGL(k_count_nonzero2, dim3(grid_for(fe.G, kBlock, 32)), dim3(kBlock), 0, c->stream, fe.cnt, fe.cnt_pre,
-                         fe.G, c->iscratch + 2 * f);
+      fa.pre[f] = fe.cnt_pre;
+      fa.drops[f] = fe.drops;
+      fa.cnt[f] = fe.cnt;
+      fa.G[f] = fe.G;
+    }
+    fa.out = c->iscratch;
+    if (c->F > 0) {
+      // few blocks: thousands of same-address adds would serialize
+      hipLaunchKernelGGL(k_finish_counts, dim3(grid_for(gmax, kBlock, 32), c->F), dim3(kBlock), 0, c->stream, fa);
       LFE_HIP(hipGetLastError());
     }
   }
