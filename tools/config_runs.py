@@ -98,10 +98,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="2,4")
     ap.add_argument("--rows4", type=int, default=50_000_000)
+    ap.add_argument("--rows5", type=int, default=500_000_000)
     a = ap.parse_args()
     for c in [int(x) for x in a.configs.split(",")]:
         if c == 2:
             run(2, 10_000_000, 5, [100_000, 1_000], "iid")
+        elif c == 5:  # config 5 on one GPU (D = 1: 44 GB of columns fit in 288 GB)
+            run(5, a.rows5, 10, [100_000, 1_000], "iid")
         elif c == 4:
             run(4, a.rows4, 10, [1_000_000, 100_000, 10_000], "cluster", cluster_fes=[1, 2])
 
