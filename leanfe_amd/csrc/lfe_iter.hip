@@ -89,10 +89,17 @@ __global__ void k_ls_base(const int32_t* __restrict__ bitems, int nb, int K, int
     }
     const int b = (int)(e / K), j = (int)(e % K);
     int32_t run = 0;
-    for (int i = bitems[b]; i < bitems[b + 1]; ++i) {
-      const int32_t t = itemcnt[(int64_t)i * K + j];
-      itemcnt[(int64_t)i * K + j] = run;
-      run += t;
+    // eight items' counts loaded before any is rewritten (the chain is latency-bound otherwise)
+    for (int i = bitems[b], i1 = bitems[b + 1]; i < i1; i += 8) {
+      int32_t t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = i + u < i1 ? itemcnt[(int64_t)(i + u) * K + j] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i + u < i1) {
+          itemcnt[(int64_t)(i + u) * K + j] = run;
+          run += t[u];
+        }
     }
     off[e] = run;
   }

@@ -401,13 +401,14 @@ __global__ void k_gather_bstart(const int32_t* __restrict__ scanned, int nb, int
 // ---------------------------------------------------------------------------
 
 // pre-filter counts from the per-item histograms of the two-FE layouts: primary group h sums
-// its bucket's items (cnt1[item][h - lo]); secondary level q sums a 1/64 slice of all items
+// its bucket's items (cnt1[item][h - lo]); secondary level q sums a 1/256 slice of all items
 __global__ void k_cnt_from_items_p(const int32_t* __restrict__ cnt1, const int32_t* __restrict__ bitems, int s,
                                    int32_t G, int32_t* __restrict__ cnt) {
   const int B = 1 << s;
   for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < G; h += gridDim.x * blockDim.x) {
     const int b = h >> s, j = h & (B - 1);
     int32_t t = 0;
+#pragma unroll 4
     for (int i = bitems[b]; i < bitems[b + 1]; ++i) t += cnt1[(int64_t)i * B + j];
     cnt[h] = t;
   }
@@ -419,6 +420,7 @@ __global__ void k_cnt_from_items_q(const int32_t* __restrict__ cnt2, int n_items
   if (q >= G) return;
   const int i0 = (int)((int64_t)blockIdx.y * n_items / gridDim.y), i1 = (int)((int64_t)(blockIdx.y + 1) * n_items / gridDim.y);
   int32_t t = 0;
+#pragma unroll 4
   for (int i = i0; i < i1; ++i) t += cnt2[(int64_t)i * G + q];
   if (t) atomicAdd(&cnt[q], t);
 }
@@ -789,7 +791,7 @@ int prepare_layout(lfe_ctx* c) {
     const int32_t* c2 = c->seg_aux + (size_t)L.n_items * B;
     hipLaunchKernelGGL(k_cnt_from_items_p, dim3(grid_for(c->fe[L.P].G)), dim3(kBlock), 0, c->stream, c1, c->bitems_d,
                        L.s, c->fe[L.P].G, c->fe[L.P].cnt_pre);
-    hipLaunchKernelGGL(k_cnt_from_items_q, dim3((c->fe[Q].G + 255) / 256, 64), dim3(256), 0, c->stream, c2,
+    hipLaunchKernelGGL(k_cnt_from_items_q, dim3((c->fe[Q].G + 255) / 256, 256), dim3(256), 0, c->stream, c2,
                        L.n_items, c->fe[Q].G, c->fe[Q].cnt_pre);
     LFE_HIP(hipGetLastError());
   } else if (L.permuted) {
