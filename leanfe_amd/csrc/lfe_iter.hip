@@ -577,6 +577,13 @@ __device__ __forceinline__ void static_for4(Fn&& fn) {
     static_for4<B + 4, E>(fn);
   }
 }
+template <int B, int E, typename Fn>
+__device__ __forceinline__ void static_for8(Fn&& fn) {
+  if constexpr (B < E) {
+    fn(std::integral_constant<int, B>{});
+    static_for8<B + 8, E>(fn);
+  }
+}
 
 // Codes of 16 consecutive 16-row groups [gb, gb + 16) are one load per lane:
 // lane (kq, c) holds quad kq of group gb + c; group gb + d's codes reach the
@@ -687,8 +694,7 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
       const int g = gb + c;
       return g < g1 ? *reinterpret_cast<const int4*>(a.seg_q + g * 16 + 4 * kq) : int4{0, 0, 0, 0};
     };
-    auto batch = [&](const int4& v, int gb) {
-      static_for4<0, kBatch>([&](auto dc) {
+    auto four = [&](const int4& v, int gb, auto dc) {
         constexpr int d = decltype(dc)::value;
         if (gb + d >= g1 || done) return;
         const int4 q[4] = {rowbc4<d>(v), rowbc4<d + 1>(v), rowbc4<d + 2>(v), rowbc4<d + 3>(v)};
@@ -716,6 +722,36 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
           if (gb + d + dd >= g1 || done) return;
           group(gb + d + dd, q[dd]);
         }
+    };
+    // 8 groups inside the segment: all 32 row gathers issued before their sums (more LDS reads in
+    // flight per wave; the pass is latency-bound at 4 waves per SIMD); else two 4-group steps
+    auto batch = [&](const int4& v, int gb) {
+      static_for8<0, kBatch>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if (gb + d >= g1 || done) return;
+        const int gs = (gb + d) * 16;
+        if (gs >= r0 && gs + 128 < r1) {
+          const int4 q[8] = {rowbc4<d>(v),     rowbc4<d + 1>(v), rowbc4<d + 2>(v), rowbc4<d + 3>(v),
+                             rowbc4<d + 4>(v), rowbc4<d + 5>(v), rowbc4<d + 6>(v), rowbc4<d + 7>(v)};
+          double t[4][NT];
+#pragma unroll
+          for (int dd = 0; dd < 8; ++dd) {
+            const int qv[4] = {q[dd].x, q[dd].y, q[dd].z, q[dd].w};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+#pragma unroll
+              for (int I = 0; I < NT; ++I) {
+                const double x = lds_row(aq, qv[s], p8, cl8[I]);
+                t[s][I] = dd == 0 ? x : t[s][I] + x;
+              }
+            }
+          }
+#pragma unroll
+          for (int I = 0; I < NT; ++I) acc[I] += (t[0][I] + t[1][I]) + (t[2][I] + t[3][I]);
+          return;
+        }
+        four(v, gb, std::integral_constant<int, d>{});
+        four(v, gb, std::integral_constant<int, d + 4>{});
       });
     };
     int4 va = load(g0), vb;
