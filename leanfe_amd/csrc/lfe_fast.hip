@@ -6,6 +6,8 @@
 //    adds them into LDS tables whose 16 lanes of a row hit 16 consecutive
 //    doubles (primary FE: the 2^s-group slice of the item's bucket; small FEs:
 //    whole tables).
+// 2. k_sums2_raw: the same for two FEs without weights, plus the raw Gram of
+//    the shifted columns on the matrix cores (the headline case).
 //
 // The alternating-projection sweeps of the two-FE case are in lfe_iter.hip.
 #include "lfe_internal.h"

@@ -907,7 +907,7 @@ static int design_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
 // by its first layout row c (a shift the FEs absorb: d - c - a - (b - c) = d~):
 //   sum d~ d~' = R + sum_h [n a a' - S a' - a S'] + sum_q [n b' b'' - V b'' - b' V']
 //   sum d~     = C - sum_h n a - sum_q n b'
-// with R, C the raw Gram / column sums of d - c over kept rows (k_sums4<RAW>),
+// with R, C the raw Gram / column sums of d - c over kept rows (k_sums2_raw / k_sums4<RAW>),
 // S the group sums, b' = b - c, V = S_Q - n c - T_Q and T_Q = sum_{i in q} a_{h_i}
 // (the last sweep's cross term, formed from the final a).  Per group the bracket is
 // n a_i a_j - V_i a_j - a_i V_j: symmetric, so only the upper triangle is summed.
