@@ -353,3 +353,30 @@ def test_empty_input_raises():
     d = {"y": np.zeros(0), "x": np.zeros(0), "a": np.zeros(0, dtype=np.int64), "b": np.zeros(0, dtype=np.int64)}
     with pytest.raises(Exception):
         leanfe_hip(d, formula="y ~ x | a + b", strategy="alt_proj", quiet=True)
+
+
+@pytest.mark.parametrize("L", [(3000, 40), (200, 30)])  # bucketed layout (deferred row index) / not
+def test_copy_demeaned_matches_oracle_in_input_order(L):
+    """lfe_copy_demeaned returns the demeaned columns in input row order (NaN on dropped rows).
+    On a bucketed layout the input row index of each layout row is written on this first use
+    (ensure_layout_orig), by an index-only rerun of the partition scatter."""
+    from leanfe_amd._lib import Engine
+    from oracle import altproj as ref
+    rng = np.random.default_rng(5)
+    n, k = 120_003, 2
+    codes = [rng.integers(0, G, n).astype(np.int32) for G in L]
+    codes[0][codes[0] >= L[0] - 5] = 0
+    codes[0][:5] = np.arange(L[0] - 5, L[0], dtype=np.int32)  # five singletons of the first FE
+    cols = [rng.standard_normal(n) for _ in range(k + 1)]
+    with Engine(0) as eng:
+        eng.load(cols, codes, list(L))
+        n_obs, _, card = eng.drop_singletons()
+        order = sorted(range(len(L)), key=lambda i: card[i])
+        iters, _ = eng.demean(order, 1e-8, 100, check_from=3)
+        out = eng.copy_demeaned()
+    keep = ref.singleton_keep(codes, list(L))
+    assert n_obs == int(keep.sum()) == n - 5
+    dm, it_ref = ref.demean_altproj(np.array(cols)[:, keep], [c[keep] for c in codes], list(L), order, 1e-8, 100)
+    assert iters == it_ref
+    assert np.all(np.isnan(out[:, ~keep]))
+    np.testing.assert_allclose(out[:, keep], dm, rtol=1e-9, atol=1e-11)
