@@ -231,14 +231,16 @@ __device__ __forceinline__ int xcd_chunk(int i, int nw) {
   return x * per + r;                      // may be >= nw: the caller's r0 >= n then
 }
 
-template <int PER, int NTH>
+// DB: two column stages, so a column's write-out overlaps the next column's staging with one
+// barrier per column instead of two (the int columns always use two int32 halves of the stage)
+template <int PER, int NTH, bool DB>
 __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   constexpr int kPartThreads = NTH;
   constexpr int kPartWaves = NTH / 64;
   constexpr int R = kPartThreads * PER;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* stage = smem;                                        // [R] (doubles or int32)
-  int32_t* cur = reinterpret_cast<int32_t*>(stage + R);        // [waves][nb] cursors
+  double* stage = smem;                                        // [R or 2R] (doubles or int32)
+  int32_t* cur = reinterpret_cast<int32_t*>(stage + (DB ? 2 : 1) * R);  // [waves][nb] cursors
   int32_t* delta = cur + kPartWaves * a.nb;                    // [nb]
   int32_t* tot = delta + a.nb;                                 // [nb + 1]
   __shared__ int32_t wsum[16];
@@ -355,26 +357,32 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   if (ncol > 0) load_col(0);
   for (int c = 0; c < ncol; ++c) {
     double* dst = c < a.p ? a.Xo + (int64_t)c * a.ld : a.wo;
+    // DB: this buffer was last read by column c - 2's write-out, which every wave finished
+    // before the barrier of column c - 1
+    double* st = DB ? stage + (c & 1) * R : stage;
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (pos[k] >= 0) stage[pos[k]] = v[k];
+      if (pos[k] >= 0) st[pos[k]] = v[k];
     if (a.pipe && c + 1 < ncol) load_col(c + 1);  // next column in flight during the write-out
     __syncthreads();
     if (a.nt & 1) {
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (dd[k] >= 0) __builtin_nontemporal_store(stage[slot_of(k)], dst + dd[k]);
+        if (dd[k] >= 0) __builtin_nontemporal_store(st[slot_of(k)], dst + dd[k]);
     } else {
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (dd[k] >= 0) dst[dd[k]] = stage[slot_of(k)];
+        if (dd[k] >= 0) dst[dd[k]] = st[slot_of(k)];
     }
-    __syncthreads();
+    if (!DB) __syncthreads();
     if (!a.pipe && c + 1 < ncol) load_col(c + 1);
   }
-  int32_t* istage = reinterpret_cast<int32_t*>(stage);
-  for (int c = a.cols ? 0 : a.F; c < a.F + a.want_orig; ++c) {  // F code arrays, then the input row index
+  if (DB && ncol > 0) __syncthreads();  // the int halves overlap the column stages
+  int32_t* istage0 = reinterpret_cast<int32_t*>(stage);
+  const int ic0 = a.cols ? 0 : a.F;
+  for (int c = ic0; c < a.F + a.want_orig; ++c) {  // F code arrays, then the input row index
     int32_t* dst = c < a.F ? a.codeo[c] : a.orig;
+    int32_t* istage = istage0 + ((c - ic0) & 1) * R;  // two int32 halves of the double stage
 #pragma unroll
     for (int k = 0; k < PER; k += 2) {
       const int64_t i = row_of(k);
@@ -387,7 +395,6 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
 #pragma unroll
     for (int k = 0; k < PER; ++k)
       if (dd[k] >= 0) dst[dd[k]] = istage[slot_of(k)];
-    __syncthreads();
   }
 }
 
@@ -642,9 +649,10 @@ static int launch_part_scatter(lfe_ctx* c, int cols, int orig) {
   const int pgrid = a.xcd_map ? ((g.nw + 7) / 8) * 8 : g.nw;
   // dynamic LDS above 64 KB must be opted in (static LDS + dynamic <= 160 KB)
   using Fn = void (*)(ScatterArgs);
-  Fn fn = g.nth == 1024 ? (g.per == 16 ? &k_part_scatter<16, 1024>
-                           : g.per == 8 ? &k_part_scatter<8, 1024> : &k_part_scatter<4, 1024>)
-                        : (g.per == 16 ? &k_part_scatter<16, 512> : &k_part_scatter<8, 512>);
+  Fn fn = g.db ? &k_part_scatter<8, 1024, true>
+         : g.nth == 1024 ? (g.per == 16 ? &k_part_scatter<16, 1024, false>
+                            : g.per == 8 ? &k_part_scatter<8, 1024, false> : &k_part_scatter<4, 1024, false>)
+                         : (g.per == 16 ? &k_part_scatter<16, 512, false> : &k_part_scatter<8, 512, false>);
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)g.lds));
   {
@@ -732,13 +740,27 @@ int prepare_layout(lfe_ctx* c) {
       const char* e = getenv("LFE_PART_CW");  // tuning: rows per chunk (8192 or 16384)
       return e ? (int64_t)atol(e) : (int64_t)16384;  // 16K: ~84-row runs per bucket at s = 9
     }();
+    static const int db_env = [] {
+      // tuning: 1 = double-buffered column stage on 8192-row chunks (one barrier per column);
+      // measured 1.996 vs 1.949 ms for one stage on 16384-row chunks, so off
+      const char* e = getenv("LFE_PART_DB");
+      return e ? atoi(e) : 0;
+    }();
     int64_t cw = nb <= 512 ? cw_env : 4096;
-    auto part_lds = [&](int nth) {
-      return sizeof(double) * cw + sizeof(int32_t) * ((size_t)(nth / 64) * nb + 2 * (size_t)nb + 1);
+    auto part_lds = [&](int nth, bool db = false) {
+      return sizeof(double) * cw * (db ? 2 : 1) + sizeof(int32_t) * ((size_t)(nth / 64) * nb + 2 * (size_t)nb + 1);
     };
     // 16 waves per chunk when their per-wave bucket cursors fit (nb <= ~1500)
     const int nth = nth_env == 1024 && part_lds(1024) <= 150 * 1024 ? 1024 : 512;
     if (cw == 16384 && (nth != 1024 || part_lds(1024) > 150 * 1024)) cw = 8192;
+    // double-buffered stage: 8192-row chunks (two 64 KB stages), one barrier per column
+    bool db = false;
+    if (db_env && nth == 1024 && nb <= 512) {
+      const int64_t keep = cw;
+      cw = 8192;
+      db = part_lds(1024, true) <= 150 * 1024;
+      if (!db) cw = keep;
+    }
     const int per = (int)(cw / nth);
     const int nw = (int)((n + cw - 1) / cw);
     const int64_t m = (int64_t)nb * nw;
@@ -756,8 +778,8 @@ int prepare_layout(lfe_ctx* c) {
     hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(nb)), dim3(kBlock), 0, c->stream, c->pcounts, nb, nw, dbstart);
     LFE_HIP(hipGetLastError());
     LFE_TRY(d2h_async(c, dbstart, sizeof(int32_t) * nb));
-    const size_t lds = std::min<size_t>(std::max(part_lds(nth), lds_min), 160 * 1024);
-    L.part = PartGeom{nth, per, nw, lds};
+    const size_t lds = std::min<size_t>(std::max(part_lds(nth, db), lds_min), 160 * 1024);
+    L.part = PartGeom{nth, per, nw, db, lds};
     // the input row index of each layout row is written only when a caller needs it
     // (ensure_layout_orig: cluster, records and demeaned-column export paths)
     LFE_TRY(launch_part_scatter(c, /*cols=*/1, /*orig=*/0));
