@@ -393,9 +393,9 @@ int sums4(lfe_ctx* c) {
   c->raw_ready = false;
   static const int sums2_env = [] {
     // tuning: 0 = k_sums4 for the two-FE Gram case; MFMA chains x groups per load: 1 = 4 x 2,
-    // 2 = 2 x 2, 3 = 4 x 1, 4 = 2 x 1
+    // 2 = 2 x 2, 3 = 4 x 1, 4 = 2 x 1 (3: 0.925 vs 0.950 ms for 1 with 24-bit LDS addressing)
     const char* e = getenv("LFE_SUMS2");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 3;
   }();
   int threads = kSumThreads;
   if (a.nq <= 1 && NT == 1) {
