@@ -635,7 +635,10 @@ static int launch_part_scatter(lfe_ctx* c, int cols, int orig) {
   }();
   a.xcd_map = xmap_env;
   static const int pipe_env = [] {
-    const char* e = getenv("LFE_PART_PIPE");  // tuning (measured: 1 is 0.5 % faster)
+    // tuning: 1 = load column c + 1 during column c's write-out. It was 0.5% faster with two
+    // barriers per int column. With one barrier per int column, 0 was 1.7% faster in some runs
+    // but bimodal (2.04 / 2.50 ms on one box, alternating A/B); 1 held 2.076 ms every run
+    const char* e = getenv("LFE_PART_PIPE");
     return e ? atoi(e) : 1;
   }();
   a.pipe = pipe_env;
