@@ -1,167 +1,350 @@
 #!/usr/bin/env python
-"""Headline benchmark: Mrows/s of demean + solve at 50M rows x 2 HDFE.
+"""Headline benchmark: Mrows/s of demean + solve at 50M rows x 2 HDFE (BASELINE.json).
 
-Workload (BASELINE.json configs[2]): synthetic counter-based panel
-(leanfe_amd/synth.py, seed 12345), N = 5e7 rows per GPU, k = 10 regressors,
-FEs with 1e5 and 1e3 levels, vcov = HC1.  One "step" = one full regression on
-device-resident inputs exactly as ``leanfe_hip`` runs it after the data
-hand-off: singleton drop -> alternating projections to convergence
-(tol 1e-6, max_iter 50, check from it=3) -> Gram (MFMA) -> host Cholesky ->
-residual + HC1 meat -> SEs.
+Workloads (BASELINE.json ``configs``; ``--config``, default 3 = the headline):
+  1  1M rows, FEs (2e4, 500), k = 3, IID
+  2  10M rows, FEs (1e5, 1e3), k = 5, IID
+  3  50M rows, FEs (1e5, 1e3), k = 10, HC1            <- metric of BASELINE.json
+  4  50M rows, FEs (1e6, 1e5, 1e4), k = 10, two-way clustered SE on fe2 x fe3 (CGM)
+  5  500M rows, FEs (1e5, 1e3), k = 10, IID
+Synthetic counter-based panel (leanfe_amd/synth.py, seed 12345) generated on the device.
+One "step" = one full regression on device-resident inputs exactly as ``leanfe_hip`` runs
+it after the data hand-off: singleton drop -> alternating projections to convergence
+(tol 1e-6, max_iter 50, check from it = 3) -> Gram (MFMA) -> Cholesky -> residual pass
+(+ HC1 meat / cluster scores) -> SEs.  tests/test_gpu_configs.py runs ``solve_step`` on
+the same workloads against the C restatement of the reference (oracle/altproj_c.c).
 
-Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): one process per
-GPU, rows sharded (rank r generates rows [r*N, (r+1)*N) of the same panel,
-weak scaling), every per-group partial sum / Gram / meat all-reduced with RCCL
-inside the engine.  Timing: W warm-up steps, then barrier + device sync, K
-timed steps, device sync + barrier; the max over ranks is reported.
+Multi-GPU: one process per GPU.  Under torchrun the rank comes from the environment;
+``python bench.py --gpus N`` without it spawns N rank processes itself (before any GPU
+call).  ``--scaling strong`` (default): ``--rows`` rows in total, sharded over the ranks;
+``--scaling weak``: ``--rows`` rows per rank.  ``--shard owner`` (default for two-FE
+unclustered fits) gives each rank every row of a contiguous range of primary-FE levels,
+so the primary FE's group tables stay rank-local and only the secondary FE's tables, the
+Gram and the SE statistics are all-reduced over RCCL; ``--shard rows`` shards contiguous
+row blocks (every group table all-reduced).  Timing: W warm-up steps, barrier + device
+sync, K timed steps, device sync + barrier; the max over ranks is reported.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from leanfe_amd import inference, synth  # noqa: E402
-from leanfe_amd._lib import Engine  # noqa: E402
-from leanfe_amd.dist import HostGroup  # noqa: E402
-
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+BASELINE_METRIC = "Mrows/sec demean+solve, 50M×2-HDFE; achieved HBM GB/s at 1/2/4/8 GPUs"
+
+# BASELINE.json configs (index = config number): rows (total), levels, k, vcov, cluster FEs
+CONFIGS = {
+    1: dict(rows=1_000_000, levels=[20_000, 500], k=3, vcov="iid", cl=None),
+    2: dict(rows=10_000_000, levels=[100_000, 1_000], k=5, vcov="iid", cl=None),
+    3: dict(rows=50_000_000, levels=[100_000, 1_000], k=10, vcov="HC1", cl=None),
+    4: dict(rows=50_000_000, levels=[1_000_000, 100_000, 10_000], k=10, vcov="cluster", cl=[1, 2]),
+    5: dict(rows=500_000_000, levels=[100_000, 1_000], k=10, vcov="iid", cl=None),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps (GPU clocks settle within ~0.1 s)")
-    ap.add_argument("--rows", type=int, default=50_000_000, help="rows per GPU")
-    ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--levels", type=str, default="100000,1000")
-    ap.add_argument("--vcov", type=str, default="HC1")
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=None, help="rows (total with --scaling strong, per GPU with weak)")
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--levels", type=str, default=None)
+    ap.add_argument("--vcov", type=str, default=None)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--shard", choices=["auto", "owner", "rows"], default="auto")
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--cpu-rows", type=int, default=50_000_000, help="CPU baseline sample (prefix rows)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-h2d", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="diagnostic: no per-kernel events (no roofline)")
     ap.add_argument("--verbose", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--print-rank-env", action="store_true",
+                    help="diagnostic: each rank prints its rank / world / device and exits (no GPU call)")
+    a = ap.parse_args(argv)
+    cfg = CONFIGS[a.config]
+    a.rows = cfg["rows"] if a.rows is None else a.rows
+    a.k = cfg["k"] if a.k is None else a.k
+    a.levels = list(cfg["levels"]) if a.levels is None else [int(x) for x in a.levels.split(",")]
+    a.vcov = cfg["vcov"] if a.vcov is None else a.vcov
+    a.cl = cfg["cl"] if a.vcov.lower() == "cluster" else None
+    if a.vcov.lower() == "cluster" and a.cl is None:
+        a.cl = list(range(1, len(a.levels)))[:2] or [0]
+    return a
 
 
-def device_sync(eng: Engine):
+def is_headline(a) -> bool:
+    return (a.rows, a.k, a.levels, a.vcov.lower()) == (50_000_000, 10, [100_000, 1_000], "hc1") \
+        and (a.scaling == "strong" or a.gpus == 1)
+
+
+def workload_label(a, world: int) -> str:
+    per = "total" if a.scaling == "strong" else "per GPU"
+    se = a.vcov if a.vcov.lower() != "cluster" else f"{len(a.cl)}-way clustered SE on " + " x ".join(
+        f"fe{f + 1}" for f in a.cl)
+    lv = ", ".join(f"{g:.0e}".replace("e+0", "e") for g in a.levels)
+    return f"configs[{a.config - 1}]: {a.rows / 1e6:g}M rows {per}, {len(a.levels)} FE ({lv} levels), k={a.k}, {se}"
+
+
+# ---------------------------------------------------------------------------
+# launcher (no GPU call, no engine import: the children initialise the GPU)
+# ---------------------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n: int, port: int, base: dict | None = None) -> list[dict]:
+    """Environment of each of the n rank processes (torchrun's variables, local node)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def spawn_ranks(n: int, argv: list[str], timeout: float | None = None) -> int:
+    """Run this script as n rank processes; if one fails the others are ended.  Returns the
+    first non-zero exit code (0 when all succeed)."""
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e)
+             for e in rank_envs(n, _free_port())]
+    t0 = time.time()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            if timeout is not None and time.time() - t0 > timeout:
+                rc = 124
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# one step (the hip backend's hot path on device-resident data)
+# ---------------------------------------------------------------------------
+
+def device_sync(eng):
     eng.sync()
-    torch = sys.modules.get("torch")  # only when already imported (multi-GPU runs)
-    if torch is not None and torch.cuda.is_available():
-        torch.cuda.synchronize()
 
 
-def solve_step(eng: Engine, vcov: str):
-    """One regression on device-resident data (the hip backend's hot path)."""
+def solve_step(eng, vcov: str, n_cl: int = 0) -> dict:
+    """One regression on the loaded shard, as ``leanfe_hip`` runs it (hip_impl.py)."""
+    from leanfe_amd import inference
+
     n_obs, dims, card = eng.drop_singletons()
-    order = sorted(range(len(card)), key=lambda i: card[i])
+    order = sorted(range(len(card)), key=lambda i: card[i])  # polars_impl.py:485
     iterations, _ = eng.demean(order, 1e-6, 50, check_from=3)
-    hc1 = vcov.lower() == "hc1"
-    # HC1: Gram + device solve + residual pass, one round trip; IID: the Gram alone
-    fused = eng.gram_resid(hc1=hc1) if hc1 else None
+    v = vcov.lower()
+    gram_only = v == "iid"  # IID without weights: residual statistics from the Gram
+    fused = None if gram_only else eng.gram_resid(hc1=v == "hc1", keep_scores=v == "cluster")
     G = fused[0] if fused is not None else eng.gram()
     XtX, Xty = inference.split_gram(G)
-    beta_full, XtX_inv = inference.solve_normal(XtX, Xty)
+    beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # host, polars_impl.py:212-226
     k = XtX.shape[0] - 1
     df_resid = n_obs - (k + 1) - (sum(dims) - len(dims))
-    stats, meat = (fused[2], fused[3]) if fused is not None else (inference.stats_from_gram(G, beta_full), None)
-    if stats is None:
-        stats, meat = eng.resid(beta_full, hc1=hc1)
-    if vcov.lower() == "hc1":
-        se = inference.se_hc1(XtX_inv[1:, 1:], meat, n_obs, df_resid)
+    Vb = XtX_inv[1:, 1:]
+    dbeta = 0.0
+    if gram_only:
+        stats, meat = inference.stats_from_gram(G, beta_full), None
+    elif fused is not None:
+        stats, meat = fused[2], fused[3]
+        # the residual pass used the device Cholesky's beta: record its distance to the host solve
+        dbeta = float(abs(fused[1] - beta_full).max() / max(abs(beta_full).max(), 1e-300))
     else:
-        se = inference.se_iid(XtX_inv[1:, 1:], stats[0], df_resid)
-    return dict(n_obs=n_obs, iterations=iterations, beta=beta_full[1:], se=se, df_resid=df_resid)
+        stats, meat = eng.resid(beta_full, hc1=v == "hc1", keep_scores=v == "cluster")
+    ncl = None
+    if v == "iid":
+        se = inference.se_iid(Vb, stats[0], df_resid)
+    elif v == "hc1":
+        se = inference.se_hc1(Vb, meat, n_obs, df_resid)
+    elif n_cl == 1:
+        meats, Gs = eng.cluster_meat()
+        se, ncl = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, True)
+    else:
+        subsets = inference.cluster_subsets(n_cl)
+        meats, Gs = eng.cluster_meat_subsets(subsets)  # intersections formed on the device
+        se, ncl = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets, n_obs, df_resid,
+                                                True)
+    return dict(n_obs=n_obs, iterations=iterations, beta=beta_full[1:], se=se, df_resid=df_resid,
+                fe_dims=list(dims), n_clusters=ncl, rss=float(stats[1]), beta_dev_vs_host=dbeta)
 
 
-def algorithmic_bytes(n: int, p: int, F: int, T: int, hc1: bool) -> dict:
-    """HBM bytes each kernel must move per launch (DESIGN.md "Kernels and their rooflines").
+def load_shard(eng, a, rank: int, world: int, shard: str) -> dict:
+    """Generate this rank's shard of the synthetic panel on the device; returns its geometry."""
+    from leanfe_amd import dist, synth
 
-    n rows/GPU, p = 1 + k data columns (f64), F fixed effects (int32 codes).  The
-    layout passes scan every row of the shard (dropped rows included).
-    """
+    total = a.rows if a.scaling == "strong" else a.rows * world
+    beta = synth.betas(a.k)
+    if shard == "owner":
+        # every row whose primary-FE code lies in this rank's level range (dist.owner_range)
+        P = max(range(len(a.levels)), key=lambda f: a.levels[f])
+        lo, hi = dist.owner_range(a.levels[P], rank, world)
+        eng.synth_load_owned(total, a.k, a.levels, beta, P, lo, hi, seed=a.seed)
+        return dict(total=total, local=eng.n, owner=(P, lo, hi))
+    lo, hi = dist.shard_range(total, rank, world)
+    eng.synth_load(hi - lo, a.k, a.levels, beta, seed=a.seed, row_offset=lo)
+    return dict(total=total, local=hi - lo, rows=(lo, hi))
+
+
+# ---------------------------------------------------------------------------
+# measurement helpers
+# ---------------------------------------------------------------------------
+
+def algorithmic_bytes(n: int, p: int, F: int) -> dict:
+    """HBM bytes each kernel must move per launch, n rows of the shard,
+    p = 1 + k f64 data columns, F int32 code columns.  Kernels absent here move only group
+    tables or scalars (latency-bound) and count as 0 in the step total."""
     return {
-        "part_hist": 4 * n,                              # primary codes
-        "part_scatter": n * (2 * 8 * p + 2 * 4 * F),      # read + write X and codes
-        "count": 4 * n,                                  # one code column per launch
-        "mark": 4 * n * F,                               # every code column (+ sparse writes)
-        "group_sums": n * (8 * p + 4 * F),               # X + codes
-        "cross": 4 * n,                                  # secondary codes in segment order
-        "gram_design": n * (8 * p + 4 * F),              # X + codes
-        "gram_resid": n * (8 * p + 4 * F),               # X + codes (HC1: no score write)
+        "part_hist": 4 * n,                          # primary codes
+        "part_scatter": n * (2 * 8 * p + 2 * 4 * F),  # read + write X and codes
+        "layout_hist": 8 * n,                        # both codes in layout order
+        "layout_scatter": n * (8 + 4 + 2),           # both codes -> seg_q (int32) + run_h (uint16)
+        "group_sums": n * (8 * p + 4 * F),           # X + codes (+ the raw Gram, MFMA)
+        "tp": 4 * n,                                 # seg_q: the cross term of the primary FE
+        "tq": 2 * n,                                 # run_h: the cross term of the secondary FE
+        "gram_design": n * (8 * p + 4 * F),          # X + codes
+        "gram_resid": n * (8 * p + 4 * F),           # X + codes (HC1: no score write)
     }
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+def pmc_traffic(kernel: str, a) -> tuple[float | None, str | None]:
+    """HBM bytes per launch of ``kernel`` from the newest rocprofv3 PMC summary for this exact
+    configuration (tools/pmc.sh + tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+    correction of MI355X_MICROARCH.md), else None."""
+    cfg = {"rows": a.rows, "k": a.k, "levels": list(a.levels), "vcov": a.vcov}
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if t.get("config") == cfg and kernel in t.get("kernels", {}):
+            return float(t["kernels"][kernel]["bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
 
 
-def pmc_traffic(kernel: str, args, levels) -> float | None:
-    """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters
-    (tools/pmc.sh + tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
-    correction of MI355X_MICROARCH.md) for this exact configuration, else None."""
+def host_info(threads: int) -> dict:
+    model = None
     try:
-        with open(PMC_TRAFFIC) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
-        return None
-    cfg = {"rows": args.rows, "k": args.k, "levels": list(levels), "vcov": args.vcov}
-    if t.get("config") != cfg or kernel not in t.get("kernels", {}):
-        return None
-    return float(t["kernels"][kernel]["bytes_per_launch"])
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, check=True).stdout.strip())
+    except (OSError, ValueError, subprocess.CalledProcessError):
+        nproc = None
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return dict(cores=threads, nproc=nproc, affinity_cpus=aff, os_cpu_count=os.cpu_count(), cpu_model=model,
+                omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
 
 
-def cpu_baseline(args, levels, eng: Engine) -> dict:
-    """CPU baseline: the C restatement of the reference alt_proj path (oracle/altproj_c.c,
-    OpenMP over columns) on the host cores, over the first ``--cpu-rows`` rows of the very
-    panel the GPU solved (copied back from the device)."""
-    from oracle.altproj_c import fit_c
+def cpu_baseline(a, cols, codes) -> dict:
+    """The C restatement of the reference alt_proj path (oracle/altproj_c.c: row-parallel
+    OpenMP, every host thread this process may use) on the first ``--cpu-rows`` rows of the
+    very panel the GPU solved."""
+    from oracle.altproj_c import default_threads, fit_c
 
-    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1, 16))
-    cols, codes = eng.copy_inputs()
-    n = min(args.cpu_rows, cols.shape[1])
+    threads = default_threads()
+    n = min(a.cpu_rows, cols.shape[1])
+    cl = [codes[f][:n] for f in a.cl] if a.cl else None
     t0 = time.perf_counter()
-    r = fit_c([c[:n] for c in cols], [c[:n] for c in codes], levels, vcov=args.vcov, threads=threads)
+    r = fit_c([c[:n] for c in cols], [c[:n] for c in codes], a.levels, vcov=a.vcov, threads=threads, cl_codes=cl,
+              cl_levels=[a.levels[f] for f in a.cl] if a.cl else None)
     dt = time.perf_counter() - t0
     whole = "the whole" if n == cols.shape[1] else f"the first {n:_} rows of the"
-    return dict(value=n / dt / 1e6, unit="Mrows/s", cores=threads, kind="port",
-                sample=f"{whole} {cols.shape[1]:_}-row panel (k={args.k}, levels={levels}, vcov={args.vcov}); "
-                       f"oracle/altproj_c.c (C restatement of polars_impl.py alt_proj), {threads} OpenMP threads, "
-                       f"{dt:.2f} s, iterations={r['iterations']}",
-                iterations=int(r["iterations"]), seconds=round(dt, 3))
+    out = dict(value=round(n / dt / 1e6, 3), unit="Mrows/s", kind="port",
+               sample=f"{whole} {cols.shape[1]:_}-row panel (k={a.k}, levels={a.levels}, vcov={a.vcov}); "
+                      f"oracle/altproj_c.c (C restatement of polars_impl.py alt_proj + std_errors.py, row-parallel "
+                      f"OpenMP), {threads} threads, {dt:.2f} s, iterations={r['iterations']}",
+               iterations=int(r["iterations"]), seconds=round(dt, 3))
+    out.update(host_info(threads))
+    return out
 
 
-def main():
-    args = parse()
-    levels = [int(x) for x in args.levels.split(",")]
+def main(argv=None):
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not under torchrun: one process per GPU, spawned before anything touches the GPU
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:] if argv is None else list(argv)))
+
+    if a.print_rank_env:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}),
+              flush=True)
+        return
+
+    import numpy as np
+
+    from leanfe_amd._lib import Engine
+    from leanfe_amd.dist import HostGroup
+
     d = HostGroup()
+    if d.world != a.gpus:
+        raise SystemExit(f"bench.py --gpus {a.gpus} but WORLD_SIZE={d.world}")
+    shard = a.shard
+    if shard == "auto":
+        shard = "owner" if (len(a.levels) == 2 and a.vcov.lower() != "cluster" and d.world > 1) else "rows"
     eng = Engine(d.local)
     if d.world > 1:
         uid = Engine.unique_id() if d.rank == 0 else None
         uid = d.bcast_bytes(uid)
         eng.set_comm(uid, d.rank, d.world)
-    beta = synth.betas(args.k)
     t0 = time.perf_counter()
-    eng.synth_load(args.rows, args.k, levels, beta, seed=args.seed, row_offset=d.rank * args.rows)
+    geo = load_shard(eng, a, d.rank, d.world, shard)
+    n_cl = len(a.cl) if a.cl else 0
+    if n_cl:
+        _, codes = eng.copy_inputs()
+        eng.load_clusters([np.ascontiguousarray(codes[f]) for f in a.cl], [a.levels[f] for f in a.cl])
     gen_s = time.perf_counter() - t0
 
-    for _ in range(args.warmup):
-        solve_step(eng, args.vcov)
+    for _ in range(a.warmup):
+        solve_step(eng, a.vcov, n_cl)
 
     d.barrier()
     device_sync(eng)
-    eng.profile(not args.no_prof)
+    eng.profile(not a.no_prof)
     t0 = time.perf_counter()
     res = None
-    for _ in range(args.steps):
-        res = solve_step(eng, args.vcov)
+    for _ in range(a.steps):
+        res = solve_step(eng, a.vcov, n_cl)
     device_sync(eng)
     t1 = time.perf_counter()
     d.barrier()
@@ -169,55 +352,79 @@ def main():
     kstats = eng.kernel_stats()
     eng.profile(False)
 
-    total_rows = args.rows * d.world
-    value = total_rows * args.steps / elapsed / 1e6
-    p = args.k + 1
-    F = len(levels)
-    T = res["iterations"]
-    ab = algorithmic_bytes(args.rows, p, F, T, args.vcov.lower() == "hc1")
-    # dominant kernel = most device time in the timed region
+    total_rows = geo["total"]
+    value = total_rows * a.steps / elapsed / 1e6
+    ms_step = elapsed / a.steps * 1e3
+    p, F = a.k + 1, len(a.levels)
+    ab = algorithmic_bytes(geo["local"], p, F)
+    # dominant kernel = most device time in the timed region (rank 0's shard)
     dom = max(kstats.items(), key=lambda kv: kv[1][0]) if kstats else ("none", (0.0, 1))
     dom_name, (dom_ms, dom_launches) = dom
     per_launch_s = dom_ms / 1e3 / max(dom_launches, 1)
-    dom_bytes = ab.get(dom_name)
     roofline = None
-    if dom_bytes:
-        achieved = dom_bytes / per_launch_s / 1e9
+    if ab.get(dom_name):
+        achieved = ab[dom_name] / per_launch_s / 1e9
+        traffic, tsrc = pmc_traffic(dom_name, a)
         roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-                    "traffic": pmc_traffic(dom_name, args, levels),
-                    "bytes_per_launch": dom_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4)}
-        if roofline["traffic"] is not None:
-            roofline["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) + " (rocprofv3 PMC, same config)"
-    cpu = None
-    if d.rank == 0 and d.world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, levels, eng)
+                    "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                    "bytes_per_launch": ab[dom_name], "avg_launch_ms": round(per_launch_s * 1e3, 4)}
+        if tsrc:
+            roofline["traffic_source"] = tsrc + " (rocprofv3 PMC, same config)"
+    # step-level roofline: every modelled kernel's algorithmic bytes x its launches per step,
+    # over the measured wall time per step (rank 0's shard; all ranks move the same amount)
+    step_bytes = sum(ab[k] * v[1] / a.steps for k, v in kstats.items() if k in ab)
+    if roofline is not None and step_bytes:
+        ach = step_bytes / (ms_step / 1e3) / 1e9
+        kern_ms = sum(v[0] for v in kstats.values()) / a.steps
+        roofline["step"] = {"bytes": int(step_bytes), "achieved": round(ach, 1), "frac": round(ach / PEAK_HBM_GBS, 4),
+                            "kernel_ms": round(kern_ms, 4), "host_gap_ms": round(ms_step - kern_ms, 4),
+                            "model": "sum over kernels of DESIGN.md §4 bytes/row x rows x launches per step"}
+
+    extra = {}
+    if d.rank == 0 and d.world == 1 and (not a.no_cpu or not a.no_h2d):
+        cols, codes = eng.copy_inputs()
+        if not a.no_cpu:
+            extra["cpu_baseline"] = cpu_baseline(a, cols, codes)
+        if not a.no_h2d:
+            # PCIe-inclusive load of the same shard from pageable host memory (never `value`)
+            t0 = time.perf_counter()
+            eng.load(list(cols), list(codes), a.levels)
+            eng.sync()
+            h2d = time.perf_counter() - t0
+            nbytes = cols.nbytes + codes.nbytes
+            extra["h2d"] = {"seconds": round(h2d, 4), "GBps": round(nbytes / h2d / 1e9, 2), "bytes": int(nbytes),
+                            "source": "pageable NumPy columns -> lfe_load (H2D + code validation)"}
+        del cols, codes
     if d.rank == 0:
+        headline = is_headline(a)
         line = {
-            "metric": "Mrows/sec demean+solve, 50M x 2-HDFE (1e5/1e3 levels), k=10, HC1",
+            "metric": BASELINE_METRIC if headline else f"Mrows/sec demean+solve, {workload_label(a, d.world)}",
             "value": round(value, 2),
             "unit": "Mrows/s",
             "n_gpus": d.world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (counter-based splitmix64 panel generated on device, seed 12345)",
-            "config": {"workload": "configs[2]: 50M rows/GPU, 2 FE (1e5, 1e3 levels), k=10, HC1 SE",
-                       "rows_per_gpu": args.rows, "total_rows": total_rows, "k": args.k, "levels": levels,
-                       "vcov": args.vcov, "iterations": T, "parallelism": f"row-shard dp{d.world}"},
+            "data": f"synthetic (counter-based splitmix64 panel generated on device, seed {a.seed})",
+            "config": {"workload": workload_label(a, d.world), "rows_total": total_rows,
+                       "rows_rank0": geo["local"], "k": a.k, "levels": a.levels, "vcov": a.vcov,
+                       "cluster_fes": a.cl, "iterations": res["iterations"],
+                       "parallelism": f"dp{d.world} ({shard}-sharded rows, RCCL inside the engine)"},
             "roofline": roofline,
-            "cpu_baseline": cpu,
-            "kernels_ms": {k: [round(v[0] / args.steps, 4), v[1] // args.steps] for k, v in kstats.items()},
+            "cpu_baseline": extra.get("cpu_baseline"),
+            "h2d": extra.get("h2d"),
+            "kernels_ms": {k: [round(v[0] / a.steps, 4), v[1] // a.steps] for k, v in kstats.items()},
             "gen_s": round(gen_s, 3),
+            "beta_dev_vs_host": res["beta_dev_vs_host"],
         }
-        if args.verbose:
+        if a.verbose:
             line["beta"] = [float(x) for x in res["beta"]]
             line["se"] = [float(x) for x in res["se"]]
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     eng.close()
     d.close()
 

@@ -84,6 +84,21 @@ int lfe_load_finish(lfe_ctx* ctx);
 int lfe_synth_load(lfe_ctx* ctx, int64_t n, int k, int n_fe, const int32_t* n_levels,
                    const double* beta, uint64_t seed, int64_t row_offset);
 
+/* Owner-sharded rows (multi-GPU, SURVEY.md §8e "balanced by fe1 segment"): declare that
+ * this rank holds EVERY row whose code of FE `fe` lies in [lo, hi) and no other row
+ * (validated against the loaded codes; LFE_EINVAL otherwise).  When `fe` is the primary
+ * FE (most levels) of a two-FE unweighted fit, the engine keeps that FE's counts, group
+ * sums S and cross term T rank-local (no all-reduce of the G x p tables of
+ * polars_impl.py:491-508's largest FE) and all-reduces only the other FE's tables, the
+ * Gram and the SE statistics.  fe = -1 clears it; every lfe_load* clears it. */
+int lfe_ctx_set_owner(lfe_ctx* ctx, int fe, int32_t lo, int32_t hi);
+
+/* The rows of the synthetic panel's rows [0, n_total) whose code of FE `owner_fe` lies in
+ * [lo, hi), generated on the device in increasing row order (the same rows and values as
+ * lfe_synth_load over the whole panel), then lfe_ctx_set_owner(ctx, owner_fe, lo, hi). */
+int lfe_synth_load_owned(lfe_ctx* ctx, int64_t n_total, int k, int n_fe, const int32_t* n_levels,
+                         const double* beta, uint64_t seed, int owner_fe, int32_t lo, int32_t hi);
+
 /* Cluster code arrays for SEs, in the same row order as lfe_load (dense int32
  * codes, n_levels[j] each).  Subsets/intersections are passed as separate
  * arrays (std_errors.py:396-408). */
@@ -195,6 +210,9 @@ int lfe_copy_inputs(lfe_ctx* ctx, double* const* cols_out, int32_t* const* codes
 
 /* Wait for all work queued on the context's stream. */
 int lfe_sync(lfe_ctx* ctx);
+
+/* Rows of the loaded shard (input rows, before the singleton drop). */
+int lfe_shard_rows(lfe_ctx* ctx, int64_t* n_out);
 
 /* Per-phase device times (ms) of the last lfe_* calls, measured with HIP
  * events on the context's stream: [prep, demean, gram, resid, cluster, last_kernel]. */

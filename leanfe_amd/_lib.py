@@ -37,6 +37,9 @@ SIGNATURES = {
     "lfe_load_rows": (C.c_int, [_vp, C.c_int64, C.c_int64, C.POINTER(_vp), C.POINTER(_vp), _vp]),
     "lfe_load_finish": (C.c_int, [_vp]),
     "lfe_synth_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, _dp, C.c_uint64, C.c_int64]),
+    "lfe_ctx_set_owner": (C.c_int, [_vp, C.c_int, C.c_int32, C.c_int32]),
+    "lfe_synth_load_owned": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, _dp, C.c_uint64, C.c_int,
+                                       C.c_int32, C.c_int32]),
     "lfe_load_clusters": (C.c_int, [_vp, C.c_int, C.POINTER(_vp), _i32p, C.c_int]),
     "lfe_drop_singletons": (C.c_int, [_vp, _i64p, _i32p, _i32p]),
     "lfe_demean": (C.c_int, [_vp, _i32p, C.c_double, C.c_int, C.c_int, _i32p, _dp]),
@@ -52,6 +55,7 @@ SIGNATURES = {
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_sync": (C.c_int, [_vp]),
+    "lfe_shard_rows": (C.c_int, [_vp, _i64p]),
     "lfe_timings": (C.c_int, [_vp, _dp]),
     "lfe_profile": (C.c_int, [_vp, C.c_int]),
     "lfe_kernel_stats": (C.c_int, [_vp, C.c_int, C.c_char_p, _dp, _i64p, _i32p]),
@@ -201,6 +205,33 @@ class Engine:
         _check(self._lib.lfe_synth_load(self._h, int(n), int(k), len(levels), lv,
                                         b.ctypes.data_as(_dp), C.c_uint64(seed), int(row_offset)))
         self.p, self.F, self.n = k + 1, len(levels), int(n)
+
+    def synth_load_owned(self, n_total: int, k: int, levels: list[int], beta: np.ndarray, owner_fe: int, lo: int,
+                         hi: int, seed: int = 12345) -> None:
+        """The rows of the synthetic panel [0, n_total) whose code of FE ``owner_fe`` lies in
+        [lo, hi), in row order, and owner sharding declared for them (lfe_synth_load_owned)."""
+        lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
+        b = np.ascontiguousarray(beta, dtype=np.float64)
+        if b.size < max(k, 1):
+            b = np.concatenate([b, np.zeros(max(k, 1) - b.size)])
+        _check(self._lib.lfe_synth_load_owned(self._h, int(n_total), int(k), len(levels), lv,
+                                              b.ctypes.data_as(_dp), C.c_uint64(seed), int(owner_fe), int(lo),
+                                              int(hi)))
+        self.p, self.F = k + 1, len(levels)
+        # shard size: copy_inputs needs it; read it back through a zero-cost query
+        self.n = self._shard_rows()
+        self.owner = (int(owner_fe), int(lo), int(hi))
+
+    def set_owner(self, fe: int | None, lo: int = 0, hi: int = 0) -> None:
+        """Declare that this rank holds every row whose code of FE ``fe`` lies in [lo, hi)
+        (lfe_ctx_set_owner; None clears it)."""
+        _check(self._lib.lfe_ctx_set_owner(self._h, -1 if fe is None else int(fe), int(lo), int(hi)))
+        self.owner = None if fe is None else (int(fe), int(lo), int(hi))
+
+    def _shard_rows(self) -> int:
+        n = C.c_int64()
+        _check(self._lib.lfe_shard_rows(self._h, C.byref(n)))
+        return int(n.value)
 
     def load_clusters(self, codes: list[np.ndarray], levels: list[int]) -> None:
         codes = [np.ascontiguousarray(c, dtype=np.int32) for c in codes]

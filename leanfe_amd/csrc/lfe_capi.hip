@@ -305,7 +305,8 @@ int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count) {
 const char* const kKernelNames[K_NUM_KERNELS] = {
     "part_hist", "scan", "part_scatter", "count", "mark", "group_sums", "cross", "check", "finalize",
     "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth",
-    "tp", "tq", "seg_build", "cluster_sort", "gram_tables"};
+    "tp", "tq", "seg_build", "cluster_sort", "gram_tables", "layout_hist", "layout_base", "layout_scatter",
+    "tq_reduce"};
 
 static hipEvent_t prof_event(lfe_ctx* c) {
   if (!c->prof.pool.empty()) {
@@ -400,6 +401,10 @@ static void free_data(lfe_ctx* c) {
   c->rows_in = 0;
   c->loading = false;
   c->L = Layout();
+  dfree(c->tq_runs);
+  c->tq_runs_cap = 0;
+  c->owner_fe = -1;
+  c->owner_on = false;
   c->loaded = c->prepared = c->demeaned = c->scores_valid = c->seg_ready = false;
   c->n = c->ld = 0;
   c->p = c->F = 0;
@@ -691,6 +696,45 @@ int lfe_synth_load(lfe_ctx* c, int64_t n, int k, int n_fe, const int32_t* n_leve
   return LFE_OK;
 }
 
+int lfe_ctx_set_owner(lfe_ctx* c, int fe, int32_t lo, int32_t hi) {
+  LFE_CTX(c);
+  if (fe < 0) {
+    c->owner_fe = -1;
+    c->prepared = false;
+    return LFE_OK;
+  }
+  if (!c->loaded) return fail(LFE_ESTATE, "load the shard before lfe_ctx_set_owner");
+  if (fe >= c->F || lo < 0 || hi < lo || hi > c->fe[fe].G) return fail(LFE_EINVAL, "bad owner FE / level range");
+  if (c->n == 0) return fail(LFE_EINVAL, "owner sharding needs at least one row on every rank");
+  LFE_TRY(ensure_iscratch(c, 16));
+  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
+  LFE_TRY(launch_validate_range(c->fe[fe].code, c->n, lo, hi, c->iscratch, c->stream));
+  int32_t bad = 0;
+  LFE_HIP(hipMemcpyAsync(&bad, c->iscratch, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  if (bad) return fail(LFE_EINVAL, "owner sharding: a row's owner-FE code lies outside [lo, hi)");
+  c->owner_fe = fe;
+  c->owner_lo = lo;
+  c->owner_hi = hi;
+  c->prepared = false;  // the layout decides again which tables stay rank-local
+  return LFE_OK;
+}
+
+int lfe_synth_load_owned(lfe_ctx* c, int64_t n_total, int k, int n_fe, const int32_t* n_levels, const double* beta,
+                         uint64_t seed, int owner_fe, int32_t lo, int32_t hi) {
+  LFE_CTX(c);
+  if (k < 0 || k + 1 > kMaxCols) return fail(LFE_EINVAL, "k out of range");
+  if (n_fe < 1 || !n_levels || owner_fe < 0 || owner_fe >= n_fe) return fail(LFE_EINVAL, "bad owner FE");
+  if (n_total < 0 || lo < 0 || hi < lo || hi > n_levels[owner_fe]) return fail(LFE_EINVAL, "bad owner level range");
+  std::vector<int64_t> base;
+  int64_t n_local = 0;
+  LFE_TRY(synth_count_owned(c, n_total, owner_fe, n_levels[owner_fe], lo, hi, seed, base, &n_local));
+  LFE_TRY(alloc_data(c, n_local, k + 1, n_fe, n_levels, false));
+  LFE_TRY(launch_synth_owned(c, n_total, k, n_levels, beta, seed, owner_fe, lo, hi, base));
+  c->loaded = true;
+  return lfe_ctx_set_owner(c, owner_fe, lo, hi);
+}
+
 int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const int32_t* cl_levels, int where) {
   LFE_CTX(c);
   if (!c->loaded) return fail(LFE_ESTATE, "lfe_load must precede lfe_load_clusters");
@@ -755,6 +799,8 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
   {
     PhaseTimer t(c, PH_DEMEAN);
     const bool fast = c->F > 0 && check_from > 0 && fast_path_ok(c, order);
+    if (c->owner_on && !fast)
+      return fail(LFE_EINVAL, "owner-sharded rows need the two-FE sweeps with the primary FE projected last");
     if (!fast)  // the two-FE sweeps write every alpha entry before reading any
       for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
     if (c->F > 0) {
@@ -854,6 +900,12 @@ int lfe_copy_inputs(lfe_ctx* c, double* const* cols_out, int32_t* const* codes_o
   for (int f = 0; f < c->F && c->n > 0 && codes_out; ++f)
     LFE_HIP(hipMemcpyAsync(codes_out[f], c->fe[f].code, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
   LFE_HIP(hipStreamSynchronize(c->stream));
+  return LFE_OK;
+}
+
+int lfe_shard_rows(lfe_ctx* c, int64_t* n_out) {
+  if (!c || !n_out) return fail(LFE_EINVAL, "null pointer");
+  *n_out = c->loaded ? c->n : 0;
   return LFE_OK;
 }
 

@@ -447,7 +447,8 @@ int sums4(lfe_ctx* c) {
     }
     c->raw_ready = true;
   }
-  for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_f64(c, c->fe[f].S, (size_t)c->fe[f].G * p));
+  for (int f = 0; f < c->F; ++f)  // owner-sharded rows: the primary FE's sums are complete on each rank
+    if (!(c->owner_on && f == P)) LFE_TRY(allreduce_sum_f64(c, c->fe[f].S, (size_t)c->fe[f].G * p));
   return LFE_OK;
 }
 

@@ -688,10 +688,11 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const double* __restric
   if (threadIdx.x == 0) out[e] = red[0];
 }
 
-__global__ void k_validate(const int32_t* __restrict__ code, int64_t n, int32_t G, int32_t* __restrict__ flag) {
+__global__ void k_validate(const int32_t* __restrict__ code, int64_t n, int32_t lo, int32_t hi,
+                           int32_t* __restrict__ flag) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t g = code[i];
-    if (g < 0 || g >= G) atomicOr(flag, 1);
+    if (g < lo || g >= hi) atomicOr(flag, 1);
   }
 }
 
@@ -714,8 +715,12 @@ __global__ void k_copy_demeaned(LayoutArgs la, const double* __restrict__ X, int
 // ===========================================================================
 
 int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* flag, hipStream_t s) {
+  return launch_validate_range(code, n, 0, G, flag, s);
+}
+
+int launch_validate_range(const int32_t* code, int64_t n, int32_t lo, int32_t hi, int32_t* flag, hipStream_t s) {
   if (n == 0) return LFE_OK;
-  hipLaunchKernelGGL(k_validate, dim3(grid_for(n)), dim3(kBlock), 0, s, code, n, G, flag);
+  hipLaunchKernelGGL(k_validate, dim3(grid_for(n)), dim3(kBlock), 0, s, code, n, lo, hi, flag);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
 }
@@ -924,6 +929,7 @@ struct TabArgs {
   int G[2];
   int p;
   const double* shift;     // [16] the raw tile's shift c
+  int q_on;                // 0: skip the secondary groups (owner-sharded ranks other than 0)
 };
 
 template <int PM>
@@ -938,7 +944,7 @@ __global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restri
   double acc[NA];
 #pragma unroll
   for (int e = 0; e < NA; ++e) acc[e] = 0.0;
-  const int total = t.G[0] + t.G[1];
+  const int total = t.G[0] + (t.q_on ? t.G[1] : 0);
   for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
     const int f = g < t.G[0] ? 0 : 1;
     const int gg = f ? g - t.G[0] : g;
@@ -1034,27 +1040,40 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev) {
   t.G[1] = c->fe[Q].G;
   t.p = p;
   t.shift = c->raw_shift;
+  // owner-sharded rows: each rank's primary groups are its own (partial sums over ranks), the
+  // secondary tables are global (counted on rank 0 only); the sums are all-reduced before the
+  // final tile.  Otherwise every rank holds the same global tables.
+  t.q_on = (!c->owner_on || c->rank == 0) ? 1 : 0;
   const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
   const int NA = PM * (PM + 1) / 2 + PM;
   const int nblk = grid_for((int64_t)t.G[0] + t.G[1], 256, 64);  // few partials: the final sum is serial
-  LFE_TRY(ensure_scratch(c, (size_t)nblk * NA));
+  LFE_TRY(ensure_scratch(c, (size_t)nblk * NA + NA));
   ProfScope _ps(c, K_GRAM_TABLES);
   double* part = c->scratch;
+  double* msum = c->scratch + (size_t)nblk * NA;
+  auto final_from = [&](auto kfinal) -> int {
+    if (!c->owner_on) {
+      hipLaunchKernelGGL(kfinal, dim3(1), dim3(256), 0, c->stream, part, nblk, c->raw_tile, p, out_dev, flag_dev);
+      return LFE_OK;
+    }
+    hipLaunchKernelGGL(k_reduce_partials, dim3(NA), dim3(256), 0, c->stream, part, nblk, (int64_t)NA, msum);
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(allreduce_sum_f64(c, msum, (size_t)NA));
+    hipLaunchKernelGGL(kfinal, dim3(1), dim3(256), 0, c->stream, msum, 1, c->raw_tile, p, out_dev, flag_dev);
+    return LFE_OK;
+  };
   switch (PM) {
     case 4:
       hipLaunchKernelGGL(k_tables_gram<4>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      hipLaunchKernelGGL(k_tables_final<4>, dim3(1), dim3(256), 0, c->stream, part, nblk, c->raw_tile, p, out_dev,
-                         flag_dev);
+      LFE_TRY(final_from(k_tables_final<4>));
       break;
     case 8:
       hipLaunchKernelGGL(k_tables_gram<8>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      hipLaunchKernelGGL(k_tables_final<8>, dim3(1), dim3(256), 0, c->stream, part, nblk, c->raw_tile, p, out_dev,
-                         flag_dev);
+      LFE_TRY(final_from(k_tables_final<8>));
       break;
     default:
       hipLaunchKernelGGL(k_tables_gram<12>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      hipLaunchKernelGGL(k_tables_final<12>, dim3(1), dim3(256), 0, c->stream, part, nblk, c->raw_tile, p, out_dev,
-                         flag_dev);
+      LFE_TRY(final_from(k_tables_final<12>));
       break;
   }
   LFE_HIP(hipGetLastError());

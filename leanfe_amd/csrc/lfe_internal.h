@@ -74,7 +74,8 @@ struct FeState {
 enum KernelId {
   K_PART_HIST = 0, K_SCAN, K_PART_SCATTER, K_COUNT, K_MARK, K_GROUP_SUMS, K_CROSS, K_CHECK, K_FINALIZE,
   K_CHECK_MAX, K_GRAM_DESIGN, K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_MISC, K_SYNTH,
-  K_TP, K_TQ, K_SEG_BUILD, K_CLUSTER_SORT, K_GRAM_TABLES, K_NUM_KERNELS
+  K_TP, K_TQ, K_SEG_BUILD, K_CLUSTER_SORT, K_GRAM_TABLES, K_LAYOUT_HIST, K_LAYOUT_BASE, K_LAYOUT_SCATTER,
+  K_TQ_REDUCE, K_NUM_KERNELS
 };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 
@@ -259,6 +260,14 @@ struct lfe_ctx {
   ncclComm_t comm = nullptr;
   struct lfe_emu* emu = nullptr;
   int rank = 0, world = 1;
+  // owner-sharded rows (lfe_ctx_set_owner): this rank holds every row whose code of FE owner_fe
+  // lies in [owner_lo, owner_hi); owner_on (prepare_layout): the primary FE's tables stay local
+  int owner_fe = -1;
+  int32_t owner_lo = 0, owner_hi = 0;
+  bool owner_on = false;
+  // deterministic T_Q: per-(bucket, q) run sums reduced in bucket order (no cross-bucket atomics)
+  double* tq_runs = nullptr;     // [nb * G_Q][p]
+  size_t tq_runs_cap = 0;
   lfe::Timings tm;
   lfe::Prof prof;
 };
@@ -309,6 +318,14 @@ int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* fl
 // --- synthetic panel (lfe_synth.hip) ---
 int launch_synth(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed,
                  int64_t row_offset);
+// owner-sharded synthetic shard: count the rows of [0, n_total) whose code of FE f is in [lo, hi)
+// (per-chunk bases, *n_local), then (after alloc_data(n_local)) generate them in row order
+int synth_count_owned(lfe_ctx* c, int64_t n_total, int f, int32_t L, int32_t lo, int32_t hi, uint64_t seed,
+                      std::vector<int64_t>& base, int64_t* n_local);
+int launch_synth_owned(lfe_ctx* c, int64_t n_total, int k, const int32_t* levels, const double* beta, uint64_t seed,
+                       int f, int32_t lo, int32_t hi, const std::vector<int64_t>& base);
+// flag (atomic max into *flag) any code outside [lo, hi)
+int launch_validate_range(const int32_t* code, int64_t n, int32_t lo, int32_t hi, int32_t* flag, hipStream_t s);
 
 // --- helpers (lfe_capi.hip) ---
 int ensure_scratch(lfe_ctx* c, size_t elems);

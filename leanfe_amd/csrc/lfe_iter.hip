@@ -437,7 +437,7 @@ static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off,
   LFE_TRY(ensure_i32(c, off, off_cap, m + 1));
   const int4* items = reinterpret_cast<const int4*>(c->items_d);
   {
-    ProfScope _ps(c, K_MISC);
+    ProfScope _ps(c, K_LAYOUT_BASE);
     hipLaunchKernelGGL(k_ls_base, dim3(grid_for((int64_t)m + 1)), dim3(kBlock), 0, c->stream, c->bitems_d, L.nb, K,
                        itemcnt, off);
   }
@@ -451,7 +451,7 @@ static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off,
                              : reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, NCUR, 8>);
   if (lds > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   {
-    ProfScope _ps(c, K_MISC);
+    ProfScope _ps(c, K_LAYOUT_SCATTER);
     if (per == 16)
       hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR, 16>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream,
                          items, L.code[P], L.code[Q], L.s, K, off, itemcnt, c->xitems_d, out);
@@ -471,7 +471,7 @@ int layout_hists(lfe_ctx* c, int Q) {
   const int32_t G_Q = c->fe[Q].G;
   const size_t n1 = (size_t)L.n_items * B;
   LFE_TRY(ensure_i32(c, c->seg_aux, c->seg_aux_cap, n1 + (size_t)L.n_items * G_Q));
-  ProfScope _ps(c, K_MISC);
+  ProfScope _ps(c, K_LAYOUT_HIST);
   hipLaunchKernelGGL(k_ls_hist2, dim3(L.n_items), dim3(256), sizeof(int32_t) * ((size_t)B + G_Q), c->stream,
                      reinterpret_cast<const int4*>(c->items_d), L.code[L.P], L.code[Q], L.s, B, (int)G_Q, c->seg_aux,
                      c->seg_aux + n1);
@@ -518,7 +518,7 @@ static int build_layouts(lfe_ctx* c, int Q) {
                                : reinterpret_cast<const void*>(&k_ls_scatter2<8>);
     if (lds2 > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
     {
-      ProfScope _ps(c, K_MISC);
+      ProfScope _ps(c, K_LAYOUT_SCATTER);
       void* args[] = {&a};
       LFE_HIP(hipLaunchKernel(fn, dim3(c->n_xgrid), dim3(kLsThreads), args, lds2, c->stream));
     }
@@ -772,11 +772,13 @@ struct TqArgs {
   const uint16_t* run_h;   // primary code - lo of each kept row, run order
   int nb, s, G_Q, G_P, p;
   const double* alphaP;  // [G_P][p]
-  double* T_Q;           // [G_Q][p], accumulated
+  double* runs;          // [nb * G_Q][p]: the sum of every (bucket, q) run (empty runs: 0)
   int split;             // workgroups per bucket (each takes 1 / split of the bucket's runs)
 };
 
-// K2: T_Q[q] += sum over the (bucket, q) runs of alpha_P[h_i]
+// K2: runs[b][q] = sum over the (bucket b, q) run of alpha_P[h_i].  Every run is summed by one
+// wave in row order and every slot is written, so T_Q[q] = sum_b runs[b][q] (k_tq_reduce, in
+// bucket order) is bit-reproducible: no cross-workgroup atomics.
 template <int NT>
 __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
   constexpr int kTqThreads = tq_threads<NT>();
@@ -807,24 +809,25 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
     const int q1 = (slot + 1) * G_Q / (NW * kTqSplit);
     if (q >= q1) continue;
     const int32_t* off = a.run_off + (int64_t)b * G_Q;
+    double* const runs = a.runs + (int64_t)b * G_Q * p;
     int r0 = off[q], r1 = off[q + 1];
     const int g0 = r0 >> 4, g1 = (off[q1] + 15) >> 4;
-    if (g0 >= g1) continue;
+    if (g0 >= g1) {  // no rows in these runs
+      for (int j = lane; j < (q1 - q) * p; j += 64) runs[(int64_t)q * p + j] = 0.0;
+      continue;
+    }
     double acc[NT];
 #pragma unroll
     for (int I = 0; I < NT; ++I) acc[I] = 0.0;
     typedef unsigned short us4 __attribute__((ext_vector_type(4)));
-    auto finalize = [&]() {  // run q complete
-      if (r1 > r0) {
+    auto finalize = [&]() {  // run q complete (an empty run stores 0)
 #pragma unroll
-        for (int I = 0; I < NT; ++I) {
-          const double t = quad_sum(acc[I]);
-          const int col = 16 * I + c;
-          if (kq == 0 && col < p) atomicAdd(&a.T_Q[(int64_t)q * p + col], t);
-        }
+      for (int I = 0; I < NT; ++I) {
+        const double t = quad_sum(acc[I]);
+        const int col = 16 * I + c;
+        if (kq == 0 && col < p) runs[(int64_t)q * p + col] = t;
+        acc[I] = 0.0;
       }
-#pragma unroll
-      for (int I = 0; I < NT; ++I) acc[I] = 0.0;
     };
     bool done = false;
     auto group = [&](int g, const us4& h4) {
@@ -912,6 +915,21 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
       batch(vb, gb);
       gb += kBatch;
     }
+  }
+}
+
+// T_Q[q][col] = sum over buckets b (in order) of runs[b][q][col]
+__global__ void k_tq_reduce(const double* __restrict__ runs, int nb, int64_t m, double* __restrict__ T) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+    double t = 0.0;
+    int b = 0;
+    for (; b + 4 <= nb; b += 4) {  // four loads in flight, added in bucket order
+      const double v0 = runs[(int64_t)b * m + e], v1 = runs[(int64_t)(b + 1) * m + e];
+      const double v2 = runs[(int64_t)(b + 2) * m + e], v3 = runs[(int64_t)(b + 3) * m + e];
+      t = (((t + v0) + v1) + v2) + v3;
+    }
+    for (; b < nb; ++b) t += runs[(int64_t)b * m + e];
+    T[e] = t;
   }
 }
 
@@ -1003,7 +1021,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   tp.p = p;
   tp.S_P = fp.S;
   tp.cntP = fp.cnt;
-  tp.fused = c->world == 1;
+  tp.fused = c->world == 1 || c->owner_on;  // owner-sharded: T_P is complete on each rank
   tp.out = tp.fused ? fp.alpha : fp.T;
   TqArgs tq{};
   tq.run_off = c->run_off;
@@ -1014,7 +1032,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   tq.G_P = fp.G;
   tq.p = p;
   tq.alphaP = fp.alpha;
-  tq.T_Q = fq.T;
+  LFE_TRY(ensure_f64(c, c->tq_runs, c->tq_runs_cap, (size_t)c->L.nb * fq.G * p));
+  tq.runs = c->tq_runs;
   static const int split_env = [] {
     const char* e = getenv("LFE_TQ_SPLIT");  // tuning
     return e ? atoi(e) : 0;
@@ -1030,8 +1049,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   double last = -1.0;
   for (int it = 1; it <= max_iter; ++it) {
     tp.alphaQ = fq.alpha;
-    tp.zeroT = fq.T;
-    tp.zero_n = (int64_t)fq.G * p;
+    tp.zeroT = nullptr;  // K2 writes every run slot; k_tq_reduce writes T_Q
+    tp.zero_n = 0;
     tp.zero_check = it >= check_from ? c->dred : nullptr;
     // T_P partials: segments with no local rows are not written by K1
     if (!tp.fused) LFE_HIP(hipMemsetAsync(fp.T, 0, sizeof(double) * (size_t)fp.G * p, c->stream));
@@ -1049,7 +1068,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       LFE_TRY(allreduce_sum_f64(c, fp.T, (size_t)fp.G * p));
       LFE_TRY(fin_check(c, P, fp.T, nullptr, fp.alpha, false));
     }
-    {  // fq.T (and the check's max) were zeroed by K1
+    {  // the check's max was zeroed by K1
       ProfScope _ps(c, K_TQ);
       switch (NT) {
         case 1: launch_tq<1>(c, tq, lds_tq); break;
@@ -1057,6 +1076,12 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
         case 3: launch_tq<3>(c, tq, lds_tq); break;
         default: launch_tq<4>(c, tq, lds_tq); break;
       }
+    }
+    LFE_HIP(hipGetLastError());
+    {
+      ProfScope _ps(c, K_TQ_REDUCE);
+      const int64_t m = (int64_t)fq.G * p;
+      hipLaunchKernelGGL(k_tq_reduce, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, c->tq_runs, c->L.nb, m, fq.T);
     }
     LFE_HIP(hipGetLastError());
     LFE_TRY(allreduce_sum_f64(c, fq.T, (size_t)fq.G * p));

@@ -695,6 +695,10 @@ int prepare_layout(lfe_ctx* c) {
   c->hists_kept = false;
   L.w = c->w;  // fast_layout_ok reads it before the layout pointers are set below
   const bool item_counts = L.permuted && fast_layout_ok(c);
+  // owner-sharded rows: every row of the primary FE's groups [owner_lo, owner_hi) is on this rank,
+  // so its counts, drops, group sums and cross term are complete without an all-reduce (the
+  // two-FE sweeps; lfe_demean refuses the general sweeps in this mode)
+  c->owner_on = c->world > 1 && c->owner_fe >= 0 && c->owner_fe == L.P && item_counts;
   // every count / drop / group-sum table and the scratch counters zeroed in one launch
   LFE_TRY(ensure_iscratch(c, 2 * kMaxFE + 8));
   {
@@ -826,7 +830,8 @@ int prepare_layout(lfe_ctx* c) {
                        reinterpret_cast<const int4*>(c->items_d), L.code[L.P], L.s, fe.G, fe.cnt_pre);
     LFE_HIP(hipGetLastError());
   }
-  for (int f = 0; f < c->F; ++f) LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt_pre, c->fe[f].G));
+  for (int f = 0; f < c->F; ++f)
+    if (!(c->owner_on && f == L.P)) LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt_pre, c->fe[f].G));
 
   // ---- single-pass singleton drop: mark, then kept counts = pre - drops ----
   int32_t* ndropped = c->iscratch + 2 * kMaxFE;
@@ -867,7 +872,7 @@ int prepare_layout(lfe_ctx* c) {
     FinishCountsArgs fa{};
     for (int f = 0; f < c->F; ++f) {
       auto& fe = c->fe[f];
-      LFE_TRY(allreduce_sum_i32(c, fe.drops, fe.G));
+      if (!(c->owner_on && f == L.P)) LFE_TRY(allreduce_sum_i32(c, fe.drops, fe.G));
       fa.pre[f] = fe.cnt_pre;
       fa.drops[f] = fe.drops;
       fa.cnt[f] = fe.cnt;
@@ -894,15 +899,25 @@ int prepare_layout(lfe_ctx* c) {
     c->fe[f].card = h[2 * f + 1];
   }
   c->hists_kept = item_counts && h[2 * kMaxFE] == 0;
-  // kept rows over all ranks
-  double kept = (double)(n - h[2 * kMaxFE]);
-  if (c->world > 1) {
-    LFE_TRY(ensure_dred(c, 1));
-    LFE_TRY(h2d_small(c, c->dred, &kept, sizeof(double)));
-    LFE_TRY(allreduce_sum_f64(c, c->dred, 1));
-    LFE_TRY(d2h_sync(c, &kept, c->dred, sizeof(double)));
+  // kept rows over all ranks (owner-sharded: with the primary FE's level counts, which each
+  // rank has for its own levels only; integers < 2^53 are exact in f64)
+  double kept[3] = {(double)(n - h[2 * kMaxFE]), 0.0, 0.0};
+  if (c->owner_on) {
+    kept[1] = c->fe[L.P].dims;
+    kept[2] = c->fe[L.P].card;
   }
-  c->n_kept = (int64_t)kept;
+  if (c->world > 1) {
+    const int nv = c->owner_on ? 3 : 1;
+    LFE_TRY(ensure_dred(c, 3));
+    LFE_TRY(h2d_small(c, c->dred, kept, sizeof(double) * nv));
+    LFE_TRY(allreduce_sum_f64(c, c->dred, nv));
+    LFE_TRY(d2h_sync(c, kept, c->dred, sizeof(double) * nv));
+  }
+  if (c->owner_on) {
+    c->fe[L.P].dims = (int32_t)kept[1];
+    c->fe[L.P].card = (int32_t)kept[2];
+  }
+  c->n_kept = (int64_t)kept[0];
   return LFE_OK;
 }
 

@@ -129,3 +129,77 @@ def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe, owne
                 tuple(ncl) if isinstance(ncl, (tuple, list)) else ncl)
         np.testing.assert_array_equal(res["beta"], out[0]["beta"])  # identical on every rank
         np.testing.assert_array_equal(res["se"], out[0]["se"])
+
+
+def _run_owned(world, n_total, k, levels, vcov, seed):
+    """Owner-sharded ranks: rank r generates every row of the panel whose primary-FE code lies in
+    dist.owner_range(G_P, r, world) (strong scaling: n_total rows in all)."""
+    from leanfe_amd._lib import EmuGroup, Engine
+    from leanfe_amd.dist import owner_range
+
+    group = EmuGroup(world)
+    out, errs = {}, {}
+    P = max(range(len(levels)), key=lambda f: levels[f])
+
+    def worker(rank):
+        try:
+            lo, hi = owner_range(levels[P], rank, world)
+            eng = Engine(0)
+            eng.set_emu(group, rank)
+            eng.synth_load_owned(n_total, k, levels, synth.betas(k), P, lo, hi, seed=seed)
+            _, codes = eng.copy_inputs()
+            assert codes[P].size == eng.n and (codes[P].min() >= lo) and (codes[P].max() < hi)
+            res = _solve(eng, vcov, None)
+            res["rows"] = eng.n
+            out[rank] = res
+            eng.close()
+        except BaseException as e:  # noqa: BLE001
+            errs[rank] = e
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+    if errs:
+        raise next(iter(errs.values()))
+    return out
+
+
+@pytest.mark.parametrize("world,n,k,levels,vcov", [
+    (2, 400_003, 10, (20000, 500), "HC1"),
+    (8, 1_000_000, 10, (40000, 800), "HC1"),    # the 8-GPU strong-scaling split, on one GPU
+    (8, 600_000, 5, (30000, 300), "iid"),
+])
+def test_emulated_owner_sharded_ranks_match_oracle(world, n, k, levels, vcov):
+    from oracle import altproj
+
+    seed = 13
+    out = _run_owned(world, n, k, list(levels), vcov, seed)
+    assert sum(out[r]["rows"] for r in range(world)) == n  # every row on exactly one rank
+    full = synth.panel(n, k, list(levels), seed=seed)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    o = altproj.fit(full, "y", xs, fes, vcov=vcov)
+    for r in range(world):
+        res = out[r]
+        assert res["iterations"] == o["iterations"]
+        assert res["n_obs"] == o["n_obs"] and res["df_resid"] == o["df_resid"]
+        assert res["fe_dims"] == list(o["fe_dims"])
+        np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=0)
+        np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(res["beta"], out[0]["beta"])
+        np.testing.assert_array_equal(res["se"], out[0]["se"])
+
+
+def test_owner_declaration_is_validated():
+    from leanfe_amd._lib import Engine
+
+    eng = Engine(0)
+    eng.synth_load(10_000, 2, [3000, 40], synth.betas(2), seed=3)
+    with pytest.raises(ValueError):
+        eng.set_owner(0, 0, 1500)  # rows with codes >= 1500 are present: not an owner shard
+    eng.set_owner(0, 0, 3000)
+    eng.set_owner(None)
+    eng.close()
