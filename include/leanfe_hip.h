@@ -196,10 +196,12 @@ int lfe_cluster_meat_subsets(lfe_ctx* ctx, int n_subsets, const int32_t* subset_
  * n host codes out, *n_levels_out = number of distinct ids.  Needs no loaded data. */
 int lfe_factorize_ids(lfe_ctx* ctx, int64_t n, const int64_t* ids, int32_t* codes_out, int32_t* n_levels_out);
 
-/* Exact number of distinct rows over the loaded regressors (columns 1..p-1, not y)
- * and FE codes, all loaded rows: the numerator of estimate_compression_ratio
- * (compress.py:187-253).  -0.0 == 0.0 and NaNs compare equal.  One process only. */
-int lfe_count_distinct_rows(lfe_ctx* ctx, int64_t* n_distinct_out);
+/* Exact number of distinct rows over the regressors x (loaded columns 1..n_x, not y
+ * and not the instruments loaded after x; n_x < 0: every column 1..p-1) and the FE
+ * codes, all loaded rows: the numerator of estimate_compression_ratio, whose key is
+ * x_cols + fe_cols (compress.py:187-253, :249-250).  -0.0 == 0.0 and NaNs compare
+ * equal.  One process only. */
+int lfe_count_distinct_rows(lfe_ctx* ctx, int n_x, int64_t* n_distinct_out);
 
 /* Debug/fixtures: copy the demeaned columns (kept rows, device order) to host. */
 int lfe_copy_demeaned(lfe_ctx* ctx, double* const* cols_out, int64_t* n_out);

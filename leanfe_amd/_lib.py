@@ -50,7 +50,7 @@ SIGNATURES = {
     "lfe_cluster_meat": (C.c_int, [_vp, _dp, _i64p]),
     "lfe_cluster_meat_subsets": (C.c_int, [_vp, C.c_int, _vp, _dp, _i64p]),
     "lfe_factorize_ids": (C.c_int, [_vp, C.c_int64, _vp, _vp, C.POINTER(C.c_int32)]),
-    "lfe_count_distinct_rows": (C.c_int, [_vp, _i64p]),
+    "lfe_count_distinct_rows": (C.c_int, [_vp, C.c_int, _i64p]),
     "lfe_compress": (C.c_int, [_vp, _i64p]),
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
@@ -250,10 +250,11 @@ class Engine:
                                            _ptr(codes) if a.size else None, C.byref(g)))
         return codes, int(g.value)
 
-    def count_distinct_rows(self) -> int:
-        """Distinct (x, FE) rows of the loaded data (estimate_compression_ratio's numerator)."""
+    def count_distinct_rows(self, n_x: int = -1) -> int:
+        """Distinct (x, FE) rows of the loaded data (estimate_compression_ratio's numerator);
+        ``n_x`` regressor columns follow y (instruments after them are not part of the key)."""
         out = C.c_int64()
-        _check(self._lib.lfe_count_distinct_rows(self._h, C.byref(out)))
+        _check(self._lib.lfe_count_distinct_rows(self._h, int(n_x), C.byref(out)))
         return int(out.value)
 
     # -- hot path ----------------------------------------------------------

@@ -471,14 +471,22 @@ struct PhaseTimer {
     LFE_HIP(hipSetDevice((c)->device));                \
   } while (0)
 
+// Runs right after the copies of lfe_load / lfe_load_finish: every return path has waited for
+// the stream, so no copy from the caller's host arrays is still in flight when it returns.
 static int validate_all(lfe_ctx* c) {
-  LFE_TRY(ensure_iscratch(c, 16));
-  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
-  for (int f = 0; f < c->F && c->n > 0; ++f)
-    LFE_TRY(launch_validate_codes(c->fe[f].code, c->n, c->fe[f].G, c->iscratch, c->stream));
   int32_t bad = 0;
-  LFE_HIP(hipMemcpyAsync(&bad, c->iscratch, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  LFE_HIP(hipStreamSynchronize(c->stream));
+  auto run = [&]() -> int {
+    LFE_TRY(ensure_iscratch(c, 16));
+    LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
+    for (int f = 0; f < c->F && c->n > 0; ++f)
+      LFE_TRY(launch_validate_codes(c->fe[f].code, c->n, c->fe[f].G, c->iscratch, c->stream));
+    LFE_HIP(hipMemcpyAsync(&bad, c->iscratch, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    return LFE_OK;
+  };
+  const int rc = run();
+  const hipError_t e = hipStreamSynchronize(c->stream);
+  if (rc != LFE_OK) return rc;
+  if (e != hipSuccess) return fail(LFE_EHIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
   if (bad) {
     free_data(c);
     return fail(LFE_EINVAL, "FE codes must be dense int32 in [0, n_levels)");
@@ -627,11 +635,16 @@ int lfe_load(lfe_ctx* c, int64_t n, int p, const double* const* cols, int F, con
   if (F > 0 && !n_levels) return fail(LFE_EINVAL, "n_levels is null");
   LFE_TRY(alloc_data(c, n, p, F, n_levels, weights != nullptr));
   const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-  for (int j = 0; j < p && n > 0; ++j)
-    LFE_HIP(hipMemcpyAsync(c->X + (size_t)j * c->ld, cols[j], sizeof(double) * n, kind, c->stream));
-  if (weights && n > 0) LFE_HIP(hipMemcpyAsync(c->w, weights, sizeof(double) * n, kind, c->stream));
-  for (int f = 0; f < F && n > 0; ++f)
-    LFE_HIP(hipMemcpyAsync(c->fe[f].code, fe_codes[f], sizeof(int32_t) * n, kind, c->stream));
+  hipError_t e = hipSuccess;
+  for (int j = 0; j < p && n > 0 && e == hipSuccess; ++j)
+    e = hipMemcpyAsync(c->X + (size_t)j * c->ld, cols[j], sizeof(double) * n, kind, c->stream);
+  if (weights && n > 0 && e == hipSuccess) e = hipMemcpyAsync(c->w, weights, sizeof(double) * n, kind, c->stream);
+  for (int f = 0; f < F && n > 0 && e == hipSuccess; ++f)
+    e = hipMemcpyAsync(c->fe[f].code, fe_codes[f], sizeof(int32_t) * n, kind, c->stream);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(c->stream);  // no copy from the caller's arrays outlives the call
+    return fail(LFE_EHIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
+  }
   LFE_TRY(validate_all(c));
   c->loaded = true;
   return LFE_OK;
@@ -740,6 +753,8 @@ int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const i
   if (!c->loaded) return fail(LFE_ESTATE, "lfe_load must precede lfe_load_clusters");
   if (m < 0 || (m > 0 && (!cl_codes || !cl_levels))) return fail(LFE_EINVAL, "bad cluster arrays");
   if (m > 30) return fail(LFE_EINVAL, "at most 30 cluster columns");
+  for (int j = 0; j < m; ++j)  // every argument checked before the first copy is issued
+    if (cl_levels[j] < 1) return fail(LFE_EINVAL, "cluster n_levels must be >= 1");
   for (auto& p : c->cl) dfree(p);
   free_cluster_ws(c);
   c->cl.assign(m, nullptr);
@@ -747,13 +762,20 @@ int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const i
   const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
   LFE_TRY(ensure_iscratch(c, 16));
   LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
-  for (int j = 0; j < m; ++j) {
-    if (cl_levels[j] < 1) return fail(LFE_EINVAL, "cluster n_levels must be >= 1");
-    LFE_TRY(dalloc(&c->cl[j], (size_t)c->ld));
-    if (c->n > 0) {
-      LFE_HIP(hipMemcpyAsync(c->cl[j], cl_codes[j], sizeof(int32_t) * c->n, kind, c->stream));
-      LFE_TRY(launch_validate_codes(c->cl[j], c->n, cl_levels[j], c->iscratch, c->stream));
+  int rc = LFE_OK;
+  for (int j = 0; j < m && rc == LFE_OK; ++j) {
+    rc = dalloc(&c->cl[j], (size_t)c->ld);
+    if (rc == LFE_OK && c->n > 0) {
+      const hipError_t e = hipMemcpyAsync(c->cl[j], cl_codes[j], sizeof(int32_t) * c->n, kind, c->stream);
+      rc = e == hipSuccess ? launch_validate_codes(c->cl[j], c->n, cl_levels[j], c->iscratch, c->stream)
+                           : fail(LFE_EHIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
     }
+  }
+  if (rc != LFE_OK) {
+    // copies from the caller's (pageable) arrays may still be in flight: finish them before
+    // the caller can release those arrays
+    (void)hipStreamSynchronize(c->stream);
+    return rc;
   }
   int32_t bad = 0;
   LFE_HIP(hipMemcpyAsync(&bad, c->iscratch, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));

@@ -5,7 +5,8 @@
 //     result, polars_impl.py:118-139; only group membership does);
 //   - lfe_count_distinct_rows: the exact number of distinct (x, FE) rows,
 //     estimate_compression_ratio's numerator (compress.py:187-253, the
-//     `lf.select(key_cols).unique()` count), over all loaded rows.
+//     `lf.select(key_cols).unique()` count, key_cols = x_cols + fe_cols,
+//     compress.py:249-250), over all loaded rows.
 // Distinct rows: 64-bit row hashes are sorted; equal rows have equal hashes, so a
 // new row starts at every hash change.  Neighbours with equal hashes are compared
 // value by value; if two different rows ever share a hash (about 1e-4 odds per 50M
@@ -313,10 +314,11 @@ int lfe_factorize_ids(lfe_ctx* c, int64_t n, const int64_t* ids, int32_t* codes_
   return LFE_OK;
 }
 
-int lfe_count_distinct_rows(lfe_ctx* c, int64_t* n_distinct_out) {
+int lfe_count_distinct_rows(lfe_ctx* c, int n_x, int64_t* n_distinct_out) {
   if (!c) return fail(LFE_EINVAL, "null context");
   if (!n_distinct_out) return fail(LFE_EINVAL, "null pointer");
   if (!c->loaded) return fail(LFE_ESTATE, "lfe_load first");
+  if (n_x >= c->p) return fail(LFE_EINVAL, "n_x exceeds the loaded regressor columns");
   if (c->world > 1) return fail(LFE_EINVAL, "lfe_count_distinct_rows counts one process's rows only");
   LFE_HIP(hipSetDevice(c->device));
   const int64_t n = c->n;
@@ -330,7 +332,7 @@ int lfe_count_distinct_rows(lfe_ctx* c, int64_t* n_distinct_out) {
   a.X = c->X;
   a.ld = c->ld;
   a.n = n;
-  a.p = c->p;
+  a.p = n_x < 0 ? c->p : 1 + n_x;  // key: x columns 1..n_x (instruments after them are not keyed)
   a.F = c->F;
   for (int f = 0; f < c->F; ++f) a.code[f] = c->fe[f].code;
   const char* hb_env = getenv("LFE_ROW_HASH_BITS");  // tests: a short hash forces collisions

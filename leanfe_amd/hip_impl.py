@@ -129,7 +129,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             # distinct (x, FE) rows / n over all loaded rows, exact (compress.py:187-253), on the
             # GPU; a row shard cannot see the other shards' rows, so sharded fits skip it
             if not sharded and n_initial:
-                est_comp_ratio = eng.count_distinct_rows() / n_initial
+                est_comp_ratio = eng.count_distinct_rows(len(x_cols)) / n_initial
             elif not sharded:
                 est_comp_ratio = 1.0
             if not fe_cols:
@@ -141,6 +141,9 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                 inferred = determine_strategy(vcov, bool(instruments), fe_cardinality, max_fe_levels=MAX_FE_LEVELS,
                                               n_obs=n_initial, n_x_cols=len(x_cols),
                                               estimated_compression_ratio=est_comp_ratio)
+                if sharded and inferred == "compress":
+                    # compress groups one process's rows; a row shard runs the same fit by alt_proj
+                    inferred = "alt_proj"
             say(f"Auto selection: Inferring {inferred} strategy. N = {n_initial:_}, "
                 f"est. compression ratio: {est_comp_ratio}")
             strategy = inferred
@@ -201,9 +204,11 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         meat = None
         if stats is not None:
             pass
-        elif fused is not None:
+        elif fused is not None and _beta_agrees(fused[1], beta_full):
             stats, meat = fused[2], fused[3]
         else:
+            # no fused pass, or its device Cholesky beta drifted from the host solve the SEs
+            # use (ill-conditioned Gram): the residual pass runs again with the host beta
             stats, meat = eng.resid(beta_full, hc1=(v == "hc1"), keep_scores=(v == "cluster"))
         rss_w, rss, sum_y, sum_y2 = stats
         n_clusters = None
@@ -228,6 +233,14 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                         n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
                         fe_dims=fe_dims, r_squared=r_squared, compression_ratio=est_comp_ratio,
                         rss=rss, tss=tss, backend="hip", timings=timings)
+
+
+def _beta_agrees(beta_dev, beta_host, rtol: float = 1e-10) -> bool:
+    """The fused residual pass used the device Cholesky's beta (lfe_gram_resid); its residuals,
+    meats and scores stand for the host solve's (polars_impl.py:212-229) only while the two
+    agree to far below the parity bar."""
+    scale = max(float(np.max(np.abs(beta_host))), 1e-300)
+    return bool(np.all(np.isfinite(beta_dev))) and float(np.max(np.abs(beta_dev - beta_host))) <= rtol * scale
 
 
 def _cluster_se(eng, cols, cluster_cols, sharded, Vb, to_meat, n_obs, df_resid, ssc):

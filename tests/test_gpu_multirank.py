@@ -203,3 +203,49 @@ def test_owner_declaration_is_validated():
     eng.set_owner(0, 0, 3000)
     eng.set_owner(None)
     eng.close()
+
+
+def test_sharded_leanfe_hip_auto_strategy_with_small_fes(monkeypatch):
+    """leanfe_hip(engine=<sharded engine>) with the default strategy='auto' and two small FEs
+    (where determine_strategy picks 'compress' for one process): every rank fits its row
+    shard by alt_proj and returns the oracle's whole-panel fit (INTEGRATION.md §4's call)."""
+    from leanfe_amd import dist, leanfe_hip
+    from leanfe_amd._lib import EmuGroup, Engine
+    from oracle import altproj
+
+    world, n, k, levels, seed = 2, 120_000, 3, [300, 40], 21
+    full = synth.panel(n, k, levels, seed=seed)
+    xs = [f"x{j + 1}" for j in range(k)]
+    # the emulated ranks share one process: the level agreement is the max over the shards,
+    # which here is the panel's own level count
+    monkeypatch.setattr(dist, "agree_levels", lambda eng, lv: [max(a, b) for a, b in zip(lv, levels)])
+    group = EmuGroup(world)
+    out, errs = {}, {}
+
+    def worker(rank):
+        try:
+            lo, hi = shard_range(n, rank, world)
+            eng = Engine(0)
+            eng.set_emu(group, rank)
+            eng.dist_group = ("emulated",)  # dist.is_sharded(eng): codes are global
+            shard = {c: np.asarray(v)[lo:hi] for c, v in full.items()}
+            out[rank] = leanfe_hip(shard, y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], vcov="HC1", quiet=True,
+                                   engine=eng)
+            eng.close()
+        except BaseException as e:  # noqa: BLE001
+            errs[rank] = e
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+    if errs:
+        raise next(iter(errs.values()))
+    o = altproj.fit(full, "y", xs, ["fe1", "fe2"], vcov="HC1")
+    for r in range(world):
+        res = out[r]
+        assert res.iterations == o["iterations"] and res.n_obs == o["n_obs"] and res.df_resid == o["df_resid"]
+        np.testing.assert_allclose([res.coefs[x] for x in xs], o["beta"], rtol=1e-10, atol=0)
+        np.testing.assert_allclose([res.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
