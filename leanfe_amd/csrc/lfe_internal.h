@@ -134,7 +134,6 @@ struct Timings {
 // [b << s, (b+1) << s).  Work item = contiguous row range inside one bucket.
 struct PartGeom {  // partition scatter launch geometry (lfe_prep.hip)
   int nth = 0, per = 0, nw = 0;
-  bool db = false;  // double-buffered column stage (8192-row chunks, 1024 threads)
   size_t lds = 0;
 };
 

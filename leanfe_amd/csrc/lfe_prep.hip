@@ -10,13 +10,14 @@
 //   k_part_hist    per-wave bucket histogram -> counts[bucket][wave]
 //   scan           exclusive scan of counts (bucket-major) -> destinations
 //   k_part_scatter per-wave LDS cursors; rows written to their bucket slot
-// Within one wave instruction same-bucket lanes are ranked by an LDS atomic,
-// so the layout does not depend on inter-wave timing.
+// Within one wave instruction same-bucket lanes are ranked in lane order by
+// ballots, so the layout is a pure function of the codes and the geometry.
 #include "lfe_internal.h"
 
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 namespace lfe {
 
@@ -199,15 +200,21 @@ int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) { return exclusive_scan2(c
 // ---------------------------------------------------------------------------
 
 // LDS-staged scatter.  A workgroup owns a chunk of kPartThreads*PER rows
-// (wave w: PER*64 consecutive rows).  It ranks its rows by bucket in LDS
-// (per-wave cursors: an LDS atomic ranks same-bucket lanes of one wave
-// instruction; waves own disjoint cursor ranges, so ranks do not depend on
-// wave timing), then moves every column through an LDS stage in bucket order,
-// so consecutive threads write consecutive addresses of one bucket run
-// (~chunk/nb rows per run) instead of 8-byte scatters.
+// (wave w: PER*64 consecutive rows).  It ranks its rows by bucket in LDS, then
+// moves every column through an LDS stage in bucket order, so consecutive
+// threads write consecutive addresses of one bucket run (~chunk/nb rows per run)
+// instead of 8-byte scatters.
+//
+// Ranking is deterministic by construction: every wave owns its own cursor per
+// bucket, and within one wave instruction the lanes of one bucket are ranked in
+// lane order from ballots of the bucket's bits (no returning atomics), so a later
+// launch of the same geometry reproduces the layout exactly (ensure_layout_orig).
+//
+// Column c + 1's loads are issued as soon as column c is staged, so they are in
+// flight during column c's write-out.
 
 struct ScatterArgs {
-  int p, F, P, s, nb, nchunks;
+  int p, F, P, s, nb, nbits, nchunks;
   int64_t n, ld;
   const double* X;
   const double* w;
@@ -217,45 +224,50 @@ struct ScatterArgs {
   int32_t* codeo[kMaxFE];
   int32_t* orig;
   const int32_t* scanned;  // [nb][nchunks] exclusive destinations
-  int xcd_map;             // 1: XCD-contiguous chunk order
-  int pipe;                // 1: load column c + 1 during column c's write-out
-  int nt;                  // bit 0: non-temporal stores, bit 1: non-temporal column loads
   int cols;                // move the X / w columns and the codes
   int want_orig;           // write the input row index of each layout row
 };
 
-// block i -> chunk: XCD x = i % 8 walks its contiguous eighth of the chunks
+// a global-memory byte pointer the compiler keeps in SGPRs (it is the same in every lane), so
+// loads and stores use the saddr + 32-bit voffset forms
+typedef __attribute__((address_space(1))) char gchar;
+__device__ __forceinline__ gchar* uniform_gptr(const void* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<gchar*>(((uint64_t)hi << 32) | lo);
+}
+
+// block i -> chunk: XCD x = i % 8 walks its contiguous eighth of the chunks, so the adjacent
+// runs that consecutive chunks write into every bucket region meet in one L2
 __device__ __forceinline__ int xcd_chunk(int i, int nw) {
   const int x = i & 7, r = i >> 3;
   const int per = (nw + 7) >> 3;          // chunks per XCD (the last XCD may have fewer)
   return x * per + r;                      // may be >= nw: the caller's r0 >= n then
 }
 
-// DB: two column stages, so a column's write-out overlaps the next column's staging with one
-// barrier per column instead of two (the int columns always use two int32 halves of the stage)
-template <int PER, int NTH, bool DB>
+// O32: every column is < 4 GiB (ld * 8 < 2^32), so loads and stores address it with 32-bit
+// byte offsets from a uniform base (the saddr + 32-bit voffset forms: one VGPR per address)
+template <int PER, int NTH, bool O32>
 __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
-  constexpr int kPartThreads = NTH;
-  constexpr int kPartWaves = NTH / 64;
-  constexpr int R = kPartThreads * PER;
+  using off_t = typename std::conditional<O32, uint32_t, int64_t>::type;
+  constexpr int kWaves = NTH / 64;
+  constexpr int R = NTH * PER;
+  static_assert(R <= 32768, "stage slots are kept as 16-bit values");
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* stage = smem;                                        // [R or 2R] (doubles or int32)
-  int32_t* cur = reinterpret_cast<int32_t*>(stage + (DB ? 2 : 1) * R);  // [waves][nb] cursors
-  int32_t* delta = cur + kPartWaves * a.nb;                    // [nb]
-  int32_t* tot = delta + a.nb;                                 // [nb + 1]
+  double* stage = smem;                                           // [R] (doubles or two int32 halves)
+  int32_t* cur = reinterpret_cast<int32_t*>(stage + R);           // [waves][nb] cursors
+  int32_t* delta = cur + kWaves * a.nb;                           // [nb]
+  int32_t* tot = delta + a.nb;                                    // [nb + 1]
   __shared__ int32_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // XCD-contiguous chunks: workgroups go round-robin to the 8 XCDs (block i on XCD
-  // i % 8); XCD x takes chunks [x nw / 8, (x + 1) nw / 8) in order, so the adjacent
-  // runs that consecutive chunks write into every bucket region meet in one L2
-  const int chunk = a.xcd_map ? xcd_chunk(blockIdx.x, a.nchunks) : (int)blockIdx.x;
+  const int chunk = xcd_chunk(blockIdx.x, a.nchunks);
   const int64_t r0 = (int64_t)chunk * R, r1 = min(a.n, r0 + R);
   if (chunk >= a.nchunks) return;
   const int64_t wbase = r0 + (int64_t)wave * PER * 64;
   // slot k of a lane holds row wbase + (k / 2) * 128 + 2 lane + (k % 2): pairs of consecutive
   // rows, so every column is read with 16-byte loads (the guide's streaming-read shape)
   auto row_of = [&](int k) -> int64_t { return wbase + (k >> 1) * 128 + 2 * lane + (k & 1); };
-  for (int j = tid; j < kPartWaves * a.nb; j += kPartThreads) cur[j] = 0;
+  for (int j = tid; j < kWaves * a.nb; j += NTH) cur[j] = 0;
   __syncthreads();
   int32_t bk[PER];
 #pragma unroll
@@ -265,14 +277,15 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
     bk[k] = i < r1 ? (g.x >> a.s) : -1;
     bk[k + 1] = i + 1 < r1 ? (g.y >> a.s) : -1;
   }
+  // per-wave bucket counts (integer adds commute: the counts do not depend on their order)
 #pragma unroll
   for (int k = 0; k < PER; ++k)
     if (bk[k] >= 0) atomicAdd(&cur[wave * a.nb + bk[k]], 1);
   __syncthreads();
   // per bucket: exclusive scan over waves, total
-  for (int b = tid; b < a.nb; b += kPartThreads) {
+  for (int b = tid; b < a.nb; b += NTH) {
     int32_t t = 0;
-    for (int w2 = 0; w2 < kPartWaves; ++w2) {
+    for (int w2 = 0; w2 < kWaves; ++w2) {
       const int32_t h = cur[w2 * a.nb + b];
       cur[w2 * a.nb + b] = t;
       t += h;
@@ -280,14 +293,14 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
     tot[b] = t;
   }
   __syncthreads();
-  // exclusive scan of tot over buckets (one thread per PERB buckets, then waves)
+  // exclusive scan of tot over buckets (one thread per `per` buckets, then waves)
   {
-    const int per = (a.nb + kPartThreads - 1) / kPartThreads;
+    const int per = (a.nb + NTH - 1) / NTH;
     const int b0 = tid * per;
-    int32_t s = 0;
+    int32_t sacc = 0;
     for (int q = 0; q < per; ++q)
-      if (b0 + q < a.nb) s += tot[b0 + q];
-    int32_t x = s;  // wave inclusive scan
+      if (b0 + q < a.nb) sacc += tot[b0 + q];
+    int32_t x = sacc;  // wave inclusive scan
     for (int off = 1; off < 64; off <<= 1) {
       const int32_t y = __shfl_up(x, off, 64);
       if (lane >= off) x += y;
@@ -296,7 +309,7 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
     __syncthreads();
     int32_t wofs = 0;
     for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[w2];
-    int32_t run = x - s + wofs;
+    int32_t run = x - sacc + wofs;
     __syncthreads();
     for (int q = 0; q < per; ++q)
       if (b0 + q < a.nb) {
@@ -306,28 +319,48 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
       }
   }
   __syncthreads();
-  for (int b = tid; b < a.nb; b += kPartThreads) {
+  for (int b = tid; b < a.nb; b += NTH) {
     const int32_t boff = tot[b];
     delta[b] = a.scanned[(int64_t)b * a.nchunks + chunk] - boff;
-    for (int w2 = 0; w2 < kPartWaves; ++w2) cur[w2 * a.nb + b] += boff;
+    for (int w2 = 0; w2 < kWaves; ++w2) cur[w2 * a.nb + b] += boff;
   }
   __syncthreads();
-  // slot -> bucket through the (not yet used) stage, then every thread keeps the
-  // global destination of the slots it writes out (j = tid + k * NTH) in registers
+  // stage slot of every row: the wave's cursor of its bucket + its rank among the lanes of this
+  // instruction with the same bucket (lane order, from the ballots of the bucket's bits); the
+  // first such lane advances the cursor.  The slot's bucket goes to the (not yet used) stage.
   int32_t* sb = reinterpret_cast<int32_t*>(stage);
-  int32_t pos[PER];
+  const uint64_t lanes_below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t posp[PER / 2];  // two 16-bit slots per register (0xffff: no row)
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    pos[k] = -1;
-    if (bk[k] >= 0) {
-      pos[k] = atomicAdd(&cur[wave * a.nb + bk[k]], 1);
-      sb[pos[k]] = bk[k];
+    const int b = bk[k];
+    const bool act = b >= 0;
+    uint32_t slot = 0xffffu;
+    uint64_t same = __ballot(act);
+    for (int bit = 0; bit < a.nbits; ++bit) {
+      const bool one = act && ((b >> bit) & 1);
+      const uint64_t m = __ballot(one);
+      same &= one ? m : ~m;
     }
+    if (act) {
+      int32_t* cw = &cur[wave * a.nb + b];
+      const int base = *cw;
+      const int rank = __popcll(same & lanes_below);
+      if (rank == 0) *cw = base + __popcll(same);
+      slot = (uint32_t)(base + rank);
+      sb[slot] = b;
+    }
+    if (k & 1) posp[k >> 1] |= slot << 16;
+    else posp[k >> 1] = slot;
   }
+  auto pos_of = [&](int k) -> int {
+    const uint32_t v = (k & 1) ? (posp[k >> 1] >> 16) : (posp[k >> 1] & 0xffffu);
+    return v == 0xffffu ? -1 : (int)v;
+  };
   __syncthreads();
   const int len = (int)(r1 - r0);
-  // write-out slot k of a thread (slot pairs with 16-byte stores measured 1 % slower)
-  auto slot_of = [&](int k) -> int { return tid + k * kPartThreads; };
+  // write-out slot k of a thread: consecutive threads read consecutive stage slots
+  auto slot_of = [&](int k) -> int { return tid + k * NTH; };
   int32_t dd[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -337,47 +370,73 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   __syncthreads();
   // ---- move columns through the stage: gather in row order, store in bucket order ----
   const int ncol = a.cols ? a.p + (a.w ? 1 : 0) : 0;
-  double v[PER];
   typedef double d2v __attribute__((ext_vector_type(2)));
-  auto load_col = [&](int c) {
-    const double* src = c < a.p ? a.X + (int64_t)c * a.ld : a.w;
+  // rows i < n are loaded in 16-byte pairs: i is even and the columns are padded to a multiple
+  // of 64 rows, so row i + 1 lies inside the column even when i + 1 == n.  A full chunk (every
+  // chunk but the last) runs without per-row predicates.
+  const bool full = len == R;
+  auto move_cols = [&](auto full_c) {
+    constexpr bool FULL = decltype(full_c)::value;
+    // the wave's rows start at wbase: the column base moves by wbase rows (uniform), a lane's
+    // offset is then 16 * lane + 1024 * (k / 2) bytes (one VGPR plus immediates)
+    const uint32_t lane_off = 16u * (uint32_t)lane;
+    auto load_col = [&](int c, double (&v)[PER]) {
+      const gchar* src = uniform_gptr(reinterpret_cast<const char*>(c < a.p ? a.X + (int64_t)c * a.ld : a.w) +
+                                      wbase * 8);
+      uint32_t lo = lane_off;
+      asm volatile("" : "+v"(lo));  // the per-row offsets are formed here, not hoisted as 64-bit pairs
 #pragma unroll
-    for (int k = 0; k < PER; k += 2) {
-      const int64_t i = row_of(k);  // even: 16-byte aligned (columns start at multiples of 64 rows)
-      if (pos[k + 1] >= 0) {
-        const d2v t = *reinterpret_cast<const d2v*>(src + i);
+      for (int k = 0; k < PER; k += 2) {
+        d2v t = d2v{0.0, 0.0};
+        if (FULL || row_of(k) < r1)
+          t = *reinterpret_cast<const __attribute__((address_space(1))) d2v*>(
+              src + (off_t)(lo + 1024u * (uint32_t)(k >> 1)));
         v[k] = t.x;
         v[k + 1] = t.y;
-      } else {
-        v[k] = pos[k] >= 0 ? src[i] : 0.0;
-        v[k + 1] = 0.0;
       }
+    };
+    auto stage_col = [&](const double (&v)[PER]) {
+      // the packed slots are decoded here, per column, instead of living unpacked in 16 more
+      // registers across the loop (the empty asm keeps the compiler from hoisting the decode)
+#pragma unroll
+      for (int k = 0; k < PER / 2; ++k) asm volatile("" : "+v"(posp[k]));
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int q = pos_of(k);
+        if (FULL || q >= 0) stage[q] = v[k];
+      }
+    };
+    auto write_col = [&](int c) {
+      gchar* dst = uniform_gptr(c < a.p ? a.Xo + (int64_t)c * a.ld : a.wo);
+#pragma unroll
+      for (int k = 0; k < PER; ++k) asm volatile("" : "+v"(dd[k]));  // no hoisted 64-bit addresses
+      // four stage reads in flight before their stores (not one LDS round trip per store)
+#pragma unroll
+      for (int k0 = 0; k0 < PER; k0 += 4) {
+        double t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[u] = stage[slot_of(k0 + u)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (FULL || dd[k0 + u] >= 0)
+            *reinterpret_cast<__attribute__((address_space(1))) double*>(dst + (off_t)dd[k0 + u] * 8) = t[u];
+      }
+    };
+    // one register set: column c + 1 is loaded while column c is written out (two register
+    // sets, loading c + 2 during c + 1's staging, measured 2.12 vs 2.09 ms)
+    double v[PER];
+    if (ncol > 0) load_col(0, v);
+    for (int c = 0; c < ncol; ++c) {
+      stage_col(v);
+      asm volatile("" ::: "memory");  // the next loads stay after the stage writes
+      if (c + 1 < ncol) load_col(c + 1, v);
+      __syncthreads();
+      write_col(c);
+      __syncthreads();
     }
   };
-  if (ncol > 0) load_col(0);
-  for (int c = 0; c < ncol; ++c) {
-    double* dst = c < a.p ? a.Xo + (int64_t)c * a.ld : a.wo;
-    // DB: this buffer was last read by column c - 2's write-out, which every wave finished
-    // before the barrier of column c - 1
-    double* st = DB ? stage + (c & 1) * R : stage;
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (pos[k] >= 0) st[pos[k]] = v[k];
-    if (a.pipe && c + 1 < ncol) load_col(c + 1);  // next column in flight during the write-out
-    __syncthreads();
-    if (a.nt & 1) {
-#pragma unroll
-      for (int k = 0; k < PER; ++k)
-        if (dd[k] >= 0) __builtin_nontemporal_store(st[slot_of(k)], dst + dd[k]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < PER; ++k)
-        if (dd[k] >= 0) dst[dd[k]] = st[slot_of(k)];
-    }
-    if (!DB) __syncthreads();
-    if (!a.pipe && c + 1 < ncol) load_col(c + 1);
-  }
-  if (DB && ncol > 0) __syncthreads();  // the int halves overlap the column stages
+  if (full) move_cols(std::true_type{});
+  else move_cols(std::false_type{});
   int32_t* istage0 = reinterpret_cast<int32_t*>(stage);
   const int ic0 = a.cols ? 0 : a.F;
   for (int c = ic0; c < a.F + a.want_orig; ++c) {  // F code arrays, then the input row index
@@ -387,9 +446,10 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
     for (int k = 0; k < PER; k += 2) {
       const int64_t i = row_of(k);
       int2 g = int2{(int32_t)i, (int32_t)i + 1};
-      if (c < a.F && pos[k] >= 0) g = *reinterpret_cast<const int2*>(a.code[c] + i);
-      if (pos[k] >= 0) istage[pos[k]] = g.x;
-      if (pos[k + 1] >= 0) istage[pos[k + 1]] = g.y;
+      const int q0 = pos_of(k), q1 = pos_of(k + 1);
+      if (c < a.F && q0 >= 0) g = *reinterpret_cast<const int2*>(a.code[c] + i);
+      if (q0 >= 0) istage[q0] = g.x;
+      if (q1 >= 0) istage[q1] = g.y;
     }
     __syncthreads();
 #pragma unroll
@@ -629,33 +689,16 @@ static int launch_part_scatter(lfe_ctx* c, int cols, int orig) {
   a.scanned = c->pcounts;
   a.cols = cols;
   a.want_orig = orig;
-  static const int xmap_env = [] {
-    const char* e = getenv("LFE_PART_XCD");  // tuning: 0 = plain chunk order
-    return e ? atoi(e) : 1;
-  }();
-  a.xcd_map = xmap_env;
-  static const int pipe_env = [] {
-    // tuning: 1 = load column c + 1 during column c's write-out. It was 0.5% faster with two
-    // barriers per int column. With one barrier per int column, 0 was 1.7% faster in some runs
-    // but bimodal (2.04 / 2.50 ms on one box, alternating A/B); 1 held 2.076 ms every run
-    const char* e = getenv("LFE_PART_PIPE");
-    return e ? atoi(e) : 1;
-  }();
-  a.pipe = pipe_env;
-  static const int nt_env = [] {
-    // tuning: non-temporal stores (1), loads (2); measured at 50M rows: stores 2.23 -> 2.74 ms,
-    // loads no change, so both stay off
-    const char* e = getenv("LFE_PART_NT");
-    return e ? atoi(e) : 0;
-  }();
-  a.nt = nt_env;
-  const int pgrid = a.xcd_map ? ((g.nw + 7) / 8) * 8 : g.nw;
+  a.nbits = 0;  // bits of a bucket id (ballot ranking)
+  while ((1 << a.nbits) < L.nb) ++a.nbits;
+  const int pgrid = ((g.nw + 7) / 8) * 8;  // xcd_chunk: a multiple of the 8 XCDs
   // dynamic LDS above 64 KB must be opted in (static LDS + dynamic <= 160 KB)
   using Fn = void (*)(ScatterArgs);
-  Fn fn = g.db ? &k_part_scatter<8, 1024, true>
-         : g.nth == 1024 ? (g.per == 16 ? &k_part_scatter<16, 1024, false>
-                            : g.per == 8 ? &k_part_scatter<8, 1024, false> : &k_part_scatter<4, 1024, false>)
-                         : (g.per == 16 ? &k_part_scatter<16, 512, false> : &k_part_scatter<8, 512, false>);
+  const bool o32 = (uint64_t)c->ld * 8 <= 0xffffffffull;
+#define PART_FN(PER, NTH) (o32 ? &k_part_scatter<PER, NTH, true> : &k_part_scatter<PER, NTH, false>)
+  Fn fn = g.nth == 1024 ? (g.per == 16 ? PART_FN(16, 1024) : g.per == 8 ? PART_FN(8, 1024) : PART_FN(4, 1024))
+                        : (g.per == 16 ? PART_FN(16, 512) : PART_FN(8, 512));
+#undef PART_FN
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)g.lds));
   {
@@ -733,41 +776,17 @@ int prepare_layout(lfe_ctx* c) {
     // 1024-thread workgroups (16 rows per thread), one workgroup per CU, 2.06 ms; 8192-row
     // chunks on 512 threads 2.28 ms.  Earlier: 4096-row chunks, several chunks per
     // workgroup and register scatter without the LDS stage were all slower.
-    static const int nth_env = [] {
-      const char* e = getenv("LFE_PART_T");  // tuning: 512 or 1024 threads per chunk
-      return e && atoi(e) == 512 ? 512 : 1024;
-    }();
     // one 16-wave workgroup per CU: with two per CU (32 waves) twice as many chunks write into
     // every bucket region at once and the scatter ran 13 % slower (measured); pad the LDS request
-    static const size_t lds_min = [] {
-      const char* e = getenv("LFE_PART_LDS_MIN");  // tuning: LDS floor in bytes
-      return e ? (size_t)atol(e) : (size_t)(82 * 1024);
-    }();
-    static const int64_t cw_env = [] {
-      const char* e = getenv("LFE_PART_CW");  // tuning: rows per chunk (8192 or 16384)
-      return e ? (int64_t)atol(e) : (int64_t)16384;  // 16K: ~84-row runs per bucket at s = 9
-    }();
-    static const int db_env = [] {
-      // tuning: 1 = double-buffered column stage on 8192-row chunks (one barrier per column);
-      // measured 1.996 vs 1.949 ms for one stage on 16384-row chunks, so off
-      const char* e = getenv("LFE_PART_DB");
-      return e ? atoi(e) : 0;
-    }();
-    int64_t cw = nb <= 512 ? cw_env : 4096;
-    auto part_lds = [&](int nth, bool db = false) {
-      return sizeof(double) * cw * (db ? 2 : 1) + sizeof(int32_t) * ((size_t)(nth / 64) * nb + 2 * (size_t)nb + 1);
+    constexpr size_t kLdsMin = 82 * 1024;
+    // 16K-row chunks: ~84-row runs per bucket at s = 9
+    int64_t cw = nb <= 512 ? 16384 : 4096;
+    auto part_lds = [&](int nth) {
+      return sizeof(double) * cw + sizeof(int32_t) * ((size_t)(nth / 64) * nb + 2 * (size_t)nb + 1);
     };
     // 16 waves per chunk when their per-wave bucket cursors fit (nb <= ~1500)
-    const int nth = nth_env == 1024 && part_lds(1024) <= 150 * 1024 ? 1024 : 512;
-    if (cw == 16384 && (nth != 1024 || part_lds(1024) > 150 * 1024)) cw = 8192;
-    // double-buffered stage: 8192-row chunks (two 64 KB stages), one barrier per column
-    bool db = false;
-    if (db_env && nth == 1024 && nb <= 512) {
-      const int64_t keep = cw;
-      cw = 8192;
-      db = part_lds(1024, true) <= 150 * 1024;
-      if (!db) cw = keep;
-    }
+    const int nth = part_lds(1024) <= 150 * 1024 ? 1024 : 512;
+    if (cw == 16384 && nth != 1024) cw = 8192;
     const int per = (int)(cw / nth);
     const int nw = (int)((n + cw - 1) / cw);
     const int64_t m = (int64_t)nb * nw;
@@ -785,8 +804,8 @@ int prepare_layout(lfe_ctx* c) {
     hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(nb)), dim3(kBlock), 0, c->stream, c->pcounts, nb, nw, dbstart);
     LFE_HIP(hipGetLastError());
     LFE_TRY(d2h_async(c, dbstart, sizeof(int32_t) * nb));
-    const size_t lds = std::min<size_t>(std::max(part_lds(nth, db), lds_min), 160 * 1024);
-    L.part = PartGeom{nth, per, nw, db, lds};
+    const size_t lds = std::min<size_t>(std::max(part_lds(nth), kLdsMin), 160 * 1024);
+    L.part = PartGeom{nth, per, nw, lds};
     // the input row index of each layout row is written only when a caller needs it
     // (ensure_layout_orig: cluster, records and demeaned-column export paths)
     LFE_TRY(launch_part_scatter(c, /*cols=*/1, /*orig=*/0));
