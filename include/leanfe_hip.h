@@ -210,6 +210,12 @@ int lfe_copy_demeaned(lfe_ctx* ctx, double* const* cols_out, int64_t* n_out);
  * order) back to host buffers. */
 int lfe_copy_inputs(lfe_ctx* ctx, double* const* cols_out, int32_t* const* codes_out);
 
+/* Whether the last group sums of the two-FE fast path accumulated exactly (int64
+ * fixed point per column, so S does not depend on the order of the adds and a
+ * repeated solve is bit-identical): *on = 1, else 0 (f64 atomic sums, or another
+ * path).  Replaces nothing in the reference (Polars' group sums are serial). */
+int lfe_exact_sums(lfe_ctx* ctx, int* on);
+
 /* Wait for all work queued on the context's stream. */
 int lfe_sync(lfe_ctx* ctx);
 

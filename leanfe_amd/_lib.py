@@ -54,6 +54,7 @@ SIGNATURES = {
     "lfe_compress": (C.c_int, [_vp, _i64p]),
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
+    "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
     "lfe_sync": (C.c_int, [_vp]),
     "lfe_shard_rows": (C.c_int, [_vp, _i64p]),
     "lfe_timings": (C.c_int, [_vp, _dp]),
@@ -377,6 +378,12 @@ class Engine:
 
     def sync(self) -> None:
         _check(self._lib.lfe_sync(self._h))
+
+    def exact_sums(self) -> bool:
+        """True when the last group sums took the exact int64 path (order-independent)."""
+        on = C.c_int32(0)
+        _check(self._lib.lfe_exact_sums(self._h, C.byref(on)))
+        return bool(on.value)
 
     def profile(self, enable: bool = True) -> None:
         _check(self._lib.lfe_profile(self._h, 1 if enable else 0))

@@ -306,7 +306,7 @@ const char* const kKernelNames[K_NUM_KERNELS] = {
     "part_hist", "scan", "part_scatter", "count", "mark", "group_sums", "cross", "check", "finalize",
     "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth",
     "tp", "tq", "seg_build", "cluster_sort", "gram_tables", "layout_hist", "layout_base", "layout_scatter",
-    "tq_reduce"};
+    "tq_reduce", "fix_sums"};
 
 static hipEvent_t prof_event(lfe_ctx* c) {
   if (!c->prof.pool.empty()) {
@@ -403,6 +403,10 @@ static void free_data(lfe_ctx* c) {
   c->L = Layout();
   dfree(c->tq_runs);
   c->tq_runs_cap = 0;
+  dfree(c->colstat);
+  dfree(c->fixq);
+  c->colstat_cap = c->fixq_cap = 0;
+  c->colstat_chunks = 0;
   c->owner_fe = -1;
   c->owner_on = false;
   c->loaded = c->prepared = c->demeaned = c->scores_valid = c->seg_ready = false;
@@ -929,6 +933,12 @@ int lfe_shard_rows(lfe_ctx* c, int64_t* n_out) {
   if (!c || !n_out) return fail(LFE_EINVAL, "null pointer");
   *n_out = c->loaded ? c->n : 0;
   return LFE_OK;
+}
+
+int lfe_exact_sums(lfe_ctx* c, int* on) {
+  LFE_CTX(c);
+  if (!on) return fail(LFE_EINVAL, "null pointer");
+  return exact_sums_on(c, on);
 }
 
 int lfe_sync(lfe_ctx* c) {

@@ -40,7 +40,19 @@ struct Sums4Args {
   int nq;               // number of non-primary FEs and their indices
   int qf[kMaxFE];
   double* raw_part;     // RAW: [blocks][256] raw Gram tiles
+  const double* fixq;   // k_sums2_raw: [kMaxCols] scales, [kMaxCols] quanta, [kMaxCols] qualified (k_fix_quanta)
 };
+
+// exact group sums (k_sums2_raw): round(x * scale) is the low mantissa of x * scale + 1.5 * 2^52
+constexpr double kFixMagic = 6755399441055744.0;  // 1.5 * 2^52
+constexpr unsigned long long kFixMagicBits = 0x4338000000000000ull;
+
+// every column qualifies: the exact sums are on for the fit
+__device__ __forceinline__ bool fix_on(const double* __restrict__ fq, int p) {
+  bool on = true;
+  for (int c = 0; c < p; ++c) on = on && fq[2 * kMaxCols + c] != 0.0;
+  return on;
+}
 
 // FQ: max non-primary FEs held in registers; GU: 16-row groups loaded before use;
 // NT: 16-column slots per lane (p <= 16 NT); TH: threads per workgroup.
@@ -207,17 +219,28 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   const double* __restrict__ xc = a.X + (int64_t)(col ? c : 0) * a.ld;
   const int qoff = a.tab_off[Q];
   double* const qtab = lds + qoff;
+  // exact sums: every value enters the tables as round(x * 2^(62-e_c)) in int64, so the tables
+  // are the same whatever order the waves' LDS adds (and the blocks' global adds) land in
+  const bool fix = fix_on(a.fixq, p);
+  const double fscale = col ? a.fixq[c] : 0.0;
   d4 racc[NACC];  // independent MFMA chains
 #pragma unroll
   for (int r = 0; r < NACC; ++r) racc[r] = d4{0.0, 0.0, 0.0, 0.0};
   for (int j = tid; j < a.G[Q] * p; j += TH) lds[qoff + j] = 0.0;
   for (int j = tid; j < a.B * p; j += TH) lds[j] = 0.0;
+  typedef unsigned long long u64;
   auto flush = [&](int b) {
     const int lo = b << s;
     for (int j = tid; j < a.B * p; j += TH) {
-      const double val = lds[j];
       const int g = lo + j / p;
-      if (val != 0.0 && g < a.G_P) atomicAdd(&a.S[P][(int64_t)g * p + (j % p)], val);
+      double* dst = &a.S[P][(int64_t)g * p + (j % p)];
+      if (fix) {
+        const u64 val = reinterpret_cast<const u64*>(lds)[j];
+        if (val != 0ull && g < a.G_P) atomicAdd(reinterpret_cast<u64*>(dst), val);
+      } else {
+        const double val = lds[j];
+        if (val != 0.0 && g < a.G_P) atomicAdd(dst, val);
+      }
       lds[j] = 0.0;
     }
   };
@@ -269,8 +292,15 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
           const double z = v ? __builtin_fma(xv, cm, zc) : 0.0;
           racc[r % NACC] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[r % NACC], 0, 0, 0);
           if (v && col) {
-            atomicAdd(lds_row_ptr(lds, hv[r] - lo, p8, c8), xv);
-            atomicAdd(lds_row_ptr(qtab, gq[r], p8, c8), xv);
+            if (fix) {  // integer adds commute: the exact path
+              // round(x * scale) as the low bits of x * scale + 1.5 * 2^52 (|x * scale| < 2^51)
+              const u64 xi = (u64)__double_as_longlong(__builtin_fma(xv, fscale, kFixMagic)) - kFixMagicBits;
+              atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(lds, hv[r] - lo, p8, c8)), xi);
+              atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(qtab, gq[r], p8, c8)), xi);
+            } else {
+              atomicAdd(lds_row_ptr(lds, hv[r] - lo, p8, c8), xv);
+              atomicAdd(lds_row_ptr(qtab, gq[r], p8, c8), xv);
+            }
           }
         }
       }
@@ -299,8 +329,13 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   __syncthreads();
   if (cur >= 0) flush(cur);
   for (int j = tid; j < a.G[Q] * p; j += TH) {
-    const double val = lds[qoff + j];
-    if (val != 0.0) atomicAdd(&a.S[Q][j], val);
+    if (fix) {
+      const u64 val = reinterpret_cast<const u64*>(lds + qoff)[j];
+      if (val != 0ull) atomicAdd(reinterpret_cast<u64*>(&a.S[Q][j]), val);
+    } else {
+      const double val = lds[qoff + j];
+      if (val != 0.0) atomicAdd(&a.S[Q][j], val);
+    }
   }
   __shared__ double rred[256];
   for (int wv = 0; wv < nwv; ++wv) {
@@ -317,6 +352,95 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   }
   __syncthreads();
   for (int e = tid; e < 256; e += TH) a.raw_part[(int64_t)blockIdx.x * 256 + e] = rred[e];
+}
+
+// ---------------------------------------------------------------------------
+// exact group sums (the two-FE Gram-from-tables case, k_sums2_raw)
+// ---------------------------------------------------------------------------
+// A column's group sums accumulate round(x * scale) in int64, scale = 2^min(62 - e, 51 - e_M) with
+// 2^e > N * max|x| (N = the largest kept group over both FEs) and 2^e_M > max|x|: no partial
+// sum can overflow (|sum| < 2^62), every scaled value is below 2^51 so one FMA with 1.5 * 2^52
+// rounds it (the low mantissa bits are the integer), and integer adds make the tables
+// independent of the order in which waves and blocks add (bit-reproducible).  Per value the
+// rounding is at most 1/(2 scale) <= N max|x| 2^-62: below double rounding for the group means
+// as long as max|x| stays within kFixRange of the column's RMS; a column outside that range
+// (or a NaN / Inf) keeps the f64 atomic sums for every column of the fit.
+constexpr double kFixRange = 64.0;
+
+// column statistics when the partition did not run (one bucket): max |x_c| bits in st[c],
+// the chunk's sum of x_c^2 in st[kColStatHead + c * nchunks + chunk] (as the partition writes them)
+__global__ __launch_bounds__(256) void k_col_stats(const double* __restrict__ X, int64_t ld, int64_t n, int p,
+                                                   int64_t chunk_rows, double* __restrict__ st) {
+  __shared__ double ws[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * chunk_rows, r1 = min(n, r0 + chunk_rows);
+  const auto fmaxop = [](double x, double y) { return fmax(x, y); };
+  const auto addop = [](double x, double y) { return x + y; };
+  for (int c = 0; c < p; ++c) {
+    double m = 0.0, q = 0.0;
+    for (int64_t i = r0 + tid; i < r1; i += 256) {
+      const double v = X[(int64_t)c * ld + i];
+      m = fmax(m, fabs(v));
+      q = __builtin_fma(v, v, q);
+    }
+    m = wave_reduce63(m, 0.0, fmaxop);
+    q = wave_reduce63(q, 0.0, addop);
+    if (lane == 63) {
+      ws[0][wave] = m;
+      ws[1][wave] = q;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      st[kColStatHead + (int64_t)c * gridDim.x + blockIdx.x] = ((ws[1][0] + ws[1][1]) + ws[1][2]) + ws[1][3];
+      const double mm = fmax(fmax(ws[0][0], ws[0][1]), fmax(ws[0][2], ws[0][3]));
+      atomicMax(reinterpret_cast<unsigned long long*>(st) + c, (unsigned long long)__double_as_longlong(mm));
+    }
+    __syncthreads();
+  }
+}
+
+// scale, quantum and qualification of column c = blockIdx.x (fq: [kMaxCols] scales, [kMaxCols]
+// quanta, [kMaxCols] 1.0 / 0.0); the per-chunk squares are summed in a fixed order
+__global__ __launch_bounds__(256) void k_fix_quanta(const double* __restrict__ st, int nchunks, int64_t n,
+                                                    const int32_t* __restrict__ cmax, int nfe,
+                                                    double* __restrict__ fq) {
+  __shared__ double ws[4];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double* sq = st + kColStatHead + (int64_t)c * nchunks;
+  double q = 0.0;
+  for (int ch = tid; ch < nchunks; ch += 256) q += sq[ch];
+  q = wave_reduce63(q, 0.0, [](double x, double y) { return x + y; });
+  if (lane == 63) ws[wave] = q;
+  __syncthreads();
+  if (tid != 0) return;
+  q = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+  int N = 1;
+  for (int f = 0; f < nfe; ++f) N = max(N, cmax[f]);
+  const double M = __longlong_as_double(reinterpret_cast<const long long*>(st)[c]);
+  const double rms = n > 0 ? sqrt(q / (double)n) : 0.0;
+  const double NM = (double)N * M;
+  const bool ok = isfinite(q) && isfinite(NM) && M <= kFixRange * rms;
+  double scale = 1.0, quantum = 1.0;
+  if (ok && M > 0.0) {
+    int e = 0, eM = 0;
+    (void)frexp(NM, &e);  // NM < 2^e
+    (void)frexp(M, &eM);  // M < 2^eM
+    const int sh = min(62 - e, 51 - eM);
+    scale = ldexp(1.0, sh);
+    quantum = ldexp(1.0, -sh);
+  }
+  fq[c] = scale;
+  fq[kMaxCols + c] = quantum;
+  fq[2 * kMaxCols + c] = ok ? 1.0 : 0.0;
+}
+
+// int64 table entries (exact path) -> double: S = round-sum * quantum of the entry's column
+__global__ void k_fix_convert(double* __restrict__ S, int64_t m, int p, const double* __restrict__ fq) {
+  if (!fix_on(fq, p)) return;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+    const long long v = reinterpret_cast<const long long*>(S)[e];
+    S[e] = (double)v * fq[kMaxCols + (int)(e % p)];
+  }
 }
 
 // raw_shift[16 + j] = this rank's shift (first layout row; 0 for an empty shard);
@@ -381,34 +505,20 @@ int sums4(lfe_ctx* c) {
   const int NT = (p + 15) / 16;
   const void* fn = nullptr;
 #define SUMS4_FN(FQ, GU, NT_, TH_) reinterpret_cast<const void*>(&k_sums4<FQ, GU, NT_, TH_, false>)
-  static const int gu_env = [] {
-    const char* e = getenv("LFE_SUMS_GU");  // tuning override
-    return e ? atoi(e) : 0;
-  }();
-  static const int raw_env = [] {
-    const char* e = getenv("LFE_TABLE_GRAM");  // 0: no Gram from tables (explicit design pass)
-    return e ? atoi(e) : 1;
-  }();
-  const bool raw = raw_env != 0 && c->F == 2 && P >= 0 && a.nq == 1 && p <= 15 && !a.w && gu_env != 4;
+  // the raw Gram of the shifted columns rides along when the Gram can come from the tables
+  const bool raw = c->F == 2 && P >= 0 && a.nq == 1 && p <= 15 && !a.w;
   c->raw_ready = false;
-  static const int sums2_env = [] {
-    // tuning: 0 = k_sums4 for the two-FE Gram case; MFMA chains x groups per load: 1 = 4 x 2,
-    // 2 = 2 x 2, 3 = 4 x 1, 4 = 2 x 1 (3: 0.925 vs 0.950 ms for 1 with 24-bit LDS addressing)
-    const char* e = getenv("LFE_SUMS2");
-    return e ? atoi(e) : 3;
-  }();
   int threads = kSumThreads;
+  bool two = false;
   if (a.nq <= 1 && NT == 1) {
-    // the 2-FE case: one workgroup per CU (LDS), so 16 waves of <= 128 VGPRs (GU 2)
-    threads = gu_env == 4 ? kSumThreads : 1024;
-    const bool two = raw && sums2_env && a.slice && a.tab_off[a.qf[0]] >= 0;
-    fn = gu_env == 4 ? SUMS4_FN(1, 4, 1, kSumThreads)
-         : two       ? (sums2_env == 2   ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 2, 2>)
-                        : sums2_env == 3 ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1>)
-                        : sums2_env == 4 ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 2, 1>)
-                                         : reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 2>))
-         : raw       ? reinterpret_cast<const void*>(&k_sums4<1, 2, 1, 1024, true>)
-                     : SUMS4_FN(1, 2, 1, 1024);
+    // the 2-FE case: one workgroup per CU (LDS), so 16 waves of <= 128 VGPRs.  k_sums2_raw: four
+    // MFMA chains, one 16-row group per load (0.925 vs 0.950 ms for 2 groups per load; 2 chains
+    // measured the same)
+    threads = 1024;
+    two = raw && a.slice && a.tab_off[a.qf[0]] >= 0;
+    fn = two   ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1>)
+         : raw ? reinterpret_cast<const void*>(&k_sums4<1, 2, 1, 1024, true>)
+               : SUMS4_FN(1, 2, 1, 1024);
   } else if (a.nq <= 1) {
     fn = NT == 2 ? SUMS4_FN(1, 2, 2, kSumThreads) : NT == 3 ? SUMS4_FN(1, 2, 3, kSumThreads)
                                                     : SUMS4_FN(1, 2, 4, kSumThreads);
@@ -426,12 +536,41 @@ int sums4(lfe_ctx* c) {
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
     a.raw_part = c->raw_part;
   }
+  const bool exact = two;
+  if (exact) {
+    ProfScope _ps(c, K_FIX_SUMS);
+    // the column statistics (the partition wrote them unless the rows stayed in place)
+    constexpr int64_t kStatRows = 16384;
+    if (c->colstat_chunks == 0) {
+      const int nch = (int)std::max<int64_t>(1, (c->n + kStatRows - 1) / kStatRows);
+      LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nch * p));
+      LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
+      hipLaunchKernelGGL(k_col_stats, dim3(nch), dim3(256), 0, c->stream, c->L.X, c->ld, c->n, p, kStatRows,
+                         c->colstat);
+      LFE_HIP(hipGetLastError());
+      c->colstat_chunks = nch;
+    }
+    LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, 3 * kMaxCols));
+    hipLaunchKernelGGL(k_fix_quanta, dim3(p), dim3(256), 0, c->stream, c->colstat, c->colstat_chunks, c->n,
+                       c->iscratch + kIscratchCmax, c->F, c->fixq);
+    LFE_HIP(hipGetLastError());
+    a.fixq = c->fixq;
+  }
+  c->exact_sums = exact;
   {
     ProfScope _ps(c, K_GROUP_SUMS);
     void* args[] = {&a};
     LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, lds, c->stream));
   }
   LFE_HIP(hipGetLastError());
+  if (exact) {
+    ProfScope _ps(c, K_FIX_SUMS);
+    for (int f = 0; f < c->F; ++f) {
+      const int64_t m = (int64_t)c->fe[f].G * p;
+      hipLaunchKernelGGL(k_fix_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, c->fe[f].S, m, p, c->fixq);
+    }
+    LFE_HIP(hipGetLastError());
+  }
   if (raw) {
     reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
     LFE_TRY(ensure_f64(c, c->raw_shift, c->raw_shift_cap, 32));
@@ -449,6 +588,16 @@ int sums4(lfe_ctx* c) {
   }
   for (int f = 0; f < c->F; ++f)  // owner-sharded rows: the primary FE's sums are complete on each rank
     if (!(c->owner_on && f == P)) LFE_TRY(allreduce_sum_f64(c, c->fe[f].S, (size_t)c->fe[f].G * p));
+  return LFE_OK;
+}
+
+int exact_sums_on(lfe_ctx* c, int* on) {
+  *on = 0;
+  if (!c->exact_sums || !c->fixq) return LFE_OK;
+  double flag[kMaxCols];
+  LFE_TRY(d2h_sync(c, flag, c->fixq + 2 * kMaxCols, sizeof(double) * c->p));
+  *on = 1;
+  for (int j = 0; j < c->p; ++j) *on = *on && flag[j] != 0.0;
   return LFE_OK;
 }
 

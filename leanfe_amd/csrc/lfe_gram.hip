@@ -725,15 +725,9 @@ int launch_validate_range(const int32_t* code, int64_t n, int32_t lo, int32_t hi
   return LFE_OK;
 }
 
-// row groups per wave iteration for the 2-FE kernels (LFE_GRAM_GU overrides, for tuning)
-static int gram_gu(int /*NT*/) {
-  static const int env = [] {
-    const char* e = getenv("LFE_GRAM_GU");
-    return e ? atoi(e) : 0;
-  }();
-  if (env == 1 || env == 2 || env == 4) return env;
-  return 2;  // measured: GU 2 beats 1 and 4 at NT = 1 (occupancy 4 vs 2 waves/SIMD)
-}
+// row groups per wave iteration for the 2-FE kernels: GU 2 beats 1 and 4 at NT = 1 (occupancy
+// 4 vs 2 waves/SIMD, measured)
+constexpr int kGramGU = 2;
 
 constexpr int kGramThreadsQL = 1024;  // alpha_Q in LDS: one 110 KB workgroup per CU, 16 waves
 
@@ -744,7 +738,6 @@ static const void* gram_kernel(bool general, bool weighted, bool ql) {
   if (general)
     return weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, true, false, kGramThreads>)
                     : reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, false, false, kGramThreads>);
-  const int gu = gram_gu(NT);
   if (ql && NT == 1) {
     // 16 waves per CU need <= 128 VGPRs: GU 2
     return weighted ? reinterpret_cast<const void*>(&k_gram<M, 1, 1, 2, true, true, kGramThreadsQL>)
@@ -752,7 +745,7 @@ static const void* gram_kernel(bool general, bool weighted, bool ql) {
   }
 #define GRAM_FN(GU) (weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, true, false, kGramThreads>) \
                               : reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, false, false, kGramThreads>))
-  return gu == 1 ? GRAM_FN(1) : gu == 2 ? GRAM_FN(2) : GRAM_FN(4);
+  return GRAM_FN(kGramGU);
 #undef GRAM_FN
 }
 
@@ -864,11 +857,6 @@ static GramArgs base_args(lfe_ctx* c) {
 }
 
 static bool resid_rows_ok(const lfe_ctx* c, const GramArgs& a) {
-  static const int off = [] {
-    const char* e = getenv("LFE_RESID_LANES");  // tuning: 1 = lane-layout kernel
-    return e ? atoi(e) : 0;
-  }();
-  if (off == 1) return false;
   // p <= 12: the meat's upper triangle stays in registers (p = 16 would spill)
   const int PM = c->p <= 4 ? 4 : c->p <= 8 ? 8 : 12;
   return c->F == 2 && c->p <= 12 && c->p >= 2 && !a.w && a.la.P >= 0 && c->L.permuted &&
@@ -1145,11 +1133,7 @@ __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __r
 
 int launch_gram(lfe_ctx* c, double* host_gram) {
   GramArgs a = base_args(c);
-  static const int lanes = [] {
-    const char* e = getenv("LFE_DESIGN_LANES");  // tuning: 1 = lane-layout MFMA kernel
-    return e ? atoi(e) : 0;
-  }();
-  if (lanes != 1 && resid_rows_ok(c, a) && c->p <= 11) {
+  if (resid_rows_ok(c, a) && c->p <= 11) {
     LFE_TRY(ensure_dred(c, 260));
     std::vector<double> h(257);
     bool done = false;

@@ -17,6 +17,11 @@ namespace lfe {
 constexpr int kMaxFE = 8;        // FE dimensions supported per regression
 constexpr int kMaxCl = 16;       // cluster columns per CGM subset
 constexpr int kMaxCols = 63;     // p = 1 + k (+ instruments) <= 63 -> Gram width <= 64
+constexpr int kColStatHead = 64; // colstat: max |x_c| bits of every column before the per-chunk sums
+// iscratch (prepare_layout): [2 F] level counts, [2 kMaxFE] dropped rows, [+1] any-singleton flag,
+// [kIscratchCmax, + F) largest kept count per FE
+constexpr int kIscratchCmax = 2 * kMaxFE + 8;
+constexpr int kIscratchInts = kIscratchCmax + kMaxFE;
 constexpr int kBlock = 256;      // threads per workgroup for simple streaming kernels
 constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
 constexpr int kLdsBudget = 64 * 1024;  // bytes of LDS tables per sweep workgroup (2 WG per CU)
@@ -75,7 +80,7 @@ enum KernelId {
   K_PART_HIST = 0, K_SCAN, K_PART_SCATTER, K_COUNT, K_MARK, K_GROUP_SUMS, K_CROSS, K_CHECK, K_FINALIZE,
   K_CHECK_MAX, K_GRAM_DESIGN, K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_MISC, K_SYNTH,
   K_TP, K_TQ, K_SEG_BUILD, K_CLUSTER_SORT, K_GRAM_TABLES, K_LAYOUT_HIST, K_LAYOUT_BASE, K_LAYOUT_SCATTER,
-  K_TQ_REDUCE, K_NUM_KERNELS
+  K_TQ_REDUCE, K_FIX_SUMS, K_NUM_KERNELS
 };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 
@@ -267,6 +272,15 @@ struct lfe_ctx {
   // deterministic T_Q: per-(bucket, q) run sums reduced in bucket order (no cross-bucket atomics)
   double* tq_runs = nullptr;     // [nb * G_Q][p]
   size_t tq_runs_cap = 0;
+  // exact group sums (k_sums2_raw): the column statistics of the loaded rows (written by the
+  // partition, or k_col_stats) fix a per-column 2^-e quantum, and the group sums accumulate
+  // round(x / quantum) in int64, so their order never changes a bit (lfe_fast.hip)
+  double* colstat = nullptr;     // [kColStatHead + p * nchunks]: max |x_c| bits (as u64), then sum x_c^2 per column and chunk
+  size_t colstat_cap = 0;
+  int colstat_chunks = 0;        // chunks of per-chunk sums of squares written for this layout
+  double* fixq = nullptr;        // [3 * kMaxCols]: scale[c], quantum[c], qualified[c]
+  size_t fixq_cap = 0;
+  bool exact_sums = false;       // the last group sums ran k_sums2_raw (exact when fixq's flag is on)
   lfe::Timings tm;
   lfe::Prof prof;
 };
@@ -276,6 +290,7 @@ namespace lfe {
 // --- prep / partition (lfe_prep.hip) ---
 int prepare_layout(lfe_ctx* c);   // partition + counts + singleton marks
 int ensure_layout_orig(lfe_ctx* c);  // L.orig written (deferred by prepare_layout)
+int exact_sums_on(lfe_ctx* c, int* on);  // did the last group sums take the exact (int64) path
 
 // --- group sums (lfe_fast.hip) ---
 int sums4(lfe_ctx* c);
@@ -397,6 +412,33 @@ __device__ __forceinline__ double lds_row(const double* t, uint32_t row, uint32_
 }
 __device__ __forceinline__ double* lds_row_ptr(double* t, uint32_t row, uint32_t p8, uint32_t col8) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(t) + (__umul24(row, p8) + col8));
+}
+
+// one 64-bit DPP lane move (two 32-bit halves); lanes without a source (or outside ROWMASK)
+// get idv
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp64(double v, double idv) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(idv), __double2loint(v), CTRL, ROWMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(idv), __double2hiint(v), CTRL, ROWMASK, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// reductions over VALU lane moves (no LDS traffic) in a fixed order, so the result is the
+// same every run.  row16: row_shr 1/2/4/8 (a scan within each row of 16; lane 15 of a row
+// holds its total); wave63: then row_bcast:15 and row_bcast:31 - lane 63 holds the total
+template <class Op>
+__device__ __forceinline__ double row16_reduce15(double v, double idv, Op op) {
+  v = op(v, dpp64<0x111, 0xF>(v, idv));
+  v = op(v, dpp64<0x112, 0xF>(v, idv));
+  v = op(v, dpp64<0x114, 0xF>(v, idv));
+  v = op(v, dpp64<0x118, 0xF>(v, idv));
+  return v;
+}
+template <class Op>
+__device__ __forceinline__ double wave_reduce63(double v, double idv, Op op) {
+  v = row16_reduce15(v, idv, op);
+  v = op(v, dpp64<0x142, 0xA>(v, idv));
+  v = op(v, dpp64<0x143, 0xC>(v, idv));
+  return v;
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t h) {

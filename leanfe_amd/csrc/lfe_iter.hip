@@ -39,9 +39,9 @@ namespace lfe {
 // 1. bucket-local counting sort (segment and run layouts)
 // ===========================================================================
 // Key of a kept row: KEYQ ? its secondary code : its primary code - lo (the
-// offset in its bucket); value stored: the other one.  Stable and
-// deterministic (per-wave cursors ranked by LDS atomics in lane order, as in
-// the partition scatter of lfe_prep.hip).
+// offset in its bucket); value stored: the other one.  Deterministic: per-wave
+// 16-bit cursors, rows ranked within a wave from ballots (as in the partition
+// scatter of lfe_prep.hip), never by the return order of LDS atomics.
 
 // both layouts' per-item histograms in one pass over the codes: itemcnt1[item][h - lo]
 // (K1 = 2^s keys) and itemcnt2[item][q] (K2 = G_Q keys)
@@ -107,22 +107,101 @@ __global__ void k_ls_base(const int32_t* __restrict__ bitems, int nb, int K, int
 
 constexpr int kLsThreads = 512;
 constexpr int kLsWaves = kLsThreads / 64;
-// rows per thread of the local sort (LFE_LS_PER: 16 or 8; fewer rows, fewer registers, more
-// resident workgroups)
-static int ls_per() {
-  static const int v = [] {
-    const char* e = getenv("LFE_LS_PER");
-    return e && atoi(e) == 16 ? 16 : 8;
-  }();
-  return v;
+// rows per thread of the local sorts (16 rows, one 8192-row item per pass and one workgroup per
+// CU: 0.575 vs 0.51 ms for the layout phase)
+constexpr int kLsPer = 8;
+static int ls_per() { return kLsPer; }
+
+static __host__ __device__ inline int even(int K) { return (K + 1) & ~1; }  // 16-bit counter rows in words
+
+
+// LDS of the single-layout sort: per-wave 16-bit counters [kLsWaves][K], run / tot / delta [K],
+// the stage [kLsRows]
+static size_t ls_scatter_lds(int K, int per = 16) {
+  return sizeof(int32_t) * (3 * (size_t)K + (size_t)kLsThreads * per) + sizeof(uint16_t) * kLsWaves * (size_t)even(K);
 }
 
-static size_t ls_scatter_lds(int K, int ncur, int per = 16) {
-  return sizeof(int32_t) * ((size_t)ncur * K + 3 * (size_t)K + (size_t)kLsThreads * per);
+// Deterministic ranking of a sub-chunk's rows by key (both local sorts).  Every wave has its
+// own 16-bit counter per key (two per 32-bit word), so a row's slot is its wave's first slot
+// for the key (ls_offsets) + the counter value its returning LDS add got.  The adds of one wave
+// are issued in slot order without waits in between (lanes without a key add 0 to the wave's
+// spare word), a wave's LDS operations complete in issue order, and the lanes of one
+// instruction that hit the same counter are served in the LDS's fixed lane order; no other
+// wave touches the counters, so the layout - and with it the summation order of every
+// segmented sum over it - does not depend on how the waves are scheduled.  (Matching the
+// lanes of a key with one ballot per key bit, as the partition scatter does for its 8-bit
+// bucket ids, costs ~15 VALU ops per bit and row: 1.06 vs 0.33 ms for this kernel.)
+template <int PER>
+__device__ __forceinline__ void wave_rank(const int32_t (&key)[PER], uint32_t* cw, uint32_t* spare,
+                                          int32_t (&rank)[PER]) {
+  uint32_t old[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const bool act = key[k] >= 0;
+    const int sh = (key[k] & 1) << 4;
+    old[k] = atomicAdd(act ? &cw[key[k] >> 1] : spare, act ? (1u << sh) : 0u);
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) rank[k] = (int32_t)((old[k] >> ((key[k] & 1) << 4)) & 0xffffu);
 }
 
-// NCUR: cursor sets (kLsWaves: one per wave, stable; 1: shared, unstable)
-template <bool KEYQ, typename VT, int NCUR, int kLsPer>
+// per key j < K (cw: [kLsWaves][Kp] 16-bit counters): cw[w][j] <- the first slot of wave w's rows with key j in the sub-chunk,
+// delta[j] <- run[j] - (the key's first slot); the keys' offsets are an exclusive scan of the
+// totals (one thread per `per` keys, then the waves)
+__device__ void ls_offsets(uint16_t* cw, int Kp, int32_t* tot, const int32_t* run, int32_t* delta, int K,
+                           int32_t* wsum, int tid, int lane, int wave) {
+  for (int j = tid; j < K; j += kLsThreads) {
+    int32_t t = 0;
+    for (int w2 = 0; w2 < kLsWaves; ++w2) {
+      const int32_t h = cw[w2 * Kp + j];
+      cw[w2 * Kp + j] = (uint16_t)t;
+      t += h;
+    }
+    tot[j] = t;
+  }
+  __syncthreads();
+  const int per = (K + kLsThreads - 1) / kLsThreads;
+  const int b0 = tid * per;
+  int32_t sum = 0;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < K) sum += tot[b0 + k];
+  int32_t x = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int32_t wofs = 0;
+  for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[w2];
+  int32_t acc = x - sum + wofs;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < K) {
+      const int32_t t = tot[b0 + k];
+      tot[b0 + k] = acc;
+      acc += t;
+    }
+  __syncthreads();
+  for (int j = tid; j < K; j += kLsThreads) {
+    const int32_t boff = tot[j];
+    delta[j] = run[j] - boff;
+    for (int w2 = 0; w2 < kLsWaves; ++w2) cw[w2 * Kp + j] = (uint16_t)(cw[w2 * Kp + j] + boff);
+  }
+  __syncthreads();
+}
+
+// kept rows of the wave's sub-chunk slice -> wkept[wave] (lane 0)
+template <int PER>
+__device__ __forceinline__ void wave_kept(const int32_t (&key)[PER], int lane, int wave, int32_t* wkept) {
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) cnt += __popcll(__ballot(key[k] >= 0));
+  if (lane == 0) wkept[wave] = cnt;
+}
+
+// one layout (the fallback when both do not fit in LDS together): KEYQ ? the run layout (key q,
+// value h - lo) : the segment layout (key h - lo, value q)
+template <bool KEYQ, typename VT, int kLsPer>
 __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restrict__ items,
                                                            const int32_t* __restrict__ codeP,
                                                            const int32_t* __restrict__ codeQ, int s, int K,
@@ -132,12 +211,14 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
                                                            VT* __restrict__ out) {
   constexpr int kLsRows = kLsThreads * kLsPer;
   extern __shared__ int32_t sm[];
-  int32_t* cur = sm;              // [NCUR][K]
-  int32_t* run = cur + NCUR * K;  // [K] next free slot of each key
-  int32_t* tot = run + K;             // [K]
-  int32_t* delta = tot + K;           // [K]
-  int32_t* stage = delta + K;         // [kLsRows] slot keys, then slot values
-  __shared__ int32_t wsum[kLsWaves];
+  int32_t* run = sm;             // [K] next free slot of each key
+  int32_t* tot = run + K;        // [K]
+  int32_t* delta = tot + K;      // [K]
+  int32_t* stage = delta + K;    // [kLsRows] slot keys, then slot values
+  const int Kp = even(K);
+  uint16_t* cw = reinterpret_cast<uint16_t*>(stage + kLsRows);  // [kLsWaves][Kp]
+  __shared__ int32_t wsum[kLsWaves], wkept[kLsWaves];
+  __shared__ uint32_t spare[kLsWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int item = xitems[blockIdx.x];  // XCD-grouped order (build_items)
   if (item < 0) return;
@@ -146,14 +227,13 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
   for (int j = tid; j < K; j += kLsThreads)
     run[j] = off[(int64_t)it.x * K + j] + itembase[(int64_t)item * K + j];
   // sub-chunks start at multiples of 4 rows and slots k .. k + 3 of a lane are 4 consecutive
-  // rows, so the codes come in 16-byte loads (rows before it.y are masked; the shared cursor
-  // set makes the order within a key free anyway)
+  // rows, so the codes come in 16-byte loads (rows before it.y are masked)
   static_assert(kLsPer % 4 == 0, "rows per thread in fours");
   for (int32_t r0 = it.y & ~3; r0 < it.z; r0 += kLsRows) {
     const int32_t r1 = min(it.z, r0 + kLsRows);
     const int32_t wbase = r0 + wave * kLsPer * 64;
     __syncthreads();
-    for (int j = tid; j < NCUR * K; j += kLsThreads) cur[j] = 0;
+    for (int j = tid; j < kLsWaves * Kp / 2; j += kLsThreads) reinterpret_cast<uint32_t*>(cw)[j] = 0u;
     __syncthreads();
     int32_t key[kLsPer], val[kLsPer];
 #pragma unroll
@@ -169,65 +249,28 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
       for (int t = 0; t < 4; ++t) {
         const int32_t i = i0 + t;
         key[k + t] = -1;
+        val[k + t] = 0;
         if (i >= it.y && i < r1 && gv[t] >= 0) {
           key[k + t] = KEYQ ? qv[t] : gv[t] - lo;
           val[k + t] = KEYQ ? gv[t] - lo : qv[t];
-          atomicAdd(&cur[(NCUR > 1 ? wave : 0) * K + key[k + t]], 1);
         }
       }
     }
-    __syncthreads();
-    for (int j = tid; j < K; j += kLsThreads) {  // per key: exclusive scan over waves
-      int32_t t = 0;
-      for (int w2 = 0; w2 < NCUR; ++w2) {
-        const int32_t hh = cur[w2 * K + j];
-        cur[w2 * K + j] = t;
-        t += hh;
-      }
-      tot[j] = t;
-    }
-    __syncthreads();
-    {  // exclusive scan of tot over keys
-      const int per = (K + kLsThreads - 1) / kLsThreads;
-      const int b0 = tid * per;
-      int32_t sum = 0;
-      for (int k = 0; k < per; ++k)
-        if (b0 + k < K) sum += tot[b0 + k];
-      int32_t x = sum;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      if (lane == 63) wsum[wave] = x;
-      __syncthreads();
-      int32_t wofs = 0;
-      for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[w2];
-      int32_t acc = x - sum + wofs;
-      __syncthreads();
-      for (int k = 0; k < per; ++k)
-        if (b0 + k < K) {
-          const int32_t t = tot[b0 + k];
-          tot[b0 + k] = acc;
-          acc += t;
-        }
-    }
-    __syncthreads();
-    for (int j = tid; j < K; j += kLsThreads) {
-      const int32_t boff = tot[j];
-      delta[j] = run[j] - boff;
-      for (int w2 = 0; w2 < NCUR; ++w2) cur[w2 * K + j] += boff;
-    }
-    __syncthreads();
     int32_t pos[kLsPer];
+    wave_rank(key, reinterpret_cast<uint32_t*>(cw + wave * Kp), &spare[wave], pos);
+    wave_kept(key, lane, wave, wkept);
+    __syncthreads();
+    ls_offsets(cw, Kp, tot, run, delta, K, wsum, tid, lane, wave);
+    int32_t nk = 0;  // kept rows of this sub-chunk
+    for (int w2 = 0; w2 < kLsWaves; ++w2) nk += wkept[w2];
 #pragma unroll
     for (int k = 0; k < kLsPer; ++k)
       if (key[k] >= 0) {
-        pos[k] = atomicAdd(&cur[(NCUR > 1 ? wave : 0) * K + key[k]], 1);
+        pos[k] += cw[wave * Kp + key[k]];
         stage[pos[k]] = key[k];
       }
     __syncthreads();
     // each thread keeps the destinations of the slots it writes out (j = tid + k * threads)
-    const int32_t nk = cur[(NCUR - 1) * K + (K - 1)];  // kept rows of this sub-chunk
     int32_t dd[kLsPer];
 #pragma unroll
     for (int k = 0; k < kLsPer; ++k) {
@@ -243,13 +286,14 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
     for (int k = 0; k < kLsPer; ++k)
       if (dd[k] >= 0) out[dd[k]] = (VT)stage[tid + k * kLsThreads];
     __syncthreads();
-    for (int j = tid; j < K; j += kLsThreads) run[j] = delta[j] + cur[(NCUR - 1) * K + j];
+    // next sub-chunk: each key continues after this one's rows (its end = the next key's start)
+    for (int j = tid; j < K; j += kLsThreads) run[j] = delta[j] + (j + 1 < K ? tot[j + 1] : nk);
   }
 }
 
 // Both layouts in one pass over the codes: the segment layout (key h - lo, value q -> seg_q)
-// and the run layout (key q, value h - lo -> run_h) of the same sub-chunk are ranked together
-// (shared cursors, as k_ls_scatter<.., 1, ..>), so the two code columns are read once.
+// and the run layout (key q, value h - lo -> run_h) of the same sub-chunk, ranked with the
+// same deterministic wave ranking as k_ls_scatter, so the two code columns are read once.
 struct Ls2Args {
   const int4* items;
   const int32_t* codeP;
@@ -265,7 +309,8 @@ struct Ls2Args {
 };
 
 static size_t ls2_lds(int K1, int K2, int per) {
-  return sizeof(int32_t) * (4 * ((size_t)K1 + K2) + 2 * (size_t)kLsThreads * per);
+  return sizeof(int32_t) * (3 * ((size_t)K1 + K2) + 2 * (size_t)kLsThreads * per) +
+         sizeof(uint16_t) * kLsWaves * ((size_t)even(K1) + even(K2));
 }
 
 template <int kLsPer>
@@ -273,17 +318,19 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter2(Ls2Args a) {
   constexpr int kLsRows = kLsThreads * kLsPer;
   extern __shared__ int32_t sm[];
   const int K1 = a.K1, K2 = a.K2;
-  int32_t* cur1 = sm;           // [K1]
-  int32_t* cur2 = cur1 + K1;    // [K2]
-  int32_t* run1 = cur2 + K2;    // [K1] next free slot of each key
+  int32_t* run1 = sm;           // [K1] next free slot of each key
   int32_t* run2 = run1 + K1;    // [K2]
-  int32_t* tot1 = run2 + K2;    // [K1] (then the keys' local offsets)
+  int32_t* tot1 = run2 + K2;    // [K1] the keys' local offsets
   int32_t* tot2 = tot1 + K1;    // [K2]
   int32_t* del1 = tot2 + K2;    // [K1]
   int32_t* del2 = del1 + K1;    // [K2]
   int32_t* st1 = del2 + K2;     // [kLsRows]
   int32_t* st2 = st1 + kLsRows; // [kLsRows]
-  __shared__ int32_t wsum[kLsWaves];
+  const int K1p = even(K1), K2p = even(K2);
+  uint16_t* cw1 = reinterpret_cast<uint16_t*>(st2 + kLsRows);  // [kLsWaves][K1p]
+  uint16_t* cw2 = cw1 + kLsWaves * K1p;                         // [kLsWaves][K2p]
+  __shared__ int32_t wsum[kLsWaves], wkept[kLsWaves];
+  __shared__ uint32_t spare[kLsWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int item = a.xitems[blockIdx.x];  // XCD-grouped order (build_items)
   if (item < 0) return;
@@ -293,38 +340,12 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter2(Ls2Args a) {
     run1[j] = a.off1[(int64_t)it.x * K1 + j] + a.base1[(int64_t)item * K1 + j];
   for (int j = tid; j < K2; j += kLsThreads)
     run2[j] = a.off2[(int64_t)it.x * K2 + j] + a.base2[(int64_t)item * K2 + j];
-  // exclusive scan of tot[0, K) in place (one thread per `per` keys, then the waves)
-  auto scan_keys = [&](int32_t* tot, int K) {
-    const int per = (K + kLsThreads - 1) / kLsThreads;
-    const int b0 = tid * per;
-    int32_t sum = 0;
-    for (int k = 0; k < per; ++k)
-      if (b0 + k < K) sum += tot[b0 + k];
-    int32_t x = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    int32_t wofs = 0;
-    for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[w2];
-    int32_t acc = x - sum + wofs;
-    __syncthreads();
-    for (int k = 0; k < per; ++k)
-      if (b0 + k < K) {
-        const int32_t t = tot[b0 + k];
-        tot[b0 + k] = acc;
-        acc += t;
-      }
-  };
   static_assert(kLsPer % 4 == 0, "rows per thread in fours");
   for (int32_t r0 = it.y & ~3; r0 < it.z; r0 += kLsRows) {
     const int32_t r1 = min(it.z, r0 + kLsRows);
     const int32_t wbase = r0 + wave * kLsPer * 64;
     __syncthreads();
-    for (int j = tid; j < K1; j += kLsThreads) cur1[j] = 0;
-    for (int j = tid; j < K2; j += kLsThreads) cur2[j] = 0;
+    for (int j = tid; j < kLsWaves * (K1p + K2p) / 2; j += kLsThreads) reinterpret_cast<uint32_t*>(cw1)[j] = 0u;
     __syncthreads();
     int32_t hk[kLsPer], qk[kLsPer];  // h - lo (key of layout 1) and q (key of layout 2); -1: not kept
 #pragma unroll
@@ -339,45 +360,29 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter2(Ls2Args a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int32_t i = i0 + t;
-        hk[k + t] = -1;
-        qk[k + t] = 0;
-        if (i >= it.y && i < r1 && gv[t] >= 0) {
-          hk[k + t] = gv[t] - lo;
-          qk[k + t] = qv[t];
-          atomicAdd(&cur1[hk[k + t]], 1);
-          atomicAdd(&cur2[qk[k + t]], 1);
-        }
+        const bool kept = i >= it.y && i < r1 && gv[t] >= 0;
+        hk[k + t] = kept ? gv[t] - lo : -1;
+        qk[k + t] = kept ? qv[t] : -1;
       }
     }
-    __syncthreads();
-    for (int j = tid; j < K1; j += kLsThreads) tot1[j] = cur1[j];
-    for (int j = tid; j < K2; j += kLsThreads) tot2[j] = cur2[j];
-    __syncthreads();
-    scan_keys(tot1, K1);
-    __syncthreads();
-    scan_keys(tot2, K2);
-    __syncthreads();
-    for (int j = tid; j < K1; j += kLsThreads) {
-      del1[j] = run1[j] - tot1[j];
-      cur1[j] = tot1[j];
-    }
-    for (int j = tid; j < K2; j += kLsThreads) {
-      del2[j] = run2[j] - tot2[j];
-      cur2[j] = tot2[j];
-    }
-    __syncthreads();
     int32_t p1[kLsPer], p2[kLsPer];
+    wave_rank(hk, reinterpret_cast<uint32_t*>(cw1 + wave * K1p), &spare[wave], p1);
+    wave_rank(qk, reinterpret_cast<uint32_t*>(cw2 + wave * K2p), &spare[wave], p2);
+    wave_kept(hk, lane, wave, wkept);
+    __syncthreads();
+    ls_offsets(cw1, K1p, tot1, run1, del1, K1, wsum, tid, lane, wave);
+    ls_offsets(cw2, K2p, tot2, run2, del2, K2, wsum, tid, lane, wave);
+    int32_t nk = 0;  // kept rows of this sub-chunk
+    for (int w2 = 0; w2 < kLsWaves; ++w2) nk += wkept[w2];
 #pragma unroll
     for (int k = 0; k < kLsPer; ++k)
       if (hk[k] >= 0) {
-        p1[k] = atomicAdd(&cur1[hk[k]], 1);
-        p2[k] = atomicAdd(&cur2[qk[k]], 1);
+        p1[k] += cw1[wave * K1p + hk[k]];
+        p2[k] += cw2[wave * K2p + qk[k]];
         st1[p1[k]] = hk[k];
         st2[p2[k]] = qk[k];
       }
     __syncthreads();
-    // kept rows of this sub-chunk = the last key's end
-    const int32_t nk = cur1[K1 - 1];
     int32_t d1[kLsPer], d2[kLsPer];
 #pragma unroll
     for (int k = 0; k < kLsPer; ++k) {
@@ -399,8 +404,8 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter2(Ls2Args a) {
       if (d2[k] >= 0) a.run_h[d2[k]] = (uint16_t)st2[tid + k * kLsThreads];
     }
     __syncthreads();
-    for (int j = tid; j < K1; j += kLsThreads) run1[j] = del1[j] + cur1[j];
-    for (int j = tid; j < K2; j += kLsThreads) run2[j] = del2[j] + cur2[j];
+    for (int j = tid; j < K1; j += kLsThreads) run1[j] = del1[j] + (j + 1 < K1 ? tot1[j + 1] : nk);
+    for (int j = tid; j < K2; j += kLsThreads) run2[j] = del2[j] + (j + 1 < K2 ? tot2[j + 1] : nk);
   }
 }
 
@@ -424,11 +429,9 @@ __global__ void k_unit_bounds(const int32_t* __restrict__ seg_off, int32_t H, in
 }
 
 // bucket-local counting sort of the kept rows given the per-item histograms
-// itemcnt [n_items][K] (k_ls_hist2); off = [nb K + 1] exclusive offsets.  Both
-// layouts rank rows with one shared LDS cursor set (unstable inside a segment or
-// run): the order there only sets the summation order of K1 / K2, and the sweeps
-// are not bit-reproducible anyway (K2's cross-workgroup atomics into T_Q); the
-// stable per-wave ranking costs O(K x waves) LDS work per sub-chunk.
+// itemcnt [n_items][K] (k_ls_hist2); off = [nb K + 1] exclusive offsets.  The rows of a
+// key are placed in the deterministic wave-ranking order (ls_offsets / wave_rank), so the
+// summation order of K1 / K2 - and with it every bit of the sweeps - repeats run to run.
 template <bool KEYQ, typename VT>
 static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off, size_t& off_cap, VT* out) {
   auto& L = c->L;
@@ -444,20 +447,14 @@ static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off,
   LFE_HIP(hipGetLastError());
   if (!out) return LFE_OK;  // per-key totals and item bases only (the fused sort scans both)
   LFE_TRY(exclusive_scan(c, off, (int64_t)m + 1));
-  constexpr int NCUR = 1;
   const int per = ls_per();
-  const size_t lds = ls_scatter_lds(K, NCUR, per);
-  const void* fn = per == 16 ? reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, NCUR, 16>)
-                             : reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, NCUR, 8>);
+  const size_t lds = ls_scatter_lds(K, per);
+  const void* fn = reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, kLsPer>);
   if (lds > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   {
     ProfScope _ps(c, K_LAYOUT_SCATTER);
-    if (per == 16)
-      hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR, 16>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream,
-                         items, L.code[P], L.code[Q], L.s, K, off, itemcnt, c->xitems_d, out);
-    else
-      hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, NCUR, 8>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream,
-                         items, L.code[P], L.code[Q], L.s, K, off, itemcnt, c->xitems_d, out);
+    hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, kLsPer>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream,
+                       items, L.code[P], L.code[Q], L.s, K, off, itemcnt, c->xitems_d, out);
   }
   LFE_HIP(hipGetLastError());
   return LFE_OK;
@@ -490,13 +487,9 @@ static int build_layouts(lfe_ctx* c, int Q) {
   c->hists_kept = false;
   LFE_TRY(ensure_i32(c, c->seg_q, c->seg_q_cap, (size_t)c->ld));
   LFE_TRY(ensure_u16(c, c->run_h, c->run_h_cap, (size_t)c->ld));
-  static const int fused_env = [] {
-    const char* e = getenv("LFE_LS_FUSED");  // tuning: 0 = one local sort per layout
-    return e ? atoi(e) : 1;
-  }();
   const int per = ls_per();
   const size_t lds2 = ls2_lds(B, G_Q, per);
-  if (fused_env && lds2 <= 150 * 1024) {
+  if (lds2 <= 150 * 1024) {
     LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, nullptr)));
     LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, nullptr)));
     LFE_TRY(exclusive_scan2(c, c->seg_off, (int64_t)L.nb * B + 1, c->run_off, (int64_t)L.nb * G_Q + 1));
@@ -514,8 +507,7 @@ static int build_layouts(lfe_ctx* c, int Q) {
     a.xitems = c->xitems_d;
     a.seg_q = c->seg_q;
     a.run_h = c->run_h;
-    const void* fn = per == 16 ? reinterpret_cast<const void*>(&k_ls_scatter2<16>)
-                               : reinterpret_cast<const void*>(&k_ls_scatter2<8>);
+    const void* fn = reinterpret_cast<const void*>(&k_ls_scatter2<kLsPer>);
     if (lds2 > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
     {
       ProfScope _ps(c, K_LAYOUT_SCATTER);
@@ -977,7 +969,7 @@ bool fast_layout_ok(const lfe_ctx* c) {
   const int64_t G_Q = c->fe[Q].G, B = 1ll << c->L.s;
   return (G_Q + 1) * p * 8 <= kIterLds                 // K1: alpha_Q in LDS
          && (B + 1) * p * 8 <= 96 * 1024               // K2: primary slice in LDS
-         && ls_scatter_lds((int)G_Q, 1) <= 150 * 1024  // run layout sort
+         && ls_scatter_lds((int)G_Q, ls_per()) <= 150 * 1024  // run layout sort
          && (B + G_Q) * 4 <= 64 * 1024                 // both histograms in LDS
          && B <= 65536;                                // uint16 offsets
 }
@@ -1034,14 +1026,9 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   tq.alphaP = fp.alpha;
   LFE_TRY(ensure_f64(c, c->tq_runs, c->tq_runs_cap, (size_t)c->L.nb * fq.G * p));
   tq.runs = c->tq_runs;
-  static const int split_env = [] {
-    const char* e = getenv("LFE_TQ_SPLIT");  // tuning
-    return e ? atoi(e) : 0;
-  }();
   // about four workgroups per CU in all (two resident at a time), so no CU is left with a lone
   // tail: 196 buckets -> 5 per bucket (tq 0.61 -> 0.49 ms per step at 50M rows, measured)
-  tq.split = split_env > 0 ? split_env
-                           : std::max(kTqSplitDefault / 2, (int)std::lround(4.0 * c->n_cu / std::max(c->L.nb, 1)));
+  tq.split = std::max(kTqSplitDefault / 2, (int)std::lround(4.0 * c->n_cu / std::max(c->L.nb, 1)));
   // sweep 1's Q projection: alpha_P = 0 -> alpha_Q = S_Q / n_Q (alpha_P is first written by K1,
   // which covers every primary group)
   LFE_TRY(fin_check(c, Q, nullptr, nullptr, fq.alpha, false));

@@ -226,6 +226,7 @@ struct ScatterArgs {
   const int32_t* scanned;  // [nb][nchunks] exclusive destinations
   int cols;                // move the X / w columns and the codes
   int want_orig;           // write the input row index of each layout row
+  double* colstat;         // with cols: max |x_c| (u64 bits, atomicMax) and per-chunk sums of x_c^2
 };
 
 // a global-memory byte pointer the compiler keeps in SGPRs (it is the same in every lane), so
@@ -259,6 +260,7 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   int32_t* delta = cur + kWaves * a.nb;                           // [nb]
   int32_t* tot = delta + a.nb;                                    // [nb + 1]
   __shared__ int32_t wsum[16];
+  __shared__ double wstat[2][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int chunk = xcd_chunk(blockIdx.x, a.nchunks);
   const int64_t r0 = (int64_t)chunk * R, r1 = min(a.n, r0 + R);
@@ -422,15 +424,52 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
             *reinterpret_cast<__attribute__((address_space(1))) double*>(dst + (off_t)dd[k0 + u] * 8) = t[u];
       }
     };
+    // column statistics for the exact group sums (lfe_fast.hip): max |x| and sum x^2 of this
+    // chunk's rows (rows past the end load as 0).  Each wave reduces its values over DPP lane
+    // moves (VALU only: the stage keeps the LDS busy); after the barrier, lanes 0-15 of wave
+    // c % 16 combine the 16 waves the same way and lane 15 writes the chunk's figures.
+    const auto fmaxop = [](double x, double y) { return fmax(x, y); };
+    const auto addop = [](double x, double y) { return x + y; };
+    auto col_stats = [&](const double (&v)[PER]) {
+      double m = 0.0, q = 0.0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        m = fmax(m, fabs(v[k]));
+        q = __builtin_fma(v[k], v[k], q);
+      }
+      // (fmax drops a NaN; the sum of squares keeps it, and the guard tests that sum)
+      m = wave_reduce63(m, 0.0, fmaxop);
+      q = wave_reduce63(q, 0.0, addop);
+      if (lane == 63) {
+        wstat[0][wave] = m;
+        wstat[1][wave] = q;
+      }
+    };
+    auto col_stats_out = [&](int c) {  // after the barrier that follows col_stats
+      if (wave != (c & (kWaves - 1)) || lane >= 16) return;
+      double m = lane < kWaves ? wstat[0][lane] : 0.0, q = lane < kWaves ? wstat[1][lane] : 0.0;
+      m = row16_reduce15(m, 0.0, fmaxop);
+      q = row16_reduce15(q, 0.0, addop);
+      if (lane == 15) {
+        a.colstat[kColStatHead + (int64_t)c * a.nchunks + chunk] = q;
+        atomicMax(reinterpret_cast<unsigned long long*>(a.colstat) + c, (unsigned long long)__double_as_longlong(m));
+      }
+    };
     // one register set: column c + 1 is loaded while column c is written out (two register
     // sets, loading c + 2 during c + 1's staging, measured 2.12 vs 2.09 ms)
     double v[PER];
     if (ncol > 0) load_col(0, v);
     for (int c = 0; c < ncol; ++c) {
       stage_col(v);
+#ifndef LFE_NO_COLSTAT
+      if (c < a.p) col_stats(v);
+#endif
       asm volatile("" ::: "memory");  // the next loads stay after the stage writes
       if (c + 1 < ncol) load_col(c + 1, v);
       __syncthreads();
+#ifndef LFE_NO_COLSTAT
+      if (c < a.p) col_stats_out(c);
+#endif
       write_col(c);
       __syncthreads();
     }
@@ -565,25 +604,29 @@ struct FinishCountsArgs {
   int32_t* cnt[kMaxFE];
   int32_t G[kMaxFE];
   int32_t* out;  // [2 F]: (levels kept, levels present) per FE
+  int32_t* cmax;  // [F]: largest kept count per FE (the exact group sums' bound, lfe_fast.hip)
 };
 
 __global__ void k_finish_counts(FinishCountsArgs a) {
   const int f = blockIdx.y;
   const int32_t G = a.G[f];
-  int la = 0, lb = 0;
+  int la = 0, lb = 0, mx = 0;
   for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
     const int32_t pre = a.pre[f][g], c = pre - a.drops[f][g];
     a.cnt[f][g] = c;
     la += c > 0;
     lb += pre > 0;
+    mx = max(mx, c);
   }
   for (int off = 32; off > 0; off >>= 1) {
     la += __shfl_down(la, off, 64);
     lb += __shfl_down(lb, off, 64);
+    mx = max(mx, __shfl_down(mx, off, 64));
   }
   if ((threadIdx.x & 63) == 0) {
     if (la) atomicAdd(&a.out[2 * f], la);
     if (lb) atomicAdd(&a.out[2 * f + 1], lb);
+    if (mx) atomicMax(&a.cmax[f], mx);
   }
 }
 
@@ -599,11 +642,7 @@ static int choose_shift(int32_t G, int smin) {
   int s = 0;
   while ((1ll << s) < G && s < 8) ++s;       // small FE: one bucket
   if ((1ll << s) >= G) return s;
-  static const int smin_env = [] {
-    const char* e = getenv("LFE_SHIFT_MIN");  // tuning override
-    return e ? atoi(e) : 0;
-  }();
-  s = smin_env >= 8 && smin_env <= 12 ? smin_env : smin;
+  s = smin;
   while (((int64_t)G + (1ll << s) - 1) >> s > 2048) ++s;  // <= 2048 buckets (LDS cursors of the scatter)
   return s;
 }
@@ -689,6 +728,7 @@ static int launch_part_scatter(lfe_ctx* c, int cols, int orig) {
   a.scanned = c->pcounts;
   a.cols = cols;
   a.want_orig = orig;
+  a.colstat = c->colstat;
   a.nbits = 0;  // bits of a bucket id (ballot ranking)
   while ((1 << a.nbits) < L.nb) ++a.nbits;
   const int pgrid = ((g.nw + 7) / 8) * 8;  // xcd_chunk: a multiple of the 8 XCDs
@@ -722,6 +762,7 @@ int prepare_layout(lfe_ctx* c) {
   const int64_t n = c->n;
   c->sums_ready = false;
   c->seg_ready = false;
+  c->colstat_chunks = 0;  // the partition (or sums4's k_col_stats) writes them again
   c->clw.lay_valid = false;  // cluster columns follow the new layout
   // primary FE: most levels (ties -> first)
   L.P = -1;
@@ -743,7 +784,7 @@ int prepare_layout(lfe_ctx* c) {
   // two-FE sweeps; lfe_demean refuses the general sweeps in this mode)
   c->owner_on = c->world > 1 && c->owner_fe >= 0 && c->owner_fe == L.P && item_counts;
   // every count / drop / group-sum table and the scratch counters zeroed in one launch
-  LFE_TRY(ensure_iscratch(c, 2 * kMaxFE + 8));
+  LFE_TRY(ensure_iscratch(c, kIscratchInts));
   {
     std::vector<std::pair<void*, size_t>> z;
     for (int f = 0; f < c->F; ++f) {
@@ -752,7 +793,7 @@ int prepare_layout(lfe_ctx* c) {
       z.push_back({fe.drops, sizeof(int32_t) * fe.G});
       z.push_back({fe.S, sizeof(double) * (size_t)fe.G * c->p});
     }
-    z.push_back({c->iscratch, sizeof(int32_t) * (2 * kMaxFE + 8)});
+    z.push_back({c->iscratch, sizeof(int32_t) * kIscratchInts});
     LFE_TRY(zero_ranges(c, z));
     c->sums_zeroed = true;
   }
@@ -789,6 +830,10 @@ int prepare_layout(lfe_ctx* c) {
     if (cw == 16384 && nth != 1024) cw = 8192;
     const int per = (int)(cw / nth);
     const int nw = (int)((n + cw - 1) / cw);
+    // column statistics of the exact group sums, written by the scatter (max |x| by atomicMax)
+    LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nw * c->p));
+    LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
+    c->colstat_chunks = nw;
     const int64_t m = (int64_t)nb * nw;
     LFE_TRY(ensure_pcounts(c, (size_t)m + nb + 1, 0));
     {
@@ -898,6 +943,7 @@ int prepare_layout(lfe_ctx* c) {
       fa.G[f] = fe.G;
     }
     fa.out = c->iscratch;
+    fa.cmax = c->iscratch + kIscratchCmax;
     if (c->F > 0) {
       // few blocks: thousands of same-address adds would serialize
       hipLaunchKernelGGL(k_finish_counts, dim3(grid_for(gmax, kBlock, 32), c->F), dim3(kBlock), 0, c->stream, fa);

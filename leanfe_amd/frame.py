@@ -109,8 +109,23 @@ def factorize(values, global_codes: bool = False, device=None) -> tuple[np.ndarr
             return v.astype(np.int32, copy=False), vmax + 1
         if device is not None and n < 2 ** 31 - 1 and (v.dtype != np.uint64 or vmax < 2 ** 63):
             return device.factorize_ids(v.astype(np.int64, copy=False))
+    elif device is not None and n < 2 ** 31 - 1 and v.dtype in (np.float64, np.float32):
+        return device.factorize_ids(float_order_keys(v))
     uniq, inv = np.unique(v, return_inverse=True)
     return inv.astype(np.int32).ravel(), int(uniq.size)
+
+
+def float_order_keys(v: np.ndarray) -> np.ndarray:
+    """int64 keys whose signed order is the float order of ``v`` (np.unique's): -0.0 and 0.0 map
+    to one key, every NaN to one key above +inf; so the device's sorted-unique codes of the
+    keys are np.unique's codes of the floats."""
+    f = np.ascontiguousarray(v, dtype=np.float64)
+    f = np.where(f == 0.0, 0.0, f)  # -0.0 -> +0.0
+    b = f.view(np.int64).copy()
+    b[np.isnan(f)] = 0x7FF8000000000000
+    neg = b < 0
+    b[neg] ^= np.int64(0x7FFFFFFFFFFFFFFF)
+    return b
 
 
 def intersect(codes: list[np.ndarray], levels: list[int]) -> tuple[np.ndarray, int]:

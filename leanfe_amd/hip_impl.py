@@ -249,7 +249,7 @@ def _cluster_se(eng, cols, cluster_cols, sharded, Vb, to_meat, n_obs, df_resid, 
     OLS, gamma' M_Z gamma for IV, :473-602)."""
     cl_codes, cl_levels = [], []
     for c in cluster_cols:
-        cc, gg = frame.factorize(cols[c], global_codes=sharded)
+        cc, gg = frame.factorize(cols[c], global_codes=sharded, device=None if sharded else eng)
         cl_codes.append(cc)
         cl_levels.append(gg)
     cl_levels = dist.agree_levels(eng, cl_levels)
@@ -303,7 +303,7 @@ def _compress_fit(eng, cols, x_cols, fe_cols, fe_card, cluster_cols, v, vcov, ss
         # polars_impl.py:407-416 passes cluster_cols whatever vcov is: they join the group key
         cl_codes, cl_levels = [], []
         for c in cluster_cols:
-            cc, gg = frame.factorize(cols[c])
+            cc, gg = frame.factorize(cols[c], device=eng)
             cl_codes.append(cc)
             cl_levels.append(gg)
         eng.load_clusters(cl_codes, cl_levels)

@@ -1,0 +1,109 @@
+"""Deterministic reductions on the headline path.
+
+The two-FE fast path's group sums accumulate each column as round(x / quantum) in int64
+(lfe_fast.hip, k_sums2_raw / k_fix_quanta), the T_Q run sums are reduced in bucket order and
+the Gram / meat partials in block order, so solving the same panel twice must give
+bit-identical beta, SE, RSS and `iterations` - within one context and across two contexts.
+(The general sweeps - F >= 3, weights, one bucket - still rank their segment layouts with
+global cursor atomics and keep f64 atomic sums: parity-exact to 1e-10, not bit-reproducible;
+DESIGN.md §8.)
+The exact path must also keep parity with the CPU restatement (oracle/altproj.py,
+polars_impl.py:468-537) at the usual 1e-10 bar, and a column whose range defeats the fixed
+point (one huge outlier) must fall back to the f64 sums and still match."""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _solve(eng, vcov="hc1"):
+    import bench
+
+    return bench.solve_step(eng, vcov)
+
+
+def _same(a, b):
+    assert a["iterations"] == b["iterations"]
+    assert a["n_obs"] == b["n_obs"] and a["df_resid"] == b["df_resid"]
+    np.testing.assert_array_equal(a["beta"], b["beta"])
+    np.testing.assert_array_equal(a["se"], b["se"])
+    assert a["rss"] == b["rss"]
+
+
+@pytest.mark.parametrize("n,L", [(2_000_000, [20_000, 500]), (3_000_017, [100_000, 1_000])])
+def test_same_panel_twice_is_bit_identical(n, L):
+    from leanfe_amd import synth
+    from leanfe_amd._lib import Engine
+
+    k = 10
+    runs = []
+    for _ in range(2):  # two contexts
+        with Engine(0) as eng:
+            eng.synth_load(n, k, L, synth.betas(k), seed=777)
+            first = _solve(eng)
+            assert eng.exact_sums(), "the headline geometry should take the exact group sums"
+            second = _solve(eng)  # same context: layout, sums and sweeps rebuilt
+            _same(first, second)
+            runs.append(first)
+    _same(runs[0], runs[1])
+
+
+def _fit_pair(data, xs):
+    from leanfe_amd import leanfe_hip
+    from oracle import altproj
+
+    r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], strategy="alt_proj", vcov="HC1",
+                   quiet=True, device=0)
+    o = altproj.fit(data, "y", xs, ["fe1", "fe2"], vcov="HC1")
+    b = np.array([r.coefs[x] for x in xs])
+    s = np.array([r.std_errors[x] for x in xs])
+    assert r.iterations == o["iterations"] and r.n_obs == o["n_obs"]
+    np.testing.assert_allclose(b, o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(s, o["se"], rtol=1e-10, atol=0)
+    return b, s, r.iterations
+
+
+def test_exact_sums_keep_oracle_parity_and_outlier_falls_back():
+    from leanfe_amd import synth
+
+    xs = [f"x{j + 1}" for j in range(6)]
+    data = synth.panel(400_000, 6, [8_000, 300], seed=4242)
+    b1, s1, it1 = _fit_pair(data, xs)
+    b2, s2, it2 = _fit_pair(data, xs)
+    np.testing.assert_array_equal(b1, b2)
+    np.testing.assert_array_equal(s1, s2)
+    assert it1 == it2
+    # one value 1e6 x the column's RMS: max|x| > 64 RMS, so that fit takes the f64 sums
+    data = dict(data)
+    x3 = np.array(data["x3"], copy=True)
+    x3[12345] = 1e6
+    data["x3"] = x3
+    _fit_pair(data, xs)
+
+
+def test_outlier_column_reports_f64_sums():
+    from leanfe_amd import synth
+    from leanfe_amd._lib import Engine
+
+    data = synth.panel(200_000, 3, [5_000, 200], seed=99)
+    cols = [np.ascontiguousarray(data[c], dtype=np.float64) for c in ["y", "x1", "x2", "x3"]]
+    cols[2] = cols[2].copy()
+    cols[2][7] = 1e9
+    codes = [np.ascontiguousarray(data[f], dtype=np.int32) for f in ["fe1", "fe2"]]
+    with Engine(0) as eng:
+        eng.load(cols, codes, [5_000, 200])
+        eng.drop_singletons()
+        assert not eng.exact_sums()
+        eng.load([np.ascontiguousarray(data[c], dtype=np.float64) for c in ["y", "x1", "x2", "x3"]], codes,
+                 [5_000, 200])
+        eng.drop_singletons()
+        assert eng.exact_sums()

@@ -92,3 +92,41 @@ def test_auto_strategy_ratio_and_device_factorized_ids():
     for x in ("x1", "x2"):
         assert r.coefs[x] == pytest.approx(ref.coefs[x], rel=1e-12)
         assert r.std_errors[x] == pytest.approx(ref.std_errors[x], rel=1e-12)
+
+
+@pytest.mark.parametrize("case", ["floats", "floats_nan_signed_zero"])
+def test_factorize_float_ids_match_np_unique(eng, case):
+    """Float FE / cluster ids go through the device sort via order-preserving int64 keys
+    (frame.float_order_keys): codes equal np.unique's inverse."""
+    from leanfe_amd import frame
+    rng = np.random.default_rng(5)
+    v = rng.normal(size=300_000) * 1e6
+    v = np.round(v[rng.integers(0, 40_000, v.size)], 3)
+    if case == "floats_nan_signed_zero":
+        v[::97] = np.nan
+        v[::89] = 0.0
+        v[::83] = -0.0
+        v[::79] = -np.inf
+    codes, G = frame.factorize(v, device=eng)
+    uniq, inv = np.unique(v, return_inverse=True)
+    assert G == uniq.size
+    np.testing.assert_array_equal(codes, inv.ravel())
+
+
+def test_sparse_cluster_ids_factorized_on_device_same_fit():
+    """Sparse int64 / float cluster ids (factorized on the device, hip_impl._cluster_se) give
+    the same two-way clustered fit as their dense codes (std_errors.py:354-441)."""
+    from leanfe_amd import leanfe_hip
+    n, L = 150_000, [2000, 60, 300]
+    data = synth.panel(n, 3, L, seed=23)
+    ref = leanfe_hip(data, formula="y ~ x1 + x2 + x3 | fe1 + fe2", vcov="cluster",
+                     cluster_cols=["fe2", "fe3"], quiet=True)
+    sparse = dict(data)
+    sparse["fe3"] = data["fe3"].astype(np.int64) * 7_000_000_000_019 + 11
+    sparse["fe2"] = data["fe2"].astype(np.float64) * 0.37 - 5.0
+    r = leanfe_hip(sparse, formula="y ~ x1 + x2 + x3 | fe1 + fe2", vcov="cluster",
+                   cluster_cols=["fe2", "fe3"], quiet=True)
+    assert r.n_clusters == ref.n_clusters and r.n_obs == ref.n_obs and r.iterations == ref.iterations
+    for x in ("x1", "x2", "x3"):
+        assert r.coefs[x] == pytest.approx(ref.coefs[x], rel=1e-12)
+        assert r.std_errors[x] == pytest.approx(ref.std_errors[x], rel=1e-12)

@@ -83,7 +83,7 @@ def test_synth_device_equals_host_bit_exact():
     (6, 400_000, (700_000, 50), 2, "iid"),           # more levels than rows: many singletons, nb > 512
     (7, 300_000, (20000, 300), 20, "HC1"),           # p = 21: two 16-column slots (NT = 2) in every kernel
     (8, 120_000, (4000, 150), 40, "iid"),            # p = 41: NT = 3
-    (9, 300_000, (20000, 7300), 1, "HC1"),           # G_Q = 7300, p = 2: separate layout sorts (fused > 150 KB LDS)
+    (9, 300_000, (20000, 4200), 1, "HC1"),           # G_Q = 4200, p = 2: separate layout sorts (fused > 150 KB LDS)
 ])
 def test_random_panels_vs_oracle(seed, n, L, k, vcov):
     data = synth.panel(n, k, list(L), seed=seed)

@@ -226,3 +226,15 @@ def test_stream_parquet_batches_cover_rows_in_order(tmp_path):
         seen.append((row0, len(b["y"])))
     assert seen[0][0] == 0 and sum(m for _, m in seen) == n
     assert all(r + m == r2 for (r, m), (r2, _) in zip(seen, seen[1:]))
+
+
+def test_float_order_keys_preserve_np_unique_order():
+    """The int64 keys behind device-factorized float ids sort like np.unique sorts the floats
+    (-0.0 == 0.0, NaNs last and alike), so sorted-unique codes agree."""
+    from leanfe_amd.frame import float_order_keys
+    v = np.array([3.5, -0.0, 0.0, np.nan, -np.inf, np.inf, -2.25, 1e-300, -1e-300, np.nan, 3.5, -7e10])
+    k = float_order_keys(v)
+    uk, ik = np.unique(k, return_inverse=True)
+    uv, iv = np.unique(v, return_inverse=True)
+    assert uk.size == uv.size
+    np.testing.assert_array_equal(ik.ravel(), iv.ravel())

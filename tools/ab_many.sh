@@ -12,7 +12,10 @@ import json, sys
 lib, keys = sys.argv[1], [k for k in sys.argv[2].split(",") if k]
 d = json.loads([l for l in open("gpurun_out/ab.log") if l.startswith("{")][-1])
 ks = d["kernels_ms"]
-print(f"{lib:>28}: {d['ms_per_step']:.3f} ms/step  " + "  ".join(f"{k}={ks[k][0]:.4f}" for k in keys if k in ks), flush=True)
+st = d.get("roofline", {}).get("step", {})
+print(f"{lib:>28}: {d['ms_per_step']:.3f} ms/step  kern={st.get('kernel_ms', 0):.3f} gap={st.get('host_gap_ms', 0):.3f}  " + "  ".join(f"{k}={ks[k][0]:.4f}" for k in keys if k in ks), flush=True)
+if len(keys) == 1 and keys[0] == "all":
+    print("   " + " ".join(f"{k}={v[0]:.4f}/{v[1]}" for k, v in ks.items()), flush=True)
 PY
   done
 done

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Tuning sweep on one box: bench.py once per value of an engine tuning variable.
-#   VAR=LFE_TQ_SPLIT VALUES="1 2 4" KEYS="tq,tp" bash tools/tune_env.sh
+#   VAR=SOME_ENV VALUES="1 2 4" KEYS="tq,tp" bash tools/tune_env.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
