@@ -959,16 +959,18 @@ __global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restri
 #pragma unroll
     for (int i = 0; i < PM; ++i) acc[NG + i] += n * av[i];
   }
+  // wave sums over DPP lane moves (VALU; a shuffle reduction of the NA sums kept this kernel
+  // on ds_bpermute latency), then the four waves in order
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const auto addop = [](double x, double y) { return x + y; };
 #pragma unroll
   for (int e = 0; e < NA; ++e) {
-    double v = acc[e];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (lane == 0) red[wave][e] = v;
+    const double v = wave_reduce63(acc[e], 0.0, addop);
+    if (lane == 63) red[wave][e] = v;
   }
   __syncthreads();
   for (int e = threadIdx.x; e < NA; e += blockDim.x)
-    partial[(int64_t)blockIdx.x * NA + e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+    partial[(int64_t)blockIdx.x * NA + e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
 }
 
 // one block: the design tile [16][16] (column 0 = intercept, 1 + j = data column j)
@@ -982,10 +984,15 @@ __global__ __launch_bounds__(256) void k_tables_final(const double* __restrict__
   __shared__ double m[NA];
   __shared__ int bad;
   if (threadIdx.x == 0) bad = 0;
-  for (int e = threadIdx.x; e < NA; e += blockDim.x) {
-    double s = 0.0;
-    for (int b = 0; b < nblk; ++b) s += partial[(int64_t)b * NA + e];
-    m[e] = s;
+  {  // wave w sums the block partials of entries w, w + 4, ... (lanes over blocks, fixed order)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const auto addop = [](double x, double y) { return x + y; };
+    for (int e = wave; e < NA; e += 4) {
+      double s = 0.0;
+      for (int b = lane; b < nblk; b += 64) s += partial[(int64_t)b * NA + e];
+      s = wave_reduce63(s, 0.0, addop);
+      if (lane == 63) m[e] = s;
+    }
   }
   __syncthreads();
   for (int t = threadIdx.x; t < 256; t += blockDim.x) {
@@ -1034,7 +1041,7 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev) {
   t.q_on = (!c->owner_on || c->rank == 0) ? 1 : 0;
   const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
   const int NA = PM * (PM + 1) / 2 + PM;
-  const int nblk = grid_for((int64_t)t.G[0] + t.G[1], 256, 64);  // few partials: the final sum is serial
+  const int nblk = grid_for((int64_t)t.G[0] + t.G[1], 256, 256);  // the final sums the partials by waves
   LFE_TRY(ensure_scratch(c, (size_t)nblk * NA + NA));
   ProfScope _ps(c, K_GRAM_TABLES);
   double* part = c->scratch;

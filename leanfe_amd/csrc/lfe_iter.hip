@@ -911,17 +911,30 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
 }
 
 // T_Q[q][col] = sum over buckets b (in order) of runs[b][q][col]
-__global__ void k_tq_reduce(const double* __restrict__ runs, int nb, int64_t m, double* __restrict__ T) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
-    double t = 0.0;
-    int b = 0;
-    for (; b + 4 <= nb; b += 4) {  // four loads in flight, added in bucket order
-      const double v0 = runs[(int64_t)b * m + e], v1 = runs[(int64_t)(b + 1) * m + e];
-      const double v2 = runs[(int64_t)(b + 2) * m + e], v3 = runs[(int64_t)(b + 3) * m + e];
+// 16 consecutive entries per block (128-byte loads), 16 bucket slices (slice s: buckets s, s + 16,
+// ...), each thread four loads in flight; the slices are added in order: a fixed summation order
+constexpr int kTqRedE = 16, kTqRedS = 16;
+__global__ __launch_bounds__(256) void k_tq_reduce(const double* __restrict__ runs, int nb, int64_t m,
+                                                   double* __restrict__ T) {
+  __shared__ double part[kTqRedS][kTqRedE];
+  const int ei = threadIdx.x % kTqRedE, sl = threadIdx.x / kTqRedE;
+  const int64_t e = (int64_t)blockIdx.x * kTqRedE + ei;
+  double t = 0.0;
+  if (e < m) {
+    int b = sl;
+    for (; b + 3 * kTqRedS < nb; b += 4 * kTqRedS) {
+      const double v0 = runs[(int64_t)b * m + e], v1 = runs[(int64_t)(b + kTqRedS) * m + e];
+      const double v2 = runs[(int64_t)(b + 2 * kTqRedS) * m + e], v3 = runs[(int64_t)(b + 3 * kTqRedS) * m + e];
       t = (((t + v0) + v1) + v2) + v3;
     }
-    for (; b < nb; ++b) t += runs[(int64_t)b * m + e];
-    T[e] = t;
+    for (; b < nb; b += kTqRedS) t += runs[(int64_t)b * m + e];
+  }
+  part[sl][ei] = t;
+  __syncthreads();
+  if (sl == 0 && e < m) {
+    double r = part[0][ei];
+    for (int k = 1; k < kTqRedS; ++k) r += part[k][ei];
+    T[e] = r;
   }
 }
 
@@ -1068,7 +1081,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     {
       ProfScope _ps(c, K_TQ_REDUCE);
       const int64_t m = (int64_t)fq.G * p;
-      hipLaunchKernelGGL(k_tq_reduce, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, c->tq_runs, c->L.nb, m, fq.T);
+      hipLaunchKernelGGL(k_tq_reduce, dim3((unsigned)((m + kTqRedE - 1) / kTqRedE)), dim3(kTqRedE * kTqRedS), 0,
+                         c->stream, c->tq_runs, c->L.nb, m, fq.T);
     }
     LFE_HIP(hipGetLastError());
     LFE_TRY(allreduce_sum_f64(c, fq.T, (size_t)fq.G * p));
