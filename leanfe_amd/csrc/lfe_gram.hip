@@ -1047,13 +1047,11 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev) {
   double* part = c->scratch;
   double* msum = c->scratch + (size_t)nblk * NA;
   auto final_from = [&](auto kfinal) -> int {
-    if (!c->owner_on) {
-      hipLaunchKernelGGL(kfinal, dim3(1), dim3(256), 0, c->stream, part, nblk, c->raw_tile, p, out_dev, flag_dev);
-      return LFE_OK;
-    }
+    // one workgroup per entry sums the block partials (a tree in fixed order), then one block
+    // forms the tile (owner-sharded rows: the sums over ranks in between)
     hipLaunchKernelGGL(k_reduce_partials, dim3(NA), dim3(256), 0, c->stream, part, nblk, (int64_t)NA, msum);
     LFE_HIP(hipGetLastError());
-    LFE_TRY(allreduce_sum_f64(c, msum, (size_t)NA));
+    if (c->owner_on) LFE_TRY(allreduce_sum_f64(c, msum, (size_t)NA));
     hipLaunchKernelGGL(kfinal, dim3(1), dim3(256), 0, c->stream, msum, 1, c->raw_tile, p, out_dev, flag_dev);
     return LFE_OK;
   };

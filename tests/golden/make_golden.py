@@ -75,6 +75,26 @@ def load_reference():
     return compress, std_errors, common
 
 
+def wls_reference_beta(compress, data, y, xs, fes, keep, weights):
+    """Weighted exact-LSDV beta from the reference's build_design_matrix + solve_wls with
+    per-row sqrt-weights (compress.py:503-680)."""
+    sel = lambda a: np.asarray(a)[keep]
+    cols = {c: sel(data[c]).astype(np.float64) for c in xs}
+    for f in fes:
+        cols[f] = sel(data[f])
+    yv = sel(data[y]).astype(np.float64)
+    w = sel(data[weights]).astype(np.float64)
+    cols["_mean_y"] = yv
+    cols["_wts"] = np.sqrt(w)
+    cols["_n"] = np.ones(yv.size)
+    cols["_sum_y"] = yv
+    cols["_sum_y_sq"] = yv ** 2
+    res = compress.DuckDBResult(cols)
+    design, Y, wts, _, _ = compress.build_design_matrix(res, xs, fes, use_sparse=True)
+    beta, _ = compress.solve_wls(design, Y, wts)
+    return np.asarray(beta[1:len(xs) + 1])
+
+
 def lsdv_reference(compress, data, y, xs, fes, keep, vcov, cluster_cols, ssc, n_obs, df_resid):
     """Exact LSDV fit + SEs computed by the reference's own functions."""
     sel = lambda a: np.asarray(a)[keep]
@@ -218,9 +238,11 @@ CASES = [
     ("synth_hc1", fx_synth, "y", ["x1", "x2", "x3", "x4"], ["fe1", "fe2"], "alt_proj", None, "HC1", None),
 ]
 
-# weighted fits: the reference's LSDV helpers take weights only as sqrt(group
-# size), so weighted goldens are pinned to the oracle restatement of
-# polars_impl.py:493-500 + :201-206 (no independent reference vector exists).
+# weighted fits: the reference's solve_wls (compress.py:659-680) takes per-row
+# sqrt-weights, so passing _wts = sqrt(w) to its LSDV fit pins the weighted beta
+# (ref_beta, "reference-wls-beta").  Its grouped SE helpers assume _wts = sqrt(_n),
+# so the weighted SEs stay pinned to the oracle restatement of polars_impl.py:493-500,
+# :201-206 and std_errors.py's weighted branches.
 WEIGHTED = [
     ("xlang_w_iid", fx_xlang, "y", ["x1", "x2", "treatment"], ["fe1", "fe2"], "alt_proj", "weight", "iid", None),
     ("panel_w_cl1", lambda: fx_panel(seed=9, weights=True), "y", ["x1", "x2", "x3"], ["fe1", "fe2"],
@@ -338,13 +360,14 @@ def yoco_reference(compress, orc, xs, fes, vcov, cl, ssc=True):
     return np.asarray(beta[1:k_x]), np.asarray(se[1:]), ncl, df_resid, float(rss_total)
 
 
-def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=None):
+def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=None, wls_beta=None):
     arrays = {f"in_{c}": np.asarray(v) for c, v in data.items()}
     meta = dict(name=name, y=y, xs=xs, fes=fes, strategy=strategy, weights=weights, vcov=vcov,
                 instruments=instruments or [],
                 cluster_cols=cl, demean_tol=1e-6, max_iter=50, ssc=True,
                 oracle_n_clusters=orc["n_clusters"], ref_n_clusters=ref[2] if ref else None,
-                pinned=("reference-iv" if instruments else "reference-lsdv") if ref else "oracle-only")
+                pinned=(("reference-iv" if instruments else "reference-lsdv") if ref else
+                        "reference-wls-beta" if wls_beta is not None else "oracle-only"))
     arrays.update(
         oracle_beta=orc["beta"], oracle_se=orc["se"], oracle_iterations=np.int64(orc["iterations"]),
         oracle_n_obs=np.int64(orc["n_obs"]), oracle_df_resid=np.int64(orc["df_resid"]),
@@ -355,6 +378,8 @@ def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, 
                            .encode(), dtype=np.uint8))
     if ref:
         arrays.update(ref_beta=ref[0], ref_se=ref[1])
+    if wls_beta is not None:
+        arrays.update(ref_beta=wls_beta)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
 
 
@@ -362,10 +387,10 @@ def _json_ncl(v):
     return list(v) if isinstance(v, tuple) else v
 
 
-def main():
+def main(only_weighted=False):
     compress, std_errors, common = load_reference()
     worst = 0.0
-    for name, recipe, y, xs, fes, strategy, weights, vcov, cl in CASES + WEIGHTED:
+    for name, recipe, y, xs, fes, strategy, weights, vcov, cl in (WEIGHTED if only_weighted else CASES + WEIGHTED):
         data = recipe()
         orc = altproj.fit(data, y, xs, fes, strategy=strategy, weights=weights, vcov=vcov,
                           cluster_cols=cl)
@@ -384,9 +409,19 @@ def main():
             print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} df={orc['df_resid']:6d} "
                   f"tight-vs-ref beta {rb:.1e} se {rs:.1e} | default-tol beta dev {db:.1e}")
         else:
-            print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} (oracle-pinned, weighted)")
-        _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight)
+            wb = wls_reference_beta(compress, data, y, xs, fes, orc["keep"], weights)
+            rb = np.max(np.abs(tight["beta"] - wb) / np.maximum(np.abs(wb), 1e-300))
+            assert rb < 1e-9, (name, rb)
+            print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} weighted: tight-vs-ref beta {rb:.1e} "
+                  f"(SE oracle-pinned)")
+            if only_weighted:
+                _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, None, orc, tight, wls_beta=wb)
+        if not only_weighted:
+            _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight,
+                  wls_beta=None if weights is None else wb)
     print(f"worst tight-oracle vs reference-LSDV relative deviation: {worst:.2e}")
+    if only_weighted:
+        return
     worst = 0.0
     for name, recipe, y, xs, fes, strategy, weights, vcov, cl, inst in IV:
         data = recipe()
@@ -432,4 +467,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(only_weighted="--weighted-only" in sys.argv)

@@ -63,6 +63,15 @@ def test_oracle_converged_matches_reference_lsdv(name):
     assert ncl(r["n_clusters"]) == ncl(meta["ref_n_clusters"])
 
 
+@pytest.mark.parametrize("name", [n for n in CASES if load(n)[0]["pinned"] == "reference-wls-beta"])
+def test_weighted_oracle_converged_matches_reference_wls(name):
+    """Weighted fits: the oracle iterated to machine precision gives the reference's exact
+    weighted LSDV beta (its solve_wls with per-row sqrt-weights, compress.py:659-680)."""
+    meta, data, exp = load(name)
+    r = _fit(meta, data, demean_tol=1e-14, max_iter=100000)
+    np.testing.assert_allclose(r["beta"], exp["ref_beta"], rtol=1e-9, atol=0)
+
+
 @pytest.mark.parametrize("name", [n for n in CASES if load(n)[0]["pinned"] == "reference-lsdv"])
 def test_default_tolerance_close_to_reference(name):
     """At the reference defaults (tol 1e-6, max_iter 50) alt-proj stops within
