@@ -393,6 +393,11 @@ static void free_data(lfe_ctx* c) {
   dfree(c->rec_lay);
   c->rec_sy_cap = c->rec_syy_cap = c->rec_lay_cap = 0;
   dfree(c->raw_part);
+  dfree(c->qpart);
+  dfree(c->dspec);
+  c->dspec_elems = 0;
+  c->gram_spec = false;
+  c->qpart_cap = 0;
   dfree(c->raw_tile);
   dfree(c->raw_shift);
   c->raw_part_cap = c->raw_tile_cap = c->raw_shift_cap = 0;
@@ -822,6 +827,7 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
   int iterations = 0;
   double last = -1.0;
   c->tq_final = false;
+  c->gram_spec = false;
   {
     PhaseTimer t(c, PH_DEMEAN);
     const bool fast = c->F > 0 && check_from > 0 && fast_path_ok(c, order);

@@ -40,6 +40,7 @@ struct Sums4Args {
   int nq;               // number of non-primary FEs and their indices
   int qf[kMaxFE];
   double* raw_part;     // RAW: [blocks][256] raw Gram tiles
+  double* qpart;        // k_sums2_raw: [blocks][G_Q * p] the block's secondary-FE table (raw bits)
   const double* fixq;   // k_sums2_raw: [kMaxCols] scales, [kMaxCols] quanta, [kMaxCols] qualified (k_fix_quanta)
 };
 
@@ -87,11 +88,13 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   };
   if (a.slice)
     for (int j = tid; j < a.B * p; j += TH) lds[j] = 0.0;
-  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
-  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  const BlockRows br = block_rows(a.la.items, a.la.n_items, lane);
   int cur = -1;
-  for (int item = i0; item < i1; ++item) {
-    const int4 it = a.la.items[item];
+  for (int item = br.first; item < a.la.n_items; ++item) {
+    int4 it = a.la.items[item];
+    if (it.y >= br.hi) break;
+    it.y = max(it.y, br.lo);
+    it.z = min(it.z, br.hi);
     const int lo = it.x << a.la.s;
     if (a.slice && it.x != cur) {
       __syncthreads();
@@ -244,11 +247,13 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
       lds[j] = 0.0;
     }
   };
-  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
-  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  const BlockRows br = block_rows(a.la.items, a.la.n_items, lane);
   int cur = -1;
-  for (int item = i0; item < i1; ++item) {
-    const int4 it = a.la.items[item];
+  for (int item = br.first; item < a.la.n_items; ++item) {
+    int4 it = a.la.items[item];
+    if (it.y >= br.hi) break;
+    it.y = max(it.y, br.lo);
+    it.z = min(it.z, br.hi);
     if (it.x != cur) {
       __syncthreads();
       if (cur >= 0) flush(cur);
@@ -328,14 +333,12 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   }
   __syncthreads();
   if (cur >= 0) flush(cur);
-  for (int j = tid; j < a.G[Q] * p; j += TH) {
-    if (fix) {
-      const u64 val = reinterpret_cast<const u64*>(lds + qoff)[j];
-      if (val != 0ull) atomicAdd(reinterpret_cast<u64*>(&a.S[Q][j]), val);
-    } else {
-      const double val = lds[qoff + j];
-      if (val != 0.0) atomicAdd(&a.S[Q][j], val);
-    }
+  // the block's secondary table goes out whole (k_qpart_reduce sums the blocks in order): every
+  // block adding into the same G_Q * p entries serialised ~256 device-scope atomics per entry
+  {
+    const int64_t m = (int64_t)a.G[Q] * p;
+    double* dst = a.qpart + (int64_t)blockIdx.x * m;
+    for (int j = tid; j < m; j += TH) dst[j] = lds[qoff + j];
   }
   __shared__ double rred[256];
   for (int wv = 0; wv < nwv; ++wv) {
@@ -443,6 +446,39 @@ __global__ void k_fix_convert(double* __restrict__ S, int64_t m, int p, const do
   }
 }
 
+// S_Q = the blocks' tables summed in block order (int64 on the exact path, then scaled to
+// double; else f64): 16
+// consecutive entries x 16 block slices per workgroup, the slices added in order
+__global__ __launch_bounds__(256) void k_qpart_reduce(const double* __restrict__ part, int nblk, int64_t m,
+                                                      const double* __restrict__ fq, int p, double* __restrict__ S) {
+  __shared__ double ps[16][16];
+  __shared__ long long pi[16][16];
+  const int ei = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int64_t e = (int64_t)blockIdx.x * 16 + ei;
+  const bool fix = fix_on(fq, p);
+  double t = 0.0;
+  long long ti = 0;
+  if (e < m)
+    for (int b = sl; b < nblk; b += 16) {
+      const double v = part[(int64_t)b * m + e];
+      t += v;
+      ti += __double_as_longlong(v);
+    }
+  ps[sl][ei] = t;
+  pi[sl][ei] = ti;
+  __syncthreads();
+  if (sl != 0 || e >= m) return;
+  if (fix) {
+    long long r = 0;
+    for (int k = 0; k < 16; ++k) r += pi[k][ei];
+    S[e] = (double)r * fq[kMaxCols + (int)(e % p)];  // k_fix_convert's conversion, fused
+  } else {
+    double r = 0.0;
+    for (int k = 0; k < 16; ++k) r += ps[k][ei];
+    S[e] = r;
+  }
+}
+
 // raw_shift[16 + j] = this rank's shift (first layout row; 0 for an empty shard);
 // raw_shift[j] = rank 0's (summed over ranks afterwards)
 __global__ void k_raw_shift(const double* __restrict__ X, int64_t ld, int p, int has_rows, int rank,
@@ -537,6 +573,10 @@ int sums4(lfe_ctx* c) {
     a.raw_part = c->raw_part;
   }
   const bool exact = two;
+  if (two) {
+    LFE_TRY(ensure_f64(c, c->qpart, c->qpart_cap, (size_t)nblocks * c->fe[a.qf[0]].G * p));
+    a.qpart = c->qpart;
+  }
   if (exact) {
     ProfScope _ps(c, K_FIX_SUMS);
     // the column statistics (the partition wrote them unless the rows stayed in place)
@@ -563,9 +603,17 @@ int sums4(lfe_ctx* c) {
     LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, lds, c->stream));
   }
   LFE_HIP(hipGetLastError());
+  if (two) {
+    ProfScope _ps(c, K_FIX_SUMS);
+    const int64_t m = (int64_t)c->fe[a.qf[0]].G * p;
+    hipLaunchKernelGGL(k_qpart_reduce, dim3((unsigned)((m + 15) / 16)), dim3(256), 0, c->stream, c->qpart, nblocks, m,
+                       c->fixq, p, c->fe[a.qf[0]].S);
+    LFE_HIP(hipGetLastError());
+  }
   if (exact) {
     ProfScope _ps(c, K_FIX_SUMS);
     for (int f = 0; f < c->F; ++f) {
+      if (f == a.qf[0]) continue;  // converted by k_qpart_reduce
       const int64_t m = (int64_t)c->fe[f].G * p;
       hipLaunchKernelGGL(k_fix_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, c->fe[f].S, m, p, c->fixq);
     }

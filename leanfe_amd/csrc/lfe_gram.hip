@@ -195,11 +195,13 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
 
   // a contiguous range of items per block (all blocks co-resident): the
   // primary slice is staged again only when the bucket changes
-  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
-  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  const BlockRows br = block_rows(a.la.items, a.la.n_items, lane);
   int staged = -1;
-  for (int item = i0; item < i1; ++item) {
-    const int4 it = a.la.items[item];
+  for (int item = br.first; item < a.la.n_items; ++item) {
+    int4 it = a.la.items[item];
+    if (it.y >= br.hi) break;
+    it.y = max(it.y, br.lo);
+    it.z = min(it.z, br.hi);
     const int lo = it.x << a.la.s;
     if (a.stage && it.x != staged) {
       __syncthreads();
@@ -407,9 +409,8 @@ __global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ pa
   block_reduce_store<NT, TH>(acc, red, out, tid);
   if (MODE == GRAM_RESID) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      for (int off = 32; off > 0; off >>= 1) st[s] += __shfl_down(st[s], off, 64);
-    if (lane == 0)
+    for (int s = 0; s < 4; ++s) st[s] = wave_reduce63(st[s], 0.0, [](double x, double y) { return x + y; });
+    if (lane == 63)
       for (int s = 0; s < 4; ++s) stat_red[wave][s] = st[s];
     __syncthreads();
     if (tid < 4) {
@@ -458,11 +459,13 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
   double st[4] = {0.0, 0.0, 0.0, 0.0};  // sum r^2 (w = 1), sum r^2, sum y~, sum y~^2
   const int32_t* codeP = a.la.code[P];
   const int32_t* codeQ = a.la.code[Q];
-  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
-  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  const BlockRows br = block_rows(a.la.items, a.la.n_items, lane);
   int staged = -1;
-  for (int item = i0; item < i1; ++item) {
-    const int4 it = a.la.items[item];
+  for (int item = br.first; item < a.la.n_items; ++item) {
+    int4 it = a.la.items[item];
+    if (it.y >= br.hi) break;
+    it.y = max(it.y, br.lo);
+    it.z = min(it.z, br.hi);
     const int lo = it.x << a.la.s;
     if (it.x != staged) {
       __syncthreads();
@@ -536,18 +539,18 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
       }
     }
   }
-  // block reduction: wave sums (xor shuffles), then the NW wave rows in LDS
+  // block reduction: wave sums over DPP lane moves (VALU, fixed order; xor shuffles of the
+  // NM + 4 sums cost ds_bpermute latency at the kernel's tail), then the NW wave rows in LDS
+  const auto addop = [](double x, double y) { return x + y; };
 #pragma unroll
   for (int e = 0; e < NM; ++e) {
-    double v = m[e];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (lane == 0) red[wave][e] = v;
+    const double v = wave_reduce63(m[e], 0.0, addop);
+    if (lane == 63) red[wave][e] = v;
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    double v = st[e];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (lane == 0) red[wave][NM + e] = v;
+    const double v = wave_reduce63(st[e], 0.0, addop);
+    if (lane == 63) red[wave][NM + e] = v;
   }
   __syncthreads();
   double* out = partial + (int64_t)blockIdx.x * pstride;
@@ -597,11 +600,13 @@ __global__ __launch_bounds__(kResThreads) void k_design_rows(GramArgs a, double*
   for (int e = 0; e < NA; ++e) acc[e] = 0.0;
   const int32_t* codeP = a.la.code[P];
   const int32_t* codeQ = a.la.code[Q];
-  const int i0 = (int)((int64_t)blockIdx.x * a.la.n_items / gridDim.x);
-  const int i1 = (int)((int64_t)(blockIdx.x + 1) * a.la.n_items / gridDim.x);
+  const BlockRows br = block_rows(a.la.items, a.la.n_items, lane);
   int staged = -1;
-  for (int item = i0; item < i1; ++item) {
-    const int4 it = a.la.items[item];
+  for (int item = br.first; item < a.la.n_items; ++item) {
+    int4 it = a.la.items[item];
+    if (it.y >= br.hi) break;
+    it.y = max(it.y, br.lo);
+    it.z = min(it.z, br.hi);
     const int lo = it.x << a.la.s;
     if (it.x != staged) {
       __syncthreads();
@@ -647,11 +652,11 @@ __global__ __launch_bounds__(kResThreads) void k_design_rows(GramArgs a, double*
       }
     }
   }
+  const auto addop = [](double x, double y) { return x + y; };
 #pragma unroll
   for (int e = 0; e < NA; ++e) {
-    double v = acc[e];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (lane == 0) red[wave][e] = v;
+    const double v = wave_reduce63(acc[e], 0.0, addop);
+    if (lane == 63) red[wave][e] = v;
   }
   __syncthreads();
   double* out = partial + (int64_t)blockIdx.x * pstride;
@@ -1138,11 +1143,16 @@ __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __r
 
 int launch_gram(lfe_ctx* c, double* host_gram) {
   GramArgs a = base_args(c);
+  const bool spec = c->gram_spec;  // the tables tile is already on the stream (lfe_demean)
+  c->gram_spec = false;
   if (resid_rows_ok(c, a) && c->p <= 11) {
     LFE_TRY(ensure_dred(c, 260));
-    std::vector<double> h(257);
+    std::vector<double> h(533);
     bool done = false;
-    if (tables_gram_ok(c)) {  // the Gram from the group tables, unless its guard trips
+    if (spec) {
+      LFE_TRY(d2h_sync(c, h.data(), c->dspec, sizeof(double) * 533));
+      done = h[532] == 1.0;
+    } else if (tables_gram_ok(c)) {  // the Gram from the group tables, unless its guard trips
       LFE_TRY(tables_gram_enqueue(c, c->dred, c->dred + 256));
       LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 257));
       done = h[256] == 1.0;
@@ -1206,27 +1216,48 @@ static int resid_rows(lfe_ctx* c, GramArgs a, double* meat, double* stats) {
 
 // Gram, device solve and residual pass with one host round trip (row-kernel case:
 // two FEs, unweighted, p <= 11).  Returns 1 (nothing done) when unavailable.
+int gram_spec_enqueue(lfe_ctx* c, int* queued) {
+  *queued = 0;
+  c->gram_spec = false;
+  GramArgs a = base_args(c);
+  if (!(resid_rows_ok(c, a) && c->p <= 11 && tables_gram_ok(c))) return LFE_OK;
+  LFE_TRY(ensure_f64(c, c->dspec, c->dspec_elems, 544));
+  LFE_TRY(tables_gram_enqueue(c, c->dspec, c->dspec + 532));
+  hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dspec, c->p, c->dspec + 520,
+                     c->dspec + 520, c->dspec + 516);
+  LFE_HIP(hipGetLastError());
+  *queued = 1;
+  return LFE_OK;
+}
+
 int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores) {
   GramArgs a = base_args(c);
+  const bool spec = c->gram_spec;  // the tables tile and beta are already on the stream (lfe_demean)
+  c->gram_spec = false;
   if (!(resid_rows_ok(c, a) && c->p <= 11)) return 1;
   const int p = c->p, k = p - 1;
   // dred: [0, 256) design tile | [256, 516) residual tile + stats | 516 ok | [520, 532) beta | 532 tables guard
   LFE_TRY(ensure_dred(c, 544));
   std::vector<double> h(533);
   for (int pass = tables_gram_ok(c) ? 0 : 1; pass < 2; ++pass) {
-    if (pass == 0) LFE_TRY(tables_gram_enqueue(c, c->dred, c->dred + 532));
-    else LFE_TRY(design_rows_enqueue(c, a, c->dred));
-    hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dred, p, c->dbeta, c->dred + 520,
-                       c->dred + 516);
+    // the speculative chain left tile, ok, beta and guard in dspec: the residual pass reads its
+    // beta there and adds its tile beside them, so one read-back returns everything
+    double* buf = pass == 0 && spec ? c->dspec : c->dred;
+    if (buf == c->dred) {
+      if (pass == 0) LFE_TRY(tables_gram_enqueue(c, c->dred, c->dred + 532));
+      else LFE_TRY(design_rows_enqueue(c, a, c->dred));
+      hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dred, p, c->dbeta, c->dred + 520,
+                         c->dred + 516);
+    }
     LFE_HIP(hipGetLastError());
     GramArgs ar = a;
     ar.nq = 1;
     ar.qf[0] = 1 - a.la.P;
     ar.G_Q = c->fe[ar.qf[0]].G;
-    ar.beta = c->dbeta;
+    ar.beta = buf == c->dred ? c->dbeta : c->dspec + 520;
     ar.scores = keep_scores ? c->scores : nullptr;
-    LFE_TRY(resid_rows_enqueue(c, ar, c->dred + 256));
-    LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 533));
+    LFE_TRY(resid_rows_enqueue(c, ar, buf + 256));
+    LFE_TRY(d2h_sync(c, h.data(), buf, sizeof(double) * 533));
     if (pass == 1 || h[532] == 1.0) break;  // guard failed: the explicit design pass
   }
   if (h[516] != 1.0) return 1;  // not positive definite: the caller takes the two-call path

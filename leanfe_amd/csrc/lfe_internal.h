@@ -228,6 +228,8 @@ struct lfe_ctx {
   // the raw Gram of the shifted data columns, so lfe_gram_resid needs no design pass
   double* raw_part = nullptr;    // [blocks][256] per-block raw tiles
   size_t raw_part_cap = 0;
+  double* qpart = nullptr;       // [blocks][G_Q * p] per-block secondary-FE sums (k_sums2_raw)
+  size_t qpart_cap = 0;
   double* raw_tile = nullptr;    // [256] raw tile: slots 0..p-1 data (shifted by raw_shift), slot 15 intercept
   size_t raw_tile_cap = 0;
   double* raw_shift = nullptr;   // [32]: [0, 16) the shift of raw_tile (rank 0's first row on every rank),
@@ -281,6 +283,11 @@ struct lfe_ctx {
   double* fixq = nullptr;        // [3 * kMaxCols]: scale[c], quantum[c], qualified[c]
   size_t fixq_cap = 0;
   bool exact_sums = false;       // the last group sums ran k_sums2_raw (exact when fixq's flag is on)
+  // speculative Gram tile + Cholesky of the converged tables (gram_spec_enqueue), valid until the
+  // next load / drop / demean: [0, 256) tile, 516 ok, [520, 532) beta, 532 guard (launch_gram_resid)
+  double* dspec = nullptr;
+  size_t dspec_elems = 0;
+  bool gram_spec = false;
   lfe::Timings tm;
   lfe::Prof prof;
 };
@@ -311,6 +318,9 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
 int launch_gram(lfe_ctx* c, double* host_gram);
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores, int icpt);
 int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores);
+// speculative Gram-from-tables + device Cholesky, enqueued behind a convergence check's read-back
+// so that the GPU keeps working while the host decides (lfe_gram.hip); *queued = 1 if enqueued
+int gram_spec_enqueue(lfe_ctx* c, int* queued);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
 void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out);  // sum of [nblocks][256] tiles
 // --- YOCO records (lfe_compress.hip) ---
@@ -439,6 +449,35 @@ __device__ __forceinline__ double wave_reduce63(double v, double idv, Op op) {
   v = op(v, dpp64<0x142, 0xA>(v, idv));
   v = op(v, dpp64<0x143, 0xC>(v, idv));
   return v;
+}
+
+// Balanced row ranges for the streaming X passes: block b of the grid walks layout rows
+// [lo, hi) (equal shares, multiples of 64), i.e. the items from `first` on, each clipped to
+// [lo, hi) (whole items per block left some blocks a full 8192-row item more than others: +30%
+// at 3 items per block).  Every wave finds `first` - the first item ending after lo - by a
+// 64-ary search over the items' ends (3 dependent loads at ~6K items).
+struct BlockRows {
+  int first, lo, hi;
+};
+__device__ __forceinline__ BlockRows block_rows(const int4* __restrict__ items, int n_items, int lane) {
+  BlockRows r{0, 0, 0};
+  if (n_items <= 0) return r;
+  const int64_t total = items[n_items - 1].z, b = blockIdx.x, nb = gridDim.x;
+  r.lo = (int)((total * b / nb) & ~63ll);
+  r.hi = b + 1 == nb ? (int)total : (int)((total * (b + 1) / nb) & ~63ll);
+  int lo = 0, hi = n_items;  // the answer lies in [lo, hi]
+  while (lo < hi) {
+    const int step = (hi - lo + 63) / 64;
+    const int idx = lo + lane * step;
+    const bool inr = idx < hi;
+    const bool past = inr && items[idx].z > r.lo;  // monotone in idx
+    const int f = __popcll(__ballot(inr && !past));
+    const int cand = lo + f * step;
+    hi = cand < hi ? cand : hi;
+    lo = step == 1 ? hi : (f > 0 ? lo + (f - 1) * step + 1 : lo);
+  }
+  r.first = lo;
+  return r;
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t h) {

@@ -1091,8 +1091,20 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     if (!check && it == max_iter) break;
     LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check));
     if (check) {
-      LFE_TRY(d2h_sync(c, &last, c->dred, sizeof(double)));
-      if (last < tol) break;  // converged after sweep `it`: keep alpha_Q of this sweep
+      // the check's read-back first, then - when this check is likely the last (the first one,
+      // or the previous was within 100x of tol: the check falls ~100x per sweep) - the Gram of
+      // the tables and its Cholesky, so the GPU works through the host's decision and the
+      // return to the caller; lfe_gram_resid then starts at the residual pass
+      LFE_TRY(d2h_async(c, c->dred, sizeof(double)));
+      int spec = 0;
+      c->tq_final = true;
+      if (it == check_from || (last >= 0.0 && last < 100.0 * tol)) LFE_TRY(gram_spec_enqueue(c, &spec));
+      c->tq_final = false;
+      LFE_TRY(d2h_wait(c, &last, sizeof(double)));
+      if (last < tol) {  // converged after sweep `it`: keep alpha_Q of this sweep
+        c->gram_spec = spec != 0;
+        break;
+      }
     }
     if (it == max_iter) break;
     std::swap(fq.alpha, c->alpha_spare);

@@ -763,6 +763,7 @@ int prepare_layout(lfe_ctx* c) {
   c->sums_ready = false;
   c->seg_ready = false;
   c->colstat_chunks = 0;  // the partition (or sums4's k_col_stats) writes them again
+  c->gram_spec = false;
   c->clw.lay_valid = false;  // cluster columns follow the new layout
   // primary FE: most levels (ties -> first)
   L.P = -1;
