@@ -33,7 +33,8 @@ enum {
   LFE_EHIP = -2,   /* HIP runtime failure (RuntimeError) */
   LFE_ERCCL = -3,  /* RCCL failure (RuntimeError) */
   LFE_ENOMEM = -4, /* device allocation failure (MemoryError) */
-  LFE_ESTATE = -5  /* call out of order (RuntimeError) */
+  LFE_ESTATE = -5, /* call out of order (RuntimeError) */
+  LFE_ENEEDPASS = -6 /* streamed X: lfe_gram needs the streamed design-Gram pass (lfe_stream_begin pass 3) */
 };
 
 enum { LFE_HOST = 0, LFE_DEVICE = 1 };
@@ -209,6 +210,31 @@ int lfe_copy_demeaned(lfe_ctx* ctx, double* const* cols_out, int64_t* n_out);
 /* Debug/fixtures: copy the loaded inputs (p columns, F code arrays; input row
  * order) back to host buffers. */
 int lfe_copy_inputs(lfe_ctx* ctx, double* const* cols_out, int32_t* const* codes_out);
+
+/* Out-of-core X (data larger than HBM; SURVEY.md §8f rank 4, the role of scan_parquet /
+ * DuckDB's disk-backed tables, polars_impl.py:341-343, duckdb_impl.py:417-452).  The FE codes
+ * stay resident (with their layouts: ~22 bytes per row); the p data columns are streamed in
+ * row chunks through three passes, each a sequence of lfe_stream_rows calls covering rows
+ * [0, n) exactly once between lfe_stream_begin and lfe_stream_end:
+ *   pass 1 (after lfe_drop_singletons): the group sums S_f of polars_impl.py:491-508 and the
+ *          raw Gram of the tables (exact int64 per chunk, folded in chunk order);
+ *   lfe_demean, then lfe_gram (the Gram from the group tables; LFE_ENEEDPASS when it is
+ *          unavailable or fails its guard: then pass 3, the Gram of [1, y~, x~]);
+ *   pass 2 (beta_full = [intercept, beta]): the residual (polars_impl.py:229), RSS / TSS and the
+ *          HC1 meat (std_errors.py:217-282).
+ * Two FEs, unweighted, p <= 11, IID / HC1 (cluster scores are not streamed).  cols = p column
+ * pointers of `rows` doubles each (kind LFE_HOST / LFE_DEVICE).  lfe_stream_end's `out`:
+ * pass 2: stats[4] then the (p-1)^2 meat; pass 3: the (p+1)^2 Gram; pass 1: unused. */
+int lfe_load_codes(lfe_ctx* ctx, int64_t n, int p, int F, const int32_t* const* fe_codes,
+                   const int32_t* n_levels, int kind);
+int lfe_stream_begin(lfe_ctx* ctx, int pass, const double* beta_full);
+int lfe_stream_rows(lfe_ctx* ctx, int64_t row0, int64_t rows, const double* const* cols, int kind);
+int lfe_stream_end(lfe_ctx* ctx, double* out);
+/* Benchmark / test helpers: lfe_synth_load's panel with only the codes resident, and one chunk
+ * of its columns generated on the device and streamed through the current pass. */
+int lfe_synth_load_codes(lfe_ctx* ctx, int64_t n, int k, int n_fe, const int32_t* n_levels, uint64_t seed);
+int lfe_stream_synth_rows(lfe_ctx* ctx, int64_t row0, int64_t rows, int k, const int32_t* n_levels,
+                          const double* beta, uint64_t seed);
 
 /* Whether the last group sums of the two-FE fast path accumulated exactly (int64
  * fixed point per column, so S does not depend on the order of the adds and a

@@ -15,7 +15,11 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LEANFE_HIP_LIB") or os.path.join(_HERE, "liblfe_hip.so")
 
-LFE_OK, LFE_EINVAL, LFE_EHIP, LFE_ERCCL, LFE_ENOMEM, LFE_ESTATE = 0, -1, -2, -3, -4, -5
+LFE_OK, LFE_EINVAL, LFE_EHIP, LFE_ERCCL, LFE_ENOMEM, LFE_ESTATE, LFE_ENEEDPASS = 0, -1, -2, -3, -4, -5, -6
+
+
+class NeedsStreamPass(RuntimeError):
+    """Streamed X: the Gram from the group tables is unavailable; stream pass 3."""
 LFE_HOST, LFE_DEVICE = 0, 1
 
 _i64p = C.POINTER(C.c_int64)
@@ -55,6 +59,12 @@ SIGNATURES = {
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
+    "lfe_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.POINTER(_vp), _i32p, C.c_int]),
+    "lfe_stream_begin": (C.c_int, [_vp, C.c_int, _dp]),
+    "lfe_stream_rows": (C.c_int, [_vp, C.c_int64, C.c_int64, C.POINTER(_vp), C.c_int]),
+    "lfe_stream_end": (C.c_int, [_vp, _dp]),
+    "lfe_synth_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, C.c_uint64]),
+    "lfe_stream_synth_rows": (C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int, _i32p, _dp, C.c_uint64]),
     "lfe_sync": (C.c_int, [_vp]),
     "lfe_shard_rows": (C.c_int, [_vp, _i64p]),
     "lfe_timings": (C.c_int, [_vp, _dp]),
@@ -96,6 +106,8 @@ def _check(rc: int) -> None:
         raise ValueError(msg)
     if rc == LFE_ENOMEM:
         raise MemoryError(msg)
+    if rc == LFE_ENEEDPASS:
+        raise NeedsStreamPass(msg)
     raise RuntimeError(f"leanfe HIP engine error {rc}: {msg}")
 
 
@@ -378,6 +390,58 @@ class Engine:
 
     def sync(self) -> None:
         _check(self._lib.lfe_sync(self._h))
+
+    # -- out-of-core X: codes resident, columns streamed in row chunks ----
+    def load_codes(self, codes: list[np.ndarray], levels: list[int], p: int) -> None:
+        """FE codes of n rows (input order); the p data columns come later in chunks."""
+        codes = [np.ascontiguousarray(c, dtype=np.int32) for c in codes]
+        n = codes[0].size if codes else 0
+        kp = (_vp * max(len(codes), 1))(*[_ptr(c) for c in codes])
+        lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
+        _check(self._lib.lfe_load_codes(self._h, n, int(p), len(codes), kp, lv, LFE_HOST))
+        self.p, self.F, self.n = int(p), len(codes), n
+
+    def stream_begin(self, pass_: int, beta_full: np.ndarray | None = None) -> None:
+        b = None if beta_full is None else np.ascontiguousarray(beta_full, dtype=np.float64)
+        _check(self._lib.lfe_stream_begin(self._h, int(pass_), None if b is None else
+                                          b.ctypes.data_as(C.POINTER(C.c_double))))
+
+    def stream_rows(self, row0: int, cols: list[np.ndarray]) -> None:
+        cols = [np.ascontiguousarray(c, dtype=np.float64) for c in cols]
+        rows = cols[0].size if cols else 0
+        if len(cols) != self.p or any(c.size != rows for c in cols):
+            raise ValueError(f"stream_rows needs {self.p} columns of equal length")
+        cp = (_vp * len(cols))(*[_ptr(c) for c in cols])
+        _check(self._lib.lfe_stream_rows(self._h, int(row0), rows, cp, LFE_HOST))
+
+    def stream_end(self) -> np.ndarray:
+        out = np.zeros(max(4 + (self.p - 1) ** 2, (self.p + 1) ** 2), dtype=np.float64)
+        _check(self._lib.lfe_stream_end(self._h, out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
+    def synth_load_codes(self, n: int, k: int, levels: list[int], seed: int = 12345) -> None:
+        lv = (C.c_int32 * len(levels))(*[int(g) for g in levels])
+        _check(self._lib.lfe_synth_load_codes(self._h, int(n), int(k), len(levels), lv, C.c_uint64(seed)))
+        self.p, self.F, self.n = int(k) + 1, len(levels), int(n)
+
+    def stream_synth_pass(self, pass_: int, k: int, levels: list[int], beta: np.ndarray, chunk_rows: int,
+                          seed: int = 12345, beta_full: np.ndarray | None = None) -> np.ndarray:
+        """One pass whose chunks are the synthetic panel's rows, generated on the device."""
+        lv = (C.c_int32 * len(levels))(*[int(g) for g in levels])
+        b = np.ascontiguousarray(beta, dtype=np.float64)
+        self.stream_begin(pass_, beta_full)
+        for r0 in range(0, self.n, chunk_rows):
+            rows = min(chunk_rows, self.n - r0)
+            _check(self._lib.lfe_stream_synth_rows(self._h, r0, rows, int(k), lv,
+                                                   b.ctypes.data_as(C.POINTER(C.c_double)), C.c_uint64(seed)))
+        return self.stream_end()
+
+    def stream_pass(self, pass_: int, chunks, beta_full: np.ndarray | None = None) -> np.ndarray:
+        """One pass over ``chunks`` (an iterable of (row0, [p columns])) between begin / end."""
+        self.stream_begin(pass_, beta_full)
+        for row0, cols in chunks:
+            self.stream_rows(row0, cols)
+        return self.stream_end()
 
     def exact_sums(self) -> bool:
         """True when the last group sums took the exact int64 path (order-independent)."""

@@ -394,6 +394,12 @@ static void free_data(lfe_ctx* c) {
   c->rec_sy_cap = c->rec_syy_cap = c->rec_lay_cap = 0;
   dfree(c->raw_part);
   dfree(c->qpart);
+  dfree(c->sw.x);
+  dfree(c->sw.s64);
+  dfree(c->sw.sdbl);
+  dfree(c->sw.tile);
+  dfree(c->sw.toff);
+  c->sw = lfe_ctx::StreamWS();
   dfree(c->dspec);
   c->dspec_elems = 0;
   c->gram_spec = false;
@@ -420,7 +426,8 @@ static void free_data(lfe_ctx* c) {
 }
 
 // allocate all per-shard buffers for (n, p, F, levels)
-static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_levels, bool weighted) {
+static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_levels, bool weighted,
+                      bool codes_only = false) {
   free_data(c);
   if (p < 1 || p > kMaxCols) return fail(LFE_EINVAL, "p must be in [1, 63] (y plus up to 62 regressors)");
   if (F < 0 || F > kMaxFE) return fail(LFE_EINVAL, "number of fixed effects must be in [0, 8]");
@@ -431,7 +438,8 @@ static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_leve
   c->ld = std::max<int64_t>((n + 63) / 64 * 64, 64);
   c->p = p;
   c->F = F;
-  LFE_TRY(dalloc(&c->X, (size_t)p * c->ld));
+  c->sw.on = codes_only;  // streamed X: no resident columns, no permuted copy
+  if (!codes_only) LFE_TRY(dalloc(&c->X, (size_t)p * c->ld));
   if (weighted) LFE_TRY(dalloc(&c->w, (size_t)c->ld));
   if (F > 0) LFE_TRY(dalloc(&c->codes_p, (size_t)F * c->ld));
   c->fe.resize(F);
@@ -454,7 +462,7 @@ static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_leve
     }
   }
   if (need_perm) {  // bucketed layout storage (rows regrouped by the primary FE)
-    LFE_TRY(dalloc(&c->Xp, (size_t)p * c->ld));
+    if (!codes_only) LFE_TRY(dalloc(&c->Xp, (size_t)p * c->ld));
     if (weighted) LFE_TRY(dalloc(&c->wp, (size_t)c->ld));
     LFE_TRY(dalloc(&c->origp, (size_t)c->ld));
   }
@@ -478,6 +486,13 @@ struct PhaseTimer {
   do {                                                 \
     if (!(c)) return fail(LFE_EINVAL, "null context"); \
     LFE_HIP(hipSetDevice((c)->device));                \
+  } while (0)
+
+// entry points that read resident data columns
+#define LFE_NO_STREAM(c)                                                                                 \
+  do {                                                                                                   \
+    if ((c)->sw.on)                                                                                      \
+      return fail(LFE_ESTATE, "not available with streamed X (lfe_load_codes): use the lfe_stream passes"); \
   } while (0)
 
 // Runs right after the copies of lfe_load / lfe_load_finish: every return path has waited for
@@ -659,6 +674,136 @@ int lfe_load(lfe_ctx* c, int64_t n, int p, const double* const* cols, int F, con
   return LFE_OK;
 }
 
+// ---------------------------------------------------------------------------
+// out-of-core X: codes resident, the data columns streamed in row chunks
+// ---------------------------------------------------------------------------
+int lfe_load_codes(lfe_ctx* c, int64_t n, int p, int F, const int32_t* const* fe_codes, const int32_t* n_levels,
+                   int kind) {
+  LFE_CTX(c);
+  if (F != 2) return fail(LFE_EINVAL, "streamed X (lfe_load_codes) supports two fixed effects");
+  if (!n_levels || (n > 0 && !fe_codes)) return fail(LFE_EINVAL, "null input pointer");
+  if (p > 11) return fail(LFE_EINVAL, "streamed X supports p <= 11 columns (y plus up to 10 regressors)");
+  if (kind != LFE_HOST && kind != LFE_DEVICE) return fail(LFE_EINVAL, "kind must be LFE_HOST or LFE_DEVICE");
+  LFE_TRY(alloc_data(c, n, p, F, n_levels, false, true));
+  const hipMemcpyKind mk = kind == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  hipError_t e = hipSuccess;
+  for (int f = 0; f < F && n > 0 && e == hipSuccess; ++f)
+    e = hipMemcpyAsync(c->fe[f].code, fe_codes[f], sizeof(int32_t) * n, mk, c->stream);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(c->stream);
+    return fail(LFE_EHIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
+  }
+  LFE_TRY(validate_all(c));
+  c->loaded = true;
+  return LFE_OK;
+}
+
+int lfe_stream_begin(lfe_ctx* c, int pass, const double* beta_full) {
+  LFE_CTX(c);
+  auto& w = c->sw;
+  if (!w.on) return fail(LFE_ESTATE, "lfe_stream_*: the context holds resident columns (use lfe_load_codes)");
+  if (pass < 1 || pass > 3) return fail(LFE_EINVAL, "pass must be 1 (group sums), 2 (residual) or 3 (design Gram)");
+  if (!c->prepared) return fail(LFE_ESTATE, "lfe_drop_singletons first");
+  if (pass == 1 && !fast_layout_ok(c))
+    return fail(LFE_EINVAL, "streamed X needs the two-FE layouts (the larger FE above 256 levels, the smaller "
+                            "within the LDS tables)");
+  if (pass > 1 && !c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
+  if (pass == 2) {
+    if (!beta_full) return fail(LFE_EINVAL, "beta_full is null");
+    LFE_TRY(h2d_small(c, c->dbeta, beta_full, sizeof(double) * c->p));
+  }
+  if (pass > 1) {
+    LFE_TRY(ensure_f64(c, w.tile, w.tile_cap, 272));
+    LFE_HIP(hipMemsetAsync(w.tile, 0, sizeof(double) * 272, c->stream));
+  }
+  if (pass == 1) c->sums_ready = c->raw_ready = false;
+  w.pass = pass;
+  w.rows_done = 0;
+  return LFE_OK;
+}
+
+int lfe_stream_rows(lfe_ctx* c, int64_t row0, int64_t rows, const double* const* cols, int kind) {
+  LFE_CTX(c);
+  auto& w = c->sw;
+  if (!w.on || w.pass == 0) return fail(LFE_ESTATE, "lfe_stream_begin first");
+  if (row0 < 0 || rows < 0 || row0 + rows > c->n) return fail(LFE_EINVAL, "rows outside the loaded codes");
+  if (rows == 0) return LFE_OK;
+  if (!cols) return fail(LFE_EINVAL, "cols is null");
+  if (kind != LFE_HOST && kind != LFE_DEVICE) return fail(LFE_EINVAL, "kind must be LFE_HOST or LFE_DEVICE");
+  const int64_t cld = (rows + 63) / 64 * 64;
+  LFE_TRY(ensure_f64(c, w.x, w.x_cap, (size_t)c->p * cld));
+  const hipMemcpyKind mk = kind == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  for (int j = 0; j < c->p; ++j) {
+    if (!cols[j]) return fail(LFE_EINVAL, "null column pointer");
+    LFE_HIP(hipMemcpyAsync(w.x + (size_t)j * cld, cols[j], sizeof(double) * rows, mk, c->stream));
+  }
+  PhaseTimer t(c, w.pass == 1 ? PH_PREP : w.pass == 2 ? PH_RESID : PH_GRAM);
+  if (w.pass == 1) LFE_TRY(stream_sums_chunk(c, w.x, cld, row0, rows, w.rows_done == 0));
+  else LFE_TRY(stream_rows_chunk(c, w.pass == 2 ? 0 : 1, w.x, cld, row0, rows));
+  w.rows_done += rows;
+  if (kind == LFE_HOST) LFE_HIP(hipStreamSynchronize(c->stream));  // the caller may reuse its buffers
+  return LFE_OK;
+}
+
+// benchmark / test helpers: the synthetic panel of lfe_synth_load with the codes resident and
+// the columns generated chunk by chunk on the device (no host copy of data larger than HBM)
+int lfe_synth_load_codes(lfe_ctx* c, int64_t n, int k, int n_fe, const int32_t* n_levels, uint64_t seed) {
+  LFE_CTX(c);
+  if (n_fe != 2 || !n_levels) return fail(LFE_EINVAL, "streamed X supports two fixed effects");
+  if (k < 1 || k > 10) return fail(LFE_EINVAL, "streamed X supports 1 <= k <= 10 regressors");
+  LFE_TRY(alloc_data(c, n, k + 1, n_fe, n_levels, false, true));
+  LFE_TRY(synth_codes(c, n_levels, seed));
+  c->loaded = true;
+  return LFE_OK;
+}
+
+int lfe_stream_synth_rows(lfe_ctx* c, int64_t row0, int64_t rows, int k, const int32_t* n_levels,
+                          const double* beta, uint64_t seed) {
+  LFE_CTX(c);
+  auto& w = c->sw;
+  if (!w.on || w.pass == 0) return fail(LFE_ESTATE, "lfe_stream_begin first");
+  if (k + 1 != c->p || !n_levels || !beta) return fail(LFE_EINVAL, "k must match the loaded p - 1");
+  if (row0 < 0 || rows < 0 || row0 + rows > c->n) return fail(LFE_EINVAL, "rows outside the loaded codes");
+  if (rows == 0) return LFE_OK;
+  const int64_t cld = (rows + 63) / 64 * 64;
+  LFE_TRY(ensure_f64(c, w.x, w.x_cap, (size_t)c->p * cld));
+  LFE_TRY(synth_chunk(c, k, n_levels, beta, seed, row0, rows, w.x, cld));
+  PhaseTimer t(c, w.pass == 1 ? PH_PREP : w.pass == 2 ? PH_RESID : PH_GRAM);
+  if (w.pass == 1) LFE_TRY(stream_sums_chunk(c, w.x, cld, row0, rows, w.rows_done == 0));
+  else LFE_TRY(stream_rows_chunk(c, w.pass == 2 ? 0 : 1, w.x, cld, row0, rows));
+  w.rows_done += rows;
+  return LFE_OK;
+}
+
+int lfe_stream_end(lfe_ctx* c, double* out) {
+  LFE_CTX(c);
+  auto& w = c->sw;
+  if (!w.on || w.pass == 0) return fail(LFE_ESTATE, "lfe_stream_begin first");
+  const int pass = w.pass;
+  w.pass = 0;
+  if (w.rows_done != c->n) return fail(LFE_EINVAL, "the streamed chunks did not cover the loaded rows");
+  const int p = c->p, k = p - 1;
+  if (pass == 1) {
+    LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
+    if (c->n > 0) LFE_HIP(hipMemcpyAsync(c->raw_tile, w.tile, sizeof(double) * 256, hipMemcpyDeviceToDevice, c->stream));
+    c->raw_ready = c->sums_ready = true;
+    c->sums_zeroed = false;
+    return LFE_OK;
+  }
+  if (!out) return fail(LFE_EINVAL, "out is null");
+  std::vector<double> h(260);
+  LFE_TRY(d2h_sync(c, h.data(), w.tile, sizeof(double) * 260));
+  if (pass == 2) {  // stats[4] (sum r^2 w, sum r^2, sum y~, sum y~^2), then the k x k HC1 meat
+    for (int e = 0; e < 4; ++e) out[e] = h[256 + e];
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < k; ++j) out[4 + i * k + j] = h[(size_t)(1 + i) * 16 + (1 + j)];
+  } else {  // the (p + 1) x (p + 1) Gram of [1, y~, x~]
+    for (int i = 0; i <= p; ++i)
+      for (int j = 0; j <= p; ++j) out[i * (p + 1) + j] = h[(size_t)i * 16 + j];
+  }
+  return LFE_OK;
+}
+
 int lfe_load_begin(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_levels, int weighted) {
   LFE_CTX(c);
   if (F > 0 && !n_levels) return fail(LFE_EINVAL, "n_levels is null");
@@ -836,7 +981,10 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
     if (!fast)  // the two-FE sweeps write every alpha entry before reading any
       for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
     if (c->F > 0) {
-      if (!c->sums_ready) LFE_TRY(sweep_group_sums(c));
+      if (!c->sums_ready) {
+        if (c->sw.on) return fail(LFE_ESTATE, "streamed X: stream the group-sums pass (lfe_stream pass 1) first");
+        LFE_TRY(sweep_group_sums(c));
+      }
       if (fast) {
         // two FEs, unweighted: segment layout + one fused codes-only kernel per sweep
         LFE_TRY(demean_fast(c, tol, max_iter, check_from, &iterations, &last));
@@ -856,11 +1004,16 @@ int lfe_gram(lfe_ctx* c, double* gram_out) {
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!gram_out) return fail(LFE_EINVAL, "gram_out is null");
   PhaseTimer t(c, PH_GRAM);
-  return launch_gram(c, gram_out);
+  const int rc = launch_gram(c, gram_out);
+  if (rc == 2)
+    return fail(LFE_ENEEDPASS, "streamed X: the Gram from the group tables is unavailable or failed its "
+                               "cancellation guard; stream the design-Gram pass (lfe_stream_begin pass 3)");
+  return rc;
 }
 
 int lfe_resid(lfe_ctx* c, const double* beta_full, double* stats_out, double* hc1_meat, int keep_scores) {
   LFE_CTX(c);
+  LFE_NO_STREAM(c);
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!beta_full || !stats_out) return fail(LFE_EINVAL, "null pointer");
   if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
@@ -870,6 +1023,7 @@ int lfe_resid(lfe_ctx* c, const double* beta_full, double* stats_out, double* hc
 
 int lfe_resid_iv(lfe_ctx* c, const double* coef, double* stats_out, double* meat_out, int keep_scores) {
   LFE_CTX(c);
+  LFE_NO_STREAM(c);
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!coef || !stats_out) return fail(LFE_EINVAL, "null pointer");
   if (keep_scores && !c->scores) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
@@ -880,6 +1034,7 @@ int lfe_resid_iv(lfe_ctx* c, const double* coef, double* stats_out, double* meat
 int lfe_gram_resid(lfe_ctx* c, double* gram_out, double* beta_full_out, double* stats_out, double* hc1_meat,
                    int keep_scores) {
   LFE_CTX(c);
+  LFE_NO_STREAM(c);
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   if (!gram_out || !beta_full_out || !stats_out) return fail(LFE_EINVAL, "null pointer");
   if (keep_scores && !c->scores && c->p > 1) LFE_TRY(dalloc(&c->scores, (size_t)c->p * c->ld));
@@ -907,6 +1062,7 @@ int lfe_cluster_meat_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, do
 
 int lfe_copy_demeaned(lfe_ctx* c, double* const* cols_out, int64_t* n_out) {
   LFE_CTX(c);
+  LFE_NO_STREAM(c);
   if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
   double* d = nullptr;
   LFE_TRY(dalloc(&d, (size_t)c->p * std::max<int64_t>(c->n, 1)));
@@ -925,6 +1081,7 @@ int lfe_copy_demeaned(lfe_ctx* c, double* const* cols_out, int64_t* n_out) {
 
 int lfe_copy_inputs(lfe_ctx* c, double* const* cols_out, int32_t* const* codes_out) {
   LFE_CTX(c);
+  LFE_NO_STREAM(c);
   if (!c->loaded) return fail(LFE_ESTATE, "nothing loaded");
   for (int j = 0; j < c->p && c->n > 0 && cols_out; ++j)
     LFE_HIP(hipMemcpyAsync(cols_out[j], c->X + (size_t)j * c->ld, sizeof(double) * c->n, hipMemcpyDeviceToHost,

@@ -201,6 +201,10 @@ int records_layout(lfe_ctx* c) {
 using namespace lfe;
 
 int lfe_compress(lfe_ctx* c, int64_t* n_records_out) {
+  if (c && c->sw.on) {
+    set_error("not available with streamed X (lfe_load_codes)");
+    return LFE_ESTATE;
+  }
   if (!c) return fail(LFE_EINVAL, "null context");
   if (!n_records_out) return fail(LFE_EINVAL, "null pointer");
   if (!c->loaded) return fail(LFE_ESTATE, "lfe_load first");

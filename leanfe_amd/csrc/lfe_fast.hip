@@ -639,6 +639,196 @@ int sums4(lfe_ctx* c) {
   return LFE_OK;
 }
 
+// ---------------------------------------------------------------------------
+// out-of-core X: group sums and raw Gram of one streamed row chunk (lfe_stream.hip)
+// ---------------------------------------------------------------------------
+// The chunk's rows in input order (no partition): lane (kq, c) holds column c of rows
+// 16 g + 4 kq + r as in k_sums2_raw; every FE's sums go to global tables (int64 on the exact
+// path, f64 otherwise), the shifted raw Gram to one MFMA chain per row.  A row is kept iff every
+// FE's pre-filter count of its code exceeds 1 (the single-pass drop, polars_impl.py:477-482).
+struct StreamSumsArgs {
+  const double* X;  // [p][ld] chunk columns
+  int64_t ld, rows;
+  int p, F;
+  const int32_t* code[kMaxFE];     // the chunk's codes (input order)
+  const int32_t* cnt_pre[kMaxFE];  // pre-filter counts (all rows)
+  int64_t toff[kMaxFE];            // table offset (entries) of FE f in s64 / sdbl
+  unsigned long long* s64;
+  double* sdbl;
+  const double* fixq;   // the chunk's quanta (k_fix_quanta)
+  const double* shift;  // [16] raw-Gram shift
+  double* raw_part;     // [blocks][256]
+};
+
+template <int NF>
+__global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kq = lane >> 4, c = lane & 15;
+  const int p = a.p;
+  const bool col = c < p;
+  const bool fix = fix_on(a.fixq, p);
+  const double fscale = col ? a.fixq[c] : 0.0;
+  const double cm = col ? 1.0 : 0.0;
+  const double zc = (c == 15 ? 1.0 : 0.0) - (col ? a.shift[c] : 0.0);
+  const double* __restrict__ xc = a.X + (int64_t)(col ? c : 0) * a.ld;
+  d4 racc = d4{0.0, 0.0, 0.0, 0.0};
+  const int64_t ngroups = (a.rows + 15) >> 4;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + wave; g < ngroups; g += (int64_t)gridDim.x * 4) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = g * 16 + kq * 4 + r;
+      bool keep = row < a.rows;
+      int32_t gc[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        gc[f] = keep ? a.code[f][row] : 0;
+        keep = keep && a.cnt_pre[f][gc[f]] > 1;
+      }
+      const double xv = row < a.rows ? xc[row] : 0.0;
+      const double z = keep ? __builtin_fma(xv, cm, zc) : 0.0;
+      racc = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc, 0, 0, 0);
+      if (keep && col) {
+        if (fix) {
+          const unsigned long long xi =
+              (unsigned long long)__double_as_longlong(__builtin_fma(xv, fscale, kFixMagic)) - kFixMagicBits;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) atomicAdd(&a.s64[a.toff[f] + (int64_t)gc[f] * p + c], xi);
+        } else {
+#pragma unroll
+          for (int f = 0; f < NF; ++f) atomicAdd(&a.sdbl[a.toff[f] + (int64_t)gc[f] * p + c], xv);
+        }
+      }
+    }
+  }
+  // waves' tiles summed in LDS in wave order (lane (kq, c) holds rows kq + 4 rr of column c)
+  __shared__ double rred[256];
+  for (int wv = 0; wv < 4; ++wv) {
+    __syncthreads();
+    if (wave == wv)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int e = (kq + 4 * rr) * 16 + c;
+        rred[e] = (wv == 0) ? racc[rr] : rred[e] + racc[rr];
+      }
+  }
+  __syncthreads();
+  for (int e = tid; e < 256; e += 256) a.raw_part[(int64_t)blockIdx.x * 256 + e] = rred[e];
+}
+
+// S_f += the chunk's sums (in chunk order: deterministic), the chunk tables cleared for the next
+__global__ void k_stream_fold(unsigned long long* __restrict__ s64, double* __restrict__ sdbl, int64_t m, int p,
+                              const double* __restrict__ fq, int F, const int64_t* __restrict__ toff_end,
+                              double* const* __restrict__ S) {
+  const bool fix = fix_on(fq, p);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+    int f = 0;
+    while (f + 1 < F && e >= toff_end[f]) ++f;
+    const int64_t j = e - (f ? toff_end[f - 1] : 0);
+    const double v = fix ? (double)(long long)s64[e] * fq[kMaxCols + (int)(j % p)] : sdbl[e];
+    S[f][j] += v;
+    s64[e] = 0ull;
+    sdbl[e] = 0.0;
+  }
+}
+
+// shift of the raw Gram for streamed chunks: the first row of the first chunk (both halves,
+// as k_raw_shift leaves them for one process)
+__global__ void k_stream_shift(const double* __restrict__ X, int64_t ld, int p, double* __restrict__ sh) {
+  const int j = threadIdx.x;
+  if (j < 16) {
+    const double v = j < p ? X[(int64_t)j * ld] : 0.0;
+    sh[j] = v;
+    sh[16 + j] = v;
+  }
+}
+
+__global__ void k_tile_add(double* __restrict__ acc, const double* __restrict__ t, int m) {
+  for (int e = threadIdx.x; e < m; e += blockDim.x) acc[e] += t[e];
+}
+
+void stream_tile_add(lfe_ctx* c, const double* t, int m) {
+  hipLaunchKernelGGL(k_tile_add, dim3(1), dim3(256), 0, c->stream, c->sw.tile, t, m);
+}
+
+// One streamed chunk of the sums pass: [p][ld] columns on the device (rows rows starting at
+// input row row0).  Column statistics and quanta of this chunk (as k_part_scatter / sums4 form
+// them), then int64 group sums into the chunk tables and their fold into S in chunk order.
+int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows, bool first) {
+  auto& w = c->sw;
+  const int p = c->p, F = c->F;
+  int64_t m = 0;
+  std::vector<int64_t> tend(F);
+  StreamSumsArgs a{};
+  for (int f = 0; f < F; ++f) {
+    a.toff[f] = m;
+    m += (int64_t)c->fe[f].G * p;
+    tend[f] = m;
+    a.code[f] = c->fe[f].code + row0;
+    a.cnt_pre[f] = c->fe[f].cnt_pre;
+  }
+  if (first) {
+    LFE_TRY(ensure_f64(c, c->raw_shift, c->raw_shift_cap, 32));
+    hipLaunchKernelGGL(k_stream_shift, dim3(1), dim3(64), 0, c->stream, X, ld, p, c->raw_shift);
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(ensure_f64(c, w.s64, w.s64_cap, (size_t)m));
+    LFE_TRY(ensure_f64(c, w.sdbl, w.sdbl_cap, (size_t)m));
+    LFE_HIP(hipMemsetAsync(w.s64, 0, sizeof(double) * m, c->stream));
+    LFE_HIP(hipMemsetAsync(w.sdbl, 0, sizeof(double) * m, c->stream));
+    LFE_TRY(ensure_f64(c, w.tile, w.tile_cap, 272));
+    LFE_HIP(hipMemsetAsync(w.tile, 0, sizeof(double) * 272, c->stream));
+    LFE_TRY(ensure_f64(c, w.toff, w.toff_cap, 2 * kMaxFE));
+    LFE_TRY(h2d_small(c, w.toff, tend.data(), sizeof(int64_t) * F));
+    std::vector<double*> sp(F);
+    for (int f = 0; f < F; ++f) sp[f] = c->fe[f].S;
+    LFE_TRY(h2d_small(c, w.toff + kMaxFE, sp.data(), sizeof(double*) * F));
+  }
+  {
+    ProfScope _ps(c, K_FIX_SUMS);
+    constexpr int64_t kStatRows = 16384;
+    const int nch = (int)std::max<int64_t>(1, (rows + kStatRows - 1) / kStatRows);
+    LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nch * p));
+    LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
+    hipLaunchKernelGGL(k_col_stats, dim3(nch), dim3(256), 0, c->stream, X, ld, rows, p, kStatRows, c->colstat);
+    LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, 3 * kMaxCols));
+    hipLaunchKernelGGL(k_fix_quanta, dim3(p), dim3(256), 0, c->stream, c->colstat, nch, rows,
+                       c->iscratch + kIscratchCmax, c->F, c->fixq);
+    LFE_HIP(hipGetLastError());
+  }
+  a.X = X;
+  a.ld = ld;
+  a.rows = rows;
+  a.p = p;
+  a.F = F;
+  a.s64 = reinterpret_cast<unsigned long long*>(w.s64);
+  a.sdbl = w.sdbl;
+  a.fixq = c->fixq;
+  a.shift = c->raw_shift;
+  const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * 8, ((rows + 15) / 16 + 3) / 4));
+  LFE_TRY(ensure_f64(c, c->raw_part, c->raw_part_cap, (size_t)nblocks * 256));
+  LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
+  a.raw_part = c->raw_part;
+  {
+    ProfScope _ps(c, K_GROUP_SUMS);
+    if (F != 2) {
+      set_error("streamed X passes support two fixed effects");
+      return LFE_EINVAL;
+    }
+    hipLaunchKernelGGL(k_stream_sums<2>, dim3(nblocks), dim3(256), 0, c->stream, a);
+    LFE_HIP(hipGetLastError());
+  }
+  {
+    ProfScope _ps(c, K_FIX_SUMS);
+    hipLaunchKernelGGL(k_stream_fold, dim3(grid_for(m)), dim3(kBlock), 0, c->stream,
+                       reinterpret_cast<unsigned long long*>(w.s64), w.sdbl, m, p, c->fixq, F,
+                       reinterpret_cast<const int64_t*>(w.toff), reinterpret_cast<double* const*>(w.toff + kMaxFE));
+    LFE_HIP(hipGetLastError());
+    reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
+    hipLaunchKernelGGL(k_tile_add, dim3(1), dim3(256), 0, c->stream, w.tile, c->raw_tile, 256);
+    LFE_HIP(hipGetLastError());
+  }
+  return LFE_OK;
+}
+
 int exact_sums_on(lfe_ctx* c, int* on) {
   *on = 0;
   if (!c->exact_sums || !c->fixq) return LFE_OK;

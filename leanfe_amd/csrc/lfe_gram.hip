@@ -1157,6 +1157,7 @@ int launch_gram(lfe_ctx* c, double* host_gram) {
       LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 257));
       done = h[256] == 1.0;
     }
+    if (!done && c->sw.on) return 2;  // streamed X: the caller streams the design-Gram pass
     if (!done) {
       LFE_TRY(design_rows_enqueue(c, a, c->dred));
       LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 256));
@@ -1166,6 +1167,7 @@ int launch_gram(lfe_ctx* c, double* host_gram) {
       for (int j = 0; j < D; ++j) host_gram[i * D + j] = h[(size_t)i * 16 + j];
     return LFE_OK;
   }
+  if (c->sw.on) return 2;
   return gram_dispatch<GRAM_DESIGN>(c, a, c->p + 1, 0, c->p + 1, host_gram, nullptr, 0);
 }
 
@@ -1211,6 +1213,154 @@ static int resid_rows(lfe_ctx* c, GramArgs a, double* meat, double* stats) {
   std::vector<double> h(260);
   LFE_TRY(d2h_sync(c, h.data(), c->dred, sizeof(double) * 260));
   unpack_resid(h.data(), c->p - 1, meat, stats);
+  return LFE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// out-of-core X: residual / design-Gram pass over one streamed chunk (lfe_stream.hip)
+// ---------------------------------------------------------------------------
+// Row per lane in input order; x~ = x - alpha_P[h] - alpha_Q[q] with the alpha rows gathered
+// from the global tables (L2 / MALL resident; the pass is bound by the host link, not by
+// these gathers).  MODE 0: r = y~ - beta0 - sum_j beta_j x~_j, RSS / TSS statistics and the HC1
+// meat (as k_resid_rows: tile (1 + i, 1 + j) = meat (i, j), stats at 256..259); MODE 1: the
+// Gram of [1, y~, x~] (as k_design_rows: column 0 = intercept, 1 + c = data column c).
+struct StreamRowArgs {
+  const double* X;
+  int64_t ld, rows;
+  int p;
+  const int32_t* code[2];
+  const int32_t* cnt_pre[2];
+  const double* alpha[2];
+  const double* beta;  // MODE 0: [p] beta_full
+};
+
+template <int PM, int MODE>
+__global__ __launch_bounds__(256) void k_stream_rows(StreamRowArgs a, double* __restrict__ partial) {
+  constexpr int KM = PM - 1;
+  constexpr int NM = MODE == 0 ? KM * (KM + 1) / 2 : (PM + 1) * (PM + 2) / 2;  // meat / Gram of [1, d]
+  constexpr int NS = MODE == 0 ? 4 : 0;
+  __shared__ double red[4][NM + NS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int p = a.p;
+  double beta[PM];
+#pragma unroll
+  for (int cc = 0; cc < PM; ++cc) beta[cc] = (MODE == 0 && cc < p) ? a.beta[cc] : 0.0;
+  double m[NM];
+#pragma unroll
+  for (int e = 0; e < NM; ++e) m[e] = 0.0;
+  double st[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t row = (int64_t)blockIdx.x * 256 + tid; row < a.rows; row += (int64_t)gridDim.x * 256) {
+    const int32_t g0 = a.code[0][row], g1 = a.code[1][row];
+    if (!(a.cnt_pre[0][g0] > 1 && a.cnt_pre[1][g1] > 1)) continue;  // dropped singleton
+    const double* a0 = a.alpha[0] + (int64_t)g0 * p;
+    const double* a1 = a.alpha[1] + (int64_t)g1 * p;
+    double xt[PM];
+#pragma unroll
+    for (int cc = 0; cc < PM; ++cc) xt[cc] = cc < p ? a.X[(int64_t)cc * a.ld + row] - a0[cc] - a1[cc] : 0.0;
+    if (MODE == 0) {
+      double res = xt[0] - beta[0];  // polars_impl.py:229
+#pragma unroll
+      for (int cc = 1; cc < PM; ++cc) res -= beta[cc] * xt[cc];
+      const double rr = res * res;
+      st[0] += rr;
+      st[1] += rr;
+      st[2] += xt[0];
+      st[3] += xt[0] * xt[0];
+      double wv[KM];
+#pragma unroll
+      for (int j = 0; j < KM; ++j) wv[j] = xt[j + 1] * res;
+      int e = 0;
+#pragma unroll
+      for (int i = 0; i < KM; ++i)
+#pragma unroll
+        for (int j = i; j < KM; ++j, ++e) m[e] += wv[i] * wv[j];
+    } else {
+      double d[PM + 1];
+      d[0] = 1.0;
+#pragma unroll
+      for (int cc = 0; cc < PM; ++cc) d[cc + 1] = xt[cc];
+      int e = 0;
+#pragma unroll
+      for (int i = 0; i <= PM; ++i)
+#pragma unroll
+        for (int j = i; j <= PM; ++j, ++e) m[e] += d[i] * d[j];
+    }
+  }
+  const auto addop = [](double x, double y) { return x + y; };
+#pragma unroll
+  for (int e = 0; e < NM; ++e) {
+    const double v = wave_reduce63(m[e], 0.0, addop);
+    if (lane == 63) red[wave][e] = v;
+  }
+#pragma unroll
+  for (int e = 0; e < NS; ++e) {
+    const double v = wave_reduce63(st[e], 0.0, addop);
+    if (lane == 63) red[wave][NM + e] = v;
+  }
+  __syncthreads();
+  double* out = partial + (int64_t)blockIdx.x * 260;
+  for (int t = tid; t < 260; t += 256) {
+    double v = 0.0;
+    if (t < 256) {
+      int i = t / 16, j = t % 16, e = -1;
+      if (MODE == 0) {
+        --i;
+        --j;  // tile (1 + i, 1 + j) = meat (i, j)
+        if (i >= 0 && j >= 0 && i < KM && j < KM) {
+          const int lo2 = i < j ? i : j, hi2 = i < j ? j : i;
+          e = lo2 * KM - lo2 * (lo2 - 1) / 2 + (hi2 - lo2);
+        }
+      } else if (i <= PM && j <= PM) {  // design index 0 = intercept, 1 + c = column c
+        const int lo2 = i < j ? i : j, hi2 = i < j ? j : i;
+        e = lo2 * (PM + 1) - lo2 * (lo2 - 1) / 2 + (hi2 - lo2);
+      }
+      if (e >= 0) v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    } else if (MODE == 0) {
+      const int e = NM + (t - 256);
+      v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    }
+    out[t] = v;
+  }
+}
+
+// One streamed chunk of the residual (mode 0) or design-Gram (mode 1) pass: the chunk's tile
+// is added to c->sw.tile in chunk order.
+int stream_rows_chunk(lfe_ctx* c, int mode, const double* X, int64_t ld, int64_t row0, int64_t rows) {
+  const int p = c->p;
+  if (c->F != 2 || p > 11) {
+    set_error("streamed X passes support two fixed effects and p <= 11");
+    return LFE_EINVAL;
+  }
+  StreamRowArgs a{};
+  a.X = X;
+  a.ld = ld;
+  a.rows = rows;
+  a.p = p;
+  for (int f = 0; f < 2; ++f) {
+    a.code[f] = c->fe[f].code + row0;
+    a.cnt_pre[f] = c->fe[f].cnt_pre;
+    a.alpha[f] = c->fe[f].alpha;
+  }
+  a.beta = c->dbeta;
+  const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * 4, (rows + 255) / 256));
+  LFE_TRY(ensure_scratch(c, (size_t)nblocks * 260));
+  {
+    ProfScope _ps(c, mode == 0 ? K_GRAM_RESID : K_GRAM_DESIGN);
+    const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
+#define SR(PM_, M_) hipLaunchKernelGGL((k_stream_rows<PM_, M_>), dim3(nblocks), dim3(256), 0, c->stream, a, c->scratch)
+    if (mode == 0) {
+      if (PM == 4) SR(4, 0); else if (PM == 8) SR(8, 0); else SR(12, 0);
+    } else {
+      if (PM == 4) SR(4, 1); else if (PM == 8) SR(8, 1); else SR(12, 1);
+    }
+#undef SR
+    LFE_HIP(hipGetLastError());
+  }
+  LFE_TRY(ensure_dred(c, 544));
+  hipLaunchKernelGGL(k_reduce_partials, dim3(260), dim3(256), 0, c->stream, c->scratch, nblocks, (int64_t)260,
+                     c->dred + 272);
+  LFE_HIP(hipGetLastError());
+  stream_tile_add(c, c->dred + 272, 260);
   return LFE_OK;
 }
 

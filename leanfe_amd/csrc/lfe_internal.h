@@ -288,6 +288,22 @@ struct lfe_ctx {
   double* dspec = nullptr;
   size_t dspec_elems = 0;
   bool gram_spec = false;
+  // out-of-core X (lfe_load_codes + lfe_stream_*): codes resident, X streamed in row chunks
+  struct StreamWS {
+    bool on = false;       // codes-only context
+    int pass = 0;          // 0 idle, 1 group sums + raw Gram, 2 residual, 3 design Gram
+    int64_t rows_done = 0;
+    double* x = nullptr;   // [p][cld] the chunk's columns
+    size_t x_cap = 0;
+    double* s64 = nullptr;   // [sum_f G_f p] chunk group sums, int64 bits (exact path)
+    size_t s64_cap = 0;
+    double* sdbl = nullptr;  // the same in f64 (a chunk whose range defeats the fixed point)
+    size_t sdbl_cap = 0;
+    double* tile = nullptr;  // [272] tile (+ statistics) accumulated over the chunks, in order
+    size_t tile_cap = 0;
+    double* toff = nullptr;  // [2 kMaxFE] 8-byte slots: table ends (int64), table pointers
+    size_t toff_cap = 0;
+  } sw;
   lfe::Timings tm;
   lfe::Prof prof;
 };
@@ -321,6 +337,10 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
 // speculative Gram-from-tables + device Cholesky, enqueued behind a convergence check's read-back
 // so that the GPU keeps working while the host decides (lfe_gram.hip); *queued = 1 if enqueued
 int gram_spec_enqueue(lfe_ctx* c, int* queued);
+// out-of-core X (lfe_fast.hip / lfe_gram.hip): one streamed chunk ([p][ld] on the device)
+int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows, bool first);
+int stream_rows_chunk(lfe_ctx* c, int mode, const double* X, int64_t ld, int64_t row0, int64_t rows);
+void stream_tile_add(lfe_ctx* c, const double* t, int m);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
 void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out);  // sum of [nblocks][256] tiles
 // --- YOCO records (lfe_compress.hip) ---
@@ -340,6 +360,9 @@ int launch_copy_demeaned(lfe_ctx* c, double* dev_out);
 int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* flag, hipStream_t s);
 
 // --- synthetic panel (lfe_synth.hip) ---
+int synth_chunk(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed, int64_t row0,
+                int64_t rows, double* X, int64_t ld);
+int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed);
 int launch_synth(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed,
                  int64_t row_offset);
 // owner-sharded synthetic shard: count the rows of [0, n_total) whose code of FE f is in [lo, hi)

@@ -315,6 +315,10 @@ int lfe_factorize_ids(lfe_ctx* c, int64_t n, const int64_t* ids, int32_t* codes_
 }
 
 int lfe_count_distinct_rows(lfe_ctx* c, int n_x, int64_t* n_distinct_out) {
+  if (c && c->sw.on) {
+    set_error("not available with streamed X (lfe_load_codes)");
+    return LFE_ESTATE;
+  }
   if (!c) return fail(LFE_EINVAL, "null context");
   if (!n_distinct_out) return fail(LFE_EINVAL, "null pointer");
   if (!c->loaded) return fail(LFE_ESTATE, "lfe_load first");

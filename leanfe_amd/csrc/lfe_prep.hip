@@ -371,7 +371,7 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   }
   __syncthreads();
   // ---- move columns through the stage: gather in row order, store in bucket order ----
-  const int ncol = a.cols ? a.p + (a.w ? 1 : 0) : 0;
+  const int ncol = a.cols == 1 ? a.p + (a.w ? 1 : 0) : 0;  // cols 2: the codes only (streamed X)
   typedef double d2v __attribute__((ext_vector_type(2)));
   // rows i < n are loaded in 16-byte pairs: i is even and the columns are padded to a multiple
   // of 64 rows, so row i + 1 lies inside the column even when i + 1 == n.  A full chunk (every
@@ -854,13 +854,13 @@ int prepare_layout(lfe_ctx* c) {
     L.part = PartGeom{nth, per, nw, lds};
     // the input row index of each layout row is written only when a caller needs it
     // (ensure_layout_orig: cluster, records and demeaned-column export paths)
-    LFE_TRY(launch_part_scatter(c, /*cols=*/1, /*orig=*/0));
+    LFE_TRY(launch_part_scatter(c, /*cols=*/c->sw.on ? 2 : 1, /*orig=*/0));
     L.orig_pending = true;
     LFE_HIP(hipGetLastError());
     L.bstart.assign(nb + 1, 0);
     LFE_TRY(d2h_wait(c, L.bstart.data(), sizeof(int32_t) * nb));
     L.bstart[nb] = (int32_t)n;
-    L.X = c->Xp;
+    L.X = c->sw.on ? nullptr : c->Xp;
     L.w = c->w ? c->wp : nullptr;
     for (int f = 0; f < c->F; ++f) L.code[f] = c->codes_p + (size_t)f * c->ld;
     L.orig = nullptr;
@@ -955,7 +955,7 @@ int prepare_layout(lfe_ctx* c) {
   LFE_TRY(d2h_async(c, c->iscratch, sizeof(h)));
   // the constant group sums S_f do not depend on the FE order: enqueue them now so the
   // GPU keeps working while the host reads the counts and returns (lfe_demean skips them)
-  if (c->F > 0 && c->n > 0) {
+  if (c->F > 0 && c->n > 0 && !c->sw.on) {  // streamed X: the sums come from lfe_stream pass 1
     LFE_TRY(sweep_group_sums(c));
     c->sums_ready = true;
   }

@@ -59,8 +59,9 @@ __global__ void k_synth_rows(SynthArgs a, double* __restrict__ X, int64_t ld, in
     int32_t g[kMaxFE];
     for (int f = 0; f < a.F; ++f) {
       g[f] = synth_code(i, f, a.L[f], seed);
-      a.code[f][r] = g[f];
+      if (a.code[f]) a.code[f][r] = g[f];
     }
+    if (!X) continue;  // codes only (streamed X keeps the codes resident, lfe_synth_load_codes)
     const double a0 = a.F > 0 ? a.eff[0][g[0]] : 0.0;
     double y = 0.0;
     for (int j = 0; j < a.k; ++j) {
@@ -153,6 +154,51 @@ static int synth_fill(lfe_ctx* c, int k, const int32_t* levels, const double* be
 
 int launch_synth(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed, int64_t row_offset) {
   return synth_fill(c, k, levels, beta, seed, row_offset, nullptr);
+}
+
+// streamed X on the synthetic panel: the [p][ld] columns of global rows [row0, row0 + rows)
+// into X (codes not written: they are resident), as lfe_synth_load would hold them
+int synth_chunk(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed, int64_t row0,
+                int64_t rows, double* X, int64_t ld) {
+  SynthArgs a{};
+  a.F = c->F;
+  a.k = k;
+  std::vector<double*> eff(c->F, nullptr);
+  double scale = 1.0;
+  for (int f = 0; f < c->F; ++f) {
+    a.L[f] = levels[f];
+    a.code[f] = nullptr;
+    LFE_HIP(hipMalloc(&eff[f], sizeof(double) * (size_t)levels[f]));
+    hipLaunchKernelGGL(k_synth_effects, dim3(grid_for(levels[f])), dim3(kBlock), 0, c->stream, eff[f], levels[f],
+                       f, scale, seed);
+    LFE_HIP(hipGetLastError());
+    a.eff[f] = eff[f];
+    scale *= 0.5;
+  }
+  for (int j = 0; j < k; ++j) a.beta[j] = beta[j];
+  if (rows)
+    hipLaunchKernelGGL(k_synth_rows, dim3(grid_for(rows, kBlock, 256 * 16)), dim3(kBlock), 0, c->stream, a, X, ld,
+                       rows, seed, row0, nullptr);
+  LFE_HIP(hipGetLastError());
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  for (int f = 0; f < c->F; ++f) LFE_HIP(hipFree(eff[f]));
+  return LFE_OK;
+}
+
+int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed) {
+  SynthArgs a{};
+  a.F = c->F;
+  a.k = 0;
+  for (int f = 0; f < c->F; ++f) {
+    a.L[f] = levels[f];
+    a.code[f] = c->fe[f].code;
+  }
+  if (c->n)
+    hipLaunchKernelGGL(k_synth_rows, dim3(grid_for(c->n, kBlock, 256 * 16)), dim3(kBlock), 0, c->stream, a,
+                       static_cast<double*>(nullptr), c->ld, c->n, seed, (int64_t)0, nullptr);
+  LFE_HIP(hipGetLastError());
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  return LFE_OK;
 }
 
 int synth_count_owned(lfe_ctx* c, int64_t n_total, int f, int32_t L, int32_t lo, int32_t hi, uint64_t seed,

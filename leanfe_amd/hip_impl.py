@@ -32,13 +32,19 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                fe_cols: list[str] | None = None, formula: str | None = None, strategy: str = "auto",
                weights: str | None = None, max_iter: int = 50, vcov: str = "iid",
                cluster_cols: list[str] | None = None, ssc: bool = True, sample_frac: float | None = None,
-               device: int | None = None, engine: Engine | None = None, quiet: bool = False) -> LeanFEResult:
+               device: int | None = None, engine: Engine | None = None, quiet: bool = False,
+               out_of_core: bool | None = None, chunk_rows: int = 1 << 22) -> LeanFEResult:
     """Fixed-effects OLS on the MI355X engine; arguments as ``leanfe_polars``.
 
     ``vcov`` accepts 'iid', 'HC1' (or 'hc1') and 'cluster'.  ``engine`` lets a
     caller reuse an ``Engine`` (e.g. one joined to an RCCL communicator with
     ``leanfe_amd.dist.attach``: every rank then passes its own row shard and
-    gets the global fit; FE/cluster columns must then be global int codes)."""
+    gets the global fit; FE/cluster columns must then be global int codes).
+
+    ``out_of_core`` (data larger than HBM; default: env ``LEANFE_HIP_OUT_OF_CORE``): only the FE
+    codes are loaded; the columns are streamed in ``chunk_rows`` row chunks through the group
+    sums, (if needed) the design Gram and the residual pass.  Two FEs, no weights,
+    instruments, factors or clusters; IID or HC1."""
     t_start = time.perf_counter()
     say = (lambda *a: None) if quiet else print
     if formula is not None:
@@ -98,6 +104,17 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             codes.append(c)
             levels.append(g)
         levels = dist.agree_levels(eng, levels)
+        if out_of_core is None:
+            out_of_core = os.environ.get("LEANFE_HIP_OUT_OF_CORE", "0") == "1"
+        if out_of_core:
+            if (len(fe_cols) != 2 or weights is not None or instruments or factor_vars or interactions
+                    or v == "cluster" or sharded or strategy not in ("auto", "alt_proj")):
+                raise ValueError("out_of_core fits take two FEs, no weights / instruments / factors / "
+                                 "clusters, vcov 'iid' or 'HC1' and strategy 'alt_proj'")
+            source = data if stream else cols
+            n_rows_oc = n_rows if stream else len(cols[y_col])
+            return _out_of_core_fit(eng, source, n_rows_oc, y_col, x_cols, fe_cols, codes, levels, v, vcov,
+                                    demean_tol, max_iter, int(chunk_rows), formula, t_start, say)
         w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
         # polars_impl.py:180: an all-ones instrument stops 2SLS from adding an intercept to Z.
         # Demeaned instruments cannot be all ones; without FEs they are the raw columns.
@@ -232,6 +249,64 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                         iterations=iterations, vcov_type=vcov, is_iv=False, n_instruments=None,
                         n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
                         fe_dims=fe_dims, r_squared=r_squared, compression_ratio=est_comp_ratio,
+                        rss=rss, tss=tss, backend="hip", timings=timings)
+
+
+def _out_of_core_fit(eng, source, n_rows, y_col, x_cols, fe_cols, codes, levels, v, vcov, demean_tol, max_iter,
+                     chunk_rows, formula, t_start, say) -> LeanFEResult:
+    """Out-of-core X (data larger than HBM): the FE codes and their layouts stay on the GPU, the
+    columns [y] + x are streamed from host memory (or a Parquet file, re-read per pass) in row
+    chunks through pass 1 (group sums S_f and the raw Gram, polars_impl.py:491-508), the
+    codes-only sweeps, the Gram from the group tables (pass 3, the explicit design Gram, when
+    that is unavailable), the host solve (:212-226) and pass 2 (residual, RSS and the HC1 meat,
+    :229, std_errors.py:217-282).  Same estimator, same stop rule and iterations."""
+    from leanfe_amd._lib import NeedsStreamPass
+
+    num_cols = [y_col] + list(x_cols)
+    p, k = len(num_cols), len(x_cols)
+    say("Using FWL/alternating projections strategy (out-of-core columns)...")
+
+    def chunks():
+        if isinstance(source, str):
+            for row0, b in frame.stream_parquet(source, num_cols, batch_rows=chunk_rows):
+                yield row0, [b[c] for c in num_cols]
+        else:
+            for r0 in range(0, n_rows, chunk_rows):
+                yield r0, [np.asarray(source[c][r0:r0 + chunk_rows], dtype=np.float64) for c in num_cols]
+
+    t0 = time.perf_counter()
+    eng.load_codes(codes, levels, p)
+    t_load = time.perf_counter() - t0
+    n_obs, fe_dims, fe_card = eng.drop_singletons()
+    eng.stream_pass(1, chunks())
+    order = sorted(range(len(fe_cols)), key=lambda i: fe_card[i])  # polars_impl.py:485
+    iterations, _ = eng.demean(order, demean_tol, max_iter, check_from=3)
+    absorbed_df = sum(fe_dims) - len(fe_cols)
+    df_resid = n_obs - (k + 1) - absorbed_df
+    try:
+        G = eng.gram()
+    except NeedsStreamPass:
+        G = eng.stream_pass(3, chunks())[:(p + 1) ** 2].reshape(p + 1, p + 1)
+    XtX, Xty = inference.split_gram(G)
+    beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # host, polars_impl.py:212-226
+    Vb = XtX_inv[1:, 1:]
+    # IID: the residual statistics from the Gram unless r'r cancels there; HC1: the meat pass
+    stats = inference.stats_from_gram(G, beta_full) if v == "iid" else None
+    if stats is None:
+        out = eng.stream_pass(2, chunks(), beta_full)
+        stats, meat = out[:4], out[4:4 + k * k].reshape(k, k)
+    if v == "iid":
+        se = inference.se_iid(Vb, stats[0], df_resid)
+    else:
+        se = inference.se_hc1(Vb, meat, n_obs, df_resid)
+    rss_w, rss, sum_y, sum_y2 = stats
+    tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
+    timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
+    return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta_full[1:]))),
+                        std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
+                        iterations=iterations, vcov_type=vcov, is_iv=False, n_instruments=None,
+                        n_clusters=None, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
+                        fe_dims=fe_dims, r_squared=1 - rss / tss if tss > 0 else None, compression_ratio=None,
                         rss=rss, tss=tss, backend="hip", timings=timings)
 
 
