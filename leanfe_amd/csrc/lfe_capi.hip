@@ -569,8 +569,7 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   dfree(c->pcounts);
   dfree(c->psums);
   dfree(c->items_d);
-  dfree(c->bitems_d);
-  dfree(c->xitems_d);
+  c->bitems_d = c->xitems_d = nullptr;  // views into items_d
   dfree(c->seg_off);
   dfree(c->seg_q);
   dfree(c->seg_aux);

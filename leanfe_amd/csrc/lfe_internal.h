@@ -180,10 +180,8 @@ struct lfe_ctx {
   int32_t* origp = nullptr;      // [ld]
   int32_t* items_d = nullptr;    // device work items [n_items][4]
   size_t items_cap = 0;
-  int32_t* bitems_d = nullptr;   // device [nb + 1]: first work item of each bucket
-  size_t bitems_cap = 0;
-  int32_t* xitems_d = nullptr;   // device [n_xgrid]: work item of each block, XCD-grouped (-1: idle)
-  size_t xitems_cap = 0;
+  int32_t* bitems_d = nullptr;   // device [nb + 1]: first work item of each bucket (in items_d)
+  int32_t* xitems_d = nullptr;   // device [n_xgrid]: work item of each block, XCD-grouped (-1: idle; in items_d)
   int n_xgrid = 0;
   // segment layout (fast path, F == 2): kept rows sorted by the primary code
   int32_t* seg_off = nullptr;    // [nb * B + 1] local row offsets of each primary group

@@ -684,20 +684,19 @@ static int build_items(lfe_ctx* c) {
     if (xg.empty()) xg.push_back(0);
     c->n_xgrid = (int)xg.size();
   }
-  LFE_TRY(ensure_items(c, L.n_items));
-  LFE_TRY(ensure_i32(c, c->bitems_d, c->bitems_cap, bfirst.size()));
-  LFE_TRY(ensure_i32(c, c->xitems_d, c->xitems_cap, xg.size()));
-  // upload through pinned staging, asynchronously (the staging buffer is next written
-  // only after later stream synchronizations)
-  const size_t ib = sizeof(int32_t) * L.hitems.size(), bb = sizeof(int32_t) * bfirst.size();
-  const size_t xb = sizeof(int32_t) * xg.size();
+  // items, bucket firsts and the XCD order share one device buffer and one upload through
+  // pinned staging, asynchronously (the staging buffer is next written only after later stream
+  // synchronizations); bitems_d / xitems_d point into it
+  const size_t ni = L.hitems.size(), nbf = bfirst.size(), nx = xg.size();
+  LFE_TRY(ensure_items(c, (ni + nbf + nx + 3) / 4));
+  c->bitems_d = c->items_d + ni;
+  c->xitems_d = c->items_d + ni + nbf;
+  const size_t ib = sizeof(int32_t) * ni, bb = sizeof(int32_t) * nbf, xb = sizeof(int32_t) * nx;
   LFE_TRY(ensure_pinned_items(c, ib + bb + xb));
   memcpy(c->hpin_items, L.hitems.data(), ib);
   memcpy(c->hpin_items + ib, bfirst.data(), bb);
   memcpy(c->hpin_items + ib + bb, xg.data(), xb);
-  LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib, hipMemcpyHostToDevice, c->stream));
-  LFE_HIP(hipMemcpyAsync(c->bitems_d, c->hpin_items + ib, bb, hipMemcpyHostToDevice, c->stream));
-  LFE_HIP(hipMemcpyAsync(c->xitems_d, c->hpin_items + ib + bb, xb, hipMemcpyHostToDevice, c->stream));
+  LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb, hipMemcpyHostToDevice, c->stream));
   return LFE_OK;
 }
 
