@@ -284,6 +284,21 @@ int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count) {
   return LFE_OK;
 }
 
+// several independent f64 sums in one RCCL group (one launch, one latency)
+int allreduce_sum_f64_many(lfe_ctx* c, const std::vector<std::pair<double*, size_t>>& bufs) {
+  if (c->world <= 1) return LFE_OK;
+  if (c->emu) {
+    for (auto& b : bufs)
+      if (b.second) LFE_TRY(emu_allreduce(c, b.first, b.second, EMU_SUM_F64));
+    return LFE_OK;
+  }
+  LFE_NCCL(ncclGroupStart());
+  for (auto& b : bufs)
+    if (b.second) LFE_NCCL(ncclAllReduce(b.first, b.first, b.second, ncclFloat64, ncclSum, c->comm, c->stream));
+  LFE_NCCL(ncclGroupEnd());
+  return LFE_OK;
+}
+
 int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count) {
   if (c->world <= 1 || count == 0) return LFE_OK;
   if (c->emu) return emu_allreduce(c, dev, count, EMU_SUM_I32);
@@ -394,6 +409,11 @@ static void free_data(lfe_ctx* c) {
   c->rec_sy_cap = c->rec_syy_cap = c->rec_lay_cap = 0;
   dfree(c->raw_part);
   dfree(c->qpart);
+  dfree(c->raw_slots);
+  c->raw_slots_cap = 0;
+  dfree(c->amax);
+  dfree(c->xq);
+  c->amax_cap = c->xq_cap = 0;
   dfree(c->sw.x);
   dfree(c->sw.s64);
   dfree(c->sw.sdbl);

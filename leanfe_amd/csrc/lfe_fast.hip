@@ -72,6 +72,20 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) racc[s] = d4{0.0, 0.0, 0.0, 0.0};
   const double shift = (RAW && c < p && a.la.n_items > 0) ? a.X[(int64_t)c * a.ld] : 0.0;
+  // exact sums (unweighted fits, k_fix_quanta): every value enters as round(x * scale_c) in int64,
+  // so the tables do not depend on the order of the adds
+  const bool fix = a.fixq != nullptr && fix_on(a.fixq, p);
+  double fsc[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) fsc[I] = (fix && 16 * I + c < p) ? a.fixq[16 * I + c] : 0.0;
+  typedef unsigned long long u64;
+  auto add = [&](double* dst, double v, int I) {
+    if (fix)
+      atomicAdd(reinterpret_cast<u64*>(dst),
+                (u64)__double_as_longlong(__builtin_fma(v, fsc[I], kFixMagic)) - kFixMagicBits);
+    else
+      atomicAdd(dst, v);
+  };
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
       for (int j = tid; j < a.G[f] * p; j += TH) lds[a.tab_off[f] + j] = 0.0;
@@ -80,9 +94,15 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   auto flush = [&](int b) {
     const int lo = b << a.la.s;
     for (int j = tid; j < a.B * p; j += TH) {
-      const double val = lds[j];
       const int g = lo + j / p;
-      if (val != 0.0 && g < a.G_P) atomicAdd(&a.S[P][(int64_t)g * p + (j % p)], val);
+      double* dst = &a.S[P][(int64_t)g * p + (j % p)];
+      if (fix) {
+        const u64 val = reinterpret_cast<const u64*>(lds)[j];
+        if (val != 0ull && g < a.G_P) atomicAdd(reinterpret_cast<u64*>(dst), val);
+      } else {
+        const double val = lds[j];
+        if (val != 0.0 && g < a.G_P) atomicAdd(dst, val);
+      }
       lds[j] = 0.0;
     }
   };
@@ -137,12 +157,12 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
             racc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[s], 0, 0, 0);
             if (c < p && valid[s]) {
               const double v = xv[u][0][s];
-              if (a.slice) atomicAdd(&lds[(hv[s] - lo) * p + c], v);
-              else atomicAdd(&a.S[P][(int64_t)hv[s] * p + c], v);
+              if (a.slice) add(&lds[(hv[s] - lo) * p + c], v, 0);
+              else add(&a.S[P][(int64_t)hv[s] * p + c], v, 0);
               const int f = a.qf[0];
               const int g = (&cq[u][0].x)[s];
-              if (a.tab_off[f] >= 0) atomicAdd(&lds[a.tab_off[f] + g * p + c], v);
-              else atomicAdd(&a.S[f][(int64_t)g * p + c], v);
+              if (a.tab_off[f] >= 0) add(&lds[a.tab_off[f] + g * p + c], v, 0);
+              else add(&a.S[f][(int64_t)g * p + c], v, 0);
             }
           }
           continue;
@@ -157,16 +177,16 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
           for (int s = 0; s < 4; ++s) {
             if (!valid[s]) continue;
             if (P >= 0) {
-              if (a.slice) atomicAdd(&lds[(hv[s] - lo) * p + col], v[s]);
-              else atomicAdd(&a.S[P][(int64_t)hv[s] * p + col], v[s]);
+              if (a.slice) add(&lds[(hv[s] - lo) * p + col], v[s], I);
+              else add(&a.S[P][(int64_t)hv[s] * p + col], v[s], I);
             }
 #pragma unroll
             for (int q = 0; q < FQ; ++q) {
               if (q >= nq) continue;
               const int f = a.qf[q];
               const int g = (&cq[u][q].x)[s];
-              if (a.tab_off[f] >= 0) atomicAdd(&lds[a.tab_off[f] + g * p + col], v[s]);
-              else atomicAdd(&a.S[f][(int64_t)g * p + col], v[s]);
+              if (a.tab_off[f] >= 0) add(&lds[a.tab_off[f] + g * p + col], v[s], I);
+              else add(&a.S[f][(int64_t)g * p + col], v[s], I);
             }
           }
         }
@@ -178,8 +198,13 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
       for (int j = tid; j < a.G[f] * p; j += TH) {
-        const double val = lds[a.tab_off[f] + j];
-        if (val != 0.0) atomicAdd(&a.S[f][j], val);
+        if (fix) {
+          const u64 val = reinterpret_cast<const u64*>(lds + a.tab_off[f])[j];
+          if (val != 0ull) atomicAdd(reinterpret_cast<u64*>(&a.S[f][j]), val);
+        } else {
+          const double val = lds[a.tab_off[f] + j];
+          if (val != 0.0) atomicAdd(&a.S[f][j], val);
+        }
       }
   if (RAW) {
     // waves' raw tiles summed in LDS (lane (kq, c) holds rows kq + 4 rr of column c)
@@ -490,24 +515,40 @@ __global__ void k_raw_shift(const double* __restrict__ X, int64_t ld, int p, int
   sh[j] = rank == 0 ? own : 0.0;
 }
 
-// re-centre this rank's raw tile from its own shift c_r to the common shift c*:
-// sum (d - c*)(d - c*)' = R + dl C' + C dl' + n dl dl',  sum (d - c*) = C + n dl,  dl = c_r - c*
-__global__ void k_raw_recenter(double* __restrict__ R, const double* __restrict__ sh, int p) {
+// multi-rank raw Gram: rank r's tile (relative to its own shift) and shift into slot r of a
+// zeroed [world][272] buffer; after one sum over ranks every rank holds all slots
+__global__ void k_raw_slot(const double* __restrict__ R, const double* __restrict__ sh, int rank,
+                           double* __restrict__ slots) {
+  double* s = slots + (int64_t)rank * 272;
+  for (int t = threadIdx.x; t < 272; t += blockDim.x) s[t] = t < 256 ? R[t] : sh[16 + (t - 256)];
+}
+
+// the global raw tile from the slots, each re-centred from its own shift c_r to rank 0's c*,
+// sum (d - c*)(d - c*)' = R + dl C' + C dl' + n dl dl', sum (d - c*) = C + n dl, dl = c_r - c*,
+// and added in rank order (every rank the same bits); raw_shift: c* in both halves
+__global__ void k_raw_combine(const double* __restrict__ slots, int world, int p, double* __restrict__ R,
+                              double* __restrict__ sh) {
   __shared__ double C[16], dl[16];
-  const int t = threadIdx.x;
-  if (t < 16) {
-    C[t] = R[15 * 16 + t];
-    dl[t] = t < p ? sh[16 + t] - sh[t] : 0.0;
-  }
-  __syncthreads();
-  const double n = R[15 * 16 + 15];
+  const int t = threadIdx.x;  // 256 threads: one tile entry each
   const int i = t / 16, j = t % 16;
-  double v = R[t];
-  if (i < p && j < p) v += dl[i] * C[j] + C[i] * dl[j] + n * dl[i] * dl[j];
-  else if (i == 15 && j < p) v += n * dl[j];
-  else if (j == 15 && i < p) v += n * dl[i];
-  __syncthreads();
-  R[t] = v;
+  double acc = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const double* s = slots + (int64_t)r * 272;
+    __syncthreads();
+    if (t < 16) {
+      C[t] = s[15 * 16 + t];
+      dl[t] = t < p ? s[256 + t] - slots[256 + t] : 0.0;
+    }
+    __syncthreads();
+    const double n = s[15 * 16 + 15];
+    double v = s[t];
+    if (i < p && j < p) v += dl[i] * C[j] + C[i] * dl[j] + n * dl[i] * dl[j];
+    else if (i == 15 && j < p) v += n * dl[j];
+    else if (j == 15 && i < p) v += n * dl[i];
+    acc = r == 0 ? v : acc + v;
+  }
+  R[t] = acc;
+  if (t < 16) sh[t] = sh[16 + t] = slots[256 + t];
 }
 
 int sums4(lfe_ctx* c) {
@@ -572,7 +613,8 @@ int sums4(lfe_ctx* c) {
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
     a.raw_part = c->raw_part;
   }
-  const bool exact = two;
+  // exact (int64) group sums for every unweighted fit: the two-FE kernel and k_sums4 alike
+  const bool exact = two || !a.w;
   if (two) {
     LFE_TRY(ensure_f64(c, c->qpart, c->qpart_cap, (size_t)nblocks * c->fe[a.qf[0]].G * p));
     a.qpart = c->qpart;
@@ -613,7 +655,7 @@ int sums4(lfe_ctx* c) {
   if (exact) {
     ProfScope _ps(c, K_FIX_SUMS);
     for (int f = 0; f < c->F; ++f) {
-      if (f == a.qf[0]) continue;  // converted by k_qpart_reduce
+      if (two && f == a.qf[0]) continue;  // converted by k_qpart_reduce
       const int64_t m = (int64_t)c->fe[f].G * p;
       hipLaunchKernelGGL(k_fix_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, c->fe[f].S, m, p, c->fixq);
     }
@@ -625,17 +667,27 @@ int sums4(lfe_ctx* c) {
     hipLaunchKernelGGL(k_raw_shift, dim3(1), dim3(64), 0, c->stream, c->L.X, c->ld, p, c->L.n_items > 0 ? 1 : 0,
                        c->rank, c->raw_shift);
     LFE_HIP(hipGetLastError());
-    if (c->world > 1) {
-      // every rank's tile re-centred on rank 0's shift, then summed: the global raw Gram
-      LFE_TRY(allreduce_sum_f64(c, c->raw_shift, 16));
-      hipLaunchKernelGGL(k_raw_recenter, dim3(1), dim3(256), 0, c->stream, c->raw_tile, c->raw_shift, p);
-      LFE_HIP(hipGetLastError());
-      LFE_TRY(allreduce_sum_f64(c, c->raw_tile, 256));
-    }
     c->raw_ready = true;
   }
-  for (int f = 0; f < c->F; ++f)  // owner-sharded rows: the primary FE's sums are complete on each rank
-    if (!(c->owner_on && f == P)) LFE_TRY(allreduce_sum_f64(c, c->fe[f].S, (size_t)c->fe[f].G * p));
+  // one grouped sum over ranks: the group tables (owner-sharded rows: the primary FE's are
+  // complete on each rank) and every rank's raw tile + shift in its own slot
+  std::vector<std::pair<double*, size_t>> bufs;
+  for (int f = 0; f < c->F; ++f)
+    if (!(c->owner_on && f == P)) bufs.push_back({c->fe[f].S, (size_t)c->fe[f].G * p});
+  if (raw && c->world > 1) {
+    LFE_TRY(ensure_f64(c, c->raw_slots, c->raw_slots_cap, (size_t)c->world * 272));
+    LFE_HIP(hipMemsetAsync(c->raw_slots, 0, sizeof(double) * c->world * 272, c->stream));
+    hipLaunchKernelGGL(k_raw_slot, dim3(1), dim3(256), 0, c->stream, c->raw_tile, c->raw_shift, c->rank,
+                       c->raw_slots);
+    LFE_HIP(hipGetLastError());
+    bufs.push_back({c->raw_slots, (size_t)c->world * 272});
+  }
+  LFE_TRY(allreduce_sum_f64_many(c, bufs));
+  if (raw && c->world > 1) {
+    hipLaunchKernelGGL(k_raw_combine, dim3(1), dim3(256), 0, c->stream, c->raw_slots, c->world, p, c->raw_tile,
+                       c->raw_shift);
+    LFE_HIP(hipGetLastError());
+  }
   return LFE_OK;
 }
 

@@ -228,6 +228,14 @@ struct lfe_ctx {
   size_t raw_part_cap = 0;
   double* qpart = nullptr;       // [blocks][G_Q * p] per-block secondary-FE sums (k_sums2_raw)
   size_t qpart_cap = 0;
+  double* raw_slots = nullptr;   // [world][272] every rank's raw tile + shift (one grouped all-reduce)
+  size_t raw_slots_cap = 0;
+  // exact cross terms of the general sweeps (lfe_seg.hip): per-FE column max |alpha| (u64 bits)
+  // and the quanta of the cross term being formed
+  double* amax = nullptr;        // [kMaxFE][kMaxCols]
+  size_t amax_cap = 0;
+  double* xq = nullptr;          // [3 * kMaxCols]
+  size_t xq_cap = 0;
   double* raw_tile = nullptr;    // [256] raw tile: slots 0..p-1 data (shifted by raw_shift), slot 15 intercept
   size_t raw_tile_cap = 0;
   double* raw_shift = nullptr;   // [32]: [0, 16) the shift of raw_tile (rank 0's first row on every rank),
@@ -405,6 +413,7 @@ int ensure_pinned_items(lfe_ctx* c, size_t bytes);
 int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds);
 int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems);
 int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count);
+int allreduce_sum_f64_many(lfe_ctx* c, const std::vector<std::pair<double*, size_t>>& bufs);
 int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count);
 int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count);
 int alltoallv_bytes(lfe_ctx* c, const char* send, const size_t* send_off, const size_t* send_bytes, char* recv,

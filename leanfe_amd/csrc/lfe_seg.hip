@@ -98,7 +98,22 @@ struct SegCrossArgs {
   int pc;                            // columns computed: p, or 1 (y only)
   int G;
   double* T;                         // [G][pc], zeroed before the launch
+  const double* xq;                  // exact sums (null: f64): [kMaxCols] scales, [kMaxCols] quanta, flag
 };
+
+// exact cross terms: a row's value v (the sum of the other FEs' effects) enters T as
+// round(v * scale) in int64 (the FMA with 1.5 * 2^52 rounds it, |v * scale| < 2^51), so T does not
+// depend on the order of the segment layout's rows nor on which partial sum lands first
+constexpr double kSegMagic = 6755399441055744.0;  // 1.5 * 2^52
+constexpr unsigned long long kSegMagicBits = 0x4338000000000000ull;
+__device__ __forceinline__ long long seg_fix(double v, double scale) {
+  return (long long)((unsigned long long)__double_as_longlong(__builtin_fma(v, scale, kSegMagic)) - kSegMagicBits);
+}
+__device__ __forceinline__ long long seg_quad_sum_i64(long long v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
 
 __device__ __forceinline__ double seg_quad_sum(double v) {
   v += __shfl_xor(v, 16, 64);
@@ -124,6 +139,10 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
 #pragma unroll
   for (int I = 0; I < NT; ++I) cl[I] = 16 * I + c < pc ? 16 * I + c : 0;
   const int32_t kept = a.seg_off[G];
+  const bool ex = a.xq != nullptr && a.xq[2 * kMaxCols] != 0.0;  // wave-uniform
+  double xs[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) xs[I] = ex ? a.xq[cl[I]] : 0.0;
   for (int u = wv; u < a.n_units; u += nwaves) {
     const int lo = u * kSegUnit;
     if (lo >= kept) break;
@@ -133,19 +152,32 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
     bool part = r0 < lo;  // segment h began in an earlier unit
     bool done = false;
     double acc[NT];
+    long long iacc[NT];
 #pragma unroll
-    for (int I = 0; I < NT; ++I) acc[I] = 0.0;
+    for (int I = 0; I < NT; ++I) {
+      acc[I] = 0.0;
+      iacc[I] = 0;
+    }
     auto finalize = [&](bool atomic) {
 #pragma unroll
       for (int I = 0; I < NT; ++I) {
-        const double t = seg_quad_sum(acc[I]);
         const int col = 16 * I + c;
-        if (kq == 0 && col < pc) {
-          double* d = a.T + (int64_t)h * pc + col;
-          if (atomic) atomicAdd(d, t);
-          else *d = t;
+        double* d = a.T + (int64_t)h * pc + col;
+        if (ex) {  // integer adds commute: a cut segment's partials may land in any order
+          const long long t = seg_quad_sum_i64(iacc[I]);
+          if (kq == 0 && col < pc) {
+            if (atomic) atomicAdd(reinterpret_cast<unsigned long long*>(d), (unsigned long long)t);
+            else *reinterpret_cast<long long*>(d) = t;
+          }
+        } else {
+          const double t = seg_quad_sum(acc[I]);
+          if (kq == 0 && col < pc) {
+            if (atomic) atomicAdd(d, t);
+            else *d = t;
+          }
         }
         acc[I] = 0.0;
+        iacc[I] = 0;
       }
     };
     for (int gs0 = lo; gs0 < hi && !done; gs0 += 16 * UNR) {
@@ -192,16 +224,26 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
         }
         while (true) {
           if (r0 <= gs && r1 >= ge) {  // the whole group lies in segment h
+            if (ex) {
 #pragma unroll
-            for (int I = 0; I < NT; ++I)
-              acc[I] += (val[U][0][I] + val[U][1][I]) + (val[U][2][I] + val[U][3][I]);
+              for (int I = 0; I < NT; ++I)
+                iacc[I] += (seg_fix(val[U][0][I], xs[I]) + seg_fix(val[U][1][I], xs[I])) +
+                           (seg_fix(val[U][2][I], xs[I]) + seg_fix(val[U][3][I], xs[I]));
+            } else {
+#pragma unroll
+              for (int I = 0; I < NT; ++I)
+                acc[I] += (val[U][0][I] + val[U][1][I]) + (val[U][2][I] + val[U][3][I]);
+            }
           } else {
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
               const int row = rb + s;
               const bool in = row >= r0 && row < r1;
 #pragma unroll
-              for (int I = 0; I < NT; ++I) acc[I] += in ? val[U][s][I] : 0.0;
+              for (int I = 0; I < NT; ++I) {
+                if (ex) iacc[I] += in ? seg_fix(val[U][s][I], xs[I]) : 0ll;
+                else acc[I] += in ? val[U][s][I] : 0.0;
+              }
             }
           }
           if (r1 > ge) break;  // segment h continues in the next group
@@ -224,6 +266,60 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
     // segment h continues past the unit: partial sum
     if (!done && h < G && r0 < hi && r1 > hi) finalize(true);
   }
+}
+
+// column max |alpha| (u64 bits) of an effect table into out[0, p) (atomicMax; per block in LDS first)
+__global__ __launch_bounds__(256) void k_alpha_colmax(const double* __restrict__ alpha, int32_t G, int p,
+                                                      unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long m[kMaxCols];
+  for (int j = threadIdx.x; j < p; j += blockDim.x) m[j] = 0ull;
+  __syncthreads();
+  const int64_t total = (int64_t)G * p;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x)
+    atomicMax(&m[e % p], (unsigned long long)__double_as_longlong(fabs(alpha[e])));
+  __syncthreads();
+  for (int j = threadIdx.x; j < p; j += blockDim.x)
+    if (m[j]) atomicMax(&out[j], m[j]);
+}
+
+// quanta of FE f's exact cross term: a row's value is bounded by M = sum over the other FEs of
+// their column max |alpha|, a group sum by N M (N = the largest kept group of f); scale =
+// 2^min(62 - e, 50 - e_M), 2^e > N M, 2^e_M > M (one bit of headroom for the rounding of the row
+// sums).  A non-finite bound (NaN / Inf effects) keeps the f64 sums.
+__global__ void k_cross_quanta(const unsigned long long* __restrict__ amax, int F, int f, int pc,
+                               const int32_t* __restrict__ cmax, double* __restrict__ xq) {
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const int col = threadIdx.x;
+  if (col < pc) {
+    double M = 0.0;
+    for (int j = 0; j < F; ++j)
+      if (j != f) M += __longlong_as_double((long long)amax[j * kMaxCols + col]);
+    const double NM = (double)max(1, cmax[f]) * M;
+    const bool ok = isfinite(NM);
+    double scale = 1.0, quantum = 1.0;
+    if (ok && M > 0.0) {
+      int e = 0, eM = 0;
+      (void)frexp(NM, &e);
+      (void)frexp(M, &eM);
+      const int sh = min(62 - e, 50 - eM);
+      scale = ldexp(1.0, sh);
+      quantum = ldexp(1.0, -sh);
+    }
+    xq[col] = scale;
+    xq[kMaxCols + col] = quantum;
+    if (!ok) atomicAdd(&bad, 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) xq[2 * kMaxCols] = bad ? 0.0 : 1.0;
+}
+
+// exact cross term (int64 bits) -> double
+__global__ void k_cross_convert(double* __restrict__ T, int64_t m, int pc, const double* __restrict__ xq) {
+  if (xq[2 * kMaxCols] == 0.0) return;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x)
+    T[e] = (double)__double_as_longlong(T[e]) * xq[kMaxCols + (int)(e % pc)];
 }
 
 // alpha_f = (S_f - T_f) / W_f   (weighted: W = sum w; else W = kept count)
@@ -366,6 +462,17 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
   a.pc = pc;
   a.G = fe.G;
   a.T = out;
+  // unweighted cross terms sum exactly (int64 per column): bit-reproducible whatever the order
+  // of the segment layout's rows (ranked by global cursor atomics) and of the cut segments' adds
+  const bool ex = !wt && c->amax != nullptr;
+  if (ex) {
+    LFE_TRY(ensure_f64(c, c->xq, c->xq_cap, 3 * kMaxCols));
+    hipLaunchKernelGGL(k_cross_quanta, dim3(1), dim3(64), 0, c->stream,
+                       reinterpret_cast<const unsigned long long*>(c->amax), c->F, f, pc,
+                       c->iscratch + kIscratchCmax, c->xq);
+    LFE_HIP(hipGetLastError());
+    a.xq = c->xq;
+  }
   if (a.n_units > 0) {
     const int nt = (pc + 15) / 16;
     CrossFn fn = cross_fn(nt, c->F - 1, wt);
@@ -375,6 +482,11 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kSegThreads), 0, c->stream, a);
   }
   LFE_HIP(hipGetLastError());
+  if (ex) {
+    const int64_t m = (int64_t)fe.G * pc;
+    hipLaunchKernelGGL(k_cross_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, out, m, pc, c->xq);
+    LFE_HIP(hipGetLastError());
+  }
   return allreduce_sum_f64(c, out, (size_t)fe.G * pc);
 }
 
@@ -417,10 +529,26 @@ static int seg_finalize(lfe_ctx* c, int f) {
   hipLaunchKernelGGL(k_finalize, dim3(grid_for((int64_t)fe.G * c->p)), dim3(kBlock), 0, c->stream, fe.S,
                      cross ? fe.T : nullptr, c->L.w ? fe.W : nullptr, fe.cnt, fe.G, c->p, fe.alpha);
   LFE_HIP(hipGetLastError());
+  if (c->amax) {  // the column bound of the new effects (the other FEs' exact cross terms)
+    unsigned long long* am = reinterpret_cast<unsigned long long*>(c->amax) + (size_t)f * kMaxCols;
+    LFE_HIP(hipMemsetAsync(am, 0, sizeof(double) * c->p, c->stream));
+    hipLaunchKernelGGL(k_alpha_colmax, dim3(grid_for((int64_t)fe.G * c->p, kBlock, 512)), dim3(kBlock), 0,
+                       c->stream, fe.alpha, fe.G, c->p, am);
+    LFE_HIP(hipGetLastError());
+  }
   return LFE_OK;
 }
 
 // max_g |mean_g(y~)| of FE f given its check cross term R (stride r_stride, null: none)
+// max_g |alpha[g][0]| (the y column of an effect table) into *out as u64 bits (atomicMax)
+__global__ void k_y_absmax(const double* __restrict__ alpha, int32_t G, int p, unsigned long long* __restrict__ out) {
+  double m = 0.0;
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x)
+    m = fmax(m, fabs(alpha[(int64_t)g * p]));
+  for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+}
+
 static int seg_check_max(lfe_ctx* c, int f, const double* R, int r_stride) {
   auto& fe = c->fe[f];
   ProfScope _ps(c, K_CHECK_MAX);
@@ -435,6 +563,9 @@ static int seg_check_max(lfe_ctx* c, int f, const double* R, int r_stride) {
 
 int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int max_iter, int check_from,
                    int* iterations_out, double* last_out) {
+  // every effect table starts at zero (lfe_demean): so do the exact cross terms' column bounds
+  LFE_TRY(ensure_f64(c, c->amax, c->amax_cap, (size_t)kMaxFE * kMaxCols));
+  LFE_HIP(hipMemsetAsync(c->amax, 0, sizeof(double) * kMaxFE * kMaxCols, c->stream));
   const int F = c->F;
   const bool cross = F > 1;
   if (cross) LFE_TRY(seg_build(c));
@@ -453,7 +584,8 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
   } else {
     bool first_ready = false;  // T of order[0] already holds the next projection's cross term
     constexpr int kStall = 20;
-    double best = 1e300;
+    constexpr double kRecRel = 0x1p-46;  // 64 ulps of y's scale
+    double best = 1e300, yscale = 0.0;
     int stall = 0;
     for (int it = 1; it <= max_iter; ++it) {
       for (size_t k = 0; k < order.size(); ++k) {
@@ -463,8 +595,15 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
       first_ready = false;
       iterations = it;
       if (it < check_from) continue;
-      LFE_TRY(ensure_dred(c, 1));
-      LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double), c->stream));
+      LFE_TRY(ensure_dred(c, 2));
+      LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double) * 2, c->stream));
+      const bool scale_now = c->records && it == check_from;
+      if (scale_now) {  // y's scale: the largest group effect of the first FE after this sweep
+        const int f0 = order[0];
+        hipLaunchKernelGGL(k_y_absmax, dim3(grid_for(c->fe[f0].G)), dim3(kBlock), 0, c->stream, c->fe[f0].alpha,
+                           c->fe[f0].G, c->p, reinterpret_cast<unsigned long long*>(c->dred + 1));
+        LFE_HIP(hipGetLastError());
+      }
       for (size_t k = 0; k < order.size(); ++k) {
         const int f = order[k];
         if (!cross) {
@@ -480,11 +619,17 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
           LFE_TRY(seg_check_max(c, f, c->fe[f].R, 1));
         }
       }
-      LFE_TRY(d2h_sync(c, &last, c->dred, sizeof(double)));
+      double chk[2] = {0.0, 0.0};
+      LFE_TRY(d2h_sync(c, chk, c->dred, sizeof(double) * (scale_now ? 2 : 1)));
+      last = chk[0];
+      if (scale_now) yscale = chk[1];
       if (last < tol) break;
       if (c->records) {
-        // records are solved to machine precision: stop once the check has not reached a
-        // new minimum for kStall checks (it only moves at rounding level from there)
+        // records are solved to machine precision: stop once the largest group mean of y~ is
+        // within kRecRel of y's scale (a scale-relative floor, so slowly converging records
+        // stop as soon as they are there), or once the check has not reached a new minimum
+        // for kStall checks (it only moves at rounding level from there)
+        if (last <= kRecRel * yscale) break;
         if (last < best) {
           best = last;
           stall = 0;

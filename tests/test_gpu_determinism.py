@@ -4,9 +4,9 @@ The two-FE fast path's group sums accumulate each column as round(x / quantum) i
 (lfe_fast.hip, k_sums2_raw / k_fix_quanta), the T_Q run sums are reduced in bucket order and
 the Gram / meat partials in block order, so solving the same panel twice must give
 bit-identical beta, SE, RSS and `iterations` - within one context and across two contexts.
-(The general sweeps - F >= 3, weights, one bucket - still rank their segment layouts with
-global cursor atomics and keep f64 atomic sums: parity-exact to 1e-10, not bit-reproducible;
-DESIGN.md §8.)
+The general sweeps (F >= 3, large secondary FE, one bucket) sum their group sums and cross
+terms in int64 too, so unweighted fits there are bit-reproducible as well; weighted fits and
+the cluster score sums keep f64 atomics.
 The exact path must also keep parity with the CPU restatement (oracle/altproj.py,
 polars_impl.py:468-537) at the usual 1e-10 bar, and a column whose range defeats the fixed
 point (one huge outlier) must fall back to the f64 sums and still match."""
@@ -107,3 +107,22 @@ def test_outlier_column_reports_f64_sums():
                  [5_000, 200])
         eng.drop_singletons()
         assert eng.exact_sums()
+
+
+@pytest.mark.parametrize("n,L,vcov", [(1_500_000, [60_000, 8_000, 500], "HC1"),   # config 4's shape (F = 3)
+                                      (1_000_000, [20_000, 5_000], "iid")])        # G_Q too large for the fast path
+def test_general_sweeps_are_bit_identical(n, L, vcov):
+    """The general sweeps (lfe_seg.hip) rank their per-FE segment layouts with global cursor
+    atomics; their group sums and cross terms sum in int64 (k_sums4 exact path,
+    k_seg_cross / k_cross_quanta), so two solves agree bit for bit anyway."""
+    from leanfe_amd import leanfe_hip, synth
+    k = 4
+    data = synth.panel(n, k, L, seed=313)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(L))]
+    runs = [leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov=vcov, quiet=True,
+                       device=0) for _ in range(2)]
+    for r in runs[1:]:
+        assert r.iterations == runs[0].iterations and r.n_obs == runs[0].n_obs
+        np.testing.assert_array_equal([r.coefs[x] for x in xs], [runs[0].coefs[x] for x in xs])
+        np.testing.assert_array_equal([r.std_errors[x] for x in xs], [runs[0].std_errors[x] for x in xs])

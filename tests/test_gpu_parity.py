@@ -268,6 +268,23 @@ def test_yoco_panels_vs_oracle(seed, n, L, k, vcov, weights):
     _assert_yoco(r, o, xs)
 
 
+def test_yoco_nearly_nested_fes_converge_to_the_exact_lsdv():
+    """Records whose second FE is almost a function of the first (99% of rows: fe2 = fe1 // 4):
+    the weighted projections converge slowly, and the records solve must still reach the exact
+    LSDV fit the reference factors directly (compress.py:659-747), stopping on the
+    scale-relative floor rather than running to max_iter."""
+    from leanfe_amd import leanfe_hip
+    d = _yoco_panel(57, 400_000, (200, 50), 2)
+    rng = np.random.default_rng(57)
+    nested = rng.random(d["fe1"].size) < 0.99
+    d["fe2"] = np.where(nested, d["fe1"] // 4, d["fe2"])
+    xs, fes = ["x1", "x2"], ["fe1", "fe2"]
+    o = yoco.fit(d, "y", xs, fes, vcov="HC1")
+    r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="compress", vcov="HC1", quiet=True)
+    _assert_yoco(r, o, xs)
+    assert r.iterations < 100_000
+
+
 def test_yoco_auto_selects_compress_and_hash_collisions_are_exact(monkeypatch):
     """strategy='auto' picks 'compress' for low-cardinality FEs with discrete x
     (compress.py:96-184), and an 8-bit row hash (forced collisions) still groups exactly."""
