@@ -520,13 +520,7 @@ static int build_layouts(lfe_ctx* c, int Q) {
     LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, c->run_h)));
   }
   // work units of ~2048 kept rows (whole segments) for K1
-#ifndef LFE_UNIT_ADAPT
-  const int64_t U = 2048;
-#else
-  // at least ~4 units per K1 wave (one 16-wave workgroup per CU), so short shards balance
-  int64_t U = 2048;
-  while (U > 256 && c->n / U < 4ll * 16 * c->n_cu) U >>= 1;
-#endif
+  const int64_t U = 2048;  // (shrinking it for short shards - 4 units per K1 wave - measured slower)
   const int32_t H = L.nb * B;
   c->n_units = (int)std::max<int64_t>(1, (c->n + U - 1) / U);
   LFE_TRY(ensure_i32(c, c->seg_units, c->seg_units_cap, (size_t)c->n_units + 1));
