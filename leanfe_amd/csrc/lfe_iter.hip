@@ -123,7 +123,7 @@ static size_t ls_scatter_lds(int K, int per = 16) {
 
 // Deterministic ranking of a sub-chunk's rows by key (both local sorts).  Every wave has its
 // own 16-bit counter per key (two per 32-bit word), so a row's slot is its wave's first slot
-// for the key (ls_offsets) + the counter value its returning LDS add got.  The adds of one wave
+// for the key (ls_offsets_n) + the counter value its returning LDS add got.  The adds of one wave
 // are issued in slot order without waits in between (lanes without a key add 0 to the wave's
 // spare word), a wave's LDS operations complete in issue order, and the lanes of one
 // instruction that hit the same counter are served in the LDS's fixed lane order; no other
@@ -147,45 +147,86 @@ __device__ __forceinline__ void wave_rank(const int32_t (&key)[PER], uint32_t* c
 
 // per key j < K (cw: [kLsWaves][Kp] 16-bit counters): cw[w][j] <- the first slot of wave w's rows with key j in the sub-chunk,
 // delta[j] <- run[j] - (the key's first slot); the keys' offsets are an exclusive scan of the
-// totals (one thread per `per` keys, then the waves)
-__device__ void ls_offsets(uint16_t* cw, int Kp, int32_t* tot, const int32_t* run, int32_t* delta, int K,
-                           int32_t* wsum, int tid, int lane, int wave) {
-  for (int j = tid; j < K; j += kLsThreads) {
-    int32_t t = 0;
-    for (int w2 = 0; w2 < kLsWaves; ++w2) {
-      const int32_t h = cw[w2 * Kp + j];
-      cw[w2 * Kp + j] = (uint16_t)t;
-      t += h;
+// totals (one thread per `per` keys, then the waves).  NS key sets (the fused sort's two
+// layouts) share the barriers, and a key's eight wave counters are read before any is rewritten
+// (one LDS round trip per pass, not a dependent chain of eight).
+struct LsKeys {
+  uint16_t* cw;
+  int Kp;
+  int32_t* tot;
+  const int32_t* run;
+  int32_t* delta;
+  int K;
+};
+template <int NS>
+__device__ void ls_offsets_n(const LsKeys (&ks)[NS], int32_t (*wsum)[kLsWaves], int tid, int lane, int wave) {
+#pragma unroll
+  for (int S = 0; S < NS; ++S) {
+    const LsKeys& k = ks[S];
+    for (int j = tid; j < k.K; j += kLsThreads) {
+      uint16_t h[kLsWaves];
+#pragma unroll
+      for (int w2 = 0; w2 < kLsWaves; ++w2) h[w2] = k.cw[w2 * k.Kp + j];
+      int32_t t = 0;
+#pragma unroll
+      for (int w2 = 0; w2 < kLsWaves; ++w2) {
+        k.cw[w2 * k.Kp + j] = (uint16_t)t;
+        t += h[w2];
+      }
+      k.tot[j] = t;
     }
-    tot[j] = t;
   }
   __syncthreads();
-  const int per = (K + kLsThreads - 1) / kLsThreads;
-  const int b0 = tid * per;
-  int32_t sum = 0;
-  for (int k = 0; k < per; ++k)
-    if (b0 + k < K) sum += tot[b0 + k];
-  int32_t x = sum;
+  int32_t x[NS], sum[NS];
+#pragma unroll
+  for (int S = 0; S < NS; ++S) {
+    const LsKeys& k = ks[S];
+    const int per = (k.K + kLsThreads - 1) / kLsThreads;
+    const int b0 = tid * per;
+    sum[S] = 0;
+    for (int q = 0; q < per; ++q)
+      if (b0 + q < k.K) sum[S] += k.tot[b0 + q];
+    x[S] = sum[S];
+  }
   for (int o = 1; o < 64; o <<= 1) {
-    const int32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wave] = x;
-  __syncthreads();
-  int32_t wofs = 0;
-  for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[w2];
-  int32_t acc = x - sum + wofs;
-  for (int k = 0; k < per; ++k)
-    if (b0 + k < K) {
-      const int32_t t = tot[b0 + k];
-      tot[b0 + k] = acc;
-      acc += t;
+#pragma unroll
+    for (int S = 0; S < NS; ++S) {
+      const int32_t y = __shfl_up(x[S], o, 64);
+      if (lane >= o) x[S] += y;
     }
+  }
+#pragma unroll
+  for (int S = 0; S < NS; ++S)
+    if (lane == 63) wsum[S][wave] = x[S];
   __syncthreads();
-  for (int j = tid; j < K; j += kLsThreads) {
-    const int32_t boff = tot[j];
-    delta[j] = run[j] - boff;
-    for (int w2 = 0; w2 < kLsWaves; ++w2) cw[w2 * Kp + j] = (uint16_t)(cw[w2 * Kp + j] + boff);
+#pragma unroll
+  for (int S = 0; S < NS; ++S) {
+    const LsKeys& k = ks[S];
+    const int per = (k.K + kLsThreads - 1) / kLsThreads;
+    const int b0 = tid * per;
+    int32_t wofs = 0;
+    for (int w2 = 0; w2 < wave; ++w2) wofs += wsum[S][w2];
+    int32_t acc = x[S] - sum[S] + wofs;
+    for (int q = 0; q < per; ++q)
+      if (b0 + q < k.K) {
+        const int32_t t = k.tot[b0 + q];
+        k.tot[b0 + q] = acc;
+        acc += t;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int S = 0; S < NS; ++S) {
+    const LsKeys& k = ks[S];
+    for (int j = tid; j < k.K; j += kLsThreads) {
+      const int32_t boff = k.tot[j];
+      k.delta[j] = k.run[j] - boff;
+      uint16_t h[kLsWaves];
+#pragma unroll
+      for (int w2 = 0; w2 < kLsWaves; ++w2) h[w2] = k.cw[w2 * k.Kp + j];
+#pragma unroll
+      for (int w2 = 0; w2 < kLsWaves; ++w2) k.cw[w2 * k.Kp + j] = (uint16_t)(h[w2] + boff);
+    }
   }
   __syncthreads();
 }
@@ -260,7 +301,10 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter(const int4* __restric
     wave_rank(key, reinterpret_cast<uint32_t*>(cw + wave * Kp), &spare[wave], pos);
     wave_kept(key, lane, wave, wkept);
     __syncthreads();
-    ls_offsets(cw, Kp, tot, run, delta, K, wsum, tid, lane, wave);
+    {
+      const LsKeys ks[1] = {{cw, Kp, tot, run, delta, K}};
+      ls_offsets_n<1>(ks, reinterpret_cast<int32_t(*)[kLsWaves]>(wsum), tid, lane, wave);
+    }
     int32_t nk = 0;  // kept rows of this sub-chunk
     for (int w2 = 0; w2 < kLsWaves; ++w2) nk += wkept[w2];
 #pragma unroll
@@ -314,7 +358,8 @@ static size_t ls2_lds(int K1, int K2, int per) {
 }
 
 template <int kLsPer>
-__global__ __launch_bounds__(kLsThreads) void k_ls_scatter2(Ls2Args a) {
+// (4 waves per SIMD, <= 128 VGPRs: two workgroups per CU, as the LDS allows)
+__global__ __launch_bounds__(kLsThreads, 4) void k_ls_scatter2(Ls2Args a) {
   constexpr int kLsRows = kLsThreads * kLsPer;
   extern __shared__ int32_t sm[];
   const int K1 = a.K1, K2 = a.K2;
@@ -329,7 +374,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter2(Ls2Args a) {
   const int K1p = even(K1), K2p = even(K2);
   uint16_t* cw1 = reinterpret_cast<uint16_t*>(st2 + kLsRows);  // [kLsWaves][K1p]
   uint16_t* cw2 = cw1 + kLsWaves * K1p;                         // [kLsWaves][K2p]
-  __shared__ int32_t wsum[kLsWaves], wkept[kLsWaves];
+  __shared__ int32_t wsum[2][kLsWaves], wkept[kLsWaves];
   __shared__ uint32_t spare[kLsWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int item = a.xitems[blockIdx.x];  // XCD-grouped order (build_items)
@@ -370,8 +415,10 @@ __global__ __launch_bounds__(kLsThreads) void k_ls_scatter2(Ls2Args a) {
     wave_rank(qk, reinterpret_cast<uint32_t*>(cw2 + wave * K2p), &spare[wave], p2);
     wave_kept(hk, lane, wave, wkept);
     __syncthreads();
-    ls_offsets(cw1, K1p, tot1, run1, del1, K1, wsum, tid, lane, wave);
-    ls_offsets(cw2, K2p, tot2, run2, del2, K2, wsum, tid, lane, wave);
+    {
+      const LsKeys ks[2] = {{cw1, K1p, tot1, run1, del1, K1}, {cw2, K2p, tot2, run2, del2, K2}};
+      ls_offsets_n<2>(ks, wsum, tid, lane, wave);
+    }
     int32_t nk = 0;  // kept rows of this sub-chunk
     for (int w2 = 0; w2 < kLsWaves; ++w2) nk += wkept[w2];
 #pragma unroll
@@ -430,7 +477,7 @@ __global__ void k_unit_bounds(const int32_t* __restrict__ seg_off, int32_t H, in
 
 // bucket-local counting sort of the kept rows given the per-item histograms
 // itemcnt [n_items][K] (k_ls_hist2); off = [nb K + 1] exclusive offsets.  The rows of a
-// key are placed in the deterministic wave-ranking order (ls_offsets / wave_rank), so the
+// key are placed in the deterministic wave-ranking order (ls_offsets_n / wave_rank), so the
 // summation order of K1 / K2 - and with it every bit of the sweeps - repeats run to run.
 template <bool KEYQ, typename VT>
 static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off, size_t& off_cap, VT* out) {
