@@ -1,10 +1,14 @@
 """Strategy selection, restating python/leanfe/compress.py:96-184
 (``determine_strategy``) and :187-253 (``estimate_compression_ratio``).
 
-The HIP backend implements the ``alt_proj`` / ``demean`` / ``ols`` strategies.
-When the cost model picks ``compress`` (YOCO, low-cardinality FEs — a
-different algorithm for the same least-squares estimates, SURVEY.md §8f rank
-3) the HIP backend runs ``alt_proj`` instead and says so.
+The HIP backend implements every strategy the cost model can pick: ``alt_proj``,
+``demean``, ``ols`` and ``compress`` (YOCO records grouped on the device,
+``lfe_compress``; ``hip_impl._compress_fit``).  A row-sharded engine maps an
+inferred ``compress`` to ``alt_proj``: YOCO groups one process's rows.
+
+``estimate_compression_ratio`` is the host restatement of the reference's
+count; the product takes the exact count from the device
+(``lfe_count_distinct_rows``) and the tests use this one as its checker.
 """
 from __future__ import annotations
 
