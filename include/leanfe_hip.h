@@ -197,6 +197,16 @@ int lfe_cluster_meat_subsets(lfe_ctx* ctx, int n_subsets, const int32_t* subset_
  * n host codes out, *n_levels_out = number of distinct ids.  Needs no loaded data. */
 int lfe_factorize_ids(lfe_ctx* ctx, int64_t n, const int64_t* ids, int32_t* codes_out, int32_t* n_levels_out);
 
+/* Dense int32 codes of a string column (the String branch of _cats_to_int,
+ * polars_impl.py:118-139: cast to Categorical, take the physical codes; only group
+ * membership matters).  Arrow layout on the host: offsets [n + 1] int64 (offsets[0] = 0,
+ * non-decreasing), string i = data[offsets[i], offsets[i + 1]) compared as bytes.  Codes are
+ * numbered in the order of 64-bit string hashes, not lexicographically; equal-hash strings
+ * are compared byte by byte, so the grouping is exact.  *n_levels_out = number of distinct
+ * strings.  Needs no loaded data. */
+int lfe_factorize_strings(lfe_ctx* ctx, int64_t n, const int64_t* offsets, const uint8_t* data, int32_t* codes_out,
+                          int32_t* n_levels_out);
+
 /* Exact number of distinct rows over the regressors x (loaded columns 1..n_x, not y
  * and not the instruments loaded after x; n_x < 0: every column 1..p-1) and the FE
  * codes, all loaded rows: the numerator of estimate_compression_ratio, whose key is

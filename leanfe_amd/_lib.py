@@ -54,6 +54,7 @@ SIGNATURES = {
     "lfe_cluster_meat": (C.c_int, [_vp, _dp, _i64p]),
     "lfe_cluster_meat_subsets": (C.c_int, [_vp, C.c_int, _vp, _dp, _i64p]),
     "lfe_factorize_ids": (C.c_int, [_vp, C.c_int64, _vp, _vp, C.POINTER(C.c_int32)]),
+    "lfe_factorize_strings": (C.c_int, [_vp, C.c_int64, _vp, _vp, _vp, C.POINTER(C.c_int32)]),
     "lfe_count_distinct_rows": (C.c_int, [_vp, C.c_int, _i64p]),
     "lfe_compress": (C.c_int, [_vp, _i64p]),
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
@@ -261,6 +262,19 @@ class Engine:
         g = C.c_int32()
         _check(self._lib.lfe_factorize_ids(self._h, a.size, _ptr(a) if a.size else None,
                                            _ptr(codes) if a.size else None, C.byref(g)))
+        return codes, int(g.value)
+
+    def factorize_strings(self, offsets: np.ndarray, data: np.ndarray) -> tuple[np.ndarray, int]:
+        """Dense int32 codes of a string column in Arrow layout (int64 offsets [n + 1] from 0,
+        uint8 bytes): exact grouping, codes numbered in string-hash order."""
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        buf = np.ascontiguousarray(data, dtype=np.uint8)
+        n = max(off.size - 1, 0)
+        codes = np.empty(n, dtype=np.int32)
+        g = C.c_int32()
+        _check(self._lib.lfe_factorize_strings(self._h, n, _ptr(off) if n else None,
+                                               _ptr(buf) if buf.size else None,
+                                               _ptr(codes) if n else None, C.byref(g)))
         return codes, int(g.value)
 
     def count_distinct_rows(self, n_x: int = -1) -> int:

@@ -204,6 +204,99 @@ __global__ void k_fz_codes(const uint64_t* __restrict__ K, const int32_t* __rest
 }
 
 // ---------------------------------------------------------------------------
+// factorization of strings (Arrow layout: int64 offsets [n + 1] + one byte buffer)
+// ---------------------------------------------------------------------------
+// 64-bit string hashes are radix-sorted; equal strings have equal hashes, so a new
+// group starts at every hash change.  Neighbours with equal hashes are compared byte
+// by byte; a hash run that holds different strings (about 1e-8 odds for 1e6 distinct
+// strings) is split exactly by k_str_exact, so the grouping is always exact.
+
+struct StrArgs {
+  const int64_t* off;   // [n + 1]
+  const uint8_t* data;  // off[n] bytes
+  int64_t n;
+  int hash_bits;        // 64; fewer only to exercise the collision path in tests
+};
+
+__device__ __forceinline__ uint64_t str_hash(const uint8_t* s, int64_t len) {
+  uint64_t h = fmix64(0x9e3779b97f4a7c15ull ^ (uint64_t)len);
+  int64_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) w |= (uint64_t)s[i + b] << (8 * b);
+    h = fmix64(h ^ w);
+  }
+  uint64_t w = 0;
+  for (int b = 0; i + b < len; ++b) w |= (uint64_t)s[i + b] << (8 * b);
+  return fmix64(h ^ w ^ 0x5bd1e995ull);
+}
+
+__device__ __forceinline__ bool str_equal(const StrArgs& a, int64_t i, int64_t j) {
+  const int64_t li = a.off[i + 1] - a.off[i], lj = a.off[j + 1] - a.off[j];
+  if (li != lj) return false;
+  const uint8_t* si = a.data + a.off[i];
+  const uint8_t* sj = a.data + a.off[j];
+  for (int64_t b = 0; b < li; ++b)
+    if (si[b] != sj[b]) return false;
+  return true;
+}
+
+__global__ void k_str_keys(StrArgs a, uint64_t* __restrict__ keys, int32_t* __restrict__ rows) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = str_hash(a.data + a.off[i], a.off[i + 1] - a.off[i]);
+    keys[i] = a.hash_bits >= 64 ? h : (h & ((1ull << a.hash_bits) - 1));
+    rows[i] = (int32_t)i;
+  }
+}
+
+// flag[q] = hash change; count neighbours with equal hashes but different strings
+__global__ void k_str_heads(StrArgs a, const uint64_t* __restrict__ K, const int32_t* __restrict__ R,
+                            int32_t* __restrict__ flag, int32_t* __restrict__ nmismatch) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += (int64_t)gridDim.x * blockDim.x) {
+    const bool head = q == 0 || K[q] != K[q - 1];
+    flag[q] = head ? 1 : 0;
+    if (!head && !str_equal(a, R[q], R[q - 1])) atomicAdd(nmismatch, 1);
+  }
+}
+
+// Exact split of hash runs (one thread per run head).  A run of d distinct strings sets
+// flag[head] = d, and adj[i] = local index of member i's string (first-occurrence order in
+// the run) minus d for every member but the head, so that after the exclusive scan of flag
+// code(i) = scan[i] + adj[i] (k_str_codes).  A run of one string: adj = 0 at the head, -1 after.
+__global__ void k_str_exact(StrArgs a, const uint64_t* __restrict__ K, const int32_t* __restrict__ R,
+                            int32_t* __restrict__ flag, int32_t* __restrict__ adj) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += (int64_t)gridDim.x * blockDim.x) {
+    if (!(q == 0 || K[q] != K[q - 1])) continue;
+    int64_t e = q + 1;
+    bool mixed = false;
+    while (e < a.n && K[e] == K[q]) {
+      mixed = mixed || !str_equal(a, R[e], R[e - 1]);
+      ++e;
+    }
+    if (!mixed) {
+      adj[q] = 0;
+      for (int64_t i = q + 1; i < e; ++i) adj[i] = -1;
+      continue;
+    }
+    int32_t d = 0;
+    for (int64_t i = q; i < e; ++i) {  // adj[i] = local index (first occurrence order)
+      int64_t j = q;
+      while (j < i && !str_equal(a, R[j], R[i])) ++j;
+      adj[i] = j == i ? d++ : adj[j];
+    }
+    flag[q] = d;
+    for (int64_t i = q + 1; i < e; ++i) adj[i] -= d;
+  }
+}
+
+__global__ void k_str_codes(const int32_t* __restrict__ scan, const int32_t* __restrict__ adj,
+                            const int32_t* __restrict__ R, int64_t n, int32_t* __restrict__ codes) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+    codes[R[q]] = scan[q] + adj[q];
+}
+
+// ---------------------------------------------------------------------------
 // distinct rows
 // ---------------------------------------------------------------------------
 
@@ -306,6 +399,84 @@ int lfe_factorize_ids(lfe_ctx* c, int64_t n, const int64_t* ids, int32_t* codes_
   // codes go to the other row buffer (free now), then to the host
   int32_t* dcodes = W.rows[1 - buf];
   hipLaunchKernelGGL(k_fz_codes, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, W.flag, R, n, dcodes);
+  LFE_HIP(hipGetLastError());
+  LFE_HIP(hipMemcpyAsync(codes_out, dcodes, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  int32_t G = 0;
+  LFE_TRY(d2h_sync(c, &G, W.flag + n, sizeof(int32_t)));
+  *n_levels_out = G;
+  return LFE_OK;
+}
+
+namespace {
+// one-call device scratch (string offsets / bytes); hipFree waits for the device
+struct ScratchBuf {
+  void* p = nullptr;
+  ~ScratchBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+int lfe_factorize_strings(lfe_ctx* c, int64_t n, const int64_t* offsets, const uint8_t* data, int32_t* codes_out,
+                          int32_t* n_levels_out) {
+  if (!c) return fail(LFE_EINVAL, "null context");
+  if (n < 0 || n >= (int64_t)INT32_MAX || !n_levels_out || (n > 0 && (!offsets || !codes_out)))
+    return fail(LFE_EINVAL, "bad arguments");
+  if (n == 0) {
+    *n_levels_out = 0;
+    return LFE_OK;
+  }
+  // the kernels index data with these offsets: they must start at 0 and never decrease
+  if (offsets[0] != 0) return fail(LFE_EINVAL, "offsets[0] must be 0");
+  for (int64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return fail(LFE_EINVAL, "offsets must be non-decreasing");
+  const int64_t nbytes = offsets[n];
+  if (nbytes > 0 && !data) return fail(LFE_EINVAL, "null string data");
+  LFE_HIP(hipSetDevice(c->device));
+  ScratchBuf boff, bdata;
+  LFE_HIP(hipMalloc(&boff.p, sizeof(int64_t) * (size_t)(n + 1)));
+  LFE_HIP(hipMalloc(&bdata.p, (size_t)std::max<int64_t>(nbytes, 1)));
+  StrArgs a{};
+  a.off = static_cast<const int64_t*>(boff.p);
+  a.data = static_cast<const uint8_t*>(bdata.p);
+  a.n = n;
+  const char* hb_env = getenv("LFE_STR_HASH_BITS");  // tests: a short hash forces collisions
+  const int hb = hb_env ? atoi(hb_env) : 64;
+  a.hash_bits = hb >= 4 && hb <= 64 ? hb : 64;
+  LFE_HIP(hipMemcpyAsync(boff.p, offsets, sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, c->stream));
+  if (nbytes > 0) LFE_HIP(hipMemcpyAsync(bdata.p, data, (size_t)nbytes, hipMemcpyHostToDevice, c->stream));
+  LFE_TRY(ensure_sort_ws(c, (size_t)n));
+  auto& W = c->clw;
+  hipLaunchKernelGGL(k_str_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, W.keys[0],
+                     W.rows[0]);
+  LFE_HIP(hipGetLastError());
+  int buf = 0;
+  LFE_TRY(radix_sort(c, n, a.hash_bits, &buf));
+  const uint64_t* K = W.keys[buf];
+  const int32_t* R = W.rows[buf];
+  LFE_TRY(ensure_dred(c, 1));
+  LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double), c->stream));
+  int32_t* nmis = reinterpret_cast<int32_t*>(c->dred);
+  LFE_HIP(hipMemsetAsync(W.flag + n, 0, sizeof(int32_t), c->stream));
+  hipLaunchKernelGGL(k_str_heads, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, K, R, W.flag,
+                     nmis);
+  LFE_HIP(hipGetLastError());
+  int32_t mismatches = 0;
+  LFE_TRY(d2h_sync(c, &mismatches, nmis, sizeof(int32_t)));
+  int32_t* adj = reinterpret_cast<int32_t*>(W.keys[1 - buf]);  // the sort's spare key buffer (n x u64)
+  if (mismatches > 0) {
+    hipLaunchKernelGGL(k_str_exact, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, K, R, W.flag,
+                       adj);
+    LFE_HIP(hipGetLastError());
+  }
+  LFE_TRY(exclusive_scan(c, W.flag, n + 1));
+  int32_t* dcodes = W.rows[1 - buf];
+  if (mismatches > 0)
+    hipLaunchKernelGGL(k_str_codes, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, W.flag, adj, R, n,
+                       dcodes);
+  else
+    hipLaunchKernelGGL(k_fz_codes, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, W.flag, R, n,
+                       dcodes);
   LFE_HIP(hipGetLastError());
   LFE_HIP(hipMemcpyAsync(codes_out, dcodes, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
   int32_t G = 0;

@@ -111,8 +111,49 @@ def factorize(values, global_codes: bool = False, device=None) -> tuple[np.ndarr
             return device.factorize_ids(v.astype(np.int64, copy=False))
     elif device is not None and n < 2 ** 31 - 1 and v.dtype in (np.float64, np.float32):
         return device.factorize_ids(float_order_keys(v))
+    elif device is not None and n < 2 ** 31 - 1 and v.dtype.kind in ("U", "S", "O"):
+        sb = string_buffers(v)
+        if sb is not None:  # strings without nulls: grouped on the device (_cats_to_int's String cast)
+            return device.factorize_strings(*sb)
     uniq, inv = np.unique(v, return_inverse=True)
     return inv.astype(np.int32).ravel(), int(uniq.size)
+
+
+def string_buffers(values) -> tuple[np.ndarray, np.ndarray] | None:
+    """Arrow layout of a string (or bytes) column: int64 offsets [n + 1] starting at 0 and the
+    uint8 bytes, for ``lfe_factorize_strings``.  None when the values are not all strings / all
+    bytes or hold nulls (those keep the host's sorted unique)."""
+    import pyarrow as pa
+
+    if isinstance(values, pa.ChunkedArray):
+        arr = values.combine_chunks()
+    elif isinstance(values, pa.Array):
+        arr = values
+    else:
+        v = np.asarray(values)
+        kinds = {"U": [pa.large_string()], "S": [pa.large_binary()], "O": [pa.large_string(), pa.large_binary()]}
+        arr = None
+        for t in kinds.get(v.dtype.kind, []):
+            try:
+                arr = pa.array(v, type=t, from_pandas=False)
+                break
+            except (pa.ArrowInvalid, pa.ArrowTypeError, TypeError):
+                continue
+        if arr is None:
+            return None
+    if arr.null_count:
+        return None
+    if pa.types.is_string(arr.type) or pa.types.is_large_string(arr.type):
+        arr = arr.cast(pa.large_string())
+    elif pa.types.is_binary(arr.type) or pa.types.is_large_binary(arr.type):
+        arr = arr.cast(pa.large_binary())
+    else:
+        return None
+    bufs = arr.buffers()
+    off = np.frombuffer(bufs[1], dtype=np.int64, count=len(arr) + 1, offset=arr.offset * 8)
+    data = np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None else np.zeros(0, np.uint8)
+    lo, hi = int(off[0]), int(off[-1])
+    return off - lo, data[lo:hi]
 
 
 def float_order_keys(v: np.ndarray) -> np.ndarray:

@@ -130,3 +130,80 @@ def test_sparse_cluster_ids_factorized_on_device_same_fit():
     for x in ("x1", "x2", "x3"):
         assert r.coefs[x] == pytest.approx(ref.coefs[x], rel=1e-12)
         assert r.std_errors[x] == pytest.approx(ref.std_errors[x], rel=1e-12)
+
+
+def _same_partition(codes, G, ref_inv, ref_G):
+    """codes and ref_inv group the rows identically (codes may be numbered differently)."""
+    assert G == ref_G
+    assert codes.min() >= 0 and codes.max() == G - 1
+    # a bijection between the two labelings: each code maps to exactly one reference code
+    pairs = np.unique(np.stack([codes.astype(np.int64), ref_inv.astype(np.int64)], axis=1), axis=0)
+    assert pairs.shape[0] == G
+
+
+def _words(rng, n, n_distinct):
+    alphabet = np.array(list("abcxyzÆøå中文 _-0123456789"))
+    pool = ["".join(rng.choice(alphabet, rng.integers(0, 24))) for _ in range(n_distinct)]
+    pool[0] = ""  # the empty string is a value of its own
+    pool[1] = "a" * 40  # long, shares a prefix with pool[2]
+    pool[2] = "a" * 39 + "b"
+    pool = list(dict.fromkeys(pool))
+    return np.array(pool, dtype=object)[rng.integers(0, len(pool), n)]
+
+
+@pytest.mark.parametrize("hash_bits", [64, 8])
+def test_factorize_strings_exact_grouping(eng, hash_bits):
+    """String FE ids (_cats_to_int's String -> Categorical cast, polars_impl.py:118-139) are
+    grouped on the device exactly as np.unique groups them; 8-bit hashes force thousands of
+    collisions through the exact split (k_str_exact)."""
+    from leanfe_amd import frame
+    rng = np.random.default_rng(31)
+    v = _words(rng, 200_000 if hash_bits == 64 else 30_000, 3000)
+    os.environ["LFE_STR_HASH_BITS"] = str(hash_bits)
+    try:
+        codes, G = frame.factorize(v, device=eng)
+    finally:
+        os.environ.pop("LFE_STR_HASH_BITS", None)
+    uniq, inv = np.unique(v.astype(str), return_inverse=True)
+    _same_partition(codes, G, inv.ravel(), uniq.size)
+
+
+@pytest.mark.parametrize("case", ["single", "all_equal", "all_empty", "bytes", "arrow_slice"])
+def test_factorize_strings_edge_cases(eng, case):
+    import pyarrow as pa
+    from leanfe_amd import frame
+    if case == "single":
+        v, ref = np.array(["only"]), np.array(["only"])
+    elif case == "all_equal":
+        v = ref = np.array(["same"] * 5000, dtype=object)
+    elif case == "all_empty":
+        v = ref = np.array([""] * 777, dtype=object)
+    elif case == "bytes":
+        v = ref = np.array([b"\x00", b"", b"\x00\x00", b"\x00", b"ab"] * 300, dtype=object)
+    else:
+        full = pa.array(["p", "q", "p", "r", "q", "p", "s"] * 200)
+        v = full.slice(3, 1000)
+        ref = np.array(v.to_pylist(), dtype=object)
+    codes, G = frame.factorize(v, device=eng)
+    uniq, inv = np.unique(ref, return_inverse=True)
+    _same_partition(codes, G, inv.ravel(), uniq.size)
+
+
+def test_string_fe_columns_same_fit():
+    """A fit with string FE and cluster columns (factorized on the device) equals the fit on
+    their integer codes (β / SE within 1e-12, integers equal)."""
+    from leanfe_amd import leanfe_hip
+    n, L = 150_000, [2000, 60, 300]
+    data = synth.panel(n, 3, L, seed=29)
+    ref = leanfe_hip(data, formula="y ~ x1 + x2 + x3 | fe1 + fe2", vcov="cluster",
+                     cluster_cols=["fe3"], quiet=True)
+    s = dict(data)
+    s["fe1"] = np.array([f"firm-{g:05d}" for g in data["fe1"]], dtype=object)
+    s["fe2"] = np.array([f"yr{g}" for g in data["fe2"]], dtype=object)
+    s["fe3"] = np.array([f"state_{g}" for g in data["fe3"]], dtype=object)
+    r = leanfe_hip(s, formula="y ~ x1 + x2 + x3 | fe1 + fe2", vcov="cluster", cluster_cols=["fe3"], quiet=True)
+    assert r.n_clusters == ref.n_clusters and r.n_obs == ref.n_obs and r.iterations == ref.iterations
+    assert sorted(r.fe_dims) == sorted(ref.fe_dims)
+    for x in ("x1", "x2", "x3"):
+        assert r.coefs[x] == pytest.approx(ref.coefs[x], rel=1e-12)
+        assert r.std_errors[x] == pytest.approx(ref.std_errors[x], rel=1e-12)

@@ -97,6 +97,21 @@ def test_factorize_fast_path_and_unique():
     assert g == 2 and c.tolist() == [0, 1, 0]
 
 
+def test_string_buffers_arrow_layout():
+    """The host hand-off of lfe_factorize_strings: int64 offsets from 0 and the bytes; None
+    for nulls and mixed types (those keep the host's sorted unique)."""
+    import pyarrow as pa
+    off, data = frame.string_buffers(np.array(["ab", "", "héllo"], dtype=object))
+    assert off.tolist() == [0, 2, 2, 8] and bytes(data) == "abhéllo".encode()
+    off, data = frame.string_buffers(pa.array(["q", "rr", "s"]).slice(1))
+    assert off.tolist() == [0, 2, 3] and bytes(data) == b"rrs"
+    off, data = frame.string_buffers(np.array([b"\x00a", b"z"], dtype=object))
+    assert off.tolist() == [0, 2, 3] and bytes(data) == b"\x00az"
+    assert frame.string_buffers(np.array(["x", None], dtype=object)) is None
+    assert frame.string_buffers(np.array([1, "a"], dtype=object)) is None
+    assert frame.string_buffers(np.array([1.5, 2.5])) is None
+
+
 def test_intersect_membership():
     a = np.array([0, 0, 1, 1, 0], dtype=np.int32)
     b = np.array([0, 1, 0, 1, 0], dtype=np.int32)
