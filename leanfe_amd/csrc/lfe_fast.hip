@@ -427,6 +427,40 @@ __global__ __launch_bounds__(256) void k_col_stats(const double* __restrict__ X,
   }
 }
 
+// weighted fits: the statistics of what their group sums add, in the same layout for p + 2
+// "columns": c < p the products w x_c (S_f), c = p the weights (W_f), c = p + 1 the raw y (Sy_f,
+// the unweighted stop test).  Rows past n read 0; dropped rows count too (a looser bound).
+__global__ __launch_bounds__(256) void k_col_stats_w(const double* __restrict__ X, const double* __restrict__ w,
+                                                     int64_t ld, int64_t n, int p, int64_t chunk_rows,
+                                                     double* __restrict__ st) {
+  __shared__ double ws[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * chunk_rows, r1 = min(n, r0 + chunk_rows);
+  const auto fmaxop = [](double x, double y) { return fmax(x, y); };
+  const auto addop = [](double x, double y) { return x + y; };
+  for (int c = 0; c < p + 2; ++c) {
+    double m = 0.0, q = 0.0;
+    for (int64_t i = r0 + tid; i < r1; i += 256) {
+      const double v = c < p ? X[(int64_t)c * ld + i] * w[i] : (c == p ? w[i] : X[i]);
+      m = fmax(m, fabs(v));
+      q = __builtin_fma(v, v, q);
+    }
+    m = wave_reduce63(m, 0.0, fmaxop);
+    q = wave_reduce63(q, 0.0, addop);
+    if (lane == 63) {
+      ws[0][wave] = m;
+      ws[1][wave] = q;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      st[kColStatHead + (int64_t)c * gridDim.x + blockIdx.x] = ((ws[1][0] + ws[1][1]) + ws[1][2]) + ws[1][3];
+      const double mm = fmax(fmax(ws[0][0], ws[0][1]), fmax(ws[0][2], ws[0][3]));
+      atomicMax(reinterpret_cast<unsigned long long*>(st) + c, (unsigned long long)__double_as_longlong(mm));
+    }
+    __syncthreads();
+  }
+}
+
 // scale, quantum and qualification of column c = blockIdx.x (fq: [kMaxCols] scales, [kMaxCols]
 // quanta, [kMaxCols] 1.0 / 0.0); the per-chunk squares are summed in a fixed order
 __global__ __launch_bounds__(256) void k_fix_quanta(const double* __restrict__ st, int nchunks, int64_t n,
@@ -613,8 +647,10 @@ int sums4(lfe_ctx* c) {
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
     a.raw_part = c->raw_part;
   }
-  // exact (int64) group sums for every unweighted fit: the two-FE kernel and k_sums4 alike
-  const bool exact = two || !a.w;
+  // exact (int64) group sums for every unweighted fit (the two-FE kernel and k_sums4 alike) and
+  // for weighted fits, whose quanta come from the statistics of w x, w and y (k_col_stats_w)
+  const bool wexact = a.w != nullptr && p + 2 <= kMaxCols;
+  const bool exact = two || !a.w || wexact;
   if (two) {
     LFE_TRY(ensure_f64(c, c->qpart, c->qpart_cap, (size_t)nblocks * c->fe[a.qf[0]].G * p));
     a.qpart = c->qpart;
@@ -623,7 +659,19 @@ int sums4(lfe_ctx* c) {
     ProfScope _ps(c, K_FIX_SUMS);
     // the column statistics (the partition wrote them unless the rows stayed in place)
     constexpr int64_t kStatRows = 16384;
-    if (c->colstat_chunks == 0) {
+    if (wexact) {
+      const int nch = (int)std::max<int64_t>(1, (c->n + kStatRows - 1) / kStatRows);
+      LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nch * (p + 2)));
+      LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
+      hipLaunchKernelGGL(k_col_stats_w, dim3(nch), dim3(256), 0, c->stream, c->L.X, c->L.w, c->ld, c->n, p,
+                         kStatRows, c->colstat);
+      LFE_HIP(hipGetLastError());
+      LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, 3 * kMaxCols));
+      hipLaunchKernelGGL(k_fix_quanta, dim3(p + 2), dim3(256), 0, c->stream, c->colstat, nch, c->n,
+                         c->iscratch + kIscratchCmax, c->F, c->fixq);
+      LFE_HIP(hipGetLastError());
+      c->colstat_chunks = 0;  // these are the weighted statistics: an unweighted pass recomputes its own
+    } else if (c->colstat_chunks == 0) {
       const int nch = (int)std::max<int64_t>(1, (c->n + kStatRows - 1) / kStatRows);
       LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nch * p));
       LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
@@ -632,10 +680,12 @@ int sums4(lfe_ctx* c) {
       LFE_HIP(hipGetLastError());
       c->colstat_chunks = nch;
     }
-    LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, 3 * kMaxCols));
-    hipLaunchKernelGGL(k_fix_quanta, dim3(p), dim3(256), 0, c->stream, c->colstat, c->colstat_chunks, c->n,
-                       c->iscratch + kIscratchCmax, c->F, c->fixq);
-    LFE_HIP(hipGetLastError());
+    if (!wexact) {
+      LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, 3 * kMaxCols));
+      hipLaunchKernelGGL(k_fix_quanta, dim3(p), dim3(256), 0, c->stream, c->colstat, c->colstat_chunks, c->n,
+                         c->iscratch + kIscratchCmax, c->F, c->fixq);
+      LFE_HIP(hipGetLastError());
+    }
     a.fixq = c->fixq;
   }
   c->exact_sums = exact;
@@ -884,10 +934,12 @@ int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int
 int exact_sums_on(lfe_ctx* c, int* on) {
   *on = 0;
   if (!c->exact_sums || !c->fixq) return LFE_OK;
+  // weighted fits: the S columns, the weights (W) and the raw y (Sy) must all qualify
+  const int nc = c->p + ((c->L.w && c->p + 2 <= kMaxCols) ? 2 : 0);
   double flag[kMaxCols];
-  LFE_TRY(d2h_sync(c, flag, c->fixq + 2 * kMaxCols, sizeof(double) * c->p));
+  LFE_TRY(d2h_sync(c, flag, c->fixq + 2 * kMaxCols, sizeof(double) * nc));
   *on = 1;
-  for (int j = 0; j < c->p; ++j) *on = *on && flag[j] != 0.0;
+  for (int j = 0; j < nc; ++j) *on = *on && flag[j] != 0.0;
   return LFE_OK;
 }
 

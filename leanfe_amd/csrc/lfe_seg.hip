@@ -286,8 +286,13 @@ __global__ __launch_bounds__(256) void k_alpha_colmax(const double* __restrict__
 // their column max |alpha|, a group sum by N M (N = the largest kept group of f); scale =
 // 2^min(62 - e, 50 - e_M), 2^e > N M, 2^e_M > M (one bit of headroom for the rounding of the row
 // sums).  A non-finite bound (NaN / Inf effects) keeps the f64 sums.
+// Weighted (wmax != null): a row adds w v, so M is scaled by max |w| (k_col_stats_w); only when the
+// weight column qualified for the exact sums (max |w| <= 64 rms(w), wfq's flag), else the quanta
+// would be coarse against typical rows and the f64 sums stay.
 __global__ void k_cross_quanta(const unsigned long long* __restrict__ amax, int F, int f, int pc,
-                               const int32_t* __restrict__ cmax, double* __restrict__ xq) {
+                               const int32_t* __restrict__ cmax, double* __restrict__ xq,
+                               const unsigned long long* __restrict__ wmax, const double* __restrict__ wfq,
+                               int wcol) {
   __shared__ int bad;
   if (threadIdx.x == 0) bad = 0;
   __syncthreads();
@@ -296,8 +301,13 @@ __global__ void k_cross_quanta(const unsigned long long* __restrict__ amax, int 
     double M = 0.0;
     for (int j = 0; j < F; ++j)
       if (j != f) M += __longlong_as_double((long long)amax[j * kMaxCols + col]);
+    bool wok = true;
+    if (wmax) {
+      wok = wfq[2 * kMaxCols + wcol] != 0.0;
+      M *= __longlong_as_double((long long)wmax[0]);
+    }
     const double NM = (double)max(1, cmax[f]) * M;
-    const bool ok = isfinite(NM);
+    const bool ok = wok && isfinite(NM);
     double scale = 1.0, quantum = 1.0;
     if (ok && M > 0.0) {
       int e = 0, eM = 0;
@@ -462,14 +472,17 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
   a.pc = pc;
   a.G = fe.G;
   a.T = out;
-  // unweighted cross terms sum exactly (int64 per column): bit-reproducible whatever the order
-  // of the segment layout's rows (ranked by global cursor atomics) and of the cut segments' adds
-  const bool ex = !wt && c->amax != nullptr;
+  // cross terms sum exactly (int64 per column): bit-reproducible whatever the order of the
+  // segment layout's rows (ranked by global cursor atomics) and of the cut segments' adds.
+  // Weighted fits too when the group sums formed the weighted statistics (max |w| in colstat[p]).
+  const bool wstat = wt && c->exact_sums && c->p + 2 <= kMaxCols && c->colstat && c->fixq;
+  const bool ex = c->amax != nullptr && (!wt || wstat);
   if (ex) {
     LFE_TRY(ensure_f64(c, c->xq, c->xq_cap, 3 * kMaxCols));
     hipLaunchKernelGGL(k_cross_quanta, dim3(1), dim3(64), 0, c->stream,
                        reinterpret_cast<const unsigned long long*>(c->amax), c->F, f, pc,
-                       c->iscratch + kIscratchCmax, c->xq);
+                       c->iscratch + kIscratchCmax, c->xq,
+                       wt ? reinterpret_cast<const unsigned long long*>(c->colstat) + c->p : nullptr, c->fixq, c->p);
     LFE_HIP(hipGetLastError());
     a.xq = c->xq;
   }

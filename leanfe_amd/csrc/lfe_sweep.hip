@@ -40,13 +40,39 @@ struct SweepArgs {
   double* out[kMaxFE];  // output tables [G] (nullptr: not a target)
   int lds_off[kMaxFE];  // LDS table offset (doubles), -1 = global atomics
   int lds_doubles;
+  const double* fq;     // exact sums (k_fix_quanta of k_col_stats_w) or null: f64 atomics
+  int fcol;             // the quanta's column of this source (p: weights, p + 1: y)
 };
+
+// exact sums: round(v * scale) is the low mantissa of v * scale + 1.5 * 2^52 (lfe_fast.hip)
+constexpr double kSwMagic = 6755399441055744.0;
+constexpr unsigned long long kSwMagicBits = 0x4338000000000000ull;
+__device__ __forceinline__ bool sweep_fix_on(const double* fq, int col) {
+  return fq != nullptr && fq[2 * kMaxCols + col] != 0.0;
+}
 
 __global__ __launch_bounds__(kSweepThreads) void k_sweep_sums(SweepArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x;
   const int P = a.la.P, s = a.la.s;
   const int B = 1 << s;
+  typedef unsigned long long u64;
+  // exact: integer adds commute, so the tables do not depend on the order of the adds
+  const bool fix = sweep_fix_on(a.fq, a.fcol);
+  const double fsc = fix ? a.fq[a.fcol] : 0.0;
+  auto add = [&](double* dst, double v) {
+    if (fix)
+      atomicAdd(reinterpret_cast<u64*>(dst), (u64)__double_as_longlong(__builtin_fma(v, fsc, kSwMagic)) - kSwMagicBits);
+    else
+      atomicAdd(dst, v);
+  };
+  auto nonzero = [&](const double* src) {
+    return fix ? *reinterpret_cast<const u64*>(src) != 0ull : *src != 0.0;
+  };
+  auto flush_add = [&](double* dst, const double* src) {
+    if (fix) atomicAdd(reinterpret_cast<u64*>(dst), *reinterpret_cast<const u64*>(src));
+    else atomicAdd(dst, *src);
+  };
 
   // zero the non-slice LDS tables once per workgroup
   for (int f = 0; f < a.la.F; ++f)
@@ -67,17 +93,16 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_sums(SweepArgs a) {
       for (int f = 0; f < a.la.F; ++f) {
         if (!a.out[f]) continue;
         const int64_t g = (f == P) ? (int64_t)(hP - lo) : (int64_t)a.la.code[f][i];
-        if (a.lds_off[f] >= 0) atomicAdd(&lds[a.lds_off[f] + g], v);
-        else atomicAdd(&a.out[f][(f == P) ? (int64_t)hP : g], v);
+        if (a.lds_off[f] >= 0) add(&lds[a.lds_off[f] + g], v);
+        else add(&a.out[f][(f == P) ? (int64_t)hP : g], v);
       }
     }
     __syncthreads();
     // flush the primary slice of this item
     if (P >= 0 && a.out[P] && a.lds_off[P] >= 0)
       for (int j = tid; j < B; j += blockDim.x) {
-        const double val = lds[a.lds_off[P] + j];
         const int g = lo + j;
-        if (val != 0.0 && g < a.G[P]) atomicAdd(&a.out[P][g], val);
+        if (nonzero(&lds[a.lds_off[P] + j]) && g < a.G[P]) flush_add(&a.out[P][g], &lds[a.lds_off[P] + j]);
       }
   }
   __syncthreads();
@@ -85,9 +110,16 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_sums(SweepArgs a) {
   for (int f = 0; f < a.la.F; ++f)
     if (a.out[f] && a.lds_off[f] >= 0 && f != P)
       for (int j = tid; j < a.G[f]; j += blockDim.x) {
-        const double val = lds[a.lds_off[f] + j];
-        if (val != 0.0) atomicAdd(&a.out[f][j], val);
+        if (nonzero(&lds[a.lds_off[f] + j])) flush_add(&a.out[f][j], &lds[a.lds_off[f] + j]);
       }
+}
+
+// exact one-column tables (int64 bits) -> double
+__global__ void k_fix_convert1(double* __restrict__ T, int64_t m, const double* __restrict__ fq, int col) {
+  if (!sweep_fix_on(fq, col)) return;
+  const double quantum = fq[kMaxCols + col];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x)
+    T[e] = (double)__double_as_longlong(T[e]) * quantum;
 }
 
 // ---------------------------------------------------------------------------
@@ -159,14 +191,27 @@ int sweep_group_sums(lfe_ctx* c) {
       LFE_HIP(hipMemsetAsync(c->fe[f].W, 0, sizeof(double) * c->fe[f].G, c->stream));
       a.out[f] = c->fe[f].W;
     }
+    // exact like S when sums4 formed the weighted quanta (columns p: w, p + 1: y)
+    const bool wq = c->exact_sums && c->p + 2 <= kMaxCols;
+    a.fq = wq ? c->fixq : nullptr;
+    a.fcol = c->p;
     a.src = SRC_WEIGHT;
     LFE_TRY(run_sums(c, a));
     for (int f = 0; f < c->F; ++f) {
       LFE_HIP(hipMemsetAsync(c->fe[f].Sy, 0, sizeof(double) * c->fe[f].G, c->stream));
       a.out[f] = c->fe[f].Sy;
     }
+    a.fcol = c->p + 1;
     a.src = SRC_Y;
     LFE_TRY(run_sums(c, a));
+    if (wq)
+      for (int f = 0; f < c->F; ++f) {
+        hipLaunchKernelGGL(k_fix_convert1, dim3(grid_for(c->fe[f].G)), dim3(kBlock), 0, c->stream, c->fe[f].W,
+                           (int64_t)c->fe[f].G, c->fixq, c->p);
+        hipLaunchKernelGGL(k_fix_convert1, dim3(grid_for(c->fe[f].G)), dim3(kBlock), 0, c->stream, c->fe[f].Sy,
+                           (int64_t)c->fe[f].G, c->fixq, c->p + 1);
+        LFE_HIP(hipGetLastError());
+      }
     for (int f = 0; f < c->F; ++f) {
       LFE_TRY(allreduce_sum_f64(c, c->fe[f].W, c->fe[f].G));
       LFE_TRY(allreduce_sum_f64(c, c->fe[f].Sy, c->fe[f].G));

@@ -5,8 +5,9 @@ The two-FE fast path's group sums accumulate each column as round(x / quantum) i
 the Gram / meat partials in block order, so solving the same panel twice must give
 bit-identical beta, SE, RSS and `iterations` - within one context and across two contexts.
 The general sweeps (F >= 3, large secondary FE, one bucket) sum their group sums and cross
-terms in int64 too, so unweighted fits there are bit-reproducible as well; weighted fits and
-the cluster score sums keep f64 atomics.
+terms in int64 too, so unweighted fits there are bit-reproducible as well, and so are weighted
+fits whose weights pass the fixed-point guard; the cluster score sums keep f64 atomics
+(DESIGN.md §5).
 The exact path must also keep parity with the CPU restatement (oracle/altproj.py,
 polars_impl.py:468-537) at the usual 1e-10 bar, and a column whose range defeats the fixed
 point (one huge outlier) must fall back to the f64 sums and still match."""
@@ -126,3 +127,38 @@ def test_general_sweeps_are_bit_identical(n, L, vcov):
         assert r.iterations == runs[0].iterations and r.n_obs == runs[0].n_obs
         np.testing.assert_array_equal([r.coefs[x] for x in xs], [runs[0].coefs[x] for x in xs])
         np.testing.assert_array_equal([r.std_errors[x] for x in xs], [runs[0].std_errors[x] for x in xs])
+
+
+@pytest.mark.parametrize("L,skew", [([20_000, 500], False), ([30_000, 2_000, 300], False), ([20_000, 500], True)])
+def test_weighted_fits_are_bit_identical_and_keep_parity(L, skew):
+    """Weighted fits sum w x, w and the stop test's raw y in int64 too (quanta from the statistics
+    of k_col_stats_w; k_sums4, k_sweep_sums and the weighted cross terms of k_seg_cross), so two
+    solves agree bit for bit and still match the oracle at 1e-10.  A weight column that defeats
+    the fixed point (one weight 1e6 x the rest) reports the f64 sums and still matches."""
+    from leanfe_amd import leanfe_hip, synth
+    from leanfe_amd._lib import Engine
+    from oracle import altproj
+    k, n = 3, 300_000
+    data = dict(synth.panel(n, k, L, seed=515))
+    w = np.random.default_rng(7).uniform(0.5, 2.0, n)
+    if skew:
+        w[4321] = 1e6
+    data["w"] = w
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(L))]
+    runs = []
+    with Engine(0) as eng:
+        for _ in range(2):
+            runs.append(leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", weights="w",
+                                   vcov="HC1", quiet=True, engine=eng))
+            assert eng.exact_sums() == (not skew)
+    if not skew:
+        r0, r1 = runs
+        assert r1.iterations == r0.iterations and r1.n_obs == r0.n_obs
+        np.testing.assert_array_equal([r1.coefs[x] for x in xs], [r0.coefs[x] for x in xs])
+        np.testing.assert_array_equal([r1.std_errors[x] for x in xs], [r0.std_errors[x] for x in xs])
+    o = altproj.fit(data, "y", xs, fes, vcov="HC1", weights="w")
+    r = runs[0]
+    assert r.iterations == o["iterations"] and r.n_obs == o["n_obs"]
+    np.testing.assert_allclose([r.coefs[x] for x in xs], o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose([r.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
