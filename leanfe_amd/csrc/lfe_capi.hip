@@ -413,7 +413,8 @@ static void free_data(lfe_ctx* c) {
   c->raw_slots_cap = 0;
   dfree(c->amax);
   dfree(c->xq);
-  c->amax_cap = c->xq_cap = 0;
+  dfree(c->chain);
+  c->amax_cap = c->xq_cap = c->chain_cap = 0;
   dfree(c->sw.x);
   dfree(c->sw.s64);
   dfree(c->sw.sdbl);

@@ -79,11 +79,14 @@ __global__ void k_cl_segoff(const uint64_t* __restrict__ K, const int32_t* __res
 // Short segments (a few rows per cluster): one sorted position per lane, its
 // score row gathered into registers, a segmented inclusive scan across the
 // wave (segment ids are non-decreasing), and the last lane of each segment
-// stores S[h]; segments cut by a wave edge add their part atomically (S zeroed).
+// stores S[h]; a segment cut by wave edges leaves its part of each wave in chain
+// ([2][nv / 64][k]: [1] its first part, [0] the parts in the following waves), which
+// k_seg_rows_chain adds in wave order.
 template <int KM>
 __global__ __launch_bounds__(256) void k_seg_rows(const uint64_t* __restrict__ K, const int32_t* __restrict__ scan,
                                                   const int32_t* __restrict__ R, int64_t nv, uint64_t drop,
-                                                  const double* __restrict__ U, int k, double* __restrict__ S) {
+                                                  const double* __restrict__ U, int k, double* __restrict__ S,
+                                                  double* __restrict__ chain) {
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
   for (int64_t wb = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64; wb < nv; wb += nwaves * 64) {
@@ -124,10 +127,32 @@ __global__ __launch_bounds__(256) void k_seg_rows(const uint64_t* __restrict__ K
       for (int j = 0; j < KM; ++j)
         if (j < k) dst[j] = v[j];
     } else {
+      const int64_t nwb = (nv + 63) >> 6;
+      double* part = chain + ((starts_here ? nwb : 0) + (wb >> 6)) * k;
 #pragma unroll
       for (int j = 0; j < KM; ++j)
-        if (j < k) atomicAdd(&dst[j], v[j]);
+        if (j < k) part[j] = v[j];
     }
+  }
+}
+
+// the segments cut by wave edges, their parts added in wave order: one thread per (wave w, column)
+// whose last segment continues into wave w + 1 and began in wave w
+__global__ void k_seg_rows_chain(const uint64_t* __restrict__ K, const int32_t* __restrict__ scan,
+                                 const int32_t* __restrict__ seg_off, int64_t nv, int k,
+                                 const double* __restrict__ chain, double* __restrict__ S) {
+  const int64_t nwb = (nv + 63) >> 6;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nwb * k; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = e / k;
+    const int j = (int)(e % k);
+    const int64_t q = (w + 1) * 64;  // first position of wave w + 1
+    if (q >= nv || K[q] != K[q - 1]) continue;  // no segment continues across this edge
+    const int32_t h = scan[q] - 1;
+    if (seg_off[h] < w * 64) continue;  // begun before wave w: a chain that starts earlier
+    const int64_t we = (seg_off[h + 1] - 1) >> 6;
+    double t = chain[(nwb + w) * k + j];
+    for (int64_t v = w + 1; v <= we; ++v) t += chain[v * k + j];
+    S[(int64_t)h * k + j] = t;
   }
 }
 
@@ -195,20 +220,26 @@ static int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K,
   if (k <= 16 && G > 0 && (int64_t)nv < 8 * (int64_t)G) {
     // short clusters (mean < 8 rows): row-per-lane segmented scan
     LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)G * k, c->stream));
+    const int64_t nwb = ((int64_t)nv + 63) / 64;
+    LFE_TRY(ensure_f64(c, c->chain, c->chain_cap, (size_t)2 * nwb * k));
+    double* chain = c->chain;
     const int grid = grid_for(((int64_t)nv + 63) / 64 * 64, 256, 8192);
     ProfScope _ps(c, K_CLUSTER_SCATTER);
     if (k <= 4)
       hipLaunchKernelGGL(k_seg_rows<4>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, drop, table,
-                         k, c->clS);
+                         k, c->clS, chain);
     else if (k <= 8)
       hipLaunchKernelGGL(k_seg_rows<8>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, drop, table,
-                         k, c->clS);
+                         k, c->clS, chain);
     else if (k <= 12)
       hipLaunchKernelGGL(k_seg_rows<12>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, drop,
-                         table, k, c->clS);
+                         table, k, c->clS, chain);
     else
       hipLaunchKernelGGL(k_seg_rows<16>, dim3(grid), dim3(256), 0, c->stream, K, W.flag, R, (int64_t)nv, drop,
-                         table, k, c->clS);
+                         table, k, c->clS, chain);
+    LFE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_seg_rows_chain, dim3(grid_for(nwb * k)), dim3(kBlock), 0, c->stream, K, W.flag, W.seg_off,
+                       (int64_t)nv, k, chain, c->clS);
   } else {
     LFE_TRY(seg_gather_sum(c, W.seg_off, G, W.ufirst, n, R, table, k, k, c->clS, K_CLUSTER_SCATTER));
   }

@@ -236,6 +236,10 @@ struct lfe_ctx {
   size_t amax_cap = 0;
   double* xq = nullptr;          // [3 * kMaxCols]
   size_t xq_cap = 0;
+  // f64 segmented sums (lfe_seg.hip, lfe_cluster.hip): the partials of segments cut by work-unit /
+  // wave edges, [2][units][cols], added in unit order by a fix-up pass instead of f64 atomics
+  double* chain = nullptr;
+  size_t chain_cap = 0;
   double* raw_tile = nullptr;    // [256] raw tile: slots 0..p-1 data (shifted by raw_shift), slot 15 intercept
   size_t raw_tile_cap = 0;
   double* raw_shift = nullptr;   // [32]: [0, 16) the shift of raw_tile (rank 0's first row on every rank),

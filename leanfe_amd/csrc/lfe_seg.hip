@@ -99,6 +99,7 @@ struct SegCrossArgs {
   int G;
   double* T;                         // [G][pc], zeroed before the launch
   const double* xq;                  // exact sums (null: f64): [kMaxCols] scales, [kMaxCols] quanta, flag
+  double* chain;                     // f64 sums: [2][n_units][pc] cut segments' parts (k_seg_chain); null: atomics
 };
 
 // exact cross terms: a row's value v (the sum of the other FEs' effects) enters T as
@@ -158,7 +159,9 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
       acc[I] = 0.0;
       iacc[I] = 0;
     }
-    auto finalize = [&](bool atomic) {
+    // mode 0: segment h lies in this unit (store); 1: its part in this unit, begun in an earlier
+    // unit; 2: its first part, continued in the next unit
+    auto finalize = [&](int mode) {
 #pragma unroll
       for (int I = 0; I < NT; ++I) {
         const int col = 16 * I + c;
@@ -166,14 +169,15 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
         if (ex) {  // integer adds commute: a cut segment's partials may land in any order
           const long long t = seg_quad_sum_i64(iacc[I]);
           if (kq == 0 && col < pc) {
-            if (atomic) atomicAdd(reinterpret_cast<unsigned long long*>(d), (unsigned long long)t);
+            if (mode) atomicAdd(reinterpret_cast<unsigned long long*>(d), (unsigned long long)t);
             else *reinterpret_cast<long long*>(d) = t;
           }
         } else {
           const double t = seg_quad_sum(acc[I]);
           if (kq == 0 && col < pc) {
-            if (atomic) atomicAdd(d, t);
-            else *d = t;
+            if (mode == 0) *d = t;
+            else if (a.chain) a.chain[((int64_t)(mode - 1) * a.n_units + u) * pc + col] = t;  // k_seg_chain adds
+            else atomicAdd(d, t);
           }
         }
         acc[I] = 0.0;
@@ -247,7 +251,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
             }
           }
           if (r1 > ge) break;  // segment h continues in the next group
-          finalize(part);      // r1 <= ge <= hi: segment h ends in this unit
+          finalize(part ? 1 : 0);  // r1 <= ge <= hi: segment h ends in this unit
           part = false;
           do {  // next non-empty segment
             ++h;
@@ -264,8 +268,38 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
       }
     }
     // segment h continues past the unit: partial sum
-    if (!done && h < G && r0 < hi && r1 > hi) finalize(true);
+    if (!done && h < G && r0 < hi && r1 > hi) finalize(part ? 1 : 2);
   }
+}
+
+// f64 segmented sums in a fixed order: a segment cut by unit edges is its first part
+// (chain[1][u0], the unit it begins in) plus its part in every following unit (chain[0][u]),
+// added in unit order (f64 atomics would add three or more parts in any order).  One thread per
+// (unit, column) whose last segment continues into the next unit.
+__global__ void k_seg_chain(const int32_t* __restrict__ seg_off, const int32_t* __restrict__ ufirst, int32_t G,
+                            int n_units, int pc, const double* __restrict__ chain, double* __restrict__ T) {
+  const int32_t kept = seg_off[G];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)n_units * pc;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int u = (int)(e / pc), col = (int)(e % pc);
+    const int64_t nxt = (int64_t)(u + 1) * kSegUnit;  // first row of unit u + 1
+    if (u + 1 >= n_units || nxt >= kept) continue;
+    const int h = ufirst[u + 1];  // the segment holding row nxt
+    const int32_t s0 = seg_off[h];
+    if (s0 >= nxt || s0 < (int64_t)u * kSegUnit) continue;  // not cut at nxt, or begun before unit u
+    const int ue = (int)((seg_off[h + 1] - 1) / kSegUnit);
+    double t = chain[((int64_t)n_units + u) * pc + col];
+    for (int v = u + 1; v <= ue; ++v) t += chain[(int64_t)v * pc + col];
+    T[(int64_t)h * pc + col] = t;
+  }
+}
+
+int launch_seg_chain(lfe_ctx* c, const int32_t* seg_off, const int32_t* ufirst, int32_t G, int n_units, int pc,
+                     double* T) {
+  hipLaunchKernelGGL(k_seg_chain, dim3(grid_for((int64_t)n_units * pc)), dim3(kBlock), 0, c->stream, seg_off, ufirst,
+                     G, n_units, pc, c->chain, T);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
 }
 
 // column max |alpha| (u64 bits) of an effect table into out[0, p) (atomicMax; per block in LDS first)
@@ -486,6 +520,10 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
     LFE_HIP(hipGetLastError());
     a.xq = c->xq;
   }
+  if (!ex && a.n_units > 0) {  // f64 sums: cut segments' parts added in unit order (k_seg_chain)
+    LFE_TRY(ensure_f64(c, c->chain, c->chain_cap, (size_t)2 * a.n_units * pc));
+    a.chain = c->chain;
+  }
   if (a.n_units > 0) {
     const int nt = (pc + 15) / 16;
     CrossFn fn = cross_fn(nt, c->F - 1, wt);
@@ -495,6 +533,7 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kSegThreads), 0, c->stream, a);
   }
   LFE_HIP(hipGetLastError());
+  if (a.chain) LFE_TRY(launch_seg_chain(c, fe.seg_off, fe.ufirst, fe.G, a.n_units, pc, out));
   if (ex) {
     const int64_t m = (int64_t)fe.G * pc;
     hipLaunchKernelGGL(k_cross_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, out, m, pc, c->xq);
@@ -523,6 +562,8 @@ int seg_gather_sum(lfe_ctx* c, const int32_t* seg_off, int32_t G, int32_t* ufirs
   a.pc = cols;
   a.G = G;
   a.T = out;
+  LFE_TRY(ensure_f64(c, c->chain, c->chain_cap, (size_t)2 * n_units * cols));
+  a.chain = c->chain;
   CrossFn fn = cross_fn((cols + 15) / 16, 1, false);
   const int grid = (n_units + kSegThreads / 64 - 1) / (kSegThreads / 64);
   {
@@ -530,7 +571,7 @@ int seg_gather_sum(lfe_ctx* c, const int32_t* seg_off, int32_t G, int32_t* ufirs
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kSegThreads), 0, c->stream, a);
   }
   LFE_HIP(hipGetLastError());
-  return LFE_OK;
+  return launch_seg_chain(c, seg_off, ufirst, G, n_units, cols, out);
 }
 
 int seg_units_needed(int64_t n_pos) { return (int)std::max<int64_t>((n_pos + kSegUnit - 1) / kSegUnit, 1); }

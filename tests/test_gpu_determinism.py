@@ -162,3 +162,30 @@ def test_weighted_fits_are_bit_identical_and_keep_parity(L, skew):
     assert r.iterations == o["iterations"] and r.n_obs == o["n_obs"]
     np.testing.assert_allclose([r.coefs[x] for x in xs], o["beta"], rtol=1e-10, atol=0)
     np.testing.assert_allclose([r.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("case", ["long_clusters", "short_clusters_with_a_long_one"])
+def test_clustered_se_is_bit_identical(case):
+    """Cluster score sums add the parts of a cluster cut by work-unit / wave edges in a fixed
+    order (k_seg_chain, k_seg_rows_chain) instead of f64 atomics: one-way clusters of ~6700 rows
+    (seg_gather_sum, many units per cluster) and two-way CGM intersections of a few rows with
+    one 3000-row cluster spanning dozens of waves (k_seg_rows) repeat bit for bit and match the
+    oracle's clustered SE (std_errors.py:289-441) at 1e-10."""
+    from leanfe_amd import leanfe_hip, synth
+    from oracle import altproj
+    n, k = 400_000, 3
+    L = [8_000, 60, 700] if case == "long_clusters" else [8_000, 20_000, 9_000]
+    data = dict(synth.panel(n, k, L, seed=808))
+    cl = ["fe2"] if case == "long_clusters" else ["fe2", "fe3"]
+    if case != "long_clusters":  # one large intersection cluster
+        fe2, fe3 = np.array(data["fe2"], copy=True), np.array(data["fe3"], copy=True)
+        fe2[1000:4000], fe3[1000:4000] = 7, 11
+        data["fe2"], data["fe3"] = fe2, fe3
+    xs = [f"x{j + 1}" for j in range(k)]
+    runs = [leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=["fe1"], strategy="alt_proj", vcov="cluster",
+                       cluster_cols=cl, quiet=True, device=0) for _ in range(2)]
+    r0, r1 = runs
+    np.testing.assert_array_equal([r1.std_errors[x] for x in xs], [r0.std_errors[x] for x in xs])
+    np.testing.assert_array_equal([r1.coefs[x] for x in xs], [r0.coefs[x] for x in xs])
+    o = altproj.fit(data, "y", xs, ["fe1"], vcov="cluster", cluster_cols=cl)
+    np.testing.assert_allclose([r0.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
