@@ -630,6 +630,24 @@ __global__ void k_finish_counts(FinishCountsArgs a) {
   }
 }
 
+// multi-rank: the kept rows and (owner-sharded) the primary FE's level counts summed over ranks
+// on the device, so the host reads them with the other counts (no extra round trip)
+constexpr int kIsKept = 2 * kMaxFE + 2;  // iscratch: kept rows (lo, hi int32 halves), primary dims, card
+__global__ void k_kept_pack(const int32_t* __restrict__ is, int64_t n, int P, int owner, double* __restrict__ d) {
+  if (threadIdx.x != 0) return;
+  d[0] = (double)(n - is[2 * kMaxFE]);
+  d[1] = owner ? (double)is[2 * P] : 0.0;
+  d[2] = owner ? (double)is[2 * P + 1] : 0.0;
+}
+__global__ void k_kept_unpack(const double* __restrict__ d, int32_t* __restrict__ is) {
+  if (threadIdx.x != 0) return;
+  const int64_t k = (int64_t)d[0];
+  is[kIsKept] = (int32_t)(uint32_t)(k & 0xffffffffll);
+  is[kIsKept + 1] = (int32_t)(k >> 32);
+  is[kIsKept + 2] = (int32_t)d[1];
+  is[kIsKept + 3] = (int32_t)d[2];
+}
+
 // ---------------------------------------------------------------------------
 // driver
 // ---------------------------------------------------------------------------
@@ -950,6 +968,15 @@ int prepare_layout(lfe_ctx* c) {
       LFE_HIP(hipGetLastError());
     }
   }
+  if (c->world > 1) {
+    LFE_TRY(ensure_dred(c, 3));
+    hipLaunchKernelGGL(k_kept_pack, dim3(1), dim3(64), 0, c->stream, c->iscratch, n, L.P, c->owner_on ? 1 : 0,
+                       c->dred);
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(allreduce_sum_f64(c, c->dred, c->owner_on ? 3 : 1));
+    hipLaunchKernelGGL(k_kept_unpack, dim3(1), dim3(64), 0, c->stream, c->dred, c->iscratch);
+    LFE_HIP(hipGetLastError());
+  }
   int32_t h[2 * kMaxFE + 8];
   LFE_TRY(d2h_async(c, c->iscratch, sizeof(h)));
   // the constant group sums S_f do not depend on the FE order: enqueue them now so the
@@ -971,12 +998,10 @@ int prepare_layout(lfe_ctx* c) {
     kept[1] = c->fe[L.P].dims;
     kept[2] = c->fe[L.P].card;
   }
-  if (c->world > 1) {
-    const int nv = c->owner_on ? 3 : 1;
-    LFE_TRY(ensure_dred(c, 3));
-    LFE_TRY(h2d_small(c, c->dred, kept, sizeof(double) * nv));
-    LFE_TRY(allreduce_sum_f64(c, c->dred, nv));
-    LFE_TRY(d2h_sync(c, kept, c->dred, sizeof(double) * nv));
+  if (c->world > 1) {  // summed over ranks on the device (k_kept_pack / k_kept_unpack)
+    kept[0] = (double)(((int64_t)h[kIsKept + 1] << 32) | (int64_t)(uint32_t)h[kIsKept]);
+    kept[1] = h[kIsKept + 2];
+    kept[2] = h[kIsKept + 3];
   }
   if (c->owner_on) {
     c->fe[L.P].dims = (int32_t)kept[1];
