@@ -508,12 +508,13 @@ __global__ void k_fix_convert(double* __restrict__ S, int64_t m, int p, const do
 // S_Q = the blocks' tables summed in block order (int64 on the exact path, then scaled to
 // double; else f64): 16
 // consecutive entries x 16 block slices per workgroup, the slices added in order
-__global__ __launch_bounds__(256) void k_qpart_reduce(const double* __restrict__ part, int nblk, int64_t m,
-                                                      const double* __restrict__ fq, int p, double* __restrict__ S) {
+__device__ __forceinline__ void qpart_reduce_block(const double* __restrict__ part, int nblk, int64_t m,
+                                                   const double* __restrict__ fq, int p, double* __restrict__ S,
+                                                   int blk) {
   __shared__ double ps[16][16];
   __shared__ long long pi[16][16];
   const int ei = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int64_t e = (int64_t)blockIdx.x * 16 + ei;
+  const int64_t e = (int64_t)blk * 16 + ei;
   const bool fix = fix_on(fq, p);
   double t = 0.0;
   long long ti = 0;
@@ -536,6 +537,69 @@ __global__ __launch_bounds__(256) void k_qpart_reduce(const double* __restrict__
     for (int k = 0; k < 16; ++k) r += ps[k][ei];
     S[e] = r;
   }
+}
+
+__global__ __launch_bounds__(256) void k_qpart_reduce(const double* __restrict__ part, int nblk, int64_t m,
+                                                      const double* __restrict__ fq, int p, double* __restrict__ S) {
+  qpart_reduce_block(part, nblk, m, fq, p, S, blockIdx.x);
+}
+
+// the two-FE sums' epilogue in one launch (four independent pieces, by block range): S_Q from the
+// blocks' tables (k_qpart_reduce), S_P's int64 -> double (k_fix_convert), the raw Gram tiles
+// summed in block order (k_reduce_partials) and the raw shift (k_raw_shift)
+struct Sums2Epi {
+  const double* qpart;
+  int nblk;
+  int64_t mq;
+  const double* fq;
+  int p;
+  double* SQ;
+  int nbq;
+  double* SP;
+  int64_t mp;
+  int nbp;
+  int exact;
+  const double* raw_part;
+  double* raw_tile;
+  const double* X;
+  int64_t ld;
+  int has_rows, rank;
+  double* raw_shift;
+};
+__global__ __launch_bounds__(256) void k_sums2_epilogue(Sums2Epi a) {
+  int b = blockIdx.x;
+  if (b < a.nbq) {
+    qpart_reduce_block(a.qpart, a.nblk, a.mq, a.fq, a.p, a.SQ, b);
+    return;
+  }
+  b -= a.nbq;
+  if (b < a.nbp) {
+    if (!a.exact || !fix_on(a.fq, a.p)) return;
+    for (int64_t e = (int64_t)b * 256 + threadIdx.x; e < a.mp; e += (int64_t)a.nbp * 256) {
+      const long long v = reinterpret_cast<const long long*>(a.SP)[e];
+      a.SP[e] = (double)v * a.fq[kMaxCols + (int)(e % a.p)];
+    }
+    return;
+  }
+  b -= a.nbp;
+  if (b < 256) {  // entry b of the raw tile: fixed-order tree over the blocks
+    __shared__ double red[256];
+    double t = 0.0;
+    for (int k = threadIdx.x; k < a.nblk; k += 256) t += a.raw_part[(int64_t)k * 256 + b];
+    red[threadIdx.x] = t;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) a.raw_tile[b] = red[0];
+    return;
+  }
+  const int j = threadIdx.x;  // the raw shift (k_raw_shift)
+  if (j >= 16) return;
+  const double own = (j < a.p && a.has_rows) ? a.X[(int64_t)j * a.ld] : 0.0;
+  a.raw_shift[16 + j] = own;
+  a.raw_shift[j] = a.rank == 0 ? own : 0.0;
 }
 
 // raw_shift[16 + j] = this rank's shift (first layout row; 0 for an empty shard);
@@ -695,23 +759,41 @@ int sums4(lfe_ctx* c) {
     LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, lds, c->stream));
   }
   LFE_HIP(hipGetLastError());
-  if (two) {
+  if (two) {  // two implies raw: one epilogue launch
     ProfScope _ps(c, K_FIX_SUMS);
-    const int64_t m = (int64_t)c->fe[a.qf[0]].G * p;
-    hipLaunchKernelGGL(k_qpart_reduce, dim3((unsigned)((m + 15) / 16)), dim3(256), 0, c->stream, c->qpart, nblocks, m,
-                       c->fixq, p, c->fe[a.qf[0]].S);
+    LFE_TRY(ensure_f64(c, c->raw_shift, c->raw_shift_cap, 32));
+    Sums2Epi e{};
+    e.qpart = c->qpart;
+    e.nblk = nblocks;
+    e.mq = (int64_t)c->fe[a.qf[0]].G * p;
+    e.fq = c->fixq;
+    e.p = p;
+    e.SQ = c->fe[a.qf[0]].S;
+    e.nbq = (int)((e.mq + 15) / 16);
+    e.SP = c->fe[P].S;
+    e.mp = (int64_t)c->fe[P].G * p;
+    e.nbp = grid_for(e.mp);
+    e.exact = exact ? 1 : 0;
+    e.raw_part = c->raw_part;
+    e.raw_tile = c->raw_tile;
+    e.X = c->L.X;
+    e.ld = c->ld;
+    e.has_rows = c->L.n_items > 0 ? 1 : 0;
+    e.rank = c->rank;
+    e.raw_shift = c->raw_shift;
+    hipLaunchKernelGGL(k_sums2_epilogue, dim3((unsigned)(e.nbq + e.nbp + 256 + 1)), dim3(256), 0, c->stream, e);
     LFE_HIP(hipGetLastError());
+    c->raw_ready = true;
   }
-  if (exact) {
+  if (exact && !two) {
     ProfScope _ps(c, K_FIX_SUMS);
     for (int f = 0; f < c->F; ++f) {
-      if (two && f == a.qf[0]) continue;  // converted by k_qpart_reduce
       const int64_t m = (int64_t)c->fe[f].G * p;
       hipLaunchKernelGGL(k_fix_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, c->fe[f].S, m, p, c->fixq);
     }
     LFE_HIP(hipGetLastError());
   }
-  if (raw) {
+  if (raw && !two) {
     reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
     LFE_TRY(ensure_f64(c, c->raw_shift, c->raw_shift_cap, 32));
     hipLaunchKernelGGL(k_raw_shift, dim3(1), dim3(64), 0, c->stream, c->L.X, c->ld, p, c->L.n_items > 0 ? 1 : 0,

@@ -79,29 +79,43 @@ __global__ __launch_bounds__(256) void k_ls_hist2(const int4* __restrict__ items
 }
 
 // per (bucket, key): exclusive scan over the bucket's items -> item bases; total -> off[b K + key]
+__device__ __forceinline__ void ls_base_one(const int32_t* __restrict__ bitems, int nb, int K,
+                                            int32_t* __restrict__ itemcnt, int32_t* __restrict__ off, int64_t e) {
+  if (e == (int64_t)nb * K) {  // the scan's trailing element (the total after the exclusive scan)
+    off[e] = 0;
+    return;
+  }
+  const int b = (int)(e / K), j = (int)(e % K);
+  int32_t run = 0;
+  // eight items' counts loaded before any is rewritten (the chain is latency-bound otherwise)
+  for (int i = bitems[b], i1 = bitems[b + 1]; i < i1; i += 8) {
+    int32_t t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = i + u < i1 ? itemcnt[(int64_t)(i + u) * K + j] : 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i + u < i1) {
+        itemcnt[(int64_t)(i + u) * K + j] = run;
+        run += t[u];
+      }
+  }
+  off[e] = run;
+}
+
 __global__ void k_ls_base(const int32_t* __restrict__ bitems, int nb, int K, int32_t* __restrict__ itemcnt,
                           int32_t* __restrict__ off) {
   const int64_t total = (int64_t)nb * K;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e <= total; e += (int64_t)gridDim.x * blockDim.x) {
-    if (e == total) {  // the scan's trailing element (the total after the exclusive scan)
-      off[e] = 0;
-      continue;
-    }
-    const int b = (int)(e / K), j = (int)(e % K);
-    int32_t run = 0;
-    // eight items' counts loaded before any is rewritten (the chain is latency-bound otherwise)
-    for (int i = bitems[b], i1 = bitems[b + 1]; i < i1; i += 8) {
-      int32_t t[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = i + u < i1 ? itemcnt[(int64_t)(i + u) * K + j] : 0;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (i + u < i1) {
-          itemcnt[(int64_t)(i + u) * K + j] = run;
-          run += t[u];
-        }
-    }
-    off[e] = run;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e <= total; e += (int64_t)gridDim.x * blockDim.x)
+    ls_base_one(bitems, nb, K, itemcnt, off, e);
+}
+
+// both layouts' item bases and key totals in one launch (the fused sort)
+__global__ void k_ls_base2(const int32_t* __restrict__ bitems, int nb, int K1, int32_t* __restrict__ cnt1,
+                           int32_t* __restrict__ off1, int K2, int32_t* __restrict__ cnt2, int32_t* __restrict__ off2) {
+  const int64_t t1 = (int64_t)nb * K1 + 1, t2 = (int64_t)nb * K2 + 1;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < t1 + t2; e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < t1) ls_base_one(bitems, nb, K1, cnt1, off1, e);
+    else ls_base_one(bitems, nb, K2, cnt2, off2, e - t1);
   }
 }
 
@@ -537,9 +551,17 @@ static int build_layouts(lfe_ctx* c, int Q) {
   const int per = ls_per();
   const size_t lds2 = ls2_lds(B, G_Q, per);
   if (lds2 <= 150 * 1024) {
-    LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, nullptr)));
-    LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, nullptr)));
-    LFE_TRY(exclusive_scan2(c, c->seg_off, (int64_t)L.nb * B + 1, c->run_off, (int64_t)L.nb * G_Q + 1));
+    // both layouts' item bases and key totals, then one scan of both
+    const size_t m1 = (size_t)L.nb * B, m2 = (size_t)L.nb * G_Q;
+    LFE_TRY(ensure_i32(c, c->seg_off, c->seg_off_cap, m1 + 1));
+    LFE_TRY(ensure_i32(c, c->run_off, c->run_off_cap, m2 + 1));
+    {
+      ProfScope _ps(c, K_LAYOUT_BASE);
+      hipLaunchKernelGGL(k_ls_base2, dim3(grid_for((int64_t)(m1 + m2 + 2))), dim3(kBlock), 0, c->stream, c->bitems_d,
+                         L.nb, B, c->seg_aux, c->seg_off, (int)G_Q, c->seg_aux + n1, c->run_off);
+    }
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(exclusive_scan2(c, c->seg_off, (int64_t)m1 + 1, c->run_off, (int64_t)m2 + 1));
     Ls2Args a{};
     a.items = reinterpret_cast<const int4*>(c->items_d);
     a.codeP = L.code[L.P];

@@ -179,7 +179,40 @@ __global__ __launch_bounds__(256) void k_scan_add(ScanPair sp, const int32_t* __
     if (base + k < m) a[base + k] += add;
 }
 
-int exclusive_scan2(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2) {
+__global__ void k_gather_bstart(const int32_t* __restrict__ scanned, int nb, int nw, int32_t* __restrict__ out) {
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x)
+    out[b] = scanned[(int64_t)b * nw];
+}
+
+// k_scan_add for few blocks (<= kScanFewBlocks): every block forms its own offset, the sum of the
+// block sums before it in its array (integer adds: any order), so k_scan_top's launch goes.
+// gather: out[b] = a1[b * gstride] for b < gn after the add (the partition's bucket starts).
+constexpr int kScanFewBlocks = 2048;
+__global__ __launch_bounds__(256) void k_scan_add_few(ScanPair sp, const int32_t* __restrict__ sums,
+                                                      int32_t* __restrict__ gout, int64_t gstride, int gn) {
+  __shared__ int32_t ws[4];
+  int64_t blk = blockIdx.x, m;
+  const int64_t first = blk < sp.nb1 ? 0 : sp.nb1;  // this array's first block
+  int32_t* __restrict__ a = sp.arr(blk, m);
+  int32_t part = 0;
+  for (int64_t j = first + threadIdx.x; j < (int64_t)blockIdx.x; j += 256) part += sums[j];
+  for (int off = 32; off > 0; off >>= 1) part += __shfl_down(part, off, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = part;
+  __syncthreads();
+  const int32_t add = (ws[0] + ws[1]) + (ws[2] + ws[3]);
+  const int64_t base = blk * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+  const bool g = gout != nullptr && blockIdx.x < sp.nb1;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k)
+    if (base + k < m) {
+      const int32_t v = a[base + k] + add;
+      a[base + k] = v;
+      if (g && (base + k) % gstride == 0 && (base + k) / gstride < gn) gout[(base + k) / gstride] = v;
+    }
+}
+
+static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2, int32_t* gout,
+                            int64_t gstride, int gn) {
   const int64_t nb1 = (m1 + kScanBlock - 1) / kScanBlock, nb2 = a2 ? (m2 + kScanBlock - 1) / kScanBlock : 0;
   const int64_t nblocks = nb1 + nb2;
   if (nblocks == 0) return LFE_OK;
@@ -187,10 +220,21 @@ int exclusive_scan2(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2
   const ScanPair sp{a1, m1, nb1, a2, m2};
   ProfScope _ps(c, K_SCAN);
   hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, c->psums, (int)nb1, (int)nb2);
-  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums);
+  if (nblocks <= kScanFewBlocks) {
+    hipLaunchKernelGGL(k_scan_add_few, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums, gout, gstride,
+                       gn);
+  } else {
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, c->psums, (int)nb1, (int)nb2);
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums);
+    if (gout) hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(gn)), dim3(kBlock), 0, c->stream, a1, gn,
+                                 (int)gstride, gout);
+  }
   LFE_HIP(hipGetLastError());
   return LFE_OK;
+}
+
+int exclusive_scan2(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2) {
+  return exclusive_scan_g(c, a1, m1, a2, m2, nullptr, 1, 0);
 }
 
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) { return exclusive_scan2(c, a, m, nullptr, 0); }
@@ -497,10 +541,6 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   }
 }
 
-__global__ void k_gather_bstart(const int32_t* __restrict__ scanned, int nb, int nw, int32_t* __restrict__ out) {
-  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x)
-    out[b] = scanned[(int64_t)b * nw];
-}
 
 // ---------------------------------------------------------------------------
 // counts on the layout + singleton marks
@@ -508,27 +548,30 @@ __global__ void k_gather_bstart(const int32_t* __restrict__ scanned, int nb, int
 
 // pre-filter counts from the per-item histograms of the two-FE layouts: primary group h sums
 // its bucket's items (cnt1[item][h - lo]); secondary level q sums a 1/256 slice of all items
-__global__ void k_cnt_from_items_p(const int32_t* __restrict__ cnt1, const int32_t* __restrict__ bitems, int s,
-                                   int32_t G, int32_t* __restrict__ cnt) {
-  const int B = 1 << s;
-  for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < G; h += gridDim.x * blockDim.x) {
+// both in one launch: blocks [0, nbp) the primary FE (one group per thread), then the secondary
+// levels in 256 item slices (block nbp + y * nqx + x: levels 256 x.., slice y)
+__global__ void k_cnt_from_items(const int32_t* __restrict__ cnt1, const int32_t* __restrict__ cnt2,
+                                 const int32_t* __restrict__ bitems, int s, int32_t G_P, int32_t* __restrict__ cntP,
+                                 int n_items, int32_t G_Q, int32_t* __restrict__ cntQ, int nbp, int nqx) {
+  if ((int)blockIdx.x < nbp) {
+    const int B = 1 << s;
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= G_P) return;
     const int b = h >> s, j = h & (B - 1);
     int32_t t = 0;
 #pragma unroll 4
     for (int i = bitems[b]; i < bitems[b + 1]; ++i) t += cnt1[(int64_t)i * B + j];
-    cnt[h] = t;
+    cntP[h] = t;
+    return;
   }
-}
-
-__global__ void k_cnt_from_items_q(const int32_t* __restrict__ cnt2, int n_items, int32_t G,
-                                   int32_t* __restrict__ cnt) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= G) return;
-  const int i0 = (int)((int64_t)blockIdx.y * n_items / gridDim.y), i1 = (int)((int64_t)(blockIdx.y + 1) * n_items / gridDim.y);
+  const int lin = blockIdx.x - nbp, x = lin % nqx, y = lin / nqx;
+  const int q = x * blockDim.x + threadIdx.x;
+  if (q >= G_Q) return;
+  const int i0 = (int)((int64_t)y * n_items / 256), i1 = (int)((int64_t)(y + 1) * n_items / 256);
   int32_t t = 0;
 #pragma unroll 4
-  for (int i = i0; i < i1; ++i) t += cnt2[(int64_t)i * G + q];
-  if (t) atomicAdd(&cnt[q], t);
+  for (int i = i0; i < i1; ++i) t += cnt2[(int64_t)i * G_Q + q];
+  if (t) atomicAdd(&cntQ[q], t);
 }
 
 // primary-FE counts: per work item an LDS slice of 2^s bins
@@ -860,12 +903,10 @@ int prepare_layout(lfe_ctx* c) {
                          nb, cw, nw, c->pcounts);
     }
     LFE_HIP(hipGetLastError());
-    LFE_TRY(exclusive_scan(c, c->pcounts, m));
-    // bucket starts depend on the scan only: fetch them now and build the work items
-    // on the host while the GPU runs the scatter
+    // bucket starts depend on the scan only (gathered by its last kernel): fetch them now and
+    // build the work items on the host while the GPU runs the scatter
     int32_t* dbstart = c->pcounts + m;
-    hipLaunchKernelGGL(k_gather_bstart, dim3(grid_for(nb)), dim3(kBlock), 0, c->stream, c->pcounts, nb, nw, dbstart);
-    LFE_HIP(hipGetLastError());
+    LFE_TRY(exclusive_scan_g(c, c->pcounts, m, nullptr, 0, dbstart, nw, nb));
     LFE_TRY(d2h_async(c, dbstart, sizeof(int32_t) * nb));
     const size_t lds = std::min<size_t>(std::max(part_lds(nth), kLdsMin), 160 * 1024);
     L.part = PartGeom{nth, per, nw, lds};
@@ -900,10 +941,9 @@ int prepare_layout(lfe_ctx* c) {
     ProfScope _ps(c, K_COUNT);
     const int32_t* c1 = c->seg_aux;
     const int32_t* c2 = c->seg_aux + (size_t)L.n_items * B;
-    hipLaunchKernelGGL(k_cnt_from_items_p, dim3(grid_for(c->fe[L.P].G)), dim3(kBlock), 0, c->stream, c1, c->bitems_d,
-                       L.s, c->fe[L.P].G, c->fe[L.P].cnt_pre);
-    hipLaunchKernelGGL(k_cnt_from_items_q, dim3((c->fe[Q].G + 255) / 256, 256), dim3(256), 0, c->stream, c2,
-                       L.n_items, c->fe[Q].G, c->fe[Q].cnt_pre);
+    const int nbp = (c->fe[L.P].G + 255) / 256, nqx = (c->fe[Q].G + 255) / 256;
+    hipLaunchKernelGGL(k_cnt_from_items, dim3(nbp + nqx * 256), dim3(256), 0, c->stream, c1, c2, c->bitems_d, L.s,
+                       c->fe[L.P].G, c->fe[L.P].cnt_pre, L.n_items, c->fe[Q].G, c->fe[Q].cnt_pre, nbp, nqx);
     LFE_HIP(hipGetLastError());
   } else if (L.permuted) {
     ProfScope _ps(c, K_COUNT);
