@@ -1007,6 +1007,48 @@ __global__ __launch_bounds__(256) void k_tq_reduce(const double* __restrict__ ru
   }
 }
 
+// one rank: k_tq_reduce and the next Q projection (k_fin_check) in one launch.  T_Q[e] is summed
+// as k_tq_reduce sums it, then alpha_new[e] = (S_Q[e] - T_Q[e]) / n and, on column 0, the stop
+// test |alpha_new - alpha_cur| (NaN propagates); wave 0 holds the block's 16 writers.
+__global__ __launch_bounds__(256) void k_tq_reduce_fin(const double* __restrict__ runs, int nb, int64_t m,
+                                                       double* __restrict__ T, const double* __restrict__ S,
+                                                       const int32_t* __restrict__ cnt, int p,
+                                                       const double* __restrict__ cur, double* __restrict__ out,
+                                                       unsigned long long* __restrict__ check) {
+  __shared__ double part[kTqRedS][kTqRedE];
+  const int ei = threadIdx.x % kTqRedE, sl = threadIdx.x / kTqRedE;
+  const int64_t e = (int64_t)blockIdx.x * kTqRedE + ei;
+  double t = 0.0;
+  if (e < m) {
+    int b = sl;
+    for (; b + 3 * kTqRedS < nb; b += 4 * kTqRedS) {
+      const double v0 = runs[(int64_t)b * m + e], v1 = runs[(int64_t)(b + kTqRedS) * m + e];
+      const double v2 = runs[(int64_t)(b + 2 * kTqRedS) * m + e], v3 = runs[(int64_t)(b + 3 * kTqRedS) * m + e];
+      t = (((t + v0) + v1) + v2) + v3;
+    }
+    for (; b < nb; b += kTqRedS) t += runs[(int64_t)b * m + e];
+  }
+  part[sl][ei] = t;
+  __syncthreads();
+  double mx = 0.0;
+  if (sl == 0 && e < m) {
+    double r = part[0][ei];
+    for (int k = 1; k < kTqRedS; ++k) r += part[k][ei];
+    T[e] = r;
+    const int32_t n = cnt[e / p];
+    const double v = n > 0 ? (S[e] - r) / (double)n : 0.0;
+    out[e] = v;
+    if (check && n > 0 && e % p == 0) mx = fabs(v - cur[e]);
+  }
+  if (check && threadIdx.x < 64) {
+    for (int off = 32; off > 0; off >>= 1) {
+      const double o = __shfl_down(mx, off, 64);
+      mx = (isnan(o) || isnan(mx)) ? __builtin_nan("") : fmax(mx, o);
+    }
+    if (threadIdx.x == 0) atomicMax(check, (unsigned long long)__double_as_longlong(fabs(mx)));
+  }
+}
+
 // alpha_new = (S - T) / cnt; check = max_g |alpha_new[g][0] - alpha_cur[g][0]| over groups present
 // (= |mean_g(y~)| after the sweep); NaN propagates (a NaN panel never converges).
 __global__ void k_fin_check(const double* __restrict__ S, const double* __restrict__ T,
@@ -1152,18 +1194,30 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       }
     }
     LFE_HIP(hipGetLastError());
-    {
-      ProfScope _ps(c, K_TQ_REDUCE);
-      const int64_t m = (int64_t)fq.G * p;
-      hipLaunchKernelGGL(k_tq_reduce, dim3((unsigned)((m + kTqRedE - 1) / kTqRedE)), dim3(kTqRedE * kTqRedS), 0,
-                         c->stream, c->tq_runs, c->L.nb, m, fq.T);
-    }
-    LFE_HIP(hipGetLastError());
-    LFE_TRY(allreduce_sum_f64(c, fq.T, (size_t)fq.G * p));
     iterations = it;
     const bool check = it >= check_from;
-    if (!check && it == max_iter) break;
-    LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check));
+    const int64_t m = (int64_t)fq.G * p;
+    const unsigned tq_grid = (unsigned)((m + kTqRedE - 1) / kTqRedE);
+    if (c->world == 1) {  // T_Q and the next Q projection in one launch
+      {
+        ProfScope _ps(c, K_TQ_REDUCE);
+        hipLaunchKernelGGL(k_tq_reduce_fin, dim3(tq_grid), dim3(kTqRedE * kTqRedS), 0, c->stream, c->tq_runs,
+                           c->L.nb, m, fq.T, fq.S, fq.cnt, p, fq.alpha, c->alpha_spare,
+                           check ? reinterpret_cast<unsigned long long*>(c->dred) : nullptr);
+      }
+      LFE_HIP(hipGetLastError());
+      if (!check && it == max_iter) break;
+    } else {
+      {
+        ProfScope _ps(c, K_TQ_REDUCE);
+        hipLaunchKernelGGL(k_tq_reduce, dim3(tq_grid), dim3(kTqRedE * kTqRedS), 0, c->stream, c->tq_runs, c->L.nb,
+                           m, fq.T);
+      }
+      LFE_HIP(hipGetLastError());
+      LFE_TRY(allreduce_sum_f64(c, fq.T, (size_t)fq.G * p));
+      if (!check && it == max_iter) break;
+      LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check));
+    }
     if (check) {
       // the check's read-back first, then - when this check is likely the last (the first one,
       // or the previous was within 100x of tol: the check falls ~100x per sweep) - the Gram of
