@@ -100,10 +100,13 @@ class HostGroup:
         if self.world > 1:
             import torch.distributed as dist
 
-            if backend == "gloo" and os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
-                # every rank on this node: gloo's pairs over loopback, not over whatever
-                # interface the container's hostname may (not) resolve to
-                os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+            if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
+                # every rank on this node: gloo's pairs and RCCL's bootstrap (the engine's
+                # communicator; its data moves over xGMI peer links) over loopback, not over
+                # whatever interface the container's hostname may (not) resolve to
+                if backend == "gloo":
+                    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+                os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
             if not dist.is_initialized():
                 dist.init_process_group(backend)
             self.dist = dist

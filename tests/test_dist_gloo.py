@@ -104,7 +104,8 @@ def _plumbing(rank):
     eng = _FakeEngine()
     attach(eng)
     uid, r, w = eng.calls[-1]
-    return dict(max=mx, sum=sm, bytes=b, uid=uid, rank=r, world=w)
+    import os
+    return dict(max=mx, sum=sm, bytes=b, uid=uid, rank=r, world=w, ifname=os.environ.get("NCCL_SOCKET_IFNAME"))
 
 
 def test_hostgroup_and_attach_gloo():
@@ -115,6 +116,7 @@ def test_hostgroup_and_attach_gloo():
     assert out[0]["uid"] == out[1]["uid"] and len(out[0]["uid"]) == 128  # same RCCL id on every rank
     assert [out[r]["rank"] for r in range(WORLD)] == [0, 1]
     assert out[0]["world"] == out[1]["world"] == WORLD
+    assert out[0]["ifname"] == out[1]["ifname"] == "lo"  # single node: RCCL bootstrap over loopback
 
 
 # ---------------------------------------------------------------------------
