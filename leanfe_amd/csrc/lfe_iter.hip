@@ -588,8 +588,11 @@ static int build_layouts(lfe_ctx* c, int Q) {
     LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, c->seg_q)));
     LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, c->run_h)));
   }
-  // work units of ~2048 kept rows (whole segments) for K1
-  const int64_t U = 2048;  // (shrinking it for short shards - 4 units per K1 wave - measured slower)
+  // work units of ~2048 kept rows (whole segments) for K1; 512 when 2048-row units would leave
+  // K1's waves idle (n < 2048 per wave).  Same-box A/B, ms per solve for K1: 1M rows (config 1)
+  // 0.339 -> 0.112; 6.25M 0.099 -> 0.097; at 50M 2048 stays best (0.478 vs 0.523 for 512).
+  const int64_t waves = (int64_t)c->n_cu * 16;  // K1: one 1024-thread workgroup per CU
+  const int64_t U = c->n >= 2048 * waves ? 2048 : 512;
   const int32_t H = L.nb * B;
   c->n_units = (int)std::max<int64_t>(1, (c->n + U - 1) / U);
   LFE_TRY(ensure_i32(c, c->seg_units, c->seg_units_cap, (size_t)c->n_units + 1));
