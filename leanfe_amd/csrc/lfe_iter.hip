@@ -1157,9 +1157,11 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   // tail: 196 buckets -> 5 per bucket (tq 0.61 -> 0.49 ms per step at 50M rows, measured)
   tq.split = std::max(kTqSplitDefault / 2, (int)std::lround(4.0 * c->n_cu / std::max(c->L.nb, 1)));
   {  // every workgroup stages its bucket's 45 KB alpha_P slice: >= 16K rows per workgroup (6.25M
-     // rows over 25 buckets: 0.126 -> 0.113 ms per 3 sweeps; 48K rows per workgroup 0.142 ms)
+     // rows over 25 buckets: 0.126 -> 0.113 ms per 3 sweeps; 48K rows per workgroup 0.142 ms);
+     // a narrower slice (p < 11) pays for proportionally fewer rows
     const int64_t per_bucket = c->n_kept / std::max(c->L.nb, 1);
-    tq.split = (int)std::max<int64_t>(1, std::min<int64_t>(tq.split, per_bucket / 16384));
+    const int64_t min_rows = std::max<int64_t>(2048, (int64_t)16384 * p / 11);
+    tq.split = (int)std::max<int64_t>(1, std::min<int64_t>(tq.split, per_bucket / min_rows));
   }
   // sweep 1's Q projection: alpha_P = 0 -> alpha_Q = S_Q / n_Q (alpha_P is first written by K1,
   // which covers every primary group)
