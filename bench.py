@@ -385,6 +385,14 @@ def main(argv=None):
         roofline["step"] = {"bytes": int(step_bytes), "achieved": round(ach, 1), "frac": round(ach / PEAK_HBM_GBS, 4),
                             "kernel_ms": round(kern_ms, 4), "host_gap_ms": round(ms_step - kern_ms, 4),
                             "model": "sum over kernels of DESIGN.md §4 bytes/row x rows x launches per step"}
+        # the traffic no design can avoid: X and the codes read once for the group sums (+ Gram), and
+        # once more for the residual pass unless the SE come from the Gram (IID)
+        passes = 1 if a.vcov.lower() == "iid" else 2
+        cb = passes * geo["local"] * (8 * p + 4 * F)
+        cach = cb / (ms_step / 1e3) / 1e9
+        roofline["step"]["compulsory"] = {"bytes": int(cb), "achieved": round(cach, 1),
+                                          "frac": round(cach / PEAK_HBM_GBS, 4),
+                                          "model": f"{passes} pass(es) over X (8p B/row) + codes (4F B/row)"}
 
     extra = {}
     if d.rank == 0 and d.world == 1 and (not a.no_cpu or not a.no_h2d):

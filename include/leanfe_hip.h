@@ -94,6 +94,18 @@ int lfe_synth_load(lfe_ctx* ctx, int64_t n, int k, int n_fe, const int32_t* n_le
  * Gram and the SE statistics.  fe = -1 clears it; every lfe_load* clears it. */
 int lfe_ctx_set_owner(lfe_ctx* ctx, int fe, int32_t lo, int32_t hi);
 
+/* Owner re-shard (multi-GPU, after every rank loaded a contiguous block of rows with lfe_load):
+ * rows move between the ranks so that rank r holds every row whose code of FE `fe` lies in
+ * [lo_r, hi_r), the ranges cut where the running count of rows over the all-reduced level counts
+ * crosses r N / world (equal rows per rank up to one level's rows).  X, the weights, every FE's
+ * codes and the loaded cluster columns move (one grouped ncclSend / ncclRecv set per column);
+ * on the receiving rank rows are ordered by (source rank, source row).  Then
+ * lfe_ctx_set_owner(ctx, fe, lo_r, hi_r); *lo_out / *hi_out receive this rank's range.  Every
+ * rank must call it (collective).  LFE_EINVAL (nothing moved) when a rank would hold no rows.
+ * Replaces the caller-side routing by owner and the level-balanced ranges
+ * of dist.owner_range. */
+int lfe_reshard_owner(lfe_ctx* ctx, int fe, int32_t* lo_out, int32_t* hi_out);
+
 /* The rows of the synthetic panel's rows [0, n_total) whose code of FE `owner_fe` lies in
  * [lo, hi), generated on the device in increasing row order (the same rows and values as
  * lfe_synth_load over the whole panel), then lfe_ctx_set_owner(ctx, owner_fe, lo, hi). */
@@ -272,6 +284,9 @@ int lfe_kernel_stats(lfe_ctx* ctx, int max, char* names, double* total_ms, int64
 
 const char* lfe_last_error(void);
 const char* lfe_version(void);
+/* Hash of the engine sources this library was built from (leanfe_amd/build.py source_hash();
+ * the Python loader refuses a library whose hash differs from the checked-out sources). */
+const char* lfe_build_hash(void);
 
 #ifdef __cplusplus
 }

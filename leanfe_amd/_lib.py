@@ -42,6 +42,7 @@ SIGNATURES = {
     "lfe_load_finish": (C.c_int, [_vp]),
     "lfe_synth_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, _dp, C.c_uint64, C.c_int64]),
     "lfe_ctx_set_owner": (C.c_int, [_vp, C.c_int, C.c_int32, C.c_int32]),
+    "lfe_reshard_owner": (C.c_int, [_vp, C.c_int, _i32p, _i32p]),
     "lfe_synth_load_owned": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, _dp, C.c_uint64, C.c_int,
                                        C.c_int32, C.c_int32]),
     "lfe_load_clusters": (C.c_int, [_vp, C.c_int, C.POINTER(_vp), _i32p, C.c_int]),
@@ -73,6 +74,7 @@ SIGNATURES = {
     "lfe_kernel_stats": (C.c_int, [_vp, C.c_int, C.c_char_p, _dp, _i64p, _i32p]),
     "lfe_last_error": (C.c_char_p, []),
     "lfe_version": (C.c_char_p, []),
+    "lfe_build_hash": (C.c_char_p, []),
 }
 
 _lock = threading.Lock()
@@ -89,6 +91,14 @@ def load_library(path: str | None = None) -> C.CDLL:
         if not os.path.exists(p):
             raise ImportError(
                 f"leanfe_amd HIP engine not found at {p}; build it with `python -m leanfe_amd.build`")
+        if path is None and os.environ.get("LFE_ALLOW_STALE") != "1":
+            # the library must be built from the sources checked out beside it (build.py stamps
+            # their hash into it): a stale build never runs silently
+            from .build import library_hash, source_hash
+            have, want = library_hash(p), source_hash()
+            if have != want:
+                raise ImportError(f"{p} was built from other sources (library {have}, sources {want}); "
+                                  "rebuild it with `python -m leanfe_amd.build`")
         lib = C.CDLL(p)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
@@ -128,6 +138,7 @@ class Engine:
         self.p = 0
         self.F = 0
         self.n = 0  # rows of the loaded shard
+        self.owner = None  # (fe, lo, hi) of owner-sharded rows (set_owner / reshard_owner)
         self._keep = []  # host arrays that must outlive async copies
 
     # -- lifecycle ---------------------------------------------------------
@@ -183,12 +194,14 @@ class Engine:
         _check(self._lib.lfe_load(self._h, n, len(cols), cp, len(codes), kp, lv,
                                   None if w is None else _ptr(w), LFE_HOST))
         self.p, self.F, self.n = len(cols), len(codes), n
+        self.owner = None
 
     # -- chunked upload (streaming ingest) --------------------------------
     def load_begin(self, n: int, p: int, levels: list[int], weighted: bool = False) -> None:
         lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
         _check(self._lib.lfe_load_begin(self._h, int(n), int(p), len(levels), lv, 1 if weighted else 0))
         self.p, self.F, self.n = int(p), len(levels), int(n)
+        self.owner = None
         self._inflight = []
 
     def load_rows(self, row0: int, cols: list[np.ndarray], codes: list[np.ndarray],
@@ -219,6 +232,7 @@ class Engine:
         _check(self._lib.lfe_synth_load(self._h, int(n), int(k), len(levels), lv,
                                         b.ctypes.data_as(_dp), C.c_uint64(seed), int(row_offset)))
         self.p, self.F, self.n = k + 1, len(levels), int(n)
+        self.owner = None
 
     def synth_load_owned(self, n_total: int, k: int, levels: list[int], beta: np.ndarray, owner_fe: int, lo: int,
                          hi: int, seed: int = 12345) -> None:
@@ -241,6 +255,16 @@ class Engine:
         (lfe_ctx_set_owner; None clears it)."""
         _check(self._lib.lfe_ctx_set_owner(self._h, -1 if fe is None else int(fe), int(lo), int(hi)))
         self.owner = None if fe is None else (int(fe), int(lo), int(hi))
+
+    def reshard_owner(self, fe: int) -> tuple[int, int]:
+        """Collective: move the loaded rows between the ranks so that this rank holds every row
+        whose code of FE ``fe`` lies in the returned level range (balanced by rows), and declare
+        owner sharding for it (lfe_reshard_owner)."""
+        lo, hi = C.c_int32(), C.c_int32()
+        _check(self._lib.lfe_reshard_owner(self._h, int(fe), C.byref(lo), C.byref(hi)))
+        self.n = self._shard_rows()
+        self.owner = (int(fe), int(lo.value), int(hi.value))
+        return int(lo.value), int(hi.value)
 
     def _shard_rows(self) -> int:
         n = C.c_int64()
@@ -414,6 +438,7 @@ class Engine:
         lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
         _check(self._lib.lfe_load_codes(self._h, n, int(p), len(codes), kp, lv, LFE_HOST))
         self.p, self.F, self.n = int(p), len(codes), n
+        self.owner = None
 
     def stream_begin(self, pass_: int, beta_full: np.ndarray | None = None) -> None:
         b = None if beta_full is None else np.ascontiguousarray(beta_full, dtype=np.float64)
@@ -437,6 +462,7 @@ class Engine:
         lv = (C.c_int32 * len(levels))(*[int(g) for g in levels])
         _check(self._lib.lfe_synth_load_codes(self._h, int(n), int(k), len(levels), lv, C.c_uint64(seed)))
         self.p, self.F, self.n = int(k) + 1, len(levels), int(n)
+        self.owner = None
 
     def stream_synth_pass(self, pass_: int, k: int, levels: list[int], beta: np.ndarray, chunk_rows: int,
                           seed: int = 12345, beta_full: np.ndarray | None = None) -> np.ndarray:

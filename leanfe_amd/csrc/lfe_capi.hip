@@ -392,6 +392,7 @@ static void free_data(lfe_ctx* c) {
     dfree(fe.T);
     dfree(fe.alpha);
     dfree(fe.R);
+    dfree(fe.hi);
     dfree(fe.seg_off);
     dfree(fe.seg_cur);
     dfree(fe.oc);
@@ -412,6 +413,8 @@ static void free_data(lfe_ctx* c) {
   dfree(c->raw_slots);
   c->raw_slots_cap = 0;
   dfree(c->amax);
+  dfree(c->astat);
+  c->astat_cap = 0;
   dfree(c->xq);
   dfree(c->chain);
   c->amax_cap = c->xq_cap = c->chain_cap = 0;
@@ -457,6 +460,7 @@ static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_leve
     if (n_levels[f] < 1) return fail(LFE_EINVAL, "n_levels must be >= 1");
   c->n = n;
   c->ld = std::max<int64_t>((n + 63) / 64 * 64, 64);
+  c->hi_dirty = false;
   c->p = p;
   c->F = F;
   c->sw.on = codes_only;  // streamed X: no resident columns, no permuted copy
@@ -477,6 +481,8 @@ static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_leve
     LFE_TRY(dalloc(&fe.T, (size_t)fe.G * p));
     LFE_TRY(dalloc(&fe.alpha, (size_t)fe.G * p));
     LFE_TRY(dalloc(&fe.R, (size_t)fe.G));
+    LFE_TRY(dalloc(&fe.hi, (size_t)fe.G * p));
+    LFE_HIP(hipMemsetAsync(fe.hi, 0, sizeof(double) * (size_t)fe.G * p, c->stream));
     if (weighted) {
       LFE_TRY(dalloc(&fe.W, (size_t)fe.G));
       LFE_TRY(dalloc(&fe.Sy, (size_t)fe.G));
@@ -488,6 +494,10 @@ static int alloc_data(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_leve
     LFE_TRY(dalloc(&c->origp, (size_t)c->ld));
   }
   return LFE_OK;
+}
+
+int alloc_shard(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_levels, bool weighted) {
+  return alloc_data(c, n, p, F, n_levels, weighted);
 }
 
 enum { PH_PREP, PH_DEMEAN, PH_GRAM, PH_RESID, PH_CLUSTER };
@@ -905,6 +915,17 @@ int lfe_ctx_set_owner(lfe_ctx* c, int fe, int32_t lo, int32_t hi) {
   c->owner_hi = hi;
   c->prepared = false;  // the layout decides again which tables stay rank-local
   return LFE_OK;
+}
+
+int lfe_reshard_owner(lfe_ctx* c, int fe, int32_t* lo_out, int32_t* hi_out) {
+  LFE_CTX(c);
+  if (!c->loaded) return fail(LFE_ESTATE, "load the shard before lfe_reshard_owner");
+  if (!lo_out || !hi_out) return fail(LFE_EINVAL, "null output pointer");
+  int32_t lo = 0, hi = 0;
+  LFE_TRY(reshard_owner(c, fe, &lo, &hi));
+  *lo_out = lo;
+  *hi_out = hi;
+  return lfe_ctx_set_owner(c, fe, lo, hi);
 }
 
 int lfe_synth_load_owned(lfe_ctx* c, int64_t n_total, int k, int n_fe, const int32_t* n_levels, const double* beta,

@@ -15,7 +15,8 @@
 // fe2 x fe3 has 48.8M clusters for 50M rows).
 //
 // Multi-rank: clusters span row shards; keys are global (codes are global).  Few
-// clusters (key table <= 64 MB): a key-indexed S table, f64 atomics, all-reduce.
+// clusters (key table <= 64 MB): the local clusters' sums (steps 2-4) are put into a
+// key-indexed S table (one store per cluster, no atomics) and all-reduced.
 // Otherwise owner-partitioned (owner_meat): local sums per cluster are sent to
 // the rank owner(key) by an all-to-all, merged there, and only the k x k meats
 // and the cluster counts are all-reduced.
@@ -156,15 +157,19 @@ __global__ void k_seg_rows_chain(const uint64_t* __restrict__ K, const int32_t* 
   }
 }
 
-// multi-rank dense form: S[key] += scores_i (span < 2^31)
-__global__ void k_cl_dense_scatter(const uint64_t* __restrict__ keys, int64_t n, uint64_t drop,
-                                   const double* __restrict__ U, int k, double* __restrict__ S,
-                                   int32_t* __restrict__ present) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t key = keys[i];
-    if (key == drop) continue;
-    present[key] = 1;
-    for (int j = 0; j < k; ++j) atomicAdd(&S[key * k + j], U[i * k + j]);
+// multi-rank dense form (span < 2^31): the local cluster h (sorted keys, segment offsets) goes to
+// row key(h) of the zeroed key-indexed table; every key occurs once, so no two stores meet
+__global__ void k_cl_dense_put(const uint64_t* __restrict__ K, const int32_t* __restrict__ seg_off, int32_t G,
+                               const double* __restrict__ Sloc, int k, double* __restrict__ S,
+                               int32_t* __restrict__ present) {
+  const int kk = k > 0 ? k : 1;  // k = 0: presence only
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)G * kk;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t h = e / kk;
+    const int j = (int)(e % kk);
+    const uint64_t key = K[seg_off[h]];
+    if (j == 0) present[key] = 1;
+    if (j < k) S[key * k + j] = Sloc[h * k + j];
   }
 }
 
@@ -390,21 +395,27 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   if (n > 0) hipLaunchKernelGGL(k_cl_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka);
   LFE_HIP(hipGetLastError());
 
+  int buf = 0;
+  if (n > 0) LFE_TRY(radix_sort(c, n, bit_length(span), &buf));
+  int32_t G = 0;
+  LFE_TRY(group_sorted(c, n, span, W.keys[buf], W.rows[buf], c->scores, k, &G));
+
   // multi-rank, few clusters: a key-indexed table, all-reduced (smaller than the exchange)
   const char* own_env = getenv("LFE_CL_OWNER_MIN_SPAN");  // tests: force the owner-partitioned form
   const uint64_t owner_min = own_env ? (uint64_t)atoll(own_env) : ((64ull << 20) / (8ull * std::max(k, 1)));
   if (c->world > 1 && span < owner_min && span < (1ull << 31)) {
     const int32_t C = (int32_t)span;
-    LFE_TRY(ensure_cluster_ws(c, (size_t)C * std::max(k, 1), (size_t)C + 4));
-    double* S = c->clS;
+    LFE_TRY(ensure_cluster_ws(c, (size_t)std::max(G, 1) * std::max(k, 1), (size_t)C + 4));
+    LFE_TRY(ensure_f64(c, W.srec, W.srec_cap, (size_t)C * std::max(k, 1)));
+    double* S = W.srec;  // the key-indexed table (the exchange's send buffer is idle here)
     int32_t* present = c->clP;
     int32_t* cntG = present + C;
     LFE_HIP(hipMemsetAsync(S, 0, sizeof(double) * (size_t)C * std::max(k, 1), c->stream));
     LFE_HIP(hipMemsetAsync(present, 0, sizeof(int32_t) * ((size_t)C + 4), c->stream));
-    if (n > 0 && k > 0) {
+    if (G > 0) {
       ProfScope _ps(c, K_CLUSTER_SCATTER);
-      hipLaunchKernelGGL(k_cl_dense_scatter, dim3(grid_for(n)), dim3(kBlock), 0, c->stream, W.keys[0], n, span,
-                         c->scores, k, S, present);
+      hipLaunchKernelGGL(k_cl_dense_put, dim3(grid_for((int64_t)G * std::max(k, 1))), dim3(kBlock), 0, c->stream,
+                         W.keys[buf], W.seg_off, G, c->clS, k, S, present);
     }
     LFE_HIP(hipGetLastError());
     LFE_TRY(allreduce_sum_f64(c, S, (size_t)C * k));
@@ -423,11 +434,6 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
     }
     return LFE_OK;
   }
-
-  int buf = 0;
-  if (n > 0) LFE_TRY(radix_sort(c, n, bit_length(span), &buf));
-  int32_t G = 0;
-  LFE_TRY(group_sorted(c, n, span, W.keys[buf], W.rows[buf], c->scores, k, &G));
   if (c->world > 1) return owner_meat(c, W.keys[buf], G, k, span, meat, G_out);
   *G_out = G;
   if (k == 0) return LFE_OK;

@@ -40,20 +40,10 @@ struct Sums4Args {
   int nq;               // number of non-primary FEs and their indices
   int qf[kMaxFE];
   double* raw_part;     // RAW: [blocks][256] raw Gram tiles
-  double* qpart;        // k_sums2_raw: [blocks][G_Q * p] the block's secondary-FE table (raw bits)
-  const double* fixq;   // k_sums2_raw: [kMaxCols] scales, [kMaxCols] quanta, [kMaxCols] qualified (k_fix_quanta)
+  double* qpart;        // k_sums2_raw: [blocks][G_Q * p] the block's secondary-FE table (fine limbs)
+  const double* fixq;   // quanta of the two-limb sums (k_fix_quanta)
+  double* hi[kMaxFE];   // coarse limbs [G][p] per FE (global f64 atomics of integer values: rare)
 };
-
-// exact group sums (k_sums2_raw): round(x * scale) is the low mantissa of x * scale + 1.5 * 2^52
-constexpr double kFixMagic = 6755399441055744.0;  // 1.5 * 2^52
-constexpr unsigned long long kFixMagicBits = 0x4338000000000000ull;
-
-// every column qualifies: the exact sums are on for the fit
-__device__ __forceinline__ bool fix_on(const double* __restrict__ fq, int p) {
-  bool on = true;
-  for (int c = 0; c < p; ++c) on = on && fq[2 * kMaxCols + c] != 0.0;
-  return on;
-}
 
 // FQ: max non-primary FEs held in registers; GU: 16-row groups loaded before use;
 // NT: 16-column slots per lane (p <= 16 NT); TH: threads per workgroup.
@@ -72,19 +62,17 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) racc[s] = d4{0.0, 0.0, 0.0, 0.0};
   const double shift = (RAW && c < p && a.la.n_items > 0) ? a.X[(int64_t)c * a.ld] : 0.0;
-  // exact sums (unweighted fits, k_fix_quanta): every value enters as round(x * scale_c) in int64,
-  // so the tables do not depend on the order of the adds
-  const bool fix = a.fixq != nullptr && fix_on(a.fixq, p);
-  double fsc[NT];
+  // two-limb fixed point (lfe_internal.h): the fine limbs go to the tables as int64, the coarse
+  // limbs of outliers to the global hi tables, so no table depends on the order of the adds
+  FixCol fc[NT];
 #pragma unroll
-  for (int I = 0; I < NT; ++I) fsc[I] = (fix && 16 * I + c < p) ? a.fixq[16 * I + c] : 0.0;
+  for (int I = 0; I < NT; ++I) fc[I] = 16 * I + c < p ? fix_col(a.fixq, 16 * I + c) : FixCol{};
   typedef unsigned long long u64;
-  auto add = [&](double* dst, double v, int I) {
-    if (fix)
-      atomicAdd(reinterpret_cast<u64*>(dst),
-                (u64)__double_as_longlong(__builtin_fma(v, fsc[I], kFixMagic)) - kFixMagicBits);
-    else
-      atomicAdd(dst, v);
+  // dst: the table entry (LDS or global), hdst: the entry's coarse limb (global)
+  auto add = [&](double* dst, double* hdst, double v, int I) {
+    double h;
+    atomicAdd(reinterpret_cast<u64*>(dst), fix_split(v, fc[I], h));
+    if (h != 0.0) atomicAdd(hdst, h);
   };
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
@@ -95,14 +83,8 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
     const int lo = b << a.la.s;
     for (int j = tid; j < a.B * p; j += TH) {
       const int g = lo + j / p;
-      double* dst = &a.S[P][(int64_t)g * p + (j % p)];
-      if (fix) {
-        const u64 val = reinterpret_cast<const u64*>(lds)[j];
-        if (val != 0ull && g < a.G_P) atomicAdd(reinterpret_cast<u64*>(dst), val);
-      } else {
-        const double val = lds[j];
-        if (val != 0.0 && g < a.G_P) atomicAdd(dst, val);
-      }
+      const u64 val = reinterpret_cast<const u64*>(lds)[j];
+      if (val != 0ull && g < a.G_P) atomicAdd(reinterpret_cast<u64*>(&a.S[P][(int64_t)g * p + (j % p)]), val);
       lds[j] = 0.0;
     }
   };
@@ -157,12 +139,14 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
             racc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[s], 0, 0, 0);
             if (c < p && valid[s]) {
               const double v = xv[u][0][s];
-              if (a.slice) add(&lds[(hv[s] - lo) * p + c], v, 0);
-              else add(&a.S[P][(int64_t)hv[s] * p + c], v, 0);
+              double* hP = &a.hi[P][(int64_t)hv[s] * p + c];
+              if (a.slice) add(&lds[(hv[s] - lo) * p + c], hP, v, 0);
+              else add(&a.S[P][(int64_t)hv[s] * p + c], hP, v, 0);
               const int f = a.qf[0];
               const int g = (&cq[u][0].x)[s];
-              if (a.tab_off[f] >= 0) add(&lds[a.tab_off[f] + g * p + c], v, 0);
-              else add(&a.S[f][(int64_t)g * p + c], v, 0);
+              double* hQ = &a.hi[f][(int64_t)g * p + c];
+              if (a.tab_off[f] >= 0) add(&lds[a.tab_off[f] + g * p + c], hQ, v, 0);
+              else add(&a.S[f][(int64_t)g * p + c], hQ, v, 0);
             }
           }
           continue;
@@ -177,16 +161,18 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
           for (int s = 0; s < 4; ++s) {
             if (!valid[s]) continue;
             if (P >= 0) {
-              if (a.slice) add(&lds[(hv[s] - lo) * p + col], v[s], I);
-              else add(&a.S[P][(int64_t)hv[s] * p + col], v[s], I);
+              double* hP = &a.hi[P][(int64_t)hv[s] * p + col];
+              if (a.slice) add(&lds[(hv[s] - lo) * p + col], hP, v[s], I);
+              else add(&a.S[P][(int64_t)hv[s] * p + col], hP, v[s], I);
             }
 #pragma unroll
             for (int q = 0; q < FQ; ++q) {
               if (q >= nq) continue;
               const int f = a.qf[q];
               const int g = (&cq[u][q].x)[s];
-              if (a.tab_off[f] >= 0) add(&lds[a.tab_off[f] + g * p + col], v[s], I);
-              else add(&a.S[f][(int64_t)g * p + col], v[s], I);
+              double* hQ = &a.hi[f][(int64_t)g * p + col];
+              if (a.tab_off[f] >= 0) add(&lds[a.tab_off[f] + g * p + col], hQ, v[s], I);
+              else add(&a.S[f][(int64_t)g * p + col], hQ, v[s], I);
             }
           }
         }
@@ -198,13 +184,8 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   for (int f = 0; f < F; ++f)
     if (f != P && a.tab_off[f] >= 0)
       for (int j = tid; j < a.G[f] * p; j += TH) {
-        if (fix) {
-          const u64 val = reinterpret_cast<const u64*>(lds + a.tab_off[f])[j];
-          if (val != 0ull) atomicAdd(reinterpret_cast<u64*>(&a.S[f][j]), val);
-        } else {
-          const double val = lds[a.tab_off[f] + j];
-          if (val != 0.0) atomicAdd(&a.S[f][j], val);
-        }
+        const u64 val = reinterpret_cast<const u64*>(lds + a.tab_off[f])[j];
+        if (val != 0ull) atomicAdd(reinterpret_cast<u64*>(&a.S[f][j]), val);
       }
   if (RAW) {
     // waves' raw tiles summed in LDS (lane (kq, c) holds rows kq + 4 rr of column c)
@@ -247,10 +228,12 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   const double* __restrict__ xc = a.X + (int64_t)(col ? c : 0) * a.ld;
   const int qoff = a.tab_off[Q];
   double* const qtab = lds + qoff;
-  // exact sums: every value enters the tables as round(x * 2^(62-e_c)) in int64, so the tables
-  // are the same whatever order the waves' LDS adds (and the blocks' global adds) land in
-  const bool fix = fix_on(a.fixq, p);
-  const double fscale = col ? a.fixq[c] : 0.0;
+  // two-limb fixed point: the fine limbs enter the LDS tables as int64 (the same whatever order
+  // the waves' LDS adds and the blocks' global adds land in), the coarse limbs of outliers go to
+  // the global hi tables as integer-valued f64 (exact in any order)
+  const FixCol fc = col ? fix_col(a.fixq, c) : FixCol{};
+  double* const hiP = a.hi[P];
+  double* const hiQ = a.hi[Q];
   d4 racc[NACC];  // independent MFMA chains
 #pragma unroll
   for (int r = 0; r < NACC; ++r) racc[r] = d4{0.0, 0.0, 0.0, 0.0};
@@ -261,14 +244,8 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
     const int lo = b << s;
     for (int j = tid; j < a.B * p; j += TH) {
       const int g = lo + j / p;
-      double* dst = &a.S[P][(int64_t)g * p + (j % p)];
-      if (fix) {
-        const u64 val = reinterpret_cast<const u64*>(lds)[j];
-        if (val != 0ull && g < a.G_P) atomicAdd(reinterpret_cast<u64*>(dst), val);
-      } else {
-        const double val = lds[j];
-        if (val != 0.0 && g < a.G_P) atomicAdd(dst, val);
-      }
+      const u64 val = reinterpret_cast<const u64*>(lds)[j];
+      if (val != 0ull && g < a.G_P) atomicAdd(reinterpret_cast<u64*>(&a.S[P][(int64_t)g * p + (j % p)]), val);
       lds[j] = 0.0;
     }
   };
@@ -321,15 +298,14 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
           const double xv = x[u][r];
           const double z = v ? __builtin_fma(xv, cm, zc) : 0.0;
           racc[r % NACC] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[r % NACC], 0, 0, 0);
-          if (v && col) {
-            if (fix) {  // integer adds commute: the exact path
-              // round(x * scale) as the low bits of x * scale + 1.5 * 2^52 (|x * scale| < 2^51)
-              const u64 xi = (u64)__double_as_longlong(__builtin_fma(xv, fscale, kFixMagic)) - kFixMagicBits;
-              atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(lds, hv[r] - lo, p8, c8)), xi);
-              atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(qtab, gq[r], p8, c8)), xi);
-            } else {
-              atomicAdd(lds_row_ptr(lds, hv[r] - lo, p8, c8), xv);
-              atomicAdd(lds_row_ptr(qtab, gq[r], p8, c8), xv);
+          if (v && col) {  // integer adds commute
+            double hh;
+            const u64 xi = fix_split(xv, fc, hh);
+            atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(lds, hv[r] - lo, p8, c8)), xi);
+            atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(qtab, gq[r], p8, c8)), xi);
+            if (hh != 0.0) {  // an outlier (or a non-finite value): its coarse limb
+              atomicAdd(&hiP[(int64_t)hv[r] * p + c], hh);
+              atomicAdd(&hiQ[(int64_t)gq[r] * p + c], hh);
             }
           }
         }
@@ -383,17 +359,11 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
 }
 
 // ---------------------------------------------------------------------------
-// exact group sums (the two-FE Gram-from-tables case, k_sums2_raw)
+// two-limb fixed-point group sums (lfe_internal.h): quanta from the column statistics
 // ---------------------------------------------------------------------------
-// A column's group sums accumulate round(x * scale) in int64, scale = 2^min(62 - e, 51 - e_M) with
-// 2^e > N * max|x| (N = the largest kept group over both FEs) and 2^e_M > max|x|: no partial
-// sum can overflow (|sum| < 2^62), every scaled value is below 2^51 so one FMA with 1.5 * 2^52
-// rounds it (the low mantissa bits are the integer), and integer adds make the tables
-// independent of the order in which waves and blocks add (bit-reproducible).  Per value the
-// rounding is at most 1/(2 scale) <= N max|x| 2^-62: below double rounding for the group means
-// as long as max|x| stays within kFixRange of the column's RMS; a column outside that range
-// (or a NaN / Inf) keeps the f64 atomic sums for every column of the fit.
-constexpr double kFixRange = 64.0;
+// The statistics (max |x_c|, per-chunk sum of x_c^2) come from the partition, or k_col_stats when
+// the rows stayed in place; both are deterministic (u64 atomicMax, chunk sums added in order).
+// Non-finite values do not need a fallback: they travel in the coarse limb.
 
 // column statistics when the partition did not run (one bucket): max |x_c| bits in st[c],
 // the chunk's sum of x_c^2 in st[kColStatHead + c * nchunks + chunk] (as the partition writes them)
@@ -461,8 +431,7 @@ __global__ __launch_bounds__(256) void k_col_stats_w(const double* __restrict__ 
   }
 }
 
-// scale, quantum and qualification of column c = blockIdx.x (fq: [kMaxCols] scales, [kMaxCols]
-// quanta, [kMaxCols] 1.0 / 0.0); the per-chunk squares are summed in a fixed order
+// quanta of column c = blockIdx.x (fix_quanta_col); the per-chunk squares are summed in a fixed order
 __global__ __launch_bounds__(256) void k_fix_quanta(const double* __restrict__ st, int nchunks, int64_t n,
                                                     const int32_t* __restrict__ cmax, int nfe,
                                                     double* __restrict__ fq) {
@@ -480,68 +449,51 @@ __global__ __launch_bounds__(256) void k_fix_quanta(const double* __restrict__ s
   for (int f = 0; f < nfe; ++f) N = max(N, cmax[f]);
   const double M = __longlong_as_double(reinterpret_cast<const long long*>(st)[c]);
   const double rms = n > 0 ? sqrt(q / (double)n) : 0.0;
-  const double NM = (double)N * M;
-  const bool ok = isfinite(q) && isfinite(NM) && M <= kFixRange * rms;
-  double scale = 1.0, quantum = 1.0;
-  if (ok && M > 0.0) {
-    int e = 0, eM = 0;
-    (void)frexp(NM, &e);  // NM < 2^e
-    (void)frexp(M, &eM);  // M < 2^eM
-    const int sh = min(62 - e, 51 - eM);
-    scale = ldexp(1.0, sh);
-    quantum = ldexp(1.0, -sh);
-  }
-  fq[c] = scale;
-  fq[kMaxCols + c] = quantum;
-  fq[2 * kMaxCols + c] = ok ? 1.0 : 0.0;
+  fix_quanta_col(M, rms, (double)N, fq, c);
 }
 
-// int64 table entries (exact path) -> double: S = round-sum * quantum of the entry's column
-__global__ void k_fix_convert(double* __restrict__ S, int64_t m, int p, const double* __restrict__ fq) {
-  if (!fix_on(fq, p)) return;
+// the entry's coarse limb (read and cleared: the hi tables stay zero between sums) when its
+// column has any
+__device__ __forceinline__ double take_hi(double* __restrict__ hi, int64_t e, const double* __restrict__ fq, int c) {
+  if (fq[FQ_BIG * kFqCols + c] == 0.0) return 0.0;
+  const double h = hi[e];
+  if (h != 0.0) hi[e] = 0.0;
+  return h;
+}
+
+// two-limb table entries (fine limb int64 bits in S, coarse limb in hi) -> double
+__global__ void k_fix_convert(double* __restrict__ S, double* __restrict__ hi, int64_t m, int p,
+                              const double* __restrict__ fq) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
-    const long long v = reinterpret_cast<const long long*>(S)[e];
-    S[e] = (double)v * fq[kMaxCols + (int)(e % p)];
+    const int c = (int)(e % p);
+    S[e] = fix_value((unsigned long long)__double_as_longlong(S[e]), take_hi(hi, e, fq, c), fq, c);
   }
 }
 
-// S_Q = the blocks' tables summed in block order (int64 on the exact path, then scaled to
-// double; else f64): 16
-// consecutive entries x 16 block slices per workgroup, the slices added in order
+// S_Q = the blocks' fine-limb tables summed in block order (int64), plus the coarse limbs: 16
+// consecutive entries x 16 block slices per workgroup
 __device__ __forceinline__ void qpart_reduce_block(const double* __restrict__ part, int nblk, int64_t m,
                                                    const double* __restrict__ fq, int p, double* __restrict__ S,
-                                                   int blk) {
-  __shared__ double ps[16][16];
-  __shared__ long long pi[16][16];
+                                                   double* __restrict__ hi, int blk) {
+  __shared__ unsigned long long pi[16][16];
   const int ei = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int64_t e = (int64_t)blk * 16 + ei;
-  const bool fix = fix_on(fq, p);
-  double t = 0.0;
-  long long ti = 0;
+  unsigned long long ti = 0;
   if (e < m)
-    for (int b = sl; b < nblk; b += 16) {
-      const double v = part[(int64_t)b * m + e];
-      t += v;
-      ti += __double_as_longlong(v);
-    }
-  ps[sl][ei] = t;
+    for (int b = sl; b < nblk; b += 16) ti += (unsigned long long)__double_as_longlong(part[(int64_t)b * m + e]);
   pi[sl][ei] = ti;
   __syncthreads();
   if (sl != 0 || e >= m) return;
-  if (fix) {
-    long long r = 0;
-    for (int k = 0; k < 16; ++k) r += pi[k][ei];
-    S[e] = (double)r * fq[kMaxCols + (int)(e % p)];  // k_fix_convert's conversion, fused
-  } else {
-    double r = 0.0;
-    for (int k = 0; k < 16; ++k) r += ps[k][ei];
-    S[e] = r;
-  }
+  unsigned long long r = 0;
+  for (int k = 0; k < 16; ++k) r += pi[k][ei];
+  const int c = (int)(e % p);
+  S[e] = fix_value(r, take_hi(hi, e, fq, c), fq, c);
 }
 
 __global__ __launch_bounds__(256) void k_qpart_reduce(const double* __restrict__ part, int nblk, int64_t m,
-                                                      const double* __restrict__ fq, int p, double* __restrict__ S) {
-  qpart_reduce_block(part, nblk, m, fq, p, S, blockIdx.x);
+                                                      const double* __restrict__ fq, int p, double* __restrict__ S,
+                                                      double* __restrict__ hi) {
+  qpart_reduce_block(part, nblk, m, fq, p, S, hi, blockIdx.x);
 }
 
 // the two-FE sums' epilogue in one launch (four independent pieces, by block range): S_Q from the
@@ -554,11 +506,12 @@ struct Sums2Epi {
   const double* fq;
   int p;
   double* SQ;
+  double* hiQ;
   int nbq;
   double* SP;
+  double* hiP;
   int64_t mp;
   int nbp;
-  int exact;
   const double* raw_part;
   double* raw_tile;
   const double* X;
@@ -569,15 +522,14 @@ struct Sums2Epi {
 __global__ __launch_bounds__(256) void k_sums2_epilogue(Sums2Epi a) {
   int b = blockIdx.x;
   if (b < a.nbq) {
-    qpart_reduce_block(a.qpart, a.nblk, a.mq, a.fq, a.p, a.SQ, b);
+    qpart_reduce_block(a.qpart, a.nblk, a.mq, a.fq, a.p, a.SQ, a.hiQ, b);
     return;
   }
   b -= a.nbq;
   if (b < a.nbp) {
-    if (!a.exact || !fix_on(a.fq, a.p)) return;
     for (int64_t e = (int64_t)b * 256 + threadIdx.x; e < a.mp; e += (int64_t)a.nbp * 256) {
-      const long long v = reinterpret_cast<const long long*>(a.SP)[e];
-      a.SP[e] = (double)v * a.fq[kMaxCols + (int)(e % a.p)];
+      const int c = (int)(e % a.p);
+      a.SP[e] = fix_value((unsigned long long)__double_as_longlong(a.SP[e]), take_hi(a.hiP, e, a.fq, c), a.fq, c);
     }
     return;
   }
@@ -665,6 +617,7 @@ int sums4(lfe_ctx* c) {
   for (int f = 0; f < c->F; ++f) {
     a.G[f] = c->fe[f].G;
     a.S[f] = c->fe[f].S;
+    a.hi[f] = c->fe[f].hi;
     a.tab_off[f] = -1;
     if (f != P && off + (size_t)c->fe[f].G * p <= budget) {
       a.tab_off[f] = (int)off;
@@ -711,15 +664,15 @@ int sums4(lfe_ctx* c) {
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
     a.raw_part = c->raw_part;
   }
-  // exact (int64) group sums for every unweighted fit (the two-FE kernel and k_sums4 alike) and
-  // for weighted fits, whose quanta come from the statistics of w x, w and y (k_col_stats_w)
-  const bool wexact = a.w != nullptr && p + 2 <= kMaxCols;
-  const bool exact = two || !a.w || wexact;
+  // two-limb fixed-point group sums for every fit: unweighted quanta from the statistics of x,
+  // weighted ones from those of w x, w and the raw y (k_col_stats_w, columns p and p + 1)
+  const bool wexact = a.w != nullptr;
   if (two) {
     LFE_TRY(ensure_f64(c, c->qpart, c->qpart_cap, (size_t)nblocks * c->fe[a.qf[0]].G * p));
     a.qpart = c->qpart;
   }
-  if (exact) {
+  LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, (size_t)kFqRows * kFqCols));
+  {
     ProfScope _ps(c, K_FIX_SUMS);
     // the column statistics (the partition wrote them unless the rows stayed in place)
     constexpr int64_t kStatRows = 16384;
@@ -730,7 +683,6 @@ int sums4(lfe_ctx* c) {
       hipLaunchKernelGGL(k_col_stats_w, dim3(nch), dim3(256), 0, c->stream, c->L.X, c->L.w, c->ld, c->n, p,
                          kStatRows, c->colstat);
       LFE_HIP(hipGetLastError());
-      LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, 3 * kMaxCols));
       hipLaunchKernelGGL(k_fix_quanta, dim3(p + 2), dim3(256), 0, c->stream, c->colstat, nch, c->n,
                          c->iscratch + kIscratchCmax, c->F, c->fixq);
       LFE_HIP(hipGetLastError());
@@ -745,14 +697,14 @@ int sums4(lfe_ctx* c) {
       c->colstat_chunks = nch;
     }
     if (!wexact) {
-      LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, 3 * kMaxCols));
       hipLaunchKernelGGL(k_fix_quanta, dim3(p), dim3(256), 0, c->stream, c->colstat, c->colstat_chunks, c->n,
                          c->iscratch + kIscratchCmax, c->F, c->fixq);
       LFE_HIP(hipGetLastError());
     }
     a.fixq = c->fixq;
   }
-  c->exact_sums = exact;
+  c->exact_sums = true;
+  LFE_TRY(hi_begin(c));
   {
     ProfScope _ps(c, K_GROUP_SUMS);
     void* args[] = {&a};
@@ -769,11 +721,12 @@ int sums4(lfe_ctx* c) {
     e.fq = c->fixq;
     e.p = p;
     e.SQ = c->fe[a.qf[0]].S;
+    e.hiQ = c->fe[a.qf[0]].hi;
     e.nbq = (int)((e.mq + 15) / 16);
     e.SP = c->fe[P].S;
+    e.hiP = c->fe[P].hi;
     e.mp = (int64_t)c->fe[P].G * p;
     e.nbp = grid_for(e.mp);
-    e.exact = exact ? 1 : 0;
     e.raw_part = c->raw_part;
     e.raw_tile = c->raw_tile;
     e.X = c->L.X;
@@ -785,14 +738,16 @@ int sums4(lfe_ctx* c) {
     LFE_HIP(hipGetLastError());
     c->raw_ready = true;
   }
-  if (exact && !two) {
+  if (!two) {
     ProfScope _ps(c, K_FIX_SUMS);
     for (int f = 0; f < c->F; ++f) {
       const int64_t m = (int64_t)c->fe[f].G * p;
-      hipLaunchKernelGGL(k_fix_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, c->fe[f].S, m, p, c->fixq);
+      hipLaunchKernelGGL(k_fix_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, c->fe[f].S, c->fe[f].hi, m,
+                         p, c->fixq);
     }
     LFE_HIP(hipGetLastError());
   }
+  hi_end(c);
   if (raw && !two) {
     reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
     LFE_TRY(ensure_f64(c, c->raw_shift, c->raw_shift_cap, 32));
@@ -850,8 +805,7 @@ __global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.p;
   const bool col = c < p;
-  const bool fix = fix_on(a.fixq, p);
-  const double fscale = col ? a.fixq[c] : 0.0;
+  const FixCol fc = col ? fix_col(a.fixq, c) : FixCol{};
   const double cm = col ? 1.0 : 0.0;
   const double zc = (c == 15 ? 1.0 : 0.0) - (col ? a.shift[c] : 0.0);
   const double* __restrict__ xc = a.X + (int64_t)(col ? c : 0) * a.ld;
@@ -871,16 +825,14 @@ __global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
       const double xv = row < a.rows ? xc[row] : 0.0;
       const double z = keep ? __builtin_fma(xv, cm, zc) : 0.0;
       racc = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc, 0, 0, 0);
-      if (keep && col) {
-        if (fix) {
-          const unsigned long long xi =
-              (unsigned long long)__double_as_longlong(__builtin_fma(xv, fscale, kFixMagic)) - kFixMagicBits;
+      if (keep && col) {  // two-limb fixed point: fine limbs in s64, coarse limbs in sdbl
+        double hh;
+        const unsigned long long xi = fix_split(xv, fc, hh);
 #pragma unroll
-          for (int f = 0; f < NF; ++f) atomicAdd(&a.s64[a.toff[f] + (int64_t)gc[f] * p + c], xi);
-        } else {
+        for (int f = 0; f < NF; ++f) atomicAdd(&a.s64[a.toff[f] + (int64_t)gc[f] * p + c], xi);
+        if (hh != 0.0)
 #pragma unroll
-          for (int f = 0; f < NF; ++f) atomicAdd(&a.sdbl[a.toff[f] + (int64_t)gc[f] * p + c], xv);
-        }
+          for (int f = 0; f < NF; ++f) atomicAdd(&a.sdbl[a.toff[f] + (int64_t)gc[f] * p + c], hh);
       }
     }
   }
@@ -903,13 +855,11 @@ __global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
 __global__ void k_stream_fold(unsigned long long* __restrict__ s64, double* __restrict__ sdbl, int64_t m, int p,
                               const double* __restrict__ fq, int F, const int64_t* __restrict__ toff_end,
                               double* const* __restrict__ S) {
-  const bool fix = fix_on(fq, p);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
     int f = 0;
     while (f + 1 < F && e >= toff_end[f]) ++f;
     const int64_t j = e - (f ? toff_end[f - 1] : 0);
-    const double v = fix ? (double)(long long)s64[e] * fq[kMaxCols + (int)(j % p)] : sdbl[e];
-    S[f][j] += v;
+    S[f][j] += fix_value(s64[e], sdbl[e], fq, (int)(j % p));
     s64[e] = 0ull;
     sdbl[e] = 0.0;
   }
@@ -973,7 +923,7 @@ int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int
     LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nch * p));
     LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
     hipLaunchKernelGGL(k_col_stats, dim3(nch), dim3(256), 0, c->stream, X, ld, rows, p, kStatRows, c->colstat);
-    LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, 3 * kMaxCols));
+    LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, (size_t)kFqRows * kFqCols));
     hipLaunchKernelGGL(k_fix_quanta, dim3(p), dim3(256), 0, c->stream, c->colstat, nch, rows,
                        c->iscratch + kIscratchCmax, c->F, c->fixq);
     LFE_HIP(hipGetLastError());
@@ -1014,14 +964,15 @@ int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int
 }
 
 int exact_sums_on(lfe_ctx* c, int* on) {
-  *on = 0;
-  if (!c->exact_sums || !c->fixq) return LFE_OK;
-  // weighted fits: the S columns, the weights (W) and the raw y (Sy) must all qualify
-  const int nc = c->p + ((c->L.w && c->p + 2 <= kMaxCols) ? 2 : 0);
-  double flag[kMaxCols];
-  LFE_TRY(d2h_sync(c, flag, c->fixq + 2 * kMaxCols, sizeof(double) * nc));
-  *on = 1;
-  for (int j = 0; j < nc; ++j) *on = *on && flag[j] != 0.0;
+  *on = c->exact_sums ? 1 : 0;  // the group sums are always two-limb fixed point
+  return LFE_OK;
+}
+
+int hi_begin(lfe_ctx* c) {
+  if (c->hi_dirty)  // an earlier sum stopped before its conversion: clear every coarse limb
+    for (auto& fe : c->fe)
+      if (fe.hi) LFE_HIP(hipMemsetAsync(fe.hi, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
+  c->hi_dirty = true;
   return LFE_OK;
 }
 

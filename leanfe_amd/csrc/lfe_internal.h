@@ -61,6 +61,8 @@ struct FeState {
   double* T = nullptr;         // [G*p] cross term of the current projection
   double* alpha = nullptr;     // [G*p] group effect subtracted so far
   double* R = nullptr;         // [G] check cross term (y column, unweighted)
+  double* hi = nullptr;        // [G*p] coarse limbs of the sum being formed (S, W, Sy, T or R), all
+                               // zero between sums: the conversion that reads an entry clears it
   // segment layout (general sweeps, lfe_seg.hip): kept rows sorted by this FE's code
   int32_t* seg_off = nullptr;  // [G + 1]
   size_t seg_off_cap = 0;
@@ -234,8 +236,11 @@ struct lfe_ctx {
   // and the quanta of the cross term being formed
   double* amax = nullptr;        // [kMaxFE][kMaxCols]
   size_t amax_cap = 0;
-  double* xq = nullptr;          // [3 * kMaxCols]
+  double* astat = nullptr;       // [kMaxFE][kAstatBlocks][64]: per-block sum cnt alpha^2 (col 63: sum cnt)
+  size_t astat_cap = 0;
+  double* xq = nullptr;          // [kFqRows][kFqCols] quanta of the cross term being formed
   size_t xq_cap = 0;
+  bool hi_dirty = false;         // a sum may have left coarse limbs in fe[].hi (hi_begin clears them)
   // f64 segmented sums (lfe_seg.hip, lfe_cluster.hip): the partials of segments cut by work-unit /
   // wave edges, [2][units][cols], added in unit order by a fix-up pass instead of f64 atomics
   double* chain = nullptr;
@@ -290,9 +295,9 @@ struct lfe_ctx {
   double* colstat = nullptr;     // [kColStatHead + p * nchunks]: max |x_c| bits (as u64), then sum x_c^2 per column and chunk
   size_t colstat_cap = 0;
   int colstat_chunks = 0;        // chunks of per-chunk sums of squares written for this layout
-  double* fixq = nullptr;        // [3 * kMaxCols]: scale[c], quantum[c], qualified[c]
+  double* fixq = nullptr;        // [kFqRows][kFqCols] quanta of the group sums (fix_quanta_col)
   size_t fixq_cap = 0;
-  bool exact_sums = false;       // the last group sums ran k_sums2_raw (exact when fixq's flag is on)
+  bool exact_sums = false;       // the group sums of this layout were formed (always two-limb fixed point)
   // speculative Gram tile + Cholesky of the converged tables (gram_spec_enqueue), valid until the
   // next load / drop / demean: [0, 256) tile, 516 ok, [520, 532) beta, 532 guard (launch_gram_resid)
   double* dspec = nullptr;
@@ -324,6 +329,10 @@ namespace lfe {
 int prepare_layout(lfe_ctx* c);   // partition + counts + singleton marks
 int ensure_layout_orig(lfe_ctx* c);  // L.orig written (deferred by prepare_layout)
 int exact_sums_on(lfe_ctx* c, int* on);  // did the last group sums take the exact (int64) path
+// coarse-limb tables fe[].hi: clean (zero) on return; the caller's kernels may then write them
+// until the conversions that read and clear them are enqueued (hi_end)
+int hi_begin(lfe_ctx* c);
+inline void hi_end(lfe_ctx* c) { c->hi_dirty = false; }
 
 // --- group sums (lfe_fast.hip) ---
 int sums4(lfe_ctx* c);
@@ -384,7 +393,12 @@ int launch_synth_owned(lfe_ctx* c, int64_t n_total, int k, const int32_t* levels
 // flag (atomic max into *flag) any code outside [lo, hi)
 int launch_validate_range(const int32_t* code, int64_t n, int32_t lo, int32_t hi, int32_t* flag, hipStream_t s);
 
+// --- owner re-shard (lfe_shard.hip) ---
+int reshard_owner(lfe_ctx* c, int fe, int32_t* lo_out, int32_t* hi_out);
+
 // --- helpers (lfe_capi.hip) ---
+// (re)allocate the shard's buffers for n rows (frees every derived table and the cluster columns)
+int alloc_shard(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_levels, bool weighted);
 int ensure_scratch(lfe_ctx* c, size_t elems);
 int ensure_dred(lfe_ctx* c, size_t elems);
 int ensure_iscratch(lfe_ctx* c, size_t elems);
@@ -483,6 +497,80 @@ __device__ __forceinline__ double wave_reduce63(double v, double idv, Op op) {
   v = op(v, dpp64<0x142, 0xA>(v, idv));
   v = op(v, dpp64<0x143, 0xC>(v, idv));
   return v;
+}
+
+// ---------------------------------------------------------------------------
+// Two-limb fixed-point sums: every group sum, cross term and weight sum of the demeaning loop
+// is order-independent, so its bits do not depend on which wave or block adds first.
+//
+// Per column a quanta table fixes a coarse quantum Qc = 2^b and a fine scale sf = 2^s.  A value
+// v enters a sum as
+//     h  = round(v / Qc)                  (the coarse limb: an integer-valued double)
+//     lo = round((v - h Qc) * sf)         (the fine limb: int64)
+// Qc / 2 exceeds every typical value (min(max |v|, 64 rms)), so h = 0 for them and only
+// outliers touch the coarse limb.  The bounds keep both limbs exact whatever the order: a sum
+// of |h| over one group stays below 2^51 (f64 adds of integers below 2^53 are exact, so the
+// coarse limbs may use f64 atomics), a sum of |lo| below 2^62 (int64 adds commute).  A
+// non-finite v goes to the coarse limb itself (NaN / Inf propagate as in an f64 sum, in any
+// order).  The sum is then lo_sum / sf + h_sum Qc.  Per value the rounding is at most
+// 1 / (2 sf) = Qc 2^-min(64 - e_N, 53) (N < 2^e_N rows per group): 2^-41 of 64 rms at N = 2^16.
+// ---------------------------------------------------------------------------
+constexpr int kFqCols = kMaxCols + 3;
+constexpr int kAstatBlocks = 256;       // blocks of the effect-table statistics (k_alpha_stats)   // quanta table columns: p data columns (+ w, raw y)
+enum { FQ_SF = 0, FQ_QF = 1, FQ_BIG = 2, FQ_IQC = 3, FQ_QC = 4, FQ_RMS = 5, FQ_MAX = 6, kFqRows = 7 };
+constexpr double kFixRange = 64.0;      // typical values: |v| <= kFixRange * rms
+constexpr double kFixMagic = 6755399441055744.0;  // 1.5 * 2^52: fma(v, s, magic) - magic = round(v s)
+constexpr unsigned long long kFixMagicBits = 0x4338000000000000ull;
+
+struct FixCol {
+  double sf = 0.0, iqc = 0.0, qc = 0.0;
+  bool big = false;  // some value of the column may have a coarse limb
+};
+__device__ __forceinline__ FixCol fix_col(const double* __restrict__ fq, int c) {
+  FixCol q;
+  q.sf = fq[FQ_SF * kFqCols + c];
+  q.big = fq[FQ_BIG * kFqCols + c] != 0.0;
+  q.iqc = fq[FQ_IQC * kFqCols + c];
+  q.qc = fq[FQ_QC * kFqCols + c];
+  return q;
+}
+// the fine limb of v (returned) and its coarse limb h (0 for a typical value)
+__device__ __forceinline__ unsigned long long fix_split(double v, const FixCol& q, double& h) {
+  h = 0.0;
+  if (q.big) {
+    h = __builtin_fma(v, q.iqc, kFixMagic) - kFixMagic;     // round(v / Qc); NaN / Inf stay
+    v = __builtin_isfinite(h) ? __builtin_fma(-h, q.qc, v) : 0.0;  // exact remainder, |.| <= Qc / 2
+  }
+  return (unsigned long long)__double_as_longlong(__builtin_fma(v, q.sf, kFixMagic)) - kFixMagicBits;
+}
+// the sum of a table entry from its limbs (fine: int64 bits, coarse: f64)
+__device__ __forceinline__ double fix_value(unsigned long long lo, double hi, const double* __restrict__ fq, int c) {
+  const double v = (double)(long long)lo * fq[FQ_QF * kFqCols + c];
+  return hi != 0.0 ? v + hi * fq[FQ_QC * kFqCols + c] : v;
+}
+// quanta of one column from its statistics: M = max |v| (maybe Inf), rms (maybe NaN), N = the
+// largest number of values one sum adds (all written to fq[r * kFqCols + c])
+__device__ inline void fix_quanta_col(double M, double rms, double N, double* __restrict__ fq, int c) {
+  const bool finite = __builtin_isfinite(M) && __builtin_isfinite(rms);
+  int eN = 0;
+  (void)frexp(fmax(N, 1.0), &eN);  // N < 2^eN
+  int b = 0;                        // Qc = 2^b
+  if (finite && M > 0.0) {
+    const double T = fmin(M, kFixRange * rms);
+    int a = 0;
+    (void)frexp(T > 0.0 ? T : M, &a);  // T < 2^a: |v| <= T rounds to h = 0 with Qc = 2^(a + 1)
+    b = a + 1;
+    while (fmax(N, 1.0) * (ldexp(M, -b) + 1.0) >= 0x1p51) ++b;  // sum of |h| over one group < 2^51
+  }
+  const int s = min(63 - eN, 52) - b;  // sum of |lo| <= N 2^(b-1) 2^s < 2^62, |lo| <= 2^51
+  fq[FQ_SF * kFqCols + c] = ldexp(1.0, s);
+  fq[FQ_QF * kFqCols + c] = ldexp(1.0, -s);
+  // (a margin below Qc / 2: a value may exceed its bound M by the rounding of the sum it came from)
+  fq[FQ_BIG * kFqCols + c] = (!finite || M >= ldexp(1.0 - 0x1p-20, b - 1)) ? 1.0 : 0.0;
+  fq[FQ_IQC * kFqCols + c] = ldexp(1.0, -b);
+  fq[FQ_QC * kFqCols + c] = ldexp(1.0, b);
+  fq[FQ_RMS * kFqCols + c] = rms;
+  fq[FQ_MAX * kFqCols + c] = M;
 }
 
 // Balanced row ranges for the streaming X passes: block b of the grid walks layout rows

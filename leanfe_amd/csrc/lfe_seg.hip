@@ -98,18 +98,14 @@ struct SegCrossArgs {
   int pc;                            // columns computed: p, or 1 (y only)
   int G;
   double* T;                         // [G][pc], zeroed before the launch
-  const double* xq;                  // exact sums (null: f64): [kMaxCols] scales, [kMaxCols] quanta, flag
-  double* chain;                     // f64 sums: [2][n_units][pc] cut segments' parts (k_seg_chain); null: atomics
+  const double* xq;                  // two-limb sums (lfe_internal.h): quanta; null: f64 (chain) sums
+  double* Thi;                       // two-limb sums: coarse limbs [G][pc] (clean on entry)
+  double* chain;                     // f64 sums: [2][n_units][pc] cut segments' parts (k_seg_chain)
 };
 
-// exact cross terms: a row's value v (the sum of the other FEs' effects) enters T as
-// round(v * scale) in int64 (the FMA with 1.5 * 2^52 rounds it, |v * scale| < 2^51), so T does not
-// depend on the order of the segment layout's rows nor on which partial sum lands first
-constexpr double kSegMagic = 6755399441055744.0;  // 1.5 * 2^52
-constexpr unsigned long long kSegMagicBits = 0x4338000000000000ull;
-__device__ __forceinline__ long long seg_fix(double v, double scale) {
-  return (long long)((unsigned long long)__double_as_longlong(__builtin_fma(v, scale, kSegMagic)) - kSegMagicBits);
-}
+// two-limb cross terms: a row's value v (the sum of the other FEs' effects) enters T as its fine
+// limb in int64 and its coarse limb (outliers only) as an integer-valued f64, so T does not depend
+// on the order of the segment layout's rows nor on which partial sum lands first
 __device__ __forceinline__ long long seg_quad_sum_i64(long long v) {
   v += __shfl_xor(v, 16, 64);
   v += __shfl_xor(v, 32, 64);
@@ -140,10 +136,10 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
 #pragma unroll
   for (int I = 0; I < NT; ++I) cl[I] = 16 * I + c < pc ? 16 * I + c : 0;
   const int32_t kept = a.seg_off[G];
-  const bool ex = a.xq != nullptr && a.xq[2 * kMaxCols] != 0.0;  // wave-uniform
-  double xs[NT];
+  const bool ex = a.xq != nullptr;  // wave-uniform
+  FixCol fcs[NT];
 #pragma unroll
-  for (int I = 0; I < NT; ++I) xs[I] = ex ? a.xq[cl[I]] : 0.0;
+  for (int I = 0; I < NT; ++I) fcs[I] = ex ? fix_col(a.xq, cl[I]) : FixCol{};
   for (int u = wv; u < a.n_units; u += nwaves) {
     const int lo = u * kSegUnit;
     if (lo >= kept) break;
@@ -152,13 +148,20 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
     int r0 = a.seg_off[h], r1 = a.seg_off[h + 1];
     bool part = r0 < lo;  // segment h began in an earlier unit
     bool done = false;
-    double acc[NT];
+    double acc[NT];  // f64 sums, or the coarse limbs of the two-limb sums
     long long iacc[NT];
 #pragma unroll
     for (int I = 0; I < NT; ++I) {
       acc[I] = 0.0;
       iacc[I] = 0;
     }
+    // the fine limb of v (column slot I); its coarse limb joins acc[I] (integer-valued: exact)
+    auto fx = [&](double v, int I) -> long long {
+      double hh;
+      const long long lo = (long long)fix_split(v, fcs[I], hh);
+      acc[I] += hh;
+      return lo;
+    };
     // mode 0: segment h lies in this unit (store); 1: its part in this unit, begun in an earlier
     // unit; 2: its first part, continued in the next unit
     auto finalize = [&](int mode) {
@@ -168,9 +171,16 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
         double* d = a.T + (int64_t)h * pc + col;
         if (ex) {  // integer adds commute: a cut segment's partials may land in any order
           const long long t = seg_quad_sum_i64(iacc[I]);
+          const double th = seg_quad_sum(acc[I]);  // integer-valued coarse limbs: exact in any order
           if (kq == 0 && col < pc) {
-            if (mode) atomicAdd(reinterpret_cast<unsigned long long*>(d), (unsigned long long)t);
-            else *reinterpret_cast<long long*>(d) = t;
+            double* dh = a.Thi + (int64_t)h * pc + col;
+            if (mode) {
+              atomicAdd(reinterpret_cast<unsigned long long*>(d), (unsigned long long)t);
+              if (th != 0.0) atomicAdd(dh, th);
+            } else {
+              *reinterpret_cast<long long*>(d) = t;
+              if (th != 0.0) *dh = th;
+            }
           }
         } else {
           const double t = seg_quad_sum(acc[I]);
@@ -231,8 +241,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
             if (ex) {
 #pragma unroll
               for (int I = 0; I < NT; ++I)
-                iacc[I] += (seg_fix(val[U][0][I], xs[I]) + seg_fix(val[U][1][I], xs[I])) +
-                           (seg_fix(val[U][2][I], xs[I]) + seg_fix(val[U][3][I], xs[I]));
+                iacc[I] += (fx(val[U][0][I], I) + fx(val[U][1][I], I)) + (fx(val[U][2][I], I) + fx(val[U][3][I], I));
             } else {
 #pragma unroll
               for (int I = 0; I < NT; ++I)
@@ -245,7 +254,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
               const bool in = row >= r0 && row < r1;
 #pragma unroll
               for (int I = 0; I < NT; ++I) {
-                if (ex) iacc[I] += in ? seg_fix(val[U][s][I], xs[I]) : 0ll;
+                if (ex) iacc[I] += in ? fx(val[U][s][I], I) : 0ll;
                 else acc[I] += in ? val[U][s][I] : 0.0;
               }
             }
@@ -302,68 +311,82 @@ int launch_seg_chain(lfe_ctx* c, const int32_t* seg_off, const int32_t* ufirst, 
   return LFE_OK;
 }
 
-// column max |alpha| (u64 bits) of an effect table into out[0, p) (atomicMax; per block in LDS first)
-__global__ __launch_bounds__(256) void k_alpha_colmax(const double* __restrict__ alpha, int32_t G, int p,
-                                                      unsigned long long* __restrict__ out) {
-  __shared__ unsigned long long m[kMaxCols];
-  for (int j = threadIdx.x; j < p; j += blockDim.x) m[j] = 0ull;
-  __syncthreads();
-  const int64_t total = (int64_t)G * p;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x)
-    atomicMax(&m[e % p], (unsigned long long)__double_as_longlong(fabs(alpha[e])));
-  __syncthreads();
-  for (int j = threadIdx.x; j < p; j += blockDim.x)
-    if (m[j]) atomicMax(&out[j], m[j]);
-}
-
-// quanta of FE f's exact cross term: a row's value is bounded by M = sum over the other FEs of
-// their column max |alpha|, a group sum by N M (N = the largest kept group of f); scale =
-// 2^min(62 - e, 50 - e_M), 2^e > N M, 2^e_M > M (one bit of headroom for the rounding of the row
-// sums).  A non-finite bound (NaN / Inf effects) keeps the f64 sums.
-// Weighted (wmax != null): a row adds w v, so M is scaled by max |w| (k_col_stats_w); only when the
-// weight column qualified for the exact sums (max |w| <= 64 rms(w), wfq's flag), else the quanta
-// would be coarse against typical rows and the f64 sums stay.
-__global__ void k_cross_quanta(const unsigned long long* __restrict__ amax, int F, int f, int pc,
-                               const int32_t* __restrict__ cmax, double* __restrict__ xq,
-                               const unsigned long long* __restrict__ wmax, const double* __restrict__ wfq,
-                               int wcol) {
-  __shared__ int bad;
-  if (threadIdx.x == 0) bad = 0;
-  __syncthreads();
-  const int col = threadIdx.x;
-  if (col < pc) {
-    double M = 0.0;
-    for (int j = 0; j < F; ++j)
-      if (j != f) M += __longlong_as_double((long long)amax[j * kMaxCols + col]);
-    bool wok = true;
-    if (wmax) {
-      wok = wfq[2 * kMaxCols + wcol] != 0.0;
-      M *= __longlong_as_double((long long)wmax[0]);
+// Statistics of an effect table for the cross terms' quanta: column max |alpha| (u64 bits, atomicMax)
+// and, per block, sum_g cnt[g] alpha[g][c]^2 (col 63: sum_g cnt[g]) into slots [kAstatBlocks][64], so
+// that rms over rows of alpha_f[g_f(i)] is formed in a fixed order (k_cross_quanta).  Block b takes
+// the groups [b G / nb, (b + 1) G / nb), wave w every fourth of them, lane c column c.
+__global__ __launch_bounds__(256) void k_alpha_stats(const double* __restrict__ alpha, const int32_t* __restrict__ cnt,
+                                                     int32_t G, int p, unsigned long long* __restrict__ amax,
+                                                     double* __restrict__ slots) {
+  __shared__ double ss[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t g0 = (int64_t)G * blockIdx.x / gridDim.x, g1 = (int64_t)G * (blockIdx.x + 1) / gridDim.x;
+  double m = 0.0, sq = 0.0, nn = 0.0;
+  for (int64_t g = g0 + wave; g < g1; g += 4) {
+    const double ng = (double)cnt[g];
+    nn += ng;
+    if (lane < p) {
+      const double v = alpha[g * p + lane];
+      m = fmax(m, fabs(v));  // (fmax drops a NaN; the squares keep it)
+      sq = __builtin_fma(ng * v, v, sq);
     }
-    const double NM = (double)max(1, cmax[f]) * M;
-    const bool ok = wok && isfinite(NM);
-    double scale = 1.0, quantum = 1.0;
-    if (ok && M > 0.0) {
-      int e = 0, eM = 0;
-      (void)frexp(NM, &e);
-      (void)frexp(M, &eM);
-      const int sh = min(62 - e, 50 - eM);
-      scale = ldexp(1.0, sh);
-      quantum = ldexp(1.0, -sh);
-    }
-    xq[col] = scale;
-    xq[kMaxCols + col] = quantum;
-    if (!ok) atomicAdd(&bad, 1);
   }
+  ss[wave][lane] = lane == 63 ? nn : sq;
+  if (lane < p && m > 0.0) atomicMax(&amax[lane], (unsigned long long)__double_as_longlong(m));
   __syncthreads();
-  if (threadIdx.x == 0) xq[2 * kMaxCols] = bad ? 0.0 : 1.0;
+  if (wave == 0) slots[(int64_t)blockIdx.x * 64 + lane] = ((ss[0][lane] + ss[1][lane]) + ss[2][lane]) + ss[3][lane];
 }
 
-// exact cross term (int64 bits) -> double
-__global__ void k_cross_convert(double* __restrict__ T, int64_t m, int pc, const double* __restrict__ xq) {
-  if (xq[2 * kMaxCols] == 0.0) return;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x)
-    T[e] = (double)__double_as_longlong(T[e]) * xq[kMaxCols + (int)(e % pc)];
+static int alpha_stat_blocks(int32_t G) { return (int)std::max<int64_t>(1, std::min<int64_t>(kAstatBlocks, (G + 63) / 64)); }
+
+// Quanta of FE f's cross term (fix_quanta_col): a row's value is bounded by M = sum over the other
+// FEs of their column max |alpha|, its typical size by the sum of their rms over rows; a sum adds
+// at most N = the largest kept group of f.  Weighted (wfq != null): a row adds w v, so M and the
+// rms are scaled by the weight column's max and rms (the weighted quanta of sums4, column wcol).
+struct CrossQArgs {
+  const unsigned long long* amax;  // [kMaxFE][kMaxCols]
+  const double* astat;             // [kMaxFE][kAstatBlocks][64]
+  int nblk[kMaxFE];
+  int F, f, pc;
+  const int32_t* cmax;
+  const double* wfq;
+  int wcol;
+  double* xq;
+};
+__global__ void k_cross_quanta(CrossQArgs a) {
+  const int col = threadIdx.x;
+  if (col >= a.pc) return;
+  double M = 0.0, rms = 0.0;
+  for (int j = 0; j < a.F; ++j) {
+    if (j == a.f) continue;
+    M += __longlong_as_double((long long)a.amax[j * kMaxCols + col]);
+    const double* sl = a.astat + (int64_t)j * kAstatBlocks * 64;
+    double sq = 0.0, nn = 0.0;
+    for (int b = 0; b < a.nblk[j]; ++b) {
+      sq += sl[b * 64 + col];
+      nn += sl[b * 64 + 63];
+    }
+    rms += nn > 0.0 ? sqrt(sq / nn) : 0.0;
+  }
+  if (a.wfq) {
+    M *= a.wfq[FQ_MAX * kFqCols + a.wcol];
+    rms *= a.wfq[FQ_RMS * kFqCols + a.wcol];
+  }
+  fix_quanta_col(M, rms, (double)max(1, a.cmax[a.f]), a.xq, col);
+}
+
+// two-limb cross term (fine limbs int64 bits in T, coarse limbs in Thi, cleared) -> double
+__global__ void k_cross_convert(double* __restrict__ T, double* __restrict__ Thi, int64_t m, int pc,
+                                const double* __restrict__ xq) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % pc);
+    double h = 0.0;
+    if (xq[FQ_BIG * kFqCols + c] != 0.0) {
+      h = Thi[e];
+      if (h != 0.0) Thi[e] = 0.0;
+    }
+    T[e] = fix_value((unsigned long long)__double_as_longlong(T[e]), h, xq, c);
+  }
 }
 
 // alpha_f = (S_f - T_f) / W_f   (weighted: W = sum w; else W = kept count)
@@ -506,24 +529,27 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
   a.pc = pc;
   a.G = fe.G;
   a.T = out;
-  // cross terms sum exactly (int64 per column): bit-reproducible whatever the order of the
-  // segment layout's rows (ranked by global cursor atomics) and of the cut segments' adds.
-  // Weighted fits too when the group sums formed the weighted statistics (max |w| in colstat[p]).
-  const bool wstat = wt && c->exact_sums && c->p + 2 <= kMaxCols && c->colstat && c->fixq;
-  const bool ex = c->amax != nullptr && (!wt || wstat);
-  if (ex) {
-    LFE_TRY(ensure_f64(c, c->xq, c->xq_cap, 3 * kMaxCols));
-    hipLaunchKernelGGL(k_cross_quanta, dim3(1), dim3(64), 0, c->stream,
-                       reinterpret_cast<const unsigned long long*>(c->amax), c->F, f, pc,
-                       c->iscratch + kIscratchCmax, c->xq,
-                       wt ? reinterpret_cast<const unsigned long long*>(c->colstat) + c->p : nullptr, c->fixq, c->p);
+  // two-limb fixed-point cross terms: bit-reproducible whatever the order of the segment layout's
+  // rows (ranked by global cursor atomics) and of the cut segments' adds
+  {
+    LFE_TRY(ensure_f64(c, c->xq, c->xq_cap, (size_t)kFqRows * kFqCols));
+    CrossQArgs q{};
+    q.amax = reinterpret_cast<const unsigned long long*>(c->amax);
+    q.astat = c->astat;
+    for (int j = 0; j < c->F; ++j) q.nblk[j] = alpha_stat_blocks(c->fe[j].G);
+    q.F = c->F;
+    q.f = f;
+    q.pc = pc;
+    q.cmax = c->iscratch + kIscratchCmax;
+    q.wfq = wt ? c->fixq : nullptr;  // sums4's weighted quanta: column p is w
+    q.wcol = c->p;
+    q.xq = c->xq;
+    hipLaunchKernelGGL(k_cross_quanta, dim3(1), dim3(64), 0, c->stream, q);
     LFE_HIP(hipGetLastError());
     a.xq = c->xq;
+    a.Thi = fe.hi;
   }
-  if (!ex && a.n_units > 0) {  // f64 sums: cut segments' parts added in unit order (k_seg_chain)
-    LFE_TRY(ensure_f64(c, c->chain, c->chain_cap, (size_t)2 * a.n_units * pc));
-    a.chain = c->chain;
-  }
+  LFE_TRY(hi_begin(c));
   if (a.n_units > 0) {
     const int nt = (pc + 15) / 16;
     CrossFn fn = cross_fn(nt, c->F - 1, wt);
@@ -533,12 +559,12 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kSegThreads), 0, c->stream, a);
   }
   LFE_HIP(hipGetLastError());
-  if (a.chain) LFE_TRY(launch_seg_chain(c, fe.seg_off, fe.ufirst, fe.G, a.n_units, pc, out));
-  if (ex) {
+  {
     const int64_t m = (int64_t)fe.G * pc;
-    hipLaunchKernelGGL(k_cross_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, out, m, pc, c->xq);
+    hipLaunchKernelGGL(k_cross_convert, dim3(grid_for(m)), dim3(kBlock), 0, c->stream, out, fe.hi, m, pc, c->xq);
     LFE_HIP(hipGetLastError());
   }
+  hi_end(c);
   return allreduce_sum_f64(c, out, (size_t)fe.G * pc);
 }
 
@@ -583,11 +609,11 @@ static int seg_finalize(lfe_ctx* c, int f) {
   hipLaunchKernelGGL(k_finalize, dim3(grid_for((int64_t)fe.G * c->p)), dim3(kBlock), 0, c->stream, fe.S,
                      cross ? fe.T : nullptr, c->L.w ? fe.W : nullptr, fe.cnt, fe.G, c->p, fe.alpha);
   LFE_HIP(hipGetLastError());
-  if (c->amax) {  // the column bound of the new effects (the other FEs' exact cross terms)
+  if (cross) {  // the statistics of the new effects (the other FEs' cross-term quanta)
     unsigned long long* am = reinterpret_cast<unsigned long long*>(c->amax) + (size_t)f * kMaxCols;
     LFE_HIP(hipMemsetAsync(am, 0, sizeof(double) * c->p, c->stream));
-    hipLaunchKernelGGL(k_alpha_colmax, dim3(grid_for((int64_t)fe.G * c->p, kBlock, 512)), dim3(kBlock), 0,
-                       c->stream, fe.alpha, fe.G, c->p, am);
+    hipLaunchKernelGGL(k_alpha_stats, dim3(alpha_stat_blocks(fe.G)), dim3(256), 0, c->stream, fe.alpha, fe.cnt, fe.G,
+                       c->p, am, c->astat + (size_t)f * kAstatBlocks * 64);
     LFE_HIP(hipGetLastError());
   }
   return LFE_OK;
@@ -620,6 +646,8 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
   // every effect table starts at zero (lfe_demean): so do the exact cross terms' column bounds
   LFE_TRY(ensure_f64(c, c->amax, c->amax_cap, (size_t)kMaxFE * kMaxCols));
   LFE_HIP(hipMemsetAsync(c->amax, 0, sizeof(double) * kMaxFE * kMaxCols, c->stream));
+  LFE_TRY(ensure_f64(c, c->astat, c->astat_cap, (size_t)kMaxFE * kAstatBlocks * 64));
+  LFE_HIP(hipMemsetAsync(c->astat, 0, sizeof(double) * kMaxFE * kAstatBlocks * 64, c->stream));
   const int F = c->F;
   const bool cross = F > 1;
   if (cross) LFE_TRY(seg_build(c));

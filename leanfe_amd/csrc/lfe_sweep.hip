@@ -40,16 +40,10 @@ struct SweepArgs {
   double* out[kMaxFE];  // output tables [G] (nullptr: not a target)
   int lds_off[kMaxFE];  // LDS table offset (doubles), -1 = global atomics
   int lds_doubles;
-  const double* fq;     // exact sums (k_fix_quanta of k_col_stats_w) or null: f64 atomics
+  const double* fq;     // quanta of the two-limb sums (k_fix_quanta of k_col_stats_w)
   int fcol;             // the quanta's column of this source (p: weights, p + 1: y)
+  double* hi[kMaxFE];   // coarse limbs [G] per FE
 };
-
-// exact sums: round(v * scale) is the low mantissa of v * scale + 1.5 * 2^52 (lfe_fast.hip)
-constexpr double kSwMagic = 6755399441055744.0;
-constexpr unsigned long long kSwMagicBits = 0x4338000000000000ull;
-__device__ __forceinline__ bool sweep_fix_on(const double* fq, int col) {
-  return fq != nullptr && fq[2 * kMaxCols + col] != 0.0;
-}
 
 __global__ __launch_bounds__(kSweepThreads) void k_sweep_sums(SweepArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -57,21 +51,17 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_sums(SweepArgs a) {
   const int P = a.la.P, s = a.la.s;
   const int B = 1 << s;
   typedef unsigned long long u64;
-  // exact: integer adds commute, so the tables do not depend on the order of the adds
-  const bool fix = sweep_fix_on(a.fq, a.fcol);
-  const double fsc = fix ? a.fq[a.fcol] : 0.0;
-  auto add = [&](double* dst, double v) {
-    if (fix)
-      atomicAdd(reinterpret_cast<u64*>(dst), (u64)__double_as_longlong(__builtin_fma(v, fsc, kSwMagic)) - kSwMagicBits);
-    else
-      atomicAdd(dst, v);
+  // two-limb fixed point (lfe_internal.h): integer adds commute, so the tables do not depend on
+  // the order of the adds; outliers' coarse limbs go to the global hi tables
+  const FixCol fc = fix_col(a.fq, a.fcol);
+  auto add = [&](double* dst, double* hdst, double v) {
+    double h;
+    atomicAdd(reinterpret_cast<u64*>(dst), fix_split(v, fc, h));
+    if (h != 0.0) atomicAdd(hdst, h);
   };
-  auto nonzero = [&](const double* src) {
-    return fix ? *reinterpret_cast<const u64*>(src) != 0ull : *src != 0.0;
-  };
+  auto nonzero = [&](const double* src) { return *reinterpret_cast<const u64*>(src) != 0ull; };
   auto flush_add = [&](double* dst, const double* src) {
-    if (fix) atomicAdd(reinterpret_cast<u64*>(dst), *reinterpret_cast<const u64*>(src));
-    else atomicAdd(dst, *src);
+    atomicAdd(reinterpret_cast<u64*>(dst), *reinterpret_cast<const u64*>(src));
   };
 
   // zero the non-slice LDS tables once per workgroup
@@ -93,8 +83,9 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_sums(SweepArgs a) {
       for (int f = 0; f < a.la.F; ++f) {
         if (!a.out[f]) continue;
         const int64_t g = (f == P) ? (int64_t)(hP - lo) : (int64_t)a.la.code[f][i];
-        if (a.lds_off[f] >= 0) add(&lds[a.lds_off[f] + g], v);
-        else add(&a.out[f][(f == P) ? (int64_t)hP : g], v);
+        const int64_t gg = (f == P) ? (int64_t)hP : g;
+        if (a.lds_off[f] >= 0) add(&lds[a.lds_off[f] + g], &a.hi[f][gg], v);
+        else add(&a.out[f][gg], &a.hi[f][gg], v);
       }
     }
     __syncthreads();
@@ -114,12 +105,18 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_sums(SweepArgs a) {
       }
 }
 
-// exact one-column tables (int64 bits) -> double
-__global__ void k_fix_convert1(double* __restrict__ T, int64_t m, const double* __restrict__ fq, int col) {
-  if (!sweep_fix_on(fq, col)) return;
-  const double quantum = fq[kMaxCols + col];
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x)
-    T[e] = (double)__double_as_longlong(T[e]) * quantum;
+// two-limb one-column tables (fine limbs int64 bits in T, coarse limbs in hi, cleared) -> double
+__global__ void k_fix_convert1(double* __restrict__ T, double* __restrict__ hi, int64_t m,
+                               const double* __restrict__ fq, int col) {
+  const bool big = fq[FQ_BIG * kFqCols + col] != 0.0;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+    double h = 0.0;
+    if (big) {
+      h = hi[e];
+      if (h != 0.0) hi[e] = 0.0;
+    }
+    T[e] = fix_value((unsigned long long)__double_as_longlong(T[e]), h, fq, col);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -186,32 +183,29 @@ int sweep_group_sums(lfe_ctx* c) {
     a.la = layout_args(c);
     a.X = c->L.X;
     a.w = c->L.w;
-    for (int f = 0; f < c->F; ++f) a.G[f] = c->fe[f].G;
     for (int f = 0; f < c->F; ++f) {
-      LFE_HIP(hipMemsetAsync(c->fe[f].W, 0, sizeof(double) * c->fe[f].G, c->stream));
-      a.out[f] = c->fe[f].W;
+      a.G[f] = c->fe[f].G;
+      a.hi[f] = c->fe[f].hi;
     }
-    // exact like S when sums4 formed the weighted quanta (columns p: w, p + 1: y)
-    const bool wq = c->exact_sums && c->p + 2 <= kMaxCols;
-    a.fq = wq ? c->fixq : nullptr;
-    a.fcol = c->p;
-    a.src = SRC_WEIGHT;
-    LFE_TRY(run_sums(c, a));
-    for (int f = 0; f < c->F; ++f) {
-      LFE_HIP(hipMemsetAsync(c->fe[f].Sy, 0, sizeof(double) * c->fe[f].G, c->stream));
-      a.out[f] = c->fe[f].Sy;
-    }
-    a.fcol = c->p + 1;
-    a.src = SRC_Y;
-    LFE_TRY(run_sums(c, a));
-    if (wq)
+    // two-limb fixed point like S, with the quanta sums4 formed from the weighted statistics
+    // (columns p: w, p + 1: y); W and Sy share the coarse-limb tables, one after the other
+    a.fq = c->fixq;
+    for (int pass = 0; pass < 2; ++pass) {
       for (int f = 0; f < c->F; ++f) {
-        hipLaunchKernelGGL(k_fix_convert1, dim3(grid_for(c->fe[f].G)), dim3(kBlock), 0, c->stream, c->fe[f].W,
-                           (int64_t)c->fe[f].G, c->fixq, c->p);
-        hipLaunchKernelGGL(k_fix_convert1, dim3(grid_for(c->fe[f].G)), dim3(kBlock), 0, c->stream, c->fe[f].Sy,
-                           (int64_t)c->fe[f].G, c->fixq, c->p + 1);
-        LFE_HIP(hipGetLastError());
+        double* out = pass == 0 ? c->fe[f].W : c->fe[f].Sy;
+        LFE_HIP(hipMemsetAsync(out, 0, sizeof(double) * c->fe[f].G, c->stream));
+        a.out[f] = out;
       }
+      a.fcol = c->p + pass;
+      a.src = pass == 0 ? SRC_WEIGHT : SRC_Y;
+      LFE_TRY(hi_begin(c));
+      LFE_TRY(run_sums(c, a));
+      for (int f = 0; f < c->F; ++f)
+        hipLaunchKernelGGL(k_fix_convert1, dim3(grid_for(c->fe[f].G)), dim3(kBlock), 0, c->stream, a.out[f],
+                           c->fe[f].hi, (int64_t)c->fe[f].G, c->fixq, a.fcol);
+      LFE_HIP(hipGetLastError());
+      hi_end(c);
+    }
     for (int f = 0; f < c->F; ++f) {
       LFE_TRY(allreduce_sum_f64(c, c->fe[f].W, c->fe[f].G));
       LFE_TRY(allreduce_sum_f64(c, c->fe[f].Sy, c->fe[f].G));

@@ -137,6 +137,17 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                 z_ones[z] = z_ones[z] and bool(np.allclose(np.asarray(cols[z], dtype=np.float64), 1.0))
             eng.load([Y] + Xc, codes, levels, w)
             n_initial = Y.size
+        cl_loaded = None
+        if sharded and len(fe_cols) == 2 and weights is None and os.environ.get("LEANFE_HIP_RESHARD", "1") != "0":
+            # contiguous row blocks -> owner-sharded rows (lfe_reshard_owner): every rank then holds
+            # all rows of a range of the primary FE's levels, and a sweep all-reduces only the other
+            # FE's table.  Cluster columns load first, so that they move with their rows.
+            if v == "cluster":
+                cl_loaded = _load_clusters(eng, cols, cluster_cols, sharded)
+            try:
+                eng.reshard_owner(max(range(2), key=lambda f: levels[f]))
+            except ValueError:  # a rank would hold no rows: every rank keeps its block (nothing moved)
+                pass
         t_load = time.perf_counter() - t0
         n_obs, fe_dims, fe_card = eng.drop_singletons()
         fe_cardinality = dict(zip(fe_cols, fe_card))
@@ -198,7 +209,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         df_resid = n_obs - (k + 1) - absorbed_df
         if instruments:
             beta, se, n_clusters, rss, stats = _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v,
-                                                       any(z_ones.values()), sharded, n_obs, df_resid, ssc)
+                                                       any(z_ones.values()), sharded, n_obs, df_resid, ssc, cl_loaded)
             timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
             return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta))),
                                 std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
@@ -234,7 +245,8 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         elif v == "hc1":
             se = inference.se_hc1(Vb, meat, n_obs, df_resid)
         else:
-            se, n_clusters = _cluster_se(eng, cols, cluster_cols, sharded, Vb, lambda M: M, n_obs, df_resid, ssc)
+            se, n_clusters = _cluster_se(eng, cols, cluster_cols, sharded, Vb, lambda M: M, n_obs, df_resid, ssc,
+                                         cl_loaded)
         tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
         r_squared = 1 - rss / tss if tss > 0 else None
         timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
@@ -318,10 +330,8 @@ def _beta_agrees(beta_dev, beta_host, rtol: float = 1e-10) -> bool:
     return bool(np.all(np.isfinite(beta_dev))) and float(np.max(np.abs(beta_dev - beta_host))) <= rtol * scale
 
 
-def _cluster_se(eng, cols, cluster_cols, sharded, Vb, to_meat, n_obs, df_resid, ssc):
-    """One-way (std_errors.py:289-347) or CGM multi-way (:354-441) SEs from the device's
-    score meats; ``to_meat`` maps a device meat to the estimator's space (identity for
-    OLS, gamma' M_Z gamma for IV, :473-602)."""
+def _load_clusters(eng, cols, cluster_cols, sharded):
+    """Cluster columns -> dense codes on the device (in the loaded rows' order)."""
     cl_codes, cl_levels = [], []
     for c in cluster_cols:
         cc, gg = frame.factorize(cols[c], global_codes=sharded, device=None if sharded else eng)
@@ -329,6 +339,16 @@ def _cluster_se(eng, cols, cluster_cols, sharded, Vb, to_meat, n_obs, df_resid, 
         cl_levels.append(gg)
     cl_levels = dist.agree_levels(eng, cl_levels)
     eng.load_clusters(cl_codes, cl_levels)
+    return cl_levels
+
+
+def _cluster_se(eng, cols, cluster_cols, sharded, Vb, to_meat, n_obs, df_resid, ssc, loaded=None):
+    """One-way (std_errors.py:289-347) or CGM multi-way (:354-441) SEs from the device's
+    score meats; ``to_meat`` maps a device meat to the estimator's space (identity for
+    OLS, gamma' M_Z gamma for IV, :473-602).  ``loaded``: the cluster columns are on the
+    device already (they moved with the rows of an owner re-shard)."""
+    if loaded is None:
+        _load_clusters(eng, cols, cluster_cols, sharded)
     if len(cluster_cols) == 1:
         meats, Gs = eng.cluster_meat()
         return inference.se_cluster_oneway(Vb, to_meat(meats[0]), int(Gs[0]), n_obs, df_resid, ssc)
@@ -339,7 +359,8 @@ def _cluster_se(eng, cols, cluster_cols, sharded, Vb, to_meat, n_obs, df_resid, 
                                          n_obs, df_resid, ssc)
 
 
-def _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, z_has_ones, sharded, n_obs, df_resid, ssc):
+def _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, z_has_ones, sharded, n_obs, df_resid, ssc,
+            cl_loaded=None):
     """IV/2SLS branch of ``_run_regression`` (polars_impl.py:176-200, 229, 254-270):
     the device Gram of [1, y~, x~, z~] -> host 2SLS (inference.IVSystem) -> one device
     residual pass r = y~ - X_hat beta_full with u = [1, x~, z~] meats / scores -> the
@@ -355,7 +376,8 @@ def _iv_fit(eng, cols, x_cols, instruments, cluster_cols, v, z_has_ones, sharded
     elif v == "hc1":
         se = inference.se_hc1(XtX_inv, iv.xhat_meat(meat_u), n_obs, df_resid)
     else:
-        se, n_clusters = _cluster_se(eng, cols, cluster_cols, sharded, XtX_inv, iv.xhat_meat, n_obs, df_resid, ssc)
+        se, n_clusters = _cluster_se(eng, cols, cluster_cols, sharded, XtX_inv, iv.xhat_meat, n_obs, df_resid, ssc,
+                                     cl_loaded)
     strip = len(iv.beta_full) == k + 1
     beta = iv.beta_full[1:] if strip else iv.beta_full
     se = se[1:] if strip else se

@@ -42,3 +42,19 @@ def test_config5_500m_rows_one_gpu_vs_c_oracle():
     import config_runs
 
     _check(config_runs.run(5, repeat=2))
+
+
+@pytest.mark.timeout(1500)
+def test_config5_500m_rows_emulated_ranks_vs_c_oracle():
+    """configs[4] as specified: 500M rows sharded over 2, 4 and 8 ranks (owner-sharded, the
+    bench's default for two FEs; and contiguous row blocks at 8 ranks, whose primary-FE tables are
+    all-reduced every sweep), through the engine's multi-rank code in an emulated group on one GPU
+    (about 12.5 GB per rank at 8).  Integers equal to the C oracle, beta / SE at 1e-10, every rank
+    bit-identical, every rank's repeat bit-identical (polars_impl.py:490-526)."""
+    import config_runs
+
+    lines = config_runs.run_multirank(5, combos=(("owner", 2), ("owner", 4), ("owner", 8), ("rows", 8)))
+    for line in lines:
+        assert line["ints_equal"], line
+        assert line["max_rel_beta"] < 1e-10 and line["max_rel_se"] < 1e-10, line
+        assert line["ranks_bit_identical"] and line["repeat_bit_identical"], line

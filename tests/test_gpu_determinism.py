@@ -1,16 +1,14 @@
-"""Deterministic reductions on the headline path.
+"""Deterministic reductions (no f64 atomics on the parity path).
 
-The two-FE fast path's group sums accumulate each column as round(x / quantum) in int64
-(lfe_fast.hip, k_sums2_raw / k_fix_quanta), the T_Q run sums are reduced in bucket order and
-the Gram / meat partials in block order, so solving the same panel twice must give
-bit-identical beta, SE, RSS and `iterations` - within one context and across two contexts.
-The general sweeps (F >= 3, large secondary FE, one bucket) sum their group sums and cross
-terms in int64 too, so unweighted fits there are bit-reproducible as well, and so are weighted
-fits whose weights pass the fixed-point guard; the cluster score sums keep f64 atomics
-(DESIGN.md §5).
-The exact path must also keep parity with the CPU restatement (oracle/altproj.py,
-polars_impl.py:468-537) at the usual 1e-10 bar, and a column whose range defeats the fixed
-point (one huge outlier) must fall back to the f64 sums and still match."""
+Every group sum, weight sum and cross term of the demeaning loop is a two-limb fixed-point sum
+(lfe_internal.h: a fine int64 limb per value, and a coarse integer-valued f64 limb that only
+outliers and non-finite values touch), the T_Q run sums are reduced in bucket order, the Gram /
+meat partials in block order and the cluster scores in sorted order, so solving the same panel
+twice must give bit-identical beta, SE, RSS and `iterations` - within one context and across
+two contexts, whatever the data's range: a column with one value 1e9 x its RMS, a heavy-tailed
+weight column and an FE level with a huge effect included.  Each case also keeps parity with
+the CPU restatement (oracle/altproj.py, polars_impl.py:468-537) at 1e-10 with equal
+`iterations` (the integer the stop test at polars_impl.py:511-526 produces)."""
 from __future__ import annotations
 
 import os
@@ -73,41 +71,85 @@ def _fit_pair(data, xs):
     return b, s, r.iterations
 
 
-def test_exact_sums_keep_oracle_parity_and_outlier_falls_back():
+def _fit_pair_fe(data, xs, fes, **kw):
+    from leanfe_amd import leanfe_hip
+    from oracle import altproj
+
+    vcov = kw.pop("vcov", "HC1")
+    r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov=vcov, quiet=True, device=0,
+                   **kw)
+    o = altproj.fit(data, "y", xs, fes, vcov=vcov, **kw)
+    b = np.array([r.coefs[x] for x in xs])
+    s = np.array([r.std_errors[x] for x in xs])
+    assert r.iterations == o["iterations"] and r.n_obs == o["n_obs"], (r.iterations, o["iterations"])
+    np.testing.assert_allclose(b, o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(s, o["se"], rtol=1e-10, atol=0)
+    return b, s, r.iterations
+
+
+def _twice(data, xs, fes, **kw):
+    b1, s1, it1 = _fit_pair_fe(data, xs, fes, **dict(kw))
+    b2, s2, it2 = _fit_pair_fe(data, xs, fes, **dict(kw))
+    np.testing.assert_array_equal(b1, b2)
+    np.testing.assert_array_equal(s1, s2)
+    assert it1 == it2
+
+
+def _with_outlier(data, col, row, value):
+    data = dict(data)
+    x = np.array(data[col], copy=True)
+    x[row] = value
+    data[col] = x
+    return data
+
+
+@pytest.mark.parametrize("value", [1e6, 1e9, -3e12])
+def test_outlier_column_is_bit_identical_and_keeps_parity(value):
+    """One value far outside the column's range (max |x| >> 64 RMS) used to make the fit fall back
+    to f64 atomic sums; the coarse limb now carries it and the fit repeats bit for bit."""
     from leanfe_amd import synth
 
     xs = [f"x{j + 1}" for j in range(6)]
     data = synth.panel(400_000, 6, [8_000, 300], seed=4242)
-    b1, s1, it1 = _fit_pair(data, xs)
-    b2, s2, it2 = _fit_pair(data, xs)
-    np.testing.assert_array_equal(b1, b2)
-    np.testing.assert_array_equal(s1, s2)
-    assert it1 == it2
-    # one value 1e6 x the column's RMS: max|x| > 64 RMS, so that fit takes the f64 sums
-    data = dict(data)
-    x3 = np.array(data["x3"], copy=True)
-    x3[12345] = 1e6
-    data["x3"] = x3
-    _fit_pair(data, xs)
+    _twice(data, xs, ["fe1", "fe2"])
+    _twice(_with_outlier(data, "x3", 12345, value), xs, ["fe1", "fe2"])
 
 
-def test_outlier_column_reports_f64_sums():
+def test_outlier_y_reports_exact_sums():
     from leanfe_amd import synth
     from leanfe_amd._lib import Engine
 
     data = synth.panel(200_000, 3, [5_000, 200], seed=99)
     cols = [np.ascontiguousarray(data[c], dtype=np.float64) for c in ["y", "x1", "x2", "x3"]]
-    cols[2] = cols[2].copy()
-    cols[2][7] = 1e9
+    cols[0] = cols[0].copy()
+    cols[0][7] = 1e9
     codes = [np.ascontiguousarray(data[f], dtype=np.int32) for f in ["fe1", "fe2"]]
     with Engine(0) as eng:
         eng.load(cols, codes, [5_000, 200])
         eng.drop_singletons()
-        assert not eng.exact_sums()
-        eng.load([np.ascontiguousarray(data[c], dtype=np.float64) for c in ["y", "x1", "x2", "x3"]], codes,
-                 [5_000, 200])
-        eng.drop_singletons()
         assert eng.exact_sums()
+
+
+@pytest.mark.parametrize("case", ["x_outlier", "large_effect_level", "heavy_tail"])
+def test_general_sweeps_with_outliers_keep_parity(case):
+    """F = 3 (lfe_seg.hip): an x outlier, one FE level whose effect is 1e8 x the others (its rows'
+    cross terms take the coarse limb) and a heavy-tailed regressor (Student t, 1 dof):
+    two solves bit-identical, beta / SE at 1e-10 of the oracle with equal iterations."""
+    from leanfe_amd import synth
+
+    L = [30_000, 4_000, 300]
+    data = dict(synth.panel(600_000, 3, L, seed=2718))
+    xs = ["x1", "x2", "x3"]
+    fes = ["fe1", "fe2", "fe3"]
+    if case == "x_outlier":
+        data = _with_outlier(data, "x2", 4321, 5e9)
+    elif case == "large_effect_level":
+        y = np.array(data["y"], copy=True)
+        y[np.asarray(data["fe2"]) == 17] += 1e8
+        data["y"] = y
+    else:
+        data["x1"] = np.random.default_rng(11).standard_t(1.0, size=600_000)
+    _twice(data, xs, fes)
 
 
 @pytest.mark.parametrize("n,L,vcov", [(1_500_000, [60_000, 8_000, 500], "HC1"),   # config 4's shape (F = 3)
@@ -129,12 +171,13 @@ def test_general_sweeps_are_bit_identical(n, L, vcov):
         np.testing.assert_array_equal([r.std_errors[x] for x in xs], [runs[0].std_errors[x] for x in xs])
 
 
-@pytest.mark.parametrize("L,skew", [([20_000, 500], False), ([30_000, 2_000, 300], False), ([20_000, 500], True)])
+@pytest.mark.parametrize("L,skew", [([20_000, 500], False), ([30_000, 2_000, 300], False), ([20_000, 500], True),
+                                    ([30_000, 2_000, 300], True)])
 def test_weighted_fits_are_bit_identical_and_keep_parity(L, skew):
-    """Weighted fits sum w x, w and the stop test's raw y in int64 too (quanta from the statistics
-    of k_col_stats_w; k_sums4, k_sweep_sums and the weighted cross terms of k_seg_cross), so two
-    solves agree bit for bit and still match the oracle at 1e-10.  A weight column that defeats
-    the fixed point (one weight 1e6 x the rest) reports the f64 sums and still matches."""
+    """Weighted fits sum w x, w and the stop test's raw y in two-limb fixed point too (quanta from
+    the statistics of k_col_stats_w; k_sums4, k_sweep_sums and the weighted cross terms of
+    k_seg_cross), so two solves agree bit for bit and still match the oracle at 1e-10 - also with
+    one weight 1e6 x the rest."""
     from leanfe_amd import leanfe_hip, synth
     from leanfe_amd._lib import Engine
     from oracle import altproj
@@ -151,12 +194,11 @@ def test_weighted_fits_are_bit_identical_and_keep_parity(L, skew):
         for _ in range(2):
             runs.append(leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", weights="w",
                                    vcov="HC1", quiet=True, engine=eng))
-            assert eng.exact_sums() == (not skew)
-    if not skew:
-        r0, r1 = runs
-        assert r1.iterations == r0.iterations and r1.n_obs == r0.n_obs
-        np.testing.assert_array_equal([r1.coefs[x] for x in xs], [r0.coefs[x] for x in xs])
-        np.testing.assert_array_equal([r1.std_errors[x] for x in xs], [r0.std_errors[x] for x in xs])
+            assert eng.exact_sums()
+    r0, r1 = runs
+    assert r1.iterations == r0.iterations and r1.n_obs == r0.n_obs
+    np.testing.assert_array_equal([r1.coefs[x] for x in xs], [r0.coefs[x] for x in xs])
+    np.testing.assert_array_equal([r1.std_errors[x] for x in xs], [r0.std_errors[x] for x in xs])
     o = altproj.fit(data, "y", xs, fes, vcov="HC1", weights="w")
     r = runs[0]
     assert r.iterations == o["iterations"] and r.n_obs == o["n_obs"]

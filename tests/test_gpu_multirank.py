@@ -131,6 +131,24 @@ def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe, owne
         np.testing.assert_array_equal(res["se"], out[0]["se"])
 
 
+@pytest.mark.parametrize("world,n,k,levels,cluster_fe", [
+    (2, 200_000, 3, (3000, 200, 9), 1),          # F = 3 sweeps + key-indexed score table
+    (3, 250_001, 5, (30000, 120), (0, 1)),       # two-way CGM through the key-indexed table
+])
+def test_emulated_key_indexed_clusters_repeat_bit_identically(world, n, k, levels, cluster_fe, monkeypatch):
+    """The multi-rank key-indexed cluster table is filled from each rank's sorted cluster sums
+    (one store per cluster, k_cl_dense_put) instead of per-row f64 atomics: two solves give the
+    same bits on every rank."""
+    monkeypatch.setenv("LFE_CL_OWNER_MIN_SPAN", str(1 << 40))
+    a = _run_group(world, n, k, list(levels), "cluster", cluster_fe, 17)
+    b = _run_group(world, n, k, list(levels), "cluster", cluster_fe, 17)
+    for r in range(world):
+        assert a[r]["iterations"] == b[r]["iterations"]
+        np.testing.assert_array_equal(a[r]["beta"], b[r]["beta"])
+        np.testing.assert_array_equal(a[r]["se"], b[r]["se"])
+        np.testing.assert_array_equal(a[r]["se"], a[0]["se"])
+
+
 def _run_owned(world, n_total, k, levels, vcov, seed):
     """Owner-sharded ranks: rank r generates every row of the panel whose primary-FE code lies in
     dist.owner_range(G_P, r, world) (strong scaling: n_total rows in all)."""
@@ -249,3 +267,72 @@ def test_sharded_leanfe_hip_auto_strategy_with_small_fes(monkeypatch):
         assert res.iterations == o["iterations"] and res.n_obs == o["n_obs"] and res.df_resid == o["df_resid"]
         np.testing.assert_allclose([res.coefs[x] for x in xs], o["beta"], rtol=1e-10, atol=0)
         np.testing.assert_allclose([res.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("world,n,k,levels,vcov,cl", [
+    (2, 400_003, 5, [20000, 500], "HC1", None),
+    (4, 600_000, 3, [30000, 300], "iid", None),
+    (3, 300_000, 3, [20000, 700], "cluster", ["fe2"]),   # the cluster column moves with its rows
+])
+def test_emulated_contiguous_blocks_reshard_to_owners(world, n, k, levels, vcov, cl, monkeypatch):
+    """leanfe_hip(engine=<sharded engine>) on contiguous row blocks (INTEGRATION.md §4's call):
+    lfe_reshard_owner moves the rows so that every rank holds all rows of a range of the
+    primary FE's levels, cut where the all-reduced counts balance the rows (not the levels);
+    the owner-sharded sweeps then run (polars_impl.py:490-526), and every rank returns the
+    oracle's whole-panel fit, bit-identical across ranks and across two runs."""
+    from leanfe_amd import dist, leanfe_hip
+    from leanfe_amd._lib import EmuGroup, Engine
+    from oracle import altproj
+
+    # skew the primary FE's level populations: equal level ranges would not balance the rows
+    full = dict(synth.panel(n, k, levels, seed=23))
+    fe1 = np.asarray(full["fe1"]).copy()
+    fe1[: n // 3] = fe1[: n // 3] % (levels[0] // 10)  # a third of the rows in the first tenth of the levels
+    full["fe1"] = fe1
+    xs = [f"x{j + 1}" for j in range(k)]
+    monkeypatch.setattr(dist, "agree_levels", lambda eng, lv: [max(a, b) for a, b in zip(lv, levels)])
+
+    def run():
+        group = EmuGroup(world)
+        out, errs = {}, {}
+
+        def worker(rank):
+            try:
+                lo, hi = shard_range(n, rank, world)
+                eng = Engine(0)
+                eng.set_emu(group, rank)
+                eng.dist_group = ("emulated",)
+                shard = {c: np.asarray(v)[lo:hi] for c, v in full.items()}
+                r = leanfe_hip(shard, y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], vcov=vcov, cluster_cols=cl,
+                               strategy="alt_proj", quiet=True, engine=eng)
+                _, codes = eng.copy_inputs()
+                out[rank] = dict(res=r, rows=eng.n, owner=eng.owner, fe1=(int(codes[0].min()), int(codes[0].max())))
+                eng.close()
+            except BaseException as e:  # noqa: BLE001
+                errs[rank] = e
+
+        threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=300)
+        assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+        if errs:
+            raise next(iter(errs.values()))
+        return out
+
+    a, b = run(), run()
+    o = altproj.fit(full, "y", xs, ["fe1", "fe2"], vcov=vcov, cluster_cols=cl)
+    counts = np.bincount(fe1, minlength=levels[0])
+    assert sum(a[r]["rows"] for r in range(world)) == n
+    assert max(a[r]["rows"] for r in range(world)) - min(a[r]["rows"] for r in range(world)) <= 2 * counts.max()
+    for r in range(world):
+        fe, lo, hi = a[r]["owner"]
+        assert fe == 0 and lo <= a[r]["fe1"][0] and a[r]["fe1"][1] < hi
+        res = a[r]["res"]
+        assert res.iterations == o["iterations"] and res.n_obs == o["n_obs"] and res.df_resid == o["df_resid"]
+        np.testing.assert_allclose([res.coefs[x] for x in xs], o["beta"], rtol=1e-10, atol=0)
+        np.testing.assert_allclose([res.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
+        for other in (a[0]["res"], b[r]["res"]):  # every rank, and a second run, give the same bits
+            np.testing.assert_array_equal([res.coefs[x] for x in xs], [other.coefs[x] for x in xs])
+            np.testing.assert_array_equal([res.std_errors[x] for x in xs], [other.std_errors[x] for x in xs])

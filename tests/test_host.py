@@ -193,6 +193,30 @@ def test_library_loads_and_exports_every_symbol():
     assert b"gfx950" in lib.lfe_version()
 
 
+def test_library_is_built_from_the_checked_out_sources(tmp_path):
+    """build.py stamps the hash of every engine source into the library (lfe_build_hash) and the
+    loader refuses a library whose stamp differs, so a stale build cannot run silently."""
+    from leanfe_amd import build as B
+    from leanfe_amd import _lib
+
+    B.build(verbose=False)  # content-hash incremental: a no-op when the library is current
+    lib = ctypes.CDLL(B.LIB)
+    lib.lfe_build_hash.restype = ctypes.c_char_p
+    assert lib.lfe_build_hash().decode() == B.source_hash() == B.library_hash()
+    stale = tmp_path / "liblfe_hip.so"
+    stale.write_bytes(open(B.LIB, "rb").read().replace(B.source_hash().encode(), b"0" * 32))
+    assert B.library_hash(str(stale)) == "0" * 32
+    old = _lib.LIB_PATH
+    try:  # the loader's check, pointed at the stale copy
+        _lib.LIB_PATH = str(stale)
+        saved, _lib._lib = _lib._lib, None
+        with pytest.raises(ImportError, match="other sources"):
+            _lib.load_library()
+    finally:
+        _lib.LIB_PATH = old
+        _lib._lib = saved
+
+
 @pytest.mark.parametrize("weighted,z_ones", [(False, False), (True, False), (False, True)])
 def test_iv_system_matches_oracle_2sls(weighted, z_ones):
     """inference.IVSystem (2SLS from the (p+1)^2 Gram of [1, y, x, z] plus the u-space

@@ -74,13 +74,105 @@ def run(cfg: int, rows: int | None = None, repeat: int = 2) -> dict:
     return line
 
 
+def _same_fit(x: dict, y: dict) -> bool:
+    return (x["iterations"] == y["iterations"] and x["n_obs"] == y["n_obs"] and np.array_equal(x["beta"], y["beta"])
+            and np.array_equal(x["se"], y["se"]))
+
+
+def run_multirank(cfg: int, combos=(("owner", 2), ("owner", 4), ("owner", 8)), rows: int | None = None) -> list[dict]:
+    """The config through the engine's multi-rank code: ``world`` contexts on one GPU joined in an
+    emulated group (EmuGroup: the collective calls of RCCL, in the same order, reduced through host
+    memory), each holding its shard of the panel (``owner``: every row of a range of primary-FE
+    levels, as bench.py --shard owner; ``rows``: contiguous row blocks) and running
+    ``bench.solve_step`` twice.  Every rank is compared with the C oracle on the whole panel, with
+    rank 0 (bit-identical) and with its own repeat (bit-identical)."""
+    import threading
+
+    from leanfe_amd import dist
+    from leanfe_amd._lib import EmuGroup
+
+    a = bench.parse(["--config", str(cfg)] + (["--rows", str(rows)] if rows else []))
+    n_cl = len(a.cl) if a.cl else 0
+    eng = Engine(0)
+    eng.synth_load(a.rows, a.k, a.levels, synth.betas(a.k), seed=a.seed)
+    cols, codes = eng.copy_inputs()
+    eng.close()
+    threads = default_threads()
+    t0 = time.perf_counter()
+    o = fit_c(list(cols), list(codes), a.levels, vcov=a.vcov, threads=threads,
+              cl_codes=[codes[f] for f in a.cl] if n_cl else None,
+              cl_levels=[a.levels[f] for f in a.cl] if n_cl else None)
+    cpu_s = time.perf_counter() - t0
+    del cols, codes
+    P = max(range(len(a.levels)), key=lambda f: a.levels[f])
+    lines = []
+    for shard, world in combos:
+        group = EmuGroup(world)
+        out, errs = {}, {}
+
+        def worker(rank):
+            try:
+                e = Engine(0)
+                e.set_emu(group, rank)
+                if shard == "owner":
+                    lo, hi = dist.owner_range(a.levels[P], rank, world)
+                    e.synth_load_owned(a.rows, a.k, a.levels, synth.betas(a.k), P, lo, hi, seed=a.seed)
+                else:
+                    lo, hi = dist.shard_range(a.rows, rank, world)
+                    e.synth_load(hi - lo, a.k, a.levels, synth.betas(a.k), seed=a.seed, row_offset=lo)
+                if n_cl:
+                    _, cd = e.copy_inputs()
+                    e.load_clusters([np.ascontiguousarray(cd[f]) for f in a.cl], [a.levels[f] for f in a.cl])
+                first = bench.solve_step(e, a.vcov, n_cl)
+                e.sync()
+                t = time.perf_counter()
+                second = bench.solve_step(e, a.vcov, n_cl)
+                e.sync()
+                out[rank] = dict(first=first, second=second, rows=e.n, seconds=time.perf_counter() - t)
+                e.close()
+            except BaseException as ex:  # noqa: BLE001
+                errs[rank] = ex
+
+        ths = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=600)
+        if any(t.is_alive() for t in ths):
+            raise RuntimeError(f"emulated group of {world} deadlocked")
+        if errs:
+            raise next(iter(errs.values()))
+        r0 = out[0]["first"]
+        line = dict(config=cfg, rows=a.rows, world=world, shard=shard, k=a.k, levels=a.levels, vcov=a.vcov,
+                    rows_per_rank=[out[r]["rows"] for r in range(world)],
+                    iterations=r0["iterations"], cpu_iterations=o["iterations"], cpu_seconds=round(cpu_s, 2),
+                    emulated_solve_seconds_max=round(max(out[r]["seconds"] for r in range(world)), 4),
+                    max_rel_beta=max(rel(out[r]["first"]["beta"], o["beta"]) for r in range(world)),
+                    max_rel_se=max(rel(out[r]["first"]["se"], o["se"]) for r in range(world)),
+                    ints_equal=all(out[r]["first"]["iterations"] == o["iterations"]
+                                   and out[r]["first"]["n_obs"] == o["n_obs"]
+                                   and out[r]["first"]["df_resid"] == o["df_resid"] for r in range(world)),
+                    ranks_bit_identical=all(_same_fit(out[r]["first"], r0) for r in range(world)),
+                    repeat_bit_identical=all(_same_fit(out[r]["first"], out[r]["second"]) for r in range(world)),
+                    beta_dev_vs_host=max(out[r]["first"]["beta_dev_vs_host"] for r in range(world)))
+        assert sum(line["rows_per_rank"]) == a.rows, line
+        print(json.dumps(line), flush=True)
+        lines.append(line)
+    return lines
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="1,2,3,4")
     ap.add_argument("--rows", type=int, default=None, help="override the config's row count")
+    ap.add_argument("--worlds", default=None, help="emulated multi-rank groups instead, e.g. 2,4,8")
+    ap.add_argument("--shards", default="owner", help="owner and/or rows")
     a = ap.parse_args()
     for c in [int(x) for x in a.configs.split(",")]:
-        run(c, a.rows)
+        if a.worlds:
+            run_multirank(c, [(sh, int(w)) for sh in a.shards.split(",") for w in a.worlds.split(",")], a.rows)
+        else:
+            run(c, a.rows)
 
 
 if __name__ == "__main__":
