@@ -235,23 +235,35 @@ int lfe_copy_inputs(lfe_ctx* ctx, double* const* cols_out, int32_t* const* codes
 
 /* Out-of-core X (data larger than HBM; SURVEY.md §8f rank 4, the role of scan_parquet /
  * DuckDB's disk-backed tables, polars_impl.py:341-343, duckdb_impl.py:417-452).  The FE codes
- * stay resident (with their layouts: ~22 bytes per row); the p data columns are streamed in
- * row chunks through three passes, each a sequence of lfe_stream_rows calls covering rows
- * [0, n) exactly once between lfe_stream_begin and lfe_stream_end:
- *   pass 1 (after lfe_drop_singletons): the group sums S_f of polars_impl.py:491-508 and the
- *          raw Gram of the tables (exact int64 per chunk, folded in chunk order);
- *   lfe_demean, then lfe_gram (the Gram from the group tables; LFE_ENEEDPASS when it is
- *          unavailable or fails its guard: then pass 3, the Gram of [1, y~, x~]);
+ * (and weights) stay resident with their layouts; the p data columns are streamed in row chunks
+ * through the passes below, each a sequence of lfe_stream_rows calls covering rows [0, n)
+ * exactly once between lfe_stream_begin and lfe_stream_end:
+ *   pass 1 (after lfe_drop_singletons): the group sums S_f of polars_impl.py:491-508 (weighted:
+ *          of w x, with W_f = sum w and the unweighted y sums of the stop test) and the raw Gram
+ *          of the tables, two-limb fixed point per chunk, folded in chunk order;
+ *   lfe_demean (any number of FEs, weighted or not), then lfe_gram (the Gram from the group
+ *          tables; LFE_ENEEDPASS when it is unavailable - three or more FEs, weights - or fails
+ *          its guard: then pass 3, the Gram of sqrt(w) [1, y~, x~], polars_impl.py:201-209);
  *   pass 2 (beta_full = [intercept, beta]): the residual (polars_impl.py:229), RSS / TSS and the
- *          HC1 meat (std_errors.py:217-282).
- * Two FEs, unweighted, p <= 11, IID / HC1 (cluster scores are not streamed).  cols = p column
- * pointers of `rows` doubles each (kind LFE_HOST / LFE_DEVICE).  lfe_stream_end's `out`:
- * pass 2: stats[4] then the (p-1)^2 meat; pass 3: the (p+1)^2 Gram; pass 1: unused. */
+ *          HC1 meat (std_errors.py:217-282); pass 4 (the 2SLS coefficients of u = [1, x~, z~]):
+ *          the IV residual and its meat over u (std_errors.py:448-602);
+ *   clustered SEs: lfe_load_clusters (input order) and lfe_stream_clusters(subset masks) before
+ *          pass 2 / 4, whose chunks then add their score rows into per-cluster sums; then
+ *          lfe_stream_cluster_meats (std_errors.py:289-441).
+ * p <= 11.  cols = p column pointers of `rows` doubles each (kind LFE_HOST / LFE_DEVICE).
+ * lfe_stream_end's `out`: pass 2: stats[4] then the (p-1)^2 meat; pass 4: stats[4] then the p^2
+ * meat; pass 3: the (p+1)^2 Gram; pass 1: unused. */
 int lfe_load_codes(lfe_ctx* ctx, int64_t n, int p, int F, const int32_t* const* fe_codes,
-                   const int32_t* n_levels, int kind);
+                   const int32_t* n_levels, const double* weights_or_null, int kind);
 int lfe_stream_begin(lfe_ctx* ctx, int pass, const double* beta_full);
 int lfe_stream_rows(lfe_ctx* ctx, int64_t row0, int64_t rows, const double* const* cols, int kind);
 int lfe_stream_end(lfe_ctx* ctx, double* out);
+/* Clustered SEs of a streamed fit: every subset (bit j = loaded cluster column j) factorized on the
+ * device once (its intersection, std_errors.py:399-408); the residual passes then fill the
+ * per-cluster score sums.  meats_out: n_subsets blocks of ks x ks (ks = p - 1, or p after pass 4);
+ * G_out: clusters per subset (among kept rows). */
+int lfe_stream_clusters(lfe_ctx* ctx, int n_subsets, const int32_t* masks);
+int lfe_stream_cluster_meats(lfe_ctx* ctx, double* meats_out, int64_t* G_out);
 /* Benchmark / test helpers: lfe_synth_load's panel with only the codes resident, and one chunk
  * of its columns generated on the device and streamed through the current pass. */
 int lfe_synth_load_codes(lfe_ctx* ctx, int64_t n, int k, int n_fe, const int32_t* n_levels, uint64_t seed);

@@ -61,7 +61,9 @@ SIGNATURES = {
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
-    "lfe_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.POINTER(_vp), _i32p, C.c_int]),
+    "lfe_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.POINTER(_vp), _i32p, _dp, C.c_int]),
+    "lfe_stream_clusters": (C.c_int, [_vp, C.c_int, _i32p]),
+    "lfe_stream_cluster_meats": (C.c_int, [_vp, _dp, _i64p]),
     "lfe_stream_begin": (C.c_int, [_vp, C.c_int, _dp]),
     "lfe_stream_rows": (C.c_int, [_vp, C.c_int64, C.c_int64, C.POINTER(_vp), C.c_int]),
     "lfe_stream_end": (C.c_int, [_vp, _dp]),
@@ -430,13 +432,16 @@ class Engine:
         _check(self._lib.lfe_sync(self._h))
 
     # -- out-of-core X: codes resident, columns streamed in row chunks ----
-    def load_codes(self, codes: list[np.ndarray], levels: list[int], p: int) -> None:
-        """FE codes of n rows (input order); the p data columns come later in chunks."""
+    def load_codes(self, codes: list[np.ndarray], levels: list[int], p: int,
+                   weights: np.ndarray | None = None) -> None:
+        """FE codes (and weights) of n rows (input order); the p data columns come later in chunks."""
         codes = [np.ascontiguousarray(c, dtype=np.int32) for c in codes]
         n = codes[0].size if codes else 0
         kp = (_vp * max(len(codes), 1))(*[_ptr(c) for c in codes])
         lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
-        _check(self._lib.lfe_load_codes(self._h, n, int(p), len(codes), kp, lv, LFE_HOST))
+        w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
+        _check(self._lib.lfe_load_codes(self._h, n, int(p), len(codes), kp, lv,
+                                        None if w is None else w.ctypes.data_as(_dp), LFE_HOST))
         self.p, self.F, self.n = int(p), len(codes), n
         self.owner = None
 
@@ -453,8 +458,23 @@ class Engine:
         cp = (_vp * len(cols))(*[_ptr(c) for c in cols])
         _check(self._lib.lfe_stream_rows(self._h, int(row0), rows, cp, LFE_HOST))
 
+    def stream_clusters(self, subsets: list[int]) -> None:
+        """Factorize every cluster subset (bit mask over the loaded cluster columns) for the
+        streamed residual passes' score sums (lfe_stream_clusters)."""
+        m = (C.c_int32 * len(subsets))(*[int(s) for s in subsets])
+        _check(self._lib.lfe_stream_clusters(self._h, len(subsets), m))
+        self._stream_subsets = len(subsets)
+
+    def stream_cluster_meats(self, ks: int) -> tuple[np.ndarray, np.ndarray]:
+        """(meats [n_subsets][ks][ks], cluster counts) after a streamed residual pass."""
+        ns = self._stream_subsets
+        meats = np.zeros((ns, ks, ks), dtype=np.float64)
+        G = np.zeros(ns, dtype=np.int64)
+        _check(self._lib.lfe_stream_cluster_meats(self._h, meats.ctypes.data_as(_dp), G.ctypes.data_as(_i64p)))
+        return meats, G
+
     def stream_end(self) -> np.ndarray:
-        out = np.zeros(max(4 + (self.p - 1) ** 2, (self.p + 1) ** 2), dtype=np.float64)
+        out = np.zeros(max(4 + self.p ** 2, (self.p + 1) ** 2), dtype=np.float64)
         _check(self._lib.lfe_stream_end(self._h, out.ctypes.data_as(C.POINTER(C.c_double))))
         return out
 

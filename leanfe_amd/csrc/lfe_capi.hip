@@ -423,6 +423,7 @@ static void free_data(lfe_ctx* c) {
   dfree(c->sw.sdbl);
   dfree(c->sw.tile);
   dfree(c->sw.toff);
+  free_stream_clusters(c);
   c->sw = lfe_ctx::StreamWS();
   dfree(c->dspec);
   c->dspec_elems = 0;
@@ -708,15 +709,16 @@ int lfe_load(lfe_ctx* c, int64_t n, int p, const double* const* cols, int F, con
 // out-of-core X: codes resident, the data columns streamed in row chunks
 // ---------------------------------------------------------------------------
 int lfe_load_codes(lfe_ctx* c, int64_t n, int p, int F, const int32_t* const* fe_codes, const int32_t* n_levels,
-                   int kind) {
+                   const double* weights, int kind) {
   LFE_CTX(c);
-  if (F != 2) return fail(LFE_EINVAL, "streamed X (lfe_load_codes) supports two fixed effects");
+  if (F < 1 || F > kMaxFE) return fail(LFE_EINVAL, "streamed X (lfe_load_codes) needs 1 to 8 fixed effects");
   if (!n_levels || (n > 0 && !fe_codes)) return fail(LFE_EINVAL, "null input pointer");
   if (p > 11) return fail(LFE_EINVAL, "streamed X supports p <= 11 columns (y plus up to 10 regressors)");
   if (kind != LFE_HOST && kind != LFE_DEVICE) return fail(LFE_EINVAL, "kind must be LFE_HOST or LFE_DEVICE");
-  LFE_TRY(alloc_data(c, n, p, F, n_levels, false, true));
+  LFE_TRY(alloc_data(c, n, p, F, n_levels, weights != nullptr, true));
   const hipMemcpyKind mk = kind == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
   hipError_t e = hipSuccess;
+  if (weights && n > 0) e = hipMemcpyAsync(c->w, weights, sizeof(double) * n, mk, c->stream);
   for (int f = 0; f < F && n > 0 && e == hipSuccess; ++f)
     e = hipMemcpyAsync(c->fe[f].code, fe_codes[f], sizeof(int32_t) * n, mk, c->stream);
   if (e != hipSuccess) {
@@ -732,15 +734,22 @@ int lfe_stream_begin(lfe_ctx* c, int pass, const double* beta_full) {
   LFE_CTX(c);
   auto& w = c->sw;
   if (!w.on) return fail(LFE_ESTATE, "lfe_stream_*: the context holds resident columns (use lfe_load_codes)");
-  if (pass < 1 || pass > 3) return fail(LFE_EINVAL, "pass must be 1 (group sums), 2 (residual) or 3 (design Gram)");
+  if (pass < 1 || pass > 4)
+    return fail(LFE_EINVAL, "pass must be 1 (group sums), 2 (residual), 3 (design Gram) or 4 (IV residual)");
   if (!c->prepared) return fail(LFE_ESTATE, "lfe_drop_singletons first");
-  if (pass == 1 && !fast_layout_ok(c))
-    return fail(LFE_EINVAL, "streamed X needs the two-FE layouts (the larger FE above 256 levels, the smaller "
-                            "within the LDS tables)");
   if (pass > 1 && !c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
-  if (pass == 2) {
+  if (pass == 2 || pass == 4) {
     if (!beta_full) return fail(LFE_EINVAL, "beta_full is null");
     LFE_TRY(h2d_small(c, c->dbeta, beta_full, sizeof(double) * c->p));
+    w.icpt = pass == 4 ? 1 : 0;
+    if (!w.cid.empty()) {  // clustered SEs: zeroed per-cluster score sums of width ks
+      w.ks = c->p - 1 + w.icpt;
+      for (size_t s = 0; s < w.cid.size(); ++s) {
+        const size_t m = (size_t)std::max(w.G[s], 1) * std::max(w.ks, 1);
+        LFE_TRY(ensure_f64(c, w.S[s], w.S_cap[s], m));
+        LFE_HIP(hipMemsetAsync(w.S[s], 0, sizeof(double) * m, c->stream));
+      }
+    }
   }
   if (pass > 1) {
     LFE_TRY(ensure_f64(c, w.tile, w.tile_cap, 272));
@@ -749,6 +758,23 @@ int lfe_stream_begin(lfe_ctx* c, int pass, const double* beta_full) {
   if (pass == 1) c->sums_ready = c->raw_ready = false;
   w.pass = pass;
   w.rows_done = 0;
+  return LFE_OK;
+}
+
+// one streamed chunk (columns in c->sw.x, leading dimension cld) through the current pass
+static int stream_chunk(lfe_ctx* c, int64_t cld, int64_t row0, int64_t rows) {
+  auto& w = c->sw;
+  PhaseTimer t(c, w.pass == 1 ? PH_PREP : w.pass == 3 ? PH_GRAM : PH_RESID);
+  if (w.pass == 1) {
+    LFE_TRY(stream_sums_chunk(c, w.x, cld, row0, rows, w.rows_done == 0));
+  } else {
+    const bool resid = w.pass == 2 || w.pass == 4;
+    const bool scored = resid && !w.cid.empty();
+    if (scored) LFE_TRY(ensure_f64(c, w.sc, w.sc_cap, (size_t)std::max<int64_t>(rows, 1) * std::max(w.ks, 1)));
+    LFE_TRY(stream_rows_chunk(c, resid ? 0 : 1, resid ? w.icpt : 0, w.x, cld, row0, rows, scored ? w.sc : nullptr));
+    if (scored) LFE_TRY(stream_clusters_chunk(c, row0, rows));
+  }
+  w.rows_done += rows;
   return LFE_OK;
 }
 
@@ -767,10 +793,7 @@ int lfe_stream_rows(lfe_ctx* c, int64_t row0, int64_t rows, const double* const*
     if (!cols[j]) return fail(LFE_EINVAL, "null column pointer");
     LFE_HIP(hipMemcpyAsync(w.x + (size_t)j * cld, cols[j], sizeof(double) * rows, mk, c->stream));
   }
-  PhaseTimer t(c, w.pass == 1 ? PH_PREP : w.pass == 2 ? PH_RESID : PH_GRAM);
-  if (w.pass == 1) LFE_TRY(stream_sums_chunk(c, w.x, cld, row0, rows, w.rows_done == 0));
-  else LFE_TRY(stream_rows_chunk(c, w.pass == 2 ? 0 : 1, w.x, cld, row0, rows));
-  w.rows_done += rows;
+  LFE_TRY(stream_chunk(c, cld, row0, rows));
   if (kind == LFE_HOST) LFE_HIP(hipStreamSynchronize(c->stream));  // the caller may reuse its buffers
   return LFE_OK;
 }
@@ -798,10 +821,7 @@ int lfe_stream_synth_rows(lfe_ctx* c, int64_t row0, int64_t rows, int k, const i
   const int64_t cld = (rows + 63) / 64 * 64;
   LFE_TRY(ensure_f64(c, w.x, w.x_cap, (size_t)c->p * cld));
   LFE_TRY(synth_chunk(c, k, n_levels, beta, seed, row0, rows, w.x, cld));
-  PhaseTimer t(c, w.pass == 1 ? PH_PREP : w.pass == 2 ? PH_RESID : PH_GRAM);
-  if (w.pass == 1) LFE_TRY(stream_sums_chunk(c, w.x, cld, row0, rows, w.rows_done == 0));
-  else LFE_TRY(stream_rows_chunk(c, w.pass == 2 ? 0 : 1, w.x, cld, row0, rows));
-  w.rows_done += rows;
+  LFE_TRY(stream_chunk(c, cld, row0, rows));
   return LFE_OK;
 }
 
@@ -816,22 +836,44 @@ int lfe_stream_end(lfe_ctx* c, double* out) {
   if (pass == 1) {
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
     if (c->n > 0) LFE_HIP(hipMemcpyAsync(c->raw_tile, w.tile, sizeof(double) * 256, hipMemcpyDeviceToDevice, c->stream));
-    c->raw_ready = c->sums_ready = true;
+    // the raw Gram tile stands for the Gram from the group tables only in the unweighted two-FE case
+    c->raw_ready = c->F == 2 && !c->w;
+    c->sums_ready = true;
     c->sums_zeroed = false;
+    LFE_TRY(stream_weight_stats(c));
+    c->exact_sums = true;
     return LFE_OK;
   }
   if (!out) return fail(LFE_EINVAL, "out is null");
   std::vector<double> h(260);
   LFE_TRY(d2h_sync(c, h.data(), w.tile, sizeof(double) * 260));
-  if (pass == 2) {  // stats[4] (sum r^2 w, sum r^2, sum y~, sum y~^2), then the k x k HC1 meat
+  if (pass == 2 || pass == 4) {  // stats[4] (sum r^2 w, sum r^2, sum y~, sum y~^2), then the HC1 meat
+    const int km = k + (pass == 4 ? 1 : 0);  // pass 4: over u = [1, x~, z~]
     for (int e = 0; e < 4; ++e) out[e] = h[256 + e];
-    for (int i = 0; i < k; ++i)
-      for (int j = 0; j < k; ++j) out[4 + i * k + j] = h[(size_t)(1 + i) * 16 + (1 + j)];
+    for (int i = 0; i < km; ++i)
+      for (int j = 0; j < km; ++j) out[4 + i * km + j] = h[(size_t)(1 + i) * 16 + (1 + j)];
   } else {  // the (p + 1) x (p + 1) Gram of [1, y~, x~]
     for (int i = 0; i <= p; ++i)
       for (int j = 0; j <= p; ++j) out[i * (p + 1) + j] = h[(size_t)i * 16 + j];
   }
   return LFE_OK;
+}
+
+int lfe_stream_clusters(lfe_ctx* c, int n_subsets, const int32_t* masks) {
+  LFE_CTX(c);
+  if (!c->sw.on) return fail(LFE_ESTATE, "lfe_stream_clusters: the context holds resident columns");
+  if (!c->prepared) return fail(LFE_ESTATE, "lfe_drop_singletons first");
+  if (n_subsets < 1 || !masks) return fail(LFE_EINVAL, "bad subsets");
+  return stream_clusters_prep(c, n_subsets, masks);
+}
+
+int lfe_stream_cluster_meats(lfe_ctx* c, double* meats_out, int64_t* G_out) {
+  LFE_CTX(c);
+  if (c->sw.cid.empty() || c->sw.ks == 0)
+    return fail(LFE_ESTATE, "lfe_stream_clusters and a residual pass (2 or 4) first");
+  if (!meats_out || !G_out) return fail(LFE_EINVAL, "null output pointer");
+  PhaseTimer t(c, PH_CLUSTER);
+  return stream_cluster_meats(c, meats_out, G_out);
 }
 
 int lfe_load_begin(lfe_ctx* c, int64_t n, int p, int F, const int32_t* n_levels, int weighted) {

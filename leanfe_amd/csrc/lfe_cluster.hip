@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void k_count_nonzero(const int32_t* __restrict
 // Clusters of sorted (key, row) pairs [0, n) (dropped rows carry key = drop and sort
 // last): segment offsets in W.seg_off, S[h] = sum of the rows' records (row-major
 // [.][k] `table`) in c->clS; *G_out clusters.
-static int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R,
+int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R,
                         const double* table, int k, int32_t* G_out) {
   auto& W = c->clw;
   LFE_TRY(ensure_i32(c, W.seg_off, W.seg_off_cap, (size_t)n + 1));

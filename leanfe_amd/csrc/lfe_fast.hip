@@ -779,36 +779,41 @@ int sums4(lfe_ctx* c) {
 }
 
 // ---------------------------------------------------------------------------
-// out-of-core X: group sums and raw Gram of one streamed row chunk (lfe_stream.hip)
+// out-of-core X: group sums and raw Gram of one streamed row chunk
 // ---------------------------------------------------------------------------
-// The chunk's rows in input order (no partition): lane (kq, c) holds column c of rows
-// 16 g + 4 kq + r as in k_sums2_raw; every FE's sums go to global tables (int64 on the exact
-// path, f64 otherwise), the shifted raw Gram to one MFMA chain per row.  A row is kept iff every
-// FE's pre-filter count of its code exceeds 1 (the single-pass drop, polars_impl.py:477-482).
+// The chunk's rows in input order (no partition): lane (kq, c) holds "column" c of rows
+// 16 g + 4 kq + r as in k_sums2_raw.  Column c < p adds x_c (weighted: w x_c, polars_impl.py:496);
+// weighted fits add two more: c = p the weight (W_f), c = p + 1 the raw y (Sy_f, the unweighted
+// stop test).  Every FE's sums go to the chunk tables [G_f][pw] in two-limb fixed point (fine
+// limbs in s64, coarse limbs in sdbl), the shifted raw Gram of the unweighted two-FE case to one
+// MFMA chain per row.  A row is kept iff every FE's pre-filter count of its code exceeds 1 (the
+// single-pass drop, polars_impl.py:477-482).
 struct StreamSumsArgs {
   const double* X;  // [p][ld] chunk columns
   int64_t ld, rows;
-  int p, F;
+  int p, F, pw;                    // pw: table columns (p, or p + 2 weighted)
   const int32_t* code[kMaxFE];     // the chunk's codes (input order)
   const int32_t* cnt_pre[kMaxFE];  // pre-filter counts (all rows)
   int64_t toff[kMaxFE];            // table offset (entries) of FE f in s64 / sdbl
+  const double* w;                 // the chunk's weights (null: unweighted)
   unsigned long long* s64;
   double* sdbl;
-  const double* fixq;   // the chunk's quanta (k_fix_quanta)
+  const double* fixq;   // the chunk's quanta (k_fix_quanta, pw columns)
   const double* shift;  // [16] raw-Gram shift
   double* raw_part;     // [blocks][256]
 };
 
-template <int NF>
 __global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kq = lane >> 4, c = lane & 15;
-  const int p = a.p;
-  const bool col = c < p;
+  const int p = a.p, pw = a.pw, F = a.F;
+  const bool col = c < pw;
   const FixCol fc = col ? fix_col(a.fixq, c) : FixCol{};
-  const double cm = col ? 1.0 : 0.0;
-  const double zc = (c == 15 ? 1.0 : 0.0) - (col ? a.shift[c] : 0.0);
-  const double* __restrict__ xc = a.X + (int64_t)(col ? c : 0) * a.ld;
+  // the raw Gram (unweighted): z = x - shift on the data lanes, 1 on lane 15 (intercept)
+  const bool dcol = c < p;
+  const double cm = dcol ? 1.0 : 0.0;
+  const double zc = (c == 15 ? 1.0 : 0.0) - (dcol ? a.shift[c] : 0.0);
+  const double* __restrict__ xc = a.X + (int64_t)(c < p ? c : 0) * a.ld;  // lane p + 1 (Sy): column 0 = y
   d4 racc = d4{0.0, 0.0, 0.0, 0.0};
   const int64_t ngroups = (a.rows + 15) >> 4;
   for (int64_t g = (int64_t)blockIdx.x * 4 + wave; g < ngroups; g += (int64_t)gridDim.x * 4) {
@@ -816,23 +821,33 @@ __global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
     for (int r = 0; r < 4; ++r) {
       const int64_t row = g * 16 + kq * 4 + r;
       bool keep = row < a.rows;
-      int32_t gc[NF];
+      int32_t gc[kMaxFE];
 #pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        gc[f] = keep ? a.code[f][row] : 0;
-        keep = keep && a.cnt_pre[f][gc[f]] > 1;
+      for (int f = 0; f < kMaxFE; ++f) {
+        gc[f] = 0;
+        if (f < F) {
+          gc[f] = keep ? a.code[f][row] : 0;
+          keep = keep && a.cnt_pre[f][gc[f]] > 1;
+        }
       }
       const double xv = row < a.rows ? xc[row] : 0.0;
       const double z = keep ? __builtin_fma(xv, cm, zc) : 0.0;
       racc = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc, 0, 0, 0);
       if (keep && col) {  // two-limb fixed point: fine limbs in s64, coarse limbs in sdbl
+        double v = xv;
+        if (a.w) {
+          const double wi = a.w[row];
+          v = c < p ? xv * wi : (c == p ? wi : xv);
+        }
         double hh;
-        const unsigned long long xi = fix_split(xv, fc, hh);
+        const unsigned long long xi = fix_split(v, fc, hh);
 #pragma unroll
-        for (int f = 0; f < NF; ++f) atomicAdd(&a.s64[a.toff[f] + (int64_t)gc[f] * p + c], xi);
+        for (int f = 0; f < kMaxFE; ++f)
+          if (f < F) atomicAdd(&a.s64[a.toff[f] + (int64_t)gc[f] * pw + c], xi);
         if (hh != 0.0)
 #pragma unroll
-          for (int f = 0; f < NF; ++f) atomicAdd(&a.sdbl[a.toff[f] + (int64_t)gc[f] * p + c], hh);
+          for (int f = 0; f < kMaxFE; ++f)
+            if (f < F) atomicAdd(&a.sdbl[a.toff[f] + (int64_t)gc[f] * pw + c], hh);
       }
     }
   }
@@ -851,15 +866,20 @@ __global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
   for (int e = tid; e < 256; e += 256) a.raw_part[(int64_t)blockIdx.x * 256 + e] = rred[e];
 }
 
-// S_f += the chunk's sums (in chunk order: deterministic), the chunk tables cleared for the next
+// S_f (W_f, Sy_f) += the chunk's sums (in chunk order: deterministic), the chunk tables cleared
+// for the next; dst: per FE [0] S, [1] W, [2] Sy
 __global__ void k_stream_fold(unsigned long long* __restrict__ s64, double* __restrict__ sdbl, int64_t m, int p,
-                              const double* __restrict__ fq, int F, const int64_t* __restrict__ toff_end,
-                              double* const* __restrict__ S) {
+                              int pw, const double* __restrict__ fq, int F, const int64_t* __restrict__ toff_end,
+                              double* const* __restrict__ dst) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
     int f = 0;
     while (f + 1 < F && e >= toff_end[f]) ++f;
     const int64_t j = e - (f ? toff_end[f - 1] : 0);
-    S[f][j] += fix_value(s64[e], sdbl[e], fq, (int)(j % p));
+    const int64_t g = j / pw;
+    const int cc = (int)(j % pw);
+    const double v = fix_value(s64[e], sdbl[e], fq, cc);
+    if (cc < p) dst[3 * f][g * p + cc] += v;
+    else dst[3 * f + (cc - p + 1)][g] += v;
     s64[e] = 0ull;
     sdbl[e] = 0.0;
   }
@@ -886,16 +906,19 @@ void stream_tile_add(lfe_ctx* c, const double* t, int m) {
 
 // One streamed chunk of the sums pass: [p][ld] columns on the device (rows rows starting at
 // input row row0).  Column statistics and quanta of this chunk (as k_part_scatter / sums4 form
-// them), then int64 group sums into the chunk tables and their fold into S in chunk order.
+// them), then two-limb group sums into the chunk tables and their fold into S (W, Sy) in chunk
+// order.
 int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows, bool first) {
   auto& w = c->sw;
   const int p = c->p, F = c->F;
+  const bool wt = c->w != nullptr;
+  const int pw = p + (wt ? 2 : 0);
   int64_t m = 0;
   std::vector<int64_t> tend(F);
   StreamSumsArgs a{};
   for (int f = 0; f < F; ++f) {
     a.toff[f] = m;
-    m += (int64_t)c->fe[f].G * p;
+    m += (int64_t)c->fe[f].G * pw;
     tend[f] = m;
     a.code[f] = c->fe[f].code + row0;
     a.cnt_pre[f] = c->fe[f].cnt_pre;
@@ -910,21 +933,34 @@ int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int
     LFE_HIP(hipMemsetAsync(w.sdbl, 0, sizeof(double) * m, c->stream));
     LFE_TRY(ensure_f64(c, w.tile, w.tile_cap, 272));
     LFE_HIP(hipMemsetAsync(w.tile, 0, sizeof(double) * 272, c->stream));
-    LFE_TRY(ensure_f64(c, w.toff, w.toff_cap, 2 * kMaxFE));
+    LFE_TRY(ensure_f64(c, w.toff, w.toff_cap, 4 * kMaxFE));
     LFE_TRY(h2d_small(c, w.toff, tend.data(), sizeof(int64_t) * F));
-    std::vector<double*> sp(F);
-    for (int f = 0; f < F; ++f) sp[f] = c->fe[f].S;
-    LFE_TRY(h2d_small(c, w.toff + kMaxFE, sp.data(), sizeof(double*) * F));
+    std::vector<double*> dst(3 * F);
+    for (int f = 0; f < F; ++f) {
+      dst[3 * f] = c->fe[f].S;
+      dst[3 * f + 1] = c->fe[f].W;
+      dst[3 * f + 2] = c->fe[f].Sy;
+      if (wt) {
+        LFE_HIP(hipMemsetAsync(c->fe[f].W, 0, sizeof(double) * c->fe[f].G, c->stream));
+        LFE_HIP(hipMemsetAsync(c->fe[f].Sy, 0, sizeof(double) * c->fe[f].G, c->stream));
+      }
+    }
+    LFE_TRY(h2d_small(c, w.toff + kMaxFE, dst.data(), sizeof(double*) * 3 * F));
   }
+  const double* wch = wt ? c->w + row0 : nullptr;
   {
     ProfScope _ps(c, K_FIX_SUMS);
     constexpr int64_t kStatRows = 16384;
     const int nch = (int)std::max<int64_t>(1, (rows + kStatRows - 1) / kStatRows);
-    LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nch * p));
+    LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nch * pw));
     LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
-    hipLaunchKernelGGL(k_col_stats, dim3(nch), dim3(256), 0, c->stream, X, ld, rows, p, kStatRows, c->colstat);
+    if (wt)
+      hipLaunchKernelGGL(k_col_stats_w, dim3(nch), dim3(256), 0, c->stream, X, wch, ld, rows, p, kStatRows,
+                         c->colstat);
+    else
+      hipLaunchKernelGGL(k_col_stats, dim3(nch), dim3(256), 0, c->stream, X, ld, rows, p, kStatRows, c->colstat);
     LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, (size_t)kFqRows * kFqCols));
-    hipLaunchKernelGGL(k_fix_quanta, dim3(p), dim3(256), 0, c->stream, c->colstat, nch, rows,
+    hipLaunchKernelGGL(k_fix_quanta, dim3(pw), dim3(256), 0, c->stream, c->colstat, nch, rows,
                        c->iscratch + kIscratchCmax, c->F, c->fixq);
     LFE_HIP(hipGetLastError());
   }
@@ -933,6 +969,8 @@ int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int
   a.rows = rows;
   a.p = p;
   a.F = F;
+  a.pw = pw;
+  a.w = wch;
   a.s64 = reinterpret_cast<unsigned long long*>(w.s64);
   a.sdbl = w.sdbl;
   a.fixq = c->fixq;
@@ -943,23 +981,36 @@ int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int
   a.raw_part = c->raw_part;
   {
     ProfScope _ps(c, K_GROUP_SUMS);
-    if (F != 2) {
-      set_error("streamed X passes support two fixed effects");
-      return LFE_EINVAL;
-    }
-    hipLaunchKernelGGL(k_stream_sums<2>, dim3(nblocks), dim3(256), 0, c->stream, a);
+    hipLaunchKernelGGL(k_stream_sums, dim3(nblocks), dim3(256), 0, c->stream, a);
     LFE_HIP(hipGetLastError());
   }
   {
     ProfScope _ps(c, K_FIX_SUMS);
     hipLaunchKernelGGL(k_stream_fold, dim3(grid_for(m)), dim3(kBlock), 0, c->stream,
-                       reinterpret_cast<unsigned long long*>(w.s64), w.sdbl, m, p, c->fixq, F,
+                       reinterpret_cast<unsigned long long*>(w.s64), w.sdbl, m, p, pw, c->fixq, F,
                        reinterpret_cast<const int64_t*>(w.toff), reinterpret_cast<double* const*>(w.toff + kMaxFE));
     LFE_HIP(hipGetLastError());
     reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
     hipLaunchKernelGGL(k_tile_add, dim3(1), dim3(256), 0, c->stream, w.tile, c->raw_tile, 256);
     LFE_HIP(hipGetLastError());
   }
+  return LFE_OK;
+}
+
+// after the sums pass of a weighted streamed fit: the weight column's max and rms over every row
+// into the quanta table's column p (the weighted cross terms' bound, k_cross_quanta)
+int stream_weight_stats(lfe_ctx* c) {
+  if (!c->w) return LFE_OK;
+  constexpr int64_t kStatRows = 16384;
+  const int nch = (int)std::max<int64_t>(1, (c->n + kStatRows - 1) / kStatRows);
+  LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nch));
+  LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
+  hipLaunchKernelGGL(k_col_stats, dim3(nch), dim3(256), 0, c->stream, c->w, c->ld, c->n, 1, kStatRows, c->colstat);
+  // one block = column 0 of a table that starts at column p of fixq
+  hipLaunchKernelGGL(k_fix_quanta, dim3(1), dim3(256), 0, c->stream, c->colstat, nch, c->n,
+                     c->iscratch + kIscratchCmax, c->F, c->fixq + c->p);
+  LFE_HIP(hipGetLastError());
+  c->exact_sums = true;
   return LFE_OK;
 }
 

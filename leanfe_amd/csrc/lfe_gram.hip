@@ -1217,31 +1217,38 @@ static int resid_rows(lfe_ctx* c, GramArgs a, double* meat, double* stats) {
 }
 
 // ---------------------------------------------------------------------------
-// out-of-core X: residual / design-Gram pass over one streamed chunk (lfe_stream.hip)
+// out-of-core X: residual / design-Gram pass over one streamed chunk
 // ---------------------------------------------------------------------------
-// Row per lane in input order; x~ = x - alpha_P[h] - alpha_Q[q] with the alpha rows gathered
-// from the global tables (L2 / MALL resident; the pass is bound by the host link, not by
-// these gathers).  MODE 0: r = y~ - beta0 - sum_j beta_j x~_j, RSS / TSS statistics and the HC1
-// meat (as k_resid_rows: tile (1 + i, 1 + j) = meat (i, j), stats at 256..259); MODE 1: the
-// Gram of [1, y~, x~] (as k_design_rows: column 0 = intercept, 1 + c = data column c).
+// Row per lane in input order; x~ = x - sum_f alpha_f[g_f] with the alpha rows gathered from the
+// global tables (L2 / MALL resident; the pass is bound by the host link, not by these gathers).
+// MODE 0: r = y~ - beta0 - sum_j beta_j x~_j (unweighted residual, polars_impl.py:229), the
+// statistics (sum w r^2, sum r^2, sum y~, sum y~^2) and the meat sum w r^2 u u' over u = x~ (IC 0)
+// or u = [1, x~, z~] (IC 1, the IV residual of std_errors.py:448-602) - tile (1 + i, 1 + j) =
+// meat (i, j), stats at 256..259 - and, with `scores`, the chunk's score rows u r w ([rows][ks]);
+// MODE 1: the Gram of sqrt(w) [1, y~, x~] (as k_design_rows: column 0 = intercept, 1 + c = data
+// column c, polars_impl.py:201-209).
 struct StreamRowArgs {
   const double* X;
   int64_t ld, rows;
-  int p;
-  const int32_t* code[2];
-  const int32_t* cnt_pre[2];
-  const double* alpha[2];
-  const double* beta;  // MODE 0: [p] beta_full
+  int p, F;
+  const int32_t* code[kMaxFE];
+  const int32_t* cnt_pre[kMaxFE];
+  const double* alpha[kMaxFE];
+  const double* w;     // the chunk's weights (null: unweighted)
+  const double* beta;  // MODE 0: [p] beta_full (IC 1: the coefficients of u)
+  double* scores;      // MODE 0: [rows][ks] score rows, or null
+  int ks;
 };
 
-template <int PM, int MODE>
+template <int PM, int MODE, int IC>
 __global__ __launch_bounds__(256) void k_stream_rows(StreamRowArgs a, double* __restrict__ partial) {
-  constexpr int KM = PM - 1;
+  constexpr int KM = PM - 1 + IC;  // meat width (u)
   constexpr int NM = MODE == 0 ? KM * (KM + 1) / 2 : (PM + 1) * (PM + 2) / 2;  // meat / Gram of [1, d]
   constexpr int NS = MODE == 0 ? 4 : 0;
   __shared__ double red[4][NM + NS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int p = a.p;
+  const int p = a.p, F = a.F;
+  const int km = p - 1 + IC;  // live meat columns
   double beta[PM];
 #pragma unroll
   for (int cc = 0; cc < PM; ++cc) beta[cc] = (MODE == 0 && cc < p) ? a.beta[cc] : 0.0;
@@ -1250,35 +1257,66 @@ __global__ __launch_bounds__(256) void k_stream_rows(StreamRowArgs a, double* __
   for (int e = 0; e < NM; ++e) m[e] = 0.0;
   double st[4] = {0.0, 0.0, 0.0, 0.0};
   for (int64_t row = (int64_t)blockIdx.x * 256 + tid; row < a.rows; row += (int64_t)gridDim.x * 256) {
-    const int32_t g0 = a.code[0][row], g1 = a.code[1][row];
-    if (!(a.cnt_pre[0][g0] > 1 && a.cnt_pre[1][g1] > 1)) continue;  // dropped singleton
-    const double* a0 = a.alpha[0] + (int64_t)g0 * p;
-    const double* a1 = a.alpha[1] + (int64_t)g1 * p;
+    bool keep = true;
+    int32_t g[kMaxFE];
+#pragma unroll
+    for (int f = 0; f < kMaxFE; ++f) {
+      g[f] = 0;
+      if (f < F) {
+        g[f] = a.code[f][row];
+        keep = keep && a.cnt_pre[f][g[f]] > 1;
+      }
+    }
+    if (!keep) {  // dropped singleton (its score row stays zero)
+      if (MODE == 0 && a.scores)
+        for (int j = 0; j < km; ++j) a.scores[row * a.ks + j] = 0.0;
+      continue;
+    }
     double xt[PM];
 #pragma unroll
-    for (int cc = 0; cc < PM; ++cc) xt[cc] = cc < p ? a.X[(int64_t)cc * a.ld + row] - a0[cc] - a1[cc] : 0.0;
+    for (int cc = 0; cc < PM; ++cc) xt[cc] = cc < p ? a.X[(int64_t)cc * a.ld + row] : 0.0;
+#pragma unroll
+    for (int f = 0; f < kMaxFE; ++f) {
+      if (f >= F) continue;
+      const double* af = a.alpha[f] + (int64_t)g[f] * p;
+#pragma unroll
+      for (int cc = 0; cc < PM; ++cc)
+        if (cc < p) xt[cc] -= af[cc];
+    }
+    const double wi = a.w ? a.w[row] : 1.0;
     if (MODE == 0) {
       double res = xt[0] - beta[0];  // polars_impl.py:229
 #pragma unroll
       for (int cc = 1; cc < PM; ++cc) res -= beta[cc] * xt[cc];
       const double rr = res * res;
-      st[0] += rr;
+      st[0] += a.w ? wi * rr : rr;
       st[1] += rr;
       st[2] += xt[0];
       st[3] += xt[0] * xt[0];
+      const double mr = a.w ? res * sqrt(wi) : res;
+      double u[KM];
+#pragma unroll
+      for (int j = 0; j < KM; ++j) u[j] = IC ? (j == 0 ? 1.0 : xt[j]) : xt[j + 1];
+      if (a.scores) {
+        const double sc = a.w ? res * wi : res;
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+          if (j < km) a.scores[row * a.ks + j] = u[j] * sc;
+      }
       double wv[KM];
 #pragma unroll
-      for (int j = 0; j < KM; ++j) wv[j] = xt[j + 1] * res;
+      for (int j = 0; j < KM; ++j) wv[j] = u[j] * mr;
       int e = 0;
 #pragma unroll
       for (int i = 0; i < KM; ++i)
 #pragma unroll
         for (int j = i; j < KM; ++j, ++e) m[e] += wv[i] * wv[j];
     } else {
+      const double sw = a.w ? sqrt(wi) : 1.0;  // X_w = X sqrt(w), polars_impl.py:202-203
       double d[PM + 1];
-      d[0] = 1.0;
+      d[0] = sw;
 #pragma unroll
-      for (int cc = 0; cc < PM; ++cc) d[cc + 1] = xt[cc];
+      for (int cc = 0; cc < PM; ++cc) d[cc + 1] = xt[cc] * sw;
       int e = 0;
 #pragma unroll
       for (int i = 0; i <= PM; ++i)
@@ -1323,12 +1361,14 @@ __global__ __launch_bounds__(256) void k_stream_rows(StreamRowArgs a, double* __
   }
 }
 
-// One streamed chunk of the residual (mode 0) or design-Gram (mode 1) pass: the chunk's tile
-// is added to c->sw.tile in chunk order.
-int stream_rows_chunk(lfe_ctx* c, int mode, const double* X, int64_t ld, int64_t row0, int64_t rows) {
+// One streamed chunk of the residual (mode 0; icpt 1: the IV residual over u = [1, x~, z~]) or
+// design-Gram (mode 1) pass: the chunk's tile is added to c->sw.tile in chunk order; `scores`
+// ([rows][ks], or null) receives the chunk's score rows for the cluster sums.
+int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t ld, int64_t row0, int64_t rows,
+                      double* scores) {
   const int p = c->p;
-  if (c->F != 2 || p > 11) {
-    set_error("streamed X passes support two fixed effects and p <= 11");
+  if (p > 11) {
+    set_error("streamed X passes support p <= 11");
     return LFE_EINVAL;
   }
   StreamRowArgs a{};
@@ -1336,22 +1376,29 @@ int stream_rows_chunk(lfe_ctx* c, int mode, const double* X, int64_t ld, int64_t
   a.ld = ld;
   a.rows = rows;
   a.p = p;
-  for (int f = 0; f < 2; ++f) {
+  a.F = c->F;
+  for (int f = 0; f < c->F; ++f) {
     a.code[f] = c->fe[f].code + row0;
     a.cnt_pre[f] = c->fe[f].cnt_pre;
     a.alpha[f] = c->fe[f].alpha;
   }
+  a.w = c->w ? c->w + row0 : nullptr;
   a.beta = c->dbeta;
+  a.scores = mode == 0 ? scores : nullptr;
+  a.ks = p - 1 + icpt;
   const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * 4, (rows + 255) / 256));
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * 260));
   {
     ProfScope _ps(c, mode == 0 ? K_GRAM_RESID : K_GRAM_DESIGN);
     const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
-#define SR(PM_, M_) hipLaunchKernelGGL((k_stream_rows<PM_, M_>), dim3(nblocks), dim3(256), 0, c->stream, a, c->scratch)
-    if (mode == 0) {
-      if (PM == 4) SR(4, 0); else if (PM == 8) SR(8, 0); else SR(12, 0);
+#define SR(PM_, M_, I_) \
+  hipLaunchKernelGGL((k_stream_rows<PM_, M_, I_>), dim3(nblocks), dim3(256), 0, c->stream, a, c->scratch)
+    if (mode == 0 && !icpt) {
+      if (PM == 4) SR(4, 0, 0); else if (PM == 8) SR(8, 0, 0); else SR(12, 0, 0);
+    } else if (mode == 0) {
+      if (PM == 4) SR(4, 0, 1); else if (PM == 8) SR(8, 0, 1); else SR(12, 0, 1);
     } else {
-      if (PM == 4) SR(4, 1); else if (PM == 8) SR(8, 1); else SR(12, 1);
+      if (PM == 4) SR(4, 1, 0); else if (PM == 8) SR(8, 1, 0); else SR(12, 1, 0);
     }
 #undef SR
     LFE_HIP(hipGetLastError());

@@ -316,8 +316,19 @@ struct lfe_ctx {
     size_t sdbl_cap = 0;
     double* tile = nullptr;  // [272] tile (+ statistics) accumulated over the chunks, in order
     size_t tile_cap = 0;
-    double* toff = nullptr;  // [2 kMaxFE] 8-byte slots: table ends (int64), table pointers
+    double* toff = nullptr;  // [4 kMaxFE] 8-byte slots: table ends (int64), S / W / Sy pointers per FE
     size_t toff_cap = 0;
+    int icpt = 0;            // pass 4: the IV residual over u = [1, x~, z~]
+    // clustered SEs (lfe_stream_clusters): every subset's dense cluster id per input row, and the
+    // per-cluster score sums the residual passes add in chunk order
+    std::vector<int32_t> masks;
+    std::vector<int32_t*> cid;   // [n] per subset (-1: dropped row)
+    std::vector<int32_t> G;      // clusters per subset
+    std::vector<double*> S;      // [G][ks] per subset
+    std::vector<size_t> S_cap;
+    int ks = 0;                  // score width of the sums in S
+    double* sc = nullptr;        // [rows][ks] the chunk's score rows
+    size_t sc_cap = 0;
   } sw;
   lfe::Timings tm;
   lfe::Prof prof;
@@ -358,7 +369,18 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
 int gram_spec_enqueue(lfe_ctx* c, int* queued);
 // out-of-core X (lfe_fast.hip / lfe_gram.hip): one streamed chunk ([p][ld] on the device)
 int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows, bool first);
-int stream_rows_chunk(lfe_ctx* c, int mode, const double* X, int64_t ld, int64_t row0, int64_t rows);
+int stream_weight_stats(lfe_ctx* c);
+// clustered SEs of streamed fits (lfe_stream.hip)
+int stream_clusters_prep(lfe_ctx* c, int n_subsets, const int32_t* masks);
+int stream_clusters_chunk(lfe_ctx* c, int64_t row0, int64_t rows);
+int stream_cluster_meats(lfe_ctx* c, double* meats, int64_t* G_out);
+void free_stream_clusters(lfe_ctx* c);
+// clusters of sorted (key, row) pairs: segment offsets in clw.seg_off, per-cluster sums of the rows'
+// records in c->clS (lfe_cluster.hip)
+int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R, const double* table,
+                 int k, int32_t* G_out);  // weighted streamed fits: w's max / rms into fixq column p
+int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t ld, int64_t row0, int64_t rows,
+                      double* scores);
 void stream_tile_add(lfe_ctx* c, const double* t, int m);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
 void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out);  // sum of [nblocks][256] tiles

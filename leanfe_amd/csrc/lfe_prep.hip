@@ -415,7 +415,9 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   }
   __syncthreads();
   // ---- move columns through the stage: gather in row order, store in bucket order ----
-  const int ncol = a.cols == 1 ? a.p + (a.w ? 1 : 0) : 0;  // cols 2: the codes only (streamed X)
+  // cols 1: X (and w) and the codes; cols 2 (streamed X): the codes and w only
+  const int ncol = a.cols == 1 ? a.p + (a.w ? 1 : 0) : (a.cols == 2 && a.w ? 1 : 0);
+  const int cbase = a.cols == 2 ? a.p : 0;  // column id of the first moved column (p: w)
   typedef double d2v __attribute__((ext_vector_type(2)));
   // rows i < n are loaded in 16-byte pairs: i is even and the columns are padded to a multiple
   // of 64 rows, so row i + 1 lies inside the column even when i + 1 == n.  A full chunk (every
@@ -502,14 +504,14 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
     // one register set: column c + 1 is loaded while column c is written out (two register
     // sets, loading c + 2 during c + 1's staging, measured 2.12 vs 2.09 ms)
     double v[PER];
-    if (ncol > 0) load_col(0, v);
-    for (int c = 0; c < ncol; ++c) {
+    if (ncol > 0) load_col(cbase, v);
+    for (int c = cbase; c < cbase + ncol; ++c) {
       stage_col(v);
 #ifndef LFE_NO_COLSTAT
       if (c < a.p) col_stats(v);
 #endif
       asm volatile("" ::: "memory");  // the next loads stay after the stage writes
-      if (c + 1 < ncol) load_col(c + 1, v);
+      if (c + 1 < cbase + ncol) load_col(c + 1, v);
       __syncthreads();
 #ifndef LFE_NO_COLSTAT
       if (c < a.p) col_stats_out(c);

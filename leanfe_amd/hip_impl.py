@@ -107,14 +107,16 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         if out_of_core is None:
             out_of_core = os.environ.get("LEANFE_HIP_OUT_OF_CORE", "0") == "1"
         if out_of_core:
-            if (len(fe_cols) != 2 or weights is not None or instruments or factor_vars or interactions
-                    or v == "cluster" or sharded or strategy not in ("auto", "alt_proj")):
-                raise ValueError("out_of_core fits take two FEs, no weights / instruments / factors / "
-                                 "clusters, vcov 'iid' or 'HC1' and strategy 'alt_proj'")
+            if (not fe_cols or factor_vars or interactions or sharded
+                    or strategy not in ("auto", "alt_proj", "demean")):
+                raise ValueError("out_of_core fits take one or more FEs, no factor / interaction terms, one "
+                                 "process, and strategy 'alt_proj' (or 'demean' for one FE)")
             source = data if stream else cols
             n_rows_oc = n_rows if stream else len(cols[y_col])
-            return _out_of_core_fit(eng, source, n_rows_oc, y_col, x_cols, fe_cols, codes, levels, v, vcov,
-                                    demean_tol, max_iter, int(chunk_rows), formula, t_start, say)
+            w_oc = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
+            return _out_of_core_fit(eng, source, cols, n_rows_oc, y_col, x_cols, instruments, fe_cols, codes, levels,
+                                    w_oc, cluster_cols, v, vcov, ssc, demean_tol, max_iter, int(chunk_rows),
+                                    formula, t_start, say)
         w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
         # polars_impl.py:180: an all-ones instrument stops 2SLS from adding an intercept to Z.
         # Demeaned instruments cannot be all ones; without FEs they are the raw columns.
@@ -264,18 +266,20 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                         rss=rss, tss=tss, backend="hip", timings=timings)
 
 
-def _out_of_core_fit(eng, source, n_rows, y_col, x_cols, fe_cols, codes, levels, v, vcov, demean_tol, max_iter,
-                     chunk_rows, formula, t_start, say) -> LeanFEResult:
-    """Out-of-core X (data larger than HBM): the FE codes and their layouts stay on the GPU, the
-    columns [y] + x are streamed from host memory (or a Parquet file, re-read per pass) in row
-    chunks through pass 1 (group sums S_f and the raw Gram, polars_impl.py:491-508), the
-    codes-only sweeps, the Gram from the group tables (pass 3, the explicit design Gram, when
-    that is unavailable), the host solve (:212-226) and pass 2 (residual, RSS and the HC1 meat,
-    :229, std_errors.py:217-282).  Same estimator, same stop rule and iterations."""
+def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_cols, codes, levels, w, cluster_cols,
+                     v, vcov, ssc, demean_tol, max_iter, chunk_rows, formula, t_start, say) -> LeanFEResult:
+    """Out-of-core X (data larger than HBM): the FE codes (and weights, cluster codes) and their
+    layouts stay on the GPU, the columns [y] + x (+ instruments) are streamed from host memory (or a
+    Parquet file, re-read per pass) in row chunks through pass 1 (group sums S_f, W_f,
+    polars_impl.py:491-508), the codes-only sweeps (any number of FEs), the Gram from the group
+    tables (pass 3, the explicit design Gram of sqrt(w) [1, y~, x~], when that is unavailable),
+    the host solve (:212-226; 2SLS for instruments, common.py:188-240) and pass 2 / 4 (residual,
+    RSS, the HC1 meat and the cluster scores, :229, std_errors.py:183-602).  Same estimator, same
+    stop rule and iterations as the resident fit."""
     from leanfe_amd._lib import NeedsStreamPass
 
-    num_cols = [y_col] + list(x_cols)
-    p, k = len(num_cols), len(x_cols)
+    num_cols = [y_col] + list(x_cols) + list(instruments)
+    p, k, mz = len(num_cols), len(x_cols), len(instruments)
     say("Using FWL/alternating projections strategy (out-of-core columns)...")
 
     def chunks():
@@ -287,39 +291,75 @@ def _out_of_core_fit(eng, source, n_rows, y_col, x_cols, fe_cols, codes, levels,
                 yield r0, [np.asarray(source[c][r0:r0 + chunk_rows], dtype=np.float64) for c in num_cols]
 
     t0 = time.perf_counter()
-    eng.load_codes(codes, levels, p)
+    eng.load_codes(codes, levels, p, weights=w)
+    subsets = None
+    if v == "cluster":
+        _load_clusters(eng, cols, cluster_cols, False)
+        subsets = inference.cluster_subsets(len(cluster_cols))
     t_load = time.perf_counter() - t0
     n_obs, fe_dims, fe_card = eng.drop_singletons()
     eng.stream_pass(1, chunks())
-    order = sorted(range(len(fe_cols)), key=lambda i: fe_card[i])  # polars_impl.py:485
-    iterations, _ = eng.demean(order, demean_tol, max_iter, check_from=3)
+    if len(fe_cols) == 1:
+        iterations, _ = eng.demean([0], demean_tol, max_iter, check_from=0)  # polars_impl.py:437-465
+    else:
+        order = sorted(range(len(fe_cols)), key=lambda i: fe_card[i])  # polars_impl.py:485
+        iterations, _ = eng.demean(order, demean_tol, max_iter, check_from=3)
     absorbed_df = sum(fe_dims) - len(fe_cols)
     df_resid = n_obs - (k + 1) - absorbed_df
+    if subsets is not None:
+        eng.stream_clusters([sum(1 << j for j in sub) for sub in subsets])
     try:
         G = eng.gram()
     except NeedsStreamPass:
         G = eng.stream_pass(3, chunks())[:(p + 1) ** 2].reshape(p + 1, p + 1)
-    XtX, Xty = inference.split_gram(G)
-    beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # host, polars_impl.py:212-226
-    Vb = XtX_inv[1:, 1:]
-    # IID: the residual statistics from the Gram unless r'r cancels there; HC1: the meat pass
-    stats = inference.stats_from_gram(G, beta_full) if v == "iid" else None
-    if stats is None:
-        out = eng.stream_pass(2, chunks(), beta_full)
-        stats, meat = out[:4], out[4:4 + k * k].reshape(k, k)
-    if v == "iid":
-        se = inference.se_iid(Vb, stats[0], df_resid)
+    n_clusters = None
+    if mz:
+        iv = inference.IVSystem(G, k, mz, z_has_ones=False)  # demeaned instruments are never all ones
+        out = eng.stream_pass(4, chunks(), iv.coef)
+        stats, meat_u = out[:4], out[4:4 + p * p].reshape(p, p)
+        Vb, to_meat = iv.XtX_inv, iv.xhat_meat
+        if v == "iid":
+            se = inference.se_iid(Vb, stats[0], df_resid)
+        elif v == "hc1":
+            se = inference.se_hc1(Vb, to_meat(meat_u), n_obs, df_resid)
+        beta_full = iv.beta_full
     else:
-        se = inference.se_hc1(Vb, meat, n_obs, df_resid)
+        XtX, Xty = inference.split_gram(G)
+        beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # host, polars_impl.py:212-226
+        Vb, to_meat = XtX_inv[1:, 1:], (lambda M: M)
+        # IID without weights: the residual statistics from the Gram unless r'r cancels there
+        stats = inference.stats_from_gram(G, beta_full) if v == "iid" and w is None else None
+        if stats is None:
+            out = eng.stream_pass(2, chunks(), beta_full)
+            stats, meat = out[:4], out[4:4 + k * k].reshape(k, k)
+        if v == "iid":
+            se = inference.se_iid(Vb, stats[0], df_resid)
+        elif v == "hc1":
+            se = inference.se_hc1(Vb, meat, n_obs, df_resid)
+    if v == "cluster":
+        ks = p if mz else k
+        meats, Gs = eng.stream_cluster_meats(ks)
+        if len(cluster_cols) == 1:
+            se, n_clusters = inference.se_cluster_oneway(Vb, to_meat(meats[0]), int(Gs[0]), n_obs, df_resid, ssc)
+        else:
+            se, n_clusters = inference.se_cluster_multiway(Vb, [to_meat(M) for M in meats], [int(g) for g in Gs],
+                                                           subsets, n_obs, df_resid, ssc)
     rss_w, rss, sum_y, sum_y2 = stats
     tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
+    if mz:
+        strip = len(beta_full) == k + 1
+        beta = beta_full[1:] if strip else beta_full
+        se = se[1:] if strip else se
+    else:
+        beta = beta_full[1:]
     timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
-    return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta_full[1:]))),
+    return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta))),
                         std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
-                        iterations=iterations, vcov_type=vcov, is_iv=False, n_instruments=None,
-                        n_clusters=None, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
-                        fe_dims=fe_dims, r_squared=1 - rss / tss if tss > 0 else None, compression_ratio=None,
-                        rss=rss, tss=tss, backend="hip", timings=timings)
+                        iterations=iterations, vcov_type=vcov, is_iv=bool(mz), n_instruments=mz or None,
+                        n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
+                        fe_dims=fe_dims, r_squared=None if mz else (1 - rss / tss if tss > 0 else None),
+                        compression_ratio=None, rss=float(rss), tss=None if mz else tss, backend="hip",
+                        timings=timings)
 
 
 def _beta_agrees(beta_dev, beta_host, rtol: float = 1e-10) -> bool:
