@@ -61,6 +61,8 @@ struct FeState {
   double* T = nullptr;         // [G*p] cross term of the current projection
   double* alpha = nullptr;     // [G*p] group effect subtracted so far
   double* R = nullptr;         // [G] check cross term (y column, unweighted)
+  double* alpha_g = nullptr;   // [G][alpha_pitch(p)] copy of alpha the general sweeps gather (whole lines)
+  size_t alpha_g_cap = 0;
   double* hi = nullptr;        // [G*p] coarse limbs of the sum being formed (S, W, Sy, T or R), all
                                // zero between sums: the conversion that reads an entry clears it
   // segment layout (general sweeps, lfe_seg.hip): kept rows sorted by this FE's code
@@ -520,6 +522,10 @@ __device__ __forceinline__ double wave_reduce63(double v, double idv, Op op) {
   v = op(v, dpp64<0x143, 0xC>(v, idv));
   return v;
 }
+
+// row pitch (doubles) of the gathered effect tables: a row of p <= 16 doubles in one 32/64/128-byte
+// aligned segment, so a random gather touches one cache line instead of up to two
+inline int alpha_pitch(int p) { return p <= 4 ? 4 : p <= 8 ? 8 : (p + 15) / 16 * 16; }
 
 // ---------------------------------------------------------------------------
 // Two-limb fixed-point sums: every group sum, cross term and weight sum of the demeaning loop

@@ -23,20 +23,19 @@ static int fail(int code, const char* msg) {
   return code;
 }
 
-constexpr int kRsThreads = 256;
+constexpr int kRsThreads = 512;
 constexpr int kRsWaves = kRsThreads / 64;
 constexpr int kRsPer = 16;                       // items per thread
-constexpr int kRsItems = kRsThreads * kRsPer;    // items per block
+constexpr int kRsItems = kRsThreads * kRsPer;    // items per block (a tile)
 constexpr int kRsBits = 8;
 constexpr int kRsBins = 1 << kRsBits;
-static_assert(kRsBins == kRsThreads, "one digit per thread in the wave prefix");
 
-// digit counts of block b: counts[d * nblk + b]
+// digit counts of tile b: counts[d * nblk + b]
 __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
                                                         int nblk, int32_t* __restrict__ counts) {
   __shared__ int32_t h[kRsBins];
   const int tid = threadIdx.x;
-  h[tid] = 0;
+  for (int j = tid; j < kRsBins; j += kRsThreads) h[j] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kRsItems;
 #pragma unroll 4
@@ -45,25 +44,32 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint64_t* __restri
     if (i < n) atomicAdd(&h[(int)((keys[i] >> shift) & (kRsBins - 1))], 1);
   }
   __syncthreads();
-  counts[(int64_t)tid * nblk + blockIdx.x] = h[tid];
+  for (int j = tid; j < kRsBins; j += kRsThreads) counts[(int64_t)j * nblk + blockIdx.x] = h[j];
 }
 
-// Stable scatter.  Wave w of block b owns items [b*4096 + w*1024, +1024) in 16
-// steps of 64; within a step, lanes with equal digits are matched by 8 ballots
-// and ranked by lane; per-wave running counts in LDS carry the rank across
-// steps; a prefix over waves and the scanned global counts give the position.
+// Stable scatter of one tile.  Wave w owns items [b*8192 + w*1024, +1024) in 16 steps of 64;
+// within a step, lanes with equal digits are matched by 8 ballots and ranked by lane; per-wave
+// running counts in LDS carry the rank across steps.  The tile is then sorted by digit in LDS
+// (position = the digit's start in the tile + the waves before + the rank) and written out by
+// consecutive threads, so every digit's run of the tile (~32 items) leaves as one contiguous
+// store sequence instead of 32 scattered ones (the partial lines at the runs' ends are the
+// only ones the L2 has to merge).
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint64_t* __restrict__ kin,
                                                            const int32_t* __restrict__ vin,
                                                            uint64_t* __restrict__ kout, int32_t* __restrict__ vout,
                                                            int64_t n, int shift, int nblk,
                                                            const int32_t* __restrict__ scanned) {
   __shared__ int32_t cnt[kRsWaves][kRsBins];
-  __shared__ int32_t base_d[kRsBins];
+  __shared__ int32_t dstart[kRsBins + 1];  // digit starts in the tile
+  __shared__ int32_t gbase[kRsBins];       // digit starts in the output, minus dstart
+  __shared__ uint64_t skey[kRsItems];
+  __shared__ int32_t sval[kRsItems];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int j = tid; j < kRsWaves * kRsBins; j += kRsThreads) (&cnt[0][0])[j] = 0;
-  base_d[tid] = scanned[(int64_t)tid * nblk + blockIdx.x];
   __syncthreads();
-  const int64_t b0 = (int64_t)blockIdx.x * kRsItems + (int64_t)w * (kRsItems / kRsWaves);
+  const int64_t t0 = (int64_t)blockIdx.x * kRsItems;
+  const int64_t b0 = t0 + (int64_t)w * (kRsItems / kRsWaves);
+  const int tlen = (int)min((int64_t)kRsItems, n - t0);
   const uint64_t lt = (1ull << lane) - 1ull;
   uint64_t key[kRsPer];
   int32_t val[kRsPer];
@@ -91,7 +97,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint64_t* __res
     if (valid && before == 0) cnt[w][d] += __popcll(m);
   }
   __syncthreads();
-  {
+  if (tid < kRsBins) {  // per digit: exclusive prefix over waves, the digit's tile total
     int run = 0;
 #pragma unroll
     for (int w2 = 0; w2 < kRsWaves; ++w2) {
@@ -99,15 +105,45 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint64_t* __res
       cnt[w2][tid] = run;
       run += t;
     }
+    dstart[tid] = run;  // total for now
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the digit totals (4 digits per lane, then the wave)
+    int v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = dstart[tid * 4 + q];
+      sum += v[q];
+    }
+    int x = sum;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    int run = x - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = tid * 4 + q;
+      gbase[d] = scanned[(int64_t)d * nblk + blockIdx.x] - run;
+      dstart[d] = run;
+      run += v[q];
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int s = 0; s < kRsPer; ++s) {
     if (b0 + s * 64 + lane >= n) continue;
     const int d = (int)((key[s] >> shift) & (kRsBins - 1));
-    const int64_t pos = (int64_t)base_d[d] + cnt[w][d] + rank[s];
-    kout[pos] = key[s];
-    vout[pos] = val[s];
+    const int q = dstart[d] + cnt[w][d] + rank[s];
+    skey[q] = key[s];
+    sval[q] = val[s];
+  }
+  __syncthreads();
+  for (int q = tid; q < tlen; q += kRsThreads) {
+    const uint64_t k = skey[q];
+    const int64_t pos = (int64_t)gbase[(int)((k >> shift) & (kRsBins - 1))] + q;
+    kout[pos] = k;
+    vout[pos] = sval[q];
   }
 }
 

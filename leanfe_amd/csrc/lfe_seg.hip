@@ -389,14 +389,18 @@ __global__ void k_cross_convert(double* __restrict__ T, double* __restrict__ Thi
   }
 }
 
-// alpha_f = (S_f - T_f) / W_f   (weighted: W = sum w; else W = kept count)
+// alpha_f = (S_f - T_f) / W_f   (weighted: W = sum w; else W = kept count), also into the
+// line-aligned gather copy alpha_g (row pitch ap)
 __global__ void k_finalize(const double* __restrict__ S, const double* __restrict__ T, const double* __restrict__ Wsum,
-                           const int32_t* __restrict__ cnt, int32_t G, int p, double* __restrict__ alpha) {
+                           const int32_t* __restrict__ cnt, int32_t G, int p, double* __restrict__ alpha,
+                           double* __restrict__ alpha_g, int ap) {
   const int64_t total = (int64_t)G * p;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t g = e / p;
     const double den = Wsum ? Wsum[g] : (double)cnt[g];
-    alpha[e] = den > 0.0 ? (S[e] - (T ? T[e] : 0.0)) / den : 0.0;
+    const double v = den > 0.0 ? (S[e] - (T ? T[e] : 0.0)) / den : 0.0;
+    alpha[e] = v;
+    if (alpha_g) alpha_g[g * ap + (e - g * p)] = v;
   }
 }
 
@@ -520,12 +524,12 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
   for (int f2 = 0; f2 < c->F; ++f2)
     if (f2 != f) {
       a.oc[j] = fe.oc + (size_t)j * c->ld;
-      a.alpha[j] = c->fe[f2].alpha;
+      a.alpha[j] = c->fe[f2].alpha_g;
       ++j;
     }
   const bool wt = (!y_only || c->records) && c->L.w != nullptr;  // the check is unweighted, except for records
   a.ws = wt ? fe.ws : nullptr;
-  a.p = c->p;
+  a.p = alpha_pitch(c->p);  // the gather copies' row pitch
   a.pc = pc;
   a.G = fe.G;
   a.T = out;
@@ -607,7 +611,8 @@ static int seg_finalize(lfe_ctx* c, int f) {
   const bool cross = c->F > 1;
   ProfScope _ps(c, K_FINALIZE);
   hipLaunchKernelGGL(k_finalize, dim3(grid_for((int64_t)fe.G * c->p)), dim3(kBlock), 0, c->stream, fe.S,
-                     cross ? fe.T : nullptr, c->L.w ? fe.W : nullptr, fe.cnt, fe.G, c->p, fe.alpha);
+                     cross ? fe.T : nullptr, c->L.w ? fe.W : nullptr, fe.cnt, fe.G, c->p, fe.alpha,
+                     cross ? fe.alpha_g : nullptr, alpha_pitch(c->p));
   LFE_HIP(hipGetLastError());
   if (cross) {  // the statistics of the new effects (the other FEs' cross-term quanta)
     unsigned long long* am = reinterpret_cast<unsigned long long*>(c->amax) + (size_t)f * kMaxCols;
@@ -647,6 +652,12 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
   LFE_TRY(ensure_f64(c, c->amax, c->amax_cap, (size_t)kMaxFE * kMaxCols));
   LFE_HIP(hipMemsetAsync(c->amax, 0, sizeof(double) * kMaxFE * kMaxCols, c->stream));
   LFE_TRY(ensure_f64(c, c->astat, c->astat_cap, (size_t)kMaxFE * kAstatBlocks * 64));
+  if (c->F > 1)  // the line-aligned gather copies of the effects, zero like the tables
+    for (auto& fe : c->fe) {
+      const size_t m = (size_t)fe.G * alpha_pitch(c->p);
+      LFE_TRY(ensure_f64(c, fe.alpha_g, fe.alpha_g_cap, m));
+      LFE_HIP(hipMemsetAsync(fe.alpha_g, 0, sizeof(double) * m, c->stream));
+    }
   LFE_HIP(hipMemsetAsync(c->astat, 0, sizeof(double) * kMaxFE * kAstatBlocks * 64, c->stream));
   const int F = c->F;
   const bool cross = F > 1;
