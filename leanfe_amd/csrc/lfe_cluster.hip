@@ -195,12 +195,13 @@ __global__ __launch_bounds__(256) void k_count_nonzero(const int32_t* __restrict
 // Clusters of sorted (key, row) pairs [0, n) (dropped rows carry key = drop and sort
 // last): segment offsets in W.seg_off, S[h] = sum of the rows' records (row-major
 // [.][k] `table`) in c->clS; *G_out clusters.
-int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R,
-                        const double* table, int k, int32_t* G_out) {
+// segments of sorted keys: head flags -> scan (clw.flag) -> offsets (clw.seg_off); *G_out clusters,
+// *nv_out kept positions (dropped rows carry key = drop and sort last)
+static int group_segments(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, int32_t* G_out,
+                          int32_t* nv_out) {
   auto& W = c->clw;
   LFE_TRY(ensure_i32(c, W.seg_off, W.seg_off_cap, (size_t)n + 1));
   LFE_TRY(ensure_i32(c, W.ufirst, W.ufirst_cap, (size_t)seg_units_needed(n)));
-  int32_t G = 0;
   LFE_HIP(hipMemsetAsync(W.flag + n, 0, sizeof(int32_t), c->stream));
   LFE_HIP(hipMemsetAsync(W.seg_off, 0, sizeof(int32_t), c->stream));
   if (n > 0) {
@@ -215,13 +216,32 @@ int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const 
                        W.seg_off);
   }
   LFE_HIP(hipGetLastError());
+  int32_t G = 0;
   LFE_TRY(d2h_sync(c, &G, W.flag + n, sizeof(int32_t)));
   *G_out = G;
-  if (k == 0) return LFE_OK;
-  LFE_TRY(ensure_cluster_ws(c, (size_t)std::max(G, 1) * k, 4));
-  // kept positions = n minus the dropped rows (sorted last): G clusters over them
   int32_t nv = 0;
-  LFE_TRY(d2h_sync(c, &nv, W.seg_off + G, sizeof(int32_t)));
+  if (G > 0) LFE_TRY(d2h_sync(c, &nv, W.seg_off + G, sizeof(int32_t)));
+  *nv_out = nv;
+  return LFE_OK;
+}
+
+static int group_sums(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R, const double* table,
+                      int k, int32_t G, int32_t nv);
+
+int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R,
+                        const double* table, int k, int32_t* G_out) {
+  int32_t G = 0, nv = 0;
+  LFE_TRY(group_segments(c, n, drop, K, &G, &nv));
+  *G_out = G;
+  if (k == 0) return LFE_OK;
+  return group_sums(c, n, drop, K, R, table, k, G, nv);
+}
+
+// S[h] = sum of the rows' records of cluster h (c->clS), the segments formed by group_segments
+static int group_sums(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R, const double* table,
+                      int k, int32_t G, int32_t nv) {
+  auto& W = c->clw;
+  LFE_TRY(ensure_cluster_ws(c, (size_t)std::max(G, 1) * k, 4));
   if (k <= 16 && G > 0 && (int64_t)nv < 8 * (int64_t)G) {
     // short clusters (mean < 8 rows): row-per-lane segmented scan
     LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)G * k, c->stream));
@@ -249,6 +269,91 @@ int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const 
     LFE_TRY(seg_gather_sum(c, W.seg_off, G, W.ufirst, n, R, table, k, k, c->clS, K_CLUSTER_SCATTER));
   }
   LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+// Mostly-singleton subsets (e.g. config 4's fe2 x fe3: 48.8M clusters over 50M rows): with D the
+// residual pass's sum of s s' over all kept rows, sum_c S_c S_c' = D + sum over clusters of two or
+// more rows of (S_c S_c' - sum_{i in c} s_i s_i'), so only those clusters' rows are gathered.
+// len2[h] = the rows of cluster h if it has two or more, else 0; one2[h] = 1 for such a cluster
+__global__ void k_multi_mark(const int32_t* __restrict__ seg_off, int32_t G, int32_t* __restrict__ len2,
+                             int32_t* __restrict__ one2) {
+  for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < G; h += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t len = seg_off[h + 1] - seg_off[h];
+    len2[h] = len >= 2 ? len : 0;
+    one2[h] = len >= 2 ? 1 : 0;
+  }
+}
+
+// the multi-row clusters' rows and offsets, compacted (scans of k_multi_mark's arrays)
+__global__ void k_multi_compact(const int32_t* __restrict__ seg_off, int32_t G, const int32_t* __restrict__ pos2,
+                                const int32_t* __restrict__ idx2, const int32_t* __restrict__ R,
+                                int32_t* __restrict__ seg2, int32_t* __restrict__ r2) {
+  for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < G; h += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t a = seg_off[h], len = seg_off[h + 1] - a;
+    if (len < 2) continue;
+    const int32_t q = pos2[h];
+    seg2[idx2[h]] = q;
+    for (int32_t j = 0; j < len; ++j) r2[q + j] = R[a + j];
+  }
+}
+
+// t2[j] = the score row of r2[j]; s2[h] = the sum of its cluster's rows, in row order
+__global__ void k_multi_rows(const int32_t* __restrict__ r2, int64_t N2, const double* __restrict__ U, int k,
+                             double* __restrict__ t2) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N2 * k; e += (int64_t)gridDim.x * blockDim.x)
+    t2[e] = U[(int64_t)r2[e / k] * k + (e % k)];
+}
+__global__ void k_multi_sums(const int32_t* __restrict__ seg2, int32_t G2, const double* __restrict__ t2, int k,
+                             double* __restrict__ s2) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)G2 * k;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t h = e / k;
+    const int j = (int)(e % k);
+    double t = 0.0;
+    for (int32_t q = seg2[h]; q < seg2[h + 1]; ++q) t += t2[(int64_t)q * k + j];
+    s2[e] = t;
+  }
+}
+
+static int singleton_meat(lfe_ctx* c, const int32_t* R, int32_t G, int k, double* meat) {
+  auto& W = c->clw;
+  LFE_TRY(ensure_i32(c, W.off2, W.off2_cap, (size_t)G + 1));
+  LFE_TRY(ensure_i32(c, W.idx2, W.idx2_cap, (size_t)G + 1));
+  LFE_HIP(hipMemsetAsync(W.off2 + G, 0, sizeof(int32_t), c->stream));
+  LFE_HIP(hipMemsetAsync(W.idx2 + G, 0, sizeof(int32_t), c->stream));
+  {
+    ProfScope _ps(c, K_CLUSTER_SCATTER);
+    hipLaunchKernelGGL(k_multi_mark, dim3(grid_for(G, kBlock, 8192)), dim3(kBlock), 0, c->stream, W.seg_off, G,
+                       W.off2, W.idx2);
+  }
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(exclusive_scan2(c, W.off2, (int64_t)G + 1, W.idx2, (int64_t)G + 1));
+  int32_t n2[2] = {0, 0};
+  LFE_TRY(d2h_sync(c, &n2[0], W.off2 + G, sizeof(int32_t)));
+  LFE_TRY(d2h_sync(c, &n2[1], W.idx2 + G, sizeof(int32_t)));
+  const int32_t N2 = n2[0], G2 = n2[1];
+  std::vector<double> A((size_t)k * k, 0.0), B((size_t)k * k, 0.0);
+  if (G2 > 0) {
+    LFE_TRY(ensure_i32(c, W.seg2, W.seg2_cap, (size_t)G2 + 1));
+    LFE_TRY(ensure_i32(c, W.r2, W.r2_cap, (size_t)N2));
+    LFE_TRY(ensure_f64(c, W.t2, W.t2_cap, (size_t)N2 * k));
+    LFE_TRY(ensure_f64(c, W.s2, W.s2_cap, (size_t)G2 * k));
+    LFE_TRY(h2d_small(c, W.seg2 + G2, &N2, sizeof(int32_t)));
+    {
+      ProfScope _ps(c, K_CLUSTER_SCATTER);
+      hipLaunchKernelGGL(k_multi_compact, dim3(grid_for(G, kBlock, 8192)), dim3(kBlock), 0, c->stream, W.seg_off, G,
+                         W.off2, W.idx2, R, W.seg2, W.r2);
+      hipLaunchKernelGGL(k_multi_rows, dim3(grid_for((int64_t)N2 * k, kBlock, 8192)), dim3(kBlock), 0, c->stream,
+                         W.r2, (int64_t)N2, c->scores, k, W.t2);
+      hipLaunchKernelGGL(k_multi_sums, dim3(grid_for((int64_t)G2 * k, kBlock, 8192)), dim3(kBlock), 0, c->stream,
+                         W.seg2, G2, W.t2, k, W.s2);
+    }
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(launch_table_gram(c, W.s2, G2, k, A.data()));
+    LFE_TRY(launch_table_gram(c, W.t2, N2, k, B.data()));
+  }
+  for (int e = 0; e < k * k; ++e) meat[e] = c->score_meat[e] + (A[e] - B[e]);
   return LFE_OK;
 }
 
@@ -397,8 +502,16 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
 
   int buf = 0;
   if (n > 0) LFE_TRY(radix_sort(c, n, bit_length(span), &buf));
-  int32_t G = 0;
-  LFE_TRY(group_sorted(c, n, span, W.keys[buf], W.rows[buf], c->scores, k, &G));
+  int32_t G = 0, nv = 0;
+  LFE_TRY(group_segments(c, n, span, W.keys[buf], &G, &nv));
+  // one process, unweighted, mostly singletons (mean cluster size below 2): D + the multi-row
+  // clusters' corrections, without gathering every row
+  if (c->world == 1 && k > 0 && c->score_meat_ok && (int)c->score_meat.size() == k * k && G > 0 &&
+      2 * (int64_t)G > (int64_t)nv && getenv("LFE_CL_NO_SINGLETON") == nullptr) {
+    *G_out = G;
+    return singleton_meat(c, W.rows[buf], G, k, meat);
+  }
+  if (k > 0) LFE_TRY(group_sums(c, n, span, W.keys[buf], W.rows[buf], c->scores, k, G, nv));
 
   // multi-rank, few clusters: a key-indexed table, all-reduced (smaller than the exchange)
   const char* own_env = getenv("LFE_CL_OWNER_MIN_SPAN");  // tests: force the owner-partitioned form

@@ -1468,6 +1468,8 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
     for (int e = 0; e < k * k; ++e) hc1[e] = meat[e];
   c->scores_valid = keep_scores != 0;
   c->score_k = k;
+  c->score_meat = meat;  // the row kernel's meat is sum s s' (unweighted two-FE case)
+  c->score_meat_ok = keep_scores && c->world == 1;
   return LFE_OK;
 }
 
@@ -1494,6 +1496,8 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
     if (hc1)
       for (int e = 0; e < k * k; ++e) hc1[e] = meat[e];
     c->scores_valid = keep_scores != 0;
+    c->score_meat = meat;
+    c->score_meat_ok = keep_scores && c->world == 1;
     return LFE_OK;
   }
   // staged columns 0..p-1 (col 0 = y, zeroed in the meat, or the intercept with icpt);
@@ -1503,6 +1507,10 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
   if (hc1)
     for (int e = 0; e < k * k; ++e) hc1[e] = meat[e];
   c->scores_valid = keep_scores != 0;
+  // the meat is sum s s' over the score rows s = u r only without weights (weighted: w r^2 u u'
+  // against scores u r w) and outside records mode
+  c->score_meat = meat;
+  c->score_meat_ok = keep_scores && c->world == 1 && !a.w && !a.yoco;
   return LFE_OK;
 }
 

@@ -123,6 +123,19 @@ struct ClusterWS {
   size_t rrec_cap = 0;
   int32_t* ocnt = nullptr;      // [world] owner counts + cursors, [world * world] count matrix
   size_t ocnt_cap = 0;
+  // mostly-singleton subsets: the clusters of two or more rows, compacted
+  int32_t* r2 = nullptr;        // [N2] their rows, cluster by cluster (sorted order)
+  size_t r2_cap = 0;
+  int32_t* off2 = nullptr;      // [G + 1] scans: positions / cluster index of the multi-row clusters
+  size_t off2_cap = 0;
+  int32_t* idx2 = nullptr;
+  size_t idx2_cap = 0;
+  int32_t* seg2 = nullptr;      // [G2 + 1] their offsets in r2
+  size_t seg2_cap = 0;
+  double* t2 = nullptr;         // [N2][k] their score rows
+  size_t t2_cap = 0;
+  double* s2 = nullptr;         // [G2][k] their sums
+  size_t s2_cap = 0;
   std::vector<int32_t*> lay;    // loaded cluster columns in layout order
   std::vector<size_t> lay_cap;
   bool lay_valid = false;
@@ -217,6 +230,10 @@ struct lfe_ctx {
   double* scores = nullptr;  // row-major [ld][score_k] score rows u r (w), layout order (p * ld allocated)
   double* dbeta = nullptr;   // [64] beta_full staging
   bool scores_valid = false;
+  // sum over kept rows of s s' for the score rows s (the residual pass's meat tile, unweighted
+  // one-process fits): the cluster meats of mostly-singleton subsets start from it (lfe_cluster.hip)
+  std::vector<double> score_meat;
+  bool score_meat_ok = false;
   int score_k = 0;           // score width: p - 1 (u = x~), or p with the intercept (IV, u = [1, x~, z~])
   // YOCO records (lfe_compress): the loaded rows are compressed records, weight = n_g (or sum w);
   // no singleton drop, weighted convergence check, lfe_resid_yoco's sufficient-statistic residuals
