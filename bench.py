@@ -221,10 +221,13 @@ def load_shard(eng, a, rank: int, world: int, shard: str) -> dict:
 # measurement helpers
 # ---------------------------------------------------------------------------
 
-def algorithmic_bytes(n: int, p: int, F: int) -> dict:
+def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False) -> dict:
     """HBM bytes each kernel must move per launch, n rows of the shard,
     p = 1 + k f64 data columns, F int32 code columns.  Kernels absent here move only group
-    tables or scalars (latency-bound) and count as 0 in the step total."""
+    tables or scalars (latency-bound) and count as 0 in the step total.  The general sweeps'
+    cross / check passes (F >= 3) read F - 1 code arrays from HBM; the effect
+    rows they gather come from L2 / MALL-resident tables and are not HBM bytes."""
+    k = p - 1
     return {
         "part_hist": 4 * n,                          # primary codes
         "part_scatter": n * (2 * 8 * p + 2 * 4 * F),  # read + write X and codes
@@ -234,8 +237,18 @@ def algorithmic_bytes(n: int, p: int, F: int) -> dict:
         "tp": 4 * n,                                 # seg_q: the cross term of the primary FE
         "tq": 2 * n,                                 # run_h: the cross term of the secondary FE
         "gram_design": n * (8 * p + 4 * F),          # X + codes
-        "gram_resid": n * (8 * p + 4 * F),           # X + codes (HC1: no score write)
+        "gram_resid": n * (8 * p + 4 * F + (8 * k if clustered else 0)),  # X + codes (+ score rows)
+        "seg_build": n * (4 * F + 4 * F * (F - 1)),  # codes -> every FE's other codes, segment order
+        "cross": 4 * n * (F - 1),                    # the other FEs' codes in segment order
+        "check": 4 * n * (F - 1),
+        **({"count": 4 * n} if F != 2 else {}),      # one FE's codes (two FEs: the layouts' histograms)
     }
+
+
+def gather_bytes(n: int, p: int, F: int) -> dict:
+    """Bytes the general sweeps gather per launch from L2 / MALL (effect rows of the other FEs, each
+    row one 128-byte line of the padded copy; the check passes one 8-byte y value)."""
+    return {"cross": n * (F - 1) * 128, "check": n * (F - 1) * 8}
 
 
 def pmc_traffic(kernel: str, a) -> tuple[float | None, str | None]:
@@ -362,7 +375,7 @@ def main(argv=None):
     value = total_rows * a.steps / elapsed / 1e6
     ms_step = elapsed / a.steps * 1e3
     p, F = a.k + 1, len(a.levels)
-    ab = algorithmic_bytes(geo["local"], p, F)
+    ab = algorithmic_bytes(geo["local"], p, F, clustered=bool(a.cl))
     # dominant kernel = most device time in the timed region (rank 0's shard)
     dom = max(kstats.items(), key=lambda kv: kv[1][0]) if kstats else ("none", (0.0, 1))
     dom_name, (dom_ms, dom_launches) = dom
@@ -376,6 +389,10 @@ def main(argv=None):
                     "bytes_per_launch": ab[dom_name], "avg_launch_ms": round(per_launch_s * 1e3, 4)}
         if tsrc:
             roofline["traffic_source"] = tsrc + " (rocprofv3 PMC, same config)"
+        gb = gather_bytes(geo["local"], p, F).get(dom_name)
+        if gb:  # the general sweeps: what the gathers move from L2 / MALL per launch
+            roofline["gathered"] = {"bytes_per_launch": gb, "GBps": round(gb / per_launch_s / 1e9, 1),
+                                    "source": "L2 / MALL (padded effect rows, 128 B each)"}
     # step-level roofline: every modelled kernel's algorithmic bytes x its launches per step,
     # over the measured wall time per step (rank 0's shard; all ranks move the same amount)
     step_bytes = sum(ab[k] * v[1] / a.steps for k, v in kstats.items() if k in ab)

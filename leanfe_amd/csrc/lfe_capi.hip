@@ -395,6 +395,8 @@ static void free_data(lfe_ctx* c) {
     dfree(fe.hi);
     dfree(fe.alpha_g);
     fe.alpha_g_cap = 0;
+    dfree(fe.alpha_y);
+    fe.alpha_y_cap = 0;
     dfree(fe.seg_off);
     dfree(fe.seg_cur);
     dfree(fe.oc);

@@ -210,10 +210,18 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
 // only test is its primary code's sign (item edges are masked once per 16-row group), LDS
 // byte offsets are one multiply-add per table, every pointer is hoisted out of the loop, and
 // the next group pair's loads are issued before the current pair is consumed.
-template <int TH, int NACC, int GU>
+// BIG: some column's values may carry a coarse limb (an outlier beyond Qc / 2, or a non-finite
+// value).  Both variants are launched; each returns at once unless the quanta say it is the one
+// (the flags live on the device), so typical data runs the fine-limb-only loop.
+template <int TH, int NACC, int GU, bool BIG>
 __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  {
+    bool any = false;
+    for (int j = 0; j < a.la.p; ++j) any = any || a.fixq[FQ_BIG * kFqCols + j] != 0.0;
+    if (any != BIG) return;
+  }
   constexpr int nwv = TH / 64, step = nwv * GU;
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.la.p, P = a.la.P, Q = a.qf[0], s = a.la.s;
@@ -299,13 +307,19 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
           const double z = v ? __builtin_fma(xv, cm, zc) : 0.0;
           racc[r % NACC] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc[r % NACC], 0, 0, 0);
           if (v && col) {  // integer adds commute
-            double hh;
-            const u64 xi = fix_split(xv, fc, hh);
-            atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(lds, hv[r] - lo, p8, c8)), xi);
-            atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(qtab, gq[r], p8, c8)), xi);
-            if (hh != 0.0) {  // an outlier (or a non-finite value): its coarse limb
-              atomicAdd(&hiP[(int64_t)hv[r] * p + c], hh);
-              atomicAdd(&hiQ[(int64_t)gq[r] * p + c], hh);
+            if (BIG) {
+              double hh;
+              const u64 xi = fix_split(xv, fc, hh);
+              atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(lds, hv[r] - lo, p8, c8)), xi);
+              atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(qtab, gq[r], p8, c8)), xi);
+              if (hh != 0.0) {  // an outlier (or a non-finite value): its coarse limb
+                atomicAdd(&hiP[(int64_t)hv[r] * p + c], hh);
+                atomicAdd(&hiQ[(int64_t)gq[r] * p + c], hh);
+              }
+            } else {  // no coarse limbs: round(x sf) as the low bits of x sf + 1.5 * 2^52
+              const u64 xi = (u64)__double_as_longlong(__builtin_fma(xv, fc.sf, kFixMagic)) - kFixMagicBits;
+              atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(lds, hv[r] - lo, p8, c8)), xi);
+              atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(qtab, gq[r], p8, c8)), xi);
             }
           }
         }
@@ -644,7 +658,7 @@ int sums4(lfe_ctx* c) {
     // measured the same)
     threads = 1024;
     two = raw && a.slice && a.tab_off[a.qf[0]] >= 0;
-    fn = two   ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1>)
+    fn = two   ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1, false>)
          : raw ? reinterpret_cast<const void*>(&k_sums4<1, 2, 1, 1024, true>)
                : SUMS4_FN(1, 2, 1, 1024);
   } else if (a.nq <= 1) {
@@ -709,6 +723,11 @@ int sums4(lfe_ctx* c) {
     ProfScope _ps(c, K_GROUP_SUMS);
     void* args[] = {&a};
     LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, lds, c->stream));
+    if (two) {  // the coarse-limb variant (returns at once unless some column needs it)
+      const void* fb = reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1, true>);
+      LFE_HIP(hipFuncSetAttribute(fb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 1)));
+      LFE_HIP(hipLaunchKernel(fb, dim3(nblocks), dim3(threads), args, lds, c->stream));
+    }
   }
   LFE_HIP(hipGetLastError());
   if (two) {  // two implies raw: one epilogue launch

@@ -63,6 +63,8 @@ struct FeState {
   double* R = nullptr;         // [G] check cross term (y column, unweighted)
   double* alpha_g = nullptr;   // [G][alpha_pitch(p)] copy of alpha the general sweeps gather (whole lines)
   size_t alpha_g_cap = 0;
+  double* alpha_y = nullptr;   // [G] the y column of alpha, dense (the y-only check passes gather it)
+  size_t alpha_y_cap = 0;
   double* hi = nullptr;        // [G*p] coarse limbs of the sum being formed (S, W, Sy, T or R), all
                                // zero between sums: the conversion that reads an entry clears it
   // segment layout (general sweeps, lfe_seg.hip): kept rows sorted by this FE's code

@@ -314,27 +314,59 @@ int launch_seg_chain(lfe_ctx* c, const int32_t* seg_off, const int32_t* ufirst, 
 // Statistics of an effect table for the cross terms' quanta: column max |alpha| (u64 bits, atomicMax)
 // and, per block, sum_g cnt[g] alpha[g][c]^2 (col 63: sum_g cnt[g]) into slots [kAstatBlocks][64], so
 // that rms over rows of alpha_f[g_f(i)] is formed in a fixed order (k_cross_quanta).  Block b takes
-// the groups [b G / nb, (b + 1) G / nb), wave w every fourth of them, lane c column c.
+// the groups [b G / nb, (b + 1) G / nb); a wave reads 64 / L groups per step (L lanes per group, lane
+// c of a group column c), four steps in flight, and the lanes of one column are combined over fixed
+// shuffles, then the waves in order.
+template <int L>
 __global__ __launch_bounds__(256) void k_alpha_stats(const double* __restrict__ alpha, const int32_t* __restrict__ cnt,
                                                      int32_t G, int p, unsigned long long* __restrict__ amax,
                                                      double* __restrict__ slots) {
+  constexpr int GPW = 64 / L;  // groups per wave step
   __shared__ double ss[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / L, c = lane % L;
   const int64_t g0 = (int64_t)G * blockIdx.x / gridDim.x, g1 = (int64_t)G * (blockIdx.x + 1) / gridDim.x;
   double m = 0.0, sq = 0.0, nn = 0.0;
-  for (int64_t g = g0 + wave; g < g1; g += 4) {
-    const double ng = (double)cnt[g];
-    nn += ng;
-    if (lane < p) {
-      const double v = alpha[g * p + lane];
-      m = fmax(m, fabs(v));  // (fmax drops a NaN; the squares keep it)
-      sq = __builtin_fma(ng * v, v, sq);
+  const int64_t stride = 4 * GPW;
+  int64_t g = g0 + wave * GPW + sub;
+  for (; g + 3 * stride < g1; g += 4 * stride) {
+    double v[4], ng[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t gu = g + u * stride;
+      ng[u] = (double)cnt[gu];
+      v[u] = c < p ? alpha[gu * p + c] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      nn += ng[u];
+      m = fmax(m, fabs(v[u]));  // (fmax drops a NaN; the squares keep it)
+      sq = __builtin_fma(ng[u] * v[u], v[u], sq);
     }
   }
-  ss[wave][lane] = lane == 63 ? nn : sq;
-  if (lane < p && m > 0.0) atomicMax(&amax[lane], (unsigned long long)__double_as_longlong(m));
+  for (; g < g1; g += stride) {
+    const double ng = (double)cnt[g];
+    const double v = c < p ? alpha[g * p + c] : 0.0;
+    nn += ng;
+    m = fmax(m, fabs(v));
+    sq = __builtin_fma(ng * v, v, sq);
+  }
+  // combine the GPW groups of the wave: lanes c, c + L, c + 2L, ... (fixed order)
+#pragma unroll
+  for (int off = L; off < 64; off <<= 1) {
+    sq += __shfl_xor(sq, off, 64);
+    nn += __shfl_xor(nn, off, 64);
+    m = fmax(m, __shfl_xor(m, off, 64));
+  }
+  if (lane < L) ss[wave][lane] = sq;
+  if (lane == 0) ss[wave][63] = nn;
+  if (lane < L && c < p && m > 0.0) atomicMax(&amax[c], (unsigned long long)__double_as_longlong(m));
   __syncthreads();
-  if (wave == 0) slots[(int64_t)blockIdx.x * 64 + lane] = ((ss[0][lane] + ss[1][lane]) + ss[2][lane]) + ss[3][lane];
+  if (wave == 0) {
+    const bool live = lane < L || lane == 63;
+    const double t = live ? ((ss[0][lane] + ss[1][lane]) + ss[2][lane]) + ss[3][lane] : 0.0;
+    slots[(int64_t)blockIdx.x * 64 + lane] = t;
+  }
 }
 
 static int alpha_stat_blocks(int32_t G) { return (int)std::max<int64_t>(1, std::min<int64_t>(kAstatBlocks, (G + 63) / 64)); }
@@ -390,17 +422,26 @@ __global__ void k_cross_convert(double* __restrict__ T, double* __restrict__ Thi
 }
 
 // alpha_f = (S_f - T_f) / W_f   (weighted: W = sum w; else W = kept count), also into the
-// line-aligned gather copy alpha_g (row pitch ap)
+// line-aligned gather copy alpha_g (row pitch ap) and the dense y column alpha_y
 __global__ void k_finalize(const double* __restrict__ S, const double* __restrict__ T, const double* __restrict__ Wsum,
                            const int32_t* __restrict__ cnt, int32_t G, int p, double* __restrict__ alpha,
-                           double* __restrict__ alpha_g, int ap) {
-  const int64_t total = (int64_t)G * p;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t g = e / p;
-    const double den = Wsum ? Wsum[g] : (double)cnt[g];
-    const double v = den > 0.0 ? (S[e] - (T ? T[e] : 0.0)) / den : 0.0;
-    alpha[e] = v;
-    if (alpha_g) alpha_g[g * ap + (e - g * p)] = v;
+                           double* __restrict__ alpha_g, int ap, double* __restrict__ alpha_y) {
+  // one thread per (group, slot of the padded row): every line of alpha_g is written whole (the
+  // pad slots as 0), so no partially written line has to be merged
+  const int q = alpha_g ? ap : p;
+  const int64_t total = (int64_t)G * q;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = t / q;
+    const int cc = (int)(t - g * q);
+    double v = 0.0;
+    if (cc < p) {
+      const int64_t e = g * p + cc;
+      const double den = Wsum ? Wsum[g] : (double)cnt[g];
+      v = den > 0.0 ? (S[e] - (T ? T[e] : 0.0)) / den : 0.0;
+      alpha[e] = v;
+      if (alpha_y && cc == 0) alpha_y[g] = v;
+    }
+    if (alpha_g) alpha_g[t] = v;
   }
 }
 
@@ -423,6 +464,82 @@ __global__ void k_check_max(const double* __restrict__ Sy, int sy_stride, const 
   }
   for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
   if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+}
+
+// ---------------------------------------------------------------------------
+// the stop test's y-only cross term, one row per lane
+// ---------------------------------------------------------------------------
+// R_f[g] = sum_{i in g} sum_{f' != f} alpha_f'[g_f'(i)][y] (unweighted, polars_impl.py:512-521).
+// k_seg_cross would run it with 16 lanes per row doing the same work for one column; here a lane
+// takes one position of the segment layout, gathers the other FEs' y effects from the dense y
+// copies (alpha_y), splits the value into two-limb fixed point, and the lanes of one segment run
+// are summed over a shuffle scan; the run's last lane adds it to R (int64 fine limbs, integer-valued
+// f64 coarse limbs: the adds commute, so R does not depend on their order).  A wave takes 4 x 64
+// consecutive positions per step.
+struct SegCheckArgs {
+  const int32_t* seg_off;  // [G + 1]
+  int32_t G;
+  const int32_t* oc[kMaxFE - 1];
+  const double* ay[kMaxFE - 1];
+  int no;
+  const double* xq;        // quanta (column 0)
+  unsigned long long* R;   // [G] fine limbs (zeroed)
+  double* Rhi;             // [G] coarse limbs (clean)
+};
+
+__global__ __launch_bounds__(256) void k_seg_check(SegCheckArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int32_t kept = a.seg_off[a.G];
+  const FixCol fc = fix_col(a.xq, 0);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 256; base < kept; base += nwaves * 256) {
+    // the segment holding position base (binary search, wave-uniform)
+    int lo = 0, hi = a.G - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.seg_off[mid] <= base) lo = mid;
+      else hi = mid - 1;
+    }
+    int h = lo;
+    double y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // every gather of the step in flight together
+      const int64_t q = base + u * 64 + lane;
+      double v = 0.0;
+      if (q < kept)
+        for (int j = 0; j < a.no; ++j) v += a.ay[j][a.oc[j][q]];
+      y[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t q = base + u * 64 + lane;
+      const bool in = q < kept;
+      int hl = h;  // this lane's segment: h, or a few after it
+      if (in)
+        while (a.seg_off[hl + 1] <= q) ++hl;
+      double hh = 0.0;
+      long long lo_i = in ? (long long)fix_split(y[u], fc, hh) : 0ll;
+      if (!in) hl = 0x7fffffff;
+      // segmented inclusive scan over the lanes (segment ids do not decrease)
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int oh = __shfl_up(hl, off, 64);
+        const long long ol = __shfl_up(lo_i, off, 64);
+        const double oH = __shfl_up(hh, off, 64);
+        if (lane >= off && oh == hl) {
+          lo_i += ol;
+          hh += oH;
+        }
+      }
+      const int nh = __shfl_down(hl, 1, 64);
+      if (in && (lane == 63 || nh != hl)) {  // the last lane of its run
+        atomicAdd(&a.R[hl], (unsigned long long)lo_i);
+        if (hh != 0.0) atomicAdd(&a.Rhi[hl], hh);
+      }
+      h = __shfl(hl, 63, 64);  // the next 64 positions start in the last lane's segment (or later)
+      if (h == 0x7fffffff) h = a.G - 1;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -524,12 +641,12 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
   for (int f2 = 0; f2 < c->F; ++f2)
     if (f2 != f) {
       a.oc[j] = fe.oc + (size_t)j * c->ld;
-      a.alpha[j] = c->fe[f2].alpha_g;
+      a.alpha[j] = y_only ? c->fe[f2].alpha_y : c->fe[f2].alpha_g;
       ++j;
     }
   const bool wt = (!y_only || c->records) && c->L.w != nullptr;  // the check is unweighted, except for records
   a.ws = wt ? fe.ws : nullptr;
-  a.p = alpha_pitch(c->p);  // the gather copies' row pitch
+  a.p = y_only ? 1 : alpha_pitch(c->p);  // the gather copies' row pitch
   a.pc = pc;
   a.G = fe.G;
   a.T = out;
@@ -554,7 +671,26 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
     a.Thi = fe.hi;
   }
   LFE_TRY(hi_begin(c));
-  if (a.n_units > 0) {
+  if (y_only && !wt) {  // the unweighted check term: one row per lane (k_seg_check)
+    SegCheckArgs k{};
+    k.seg_off = fe.seg_off;
+    k.G = fe.G;
+    for (int j2 = 0; j2 < c->F - 1; ++j2) {
+      k.oc[j2] = a.oc[j2];
+      k.ay[j2] = a.alpha[j2];
+    }
+    k.no = c->F - 1;
+    k.xq = c->xq;
+    k.R = reinterpret_cast<unsigned long long*>(out);
+    k.Rhi = fe.hi;
+    const int64_t n_kept = c->n;  // an upper bound on the kept positions (the kernel reads seg_off[G])
+    if (n_kept > 0 && fe.G > 0) {
+      ProfScope _ps(c, kid);
+      hipLaunchKernelGGL(k_seg_check, dim3(grid_for((n_kept + 255) / 256 * 64, 256, 4096)), dim3(256), 0, c->stream,
+                         k);
+    }
+    LFE_HIP(hipGetLastError());
+  } else if (a.n_units > 0) {
     const int nt = (pc + 15) / 16;
     CrossFn fn = cross_fn(nt, c->F - 1, wt);
     const int waves_per_block = kSegThreads / 64;
@@ -610,15 +746,20 @@ static int seg_finalize(lfe_ctx* c, int f) {
   auto& fe = c->fe[f];
   const bool cross = c->F > 1;
   ProfScope _ps(c, K_FINALIZE);
-  hipLaunchKernelGGL(k_finalize, dim3(grid_for((int64_t)fe.G * c->p)), dim3(kBlock), 0, c->stream, fe.S,
+  hipLaunchKernelGGL(k_finalize, dim3(grid_for((int64_t)fe.G * (cross ? alpha_pitch(c->p) : c->p))), dim3(kBlock), 0,
+                     c->stream, fe.S,
                      cross ? fe.T : nullptr, c->L.w ? fe.W : nullptr, fe.cnt, fe.G, c->p, fe.alpha,
-                     cross ? fe.alpha_g : nullptr, alpha_pitch(c->p));
+                     cross ? fe.alpha_g : nullptr, alpha_pitch(c->p), cross ? fe.alpha_y : nullptr);
   LFE_HIP(hipGetLastError());
   if (cross) {  // the statistics of the new effects (the other FEs' cross-term quanta)
     unsigned long long* am = reinterpret_cast<unsigned long long*>(c->amax) + (size_t)f * kMaxCols;
     LFE_HIP(hipMemsetAsync(am, 0, sizeof(double) * c->p, c->stream));
-    hipLaunchKernelGGL(k_alpha_stats, dim3(alpha_stat_blocks(fe.G)), dim3(256), 0, c->stream, fe.alpha, fe.cnt, fe.G,
-                       c->p, am, c->astat + (size_t)f * kAstatBlocks * 64);
+    double* slots = c->astat + (size_t)f * kAstatBlocks * 64;
+    const dim3 grid(alpha_stat_blocks(fe.G));
+    if (c->p <= 8) hipLaunchKernelGGL(k_alpha_stats<8>, grid, dim3(256), 0, c->stream, fe.alpha, fe.cnt, fe.G, c->p, am, slots);
+    else if (c->p <= 16) hipLaunchKernelGGL(k_alpha_stats<16>, grid, dim3(256), 0, c->stream, fe.alpha, fe.cnt, fe.G, c->p, am, slots);
+    else if (c->p <= 32) hipLaunchKernelGGL(k_alpha_stats<32>, grid, dim3(256), 0, c->stream, fe.alpha, fe.cnt, fe.G, c->p, am, slots);
+    else hipLaunchKernelGGL(k_alpha_stats<64>, grid, dim3(256), 0, c->stream, fe.alpha, fe.cnt, fe.G, c->p, am, slots);
     LFE_HIP(hipGetLastError());
   }
   return LFE_OK;
@@ -657,6 +798,8 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
       const size_t m = (size_t)fe.G * alpha_pitch(c->p);
       LFE_TRY(ensure_f64(c, fe.alpha_g, fe.alpha_g_cap, m));
       LFE_HIP(hipMemsetAsync(fe.alpha_g, 0, sizeof(double) * m, c->stream));
+      LFE_TRY(ensure_f64(c, fe.alpha_y, fe.alpha_y_cap, (size_t)fe.G));
+      LFE_HIP(hipMemsetAsync(fe.alpha_y, 0, sizeof(double) * fe.G, c->stream));
     }
   LFE_HIP(hipMemsetAsync(c->astat, 0, sizeof(double) * kMaxFE * kAstatBlocks * 64, c->stream));
   const int F = c->F;
