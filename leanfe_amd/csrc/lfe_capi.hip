@@ -841,7 +841,19 @@ int lfe_stream_end(lfe_ctx* c, double* out) {
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
     if (c->n > 0) LFE_HIP(hipMemcpyAsync(c->raw_tile, w.tile, sizeof(double) * 256, hipMemcpyDeviceToDevice, c->stream));
     // the raw Gram tile stands for the Gram from the group tables only in the unweighted two-FE case
-    c->raw_ready = c->F == 2 && !c->w;
+    // of one process (ranks' tiles have their own shifts: a sharded fit streams the design Gram)
+    c->raw_ready = c->F == 2 && !c->w && c->world == 1;
+    if (c->world > 1) {  // every rank streamed its own rows: the group sums over all ranks
+      std::vector<std::pair<double*, size_t>> bufs;
+      for (auto& fe : c->fe) {
+        bufs.push_back({fe.S, (size_t)fe.G * p});
+        if (c->w) {
+          bufs.push_back({fe.W, (size_t)fe.G});
+          bufs.push_back({fe.Sy, (size_t)fe.G});
+        }
+      }
+      LFE_TRY(allreduce_sum_f64_many(c, bufs));
+    }
     c->sums_ready = true;
     c->sums_zeroed = false;
     LFE_TRY(stream_weight_stats(c));
@@ -849,6 +861,7 @@ int lfe_stream_end(lfe_ctx* c, double* out) {
     return LFE_OK;
   }
   if (!out) return fail(LFE_EINVAL, "out is null");
+  LFE_TRY(allreduce_sum_f64(c, w.tile, 260));  // sharded: every rank's rows
   std::vector<double> h(260);
   LFE_TRY(d2h_sync(c, h.data(), w.tile, sizeof(double) * 260));
   if (pass == 2 || pass == 4) {  // stats[4] (sum r^2 w, sum r^2, sum y~, sum y~^2), then the HC1 meat
@@ -868,6 +881,7 @@ int lfe_stream_clusters(lfe_ctx* c, int n_subsets, const int32_t* masks) {
   if (!c->sw.on) return fail(LFE_ESTATE, "lfe_stream_clusters: the context holds resident columns");
   if (!c->prepared) return fail(LFE_ESTATE, "lfe_drop_singletons first");
   if (n_subsets < 1 || !masks) return fail(LFE_EINVAL, "bad subsets");
+  if (c->world > 1) return fail(LFE_EINVAL, "streamed clustered SEs run in one process");
   return stream_clusters_prep(c, n_subsets, masks);
 }
 

@@ -107,10 +107,10 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         if out_of_core is None:
             out_of_core = os.environ.get("LEANFE_HIP_OUT_OF_CORE", "0") == "1"
         if out_of_core:
-            if (not fe_cols or factor_vars or interactions or sharded
+            if (not fe_cols or factor_vars or interactions or (sharded and v == "cluster")
                     or strategy not in ("auto", "alt_proj", "demean")):
-                raise ValueError("out_of_core fits take one or more FEs, no factor / interaction terms, one "
-                                 "process, and strategy 'alt_proj' (or 'demean' for one FE)")
+                raise ValueError("out_of_core fits take one or more FEs, no factor / interaction terms, "
+                                 "strategy 'alt_proj' (or 'demean' for one FE), and clustered SEs in one process")
             source = data if stream else cols
             n_rows_oc = n_rows if stream else len(cols[y_col])
             w_oc = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
@@ -291,7 +291,7 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
                 yield r0, [np.asarray(source[c][r0:r0 + chunk_rows], dtype=np.float64) for c in num_cols]
 
     t0 = time.perf_counter()
-    eng.load_codes(codes, levels, p, weights=w)
+    eng.load_codes(codes, levels, p, weights=w)  # a sharded engine: this rank's rows (global codes)
     subsets = None
     if v == "cluster":
         _load_clusters(eng, cols, cluster_cols, False)

@@ -336,3 +336,57 @@ def test_emulated_contiguous_blocks_reshard_to_owners(world, n, k, levels, vcov,
         for other in (a[0]["res"], b[r]["res"]):  # every rank, and a second run, give the same bits
             np.testing.assert_array_equal([res.coefs[x] for x in xs], [other.coefs[x] for x in xs])
             np.testing.assert_array_equal([res.std_errors[x] for x in xs], [other.std_errors[x] for x in xs])
+
+
+@pytest.mark.parametrize("world,n,k,levels,vcov,weighted", [
+    (2, 300_001, 4, [12_000, 300], "HC1", False),        # two FEs: the fast sweeps on streamed codes
+    (3, 240_000, 3, [9_000, 800, 120], "iid", True),      # three FEs, weighted: the general sweeps
+])
+def test_emulated_out_of_core_ranks_match_oracle(world, n, k, levels, vcov, weighted, monkeypatch):
+    """Out-of-core fits on a sharded engine: every rank streams the columns of its
+    own contiguous row block; the streamed group sums and every pass's tile are summed over the ranks
+    (the design Gram streams: the ranks' raw tiles have their own shifts).  Every rank returns the
+    oracle's whole-panel fit, bit-identical across ranks."""
+    from leanfe_amd import dist, leanfe_hip
+    from leanfe_amd._lib import EmuGroup, Engine
+    from oracle import altproj
+
+    full = dict(synth.panel(n, k, levels, seed=29))
+    if weighted:
+        full["w"] = np.random.default_rng(30).uniform(0.5, 2.0, n)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    monkeypatch.setattr(dist, "agree_levels", lambda eng, lv: [max(a, b) for a, b in zip(lv, levels)])
+    group = EmuGroup(world)
+    out, errs = {}, {}
+
+    def worker(rank):
+        try:
+            lo, hi = shard_range(n, rank, world)
+            eng = Engine(0)
+            eng.set_emu(group, rank)
+            eng.dist_group = ("emulated",)
+            shard = {c: np.asarray(v)[lo:hi] for c, v in full.items()}
+            out[rank] = leanfe_hip(shard, y_col="y", x_cols=xs, fe_cols=fes, vcov=vcov, strategy="alt_proj",
+                                   weights="w" if weighted else None, quiet=True, engine=eng, out_of_core=True,
+                                   chunk_rows=40_000 + 7_777 * rank)
+            eng.close()
+        except BaseException as e:  # noqa: BLE001
+            errs[rank] = e
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+    if errs:
+        raise next(iter(errs.values()))
+    o = altproj.fit(full, "y", xs, fes, vcov=vcov, weights="w" if weighted else None)
+    for r in range(world):
+        res = out[r]
+        assert res.iterations == o["iterations"] and res.n_obs == o["n_obs"] and res.df_resid == o["df_resid"]
+        np.testing.assert_allclose([res.coefs[x] for x in xs], o["beta"], rtol=1e-10, atol=0)
+        np.testing.assert_allclose([res.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
+        np.testing.assert_array_equal([res.coefs[x] for x in xs], [out[0].coefs[x] for x in xs])
+        np.testing.assert_array_equal([res.std_errors[x] for x in xs], [out[0].std_errors[x] for x in xs])
