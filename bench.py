@@ -256,7 +256,7 @@ def pmc_traffic(kernel: str, a) -> tuple[float | None, str | None]:
     configuration (tools/pmc.sh + tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
     correction of MI355X_MICROARCH.md), else None."""
     cfg = {"rows": a.rows, "k": a.k, "levels": list(a.levels), "vcov": a.vcov}
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         try:
             with open(path) as f:
