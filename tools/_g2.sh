@@ -1,5 +1,5 @@
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_determinism.py tests/test_gpu_parity.py > gpurun_out/pt2.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_determinism.py tests/test_gpu_multirank.py tests/test_gpu_stream.py tests/test_gpu_parity.py > gpurun_out/pt2.log 2>&1; rc=$?
 tail -4 gpurun_out/pt2.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python bench.py --no-cpu --no-h2d --steps 20 --warmup 5 > gpurun_out/b1.log 2>&1 || exit 1
