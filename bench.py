@@ -63,6 +63,9 @@ def parse(argv=None):
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--shard", choices=["auto", "owner", "rows"], default="auto")
     ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--emulate-rank", type=str, default=None, metavar="R/N",
+                    help="diagnostic: solve rank R's owner shard of an N-rank strong-scaled run alone on one "
+                         "GPU (no collectives): the per-rank compute and fixed cost of the N-GPU run")
     ap.add_argument("--cpu-rows", type=int, default=50_000_000, help="CPU baseline sample (prefix rows)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-h2d", action="store_true")
@@ -84,7 +87,7 @@ def parse(argv=None):
 
 def is_headline(a) -> bool:
     return (a.rows, a.k, a.levels, a.vcov.lower()) == (50_000_000, 10, [100_000, 1_000], "hc1") \
-        and (a.scaling == "strong" or a.gpus == 1)
+        and (a.scaling == "strong" or a.gpus == 1) and not a.emulate_rank
 
 
 def workload_label(a, world: int) -> str:
@@ -206,6 +209,9 @@ def load_shard(eng, a, rank: int, world: int, shard: str) -> dict:
 
     total = a.rows if a.scaling == "strong" else a.rows * world
     beta = synth.betas(a.k)
+    if a.emulate_rank:
+        rank, world = (int(x) for x in a.emulate_rank.split("/"))
+        shard = "owner"
     if shard == "owner":
         # every row whose primary-FE code lies in this rank's level range (dist.owner_range)
         P = max(range(len(a.levels)), key=lambda f: a.levels[f])
@@ -371,7 +377,7 @@ def main(argv=None):
         kstats = eng.kernel_stats()
         eng.profile(False)
 
-    total_rows = geo["total"]
+    total_rows = geo["total"] if not a.emulate_rank else geo["local"]
     value = total_rows * a.steps / elapsed / 1e6
     ms_step = elapsed / a.steps * 1e3
     p, F = a.k + 1, len(a.levels)
@@ -444,7 +450,8 @@ def main(argv=None):
             "config": {"workload": workload_label(a, d.world), "rows_total": total_rows,
                        "rows_rank0": geo["local"], "k": a.k, "levels": a.levels, "vcov": a.vcov,
                        "cluster_fes": a.cl, "iterations": res["iterations"],
-                       "parallelism": f"dp{d.world} ({shard}-sharded rows, RCCL inside the engine)"},
+                       "parallelism": f"dp{d.world} ({shard}-sharded rows, RCCL inside the engine)"
+                       if not a.emulate_rank else f"rank {a.emulate_rank} owner shard solved alone (diagnostic)"},
             "roofline": roofline,
             "cpu_baseline": extra.get("cpu_baseline"),
             "h2d": extra.get("h2d"),

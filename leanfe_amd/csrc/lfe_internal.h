@@ -202,6 +202,8 @@ struct lfe_ctx {
   int32_t* bitems_d = nullptr;   // device [nb + 1]: first work item of each bucket (in items_d)
   int32_t* xitems_d = nullptr;   // device [n_xgrid]: work item of each block, XCD-grouped (-1: idle; in items_d)
   int n_xgrid = 0;
+  int32_t* blist_d = nullptr;    // device [nbe]: the buckets that hold rows, in order (in items_d)
+  int nbe = 0;                   // buckets that hold rows (an owner shard: its own levels' buckets)
   // segment layout (fast path, F == 2): kept rows sorted by the primary code
   int32_t* seg_off = nullptr;    // [nb * B + 1] local row offsets of each primary group
   size_t seg_off_cap = 0;
@@ -295,6 +297,7 @@ struct lfe_ctx {
   bool loading = false;
   // state
   int64_t n_kept = 0;
+  int64_t n_kept_local = 0;  // kept rows of this shard
   bool loaded = false, prepared = false, demeaned = false;
   bool sums_ready = false;  // S (and W, Sy) already enqueued by lfe_drop_singletons
   bool seg_ready = false;   // segment layouts built for the current drop_singletons

@@ -485,6 +485,15 @@ __global__ void k_unit_bounds(const int32_t* __restrict__ seg_off, int32_t H, in
       if (seg_off[mid] < target) lo = mid + 1;
       else hi = mid;
     }
+    // then the first segment from there on that holds rows (H: none), so no unit starts with a
+    // run of empty segments (an owner shard's buckets hold every other rank's levels too)
+    const int32_t t = lo < H ? seg_off[lo] : 0;
+    hi = H;
+    while (lo < hi) {  // first h with seg_off[h + 1] > t
+      const int mid = (lo + hi) >> 1;
+      if (seg_off[mid + 1] <= t) lo = mid + 1;
+      else hi = mid;
+    }
     units[k] = lo;
   }
 }
@@ -592,9 +601,9 @@ static int build_layouts(lfe_ctx* c, int Q) {
   // K1's waves idle (n < 2048 per wave).  Same-box A/B, ms per solve for K1: 1M rows (config 1)
   // 0.339 -> 0.112; 6.25M 0.099 -> 0.097; at 50M 2048 stays best (0.478 vs 0.523 for 512).
   const int64_t waves = (int64_t)c->n_cu * 16;  // K1: one 1024-thread workgroup per CU
-  const int64_t U = c->n >= 2048 * waves ? 2048 : 512;
+  const int64_t U = c->n_kept_local >= 2048 * waves ? 2048 : 512;
   const int32_t H = L.nb * B;
-  c->n_units = (int)std::max<int64_t>(1, (c->n + U - 1) / U);
+  c->n_units = (int)std::max<int64_t>(1, (c->n_kept_local + U - 1) / U);
   LFE_TRY(ensure_i32(c, c->seg_units, c->seg_units_cap, (size_t)c->n_units + 1));
   {
     ProfScope _ps(c, K_MISC);
@@ -695,6 +704,7 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
     if (h >= h1) continue;
     int r0 = a.seg_off[h], r1 = a.seg_off[h + 1];
     const int g0 = r0 >> 4, g1 = (a.seg_off[h1] + 15) >> 4;
+    const int rend = a.seg_off[h1];  // the unit's rows end here
     double acc[NT];
 #pragma unroll
     for (int I = 0; I < NT; ++I) acc[I] = 0.0;
@@ -716,6 +726,32 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
       }
     };
     bool done = false;
+    // the ends of segments hb .. hb + 63 in the lanes of one register (no global load per
+    // segment).  Segments without rows are passed over unwritten: their outputs are 0 from the
+    // zeroed table (T_P: the memset before K1; alpha_P: prepare_layout)
+    int hb = h;
+    int win = hb + lane < h1 ? a.seg_off[hb + lane + 1] : 0x7fffffff;
+    auto next_seg = [&]() -> bool {  // segment h is complete
+      ++h;
+      r0 = r1;
+      if (r0 >= rend) return false;  // the rest of the unit's segments are empty
+      while (true) {  // a segment with rows lies ahead in the unit
+        const int d = h - hb;
+        if (d >= 64) {
+          hb = h;
+          win = hb + lane < h1 ? a.seg_off[hb + lane + 1] : 0x7fffffff;
+          continue;
+        }
+        const uint64_t m = __ballot(win > r0) & (~0ull << d);
+        if (m) {
+          const int k = (int)__builtin_ctzll(m);
+          h = hb + k;
+          r1 = __builtin_amdgcn_readlane(win, k);
+          return true;
+        }
+        h = hb + 64;
+      }
+    };
     // one 16-row group: lane rows g*16 + 4 kq + s
     auto group = [&](int g, const int4& q4) {
       const int gs = g * 16, rb = gs + 4 * kq;
@@ -728,12 +764,7 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
         }
         if (gs + 16 < r1) return;
         finalize();
-        if (++h >= h1) {
-          done = true;
-          return;
-        }
-        r0 = r1;
-        r1 = a.seg_off[h + 1];
+        if (!next_seg()) done = true;
         return;
       }
       while (true) {  // the group holds a segment boundary
@@ -746,12 +777,10 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
         }
         if (r1 > gs + 16) return;  // segment h continues in the next group
         finalize();
-        if (++h >= h1) {
+        if (!next_seg()) {
           done = true;
           return;
         }
-        r0 = r1;
-        r1 = a.seg_off[h + 1];
       }
     };
     auto load = [&](int gb) -> int4 {
@@ -834,15 +863,17 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
 struct TqArgs {
   const int32_t* run_off;  // [nb * G_Q + 1] run offsets
   const uint16_t* run_h;   // primary code - lo of each kept row, run order
-  int nb, s, G_Q, G_P, p;
+  const int32_t* blist;    // [nbe] the buckets that hold rows, in order
+  int nbe, s, G_Q, G_P, p;
   const double* alphaP;  // [G_P][p]
-  double* runs;          // [nb * G_Q][p]: the sum of every (bucket, q) run (empty runs: 0)
+  double* runs;          // [nbe * G_Q][p]: the sum of every (listed bucket, q) run (empty runs: 0)
   int split;             // workgroups per bucket (each takes 1 / split of the bucket's runs)
 };
 
-// K2: runs[b][q] = sum over the (bucket b, q) run of alpha_P[h_i].  Every run is summed by one
-// wave in row order and every slot is written, so T_Q[q] = sum_b runs[b][q] (k_tq_reduce, in
-// bucket order) is bit-reproducible: no cross-workgroup atomics.
+// K2: runs[i][q] = sum over the (bucket blist[i], q) run of alpha_P[h_i].  Every run is summed by
+// one wave in row order and every slot is written, so T_Q[q] = sum_i runs[i][q] (k_tq_reduce, in
+// bucket order) is bit-reproducible: no cross-workgroup atomics.  Buckets without rows contribute
+// nothing and are not visited.
 template <int NT>
 __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
   constexpr int kTqThreads = tq_threads<NT>();
@@ -857,8 +888,9 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
   for (int I = 0; I < NT; ++I) cl8[I] = 8 * (16 * I + c < p ? 16 * I + c : 0);
   const uint32_t p8 = 8 * p;
   const int kTqSplit = a.split;
-  for (int bs = blockIdx.x; bs < a.nb * kTqSplit; bs += gridDim.x) {
-    const int b = bs / kTqSplit, part = bs % kTqSplit;
+  for (int bs = blockIdx.x; bs < a.nbe * kTqSplit; bs += gridDim.x) {
+    const int bi = bs / kTqSplit, part = bs % kTqSplit;
+    const int b = a.blist[bi];
     const int lo = b << a.s;
     __syncthreads();
     for (int j = tid; j < B * p; j += kTqThreads) {
@@ -873,7 +905,7 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
     const int q1 = (slot + 1) * G_Q / (NW * kTqSplit);
     if (q >= q1) continue;
     const int32_t* off = a.run_off + (int64_t)b * G_Q;
-    double* const runs = a.runs + (int64_t)b * G_Q * p;
+    double* const runs = a.runs + (int64_t)bi * G_Q * p;
     int r0 = off[q], r1 = off[q + 1];
     const int g0 = r0 >> 4, g1 = (off[q1] + 15) >> 4;
     if (g0 >= g1) {  // no rows in these runs
@@ -1107,7 +1139,7 @@ static void launch_tp(lfe_ctx* c, const TpArgs& a, size_t lds) {
 }
 template <int NT>
 static void launch_tq(lfe_ctx* c, const TqArgs& a, size_t lds) {
-  hipLaunchKernelGGL(k_tq<NT>, dim3(a.nb * a.split), dim3(tq_threads<NT>()), lds, c->stream, a);
+  hipLaunchKernelGGL(k_tq<NT>, dim3(std::max(a.nbe, 1) * a.split), dim3(tq_threads<NT>()), lds, c->stream, a);
 }
 
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out) {
@@ -1145,21 +1177,23 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   TqArgs tq{};
   tq.run_off = c->run_off;
   tq.run_h = c->run_h;
-  tq.nb = c->L.nb;
+  tq.blist = c->blist_d;
+  tq.nbe = c->nbe;
   tq.s = c->L.s;
   tq.G_Q = fq.G;
   tq.G_P = fp.G;
   tq.p = p;
   tq.alphaP = fp.alpha;
-  LFE_TRY(ensure_f64(c, c->tq_runs, c->tq_runs_cap, (size_t)c->L.nb * fq.G * p));
+  const int nbe = std::max(c->nbe, 1);
+  LFE_TRY(ensure_f64(c, c->tq_runs, c->tq_runs_cap, (size_t)nbe * fq.G * p));
   tq.runs = c->tq_runs;
   // about four workgroups per CU in all (two resident at a time), so no CU is left with a lone
   // tail: 196 buckets -> 5 per bucket (tq 0.61 -> 0.49 ms per step at 50M rows, measured)
-  tq.split = std::max(kTqSplitDefault / 2, (int)std::lround(4.0 * c->n_cu / std::max(c->L.nb, 1)));
+  tq.split = std::max(kTqSplitDefault / 2, (int)std::lround(4.0 * c->n_cu / nbe));
   {  // every workgroup stages its bucket's 45 KB alpha_P slice: >= 16K rows per workgroup (6.25M
      // rows over 25 buckets: 0.126 -> 0.113 ms per 3 sweeps; 48K rows per workgroup 0.142 ms);
      // a narrower slice (p < 11) pays for proportionally fewer rows
-    const int64_t per_bucket = c->n_kept / std::max(c->L.nb, 1);
+    const int64_t per_bucket = c->n_kept_local / nbe;
     const int64_t min_rows = std::max<int64_t>(2048, (int64_t)16384 * p / 11);
     tq.split = (int)std::max<int64_t>(1, std::min<int64_t>(tq.split, per_bucket / min_rows));
   }
@@ -1207,7 +1241,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       {
         ProfScope _ps(c, K_TQ_REDUCE);
         hipLaunchKernelGGL(k_tq_reduce_fin, dim3(tq_grid), dim3(kTqRedE * kTqRedS), 0, c->stream, c->tq_runs,
-                           c->L.nb, m, fq.T, fq.S, fq.cnt, p, fq.alpha, c->alpha_spare,
+                           c->nbe, m, fq.T, fq.S, fq.cnt, p, fq.alpha, c->alpha_spare,
                            check ? reinterpret_cast<unsigned long long*>(c->dred) : nullptr);
       }
       LFE_HIP(hipGetLastError());
@@ -1215,7 +1249,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     } else {
       {
         ProfScope _ps(c, K_TQ_REDUCE);
-        hipLaunchKernelGGL(k_tq_reduce, dim3(tq_grid), dim3(kTqRedE * kTqRedS), 0, c->stream, c->tq_runs, c->L.nb,
+        hipLaunchKernelGGL(k_tq_reduce, dim3(tq_grid), dim3(kTqRedE * kTqRedS), 0, c->stream, c->tq_runs, c->nbe,
                            m, fq.T);
       }
       LFE_HIP(hipGetLastError());

@@ -747,19 +747,29 @@ static int build_items(lfe_ctx* c) {
     if (xg.empty()) xg.push_back(0);
     c->n_xgrid = (int)xg.size();
   }
-  // items, bucket firsts and the XCD order share one device buffer and one upload through
-  // pinned staging, asynchronously (the staging buffer is next written only after later stream
-  // synchronizations); bitems_d / xitems_d point into it
-  const size_t ni = L.hitems.size(), nbf = bfirst.size(), nx = xg.size();
-  LFE_TRY(ensure_items(c, (ni + nbf + nx + 3) / 4));
+  // the buckets that hold rows, in order: the secondary cross term (K2) runs over these only.  An
+  // owner shard of N ranks holds ~1/N of the primary FE's buckets; the rest are empty
+  std::vector<int32_t> bl;
+  for (int b = 0; b < L.nb; ++b)
+    if (L.bstart[b + 1] > L.bstart[b]) bl.push_back(b);
+  c->nbe = (int)bl.size();
+  if (bl.empty()) bl.push_back(0);
+  // items, bucket firsts, the XCD order and the bucket list share one device buffer and one upload
+  // through pinned staging, asynchronously (the staging buffer is next written only after later
+  // stream synchronizations); bitems_d / xitems_d / blist_d point into it
+  const size_t ni = L.hitems.size(), nbf = bfirst.size(), nx = xg.size(), nl = bl.size();
+  LFE_TRY(ensure_items(c, (ni + nbf + nx + nl + 3) / 4));
   c->bitems_d = c->items_d + ni;
   c->xitems_d = c->items_d + ni + nbf;
-  const size_t ib = sizeof(int32_t) * ni, bb = sizeof(int32_t) * nbf, xb = sizeof(int32_t) * nx;
-  LFE_TRY(ensure_pinned_items(c, ib + bb + xb));
+  c->blist_d = c->items_d + ni + nbf + nx;
+  const size_t ib = sizeof(int32_t) * ni, bb = sizeof(int32_t) * nbf, xb = sizeof(int32_t) * nx,
+               lb = sizeof(int32_t) * nl;
+  LFE_TRY(ensure_pinned_items(c, ib + bb + xb + lb));
   memcpy(c->hpin_items, L.hitems.data(), ib);
   memcpy(c->hpin_items + ib, bfirst.data(), bb);
   memcpy(c->hpin_items + ib + bb, xg.data(), xb);
-  LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb, hipMemcpyHostToDevice, c->stream));
+  memcpy(c->hpin_items + ib + bb + xb, bl.data(), lb);
+  LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb + lb, hipMemcpyHostToDevice, c->stream));
   return LFE_OK;
 }
 
@@ -856,6 +866,9 @@ int prepare_layout(lfe_ctx* c) {
       z.push_back({fe.drops, sizeof(int32_t) * fe.G});
       z.push_back({fe.S, sizeof(double) * (size_t)fe.G * c->p});
     }
+    // the primary FE's effects: the two-FE sweeps' K1 writes only the levels with rows on this
+    // shard (an owner shard's other levels, levels whose rows were all dropped stay 0)
+    if (L.P >= 0) z.push_back({c->fe[L.P].alpha, sizeof(double) * (size_t)c->fe[L.P].G * c->p});
     z.push_back({c->iscratch, sizeof(int32_t) * kIscratchInts});
     LFE_TRY(zero_ranges(c, z));
     c->sums_zeroed = true;
@@ -1050,6 +1063,7 @@ int prepare_layout(lfe_ctx* c) {
     c->fe[L.P].card = (int32_t)kept[2];
   }
   c->n_kept = (int64_t)kept[0];
+  c->n_kept_local = n - h[2 * kMaxFE];
   return LFE_OK;
 }
 
