@@ -896,8 +896,19 @@ int prepare_layout(lfe_ctx* c) {
     // one 16-wave workgroup per CU: with two per CU (32 waves) twice as many chunks write into
     // every bucket region at once and the scatter ran 13 % slower (measured); pad the LDS request
     constexpr size_t kLdsMin = 82 * 1024;
-    // 16K-row chunks: ~84-row runs per bucket at s = 9
+    // 16K-row chunks: ~84-row runs per bucket at s = 9.  One workgroup per CU: a shard of few
+    // chunks (the 8-GPU shard: 382 for 256 CUs) leaves CUs idle in the last round, so the chunk
+    // halves (down to 4K rows) while that fills the rounds markedly better
     int64_t cw = nb <= 512 ? 16384 : 4096;
+    if (cw == 16384) {
+      auto fill = [&](int64_t w) {
+        const int64_t k = (n + w - 1) / w, r = (k + c->n_cu - 1) / c->n_cu;
+        return (double)k / (double)(std::max<int64_t>(r, 1) * c->n_cu);
+      };
+      for (int64_t w = 8192; w >= 4096; w /= 2)
+        if (fill(w) > fill(cw) + 0.1) cw = w;
+    }
+    if (const char* e = getenv("LFE_PART_CW")) cw = atoll(e);  // A/B only
     auto part_lds = [&](int nth) {
       return sizeof(double) * cw + sizeof(int32_t) * ((size_t)(nth / 64) * nb + 2 * (size_t)nb + 1);
     };
