@@ -114,6 +114,7 @@ struct ClusterWS {
   size_t seg_off_cap = 0;
   int32_t* ufirst = nullptr;
   size_t ufirst_cap = 0;
+  bool lay_move = false;        // the partition moves the cluster columns into lay (prepare_layout)
   // owner-partitioned exchange (multi-rank, many clusters)
   uint64_t* skey = nullptr;     // [G_local] segment keys -> send order
   size_t skey_cap = 0;

@@ -270,6 +270,9 @@ struct ScatterArgs {
   const int32_t* scanned;  // [nb][nchunks] exclusive destinations
   int cols;                // move the X / w columns and the codes
   int want_orig;           // write the input row index of each layout row
+  int ncl;                 // with cols: loaded cluster columns moved into layout order too
+  const int32_t* cl[kMaxCl];
+  int32_t* clo[kMaxCl];
   double* colstat;         // with cols: max |x_c| (u64 bits, atomicMax) and per-chunk sums of x_c^2
 };
 
@@ -523,16 +526,18 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   if (full) move_cols(std::true_type{});
   else move_cols(std::false_type{});
   int32_t* istage0 = reinterpret_cast<int32_t*>(stage);
-  const int ic0 = a.cols ? 0 : a.F;
-  for (int c = ic0; c < a.F + a.want_orig; ++c) {  // F code arrays, then the input row index
-    int32_t* dst = c < a.F ? a.codeo[c] : a.orig;
+  const int ic0 = a.cols ? 0 : a.F + a.ncl;
+  // F code arrays, the cluster columns, then the input row index
+  for (int c = ic0; c < a.F + a.ncl + a.want_orig; ++c) {
+    const int32_t* src = c < a.F ? a.code[c] : c < a.F + a.ncl ? a.cl[c - a.F] : nullptr;
+    int32_t* dst = c < a.F ? a.codeo[c] : c < a.F + a.ncl ? a.clo[c - a.F] : a.orig;
     int32_t* istage = istage0 + ((c - ic0) & 1) * R;  // two int32 halves of the double stage
 #pragma unroll
     for (int k = 0; k < PER; k += 2) {
       const int64_t i = row_of(k);
       int2 g = int2{(int32_t)i, (int32_t)i + 1};
       const int q0 = pos_of(k), q1 = pos_of(k + 1);
-      if (c < a.F && q0 >= 0) g = *reinterpret_cast<const int2*>(a.code[c] + i);
+      if (src && q0 >= 0) g = *reinterpret_cast<const int2*>(src + i);
       if (q0 >= 0) istage[q0] = g.x;
       if (q1 >= 0) istage[q1] = g.y;
     }
@@ -800,6 +805,15 @@ static int launch_part_scatter(lfe_ctx* c, int cols, int orig) {
   a.scanned = c->pcounts;
   a.cols = cols;
   a.want_orig = orig;
+  // the cluster columns ride along with the codes when their layout copies are wanted now
+  a.ncl = 0;
+  if (cols && c->clw.lay_move) {
+    a.ncl = (int)c->cl.size();
+    for (int j = 0; j < a.ncl; ++j) {
+      a.cl[j] = c->cl[j];
+      a.clo[j] = c->clw.lay[j];
+    }
+  }
   a.colstat = c->colstat;
   a.nbits = 0;  // bits of a bucket id (ballot ranking)
   while ((1 << a.nbits) < L.nb) ++a.nbits;
@@ -938,7 +952,19 @@ int prepare_layout(lfe_ctx* c) {
     L.part = PartGeom{nth, per, nw, lds};
     // the input row index of each layout row is written only when a caller needs it
     // (ensure_layout_orig: cluster, records and demeaned-column export paths)
+    // loaded cluster columns (clustered SEs follow this solve) move with the codes: no later
+    // orig-only launch and row-index gathers (lfe_cluster.hip launch_cluster_subsets)
+    auto& W = c->clw;
+    W.lay_move = !c->sw.on && !c->cl.empty() && (int)c->cl.size() <= kMaxCl;
+    if (W.lay_move) {
+      const int m = (int)c->cl.size();
+      W.lay.resize(m, nullptr);
+      W.lay_cap.resize(m, 0);
+      for (int j = 0; j < m; ++j) LFE_TRY(ensure_i32(c, W.lay[j], W.lay_cap[j], (size_t)c->ld));
+    }
     LFE_TRY(launch_part_scatter(c, /*cols=*/c->sw.on ? 2 : 1, /*orig=*/0));
+    W.lay_valid = W.lay_move;
+    W.lay_move = false;
     L.orig_pending = true;
     LFE_HIP(hipGetLastError());
     L.bstart.assign(nb + 1, 0);

@@ -385,21 +385,35 @@ struct CrossQArgs {
   int wcol;
   double* xq;
 };
-__global__ void k_cross_quanta(CrossQArgs a) {
-  const int col = threadIdx.x;
-  if (col >= a.pc) return;
-  double M = 0.0, rms = 0.0;
+// one block of 1024 threads: wave w sums the slots of blocks b = w, w + 16, ... (lane = column, lane
+// 63 the counts), then lane col adds the 16 wave partials in order (a fixed order; the slots of
+// up to kAstatBlocks blocks were one thread's serial loop, ~0.15 ms per launch)
+__global__ __launch_bounds__(1024) void k_cross_quanta(CrossQArgs a) {
+  __shared__ double part[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double rms = 0.0;
   for (int j = 0; j < a.F; ++j) {
     if (j == a.f) continue;
-    M += __longlong_as_double((long long)a.amax[j * kMaxCols + col]);
     const double* sl = a.astat + (int64_t)j * kAstatBlocks * 64;
-    double sq = 0.0, nn = 0.0;
-    for (int b = 0; b < a.nblk[j]; ++b) {
-      sq += sl[b * 64 + col];
-      nn += sl[b * 64 + 63];
+    double t = 0.0;
+    for (int b = wave; b < a.nblk[j]; b += 16) t += sl[b * 64 + lane];
+    part[wave][lane] = t;
+    __syncthreads();
+    if (wave == 0) {
+      double sq = 0.0, nn = 0.0;
+      for (int w = 0; w < 16; ++w) {
+        sq += part[w][lane];
+        nn += part[w][63];
+      }
+      rms += nn > 0.0 ? sqrt(sq / nn) : 0.0;
     }
-    rms += nn > 0.0 ? sqrt(sq / nn) : 0.0;
+    __syncthreads();
   }
+  const int col = lane;
+  if (wave != 0 || col >= a.pc) return;
+  double M = 0.0;
+  for (int j = 0; j < a.F; ++j)
+    if (j != a.f) M += __longlong_as_double((long long)a.amax[j * kMaxCols + col]);
   if (a.wfq) {
     M *= a.wfq[FQ_MAX * kFqCols + a.wcol];
     rms *= a.wfq[FQ_RMS * kFqCols + a.wcol];
@@ -665,7 +679,7 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
     q.wfq = wt ? c->fixq : nullptr;  // sums4's weighted quanta: column p is w
     q.wcol = c->p;
     q.xq = c->xq;
-    hipLaunchKernelGGL(k_cross_quanta, dim3(1), dim3(64), 0, c->stream, q);
+    hipLaunchKernelGGL(k_cross_quanta, dim3(1), dim3(1024), 0, c->stream, q);
     LFE_HIP(hipGetLastError());
     a.xq = c->xq;
     a.Thi = fe.hi;
