@@ -286,35 +286,46 @@ __global__ void k_str_keys(StrArgs a, uint64_t* __restrict__ keys, int32_t* __re
   }
 }
 
-// flag[q] = hash change; count neighbours with equal hashes but different strings
+// flag[q] = hash change; mm[q] = 1 where a neighbour has an equal hash but a different string
+// (counted into nmismatch)
 __global__ void k_str_heads(StrArgs a, const uint64_t* __restrict__ K, const int32_t* __restrict__ R,
-                            int32_t* __restrict__ flag, int32_t* __restrict__ nmismatch) {
+                            int32_t* __restrict__ flag, int32_t* __restrict__ nmismatch, int32_t* __restrict__ mm) {
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += (int64_t)gridDim.x * blockDim.x) {
     const bool head = q == 0 || K[q] != K[q - 1];
     flag[q] = head ? 1 : 0;
-    if (!head && !str_equal(a, R[q], R[q - 1])) atomicAdd(nmismatch, 1);
+    const bool mis = !head && !str_equal(a, R[q], R[q - 1]);
+    mm[q] = mis ? 1 : 0;
+    if (mis) atomicAdd(nmismatch, 1);
   }
 }
 
-// Exact split of hash runs (one thread per run head).  A run of d distinct strings sets
-// flag[head] = d, and adj[i] = local index of member i's string (first-occurrence order in
-// the run) minus d for every member but the head, so that after the exclusive scan of flag
-// code(i) = scan[i] + adj[i] (k_str_codes).  A run of one string: adj = 0 at the head, -1 after.
+// Collision path, step 1: adj = 0 at every run head, -1 elsewhere (a run of one string), and the
+// head of every run holding a mismatch is marked flag = -1 (the mismatching position walks back
+// to its head: collisions are rare, so are these walks)
+__global__ void k_str_mark(const uint64_t* __restrict__ K, const int32_t* __restrict__ mm, int64_t n,
+                           int32_t* __restrict__ flag, int32_t* __restrict__ adj) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+    const bool head = q == 0 || K[q] != K[q - 1];
+    adj[q] = head ? 0 : -1;
+    if (mm[q]) {
+      int64_t h = q;
+      while (h > 0 && K[h - 1] == K[q]) --h;
+      flag[h] = -1;  // (every writer stores the same value)
+    }
+  }
+}
+
+// Step 2: exact split of the marked runs (one thread per marked head).  A run of d distinct
+// strings sets flag[head] = d, and adj[i] = local index of member i's string (first-occurrence
+// order in the run) minus d for every member but the head, so that after the exclusive scan of
+// flag code(i) = scan[i] + adj[i] (k_str_codes).  Runs of one string keep step 1's adj and are not
+// walked (a frequent string with no colliding neighbour costs nothing here).
 __global__ void k_str_exact(StrArgs a, const uint64_t* __restrict__ K, const int32_t* __restrict__ R,
                             int32_t* __restrict__ flag, int32_t* __restrict__ adj) {
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += (int64_t)gridDim.x * blockDim.x) {
-    if (!(q == 0 || K[q] != K[q - 1])) continue;
+    if (flag[q] != -1) continue;
     int64_t e = q + 1;
-    bool mixed = false;
-    while (e < a.n && K[e] == K[q]) {
-      mixed = mixed || !str_equal(a, R[e], R[e - 1]);
-      ++e;
-    }
-    if (!mixed) {
-      adj[q] = 0;
-      for (int64_t i = q + 1; i < e; ++i) adj[i] = -1;
-      continue;
-    }
+    while (e < a.n && K[e] == K[q]) ++e;
     int32_t d = 0;
     for (int64_t i = q; i < e; ++i) {  // adj[i] = local index (first occurrence order)
       int64_t j = q;
@@ -494,13 +505,18 @@ int lfe_factorize_strings(lfe_ctx* c, int64_t n, const int64_t* offsets, const u
   LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double), c->stream));
   int32_t* nmis = reinterpret_cast<int32_t*>(c->dred);
   LFE_HIP(hipMemsetAsync(W.flag + n, 0, sizeof(int32_t), c->stream));
+  // the sort's spare key buffer (n x u64): adj [n] and the mismatch marks [n]
+  int32_t* adj = reinterpret_cast<int32_t*>(W.keys[1 - buf]);
+  int32_t* mm = adj + n;
   hipLaunchKernelGGL(k_str_heads, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, K, R, W.flag,
-                     nmis);
+                     nmis, mm);
   LFE_HIP(hipGetLastError());
   int32_t mismatches = 0;
   LFE_TRY(d2h_sync(c, &mismatches, nmis, sizeof(int32_t)));
-  int32_t* adj = reinterpret_cast<int32_t*>(W.keys[1 - buf]);  // the sort's spare key buffer (n x u64)
   if (mismatches > 0) {
+    hipLaunchKernelGGL(k_str_mark, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, K, mm, n, W.flag,
+                       adj);
+    LFE_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_str_exact, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, K, R, W.flag,
                        adj);
     LFE_HIP(hipGetLastError());

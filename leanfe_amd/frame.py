@@ -81,15 +81,19 @@ def factorize(values, global_codes: bool = False, device=None) -> tuple[np.ndarr
 
     Non-negative integer columns whose maximum is below max(4n, 2^20) are used
     as codes directly (O(n); unused code values are empty groups, which every
-    kernel ignores).  Anything else (strings, floats, sparse ids) goes through
-    a sorted unique.  Only group membership matters for the estimator.
+    kernel ignores).  Without ``device`` anything else (strings, floats, sparse
+    ids) goes through a sorted unique.  Only group membership matters for the
+    estimator: the codes' numbering is not part of the result.
 
     ``global_codes`` (row shards of one fit): the values must already be global
     non-negative integer codes and are used as they are, since a per-shard
     unique would number the groups differently on every rank.
 
-    ``device`` (an ``Engine``): sparse integer ids are factorized on the GPU
-    (``Engine.factorize_ids``, a radix sort; same codes as the sorted unique)."""
+    ``device`` (an ``Engine``): sparse integer and float ids are factorized on the GPU
+    (``Engine.factorize_ids``, a radix sort; same codes as the sorted unique); strings and
+    bytes without nulls too (``Engine.factorize_strings``), whose codes follow the order of
+    the strings' 64-bit hashes, not lexicographic order (same groups as the sorted unique).
+    String columns with nulls, or without pyarrow, keep the sorted unique."""
     v = np.asarray(values)
     n = v.size
     if global_codes:
@@ -122,8 +126,11 @@ def factorize(values, global_codes: bool = False, device=None) -> tuple[np.ndarr
 def string_buffers(values) -> tuple[np.ndarray, np.ndarray] | None:
     """Arrow layout of a string (or bytes) column: int64 offsets [n + 1] starting at 0 and the
     uint8 bytes, for ``lfe_factorize_strings``.  None when the values are not all strings / all
-    bytes or hold nulls (those keep the host's sorted unique)."""
-    import pyarrow as pa
+    bytes or hold nulls (those keep the host's sorted unique), and None without pyarrow."""
+    try:
+        import pyarrow as pa
+    except ImportError:
+        return None
 
     if isinstance(values, pa.ChunkedArray):
         arr = values.combine_chunks()

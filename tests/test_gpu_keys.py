@@ -168,6 +168,29 @@ def test_factorize_strings_exact_grouping(eng, hash_bits):
     _same_partition(codes, G, inv.ravel(), uniq.size)
 
 
+def test_factorize_strings_frequent_value_beside_collisions(eng):
+    """A very frequent string whose hash run holds only that string is not walked by the exact
+    split, even when other runs collide (20-bit hashes over 20K strings: ~200 colliding pairs);
+    the grouping is exact (k_str_exact walked every run head serially)."""
+    import time
+
+    from leanfe_amd import frame
+    rng = np.random.default_rng(5)
+    pool = _words(rng, 20_000, 20_000)
+    v = np.concatenate([np.array(["the frequent value"] * 1_000_000, dtype=object), pool[rng.integers(0, pool.size, 500_000)]])
+    v = v[rng.permutation(v.size)]
+    os.environ["LFE_STR_HASH_BITS"] = "20"
+    try:
+        t0 = time.perf_counter()
+        codes, G = frame.factorize(v, device=eng)
+        dt = time.perf_counter() - t0
+    finally:
+        os.environ.pop("LFE_STR_HASH_BITS", None)
+    uniq, inv = np.unique(v.astype(str), return_inverse=True)
+    _same_partition(codes, G, inv.ravel(), uniq.size)
+    assert dt < 10.0, dt
+
+
 @pytest.mark.parametrize("case", ["single", "all_equal", "all_empty", "bytes", "arrow_slice"])
 def test_factorize_strings_edge_cases(eng, case):
     import pyarrow as pa
