@@ -578,6 +578,9 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->hpin_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->up_ev0, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->up_ev1, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->hpin), kPinSmall, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess) {
     delete c;
@@ -620,6 +623,9 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   for (auto& e : c->load_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->aux_ev) (void)hipEventDestroy(c->aux_ev);
+  if (c->up_ev0) (void)hipEventDestroy(c->up_ev0);
+  if (c->up_ev1) (void)hipEventDestroy(c->up_ev1);
+  if (c->up_stream) (void)hipStreamDestroy(c->up_stream);
   dfree(c->clS);
   dfree(c->clP);
   if (c->comm) ncclCommDestroy(c->comm);

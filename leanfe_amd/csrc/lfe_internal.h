@@ -230,6 +230,10 @@ struct lfe_ctx {
   char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
   hipEvent_t hpin_ev = nullptr;    // last H2D from the staging region
   hipEvent_t aux_ev = nullptr;     // completion of an asynchronous D2H into the staging region
+  // the layout's work-item upload runs on its own stream while the partition scatter runs:
+  // up_ev0 (main stream, before the scatter: earlier readers of items_d are done), up_ev1 (upload done)
+  hipStream_t up_stream = nullptr;
+  hipEvent_t up_ev0 = nullptr, up_ev1 = nullptr;
   char* hpin_items = nullptr;      // work-item upload staging
   size_t hpin_items_cap = 0;
   double* scores = nullptr;  // row-major [ld][score_k] score rows u r (w), layout order (p * ld allocated)

@@ -708,6 +708,17 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
     double acc[NT];
 #pragma unroll
     for (int I = 0; I < NT; ++I) acc[I] = 0.0;
+    // the fused projection's operands of segment h (count, S_P row), loaded when the segment
+    // starts so that their latency hides under its rows (short segments: one stall each before)
+    int32_t pn = 0;
+    double ps[NT];
+    auto prefetch = [&]() {
+      if (!a.fused || h >= a.G_P) return;
+      pn = a.cntP[h];
+#pragma unroll
+      for (int I = 0; I < NT; ++I) ps[I] = a.S_P[(int64_t)h * p + (16 * I + c < p ? 16 * I + c : 0)];
+    };
+    prefetch();
     auto finalize = [&]() {  // segment h complete
 #pragma unroll
       for (int I = 0; I < NT; ++I) {
@@ -715,12 +726,8 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
         const int col = 16 * I + c;
         if (kq == 0 && col < p && h < a.G_P) {
           const int64_t e = (int64_t)h * p + col;
-          if (a.fused) {
-            const int32_t n = a.cntP[h];
-            a.out[e] = n > 0 ? (a.S_P[e] - t) / (double)n : 0.0;
-          } else {
-            a.out[e] = t;
-          }
+          if (a.fused) a.out[e] = pn > 0 ? (ps[I] - t) / (double)pn : 0.0;
+          else a.out[e] = t;
         }
         acc[I] = 0.0;
       }
@@ -747,6 +754,7 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
           const int k = (int)__builtin_ctzll(m);
           h = hb + k;
           r1 = __builtin_amdgcn_readlane(win, k);
+          prefetch();
           return true;
         }
         h = hb + 64;
@@ -912,6 +920,16 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
       for (int j = lane; j < (q1 - q) * p; j += 64) runs[(int64_t)q * p + j] = 0.0;
       continue;
     }
+    // the ends of runs qb .. qb + 63 in the lanes of one register: no global load per run
+    int qb = q;
+    int win = qb + lane < q1 ? off[qb + lane + 1] : 0;
+    auto run_end = [&](int qq) -> int {
+      if (qq - qb >= 64) {
+        qb = qq;
+        win = qb + lane < q1 ? off[qb + lane + 1] : 0;
+      }
+      return __builtin_amdgcn_readlane(win, qq - qb);
+    };
     double acc[NT];
 #pragma unroll
     for (int I = 0; I < NT; ++I) acc[I] = 0.0;
@@ -941,7 +959,7 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
           return;
         }
         r0 = r1;
-        r1 = off[q + 1];
+        r1 = run_end(q);
         return;
       }
       while (true) {  // the group holds a run boundary
@@ -959,7 +977,7 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
           return;
         }
         r0 = r1;
-        r1 = off[q + 1];
+        r1 = run_end(q);
       }
     };
     // ushort4 of codes = 2 dwords per lane; broadcast dword-wise
@@ -1196,6 +1214,10 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     const int64_t per_bucket = c->n_kept_local / nbe;
     const int64_t min_rows = std::max<int64_t>(2048, (int64_t)16384 * p / 11);
     tq.split = (int)std::max<int64_t>(1, std::min<int64_t>(tq.split, per_bucket / min_rows));
+    // ... but no fewer workgroups than CUs while each keeps >= 8K rows (6.25M rows over 196
+    // buckets: 196 -> 392 workgroups)
+    const int64_t fill = (c->n_cu + nbe - 1) / nbe;
+    if (tq.split < fill && per_bucket / fill >= 8192) tq.split = (int)fill;
   }
   // sweep 1's Q projection: alpha_P = 0 -> alpha_Q = S_Q / n_Q (alpha_P is first written by K1,
   // which covers every primary group)

@@ -715,7 +715,9 @@ static int choose_shift(int32_t G, int smin) {
   return s;
 }
 
-static int build_items(lfe_ctx* c) {
+// side: upload on up_stream after up_ev0 (recorded before the partition scatter), the main
+// stream waiting for it, so the copy overlaps the scatter instead of following it
+static int build_items(lfe_ctx* c, bool side) {
   auto& L = c->L;
   L.hitems.clear();
   std::vector<int32_t> bfirst(L.nb + 1, 0);
@@ -774,7 +776,14 @@ static int build_items(lfe_ctx* c) {
   memcpy(c->hpin_items + ib, bfirst.data(), bb);
   memcpy(c->hpin_items + ib + bb, xg.data(), xb);
   memcpy(c->hpin_items + ib + bb + xb, bl.data(), lb);
-  LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb + lb, hipMemcpyHostToDevice, c->stream));
+  if (side) {
+    LFE_HIP(hipStreamWaitEvent(c->up_stream, c->up_ev0, 0));
+    LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb + lb, hipMemcpyHostToDevice, c->up_stream));
+    LFE_HIP(hipEventRecord(c->up_ev1, c->up_stream));
+    LFE_HIP(hipStreamWaitEvent(c->stream, c->up_ev1, 0));
+  } else {
+    LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb + lb, hipMemcpyHostToDevice, c->stream));
+  }
   return LFE_OK;
 }
 
@@ -965,6 +974,7 @@ int prepare_layout(lfe_ctx* c) {
       W.lay_cap.resize(m, 0);
       for (int j = 0; j < m; ++j) LFE_TRY(ensure_i32(c, W.lay[j], W.lay_cap[j], (size_t)c->ld));
     }
+    LFE_HIP(hipEventRecord(c->up_ev0, c->stream));  // items_d is free from here (build_items)
     LFE_TRY(launch_part_scatter(c, /*cols=*/c->sw.on ? 2 : 1, /*orig=*/0));
     W.lay_valid = W.lay_move;
     W.lay_move = false;
@@ -988,7 +998,7 @@ int prepare_layout(lfe_ctx* c) {
     }
     L.orig = nullptr;
   }
-  LFE_TRY(build_items(c));
+  LFE_TRY(build_items(c, L.permuted));
 
   if (item_counts) {
     const int Q = 1 - L.P, B = 1 << L.s;
