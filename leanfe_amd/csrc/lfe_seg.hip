@@ -28,6 +28,7 @@
 #include "lfe_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace lfe {
 
@@ -67,6 +68,104 @@ __global__ __launch_bounds__(256) void k_seg_scatter(SegScatterArgs a) {
     const double wi = a.w ? a.w[i] : 0.0;
     for (int f = 0; f < a.F; ++f) {
       const int64_t pos = atomicAdd(&a.cur[f][g[f]], 1);
+      int j = 0;
+      for (int f2 = 0; f2 < a.F; ++f2)
+        if (f2 != f) a.oc[f][(int64_t)(j++) * a.ld + pos] = g[f2];
+      if (a.ws[f]) a.ws[f][pos] = wi;
+    }
+  }
+}
+
+// Block-aggregated variant: a workgroup takes kSegBlkRows consecutive layout rows.  For every FE
+// whose codes in the block fall in a range of at most kSegLocalBins (the whole code range of a
+// small FE; the primary FE's few buckets in the bucket-sorted layout) it counts the block's rows
+// per code in LDS, reserves each code's slots with ONE returning global add, and ranks its rows in
+// LDS; the other FEs keep one returning global add per row.  The slots of a (block, code) pair are
+// consecutive, so the block's stores of the other codes land in short contiguous pieces.  (The
+// order within a pair follows LDS atomics: unstable, as k_seg_scatter; the cross terms' two-limb
+// sums do not depend on it.)
+constexpr int kSegBlkRows = 32768;
+constexpr int kSegBlkThreads = 1024;
+constexpr int kSegLocalBins = 24576;  // LDS bins over all local FEs (96 KB)
+
+struct SegScatter2Args {
+  SegScatterArgs s;
+  int32_t G[kMaxFE];
+  int P;  // the bucketed primary FE (its codes are sorted by bucket in layout order), or -1
+};
+
+__global__ __launch_bounds__(kSegBlkThreads) void k_seg_scatter2(SegScatter2Args A) {
+  const SegScatterArgs& a = A.s;
+  __shared__ int32_t bins[kSegLocalBins];
+  __shared__ int32_t klo[kMaxFE], kw[kMaxFE], boff[kMaxFE + 1];
+  __shared__ int32_t pmin, pmax;
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * kSegBlkRows, r1 = min(a.n, r0 + kSegBlkRows);
+  if (tid == 0) {
+    pmin = 0x7fffffff;
+    pmax = -1;
+  }
+  __syncthreads();
+  // the primary FE's code range in this block (kept rows)
+  if (A.P >= 0) {
+    int32_t mn = 0x7fffffff, mx = -1;
+    for (int64_t i = r0 + tid; i < r1; i += kSegBlkThreads) {
+      if (a.keep[i] < 0) continue;
+      const int32_t g = a.code[A.P][i];
+      mn = min(mn, g);
+      mx = max(mx, g);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      mn = min(mn, __shfl_xor(mn, off, 64));
+      mx = max(mx, __shfl_xor(mx, off, 64));
+    }
+    if ((tid & 63) == 0) {
+      atomicMin(&pmin, mn);
+      atomicMax(&pmax, mx);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {  // which FEs are ranked in LDS, and where their bins live
+    int used = 0;
+    for (int f = 0; f < a.F; ++f) {
+      int lo = 0, w = A.G[f];
+      if (f == A.P) {
+        lo = pmax >= 0 ? pmin : 0;
+        w = pmax >= 0 ? pmax - pmin + 1 : 0;
+      }
+      const bool local = w <= kSegLocalBins - used;
+      klo[f] = lo;
+      kw[f] = local ? w : -1;
+      boff[f] = used;
+      if (local) used += w;
+    }
+    boff[a.F] = used;
+  }
+  __syncthreads();
+  for (int j = tid; j < boff[a.F]; j += kSegBlkThreads) bins[j] = 0;
+  __syncthreads();
+  for (int64_t i = r0 + tid; i < r1; i += kSegBlkThreads) {
+    if (a.keep[i] < 0) continue;
+    for (int f = 0; f < a.F; ++f)
+      if (kw[f] >= 0) atomicAdd(&bins[boff[f] + a.code[f][i] - klo[f]], 1);
+  }
+  __syncthreads();
+  // one returning global add per (local FE, code present): the first slot of the block's rows
+  for (int f = 0; f < a.F; ++f) {
+    if (kw[f] < 0) continue;
+    for (int j = tid; j < kw[f]; j += kSegBlkThreads) {
+      const int32_t cnt = bins[boff[f] + j];
+      if (cnt > 0) bins[boff[f] + j] = atomicAdd(&a.cur[f][klo[f] + j], cnt);
+    }
+  }
+  __syncthreads();
+  for (int64_t i = r0 + tid; i < r1; i += kSegBlkThreads) {
+    if (a.keep[i] < 0) continue;
+    int32_t g[kMaxFE];
+    for (int f = 0; f < a.F; ++f) g[f] = a.code[f][i];
+    const double wi = a.w ? a.w[i] : 0.0;
+    for (int f = 0; f < a.F; ++f) {
+      const int64_t pos = kw[f] >= 0 ? atomicAdd(&bins[boff[f] + g[f] - klo[f]], 1) : atomicAdd(&a.cur[f][g[f]], 1);
       int j = 0;
       for (int f2 = 0; f2 < a.F; ++f2)
         if (f2 != f) a.oc[f][(int64_t)(j++) * a.ld + pos] = g[f2];
@@ -629,7 +728,16 @@ int seg_build(lfe_ctx* c) {
   }
   {
     ProfScope _ps(c, K_SEG_BUILD);
-    if (n > 0) hipLaunchKernelGGL(k_seg_scatter, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, a);
+    if (n > 0 && getenv("LFE_SEG_SCATTER_ROWS") == nullptr) {  // (env: the per-row kernel, A/B only)
+      SegScatter2Args a2{};
+      a2.s = a;
+      for (int f = 0; f < c->F; ++f) a2.G[f] = c->fe[f].G;
+      a2.P = L.permuted ? L.P : -1;
+      hipLaunchKernelGGL(k_seg_scatter2, dim3((unsigned)((n + kSegBlkRows - 1) / kSegBlkRows)), dim3(kSegBlkThreads),
+                         0, c->stream, a2);
+    } else if (n > 0) {
+      hipLaunchKernelGGL(k_seg_scatter, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, a);
+    }
     LFE_HIP(hipGetLastError());
     for (int f = 0; f < c->F; ++f) {
       auto& fe = c->fe[f];
