@@ -341,7 +341,9 @@ def main(argv=None):
     shard = a.shard
     if shard == "auto":
         shard = "owner" if (len(a.levels) == 2 and a.vcov.lower() != "cluster" and d.world > 1) else "rows"
-    eng = Engine(d.local)
+    # LEANFE_BENCH_DEVICE (diagnostic): every rank on that one device, e.g. to run the RCCL path of
+    # a multi-rank solve on a one-GPU box (RCCL must accept several ranks on one device)
+    eng = Engine(int(os.environ.get("LEANFE_BENCH_DEVICE", d.local)))
     if d.world > 1:
         uid = Engine.unique_id() if d.rank == 0 else None
         uid = d.bcast_bytes(uid)
