@@ -978,55 +978,21 @@ __global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restri
     partial[(int64_t)blockIdx.x * NA + e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
 }
 
-// one block: the design tile [16][16] (column 0 = intercept, 1 + j = data column j)
-// from the raw tile + table partials; *flag = 1 when the cancellation guard holds
-template <int PM>
-__global__ __launch_bounds__(256) void k_tables_final(const double* __restrict__ partial, int nblk,
-                                                      const double* __restrict__ raw, int p,
-                                                      double* __restrict__ tile, double* __restrict__ flag) {
-  constexpr int NG = PM * (PM + 1) / 2;
-  constexpr int NA = NG + PM;
-  __shared__ double m[NA];
-  __shared__ int bad;
-  if (threadIdx.x == 0) bad = 0;
-  {  // wave w sums the block partials of entries w, w + 4, ... (lanes over blocks, fixed order)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const auto addop = [](double x, double y) { return x + y; };
-    for (int e = wave; e < NA; e += 4) {
-      double s = 0.0;
-      for (int b = lane; b < nblk; b += 64) s += partial[(int64_t)b * NA + e];
-      s = wave_reduce63(s, 0.0, addop);
-      if (lane == 63) m[e] = s;
-    }
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < 256; t += blockDim.x) {
-    const int i = t / 16 - 1, j = t % 16 - 1;  // design indices -> data columns
-    double v = 0.0;
-    if (i < p && j < p) {
-      if (i < 0 && j < 0) {
-        v = raw[15 * 16 + 15];
-      } else if (i < 0 || j < 0) {
-        const int d = i < 0 ? j : i;
-        v = raw[15 * 16 + d] - m[NG + d];
-      } else {
-        const int lo = i < j ? i : j, hi = i < j ? j : i;
-        v = raw[i * 16 + j] + m[lo * PM - lo * (lo - 1) / 2 + (hi - lo)];
-        if (i == j && !(v > 0.0 && raw[i * 16 + i] <= kTabKappa * v)) atomicAdd(&bad, 1);
-      }
-    }
-    tile[t] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) *flag = bad ? 0.0 : 1.0;
-}
-
 static bool tables_gram_ok(const lfe_ctx* c) {
   return c->raw_ready && c->tq_final && c->F == 2 && c->p <= 12 && c->L.P >= 0 && !c->L.w;
 }
 
-// design tile into out_dev[0, 256) and the guard flag into *flag_dev, from the group tables
-static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev) {
+template <int PM>
+__global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __restrict__ partial, int nblk,
+                                                            const double* __restrict__ raw, int p,
+                                                            double* __restrict__ tile, double* __restrict__ flag,
+                                                            double* __restrict__ beta, double* __restrict__ beta_copy,
+                                                            double* __restrict__ ok);
+
+// design tile into out_dev[0, 256) and the guard flag into *flag_dev, from the group tables; with
+// beta, also the Cholesky solve of the tile (beta, beta_copy, ok as k_chol_solve)
+static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, double* beta = nullptr,
+                               double* beta_copy = nullptr, double* ok = nullptr) {
   const int P = c->L.P, Q = 1 - P, p = c->p;
   TabArgs t{};
   t.alpha[0] = c->fe[P].alpha;
@@ -1052,26 +1018,34 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev) {
   double* part = c->scratch;
   double* msum = c->scratch + (size_t)nblk * NA;
   auto final_from = [&](auto kfinal) -> int {
-    // one workgroup per entry sums the block partials (a tree in fixed order), then one block
-    // forms the tile (owner-sharded rows: the sums over ranks in between)
-    hipLaunchKernelGGL(k_reduce_partials, dim3(NA), dim3(256), 0, c->stream, part, nblk, (int64_t)NA, msum);
-    LFE_HIP(hipGetLastError());
-    if (c->owner_on) LFE_TRY(allreduce_sum_f64(c, msum, (size_t)NA));
-    hipLaunchKernelGGL(kfinal, dim3(1), dim3(256), 0, c->stream, msum, 1, c->raw_tile, p, out_dev, flag_dev);
+    // one block sums the block partials in a fixed order, forms the tile and (beta) solves it.
+    // Owner-sharded rows: one workgroup per entry sums the partials first, then the sums over
+    // ranks, then the tile
+    const double* src = part;
+    int ns = nblk;
+    if (c->owner_on) {
+      hipLaunchKernelGGL(k_reduce_partials, dim3(NA), dim3(256), 0, c->stream, part, nblk, (int64_t)NA, msum);
+      LFE_HIP(hipGetLastError());
+      LFE_TRY(allreduce_sum_f64(c, msum, (size_t)NA));
+      src = msum;
+      ns = 1;
+    }
+    hipLaunchKernelGGL(kfinal, dim3(1), dim3(1024), 0, c->stream, src, ns, c->raw_tile, p, out_dev, flag_dev, beta,
+                       beta_copy, ok);
     return LFE_OK;
   };
   switch (PM) {
     case 4:
       hipLaunchKernelGGL(k_tables_gram<4>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      LFE_TRY(final_from(k_tables_final<4>));
+      LFE_TRY(final_from(k_tables_final_chol<4>));
       break;
     case 8:
       hipLaunchKernelGGL(k_tables_gram<8>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      LFE_TRY(final_from(k_tables_final<8>));
+      LFE_TRY(final_from(k_tables_final_chol<8>));
       break;
     default:
       hipLaunchKernelGGL(k_tables_gram<12>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      LFE_TRY(final_from(k_tables_final<12>));
+      LFE_TRY(final_from(k_tables_final_chol<12>));
       break;
   }
   LFE_HIP(hipGetLastError());
@@ -1088,14 +1062,13 @@ void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out) {
 // beta_full from the Gram tile by Cholesky (p <= 12).  Fixed loop bounds with
 // guards unroll completely, so L stays in registers (a runtime-bounded version
 // indexed a scratch array and took ~70 us).
-__global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __restrict__ beta,
-                             double* __restrict__ beta_copy, double* __restrict__ ok) {
-  // one wave: right-looking Cholesky in LDS (a column step is a sqrt, a scaled column and a
-  // trailing update spread over the lanes), then the two triangular solves on lane 0
-  constexpr int M = 12;
-  __shared__ double L[M][M + 1];
-  __shared__ double b[M];
-  __shared__ int bad;
+// the block's threads: right-looking Cholesky in LDS (a column step is a sqrt, a scaled column
+// and a trailing update spread over the threads), then the two triangular solves on thread 0.
+// tile: global or LDS.  Every thread of the block must call it (it holds barriers).
+constexpr int kCholM = 12;
+__device__ void chol_solve_block(const double* tile, int p, double* __restrict__ beta, double* __restrict__ beta_copy,
+                                 double* __restrict__ ok, double (*L)[kCholM + 1], double* b, int& bad) {
+  constexpr int M = kCholM;
   const int t = threadIdx.x;
   const int m = p;  // intercept + k regressors
   auto idx = [](int i) { return i == 0 ? 0 : i + 1; };
@@ -1139,6 +1112,67 @@ __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __r
   }
   for (int i = 0; i < m; ++i) beta[i] = beta_copy[i] = b[i];
   *ok = 1.0;
+}
+
+__global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __restrict__ beta,
+                             double* __restrict__ beta_copy, double* __restrict__ ok) {
+  __shared__ double L[kCholM][kCholM + 1];
+  __shared__ double b[kCholM];
+  __shared__ int bad;
+  chol_solve_block(tile, p, beta, beta_copy, ok, L, b, bad);
+}
+
+// The design tile from the raw tile + the table partials (16 waves sum the block partials of one
+// entry each, lanes over blocks in a fixed order); *flag = 1 when the cancellation guard holds;
+// with beta, the Cholesky solve of the tile too, in the same launch
+template <int PM>
+__global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __restrict__ partial, int nblk,
+                                                            const double* __restrict__ raw, int p,
+                                                            double* __restrict__ tile, double* __restrict__ flag,
+                                                            double* __restrict__ beta, double* __restrict__ beta_copy,
+                                                            double* __restrict__ ok) {
+  constexpr int NG = PM * (PM + 1) / 2;
+  constexpr int NA = NG + PM;
+  __shared__ double m[NA];
+  __shared__ double tl[256];
+  __shared__ int bad;
+  __shared__ double L[kCholM][kCholM + 1];
+  __shared__ double b[kCholM];
+  __shared__ int cbad;
+  if (threadIdx.x == 0) bad = 0;
+  {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const auto addop = [](double x, double y) { return x + y; };
+    for (int e = wave; e < NA; e += 16) {
+      double s = 0.0;
+      for (int q = lane; q < nblk; q += 64) s += partial[(int64_t)q * NA + e];
+      s = wave_reduce63(s, 0.0, addop);
+      if (lane == 63) m[e] = s;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const int t = threadIdx.x;
+    const int i = t / 16 - 1, j = t % 16 - 1;  // design indices -> data columns
+    double v = 0.0;
+    if (i < p && j < p) {
+      if (i < 0 && j < 0) {
+        v = raw[15 * 16 + 15];
+      } else if (i < 0 || j < 0) {
+        const int d = i < 0 ? j : i;
+        v = raw[15 * 16 + d] - m[NG + d];
+      } else {
+        const int lo = i < j ? i : j, hi = i < j ? j : i;
+        v = raw[i * 16 + j] + m[lo * PM - lo * (lo - 1) / 2 + (hi - lo)];
+        if (i == j && !(v > 0.0 && raw[i * 16 + i] <= kTabKappa * v)) atomicAdd(&bad, 1);
+      }
+    }
+    tile[t] = v;
+    tl[t] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = bad ? 0.0 : 1.0;
+  if (beta) chol_solve_block(tl, p, beta, beta_copy, ok, L, b, cbad);
 }
 
 int launch_gram(lfe_ctx* c, double* host_gram) {
@@ -1419,10 +1453,7 @@ int gram_spec_enqueue(lfe_ctx* c, int* queued) {
   GramArgs a = base_args(c);
   if (!(resid_rows_ok(c, a) && c->p <= 11 && tables_gram_ok(c))) return LFE_OK;
   LFE_TRY(ensure_f64(c, c->dspec, c->dspec_elems, 544));
-  LFE_TRY(tables_gram_enqueue(c, c->dspec, c->dspec + 532));
-  hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dspec, c->p, c->dspec + 520,
-                     c->dspec + 520, c->dspec + 516);
-  LFE_HIP(hipGetLastError());
+  LFE_TRY(tables_gram_enqueue(c, c->dspec, c->dspec + 532, c->dspec + 520, c->dspec + 520, c->dspec + 516));
   *queued = 1;
   return LFE_OK;
 }
@@ -1441,10 +1472,13 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
     // beta there and adds its tile beside them, so one read-back returns everything
     double* buf = pass == 0 && spec ? c->dspec : c->dred;
     if (buf == c->dred) {
-      if (pass == 0) LFE_TRY(tables_gram_enqueue(c, c->dred, c->dred + 532));
-      else LFE_TRY(design_rows_enqueue(c, a, c->dred));
-      hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dred, p, c->dbeta, c->dred + 520,
-                         c->dred + 516);
+      if (pass == 0) {
+        LFE_TRY(tables_gram_enqueue(c, c->dred, c->dred + 532, c->dbeta, c->dred + 520, c->dred + 516));
+      } else {
+        LFE_TRY(design_rows_enqueue(c, a, c->dred));
+        hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, c->dred, p, c->dbeta, c->dred + 520,
+                           c->dred + 516);
+      }
     }
     LFE_HIP(hipGetLastError());
     GramArgs ar = a;
