@@ -597,11 +597,13 @@ static int build_layouts(lfe_ctx* c, int Q) {
     LFE_TRY((local_sort<false, int32_t>(c, Q, B, c->seg_aux, c->seg_off, c->seg_off_cap, c->seg_q)));
     LFE_TRY((local_sort<true, uint16_t>(c, Q, G_Q, c->seg_aux + n1, c->run_off, c->run_off_cap, c->run_h)));
   }
-  // work units of ~2048 kept rows (whole segments) for K1; 512 when 2048-row units would leave
-  // K1's waves idle (n < 2048 per wave).  Same-box A/B, ms per solve for K1: 1M rows (config 1)
-  // 0.339 -> 0.112; 6.25M 0.099 -> 0.097; at 50M 2048 stays best (0.478 vs 0.523 for 512).
+  // K1 work units: one per wave, rows / waves each (whole segments, multiples of 16 rows).  A
+  // unit start costs a chain of dependent loads (unit bounds, segment ends, codes); same-box A/B,
+  // ms per solve for K1: 50M rows 0.505 -> 0.474 (2048-row units before), 6.25M (8-rank owner
+  // shard) 0.107 -> 0.090 (512), 1M (config 1) 0.121 -> 0.080 (512).  LFE_K1_UNIT: a fixed size.
   const int64_t waves = (int64_t)c->n_cu * 16;  // K1: one 1024-thread workgroup per CU
-  const int64_t U = c->n_kept_local >= 2048 * waves ? 2048 : 512;
+  int64_t U = std::max<int64_t>(256, ((c->n_kept_local + waves - 1) / waves + 15) / 16 * 16);
+  if (const char* e = getenv("LFE_K1_UNIT")) U = std::max<int64_t>(16, atoll(e) / 16 * 16);
   const int32_t H = L.nb * B;
   c->n_units = (int)std::max<int64_t>(1, (c->n_kept_local + U - 1) / U);
   LFE_TRY(ensure_i32(c, c->seg_units, c->seg_units_cap, (size_t)c->n_units + 1));
@@ -855,8 +857,11 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
         four(v, gb, std::integral_constant<int, d + 4>{});
       });
     };
-    int4 va = load(g0), vb;
-    for (int gb = g0; gb < g1 && !done;) {
+    // batches on absolute 16-group boundaries (the groups before the unit's first add zero rows),
+    // so a segment's summation tree depends on its rows only, not on where units begin
+    const int ga = g0 & ~(kBatch - 1);
+    int4 va = load(ga), vb;
+    for (int gb = ga; gb < g1 && !done;) {
       vb = load(gb + kBatch);
       batch(va, gb);
       gb += kBatch;
