@@ -446,10 +446,11 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
   const int p = a.la.p, P = a.la.P;
   const int Q = a.qf[0];
   const double* aQg = a.la.alpha[Q];
-  for (int j = tid; j < a.G_Q * PM; j += kResThreads) {
-    const int g = j / PM, cc = j % PM;
-    aqL[j] = cc < p ? aQg[(int64_t)g * p + cc] : 0.0;
-  }
+  // the pad columns [p, PM) of both tables once, then the rows (the slice rows are restaged per
+  // bucket below; their pads stay 0)
+  for (int j = tid; j < (a.B + a.G_Q) * PM; j += kResThreads)
+    if (j % PM >= p) lds[j] = 0.0;
+  stage_lds<kResThreads>(aqL, aQg, a.G_Q * p, tid, p, PM);
   double beta[PM];
 #pragma unroll
   for (int cc = 0; cc < PM; ++cc) beta[cc] = cc < p ? a.beta[cc] : 0.0;
@@ -469,9 +470,10 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
     const int lo = it.x << a.la.s;
     if (it.x != staged) {
       __syncthreads();
-      for (int j = tid; j < a.B * PM; j += kResThreads) {
-        const int g = lo + j / PM, cc = j % PM;
-        slice[j] = (g < a.G_P && cc < p) ? a.la.alpha[P][(int64_t)g * p + cc] : 0.0;
+      {  // rows past G_P: data columns cleared (their codes never occur)
+        const int nr = max(0, min(a.B, a.G_P - lo));
+        stage_lds<kResThreads>(slice, a.la.alpha[P] + (int64_t)lo * p, nr * p, tid, p, PM);
+        for (int j = nr * PM + tid; j < a.B * PM; j += kResThreads) slice[j] = 0.0;
       }
       __syncthreads();
       staged = it.x;

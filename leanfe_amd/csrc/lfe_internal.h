@@ -519,6 +519,43 @@ __device__ __forceinline__ uint64_t canon_bits(double v) {
 __device__ __forceinline__ double lds_row(const double* t, uint32_t row, uint32_t p8, uint32_t col8) {
   return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(t) + (__umul24(row, p8) + col8));
 }
+// Stage n contiguous doubles (global, 16-byte aligned) into LDS (16-byte aligned) as dst[0, n),
+// or, with pitch > 0, row g of `width` doubles to dst + g * pitch (rows of a table into padded LDS
+// rows).  Every thread issues up to 8 16-byte loads before its stores, so a staging loop no longer
+// waits out one global latency per element per thread (K1 / K2 / residual-pass prologues).
+template <int NTH>
+__device__ __forceinline__ void stage_lds(double* __restrict__ dst, const double* __restrict__ src, int n, int tid,
+                                          int width = 0, int pitch = 0) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int n2 = n >> 1;
+  const d2* s2 = reinterpret_cast<const d2*>(src);
+  auto put = [&](int j, double v) {
+    if (pitch > 0) {
+      const int g = j / width;
+      dst[g * pitch + (j - g * width)] = v;
+    } else {
+      dst[j] = v;
+    }
+  };
+  for (int base = 0; base < n2; base += 8 * NTH) {
+    d2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * NTH + tid;
+      v[u] = i < n2 ? s2[i] : d2{0.0, 0.0};
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * NTH + tid;
+      if (i < n2) {
+        put(2 * i, v[u].x);
+        put(2 * i + 1, v[u].y);
+      }
+    }
+  }
+  if ((n & 1) && tid == 0) put(n - 1, src[n - 1]);
+}
+
 __device__ __forceinline__ double* lds_row_ptr(double* t, uint32_t row, uint32_t p8, uint32_t col8) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(t) + (__umul24(row, p8) + col8));
 }

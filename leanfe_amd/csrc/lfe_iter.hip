@@ -689,7 +689,7 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.p, G_Q = a.G_Q;
-  for (int j = tid; j < G_Q * p; j += kTpThreads) aq[j] = a.alphaQ[j];
+  stage_lds<kTpThreads>(aq, a.alphaQ, G_Q * p, tid);
   for (int j = tid; j < p; j += kTpThreads) aq[G_Q * p + j] = 0.0;
   for (int64_t j = (int64_t)blockIdx.x * kTpThreads + tid; j < a.zero_n; j += (int64_t)gridDim.x * kTpThreads)
     a.zeroT[j] = 0.0;
@@ -906,11 +906,12 @@ __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
     const int b = a.blist[bi];
     const int lo = b << a.s;
     __syncthreads();
-    for (int j = tid; j < B * p; j += kTqThreads) {
-      const int g = lo + j / p;
-      sl[j] = g < a.G_P ? a.alphaP[(int64_t)g * p + (j % p)] : 0.0;
+    {  // the bucket's rows of alpha_P are contiguous (16-byte aligned: lo p 8 = b 2^s p 8); rows
+       // past G_P and the zero row B are cleared
+      const int nv = max(0, min(B, a.G_P - lo)) * p;
+      stage_lds<kTqThreads>(sl, a.alphaP + (int64_t)lo * p, nv, tid);
+      for (int j = nv + tid; j < (B + 1) * p; j += kTqThreads) sl[j] = 0.0;
     }
-    for (int j = tid; j < p; j += kTqThreads) sl[B * p + j] = 0.0;
     __syncthreads();
     // wave: runs q in [q, q1) of bucket b
     const int slot = part * NW + wave;
