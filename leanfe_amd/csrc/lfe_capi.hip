@@ -135,12 +135,18 @@ struct ZeroArgs {
   int n;
 };
 
+// every range over the whole grid in turn, its 16-byte-aligned body in 16-byte stores
 __global__ void k_zero_ranges(ZeroArgs a) {
-  const int64_t total = a.end[a.n - 1];
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    int j = 0;
-    while (e >= a.end[j]) ++j;
-    a.p[j][e - (j ? a.end[j - 1] : 0)] = 0u;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+  for (int j = 0; j < a.n; ++j) {
+    uint32_t* p = a.p[j];
+    const int64_t len = a.end[j] - (j ? a.end[j - 1] : 0);
+    const int64_t head = min(len, (int64_t)(((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4));
+    const int64_t nb = (len - head) / 4;
+    uint4* q = reinterpret_cast<uint4*>(p + head);
+    for (int64_t e = t; e < head; e += nt) p[e] = 0u;
+    for (int64_t e = t; e < nb; e += nt) q[e] = uint4{0u, 0u, 0u, 0u};
+    for (int64_t e = head + 4 * nb + t; e < len; e += nt) p[e] = 0u;
   }
 }
 
@@ -155,7 +161,7 @@ int zero_ranges(lfe_ctx* c, const std::vector<std::pair<void*, size_t>>& ranges)
     a.end[a.n++] = off;
   }
   if (a.n == 0) return LFE_OK;
-  hipLaunchKernelGGL(k_zero_ranges, dim3(grid_for(off, 256, 1024)), dim3(256), 0, c->stream, a);
+  hipLaunchKernelGGL(k_zero_ranges, dim3(grid_for((off + 3) / 4, 256, 1024)), dim3(256), 0, c->stream, a);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
 }
