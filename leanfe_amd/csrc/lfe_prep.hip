@@ -53,6 +53,39 @@ __global__ __launch_bounds__(256) void k_hist_lds(const int32_t* __restrict__ co
     if (h[g]) atomicAdd(&cnt[g], h[g]);
 }
 
+// Key ranges of kHistRange counters (128 KB of LDS) for G > kLdsHistMax: block (x, y) counts the
+// codes in [y R, (y + 1) R) of its rows in LDS and flushes its non-zero bins with coalesced adds.
+// Per-row global atomics into a 1e5-level table (config 4's second FE) ran at ~25 G adds/s:
+// 1.96 ms for 50M rows; the ranges read the codes once per range instead.
+constexpr int kHistRange = 32768;
+constexpr int kHistMaxRanges = 8;
+__global__ __launch_bounds__(1024) void k_hist_lds_range(const int32_t* __restrict__ code, int64_t n, int32_t G,
+                                                         int32_t* __restrict__ cnt) {
+  extern __shared__ int32_t h[];
+  const int32_t k0 = (int32_t)blockIdx.y * kHistRange, nk = min(kHistRange, G - k0);
+  for (int g = threadIdx.x; g < nk; g += blockDim.x) h[g] = 0;
+  __syncthreads();
+  const int64_t n4 = n >> 2;
+  const int4* c4 = reinterpret_cast<const int4*>(code);
+  auto one = [&](int32_t v) {
+    const uint32_t d = (uint32_t)(v - k0);
+    if (d < (uint32_t)nk) atomicAdd(&h[d], 1);
+  };
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int4 v = c4[i];
+    one(v.x);
+    one(v.y);
+    one(v.z);
+    one(v.w);
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    one(code[i]);
+  __syncthreads();
+  for (int g = threadIdx.x; g < nk; g += blockDim.x)
+    if (h[g]) atomicAdd(&cnt[k0 + g], h[g]);
+}
+
 __global__ void k_hist_global(const int32_t* __restrict__ code, int64_t n, int32_t* __restrict__ cnt) {
   GRID_STRIDE(i, n) atomicAdd(&cnt[code[i]], 1);
 }
@@ -127,6 +160,31 @@ struct ScanPair {
   }
 };
 
+// a thread's kScanPer consecutive elements: two 16-byte accesses when all lie inside the array
+// (base is a multiple of 8 elements; element-wise 4-byte accesses put the lanes of one
+// instruction 32 bytes apart, eight instructions per 2 KB: 0.5 TB/s on config 4's 49M-entry scans)
+static_assert(kScanPer == 8, "two int4 per thread");
+__device__ __forceinline__ void scan_load8(const int32_t* a, int64_t base, int64_t m, int32_t (&v)[8]) {
+  if (base + 8 <= m) {
+    const int4 x = *reinterpret_cast<const int4*>(a + base), y = *reinterpret_cast<const int4*>(a + base + 4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = base + k < m ? a[base + k] : 0;
+  }
+}
+__device__ __forceinline__ void scan_store8(int32_t* a, int64_t base, int64_t m, const int32_t (&v)[8]) {
+  if (base + 8 <= m) {
+    *reinterpret_cast<int4*>(a + base) = int4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<int4*>(a + base + 4) = int4{v[4], v[5], v[6], v[7]};
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (base + k < m) a[base + k] = v[k];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_scan_blocks(ScanPair sp, int32_t* __restrict__ sums) {
   __shared__ int32_t tmp[8];
   __shared__ int32_t total;
@@ -134,18 +192,18 @@ __global__ __launch_bounds__(256) void k_scan_blocks(ScanPair sp, int32_t* __res
   int32_t* __restrict__ a = sp.arr(blk, m);
   const int64_t base = blk * kScanBlock + (int64_t)threadIdx.x * kScanPer;
   int32_t v[kScanPer];
+  scan_load8(a, base, m, v);
   int32_t s = 0;
 #pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    v[k] = (base + k < m) ? a[base + k] : 0;
-    s += v[k];
-  }
+  for (int k = 0; k < kScanPer; ++k) s += v[k];
   int32_t off = block_excl_scan(s, tmp, &total);
+  int32_t o[kScanPer];
 #pragma unroll
   for (int k = 0; k < kScanPer; ++k) {
-    if (base + k < m) a[base + k] = off;
+    o[k] = off;
     off += v[k];
   }
+  scan_store8(a, base, m, o);
   if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
@@ -174,9 +232,11 @@ __global__ __launch_bounds__(256) void k_scan_add(ScanPair sp, const int32_t* __
   int32_t* __restrict__ a = sp.arr(blk, m);
   const int64_t base = blk * kScanBlock + (int64_t)threadIdx.x * kScanPer;
   const int32_t add = sums[blockIdx.x];
+  int32_t v[kScanPer];
+  scan_load8(a, base, m, v);
 #pragma unroll
-  for (int k = 0; k < kScanPer; ++k)
-    if (base + k < m) a[base + k] += add;
+  for (int k = 0; k < kScanPer; ++k) v[k] += add;
+  scan_store8(a, base, m, v);
 }
 
 __global__ void k_gather_bstart(const int32_t* __restrict__ scanned, int nb, int nw, int32_t* __restrict__ out) {
@@ -217,6 +277,10 @@ static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, in
   const int64_t nblocks = nb1 + nb2;
   if (nblocks == 0) return LFE_OK;
   LFE_TRY(ensure_pcounts(c, 0, (size_t)nblocks + 1));
+  if (((uintptr_t)a1 | (uintptr_t)a2) & 15) {  // scan_load8 / scan_store8: 16-byte accesses
+    set_error("exclusive_scan: arrays must be 16-byte aligned");
+    return LFE_EINVAL;
+  }
   const ScanPair sp{a1, m1, nb1, a2, m2};
   ProfScope _ps(c, K_SCAN);
   hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums);
@@ -901,10 +965,18 @@ int prepare_layout(lfe_ctx* c) {
     auto& fe = c->fe[f];
     if (n == 0 || (f == L.P && L.permuted) || item_counts) continue;
     ProfScope _ps(c, K_COUNT);
-    if (fe.G <= kLdsHistMax)
+    const int nr = (fe.G + kHistRange - 1) / kHistRange;
+    if (fe.G <= kLdsHistMax) {
       hipLaunchKernelGGL(k_hist_lds, dim3(grid_for((n + 3) / 4, 256, 2048)), dim3(256), sizeof(int32_t) * fe.G, c->stream,
                          fe.code, n, fe.G, fe.cnt_pre);
-    else
+    } else if (nr <= kHistMaxRanges) {
+      // about two blocks per CU over all ranges, and at least ~64K rows per block
+      const int bx = (int)std::max<int64_t>(1, std::min<int64_t>((2 * (int64_t)c->n_cu + nr - 1) / nr, n / 65536 + 1));
+      const size_t lds = sizeof(int32_t) * kHistRange;
+      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist_lds_range),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_hist_lds_range, dim3(bx, nr), dim3(1024), lds, c->stream, fe.code, n, fe.G, fe.cnt_pre);
+    } else
       hipLaunchKernelGGL(k_hist_global, dim3(grid_for(n)), dim3(kBlock), 0, c->stream, fe.code, n, fe.cnt_pre);
     LFE_HIP(hipGetLastError());
   }
