@@ -1214,11 +1214,14 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   // about four workgroups per CU in all (two resident at a time), so no CU is left with a lone
   // tail: 196 buckets -> 5 per bucket (tq 0.61 -> 0.49 ms per step at 50M rows, measured)
   tq.split = std::max(kTqSplitDefault / 2, (int)std::lround(4.0 * c->n_cu / nbe));
-  {  // every workgroup stages its bucket's 45 KB alpha_P slice: >= 16K rows per workgroup (6.25M
-     // rows over 25 buckets: 0.126 -> 0.113 ms per 3 sweeps; 48K rows per workgroup 0.142 ms);
-     // a narrower slice (p < 11) pays for proportionally fewer rows
+  {  // every workgroup stages its bucket's 45 KB alpha_P slice: >= 8K rows per workgroup at p = 11
+     // (LFE_K2_MINROWS sweep, ms per solve for K2: 6.25M rows over 25 buckets 0.113 at 16K, 0.105
+     // at 8K, 0.117 at 4K; 48K 0.142; config 2 (p = 6) 0.362 / 0.314 / 0.314 at 16K / 8K / 4K, config
+     // 1 (p = 4) 0.108 / 0.075 at 8K / 4K; 50M rows unchanged); a narrower slice (p < 11) pays for
+     // proportionally fewer rows
     const int64_t per_bucket = c->n_kept_local / nbe;
-    const int64_t min_rows = std::max<int64_t>(2048, (int64_t)16384 * p / 11);
+    int64_t min_rows = std::max<int64_t>(2048, (int64_t)8192 * p / 11);
+    if (const char* e = getenv("LFE_K2_MINROWS")) min_rows = std::max<int64_t>(256, atoll(e));  // A/B only
     tq.split = (int)std::max<int64_t>(1, std::min<int64_t>(tq.split, per_bucket / min_rows));
     // ... but no fewer workgroups than CUs while each keeps >= 8K rows (6.25M rows over 196
     // buckets: 196 -> 392 workgroups)
