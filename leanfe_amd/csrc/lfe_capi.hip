@@ -420,6 +420,8 @@ static void free_data(lfe_ctx* c) {
   c->rec_sy_cap = c->rec_syy_cap = c->rec_lay_cap = 0;
   dfree(c->raw_part);
   dfree(c->qpart);
+  dfree(c->colsum_part);
+  c->colsum_part_cap = 0;
   dfree(c->raw_slots);
   c->raw_slots_cap = 0;
   dfree(c->amax);

@@ -205,6 +205,55 @@ __global__ __launch_bounds__(TH) void k_sums4(Sums4Args a) {
   }
 }
 
+// Group sums of one non-primary FE whose [G][p] table does not fit LDS but one column of it does
+// (G <= kColSumsMax: config 4's third FE, 1e4 levels), one column per blockIdx.y: the block adds
+// the fine limbs of its rows' column-c values into an LDS column [G] and writes it whole to
+// part[c][block][G]; k_col_sums_fold adds the blocks per entry (integers: any order) into S_f.
+// Per-row global int64 adds into the [G][p] table (k_sums4's path for tables that do not fit)
+// ran at the chip's atomic rate, ~4.5 ms of config 4's 10 ms group sums for this FE; here every
+// block rereads the codes once per column (12 B per row and column in all).
+constexpr int kColSumsMax = 16384;
+__global__ __launch_bounds__(1024) void k_col_sums(const int32_t* __restrict__ code, const int32_t* __restrict__ codeP,
+                                                   const double* __restrict__ X, int64_t ld,
+                                                   const double* __restrict__ w, int64_t n, int G, int p,
+                                                   const double* __restrict__ fixq, double* __restrict__ hi,
+                                                   unsigned long long* __restrict__ part) {
+  extern __shared__ unsigned long long tab[];  // [G]
+  const int c = blockIdx.y;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) tab[g] = 0ull;
+  __syncthreads();
+  const FixCol fc = fix_col(fixq, c);
+  const double* __restrict__ xc = X + (int64_t)c * ld;
+  const int64_t per = ((n + gridDim.x - 1) / gridDim.x + 3) & ~(int64_t)3;
+  const int64_t r0 = (int64_t)blockIdx.x * per, r1 = min(n, r0 + per);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+    if (codeP && codeP[i] < 0) continue;  // dropped row (singleton filter)
+    const int32_t g = code[i];
+    double v = xc[i];
+    if (w) v *= w[i];  // sum of (c * w), polars_impl.py:496
+    double h;
+    atomicAdd(&tab[g], fix_split(v, fc, h));
+    if (h != 0.0) atomicAdd(&hi[(int64_t)g * p + c], h);
+  }
+  __syncthreads();
+  unsigned long long* dst = part + ((int64_t)c * gridDim.x + blockIdx.x) * G;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) dst[g] = tab[g];
+}
+
+// S_f[g][c] fine limbs (u64 bits, as k_sums4's adds leave them) = sum over the blocks of column c
+__global__ void k_col_sums_fold(const unsigned long long* __restrict__ part, int nblk, int G, int p,
+                                double* __restrict__ S) {
+  const int64_t m = (int64_t)G * p;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % p);
+    const int64_t g = e / p;
+    const unsigned long long* src = part + (int64_t)c * nblk * G + g;
+    unsigned long long t = 0ull;
+    for (int b = 0; b < nblk; ++b) t += src[(int64_t)b * G];
+    S[e] = __longlong_as_double((long long)t);
+  }
+}
+
 // The two-FE Gram-from-tables case of k_sums4 (RAW, unweighted, p <= 15, primary slice and
 // secondary table both in LDS) with the per-row work cut to what the data needs: a row's
 // only test is its primary code's sign (item edges are masked once per 16-row group), LDS
@@ -639,9 +688,16 @@ int sums4(lfe_ctx* c) {
     }
     if (!c->sums_zeroed) LFE_HIP(hipMemsetAsync(c->fe[f].S, 0, sizeof(double) * (size_t)c->fe[f].G * p, c->stream));
   }
+  // non-primary FEs whose table does not fit LDS but one column of it does: column-split LDS sums
+  // (k_col_sums) instead of k_sums4's per-row global adds
+  bool colsplit[kMaxFE] = {};
   a.nq = 0;
-  for (int f = 0; f < c->F; ++f)
-    if (f != P) a.qf[a.nq++] = f;
+  for (int f = 0; f < c->F; ++f) {
+    if (f == P) continue;
+    // (three or more FEs: a two-FE fit keeps its secondary FE in k_sums4 for the raw Gram)
+    colsplit[f] = c->F >= 3 && a.tab_off[f] < 0 && c->fe[f].G <= kColSumsMax && c->n > 0;
+    if (!colsplit[f]) a.qf[a.nq++] = f;
+  }
   c->sums_zeroed = false;
   const size_t lds = off * 8;
   const int NT = (p + 15) / 16;
@@ -730,6 +786,22 @@ int sums4(lfe_ctx* c) {
     }
   }
   LFE_HIP(hipGetLastError());
+  for (int f = 0; f < c->F; ++f) {
+    if (!colsplit[f]) continue;
+    ProfScope _ps(c, K_GROUP_SUMS);
+    const int G = c->fe[f].G;
+    const int nb = std::max(1, (2 * c->n_cu + p - 1) / p);  // ~2 blocks per CU over the p columns
+    LFE_TRY(ensure_f64(c, c->colsum_part, c->colsum_part_cap, (size_t)p * nb * G));
+    const size_t lds = sizeof(unsigned long long) * G;
+    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col_sums), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)std::max<size_t>(lds, 1)));
+    auto* part = reinterpret_cast<unsigned long long*>(c->colsum_part);
+    hipLaunchKernelGGL(k_col_sums, dim3(nb, p), dim3(1024), lds, c->stream, c->L.code[f],
+                       P >= 0 ? c->L.code[P] : nullptr, c->L.X, c->ld, c->L.w, c->n, G, p, c->fixq, c->fe[f].hi, part);
+    hipLaunchKernelGGL(k_col_sums_fold, dim3(grid_for((int64_t)G * p)), dim3(kBlock), 0, c->stream, part, nb, G, p,
+                       c->fe[f].S);
+    LFE_HIP(hipGetLastError());
+  }
   if (two) {  // two implies raw: one epilogue launch
     ProfScope _ps(c, K_FIX_SUMS);
     LFE_TRY(ensure_f64(c, c->raw_shift, c->raw_shift_cap, 32));

@@ -194,6 +194,8 @@ struct lfe_ctx {
   std::vector<lfe::FeState> fe;
   // layout (bucket order) storage
   lfe::Layout L;
+  double* colsum_part = nullptr;  // [p][blocks][G] fine-limb columns of k_col_sums (lfe_fast.hip)
+  size_t colsum_part_cap = 0;
   double* Xp = nullptr;          // [p][ld] permuted columns
   double* wp = nullptr;          // [ld] permuted weights
   int32_t* codes_p = nullptr;    // [F][ld] permuted / working codes
