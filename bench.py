@@ -227,13 +227,17 @@ def load_shard(eng, a, rank: int, world: int, shard: str) -> dict:
 # measurement helpers
 # ---------------------------------------------------------------------------
 
-def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False) -> dict:
+def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cells: int = 0) -> dict:
     """HBM bytes each kernel must move per launch, n rows of the shard,
     p = 1 + k f64 data columns, F int32 code columns.  Kernels absent here move only group
     tables or scalars (latency-bound) and count as 0 in the step total.  The general sweeps'
     cross / check passes (F >= 3) read F - 1 code arrays from HBM; the effect
-    rows they gather come from L2 / MALL-resident tables and are not HBM bytes."""
+    rows they gather come from L2 / MALL-resident tables and are not HBM bytes.  With the dense
+    two-FE cross terms (``dense_cells`` > 0, lfe_dense.hip) the table build reads both codes and
+    writes two uint16 count tables, and each cross-term pass reads one of them."""
     k = p - 1
+    dense = {"layout_scatter": 8 * n + 2 * 2 * dense_cells, "tp": 2 * dense_cells, "tq": 2 * dense_cells,
+             "layout_base": 0} if dense_cells else {}
     return {
         "part_hist": 4 * n,                          # primary codes
         "part_scatter": n * (2 * 8 * p + 2 * 4 * F),  # read + write X and codes
@@ -248,6 +252,7 @@ def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False) -> dict:
         "cross": 4 * n * (F - 1),                    # the other FEs' codes in segment order
         "check": 4 * n * (F - 1),
         **({"count": 4 * n} if F != 2 else {}),      # one FE's codes (two FEs: the layouts' histograms)
+        **dense,
     }
 
 
@@ -383,7 +388,8 @@ def main(argv=None):
     value = total_rows * a.steps / elapsed / 1e6
     ms_step = elapsed / a.steps * 1e3
     p, F = a.k + 1, len(a.levels)
-    ab = algorithmic_bytes(geo["local"], p, F, clustered=bool(a.cl))
+    cells = eng.dense_cells()
+    ab = algorithmic_bytes(geo["local"], p, F, clustered=bool(a.cl), dense_cells=cells)
     # dominant kernel = most device time in the timed region (rank 0's shard)
     dom = max(kstats.items(), key=lambda kv: kv[1][0]) if kstats else ("none", (0.0, 1))
     dom_name, (dom_ms, dom_launches) = dom
@@ -452,6 +458,7 @@ def main(argv=None):
             "config": {"workload": workload_label(a, d.world), "rows_total": total_rows,
                        "rows_rank0": geo["local"], "k": a.k, "levels": a.levels, "vcov": a.vcov,
                        "cluster_fes": a.cl, "iterations": res["iterations"],
+                       "cross_terms": f"dense count tables ({cells} cells, MFMA)" if cells else "row layouts",
                        "parallelism": f"dp{d.world} ({shard}-sharded rows, RCCL inside the engine)"
                        if not a.emulate_rank else f"rank {a.emulate_rank} owner shard solved alone (diagnostic)"},
             "roofline": roofline,

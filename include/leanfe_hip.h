@@ -276,6 +276,12 @@ int lfe_stream_synth_rows(lfe_ctx* ctx, int64_t row0, int64_t rows, int k, const
  * path).  Replaces nothing in the reference (Polars' group sums are serial). */
 int lfe_exact_sums(lfe_ctx* ctx, int* on);
 
+/* Cells of the count tables the last two-FE lfe_demean multiplied on the matrix cores (the dense
+ * cross terms, buckets x primary groups per bucket x secondary levels rounded to 16), or 0 when it
+ * took the row layouts (lfe_dense.hip).  A diagnostic for the byte model of bench.py; replaces
+ * nothing in the reference. */
+int lfe_dense_cells(lfe_ctx* ctx, int64_t* cells);
+
 /* Wait for all work queued on the context's stream. */
 int lfe_sync(lfe_ctx* ctx);
 

@@ -61,6 +61,7 @@ SIGNATURES = {
     "lfe_copy_demeaned": (C.c_int, [_vp, C.POINTER(_vp), _i64p]),
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
+    "lfe_dense_cells": (C.c_int, [_vp, _i64p]),
     "lfe_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.POINTER(_vp), _i32p, _dp, C.c_int]),
     "lfe_stream_clusters": (C.c_int, [_vp, C.c_int, _i32p]),
     "lfe_stream_cluster_meats": (C.c_int, [_vp, _dp, _i64p]),
@@ -508,6 +509,13 @@ class Engine:
         on = C.c_int32(0)
         _check(self._lib.lfe_exact_sums(self._h, C.byref(on)))
         return bool(on.value)
+
+    def dense_cells(self) -> int:
+        """Cells of the count tables the last two-FE demean multiplied on the matrix cores (0: the row
+        layouts ran; lfe_dense.hip)."""
+        v = C.c_int64(0)
+        _check(self._lib.lfe_dense_cells(self._h, C.byref(v)))
+        return int(v.value)
 
     def profile(self, enable: bool = True) -> None:
         _check(self._lib.lfe_profile(self._h, 1 if enable else 0))

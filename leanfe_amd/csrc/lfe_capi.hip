@@ -422,6 +422,9 @@ static void free_data(lfe_ctx* c) {
   dfree(c->qpart);
   dfree(c->colsum_part);
   c->colsum_part_cap = 0;
+  dfree(c->dn_na);
+  dfree(c->dn_nb);
+  c->dn_na_cap = c->dn_nb_cap = 0;
   dfree(c->raw_slots);
   c->raw_slots_cap = 0;
   dfree(c->amax);
@@ -1084,6 +1087,7 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
       if (chk[f] != f) return fail(LFE_EINVAL, "fe_order must be a permutation of 0..F-1");
   }
   if (check_from > 0 && max_iter < 1) return fail(LFE_EINVAL, "max_iter must be >= 1");
+  c->dense_cells = 0;  // demean_fast sets it when the dense cross terms run
   int iterations = 0;
   double last = -1.0;
   c->tq_final = false;
@@ -1217,6 +1221,13 @@ int lfe_exact_sums(lfe_ctx* c, int* on) {
   LFE_CTX(c);
   if (!on) return fail(LFE_EINVAL, "null pointer");
   return exact_sums_on(c, on);
+}
+
+int lfe_dense_cells(lfe_ctx* c, int64_t* cells) {
+  LFE_CTX(c);
+  if (!cells) return fail(LFE_EINVAL, "null pointer");
+  *cells = c->dense_cells;
+  return LFE_OK;
 }
 
 int lfe_sync(lfe_ctx* c) {

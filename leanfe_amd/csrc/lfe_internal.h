@@ -55,6 +55,7 @@ struct FeState {
   int32_t* cnt_pre = nullptr;  // [G] pre-filter counts
   int32_t* drops = nullptr;    // [G] dropped-row counts (singleton filter)
   int32_t* cnt = nullptr;      // [G] kept counts
+  int32_t cmax = 0;            // largest kept count (host copy, after the singleton drop)
   double* W = nullptr;         // [G] sum of weights over kept rows (weighted fits only)
   double* S = nullptr;         // [G*p] sum_{i in g} w_i x_i  (constant per solve)
   double* Sy = nullptr;        // [G] unweighted sum of y (weighted fits; the check is unweighted)
@@ -194,6 +195,11 @@ struct lfe_ctx {
   std::vector<lfe::FeState> fe;
   // layout (bucket order) storage
   lfe::Layout L;
+  int64_t dense_cells = 0;        // cells of the last demean's dense count tables (0: row layouts)
+  uint16_t* dn_na = nullptr;      // dense cross-term count tables (lfe_dense.hip)
+  size_t dn_na_cap = 0;
+  uint16_t* dn_nb = nullptr;
+  size_t dn_nb_cap = 0;
   double* colsum_part = nullptr;  // [p][blocks][G] fine-limb columns of k_col_sums (lfe_fast.hip)
   size_t colsum_part_cap = 0;
   double* Xp = nullptr;          // [p][ld] permuted columns
@@ -383,6 +389,11 @@ bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order);
 bool fast_layout_ok(const lfe_ctx* c);            // the two-FE layouts fit (any FE order)
 int layout_hists(lfe_ctx* c, int Q);              // per-item histograms of both codes -> seg_aux
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out);
+// lfe_dense.hip: the two-FE cross terms as count-table products on the matrix cores
+bool dense_ok(const lfe_ctx* c);
+int dense_build(lfe_ctx* c);
+int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check);
+int dense_tq(lfe_ctx* c, double* runs);
 
 // --- constant sums (lfe_sweep.hip) ---
 int sweep_group_sums(lfe_ctx* c);

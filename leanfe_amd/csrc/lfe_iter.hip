@@ -1171,7 +1171,16 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   auto& fp = c->fe[P];
   auto& fq = c->fe[Q];
   const int NT = (p + 15) / 16;
-  LFE_TRY(build_layouts(c, Q));
+  // dense count tables where the primary x secondary table holds >= ~0.15 rows per cell (both
+  // cross terms on the matrix cores, lfe_dense.hip); else the segment / run layouts
+  const bool dense = dense_ok(c);
+  c->dense_cells = 0;
+  if (dense) {
+    c->hists_kept = false;
+    LFE_TRY(dense_build(c));
+  } else {
+    LFE_TRY(build_layouts(c, Q));
+  }
   LFE_TRY(ensure_f64(c, c->alpha_spare, c->alpha_spare_cap, (size_t)fq.G * p));
   LFE_TRY(ensure_dred(c, 1));
   const size_t lds_tp = sizeof(double) * ((size_t)fq.G + 1) * p;
@@ -1240,7 +1249,10 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     tp.zero_check = it >= check_from ? c->dred : nullptr;
     // T_P partials: segments with no local rows are not written by K1
     if (!tp.fused) LFE_HIP(hipMemsetAsync(fp.T, 0, sizeof(double) * (size_t)fp.G * p, c->stream));
-    {
+    if (dense) {
+      ProfScope _ps(c, K_TP);
+      LFE_TRY(dense_tp(c, fq.alpha, tp.zero_check));
+    } else {
       ProfScope _ps(c, K_TP);
       switch (NT) {
         case 1: launch_tp<1>(c, tp, lds_tp); break;
@@ -1254,7 +1266,10 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       LFE_TRY(allreduce_sum_f64(c, fp.T, (size_t)fp.G * p));
       LFE_TRY(fin_check(c, P, fp.T, nullptr, fp.alpha, false));
     }
-    {  // the check's max was zeroed by K1
+    if (dense) {  // the check's max was zeroed by K1
+      ProfScope _ps(c, K_TQ);
+      LFE_TRY(dense_tq(c, c->tq_runs));
+    } else {
       ProfScope _ps(c, K_TQ);
       switch (NT) {
         case 1: launch_tq<1>(c, tq, lds_tq); break;

@@ -1154,7 +1154,7 @@ int prepare_layout(lfe_ctx* c) {
     hipLaunchKernelGGL(k_kept_unpack, dim3(1), dim3(64), 0, c->stream, c->dred, c->iscratch);
     LFE_HIP(hipGetLastError());
   }
-  int32_t h[2 * kMaxFE + 8];
+  int32_t h[kIscratchInts];  // dims / card per FE, dropped rows, kept sums, largest kept counts
   LFE_TRY(d2h_async(c, c->iscratch, sizeof(h)));
   // the constant group sums S_f do not depend on the FE order: enqueue them now so the
   // GPU keeps working while the host reads the counts and returns (lfe_demean skips them)
@@ -1166,6 +1166,7 @@ int prepare_layout(lfe_ctx* c) {
   for (int f = 0; f < c->F; ++f) {
     c->fe[f].dims = h[2 * f];
     c->fe[f].card = h[2 * f + 1];
+    c->fe[f].cmax = h[kIscratchCmax + f];
   }
   c->hists_kept = item_counts && h[2 * kMaxFE] == 0;
   // kept rows over all ranks (owner-sharded: with the primary FE's level counts, which each

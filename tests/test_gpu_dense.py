@@ -1,0 +1,132 @@
+"""Dense count-table cross terms (leanfe_amd/csrc/lfe_dense.hip).
+
+For two FEs the sweep's cross terms T_P = N alpha_Q and T_Q = N' alpha_P (N[h][q] = kept rows with
+codes (h, q) per bucket of the primary FE) run on the matrix cores when the table holds >= ~0.15
+rows per cell; otherwise the segment / run layouts of lfe_iter.hip gather row by row.  Both are
+restatements of the same projection loop (polars_impl.py:490-526), so:
+- each path matches the CPU oracle (oracle/altproj.py) at 1e-10 with equal `iterations`;
+- the two paths agree with each other to rounding;
+- the dense path repeats bit for bit;
+- a panel whose (h, q) pairs hold more than 255 rows takes the build's 16-bit recount (its 8-bit
+  counters overflow) and still matches the oracle;
+- an owner shard (strong scaling, few buckets) takes it too.
+LFE_DENSE=1 forces the dense path wherever it fits, LFE_DENSE=0 turns it off."""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _fit(data, xs, vcov="HC1"):
+    from leanfe_amd import leanfe_hip
+
+    r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], strategy="alt_proj", vcov=vcov, quiet=True,
+                   device=0)
+    return (np.array([r.coefs[x] for x in xs]), np.array([r.std_errors[x] for x in xs]), r.iterations, r.n_obs,
+            r.df_resid)
+
+
+def _oracle(data, xs, vcov="HC1"):
+    from oracle import altproj
+
+    return altproj.fit(data, "y", xs, ["fe1", "fe2"], vcov=vcov)
+
+
+def _check(res, o):
+    b, s, it, n_obs, df = res
+    assert it == o["iterations"] and n_obs == o["n_obs"] and df == o["df_resid"], (it, o["iterations"])
+    np.testing.assert_allclose(b, o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(s, o["se"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("vcov", ["HC1", "iid"])
+def test_dense_and_row_paths_match_oracle_and_each_other(vcov, monkeypatch):
+    from leanfe_amd import synth
+
+    k = 5
+    xs = [f"x{j + 1}" for j in range(k)]
+    # 0.6 rows per cell: the default picks the dense path
+    data = synth.panel(1_200_000, k, [4_000, 500], seed=2024)
+    o = _oracle(data, xs, vcov)
+    monkeypatch.setenv("LFE_DENSE", "0")
+    rows = _fit(data, xs, vcov)
+    monkeypatch.delenv("LFE_DENSE")
+    dense = _fit(data, xs, vcov)
+    _check(rows, o)
+    _check(dense, o)
+    np.testing.assert_allclose(dense[0], rows[0], rtol=1e-13, atol=0)
+    again = _fit(data, xs, vcov)
+    np.testing.assert_array_equal(dense[0], again[0])
+    np.testing.assert_array_equal(dense[1], again[1])
+
+
+def test_dense_with_singletons_and_ragged_bucket(monkeypatch):
+    """Singleton rows dropped before the table is built; a primary FE whose last bucket is partial
+    (G_P = 3,001) and a secondary FE that is not a multiple of 16 levels (G_Q = 77)."""
+    from leanfe_amd import synth
+
+    k = 3
+    xs = [f"x{j + 1}" for j in range(k)]
+    data = synth.panel(300_000, k, [3_001, 77], seed=5)
+    fe1 = np.array(data["fe1"], copy=True)
+    fe1[:40] = np.arange(40) + 2_961  # levels with one row (and their rows' partners) drop
+    data = dict(data, fe1=fe1)
+    monkeypatch.setenv("LFE_DENSE", "1")
+    _check(_fit(data, xs), _oracle(data, xs))
+
+
+def test_dense_counts_beyond_8_bits(monkeypatch):
+    """(h, q) pairs with hundreds of rows: the 8-bit counters of the build overflow and the chunk is
+    counted again on 16-bit counters."""
+    rng = np.random.default_rng(11)
+    n, k = 400_000, 3
+    fe1 = rng.integers(0, 1_000, n).astype(np.int32)
+    fe2 = rng.integers(0, 40, n).astype(np.int32)
+    heavy = rng.random(n) < 0.25  # a quarter of the rows on two (h, q) pairs: ~50K rows each
+    fe1[heavy] = np.where(rng.random(heavy.sum()) < 0.5, 7, 700).astype(np.int32)
+    fe2[heavy] = 3
+    x = rng.standard_normal((n, k))
+    a1 = rng.standard_normal(1_000)
+    a2 = rng.standard_normal(40)
+    y = x @ np.array([1.0, -0.5, 0.25]) + a1[fe1] + a2[fe2] + rng.standard_normal(n)
+    data = {"y": y, "fe1": fe1, "fe2": fe2, **{f"x{j + 1}": x[:, j].copy() for j in range(k)}}
+    xs = ["x1", "x2", "x3"]
+    o = _oracle(data, xs)
+    monkeypatch.setenv("LFE_DENSE", "1")
+    dense = _fit(data, xs)
+    _check(dense, o)
+    monkeypatch.setenv("LFE_DENSE", "0")
+    _check(_fit(data, xs), o)
+
+
+def test_dense_owner_shard_matches_whole_panel(monkeypatch):
+    """Rank 7 of 8 of the strong-scaled headline schedule solved alone (bench --emulate-rank): its
+    few buckets take the dense path and the owner shard matches the oracle on the same rows."""
+    import bench
+    from leanfe_amd import synth
+    from leanfe_amd._lib import Engine
+    from oracle import altproj
+
+    n, k, L = 2_000_000, 4, [40_000, 300]
+    monkeypatch.setenv("LFE_DENSE", "1")
+    with Engine(0) as eng:
+        eng.synth_load_owned(n, k, L, synth.betas(k), 0, 35_000, 40_000, seed=31)
+        got = bench.solve_step(eng, "iid")
+        again = bench.solve_step(eng, "iid")
+    np.testing.assert_array_equal(got["beta"], again["beta"])
+    data = synth.panel(n, k, L, seed=31)
+    keep = (data["fe1"] >= 35_000) & (data["fe1"] < 40_000)
+    sub = {c: np.asarray(v)[keep] for c, v in data.items()}
+    o = altproj.fit(sub, "y", [f"x{j + 1}" for j in range(k)], ["fe1", "fe2"], vcov="iid")
+    assert got["iterations"] == o["iterations"]
+    np.testing.assert_allclose(got["beta"], o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(got["se"], o["se"], rtol=1e-10, atol=0)
