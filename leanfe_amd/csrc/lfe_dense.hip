@@ -156,24 +156,29 @@ struct DnPassArgs {
   double* runs;
 };
 
-// One output block of 16 rows (K1: primary groups of one bucket; K2: secondary levels) x 16
-// columns per wave (or per KP waves, each over 1 / KP of the k range).  The B operand (the other
-// FE's effects) comes from LDS: K1 the whole alpha_Q, K2 the bucket's alpha_P slice.
+// R output blocks of 16 rows (K1: primary groups of one bucket; K2: secondary levels) x 16 columns
+// per wave (or per KP waves, each over 1 / KP of the k range).  The B operand (the other FE's
+// effects) comes from LDS - K1 the whole alpha_Q, K2 the bucket's alpha_P slice - and one B value
+// feeds the wave's R blocks.  R = 1: two blocks per wave (half the B reads per MFMA) measured
+// slower, K1 + K2 0.71 vs 0.65 ms per solve at 50M rows on one box: the passes are not bound by
+// the B operand's LDS reads.
+constexpr int kDnR = 1;
 template <bool K2>
 __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
+  constexpr int R = kDnR;
   extern __shared__ __attribute__((aligned(16))) double tb[];  // K1: [GQ16][p]; K2: [B][p]
   __shared__ d4 red[kDnWaves][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.p, nqb = a.GQ16 >> 4, nhb = a.B >> 4;
-  const int upw = kDnWaves / a.KP;                 // output blocks per workgroup
+  const int upw = kDnWaves / a.KP * R;             // output blocks per workgroup
   const int nrb = K2 ? nqb : nhb;                  // output blocks per bucket
   const int nkb = K2 ? nhb : nqb;                  // k blocks per output block
   // workgroups never straddle buckets (K2 stages the bucket's slice)
   const int wgpb = (nrb + upw - 1) / upw;
   const int bi = blockIdx.x / wgpb;
-  const int rb = (blockIdx.x - bi * wgpb) * upw + wave / a.KP;
+  const int rb0 = (blockIdx.x - bi * wgpb) * upw + (wave / a.KP) * R;  // the wave's first block
   const int part = wave % a.KP;
   const int b = a.blist[bi];
   const int lo = b << a.s;
@@ -186,29 +191,30 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
     if (a.zero_check && blockIdx.x == 0 && tid == 0) *a.zero_check = 0.0;
   }
   __syncthreads();
-  const bool live = rb < nrb;
   const int cc = c < p ? c : 0;
   const double cm = c < p ? 1.0 : 0.0;
-  d4 acc[4];
+  d4 acc[R][2];  // per block two chains (steps t even / odd)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
-  if (live) {
+  for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = d4{0.0, 0.0, 0.0, 0.0};
+  if (rb0 < nrb) {
     const int k0 = part * nkb / a.KP, k1 = (part + 1) * nkb / a.KP;
-    const uint16_t* nm = a.Nm + (((int64_t)bi * nrb + rb) * nkb) * 256 + c * 16 + 4 * kq;
-    // lane (kq, c): counts of row 16 rb + c at k = 16 kb + 4 kq + t; the matching B row is k
+    // lane (kq, c): counts of row 16 rb + c at k = 16 kb + 4 kq + t; the matching B row is k.  A
+    // block past the bucket's last (odd nrb) reads block rb0's counts and is not stored.
+    const uint16_t* nm[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      nm[r] = a.Nm + (((int64_t)bi * nrb + min(rb0 + r, nrb - 1)) * nkb) * 256 + c * 16 + 4 * kq;
     // two register sets of U k blocks' counts: the next set is in flight while the MFMAs consume
-    // the current one (an f64 16x16x4 MFMA takes 64 cycles: U = 4 blocks, 1024 per set)
-#ifdef LFE_DN_SINGLE
-    constexpr int U = 8;
-#else
+    // the current one (an f64 16x16x4 MFMA takes 64 cycles)
     constexpr int U = 4;
-#endif
-    auto load = [&](us4 (&nv)[U], int kb) {
+    auto load = [&](us4 (&nv)[U][R], int kb) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        nv[u] = kb + u < k1 ? *reinterpret_cast<const us4*>(nm + (int64_t)(kb + u) * 256) : us4{0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          nv[u][r] = kb + u < k1 ? *reinterpret_cast<const us4*>(nm[r] + (int64_t)(kb + u) * 256) : us4{0, 0, 0, 0};
     };
-    auto use = [&](const us4 (&nv)[U], int kb) {
+    auto use = [&](const us4 (&nv)[U][R], int kb) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (kb + u >= k1) break;
@@ -216,18 +222,13 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const double bv = tb[(kr + t) * p + cc] * cm;
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)nv[u][t], bv, acc[t], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            acc[r][t & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)nv[u][r][t], bv, acc[r][t & 1], 0, 0, 0);
         }
       }
     };
-#ifdef LFE_DN_SINGLE
-    for (int kb = k0; kb < k1; kb += U) {
-      us4 nv[U];
-      load(nv, kb);
-      use(nv, kb);
-    }
-#else
-    us4 na[U], nb[U];
+    us4 na[U][R], nb[U][R];
     load(na, k0);
     for (int kb = k0; kb < k1; kb += 2 * U) {
       load(nb, kb + U);
@@ -236,28 +237,32 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
       load(na, kb + 2 * U);
       use(nb, kb + U);
     }
-#endif
   }
-  d4 d = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  if (a.KP > 1) {  // the KP parts of an output block, added in part order
-    red[wave][lane] = d;
-    __syncthreads();
-    if (part != 0) return;
-    for (int k = 1; k < a.KP; ++k) d += red[wave + k][lane];
-  }
-  if (!live || c >= p) return;
-  // lane (kq, c), register rr: row 16 rb + kq + 4 rr of the output block, column c
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int row = rb * 16 + kq + 4 * rr;
-    if (K2) {
-      if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * p + c] = d[rr];
-    } else {
-      const int h = lo + row;
-      if (row < a.B && h < a.G_P) {
-        const int32_t n = a.cntP[h];
-        const int64_t e = (int64_t)h * p + c;
-        a.alphaP[e] = n > 0 ? (a.S_P[e] - d[rr]) / (double)n : 0.0;
+  for (int r = 0; r < R; ++r) {
+    d4 d = acc[r][0] + acc[r][1];
+    if (a.KP > 1) {  // the KP parts of an output block, added in part order (every wave syncs)
+      __syncthreads();
+      if (part != 0) red[wave][lane] = d;
+      __syncthreads();
+      if (part != 0) continue;
+      for (int k = 1; k < a.KP; ++k) d += red[wave + k][lane];
+    }
+    const int rb = rb0 + r;
+    if (rb >= nrb || c >= p) continue;
+    // lane (kq, c), register rr: row 16 rb + kq + 4 rr of the output block, column c
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = rb * 16 + kq + 4 * rr;
+      if (K2) {
+        if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * p + c] = d[rr];
+      } else {
+        const int h = lo + row;
+        if (row < a.B && h < a.G_P) {
+          const int32_t n = a.cntP[h];
+          const int64_t e = (int64_t)h * p + c;
+          a.alphaP[e] = n > 0 ? (a.S_P[e] - d[rr]) / (double)n : 0.0;
+        }
       }
     }
   }
@@ -283,8 +288,10 @@ bool dense_ok(const lfe_ctx* c) {
   if (GQ16 * p * 8 > 100 * 1024 || B * p * 8 > 64 * 1024) return false;  // the B operand tables in LDS
   if (kDnHC * GQ16 * 2 > 150 * 1024) return false;                        // the build's counters
   if (c->fe[P].cmax > 65535) return false;                                 // uint16 counts
-  // the products cost ~ the cells, the row passes ~ the rows: dense from 0.15 rows per cell
-  if (!(e && e[0] == '1') && (double)c->n_kept_local < 0.15 * (double)dn_cells(c)) return false;
+  // the products cost ~ the cells (~1.1 ns per cell and pass), the row passes ~ the rows (~3.2 ns
+  // per row and pass): dense from 0.3 rows per cell (50M rows over 1e5 x 1e3: 0.5; config 2's 10M:
+  // 0.1, where the dense passes measured 1.5x the row passes)
+  if (!(e && e[0] == '1') && (double)c->n_kept_local < 0.3 * (double)dn_cells(c)) return false;
   return true;
 }
 
@@ -321,11 +328,12 @@ int dense_build(lfe_ctx* c) {
   return LFE_OK;
 }
 
-// k-range parts per output block: waves for about four rounds of the resident waves (wpc per CU),
-// so the last round's tail is short (an owner shard has few buckets)
+// k-range parts per output block: at least one round of the resident waves (wpc per CU; an owner
+// shard has few buckets).  More parts per block cost more than the shorter tail saves (headline,
+// same box: K1 + K2 0.66 ms per solve at one round, 0.85 ms at four)
 static int dn_parts(const lfe_ctx* c, int blocks, int wpc) {
   int kp = 1;
-  int64_t rounds = 4;
+  int64_t rounds = 1;
   if (const char* e = getenv("LFE_DN_ROUNDS")) rounds = std::max(1ll, atoll(e));  // A/B only
   while (kp < kDnWaves && (int64_t)blocks * kp < rounds * c->n_cu * wpc) kp *= 2;
   return kp;
@@ -355,8 +363,8 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
   a.alphaP = c->fe[P].alpha;
   a.zero_check = zero_check;
   const int nrb = a.B / 16;
-  a.KP = dn_parts(c, c->nbe * nrb, 16);  // alpha_Q in LDS: one workgroup per CU
-  const int upw = kDnWaves / a.KP, wgpb = (nrb + upw - 1) / upw;
+  a.KP = dn_parts(c, c->nbe * ((nrb + kDnR - 1) / kDnR), 16);  // alpha_Q in LDS: one workgroup per CU
+  const int upw = kDnWaves / a.KP * kDnR, wgpb = (nrb + upw - 1) / upw;
   const size_t lds = sizeof(double) * a.GQ16 * a.p;
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn_pass<false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -371,8 +379,8 @@ int dense_tq(lfe_ctx* c, double* runs) {
   a.alpha = c->fe[c->L.P].alpha;
   a.runs = runs;
   const int nrb = a.GQ16 / 16;
-  a.KP = dn_parts(c, c->nbe * nrb, 32);  // a 45 KB slice: two workgroups per CU
-  const int upw = kDnWaves / a.KP, wgpb = (nrb + upw - 1) / upw;
+  a.KP = dn_parts(c, c->nbe * ((nrb + kDnR - 1) / kDnR), 32);  // a 45 KB slice: two workgroups per CU
+  const int upw = kDnWaves / a.KP * kDnR, wgpb = (nrb + upw - 1) / upw;
   const size_t lds = sizeof(double) * a.B * a.p;
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn_pass<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
