@@ -192,10 +192,11 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
   }
   __syncthreads();
   const int cc = c < p ? c : 0;
-  const double cm = c < p ? 1.0 : 0.0;
-  d4 acc[R][2];  // per block two chains (steps t even / odd)
+  d4 acc[R][4];  // per block four chains (steps t)
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[r][t] = d4{0.0, 0.0, 0.0, 0.0};
   if (rb0 < nrb) {
     const int k0 = part * nkb / a.KP, k1 = (part + 1) * nkb / a.KP;
     // lane (kq, c): counts of row 16 rb + c at k = 16 kb + 4 kq + t; the matching B row is k.  A
@@ -205,26 +206,34 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
     for (int r = 0; r < R; ++r)
       nm[r] = a.Nm + (((int64_t)bi * nrb + min(rb0 + r, nrb - 1)) * nkb) * 256 + c * 16 + 4 * kq;
     // two register sets of U k blocks' counts: the next set is in flight while the MFMAs consume
-    // the current one (an f64 16x16x4 MFMA takes 64 cycles)
+    // the current one.  Loads are unconditional (a block index past the range is clamped: valid
+    // memory, its MFMAs skipped), so the compiler keeps them out of branches, and a set's B values
+    // are all read from LDS before its MFMAs; four accumulator chains per block.
     constexpr int U = 4;
     auto load = [&](us4 (&nv)[U][R], int kb) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int r = 0; r < R; ++r)
-          nv[u][r] = kb + u < k1 ? *reinterpret_cast<const us4*>(nm[r] + (int64_t)(kb + u) * 256) : us4{0, 0, 0, 0};
+          nv[u][r] = *reinterpret_cast<const us4*>(nm[r] + (int64_t)min(kb + u, k1 - 1) * 256);
     };
     auto use = [&](const us4 (&nv)[U][R], int kb) {
+      double bv[U][4];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (kb + u >= k1) break;
-        const int kr = (kb + u) * 16 + 4 * kq;
+        const int kr = min(kb + u, k1 - 1) * 16 + 4 * kq;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bv[u][t] = tb[(kr + t) * p + cc];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (kb + u >= k1) break;  // wave-uniform
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const double bv = tb[(kr + t) * p + cc] * cm;
+          const double b = c < p ? bv[u][t] : 0.0;
 #pragma unroll
           for (int r = 0; r < R; ++r)
-            acc[r][t & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)nv[u][r][t], bv, acc[r][t & 1], 0, 0, 0);
+            acc[r][t] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)nv[u][r][t], b, acc[r][t], 0, 0, 0);
         }
       }
     };
@@ -240,7 +249,7 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    d4 d = acc[r][0] + acc[r][1];
+    d4 d = (acc[r][0] + acc[r][1]) + (acc[r][2] + acc[r][3]);
     if (a.KP > 1) {  // the KP parts of an output block, added in part order (every wave syncs)
       __syncthreads();
       if (part != 0) red[wave][lane] = d;
