@@ -64,7 +64,8 @@ __device__ bool dn_count(const DnBuildArgs& a, uint32_t* cw, int hlo, int HW, in
     if (sizeof(CT) == 1 && ((old >> sh) & 0xffu) == 0xffu) over = true;  // carried into the next byte
   };
   // 16-byte code loads over the 4-aligned middle, four of each in flight per thread (the rows of
-  // a bucket are read by its workgroups: from L2 or the Infinity Cache after the first)
+  // a bucket are read by its workgroups: from L2 or the Infinity Cache after the first; eight in
+  // flight measured the same, 0.276 vs 0.269 ms per build at 50M rows)
   const int a0 = min(r1, (r0 + 3) & ~3), a1 = max(a0, r1 & ~3);
   for (int row = r0 + (int)threadIdx.x; row < a0; row += blockDim.x) one(a.codeP[row], a.codeQ[row]);
   for (int row = a1 + (int)threadIdx.x; row < r1; row += blockDim.x) one(a.codeP[row], a.codeQ[row]);
