@@ -193,11 +193,15 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
   }
   __syncthreads();
   const int cc = c < p ? c : 0;
-  d4 acc[R][4];  // per block four chains (steps t)
+#ifndef LFE_DN_CH
+#define LFE_DN_CH 4
+#endif
+  constexpr int CH = LFE_DN_CH;  // accumulator chains per block (steps t, and k-block parity at 8)
+  d4 acc[R][CH];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[r][t] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < CH; ++t) acc[r][t] = d4{0.0, 0.0, 0.0, 0.0};
   if (rb0 < nrb) {
     const int k0 = part * nkb / a.KP, k1 = (part + 1) * nkb / a.KP;
     // lane (kq, c): counts of row 16 rb + c at k = 16 kb + 4 kq + t; the matching B row is k.  A
@@ -234,7 +238,8 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
           const double b = c < p ? bv[u][t] : 0.0;
 #pragma unroll
           for (int r = 0; r < R; ++r)
-            acc[r][t] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)nv[u][r][t], b, acc[r][t], 0, 0, 0);
+            acc[r][(t + 4 * u) % CH] =
+                __builtin_amdgcn_mfma_f64_16x16x4f64((double)nv[u][r][t], b, acc[r][(t + 4 * u) % CH], 0, 0, 0);
         }
       }
     };
@@ -251,6 +256,8 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     d4 d = (acc[r][0] + acc[r][1]) + (acc[r][2] + acc[r][3]);
+#pragma unroll
+    for (int t = 4; t < CH; ++t) d += acc[r][t];
     if (a.KP > 1) {  // the KP parts of an output block, added in part order (every wave syncs)
       __syncthreads();
       if (part != 0) red[wave][lane] = d;

@@ -70,15 +70,16 @@ def test_dense_and_row_paths_match_oracle_and_each_other(vcov, monkeypatch):
 
 
 def test_dense_with_singletons_and_ragged_bucket(monkeypatch):
-    """Singleton rows dropped before the table is built; a primary FE whose last bucket is partial
-    (G_P = 3,001) and a secondary FE that is not a multiple of 16 levels (G_Q = 77)."""
+    """Singleton rows dropped before the table is built (40 primary levels with one row each); a
+    primary FE whose last bucket is partial (G_P = 3,041) and a secondary FE that is not a multiple
+    of 16 levels (G_Q = 77)."""
     from leanfe_amd import synth
 
     k = 3
     xs = [f"x{j + 1}" for j in range(k)]
     data = synth.panel(300_000, k, [3_001, 77], seed=5)
     fe1 = np.array(data["fe1"], copy=True)
-    fe1[:40] = np.arange(40) + 2_961  # levels with one row (and their rows' partners) drop
+    fe1[:40] = np.arange(40) + 3_001  # 40 new levels of one row each: singletons, dropped
     data = dict(data, fe1=fe1)
     monkeypatch.setenv("LFE_DENSE", "1")
     _check(_fit(data, xs), _oracle(data, xs))
