@@ -330,8 +330,12 @@ int dense_build(lfe_ctx* c) {
   a.s = L.s;
   a.B = B;
   a.GQ16 = GQ16;
-  // 128-group chunks on 8-bit counters when they fit LDS, else 64-group chunks on 16-bit ones
-  const bool c8 = (size_t)2 * kDnHC * GQ16 <= 150 * 1024 && B % (2 * kDnHC) == 0;
+  // 128-group chunks on 8-bit counters (each bucket's codes read B / 128 times) when they fit LDS
+  // and still give every CU a workgroup; else 64-group chunks on 16-bit counters (twice the
+  // workgroups).  Same box, ms per build: 50M rows 0.269 (8-bit) vs 0.368 (16-bit); the 8-rank
+  // owner shard's 25 buckets 0.068 vs 0.055
+  const bool c8 = (size_t)2 * kDnHC * GQ16 <= 150 * 1024 && B % (2 * kDnHC) == 0 &&
+                  (int64_t)c->nbe * (B / (2 * kDnHC)) >= c->n_cu;
   a.nch = B / (c8 ? 2 * kDnHC : kDnHC);
   a.NA = c->dn_na;
   a.NB = c->dn_nb;
