@@ -70,6 +70,17 @@ def test_step_byte_model_covers_the_headline_kernels():
     assert ab["part_scatter"] == 50_000_000 * (16 * 11 + 8 * 2)
 
 
+def test_step_byte_model_of_the_dense_cross_terms():
+    """With the count tables (lfe_dense.hip) the table build reads both codes and writes two uint16
+    tables, each cross-term pass reads one table, and the layout bases are gone."""
+    n, cells = 50_000_000, 196 * 512 * 1008
+    rows = bench.algorithmic_bytes(n, 11, 2)
+    dense = bench.algorithmic_bytes(n, 11, 2, dense_cells=cells)
+    assert dense["tp"] == dense["tq"] == 2 * cells
+    assert dense["layout_scatter"] == 8 * n + 4 * cells and dense["layout_base"] == 0
+    assert dense["part_scatter"] == rows["part_scatter"] and dense["gram_resid"] == rows["gram_resid"]
+
+
 @pytest.mark.parametrize("G,world", [(100_000, 1), (100_000, 2), (100_000, 8), (1000, 8), (7, 3), (40_000, 8)])
 def test_owner_range_partitions_levels(G, world):
     parts = [owner_range(G, r, world) for r in range(world)]
