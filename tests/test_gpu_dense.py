@@ -1,7 +1,7 @@
 """Dense count-table cross terms (leanfe_amd/csrc/lfe_dense.hip).
 
 For two FEs the sweep's cross terms T_P = N alpha_Q and T_Q = N' alpha_P (N[h][q] = kept rows with
-codes (h, q) per bucket of the primary FE) run on the matrix cores when the table holds >= ~0.15
+codes (h, q) per bucket of the primary FE) run on the matrix cores when the table holds >= 0.3
 rows per cell; otherwise the segment / run layouts of lfe_iter.hip gather row by row.  Both are
 restatements of the same projection loop (polars_impl.py:490-526), so:
 - each path matches the CPU oracle (oracle/altproj.py) at 1e-10 with equal `iterations`;
