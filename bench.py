@@ -49,6 +49,22 @@ CONFIGS = {
     5: dict(rows=500_000_000, levels=[100_000, 1_000], k=10, vcov="iid", cl=None),
 }
 
+# The reference's own benchmark panels (python/tests/create_data.py:143-194, formulas and cluster
+# columns python/tests/reg_test.py:26-97): the only shapes BASELINE.md has timings for
+# (benchmark_results132132.csv:2-7, benchmark_results3.csv:2-10, benchmark_results2.csv:27,29).
+# FE 0 = firm_id, 1 = worker_id, 2 = city_id; k = 4 named regressors (+ 16 / 10 extra x's).
+# The synthetic generator stands in for create_data.py's polars_ds draws (not importable here).
+PRESETS = {
+    "hdfe_base": dict(rows=15_000_000, levels=[10_000, 2_000], k=4, vcov="iid", cl=None),
+    "hdfe_cluster1": dict(rows=15_000_000, levels=[10_000, 2_000], k=4, vcov="cluster", cl=[0]),
+    "hdfe_cluster2": dict(rows=15_000_000, levels=[10_000, 2_000], k=4, vcov="cluster", cl=[0, 1]),
+    "uhdfe_base": dict(rows=15_000_000, levels=[10_000, 2_000, 500], k=20, vcov="iid", cl=None),
+    "uhdfe_cluster2": dict(rows=15_000_000, levels=[10_000, 2_000, 500], k=20, vcov="cluster", cl=[0, 1]),
+    "mega_base": dict(rows=50_000_000, levels=[20_000, 4_000, 1_000], k=14, vcov="iid", cl=None),
+    "mega_cluster1": dict(rows=50_000_000, levels=[20_000, 4_000, 1_000], k=14, vcov="cluster", cl=[0]),
+    "mega_cluster2": dict(rows=50_000_000, levels=[20_000, 4_000, 1_000], k=14, vcov="cluster", cl=[0, 1]),
+}
+
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
@@ -56,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps (GPU clocks settle within ~0.1 s)")
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--preset", type=str, default=None, choices=sorted(PRESETS),
+                    help="one of the reference's own benchmark panels instead of a BASELINE config")
+    ap.add_argument("--runs", type=int, default=5, help="timed runs the K steps are split into (value = median)")
     ap.add_argument("--rows", type=int, default=None, help="rows (total with --scaling strong, per GPU with weak)")
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--levels", type=str, default=None)
@@ -74,7 +93,7 @@ def parse(argv=None):
     ap.add_argument("--print-rank-env", action="store_true",
                     help="diagnostic: each rank prints its rank / world / device and exits (no GPU call)")
     a = ap.parse_args(argv)
-    cfg = CONFIGS[a.config]
+    cfg = PRESETS[a.preset] if a.preset else CONFIGS[a.config]
     a.rows = cfg["rows"] if a.rows is None else a.rows
     a.k = cfg["k"] if a.k is None else a.k
     a.levels = list(cfg["levels"]) if a.levels is None else [int(x) for x in a.levels.split(",")]
@@ -87,7 +106,7 @@ def parse(argv=None):
 
 def is_headline(a) -> bool:
     return (a.rows, a.k, a.levels, a.vcov.lower()) == (50_000_000, 10, [100_000, 1_000], "hc1") \
-        and (a.scaling == "strong" or a.gpus == 1) and not a.emulate_rank
+        and (a.scaling == "strong" or a.gpus == 1) and not a.emulate_rank and not a.preset
 
 
 def workload_label(a, world: int) -> str:
@@ -95,7 +114,14 @@ def workload_label(a, world: int) -> str:
     se = a.vcov if a.vcov.lower() != "cluster" else f"{len(a.cl)}-way clustered SE on " + " x ".join(
         f"fe{f + 1}" for f in a.cl)
     lv = ", ".join(f"{g:.0e}".replace("e+0", "e") for g in a.levels)
-    return f"configs[{a.config - 1}]: {a.rows / 1e6:g}M rows {per}, {len(a.levels)} FE ({lv} levels), k={a.k}, {se}"
+    name = f"reference panel {a.preset.upper()}" if a.preset else f"configs[{a.config - 1}]"
+    return f"{name}: {a.rows / 1e6:g}M rows {per}, {len(a.levels)} FE ({lv} levels), k={a.k}, {se}"
+
+
+def split_runs(steps: int, runs: int) -> list[int]:
+    """The K timed steps as ``runs`` consecutive timed runs (sizes differ by at most one)."""
+    runs = max(1, min(runs, steps))
+    return [steps // runs + (1 if i < steps % runs else 0) for i in range(runs)]
 
 
 # ---------------------------------------------------------------------------
@@ -364,16 +390,25 @@ def main(argv=None):
     for _ in range(a.warmup):
         solve_step(eng, a.vcov, n_cl)
 
-    d.barrier()
-    device_sync(eng)
-    t0 = time.perf_counter()
+    # the K timed steps as `runs` timed runs, each bracketed by barrier + device sync and timed as
+    # the max over ranks; `value` is the median run's rate, the mean is kept
     res = None
-    for _ in range(a.steps):
-        res = solve_step(eng, a.vcov, n_cl)
-    device_sync(eng)
-    t1 = time.perf_counter()
-    d.barrier()
-    elapsed = d.max(t1 - t0)
+    run_s = []
+    sizes = split_runs(a.steps, a.runs)
+    for m in sizes:
+        d.barrier()
+        device_sync(eng)
+        t0 = time.perf_counter()
+        for _ in range(m):
+            res = solve_step(eng, a.vcov, n_cl)
+        device_sync(eng)
+        t1 = time.perf_counter()
+        d.barrier()
+        run_s.append(d.max(t1 - t0))
+    elapsed = sum(run_s)
+    per_step = sorted(s / m for s, m in zip(run_s, sizes))
+    med_step = per_step[len(per_step) // 2] if len(per_step) % 2 else 0.5 * (
+        per_step[len(per_step) // 2 - 1] + per_step[len(per_step) // 2])
     # per-kernel times from a second pass of the same steps with an event pair around every
     # launch (the events cost ~0.2 ms of host time per step, so they stay out of `value`)
     kstats = {}
@@ -385,8 +420,9 @@ def main(argv=None):
         eng.profile(False)
 
     total_rows = geo["total"] if not a.emulate_rank else geo["local"]
-    value = total_rows * a.steps / elapsed / 1e6
-    ms_step = elapsed / a.steps * 1e3
+    value = total_rows / med_step / 1e6
+    ms_step = med_step * 1e3
+    value_mean = total_rows * a.steps / elapsed / 1e6
     p, F = a.k + 1, len(a.levels)
     cells = eng.dense_cells()
     ab = algorithmic_bytes(geo["local"], p, F, clustered=bool(a.cl), dense_cells=cells)
@@ -450,6 +486,10 @@ def main(argv=None):
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_step, 3),
+            "statistic": f"median over {len(sizes)} timed runs of {'/'.join(map(str, sizes))} steps",
+            "value_mean": round(value_mean, 2),
+            "ms_per_step_mean": round(elapsed / a.steps * 1e3, 3),
+            "runs_ms_per_step": [round(s / m * 1e3, 3) for s, m in zip(run_s, sizes)],
             "higher_is_better": True,
             "scaling": a.scaling,
             "vs_baseline": None,

@@ -437,6 +437,7 @@ static void free_data(lfe_ctx* c) {
   dfree(c->sw.s64);
   dfree(c->sw.sdbl);
   dfree(c->sw.tile);
+  dfree(c->sw.red);
   dfree(c->sw.toff);
   free_stream_clusters(c);
   c->sw = lfe_ctx::StreamWS();
@@ -734,8 +735,9 @@ int lfe_load_codes(lfe_ctx* c, int64_t n, int p, int F, const int32_t* const* fe
   LFE_CTX(c);
   if (F < 1 || F > kMaxFE) return fail(LFE_EINVAL, "streamed X (lfe_load_codes) needs 1 to 8 fixed effects");
   if (!n_levels || (n > 0 && !fe_codes)) return fail(LFE_EINVAL, "null input pointer");
-  if (p > 11) return fail(LFE_EINVAL, "streamed X supports p <= 11 columns (y plus up to 10 regressors)");
   if (kind != LFE_HOST && kind != LFE_DEVICE) return fail(LFE_EINVAL, "kind must be LFE_HOST or LFE_DEVICE");
+  if (weights && p + 2 > kColStatHead)  // the weighted sums add w and the raw y as two more columns
+    return fail(LFE_EINVAL, "weighted streamed X supports p <= 62 columns");
   LFE_TRY(alloc_data(c, n, p, F, n_levels, weights != nullptr, true));
   const hipMemcpyKind mk = kind == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
   hipError_t e = hipSuccess;
@@ -773,8 +775,10 @@ int lfe_stream_begin(lfe_ctx* c, int pass, const double* beta_full) {
     }
   }
   if (pass > 1) {
-    LFE_TRY(ensure_f64(c, w.tile, w.tile_cap, 272));
-    LFE_HIP(hipMemsetAsync(w.tile, 0, sizeof(double) * 272, c->stream));
+    w.ts = stream_tile_stride(c->p);
+    const size_t tl = stream_tile_len(c->p);
+    LFE_TRY(ensure_f64(c, w.tile, w.tile_cap, tl));
+    LFE_HIP(hipMemsetAsync(w.tile, 0, sizeof(double) * tl, c->stream));
   }
   if (pass == 1) c->sums_ready = c->raw_ready = false;
   w.pass = pass;
@@ -823,8 +827,8 @@ int lfe_stream_rows(lfe_ctx* c, int64_t row0, int64_t rows, const double* const*
 // the columns generated chunk by chunk on the device (no host copy of data larger than HBM)
 int lfe_synth_load_codes(lfe_ctx* c, int64_t n, int k, int n_fe, const int32_t* n_levels, uint64_t seed) {
   LFE_CTX(c);
-  if (n_fe != 2 || !n_levels) return fail(LFE_EINVAL, "streamed X supports two fixed effects");
-  if (k < 1 || k > 10) return fail(LFE_EINVAL, "streamed X supports 1 <= k <= 10 regressors");
+  if (n_fe < 1 || n_fe > kMaxFE || !n_levels) return fail(LFE_EINVAL, "streamed X needs 1 to 8 fixed effects");
+  if (k < 1 || k + 1 > kMaxCols) return fail(LFE_EINVAL, "k out of range");
   LFE_TRY(alloc_data(c, n, k + 1, n_fe, n_levels, false, true));
   LFE_TRY(synth_codes(c, n_levels, seed));
   c->loaded = true;
@@ -858,8 +862,9 @@ int lfe_stream_end(lfe_ctx* c, double* out) {
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
     if (c->n > 0) LFE_HIP(hipMemcpyAsync(c->raw_tile, w.tile, sizeof(double) * 256, hipMemcpyDeviceToDevice, c->stream));
     // the raw Gram tile stands for the Gram from the group tables only in the unweighted two-FE case
-    // of one process (ranks' tiles have their own shifts: a sharded fit streams the design Gram)
-    c->raw_ready = c->F == 2 && !c->w && c->world == 1;
+    // of one process (ranks' tiles have their own shifts: a sharded fit streams the design Gram) and
+    // when it fits one 16 x 16 MFMA tile (intercept in slot 15)
+    c->raw_ready = c->F == 2 && !c->w && c->world == 1 && p <= 15;
     if (c->world > 1) {  // every rank streamed its own rows: the group sums over all ranks
       std::vector<std::pair<double*, size_t>> bufs;
       for (auto& fe : c->fe) {
@@ -878,17 +883,19 @@ int lfe_stream_end(lfe_ctx* c, double* out) {
     return LFE_OK;
   }
   if (!out) return fail(LFE_EINVAL, "out is null");
-  LFE_TRY(allreduce_sum_f64(c, w.tile, 260));  // sharded: every rank's rows
-  std::vector<double> h(260);
-  LFE_TRY(d2h_sync(c, h.data(), w.tile, sizeof(double) * 260));
+  // tile (i, j) at i * ts + j, the statistics after ts * ts (ts = 16: the p <= 11 passes)
+  const size_t ts = (size_t)w.ts, tl = ts * ts + 4;
+  LFE_TRY(allreduce_sum_f64(c, w.tile, tl));  // sharded: every rank's rows
+  std::vector<double> h(tl);
+  LFE_TRY(d2h_sync(c, h.data(), w.tile, sizeof(double) * tl));
   if (pass == 2 || pass == 4) {  // stats[4] (sum r^2 w, sum r^2, sum y~, sum y~^2), then the HC1 meat
     const int km = k + (pass == 4 ? 1 : 0);  // pass 4: over u = [1, x~, z~]
-    for (int e = 0; e < 4; ++e) out[e] = h[256 + e];
+    for (int e = 0; e < 4; ++e) out[e] = h[ts * ts + e];
     for (int i = 0; i < km; ++i)
-      for (int j = 0; j < km; ++j) out[4 + i * km + j] = h[(size_t)(1 + i) * 16 + (1 + j)];
+      for (int j = 0; j < km; ++j) out[4 + i * km + j] = h[(size_t)(1 + i) * ts + (1 + j)];
   } else {  // the (p + 1) x (p + 1) Gram of [1, y~, x~]
     for (int i = 0; i <= p; ++i)
-      for (int j = 0; j <= p; ++j) out[i * (p + 1) + j] = h[(size_t)i * 16 + j];
+      for (int j = 0; j <= p; ++j) out[i * (p + 1) + j] = h[(size_t)i * ts + j];
   }
   return LFE_OK;
 }
@@ -898,7 +905,7 @@ int lfe_stream_clusters(lfe_ctx* c, int n_subsets, const int32_t* masks) {
   if (!c->sw.on) return fail(LFE_ESTATE, "lfe_stream_clusters: the context holds resident columns");
   if (!c->prepared) return fail(LFE_ESTATE, "lfe_drop_singletons first");
   if (n_subsets < 1 || !masks) return fail(LFE_EINVAL, "bad subsets");
-  if (c->world > 1) return fail(LFE_EINVAL, "streamed clustered SEs run in one process");
+  if (c->sw.pass != 0) return fail(LFE_ESTATE, "lfe_stream_clusters: a streamed pass is open (lfe_stream_end first)");
   return stream_clusters_prep(c, n_subsets, masks);
 }
 

@@ -364,10 +364,15 @@ __device__ __forceinline__ int cl_owner(uint64_t key, int world) {
   return (int)(key % (uint64_t)world);
 }
 
+// the key of cluster h: K[seg_off[h]] over sorted row keys, or K[h] when K holds one key per cluster
+__device__ __forceinline__ uint64_t cl_key(const uint64_t* K, const int32_t* seg_off, int h) {
+  return seg_off ? K[seg_off[h]] : K[h];
+}
+
 __global__ void k_cl_owner_count(const uint64_t* __restrict__ K, const int32_t* __restrict__ seg_off, int32_t G,
                                  int world, int32_t* __restrict__ cnt) {
   for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < G; h += gridDim.x * blockDim.x)
-    atomicAdd(&cnt[cl_owner(K[seg_off[h]], world)], 1);
+    atomicAdd(&cnt[cl_owner(cl_key(K, seg_off, h), world)], 1);
 }
 
 // send record of cluster h: its key and S[h][0, k), grouped by owner rank
@@ -376,7 +381,7 @@ __global__ void k_cl_owner_scatter(const uint64_t* __restrict__ K, const int32_t
                                    int32_t* __restrict__ cursor, uint64_t* __restrict__ skey,
                                    double* __restrict__ srec) {
   for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < G; h += gridDim.x * blockDim.x) {
-    const uint64_t key = K[seg_off[h]];
+    const uint64_t key = cl_key(K, seg_off, h);
     const int32_t pos = atomicAdd(&cursor[cl_owner(key, world)], 1);
     skey[pos] = key;
     for (int j = 0; j < k; ++j) srec[(int64_t)pos * k + j] = S[(int64_t)h * k + j];
@@ -392,10 +397,11 @@ __global__ void k_iota_pairs(const uint64_t* __restrict__ kin, int64_t n, uint64
 }
 
 // Owner-partitioned reduction of the local cluster sums: cluster h's
-// record goes to rank owner(key); every owner merges what it received by key, forms
-// S'S of its clusters, and only the k x k meats and cluster counts are all-reduced.
-static int owner_meat(lfe_ctx* c, const uint64_t* K, int32_t G, int k, uint64_t span, double* meat,
-                      int64_t* G_out) {
+// record (its key and row S[h][0, k)) goes to rank owner(key); every owner merges what it received
+// by key, forms S'S of its clusters, and only the k x k meats and cluster counts are all-reduced.
+// Cluster h's key is K[seg_off[h]] (sorted row keys) or, with seg_off null, K[h].
+int owner_meat(lfe_ctx* c, const uint64_t* K, const int32_t* seg_off, const double* S, int32_t G, int k,
+               uint64_t span, double* meat, int64_t* G_out) {
   auto& W = c->clw;
   const int world = c->world, rank = c->rank;
   LFE_TRY(ensure_u64(c, W.skey, W.skey_cap, (size_t)std::max(G, 1)));
@@ -406,7 +412,7 @@ static int owner_meat(lfe_ctx* c, const uint64_t* K, int32_t G, int k, uint64_t 
   int32_t* mat = W.ocnt + 2 * world;   // [world][world] records from rank r to rank q
   LFE_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * world, c->stream));
   if (G > 0)
-    hipLaunchKernelGGL(k_cl_owner_count, dim3(grid_for(G)), dim3(kBlock), 0, c->stream, K, W.seg_off, G, world, cnt);
+    hipLaunchKernelGGL(k_cl_owner_count, dim3(grid_for(G)), dim3(kBlock), 0, c->stream, K, seg_off, G, world, cnt);
   LFE_HIP(hipGetLastError());
   std::vector<int32_t> mine(world), offs(world);
   LFE_TRY(d2h_sync(c, mine.data(), cnt, sizeof(int32_t) * world));
@@ -416,7 +422,7 @@ static int owner_meat(lfe_ctx* c, const uint64_t* K, int32_t G, int k, uint64_t 
   }
   LFE_TRY(h2d_small(c, cur, offs.data(), sizeof(int32_t) * world));
   if (G > 0)
-    hipLaunchKernelGGL(k_cl_owner_scatter, dim3(grid_for(G)), dim3(kBlock), 0, c->stream, K, W.seg_off, c->clS, G, k,
+    hipLaunchKernelGGL(k_cl_owner_scatter, dim3(grid_for(G)), dim3(kBlock), 0, c->stream, K, seg_off, S, G, k,
                        world, cur, W.skey, W.srec);
   LFE_HIP(hipGetLastError());
   // who sends how much to whom
@@ -547,7 +553,7 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
     }
     return LFE_OK;
   }
-  if (c->world > 1) return owner_meat(c, W.keys[buf], G, k, span, meat, G_out);
+  if (c->world > 1) return owner_meat(c, W.keys[buf], W.seg_off, c->clS, G, k, span, meat, G_out);
   *G_out = G;
   if (k == 0) return LFE_OK;
   return launch_table_gram(c, c->clS, G, k, meat);

@@ -334,8 +334,9 @@ int dense_build(lfe_ctx* c) {
   // and still give every CU a workgroup; else 64-group chunks on 16-bit counters (twice the
   // workgroups).  Same box, ms per build: 50M rows 0.269 (8-bit) vs 0.368 (16-bit); the 8-rank
   // owner shard's 25 buckets 0.068 vs 0.055
-  const bool c8 = (size_t)2 * kDnHC * GQ16 <= 150 * 1024 && B % (2 * kDnHC) == 0 &&
-                  (int64_t)c->nbe * (B / (2 * kDnHC)) >= c->n_cu;
+  const bool c8_fits = (size_t)2 * kDnHC * GQ16 <= 150 * 1024 && B % (2 * kDnHC) == 0;
+  bool c8 = c8_fits && (int64_t)c->nbe * (B / (2 * kDnHC)) >= c->n_cu;
+  if (const char* e = getenv("LFE_DN_C8")) c8 = c8_fits && e[0] == '1';  // tests: force either form
   a.nch = B / (c8 ? 2 * kDnHC : kDnHC);
   a.NA = c->dn_na;
   a.NB = c->dn_nb;

@@ -872,12 +872,12 @@ int sums4(lfe_ctx* c) {
 // ---------------------------------------------------------------------------
 // out-of-core X: group sums and raw Gram of one streamed row chunk
 // ---------------------------------------------------------------------------
-// The chunk's rows in input order (no partition): lane (kq, c) holds "column" c of rows
-// 16 g + 4 kq + r as in k_sums2_raw.  Column c < p adds x_c (weighted: w x_c, polars_impl.py:496);
+// The chunk's rows in input order (no partition): lane (kq, c) holds "columns" c + 16 J (J < NJ)
+// of rows 16 g + 4 kq + r as in k_sums2_raw.  Column c < p adds x_c (weighted: w x_c, polars_impl.py:496);
 // weighted fits add two more: c = p the weight (W_f), c = p + 1 the raw y (Sy_f, the unweighted
 // stop test).  Every FE's sums go to the chunk tables [G_f][pw] in two-limb fixed point (fine
-// limbs in s64, coarse limbs in sdbl), the shifted raw Gram of the unweighted two-FE case to one
-// MFMA chain per row.  A row is kept iff every FE's pre-filter count of its code exceeds 1 (the
+// limbs in s64, coarse limbs in sdbl), the shifted raw Gram of the unweighted two-FE case (p <= 15,
+// one column group) to one MFMA chain per row.  A row is kept iff every FE's pre-filter count of its code exceeds 1 (the
 // single-pass drop, polars_impl.py:477-482).
 struct StreamSumsArgs {
   const double* X;  // [p][ld] chunk columns
@@ -894,17 +894,25 @@ struct StreamSumsArgs {
   double* raw_part;     // [blocks][256]
 };
 
+template <int NJ>
 __global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.p, pw = a.pw, F = a.F;
-  const bool col = c < pw;
-  const FixCol fc = col ? fix_col(a.fixq, c) : FixCol{};
-  // the raw Gram (unweighted): z = x - shift on the data lanes, 1 on lane 15 (intercept)
+  bool col[NJ];
+  FixCol fc[NJ];
+  const double* __restrict__ xc[NJ];
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) {
+    const int cj = c + 16 * J;
+    col[J] = cj < pw;
+    fc[J] = col[J] ? fix_col(a.fixq, cj) : FixCol{};
+    xc[J] = a.X + (int64_t)(cj < p ? cj : 0) * a.ld;  // lane p + 1 (Sy): column 0 = y
+  }
+  // the raw Gram (unweighted, one column group): z = x - shift on the data lanes, 1 on lane 15
   const bool dcol = c < p;
   const double cm = dcol ? 1.0 : 0.0;
-  const double zc = (c == 15 ? 1.0 : 0.0) - (dcol ? a.shift[c] : 0.0);
-  const double* __restrict__ xc = a.X + (int64_t)(c < p ? c : 0) * a.ld;  // lane p + 1 (Sy): column 0 = y
+  const double zc = NJ == 1 ? (c == 15 ? 1.0 : 0.0) - (dcol ? a.shift[c] : 0.0) : 0.0;
   d4 racc = d4{0.0, 0.0, 0.0, 0.0};
   const int64_t ngroups = (a.rows + 15) >> 4;
   for (int64_t g = (int64_t)blockIdx.x * 4 + wave; g < ngroups; g += (int64_t)gridDim.x * 4) {
@@ -921,27 +929,32 @@ __global__ __launch_bounds__(256) void k_stream_sums(StreamSumsArgs a) {
           keep = keep && a.cnt_pre[f][gc[f]] > 1;
         }
       }
-      const double xv = row < a.rows ? xc[row] : 0.0;
-      const double z = keep ? __builtin_fma(xv, cm, zc) : 0.0;
-      racc = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc, 0, 0, 0);
-      if (keep && col) {  // two-limb fixed point: fine limbs in s64, coarse limbs in sdbl
-        double v = xv;
-        if (a.w) {
-          const double wi = a.w[row];
-          v = c < p ? xv * wi : (c == p ? wi : xv);
-        }
-        double hh;
-        const unsigned long long xi = fix_split(v, fc, hh);
+      const double wi = (a.w && keep) ? a.w[row] : 1.0;
 #pragma unroll
-        for (int f = 0; f < kMaxFE; ++f)
-          if (f < F) atomicAdd(&a.s64[a.toff[f] + (int64_t)gc[f] * pw + c], xi);
-        if (hh != 0.0)
+      for (int J = 0; J < NJ; ++J) {
+        const int cj = c + 16 * J;
+        const double xv = row < a.rows ? xc[J][row] : 0.0;
+        if (NJ == 1) {
+          const double z = keep ? __builtin_fma(xv, cm, zc) : 0.0;
+          racc = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, racc, 0, 0, 0);
+        }
+        if (keep && col[J]) {  // two-limb fixed point: fine limbs in s64, coarse limbs in sdbl
+          double v = xv;
+          if (a.w) v = cj < p ? xv * wi : (cj == p ? wi : xv);
+          double hh;
+          const unsigned long long xi = fix_split(v, fc[J], hh);
 #pragma unroll
           for (int f = 0; f < kMaxFE; ++f)
-            if (f < F) atomicAdd(&a.sdbl[a.toff[f] + (int64_t)gc[f] * pw + c], hh);
+            if (f < F) atomicAdd(&a.s64[a.toff[f] + (int64_t)gc[f] * pw + cj], xi);
+          if (hh != 0.0)
+#pragma unroll
+            for (int f = 0; f < kMaxFE; ++f)
+              if (f < F) atomicAdd(&a.sdbl[a.toff[f] + (int64_t)gc[f] * pw + cj], hh);
+        }
       }
     }
   }
+  if (NJ > 1) return;  // no raw Gram: the caller streams the design Gram (pass 3)
   // waves' tiles summed in LDS in wave order (lane (kq, c) holds rows kq + 4 rr of column c)
   __shared__ double rred[256];
   for (int wv = 0; wv < 4; ++wv) {
@@ -1070,9 +1083,16 @@ int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int
   LFE_TRY(ensure_f64(c, c->raw_part, c->raw_part_cap, (size_t)nblocks * 256));
   LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
   a.raw_part = c->raw_part;
+  const int nj = (pw + 15) / 16;  // column groups per lane (one: the raw Gram rides along)
   {
     ProfScope _ps(c, K_GROUP_SUMS);
-    hipLaunchKernelGGL(k_stream_sums, dim3(nblocks), dim3(256), 0, c->stream, a);
+    switch (nj) {
+      case 1: hipLaunchKernelGGL(k_stream_sums<1>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+      case 2: hipLaunchKernelGGL(k_stream_sums<2>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+      case 3: hipLaunchKernelGGL(k_stream_sums<3>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+      case 4: hipLaunchKernelGGL(k_stream_sums<4>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+      default: hipLaunchKernelGGL(k_stream_sums<5>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+    }
     LFE_HIP(hipGetLastError());
   }
   {
@@ -1081,9 +1101,11 @@ int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int
                        reinterpret_cast<unsigned long long*>(w.s64), w.sdbl, m, p, pw, c->fixq, F,
                        reinterpret_cast<const int64_t*>(w.toff), reinterpret_cast<double* const*>(w.toff + kMaxFE));
     LFE_HIP(hipGetLastError());
-    reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
-    hipLaunchKernelGGL(k_tile_add, dim3(1), dim3(256), 0, c->stream, w.tile, c->raw_tile, 256);
-    LFE_HIP(hipGetLastError());
+    if (nj == 1) {
+      reduce_tiles(c, c->raw_part, nblocks, c->raw_tile);
+      hipLaunchKernelGGL(k_tile_add, dim3(1), dim3(256), 0, c->stream, w.tile, c->raw_tile, 256);
+      LFE_HIP(hipGetLastError());
+    }
   }
   return LFE_OK;
 }

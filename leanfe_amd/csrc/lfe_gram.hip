@@ -1397,16 +1397,194 @@ __global__ __launch_bounds__(256) void k_stream_rows(StreamRowArgs a, double* __
   }
 }
 
+// Wide fits (p > 11: the row-per-lane kernel above would hold a (p + 1)^2 / 2 accumulator per lane).
+// The MFMA lane layout of k_gram over the chunk's rows in input order: lane (kq, c) owns design
+// column 16 I + c (I < NT) of rows 16 g + 4 kq + s, gathers its columns of every FE's alpha rows
+// from the global tables, and the Gram / meat accumulates on v_mfma_f64_16x16x4f64 in NT (NT + 1) / 2
+// output blocks.  MODE 1: column 0 = sqrt(w), 1 + c = sqrt(w) x~_c (the Gram of X_w = [1, y~, x~] sqrt(w),
+// polars_impl.py:201-209).  MODE 0: the residual r = y~ - beta0 - sum_j beta_j x~_j (polars_impl.py:229)
+// is one 16-lane DPP sum per row; the meat columns are u r sqrt(w) with u = x~ (IC 0: column c = x~_c,
+// tile (1 + i, 1 + j) = meat (i, j)) or u = [1, x~, z~] (IC 1: the intercept in y's column 0; the
+// tile conversion shifts it by one so both forms unpack alike), the statistics after the blocks.
+template <int NT, int MODE, int IC>
+__global__ __launch_bounds__(256) void k_stream_wide(StreamRowArgs a, double* __restrict__ partial, int64_t pstride) {
+  using Sh = GramShape<NT>;
+  __shared__ double red[Sh::LEN];
+  __shared__ double stat_red[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kq = lane >> 4, c = lane & 15;
+  const int p = a.p, F = a.F;
+  d4 acc[Sh::NP];
+#pragma unroll
+  for (int q = 0; q < Sh::NP; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  double st[4] = {0.0, 0.0, 0.0, 0.0};
+  int xl[NT];
+  bool dat[NT], one[NT];
+  double fill[NT], coef[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) {
+    const int col = 16 * I + c;
+    int xc = MODE == 1 ? col - 1 : col;  // MODE 1: column 0 = intercept
+    if (xc >= p) xc = -2;
+    xl[I] = xc >= 0 ? xc : 0;
+    fill[I] = xc == -1 ? 1.0 : 0.0;
+    coef[I] = MODE == 0 ? (xc == 0 ? 1.0 : (xc >= 1 ? -a.beta[xc] : 0.0)) : 0.0;
+    one[I] = MODE == 0 && IC && xc == 0;
+    dat[I] = MODE == 0 ? (xc >= 1 || one[I]) : xc >= 0;
+  }
+  const double beta0 = MODE == 0 ? a.beta[0] : 0.0;
+  const int64_t ngroups = (a.rows + 15) >> 4;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + wave; g < ngroups; g += (int64_t)gridDim.x * 4) {
+    const int64_t r = g * 16 + kq * 4;
+    double xt[4][NT], wv[4];
+    bool valid[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int64_t row = r + s;
+      bool keep = row < a.rows;
+      int32_t gc[kMaxFE];
+#pragma unroll
+      for (int f = 0; f < kMaxFE; ++f) {
+        gc[f] = 0;
+        if (f < F) {
+          gc[f] = keep ? a.code[f][row] : 0;
+          keep = keep && a.cnt_pre[f][gc[f]] > 1;
+        }
+      }
+      valid[s] = keep;
+      wv[s] = (a.w && keep) ? a.w[row] : 1.0;
+#pragma unroll
+      for (int I = 0; I < NT; ++I) xt[s][I] = row < a.rows ? a.X[(int64_t)xl[I] * a.ld + row] : 0.0;
+#pragma unroll
+      for (int f = 0; f < kMaxFE; ++f) {
+        if (f >= F) continue;
+        const double* af = a.alpha[f] + (int64_t)gc[f] * p;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) xt[s][I] -= af[xl[I]];
+      }
+    }
+    double z[4][NT];
+    if (MODE == 1) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double sw = a.w ? sqrt(wv[s]) : 1.0;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) z[s][I] = valid[s] ? (dat[I] ? xt[s][I] : fill[I]) * sw : 0.0;
+      }
+    } else {
+      double sc[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        double t = coef[0] * xt[s][0];
+#pragma unroll
+        for (int I = 1; I < NT; ++I) t += coef[I] * xt[s][I];
+        const double res = row16_sum(t) - beta0;
+        if (c == 0 && valid[s]) {  // lane c = 0 holds y~ (column 0)
+          const double rr = res * res;
+          st[0] += a.w ? wv[s] * rr : rr;
+          st[1] += rr;
+          st[2] += xt[s][0];
+          st[3] += xt[s][0] * xt[s][0];
+        }
+        sc[s] = a.w ? res * wv[s] : res;
+        const double m = a.w ? res * sqrt(wv[s]) : res;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) z[s][I] = (valid[s] && dat[I]) ? (one[I] ? 1.0 : xt[s][I]) * m : 0.0;
+      }
+      if (a.scores) {  // row-major [rows][ks]; a dropped row's score row is zero
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+          if (!dat[I]) continue;
+          const int j = xl[I] - 1 + IC;
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            if (r + s < a.rows) a.scores[(r + s) * a.ks + j] = valid[s] ? (one[I] ? 1.0 : xt[s][I]) * sc[s] : 0.0;
+        }
+      }
+    }
+    mfma_rows<NT>(z, acc);
+  }
+  double* out = partial + (int64_t)blockIdx.x * pstride;
+  block_reduce_store<NT, 256>(acc, red, out, tid);
+  if (MODE == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) st[e] = wave_reduce63(st[e], 0.0, [](double x, double y) { return x + y; });
+    if (lane == 63)
+      for (int e = 0; e < 4; ++e) stat_red[wave][e] = st[e];
+    __syncthreads();
+    if (tid < 4) out[Sh::LEN + tid] = ((stat_red[0][tid] + stat_red[1][tid]) + stat_red[2][tid]) + stat_red[3][tid];
+  } else if (tid < 4) {
+    out[Sh::LEN + tid] = 0.0;
+  }
+}
+
+// tile[(16 I + i + off) * ts + 16 J + j + off] += block (I, J)[i][j] (both triangles), statistics after
+// ts * ts: the chunk's reduced MFMA blocks added to the streamed tile in chunk order
+__global__ void k_wide_tile_add(double* __restrict__ tile, const double* __restrict__ blk, int NT, int ts, int off) {
+  const int np = NT * (NT + 1) / 2;
+  for (int e = threadIdx.x; e < np * 256; e += blockDim.x) {
+    const int q = e >> 8, i = (e >> 4) & 15, j = e & 15;
+    int I = 0, rem = q;
+    while (rem >= NT - I) {
+      rem -= NT - I;
+      ++I;
+    }
+    const int J = I + rem;
+    const int gi = 16 * I + i + off, gj = 16 * J + j + off;
+    if (gi >= ts || gj >= ts) continue;
+    tile[(size_t)gi * ts + gj] += blk[e];
+    if (I != J) tile[(size_t)gj * ts + gi] += blk[e];
+  }
+  if (threadIdx.x < 4) tile[(size_t)ts * ts + threadIdx.x] += blk[np * 256 + threadIdx.x];
+}
+
+// the wide (p > 11) form of stream_rows_chunk: k_stream_wide, its blocks reduced in block order and
+// added to the streamed tile (stride c->sw.ts = 16 NT)
+static int stream_wide_chunk(lfe_ctx* c, int mode, int icpt, const StreamRowArgs& a) {
+  auto& w = c->sw;
+  const int NT = w.ts / 16;
+  const int np = NT * (NT + 1) / 2;
+  const int64_t len = (int64_t)np * 256 + 4;
+  const int64_t groups = (a.rows + 15) / 16;
+  const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * 4, (groups + 3) / 4));
+  LFE_TRY(ensure_scratch(c, (size_t)nblocks * len));
+  LFE_TRY(ensure_f64(c, w.red, w.red_cap, (size_t)len));
+  {
+    ProfScope _ps(c, mode == 0 ? K_GRAM_RESID : K_GRAM_DESIGN);
+#define SW(NT_, M_, I_) \
+  hipLaunchKernelGGL((k_stream_wide<NT_, M_, I_>), dim3(nblocks), dim3(256), 0, c->stream, a, c->scratch, len)
+#define SWM(M_, I_)                      \
+  switch (NT) {                          \
+    case 1: SW(1, M_, I_); break;        \
+    case 2: SW(2, M_, I_); break;        \
+    case 3: SW(3, M_, I_); break;        \
+    default: SW(4, M_, I_); break;       \
+  }
+    if (mode == 1) {
+      SWM(1, 0)
+    } else if (icpt) {
+      SWM(0, 1)
+    } else {
+      SWM(0, 0)
+    }
+#undef SWM
+#undef SW
+    LFE_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_reduce_partials, dim3(len), dim3(256), 0, c->stream, c->scratch, nblocks, len, w.red);
+  LFE_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_wide_tile_add, dim3(1), dim3(256), 0, c->stream, w.tile, w.red, NT, w.ts,
+                     mode == 0 && icpt ? 1 : 0);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
 // One streamed chunk of the residual (mode 0; icpt 1: the IV residual over u = [1, x~, z~]) or
 // design-Gram (mode 1) pass: the chunk's tile is added to c->sw.tile in chunk order; `scores`
 // ([rows][ks], or null) receives the chunk's score rows for the cluster sums.
 int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t ld, int64_t row0, int64_t rows,
                       double* scores) {
   const int p = c->p;
-  if (p > 11) {
-    set_error("streamed X passes support p <= 11");
-    return LFE_EINVAL;
-  }
   StreamRowArgs a{};
   a.X = X;
   a.ld = ld;
@@ -1422,6 +1600,7 @@ int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t l
   a.beta = c->dbeta;
   a.scores = mode == 0 ? scores : nullptr;
   a.ks = p - 1 + icpt;
+  if (p > 11) return stream_wide_chunk(c, mode, icpt, a);
   const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * 4, (rows + 255) / 256));
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * 260));
   {

@@ -351,8 +351,11 @@ struct lfe_ctx {
     size_t s64_cap = 0;
     double* sdbl = nullptr;  // the same in f64 (a chunk whose range defeats the fixed point)
     size_t sdbl_cap = 0;
-    double* tile = nullptr;  // [272] tile (+ statistics) accumulated over the chunks, in order
+    double* tile = nullptr;  // [ts * ts + 4] tile (+ statistics) accumulated over the chunks, in order
     size_t tile_cap = 0;
+    int ts = 16;             // tile stride: 16 for p <= 11 (row-per-lane passes), else 16 * ceil((p + 1) / 16)
+    double* red = nullptr;   // wide passes: the chunk's reduced MFMA blocks (+ statistics)
+    size_t red_cap = 0;
     double* toff = nullptr;  // [4 kMaxFE] 8-byte slots: table ends (int64), S / W / Sy pointers per FE
     size_t toff_cap = 0;
     int icpt = 0;            // pass 4: the IV residual over u = [1, x~, z~]
@@ -362,6 +365,8 @@ struct lfe_ctx {
     std::vector<int32_t*> cid;   // [n] per subset (-1: dropped row)
     std::vector<int32_t> G;      // clusters per subset
     std::vector<double*> S;      // [G][ks] per subset
+    std::vector<uint64_t*> ukey; // multi-rank: [G] the intersection key of every local cluster per subset
+    std::vector<uint64_t> span;  // key span per subset
     std::vector<size_t> S_cap;
     int ks = 0;                  // score width of the sums in S
     double* sc = nullptr;        // [rows][ks] the chunk's score rows
@@ -423,6 +428,10 @@ int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const 
                  int k, int32_t* G_out);  // weighted streamed fits: w's max / rms into fixq column p
 int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t ld, int64_t row0, int64_t rows,
                       double* scores);
+// streamed tile stride for p data columns: the p <= 11 row-per-lane passes use the 16 x 16 tile of
+// the resident kernels; wider fits the MFMA passes' 16 * ceil((p + 1) / 16) (design Gram of [1, y~, x~])
+inline int stream_tile_stride(int p) { return p <= 11 ? 16 : 16 * ((p + 1 + 15) / 16); }
+inline size_t stream_tile_len(int p) { const size_t t = (size_t)stream_tile_stride(p); return t * t + 4; }
 void stream_tile_add(lfe_ctx* c, const double* t, int m);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
 void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out);  // sum of [nblocks][256] tiles
@@ -434,6 +443,10 @@ int ensure_sort_ws(lfe_ctx* c, size_t n);
 int radix_sort(lfe_ctx* c, int64_t n, int bits, int* out_buf);
 // --- clusters (lfe_cluster.hip) ---
 int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, double* meats, int64_t* G_out);
+// multi-rank: per-cluster score rows S[G][k] (keys K[seg_off[h]], or K[h] with seg_off null) exchanged
+// to their owner ranks, merged by key; the k x k meat and the global cluster count
+int owner_meat(lfe_ctx* c, const uint64_t* K, const int32_t* seg_off, const double* S, int32_t G, int k,
+               uint64_t span, double* meat, int64_t* G_out);
 void free_cluster_ws(lfe_ctx* c);
 // --- segmented gather-sums (lfe_seg.hip) ---
 int seg_gather_sum(lfe_ctx* c, const int32_t* seg_off, int32_t G, int32_t* ufirst, int64_t n_pos,

@@ -22,6 +22,7 @@
 #include "lfe_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace lfe {
 
@@ -98,18 +99,20 @@ int reshard_owner(lfe_ctx* c, int fe, int32_t* lo_out, int32_t* hi_out) {
   std::vector<int64_t> rank_rows(world, 0);
   for (int r = 0; r < world; ++r)
     for (int g = bounds[r]; g < bounds[r + 1]; ++g) rank_rows[r] += hc[g];
+  // every refusal before the data moves is decided from the same all-reduced counts on every rank,
+  // so all ranks return the same code and keep their blocks (nothing has moved yet)
   for (int r = 0; r < world; ++r)
-    if (rank_rows[r] == 0) {  // every rank decides alike (same counts): nothing has moved yet
+    if (rank_rows[r] == 0) {
       set_error("owner re-shard: a rank would hold no rows (fewer populated levels than ranks)");
       return LFE_EINVAL;
     }
-  *lo_out = bounds[rank];
-  *hi_out = bounds[rank + 1];
-  if (world == 1) return LFE_OK;
-  if (rank_rows[rank] >= (int64_t)INT32_MAX) {
+  if (*std::max_element(rank_rows.begin(), rank_rows.end()) >= (int64_t)INT32_MAX) {
     set_error("owner re-shard: a rank would hold 2^31 rows or more");
     return LFE_EINVAL;
   }
+  *lo_out = bounds[rank];
+  *hi_out = bounds[rank + 1];
+  if (world == 1) return LFE_OK;
 
   // 2. destinations, stable sort by destination
   int32_t* dbounds = cnt + G;          // [world + 1]
@@ -142,16 +145,41 @@ int reshard_owner(lfe_ctx* c, int fe, int32_t* lo_out, int32_t* hi_out) {
   }
   const int64_t n_new = roff[world];
 
-  // 3. gather every column in destination order into staging (f64 columns, then int32 columns)
+  // 3. gather every column in destination order into staging (f64 columns, then int32 columns).
+  // The staging copy and the re-allocated shard coexist: every rank checks that both fit (the old
+  // shard's columns are freed in between) and the ranks agree on the outcome before anything moves,
+  // so a rank short of memory makes every rank return LFE_ENOMEM with its block in place.
   const int nf64 = p + (weighted ? 1 : 0), ni32 = F + m;
   const size_t ldn = (size_t)std::max<int64_t>(n, 1);
+  const size_t row_bytes = sizeof(double) * nf64 + sizeof(int32_t) * std::max(ni32, 1);
   double* sf = nullptr;
   int32_t* si = nullptr;
-  LFE_HIP(hipMalloc(reinterpret_cast<void**>(&sf), sizeof(double) * ldn * nf64));
-  if (hipMalloc(reinterpret_cast<void**>(&si), sizeof(int32_t) * ldn * std::max(ni32, 1)) != hipSuccess) {
-    (void)hipFree(sf);
-    set_error("owner re-shard: out of device memory for the staging buffer");
-    return LFE_ENOMEM;
+  int32_t short_mem = 0;
+  if (hipMalloc(reinterpret_cast<void**>(&sf), sizeof(double) * ldn * nf64) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&si), sizeof(int32_t) * ldn * std::max(ni32, 1)) != hipSuccess) {
+    short_mem = 1;
+  } else {
+    size_t free_b = 0, total_b = 0;
+    const size_t need = row_bytes * (size_t)std::max<int64_t>(n_new, 1), have_old = row_bytes * ldn;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b + have_old < need + ((size_t)256 << 20))
+      short_mem = 1;
+  }
+  (void)hipGetLastError();  // a failed allocation is decided below, with the other ranks
+  if (const char* e = getenv("LFE_TEST_RESHARD_SHORT_RANK"))  // tests: one rank short of memory
+    if (atoi(e) == rank) short_mem = 1;
+  {
+    int32_t* dflag = W.ocnt;  // [world * world] is free again after the counts above
+    LFE_TRY(h2d_small(c, dflag, &short_mem, sizeof(int32_t)));
+    LFE_TRY(allreduce_sum_i32(c, dflag, 1));
+    int32_t any_short = 0;
+    LFE_TRY(d2h_sync(c, &any_short, dflag, sizeof(int32_t)));
+    if (any_short) {
+      if (sf) (void)hipFree(sf);
+      if (si) (void)hipFree(si);
+      set_error("owner re-shard: a rank lacks device memory for the staging copy and the new shard "
+                "(every rank keeps its row block)");
+      return LFE_ENOMEM;
+    }
   }
   struct Staging {
     double* f;

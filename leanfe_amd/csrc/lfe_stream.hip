@@ -12,6 +12,10 @@
 //      added into the subset's table S[G][k] in chunk order - one add per cluster and chunk, so
 //      the sums do not depend on scheduling;
 //   3. lfe_stream_cluster_meats: S'S per subset (the table Gram of lfe_gram.hip) and the counts.
+//      A sharded engine (every rank streams its own rows; cluster codes are global) keeps each local
+//      cluster's intersection key, and the per-cluster sums go through the owner-partitioned exchange
+//      of the resident fits (owner_meat, lfe_cluster.hip): a cluster split across ranks is merged by
+//      its owner, and only the k x k meats and the cluster counts are all-reduced.
 #include "lfe_internal.h"
 
 #include <algorithm>
@@ -71,12 +75,21 @@ __global__ void k_scl_accum(const uint64_t* __restrict__ K, const int32_t* __res
   }
 }
 
+// the key of every local cluster (the first row of its sorted segment)
+__global__ void k_scl_ukey(const uint64_t* __restrict__ K, const int32_t* __restrict__ seg_off, int32_t G,
+                           uint64_t* __restrict__ ukey) {
+  for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < G; h += gridDim.x * blockDim.x) ukey[h] = K[seg_off[h]];
+}
+
 void free_stream_clusters(lfe_ctx* c) {
   auto& w = c->sw;
   for (auto& p : w.cid) dfree_any(p);
   for (auto& p : w.S) dfree_any(p);
+  for (auto& p : w.ukey) dfree_any(p);
   w.cid.clear();
   w.S.clear();
+  w.ukey.clear();
+  w.span.clear();
   w.S_cap.clear();
   w.G.clear();
   w.masks.clear();
@@ -130,19 +143,28 @@ int stream_clusters_prep(lfe_ctx* c, int n_subsets, const int32_t* masks) {
     w.cid.push_back(cid);
     w.masks.push_back(masks[s]);
     int32_t G = 0;
+    int buf = 0;
     if (n > 0) {
       {
         ProfScope _ps(c, K_CLUSTER_SORT);
         hipLaunchKernelGGL(k_scl_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka);
       }
       LFE_HIP(hipGetLastError());
-      int buf = 0;
       LFE_TRY(radix_sort(c, n, bit_length(span), &buf));
       LFE_TRY(group_sorted(c, n, span, W.keys[buf], W.rows[buf], nullptr, 0, &G));
       hipLaunchKernelGGL(k_scl_cid, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, W.keys[buf],
                          W.rows[buf], W.flag, n, span, cid);
       LFE_HIP(hipGetLastError());
     }
+    uint64_t* ukey = nullptr;
+    if (c->world > 1) {  // sharded: the owner exchange needs every local cluster's key
+      LFE_HIP(hipMalloc(reinterpret_cast<void**>(&ukey), sizeof(uint64_t) * (size_t)std::max(G, 1)));
+      if (G > 0)
+        hipLaunchKernelGGL(k_scl_ukey, dim3(grid_for(G)), dim3(kBlock), 0, c->stream, W.keys[buf], W.seg_off, G, ukey);
+      LFE_HIP(hipGetLastError());
+    }
+    w.ukey.push_back(ukey);
+    w.span.push_back(span);
     w.G.push_back(G);
     w.S.push_back(nullptr);
     w.S_cap.push_back(0);
@@ -182,6 +204,10 @@ int stream_cluster_meats(lfe_ctx* c, double* meats, int64_t* G_out) {
   for (size_t s = 0; s < w.cid.size(); ++s) {
     G_out[s] = w.G[s];
     double* meat = meats + s * (size_t)k * k;
+    if (c->world > 1) {  // every rank takes part, whatever its local cluster count
+      LFE_TRY(owner_meat(c, w.ukey[s], nullptr, w.S[s], w.G[s], k, w.span[s], meat, G_out + s));
+      continue;
+    }
     if (w.G[s] == 0 || k == 0) {
       std::fill(meat, meat + (size_t)k * k, 0.0);
       continue;

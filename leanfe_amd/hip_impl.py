@@ -42,9 +42,11 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     gets the global fit; FE/cluster columns must then be global int codes).
 
     ``out_of_core`` (data larger than HBM; default: env ``LEANFE_HIP_OUT_OF_CORE``): only the FE
-    codes are loaded; the columns are streamed in ``chunk_rows`` row chunks through the group
-    sums, (if needed) the design Gram and the residual pass.  Two FEs, no weights,
-    instruments, factors or clusters; IID or HC1."""
+    codes (and weights, cluster codes) are loaded; the columns [y] + x + instruments are streamed
+    in ``chunk_rows`` row chunks through the group sums, (if needed) the design Gram and the
+    residual pass.  Any number of FEs and regressors, weights, IV, IID / HC1 /
+    one-way and multi-way clustered SEs, one process or a sharded engine; factor and interaction
+    terms must be expanded into columns first."""
     t_start = time.perf_counter()
     say = (lambda *a: None) if quiet else print
     if formula is not None:
@@ -107,16 +109,15 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         if out_of_core is None:
             out_of_core = os.environ.get("LEANFE_HIP_OUT_OF_CORE", "0") == "1"
         if out_of_core:
-            if (not fe_cols or factor_vars or interactions or (sharded and v == "cluster")
-                    or strategy not in ("auto", "alt_proj", "demean")):
-                raise ValueError("out_of_core fits take one or more FEs, no factor / interaction terms, "
-                                 "strategy 'alt_proj' (or 'demean' for one FE), and clustered SEs in one process")
+            if not fe_cols or factor_vars or interactions or strategy not in ("auto", "alt_proj", "demean"):
+                raise ValueError("out_of_core fits take one or more FEs, no factor / interaction terms, and "
+                                 "strategy 'alt_proj' (or 'demean' for one FE)")
             source = data if stream else cols
             n_rows_oc = n_rows if stream else len(cols[y_col])
             w_oc = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
             return _out_of_core_fit(eng, source, cols, n_rows_oc, y_col, x_cols, instruments, fe_cols, codes, levels,
                                     w_oc, cluster_cols, v, vcov, ssc, demean_tol, max_iter, int(chunk_rows),
-                                    formula, t_start, say)
+                                    formula, t_start, say, sharded)
         w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
         # polars_impl.py:180: an all-ones instrument stops 2SLS from adding an intercept to Z.
         # Demeaned instruments cannot be all ones; without FEs they are the raw columns.
@@ -148,7 +149,10 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                 cl_loaded = _load_clusters(eng, cols, cluster_cols, sharded)
             try:
                 eng.reshard_owner(max(range(2), key=lambda f: levels[f]))
-            except ValueError:  # a rank would hold no rows: every rank keeps its block (nothing moved)
+            except (ValueError, MemoryError):
+                # refused before any row moved, by a decision every rank takes alike from all-reduced
+                # counts / memory flags (a rank would hold no rows or 2^31+ rows, or lacks device
+                # memory for the staging copy): every rank keeps its contiguous block
                 pass
         t_load = time.perf_counter() - t0
         n_obs, fe_dims, fe_card = eng.drop_singletons()
@@ -267,7 +271,8 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
 
 
 def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_cols, codes, levels, w, cluster_cols,
-                     v, vcov, ssc, demean_tol, max_iter, chunk_rows, formula, t_start, say) -> LeanFEResult:
+                     v, vcov, ssc, demean_tol, max_iter, chunk_rows, formula, t_start, say,
+                     sharded=False) -> LeanFEResult:
     """Out-of-core X (data larger than HBM): the FE codes (and weights, cluster codes) and their
     layouts stay on the GPU, the columns [y] + x (+ instruments) are streamed from host memory (or a
     Parquet file, re-read per pass) in row chunks through pass 1 (group sums S_f, W_f,
@@ -275,7 +280,9 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
     tables (pass 3, the explicit design Gram of sqrt(w) [1, y~, x~], when that is unavailable),
     the host solve (:212-226; 2SLS for instruments, common.py:188-240) and pass 2 / 4 (residual,
     RSS, the HC1 meat and the cluster scores, :229, std_errors.py:183-602).  Same estimator, same
-    stop rule and iterations as the resident fit."""
+    stop rule and iterations as the resident fit.  A sharded engine streams this rank's rows; the
+    group sums, Gram tiles and SE statistics are all-reduced, and the per-cluster score sums go to
+    their owner ranks (lfe_stream.hip), so cluster columns must hold global codes."""
     from leanfe_amd._lib import NeedsStreamPass
 
     num_cols = [y_col] + list(x_cols) + list(instruments)
@@ -294,7 +301,7 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
     eng.load_codes(codes, levels, p, weights=w)  # a sharded engine: this rank's rows (global codes)
     subsets = None
     if v == "cluster":
-        _load_clusters(eng, cols, cluster_cols, False)
+        _load_clusters(eng, cols, cluster_cols, sharded)
         subsets = inference.cluster_subsets(len(cluster_cols))
     t_load = time.perf_counter() - t0
     n_obs, fe_dims, fe_card = eng.drop_singletons()

@@ -86,8 +86,11 @@ def test_dense_with_singletons_and_ragged_bucket(monkeypatch):
 
 
 def test_dense_counts_beyond_8_bits(monkeypatch):
-    """(h, q) pairs with hundreds of rows: the 8-bit counters of the build overflow and the chunk is
-    counted again on 16-bit counters."""
+    """(h, q) pairs with ~50K rows: on the 8-bit counters of the build (forced with LFE_DN_C8=1: at
+    1,000 primary levels the build would otherwise pick 16-bit chunks, since 8-bit ones would leave
+    CUs idle) these pairs overflow, and the chunk is counted again on 16-bit counters.  A wrapped
+    count would move beta far from the oracle; the recounted table gives the same bits as the build
+    that starts on 16-bit counters, and agrees with the row layouts (LFE_DENSE=0) at 1e-13."""
     rng = np.random.default_rng(11)
     n, k = 400_000, 3
     fe1 = rng.integers(0, 1_000, n).astype(np.int32)
@@ -103,10 +106,18 @@ def test_dense_counts_beyond_8_bits(monkeypatch):
     xs = ["x1", "x2", "x3"]
     o = _oracle(data, xs)
     monkeypatch.setenv("LFE_DENSE", "1")
-    dense = _fit(data, xs)
-    _check(dense, o)
+    monkeypatch.setenv("LFE_DN_C8", "1")
+    dense8 = _fit(data, xs)
+    _check(dense8, o)
+    monkeypatch.setenv("LFE_DN_C8", "0")
+    dense16 = _fit(data, xs)
+    np.testing.assert_array_equal(dense8[0], dense16[0])
+    np.testing.assert_array_equal(dense8[1], dense16[1])
+    monkeypatch.delenv("LFE_DN_C8")
     monkeypatch.setenv("LFE_DENSE", "0")
-    _check(_fit(data, xs), o)
+    rows = _fit(data, xs)
+    _check(rows, o)
+    np.testing.assert_allclose(dense8[0], rows[0], rtol=1e-13, atol=0)
 
 
 def test_dense_owner_shard_matches_whole_panel(monkeypatch):

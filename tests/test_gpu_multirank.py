@@ -338,25 +338,21 @@ def test_emulated_contiguous_blocks_reshard_to_owners(world, n, k, levels, vcov,
             np.testing.assert_array_equal([res.std_errors[x] for x in xs], [other.std_errors[x] for x in xs])
 
 
-@pytest.mark.parametrize("world,n,k,levels,vcov,weighted", [
-    (2, 300_001, 4, [12_000, 300], "HC1", False),        # two FEs: the fast sweeps on streamed codes
-    (3, 240_000, 3, [9_000, 800, 120], "iid", True),      # three FEs, weighted: the general sweeps
-])
-def test_emulated_out_of_core_ranks_match_oracle(world, n, k, levels, vcov, weighted, monkeypatch):
-    """Out-of-core fits on a sharded engine: every rank streams the columns of its
-    own contiguous row block; the streamed group sums and every pass's tile are summed over the ranks
-    (the design Gram streams: the ranks' raw tiles have their own shifts).  Every rank returns the
-    oracle's whole-panel fit, bit-identical across ranks."""
+def test_reshard_memory_refusal_is_decided_by_every_rank(monkeypatch):
+    """a re-shard refusal on one rank (here: rank 1 "short of device memory" for the
+    staging copy, LFE_TEST_RESHARD_SHORT_RANK) must be an all-rank decision taken before any row
+    moves - every rank returns LFE_ENOMEM, keeps its contiguous block and the fit goes on with the
+    row-block schedule, equal to the oracle and bit-identical across ranks (no rank is left inside a
+    collective the others skipped)."""
     from leanfe_amd import dist, leanfe_hip
     from leanfe_amd._lib import EmuGroup, Engine
     from oracle import altproj
 
-    full = dict(synth.panel(n, k, levels, seed=29))
-    if weighted:
-        full["w"] = np.random.default_rng(30).uniform(0.5, 2.0, n)
+    world, n, k, levels = 3, 240_000, 3, [15_000, 400]
+    full = dict(synth.panel(n, k, levels, seed=31))
     xs = [f"x{j + 1}" for j in range(k)]
-    fes = [f"fe{f + 1}" for f in range(len(levels))]
     monkeypatch.setattr(dist, "agree_levels", lambda eng, lv: [max(a, b) for a, b in zip(lv, levels)])
+    monkeypatch.setenv("LFE_TEST_RESHARD_SHORT_RANK", "1")
     group = EmuGroup(world)
     out, errs = {}, {}
 
@@ -367,9 +363,9 @@ def test_emulated_out_of_core_ranks_match_oracle(world, n, k, levels, vcov, weig
             eng.set_emu(group, rank)
             eng.dist_group = ("emulated",)
             shard = {c: np.asarray(v)[lo:hi] for c, v in full.items()}
-            out[rank] = leanfe_hip(shard, y_col="y", x_cols=xs, fe_cols=fes, vcov=vcov, strategy="alt_proj",
-                                   weights="w" if weighted else None, quiet=True, engine=eng, out_of_core=True,
-                                   chunk_rows=40_000 + 7_777 * rank)
+            r = leanfe_hip(shard, y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], vcov="HC1", strategy="alt_proj",
+                           quiet=True, engine=eng)
+            out[rank] = dict(res=r, rows=eng.n, owner=eng.owner)
             eng.close()
         except BaseException as e:  # noqa: BLE001
             errs[rank] = e
@@ -382,7 +378,69 @@ def test_emulated_out_of_core_ranks_match_oracle(world, n, k, levels, vcov, weig
     assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
     if errs:
         raise next(iter(errs.values()))
-    o = altproj.fit(full, "y", xs, fes, vcov=vcov, weights="w" if weighted else None)
+    o = altproj.fit(full, "y", xs, ["fe1", "fe2"], vcov="HC1")
+    for r in range(world):
+        lo, hi = shard_range(n, r, world)
+        assert out[r]["rows"] == hi - lo and out[r]["owner"] is None  # every rank kept its block
+        res = out[r]["res"]
+        assert res.iterations == o["iterations"] and res.n_obs == o["n_obs"]
+        np.testing.assert_allclose([res.coefs[x] for x in xs], o["beta"], rtol=1e-10, atol=0)
+        np.testing.assert_allclose([res.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
+        np.testing.assert_array_equal([res.coefs[x] for x in xs], [out[0]["res"].coefs[x] for x in xs])
+
+
+@pytest.mark.parametrize("world,n,k,levels,vcov,weighted,cl", [
+    (2, 300_001, 4, [12_000, 300], "HC1", False, None),          # two FEs: the fast sweeps on streamed codes
+    (3, 240_000, 3, [9_000, 800, 120], "iid", True, None),        # three FEs, weighted: the general sweeps
+    (2, 300_001, 4, [12_000, 300], "cluster", False, ["fe2"]),    # one-way clustered: owner exchange of scores
+    (4, 320_000, 3, [9_000, 800, 150], "cluster", False, ["fe2", "fe3"]),  # CGM, 4 ranks
+    (2, 200_000, 20, [6_000, 500, 90], "cluster", False, ["fe1", "fe2"]),  # k = 20: the wide MFMA passes
+    (3, 210_000, 14, [7_000, 400], "HC1", True, None),            # k = 14, weighted
+])
+def test_emulated_out_of_core_ranks_match_oracle(world, n, k, levels, vcov, weighted, cl, monkeypatch):
+    """Out-of-core fits on a sharded engine: every rank streams the columns of
+    its own contiguous row block; the streamed group sums and every pass's tile are summed over the
+    ranks (the design Gram streams: the ranks' raw tiles have their own shifts), and the clustered
+    fits' per-cluster score sums go to their owner ranks (lfe_stream.hip, std_errors.py:289-441).
+    Every rank returns the oracle's whole-panel fit, bit-identical across ranks."""
+    from leanfe_amd import dist, leanfe_hip
+    from leanfe_amd._lib import EmuGroup, Engine
+    from oracle import altproj
+
+    full = dict(synth.panel(n, k, levels, seed=29))
+    if weighted:
+        full["w"] = np.random.default_rng(30).uniform(0.5, 2.0, n)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    known = sorted(levels)
+    # global level counts: a shard's local max code + 1 rounds up to the panel's (FE and cluster columns)
+    monkeypatch.setattr(dist, "agree_levels", lambda eng, lv: [min(g for g in known if g >= x) for x in lv])
+    group = EmuGroup(world)
+    out, errs = {}, {}
+
+    def worker(rank):
+        try:
+            lo, hi = shard_range(n, rank, world)
+            eng = Engine(0)
+            eng.set_emu(group, rank)
+            eng.dist_group = ("emulated",)
+            shard = {c: np.asarray(v)[lo:hi] for c, v in full.items()}
+            out[rank] = leanfe_hip(shard, y_col="y", x_cols=xs, fe_cols=fes, vcov=vcov, strategy="alt_proj",
+                                   cluster_cols=cl, weights="w" if weighted else None, quiet=True, engine=eng,
+                                   out_of_core=True, chunk_rows=40_000 + 7_777 * rank)
+            eng.close()
+        except BaseException as e:  # noqa: BLE001
+            errs[rank] = e
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+    if errs:
+        raise next(iter(errs.values()))
+    o = altproj.fit(full, "y", xs, fes, vcov=vcov, cluster_cols=cl, weights="w" if weighted else None)
     for r in range(world):
         res = out[r]
         assert res.iterations == o["iterations"] and res.n_obs == o["n_obs"] and res.df_resid == o["df_resid"]
@@ -390,6 +448,10 @@ def test_emulated_out_of_core_ranks_match_oracle(world, n, k, levels, vcov, weig
         np.testing.assert_allclose([res.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
         np.testing.assert_array_equal([res.coefs[x] for x in xs], [out[0].coefs[x] for x in xs])
         np.testing.assert_array_equal([res.std_errors[x] for x in xs], [out[0].std_errors[x] for x in xs])
+        if cl is not None:
+            got, want = res.n_clusters, o["n_clusters"]
+            assert (tuple(got) if isinstance(got, (tuple, list)) else got) == (
+                tuple(want) if isinstance(want, (tuple, list)) else want)
 
 
 @pytest.mark.parametrize("rank", [0, 7])

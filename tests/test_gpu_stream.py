@@ -144,6 +144,15 @@ GENERAL = [
     ("fe1_demean", 300_000, 3, [5_000], "HC1", None, False, False, 64_000),
     ("iv_hc1", 300_000, 2, [8_000, 200], "HC1", None, False, True, 100_000),
     ("iv_cl2_weighted", 300_000, 2, [8_000, 200, 500], "cluster", ["fe2", "fe3"], True, True, 70_000),
+    # wider than the row-per-lane passes (p > 11): the MFMA passes of k_stream_wide,
+    # the column groups of k_stream_sums, the design Gram streamed (no raw tile past one 16-column group)
+    ("k20_iid", 300_000, 20, [9_000, 2_000, 500], "iid", None, False, False, 90_000),
+    ("k20_hc1_fe2", 300_001, 20, [9_000, 2_000], "HC1", None, False, False, 100_000),
+    ("k20_cgm", 300_000, 20, [9_000, 2_000, 500], "cluster", ["fe1", "fe2"], False, False, 80_000),
+    ("k14_weighted_cl1", 250_000, 14, [7_000, 300], "cluster", ["fe2"], True, False, 64_000),
+    ("k40_hc1", 200_000, 40, [5_000, 300], "HC1", None, False, False, 70_000),
+    ("iv_k8_hc1", 250_000, 8, [8_000, 200], "HC1", None, False, True, 90_000),
+    ("iv_k8_cl1_weighted", 250_000, 8, [8_000, 200], "cluster", ["fe2"], True, True, 60_000),
 ]
 
 
@@ -185,3 +194,23 @@ def test_streamed_general_fits_match_oracle(name, n, k, L, vcov, cl, weighted, i
              leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, chunk_rows=chunk, **kw))
     np.testing.assert_array_equal([again.coefs[x] for x in xs], b0)
     np.testing.assert_array_equal([again.std_errors[x] for x in xs], s0)
+
+
+def test_stream_clusters_refused_while_a_pass_is_open():
+    """C-API misuse: lfe_stream_clusters inside an open streamed pass would rebuild the
+    cluster ids under the pass and leave its score tables unallocated; it returns LFE_ESTATE, and the
+    fit continues normally once the pass is closed."""
+    from leanfe_amd._lib import Engine
+    n, k, L = 50_000, 2, [2_000, 50]
+    d = synth.panel(n, k, L, seed=3)
+    cols = [np.asarray(d[c]) for c in ("y", "x1", "x2")]
+    with Engine(0) as eng:
+        eng.load_codes([d["fe1"], d["fe2"]], L, k + 1)
+        eng.load_clusters([np.asarray(d["fe2"])], [L[1]])
+        eng.drop_singletons()
+        eng.stream_begin(1)
+        with pytest.raises(RuntimeError, match="pass is open"):
+            eng.stream_clusters([1])
+        eng.stream_rows(0, cols)
+        eng.stream_end()
+        eng.stream_clusters([1])  # allowed between passes

@@ -29,8 +29,14 @@ def rel(a, b) -> float:
     return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300))) if a.size else 0.0
 
 
-def run(cfg: int, rows: int | None = None, repeat: int = 2) -> dict:
-    a = bench.parse(["--config", str(cfg)] + (["--rows", str(rows)] if rows else []))
+def _args(cfg, rows):
+    """A BASELINE config number or the name of one of the reference's panels (bench.PRESETS)."""
+    sel = ["--preset", cfg] if isinstance(cfg, str) else ["--config", str(cfg)]
+    return bench.parse(sel + (["--rows", str(rows)] if rows else []))
+
+
+def run(cfg: int | str, rows: int | None = None, repeat: int = 2) -> dict:
+    a = _args(cfg, rows)
     eng = Engine(0)
     eng.synth_load(a.rows, a.k, a.levels, synth.betas(a.k), seed=a.seed)
     n_cl = len(a.cl) if a.cl else 0
@@ -91,7 +97,7 @@ def run_multirank(cfg: int, combos=(("owner", 2), ("owner", 4), ("owner", 8)), r
     from leanfe_amd import dist
     from leanfe_amd._lib import EmuGroup
 
-    a = bench.parse(["--config", str(cfg)] + (["--rows", str(rows)] if rows else []))
+    a = _args(cfg, rows)
     n_cl = len(a.cl) if a.cl else 0
     eng = Engine(0)
     eng.synth_load(a.rows, a.k, a.levels, synth.betas(a.k), seed=a.seed)
@@ -163,12 +169,12 @@ def run_multirank(cfg: int, combos=(("owner", 2), ("owner", 4), ("owner", 8)), r
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="1,2,3,4")
+    ap.add_argument("--configs", default="1,2,3,4", help="config numbers and / or bench.PRESETS names")
     ap.add_argument("--rows", type=int, default=None, help="override the config's row count")
     ap.add_argument("--worlds", default=None, help="emulated multi-rank groups instead, e.g. 2,4,8")
     ap.add_argument("--shards", default="owner", help="owner and/or rows")
     a = ap.parse_args()
-    for c in [int(x) for x in a.configs.split(",")]:
+    for c in [int(x) if x.isdigit() else x for x in a.configs.split(",")]:
         if a.worlds:
             run_multirank(c, [(sh, int(w)) for sh in a.shards.split(",") for w in a.worlds.split(",")], a.rows)
         else:
