@@ -360,11 +360,12 @@ def yoco_reference(compress, orc, xs, fes, vcov, cl, ssc=True):
     return np.asarray(beta[1:k_x]), np.asarray(se[1:]), ncl, df_resid, float(rss_total)
 
 
-def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=None, wls_beta=None):
+def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=None, wls_beta=None,
+          ssc=True):
     arrays = {f"in_{c}": np.asarray(v) for c, v in data.items()}
     meta = dict(name=name, y=y, xs=xs, fes=fes, strategy=strategy, weights=weights, vcov=vcov,
                 instruments=instruments or [],
-                cluster_cols=cl, demean_tol=1e-6, max_iter=50, ssc=True,
+                cluster_cols=cl, demean_tol=1e-6, max_iter=50, ssc=bool(ssc),
                 oracle_n_clusters=orc["n_clusters"], ref_n_clusters=ref[2] if ref else None,
                 pinned=(("reference-iv" if instruments else "reference-lsdv") if ref else
                         "reference-wls-beta" if wls_beta is not None else "oracle-only"))
@@ -385,6 +386,56 @@ def _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, 
 
 def _json_ncl(v):
     return list(v) if isinstance(v, tuple) else v
+
+
+# ssc=False (std_errors.py:339-342 one-way G/(G-1) only; :434-436 no (n-1)/df_resid after the
+# G_min rule): pinned to the reference's compute_se_compress / _compute_se_cluster_*_iv with
+# apply_small_sample_correction / ssc False, whose adjustments are the same expressions
+NOSSC = [
+    ("panel_cl1_nossc", lambda: fx_panel(seed=13), "y", ["x1", "x2", "x3"], ["fe1", "fe2"], "alt_proj", None,
+     "cluster", ["cl1"]),
+    ("panel_cl2_nossc", lambda: fx_panel(seed=15), "y", ["x1", "x2", "x3"], ["fe1", "fe2"], "alt_proj", None,
+     "cluster", ["cl1", "cl2"]),
+    ("xlang_cl2_nossc", fx_xlang, "y", ["x1", "x2", "treatment"], ["fe1", "fe2"], "alt_proj", None, "cluster",
+     ["cluster", "fe2"]),
+]
+NOSSC_IV = [
+    ("iv_cl1_nossc", lambda: fx_iv(seed=27), "y", ["x1", "x2"], ["fe1", "fe2"], "alt_proj", None, "cluster", ["cl1"],
+     ["z1", "x2"]),
+    ("iv_cl2_nossc", lambda: fx_iv(seed=29), "y", ["x1", "x2"], ["fe1", "fe2"], "alt_proj", None, "cluster",
+     ["cl1", "cl2"], ["z1", "x2"]),
+]
+
+
+def main_nossc():
+    compress, std_errors, common = load_reference()
+    for name, recipe, y, xs, fes, strategy, weights, vcov, cl in NOSSC:
+        data = recipe()
+        orc = altproj.fit(data, y, xs, fes, strategy=strategy, vcov=vcov, cluster_cols=cl, ssc=False)
+        tight = altproj.fit(data, y, xs, fes, strategy=strategy, vcov=vcov, cluster_cols=cl, ssc=False,
+                            demean_tol=1e-14, max_iter=100000)
+        ref = lsdv_reference(compress, data, y, xs, fes, orc["keep"], vcov, cl, False, orc["n_obs"], orc["df_resid"])
+        rb = np.max(np.abs(tight["beta"] - ref[0]) / np.maximum(np.abs(ref[0]), 1e-300))
+        rs = np.max(np.abs(tight["se"] - ref[1]) / np.maximum(np.abs(ref[1]), 1e-300))
+        assert rb < 1e-9 and rs < 1e-9, (name, rb, rs)
+        assert _json_ncl(ref[2]) == _json_ncl(orc["n_clusters"]), (name, ref[2], orc["n_clusters"])
+        with_ssc = altproj.fit(data, y, xs, fes, strategy=strategy, vcov=vcov, cluster_cols=cl, ssc=True)
+        assert not np.allclose(with_ssc["se"], orc["se"], rtol=1e-6), name  # the flag changes the SEs
+        print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} tight-vs-ref beta {rb:.1e} se {rs:.1e}")
+        _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, ssc=False)
+    for name, recipe, y, xs, fes, strategy, weights, vcov, cl, inst in NOSSC_IV:
+        data = recipe()
+        orc = altproj.fit(data, y, xs, fes, strategy=strategy, vcov=vcov, cluster_cols=cl, instruments=inst,
+                          ssc=False)
+        tight = altproj.fit(data, y, xs, fes, strategy=strategy, vcov=vcov, cluster_cols=cl, instruments=inst,
+                            ssc=False, demean_tol=1e-14, max_iter=100000)
+        ref = iv_reference(std_errors, common, orc, data, weights, vcov, cl, ssc=False)
+        rb = np.max(np.abs(orc["beta"] - ref[0]) / np.abs(ref[0]))
+        rs = np.max(np.abs(orc["se"] - ref[1]) / np.abs(ref[1]))
+        assert rb < 1e-11 and rs < 1e-11, (name, rb, rs)
+        assert _json_ncl(ref[2]) == _json_ncl(orc["n_clusters"]), (name, ref[2], orc["n_clusters"])
+        print(f"{name:18s} it={orc['iterations']:3d} n={orc['n_obs']:6d} oracle-vs-ref IV beta {rb:.1e} se {rs:.1e}")
+        _pack(name, data, y, xs, fes, strategy, weights, vcov, cl, ref, orc, tight, instruments=inst, ssc=False)
 
 
 def main(only_weighted=False):
@@ -467,4 +518,8 @@ def main(only_weighted=False):
 
 
 if __name__ == "__main__":
-    main(only_weighted="--weighted-only" in sys.argv)
+    if "--nossc-only" in sys.argv:
+        main_nossc()
+    else:
+        main(only_weighted="--weighted-only" in sys.argv)
+        main_nossc()
