@@ -128,6 +128,8 @@ int ensure_i32(lfe_ctx*, int32_t*& p, size_t& cap, size_t elems) { return ensure
 int ensure_f64(lfe_ctx*, double*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 int ensure_u16(lfe_ctx*, uint16_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 int ensure_u64(lfe_ctx*, uint64_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
+int ensure_i8(lfe_ctx*, int8_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
+int ensure_u8(lfe_ctx*, uint8_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 
 struct ZeroArgs {
   uint32_t* p[32];
@@ -425,6 +427,14 @@ static void free_data(lfe_ctx* c) {
   dfree(c->dn_na);
   dfree(c->dn_nb);
   c->dn_na_cap = c->dn_nb_cap = 0;
+  dfree(c->dn8_a);
+  dfree(c->dn8_b);
+  dfree(c->dn8_fa);
+  dfree(c->dn8_fb);
+  dfree(c->dn8_dq);
+  dfree(c->dn8_eq);
+  c->dn8_a_cap = c->dn8_b_cap = c->dn8_fa_cap = c->dn8_fb_cap = c->dn8_dq_cap = c->dn8_eq_cap = 0;
+  c->dn8 = false;
   dfree(c->raw_slots);
   c->raw_slots_cap = 0;
   dfree(c->amax);

@@ -20,6 +20,17 @@
 // Every T entry is a fixed sequence of MFMAs and fixed-order adds: the bits repeat run to run.
 // T_Q,b goes to the same per-bucket slots (tq_runs) as K2 of lfe_iter.hip, so the bucket
 // reduction, the Q projection, the stop test and the multi-rank all-reduce are shared.
+//
+// Exact integer form ("dn8", the default where it fits).  The f64 MFMA is 64 cycles per 16x16x4
+// product; v_mfma_i32_16x16x64_i8 is 16 cycles per 16x16x64, 16x the MACs per cycle, and sums
+// exactly in int32.  The counts are small integers (i8 when <= 127) and the other FE's effects
+// are cut into exact integer digits: per tile of 512 k rows and per column, with 2^e > max |alpha|,
+//     round(alpha 2^(54 - e)) = sum_{d < 8} digit_d 128^d,   digit_d in [-64, 63]
+// so T = sum_d (N digit_d) 128^d 2^(e - 54) with every N digit_d product summed exactly on the
+// matrix cores and one f64 conversion per tile - the effects rounded to 2^-54 of the tile's largest,
+// below the f64 rounding of a sum of them.  The i8 tables hold 1 byte per cell (half the u16 tables'
+// traffic per pass) in MFMA fragment order; a 16 x 64 block with a cell over 127 is flagged and
+// zero in the i8 table, and its u16 counts (NA / NB storage) are summed in f64 by the pass.
 #include "lfe_internal.h"
 
 #include <algorithm>
@@ -41,8 +52,15 @@ struct DnBuildArgs {
   const int32_t* codeP;   // layout order; -1: a dropped row
   const int32_t* codeQ;
   int nbe, s, B, GQ16, nch;
-  uint16_t* NA;
+  int GQW;                // LDS counter row width (GQ16, or GQ64 for the i8 tables)
+  uint16_t* NA;           // u16 tables (dn8: the counts of flagged blocks only, 16 x 64 natural order)
   uint16_t* NB;
+  // dn8: i8 fragment tables and per-block flags
+  int dn8, GQ64, fa_stride, fb_stride;
+  int8_t* NA8;            // [bi][hb][q kb] 1 KB: lane (g, i) bytes jj = count (16 hb + i, 64 kb + 16 g + jj)
+  int8_t* NB8;            // [bi][qb][h kb] 1 KB: lane (g, i) bytes jj = count (64 kb + 16 g + jj, 16 qb + i)
+  uint8_t* FA;            // [bi][hb][fa_stride]: block has a count > 127
+  uint8_t* FB;            // [bi][qb][fb_stride]
 };
 
 // Counts of the bucket's kept rows with h in [hlo, hlo + HW) into LDS counters of CT (8 or 16
@@ -50,7 +68,7 @@ struct DnBuildArgs {
 template <typename CT>
 __device__ bool dn_count(const DnBuildArgs& a, uint32_t* cw, int hlo, int HW, int r0, int r1) {
   constexpr int PER = 4 / sizeof(CT), SH = 8 * sizeof(CT);
-  const int W = a.GQ16 / PER;  // words per group row
+  const int W = a.GQW / PER;  // words per group row
   __shared__ int ovf;
   for (int j = threadIdx.x; j < HW * W; j += blockDim.x) cw[j] = 0u;
   if (threadIdx.x == 0) ovf = 0;
@@ -101,14 +119,94 @@ __device__ void dn_write(const DnBuildArgs& a, const CT* cnt, int bi, int hb0, i
   us4* na = reinterpret_cast<us4*>(a.NA + (int64_t)bi * nhb * nqb * 256);
   for (int e = threadIdx.x; e < nel4; e += blockDim.x) {  // NA blocks (hb, qb): rows h, 4 q's per store
     const int blk = e >> 6, el = (e & 63) * 4, hbl = blk / nqb, qb = blk - hbl * nqb;
-    const CT* src = cnt + (hbl * 16 + (el >> 4)) * a.GQ16 + qb * 16 + (el & 15);
+    const CT* src = cnt + (hbl * 16 + (el >> 4)) * a.GQW + qb * 16 + (el & 15);
     na[((int64_t)(hb0 + hbl) * nqb + qb) * 64 + (e & 63)] = us4{src[0], src[1], src[2], src[3]};
   }
   us4* nbp = reinterpret_cast<us4*>(a.NB + (int64_t)bi * nqb * nhb * 256);
   for (int e = threadIdx.x; e < nel4; e += blockDim.x) {  // NB blocks (qb, hb): rows q, 4 h's per store
     const int blk = e >> 6, el = (e & 63) * 4, qb = blk / hbl_n, hbl = blk - qb * hbl_n;
-    const CT* src = cnt + (hbl * 16 + (el & 15)) * a.GQ16 + qb * 16 + (el >> 4);
-    nbp[((int64_t)qb * nhb + hb0 + hbl) * 64 + (e & 63)] = us4{src[0], src[a.GQ16], src[2 * a.GQ16], src[3 * a.GQ16]};
+    const CT* src = cnt + (hbl * 16 + (el & 15)) * a.GQW + qb * 16 + (el >> 4);
+    nbp[((int64_t)qb * nhb + hb0 + hbl) * 64 + (e & 63)] = us4{src[0], src[a.GQW], src[2 * a.GQW], src[3 * a.GQW]};
+  }
+}
+
+// dn8: the i8 fragment blocks of the primary rows [hb0 16, hb0 16 + HW) (HW = 64 or 128: whole
+// 64-row h k-blocks) from the LDS counters.  Every fragment is written as its counts' low bytes in
+// one pass (an NA8 fragment is 16 contiguous counters, an NB8 fragment 16 counters a row apart);
+// a block holding a count over 127 is flagged, then (rare) zeroed in the i8 table and stored as u16
+// (16 x 64, natural order) in NA / NB.
+template <typename CT>
+__device__ void dn_write8(const DnBuildArgs& a, const CT* cnt, int bi, int hb0, int HW) {
+  __shared__ int ov[1024];
+  typedef int v4 __attribute__((ext_vector_type(4)));
+  const int nkq = a.GQ64 >> 6, nhb = a.B >> 4, nqb = a.GQ64 >> 4, nhk = a.B >> 6;
+  const int hbl_n = HW >> 4, hkl_n = HW >> 6, hk0 = hb0 >> 2;
+  const int na_b = hbl_n * nkq, nb_b = nqb * hkl_n;
+  for (int j = threadIdx.x; j < na_b + nb_b; j += blockDim.x) ov[j] = 0;
+  __syncthreads();
+  for (int e = threadIdx.x; e < na_b * 64; e += blockDim.x) {
+    const int blk = e >> 6, l = e & 63, hbl = blk / nkq, kb = blk - hbl * nkq;
+    const CT* src = cnt + (hbl * 16 + (l & 15)) * a.GQW + kb * 64 + 16 * (l >> 4);
+    v4 w;
+    bool big;
+    if (sizeof(CT) == 1) {  // 16 byte counters: one 16-byte LDS read, a byte over 127 has its top bit
+      w = *reinterpret_cast<const v4*>(src);
+      big = ((w.x | w.y | w.z | w.w) & 0x80808080) != 0;
+    } else {
+      const v4 u0 = reinterpret_cast<const v4*>(src)[0], u1 = reinterpret_cast<const v4*>(src)[1];
+      const int hi = (u0.x | u0.y | u0.z | u0.w | u1.x | u1.y | u1.z | u1.w) & (int)0xff80ff80;
+      big = hi != 0;
+      // two u16 counters per word -> their low bytes, four per word
+      auto pk = [](int x, int y) {
+        const uint32_t ux = (uint32_t)x, uy = (uint32_t)y;
+        return (int)((ux & 0xffu) | ((ux >> 8) & 0xff00u) | ((uy & 0xffu) << 16) | ((uy << 8) & 0xff000000u));
+      };
+      w = v4{pk(u0.x, u0.y), pk(u0.z, u0.w), pk(u1.x, u1.y), pk(u1.z, u1.w)};
+    }
+    if (big) ov[blk] = 1;
+    *reinterpret_cast<v4*>(a.NA8 + (((int64_t)bi * nhb + hb0 + hbl) * nkq + kb) * 1024 + l * 16) = w;
+  }
+  for (int e = threadIdx.x; e < nb_b * 64; e += blockDim.x) {
+    const int blk = e >> 6, l = e & 63, qb = blk / hkl_n, hkl = blk - qb * hkl_n;
+    const CT* src = cnt + (hkl * 64 + 16 * (l >> 4)) * a.GQW + qb * 16 + (l & 15);
+    v4 w = v4{0, 0, 0, 0};
+    int m = 0;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int v = (int)src[jj * a.GQW];
+      m |= v;
+      w[jj >> 2] |= (v & 0xff) << (8 * (jj & 3));
+    }
+    if (m & ~127) ov[na_b + blk] = 1;
+    *reinterpret_cast<v4*>(a.NB8 + (((int64_t)bi * nqb + qb) * nhk + hk0 + hkl) * 1024 + l * 16) = w;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < na_b; j += blockDim.x) {
+    const int hbl = j / nkq, kb = j - hbl * nkq;
+    a.FA[((int64_t)bi * nhb + hb0 + hbl) * a.fa_stride + kb] = (uint8_t)ov[j];
+  }
+  for (int j = threadIdx.x; j < nb_b; j += blockDim.x) {
+    const int qb = j / hkl_n, hkl = j - qb * hkl_n;
+    a.FB[((int64_t)bi * nqb + qb) * a.fb_stride + hk0 + hkl] = (uint8_t)ov[na_b + j];
+  }
+  // the flagged blocks (rare: a (h, q) pair with more than 127 kept rows): i8 block zeroed, counts as u16
+  for (int blk = 0; blk < na_b + nb_b; ++blk) {
+    if (!ov[blk]) continue;  // uniform (LDS)
+    if (blk < na_b) {
+      const int hbl = blk / nkq, kb = blk - hbl * nkq;
+      const int64_t bo = (((int64_t)bi * nhb + hb0 + hbl) * nkq + kb) * 1024;
+      for (int t = threadIdx.x; t < 1024; t += blockDim.x) {
+        a.NA[bo + t] = (uint16_t)cnt[(hbl * 16 + (t >> 6)) * a.GQW + kb * 64 + (t & 63)];
+        a.NA8[bo + t] = 0;
+      }
+    } else {
+      const int qb = (blk - na_b) / hkl_n, hkl = (blk - na_b) - qb * hkl_n;
+      const int64_t bo = (((int64_t)bi * nqb + qb) * nhk + hk0 + hkl) * 1024;
+      for (int t = threadIdx.x; t < 1024; t += blockDim.x) {
+        a.NB[bo + t] = (uint16_t)cnt[(hkl * 64 + (t & 63)) * a.GQW + qb * 16 + (t >> 6)];
+        a.NB8[bo + t] = 0;
+      }
+    }
   }
 }
 
@@ -128,18 +226,21 @@ __global__ __launch_bounds__(1024) void k_dn_build(DnBuildArgs a) {
   const int HC = a.B / a.nch, hlo = (b << a.s) + chunk * HC, hb0 = chunk * (HC / 16);
   if (HC == 2 * kDnHC) {
     if (!dn_count<uint8_t>(a, cw, hlo, HC, r0, r1)) {
-      dn_write<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
+      if (a.dn8) dn_write8<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
+      else dn_write<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
       return;
     }
     for (int half = 0; half < 2; ++half) {
       __syncthreads();
       dn_count<uint16_t>(a, cw, hlo + half * kDnHC, kDnHC, r0, r1);
-      dn_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
+      if (a.dn8) dn_write8<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
+      else dn_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
     }
     return;
   }
   dn_count<uint16_t>(a, cw, hlo, HC, r0, r1);
-  dn_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0, HC);
+  if (a.dn8) dn_write8<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0, HC);
+  else dn_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0, HC);
 }
 
 struct DnPassArgs {
@@ -286,6 +387,257 @@ __global__ __launch_bounds__(kDnThreads) void k_dn_pass(DnPassArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// dn8: the passes on v_mfma_i32_16x16x64_i8
+// ---------------------------------------------------------------------------
+// Operand maps (tools/mfma_i8_probe.hip, exact integer data): lane l = (g = l >> 4, i = l & 15)
+// holds A[row i][k = 16 g + jj] and B[k = 16 g + jj][col i] in bytes jj = 0..15; D (4 x i32):
+// row 4 g + x, col i.  A = the count fragments of the tables, B = the digit fragments of the other
+// FE's effects, [kb][digit][1 KB] per 512-row tile, lane l's 16 bytes at l * 16.
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int kDn8Tile = 512;           // k rows per digit tile (8 k blocks of 64)
+constexpr int kDn8TileBytes = 8 * 8 * 1024;
+
+// balanced base-128 digits of round(v * sin): 8 digits in [-64, 63] (|v sin| <= 2^54)
+__device__ __forceinline__ void dn8_split(double v, double sin, int (&dg)[8]) {
+  long long A = __double2ll_rn(v * sin);
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    int lo = (int)(A & 127);
+    lo -= (lo & 64) << 1;
+    dg[d] = lo;
+    A = (A - lo) >> 7;
+  }
+}
+
+// One tile of rows [0, rows) (rows <= 512) of a row-major [.][p] table (p <= 16) into digit
+// fragments fr [8 kb][8 d][1024] and per-column scales sc[16] = 2^(e - 54) (NaN for a column with a
+// non-finite value, so that it propagates), by a block of NT threads.  Thread t holds column t & 15
+// of RPT consecutive rows in registers: one round of loads, no dependent load chain.
+template <int NT>
+__device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p, int8_t* __restrict__ fr,
+                                double* __restrict__ sc, double* __restrict__ red) {
+  constexpr int RPT = kDn8Tile * 16 / NT;  // rows per thread (32 or 16)
+  const int tid = threadIdx.x, col = tid & 15, r0 = (tid >> 4) * RPT;
+  double v[RPT];
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) v[u] = (col < p && r0 + u < rows) ? src[(int64_t)(r0 + u) * p + col] : 0.0;
+  double m = 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) {
+    bad |= !isfinite(v[u]);
+    m = fmax(m, fabs(v[u]));
+  }
+  red[tid] = bad ? __builtin_nan("") : m;
+  __syncthreads();
+  if (tid < 16) {
+    double mm = 0.0;
+    bool nb = false;
+    for (int t = tid; t < NT; t += 16) {
+      nb |= isnan(red[t]);
+      mm = fmax(mm, red[t]);
+    }
+    const int e = mm > 0.0 ? ilogb(mm) + 1 : 0;  // max |alpha| < 2^e
+    sc[tid] = nb ? __builtin_nan("") : ldexp(1.0, e - 54);
+    red[NT + tid] = ldexp(1.0, 54 - e);
+  }
+  __syncthreads();
+  const double sin = red[NT + col];
+  // rows 4 q .. 4 q + 3 of the thread's -> one 32-bit word per digit at lane (16 g + col), bytes 4 jq
+#pragma unroll
+  for (int q4 = 0; q4 < RPT / 4; ++q4) {
+    const int rq = (r0 >> 2) + q4, kb = rq >> 4, g = (rq >> 2) & 3, jq = rq & 3;
+    int word[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double x = v[4 * q4 + u];
+      int dg[8];
+      dn8_split(isfinite(x) ? x : 0.0, sin, dg);
+#pragma unroll
+      for (int d = 0; d < 8; ++d) word[d] |= (dg[d] & 255) << (8 * u);
+    }
+    const int off = (16 * g + col) * 16 + 4 * jq;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) *reinterpret_cast<int*>(fr + (kb * 8 + d) * 1024 + off) = word[d];
+  }
+}
+
+// alpha_Q -> digit tiles dq [tile][kb][d][1 KB] and scales eq [tile][16] (one block per tile)
+__global__ __launch_bounds__(256) void k_dn8_digits(const double* __restrict__ alpha, int G, int p,
+                                                    int8_t* __restrict__ dq, double* __restrict__ eq) {
+  extern __shared__ __attribute__((aligned(16))) int8_t fr[];
+  __shared__ double red[256 + 16];
+  __shared__ double sc[16];
+  const int t = blockIdx.x, r0 = t * kDn8Tile;
+  dn8_tile_digits<256>(alpha + (int64_t)r0 * p, min(kDn8Tile, G - r0), p, fr, sc, red);
+  __syncthreads();
+  const int4* s4 = reinterpret_cast<const int4*>(fr);
+  int4* d4p = reinterpret_cast<int4*>(dq + (int64_t)t * kDn8TileBytes);
+  for (int j = threadIdx.x; j < kDn8TileBytes / 16; j += blockDim.x) d4p[j] = s4[j];
+  if (threadIdx.x < 16) eq[t * 16 + threadIdx.x] = sc[threadIdx.x];
+}
+
+struct Dn8Args {
+  const int8_t* Nm;       // NA8 (K1) or NB8 (K2)
+  const uint8_t* flags;   // FA / FB: block holds a count over 127 (its u16 counts in X)
+  int fstride;
+  const uint16_t* X;      // the flagged blocks' u16 counts (16 x 64, natural order)
+  const int32_t* blist;
+  int nbe, s, B, G_Q, G_P, p;
+  int nkb;                // 64-row k blocks per output block (K1: GQ64 / 64, K2: B / 64)
+  int nrb;                // output blocks per bucket (K1: B / 16, K2: GQ64 / 16)
+  int rbw;                // output blocks per workgroup
+  const int8_t* dq;       // K1: alpha_Q digit tiles
+  const double* eq;       // K1: their scales
+  const double* alpha;    // K1: alpha_Q (flagged blocks); K2: alpha_P (digitized per bucket tile)
+  const double* S_P;      // K1: alpha_P = (S_P - T_P) / n_P
+  const int32_t* cntP;
+  double* alphaP;
+  double* zero_check;
+  double* runs;           // K2: per-bucket slots [nbe][G_Q][p]
+};
+
+// K1 (K2 = false): T_P of R output blocks (16 primary groups each) per wave; K2: T_Q,b of R blocks
+// of 16 secondary levels.  Per tile: its digit fragments staged in LDS (K1: copied from k_dn8_digits'
+// output; K2: the bucket's alpha_P rows digitized here), the A fragments of the next k block in
+// flight while 8 digit MFMAs per block run, then the int32 sums of the tile to f64 and the flagged
+// blocks' f64 sums, in that fixed order.
+template <bool K2, int R>
+__global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
+  extern __shared__ __attribute__((aligned(16))) int8_t fr[];  // [8 kb][8 d][1024]
+  __shared__ double red[512 + 16];
+  __shared__ double sc[16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  const int p = a.p;
+  const int wgpb = (a.nrb + a.rbw - 1) / a.rbw;
+  const int bi = blockIdx.x / wgpb;
+  const int rb0 = (blockIdx.x - bi * wgpb) * a.rbw + wave * R;
+  const int b = a.blist[bi];
+  const int lo = b << a.s;
+  if (!K2 && a.zero_check && blockIdx.x == 0 && tid == 0) *a.zero_check = 0.0;
+  double acc[R][4];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) acc[r][x] = 0.0;
+  const int8_t* nm[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    nm[r] = a.Nm + ((int64_t)bi * a.nrb + min(rb0 + r, a.nrb - 1)) * a.nkb * 1024 + lane * 16;
+  const int ntile = (a.nkb + 7) / 8;
+  for (int t = 0; t < ntile; ++t) {
+    const int kb0 = t * 8, nk = min(8, a.nkb - kb0);
+    __syncthreads();
+    if (K2) {
+      const int r0 = lo + t * kDn8Tile;
+      dn8_tile_digits<512>(a.alpha + (int64_t)r0 * p, max(0, min(kDn8Tile, min(a.B - t * kDn8Tile, a.G_P - r0))),
+                           p, fr, sc, red);
+    } else {
+      // the tile's fragments, every load of a thread issued before its stores (4 KB per thread
+      // round: no chain of L2 round trips)
+      const int4* s4 = reinterpret_cast<const int4*>(a.dq + (int64_t)t * kDn8TileBytes);
+      int4* d4p = reinterpret_cast<int4*>(fr);
+      constexpr int kStage = 16;  // int4 per thread per round (256 threads: one 64 KB tile)
+      for (int j0 = 0; j0 < nk * 512; j0 += kStage * (int)blockDim.x) {
+        int4 tmp[kStage];
+#pragma unroll
+        for (int u = 0; u < kStage; ++u) {
+          const int j = j0 + u * (int)blockDim.x + tid;
+          tmp[u] = j < nk * 512 ? s4[j] : int4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < kStage; ++u) {
+          const int j = j0 + u * (int)blockDim.x + tid;
+          if (j < nk * 512) d4p[j] = tmp[u];
+        }
+      }
+      if (tid < 16) sc[tid] = a.eq[t * 16 + tid];
+    }
+    // the tile's A fragments, all in flight together (the table streams from HBM)
+    v4i A[R][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        A[r][k] = *reinterpret_cast<const v4i*>(nm[r] + (int64_t)(kb0 + min(k, nk - 1)) * 1024);
+    __syncthreads();
+    v4i D[R][8];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int d = 0; d < 8; ++d) D[r][d] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= nk) break;  // uniform
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        const v4i bv = *reinterpret_cast<const v4i*>(fr + (k * 8 + d) * 1024 + lane * 16);
+#pragma unroll
+        for (int r = 0; r < R; ++r) D[r][d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[r][k], bv, D[r][d], 0, 0, 0);
+      }
+    }
+    // the tile's exact digit sums -> f64 (digit order), then its flagged blocks
+    const double s0 = sc[c];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      double tsum[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int d = 7; d >= 0; --d) {
+        const double sd = ldexp(s0, 7 * d);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) tsum[x] += (double)D[r][d][x] * sd;
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) acc[r][x] += tsum[x];
+      const int rb = rb0 + r;
+      if (rb >= a.nrb) continue;
+      const uint8_t* fl = a.flags + ((int64_t)bi * a.nrb + rb) * a.fstride + kb0;
+      for (int k = 0; k < nk; ++k) {
+        if (!fl[k]) continue;  // wave-uniform
+        const uint16_t* X = a.X + (((int64_t)bi * a.nrb + rb) * a.nkb + kb0 + k) * 1024;
+        const int kr0 = (kb0 + k) * 64;  // first k row of the block
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          double sx = 0.0;
+          for (int jj = 0; jj < 64; ++jj) {
+            const int kr = kr0 + jj;
+            double al = 0.0;
+            if (c < p) {
+              if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * p + c] : 0.0;
+              else al = kr < a.G_Q ? a.alpha[(int64_t)kr * p + c] : 0.0;
+            }
+            sx += (double)X[(4 * g + x) * 64 + jj] * al;
+          }
+          acc[r][x] += sx;
+        }
+      }
+    }
+  }
+  // lane (g, c), register x: row 16 rb + 4 g + x of the output block, column c
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int rb = rb0 + r;
+    if (rb >= a.nrb || c >= p) continue;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int row = rb * 16 + 4 * g + x;
+      if (K2) {
+        if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * p + c] = acc[r][x];
+      } else {
+        const int h = lo + row;
+        if (row < a.B && h < a.G_P) {
+          const int32_t n = a.cntP[h];
+          const int64_t e = (int64_t)h * p + c;
+          a.alphaP[e] = n > 0 ? (a.S_P[e] - acc[r][x]) / (double)n : 0.0;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 
@@ -293,6 +645,17 @@ static int64_t dn_cells(const lfe_ctx* c) {
   const int Q = 1 - c->L.P;
   const int64_t GQ16 = ((int64_t)c->fe[Q].G + 15) / 16 * 16;
   return (int64_t)std::max(c->nbe, 1) * ((int64_t)1 << c->L.s) * GQ16;
+}
+
+static int dn_gq64(const lfe_ctx* c) { return (c->fe[1 - c->L.P].G + 63) / 64 * 64; }
+
+// the exact i8 passes: the counters of a 64-group chunk of GQ64 columns fit the build's LDS, the
+// bucket is whole 64-row k blocks (LFE_DN8=0: the f64 passes, for A/B)
+static bool dn8_ok(const lfe_ctx* c) {
+  const char* e = getenv("LFE_DN8");
+  if (e && e[0] == '0') return false;
+  const int64_t B = 1ll << c->L.s;
+  return B % 64 == 0 && (size_t)kDnHC * dn_gq64(c) * 2 <= 150 * 1024 && c->p <= 16;
 }
 
 bool dense_ok(const lfe_ctx* c) {
@@ -316,11 +679,29 @@ int dense_build(lfe_ctx* c) {
   auto& L = c->L;
   const int Q = 1 - L.P;
   const int B = 1 << L.s, GQ16 = (c->fe[Q].G + 15) / 16 * 16;
-  const size_t cells = (size_t)dn_cells(c);
+  c->dn8 = dn8_ok(c);
+  const int GQ64 = dn_gq64(c), GQW = c->dn8 ? GQ64 : GQ16;
+  const size_t cells = c->dn8 ? (size_t)std::max(c->nbe, 1) * B * GQ64 : (size_t)dn_cells(c);
   c->dense_cells = (int64_t)cells;
   LFE_TRY(ensure_u16(c, c->dn_na, c->dn_na_cap, cells));
   LFE_TRY(ensure_u16(c, c->dn_nb, c->dn_nb_cap, cells));
   DnBuildArgs a{};
+  a.GQW = GQW;
+  if (c->dn8) {
+    const int nbe = std::max(c->nbe, 1);
+    a.dn8 = 1;
+    a.GQ64 = GQ64;
+    a.fa_stride = (GQ64 / 64 + 7) / 8 * 8;
+    a.fb_stride = (B / 64 + 7) / 8 * 8;
+    LFE_TRY(ensure_i8(c, c->dn8_a, c->dn8_a_cap, cells));
+    LFE_TRY(ensure_i8(c, c->dn8_b, c->dn8_b_cap, cells));
+    LFE_TRY(ensure_u8(c, c->dn8_fa, c->dn8_fa_cap, (size_t)nbe * (B / 16) * a.fa_stride));
+    LFE_TRY(ensure_u8(c, c->dn8_fb, c->dn8_fb_cap, (size_t)nbe * (GQ64 / 16) * a.fb_stride));
+    a.NA8 = c->dn8_a;
+    a.NB8 = c->dn8_b;
+    a.FA = c->dn8_fa;
+    a.FB = c->dn8_fb;
+  }
   a.items = reinterpret_cast<const int4*>(c->items_d);
   a.bitems = c->bitems_d;
   a.blist = c->blist_d;
@@ -334,13 +715,13 @@ int dense_build(lfe_ctx* c) {
   // and still give every CU a workgroup; else 64-group chunks on 16-bit counters (twice the
   // workgroups).  Same box, ms per build: 50M rows 0.269 (8-bit) vs 0.368 (16-bit); the 8-rank
   // owner shard's 25 buckets 0.068 vs 0.055
-  const bool c8_fits = (size_t)2 * kDnHC * GQ16 <= 150 * 1024 && B % (2 * kDnHC) == 0;
+  const bool c8_fits = (size_t)2 * kDnHC * GQW <= 150 * 1024 && B % (2 * kDnHC) == 0;
   bool c8 = c8_fits && (int64_t)c->nbe * (B / (2 * kDnHC)) >= c->n_cu;
   if (const char* e = getenv("LFE_DN_C8")) c8 = c8_fits && e[0] == '1';  // tests: force either form
   a.nch = B / (c8 ? 2 * kDnHC : kDnHC);
   a.NA = c->dn_na;
   a.NB = c->dn_nb;
-  const size_t lds = sizeof(uint16_t) * kDnHC * GQ16;  // both forms
+  const size_t lds = sizeof(uint16_t) * kDnHC * GQW;  // both forms
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn_build), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds));
   const int grid = (c->nbe + 7) / 8 * 8 * a.nch;
@@ -375,8 +756,67 @@ static DnPassArgs dn_args(const lfe_ctx* c) {
   return a;
 }
 
+static Dn8Args dn8_args(const lfe_ctx* c) {
+  const int P = c->L.P, Q = 1 - P;
+  Dn8Args a{};
+  a.blist = c->blist_d;
+  a.nbe = c->nbe;
+  a.s = c->L.s;
+  a.B = 1 << c->L.s;
+  a.G_Q = c->fe[Q].G;
+  a.G_P = c->fe[P].G;
+  a.p = c->p;
+  return a;
+}
+
+template <bool K2>
+static int dn8_launch(lfe_ctx* c, const Dn8Args& a, int waves, int grid) {
+  const size_t lds = kDn8TileBytes;
+  const void* f1 = reinterpret_cast<const void*>(&k_dn8_pass<K2, 1>);
+  const void* f2 = reinterpret_cast<const void*>(&k_dn8_pass<K2, 2>);
+  const bool two = a.rbw == 2 * waves;
+  LFE_HIP(hipFuncSetAttribute(two ? f2 : f1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (two) hipLaunchKernelGGL((k_dn8_pass<K2, 2>), dim3(grid), dim3(64 * waves), lds, c->stream, a);
+  else hipLaunchKernelGGL((k_dn8_pass<K2, 1>), dim3(grid), dim3(64 * waves), lds, c->stream, a);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+// output blocks per wave: two while that leaves >= 2 workgroups per CU, else one
+static int dn8_rbw(const lfe_ctx* c, int nrb, int waves) {
+  const int64_t wg2 = (int64_t)std::max(c->nbe, 1) * ((nrb + 2 * waves - 1) / (2 * waves));
+  return wg2 >= 2 * (int64_t)c->n_cu ? 2 * waves : waves;
+}
+
 int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
   const int P = c->L.P;
+  if (c->dn8) {
+    Dn8Args a = dn8_args(c);
+    const int GQ64 = dn_gq64(c), nkb = GQ64 / 64, ntile = (nkb + 7) / 8;
+    LFE_TRY(ensure_i8(c, c->dn8_dq, c->dn8_dq_cap, (size_t)ntile * kDn8TileBytes));
+    LFE_TRY(ensure_f64(c, c->dn8_eq, c->dn8_eq_cap, (size_t)ntile * 16));
+    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_digits), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kDn8TileBytes));
+    hipLaunchKernelGGL(k_dn8_digits, dim3(ntile), dim3(256), kDn8TileBytes, c->stream, alphaQ, a.G_Q, a.p, c->dn8_dq,
+                       c->dn8_eq);
+    LFE_HIP(hipGetLastError());
+    a.Nm = c->dn8_a;
+    a.flags = c->dn8_fa;
+    a.fstride = (nkb + 7) / 8 * 8;
+    a.X = c->dn_na;
+    a.nkb = nkb;
+    a.nrb = a.B / 16;
+    a.dq = c->dn8_dq;
+    a.eq = c->dn8_eq;
+    a.alpha = alphaQ;
+    a.S_P = c->fe[P].S;
+    a.cntP = c->fe[P].cnt;
+    a.alphaP = c->fe[P].alpha;
+    a.zero_check = zero_check;
+    constexpr int waves = 4;
+    a.rbw = dn8_rbw(c, a.nrb, waves);
+    return dn8_launch<false>(c, a, waves, std::max(c->nbe, 1) * ((a.nrb + a.rbw - 1) / a.rbw));
+  }
   DnPassArgs a = dn_args(c);
   a.Nm = c->dn_na;
   a.alpha = alphaQ;
@@ -396,6 +836,21 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
 }
 
 int dense_tq(lfe_ctx* c, double* runs) {
+  if (c->dn8) {
+    Dn8Args a = dn8_args(c);
+    const int GQ64 = dn_gq64(c);
+    a.Nm = c->dn8_b;
+    a.flags = c->dn8_fb;
+    a.nkb = a.B / 64;
+    a.fstride = (a.nkb + 7) / 8 * 8;
+    a.X = c->dn_nb;
+    a.nrb = GQ64 / 16;
+    a.alpha = c->fe[c->L.P].alpha;
+    a.runs = runs;
+    constexpr int waves = 8;  // every workgroup digitizes its bucket's alpha_P rows: 16 blocks each
+    a.rbw = dn8_rbw(c, a.nrb, waves);
+    return dn8_launch<true>(c, a, waves, std::max(c->nbe, 1) * ((a.nrb + a.rbw - 1) / a.rbw));
+  }
   DnPassArgs a = dn_args(c);
   a.Nm = c->dn_nb;
   a.alpha = c->fe[c->L.P].alpha;

@@ -200,6 +200,22 @@ struct lfe_ctx {
   size_t dn_na_cap = 0;
   uint16_t* dn_nb = nullptr;
   size_t dn_nb_cap = 0;
+  // exact integer form of the dense passes (lfe_dense.hip, "dn8"): i8 count tables in MFMA fragment
+  // order, per-block flags of cells over 127 (those blocks' counts stay in dn_na / dn_nb as u16),
+  // and the secondary effects' base-128 digit fragments with their per-tile scales
+  bool dn8 = false;
+  int8_t* dn8_a = nullptr;
+  size_t dn8_a_cap = 0;
+  int8_t* dn8_b = nullptr;
+  size_t dn8_b_cap = 0;
+  uint8_t* dn8_fa = nullptr;
+  size_t dn8_fa_cap = 0;
+  uint8_t* dn8_fb = nullptr;
+  size_t dn8_fb_cap = 0;
+  int8_t* dn8_dq = nullptr;
+  size_t dn8_dq_cap = 0;
+  double* dn8_eq = nullptr;
+  size_t dn8_eq_cap = 0;
   double* colsum_part = nullptr;  // [p][blocks][G] fine-limb columns of k_col_sums (lfe_fast.hip)
   size_t colsum_part_cap = 0;
   double* Xp = nullptr;          // [p][ld] permuted columns
@@ -399,6 +415,8 @@ bool dense_ok(const lfe_ctx* c);
 int dense_build(lfe_ctx* c);
 int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check);
 int dense_tq(lfe_ctx* c, double* runs);
+// the secondary effects' digit fragments for the exact K1 pass (after every alpha_Q update)
+int dense_digits_q(lfe_ctx* c, const double* alphaQ);
 
 // --- constant sums (lfe_sweep.hip) ---
 int sweep_group_sums(lfe_ctx* c);
@@ -485,6 +503,8 @@ int ensure_i32(lfe_ctx* c, int32_t*& p, size_t& cap, size_t elems);
 int ensure_f64(lfe_ctx* c, double*& p, size_t& cap, size_t elems);
 int ensure_u16(lfe_ctx* c, uint16_t*& p, size_t& cap, size_t elems);
 int ensure_u64(lfe_ctx* c, uint64_t*& p, size_t& cap, size_t elems);
+int ensure_i8(lfe_ctx* c, int8_t*& p, size_t& cap, size_t elems);
+int ensure_u8(lfe_ctx* c, uint8_t*& p, size_t& cap, size_t elems);
 template <typename T>
 inline void dfree_any(T*& p) {
   if (p) (void)hipFree(p);

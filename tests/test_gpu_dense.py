@@ -9,7 +9,10 @@ restatements of the same projection loop (polars_impl.py:490-526), so:
 - the dense path repeats bit for bit;
 - a panel whose (h, q) pairs hold more than 255 rows takes the build's 16-bit recount (its 8-bit
   counters overflow) and still matches the oracle;
-- an owner shard (strong scaling, few buckets) takes it too.
+- an owner shard (strong scaling, few buckets) takes it too;
+- the exact integer form (i8 count tables x base-128 digits of the effects on
+  v_mfma_i32_16x16x64_i8, the default) agrees with the f64-MFMA form (LFE_DN8=0) to rounding,
+  including blocks with cells over 127 rows (summed in f64 from their u16 counts).
 LFE_DENSE=1 forces the dense path wherever it fits, LFE_DENSE=0 turns it off."""
 from __future__ import annotations
 
@@ -142,3 +145,55 @@ def test_dense_owner_shard_matches_whole_panel(monkeypatch):
     assert got["iterations"] == o["iterations"]
     np.testing.assert_allclose(got["beta"], o["beta"], rtol=1e-10, atol=0)
     np.testing.assert_allclose(got["se"], o["se"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("vcov,p_k", [("HC1", 10), ("iid", 3), ("HC1", 15)])
+def test_dense_i8_digits_match_f64_mfma_and_oracle(vcov, p_k, monkeypatch):
+    """The i8 passes (default) against the f64-MFMA passes (LFE_DN8=0) and the oracle: equal
+    integers, beta / SE at 1e-10 of the oracle and 1e-12 of each other, bit-identical repeats;
+    k = 15 fills all 16 MFMA columns (p = 16)."""
+    from leanfe_amd import synth
+
+    xs = [f"x{j + 1}" for j in range(p_k)]
+    data = synth.panel(900_000, p_k, [3_000, 600], seed=77)
+    o = _oracle(data, xs, vcov)
+    monkeypatch.setenv("LFE_DENSE", "1")
+    monkeypatch.setenv("LFE_DN8", "0")
+    f64 = _fit(data, xs, vcov)
+    monkeypatch.delenv("LFE_DN8")
+    i8 = _fit(data, xs, vcov)
+    _check(f64, o)
+    _check(i8, o)
+    np.testing.assert_allclose(i8[0], f64[0], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(i8[1], f64[1], rtol=1e-12, atol=0)
+    again = _fit(data, xs, vcov)
+    np.testing.assert_array_equal(i8[0], again[0])
+    np.testing.assert_array_equal(i8[1], again[1])
+
+
+def test_dense_i8_flagged_blocks_mixed_with_exact_blocks(monkeypatch):
+    """A few (h, q) pairs with 128-400 rows among ordinary cells: their 16 x 64 blocks are flagged
+    (zero in the i8 tables, u16 counts summed in f64) while every other block runs on the i8
+    MFMAs - both orientations (K1 and K2 blocks) - against the oracle and the f64 passes."""
+    rng = np.random.default_rng(5)
+    n, k = 600_000, 4
+    fe1 = rng.integers(0, 2_000, n).astype(np.int32)
+    fe2 = rng.integers(0, 300, n).astype(np.int32)
+    pairs = [(17, 5, 128), (900, 299, 400), (1_500, 64, 200), (1_999, 0, 131)]
+    i0 = 0
+    for h, q, m in pairs:
+        fe1[i0:i0 + m] = h
+        fe2[i0:i0 + m] = q
+        i0 += m
+    x = rng.standard_normal((n, k))
+    y = x @ np.linspace(1.0, 0.2, k) + rng.standard_normal(2_000)[fe1] + rng.standard_normal(300)[fe2] + \
+        rng.standard_normal(n)
+    data = {"y": y, "fe1": fe1, "fe2": fe2, **{f"x{j + 1}": x[:, j].copy() for j in range(k)}}
+    xs = [f"x{j + 1}" for j in range(k)]
+    o = _oracle(data, xs)
+    monkeypatch.setenv("LFE_DENSE", "1")
+    i8 = _fit(data, xs)
+    _check(i8, o)
+    monkeypatch.setenv("LFE_DN8", "0")
+    f64 = _fit(data, xs)
+    np.testing.assert_allclose(i8[0], f64[0], rtol=1e-12, atol=0)
