@@ -17,11 +17,12 @@ the same workloads against the C restatement of the reference (oracle/altproj_c.
 Multi-GPU: one process per GPU.  Under torchrun the rank comes from the environment;
 ``python bench.py --gpus N`` without it spawns N rank processes itself (before any GPU
 call).  ``--scaling strong`` (default): ``--rows`` rows in total, sharded over the ranks;
-``--scaling weak``: ``--rows`` rows per rank.  ``--shard owner`` (default for two-FE
-unclustered fits) gives each rank every row of a contiguous range of primary-FE levels,
-so the primary FE's group tables stay rank-local and only the secondary FE's tables, the
-Gram and the SE statistics are all-reduced over RCCL; ``--shard rows`` shards contiguous
-row blocks (every group table all-reduced).  Timing: W warm-up steps, barrier + device
+``--scaling weak``: ``--rows`` rows per rank.  ``--shard owner`` (default for fits with two
+or more FEs) gives each rank every row of a contiguous range of the primary FE's (most
+levels) levels, so the primary FE's group tables stay rank-local and only the other FEs'
+tables, the Gram and the SE statistics are all-reduced over RCCL (clustered scores go to
+their owner ranks by cluster key); ``--shard rows`` shards contiguous row blocks (every
+group table all-reduced).  Timing: W warm-up steps, barrier + device
 sync, K timed steps, device sync + barrier; the max over ranks is reported.
 """
 from __future__ import annotations
@@ -253,16 +254,19 @@ def load_shard(eng, a, rank: int, world: int, shard: str) -> dict:
 # measurement helpers
 # ---------------------------------------------------------------------------
 
-def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cells: int = 0) -> dict:
+def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cells: int = 0,
+                      cell_bytes: int = 2) -> dict:
     """HBM bytes each kernel must move per launch, n rows of the shard,
     p = 1 + k f64 data columns, F int32 code columns.  Kernels absent here move only group
     tables or scalars (latency-bound) and count as 0 in the step total.  The general sweeps'
     cross / check passes (F >= 3) read F - 1 code arrays from HBM; the effect
     rows they gather come from L2 / MALL-resident tables and are not HBM bytes.  With the dense
     two-FE cross terms (``dense_cells`` > 0, lfe_dense.hip) the table build reads both codes and
-    writes two uint16 count tables, and each cross-term pass reads one of them."""
+    writes two count tables of ``cell_bytes`` per cell (1: the exact i8 form, 2: u16), and each
+    cross-term pass reads one of them."""
     k = p - 1
-    dense = {"layout_scatter": 8 * n + 2 * 2 * dense_cells, "tp": 2 * dense_cells, "tq": 2 * dense_cells,
+    cb = cell_bytes
+    dense = {"layout_scatter": 8 * n + 2 * cb * dense_cells, "tp": cb * dense_cells, "tq": cb * dense_cells,
              "layout_base": 0} if dense_cells else {}
     return {
         "part_hist": 4 * n,                          # primary codes
@@ -371,7 +375,7 @@ def main(argv=None):
         raise SystemExit(f"bench.py --gpus {a.gpus} but WORLD_SIZE={d.world}")
     shard = a.shard
     if shard == "auto":
-        shard = "owner" if (len(a.levels) == 2 and a.vcov.lower() != "cluster" and d.world > 1) else "rows"
+        shard = "owner" if (len(a.levels) >= 2 and d.world > 1) else "rows"
     # LEANFE_BENCH_DEVICE (diagnostic): every rank on that one device, e.g. to run the RCCL path of
     # a multi-rank solve on a one-GPU box (RCCL must accept several ranks on one device)
     eng = Engine(int(os.environ.get("LEANFE_BENCH_DEVICE", d.local)))
@@ -425,7 +429,8 @@ def main(argv=None):
     value_mean = total_rows * a.steps / elapsed / 1e6
     p, F = a.k + 1, len(a.levels)
     cells = eng.dense_cells()
-    ab = algorithmic_bytes(geo["local"], p, F, clustered=bool(a.cl), dense_cells=cells)
+    cbytes = eng.dense_cell_bytes() if cells else 0
+    ab = algorithmic_bytes(geo["local"], p, F, clustered=bool(a.cl), dense_cells=cells, cell_bytes=cbytes or 2)
     # dominant kernel = most device time in the timed region (rank 0's shard)
     dom = max(kstats.items(), key=lambda kv: kv[1][0]) if kstats else ("none", (0.0, 1))
     dom_name, (dom_ms, dom_launches) = dom
@@ -498,7 +503,9 @@ def main(argv=None):
             "config": {"workload": workload_label(a, d.world), "rows_total": total_rows,
                        "rows_rank0": geo["local"], "k": a.k, "levels": a.levels, "vcov": a.vcov,
                        "cluster_fes": a.cl, "iterations": res["iterations"],
-                       "cross_terms": f"dense count tables ({cells} cells, MFMA)" if cells else "row layouts",
+                       "cross_terms": (f"dense count tables ({cells} cells, "
+                                       + ("exact i8 x base-128 digits, v_mfma_i32_16x16x64_i8)" if cbytes == 1
+                                          else "u16, v_mfma_f64_16x16x4f64)")) if cells else "row layouts",
                        "parallelism": f"dp{d.world} ({shard}-sharded rows, RCCL inside the engine)"
                        if not a.emulate_rank else f"rank {a.emulate_rank} owner shard solved alone (diagnostic)"},
             "roofline": roofline,

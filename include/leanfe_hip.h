@@ -250,7 +250,11 @@ int lfe_copy_inputs(lfe_ctx* ctx, double* const* cols_out, int32_t* const* codes
  *   clustered SEs: lfe_load_clusters (input order) and lfe_stream_clusters(subset masks) before
  *          pass 2 / 4, whose chunks then add their score rows into per-cluster sums; then
  *          lfe_stream_cluster_meats (std_errors.py:289-441).
- * p <= 11.  cols = p column pointers of `rows` doubles each (kind LFE_HOST / LFE_DEVICE).
+ * p <= 63 (weighted: 62): up to p = 11 the passes run row per lane (16 x 16 tiles), wider fits on
+ * the MFMA lane layout with 16 ceil((p + 1) / 16)-wide tiles.  A sharded engine (lfe_ctx_set_comm)
+ * streams its own rows: the sums and every pass's tile are all-reduced, and the clustered score
+ * sums go to their owner ranks by cluster key (cluster codes must then be global).
+ * cols = p column pointers of `rows` doubles each (kind LFE_HOST / LFE_DEVICE).
  * lfe_stream_end's `out`: pass 2: stats[4] then the (p-1)^2 meat; pass 4: stats[4] then the p^2
  * meat; pass 3: the (p+1)^2 Gram; pass 1: unused. */
 int lfe_load_codes(lfe_ctx* ctx, int64_t n, int p, int F, const int32_t* const* fe_codes,
@@ -281,6 +285,9 @@ int lfe_exact_sums(lfe_ctx* ctx, int* on);
  * took the row layouts (lfe_dense.hip).  A diagnostic for the byte model of bench.py; replaces
  * nothing in the reference. */
 int lfe_dense_cells(lfe_ctx* ctx, int64_t* cells);
+/* Bytes per cell of those tables as the passes read them: 1 for the exact i8 form (count tables
+ * x base-128 digits of the effects on v_mfma_i32_16x16x64_i8), 2 for the u16 / f64-MFMA form. */
+int lfe_dense_cell_bytes(lfe_ctx* ctx, int32_t* bytes);
 
 /* Wait for all work queued on the context's stream. */
 int lfe_sync(lfe_ctx* ctx);

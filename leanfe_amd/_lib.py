@@ -62,6 +62,7 @@ SIGNATURES = {
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
     "lfe_dense_cells": (C.c_int, [_vp, _i64p]),
+    "lfe_dense_cell_bytes": (C.c_int, [_vp, C.POINTER(C.c_int32)]),
     "lfe_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.POINTER(_vp), _i32p, _dp, C.c_int]),
     "lfe_stream_clusters": (C.c_int, [_vp, C.c_int, _i32p]),
     "lfe_stream_cluster_meats": (C.c_int, [_vp, _dp, _i64p]),
@@ -517,6 +518,12 @@ class Engine:
         _check(self._lib.lfe_dense_cells(self._h, C.byref(v)))
         return int(v.value)
 
+
+    def dense_cell_bytes(self) -> int:
+        """Bytes per cell the dense passes read (1: the exact i8 tables, 2: u16; 0: row layouts)."""
+        v = C.c_int32(0)
+        _check(self._lib.lfe_dense_cell_bytes(self._h, C.byref(v)))
+        return int(v.value)
     def profile(self, enable: bool = True) -> None:
         _check(self._lib.lfe_profile(self._h, 1 if enable else 0))
 

@@ -210,7 +210,7 @@ struct lfe_emu {
 
 namespace lfe {
 
-enum EmuOp { EMU_SUM_F64, EMU_SUM_I32, EMU_MAX_F64 };
+enum EmuOp { EMU_SUM_F64, EMU_SUM_I32, EMU_MAX_F64, EMU_MAX_U64 };
 
 static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
   lfe_emu* e = c->emu;
@@ -226,6 +226,9 @@ static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
       for (size_t i = 0; i < count; ++i) {
         if (op == EMU_SUM_I32) {
           reinterpret_cast<int32_t*>(e->result.data())[i] += reinterpret_cast<const int32_t*>(e->slots[r].data())[i];
+        } else if (op == EMU_MAX_U64) {
+          uint64_t& acc = reinterpret_cast<uint64_t*>(e->result.data())[i];
+          acc = std::max(acc, reinterpret_cast<const uint64_t*>(e->slots[r].data())[i]);
         } else {
           double& acc = reinterpret_cast<double*>(e->result.data())[i];
           const double v = reinterpret_cast<const double*>(e->slots[r].data())[i];
@@ -311,6 +314,14 @@ int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count) {
   if (c->world <= 1 || count == 0) return LFE_OK;
   if (c->emu) return emu_allreduce(c, dev, count, EMU_SUM_I32);
   LFE_NCCL(ncclAllReduce(dev, dev, count, ncclInt32, ncclSum, c->comm, c->stream));
+  return LFE_OK;
+}
+
+// max of u64 (the bits of non-negative doubles, NaN above every number: a max that keeps NaN)
+int allreduce_max_u64(lfe_ctx* c, uint64_t* dev, size_t count) {
+  if (c->world <= 1 || count == 0) return LFE_OK;
+  if (c->emu) return emu_allreduce(c, dev, count, EMU_MAX_U64);
+  LFE_NCCL(ncclAllReduce(dev, dev, count, ncclUint64, ncclMax, c->comm, c->stream));
   return LFE_OK;
 }
 
@@ -1112,8 +1123,6 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
   {
     PhaseTimer t(c, PH_DEMEAN);
     const bool fast = c->F > 0 && check_from > 0 && fast_path_ok(c, order);
-    if (c->owner_on && !fast)
-      return fail(LFE_EINVAL, "owner-sharded rows need the two-FE sweeps with the primary FE projected last");
     if (!fast)  // the two-FE sweeps write every alpha entry before reading any
       for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
     if (c->F > 0) {
@@ -1244,6 +1253,13 @@ int lfe_dense_cells(lfe_ctx* c, int64_t* cells) {
   LFE_CTX(c);
   if (!cells) return fail(LFE_EINVAL, "null pointer");
   *cells = c->dense_cells;
+  return LFE_OK;
+}
+
+int lfe_dense_cell_bytes(lfe_ctx* c, int32_t* bytes) {
+  LFE_CTX(c);
+  if (!bytes) return fail(LFE_EINVAL, "null output pointer");
+  *bytes = c->dense_cells ? (c->dn8 ? 1 : 2) : 0;
   return LFE_OK;
 }
 

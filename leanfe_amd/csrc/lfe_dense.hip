@@ -397,15 +397,28 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int kDn8Tile = 512;           // k rows per digit tile (8 k blocks of 64)
 constexpr int kDn8TileBytes = 8 * 8 * 1024;
 
-// balanced base-128 digits of round(v * sin): 8 digits in [-64, 63] (|v sin| <= 2^54)
+// balanced base-128 digits of A = round(v * sin) (|A| <= 2^54): A = hi 2^28 + lo with |hi| <= 2^26,
+// |lo| <= 2^27 split in f64 (exact: integers), then four digits in [-64, 63] from each int32 half
+// (lo's remainder, in [-1, 1], carried into hi)
 __device__ __forceinline__ void dn8_split(double v, double sin, int (&dg)[8]) {
-  long long A = __double2ll_rn(v * sin);
+  const double A = rint(v * sin);
+  const double hf = rint(A * 0x1p-28);
+  int lo = (int)__builtin_fma(hf, -0x1p28, A);
+  int hi = (int)hf;
 #pragma unroll
-  for (int d = 0; d < 8; ++d) {
-    int lo = (int)(A & 127);
-    lo -= (lo & 64) << 1;
-    dg[d] = lo;
-    A = (A - lo) >> 7;
+  for (int d = 0; d < 4; ++d) {
+    int r = lo & 127;
+    r -= (r & 64) << 1;
+    dg[d] = r;
+    lo = (lo - r) >> 7;
+  }
+  hi += lo;
+#pragma unroll
+  for (int d = 4; d < 8; ++d) {
+    int r = hi & 127;
+    r -= (r & 64) << 1;
+    dg[d] = r;
+    hi = (hi - r) >> 7;
   }
 }
 
@@ -555,13 +568,18 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
       }
       if (tid < 16) sc[tid] = a.eq[t * 16 + tid];
     }
-    // the tile's A fragments, all in flight together (the table streams from HBM)
+    // the tile's A fragments, all in flight together (the table streams from HBM), and its blocks'
+    // flags: one 8-byte word per output block (fstride and kb0 are multiples of 8)
     v4i A[R][8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
 #pragma unroll
       for (int r = 0; r < R; ++r)
         A[r][k] = *reinterpret_cast<const v4i*>(nm[r] + (int64_t)(kb0 + min(k, nk - 1)) * 1024);
+    uint64_t fw[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      fw[r] = *reinterpret_cast<const uint64_t*>(a.flags + ((int64_t)bi * a.nrb + min(rb0 + r, a.nrb - 1)) * a.fstride + kb0);
     __syncthreads();
     v4i D[R][8];
 #pragma unroll
@@ -592,10 +610,9 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
 #pragma unroll
       for (int x = 0; x < 4; ++x) acc[r][x] += tsum[x];
       const int rb = rb0 + r;
-      if (rb >= a.nrb) continue;
-      const uint8_t* fl = a.flags + ((int64_t)bi * a.nrb + rb) * a.fstride + kb0;
+      if (rb >= a.nrb || fw[r] == 0) continue;  // wave-uniform; a flagged block is rare
       for (int k = 0; k < nk; ++k) {
-        if (!fl[k]) continue;  // wave-uniform
+        if (!((fw[r] >> (8 * k)) & 0xff)) continue;
         const uint16_t* X = a.X + (((int64_t)bi * a.nrb + rb) * a.nkb + kb0 + k) * 1024;
         const int kr0 = (kb0 + k) * 64;  // first k row of the block
 #pragma unroll
@@ -637,6 +654,194 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
   }
 }
 
+// Streaming forms of the two passes (the default where the k range fits LDS: K1 <= 16 k blocks,
+// K2 <= 8).  The passes move ~100 MB of i8 table each and ~2 MFMA-microseconds of work, so their
+// time is the table's latency-bound streaming: every wave keeps the next output block's whole
+// k range of A fragments (16 x 16 B per lane) in flight while it computes the current one, with the
+// digit fragments staged once per workgroup (K1: all of alpha_Q's, persistent workgroups, one per
+// CU; K2: the bucket's, two workgroups per bucket and CU).
+constexpr int kDn8MaxKb = 16;
+
+template <int MK>  // k blocks held (16: K1, 8: K2)
+struct Dn8Blk {
+  v4i A[MK];
+  uint64_t fw[2];  // the block's flag words (tiles 0, 1)
+};
+
+template <int MK>
+__device__ __forceinline__ void dn8_load_blk(Dn8Blk<MK>& x, const Dn8Args& a, int64_t blk_row, int lane) {
+  const int8_t* nm = a.Nm + blk_row * a.nkb * 1024 + lane * 16;
+#pragma unroll
+  for (int k = 0; k < MK; ++k) x.A[k] = *reinterpret_cast<const v4i*>(nm + (int64_t)min(k, a.nkb - 1) * 1024);
+  const uint8_t* fl = a.flags + blk_row * a.fstride;
+  x.fw[0] = *reinterpret_cast<const uint64_t*>(fl);
+  x.fw[1] = (MK > 8 && a.nkb > 8) ? *reinterpret_cast<const uint64_t*>(fl + 8) : 0ull;
+}
+
+// T of one output block (16 rows x 16 columns; lane (g, c) holds rows 4 g + x of column c) from its
+// A fragments and the staged digit tiles fr [tile][kb][d][1 KB] with scales sc [tile][16]
+template <bool K2, int MK>
+__device__ __forceinline__ void dn8_block(const Dn8Blk<MK>& x, const Dn8Args& a, const int8_t* fr, const double* sc,
+                                          int bi, int rb, int lo, int lane, double (&acc)[4]) {
+  const int g = lane >> 4, c = lane & 15, p = a.p;
+#pragma unroll
+  for (int t = 0; t < MK / 8; ++t) {
+    if (t * 8 >= a.nkb) break;  // uniform
+    v4i D[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) D[d] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (t * 8 + k >= a.nkb) break;  // uniform
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        const v4i bv = *reinterpret_cast<const v4i*>(fr + ((t * 8 + k) * 8 + d) * 1024 + lane * 16);
+        D[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x.A[t * 8 + k], bv, D[d], 0, 0, 0);
+      }
+    }
+    const double s0 = sc[t * 16 + c];
+    double ts[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int d = 7; d >= 0; --d) {
+      const double sd = ldexp(s0, 7 * d);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ts[q] += (double)D[d][q] * sd;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += ts[q];
+    const uint64_t fw = x.fw[t];
+    if (fw == 0) continue;  // a flagged block (a count over 127) is rare
+    for (int k = 0; k < 8 && t * 8 + k < a.nkb; ++k) {
+      if (!((fw >> (8 * k)) & 0xff)) continue;
+      const int kb = t * 8 + k;
+      const uint16_t* X = a.X + (((int64_t)bi * a.nrb + rb) * a.nkb + kb) * 1024;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double sx = 0.0;
+        for (int jj = 0; jj < 64; ++jj) {
+          const int kr = kb * 64 + jj;
+          double al = 0.0;
+          if (c < p) {
+            if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * p + c] : 0.0;
+            else al = kr < a.G_Q ? a.alpha[(int64_t)kr * p + c] : 0.0;
+          }
+          sx += (double)X[(4 * g + q) * 64 + jj] * al;
+        }
+        acc[q] += sx;
+      }
+    }
+  }
+}
+
+// K1, persistent: workgroup i takes output blocks [i T / grid, (i + 1) T / grid) of the T = nbe x B/16
+// primary blocks, wave w every W-th of them
+__global__ __launch_bounds__(512) void k_dn8_k1s(Dn8Args a) {
+  extern __shared__ __attribute__((aligned(16))) int8_t fr[];  // [ntile][8 kb][8 d][1 KB]
+  __shared__ double sc[32];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), W = blockDim.x >> 6;
+  const int g = lane >> 4, c = lane & 15, p = a.p;
+  if (a.zero_check && blockIdx.x == 0 && tid == 0) *a.zero_check = 0.0;
+  const int64_t total = (int64_t)a.nbe * a.nrb;
+  const int64_t i0 = total * blockIdx.x / gridDim.x, i1 = total * (blockIdx.x + 1) / gridDim.x;
+  Dn8Blk<16> xa, xb;
+  if (i0 + wave < i1) dn8_load_blk(xa, a, i0 + wave, lane);  // in flight while the tiles stage
+  {
+    const int n4 = a.nkb * 512;  // int4 of the staged tiles
+    const int4* s4 = reinterpret_cast<const int4*>(a.dq);
+    int4* d4p = reinterpret_cast<int4*>(fr);
+    constexpr int kStage = 8;
+    for (int j0 = 0; j0 < n4; j0 += kStage * (int)blockDim.x) {
+      int4 tmp[kStage];
+#pragma unroll
+      for (int u = 0; u < kStage; ++u) {
+        const int j = j0 + u * (int)blockDim.x + tid;
+        tmp[u] = j < n4 ? s4[j] : int4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int u = 0; u < kStage; ++u) {
+        const int j = j0 + u * (int)blockDim.x + tid;
+        if (j < n4) d4p[j] = tmp[u];
+      }
+    }
+    if (tid < 32) sc[tid] = tid < 16 * ((a.nkb + 7) / 8) ? a.eq[tid] : 0.0;
+  }
+  __syncthreads();
+  auto finish = [&](int64_t i, const double (&acc)[4]) {
+    const int bi = (int)(i / a.nrb), rb = (int)(i - (int64_t)bi * a.nrb);
+    if (c >= p) return;
+    const int lo = a.blist[bi] << a.s;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = rb * 16 + 4 * g + q, h = lo + row;
+      if (row < a.B && h < a.G_P) {
+        const int32_t n = a.cntP[h];
+        const int64_t e = (int64_t)h * p + c;
+        a.alphaP[e] = n > 0 ? (a.S_P[e] - acc[q]) / (double)n : 0.0;
+      }
+    }
+  };
+  for (int64_t i = i0 + wave; i < i1; i += 2 * W) {
+    if (i + W < i1) dn8_load_blk(xb, a, i + W, lane);
+    {
+      const int bi = (int)(i / a.nrb), rb = (int)(i - (int64_t)bi * a.nrb);
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      dn8_block<false>(xa, a, fr, sc, bi, rb, 0, lane, acc);
+      finish(i, acc);
+    }
+    if (i + W >= i1) break;
+    if (i + 2 * W < i1) dn8_load_blk(xa, a, i + 2 * W, lane);
+    {
+      const int64_t j = i + W;
+      const int bi = (int)(j / a.nrb), rb = (int)(j - (int64_t)bi * a.nrb);
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      dn8_block<false>(xb, a, fr, sc, bi, rb, 0, lane, acc);
+      finish(j, acc);
+    }
+  }
+}
+
+// K2: workgroup (bucket bi, part j of np): digitizes the bucket's alpha_P rows, then output blocks
+// [j nrb / np, (j + 1) nrb / np) of the bucket's secondary blocks, wave w every W-th
+__global__ __launch_bounds__(512) void k_dn8_k2s(Dn8Args a, int np) {
+  extern __shared__ __attribute__((aligned(16))) int8_t fr[];  // [8 kb][8 d][1 KB]
+  __shared__ double red[512 + 16];
+  __shared__ double sc[32];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), W = blockDim.x >> 6;
+  const int g = lane >> 4, c = lane & 15, p = a.p;
+  const int bi = blockIdx.x / np, part = blockIdx.x - bi * np;
+  const int lo = a.blist[bi] << a.s;
+  const int i0 = a.nrb * part / np, i1 = a.nrb * (part + 1) / np;
+  Dn8Blk<8> xa, xb;
+  if (i0 + wave < i1) dn8_load_blk(xa, a, (int64_t)bi * a.nrb + i0 + wave, lane);
+  dn8_tile_digits<512>(a.alpha + (int64_t)lo * p, max(0, min(a.B, a.G_P - lo)), p, fr, sc, red);
+  __syncthreads();
+  auto finish = [&](int rb, const double (&acc)[4]) {
+    if (c >= p) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = rb * 16 + 4 * g + q;
+      if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * p + c] = acc[q];
+    }
+  };
+  for (int i = i0 + wave; i < i1; i += 2 * W) {
+    if (i + W < i1) dn8_load_blk(xb, a, (int64_t)bi * a.nrb + i + W, lane);
+    {
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      dn8_block<true>(xa, a, fr, sc, bi, i, lo, lane, acc);
+      finish(i, acc);
+    }
+    if (i + W >= i1) break;
+    if (i + 2 * W < i1) dn8_load_blk(xa, a, (int64_t)bi * a.nrb + i + 2 * W, lane);
+    {
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      dn8_block<true>(xb, a, fr, sc, bi, i + W, lo, lane, acc);
+      finish(i + W, acc);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -651,6 +856,11 @@ static int dn_gq64(const lfe_ctx* c) { return (c->fe[1 - c->L.P].G + 63) / 64 * 
 
 // the exact i8 passes: the counters of a 64-group chunk of GQ64 columns fit the build's LDS, the
 // bucket is whole 64-row k blocks (LFE_DN8=0: the f64 passes, for A/B)
+static bool dn8_tiled() {  // A/B: the tiled forms of the i8 passes
+  const char* e = getenv("LFE_DN8_TILED");
+  return e && e[0] == '1';
+}
+
 static bool dn8_ok(const lfe_ctx* c) {
   const char* e = getenv("LFE_DN8");
   if (e && e[0] == '0') return false;
@@ -813,6 +1023,16 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
     a.cntP = c->fe[P].cnt;
     a.alphaP = c->fe[P].alpha;
     a.zero_check = zero_check;
+    if (nkb <= kDn8MaxKb && !dn8_tiled()) {  // persistent streaming form (LFE_DN8_TILED: A/B)
+      const size_t lds = (size_t)ntile * kDn8TileBytes;
+      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k1s), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+      const int64_t total = (int64_t)std::max(c->nbe, 1) * a.nrb;
+      const int grid = (int)std::min<int64_t>(c->n_cu, (total + 7) / 8);
+      hipLaunchKernelGGL(k_dn8_k1s, dim3(grid), dim3(512), lds, c->stream, a);
+      LFE_HIP(hipGetLastError());
+      return LFE_OK;
+    }
     constexpr int waves = 4;
     a.rbw = dn8_rbw(c, a.nrb, waves);
     return dn8_launch<false>(c, a, waves, std::max(c->nbe, 1) * ((a.nrb + a.rbw - 1) / a.rbw));
@@ -847,6 +1067,16 @@ int dense_tq(lfe_ctx* c, double* runs) {
     a.nrb = GQ64 / 16;
     a.alpha = c->fe[c->L.P].alpha;
     a.runs = runs;
+    if (a.nkb <= 8 && !dn8_tiled()) {  // streaming form: two workgroups per bucket and CU
+      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k2s), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kDn8TileBytes));
+      const int nbe = std::max(c->nbe, 1);
+      int np = (int)std::max<int64_t>(1, (2 * (int64_t)c->n_cu + nbe - 1) / nbe);  // >= 2 workgroups per CU
+      np = std::min(np, std::max(1, a.nrb / 8));                                   // >= 8 blocks each
+      hipLaunchKernelGGL(k_dn8_k2s, dim3(nbe * np), dim3(512), kDn8TileBytes, c->stream, a, np);
+      LFE_HIP(hipGetLastError());
+      return LFE_OK;
+    }
     constexpr int waves = 8;  // every workgroup digitizes its bucket's alpha_P rows: 16 blocks each
     a.rbw = dn8_rbw(c, a.nrb, waves);
     return dn8_launch<true>(c, a, waves, std::max(c->nbe, 1) * ((a.nrb + a.rbw - 1) / a.rbw));

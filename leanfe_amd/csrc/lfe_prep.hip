@@ -940,9 +940,9 @@ int prepare_layout(lfe_ctx* c) {
   L.w = c->w;  // fast_layout_ok reads it before the layout pointers are set below
   const bool item_counts = L.permuted && fast_layout_ok(c);
   // owner-sharded rows: every row of the primary FE's groups [owner_lo, owner_hi) is on this rank,
-  // so its counts, drops, group sums and cross term are complete without an all-reduce (the
-  // two-FE sweeps; lfe_demean refuses the general sweeps in this mode)
-  c->owner_on = c->world > 1 && c->owner_fe >= 0 && c->owner_fe == L.P && item_counts;
+  // so its counts, drops, group sums (W, Sy), cross term and effects are complete without an
+  // all-reduce - in the two-FE sweeps and in the general sweeps (any F, weights) alike
+  c->owner_on = c->world > 1 && c->owner_fe >= 0 && c->owner_fe == L.P && !c->records;
   // every count / drop / group-sum table and the scratch counters zeroed in one launch
   LFE_TRY(ensure_iscratch(c, kIscratchInts));
   {

@@ -827,6 +827,9 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
     LFE_HIP(hipGetLastError());
   }
   hi_end(c);
+  // owner-sharded rows: the primary FE's cross term is complete on its owner rank (its other
+  // levels have no rows here and are never read); every other FE's is summed over the ranks
+  if (c->owner_on && f == c->L.P) return LFE_OK;
   return allreduce_sum_f64(c, out, (size_t)fe.G * pc);
 }
 
@@ -977,6 +980,8 @@ int demean_generic(lfe_ctx* c, const std::vector<int>& order, double tol, int ma
           LFE_TRY(seg_check_max(c, f, c->fe[f].R, 1));
         }
       }
+      // owner-sharded rows: each rank's check covers its own primary levels; the max over ranks
+      if (c->owner_on) LFE_TRY(allreduce_max_u64(c, reinterpret_cast<uint64_t*>(c->dred), 1));
       double chk[2] = {0.0, 0.0};
       LFE_TRY(d2h_sync(c, chk, c->dred, sizeof(double) * (scale_now ? 2 : 1)));
       last = chk[0];

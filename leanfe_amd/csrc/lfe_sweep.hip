@@ -207,6 +207,7 @@ int sweep_group_sums(lfe_ctx* c) {
       hi_end(c);
     }
     for (int f = 0; f < c->F; ++f) {
+      if (c->owner_on && f == c->L.P) continue;  // owner-sharded: the primary FE's are complete
       LFE_TRY(allreduce_sum_f64(c, c->fe[f].W, c->fe[f].G));
       LFE_TRY(allreduce_sum_f64(c, c->fe[f].Sy, c->fe[f].G));
     }

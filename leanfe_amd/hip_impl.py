@@ -141,14 +141,16 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             eng.load([Y] + Xc, codes, levels, w)
             n_initial = Y.size
         cl_loaded = None
-        if sharded and len(fe_cols) == 2 and weights is None and os.environ.get("LEANFE_HIP_RESHARD", "1") != "0":
+        if (sharded and len(fe_cols) >= 2 and strategy in ("auto", "alt_proj")
+                and os.environ.get("LEANFE_HIP_RESHARD", "1") != "0"):
             # contiguous row blocks -> owner-sharded rows (lfe_reshard_owner): every rank then holds
-            # all rows of a range of the primary FE's levels, and a sweep all-reduces only the other
-            # FE's table.  Cluster columns load first, so that they move with their rows.
+            # all rows of a range of the primary FE's (most levels) levels, and a projection
+            # all-reduces only the other FEs' tables - two FEs or more, weighted or not.  Cluster
+            # columns load first, so that they move with their rows.
             if v == "cluster":
                 cl_loaded = _load_clusters(eng, cols, cluster_cols, sharded)
             try:
-                eng.reshard_owner(max(range(2), key=lambda f: levels[f]))
+                eng.reshard_owner(max(range(len(fe_cols)), key=lambda f: levels[f]))
             except (ValueError, MemoryError):
                 # refused before any row moved, by a decision every rank takes alike from all-reduced
                 # counts / memory flags (a rank would hold no rows or 2^31+ rows, or lacks device

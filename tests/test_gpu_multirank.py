@@ -211,6 +211,82 @@ def test_emulated_owner_sharded_ranks_match_oracle(world, n, k, levels, vcov):
         np.testing.assert_array_equal(res["se"], out[0]["se"])
 
 
+def _run_owned_cl(world, n_total, k, levels, vcov, cl, seed, weights=False):
+    """As _run_owned, with cluster columns (global FE codes) and optional weights (the same
+    counter-based draw for every rank's rows, by global row index)."""
+    from leanfe_amd._lib import EmuGroup, Engine
+    from leanfe_amd.dist import owner_range
+
+    group = EmuGroup(world)
+    out, errs = {}, {}
+    P = max(range(len(levels)), key=lambda f: levels[f])
+
+    def worker(rank):
+        try:
+            lo, hi = owner_range(levels[P], rank, world)
+            eng = Engine(0)
+            eng.set_emu(group, rank)
+            eng.synth_load_owned(n_total, k, levels, synth.betas(k), P, lo, hi, seed=seed)
+            cols, codes = eng.copy_inputs()
+            if weights:  # reload the same rows with weights (a function of the row's codes)
+                w = 0.5 + (codes[0] % 7) / 4.0 + (codes[-1] % 3) / 8.0
+                eng.load(list(cols), list(codes), list(levels), w)
+                eng.set_owner(P, lo, hi)
+            if cl:
+                eng.load_clusters([np.ascontiguousarray(codes[f]) for f in cl], [levels[f] for f in cl])
+            out[rank] = dict(first=_solve(eng, vcov, [levels[f] for f in cl] if cl else None),
+                             second=_solve(eng, vcov, [levels[f] for f in cl] if cl else None), rows=eng.n)
+            eng.close()
+        except BaseException as e:  # noqa: BLE001
+            errs[rank] = e
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+    if errs:
+        raise next(iter(errs.values()))
+    return out
+
+
+@pytest.mark.parametrize("world,n,k,levels,vcov,cl,weights", [
+    (4, 800_000, 10, (60_000, 6_000, 600), "cluster", [1, 2], False),  # config-4-shaped: three FEs, CGM
+    (8, 800_000, 10, (60_000, 6_000, 600), "cluster", [1, 2], False),
+    (8, 600_000, 14, (20_000, 4_000, 1_000), "iid", None, False),      # MEGA-shaped
+    (4, 500_000, 5, (30_000, 700), "HC1", None, True),                 # two FEs, weighted
+    (3, 500_000, 4, (12_000, 2_000, 500), "HC1", None, True),          # three FEs, weighted
+])
+def test_emulated_owner_sharded_general_sweeps(world, n, k, levels, vcov, cl, weights):
+    """Owner sharding beyond two unweighted FEs: the general sweeps keep the primary
+    FE's counts, sums (W, Sy), cross term and effects on its owner rank and all-reduce only the other
+    FEs' tables; the stop test is a max over ranks.  Every rank equals the oracle on the whole panel
+    (equal integers, beta / SE at 1e-10), bit-identical across ranks and across repeats."""
+    from oracle import altproj
+
+    seed = 17
+    out = _run_owned_cl(world, n, k, list(levels), vcov, cl, seed, weights)
+    assert sum(out[r]["rows"] for r in range(world)) == n
+    full = dict(synth.panel(n, k, list(levels), seed=seed))
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    if weights:
+        full["w"] = 0.5 + (full["fe1"] % 7) / 4.0 + (full[fes[-1]] % 3) / 8.0
+    xs = [f"x{j + 1}" for j in range(k)]
+    o = altproj.fit(full, "y", xs, fes, vcov=vcov, cluster_cols=[fes[f] for f in cl] if cl else None,
+                    weights="w" if weights else None)
+    for r in range(world):
+        for res in (out[r]["first"], out[r]["second"]):
+            assert res["iterations"] == o["iterations"] and res["n_obs"] == o["n_obs"]
+            assert res["df_resid"] == o["df_resid"] and res["fe_dims"] == list(o["fe_dims"])
+            np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=0)
+            np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
+            np.testing.assert_array_equal(res["beta"], out[0]["first"]["beta"])
+            np.testing.assert_array_equal(res["se"], out[0]["first"]["se"])
+        if cl:
+            assert tuple(out[r]["first"]["n_clusters"]) == tuple(o["n_clusters"])
+
+
 def test_owner_declaration_is_validated():
     from leanfe_amd._lib import Engine
 
