@@ -61,7 +61,35 @@ struct DnBuildArgs {
   int8_t* NB8;            // [bi][qb][h kb] 1 KB: lane (g, i) bytes jj = count (64 kb + 16 g + jj, 16 qb + i)
   uint8_t* FA;            // [bi][hb][fa_stride]: block has a count > 127
   uint8_t* FB;            // [bi][qb][fb_stride]
+  // pre-filter mode (the table built before the singleton marks, every row counted): the
+  // pre-filter counts of both FEs from the table's row / column sums, replacing the layout
+  // histograms; flag: a primary level with more than 65535 rows (a 16-bit cell could have wrapped)
+  int32_t* cntP;
+  int32_t* cntQ;
+  int32_t* flag;
+  int G_P, G_Q;
 };
+
+// pre-filter mode: row sums of the chunk's counters = the primary counts of its groups (each group is
+// one workgroup's), column sums added into the secondary counts (integer atomics: any order)
+template <typename CT>
+__device__ void dn_counts(const DnBuildArgs& a, const CT* cnt, int hlo, int HW) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int r = wave; r < HW; r += nw) {
+    int s = 0;
+    for (int q = lane; q < a.GQW; q += 64) s += (int)cnt[r * a.GQW + q];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+    if (lane == 0 && hlo + r < a.G_P) {
+      a.cntP[hlo + r] = s;
+      if (s > 65535) atomicOr(a.flag, 1);
+    }
+  }
+  for (int q = threadIdx.x; q < a.G_Q; q += blockDim.x) {
+    int s = 0;
+    for (int r = 0; r < HW; ++r) s += (int)cnt[r * a.GQW + q];
+    if (s) atomicAdd(&a.cntQ[q], s);
+  }
+}
 
 // Counts of the bucket's kept rows with h in [hlo, hlo + HW) into LDS counters of CT (8 or 16
 // bits, packed in 32-bit words: cnt[h - hlo][q]); returns whether some 8-bit counter overflowed.
@@ -226,6 +254,7 @@ __global__ __launch_bounds__(1024) void k_dn_build(DnBuildArgs a) {
   const int HC = a.B / a.nch, hlo = (b << a.s) + chunk * HC, hb0 = chunk * (HC / 16);
   if (HC == 2 * kDnHC) {
     if (!dn_count<uint8_t>(a, cw, hlo, HC, r0, r1)) {
+      if (a.cntP) dn_counts<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), hlo, HC);
       if (a.dn8) dn_write8<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
       else dn_write<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
       return;
@@ -233,12 +262,14 @@ __global__ __launch_bounds__(1024) void k_dn_build(DnBuildArgs a) {
     for (int half = 0; half < 2; ++half) {
       __syncthreads();
       dn_count<uint16_t>(a, cw, hlo + half * kDnHC, kDnHC, r0, r1);
+      if (a.cntP) dn_counts<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), hlo + half * kDnHC, kDnHC);
       if (a.dn8) dn_write8<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
       else dn_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
     }
     return;
   }
   dn_count<uint16_t>(a, cw, hlo, HC, r0, r1);
+  if (a.cntP) dn_counts<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), hlo, HC);
   if (a.dn8) dn_write8<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0, HC);
   else dn_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0, HC);
 }
@@ -654,192 +685,172 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
   }
 }
 
-// Streaming forms of the two passes (the default where the k range fits LDS: K1 <= 16 k blocks,
-// K2 <= 8).  The passes move ~100 MB of i8 table each and ~2 MFMA-microseconds of work, so their
-// time is the table's latency-bound streaming: every wave keeps the next output block's whole
-// k range of A fragments (16 x 16 B per lane) in flight while it computes the current one, with the
-// digit fragments staged once per workgroup (K1: all of alpha_Q's, persistent workgroups, one per
-// CU; K2: the bucket's, two workgroups per bucket and CU).
+// Streaming forms of the two passes (the default where the k range fits LDS: K1 <= 16 k blocks of
+// alpha_Q digits, K2 <= 8).  A pass moves ~100 MB of i8 table against ~2 MFMA-microseconds of
+// work: its time is the table's streaming.  Every wave walks the flattened (output block, k block)
+// steps of its output blocks with a ring of kDn8Ring A fragments in flight (a load issued 8 steps
+// before its MFMAs, across block boundaries), the 8 digit fragments of a step read from LDS into
+// separate registers before its 8 MFMAs; per 8 k blocks (one digit tile) the int32 sums go to f64.
+// The digit tiles are formed in the workgroup's prologue (K1: all of alpha_Q, persistent
+// workgroups, one per CU; K2: the bucket's alpha_P rows, two workgroups per CU).
 constexpr int kDn8MaxKb = 16;
+constexpr int kDn8Ring = 8;
 
-template <int MK>  // k blocks held (16: K1, 8: K2)
-struct Dn8Blk {
-  v4i A[MK];
-  uint64_t fw[2];  // the block's flag words (tiles 0, 1)
-};
-
-template <int MK>
-__device__ __forceinline__ void dn8_load_blk(Dn8Blk<MK>& x, const Dn8Args& a, int64_t blk_row, int lane) {
-  const int8_t* nm = a.Nm + blk_row * a.nkb * 1024 + lane * 16;
+// the steps of one wave: output blocks first, first + stride, ... < end (table rows base + i)
+template <bool K2>
+__device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* __restrict__ fr,
+                                                const double* __restrict__ sc, int64_t base, int first, int stride,
+                                                int end, int lane) {
+  const int g = lane >> 4, c = lane & 15, p = a.p, nkb = a.nkb;
+  if (first >= end) return;
+  const int nblk = (end - first + stride - 1) / stride;
+  const int steps = nblk * nkb;
+  const int8_t* tab = a.Nm + lane * 16;
+  v4i A[kDn8Ring];
+  // load cursor: step jl -> (row rl, k block kl)
+  int64_t rl = base + first;
+  int kl = 0;
+  auto adv_l = [&]() {
+    if (++kl == nkb) {
+      kl = 0;
+      rl += stride;
+    }
+  };
 #pragma unroll
-  for (int k = 0; k < MK; ++k) x.A[k] = *reinterpret_cast<const v4i*>(nm + (int64_t)min(k, a.nkb - 1) * 1024);
-  const uint8_t* fl = a.flags + blk_row * a.fstride;
-  x.fw[0] = *reinterpret_cast<const uint64_t*>(fl);
-  x.fw[1] = (MK > 8 && a.nkb > 8) ? *reinterpret_cast<const uint64_t*>(fl + 8) : 0ull;
-}
-
-// T of one output block (16 rows x 16 columns; lane (g, c) holds rows 4 g + x of column c) from its
-// A fragments and the staged digit tiles fr [tile][kb][d][1 KB] with scales sc [tile][16]
-template <bool K2, int MK>
-__device__ __forceinline__ void dn8_block(const Dn8Blk<MK>& x, const Dn8Args& a, const int8_t* fr, const double* sc,
-                                          int bi, int rb, int lo, int lane, double (&acc)[4]) {
-  const int g = lane >> 4, c = lane & 15, p = a.p;
+  for (int u = 0; u < kDn8Ring; ++u) {
+    if (u < steps) A[u] = *reinterpret_cast<const v4i*>(tab + (rl * nkb + kl) * 1024);
+    adv_l();
+  }
+  // consume cursor
+  int64_t rc = base + first;
+  int kc = 0;
+  v4i D[8];
 #pragma unroll
-  for (int t = 0; t < MK / 8; ++t) {
-    if (t * 8 >= a.nkb) break;  // uniform
-    v4i D[8];
+  for (int d = 0; d < 8; ++d) D[d] = v4i{0, 0, 0, 0};
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  uint64_t fw0 = 0, fw1 = 0;
+  for (int j0 = 0; j0 < steps; j0 += kDn8Ring) {
 #pragma unroll
-    for (int d = 0; d < 8; ++d) D[d] = v4i{0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (t * 8 + k >= a.nkb) break;  // uniform
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        const v4i bv = *reinterpret_cast<const v4i*>(fr + ((t * 8 + k) * 8 + d) * 1024 + lane * 16);
-        D[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x.A[t * 8 + k], bv, D[d], 0, 0, 0);
+    for (int u = 0; u < kDn8Ring; ++u) {
+      if (j0 + u >= steps) break;  // uniform
+      if (kc == 0) {  // the block's flag words (read at its first step, used at its tile ends)
+        const uint8_t* fl = a.flags + rc * a.fstride;
+        fw0 = *reinterpret_cast<const uint64_t*>(fl);
+        fw1 = nkb > 8 ? *reinterpret_cast<const uint64_t*>(fl + 8) : 0ull;
       }
-    }
-    const double s0 = sc[t * 16 + c];
-    double ts[4] = {0.0, 0.0, 0.0, 0.0};
+      const v4i av = A[u];
+      if (j0 + u + kDn8Ring < steps) A[u] = *reinterpret_cast<const v4i*>(tab + (rl * nkb + kl) * 1024);
+      adv_l();
 #pragma unroll
-    for (int d = 7; d >= 0; --d) {
-      const double sd = ldexp(s0, 7 * d);
+      for (int h = 0; h < 2; ++h) {  // the digit fragments in two halves of four (register pressure)
+        v4i bv[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ts[q] += (double)D[d][q] * sd;
-    }
+        for (int d = 0; d < 4; ++d) bv[d] = *reinterpret_cast<const v4i*>(fr + (kc * 8 + 4 * h + d) * 1024 + lane * 16);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] += ts[q];
-    const uint64_t fw = x.fw[t];
-    if (fw == 0) continue;  // a flagged block (a count over 127) is rare
-    for (int k = 0; k < 8 && t * 8 + k < a.nkb; ++k) {
-      if (!((fw >> (8 * k)) & 0xff)) continue;
-      const int kb = t * 8 + k;
-      const uint16_t* X = a.X + (((int64_t)bi * a.nrb + rb) * a.nkb + kb) * 1024;
+        for (int d = 0; d < 4; ++d) D[4 * h + d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv[d], D[4 * h + d], 0, 0, 0);
+      }
+      if ((kc & 7) == 7 || kc == nkb - 1) {  // a digit tile ends: its exact sums to f64, then its flagged blocks
+        const int t = kc >> 3;
+        const double s0 = sc[t * 16 + c];
+        double ts[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double sx = 0.0;
-        for (int jj = 0; jj < 64; ++jj) {
-          const int kr = kb * 64 + jj;
-          double al = 0.0;
-          if (c < p) {
-            if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * p + c] : 0.0;
-            else al = kr < a.G_Q ? a.alpha[(int64_t)kr * p + c] : 0.0;
-          }
-          sx += (double)X[(4 * g + q) * 64 + jj] * al;
+        for (int d = 7; d >= 0; --d) {
+          const double sd = ldexp(s0, 7 * d);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ts[q] += (double)D[d][q] * sd;
+          D[d] = v4i{0, 0, 0, 0};
         }
-        acc[q] += sx;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += ts[q];
+        const uint64_t fw = t ? fw1 : fw0;
+        if (fw != 0) {  // rare: blocks with a count over 127, summed in f64 from their u16 counts
+          const int bi = (int)(rc / a.nrb), rb = (int)(rc - (int64_t)bi * a.nrb);
+          const int lo = a.blist[bi] << a.s;
+          for (int k = 0; k < 8 && t * 8 + k < nkb; ++k) {
+            if (!((fw >> (8 * k)) & 0xff)) continue;
+            const int kb = t * 8 + k;
+            const uint16_t* X = a.X + (((int64_t)bi * a.nrb + rb) * nkb + kb) * 1024;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              double sx = 0.0;
+              for (int jj = 0; jj < 64; ++jj) {
+                const int kr = kb * 64 + jj;
+                double al = 0.0;
+                if (c < p) {
+                  if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * p + c] : 0.0;
+                  else al = kr < a.G_Q ? a.alpha[(int64_t)kr * p + c] : 0.0;
+                }
+                sx += (double)X[(4 * g + q) * 64 + jj] * al;
+              }
+              acc[q] += sx;
+            }
+          }
+        }
+      }
+      if (kc == nkb - 1) {  // the block's outputs: lane (g, c) holds rows 16 rb + 4 g + q of column c
+        const int bi = (int)(rc / a.nrb), rb = (int)(rc - (int64_t)bi * a.nrb);
+        if (c < p) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = rb * 16 + 4 * g + q;
+            if (K2) {
+              if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * p + c] = acc[q];
+            } else {
+              const int h = (a.blist[bi] << a.s) + row;
+              if (row < a.B && h < a.G_P) {
+                const int32_t n = a.cntP[h];
+                const int64_t e = (int64_t)h * p + c;
+                a.alphaP[e] = n > 0 ? (a.S_P[e] - acc[q]) / (double)n : 0.0;
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = 0.0;
+      }
+      if (++kc == nkb) {
+        kc = 0;
+        rc += stride;
       }
     }
   }
 }
 
-// K1, persistent: workgroup i takes output blocks [i T / grid, (i + 1) T / grid) of the T = nbe x B/16
-// primary blocks, wave w every W-th of them
-__global__ __launch_bounds__(512) void k_dn8_k1s(Dn8Args a) {
+// K1, persistent: the digit tiles of alpha_Q formed in LDS by every workgroup, then workgroup i takes
+// output blocks [i T / grid, (i + 1) T / grid) of the T = nbe x B/16 primary blocks, wave w every 16th
+__global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
   extern __shared__ __attribute__((aligned(16))) int8_t fr[];  // [ntile][8 kb][8 d][1 KB]
+  __shared__ double red[1024 + 16];
   __shared__ double sc[32];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), W = blockDim.x >> 6;
-  const int g = lane >> 4, c = lane & 15, p = a.p;
   if (a.zero_check && blockIdx.x == 0 && tid == 0) *a.zero_check = 0.0;
-  const int64_t total = (int64_t)a.nbe * a.nrb;
-  const int64_t i0 = total * blockIdx.x / gridDim.x, i1 = total * (blockIdx.x + 1) / gridDim.x;
-  Dn8Blk<16> xa, xb;
-  if (i0 + wave < i1) dn8_load_blk(xa, a, i0 + wave, lane);  // in flight while the tiles stage
-  {
-    const int n4 = a.nkb * 512;  // int4 of the staged tiles
-    const int4* s4 = reinterpret_cast<const int4*>(a.dq);
-    int4* d4p = reinterpret_cast<int4*>(fr);
-    constexpr int kStage = 8;
-    for (int j0 = 0; j0 < n4; j0 += kStage * (int)blockDim.x) {
-      int4 tmp[kStage];
-#pragma unroll
-      for (int u = 0; u < kStage; ++u) {
-        const int j = j0 + u * (int)blockDim.x + tid;
-        tmp[u] = j < n4 ? s4[j] : int4{0, 0, 0, 0};
-      }
-#pragma unroll
-      for (int u = 0; u < kStage; ++u) {
-        const int j = j0 + u * (int)blockDim.x + tid;
-        if (j < n4) d4p[j] = tmp[u];
-      }
-    }
-    if (tid < 32) sc[tid] = tid < 16 * ((a.nkb + 7) / 8) ? a.eq[tid] : 0.0;
+  const int ntile = (a.nkb + 7) / 8;
+  for (int t = 0; t < ntile; ++t) {
+    if (t) __syncthreads();
+    dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.p, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p,
+                          fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red);
   }
   __syncthreads();
-  auto finish = [&](int64_t i, const double (&acc)[4]) {
-    const int bi = (int)(i / a.nrb), rb = (int)(i - (int64_t)bi * a.nrb);
-    if (c >= p) return;
-    const int lo = a.blist[bi] << a.s;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = rb * 16 + 4 * g + q, h = lo + row;
-      if (row < a.B && h < a.G_P) {
-        const int32_t n = a.cntP[h];
-        const int64_t e = (int64_t)h * p + c;
-        a.alphaP[e] = n > 0 ? (a.S_P[e] - acc[q]) / (double)n : 0.0;
-      }
-    }
-  };
-  for (int64_t i = i0 + wave; i < i1; i += 2 * W) {
-    if (i + W < i1) dn8_load_blk(xb, a, i + W, lane);
-    {
-      const int bi = (int)(i / a.nrb), rb = (int)(i - (int64_t)bi * a.nrb);
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      dn8_block<false>(xa, a, fr, sc, bi, rb, 0, lane, acc);
-      finish(i, acc);
-    }
-    if (i + W >= i1) break;
-    if (i + 2 * W < i1) dn8_load_blk(xa, a, i + 2 * W, lane);
-    {
-      const int64_t j = i + W;
-      const int bi = (int)(j / a.nrb), rb = (int)(j - (int64_t)bi * a.nrb);
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      dn8_block<false>(xb, a, fr, sc, bi, rb, 0, lane, acc);
-      finish(j, acc);
-    }
-  }
+  const int64_t total = (int64_t)a.nbe * a.nrb;
+  const int i0 = (int)(total * blockIdx.x / gridDim.x), i1 = (int)(total * (blockIdx.x + 1) / gridDim.x);
+  dn8_wave_stream<false>(a, fr, sc, 0, i0 + wave, W, i1, lane);
 }
 
-// K2: workgroup (bucket bi, part j of np): digitizes the bucket's alpha_P rows, then output blocks
-// [j nrb / np, (j + 1) nrb / np) of the bucket's secondary blocks, wave w every W-th
-__global__ __launch_bounds__(512) void k_dn8_k2s(Dn8Args a, int np) {
+// K2: workgroup (bucket bi, part j of np): the bucket's alpha_P rows digitized in LDS, then output
+// blocks [j nrb / np, (j + 1) nrb / np) of the bucket's secondary blocks, wave w every 8th
+__global__ __launch_bounds__(512, 4) void k_dn8_k2s(Dn8Args a, int np) {
   extern __shared__ __attribute__((aligned(16))) int8_t fr[];  // [8 kb][8 d][1 KB]
   __shared__ double red[512 + 16];
-  __shared__ double sc[32];
+  __shared__ double sc[16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), W = blockDim.x >> 6;
-  const int g = lane >> 4, c = lane & 15, p = a.p;
   const int bi = blockIdx.x / np, part = blockIdx.x - bi * np;
   const int lo = a.blist[bi] << a.s;
-  const int i0 = a.nrb * part / np, i1 = a.nrb * (part + 1) / np;
-  Dn8Blk<8> xa, xb;
-  if (i0 + wave < i1) dn8_load_blk(xa, a, (int64_t)bi * a.nrb + i0 + wave, lane);
-  dn8_tile_digits<512>(a.alpha + (int64_t)lo * p, max(0, min(a.B, a.G_P - lo)), p, fr, sc, red);
+  dn8_tile_digits<512>(a.alpha + (int64_t)lo * a.p, max(0, min(a.B, a.G_P - lo)), a.p, fr, sc, red);
   __syncthreads();
-  auto finish = [&](int rb, const double (&acc)[4]) {
-    if (c >= p) return;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = rb * 16 + 4 * g + q;
-      if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * p + c] = acc[q];
-    }
-  };
-  for (int i = i0 + wave; i < i1; i += 2 * W) {
-    if (i + W < i1) dn8_load_blk(xb, a, (int64_t)bi * a.nrb + i + W, lane);
-    {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      dn8_block<true>(xa, a, fr, sc, bi, i, lo, lane, acc);
-      finish(i, acc);
-    }
-    if (i + W >= i1) break;
-    if (i + 2 * W < i1) dn8_load_blk(xa, a, (int64_t)bi * a.nrb + i + 2 * W, lane);
-    {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      dn8_block<true>(xb, a, fr, sc, bi, i + W, lo, lane, acc);
-      finish(i + W, acc);
-    }
-  }
+  const int i0 = a.nrb * part / np, i1 = a.nrb * (part + 1) / np;
+  dn8_wave_stream<true>(a, fr, sc, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -854,6 +865,11 @@ static int64_t dn_cells(const lfe_ctx* c) {
 
 static int dn_gq64(const lfe_ctx* c) { return (c->fe[1 - c->L.P].G + 63) / 64 * 64; }
 
+// cells of the tables dense_build writes (i8 tables: GQ64 columns)
+int64_t dense_table_cells(const lfe_ctx* c) {
+  return c->dn8 ? (int64_t)std::max(c->nbe, 1) * ((int64_t)1 << c->L.s) * dn_gq64(c) : dn_cells(c);
+}
+
 // the exact i8 passes: the counters of a 64-group chunk of GQ64 columns fit the build's LDS, the
 // bucket is whole 64-row k blocks (LFE_DN8=0: the f64 passes, for A/B)
 static bool dn8_tiled() {  // A/B: the tiled forms of the i8 passes
@@ -866,6 +882,24 @@ static bool dn8_ok(const lfe_ctx* c) {
   if (e && e[0] == '0') return false;
   const int64_t B = 1ll << c->L.s;
   return B % 64 == 0 && (size_t)kDnHC * dn_gq64(c) * 2 <= 150 * 1024 && c->p <= 16;
+}
+
+static bool dn8_ok(const lfe_ctx* c);
+
+// before the singleton marks (prepare_layout, two-FE item path): build the i8 tables on every row and
+// take the pre-filter counts from them (dense_build(c, true)) where the dense passes would run on a
+// panel without drops (the cmax bound is checked on the device) - LFE_DN_PRE=0 turns it off
+bool dense_pre_ok(const lfe_ctx* c) {
+  const char* e = getenv("LFE_DENSE");
+  if (e && e[0] == '0') return false;
+  const char* pe = getenv("LFE_DN_PRE");
+  if (pe && pe[0] == '0') return false;
+  const int P = c->L.P, Q = 1 - P, p = c->p;
+  if (!(c->world == 1 || c->owner_on) || p > 16 || c->nbe < 1 || !dn8_ok(c)) return false;
+  const int64_t B = 1ll << c->L.s, GQ16 = ((int64_t)c->fe[Q].G + 15) / 16 * 16;
+  if (B % kDnHC != 0) return false;
+  if (GQ16 * p * 8 > 100 * 1024 || B * p * 8 > 64 * 1024) return false;
+  return (e && e[0] == '1') || (double)c->n >= 0.3 * (double)dn_cells(c);
 }
 
 bool dense_ok(const lfe_ctx* c) {
@@ -885,7 +919,7 @@ bool dense_ok(const lfe_ctx* c) {
   return true;
 }
 
-int dense_build(lfe_ctx* c) {
+int dense_build(lfe_ctx* c, bool pre) {
   auto& L = c->L;
   const int Q = 1 - L.P;
   const int B = 1 << L.s, GQ16 = (c->fe[Q].G + 15) / 16 * 16;
@@ -897,6 +931,13 @@ int dense_build(lfe_ctx* c) {
   LFE_TRY(ensure_u16(c, c->dn_nb, c->dn_nb_cap, cells));
   DnBuildArgs a{};
   a.GQW = GQW;
+  a.G_P = c->fe[L.P].G;
+  a.G_Q = c->fe[Q].G;
+  if (pre) {
+    a.cntP = c->fe[L.P].cnt_pre;
+    a.cntQ = c->fe[Q].cnt_pre;
+    a.flag = c->iscratch + kIsDnPre;
+  }
   if (c->dn8) {
     const int nbe = std::max(c->nbe, 1);
     a.dn8 = 1;
@@ -1003,13 +1044,6 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
   if (c->dn8) {
     Dn8Args a = dn8_args(c);
     const int GQ64 = dn_gq64(c), nkb = GQ64 / 64, ntile = (nkb + 7) / 8;
-    LFE_TRY(ensure_i8(c, c->dn8_dq, c->dn8_dq_cap, (size_t)ntile * kDn8TileBytes));
-    LFE_TRY(ensure_f64(c, c->dn8_eq, c->dn8_eq_cap, (size_t)ntile * 16));
-    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_digits), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kDn8TileBytes));
-    hipLaunchKernelGGL(k_dn8_digits, dim3(ntile), dim3(256), kDn8TileBytes, c->stream, alphaQ, a.G_Q, a.p, c->dn8_dq,
-                       c->dn8_eq);
-    LFE_HIP(hipGetLastError());
     a.Nm = c->dn8_a;
     a.flags = c->dn8_fa;
     a.fstride = (nkb + 7) / 8 * 8;
@@ -1023,16 +1057,24 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
     a.cntP = c->fe[P].cnt;
     a.alphaP = c->fe[P].alpha;
     a.zero_check = zero_check;
-    if (nkb <= kDn8MaxKb && !dn8_tiled()) {  // persistent streaming form (LFE_DN8_TILED: A/B)
+    if (nkb <= kDn8MaxKb && !dn8_tiled()) {  // persistent streaming form (LFE_DN8_TILED=1: A/B)
       const size_t lds = (size_t)ntile * kDn8TileBytes;
       LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k1s), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
       const int64_t total = (int64_t)std::max(c->nbe, 1) * a.nrb;
-      const int grid = (int)std::min<int64_t>(c->n_cu, (total + 7) / 8);
-      hipLaunchKernelGGL(k_dn8_k1s, dim3(grid), dim3(512), lds, c->stream, a);
+      const int grid = (int)std::min<int64_t>(c->n_cu, (total + 15) / 16);
+      hipLaunchKernelGGL(k_dn8_k1s, dim3(grid), dim3(1024), lds, c->stream, a);
       LFE_HIP(hipGetLastError());
       return LFE_OK;
     }
+    // tiled form: alpha_Q's digit tiles formed once per pass by k_dn8_digits
+    LFE_TRY(ensure_i8(c, c->dn8_dq, c->dn8_dq_cap, (size_t)ntile * kDn8TileBytes));
+    LFE_TRY(ensure_f64(c, c->dn8_eq, c->dn8_eq_cap, (size_t)ntile * 16));
+    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_digits), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kDn8TileBytes));
+    hipLaunchKernelGGL(k_dn8_digits, dim3(ntile), dim3(256), kDn8TileBytes, c->stream, alphaQ, a.G_Q, a.p, c->dn8_dq,
+                       c->dn8_eq);
+    LFE_HIP(hipGetLastError());
     constexpr int waves = 4;
     a.rbw = dn8_rbw(c, a.nrb, waves);
     return dn8_launch<false>(c, a, waves, std::max(c->nbe, 1) * ((a.nrb + a.rbw - 1) / a.rbw));

@@ -21,6 +21,7 @@ constexpr int kColStatHead = 64; // colstat: max |x_c| bits of every column befo
 // iscratch (prepare_layout): [2 F] level counts, [2 kMaxFE] dropped rows, [+1] any-singleton flag,
 // [kIscratchCmax, + F) largest kept count per FE
 constexpr int kIscratchCmax = 2 * kMaxFE + 8;
+constexpr int kIsDnPre = 2 * kMaxFE + 6;  // iscratch: a primary level of > 65535 rows in the pre-filter table build
 constexpr int kIscratchInts = kIscratchCmax + kMaxFE;
 constexpr int kBlock = 256;      // threads per workgroup for simple streaming kernels
 constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
@@ -304,6 +305,8 @@ struct lfe_ctx {
   bool raw_ready = false;        // raw_tile holds this layout's kept rows
   bool tq_final = false;         // fe[Q].T = sum over q of the final alpha_P (demean_fast)
   bool hists_kept = false;       // seg_aux holds the kept rows' per-item histograms (no row dropped)
+  bool dn_pre = false;           // prepare_layout built the dense tables on every row (pre-filter counts)
+  bool dn_pre_valid = false;     // ... and they hold the kept rows (nothing dropped, no 16-bit overflow)
   bool sums_zeroed = false;      // prepare_layout zeroed the S tables (sums4 skips its memsets)
   // scratch
   double* scratch = nullptr;     // device partials
@@ -412,7 +415,9 @@ int layout_hists(lfe_ctx* c, int Q);              // per-item histograms of both
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out);
 // lfe_dense.hip: the two-FE cross terms as count-table products on the matrix cores
 bool dense_ok(const lfe_ctx* c);
-int dense_build(lfe_ctx* c);
+int dense_build(lfe_ctx* c, bool pre = false);  // pre: before the marks, every row, with the pre-filter counts
+bool dense_pre_ok(const lfe_ctx* c);
+int64_t dense_table_cells(const lfe_ctx* c);
 int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check);
 int dense_tq(lfe_ctx* c, double* runs);
 // the secondary effects' digit fragments for the exact K1 pass (after every alpha_Q update)

@@ -1173,11 +1173,13 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   const int NT = (p + 15) / 16;
   // dense count tables where the primary x secondary table holds >= ~0.15 rows per cell (both
   // cross terms on the matrix cores, lfe_dense.hip); else the segment / run layouts
-  const bool dense = dense_ok(c);
+  // the tables prepare_layout built on every row hold the kept rows when nothing was dropped
+  const bool dense = c->dn_pre_valid || dense_ok(c);
   c->dense_cells = 0;
   if (dense) {
     c->hists_kept = false;
-    LFE_TRY(dense_build(c));
+    if (c->dn_pre_valid) c->dense_cells = dense_table_cells(c);
+    else LFE_TRY(dense_build(c));
   } else {
     LFE_TRY(build_layouts(c, Q));
   }

@@ -1072,7 +1072,14 @@ int prepare_layout(lfe_ctx* c) {
   }
   LFE_TRY(build_items(c, L.permuted));
 
-  if (item_counts) {
+  c->dn_pre = c->dn_pre_valid = false;
+  if (item_counts && dense_pre_ok(c)) {
+    // the dense cross terms will run: their count tables, built on every row now, give both FEs'
+    // pre-filter counts (row / column sums) in place of the layout histograms, and serve the sweeps
+    // as they are when no row is dropped
+    LFE_TRY(dense_build(c, true));
+    c->dn_pre = true;
+  } else if (item_counts) {
     const int Q = 1 - L.P, B = 1 << L.s;
     LFE_TRY(layout_hists(c, Q));
     ProfScope _ps(c, K_COUNT);
@@ -1168,7 +1175,8 @@ int prepare_layout(lfe_ctx* c) {
     c->fe[f].card = h[2 * f + 1];
     c->fe[f].cmax = h[kIscratchCmax + f];
   }
-  c->hists_kept = item_counts && h[2 * kMaxFE] == 0;
+  c->hists_kept = item_counts && !c->dn_pre && h[2 * kMaxFE] == 0;
+  c->dn_pre_valid = c->dn_pre && h[2 * kMaxFE] == 0 && h[kIsDnPre] == 0;
   // kept rows over all ranks (owner-sharded: with the primary FE's level counts, which each
   // rank has for its own levels only; integers < 2^53 are exact in f64)
   double kept[3] = {(double)(n - h[2 * kMaxFE]), 0.0, 0.0};

@@ -58,3 +58,16 @@ def test_config5_500m_rows_emulated_ranks_vs_c_oracle():
         assert line["ints_equal"], line
         assert line["max_rel_beta"] < 1e-10 and line["max_rel_se"] < 1e-10, line
         assert line["ranks_bit_identical"] and line["repeat_bit_identical"], line
+
+
+@pytest.mark.parametrize("preset", ["hdfe_base", "hdfe_cluster1", "hdfe_cluster2", "uhdfe_base", "uhdfe_cluster2",
+                                    "mega_base", "mega_cluster2"])
+@pytest.mark.timeout(900)
+def test_reference_panel_vs_c_oracle(preset):
+    """The reference's own benchmark panels (bench.PRESETS: python/tests/create_data.py:143-194 shapes,
+    reg_test.py:26-97 formulas and cluster columns) at full size - 15M / 50M rows, k = 4 / 14 / 20,
+    two and three FEs, IID and one / two-way clustered SEs - through bench.solve_step against the C
+    restatement of the reference: integers equal, beta / SE at 1e-10, bit-identical repeats."""
+    import config_runs
+
+    _check(config_runs.run(preset))
