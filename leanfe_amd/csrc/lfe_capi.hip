@@ -446,6 +446,7 @@ static void free_data(lfe_ctx* c) {
   dfree(c->dn8_eq);
   c->dn8_a_cap = c->dn8_b_cap = c->dn8_fa_cap = c->dn8_fb_cap = c->dn8_dq_cap = c->dn8_eq_cap = 0;
   c->dn8 = false;
+  free_dense3(c);
   dfree(c->raw_slots);
   c->raw_slots_cap = 0;
   dfree(c->amax);
@@ -1116,6 +1117,7 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
   }
   if (check_from > 0 && max_iter < 1) return fail(LFE_EINVAL, "max_iter must be >= 1");
   c->dense_cells = 0;  // demean_fast sets it when the dense cross terms run
+  c->d3.on = false;    // ... demean_dense3 this
   int iterations = 0;
   double last = -1.0;
   c->tq_final = false;
@@ -1133,6 +1135,9 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
       if (fast) {
         // two FEs, unweighted: segment layout + one fused codes-only kernel per sweep
         LFE_TRY(demean_fast(c, tol, max_iter, check_from, &iterations, &last));
+      } else if (dense3_ok(c, order, check_from)) {
+        // three or more FEs, unweighted, small pair tables: every cross term on the matrix cores
+        LFE_TRY(demean_dense3(c, order, tol, max_iter, check_from, &iterations, &last));
       } else {
         LFE_TRY(demean_generic(c, order, tol, max_iter, check_from, &iterations, &last));
       }

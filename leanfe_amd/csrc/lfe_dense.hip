@@ -458,13 +458,13 @@ __device__ __forceinline__ void dn8_split(double v, double sin, int (&dg)[8]) {
 // non-finite value, so that it propagates), by a block of NT threads.  Thread t holds column t & 15
 // of RPT consecutive rows in registers: one round of loads, no dependent load chain.
 template <int NT>
-__device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p, int8_t* __restrict__ fr,
+__device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p, int ld, int8_t* __restrict__ fr,
                                 double* __restrict__ sc, double* __restrict__ red) {
   constexpr int RPT = kDn8Tile * 16 / NT;  // rows per thread (32 or 16)
   const int tid = threadIdx.x, col = tid & 15, r0 = (tid >> 4) * RPT;
   double v[RPT];
 #pragma unroll
-  for (int u = 0; u < RPT; ++u) v[u] = (col < p && r0 + u < rows) ? src[(int64_t)(r0 + u) * p + col] : 0.0;
+  for (int u = 0; u < RPT; ++u) v[u] = (col < p && r0 + u < rows) ? src[(int64_t)(r0 + u) * ld + col] : 0.0;
   double m = 0.0;
   bool bad = false;
 #pragma unroll
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(256) void k_dn8_digits(const double* __restrict__ a
   __shared__ double red[256 + 16];
   __shared__ double sc[16];
   const int t = blockIdx.x, r0 = t * kDn8Tile;
-  dn8_tile_digits<256>(alpha + (int64_t)r0 * p, min(kDn8Tile, G - r0), p, fr, sc, red);
+  dn8_tile_digits<256>(alpha + (int64_t)r0 * p, min(kDn8Tile, G - r0), p, p, fr, sc, red);
   __syncthreads();
   const int4* s4 = reinterpret_cast<const int4*>(fr);
   int4* d4p = reinterpret_cast<int4*>(dq + (int64_t)t * kDn8TileBytes);
@@ -528,6 +528,7 @@ struct Dn8Args {
   const uint16_t* X;      // the flagged blocks' u16 counts (16 x 64, natural order)
   const int32_t* blist;
   int nbe, s, B, G_Q, G_P, p;
+  int lda, ldo;           // K2: row strides of alpha_P and of the slots (p for the two-FE passes)
   int nkb;                // 64-row k blocks per output block (K1: GQ64 / 64, K2: B / 64)
   int nrb;                // output blocks per bucket (K1: B / 16, K2: GQ64 / 16)
   int rbw;                // output blocks per workgroup
@@ -576,8 +577,8 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
     __syncthreads();
     if (K2) {
       const int r0 = lo + t * kDn8Tile;
-      dn8_tile_digits<512>(a.alpha + (int64_t)r0 * p, max(0, min(kDn8Tile, min(a.B - t * kDn8Tile, a.G_P - r0))),
-                           p, fr, sc, red);
+      dn8_tile_digits<512>(a.alpha + (int64_t)r0 * a.lda, max(0, min(kDn8Tile, min(a.B - t * kDn8Tile, a.G_P - r0))),
+                           p, a.lda, fr, sc, red);
     } else {
       // the tile's fragments, every load of a thread issued before its stores (4 KB per thread
       // round: no chain of L2 round trips)
@@ -653,7 +654,7 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
             const int kr = kr0 + jj;
             double al = 0.0;
             if (c < p) {
-              if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * p + c] : 0.0;
+              if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * a.lda + c] : 0.0;
               else al = kr < a.G_Q ? a.alpha[(int64_t)kr * p + c] : 0.0;
             }
             sx += (double)X[(4 * g + x) * 64 + jj] * al;
@@ -672,7 +673,7 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
     for (int x = 0; x < 4; ++x) {
       const int row = rb * 16 + 4 * g + x;
       if (K2) {
-        if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * p + c] = acc[r][x];
+        if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * a.ldo + c] = acc[r][x];
       } else {
         const int h = lo + row;
         if (row < a.B && h < a.G_P) {
@@ -777,7 +778,7 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
                 const int kr = kb * 64 + jj;
                 double al = 0.0;
                 if (c < p) {
-                  if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * p + c] : 0.0;
+                  if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * a.lda + c] : 0.0;
                   else al = kr < a.G_Q ? a.alpha[(int64_t)kr * p + c] : 0.0;
                 }
                 sx += (double)X[(4 * g + q) * 64 + jj] * al;
@@ -794,7 +795,7 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
           for (int q = 0; q < 4; ++q) {
             const int row = rb * 16 + 4 * g + q;
             if (K2) {
-              if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * p + c] = acc[q];
+              if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * a.ldo + c] = acc[q];
             } else {
               const int h = (a.blist[bi] << a.s) + row;
               if (row < a.B && h < a.G_P) {
@@ -828,7 +829,7 @@ __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
   const int ntile = (a.nkb + 7) / 8;
   for (int t = 0; t < ntile; ++t) {
     if (t) __syncthreads();
-    dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.p, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p,
+    dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.p, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p, a.p,
                           fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red);
   }
   __syncthreads();
@@ -847,7 +848,7 @@ __global__ __launch_bounds__(512, 4) void k_dn8_k2s(Dn8Args a, int np) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), W = blockDim.x >> 6;
   const int bi = blockIdx.x / np, part = blockIdx.x - bi * np;
   const int lo = a.blist[bi] << a.s;
-  dn8_tile_digits<512>(a.alpha + (int64_t)lo * a.p, max(0, min(a.B, a.G_P - lo)), a.p, fr, sc, red);
+  dn8_tile_digits<512>(a.alpha + (int64_t)lo * a.lda, max(0, min(a.B, a.G_P - lo)), a.p, a.lda, fr, sc, red);
   __syncthreads();
   const int i0 = a.nrb * part / np, i1 = a.nrb * (part + 1) / np;
   dn8_wave_stream<true>(a, fr, sc, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane);
@@ -1017,6 +1018,7 @@ static Dn8Args dn8_args(const lfe_ctx* c) {
   a.G_Q = c->fe[Q].G;
   a.G_P = c->fe[P].G;
   a.p = c->p;
+  a.lda = a.ldo = c->p;
   return a;
 }
 
@@ -1134,6 +1136,38 @@ int dense_tq(lfe_ctx* c, double* runs) {
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn_pass<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k_dn_pass<true>, dim3(c->nbe * wgpb), dim3(kDnThreads), lds, c->stream, a);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+// one pair-table pass of the general dense sweeps (lfe_dense3.hip): the K2 streaming kernel with
+// "buckets" = the 512-level tiles of the k-side FE and "secondary levels" = the output FE's levels
+int dn8_pair_pass(lfe_ctx* c, const PairPass& pp) {
+  if (pp.ntile_k < 1 || pp.nrb < 1) return LFE_OK;
+  Dn8Args a{};
+  a.Nm = pp.tab;
+  a.flags = pp.flg;
+  a.fstride = 8;
+  a.X = pp.X;
+  a.blist = pp.tiles;
+  a.nbe = pp.ntile_k;
+  a.s = 9;
+  a.B = kDn8Tile;
+  a.G_Q = pp.G_rows;
+  a.G_P = pp.G_k;
+  a.p = pp.pc;
+  a.lda = pp.lda;
+  a.ldo = pp.ldo;
+  a.nkb = 8;
+  a.nrb = pp.nrb;
+  a.alpha = pp.alpha;
+  a.runs = pp.runs;
+  LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k2s), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kDn8TileBytes));
+  // >= 2 workgroups per CU over the tiles, >= 8 output blocks each
+  int np = (int)std::max<int64_t>(1, (2 * (int64_t)c->n_cu + pp.ntile_k - 1) / pp.ntile_k);
+  np = std::min(np, std::max(1, a.nrb / 8));
+  hipLaunchKernelGGL(k_dn8_k2s, dim3(pp.ntile_k * np), dim3(512), kDn8TileBytes, c->stream, a, np);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
 }

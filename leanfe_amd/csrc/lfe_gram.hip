@@ -1068,60 +1068,92 @@ void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out) {
 // and a trailing update spread over the threads), then the two triangular solves on thread 0.
 // tile: global or LDS.  Every thread of the block must call it (it holds barriers).
 constexpr int kCholM = 12;
-__device__ void chol_solve_block(const double* tile, int p, double* __restrict__ beta, double* __restrict__ beta_copy,
-                                 double* __restrict__ ok, double (*L)[kCholM + 1], double* b, int& bad) {
+// beta_full from the Cholesky factor of the design tile (intercept + the k regressors: tile rows
+// 0, 2, 3, ..), by ONE wave in registers: lane i holds row i of L (columns by register), the
+// column elements other lanes need arrive by shuffles, and the forward / back substitutions run
+// in the order of the serial loops of polars_impl.py:212-226's LAPACK-free restatement (so the
+// bits are those of the one-thread form this replaced: ~1.5 us instead of ~15 us of LDS round trips)
+__device__ void chol_solve_wave(const double* tile, int p, double* __restrict__ beta, double* __restrict__ beta_copy,
+                                double* __restrict__ ok, double (*Ls)[kCholM + 1]) {
   constexpr int M = kCholM;
-  const int t = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int m = p;  // intercept + k regressors
   auto idx = [](int i) { return i == 0 ? 0 : i + 1; };
-  for (int e = t; e < M * M; e += blockDim.x) {
-    const int i = e / M, j = e % M;
-    L[i][j] = (i < m && j < m) ? tile[idx(i) * 16 + idx(j)] : 0.0;
-  }
-  if (t < M) b[t] = t < m ? tile[idx(t) * 16 + 1] : 0.0;
-  if (t == 0) bad = 0;
-  __syncthreads();
-  for (int j = 0; j < m; ++j) {
-    if (t == 0) {
-      const double d = L[j][j];
-      if (!(d > 0.0)) bad = 1;
-      L[j][j] = sqrt(d > 0.0 ? d : 1.0);
+  double r[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) r[k] = (lane < m && k < m) ? tile[idx(lane) * 16 + idx(k)] : 0.0;
+  const double bv = lane < m ? tile[idx(lane) * 16 + 1] : 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    if (j >= m) break;  // uniform
+    const double d = __shfl(r[j], j, 64);
+    bad |= !(d > 0.0);
+    const double ljj = sqrt(d > 0.0 ? d : 1.0);
+    if (lane == j) r[j] = ljj;
+    else if (lane > j && lane < m) r[j] /= ljj;
+#pragma unroll
+    for (int k = j + 1; k < M; ++k) {
+      if (k >= m) break;
+      const double lkj = __shfl(r[j], k, 64);
+      if (lane >= k && lane < m) r[k] -= r[j] * lkj;  // L[i][k] -= L[i][j] L[k][j], j < k <= i
     }
-    __syncthreads();
-    if (t > j && t < m) L[t][j] /= L[j][j];
-    __syncthreads();
-    for (int e = t; e < M * M; e += blockDim.x) {
-      const int i = e / M, k = e % M;
-      if (i > j && k > j && k <= i && i < m) L[i][k] -= L[i][j] * L[k][j];
-    }
-    __syncthreads();
   }
-  if (t != 0) return;
   if (bad) {
-    *ok = 0.0;
+    if (lane == 0) *ok = 0.0;
     return;
   }
-  // in place on the LDS right-hand side (a dynamically indexed private array would live in scratch)
-  for (int i = 0; i < m; ++i) {
-    double v = b[i];
-    for (int k = 0; k < i; ++k) v -= L[i][k] * b[k];
-    b[i] = v / L[i][i];
+  // forward: y_i = (b_i - sum_{k < i} L[i][k] y_k) / L[i][i], the k in ascending order
+  double acc = bv;
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    if (k >= m) break;
+    const double yk = __shfl(acc / r[k], k, 64);  // lane k: r[k] = L[k][k]
+    if (lane == k) acc = yk;
+    else if (lane > k) acc -= r[k] * yk;
   }
-  for (int i = m - 1; i >= 0; --i) {
-    double v = b[i];
-    for (int k = i + 1; k < m; ++k) v -= L[k][i] * b[k];
-    b[i] = v / L[i][i];
+  // back: x_i = (y_i - sum_{k > i} L[k][i] x_k) / L[i][i], k ascending: lane i's column of L via LDS
+  if (lane < m)
+#pragma unroll
+    for (int k = 0; k < M; ++k) Ls[lane][k] = r[k];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  double col[M], xs[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    col[k] = (lane < m && k < m) ? Ls[k][lane] : 0.0;
+    xs[k] = 0.0;
   }
-  for (int i = 0; i < m; ++i) beta[i] = beta_copy[i] = b[i];
-  *ok = 1.0;
+  double diag = 1.0;
+#pragma unroll
+  for (int k = 0; k < M; ++k)
+    if (k == lane) diag = r[k];
+#pragma unroll
+  for (int i = M - 1; i >= 0; --i) {
+    if (i >= m) continue;
+    double v = acc;  // lane i: y_i
+#pragma unroll
+    for (int k = i + 1; k < M; ++k)
+      if (k < m) v -= col[k] * xs[k];
+    const double xi = __shfl(v / diag, i, 64);
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+      if (k == i) xs[k] = xi;
+  }
+  if (lane < m) {
+    double x = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+      if (k == lane) x = xs[k];
+    beta[lane] = beta_copy[lane] = x;
+  }
+  if (lane == 0) *ok = 1.0;
 }
 
 __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __restrict__ beta,
                              double* __restrict__ beta_copy, double* __restrict__ ok) {
   __shared__ double L[kCholM][kCholM + 1];
-  __shared__ double b[kCholM];
-  __shared__ int bad;
-  chol_solve_block(tile, p, beta, beta_copy, ok, L, b, bad);
+  if (threadIdx.x < 64) chol_solve_wave(tile, p, beta, beta_copy, ok, L);
 }
 
 // The design tile from the raw tile + the table partials (16 waves sum the block partials of one
@@ -1139,17 +1171,30 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
   __shared__ double tl[256];
   __shared__ int bad;
   __shared__ double L[kCholM][kCholM + 1];
-  __shared__ double b[kCholM];
-  __shared__ int cbad;
   if (threadIdx.x == 0) bad = 0;
   {
+    // wave w sums entries w, w + 16, ..; lane l the blocks l, l + 64, .. (<= 256 blocks) in that
+    // order: every load issued before the first add
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const auto addop = [](double x, double y) { return x + y; };
-    for (int e = wave; e < NA; e += 16) {
+    constexpr int EU = (NA + 15) / 16;
+    double v[EU][4];
+#pragma unroll
+    for (int u = 0; u < EU; ++u)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int e = wave + 16 * u, q = lane + 64 * rr;
+        v[u][rr] = (e < NA && q < nblk) ? partial[(int64_t)q * NA + e] : 0.0;
+      }
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      const int e = wave + 16 * u;
       double s = 0.0;
-      for (int q = lane; q < nblk; q += 64) s += partial[(int64_t)q * NA + e];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        if (lane + 64 * rr < nblk) s += v[u][rr];
       s = wave_reduce63(s, 0.0, addop);
-      if (lane == 63) m[e] = s;
+      if (lane == 63 && e < NA) m[e] = s;
     }
   }
   __syncthreads();
@@ -1174,7 +1219,7 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
   }
   __syncthreads();
   if (threadIdx.x == 0) *flag = bad ? 0.0 : 1.0;
-  if (beta) chol_solve_block(tl, p, beta, beta_copy, ok, L, b, cbad);
+  if (beta && threadIdx.x < 64) chol_solve_wave(tl, p, beta, beta_copy, ok, L);
 }
 
 int launch_gram(lfe_ctx* c, double* host_gram) {

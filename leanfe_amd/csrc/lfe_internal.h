@@ -217,6 +217,27 @@ struct lfe_ctx {
   size_t dn8_dq_cap = 0;
   double* dn8_eq = nullptr;
   size_t dn8_eq_cap = 0;
+  // general dense sweeps (lfe_dense3.hip, three or more FEs): per ordered FE pair (a, b) the i8
+  // count table of a's levels x b's levels in the K2 fragment form of the two-FE passes ([tile of 512
+  // b levels][16-row block of a][8 k blocks][1 KB]), its block flags and the flagged blocks' u16
+  // counts; per FE the slots of its cross term (one per tile of every other FE)
+  struct D3WS {
+    bool on = false;                // the last demean ran the pair-table sweeps
+    int8_t* tab[lfe::kMaxFE][lfe::kMaxFE] = {};
+    size_t tab_cap[lfe::kMaxFE][lfe::kMaxFE] = {};
+    uint8_t* flg[lfe::kMaxFE][lfe::kMaxFE] = {};
+    size_t flg_cap[lfe::kMaxFE][lfe::kMaxFE] = {};
+    uint16_t* X[lfe::kMaxFE][lfe::kMaxFE] = {};
+    size_t X_cap[lfe::kMaxFE][lfe::kMaxFE] = {};
+    double* runs[lfe::kMaxFE] = {};
+    size_t runs_cap[lfe::kMaxFE] = {};
+    uint32_t* part = nullptr;       // kept rows' (a & 63, b) codes, partitioned by a >> 6
+    size_t part_cap = 0;
+    int32_t* hist = nullptr;        // [bins][workgroups] counts -> scanned bases
+    size_t hist_cap = 0;
+    int32_t* tiles = nullptr;       // [128] 0, 1, 2, ...: the passes' tile list
+    int64_t table_bytes = 0;        // i8 table bytes over all ordered pairs
+  } d3;
   double* colsum_part = nullptr;  // [p][blocks][G] fine-limb columns of k_col_sums (lfe_fast.hip)
   size_t colsum_part_cap = 0;
   double* Xp = nullptr;          // [p][ld] permuted columns
@@ -422,6 +443,25 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check);
 int dense_tq(lfe_ctx* c, double* runs);
 // the secondary effects' digit fragments for the exact K1 pass (after every alpha_Q update)
 int dense_digits_q(lfe_ctx* c, const double* alphaQ);
+// one product pass over a pair table in the K2 fragment form (lfe_dense.hip): slots
+// runs[t][G_rows][ldo] (columns [0, pc)) = the table's tile t times alpha_k's rows of that tile
+struct PairPass {
+  const int8_t* tab;
+  const uint8_t* flg;
+  const uint16_t* X;
+  const int32_t* tiles;   // [ntile_k] 0, 1, ...
+  int ntile_k, nrb;       // tiles of the k-side FE, 16-row blocks of the output FE
+  int G_rows, G_k, pc;    // levels of both FEs, columns of this pass (<= 16)
+  int lda, ldo;           // row strides of alpha_k and of the slots
+  const double* alpha;    // alpha_k (+ the column offset)
+  double* runs;           // the slots (+ the column offset)
+};
+int dn8_pair_pass(lfe_ctx* c, const PairPass& pp);
+// lfe_dense3.hip: three or more FEs, unweighted - every cross term from the pair tables
+bool dense3_ok(const lfe_ctx* c, const std::vector<int>& order, int check_from);
+int demean_dense3(lfe_ctx* c, const std::vector<int>& order, double tol, int max_iter, int check_from,
+                  int* iterations_out, double* last_out);
+void free_dense3(lfe_ctx* c);
 
 // --- constant sums (lfe_sweep.hip) ---
 int sweep_group_sums(lfe_ctx* c);
