@@ -257,3 +257,116 @@ def test_sharded_schedule_matches_oracle(n, k, levels, vcov, cluster_fe):
         if cluster_fe is not None:
             assert res["n_clusters"] == o["n_clusters"]
     np.testing.assert_array_equal(out[0]["beta"], out[1]["beta"])  # bit-identical across ranks
+
+
+# ---------------------------------------------------------------------------
+# the owner schedule (lfe_ctx_set_owner / bench --shard owner): rank r holds every row whose code of
+# the primary FE (most levels) lies in its level range, so the primary FE's counts, sums, cross
+# terms and effects are complete on the rank and never all-reduced; the other FEs' are, and the
+# stop test's max is taken over ranks (lfe_prep.hip, lfe_sweep.hip, lfe_seg.hip, lfe_dense3.hip)
+# ---------------------------------------------------------------------------
+
+def _allmax(x: float) -> float:
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _owner_fit(rank, n, k, levels, seed, vcov, cluster_fe, tol=1e-6, max_iter=50):
+    F = len(levels)
+    G = list(levels)
+    P = int(np.argmax(G))
+    lo, hi = shard_range(G[P], rank, WORLD)  # this rank's primary levels
+    full = synth.panel(n, k, levels, seed=seed)
+    own = (full[f"fe{P + 1}"] >= lo) & (full[f"fe{P + 1}"] < hi)
+    cols = np.stack([full["y"][own]] + [full[f"x{j + 1}"][own] for j in range(k)])
+    codes = [full[f"fe{f + 1}"][own].astype(np.int64) for f in range(F)]
+    cl = codes[cluster_fe] if cluster_fe is not None else None
+    local = lambda f: f == P  # noqa: E731 - the primary FE's tables are complete on the rank
+    red = lambda f, a: a if local(f) else _allreduce(a)  # noqa: E731
+    cnt_pre = [red(f, np.bincount(c, minlength=G[f]).astype(np.int64)) for f, c in enumerate(codes)]
+    card = [int(_allreduce(np.array([(cnt_pre[f] > 0).sum()]))[0]) if local(f) else int((cnt_pre[f] > 0).sum())
+            for f in range(F)]
+    keep = np.all([cnt_pre[f][codes[f]] > 1 for f in range(F)], axis=0)
+    cols = cols[:, keep]
+    codes = [c[keep] for c in codes]
+    cl = cl[keep] if cl is not None else None
+    cnt = [red(f, np.bincount(c, minlength=G[f]).astype(np.int64)) for f, c in enumerate(codes)]
+    fe_dims = [int(_allreduce(np.array([(cnt[f] > 0).sum()]))[0]) if local(f) else int((cnt[f] > 0).sum())
+               for f in range(F)]
+    n_obs = int(_allreduce(np.array([keep.sum()], dtype=np.int64))[0])
+    order = sorted(range(F), key=lambda f: card[f])
+    S = [red(f, _gsum(cols, codes[f], G[f])) for f in range(F)]
+    alpha = [np.zeros((G[f], cols.shape[0])) for f in range(F)]
+    safe = [np.maximum(c, 1)[:, None] for c in cnt]
+    it = 0
+    for it in range(1, max_iter + 1):
+        for f in order:
+            other = sum(alpha[g][codes[g]] for g in range(F) if g != f)
+            T = red(f, _gsum(np.asarray(other).T, codes[f], G[f]))
+            alpha[f] = np.where(cnt[f][:, None] > 0, (S[f] - T) / safe[f], 0.0)
+        if it >= 3:
+            ytil = cols[0] - sum(alpha[f][codes[f], 0] for f in range(F))
+            m = 0.0
+            for f in range(F):
+                sy = red(f, _gsum(ytil, codes[f], G[f]))
+                present = cnt[f] > 0
+                if local(f):  # only this rank's primary levels
+                    present &= (np.arange(G[f]) >= lo) & (np.arange(G[f]) < hi)
+                if present.any():
+                    m = max(m, float(np.max(np.abs(sy[present] / cnt[f][present]))))
+            if _allmax(m) < tol:
+                break
+    Xd = cols - sum(alpha[f][codes[f]].T for f in range(F))
+    Z = np.vstack([np.ones(Xd.shape[1]), Xd[1:]])
+    XtX = _allreduce(Z @ Z.T)
+    Xty = _allreduce(Z @ Xd[0])
+    L = np.linalg.cholesky(XtX)
+    beta_full = np.linalg.solve(L.T, np.linalg.solve(L, Xty))
+    XtX_inv = np.linalg.solve(L.T, np.linalg.solve(L, np.eye(k + 1)))
+    r = Xd[0] - beta_full @ Z
+    rss = float(_allreduce(np.array([r @ r]))[0])
+    df_resid = n_obs - (k + 1) - (sum(fe_dims) - F)
+    Vb = XtX_inv[1:, 1:]
+    ncl = None
+    if vcov == "iid":
+        V = Vb * (rss / df_resid)
+    elif vcov == "HC1":
+        x = Xd[1:]
+        V = Vb @ _allreduce((x * r * r) @ x.T) @ Vb * (n_obs / df_resid)
+    else:
+        C = int(levels[cluster_fe])
+        sc = _allreduce(_gsum(Xd[1:] * r, cl, C))
+        ncl = int((_allreduce(np.bincount(cl, minlength=C).astype(np.int64)) > 0).sum())
+        V = Vb @ (sc.T @ sc) @ Vb * (ncl / (ncl - 1)) * ((n_obs - 1) / df_resid)
+    se = np.sqrt(np.maximum(np.diag(V), 0.0))
+    return dict(beta=beta_full[1:], se=se, iterations=it, n_obs=n_obs, df_resid=df_resid, fe_dims=fe_dims,
+                n_clusters=ncl, rows=int(own.sum()))
+
+
+@pytest.mark.parametrize("n,k,levels,vcov,cluster_fe", [
+    (20_000, 3, (400, 30), "HC1", None),
+    (18_000, 2, (300, 25, 6), "cluster", 1),
+    (16_000, 2, (40, 350, 12), "iid", None),  # the primary FE is not the first
+])
+def test_owner_schedule_matches_oracle(n, k, levels, vcov, cluster_fe):
+    from oracle import altproj
+
+    seed = 11
+    out = _run(_owner_fit, n, k, list(levels), seed, vcov, cluster_fe)
+    full = synth.panel(n, k, list(levels), seed=seed)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    cl = [fes[cluster_fe]] if cluster_fe is not None else None
+    o = altproj.fit(full, "y", xs, fes, vcov=vcov, cluster_cols=cl)
+    assert sum(out[r]["rows"] for r in range(WORLD)) == n  # the level ranges partition the rows
+    for r in range(WORLD):
+        res = out[r]
+        np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=1e-13)
+        np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=1e-14)
+        assert res["iterations"] == o["iterations"]
+        assert (res["n_obs"], res["df_resid"]) == (o["n_obs"], o["df_resid"])
+        assert list(res["fe_dims"]) == list(o["fe_dims"])
+        if cluster_fe is not None:
+            assert res["n_clusters"] == o["n_clusters"]
+    np.testing.assert_array_equal(out[0]["beta"], out[1]["beta"])
