@@ -12,7 +12,8 @@
 //   tab[a][b] = [tile t of 512 b levels][16-row block of a levels][8 k blocks of 64][1 KB], lane
 //   (g, i) bytes jj = N_ab[16 rb + i][512 t + 64 kb + 16 g + jj]; a block with a count over 127 is
 //   flagged, zero in the i8 table, and its counts kept as u16 in X[a][b] (16 x 64, natural order).
-// The build partitions the kept rows' (a, b) code pairs by a >> 6 (a counting sort), counts each
+// The build partitions the kept rows' codes by a >> 6 (a counting sort; one partition carries the
+// codes of every partner of a, up to three), counts each
 // 64-level chunk of a against 2048 columns of b at a time in LDS (8-bit counters; a chunk where some
 // cell passes 255 is counted again on 16-bit counters in two halves) and writes both orientations.
 //
@@ -55,10 +56,17 @@ __global__ __launch_bounds__(256) void k_d3_hist(const int32_t* __restrict__ cod
   for (int j = threadIdx.x; j < nbin; j += blockDim.x) cnt[(int64_t)j * gridDim.x + blockIdx.x] = h[j];
 }
 
-// the same rows to their bin's range (bases: the scanned counts): (a & 63) << 26 | b
+// the same rows to their bin's range (bases: the scanned counts), packed as a & 63 in bits [0, 6) and
+// the codes of up to three partner FEs b_j in bits [6 + 16 j, 22 + 16 j) (levels <= 65536): one
+// partition serves every pair the FE with more levels forms
+constexpr int kD3Slots = 3;
+struct D3Codes {
+  const int32_t* b[kD3Slots];
+  int nb;
+};
 __global__ __launch_bounds__(256) void k_d3_scatter(const int32_t* __restrict__ codeP, const int32_t* __restrict__ codeA,
-                                                    const int32_t* __restrict__ codeB, int64_t n, int nbin,
-                                                    const int32_t* __restrict__ base, uint32_t* __restrict__ out) {
+                                                    D3Codes cb, int64_t n, int nbin, const int32_t* __restrict__ base,
+                                                    uint64_t* __restrict__ out) {
   extern __shared__ int32_t cur[];
   for (int j = threadIdx.x; j < nbin; j += blockDim.x) cur[j] = base[(int64_t)j * gridDim.x + blockIdx.x];
   __syncthreads();
@@ -66,13 +74,18 @@ __global__ __launch_bounds__(256) void k_d3_scatter(const int32_t* __restrict__ 
   for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
     if (codeP[i] < 0) continue;
     const int32_t a = codeA[i];
+    uint64_t v = (uint64_t)(a & 63);
+#pragma unroll
+    for (int j = 0; j < kD3Slots; ++j)
+      if (j < cb.nb) v |= (uint64_t)(uint32_t)cb.b[j][i] << (6 + 16 * j);
     const int pos = atomicAdd(&cur[a >> 6], 1);
-    out[pos] = ((uint32_t)(a & 63) << 26) | (uint32_t)codeB[i];
+    out[pos] = v;
   }
 }
 
 struct D3Build {
-  const uint32_t* part;
+  const uint64_t* part;
+  int slot;              // the partner FE's 16-bit field in the packed rows
   const int32_t* base;   // scanned [bin][nwg] (+ the total): bin j's rows are [base[j nwg], base[(j + 1) nwg])
   int nwg, nbr, NA512, NB512;
   int8_t* tab_ab;        // rows a, k b: [tile of b][NA512 / 16][8][1 KB]
@@ -86,7 +99,7 @@ struct D3Build {
 // the chunk's rows with b in [bc0, bc0 + W) into LDS counters cnt[a & 63][b - bc0] of CT (8 or 16
 // bits, packed in words); returns whether an 8-bit counter overflowed
 template <typename CT>
-__device__ bool d3_count(const uint32_t* __restrict__ part, uint32_t* cw, int r0, int r1, int bc0, int W) {
+__device__ bool d3_count(const uint64_t* __restrict__ part, int slot, uint32_t* cw, int r0, int r1, int bc0, int W) {
   constexpr int PER = 4 / sizeof(CT), SH = 8 * sizeof(CT);
   __shared__ int ovf;
   const int words = kD3Chunk * W / PER;
@@ -96,18 +109,18 @@ __device__ bool d3_count(const uint32_t* __restrict__ part, uint32_t* cw, int r0
   bool over = false;
   constexpr int V = 8;  // loads in flight per thread
   for (int i0 = r0 + (int)threadIdx.x; i0 < r1; i0 += V * (int)blockDim.x) {
-    uint32_t v[V];
+    uint64_t v[V];
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       const int i = i0 + u * (int)blockDim.x;
-      v[u] = i < r1 ? part[i] : 0xffffffffu;
+      v[u] = i < r1 ? part[i] : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       if (i0 + u * (int)blockDim.x >= r1) break;
-      const uint32_t b = (v[u] & 0x3ffffffu) - (uint32_t)bc0;
+      const uint32_t b = (uint32_t)((v[u] >> (6 + 16 * slot)) & 0xffffu) - (uint32_t)bc0;
       if (b >= (uint32_t)W) continue;
-      const uint32_t idx = (v[u] >> 26) * (uint32_t)W + b;
+      const uint32_t idx = (uint32_t)(v[u] & 63u) * (uint32_t)W + b;
       const int sh = (int)(idx % PER) * SH;
       const uint32_t old = atomicAdd(&cw[idx / PER], 1u << sh);
       if (sizeof(CT) == 1 && ((old >> sh) & 0xffu) == 0xffu) over = true;  // carried into the next byte
@@ -198,14 +211,14 @@ __global__ __launch_bounds__(1024) void k_d3_build(D3Build a) {
   const int bin = blockIdx.x / a.nbr, br = blockIdx.x - bin * a.nbr;
   const int r0 = a.base[(int64_t)bin * a.nwg], r1 = a.base[(int64_t)(bin + 1) * a.nwg];
   const int bc0 = br * kD3W, W = min(kD3W, a.NB512 - bc0);
-  if (!d3_count<uint8_t>(a.part, cw, r0, r1, bc0, W)) {
+  if (!d3_count<uint8_t>(a.part, a.slot, cw, r0, r1, bc0, W)) {
     d3_write<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bin, bc0, W);
     return;
   }
   const int W2 = W / 2;  // a multiple of 256 (W is one of 512)
   for (int half = 0; half < 2; ++half) {
     __syncthreads();
-    d3_count<uint16_t>(a.part, cw, r0, r1, bc0 + half * W2, W2);
+    d3_count<uint16_t>(a.part, a.slot, cw, r0, r1, bc0 + half * W2, W2);
     d3_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bin, bc0 + half * W2, W2);
   }
 }
@@ -341,55 +354,70 @@ static int d3_build(lfe_ctx* c) {
   const size_t lds = (size_t)kD3Chunk * kD3W;  // 8-bit counters (16-bit: half the columns)
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_d3_build), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds));
+  // every unordered pair is counted from the partition of its FE with more levels (more chunks):
+  // one partition (histogram, scan, scatter) per such FE and up to kD3Slots partners
+  std::vector<std::vector<int>> partners(F);
   for (int x = 0; x < F; ++x)
     for (int y = x + 1; y < F; ++y) {
-      // partition by the FE with more levels (more chunks), columns = the other's
-      const int a = c->fe[x].G >= c->fe[y].G ? x : y, b = a == x ? y : x;
-      const int64_t NA = n512(c->fe[a].G), NB = n512(c->fe[b].G), cells = NA * NB;
-      d.table_bytes += 2 * cells;
-      LFE_TRY(ensure_dev(d.tab[a][b], d.tab_cap[a][b], (size_t)cells));
-      LFE_TRY(ensure_dev(d.tab[b][a], d.tab_cap[b][a], (size_t)cells));
-      LFE_TRY(ensure_dev(d.flg[a][b], d.flg_cap[a][b], (size_t)cells / 1024));
-      LFE_TRY(ensure_dev(d.flg[b][a], d.flg_cap[b][a], (size_t)cells / 1024));
-      LFE_TRY(ensure_dev(d.X[a][b], d.X_cap[a][b], (size_t)cells));
-      LFE_TRY(ensure_dev(d.X[b][a], d.X_cap[b][a], (size_t)cells));
-      const int nbin = (int)(NA / kD3Chunk);
-      const int nwg = (int)std::max<int64_t>(1, std::min<int64_t>(kD3Wgs, (n + 4095) / 4096));
-      const size_t hm = (size_t)nbin * nwg;
-      LFE_TRY(ensure_dev(d.hist, d.hist_cap, hm + 4));
-      LFE_HIP(hipMemsetAsync(d.hist + hm, 0, sizeof(int32_t) * 4, c->stream));
-      {
-        ProfScope _ps(c, K_LAYOUT_HIST);
-        hipLaunchKernelGGL(k_d3_hist, dim3(nwg), dim3(256), sizeof(int32_t) * nbin, c->stream, c->L.code[c->L.P],
-                           c->L.code[a], n, nbin, d.hist);
-        LFE_HIP(hipGetLastError());
-      }
-      LFE_TRY(exclusive_scan(c, d.hist, (int64_t)hm + 1));
+      const int a = c->fe[x].G >= c->fe[y].G ? x : y;
+      partners[a].push_back(a == x ? y : x);
+    }
+  const int nwg = (int)std::max<int64_t>(1, std::min<int64_t>(kD3Wgs, (n + 4095) / 4096));
+  for (int a = 0; a < F; ++a) {
+    if (partners[a].empty()) continue;
+    const int64_t NA = n512(c->fe[a].G);
+    const int nbin = (int)(NA / kD3Chunk);
+    const size_t hm = (size_t)nbin * nwg;
+    LFE_TRY(ensure_dev(d.hist, d.hist_cap, hm + 4));
+    LFE_HIP(hipMemsetAsync(d.hist + hm, 0, sizeof(int32_t) * 4, c->stream));
+    {
+      ProfScope _ps(c, K_LAYOUT_HIST);
+      hipLaunchKernelGGL(k_d3_hist, dim3(nwg), dim3(256), sizeof(int32_t) * nbin, c->stream, c->L.code[c->L.P],
+                         c->L.code[a], n, nbin, d.hist);
+      LFE_HIP(hipGetLastError());
+    }
+    LFE_TRY(exclusive_scan(c, d.hist, (int64_t)hm + 1));
+    const auto& pb = partners[a];
+    for (size_t j0 = 0; j0 < pb.size(); j0 += kD3Slots) {
+      D3Codes cb{};
+      cb.nb = (int)std::min<size_t>(kD3Slots, pb.size() - j0);
+      for (int j = 0; j < cb.nb; ++j) cb.b[j] = c->L.code[pb[j0 + j]];
       {
         ProfScope _ps(c, K_LAYOUT_SCATTER);
         hipLaunchKernelGGL(k_d3_scatter, dim3(nwg), dim3(256), sizeof(int32_t) * nbin, c->stream, c->L.code[c->L.P],
-                           c->L.code[a], c->L.code[b], n, nbin, d.hist, d.part);
+                           c->L.code[a], cb, n, nbin, d.hist, d.part);
         LFE_HIP(hipGetLastError());
       }
-      D3Build ba{};
-      ba.part = d.part;
-      ba.base = d.hist;
-      ba.nwg = nwg;
-      ba.nbr = (int)((NB + kD3W - 1) / kD3W);
-      ba.NA512 = (int)NA;
-      ba.NB512 = (int)NB;
-      ba.tab_ab = d.tab[a][b];
-      ba.flg_ab = d.flg[a][b];
-      ba.X_ab = d.X[a][b];
-      ba.tab_ba = d.tab[b][a];
-      ba.flg_ba = d.flg[b][a];
-      ba.X_ba = d.X[b][a];
-      {
+      for (int j = 0; j < cb.nb; ++j) {
+        const int b = pb[j0 + j];
+        const int64_t NB = n512(c->fe[b].G), cells = NA * NB;
+        d.table_bytes += 2 * cells;
+        LFE_TRY(ensure_dev(d.tab[a][b], d.tab_cap[a][b], (size_t)cells));
+        LFE_TRY(ensure_dev(d.tab[b][a], d.tab_cap[b][a], (size_t)cells));
+        LFE_TRY(ensure_dev(d.flg[a][b], d.flg_cap[a][b], (size_t)cells / 1024));
+        LFE_TRY(ensure_dev(d.flg[b][a], d.flg_cap[b][a], (size_t)cells / 1024));
+        LFE_TRY(ensure_dev(d.X[a][b], d.X_cap[a][b], (size_t)cells));
+        LFE_TRY(ensure_dev(d.X[b][a], d.X_cap[b][a], (size_t)cells));
+        D3Build ba{};
+        ba.part = d.part;
+        ba.slot = j;
+        ba.base = d.hist;
+        ba.nwg = nwg;
+        ba.nbr = (int)((NB + kD3W - 1) / kD3W);
+        ba.NA512 = (int)NA;
+        ba.NB512 = (int)NB;
+        ba.tab_ab = d.tab[a][b];
+        ba.flg_ab = d.flg[a][b];
+        ba.X_ab = d.X[a][b];
+        ba.tab_ba = d.tab[b][a];
+        ba.flg_ba = d.flg[b][a];
+        ba.X_ba = d.X[b][a];
         ProfScope _ps(c, K_SEG_BUILD);
         hipLaunchKernelGGL(k_d3_build, dim3(nbin * ba.nbr), dim3(1024), lds, c->stream, ba);
         LFE_HIP(hipGetLastError());
       }
     }
+  }
   return LFE_OK;
 }
 
@@ -474,6 +502,8 @@ int demean_dense3(lfe_ctx* c, const std::vector<int>& order, double tol, int max
   int iterations = 0;
   double last = -1.0;
   bool first_ready = false;  // alpha_spare holds order[0]'s next projection (formed by the last check)
+  bool checked = false;      // the last sweep ran the stop test (order[0]'s T is then from the final effects)
+  c->d3.t_final = 0;
   for (int it = 1; it <= max_iter; ++it) {
     for (int k = 0; k < F; ++k) {
       const int f = order[k];
@@ -485,8 +515,10 @@ int demean_dense3(lfe_ctx* c, const std::vector<int>& order, double tol, int max
       LFE_TRY(d3_project(c, f, c->fe[f].alpha, c->fe[f].alpha, false));
     }
     first_ready = false;
+    checked = false;
     iterations = it;
     if (it < check_from) continue;
+    checked = true;
     LFE_HIP(hipMemsetAsync(c->dred, 0, sizeof(double), c->stream));
     for (int k = 0; k < F; ++k) {
       const int f = order[k];
@@ -510,8 +542,24 @@ int demean_dense3(lfe_ctx* c, const std::vector<int>& order, double tol, int max
     LFE_TRY(d2h_sync(c, &last, c->dred, sizeof(double)));
     if (last < tol) break;
   }
+  // the last FE's T used every other FE's final effects; so did order[0]'s from the stop test
+  c->d3.t_final = (1u << order[F - 1]) | (checked ? 1u << f0 : 0u);
   *iterations_out = iterations;
   *last_out = last;
+  return LFE_OK;
+}
+
+int dense3_final_T(lfe_ctx* c) {
+  for (int f = 0; f < c->F; ++f) {
+    if (c->d3.t_final & (1u << f)) continue;
+    auto& fe = c->fe[f];
+    int ns = 0;
+    LFE_TRY(d3_cross(c, f, false, &ns));
+    const int64_t m = (int64_t)fe.G * c->p;
+    LFE_TRY(d3_reduce(c, c->d3.runs[f], ns, m, fe.T, f, nullptr, nullptr, false));
+    if (!(c->world == 1 || (c->owner_on && f == c->L.P))) LFE_TRY(allreduce_sum_f64(c, fe.T, (size_t)m));
+    c->d3.t_final |= 1u << f;
+  }
   return LFE_OK;
 }
 

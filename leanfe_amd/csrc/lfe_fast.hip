@@ -664,6 +664,132 @@ __global__ void k_raw_combine(const double* __restrict__ slots, int world, int p
   if (t < 16) sh[t] = sh[16 + t] = slots[256 + t];
 }
 
+// Group sums of three or more FEs whose non-primary tables do not fit LDS whole (the reference's
+// 3-FE panels: 2e4 x 4e3 x 1e3 levels at p = 15, 1e4 x 2e3 x 500 at p = 21), by column groups:
+// workgroup (column group cg of nc columns, row part) keeps the primary slice [B][nc] and every other
+// FE's table [G_f][nc] in LDS (nc from the LDS budget), reads its nc columns and the codes of its
+// rows once, and adds the fine limbs there; the slice goes to S_P at each bucket change, the tables
+// at the end (integer adds: any order).  Replaces k_sums4's per-row global adds for tables that do
+// not fit (~1 / 30 of the LDS rate) and k_col_sums' reread of the codes for every column.  The
+// workgroups of one row part share an XCD (block i -> XCD i % 8), so its codes come from one L2.
+constexpr int kCgThreads = 1024;
+constexpr int kCgMaxNc = 8;
+constexpr int kCgMaxF = 4;
+constexpr int kCgRows = 2;  // rows per thread per round, every load issued first
+
+struct SumsCgArgs {
+  const int4* items;
+  int n_items, s, P, nq;
+  const int32_t* codeP;
+  const int32_t* codeq[kCgMaxF - 1];
+  int qf[kCgMaxF - 1];
+  const double* X;
+  int64_t ld;
+  const double* w;
+  int p, nc, ncg, nparts, B, G_P;
+  int Gq[kCgMaxF - 1];
+  int q_off[kCgMaxF - 1];  // u64 LDS offset of [G_q][nc] (the slice [B][nc] at 0)
+  int lds_words;
+  double* SP;
+  double* Sq[kCgMaxF - 1];
+  double* hiP;
+  double* hiq[kCgMaxF - 1];
+  const double* fixq;
+};
+
+__global__ __launch_bounds__(kCgThreads) void k_sums_cg(SumsCgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long tl[];
+  typedef unsigned long long u64;
+  const int bid = blockIdx.x, cg = (bid >> 3) % a.ncg, part = (bid / (8 * a.ncg)) * 8 + (bid & 7);
+  if (part >= a.nparts) return;  // uniform
+  const int tid = threadIdx.x, lane = tid & 63, p = a.p;
+  const int c0 = cg * a.nc, nc = min(a.nc, p - c0);
+  for (int j = tid; j < a.lds_words; j += kCgThreads) tl[j] = 0ull;
+  FixCol fc[kCgMaxNc];
+#pragma unroll
+  for (int cc = 0; cc < kCgMaxNc; ++cc) fc[cc] = cc < nc ? fix_col(a.fixq, c0 + cc) : FixCol{};
+  auto add = [&](u64* dst, double* hdst, double v, const FixCol& q) {
+    double h;
+    atomicAdd(dst, fix_split(v, q, h));
+    if (h != 0.0) atomicAdd(hdst, h);
+  };
+  auto flush = [&](int b) {
+    const int lo = b << a.s;
+    for (int j = tid; j < a.B * nc; j += kCgThreads) {
+      const int g = lo + j / nc, cc = j - (j / nc) * nc;
+      const u64 v = tl[j];
+      if (v != 0ull && g < a.G_P) atomicAdd(reinterpret_cast<u64*>(&a.SP[(int64_t)g * p + c0 + cc]), v);
+      tl[j] = 0ull;
+    }
+  };
+  __syncthreads();
+  const BlockRows br = block_rows(a.items, a.n_items, lane, part, a.nparts);
+  int cur = -1;
+  for (int item = br.first; item < a.n_items; ++item) {
+    int4 it = a.items[item];
+    if (it.y >= br.hi) break;
+    it.y = max(it.y, br.lo);
+    it.z = min(it.z, br.hi);
+    if (it.x != cur) {
+      __syncthreads();
+      if (cur >= 0) flush(cur);
+      __syncthreads();
+      cur = it.x;
+    }
+    const int lo = it.x << a.s;
+    for (int i0 = it.y + tid; i0 < it.z; i0 += kCgRows * kCgThreads) {
+      int hp[kCgRows], hq[kCgRows][kCgMaxF - 1];
+      double x[kCgRows][kCgMaxNc], wv[kCgRows];
+#pragma unroll
+      for (int r = 0; r < kCgRows; ++r) {
+        const int i = i0 + r * kCgThreads;
+        const bool live = i < it.z;
+        hp[r] = live ? a.codeP[i] : -1;
+#pragma unroll
+        for (int q = 0; q < kCgMaxF - 1; ++q) hq[r][q] = (q < a.nq && live) ? a.codeq[q][i] : 0;
+#pragma unroll
+        for (int cc = 0; cc < kCgMaxNc; ++cc) x[r][cc] = (cc < nc && live) ? a.X[(int64_t)(c0 + cc) * a.ld + i] : 0.0;
+        wv[r] = (a.w && live) ? a.w[i] : 1.0;
+      }
+#pragma unroll
+      for (int r = 0; r < kCgRows; ++r) {
+        if (hp[r] < 0) continue;  // dropped row (singleton filter) or past the item
+#pragma unroll
+        for (int cc = 0; cc < kCgMaxNc; ++cc) {
+          if (cc >= nc) break;
+          const double v = a.w ? x[r][cc] * wv[r] : x[r][cc];  // sum of (c * w), polars_impl.py:496
+          add(&tl[(hp[r] - lo) * nc + cc], &a.hiP[(int64_t)hp[r] * p + c0 + cc], v, fc[cc]);
+#pragma unroll
+          for (int q = 0; q < kCgMaxF - 1; ++q)
+            if (q < a.nq)
+              add(&tl[a.q_off[q] + hq[r][q] * nc + cc], &a.hiq[q][(int64_t)hq[r][q] * p + c0 + cc], v, fc[cc]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (cur >= 0) flush(cur);
+  for (int q = 0; q < a.nq; ++q)
+    for (int j = tid; j < a.Gq[q] * nc; j += kCgThreads) {
+      const u64 v = tl[a.q_off[q] + j];
+      const int g = j / nc, cc = j - g * nc;
+      if (v != 0ull) atomicAdd(reinterpret_cast<u64*>(&a.Sq[q][(int64_t)g * p + c0 + cc]), v);
+    }
+}
+
+// column groups for k_sums_cg: columns per group from the LDS budget (0: the tables do not fit)
+static int sums_cg_nc(const lfe_ctx* c) {
+  const int P = c->L.P;
+  if (c->F < 3 || c->F > kCgMaxF || P < 0) return 0;
+  const char* e = getenv("LFE_SUMS_CG");  // "0": off (A/B)
+  if (e && e[0] == '0') return 0;
+  int64_t per_col = (int64_t)1 << c->L.s;
+  for (int f = 0; f < c->F; ++f)
+    if (f != P) per_col += c->fe[f].G;
+  const int64_t nc = std::min<int64_t>({(int64_t)kCgMaxNc, (int64_t)c->p, (150 * 1024 / 8) / per_col});
+  return (int)std::max<int64_t>(nc, 0);
+}
+
 int sums4(lfe_ctx* c) {
   Sums4Args a{};
   a.la = layout_args(c);
@@ -699,6 +825,16 @@ int sums4(lfe_ctx* c) {
     if (!colsplit[f]) a.qf[a.nq++] = f;
   }
   c->sums_zeroed = false;
+  // three or more FEs with a table that does not fit LDS whole: the column-group sums
+  int cg_nc = 0;
+  {
+    bool all_fit = a.slice != 0;
+    for (int f = 0; f < c->F; ++f)
+      if (f != P && a.tab_off[f] < 0) all_fit = false;
+    if (!all_fit) cg_nc = sums_cg_nc(c);
+    if (cg_nc > 0)
+      for (int f = 0; f < c->F; ++f) colsplit[f] = false;
+  }
   const size_t lds = off * 8;
   const int NT = (p + 15) / 16;
   const void* fn = nullptr;
@@ -775,7 +911,45 @@ int sums4(lfe_ctx* c) {
   }
   c->exact_sums = true;
   LFE_TRY(hi_begin(c));
-  {
+  if (cg_nc > 0) {
+    SumsCgArgs g{};
+    g.items = reinterpret_cast<const int4*>(c->items_d);
+    g.n_items = c->L.n_items;
+    g.s = c->L.s;
+    g.P = P;
+    g.codeP = c->L.code[P];
+    g.X = c->L.X;
+    g.ld = c->ld;
+    g.w = c->L.w;
+    g.p = p;
+    g.nc = cg_nc;
+    g.ncg = (p + cg_nc - 1) / cg_nc;
+    g.B = 1 << c->L.s;
+    g.G_P = c->fe[P].G;
+    g.SP = c->fe[P].S;
+    g.hiP = c->fe[P].hi;
+    g.fixq = c->fixq;
+    int off_w = g.B * cg_nc;
+    for (int f = 0; f < c->F; ++f) {
+      if (f == P) continue;
+      const int q = g.nq++;
+      g.qf[q] = f;
+      g.codeq[q] = c->L.code[f];
+      g.Gq[q] = c->fe[f].G;
+      g.q_off[q] = off_w;
+      off_w += c->fe[f].G * cg_nc;
+      g.Sq[q] = c->fe[f].S;
+      g.hiq[q] = c->fe[f].hi;
+    }
+    g.lds_words = off_w;
+    // one workgroup per CU in all (LDS), the row parts spread over the column groups
+    g.nparts = std::max(1, std::min(c->L.n_items * 4, (c->n_cu + g.ncg - 1) / g.ncg));
+    const size_t lds_cg = sizeof(unsigned long long) * off_w;
+    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sums_cg), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_cg));
+    ProfScope _ps(c, K_GROUP_SUMS);
+    hipLaunchKernelGGL(k_sums_cg, dim3((g.nparts + 7) / 8 * 8 * g.ncg), dim3(kCgThreads), lds_cg, c->stream, g);
+  } else {
     ProfScope _ps(c, K_GROUP_SUMS);
     void* args[] = {&a};
     LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, lds, c->stream));

@@ -1222,7 +1222,264 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
   if (beta && threadIdx.x < 64) chol_solve_wave(tl, p, beta, beta_copy, ok, L);
 }
 
+// ---------------------------------------------------------------------------
+// Gram from group tables, three or more FEs (after the pair-table sweeps of lfe_dense3.hip,
+// unweighted, one process).  With d' = d - c (every data column shifted by the first layout row),
+// a'_f = alpha_f except a'_s = alpha_s - c for one FE s (the FEs absorb the shift), S'_f = S_f - n c
+// and T'_f[g] = sum over g's rows of sum_{h != f} a'_h (the final cross term, T_f - n c for f != s):
+//   sum d~ d~' = R + sum_f sum_g [n a' a'' - V a'' - a' V'],   V = S' - T' / 2
+//   sum d~     = C - sum_f sum_g n a'
+// (the cross products sum_{f != h} a'_f a'_h' over the rows are sum_f sum_g a' T'', symmetric in
+// total, so each FE carries half of its T').  R, C: the raw Gram of [1, d'] over the kept rows, one
+// MFMA pass over X with no effect gathers (k_raw_gram); the table terms are one pass over the
+// groups of every FE (k_tab3_gram).  Cancellation guard as the two-FE form (kTabKappa).
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(kGramThreads) void k_raw_gram(GramArgs a, double* __restrict__ partial, int64_t pstride) {
+  using Sh = GramShape<NT>;
+  __shared__ double red[Sh::LEN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kq = lane >> 4, c = lane & 15;
+  const int p = a.la.p, P = a.la.P;
+  d4 acc[Sh::NP];
+#pragma unroll
+  for (int q = 0; q < Sh::NP; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  const double* xb[NT];
+  double sh[NT], fill[NT];
+  bool dat[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) {
+    int xc = 16 * I + c - 1;  // design column 0 = intercept, 1 + d = data column d
+    if (xc >= p) xc = -2;
+    dat[I] = xc >= 0;
+    fill[I] = xc == -1 ? 1.0 : 0.0;
+    xb[I] = a.X + (int64_t)(xc >= 0 ? xc : 0) * a.ld;
+    sh[I] = dat[I] && a.la.n_items > 0 ? xb[I][0] : 0.0;
+  }
+  constexpr int GU = 2;
+  const BlockRows br = block_rows(a.la.items, a.la.n_items, lane);
+  for (int item = br.first; item < a.la.n_items; ++item) {
+    int4 it = a.la.items[item];
+    if (it.y >= br.hi) break;
+    it.y = max(it.y, br.lo);
+    it.z = min(it.z, br.hi);
+    const int g0 = it.y >> 4, g1 = (it.z + 15) >> 4;
+    for (int gb = g0 + wave * GU; gb < g1; gb += (kGramThreads / 64) * GU) {
+      int4 h[GU];
+      d4 xv[GU][NT];
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {  // every load of the GU groups first
+        const int gi = gb + u, r = gi * 16 + kq * 4;
+        h[u] = gi < g1 ? *reinterpret_cast<const int4*>(a.la.code[P] + r) : int4{-1, -1, -1, -1};
+#pragma unroll
+        for (int I = 0; I < NT; ++I) xv[u][I] = gi < g1 ? ld4(xb[I] + r) : d4{0.0, 0.0, 0.0, 0.0};
+      }
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int r = (gb + u) * 16 + kq * 4;
+        const int hv[4] = {h[u].x, h[u].y, h[u].z, h[u].w};
+        double z[4][NT];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bool valid = hv[s] >= 0 && r + s >= it.y && r + s < it.z;
+#pragma unroll
+          for (int I = 0; I < NT; ++I) z[s][I] = valid ? (dat[I] ? xv[u][I][s] - sh[I] : fill[I]) : 0.0;
+        }
+        mfma_rows<NT>(z, acc);
+      }
+    }
+  }
+  block_reduce_store<NT, kGramThreads>(acc, red, partial + (int64_t)blockIdx.x * pstride, tid);
+}
+
+constexpr int kT3Chunk = 64;  // groups staged per round
+constexpr int kT3MaxP = 32;   // (NG + p <= 560 entries: three per thread)
+constexpr int kT3E = 3;
+
+struct Tab3Args {
+  const double* alpha[kMaxFE];
+  const double* S[kMaxFE];
+  const double* T[kMaxFE];
+  const int32_t* cnt[kMaxFE];
+  int64_t gstart[kMaxFE + 1];  // FE f's groups are [gstart[f], gstart[f + 1]) of the concatenation
+  int F, p, sfe;               // sfe: the FE whose effects absorb the shift
+  const double* X;             // the shift c_d = X[d][0] (the raw pass's)
+  int64_t ld;
+};
+
+// block partials [NG upper-triangle entries of sum_g (n a' a'' - V a'' - a' V')][p entries of sum_g n a']
+__global__ __launch_bounds__(256) void k_tab3_gram(Tab3Args t, double* __restrict__ partial, int pstride) {
+  __shared__ double av[kT3Chunk][kT3MaxP + 1];
+  __shared__ double vv[kT3Chunk][kT3MaxP + 1];
+  __shared__ double nn[kT3Chunk];
+  const int p = t.p, tid = threadIdx.x, NG = p * (p + 1) / 2;
+  const int64_t total = t.gstart[t.F];
+  int ei[kT3E], ej[kT3E];
+#pragma unroll
+  for (int k = 0; k < kT3E; ++k) {  // entry -> (i, j), j >= i; or the column sums (i = -1)
+    int e = tid + 256 * k, i = -2, j = 0;
+    if (e < NG) {
+      i = 0;
+      while (e >= p - i) {
+        e -= p - i;
+        ++i;
+      }
+      j = i + e;
+    } else if (e < NG + p) {
+      i = -1;
+      j = e - NG;
+    }
+    ei[k] = i;
+    ej[k] = j;
+  }
+  double acc[kT3E] = {0.0, 0.0, 0.0};
+  for (int64_t g0 = (int64_t)blockIdx.x * kT3Chunk; g0 < total; g0 += (int64_t)gridDim.x * kT3Chunk) {
+    __syncthreads();
+    for (int idx = tid; idx < kT3Chunk * p; idx += 256) {
+      const int gl = idx / p, d = idx - gl * p;
+      const int64_t g = g0 + gl;
+      double a = 0.0, v = 0.0, n = 0.0;
+      if (g < total) {
+        int f = 0;
+        while (g >= t.gstart[f + 1]) ++f;
+        const int64_t gg = g - t.gstart[f], e = gg * p + d;
+        n = (double)t.cnt[f][gg];
+        if (n > 0.0) {
+          const double c = t.X[(int64_t)d * t.ld];
+          a = f == t.sfe ? t.alpha[f][e] - c : t.alpha[f][e];
+          const double Tp = f == t.sfe ? t.T[f][e] : t.T[f][e] - n * c;
+          v = t.S[f][e] - n * c - 0.5 * Tp;
+        }
+      }
+      av[gl][d] = a;
+      vv[gl][d] = v;
+      if (d == 0) nn[gl] = n;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kT3E; ++k) {
+      const int i = ei[k], j = ej[k];
+      if (i == -2) continue;
+      double s = 0.0;
+      if (i >= 0) {
+        for (int gl = 0; gl < kT3Chunk; ++gl) s += (nn[gl] * av[gl][i] - vv[gl][i]) * av[gl][j] - av[gl][i] * vv[gl][j];
+      } else {
+        for (int gl = 0; gl < kT3Chunk; ++gl) s += nn[gl] * av[gl][j];
+      }
+      acc[k] += s;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kT3E; ++k)
+    if (ei[k] != -2) partial[(int64_t)blockIdx.x * pstride + tid + 256 * k] = acc[k];
+}
+
+// the design tiles (I <= J tiles of 16 x 16, design column 0 = intercept, 1 + d = data column d)
+// from the raw tiles and the table sums m; *flag = 1 when the cancellation guard holds
+__global__ __launch_bounds__(256) void k_tab3_assemble(const double* __restrict__ raw, const double* __restrict__ m,
+                                                       int p, int NT, double* __restrict__ tile,
+                                                       double* __restrict__ flag) {
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const int NG = p * (p + 1) / 2, len = NT * (NT + 1) / 2 * 256, D = p + 1;
+  for (int t = threadIdx.x; t < len; t += blockDim.x) {
+    int q = t >> 8, I = 0;
+    while (q >= NT - I) {
+      q -= NT - I;
+      ++I;
+    }
+    const int J = I + q, a = 16 * I + ((t & 255) >> 4), b = 16 * J + (t & 15);
+    double v = raw[t];
+    if (a < D && b < D) {
+      if (a == 0 && b == 0) {
+      } else if (a == 0 || b == 0) {
+        v -= m[NG + (a > b ? a : b) - 1];
+      } else {
+        const int lo = (a < b ? a : b) - 1, hi = (a < b ? b : a) - 1;
+        v += m[lo * p - lo * (lo - 1) / 2 + (hi - lo)];
+        if (a == b && !(v > 0.0 && raw[t] <= kTabKappa * v)) atomicAdd(&bad, 1);
+      }
+    }
+    tile[t] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = bad ? 0.0 : 1.0;
+}
+
+static bool tables3_ok(const lfe_ctx* c) {
+  const char* e = getenv("LFE_TAB3");  // "0": the design pass (A/B)
+  if (e && e[0] == '0') return false;
+  return c->d3.on && c->world == 1 && !c->L.w && !c->records && !c->sw.on && c->p <= kT3MaxP && c->L.P >= 0 &&
+         c->L.n_items > 0;
+}
+
+// the design Gram of [1, y~, x~] from the raw pass and the group tables into host_out (dense D x D);
+// returns 1 when the guard trips (the caller runs the design pass)
+template <int NT>
+static int tables3_gram(lfe_ctx* c, double* host_out) {
+  using Sh = GramShape<NT>;
+  const int p = c->p, D = p + 1, NG = p * (p + 1) / 2;
+  LFE_TRY(dense3_final_T(c));
+  GramArgs a = base_args(c);
+  const void* fn = reinterpret_cast<const void*>(&k_raw_gram<NT>);
+  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kGramThreads, 0)));
+  const int64_t pstride = Sh::LEN;
+  int64_t total = 0;
+  Tab3Args t{};
+  for (int f = 0; f < c->F; ++f) {
+    t.alpha[f] = c->fe[f].alpha;
+    t.S[f] = c->fe[f].S;
+    t.T[f] = c->fe[f].T;
+    t.cnt[f] = c->fe[f].cnt;
+    t.gstart[f] = total;
+    total += c->fe[f].G;
+  }
+  t.gstart[c->F] = total;
+  t.F = c->F;
+  t.p = p;
+  t.sfe = c->L.P;
+  t.X = c->L.X;
+  t.ld = c->ld;
+  const int nblk3 = (int)std::max<int64_t>(1, std::min<int64_t>(256, (total + kT3Chunk - 1) / kT3Chunk));
+  const int ps3 = 256 * kT3E;
+  LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride + (size_t)nblk3 * ps3));
+  LFE_TRY(ensure_dred(c, (size_t)2 * Sh::LEN + NG + p + 8));
+  double* part = c->scratch;
+  double* part3 = c->scratch + (size_t)nblocks * pstride;
+  double* raw = c->dred;                // [LEN] reduced raw tiles
+  double* m = c->dred + Sh::LEN;        // [NG + p] table sums
+  double* tile = m + NG + p;            // [LEN] design tiles, then the flag
+  {
+    ProfScope _ps(c, K_GRAM_DESIGN);
+    void* args[] = {&a, &part, const_cast<int64_t*>(&pstride)};
+    LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(kGramThreads), args, 0, c->stream));
+  }
+  LFE_HIP(hipGetLastError());
+  {
+    ProfScope _ps(c, K_GRAM_TABLES);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(Sh::LEN), dim3(256), 0, c->stream, part, nblocks, pstride, raw);
+    hipLaunchKernelGGL(k_tab3_gram, dim3(nblk3), dim3(256), 0, c->stream, t, part3, ps3);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(NG + p), dim3(256), 0, c->stream, part3, nblk3, (int64_t)ps3, m);
+    hipLaunchKernelGGL(k_tab3_assemble, dim3(1), dim3(256), 0, c->stream, raw, m, p, NT, tile, tile + Sh::LEN);
+  }
+  LFE_HIP(hipGetLastError());
+  std::vector<double> h((size_t)Sh::LEN + 1);
+  LFE_TRY(d2h_sync(c, h.data(), tile, sizeof(double) * (Sh::LEN + 1)));
+  if (h[Sh::LEN] != 1.0) return 1;
+  std::vector<double> full((size_t)D * D);
+  unpack_tiles(h.data(), NT, D, full.data());
+  for (int e = 0; e < D * D; ++e) host_out[e] = full[e];
+  return LFE_OK;
+}
+
 int launch_gram(lfe_ctx* c, double* host_gram) {
+  if (tables3_ok(c)) {  // three or more FEs after the pair-table sweeps: no effect gathers
+    const int NT = (c->p + 1 + 15) / 16;
+    const int rc = NT == 1 ? tables3_gram<1>(c, host_gram) : tables3_gram<2>(c, host_gram);
+    if (rc != 1) return rc;  // else the guard tripped: the design pass
+  }
+
   GramArgs a = base_args(c);
   const bool spec = c->gram_spec;  // the tables tile is already on the stream (lfe_demean)
   c->gram_spec = false;

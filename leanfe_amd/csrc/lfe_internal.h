@@ -231,12 +231,13 @@ struct lfe_ctx {
     size_t X_cap[lfe::kMaxFE][lfe::kMaxFE] = {};
     double* runs[lfe::kMaxFE] = {};
     size_t runs_cap[lfe::kMaxFE] = {};
-    uint32_t* part = nullptr;       // kept rows' (a & 63, b) codes, partitioned by a >> 6
+    uint64_t* part = nullptr;       // kept rows' a & 63 and partner codes, partitioned by a >> 6
     size_t part_cap = 0;
     int32_t* hist = nullptr;        // [bins][workgroups] counts -> scanned bases
     size_t hist_cap = 0;
     int32_t* tiles = nullptr;       // [128] 0, 1, 2, ...: the passes' tile list
     int64_t table_bytes = 0;        // i8 table bytes over all ordered pairs
+    uint32_t t_final = 0;           // FEs whose fe[f].T holds the cross term of the final effects
   } d3;
   double* colsum_part = nullptr;  // [p][blocks][G] fine-limb columns of k_col_sums (lfe_fast.hip)
   size_t colsum_part_cap = 0;
@@ -462,6 +463,8 @@ bool dense3_ok(const lfe_ctx* c, const std::vector<int>& order, int check_from);
 int demean_dense3(lfe_ctx* c, const std::vector<int>& order, double tol, int max_iter, int check_from,
                   int* iterations_out, double* last_out);
 void free_dense3(lfe_ctx* c);
+// the cross terms fe[f].T of every FE from the final effects (the Gram from the tables)
+int dense3_final_T(lfe_ctx* c);
 
 // --- constant sums (lfe_sweep.hip) ---
 int sweep_group_sums(lfe_ctx* c);
@@ -765,10 +768,15 @@ __device__ inline void fix_quanta_col(double M, double rms, double N, double* __
 struct BlockRows {
   int first, lo, hi;
 };
-__device__ __forceinline__ BlockRows block_rows(const int4* __restrict__ items, int n_items, int lane) {
+__device__ __forceinline__ BlockRows block_rows(const int4* __restrict__ items, int n_items, int lane,
+                                                int64_t b = -1, int64_t nb = -1) {
   BlockRows r{0, 0, 0};
   if (n_items <= 0) return r;
-  const int64_t total = items[n_items - 1].z, b = blockIdx.x, nb = gridDim.x;
+  if (b < 0) {  // block b of nb (default: this block of the grid)
+    b = blockIdx.x;
+    nb = gridDim.x;
+  }
+  const int64_t total = items[n_items - 1].z;
   r.lo = (int)((total * b / nb) & ~63ll);
   r.hi = b + 1 == nb ? (int)total : (int)((total * (b + 1) / nb) & ~63ll);
   int lo = 0, hi = n_items;  // the answer lies in [lo, hi]

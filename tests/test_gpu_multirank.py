@@ -569,3 +569,28 @@ def test_owner_shard_solves_in_its_share_of_time(rank):
     assert r["iterations"] == o["iterations"] and r["n_obs"] == o["n_obs"]
     np.testing.assert_allclose(r["beta"], o["beta"], rtol=1e-10, atol=0)
     np.testing.assert_allclose(r["se"], o["se"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("world,n,k,levels,vcov,cl", [
+    (4, 600_000, 14, (20_000, 4_000, 1_000), "iid", None),  # MEGA-shaped, p = 15
+    (3, 500_000, 4, (3_000, 500, 120), "cluster", [1, 2]),
+])
+def test_emulated_owner_sharded_pair_tables(world, n, k, levels, vcov, cl, monkeypatch):
+    """The pair-table sweeps (lfe_dense3.hip, forced with LFE_DENSE=1) on owner shards: each rank's
+    tables count its own rows, the primary FE's cross term stays local and the others' are
+    all-reduced; every rank equals the oracle and repeats bit for bit."""
+    from oracle import altproj
+
+    monkeypatch.setenv("LFE_DENSE", "1")
+    seed = 19
+    out = _run_owned_cl(world, n, k, list(levels), vcov, cl, seed)
+    full = dict(synth.panel(n, k, list(levels), seed=seed))
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    xs = [f"x{j + 1}" for j in range(k)]
+    o = altproj.fit(full, "y", xs, fes, vcov=vcov, cluster_cols=[fes[f] for f in cl] if cl else None)
+    for r in range(world):
+        for res in (out[r]["first"], out[r]["second"]):
+            assert res["iterations"] == o["iterations"] and res["n_obs"] == o["n_obs"]
+            np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=0)
+            np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
+            np.testing.assert_array_equal(res["beta"], out[0]["first"]["beta"])
