@@ -238,11 +238,142 @@ __device__ void dn_write8(const DnBuildArgs& a, const CT* cnt, int bi, int hb0, 
   }
 }
 
+
+// 4-bit counters (eight per word, row-major [HW][GQW]) of the chunk's rows with h in [hlo, hlo + HW);
+// returns whether a counter reached 16 (it carried into its neighbour: the chunk is counted again)
+__device__ bool dn_count4(const DnBuildArgs& a, uint32_t* cw, int hlo, int HW, int r0, int r1) {
+  const int W = a.GQW / 8;
+  __shared__ int ovf4;
+  for (int j = threadIdx.x; j < HW * W; j += blockDim.x) cw[j] = 0u;
+  if (threadIdx.x == 0) ovf4 = 0;
+  __syncthreads();
+  bool over = false;
+  auto one = [&](int h, int q) {
+    const uint32_t d = (uint32_t)(h - hlo);
+    if (h < 0 || d >= (uint32_t)HW) return;
+    const int sh = (q & 7) * 4;
+    const uint32_t old = atomicAdd(&cw[d * W + (q >> 3)], 1u << sh);
+    if (((old >> sh) & 0xfu) == 0xfu) over = true;
+  };
+  const int a0 = min(r1, (r0 + 3) & ~3), a1 = max(a0, r1 & ~3);
+  for (int row = r0 + (int)threadIdx.x; row < a0; row += blockDim.x) one(a.codeP[row], a.codeQ[row]);
+  for (int row = a1 + (int)threadIdx.x; row < r1; row += blockDim.x) one(a.codeP[row], a.codeQ[row]);
+  const int4* cP = reinterpret_cast<const int4*>(a.codeP);
+  const int4* cQ = reinterpret_cast<const int4*>(a.codeQ);
+  constexpr int V = 4;
+  for (int v0 = a0 / 4 + (int)threadIdx.x; v0 < a1 / 4; v0 += V * blockDim.x) {
+    int4 hv[V], qv[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int v = v0 + u * blockDim.x;
+      hv[u] = v < a1 / 4 ? cP[v] : int4{-1, -1, -1, -1};
+      qv[u] = v < a1 / 4 ? cQ[v] : int4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      one(hv[u].x, qv[u].x);
+      one(hv[u].y, qv[u].y);
+      one(hv[u].z, qv[u].z);
+      one(hv[u].w, qv[u].w);
+    }
+  }
+  if (over) ovf4 = 1;
+  __syncthreads();
+  return ovf4 != 0;
+}
+
+// four nibbles (the low 16 bits) -> four bytes, in order
+__device__ __forceinline__ int nib_spread(uint32_t w) {
+  uint32_t t = w & 0xffffu;
+  t = (t | (t << 8)) & 0x00ff00ffu;
+  t = (t | (t << 4)) & 0x0f0f0f0fu;
+  return (int)t;
+}
+
+// pre-filter mode on 4-bit counters: as dn_counts
+__device__ void dn_counts4(const DnBuildArgs& a, const uint32_t* cw, int hlo, int HW) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6, W = a.GQW / 8;
+  for (int r = wave; r < HW; r += nw) {
+    int s = 0;
+    for (int j = lane; j < W; j += 64) {
+      const uint32_t w = cw[r * W + j];
+      const uint32_t b = (w & 0x0f0f0f0fu) + ((w >> 4) & 0x0f0f0f0fu);  // four byte sums <= 30
+      s += (int)((b * 0x01010101u) >> 24);
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+    if (lane == 0 && hlo + r < a.G_P) {
+      a.cntP[hlo + r] = s;
+      if (s > 65535) atomicOr(a.flag, 1);
+    }
+  }
+  for (int q = threadIdx.x; q < a.G_Q; q += blockDim.x) {
+    int s = 0;
+    const int sh = (q & 7) * 4;
+    for (int r = 0; r < HW; ++r) s += (int)((cw[r * W + (q >> 3)] >> sh) & 0xfu);
+    if (s) atomicAdd(&a.cntQ[q], s);
+  }
+}
+
+// dn8 fragments of the primary rows [hb0 16, hb0 16 + HW) from 4-bit counters: no count exceeds 15,
+// so no block is flagged
+__device__ void dn_write4(const DnBuildArgs& a, const uint32_t* cw, int bi, int hb0, int HW) {
+  typedef int v4 __attribute__((ext_vector_type(4)));
+  const int W = a.GQW / 8;
+  const int nkq = a.GQ64 >> 6, nhb = a.B >> 4, nqb = a.GQ64 >> 4, nhk = a.B >> 6;
+  const int hbl_n = HW >> 4, hkl_n = HW >> 6, hk0 = hb0 >> 2;
+  const int na_b = hbl_n * nkq, nb_b = nqb * hkl_n;
+  for (int e = threadIdx.x; e < na_b * 64; e += blockDim.x) {
+    const int blk = e >> 6, l = e & 63, hbl = blk / nkq, kb = blk - hbl * nkq;
+    const uint32_t* src = cw + (hbl * 16 + (l & 15)) * W + ((kb * 64 + 16 * (l >> 4)) >> 3);
+    const uint32_t w0 = src[0], w1 = src[1];
+    const v4 w = v4{nib_spread(w0), nib_spread(w0 >> 16), nib_spread(w1), nib_spread(w1 >> 16)};
+    *reinterpret_cast<v4*>(a.NA8 + (((int64_t)bi * nhb + hb0 + hbl) * nkq + kb) * 1024 + l * 16) = w;
+  }
+  for (int e = threadIdx.x; e < nb_b * 64; e += blockDim.x) {
+    const int blk = e >> 6, l = e & 63, qb = blk / hkl_n, hkl = blk - qb * hkl_n;
+    const int row = hkl * 64 + 16 * (l >> 4), q = qb * 16 + (l & 15), sh = (q & 7) * 4;
+    const uint32_t* src = cw + row * W + (q >> 3);
+    v4 w = v4{0, 0, 0, 0};
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) w[jj >> 2] |= (int)((src[jj * W] >> sh) & 0xfu) << (8 * (jj & 3));
+    *reinterpret_cast<v4*>(a.NB8 + (((int64_t)bi * nqb + qb) * nhk + hk0 + hkl) * 1024 + l * 16) = w;
+  }
+  for (int j = threadIdx.x; j < na_b; j += blockDim.x) {
+    const int hbl = j / nkq, kb = j - hbl * nkq;
+    a.FA[((int64_t)bi * nhb + hb0 + hbl) * a.fa_stride + kb] = 0;
+  }
+  for (int j = threadIdx.x; j < nb_b; j += blockDim.x) {
+    const int qb = j / hkl_n, hkl = j - qb * hkl_n;
+    a.FB[((int64_t)bi * nqb + qb) * a.fb_stride + hk0 + hkl] = 0;
+  }
+}
+
+// one 128-group chunk on 8-bit counters, recounted in two halves on 16-bit counters if a pair
+// passes 255 rows
+__device__ void dn_chunk8(const DnBuildArgs& a, uint32_t* cw, int bi, int hlo, int hb0, int r0, int r1) {
+  constexpr int HC = 2 * kDnHC;
+  if (!dn_count<uint8_t>(a, cw, hlo, HC, r0, r1)) {
+    if (a.cntP) dn_counts<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), hlo, HC);
+    if (a.dn8) dn_write8<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
+    else dn_write<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
+    return;
+  }
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();
+    dn_count<uint16_t>(a, cw, hlo + half * kDnHC, kDnHC, r0, r1);
+    if (a.cntP) dn_counts<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), hlo + half * kDnHC, kDnHC);
+    if (a.dn8) dn_write8<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
+    else dn_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
+  }
+}
+
 // Workgroup (bucket bi, chunk of HC primary groups): counts the chunk's rows in LDS and writes its
 // NA and NB blocks.  HC = 128 groups on 8-bit counters (the bucket's codes are read by B / 128
 // workgroups); a chunk where some (h, q) pair holds more than 255 rows is counted again in two
-// halves on 16-bit counters (counts <= 65535 by the caller's check).  The workgroups of a bucket
-// share an XCD (block i -> XCD i % 8), so its codes are read from one L2.
+// halves on 16-bit counters (counts <= 65535 by the caller's check).  dn8 tables of sparse panels
+// (~0.5 rows per cell): HC = 256 groups on 4-bit counters (the codes read B / 256 times), a chunk
+// with a 16-row cell counted again as two 128-group chunks.  The workgroups of a bucket share an
+// XCD (block i -> XCD i % 8), so its codes are read from one L2.
 __global__ __launch_bounds__(1024) void k_dn_build(DnBuildArgs a) {
   extern __shared__ uint32_t cw[];  // [HC][GQ16] 8-bit or [HC / 2][GQ16] 16-bit counters
   const int i = blockIdx.x, x = i & 7, r = i >> 3;
@@ -252,20 +383,20 @@ __global__ __launch_bounds__(1024) void k_dn_build(DnBuildArgs a) {
   const int it0 = a.bitems[b], it1 = a.bitems[b + 1];
   const int r0 = it1 > it0 ? a.items[it0].y : 0, r1 = it1 > it0 ? a.items[it1 - 1].z : 0;
   const int HC = a.B / a.nch, hlo = (b << a.s) + chunk * HC, hb0 = chunk * (HC / 16);
-  if (HC == 2 * kDnHC) {
-    if (!dn_count<uint8_t>(a, cw, hlo, HC, r0, r1)) {
-      if (a.cntP) dn_counts<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), hlo, HC);
-      if (a.dn8) dn_write8<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
-      else dn_write<uint8_t>(a, reinterpret_cast<const uint8_t*>(cw), bi, hb0, HC);
+  if (HC == 4 * kDnHC) {  // 4-bit counters (dn8 only)
+    if (!dn_count4(a, cw, hlo, HC, r0, r1)) {
+      if (a.cntP) dn_counts4(a, cw, hlo, HC);
+      dn_write4(a, cw, bi, hb0, HC);
       return;
     }
     for (int half = 0; half < 2; ++half) {
       __syncthreads();
-      dn_count<uint16_t>(a, cw, hlo + half * kDnHC, kDnHC, r0, r1);
-      if (a.cntP) dn_counts<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), hlo + half * kDnHC, kDnHC);
-      if (a.dn8) dn_write8<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
-      else dn_write<uint16_t>(a, reinterpret_cast<const uint16_t*>(cw), bi, hb0 + half * (kDnHC / 16), kDnHC);
+      dn_chunk8(a, cw, bi, hlo + half * 2 * kDnHC, hb0 + half * (2 * kDnHC / 16), r0, r1);
     }
+    return;
+  }
+  if (HC == 2 * kDnHC) {
+    dn_chunk8(a, cw, bi, hlo, hb0, r0, r1);
     return;
   }
   dn_count<uint16_t>(a, cw, hlo, HC, r0, r1);
@@ -970,7 +1101,13 @@ int dense_build(lfe_ctx* c, bool pre) {
   const bool c8_fits = (size_t)2 * kDnHC * GQW <= 150 * 1024 && B % (2 * kDnHC) == 0;
   bool c8 = c8_fits && (int64_t)c->nbe * (B / (2 * kDnHC)) >= c->n_cu;
   if (const char* e = getenv("LFE_DN_C8")) c8 = c8_fits && e[0] == '1';  // tests: force either form
-  a.nch = B / (c8 ? 2 * kDnHC : kDnHC);
+  // 256-group chunks on 4-bit counters (the i8 tables; half the code reads of the 8-bit form) where
+  // cells average under 2 rows (a 16-row cell is then rare) and the chunks still fill the CUs
+  const bool c4_fits = c8_fits && c->dn8 && B % (4 * kDnHC) == 0;
+  bool c4 = c4_fits && (int64_t)c->nbe * (B / (4 * kDnHC)) >= c->n_cu &&
+            (double)c->n < 2.0 * (double)std::max(c->nbe, 1) * B * GQ64;
+  if (const char* e = getenv("LFE_DN_C4")) c4 = c4_fits && e[0] == '1';  // A/B, tests
+  a.nch = B / (c4 ? 4 * kDnHC : c8 ? 2 * kDnHC : kDnHC);
   a.NA = c->dn_na;
   a.NB = c->dn_nb;
   const size_t lds = sizeof(uint16_t) * kDnHC * GQW;  // both forms
@@ -1020,6 +1157,15 @@ static Dn8Args dn8_args(const lfe_ctx* c) {
   a.p = c->p;
   a.lda = a.ldo = c->p;
   return a;
+}
+
+// K2 streaming workgroups per bucket (tile): two are resident per CU (64 KB of LDS each), so the
+// parts fill one round of those 2 n_cu slots (a second, partial round costs a whole workgroup time:
+// 196 buckets x 3 parts = 588 > 512), at least 8 output blocks each
+static int k2_parts(const lfe_ctx* c, int nbe, int nrb) {
+  int np = (int)std::max<int64_t>(1, (2 * (int64_t)c->n_cu) / std::max(nbe, 1));
+  if (const char* e = getenv("LFE_K2_NP")) np = std::max(1, atoi(e));  // A/B only
+  return std::min(np, std::max(1, nrb / 8));
 }
 
 template <bool K2>
@@ -1115,8 +1261,7 @@ int dense_tq(lfe_ctx* c, double* runs) {
       LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k2s), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   kDn8TileBytes));
       const int nbe = std::max(c->nbe, 1);
-      int np = (int)std::max<int64_t>(1, (2 * (int64_t)c->n_cu + nbe - 1) / nbe);  // >= 2 workgroups per CU
-      np = std::min(np, std::max(1, a.nrb / 8));                                   // >= 8 blocks each
+      const int np = k2_parts(c, nbe, a.nrb);
       hipLaunchKernelGGL(k_dn8_k2s, dim3(nbe * np), dim3(512), kDn8TileBytes, c->stream, a, np);
       LFE_HIP(hipGetLastError());
       return LFE_OK;
@@ -1164,9 +1309,7 @@ int dn8_pair_pass(lfe_ctx* c, const PairPass& pp) {
   a.runs = pp.runs;
   LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k2s), hipFuncAttributeMaxDynamicSharedMemorySize,
                               kDn8TileBytes));
-  // >= 2 workgroups per CU over the tiles, >= 8 output blocks each
-  int np = (int)std::max<int64_t>(1, (2 * (int64_t)c->n_cu + pp.ntile_k - 1) / pp.ntile_k);
-  np = std::min(np, std::max(1, a.nrb / 8));
+  const int np = k2_parts(c, pp.ntile_k, a.nrb);
   hipLaunchKernelGGL(k_dn8_k2s, dim3(pp.ntile_k * np), dim3(512), kDn8TileBytes, c->stream, a, np);
   LFE_HIP(hipGetLastError());
   return LFE_OK;

@@ -991,6 +991,9 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
                                                             double* __restrict__ beta, double* __restrict__ beta_copy,
                                                             double* __restrict__ ok);
 
+__global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __restrict__ beta,
+                             double* __restrict__ beta_copy, double* __restrict__ ok);
+
 // design tile into out_dev[0, 256) and the guard flag into *flag_dev, from the group tables; with
 // beta, also the Cholesky solve of the tile (beta, beta_copy, ok as k_chol_solve)
 static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, double* beta = nullptr,
@@ -1032,8 +1035,14 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, do
       src = msum;
       ns = 1;
     }
-    hipLaunchKernelGGL(kfinal, dim3(1), dim3(1024), 0, c->stream, src, ns, c->raw_tile, p, out_dev, flag_dev, beta,
-                       beta_copy, ok);
+    static const bool split = [] {  // diagnostic: the Cholesky as its own launch (rocprof A/B)
+      const char* e = getenv("LFE_CHOL_SPLIT");
+      return e && e[0] == '1';
+    }();
+    hipLaunchKernelGGL(kfinal, dim3(1), dim3(1024), 0, c->stream, src, ns, c->raw_tile, p, out_dev, flag_dev,
+                       split ? nullptr : beta, beta_copy, ok);
+    if (split && beta)
+      hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, out_dev, p, beta, beta_copy, ok);
     return LFE_OK;
   };
   switch (PM) {
@@ -1073,8 +1082,18 @@ constexpr int kCholM = 12;
 // column elements other lanes need arrive by shuffles, and the forward / back substitutions run
 // in the order of the serial loops of polars_impl.py:212-226's LAPACK-free restatement (so the
 // bits are those of the one-thread form this replaced: ~1.5 us instead of ~15 us of LDS round trips)
-__device__ void chol_solve_wave(const double* tile, int p, double* __restrict__ beta, double* __restrict__ beta_copy,
-                                double* __restrict__ ok, double (*Ls)[kCholM + 1]) {
+// lane k's value to every lane (k wave-uniform: two v_readlane, no LDS round trip as ds_bpermute)
+__device__ __forceinline__ double bcast_lane(double v, int k) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ void chol_solve_wave(const double* tile, int p, double* __restrict__ beta,
+                                                double* __restrict__ beta_copy, double* __restrict__ ok,
+                                                double (*Ls)[kCholM + 1]) {
+  // every loop runs its constant bound with the active range as a predicate, so all of them
+  // unroll and r / col / xs stay in registers (a loop left rolled indexes them in scratch memory)
   constexpr int M = kCholM;
   const int lane = threadIdx.x & 63;
   const int m = p;  // intercept + k regressors
@@ -1086,17 +1105,18 @@ __device__ void chol_solve_wave(const double* tile, int p, double* __restrict__ 
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < M; ++j) {
-    if (j >= m) break;  // uniform
-    const double d = __shfl(r[j], j, 64);
-    bad |= !(d > 0.0);
+    const bool live = j < m;  // uniform
+    const double d = bcast_lane(r[j], j);
+    bad |= live && !(d > 0.0);
     const double ljj = sqrt(d > 0.0 ? d : 1.0);
-    if (lane == j) r[j] = ljj;
-    else if (lane > j && lane < m) r[j] /= ljj;
+    if (live) {
+      if (lane == j) r[j] = ljj;
+      else if (lane > j && lane < m) r[j] /= ljj;
+    }
 #pragma unroll
     for (int k = j + 1; k < M; ++k) {
-      if (k >= m) break;
-      const double lkj = __shfl(r[j], k, 64);
-      if (lane >= k && lane < m) r[k] -= r[j] * lkj;  // L[i][k] -= L[i][j] L[k][j], j < k <= i
+      const double lkj = bcast_lane(r[j], k);
+      if (live && k < m && lane >= k && lane < m) r[k] -= r[j] * lkj;  // L[i][k] -= L[i][j] L[k][j], j < k <= i
     }
   }
   if (bad) {
@@ -1107,10 +1127,11 @@ __device__ void chol_solve_wave(const double* tile, int p, double* __restrict__ 
   double acc = bv;
 #pragma unroll
   for (int k = 0; k < M; ++k) {
-    if (k >= m) break;
-    const double yk = __shfl(acc / r[k], k, 64);  // lane k: r[k] = L[k][k]
-    if (lane == k) acc = yk;
-    else if (lane > k) acc -= r[k] * yk;
+    const double yk = bcast_lane(acc / (r[k] != 0.0 ? r[k] : 1.0), k);  // lane k: r[k] = L[k][k]
+    if (k < m) {
+      if (lane == k) acc = yk;
+      else if (lane > k) acc -= r[k] * yk;
+    }
   }
   // back: x_i = (y_i - sum_{k > i} L[k][i] x_k) / L[i][i], k ascending: lane i's column of L via LDS
   if (lane < m)
@@ -1130,15 +1151,11 @@ __device__ void chol_solve_wave(const double* tile, int p, double* __restrict__ 
     if (k == lane) diag = r[k];
 #pragma unroll
   for (int i = M - 1; i >= 0; --i) {
-    if (i >= m) continue;
     double v = acc;  // lane i: y_i
 #pragma unroll
-    for (int k = i + 1; k < M; ++k)
-      if (k < m) v -= col[k] * xs[k];
-    const double xi = __shfl(v / diag, i, 64);
-#pragma unroll
-    for (int k = 0; k < M; ++k)
-      if (k == i) xs[k] = xi;
+    for (int k = i + 1; k < M; ++k) v -= col[k] * xs[k];  // xs[k] = 0 for k >= m
+    const double xi = bcast_lane(v / diag, i);
+    if (i < m) xs[i] = xi;
   }
   if (lane < m) {
     double x = 0.0;

@@ -197,3 +197,34 @@ def test_dense_i8_flagged_blocks_mixed_with_exact_blocks(monkeypatch):
     monkeypatch.setenv("LFE_DN8", "0")
     f64 = _fit(data, xs)
     np.testing.assert_allclose(i8[0], f64[0], rtol=1e-12, atol=0)
+
+
+def test_dense_four_bit_counters(monkeypatch):
+    """The 256-group chunks on 4-bit counters (LFE_DN_C4=1): a sparse panel's tables are the same
+    bits as the 8-bit build's, and a panel with cells of 16+ rows (two ~50K-row pairs and many
+    2-16-row ones) recounts those chunks on 8- and 16-bit counters and still matches the oracle."""
+    from leanfe_amd import synth
+
+    xs = ["x1", "x2", "x3"]
+    data = synth.panel(1_000_000, 3, [4_096, 1_000], seed=13)
+    monkeypatch.setenv("LFE_DENSE", "1")
+    monkeypatch.setenv("LFE_DN_C4", "1")
+    c4 = _fit(data, xs)
+    monkeypatch.setenv("LFE_DN_C4", "0")
+    c8 = _fit(data, xs)
+    np.testing.assert_array_equal(c4[0], c8[0])
+    np.testing.assert_array_equal(c4[1], c8[1])
+    _check(c4, _oracle(data, xs))
+    rng = np.random.default_rng(17)
+    n = 400_000
+    fe1 = rng.integers(0, 1_024, n).astype(np.int32)
+    fe2 = rng.integers(0, 40, n).astype(np.int32)
+    heavy = rng.random(n) < 0.25
+    fe1[heavy] = np.where(rng.random(heavy.sum()) < 0.5, 7, 700).astype(np.int32)
+    fe2[heavy] = 3
+    x = rng.standard_normal((n, 3))
+    y = x @ np.array([1.0, -0.5, 0.25]) + rng.standard_normal(1_024)[fe1] + rng.standard_normal(40)[fe2] + \
+        rng.standard_normal(n)
+    heavy_data = {"y": y, "fe1": fe1, "fe2": fe2, **{f"x{j + 1}": x[:, j].copy() for j in range(3)}}
+    monkeypatch.setenv("LFE_DN_C4", "1")
+    _check(_fit(heavy_data, xs), _oracle(heavy_data, xs))
