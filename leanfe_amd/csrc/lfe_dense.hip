@@ -34,7 +34,9 @@
 #include "lfe_internal.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 namespace lfe {
 
@@ -603,14 +605,25 @@ __device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p,
     bad |= !isfinite(v[u]);
     m = fmax(m, fabs(v[u]));
   }
-  red[tid] = bad ? __builtin_nan("") : m;
+  // column max over the wave's four row groups (lanes c, c + 16, c + 32, c + 48), then over the
+  // waves: 16 LDS values per column instead of a 64-long serial loop (NaN marks a bad column)
+  double mv = bad ? __builtin_nan("") : m;
+#pragma unroll
+  for (int off = 16; off < 64; off <<= 1) {
+    const double o = __shfl_xor(mv, off, 64);
+    mv = (isnan(o) || isnan(mv)) ? __builtin_nan("") : fmax(mv, o);
+  }
+  constexpr int NW = NT / 64;
+  if ((tid & 63) < 16) red[(tid >> 6) * 16 + col] = mv;
   __syncthreads();
   if (tid < 16) {
     double mm = 0.0;
     bool nb = false;
-    for (int t = tid; t < NT; t += 16) {
-      nb |= isnan(red[t]);
-      mm = fmax(mm, red[t]);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const double t = red[w * 16 + tid];
+      nb |= isnan(t);
+      mm = fmax(mm, t);
     }
     const int e = mm > 0.0 ? ilogb(mm) + 1 : 0;  // max |alpha| < 2^e
     sc[tid] = nb ? __builtin_nan("") : ldexp(1.0, e - 54);
@@ -671,6 +684,7 @@ struct Dn8Args {
   double* alphaP;
   double* zero_check;
   double* runs;           // K2: per-bucket slots [nbe][G_Q][p]
+  unsigned long long* dbg;  // diagnostic (LFE_DN8_TIMING): per workgroup wall clock at start / prologue end / end
 };
 
 // K1 (K2 = false): T_P of R output blocks (16 primary groups each) per wave; K2: T_Q,b of R blocks
@@ -828,31 +842,48 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
 constexpr int kDn8MaxKb = 16;
 constexpr int kDn8Ring = 8;
 
+// the A-fragment ring of one wave: its first kDn8Ring loads are issued before the workgroup's
+// digit prologue, so the table's HBM latency overlaps the digitization
+struct Dn8Ring {
+  v4i A[kDn8Ring];
+  int64_t rl;  // load cursor: step -> (row rl, k block kl)
+  int kl;
+};
+
+__device__ __forceinline__ void dn8_ring_fill(const Dn8Args& a, Dn8Ring& R, int64_t base, int first, int stride,
+                                              int end, int lane) {
+  R.rl = base + first;
+  R.kl = 0;
+  if (first >= end) return;
+  const int nkb = a.nkb;
+  const int steps = (end - first + stride - 1) / stride * nkb;
+  const int8_t* tab = a.Nm + lane * 16;
+#pragma unroll
+  for (int u = 0; u < kDn8Ring; ++u) {
+    if (u < steps) R.A[u] = *reinterpret_cast<const v4i*>(tab + (R.rl * nkb + R.kl) * 1024);
+    if (++R.kl == nkb) {
+      R.kl = 0;
+      R.rl += stride;
+    }
+  }
+}
+
 // the steps of one wave: output blocks first, first + stride, ... < end (table rows base + i)
 template <bool K2>
 __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* __restrict__ fr,
                                                 const double* __restrict__ sc, int64_t base, int first, int stride,
-                                                int end, int lane) {
+                                                int end, int lane, Dn8Ring& R) {
   const int g = lane >> 4, c = lane & 15, p = a.p, nkb = a.nkb;
   if (first >= end) return;
   const int nblk = (end - first + stride - 1) / stride;
   const int steps = nblk * nkb;
   const int8_t* tab = a.Nm + lane * 16;
-  v4i A[kDn8Ring];
-  // load cursor: step jl -> (row rl, k block kl)
-  int64_t rl = base + first;
-  int kl = 0;
   auto adv_l = [&]() {
-    if (++kl == nkb) {
-      kl = 0;
-      rl += stride;
+    if (++R.kl == nkb) {
+      R.kl = 0;
+      R.rl += stride;
     }
   };
-#pragma unroll
-  for (int u = 0; u < kDn8Ring; ++u) {
-    if (u < steps) A[u] = *reinterpret_cast<const v4i*>(tab + (rl * nkb + kl) * 1024);
-    adv_l();
-  }
   // consume cursor
   int64_t rc = base + first;
   int kc = 0;
@@ -861,6 +892,11 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
   for (int d = 0; d < 8; ++d) D[d] = v4i{0, 0, 0, 0};
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   uint64_t fw0 = 0, fw1 = 0;
+  // K1: the block's projection operands (n_P and S_P of its rows), loaded at its first step and
+  // used at its last, so the epilogue does not wait on dependent global loads
+  double sp[4] = {0.0, 0.0, 0.0, 0.0};
+  int32_t np4[4] = {0, 0, 0, 0};
+  int hrow = 0;
   for (int j0 = 0; j0 < steps; j0 += kDn8Ring) {
 #pragma unroll
     for (int u = 0; u < kDn8Ring; ++u) {
@@ -869,9 +905,21 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
         const uint8_t* fl = a.flags + rc * a.fstride;
         fw0 = *reinterpret_cast<const uint64_t*>(fl);
         fw1 = nkb > 8 ? *reinterpret_cast<const uint64_t*>(fl + 8) : 0ull;
+        if (!K2) {
+          const int bi = (int)(rc / a.nrb), rb = (int)(rc - (int64_t)bi * a.nrb);
+          hrow = (a.blist[bi] << a.s) + rb * 16 + 4 * g;  // rows hrow + q, q < 4
+          const int lo = a.blist[bi] << a.s;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int h = hrow + q, row = h - lo;
+            const bool ok = c < p && row < a.B && h < a.G_P;
+            np4[q] = ok ? a.cntP[h] : 0;
+            sp[q] = ok ? a.S_P[(int64_t)h * p + c] : 0.0;
+          }
+        }
       }
-      const v4i av = A[u];
-      if (j0 + u + kDn8Ring < steps) A[u] = *reinterpret_cast<const v4i*>(tab + (rl * nkb + kl) * 1024);
+      const v4i av = R.A[u];
+      if (j0 + u + kDn8Ring < steps) R.A[u] = *reinterpret_cast<const v4i*>(tab + (R.rl * nkb + R.kl) * 1024);
       adv_l();
 #pragma unroll
       for (int h = 0; h < 2; ++h) {  // the digit fragments in two halves of four (register pressure)
@@ -928,12 +976,9 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
             if (K2) {
               if (row < a.G_Q) a.runs[((int64_t)bi * a.G_Q + row) * a.ldo + c] = acc[q];
             } else {
-              const int h = (a.blist[bi] << a.s) + row;
-              if (row < a.B && h < a.G_P) {
-                const int32_t n = a.cntP[h];
-                const int64_t e = (int64_t)h * p + c;
-                a.alphaP[e] = n > 0 ? (a.S_P[e] - acc[q]) / (double)n : 0.0;
-              }
+              const int h = hrow + q;
+              if (row < a.B && h < a.G_P)
+                a.alphaP[(int64_t)h * p + c] = np4[q] > 0 ? (sp[q] - acc[q]) / (double)np4[q] : 0.0;
             }
           }
         }
@@ -957,6 +1002,11 @@ __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), W = blockDim.x >> 6;
   if (a.zero_check && blockIdx.x == 0 && tid == 0) *a.zero_check = 0.0;
+  const int64_t total = (int64_t)a.nbe * a.nrb;
+  const int i0 = (int)(total * blockIdx.x / gridDim.x), i1 = (int)(total * (blockIdx.x + 1) / gridDim.x);
+  if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3] = wall_clock64();
+  Dn8Ring R;
+  dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
   const int ntile = (a.nkb + 7) / 8;
   for (int t = 0; t < ntile; ++t) {
     if (t) __syncthreads();
@@ -964,9 +1014,12 @@ __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
                           fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red);
   }
   __syncthreads();
-  const int64_t total = (int64_t)a.nbe * a.nrb;
-  const int i0 = (int)(total * blockIdx.x / gridDim.x), i1 = (int)(total * (blockIdx.x + 1) / gridDim.x);
-  dn8_wave_stream<false>(a, fr, sc, 0, i0 + wave, W, i1, lane);
+  if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3 + 1] = wall_clock64();
+  dn8_wave_stream<false>(a, fr, sc, 0, i0 + wave, W, i1, lane, R);
+  if (a.dbg) {
+    __syncthreads();
+    if (tid == 0) a.dbg[blockIdx.x * 3 + 2] = wall_clock64();
+  }
 }
 
 // K2: workgroup (bucket bi, part j of np): the bucket's alpha_P rows digitized in LDS, then output
@@ -978,11 +1031,48 @@ __global__ __launch_bounds__(512, 4) void k_dn8_k2s(Dn8Args a, int np) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), W = blockDim.x >> 6;
   const int bi = blockIdx.x / np, part = blockIdx.x - bi * np;
+  const int i0 = a.nrb * part / np, i1 = a.nrb * (part + 1) / np;
+  if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3] = wall_clock64();
+  Dn8Ring R;
+  dn8_ring_fill(a, R, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane);
   const int lo = a.blist[bi] << a.s;
   dn8_tile_digits<512>(a.alpha + (int64_t)lo * a.lda, max(0, min(a.B, a.G_P - lo)), a.p, a.lda, fr, sc, red);
   __syncthreads();
-  const int i0 = a.nrb * part / np, i1 = a.nrb * (part + 1) / np;
-  dn8_wave_stream<true>(a, fr, sc, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane);
+  if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3 + 1] = wall_clock64();
+  dn8_wave_stream<true>(a, fr, sc, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane, R);
+  if (a.dbg) {
+    __syncthreads();
+    if (tid == 0) a.dbg[blockIdx.x * 3 + 2] = wall_clock64();
+  }
+}
+
+// LFE_DN8_TIMING=1 (diagnostic): per-workgroup phase times of the last K1 / K2 launch to stderr
+static bool dn8_timing() {
+  static const bool on = [] {
+    const char* e = getenv("LFE_DN8_TIMING");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+static unsigned long long* g_dn8_dbg = nullptr;
+static int dn8_timing_report(lfe_ctx* c, const char* name, int grid) {
+  std::vector<unsigned long long> h((size_t)grid * 3);
+  LFE_HIP(hipStreamSynchronize(c->stream));
+  LFE_HIP(hipMemcpy(h.data(), g_dn8_dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+  unsigned long long t0 = ~0ull, t1 = 0;
+  double pro = 0, str = 0, pro_max = 0, str_max = 0;
+  for (int b = 0; b < grid; ++b) {
+    t0 = std::min(t0, h[3 * b]);
+    t1 = std::max(t1, h[3 * b + 2]);
+    const double p = (double)(h[3 * b + 1] - h[3 * b]) / 100.0, q = (double)(h[3 * b + 2] - h[3 * b + 1]) / 100.0;
+    pro += p;
+    str += q;
+    pro_max = std::max(pro_max, p);
+    str_max = std::max(str_max, q);
+  }
+  fprintf(stderr, "[dn8 %s] grid %d span %.1f us, prologue avg %.1f max %.1f us, stream avg %.1f max %.1f us\n", name,
+          grid, (double)(t1 - t0) / 100.0, pro / grid, pro_max, str / grid, str_max);
+  return LFE_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1211,8 +1301,13 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
                                   (int)lds));
       const int64_t total = (int64_t)std::max(c->nbe, 1) * a.nrb;
       const int grid = (int)std::min<int64_t>(c->n_cu, (total + 15) / 16);
+      if (dn8_timing()) {
+        if (!g_dn8_dbg) LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 3 * 65536));
+        a.dbg = g_dn8_dbg;
+      }
       hipLaunchKernelGGL(k_dn8_k1s, dim3(grid), dim3(1024), lds, c->stream, a);
       LFE_HIP(hipGetLastError());
+      if (a.dbg) return dn8_timing_report(c, "K1", grid);
       return LFE_OK;
     }
     // tiled form: alpha_Q's digit tiles formed once per pass by k_dn8_digits
@@ -1262,8 +1357,13 @@ int dense_tq(lfe_ctx* c, double* runs) {
                                   kDn8TileBytes));
       const int nbe = std::max(c->nbe, 1);
       const int np = k2_parts(c, nbe, a.nrb);
+      if (dn8_timing()) {
+        if (!g_dn8_dbg) LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 3 * 65536));
+        a.dbg = g_dn8_dbg;
+      }
       hipLaunchKernelGGL(k_dn8_k2s, dim3(nbe * np), dim3(512), kDn8TileBytes, c->stream, a, np);
       LFE_HIP(hipGetLastError());
+      if (a.dbg) return dn8_timing_report(c, "K2", nbe * np);
       return LFE_OK;
     }
     constexpr int waves = 8;  // every workgroup digitizes its bucket's alpha_P rows: 16 blocks each

@@ -976,8 +976,25 @@ __global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restri
     if (lane == 63) red[wave][e] = v;
   }
   __syncthreads();
+  // entry-major [NA][blocks]: the final kernel's lanes then read consecutive blocks of one entry
   for (int e = threadIdx.x; e < NA; e += blockDim.x)
-    partial[(int64_t)blockIdx.x * NA + e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    partial[(int64_t)e * gridDim.x + blockIdx.x] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+}
+
+// out[e] = sum over the row e of an entry-major [rows][nblk] partial table, blocks in order
+__global__ __launch_bounds__(256) void k_sum_rows(const double* __restrict__ partial, int nblk,
+                                                  double* __restrict__ out) {
+  __shared__ double red[256];
+  const int e = blockIdx.x;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += 256) s += partial[(int64_t)e * nblk + b];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[e] = red[0];
 }
 
 static bool tables_gram_ok(const lfe_ctx* c) {
@@ -1029,7 +1046,7 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, do
     const double* src = part;
     int ns = nblk;
     if (c->owner_on) {
-      hipLaunchKernelGGL(k_reduce_partials, dim3(NA), dim3(256), 0, c->stream, part, nblk, (int64_t)NA, msum);
+      hipLaunchKernelGGL(k_sum_rows, dim3(NA), dim3(256), 0, c->stream, part, nblk, msum);
       LFE_HIP(hipGetLastError());
       LFE_TRY(allreduce_sum_f64(c, msum, (size_t)NA));
       src = msum;
@@ -1201,7 +1218,7 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int e = wave + 16 * u, q = lane + 64 * rr;
-        v[u][rr] = (e < NA && q < nblk) ? partial[(int64_t)q * NA + e] : 0.0;
+        v[u][rr] = (e < NA && q < nblk) ? partial[(int64_t)e * nblk + q] : 0.0;
       }
 #pragma unroll
     for (int u = 0; u < EU; ++u) {
