@@ -672,7 +672,8 @@ struct Dn8Args {
   const uint16_t* X;      // the flagged blocks' u16 counts (16 x 64, natural order)
   const int32_t* blist;
   int nbe, s, B, G_Q, G_P, p;
-  int lda, ldo;           // K2: row strides of alpha_P and of the slots (p for the two-FE passes)
+  int lda, ldo;           // row strides: K1 alpha_Q / S_P and alpha_P, K2 alpha_P / the slots (the
+                          // fit's p; `p` is then the pass's column group, <= 16)
   int nkb;                // 64-row k blocks per output block (K1: GQ64 / 64, K2: B / 64)
   int nrb;                // output blocks per bucket (K1: B / 16, K2: GQ64 / 16)
   int rbw;                // output blocks per workgroup
@@ -800,7 +801,7 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
             double al = 0.0;
             if (c < p) {
               if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * a.lda + c] : 0.0;
-              else al = kr < a.G_Q ? a.alpha[(int64_t)kr * p + c] : 0.0;
+              else al = kr < a.G_Q ? a.alpha[(int64_t)kr * a.lda + c] : 0.0;
             }
             sx += (double)X[(4 * g + x) * 64 + jj] * al;
           }
@@ -823,7 +824,7 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
         const int h = lo + row;
         if (row < a.B && h < a.G_P) {
           const int32_t n = a.cntP[h];
-          const int64_t e = (int64_t)h * p + c;
+          const int64_t e = (int64_t)h * a.ldo + c;
           a.alphaP[e] = n > 0 ? (a.S_P[e] - acc[r][x]) / (double)n : 0.0;
         }
       }
@@ -914,7 +915,7 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
             const int h = hrow + q, row = h - lo;
             const bool ok = c < p && row < a.B && h < a.G_P;
             np4[q] = ok ? a.cntP[h] : 0;
-            sp[q] = ok ? a.S_P[(int64_t)h * p + c] : 0.0;
+            sp[q] = ok ? a.S_P[(int64_t)h * a.ldo + c] : 0.0;
           }
         }
       }
@@ -958,7 +959,7 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
                 double al = 0.0;
                 if (c < p) {
                   if (K2) al = (kr < a.B && lo + kr < a.G_P) ? a.alpha[(int64_t)(lo + kr) * a.lda + c] : 0.0;
-                  else al = kr < a.G_Q ? a.alpha[(int64_t)kr * p + c] : 0.0;
+                  else al = kr < a.G_Q ? a.alpha[(int64_t)kr * a.lda + c] : 0.0;
                 }
                 sx += (double)X[(4 * g + q) * 64 + jj] * al;
               }
@@ -978,7 +979,7 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
             } else {
               const int h = hrow + q;
               if (row < a.B && h < a.G_P)
-                a.alphaP[(int64_t)h * p + c] = np4[q] > 0 ? (sp[q] - acc[q]) / (double)np4[q] : 0.0;
+                a.alphaP[(int64_t)h * a.ldo + c] = np4[q] > 0 ? (sp[q] - acc[q]) / (double)np4[q] : 0.0;
             }
           }
         }
@@ -1010,7 +1011,7 @@ __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
   const int ntile = (a.nkb + 7) / 8;
   for (int t = 0; t < ntile; ++t) {
     if (t) __syncthreads();
-    dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.p, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p, a.p,
+    dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.lda, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p, a.lda,
                           fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red);
   }
   __syncthreads();
@@ -1103,7 +1104,9 @@ static bool dn8_ok(const lfe_ctx* c) {
   const char* e = getenv("LFE_DN8");
   if (e && e[0] == '0') return false;
   const int64_t B = 1ll << c->L.s;
-  return B % 64 == 0 && (size_t)kDnHC * dn_gq64(c) * 2 <= 150 * 1024 && c->p <= 16;
+  if (!(B % 64 == 0 && (size_t)kDnHC * dn_gq64(c) * 2 <= 150 * 1024)) return false;
+  // more than 16 columns: the streaming passes, one per 16-column group (K1's digit tiles in LDS)
+  return c->p <= 16 || (dn_gq64(c) / 64 <= kDn8MaxKb && !dn8_tiled());
 }
 
 static bool dn8_ok(const lfe_ctx* c);
@@ -1116,11 +1119,12 @@ bool dense_pre_ok(const lfe_ctx* c) {
   if (e && e[0] == '0') return false;
   const char* pe = getenv("LFE_DN_PRE");
   if (pe && pe[0] == '0') return false;
-  const int P = c->L.P, Q = 1 - P, p = c->p;
-  if (!(c->world == 1 || c->owner_on) || p > 16 || c->nbe < 1 || !dn8_ok(c)) return false;
-  const int64_t B = 1ll << c->L.s, GQ16 = ((int64_t)c->fe[Q].G + 15) / 16 * 16;
+  const int P = c->L.P, Q = 1 - P;
+  (void)P;
+  if (!(c->world == 1 || c->owner_on) || c->nbe < 1 || !dn8_ok(c)) return false;
+  const int64_t B = 1ll << c->L.s;
+  (void)Q;
   if (B % kDnHC != 0) return false;
-  if (GQ16 * p * 8 > 100 * 1024 || B * p * 8 > 64 * 1024) return false;
   return (e && e[0] == '1') || (double)c->n >= 0.3 * (double)dn_cells(c);
 }
 
@@ -1128,10 +1132,11 @@ bool dense_ok(const lfe_ctx* c) {
   const char* e = getenv("LFE_DENSE");  // "0": never (A/B); "1": whenever it fits
   if (e && e[0] == '0') return false;
   const int P = c->L.P, Q = 1 - P, p = c->p;
-  if (!(c->world == 1 || c->owner_on) || p > 16 || c->nbe < 1) return false;
+  if (!(c->world == 1 || c->owner_on) || c->nbe < 1) return false;
   const int64_t B = 1ll << c->L.s, GQ16 = ((int64_t)c->fe[Q].G + 15) / 16 * 16;
   if (B % kDnHC != 0) return false;
-  if (GQ16 * p * 8 > 100 * 1024 || B * p * 8 > 64 * 1024) return false;  // the B operand tables in LDS
+  // the f64 passes hold the B operand tables in LDS (p <= 16); the i8 passes their digit tiles
+  if (!dn8_ok(c) && (p > 16 || GQ16 * p * 8 > 100 * 1024 || B * p * 8 > 64 * 1024)) return false;
   if (kDnHC * GQ16 * 2 > 150 * 1024) return false;                        // the build's counters
   if (c->fe[P].cmax > 65535) return false;                                 // uint16 counts
   // the products cost ~ the cells (~1.1 ns per cell and pass), the row passes ~ the rows (~3.2 ns
@@ -1305,8 +1310,18 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
         if (!g_dn8_dbg) LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 3 * 65536));
         a.dbg = g_dn8_dbg;
       }
-      hipLaunchKernelGGL(k_dn8_k1s, dim3(grid), dim3(1024), lds, c->stream, a);
-      LFE_HIP(hipGetLastError());
+      // wide fits: one pass per 16-column group (each projects its own columns of alpha_P)
+      const int p = c->p;
+      for (int c0 = 0; c0 < p; c0 += 16) {
+        Dn8Args g = a;
+        g.p = std::min(16, p - c0);
+        g.alpha = alphaQ + c0;
+        g.S_P = a.S_P + c0;
+        g.alphaP = a.alphaP + c0;
+        if (c0) g.zero_check = nullptr;
+        hipLaunchKernelGGL(k_dn8_k1s, dim3(grid), dim3(1024), lds, c->stream, g);
+        LFE_HIP(hipGetLastError());
+      }
       if (a.dbg) return dn8_timing_report(c, "K1", grid);
       return LFE_OK;
     }
@@ -1361,8 +1376,15 @@ int dense_tq(lfe_ctx* c, double* runs) {
         if (!g_dn8_dbg) LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 3 * 65536));
         a.dbg = g_dn8_dbg;
       }
-      hipLaunchKernelGGL(k_dn8_k2s, dim3(nbe * np), dim3(512), kDn8TileBytes, c->stream, a, np);
-      LFE_HIP(hipGetLastError());
+      const int p = c->p;
+      for (int c0 = 0; c0 < p; c0 += 16) {  // wide fits: one pass per 16-column group
+        Dn8Args g = a;
+        g.p = std::min(16, p - c0);
+        g.alpha = a.alpha + c0;
+        g.runs = runs + c0;
+        hipLaunchKernelGGL(k_dn8_k2s, dim3(nbe * np), dim3(512), kDn8TileBytes, c->stream, g, np);
+        LFE_HIP(hipGetLastError());
+      }
       if (a.dbg) return dn8_timing_report(c, "K2", nbe * np);
       return LFE_OK;
     }

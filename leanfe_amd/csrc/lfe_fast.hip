@@ -664,8 +664,9 @@ __global__ void k_raw_combine(const double* __restrict__ slots, int world, int p
   if (t < 16) sh[t] = sh[16 + t] = slots[256 + t];
 }
 
-// Group sums of three or more FEs whose non-primary tables do not fit LDS whole (the reference's
-// 3-FE panels: 2e4 x 4e3 x 1e3 levels at p = 15, 1e4 x 2e3 x 500 at p = 21), by column groups:
+// Group sums of FEs whose primary slice and other tables do not fit LDS whole (the reference's 3-FE
+// panels: 2e4 x 4e3 x 1e3 levels at p = 15, 1e4 x 2e3 x 500 at p = 21; two FEs at p > 15), by
+// column groups:
 // workgroup (column group cg of nc columns, row part) keeps the primary slice [B][nc] and every other
 // FE's table [G_f][nc] in LDS (nc from the LDS budget), reads its nc columns and the codes of its
 // rows once, and adds the fine limbs there; the slice goes to S_P at each bucket change, the tables
@@ -780,7 +781,7 @@ __global__ __launch_bounds__(kCgThreads) void k_sums_cg(SumsCgArgs a) {
 // column groups for k_sums_cg: columns per group from the LDS budget (0: the tables do not fit)
 static int sums_cg_nc(const lfe_ctx* c) {
   const int P = c->L.P;
-  if (c->F < 3 || c->F > kCgMaxF || P < 0) return 0;
+  if (c->F < 2 || c->F > kCgMaxF || P < 0) return 0;
   const char* e = getenv("LFE_SUMS_CG");  // "0": off (A/B)
   if (e && e[0] == '0') return 0;
   int64_t per_col = (int64_t)1 << c->L.s;

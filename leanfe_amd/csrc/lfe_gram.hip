@@ -1337,6 +1337,7 @@ struct Tab3Args {
   const int32_t* cnt[kMaxFE];
   int64_t gstart[kMaxFE + 1];  // FE f's groups are [gstart[f], gstart[f + 1]) of the concatenation
   int F, p, sfe;               // sfe: the FE whose effects absorb the shift
+  double tw[kMaxFE];           // share of its cross term each FE carries (1/2 each; two FEs: 0 and 1)
   const double* X;             // the shift c_d = X[d][0] (the raw pass's)
   int64_t ld;
 };
@@ -1381,8 +1382,9 @@ __global__ __launch_bounds__(256) void k_tab3_gram(Tab3Args t, double* __restric
         if (n > 0.0) {
           const double c = t.X[(int64_t)d * t.ld];
           a = f == t.sfe ? t.alpha[f][e] - c : t.alpha[f][e];
-          const double Tp = f == t.sfe ? t.T[f][e] : t.T[f][e] - n * c;
-          v = t.S[f][e] - n * c - 0.5 * Tp;
+          const double w = t.tw[f];
+          const double Tp = w == 0.0 ? 0.0 : (f == t.sfe ? t.T[f][e] : t.T[f][e] - n * c);
+          v = t.S[f][e] - n * c - w * Tp;
         }
       }
       av[gl][d] = a;
@@ -1444,8 +1446,11 @@ __global__ __launch_bounds__(256) void k_tab3_assemble(const double* __restrict_
 static bool tables3_ok(const lfe_ctx* c) {
   const char* e = getenv("LFE_TAB3");  // "0": the design pass (A/B)
   if (e && e[0] == '0') return false;
-  return c->d3.on && c->world == 1 && !c->L.w && !c->records && !c->sw.on && c->p <= kT3MaxP && c->L.P >= 0 &&
-         c->L.n_items > 0;
+  if (!(c->world == 1 && !c->L.w && !c->records && !c->sw.on && c->p <= kT3MaxP && c->L.P >= 0 && c->L.n_items > 0))
+    return false;
+  // three or more FEs after the pair-table sweeps, or two FEs too wide for the raw Gram of the
+  // group-sum pass (p > 12) whose sweeps left T_Q from the final alpha_P
+  return c->d3.on || (c->F == 2 && c->tq_final && c->p > 12);
 }
 
 // the design Gram of [1, y~, x~] from the raw pass and the group tables into host_out (dense D x D);
@@ -1454,7 +1459,7 @@ template <int NT>
 static int tables3_gram(lfe_ctx* c, double* host_out) {
   using Sh = GramShape<NT>;
   const int p = c->p, D = p + 1, NG = p * (p + 1) / 2;
-  LFE_TRY(dense3_final_T(c));
+  if (c->d3.on) LFE_TRY(dense3_final_T(c));
   GramArgs a = base_args(c);
   const void* fn = reinterpret_cast<const void*>(&k_raw_gram<NT>);
   const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kGramThreads, 0)));
@@ -1472,7 +1477,15 @@ static int tables3_gram(lfe_ctx* c, double* host_out) {
   t.gstart[c->F] = total;
   t.F = c->F;
   t.p = p;
-  t.sfe = c->L.P;
+  if (c->d3.on) {  // every FE carries half of its cross term (all final)
+    t.sfe = c->L.P;
+    for (int f = 0; f < c->F; ++f) t.tw[f] = 0.5;
+  } else {  // two FEs: the whole cross term on Q's side (T_Q final), the shift on Q's effects
+    const int Q = 1 - c->L.P;
+    t.sfe = Q;
+    t.tw[c->L.P] = 0.0;
+    t.tw[Q] = 1.0;
+  }
   t.X = c->L.X;
   t.ld = c->ld;
   const int nblk3 = (int)std::max<int64_t>(1, std::min<int64_t>(256, (total + kT3Chunk - 1) / kT3Chunk));

@@ -1142,8 +1142,15 @@ static int fin_check(lfe_ctx* c, int f, const double* T, const double* cur, doub
   return LFE_OK;
 }
 
+// two FEs whose row layouts do not fit LDS (wide fits: alpha_Q or the primary slice too large)
+// but whose dense count tables serve both cross terms (lfe_dense.hip, 16-column groups)
+static bool fast_dense_only_ok(const lfe_ctx* c) {
+  if (c->F != 2 || c->L.w || c->L.P < 0 || !c->L.permuted || (1ll << c->L.s) > 65536) return false;
+  return dense_ok(c);
+}
+
 bool fast_path_ok(const lfe_ctx* c, const std::vector<int>& order) {
-  return order.back() == c->L.P && fast_layout_ok(c);
+  return order.back() == c->L.P && (fast_layout_ok(c) || fast_dense_only_ok(c));
 }
 
 bool fast_layout_ok(const lfe_ctx* c) {
@@ -1195,8 +1202,10 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
                     : NT == 2 ? reinterpret_cast<const void*>(&k_tq<2>)
                     : NT == 3 ? reinterpret_cast<const void*>(&k_tq<3>)
                               : reinterpret_cast<const void*>(&k_tq<4>);
-  LFE_HIP(hipFuncSetAttribute(ftp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds_tp, 1)));
-  LFE_HIP(hipFuncSetAttribute(ftq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds_tq, 1)));
+  if (!dense) {  // the row passes' LDS tables (a wide fit runs the dense passes only)
+    LFE_HIP(hipFuncSetAttribute(ftp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds_tp, 1)));
+    LFE_HIP(hipFuncSetAttribute(ftq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds_tq, 1)));
+  }
   TpArgs tp{};
   tp.seg_off = c->seg_off;
   tp.seg_q = c->seg_q;

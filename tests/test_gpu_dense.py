@@ -228,3 +228,25 @@ def test_dense_four_bit_counters(monkeypatch):
     heavy_data = {"y": y, "fe1": fe1, "fe2": fe2, **{f"x{j + 1}": x[:, j].copy() for j in range(3)}}
     monkeypatch.setenv("LFE_DN_C4", "1")
     _check(_fit(heavy_data, xs), _oracle(heavy_data, xs))
+
+
+@pytest.mark.parametrize("vcov,p_k", [("HC1", 14), ("iid", 20), ("HC1", 20)])
+def test_dense_wide_fits(vcov, p_k, monkeypatch):
+    """Two FEs at p = 15 and 21: the dense passes in 16-column groups (the row layouts' LDS tables
+    do not fit), the column-group group sums and the Gram from the group tables (raw MFMA pass +
+    table terms) against the oracle and the general sweeps (LFE_DENSE=0), bit-identical repeats."""
+    from leanfe_amd import synth
+
+    xs = [f"x{j + 1}" for j in range(p_k)]
+    data = synth.panel(900_000, p_k, [3_000, 600], seed=91)
+    o = _oracle(data, xs, vcov)
+    dense = _fit(data, xs, vcov)
+    _check(dense, o)
+    again = _fit(data, xs, vcov)
+    np.testing.assert_array_equal(dense[0], again[0])
+    np.testing.assert_array_equal(dense[1], again[1])
+    monkeypatch.setenv("LFE_DENSE", "0")
+    rows = _fit(data, xs, vcov)
+    _check(rows, o)
+    np.testing.assert_allclose(dense[0], rows[0], rtol=1e-11, atol=0)
+    np.testing.assert_allclose(dense[1], rows[1], rtol=1e-11, atol=0)
