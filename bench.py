@@ -263,11 +263,21 @@ def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cel
     rows they gather come from L2 / MALL-resident tables and are not HBM bytes.  With the dense
     two-FE cross terms (``dense_cells`` > 0, lfe_dense.hip) the table build reads both codes and
     writes two count tables of ``cell_bytes`` per cell (1: the exact i8 form, 2: u16), and each
-    cross-term pass reads one of them."""
+    cross-term pass reads one of them; with three or more FEs on pair tables (lfe_dense3.hip) the
+    projections read the tables instead of gathering rows."""
     k = p - 1
     cb = cell_bytes
     dense = {"layout_scatter": 8 * n + 2 * cb * dense_cells, "tp": cb * dense_cells, "tq": cb * dense_cells,
              "layout_base": 0} if dense_cells else {}
+    if dense_cells and F >= 3:
+        # pair-table sweeps (lfe_dense3.hip; dense_cells = i8 bytes of every ordered pair's table):
+        # a projection reads its FE's tables once per 16-column group, a y-only check pass once; the
+        # build partitions the kept rows' codes (P, a, partners: <= 20 B read, 8 B written per row)
+        # per partition FE and counts each pair from it (8 B per row read, both tables written)
+        npairs = F * (F - 1) // 2
+        ncg = (p + 15) // 16
+        dense = {"cross": dense_cells * ncg / F, "check": dense_cells / F, "layout_hist": 8 * n,
+                 "layout_scatter": 28 * n, "seg_build": 8 * n + dense_cells / npairs}
     return {
         "part_hist": 4 * n,                          # primary codes
         "part_scatter": n * (2 * 8 * p + 2 * 4 * F),  # read + write X and codes
