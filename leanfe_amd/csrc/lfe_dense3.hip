@@ -43,15 +43,27 @@ static int tiles_of(int32_t G) { return (int)(((int64_t)G + kD3Tile - 1) / kD3Ti
 // build
 // ---------------------------------------------------------------------------
 
-// kept rows (code_P >= 0) of workgroup w's row range, counted per bin a >> 6 -> cnt[bin][w]
+// kept rows (code_P >= 0) of workgroup w's row range, counted per bin a >> 6 -> cnt[bin][w]; every
+// thread keeps kD3U rows' loads in flight (one load per wave at a time left the pass latency-bound)
+constexpr int kD3U = 8;
 __global__ __launch_bounds__(256) void k_d3_hist(const int32_t* __restrict__ codeP, const int32_t* __restrict__ codeA,
                                                  int64_t n, int nbin, int32_t* __restrict__ cnt) {
   extern __shared__ int32_t h[];
   for (int j = threadIdx.x; j < nbin; j += blockDim.x) h[j] = 0;
   __syncthreads();
   const int64_t r0 = n * blockIdx.x / gridDim.x, r1 = n * (blockIdx.x + 1) / gridDim.x;
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x)
-    if (codeP[i] >= 0) atomicAdd(&h[codeA[i] >> 6], 1);
+  for (int64_t i0 = r0 + threadIdx.x; i0 < r1; i0 += kD3U * (int64_t)blockDim.x) {
+    int32_t hp[kD3U], ha[kD3U];
+#pragma unroll
+    for (int u = 0; u < kD3U; ++u) {
+      const int64_t i = i0 + u * (int64_t)blockDim.x;
+      hp[u] = i < r1 ? codeP[i] : -1;
+      ha[u] = i < r1 ? codeA[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kD3U; ++u)
+      if (hp[u] >= 0) atomicAdd(&h[ha[u] >> 6], 1);
+  }
   __syncthreads();
   for (int j = threadIdx.x; j < nbin; j += blockDim.x) cnt[(int64_t)j * gridDim.x + blockIdx.x] = h[j];
 }
@@ -67,6 +79,8 @@ struct D3Codes {
 __global__ __launch_bounds__(256) void k_d3_scatter(const int32_t* __restrict__ codeP, const int32_t* __restrict__ codeA,
                                                     D3Codes cb, int64_t n, int nbin, const int32_t* __restrict__ base,
                                                     uint64_t* __restrict__ out) {
+  // one row per thread and iteration (eight in flight measured slower: the returning LDS cursor adds
+  // of a workgroup's few bins serialize either way, and the stores follow them)
   extern __shared__ int32_t cur[];
   for (int j = threadIdx.x; j < nbin; j += blockDim.x) cur[j] = base[(int64_t)j * gridDim.x + blockIdx.x];
   __syncthreads();
