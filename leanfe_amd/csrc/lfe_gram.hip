@@ -145,8 +145,11 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_table(GramArgs a, double*
 // Every load address is valid for every lane: lanes without a data column read
 // column 0 and rows outside the item get primary code -1, so nothing is
 // predicated and each row's validity is the single test h >= 0.
+// (NT = 2, GU = 1, 256 threads: three workgroups per CU, i.e. three waves per SIMD - the register
+// budget 168 the unweighted residual variant needs four registers of spill-free slack for)
 template <int MODE, int NT, int FQ, int GU, bool WT, bool QL, int TH>
-__global__ __launch_bounds__(TH) void k_gram(GramArgs a, double* __restrict__ partial, int64_t pstride) {
+__global__ __launch_bounds__(TH, (NT == 2 && GU == 1 && TH == 256 && FQ == 1) ? 3 : 1) void k_gram(
+    GramArgs a, double* __restrict__ partial, int64_t pstride) {
   using Sh = GramShape<NT>;
   constexpr int NW = TH / 64;
   __shared__ double red[Sh::LEN];
@@ -752,6 +755,13 @@ static const void* gram_kernel(bool general, bool weighted, bool ql) {
   }
 #define GRAM_FN(GU) (weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, true, false, kGramThreads>) \
                               : reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, false, false, kGramThreads>))
+  // wide fits: one 16-row group per wave iteration (GU 2 holds 232 registers at NT = 2: two waves
+  // per SIMD) unless LFE_GRAM_GU=2 (A/B)
+  static const int gu_wide = [] {
+    const char* e = getenv("LFE_GRAM_GU");
+    return e ? atoi(e) : 1;
+  }();
+  if (NT >= 2 && gu_wide == 1) return GRAM_FN(1);
   return GRAM_FN(kGramGU);
 #undef GRAM_FN
 }
