@@ -367,8 +367,11 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   static_assert(R <= 32768, "stage slots are kept as 16-bit values");
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* stage = smem;                                           // [R] (doubles or two int32 halves)
-  int32_t* cur = reinterpret_cast<int32_t*>(stage + R);           // [waves][nb] cursors
-  int32_t* delta = cur + kWaves * a.nb;                           // [nb]
+  // [waves][nb] 16-bit cursors (< R <= 32768): half the LDS of 32-bit ones, so 16 waves' cursors
+  // fit beside the 128 KB stage up to ~700 buckets (a wide fit's 391)
+  uint16_t* cur = reinterpret_cast<uint16_t*>(stage + R);
+  const int ncur = (kWaves * a.nb + 1) & ~1;
+  int32_t* delta = reinterpret_cast<int32_t*>(cur + ncur);        // [nb]
   int32_t* tot = delta + a.nb;                                    // [nb + 1]
   __shared__ int32_t wsum[16];
   __shared__ double wstat[2][16];
@@ -393,7 +396,10 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
   // per-wave bucket counts (integer adds commute: the counts do not depend on their order)
 #pragma unroll
   for (int k = 0; k < PER; ++k)
-    if (bk[k] >= 0) atomicAdd(&cur[wave * a.nb + bk[k]], 1);
+    if (bk[k] >= 0) {  // 32-bit adds into the cursor pair (a wave counts <= PER * 64 rows: no carry)
+      const int idx = wave * a.nb + bk[k];
+      atomicAdd(reinterpret_cast<uint32_t*>(cur) + (idx >> 1), 1u << (16 * (idx & 1)));
+    }
   __syncthreads();
   // per bucket: exclusive scan over waves, total
   for (int b = tid; b < a.nb; b += NTH) {
@@ -456,10 +462,10 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
       same &= one ? m : ~m;
     }
     if (act) {
-      int32_t* cw = &cur[wave * a.nb + b];
+      uint16_t* cw = &cur[wave * a.nb + b];
       const int base = *cw;
       const int rank = __popcll(same & lanes_below);
-      if (rank == 0) *cw = base + __popcll(same);
+      if (rank == 0) *cw = (uint16_t)(base + __popcll(same));
       slot = (uint32_t)(base + rank);
       sb[slot] = b;
     }
@@ -1009,8 +1015,9 @@ int prepare_layout(lfe_ctx* c) {
         if (fill(w) > fill(cw) + 0.1) cw = w;
     }
     if (const char* e = getenv("LFE_PART_CW")) cw = atoll(e);  // A/B only
-    auto part_lds = [&](int nth) {
-      return sizeof(double) * cw + sizeof(int32_t) * ((size_t)(nth / 64) * nb + 2 * (size_t)nb + 1);
+    auto part_lds = [&](int nth) {  // stage, 16-bit per-wave cursors, deltas and totals
+      return sizeof(double) * cw + sizeof(uint16_t) * (((size_t)(nth / 64) * nb + 1) & ~(size_t)1) +
+             sizeof(int32_t) * (2 * (size_t)nb + 1);
     };
     // 16 waves per chunk when their per-wave bucket cursors fit (nb <= ~1500)
     const int nth = part_lds(1024) <= 150 * 1024 ? 1024 : 512;
