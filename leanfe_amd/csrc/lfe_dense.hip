@@ -1025,13 +1025,13 @@ __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
 
 // K2: workgroup (bucket bi, part j of np): the bucket's alpha_P rows digitized in LDS, then output
 // blocks [j nrb / np, (j + 1) nrb / np) of the bucket's secondary blocks, wave w every 8th
-__global__ __launch_bounds__(512, 4) void k_dn8_k2s(Dn8Args a, int np) {
+__device__ __forceinline__ void dn8_k2s_body(const Dn8Args& a, int np, int blk) {
   extern __shared__ __attribute__((aligned(16))) int8_t fr[];  // [8 kb][8 d][1 KB]
   __shared__ double red[512 + 16];
   __shared__ double sc[16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), W = blockDim.x >> 6;
-  const int bi = blockIdx.x / np, part = blockIdx.x - bi * np;
+  const int bi = blk / np, part = blk - bi * np;
   const int i0 = a.nrb * part / np, i1 = a.nrb * (part + 1) / np;
   if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3] = wall_clock64();
   Dn8Ring R;
@@ -1045,6 +1045,24 @@ __global__ __launch_bounds__(512, 4) void k_dn8_k2s(Dn8Args a, int np) {
     __syncthreads();
     if (tid == 0) a.dbg[blockIdx.x * 3 + 2] = wall_clock64();
   }
+}
+
+__global__ __launch_bounds__(512, 4) void k_dn8_k2s(Dn8Args a, int np) { dn8_k2s_body(a, np, blockIdx.x); }
+
+// several K2-form passes in one launch (the pair-table sweeps: every partner FE and column group of
+// one projection), workgroups [start[j], start[j + 1]) running pass j: one launch's latency and
+// digit prologues in parallel instead of one launch after another
+constexpr int kDn8Batch = 8;
+struct Dn8Batch {
+  Dn8Args a[kDn8Batch];
+  int np[kDn8Batch];
+  int start[kDn8Batch + 1];
+  int n;
+};
+__global__ __launch_bounds__(512, 4) void k_dn8_k2s_batch(Dn8Batch b) {
+  int j = 0;
+  while (j + 1 < b.n && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  dn8_k2s_body(b.a[j], b.np[j], (int)blockIdx.x - b.start[j]);
 }
 
 // LFE_DN8_TIMING=1 (diagnostic): per-workgroup phase times of the last K1 / K2 launch to stderr
@@ -1409,8 +1427,7 @@ int dense_tq(lfe_ctx* c, double* runs) {
 
 // one pair-table pass of the general dense sweeps (lfe_dense3.hip): the K2 streaming kernel with
 // "buckets" = the 512-level tiles of the k-side FE and "secondary levels" = the output FE's levels
-int dn8_pair_pass(lfe_ctx* c, const PairPass& pp) {
-  if (pp.ntile_k < 1 || pp.nrb < 1) return LFE_OK;
+static Dn8Args pair_args(const PairPass& pp) {
   Dn8Args a{};
   a.Nm = pp.tab;
   a.flags = pp.flg;
@@ -1429,11 +1446,43 @@ int dn8_pair_pass(lfe_ctx* c, const PairPass& pp) {
   a.nrb = pp.nrb;
   a.alpha = pp.alpha;
   a.runs = pp.runs;
-  LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k2s), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kDn8TileBytes));
-  const int np = k2_parts(c, pp.ntile_k, a.nrb);
-  hipLaunchKernelGGL(k_dn8_k2s, dim3(pp.ntile_k * np), dim3(512), kDn8TileBytes, c->stream, a, np);
-  LFE_HIP(hipGetLastError());
+  return a;
+}
+
+int dn8_pair_pass(lfe_ctx* c, const PairPass& pp) { return dn8_pair_passes(c, &pp, 1); }
+
+int dn8_pair_passes(lfe_ctx* c, const PairPass* pp, int n) {
+  static bool attr = false;
+  if (!attr) {
+    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k2s_batch),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kDn8TileBytes));
+    attr = true;
+  }
+  for (int j0 = 0; j0 < n; j0 += kDn8Batch) {
+    Dn8Batch b{};
+    int grid = 0;
+    for (int j = j0; j < n && b.n < kDn8Batch; ++j) {
+      if (pp[j].ntile_k < 1 || pp[j].nrb < 1) continue;
+      const int q = b.n++;
+      b.a[q] = pair_args(pp[j]);
+      // the batch shares the chip: its passes' workgroups together fill one round of the resident ones
+      b.np[q] = 1;
+      b.start[q] = grid;
+      grid += pp[j].ntile_k;
+    }
+    if (b.n == 0) continue;
+    // parts per tile: as many as keep the whole batch within one round (two per CU), >= 8 blocks each
+    const int per = std::max(1, (int)((2 * (int64_t)c->n_cu) / std::max(grid, 1)));
+    grid = 0;
+    for (int q = 0; q < b.n; ++q) {
+      b.np[q] = std::min(per, std::max(1, b.a[q].nrb / 8));
+      b.start[q] = grid;
+      grid += b.a[q].nbe * b.np[q];
+    }
+    b.start[b.n] = grid;
+    hipLaunchKernelGGL(k_dn8_k2s_batch, dim3(grid), dim3(512), kDn8TileBytes, c->stream, b);
+    LFE_HIP(hipGetLastError());
+  }
   return LFE_OK;
 }
 

@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 namespace lfe {
 
@@ -446,6 +447,7 @@ static int d3_cross(lfe_ctx* c, int f, bool y_only, int* ns_out) {
   LFE_TRY(ensure_dev(d.runs[f], d.runs_cap[f], (size_t)ns * Gf * p));
   ProfScope _ps(c, y_only ? K_CHECK : K_CROSS);
   int slot = 0;
+  std::vector<PairPass> passes;
   for (int b = 0; b < c->F; ++b) {
     if (b == f) continue;
     for (int c0 = 0; c0 < pcols; c0 += 16) {
@@ -463,9 +465,19 @@ static int d3_cross(lfe_ctx* c, int f, bool y_only, int* ns_out) {
       pp.ldo = ldo;
       pp.alpha = c->fe[b].alpha + c0;
       pp.runs = d.runs[f] + (size_t)slot * Gf * ldo + c0;
-      LFE_TRY(dn8_pair_pass(c, pp));
+      passes.push_back(pp);
     }
     slot += tiles_of(c->fe[b].G);
+  }
+  // every partner and column group of the projection in one launch (LFE_D3_BATCH=0: one each, A/B)
+  static const bool batch = [] {
+    const char* e = getenv("LFE_D3_BATCH");
+    return !(e && e[0] == '0');
+  }();
+  if (batch) {
+    LFE_TRY(dn8_pair_passes(c, passes.data(), (int)passes.size()));
+  } else {
+    for (const auto& pp : passes) LFE_TRY(dn8_pair_pass(c, pp));
   }
   *ns_out = ns;
   return LFE_OK;

@@ -458,6 +458,7 @@ struct PairPass {
   double* runs;           // the slots (+ the column offset)
 };
 int dn8_pair_pass(lfe_ctx* c, const PairPass& pp);
+int dn8_pair_passes(lfe_ctx* c, const PairPass* pp, int n);  // up to 8 per launch
 // lfe_dense3.hip: three or more FEs, unweighted - every cross term from the pair tables
 bool dense3_ok(const lfe_ctx* c, const std::vector<int>& order, int check_from);
 int demean_dense3(lfe_ctx* c, const std::vector<int>& order, double tol, int max_iter, int check_from,
