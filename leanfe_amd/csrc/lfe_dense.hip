@@ -590,14 +590,25 @@ __device__ __forceinline__ void dn8_split(double v, double sin, int (&dg)[8]) {
 // fragments fr [8 kb][8 d][1024] and per-column scales sc[16] = 2^(e - 54) (NaN for a column with a
 // non-finite value, so that it propagates), by a block of NT threads.  Thread t holds column t & 15
 // of RPT consecutive rows in registers: one round of loads, no dependent load chain.
-template <int NT>
+// mid() runs right after the tile's loads are issued (the caller's own loads - the streaming
+// passes' A ring - then queue behind them instead of in front: vmcnt retires loads in order)
+struct Dn8NoMid {
+  __device__ void operator()() const {}
+};
+template <int NT, class Mid = Dn8NoMid>
 __device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p, int ld, int8_t* __restrict__ fr,
-                                double* __restrict__ sc, double* __restrict__ red) {
+                                double* __restrict__ sc, double* __restrict__ red, Mid mid = Mid(),
+                                unsigned long long* tdbg = nullptr) {
   constexpr int RPT = kDn8Tile * 16 / NT;  // rows per thread (32 or 16)
   const int tid = threadIdx.x, col = tid & 15, r0 = (tid >> 4) * RPT;
   double v[RPT];
 #pragma unroll
   for (int u = 0; u < RPT; ++u) v[u] = (col < p && r0 + u < rows) ? src[(int64_t)(r0 + u) * ld + col] : 0.0;
+  mid();
+  if (tdbg && tid == 0) {  // diagnostic phase stamps (LFE_DN8_TIMING): this thread's loads landed
+    __builtin_amdgcn_s_waitcnt(0);
+    tdbg[0] = wall_clock64();
+  }
   double m = 0.0;
   bool bad = false;
 #pragma unroll
@@ -616,6 +627,7 @@ __device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p,
   constexpr int NW = NT / 64;
   if ((tid & 63) < 16) red[(tid >> 6) * 16 + col] = mv;
   __syncthreads();
+  if (tdbg && tid == 0) tdbg[1] = wall_clock64();
   if (tid < 16) {
     double mm = 0.0;
     bool nb = false;
@@ -630,6 +642,7 @@ __device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p,
     red[NT + tid] = ldexp(1.0, 54 - e);
   }
   __syncthreads();
+  if (tdbg && tid == 0) tdbg[2] = wall_clock64();
   const double sin = red[NT + col];
   // rows 4 q .. 4 q + 3 of the thread's -> one 32-bit word per digit at lane (16 g + col), bytes 4 jq
 #pragma unroll
@@ -1007,13 +1020,16 @@ __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
   const int i0 = (int)(total * blockIdx.x / gridDim.x), i1 = (int)(total * (blockIdx.x + 1) / gridDim.x);
   if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3] = wall_clock64();
   Dn8Ring R;
-  dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
   const int ntile = (a.nkb + 7) / 8;
   for (int t = 0; t < ntile; ++t) {
     if (t) __syncthreads();
+    auto mid = [&]() {
+      if (t == 0) dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
+    };
     dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.lda, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p, a.lda,
-                          fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red);
+                          fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red, mid);
   }
+  if (ntile == 0) dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
   __syncthreads();
   if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3 + 1] = wall_clock64();
   dn8_wave_stream<false>(a, fr, sc, 0, i0 + wave, W, i1, lane, R);
@@ -1035,9 +1051,10 @@ __device__ __forceinline__ void dn8_k2s_body(const Dn8Args& a, int np, int blk) 
   const int i0 = a.nrb * part / np, i1 = a.nrb * (part + 1) / np;
   if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3] = wall_clock64();
   Dn8Ring R;
-  dn8_ring_fill(a, R, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane);
   const int lo = a.blist[bi] << a.s;
-  dn8_tile_digits<512>(a.alpha + (int64_t)lo * a.lda, max(0, min(a.B, a.G_P - lo)), a.p, a.lda, fr, sc, red);
+  dn8_tile_digits<512>(a.alpha + (int64_t)lo * a.lda, max(0, min(a.B, a.G_P - lo)), a.p, a.lda, fr, sc, red,
+                       [&]() { dn8_ring_fill(a, R, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane); },
+                       a.dbg ? a.dbg + 3 * 65536 + (size_t)blockIdx.x * 4 : nullptr);
   __syncthreads();
   if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3 + 1] = wall_clock64();
   dn8_wave_stream<true>(a, fr, sc, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane, R);
@@ -1091,6 +1108,22 @@ static int dn8_timing_report(lfe_ctx* c, const char* name, int grid) {
   }
   fprintf(stderr, "[dn8 %s] grid %d span %.1f us, prologue avg %.1f max %.1f us, stream avg %.1f max %.1f us\n", name,
           grid, (double)(t1 - t0) / 100.0, pro / grid, pro_max, str / grid, str_max);
+  std::vector<unsigned long long> hd((size_t)grid * 4);
+  LFE_HIP(hipMemcpy(hd.data(), g_dn8_dbg + 3 * 65536, sizeof(unsigned long long) * hd.size(), hipMemcpyDeviceToHost));
+  double l = 0, r = 0, q = 0, sp = 0;
+  int cnt = 0;
+  for (int b = 0; b < grid; ++b) {
+    if (hd[4 * b] == 0 || hd[4 * b] < h[3 * b]) continue;
+    l += (double)(hd[4 * b] - h[3 * b]) / 100.0;
+    r += (double)(hd[4 * b + 1] - hd[4 * b]) / 100.0;
+    q += (double)(hd[4 * b + 2] - hd[4 * b + 1]) / 100.0;
+    sp += (double)(h[3 * b + 1] - hd[4 * b + 2]) / 100.0;
+    ++cnt;
+  }
+  if (cnt)
+    fprintf(stderr, "[dn8 %s] first tile: loads %.1f, max + barrier %.1f, scale + barrier %.1f, split + rest %.1f us\n",
+            name, l / cnt, r / cnt, q / cnt, sp / cnt);
+  LFE_HIP(hipMemset(g_dn8_dbg + 3 * 65536, 0, sizeof(unsigned long long) * hd.size()));
   return LFE_OK;
 }
 
@@ -1325,7 +1358,10 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
       const int64_t total = (int64_t)std::max(c->nbe, 1) * a.nrb;
       const int grid = (int)std::min<int64_t>(c->n_cu, (total + 15) / 16);
       if (dn8_timing()) {
-        if (!g_dn8_dbg) LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 3 * 65536));
+        if (!g_dn8_dbg) {
+          LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 7 * 65536));
+          LFE_HIP(hipMemset(g_dn8_dbg, 0, sizeof(unsigned long long) * 7 * 65536));
+        }
         a.dbg = g_dn8_dbg;
       }
       // wide fits: one pass per 16-column group (each projects its own columns of alpha_P)
@@ -1391,7 +1427,10 @@ int dense_tq(lfe_ctx* c, double* runs) {
       const int nbe = std::max(c->nbe, 1);
       const int np = k2_parts(c, nbe, a.nrb);
       if (dn8_timing()) {
-        if (!g_dn8_dbg) LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 3 * 65536));
+        if (!g_dn8_dbg) {
+          LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 7 * 65536));
+          LFE_HIP(hipMemset(g_dn8_dbg, 0, sizeof(unsigned long long) * 7 * 65536));
+        }
         a.dbg = g_dn8_dbg;
       }
       const int p = c->p;
