@@ -876,8 +876,11 @@ static GramArgs base_args(lfe_ctx* c) {
 static bool resid_rows_ok(const lfe_ctx* c, const GramArgs& a) {
   // p <= 12: the meat's upper triangle stays in registers (p = 16 would spill)
   const int PM = c->p <= 4 ? 4 : c->p <= 8 ? 8 : 12;
+  // both alpha tables as dynamic LDS beside the row kernels' static LDS (k_design_rows /
+  // k_resid_rows: at most 960, 2880, 4992 bytes for PM 4, 8, 12) within the CU's 160 KB
+  const size_t stat = PM == 4 ? 1024 : PM == 8 ? 3072 : 5120;
   return c->F == 2 && c->p <= 12 && c->p >= 2 && !a.w && a.la.P >= 0 && c->L.permuted &&
-         ((size_t)a.B + c->fe[1 - a.la.P].G) * PM * 8 <= 150 * 1024;
+         ((size_t)a.B + c->fe[1 - a.la.P].G) * PM * 8 + stat <= 160 * 1024;
 }
 
 // row-per-lane design Gram (k_design_rows): the reduced [16][16] tile (column 0 =
