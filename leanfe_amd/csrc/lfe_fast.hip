@@ -865,7 +865,7 @@ int sums4(lfe_ctx* c) {
   }
 #undef SUMS4_FN
   LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 1)));
-  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, threads, lds)));
+  const int nblocks = row_blocks(c, resident_blocks(c, fn, threads, lds));
   if (raw) {
     LFE_TRY(ensure_f64(c, c->raw_part, c->raw_part_cap, (size_t)nblocks * 256));
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));

@@ -795,7 +795,7 @@ static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
     fn = gram_kernel<MODE, NT>(a.nq > 1, a.w != nullptr, ql);
     if (dyn > 64 * 1024)  // dynamic LDS above 64 KB must be opted in
       LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-    nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, threads, dyn)));
+    nblocks = row_blocks(c, resident_blocks(c, fn, threads, dyn));
   }
   const int64_t pstride = Sh::LEN + 4;
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
@@ -896,7 +896,7 @@ static int design_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
                    : PM == 8 ? reinterpret_cast<const void*>(&k_design_rows<8, 2>)
                              : reinterpret_cast<const void*>(&k_design_rows<11, 1>);
   if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kResThreads, dyn)));
+  const int nblocks = row_blocks(c, resident_blocks(c, fn, kResThreads, dyn));
   const int64_t pstride = 256 + 4;
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
   {
@@ -1475,7 +1475,7 @@ static int tables3_gram(lfe_ctx* c, double* host_out) {
   if (c->d3.on) LFE_TRY(dense3_final_T(c));
   GramArgs a = base_args(c);
   const void* fn = reinterpret_cast<const void*>(&k_raw_gram<NT>);
-  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kGramThreads, 0)));
+  const int nblocks = row_blocks(c, resident_blocks(c, fn, kGramThreads, 0));
   const int64_t pstride = Sh::LEN;
   int64_t total = 0;
   Tab3Args t{};
@@ -1580,7 +1580,7 @@ static int resid_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
                    : PM == 8 ? reinterpret_cast<const void*>(&k_resid_rows<8, 2>)
                              : reinterpret_cast<const void*>(&k_resid_rows<12, 2>);
   if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-  const int nblocks = std::max(1, std::min(c->L.n_items, resident_blocks(c, fn, kResThreads, dyn)));
+  const int nblocks = row_blocks(c, resident_blocks(c, fn, kResThreads, dyn));
   const int64_t pstride = 256 + 4;
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
   {

@@ -268,6 +268,9 @@ struct lfe_ctx {
   size_t run_h_cap = 0;
   int n_units = 0;
   double* alpha_spare = nullptr; // [G_Q * p] double buffer for the secondary alpha
+  double* sweep_ws = nullptr;    // k_sweeps: result[4], barrier words, per-sweep stop tests
+  size_t sweep_ws_cap = 0;
+  uint64_t sweep_tag = 0;
   size_t alpha_spare_cap = 0;
   // clusters (input row order)
   std::vector<int32_t*> cl;
@@ -575,6 +578,16 @@ int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes);
 int ensure_pinned_items(lfe_ctx* c, size_t bytes);
 // blocks of `fn` that fit on the whole device at once (occupancy API x CUs)
 int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds);
+// grid of a row pass over the work items (block_rows splits the rows evenly over the grid):
+// the resident blocks, but no more than one per kRowBlockMin rows or per item, whichever is more
+// (a small fit's few items no longer leave CUs idle: 1M rows = ~160 items for 256 CUs)
+constexpr int64_t kRowBlockMin = 2048;
+inline int row_blocks(const lfe_ctx* c, int resident) {
+  const auto& h = c->L.hitems;
+  const int64_t rows = h.size() >= 4 ? h[h.size() - 2] : 0;
+  const int64_t want = std::max<int64_t>(c->L.n_items, (rows + kRowBlockMin - 1) / kRowBlockMin);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(resident, want));
+}
 int ensure_cluster_ws(lfe_ctx* c, size_t table_elems, size_t flag_elems);
 int allreduce_sum_f64(lfe_ctx* c, double* dev, size_t count);
 int allreduce_sum_f64_many(lfe_ctx* c, const std::vector<std::pair<double*, size_t>>& bufs);
