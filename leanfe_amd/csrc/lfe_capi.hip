@@ -650,7 +650,6 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   dfree(c->run_off);
   dfree(c->run_h);
   dfree(c->alpha_spare);
-  dfree(c->sweep_ws);
   dfree(c->dbeta);
   if (c->hpin) (void)hipHostFree(c->hpin);
   if (c->hpin_items) (void)hipHostFree(c->hpin_items);

@@ -268,9 +268,6 @@ struct lfe_ctx {
   size_t run_h_cap = 0;
   int n_units = 0;
   double* alpha_spare = nullptr; // [G_Q * p] double buffer for the secondary alpha
-  double* sweep_ws = nullptr;    // k_sweeps: result[4], barrier words, per-sweep stop tests
-  size_t sweep_ws_cap = 0;
-  uint64_t sweep_tag = 0;
   size_t alpha_spare_cap = 0;
   // clusters (input row order)
   std::vector<int32_t*> cl;

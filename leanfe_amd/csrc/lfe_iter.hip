@@ -682,7 +682,7 @@ struct TpArgs {
 };
 
 // K1: T_P[h] = sum_{i in h} alpha_Q[q_i]; fused: alpha_P[h] = (S_P[h] - T_P[h]) / n_h
-// (the body of k_tp as workgroup blk of nblk, aq = [G_Q + 1][p] LDS: also one phase of k_sweeps)
+// (the body of k_tp as workgroup blk of nblk, aq = [G_Q + 1][p] LDS)
 template <int NT>
 __device__ __forceinline__ void tp_body(const TpArgs& a, double* __restrict__ aq, int blk, int nblk) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -893,7 +893,7 @@ struct TqArgs {
 // one wave in row order and every slot is written, so T_Q[q] = sum_i runs[i][q] (k_tq_reduce, in
 // bucket order) is bit-reproducible: no cross-workgroup atomics.  Buckets without rows contribute
 // nothing and are not visited.
-// (the body of k_tq as workgroup blk of nblk, sl = [B + 1][p] LDS: also one phase of k_sweeps)
+// (the body of k_tq as workgroup blk of nblk, sl = [B + 1][p] LDS)
 template <int NT>
 __device__ __forceinline__ void tq_body(const TqArgs& a, double* __restrict__ sl, int blk, int nblk) {
   constexpr int kTqThreads = tq_threads<NT>();
@@ -1125,136 +1125,6 @@ __global__ __launch_bounds__(256) void k_tq_reduce_fin(const double* __restrict_
   if (check && threadIdx.x < 64) tq_red_check(mx, threadIdx.x, check);
 }
 
-// ---------------------------------------------------------------------------
-// k_sweeps: the whole sweep loop of one rank in one launch (row layouts, p <= 16).  Every
-// workgroup stays resident (grid <= the occupancy bound) and the three phases of a sweep - K1
-// (alpha_P), K2 (the run sums) and the reduction with the next Q projection and the stop test -
-// are separated by grid barriers; the stop test is read on the device, so no host round trip
-// and no launch sits between sweeps.  Each phase is the separate kernels' own body (same work
-// split per output, same summation order), so the results are bit-identical to them.
-// ---------------------------------------------------------------------------
-struct SweepArgs {
-  TpArgs tp;                 // alphaQ set per sweep
-  TqArgs tq;
-  double* A[2];              // alpha_Q ping-pong: A[0] the input (fq.alpha), A[1] the spare
-  double* T;                 // T_Q
-  const double* S;           // S_Q
-  const int32_t* cnt;        // n_Q
-  int64_t m;                 // G_Q * p
-  int nb, p;                 // run slots (buckets), columns
-  int max_iter, check_from;
-  double tol;
-  unsigned long long* chk;   // [max_iter + 1] the stop test's max of each sweep (zeroed here)
-  unsigned* bar;             // [2] barrier arrivals, generation (arrivals 0 between launches)
-  double* result;            // [0] sweeps run, [1] the last stop test (-1: none), [2] tag: done, [3] tag: a barrier timed out
-  double tag;                // this launch's tag (the host's launch count)
-  unsigned long long* dbg;   // LFE_SWEEP_TIMING: [block][64] wall-clock stamps (arrive, leave per barrier)
-};
-
-constexpr long long kBarSpins = 1ll << 24;  // ~1 s of s_sleep: a barrier that never opens fails the launch
-
-// grid barrier (self-resetting: the last arrival clears the count and opens the next generation).
-// One agent-scope release fence before arriving and one acquire fence after the wait publish every
-// workgroup's writes to every XCD; the count and the generation are relaxed atomics (the wait
-// polls with plain device-coherent loads: an acquire per poll would invalidate the caches each
-// time).  Returns false in every workgroup whose wait timed out (the caller leaves the kernel;
-// the host falls back).
-__device__ __forceinline__ bool grid_sync(unsigned* bar, int* fail) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const unsigned g = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned arrived = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == gridDim.x - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the cleared count before the new generation
-      __hip_atomic_store(bar + 1, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      long long spins = 0;
-      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > kBarSpins) {
-          *fail = 1;
-          break;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-  return *fail == 0;
-}
-
-template <int NT>
-__global__ __launch_bounds__(1024) void k_sweeps(SweepArgs s) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];  // max of K1's and K2's tables
-  __shared__ double part[4][kTqRedS][kTqRedE];
-  __shared__ int fail;
-  const int tid = threadIdx.x;
-  if (tid == 0) fail = 0;
-  int nst = 0;  // LFE_SWEEP_TIMING stamps
-  auto stamp = [&]() {
-    if (s.dbg && tid == 0 && nst < 64) s.dbg[blockIdx.x * 64 + nst] = wall_clock64();
-    ++nst;
-  };
-  stamp();
-  for (int j = blockIdx.x * 1024 + tid; j <= s.max_iter; j += gridDim.x * 1024) s.chk[j] = 0ull;
-  if (!grid_sync(s.bar, &fail)) {
-    if (tid == 0) s.result[3] = s.tag;
-    return;
-  }
-  // the reduction: four 256-thread slices per workgroup, each k_tq_reduce_fin's block vb
-  const int sub = tid >> 8, t = tid & 255, ei = t % kTqRedE, sl = t / kTqRedE;
-  const int64_t nvb = (s.m + kTqRedE - 1) / kTqRedE;
-  const int64_t rounds = (nvb + 4ll * gridDim.x - 1) / (4ll * gridDim.x);
-  double last = -1.0;
-  for (int it = 1;; ++it) {
-    const double* cur = s.A[(it - 1) & 1];
-    double* nxt = s.A[it & 1];
-    TpArgs tp = s.tp;
-    tp.alphaQ = cur;
-    stamp();
-    tp_body<NT>(tp, lds, blockIdx.x, gridDim.x);
-    stamp();
-    if (!grid_sync(s.bar, &fail)) break;
-    stamp();
-    tq_body<NT>(s.tq, lds, blockIdx.x, gridDim.x);
-    stamp();
-    if (!grid_sync(s.bar, &fail)) break;
-    stamp();
-    const bool check = it >= s.check_from;
-    for (int64_t r = 0; r < rounds; ++r) {
-      const int64_t e = ((r * gridDim.x + blockIdx.x) * 4 + sub) * kTqRedE + ei;
-      const double v = tq_red_slice(s.tq.runs, s.nb, s.m, e, sl);
-      __syncthreads();  // the previous round's totals are read
-      part[sub][sl][ei] = v;
-      __syncthreads();
-      double mx = 0.0;
-      if (sl == 0 && e < s.m) mx = tq_red_fin(tq_red_total(part[sub], ei), e, s.T, s.S, s.cnt, s.p, cur, nxt, check);
-      if (check && t < 64) tq_red_check(mx, t, s.chk + it);
-    }
-    stamp();
-    if (!grid_sync(s.bar, &fail)) break;
-    bool stop = it >= s.max_iter;
-    if (check) {
-      last = __longlong_as_double(
-          (long long)__hip_atomic_load(s.chk + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (last < s.tol) stop = true;  // NaN never converges
-    }
-    if (stop) {  // the sweep's input alpha_Q is the result: into A[0] if it is in the spare
-      if ((it - 1) & 1)
-        for (int64_t j = (int64_t)blockIdx.x * 1024 + tid; j < s.m; j += (int64_t)gridDim.x * 1024) s.A[0][j] = s.A[1][j];
-      if (blockIdx.x == 0 && tid == 0) {
-        s.result[0] = it;
-        s.result[1] = last;
-        s.result[2] = s.tag;
-      }
-      return;
-    }
-  }
-  if (tid == 0) s.result[3] = s.tag;
-}
-
 // alpha_new = (S - T) / cnt; check = max_g |alpha_new[g][0] - alpha_cur[g][0]| over groups present
 // (= |mean_g(y~)| after the sweep); NaN propagates (a NaN panel never converges).
 __global__ void k_fin_check(const double* __restrict__ S, const double* __restrict__ T,
@@ -1318,95 +1188,6 @@ static void launch_tp(lfe_ctx* c, const TpArgs& a, size_t lds) {
 template <int NT>
 static void launch_tq(lfe_ctx* c, const TqArgs& a, size_t lds) {
   hipLaunchKernelGGL(k_tq<NT>, dim3(std::max(a.nbe, 1) * a.split), dim3(tq_threads<NT>()), lds, c->stream, a);
-}
-
-// the sweep loop as one k_sweeps launch (one rank, row layouts, p <= 16): returns LFE_OK with the
-// sweeps run and the last stop test, or 1 when it cannot run or a barrier timed out (the caller
-// then runs the separate kernels from the first sweep)
-static int sweeps_persist(lfe_ctx* c, const TpArgs& tp, const TqArgs& tq, size_t lds_tp, size_t lds_tq, double tol,
-                          int max_iter, int check_from, int* it_out, double* last_out) {
-  const char* pe = getenv("LFE_PERSIST");  // opt-in while the barrier cost is measured ("1": on)
-  if (!pe || pe[0] != '1') return 1;
-  auto& fq = c->fe[1 - c->L.P];
-  const size_t need = 8 + (size_t)max_iter + 1;
-  if (c->sweep_ws_cap < need) {  // fresh: the barrier words start at 0
-    LFE_TRY(ensure_f64(c, c->sweep_ws, c->sweep_ws_cap, need));
-    LFE_HIP(hipMemsetAsync(c->sweep_ws, 0, sizeof(double) * c->sweep_ws_cap, c->stream));
-  }
-  const void* fn = reinterpret_cast<const void*>(&k_sweeps<1>);
-  const size_t lds = std::max<size_t>({lds_tp, lds_tq, 1});
-  LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  // every workgroup must be resident at once (the barriers wait for all of them)
-  const int grid = std::min(resident_blocks(c, fn, 1024, lds), 2 * c->n_cu);
-  if (grid < c->n_cu) return 1;
-  SweepArgs s{};
-  s.tp = tp;
-  s.tp.zeroT = nullptr;
-  s.tp.zero_n = 0;
-  s.tp.zero_check = nullptr;
-  s.tq = tq;
-  s.A[0] = fq.alpha;
-  s.A[1] = c->alpha_spare;
-  s.T = fq.T;
-  s.S = fq.S;
-  s.cnt = fq.cnt;
-  s.m = (int64_t)fq.G * c->p;
-  s.nb = c->nbe;
-  s.p = c->p;
-  s.max_iter = max_iter;
-  s.check_from = check_from;
-  s.tol = tol;
-  s.result = c->sweep_ws;
-  s.bar = reinterpret_cast<unsigned*>(c->sweep_ws + 4);
-  s.chk = reinterpret_cast<unsigned long long*>(c->sweep_ws + 8);
-  s.tag = (double)++c->sweep_tag;
-  const bool timing = getenv("LFE_SWEEP_TIMING") != nullptr;  // diagnostic: per-phase wall clock to stderr
-  std::vector<unsigned long long> hdbg;
-  if (timing) {
-    hdbg.assign((size_t)grid * 64, 0ull);
-    LFE_HIP(hipMalloc(&s.dbg, sizeof(unsigned long long) * hdbg.size()));
-    LFE_HIP(hipMemsetAsync(s.dbg, 0, sizeof(unsigned long long) * hdbg.size(), c->stream));
-  }
-  {
-    ProfScope _ps(c, K_TQ);
-    hipLaunchKernelGGL(k_sweeps<1>, dim3(grid), dim3(1024), lds, c->stream, s);
-  }
-  LFE_HIP(hipGetLastError());
-  // the Gram of the tables queued behind the sweeps (as the last check of the loop below does)
-  int spec = 0;
-  c->tq_final = true;
-  LFE_TRY(gram_spec_enqueue(c, &spec));
-  c->tq_final = false;
-  LFE_TRY(d2h_async(c, c->sweep_ws, 4 * sizeof(double)));
-  double r[4];
-  LFE_TRY(d2h_wait(c, r, sizeof(r)));
-  if (r[2] != s.tag || r[3] == s.tag) {  // a barrier timed out: reset it, run the separate kernels
-    LFE_HIP(hipMemsetAsync(s.bar, 0, 2 * sizeof(unsigned), c->stream));
-    return 1;
-  }
-  *it_out = (int)r[0];
-  *last_out = r[1];
-  c->gram_spec = spec != 0 && r[1] >= 0.0 && r[1] < tol;
-  if (timing) {  // stamps per block: start, then per sweep K1 in / out, K2 in / out, reduction in / out
-    LFE_HIP(hipMemcpy(hdbg.data(), s.dbg, sizeof(unsigned long long) * hdbg.size(), hipMemcpyDeviceToHost));
-    (void)hipFree(s.dbg);
-    unsigned long long t0 = ~0ull;
-    for (int b = 0; b < grid; ++b) t0 = std::min(t0, hdbg[(size_t)b * 64]);
-    const int nst = 1 + 6 * *it_out;
-    fprintf(stderr, "k_sweeps timing (us from the first start, min / max over %d blocks):", grid);
-    for (int k = 0; k < nst && k < 64; ++k) {
-      unsigned long long lo = ~0ull, hi = 0;
-      for (int b = 0; b < grid; ++b) {
-        const unsigned long long v = hdbg[(size_t)b * 64 + k];
-        if (!v) continue;
-        lo = std::min(lo, v);
-        hi = std::max(hi, v);
-      }
-      fprintf(stderr, " %s%.2f/%.2f", k % 6 == 1 ? "| " : "", (lo - t0) / 100.0, (hi - t0) / 100.0);
-    }
-    fprintf(stderr, "\n");
-  }
-  return LFE_OK;
 }
 
 int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* iterations_out, double* last_out) {
@@ -1489,17 +1270,6 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   LFE_TRY(fin_check(c, Q, nullptr, nullptr, fq.alpha, false));
   int iterations = 0;
   double last = -1.0;
-  if (!dense && c->world == 1 && NT == 1) {  // one rank: the whole loop in one launch
-    const int rc = sweeps_persist(c, tp, tq, lds_tp, lds_tq, tol, max_iter, check_from, &iterations, &last);
-    if (rc == LFE_OK) {
-      *iterations_out = iterations;
-      *last_out = last;
-      c->tq_final = true;
-      return LFE_OK;
-    }
-    if (rc != 1) return rc;
-    LFE_TRY(fin_check(c, Q, nullptr, nullptr, fq.alpha, false));  // from the first sweep again
-  }
   for (int it = 1; it <= max_iter; ++it) {
     tp.alphaQ = fq.alpha;
     tp.zeroT = nullptr;  // K2 writes every run slot; k_tq_reduce writes T_Q

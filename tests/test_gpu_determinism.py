@@ -73,47 +73,6 @@ def test_sweep_work_units_do_not_change_bits(units, monkeypatch):
     _same(ref, other)
 
 
-@pytest.mark.parametrize("n,L,k,vcov", [(1_000_000, [20_000, 500], 3, "iid"), (2_000_000, [100_000, 1_000], 6, "hc1"),
-                                        (300_001, [5_000, 1_000], 12, "cluster")])
-def test_single_launch_sweeps_match_separate_kernels(n, L, k, vcov, monkeypatch):
-    """One rank with row layouts runs the whole sweep loop as one k_sweeps launch (lfe_iter.hip:
-    grid barriers between K1, K2 and the reduction, the stop test read on the device); every
-    phase is the separate kernels' body, so beta, SE, RSS and `iterations` are bit-identical to
-    the launch-per-phase loop (LFE_PERSIST=0), and so are the demeaned tables after a sweep cap
-    (max_iter reached before the stop test passes)."""
-    from leanfe_amd import synth
-    from leanfe_amd._lib import Engine
-
-    with Engine(0) as eng:
-        eng.synth_load(n, k, L, synth.betas(k), seed=4242)
-        if vcov == "cluster":
-            _, codes = eng.copy_inputs()
-            eng.load_clusters([np.ascontiguousarray(codes[0])], [L[0]])
-        monkeypatch.setenv("LFE_PERSIST", "1")
-        one = bench_solve(eng, vcov)
-        monkeypatch.setenv("LFE_PERSIST", "0")
-        sep = bench_solve(eng, vcov)
-        _same(one, sep)
-        # capped sweeps: the same state after max_iter sweeps either way (the Gram of the tables)
-        for cap, cf in ((2, 3), (4, 1), (1, 0)):
-            monkeypatch.setenv("LFE_PERSIST", "0")
-            eng.drop_singletons()
-            it0, last0 = eng.demean([1, 0], 1e-30, cap, check_from=cf)
-            g0 = eng.gram()
-            monkeypatch.setenv("LFE_PERSIST", "1")
-            eng.drop_singletons()
-            it1, last1 = eng.demean([1, 0], 1e-30, cap, check_from=cf)
-            g1 = eng.gram()
-            assert (it0, last0) == (it1, last1) and it1 == cap
-            np.testing.assert_array_equal(g0, g1)
-
-
-def bench_solve(eng, vcov):
-    import bench
-
-    return bench.solve_step(eng, vcov, 1 if vcov == "cluster" else 0)
-
-
 def _fit_pair(data, xs):
     from leanfe_amd import leanfe_hip
     from oracle import altproj

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in ${LIBS}; do
-    LEANFE_HIP_LIB=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu --no-h2d --steps ${STEPS:-10} --warmup 5 ${BENCH_ARGS:-} > gpurun_out/ab.log 2>&1
+    LFE_ALLOW_STALE=1 LEANFE_HIP_LIB=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu --no-h2d --steps ${STEPS:-10} --warmup 5 ${BENCH_ARGS:-} > gpurun_out/ab.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "$lib rc=$rc"; tail -3 gpurun_out/ab.log; exit $rc; }
     python - "$lib" "${KEYS:-}" <<'PY'
 import json, sys
