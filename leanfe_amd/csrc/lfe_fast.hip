@@ -260,17 +260,11 @@ __global__ void k_col_sums_fold(const unsigned long long* __restrict__ part, int
 // byte offsets are one multiply-add per table, every pointer is hoisted out of the loop, and
 // the next group pair's loads are issued before the current pair is consumed.
 // BIG: some column's values may carry a coarse limb (an outlier beyond Qc / 2, or a non-finite
-// value).  Both variants are launched; each returns at once unless the quanta say it is the one
-// (the flags live on the device), so typical data runs the fine-limb-only loop.
+// value).  One launch: the kernel reads the quanta's flags (they live on the device) and runs the
+// matching body, so typical data runs the fine-limb-only loop.
 template <int TH, int NACC, int GU, bool BIG>
-__global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+__device__ __forceinline__ void sums2_raw_body(const Sums4Args& a, double* __restrict__ lds, double* __restrict__ rred) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  {
-    bool any = false;
-    for (int j = 0; j < a.la.p; ++j) any = any || a.fixq[FQ_BIG * kFqCols + j] != 0.0;
-    if (any != BIG) return;
-  }
   constexpr int nwv = TH / 64, step = nwv * GU;
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.la.p, P = a.la.P, Q = a.qf[0], s = a.la.s;
@@ -404,7 +398,6 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
     double* dst = a.qpart + (int64_t)blockIdx.x * m;
     for (int j = tid; j < m; j += TH) dst[j] = lds[qoff + j];
   }
-  __shared__ double rred[256];
   for (int wv = 0; wv < nwv; ++wv) {
     __syncthreads();
     if (wave == wv)
@@ -419,6 +412,16 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   }
   __syncthreads();
   for (int e = tid; e < 256; e += TH) a.raw_part[(int64_t)blockIdx.x * 256 + e] = rred[e];
+}
+
+template <int TH, int NACC, int GU>
+__global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ double rred[256];
+  bool any = false;
+  for (int j = 0; j < a.la.p; ++j) any = any || a.fixq[FQ_BIG * kFqCols + j] != 0.0;
+  if (any) sums2_raw_body<TH, NACC, GU, true>(a, lds, rred);
+  else sums2_raw_body<TH, NACC, GU, false>(a, lds, rred);
 }
 
 // ---------------------------------------------------------------------------
@@ -851,7 +854,7 @@ int sums4(lfe_ctx* c) {
     // measured the same)
     threads = 1024;
     two = raw && a.slice && a.tab_off[a.qf[0]] >= 0;
-    fn = two   ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1, false>)
+    fn = two   ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1>)
          : raw ? reinterpret_cast<const void*>(&k_sums4<1, 2, 1, 1024, true>)
                : SUMS4_FN(1, 2, 1, 1024);
   } else if (a.nq <= 1) {
@@ -954,11 +957,6 @@ int sums4(lfe_ctx* c) {
     ProfScope _ps(c, K_GROUP_SUMS);
     void* args[] = {&a};
     LFE_HIP(hipLaunchKernel(fn, dim3(nblocks), dim3(threads), args, lds, c->stream));
-    if (two) {  // the coarse-limb variant (returns at once unless some column needs it)
-      const void* fb = reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1, true>);
-      LFE_HIP(hipFuncSetAttribute(fb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 1)));
-      LFE_HIP(hipLaunchKernel(fb, dim3(nblocks), dim3(threads), args, lds, c->stream));
-    }
   }
   LFE_HIP(hipGetLastError());
   for (int f = 0; f < c->F; ++f) {

@@ -259,7 +259,7 @@ struct lfe_ctx {
   size_t seg_q_cap = 0;
   int32_t* seg_aux = nullptr;    // [n_items * B] per-item counts -> bases
   size_t seg_aux_cap = 0;
-  int32_t* seg_units = nullptr;  // [n_units + 1] first primary group of each work unit
+  int32_t* seg_units = nullptr;  // [n_units] K1 work unit descriptors (int4: first / end segment, first / end row)
   size_t seg_units_cap = 0;
   // run layout (fast path): kept rows of each bucket sorted by the secondary code
   int32_t* run_off = nullptr;    // [nb * G_Q + 1] offsets of the (bucket, q) runs

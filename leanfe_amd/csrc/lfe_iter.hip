@@ -471,30 +471,36 @@ __global__ __launch_bounds__(kLsThreads, 4) void k_ls_scatter2(Ls2Args a) {
 }
 
 // first segment (primary group) of each work unit of ~U kept rows
+// first segment of work unit k (H past the last unit): the first h with seg_off[h] >= k U, then
+// the first segment from there on that holds rows, so no unit starts with a run of empty segments
+// (an owner shard's buckets hold every other rank's levels too)
+__device__ __forceinline__ int unit_first(const int32_t* __restrict__ seg_off, int32_t H, int64_t U, int k,
+                                          int n_units) {
+  if (k >= n_units) return H;
+  const int64_t target = (int64_t)k * U;
+  int lo = 0, hi = H;  // first h with seg_off[h] >= target
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (seg_off[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  const int32_t t = lo < H ? seg_off[lo] : 0;
+  hi = H;
+  while (lo < hi) {  // first h with seg_off[h + 1] > t
+    const int mid = (lo + hi) >> 1;
+    if (seg_off[mid + 1] <= t) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// K1's unit descriptors {first segment h, end segment h1, first row seg_off[h], end row
+// seg_off[h1]}: one 16-byte load starts a unit (no dependent segment-offset loads)
 __global__ void k_unit_bounds(const int32_t* __restrict__ seg_off, int32_t H, int64_t U, int n_units,
-                              int32_t* __restrict__ units) {
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k <= n_units; k += gridDim.x * blockDim.x) {
-    if (k == n_units) {
-      units[k] = H;
-      continue;
-    }
-    const int64_t target = (int64_t)k * U;
-    int lo = 0, hi = H;  // first h with seg_off[h] >= target
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (seg_off[mid] < target) lo = mid + 1;
-      else hi = mid;
-    }
-    // then the first segment from there on that holds rows (H: none), so no unit starts with a
-    // run of empty segments (an owner shard's buckets hold every other rank's levels too)
-    const int32_t t = lo < H ? seg_off[lo] : 0;
-    hi = H;
-    while (lo < hi) {  // first h with seg_off[h + 1] > t
-      const int mid = (lo + hi) >> 1;
-      if (seg_off[mid + 1] <= t) lo = mid + 1;
-      else hi = mid;
-    }
-    units[k] = lo;
+                              int4* __restrict__ desc) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_units; k += gridDim.x * blockDim.x) {
+    const int h = unit_first(seg_off, H, U, k, n_units), h1 = unit_first(seg_off, H, U, k + 1, n_units);
+    desc[k] = int4{h, h1, seg_off[h], seg_off[h1]};
   }
 }
 
@@ -606,11 +612,11 @@ static int build_layouts(lfe_ctx* c, int Q) {
   if (const char* e = getenv("LFE_K1_UNIT")) U = std::max<int64_t>(16, atoll(e) / 16 * 16);
   const int32_t H = L.nb * B;
   c->n_units = (int)std::max<int64_t>(1, (c->n_kept_local + U - 1) / U);
-  LFE_TRY(ensure_i32(c, c->seg_units, c->seg_units_cap, (size_t)c->n_units + 1));
+  LFE_TRY(ensure_i32(c, c->seg_units, c->seg_units_cap, (size_t)4 * c->n_units));
   {
     ProfScope _ps(c, K_MISC);
-    hipLaunchKernelGGL(k_unit_bounds, dim3(grid_for(c->n_units + 1)), dim3(kBlock), 0, c->stream, c->seg_off, H, U,
-                       c->n_units, c->seg_units);
+    hipLaunchKernelGGL(k_unit_bounds, dim3(grid_for(c->n_units)), dim3(kBlock), 0, c->stream, c->seg_off, H, U,
+                       c->n_units, reinterpret_cast<int4*>(c->seg_units));
   }
   LFE_HIP(hipGetLastError());
   return LFE_OK;
@@ -668,7 +674,7 @@ constexpr int kBatch = 16;
 struct TpArgs {
   const int32_t* seg_off;  // [H + 1] segment offsets (h = bucket * B + offset)
   const int32_t* seg_q;    // secondary code of each kept row, segment order
-  const int32_t* units;    // [n_units + 1] first segment of each work unit
+  const int4* units;       // [n_units] work unit descriptors (k_unit_bounds)
   int n_units;
   int G_Q, G_P, p;
   const double* alphaQ;  // [G_Q][p]
@@ -689,6 +695,9 @@ __device__ __forceinline__ void tp_body(const TpArgs& a, double* __restrict__ aq
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kq = lane >> 4, c = lane & 15;
   const int p = a.p, G_Q = a.G_Q;
+  // the wave's first unit descriptor is loaded before the staging, so its latency overlaps it
+  const int u_first = blk * (kTpThreads / 64) + wave;
+  const int4 d_first = u_first < a.n_units ? a.units[u_first] : int4{0, 0, 0, 0};
   stage_lds<kTpThreads>(aq, a.alphaQ, G_Q * p, tid);
   for (int j = tid; j < p; j += kTpThreads) aq[G_Q * p + j] = 0.0;
   for (int64_t j = (int64_t)blk * kTpThreads + tid; j < a.zero_n; j += (int64_t)nblk * kTpThreads)
@@ -700,13 +709,14 @@ __device__ __forceinline__ void tp_body(const TpArgs& a, double* __restrict__ aq
   for (int I = 0; I < NT; ++I) cl8[I] = 8 * (16 * I + c < p ? 16 * I + c : 0);
   const uint32_t p8 = 8 * p;
   const int nwaves = nblk * (kTpThreads / 64);
-  for (int u = blk * (kTpThreads / 64) + wave; u < a.n_units; u += nwaves) {
-    int h = a.units[u];
-    const int h1 = a.units[u + 1];
+  for (int u = u_first; u < a.n_units; u += nwaves) {
+    const int4 ud = u == u_first ? d_first : a.units[u];
+    int h = ud.x;
+    const int h1 = ud.y;
     if (h >= h1) continue;
-    int r0 = a.seg_off[h], r1 = a.seg_off[h + 1];
-    const int g0 = r0 >> 4, g1 = (a.seg_off[h1] + 15) >> 4;
-    const int rend = a.seg_off[h1];  // the unit's rows end here
+    int r0 = ud.z;
+    const int rend = ud.w;  // the unit's rows end here
+    const int g0 = r0 >> 4, g1 = (rend + 15) >> 4;
     double acc[NT];
 #pragma unroll
     for (int I = 0; I < NT; ++I) acc[I] = 0.0;
@@ -740,6 +750,7 @@ __device__ __forceinline__ void tp_body(const TpArgs& a, double* __restrict__ aq
     // zeroed table (T_P: the memset before K1; alpha_P: prepare_layout)
     int hb = h;
     int win = hb + lane < h1 ? a.seg_off[hb + lane + 1] : 0x7fffffff;
+    int r1 = __builtin_amdgcn_readlane(win, 0);  // seg_off[h + 1]
     auto next_seg = [&]() -> bool {  // segment h is complete
       ++h;
       r0 = r1;
@@ -882,7 +893,7 @@ __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
 struct TqArgs {
   const int32_t* run_off;  // [nb * G_Q + 1] run offsets
   const uint16_t* run_h;   // primary code - lo of each kept row, run order
-  const int32_t* blist;    // [nbe] the buckets that hold rows, in order
+  const int32_t* blist;    // [nbe] the buckets that hold rows, in order (null: all nb buckets)
   int nbe, s, G_Q, G_P, p;
   const double* alphaP;  // [G_P][p]
   double* runs;          // [nbe * G_Q][p]: the sum of every (listed bucket, q) run (empty runs: 0)
@@ -909,8 +920,21 @@ __device__ __forceinline__ void tq_body(const TqArgs& a, double* __restrict__ sl
   const int kTqSplit = a.split;
   for (int bs = blk; bs < a.nbe * kTqSplit; bs += nblk) {
     const int bi = bs / kTqSplit, part = bs % kTqSplit;
-    const int b = a.blist[bi];
+    const int b = a.blist ? a.blist[bi] : bi;  // no list: every bucket holds rows
     const int lo = b << a.s;
+    // wave: runs q in [q, q1) of bucket b; their offsets (and the ends of runs q .. q + 63 in the
+    // lanes of one register) are loaded before the staging, so their latency overlaps it
+    const int slot = part * NW + wave;
+    int q = slot * G_Q / (NW * kTqSplit);
+    const int q1 = (slot + 1) * G_Q / (NW * kTqSplit);
+    const int32_t* off = a.run_off + (int64_t)b * G_Q;
+    int r0 = 0, r1 = 0, rq1 = 0, win = 0;
+    if (q < q1) {
+      r0 = off[q];
+      r1 = off[q + 1];
+      rq1 = off[q1];
+      win = q + lane < q1 ? off[q + lane + 1] : 0;
+    }
     __syncthreads();
     {  // the bucket's rows of alpha_P are contiguous (16-byte aligned: lo p 8 = b 2^s p 8); rows
        // past G_P and the zero row B are cleared
@@ -919,22 +943,14 @@ __device__ __forceinline__ void tq_body(const TqArgs& a, double* __restrict__ sl
       for (int j = nv + tid; j < (B + 1) * p; j += kTqThreads) sl[j] = 0.0;
     }
     __syncthreads();
-    // wave: runs q in [q, q1) of bucket b
-    const int slot = part * NW + wave;
-    int q = slot * G_Q / (NW * kTqSplit);
-    const int q1 = (slot + 1) * G_Q / (NW * kTqSplit);
     if (q >= q1) continue;
-    const int32_t* off = a.run_off + (int64_t)b * G_Q;
     double* const runs = a.runs + (int64_t)bi * G_Q * p;
-    int r0 = off[q], r1 = off[q + 1];
-    const int g0 = r0 >> 4, g1 = (off[q1] + 15) >> 4;
+    const int g0 = r0 >> 4, g1 = (rq1 + 15) >> 4;
     if (g0 >= g1) {  // no rows in these runs
       for (int j = lane; j < (q1 - q) * p; j += 64) runs[(int64_t)q * p + j] = 0.0;
       continue;
     }
-    // the ends of runs qb .. qb + 63 in the lanes of one register: no global load per run
-    int qb = q;
-    int win = qb + lane < q1 ? off[qb + lane + 1] : 0;
+    int qb = q;  // win holds the ends of runs qb .. qb + 63: no global load per run
     auto run_end = [&](int qq) -> int {
       if (qq - qb >= 64) {
         qb = qq;
@@ -1226,7 +1242,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   TpArgs tp{};
   tp.seg_off = c->seg_off;
   tp.seg_q = c->seg_q;
-  tp.units = c->seg_units;
+  tp.units = reinterpret_cast<const int4*>(c->seg_units);
   tp.n_units = c->n_units;
   tp.G_Q = fq.G;
   tp.G_P = fp.G;
@@ -1238,7 +1254,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   TqArgs tq{};
   tq.run_off = c->run_off;
   tq.run_h = c->run_h;
-  tq.blist = c->blist_d;
+  tq.blist = c->nbe == c->L.nb ? nullptr : c->blist_d;
   tq.nbe = c->nbe;
   tq.s = c->L.s;
   tq.G_Q = fq.G;

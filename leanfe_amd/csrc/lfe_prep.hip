@@ -271,6 +271,42 @@ __global__ __launch_bounds__(256) void k_scan_add_few(ScanPair sp, const int32_t
     }
 }
 
+// small scans in one launch: one 1024-thread block walks a1 then a2 in 8192-element rounds
+// (eight per thread, carried from round to round), with out[b] = a1[b * gstride] from registers
+constexpr int64_t kScanOneMax = 16384;
+__global__ __launch_bounds__(1024) void k_scan_one(ScanPair sp, int32_t* __restrict__ gout, int64_t gstride, int gn) {
+  __shared__ int32_t tmp[16];
+  __shared__ int32_t total;
+  for (int arr = 0; arr < 2; ++arr) {
+    int32_t* a = arr ? sp.a2 : sp.a1;
+    const int64_t m = arr ? sp.m2 : sp.m1;
+    if (!a) continue;
+    int32_t carry = 0;
+    for (int64_t r0 = 0; r0 < m; r0 += 1024 * kScanPer) {
+      const int64_t base = r0 + (int64_t)threadIdx.x * kScanPer;
+      int32_t v[kScanPer];
+      scan_load8(a, base, m, v);
+      int32_t t = 0;
+#pragma unroll
+      for (int k = 0; k < kScanPer; ++k) t += v[k];
+      int32_t off = block_excl_scan(t, tmp, &total) + carry;
+      int32_t o[kScanPer];
+#pragma unroll
+      for (int k = 0; k < kScanPer; ++k) {
+        o[k] = off;
+        off += v[k];
+      }
+      scan_store8(a, base, m, o);
+      if (gout && arr == 0)
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k)
+          if (base + k < m && (base + k) % gstride == 0 && (base + k) / gstride < gn) gout[(base + k) / gstride] = o[k];
+      carry += total;
+      __syncthreads();  // total is rewritten by the next round
+    }
+  }
+}
+
 static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2, int32_t* gout,
                             int64_t gstride, int gn) {
   const int64_t nb1 = (m1 + kScanBlock - 1) / kScanBlock, nb2 = a2 ? (m2 + kScanBlock - 1) / kScanBlock : 0;
@@ -283,6 +319,11 @@ static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, in
   }
   const ScanPair sp{a1, m1, nb1, a2, m2};
   ProfScope _ps(c, K_SCAN);
+  if (m1 + (a2 ? m2 : 0) <= kScanOneMax) {  // one launch instead of two
+    hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(1024), 0, c->stream, sp, gout, gstride, gn);
+    LFE_HIP(hipGetLastError());
+    return LFE_OK;
+  }
   hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums);
   if (nblocks <= kScanFewBlocks) {
     hipLaunchKernelGGL(k_scan_add_few, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->psums, gout, gstride,
