@@ -218,7 +218,11 @@ static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
   const size_t bytes = count * esz;
   LFE_HIP(hipStreamSynchronize(c->stream));
   e->slots[c->rank].resize(bytes);
-  LFE_HIP(hipMemcpy(e->slots[c->rank].data(), dev, bytes, hipMemcpyDeviceToHost));
+  // copies on this context's stream, waited for: a plain hipMemcpy runs on the null stream, which
+  // a non-blocking context stream does not order against (a later kernel could read the result
+  // before a host-to-device copy lands)
+  LFE_HIP(hipMemcpyAsync(e->slots[c->rank].data(), dev, bytes, hipMemcpyDeviceToHost, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
   e->barrier();
   if (c->rank == 0) {  // fixed rank order: deterministic
     e->result = e->slots[0];
@@ -237,7 +241,8 @@ static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
       }
   }
   e->barrier();
-  LFE_HIP(hipMemcpy(dev, e->result.data(), bytes, hipMemcpyHostToDevice));
+  LFE_HIP(hipMemcpyAsync(dev, e->result.data(), bytes, hipMemcpyHostToDevice, c->stream));
+  LFE_HIP(hipStreamSynchronize(c->stream));
   e->barrier();  // every rank has its copy before the result buffer is reused
   return LFE_OK;
 }
@@ -269,9 +274,12 @@ int alltoallv_bytes(lfe_ctx* c, const char* send, const size_t* send_off, const 
     for (int q = 0; q < W; ++q) {
       const size_t b = e->a2a_bytes[q][c->rank];
       if (b != recv_bytes[q]) return fail(LFE_EINVAL, "alltoallv: peer block size mismatch");
-      if (b) LFE_HIP(hipMemcpy(recv + recv_off[q], e->a2a_send[q] + e->a2a_off[q][c->rank], b,
-                               hipMemcpyDeviceToDevice));
+      if (b) LFE_HIP(hipMemcpyAsync(recv + recv_off[q], e->a2a_send[q] + e->a2a_off[q][c->rank], b,
+                                    hipMemcpyDeviceToDevice, c->stream));
     }
+    // the copies complete before the peers go on (a plain device-to-device hipMemcpy may return
+    // before its copy is done, and runs on the null stream, unordered with this context's stream)
+    LFE_HIP(hipStreamSynchronize(c->stream));
     e->barrier();  // every peer has read this rank's buffer
     return LFE_OK;
   }

@@ -685,6 +685,7 @@ struct TpArgs {
   double* zeroT;         // T_Q [zero_n], zeroed for the K2 pass that follows (saves a fill launch)
   int64_t zero_n;
   double* zero_check;    // the stop test's max, zeroed for the check after K2 (or null)
+  unsigned long long* dbg;  // LFE_SWEEP_TIMING (diagnostic): [block][2] wall-clock start, end
 };
 
 // K1: T_P[h] = sum_{i in h} alpha_Q[q_i]; fused: alpha_P[h] = (S_P[h] - T_P[h]) / n_h
@@ -887,7 +888,12 @@ __device__ __forceinline__ void tp_body(const TpArgs& a, double* __restrict__ aq
 template <int NT>
 __global__ __launch_bounds__(kTpThreads) void k_tp(TpArgs a) {
   extern __shared__ __attribute__((aligned(16))) double aq[];  // [G_Q + 1][p], row G_Q = 0
+  if (a.dbg && threadIdx.x == 0) a.dbg[2 * blockIdx.x] = wall_clock64();
   tp_body<NT>(a, aq, blockIdx.x, gridDim.x);
+  if (a.dbg) {
+    __syncthreads();
+    if (threadIdx.x == 0) a.dbg[2 * blockIdx.x + 1] = wall_clock64();
+  }
 }
 
 struct TqArgs {
@@ -898,6 +904,7 @@ struct TqArgs {
   const double* alphaP;  // [G_P][p]
   double* runs;          // [nbe * G_Q][p]: the sum of every (listed bucket, q) run (empty runs: 0)
   int split;             // workgroups per bucket (each takes 1 / split of the bucket's runs)
+  unsigned long long* dbg;  // LFE_SWEEP_TIMING (diagnostic): [block][2] wall-clock start, end
 };
 
 // K2: runs[i][q] = sum over the (bucket blist[i], q) run of alpha_P[h_i].  Every run is summed by
@@ -1063,7 +1070,12 @@ __device__ __forceinline__ void tq_body(const TqArgs& a, double* __restrict__ sl
 template <int NT>
 __global__ __launch_bounds__(tq_threads<NT>()) void k_tq(TqArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sl[];  // [B + 1][p], row B = 0
+  if (a.dbg && threadIdx.x == 0) a.dbg[2 * blockIdx.x] = wall_clock64();
   tq_body<NT>(a, sl, blockIdx.x, gridDim.x);
+  if (a.dbg) {
+    __syncthreads();
+    if (threadIdx.x == 0) a.dbg[2 * blockIdx.x + 1] = wall_clock64();
+  }
 }
 
 // T_Q[q][col] = sum over buckets b (in order) of runs[b][q][col]
@@ -1280,6 +1292,30 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     // buckets: 196 -> 392 workgroups)
     const int64_t fill = (c->n_cu + nbe - 1) / nbe;
     if (tq.split < fill && per_bucket / fill >= 8192) tq.split = (int)fill;
+    // whole rounds of resident workgroups: the split with the least rounds per share of a bucket
+    // (a workgroup's time goes as 1 / split), e.g. config 1's 40 buckets at one resident workgroup
+    // per CU: 6 per bucket (240, one round) instead of 8 (320: two rounds; K2 16.4 -> 12.9 us,
+    // per-workgroup wall clock from LFE_SWEEP_TIMING; config 1 0.46 -> 0.42 ms per solve)
+    if (!dense) {
+      const int res = std::max(1, resident_blocks(c, ftq, NT <= 2 ? 1024 : 512, std::max<size_t>(lds_tq, 1)));
+      double best = 1e30;
+      int bs = tq.split;
+      for (int sp = tq.split; sp >= 1; --sp) {
+        const double cost = (double)(((int64_t)nbe * sp + res - 1) / res) / sp;
+        if (cost < best - 1e-12) {
+          best = cost;
+          bs = sp;
+        }
+      }
+      tq.split = bs;
+    }
+  }
+  // LFE_SWEEP_TIMING (diagnostic): per-workgroup wall clock of the last K1 / K2 launch to stderr
+  const bool timing = !dense && getenv("LFE_SWEEP_TIMING") != nullptr;
+  const int tp_grid = c->n_cu, tq_grid_wg = std::max(tq.nbe, 1) * tq.split;
+  if (timing) {
+    LFE_HIP(hipMalloc(&tp.dbg, sizeof(unsigned long long) * 2 * tp_grid));
+    LFE_HIP(hipMalloc(&tq.dbg, sizeof(unsigned long long) * 2 * tq_grid_wg));
   }
   // sweep 1's Q projection: alpha_P = 0 -> alpha_Q = S_Q / n_Q (alpha_P is first written by K1,
   // which covers every primary group)
@@ -1365,6 +1401,29 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     }
     if (it == max_iter) break;
     std::swap(fq.alpha, c->alpha_spare);
+  }
+  if (timing) {
+    auto report = [&](const char* name, unsigned long long* d, int n) -> int {
+      std::vector<unsigned long long> h((size_t)2 * n);
+      LFE_HIP(hipMemcpy(h.data(), d, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+      (void)hipFree(d);
+      unsigned long long t0 = ~0ull, t1 = 0;
+      std::vector<double> dur(n), st(n);
+      for (int b = 0; b < n; ++b) t0 = std::min(t0, h[2 * b]);
+      for (int b = 0; b < n; ++b) {
+        st[b] = (h[2 * b] - t0) / 100.0;
+        dur[b] = (h[2 * b + 1] - h[2 * b]) / 100.0;
+        t1 = std::max(t1, h[2 * b + 1]);
+      }
+      std::vector<double> sd = dur, ss = st;
+      std::sort(sd.begin(), sd.end());
+      std::sort(ss.begin(), ss.end());
+      fprintf(stderr, "%s: %d workgroups, span %.2f us; start offset median %.2f max %.2f; duration min %.2f median %.2f p90 %.2f max %.2f us\n",
+              name, n, (t1 - t0) / 100.0, ss[n / 2], ss[n - 1], sd[0], sd[n / 2], sd[(n * 9) / 10], sd[n - 1]);
+      return LFE_OK;
+    };
+    LFE_TRY(report("K1 k_tp", tp.dbg, tp_grid));
+    LFE_TRY(report("K2 k_tq", tq.dbg, tq_grid_wg));
   }
   *iterations_out = iterations;
   *last_out = last;
