@@ -189,8 +189,11 @@ def device_sync(eng):
 
 
 def solve_step(eng, vcov: str, n_cl: int = 0) -> dict:
-    """One regression on the loaded shard, as ``leanfe_hip`` runs it (hip_impl.py)."""
+    """One regression on the loaded shard, as ``leanfe_hip`` runs it (hip_impl.py:230-250, the same
+    fallbacks: a second residual pass when r'r cancels in the Gram or the device Cholesky's beta
+    drifted from the host solve)."""
     from leanfe_amd import inference
+    from leanfe_amd.hip_impl import _beta_agrees
 
     n_obs, dims, card = eng.drop_singletons()
     order = sorted(range(len(card)), key=lambda i: card[i])  # polars_impl.py:485
@@ -205,9 +208,10 @@ def solve_step(eng, vcov: str, n_cl: int = 0) -> dict:
     df_resid = n_obs - (k + 1) - (sum(dims) - len(dims))
     Vb = XtX_inv[1:, 1:]
     dbeta = 0.0
-    if gram_only:
-        stats, meat = inference.stats_from_gram(G, beta_full), None
-    elif fused is not None:
+    stats, meat = (inference.stats_from_gram(G, beta_full), None) if gram_only else (None, None)
+    if stats is not None:
+        pass
+    elif fused is not None and _beta_agrees(fused[1], beta_full):
         stats, meat = fused[2], fused[3]
         # the residual pass used the device Cholesky's beta: record its distance to the host solve
         dbeta = float(abs(fused[1] - beta_full).max() / max(abs(beta_full).max(), 1e-300))
@@ -306,9 +310,13 @@ def pmc_traffic(kernel: str, a) -> tuple[float | None, str | None]:
     """HBM bytes per launch of ``kernel`` from the newest rocprofv3 PMC summary for this exact
     configuration (tools/pmc.sh + tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
     correction of MI355X_MICROARCH.md), else None."""
+    import glob
+    import re
+
     cfg = {"rows": a.rows, "k": a.k, "levels": list(a.levels), "vcov": a.vcov}
-    for rnd in ("r03", "r02", "r01"):
-        path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+    rounds = glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "pmc_traffic.json"))
+    rounds.sort(key=lambda p: int(re.search(r"r(\d+)", os.path.basename(os.path.dirname(p))).group(1)), reverse=True)
+    for path in rounds:
         try:
             with open(path) as f:
                 t = json.load(f)

@@ -289,6 +289,12 @@ int lfe_dense_cells(lfe_ctx* ctx, int64_t* cells);
  * x base-128 digits of the effects on v_mfma_i32_16x16x64_i8), 2 for the u16 / f64-MFMA form. */
 int lfe_dense_cell_bytes(lfe_ctx* ctx, int32_t* bytes);
 
+/* Test-only switches of one context (0 clears them; production code never sets any).
+ * LFE_TEST_SHORT_MEMORY: lfe_reshard_owner on this rank reports too little device memory for
+ * its staging copy, so that the all-rank refusal can be tested (every rank keeps its rows). */
+#define LFE_TEST_SHORT_MEMORY 1
+int lfe_ctx_test_hooks(lfe_ctx* ctx, int flags);
+
 /* Wait for all work queued on the context's stream. */
 int lfe_sync(lfe_ctx* ctx);
 

@@ -62,6 +62,7 @@ SIGNATURES = {
     "lfe_copy_inputs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
     "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
     "lfe_dense_cells": (C.c_int, [_vp, _i64p]),
+    "lfe_ctx_test_hooks": (C.c_int, [_vp, C.c_int]),
     "lfe_dense_cell_bytes": (C.c_int, [_vp, C.POINTER(C.c_int32)]),
     "lfe_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.POINTER(_vp), _i32p, _dp, C.c_int]),
     "lfe_stream_clusters": (C.c_int, [_vp, C.c_int, _i32p]),
@@ -510,6 +511,11 @@ class Engine:
         on = C.c_int32(0)
         _check(self._lib.lfe_exact_sums(self._h, C.byref(on)))
         return bool(on.value)
+
+    def test_hooks(self, flags: int) -> None:
+        """Test-only switches (lfe_ctx_test_hooks; 1 = LFE_TEST_SHORT_MEMORY: this rank's owner
+        re-shard reports too little device memory)."""
+        _check(self._lib.lfe_ctx_test_hooks(self._h, int(flags)))
 
     def dense_cells(self) -> int:
         """Cells of the count tables the last two-FE demean multiplied on the matrix cores (0: the row

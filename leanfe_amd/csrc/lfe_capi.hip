@@ -452,6 +452,8 @@ static void free_data(lfe_ctx* c) {
   dfree(c->dn8_fb);
   dfree(c->dn8_dq);
   dfree(c->dn8_eq);
+  dfree(c->rflag);
+  c->rflag_cap = 0;
   c->dn8_a_cap = c->dn8_b_cap = c->dn8_fa_cap = c->dn8_fb_cap = c->dn8_dq_cap = c->dn8_eq_cap = 0;
   c->dn8 = false;
   free_dense3(c);
@@ -1124,32 +1126,40 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
       if (chk[f] != f) return fail(LFE_EINVAL, "fe_order must be a permutation of 0..F-1");
   }
   if (check_from > 0 && max_iter < 1) return fail(LFE_EINVAL, "max_iter must be >= 1");
-  c->dense_cells = 0;  // demean_fast sets it when the dense cross terms run
-  c->d3.on = false;    // ... demean_dense3 this
   int iterations = 0;
   double last = -1.0;
-  c->tq_final = false;
-  c->gram_spec = false;
+  c->dense_coarse = c->dense_off = false;
   {
     PhaseTimer t(c, PH_DEMEAN);
-    const bool fast = c->F > 0 && check_from > 0 && fast_path_ok(c, order);
-    if (!fast)  // the two-FE sweeps write every alpha entry before reading any
-      for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
-    if (c->F > 0) {
-      if (!c->sums_ready) {
-        if (c->sw.on) return fail(LFE_ESTATE, "streamed X: stream the group-sums pass (lfe_stream pass 1) first");
-        LFE_TRY(sweep_group_sums(c));
+    // a second attempt only when the i8 digits' dynamic-range guard fired on the first (every rank
+    // sees the same flag): the same solve without the dense cross terms (lfe_dense.hip)
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      c->dense_cells = 0;  // demean_fast sets it when the dense cross terms run
+      c->d3.on = false;    // ... demean_dense3 this
+      c->tq_final = false;
+      c->gram_spec = false;
+      const bool fast = c->F > 0 && check_from > 0 && fast_path_ok(c, order);
+      if (!fast)  // the two-FE sweeps write every alpha entry before reading any
+        for (auto& fe : c->fe) LFE_HIP(hipMemsetAsync(fe.alpha, 0, sizeof(double) * (size_t)fe.G * c->p, c->stream));
+      if (c->F > 0) {
+        if (!c->sums_ready) {
+          if (c->sw.on) return fail(LFE_ESTATE, "streamed X: stream the group-sums pass (lfe_stream pass 1) first");
+          LFE_TRY(sweep_group_sums(c));
+        }
+        if (fast) {
+          // two FEs, unweighted: segment layout + one fused codes-only kernel per sweep
+          LFE_TRY(demean_fast(c, tol, max_iter, check_from, &iterations, &last));
+        } else if (dense3_ok(c, order, check_from)) {
+          // three or more FEs, unweighted, small pair tables: every cross term on the matrix cores
+          LFE_TRY(demean_dense3(c, order, tol, max_iter, check_from, &iterations, &last));
+        } else {
+          LFE_TRY(demean_generic(c, order, tol, max_iter, check_from, &iterations, &last));
+        }
       }
-      if (fast) {
-        // two FEs, unweighted: segment layout + one fused codes-only kernel per sweep
-        LFE_TRY(demean_fast(c, tol, max_iter, check_from, &iterations, &last));
-      } else if (dense3_ok(c, order, check_from)) {
-        // three or more FEs, unweighted, small pair tables: every cross term on the matrix cores
-        LFE_TRY(demean_dense3(c, order, tol, max_iter, check_from, &iterations, &last));
-      } else {
-        LFE_TRY(demean_generic(c, order, tol, max_iter, check_from, &iterations, &last));
-      }
+      if (!c->dense_coarse || c->dense_off) break;
+      c->dense_off = true;
     }
+    c->dense_off = false;
   }
   if (iterations_out) *iterations_out = iterations;
   if (last_check_out) *last_check_out = last;
@@ -1260,6 +1270,13 @@ int lfe_exact_sums(lfe_ctx* c, int* on) {
   LFE_CTX(c);
   if (!on) return fail(LFE_EINVAL, "null pointer");
   return exact_sums_on(c, on);
+}
+
+int lfe_ctx_test_hooks(lfe_ctx* c, int flags) {
+  LFE_CTX(c);
+  if (flags & ~LFE_TEST_SHORT_MEMORY) return fail(LFE_EINVAL, "unknown test hook");
+  c->test_hooks = flags;
+  return LFE_OK;
 }
 
 int lfe_dense_cells(lfe_ctx* c, int64_t* cells) {

@@ -561,11 +561,12 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int kDn8Tile = 512;           // k rows per digit tile (8 k blocks of 64)
 constexpr int kDn8TileBytes = 8 * 8 * 1024;
 
-// balanced base-128 digits of A = round(v * sin) (|A| <= 2^54): A = hi 2^28 + lo with |hi| <= 2^26,
-// |lo| <= 2^27 split in f64 (exact: integers), then four digits in [-64, 63] from each int32 half
-// (lo's remainder, in [-1, 1], carried into hi)
-__device__ __forceinline__ void dn8_split(double v, double sin, int (&dg)[8]) {
-  const double A = rint(v * sin);
+// balanced base-128 digits of A = round(v * s1 * s2) (|A| <= 2^54; s1, s2 powers of two, so both
+// products are exact): A = hi 2^28 + lo with |hi| <= 2^26, |lo| <= 2^27 split in f64 (exact:
+// integers), then four digits in [-64, 63] from each int32 half (lo's remainder, in [-1, 1], carried
+// into hi)
+__device__ __forceinline__ void dn8_split(double v, double s1, double s2, int (&dg)[8]) {
+  const double A = rint(v * s1 * s2);
   const double hf = rint(A * 0x1p-28);
   int lo = (int)__builtin_fma(hf, -0x1p28, A);
   int hi = (int)hf;
@@ -595,10 +596,18 @@ __device__ __forceinline__ void dn8_split(double v, double sin, int (&dg)[8]) {
 struct Dn8NoMid {
   __device__ void operator()() const {}
 };
+// Dynamic-range guard.  Digits keep every effect to 2^-54 of its tile's largest, so
+// an effect below 2^-kDn8RangeBits of the largest keeps fewer than 54 - kDn8RangeBits bits (f64
+// keeps 53 of each).  When more than a quarter of a tile column's nonzero effects lie that far
+// below its largest (one level with a 1e8 effect, a 5e9 outlier's group), the tile sets *rflag and
+// the solve is redone without the dense cross terms (lfe_demean): the result is then the row
+// passes', whose rounding is the f64 sums' own.
+constexpr int kDn8RangeBits = 16;
+
 template <int NT, class Mid = Dn8NoMid>
 __device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p, int ld, int8_t* __restrict__ fr,
                                 double* __restrict__ sc, double* __restrict__ red, Mid mid = Mid(),
-                                unsigned long long* tdbg = nullptr) {
+                                unsigned long long* tdbg = nullptr, double* rflag = nullptr) {
   constexpr int RPT = kDn8Tile * 16 / NT;  // rows per thread (32 or 16)
   const int tid = threadIdx.x, col = tid & 15, r0 = (tid >> 4) * RPT;
   double v[RPT];
@@ -637,13 +646,17 @@ __device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p,
       nb |= isnan(t);
       mm = fmax(mm, t);
     }
-    const int e = mm > 0.0 ? ilogb(mm) + 1 : 0;  // max |alpha| < 2^e
+    // max |alpha| < 2^e.  The digit scale 2^(54 - e) goes in two factors, each finite down to the
+    // smallest subnormals (one factor overflows for e < -969); e >= -1020 keeps the
+    // inverse scale 2^(e - 54) >= 2^-1074 exact, and every subnormal effect an exact integer
+    const int e = mm > 0.0 ? max(ilogb(mm) + 1, -1020) : 0;
     sc[tid] = nb ? __builtin_nan("") : ldexp(1.0, e - 54);
-    red[NT + tid] = ldexp(1.0, 54 - e);
+    red[NT + tid] = (double)e;
   }
   __syncthreads();
   if (tdbg && tid == 0) tdbg[2] = wall_clock64();
-  const double sin = red[NT + col];
+  const int ec = (int)red[NT + col], h1 = (54 - ec) >> 1;
+  const double s1 = ldexp(1.0, h1), s2 = ldexp(1.0, 54 - ec - h1);
   // rows 4 q .. 4 q + 3 of the thread's -> one 32-bit word per digit at lane (16 g + col), bytes 4 jq
 #pragma unroll
   for (int q4 = 0; q4 < RPT / 4; ++q4) {
@@ -653,7 +666,7 @@ __device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p,
     for (int u = 0; u < 4; ++u) {
       const double x = v[4 * q4 + u];
       int dg[8];
-      dn8_split(isfinite(x) ? x : 0.0, sin, dg);
+      dn8_split(isfinite(x) ? x : 0.0, s1, s2, dg);
 #pragma unroll
       for (int d = 0; d < 8; ++d) word[d] |= (dg[d] & 255) << (8 * u);
     }
@@ -661,16 +674,43 @@ __device__ void dn8_tile_digits(const double* __restrict__ src, int rows, int p,
 #pragma unroll
     for (int d = 0; d < 8; ++d) *reinterpret_cast<int*>(fr + (kb * 8 + d) * 1024 + off) = word[d];
   }
+  if (rflag) {  // the guard: per column, effects far below the largest vs nonzero effects
+    const double thr = ldexp(1.0, ec - kDn8RangeBits);
+    int pk = 0;  // small | nonzero << 16 (each <= 512 per column)
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const double x = fabs(v[u]);
+      // (a subnormal effect keeps fewer bits in f64 too: not counted as small)
+      pk += (x != 0.0) ? ((x < thr && x >= 0x1p-1022 ? 1 : 0) | (1 << 16)) : 0;
+    }
+    pk += __shfl_xor(pk, 16, 64);
+    pk += __shfl_xor(pk, 32, 64);
+    // red's first NW x 16 slots (the column maxima) were read before the second barrier
+    if ((tid & 63) < 16) red[(tid >> 6) * 16 + col] = (double)pk;
+    __syncthreads();
+    if (tid < 16 && !isnan(sc[tid])) {
+      int small = 0, nz = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int t = (int)red[w * 16 + tid];
+        small += t & 0xffff;
+        nz += t >> 16;
+      }
+      if (4 * small > nz) *rflag = 1.0;
+    }
+  }
 }
 
 // alpha_Q -> digit tiles dq [tile][kb][d][1 KB] and scales eq [tile][16] (one block per tile)
 __global__ __launch_bounds__(256) void k_dn8_digits(const double* __restrict__ alpha, int G, int p,
-                                                    int8_t* __restrict__ dq, double* __restrict__ eq) {
+                                                    int8_t* __restrict__ dq, double* __restrict__ eq,
+                                                    double* __restrict__ rflag) {
   extern __shared__ __attribute__((aligned(16))) int8_t fr[];
   __shared__ double red[256 + 16];
   __shared__ double sc[16];
   const int t = blockIdx.x, r0 = t * kDn8Tile;
-  dn8_tile_digits<256>(alpha + (int64_t)r0 * p, min(kDn8Tile, G - r0), p, p, fr, sc, red);
+  dn8_tile_digits<256>(alpha + (int64_t)r0 * p, min(kDn8Tile, G - r0), p, p, fr, sc, red, Dn8NoMid(), nullptr,
+                       rflag);
   __syncthreads();
   const int4* s4 = reinterpret_cast<const int4*>(fr);
   int4* d4p = reinterpret_cast<int4*>(dq + (int64_t)t * kDn8TileBytes);
@@ -698,6 +738,7 @@ struct Dn8Args {
   double* alphaP;
   double* zero_check;
   double* runs;           // K2: per-bucket slots [nbe][G_Q][p]
+  double* rflag;          // the digits' dynamic-range guard (dn8_tile_digits: 1.0 when set), null: off
   unsigned long long* dbg;  // diagnostic (LFE_DN8_TIMING): per workgroup wall clock at start / prologue end / end
 };
 
@@ -737,7 +778,7 @@ __global__ __launch_bounds__(512) void k_dn8_pass(Dn8Args a) {
     if (K2) {
       const int r0 = lo + t * kDn8Tile;
       dn8_tile_digits<512>(a.alpha + (int64_t)r0 * a.lda, max(0, min(kDn8Tile, min(a.B - t * kDn8Tile, a.G_P - r0))),
-                           p, a.lda, fr, sc, red);
+                           p, a.lda, fr, sc, red, Dn8NoMid(), nullptr, a.rflag);
     } else {
       // the tile's fragments, every load of a thread issued before its stores (4 KB per thread
       // round: no chain of L2 round trips)
@@ -1027,7 +1068,8 @@ __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
       if (t == 0) dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
     };
     dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.lda, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p, a.lda,
-                          fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red, mid);
+                          fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red, mid, nullptr,
+                          blockIdx.x == 0 ? a.rflag : nullptr);  // every workgroup forms the same digits
   }
   if (ntile == 0) dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
   __syncthreads();
@@ -1054,7 +1096,7 @@ __device__ __forceinline__ void dn8_k2s_body(const Dn8Args& a, int np, int blk) 
   const int lo = a.blist[bi] << a.s;
   dn8_tile_digits<512>(a.alpha + (int64_t)lo * a.lda, max(0, min(a.B, a.G_P - lo)), a.p, a.lda, fr, sc, red,
                        [&]() { dn8_ring_fill(a, R, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane); },
-                       a.dbg ? a.dbg + 3 * 65536 + (size_t)blockIdx.x * 4 : nullptr);
+                       a.dbg ? a.dbg + 3 * 65536 + (size_t)blockIdx.x * 4 : nullptr, a.rflag);
   __syncthreads();
   if (a.dbg && tid == 0) a.dbg[blockIdx.x * 3 + 1] = wall_clock64();
   dn8_wave_stream<true>(a, fr, sc, (int64_t)bi * a.nrb, i0 + wave, W, i1, lane, R);
@@ -1166,6 +1208,7 @@ static bool dn8_ok(const lfe_ctx* c);
 // take the pre-filter counts from them (dense_build(c, true)) where the dense passes would run on a
 // panel without drops (the cmax bound is checked on the device) - LFE_DN_PRE=0 turns it off
 bool dense_pre_ok(const lfe_ctx* c) {
+  if (c->dense_off) return false;
   const char* e = getenv("LFE_DENSE");
   if (e && e[0] == '0') return false;
   const char* pe = getenv("LFE_DN_PRE");
@@ -1180,6 +1223,7 @@ bool dense_pre_ok(const lfe_ctx* c) {
 }
 
 bool dense_ok(const lfe_ctx* c) {
+  if (c->dense_off) return false;  // the digits' range guard fired (lfe_demean)
   const char* e = getenv("LFE_DENSE");  // "0": never (A/B); "1": whenever it fits
   if (e && e[0] == '0') return false;
   const int P = c->L.P, Q = 1 - P, p = c->p;
@@ -1189,12 +1233,18 @@ bool dense_ok(const lfe_ctx* c) {
   // the f64 passes hold the B operand tables in LDS (p <= 16); the i8 passes their digit tiles
   if (!dn8_ok(c) && (p > 16 || GQ16 * p * 8 > 100 * 1024 || B * p * 8 > 64 * 1024)) return false;
   if (kDnHC * GQ16 * 2 > 150 * 1024) return false;                        // the build's counters
-  if (c->fe[P].cmax > 65535) return false;                                 // uint16 counts
+  if (c->fe[P].cmax > 65535 || c->cmax_over_ranks > 0) return false;      // uint16 counts
   // the products cost ~ the cells (~1.1 ns per cell and pass), the row passes ~ the rows (~3.2 ns
   // per row and pass): dense from 0.3 rows per cell (50M rows over 1e5 x 1e3: 0.5; config 2's 10M:
-  // 0.1, where the dense passes measured 1.5x the row passes)
-  if (!(e && e[0] == '1') && (double)c->n_kept_local < 0.3 * (double)dn_cells(c)) return false;
-  return true;
+  // 0.1, where the dense passes measured 1.5x the row passes).  Owner-sharded ranks decide from the
+  // whole panel's rows and cells, so every rank takes the same sweeps (a rank on the row
+  // layouts beside ranks on the tables rounds its cross terms differently)
+  if (e && e[0] == '1') return true;
+  if (c->owner_on && c->world > 1) {
+    const int64_t nb_all = ((int64_t)c->fe[P].G + B - 1) / B;
+    return (double)c->n_kept >= 0.3 * (double)(nb_all * B * GQ16);
+  }
+  return (double)c->n_kept_local >= 0.3 * (double)dn_cells(c);
 }
 
 int dense_build(lfe_ctx* c, bool pre) {
@@ -1302,7 +1352,14 @@ static Dn8Args dn8_args(const lfe_ctx* c) {
   a.G_P = c->fe[P].G;
   a.p = c->p;
   a.lda = a.ldo = c->p;
+  a.rflag = c->rflag;
   return a;
+}
+
+int range_flag_reset(lfe_ctx* c) {
+  LFE_TRY(ensure_f64(c, c->rflag, c->rflag_cap, 2));
+  LFE_HIP(hipMemsetAsync(c->rflag, 0, sizeof(double) * 2, c->stream));
+  return LFE_OK;
 }
 
 // K2 streaming workgroups per bucket (tile): two are resident per CU (64 KB of LDS each), so the
@@ -1385,7 +1442,7 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
     LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_digits), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kDn8TileBytes));
     hipLaunchKernelGGL(k_dn8_digits, dim3(ntile), dim3(256), kDn8TileBytes, c->stream, alphaQ, a.G_Q, a.p, c->dn8_dq,
-                       c->dn8_eq);
+                       c->dn8_eq, a.rflag);
     LFE_HIP(hipGetLastError());
     constexpr int waves = 4;
     a.rbw = dn8_rbw(c, a.nrb, waves);
@@ -1504,6 +1561,7 @@ int dn8_pair_passes(lfe_ctx* c, const PairPass* pp, int n) {
       if (pp[j].ntile_k < 1 || pp[j].nrb < 1) continue;
       const int q = b.n++;
       b.a[q] = pair_args(pp[j]);
+      b.a[q].rflag = c->rflag;
       // the batch shares the chip: its passes' workgroups together fill one round of the resident ones
       b.np[q] = 1;
       b.start[q] = grid;

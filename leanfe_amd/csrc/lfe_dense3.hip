@@ -303,6 +303,7 @@ __global__ __launch_bounds__(256) void k_d3_ycheck(const double* __restrict__ S,
 
 bool dense3_ok(const lfe_ctx* c, const std::vector<int>& order, int check_from) {
   (void)order;
+  if (c->dense_off) return false;  // the digits' range guard fired (lfe_demean)
   const char* e = getenv("LFE_DENSE");  // "0": never (A/B); "1": whenever it fits
   if (e && e[0] == '0') return false;
   const bool force = e && e[0] == '1';
@@ -311,17 +312,24 @@ bool dense3_ok(const lfe_ctx* c, const std::vector<int>& order, int check_from) 
   if (!(c->world == 1 || c->owner_on)) return false;
   for (int f = 0; f < F; ++f)
     if (c->fe[f].G < 1 || c->fe[f].G > kD3MaxG) return false;
+  // owner-sharded ranks: the primary FE's largest level over all ranks (other FEs' counts are
+  // all-reduced), and the whole panel's rows per rank, so that every rank decides alike
+  const bool owner = c->owner_on && c->world > 1;
+  auto cmax = [&](int f) {
+    return owner && f == c->L.P ? (c->cmax_over_ranks > 0 ? 65536 : 0) : c->fe[f].cmax;
+  };
   int64_t bytes = 0;
   for (int a = 0; a < F; ++a)
     for (int b = a + 1; b < F; ++b) {
-      if (std::min(c->fe[a].cmax, c->fe[b].cmax) > 65535) return false;  // u16 counts
+      if (std::min(cmax(a), cmax(b)) > 65535) return false;  // u16 counts
       bytes += 2 * n512(c->fe[a].G) * n512(c->fe[b].G);
     }
   if (bytes > (int64_t)24 << 30) return false;
   // a pass reads a table byte per cell and 16 columns; the row gathers cost ~75 ps per row and sweep
   // against ~0.25 ps per table byte: dense from 16 table bytes per kept row
   const int64_t ncg = (c->p + 15) / 16;
-  return force || bytes * ncg <= 16 * std::max<int64_t>(c->n_kept_local, 1);
+  const int64_t rows = owner ? c->n_kept / c->world : c->n_kept_local;
+  return force || bytes * ncg <= 16 * std::max<int64_t>(rows, 1);
 }
 
 void free_dense3(lfe_ctx* c) {
@@ -361,7 +369,7 @@ static int d3_build(lfe_ctx* c) {
     LFE_HIP(hipMalloc(reinterpret_cast<void**>(&d.tiles), sizeof(int32_t) * (kD3MaxG / kD3Tile)));
     std::vector<int32_t> id(kD3MaxG / kD3Tile);
     for (size_t i = 0; i < id.size(); ++i) id[i] = (int32_t)i;
-    LFE_HIP(hipMemcpy(d.tiles, id.data(), sizeof(int32_t) * id.size(), hipMemcpyHostToDevice));
+    LFE_TRY(h2d_small(c, d.tiles, id.data(), sizeof(int32_t) * id.size()));  // on c->stream (pinned staging)
   }
   const int64_t n = c->n;
   LFE_TRY(ensure_dev(d.part, d.part_cap, (size_t)std::max<int64_t>(c->n_kept_local, 1)));
@@ -524,7 +532,8 @@ int demean_dense3(lfe_ctx* c, const std::vector<int>& order, double tol, int max
   c->dn8 = true;
   const int F = c->F, p = c->p, f0 = order[0];
   LFE_TRY(ensure_f64(c, c->alpha_spare, c->alpha_spare_cap, (size_t)c->fe[f0].G * p));
-  LFE_TRY(ensure_dred(c, 1));
+  LFE_TRY(ensure_dred(c, 2));
+  LFE_TRY(range_flag_reset(c));  // the digits' dynamic-range guard (lfe_dense.hip)
   int iterations = 0;
   double last = -1.0;
   bool first_ready = false;  // alpha_spare holds order[0]'s next projection (formed by the last check)
@@ -563,10 +572,24 @@ int demean_dense3(lfe_ctx* c, const std::vector<int>& order, double tol, int max
         LFE_TRY(d3_ycheck(c, f, fe.R, 1));
       }
     }
-    // owner-sharded rows: each rank's check covers its own primary levels; the max over ranks
-    if (c->owner_on) LFE_TRY(allreduce_max_u64(c, reinterpret_cast<uint64_t*>(c->dred), 1));
-    LFE_TRY(d2h_sync(c, &last, c->dred, sizeof(double)));
+    // owner-sharded rows: each rank's check covers its own primary levels (and its digits flag
+    // their own effects); the max over ranks of both
+    LFE_HIP(hipMemcpyAsync(c->dred + 1, c->rflag, sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    if (c->owner_on) LFE_TRY(allreduce_max_u64(c, reinterpret_cast<uint64_t*>(c->dred), 2));
+    double rb[2];
+    LFE_TRY(d2h_sync(c, rb, c->dred, sizeof(rb)));
+    last = rb[0];
+    if (rb[1] != 0.0) {  // a tile's digits lost precision: lfe_demean redoes the solve without them
+      c->dense_coarse = true;
+      break;
+    }
     if (last < tol) break;
+  }
+  if (!c->dense_coarse && !checked) {  // the loop ended without a check
+    if (c->owner_on) LFE_TRY(allreduce_max_u64(c, reinterpret_cast<uint64_t*>(c->rflag), 1));
+    double f = 0.0;
+    LFE_TRY(d2h_sync(c, &f, c->rflag, sizeof(double)));
+    c->dense_coarse = f != 0.0;
   }
   // the last FE's T used every other FE's final effects; so did order[0]'s from the stop test
   c->d3.t_final = (1u << order[F - 1]) | (checked ? 1u << f0 : 0u);

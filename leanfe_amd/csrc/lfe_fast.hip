@@ -360,7 +360,7 @@ __device__ __forceinline__ void sums2_raw_body(const Sums4Args& a, double* __res
                 atomicAdd(&hiQ[(int64_t)gq[r] * p + c], hh);
               }
             } else {  // no coarse limbs: round(x sf) as the low bits of x sf + 1.5 * 2^52
-              const u64 xi = (u64)__double_as_longlong(__builtin_fma(xv, fc.sf, kFixMagic)) - kFixMagicBits;
+              const u64 xi = (u64)__double_as_longlong(__builtin_fma(xv * fc.sf2, fc.sf, kFixMagic)) - kFixMagicBits;
               atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(lds, hv[r] - lo, p8, c8)), xi);
               atomicAdd(reinterpret_cast<u64*>(lds_row_ptr(qtab, gq[r], p8, c8)), xi);
             }
@@ -843,8 +843,9 @@ int sums4(lfe_ctx* c) {
   const int NT = (p + 15) / 16;
   const void* fn = nullptr;
 #define SUMS4_FN(FQ, GU, NT_, TH_) reinterpret_cast<const void*>(&k_sums4<FQ, GU, NT_, TH_, false>)
-  // the raw Gram of the shifted columns rides along when the Gram can come from the tables
-  const bool raw = c->F == 2 && P >= 0 && a.nq == 1 && p <= 15 && !a.w;
+  // the raw Gram of the shifted columns rides along when the Gram can come from the tables (not
+  // in the column-group sums, which form no raw tile: the Gram then takes its own raw pass)
+  const bool raw = cg_nc == 0 && c->F == 2 && P >= 0 && a.nq == 1 && p <= 15 && !a.w;
   c->raw_ready = false;
   int threads = kSumThreads;
   bool two = false;

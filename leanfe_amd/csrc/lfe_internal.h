@@ -22,6 +22,7 @@ constexpr int kColStatHead = 64; // colstat: max |x_c| bits of every column befo
 // [kIscratchCmax, + F) largest kept count per FE
 constexpr int kIscratchCmax = 2 * kMaxFE + 8;
 constexpr int kIsDnPre = 2 * kMaxFE + 6;  // iscratch: a primary level of > 65535 rows in the pre-filter table build
+constexpr int kIsCmaxOver = 2 * kMaxFE + 7;  // iscratch: ranks whose primary FE keeps a level of > 65535 rows (owner)
 constexpr int kIscratchInts = kIscratchCmax + kMaxFE;
 constexpr int kBlock = 256;      // threads per workgroup for simple streaming kernels
 constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
@@ -217,6 +218,13 @@ struct lfe_ctx {
   size_t dn8_dq_cap = 0;
   double* dn8_eq = nullptr;
   size_t dn8_eq_cap = 0;
+  // the digits' dynamic-range guard (lfe_dense.hip dn8_tile_digits): [0] nonzero when some tile of
+  // effects held most of its values 2^16 below its largest; lfe_demean then redoes the solve
+  // without the dense cross terms (dense_off), and dense_coarse records that it did
+  double* rflag = nullptr;
+  size_t rflag_cap = 0;
+  bool dense_off = false;
+  bool dense_coarse = false;
   // general dense sweeps (lfe_dense3.hip, three or more FEs): per ordered FE pair (a, b) the i8
   // count table of a's levels x b's levels in the K2 fragment form of the two-FE passes ([tile of 512
   // b levels][16-row block of a][8 k blocks][1 KB]), its block flags and the flagged blocks' u16
@@ -352,6 +360,9 @@ struct lfe_ctx {
   // state
   int64_t n_kept = 0;
   int64_t n_kept_local = 0;  // kept rows of this shard
+  // owner-sharded ranks whose primary FE keeps a level of more than 65535 rows (summed with the kept
+  // rows): the dense-path decisions use it so that every rank takes the same sweeps
+  int32_t cmax_over_ranks = 0;
   bool loaded = false, prepared = false, demeaned = false;
   bool sums_ready = false;  // S (and W, Sy) already enqueued by lfe_drop_singletons
   bool seg_ready = false;   // segment layouts built for the current drop_singletons
@@ -364,6 +375,7 @@ struct lfe_ctx {
   int owner_fe = -1;
   int32_t owner_lo = 0, owner_hi = 0;
   bool owner_on = false;
+  int test_hooks = 0;  // lfe_ctx_test_hooks (LFE_TEST_* bits; tests only, 0 in production)
   // deterministic T_Q: per-(bucket, q) run sums reduced in bucket order (no cross-bucket atomics)
   double* tq_runs = nullptr;     // [nb * G_Q][p]
   size_t tq_runs_cap = 0;
@@ -439,6 +451,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
 bool dense_ok(const lfe_ctx* c);
 int dense_build(lfe_ctx* c, bool pre = false);  // pre: before the marks, every row, with the pre-filter counts
 bool dense_pre_ok(const lfe_ctx* c);
+// the guard's flag: zeroed at the start of a dense solve; read with the stop test (read_check)
+int range_flag_reset(lfe_ctx* c);
 int64_t dense_table_cells(const lfe_ctx* c);
 int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check);
 int dense_tq(lfe_ctx* c, double* runs);
@@ -715,18 +729,20 @@ inline int alpha_pitch(int p) { return p <= 4 ? 4 : p <= 8 ? 8 : (p + 15) / 16 *
 // ---------------------------------------------------------------------------
 constexpr int kFqCols = kMaxCols + 3;
 constexpr int kAstatBlocks = 256;       // blocks of the effect-table statistics (k_alpha_stats)   // quanta table columns: p data columns (+ w, raw y)
-enum { FQ_SF = 0, FQ_QF = 1, FQ_BIG = 2, FQ_IQC = 3, FQ_QC = 4, FQ_RMS = 5, FQ_MAX = 6, kFqRows = 7 };
+enum { FQ_SF = 0, FQ_QF = 1, FQ_BIG = 2, FQ_IQC = 3, FQ_QC = 4, FQ_RMS = 5, FQ_MAX = 6, FQ_SF2 = 7, kFqRows = 8 };
 constexpr double kFixRange = 64.0;      // typical values: |v| <= kFixRange * rms
 constexpr double kFixMagic = 6755399441055744.0;  // 1.5 * 2^52: fma(v, s, magic) - magic = round(v s)
 constexpr unsigned long long kFixMagicBits = 0x4338000000000000ull;
 
 struct FixCol {
   double sf = 0.0, iqc = 0.0, qc = 0.0;
+  double sf2 = 1.0;  // the fine scale is sf * sf2 (two exact powers of two: 2^s overflows past s = 1023)
   bool big = false;  // some value of the column may have a coarse limb
 };
 __device__ __forceinline__ FixCol fix_col(const double* __restrict__ fq, int c) {
   FixCol q;
   q.sf = fq[FQ_SF * kFqCols + c];
+  q.sf2 = fq[FQ_SF2 * kFqCols + c];
   q.big = fq[FQ_BIG * kFqCols + c] != 0.0;
   q.iqc = fq[FQ_IQC * kFqCols + c];
   q.qc = fq[FQ_QC * kFqCols + c];
@@ -739,7 +755,7 @@ __device__ __forceinline__ unsigned long long fix_split(double v, const FixCol& 
     h = __builtin_fma(v, q.iqc, kFixMagic) - kFixMagic;     // round(v / Qc); NaN / Inf stay
     v = __builtin_isfinite(h) ? __builtin_fma(-h, q.qc, v) : 0.0;  // exact remainder, |.| <= Qc / 2
   }
-  return (unsigned long long)__double_as_longlong(__builtin_fma(v, q.sf, kFixMagic)) - kFixMagicBits;
+  return (unsigned long long)__double_as_longlong(__builtin_fma(v * q.sf2, q.sf, kFixMagic)) - kFixMagicBits;
 }
 // the sum of a table entry from its limbs (fine: int64 bits, coarse: f64)
 __device__ __forceinline__ double fix_value(unsigned long long lo, double hi, const double* __restrict__ fq, int c) {
@@ -759,9 +775,14 @@ __device__ inline void fix_quanta_col(double M, double rms, double N, double* __
     (void)frexp(T > 0.0 ? T : M, &a);  // T < 2^a: |v| <= T rounds to h = 0 with Qc = 2^(a + 1)
     b = a + 1;
     while (fmax(N, 1.0) * (ldexp(M, -b) + 1.0) >= 0x1p51) ++b;  // sum of |h| over one group < 2^51
+    b = min(b, 1023);  // Qc finite (a column of values near DBL_MAX)
   }
-  const int s = min(63 - eN, 52) - b;  // sum of |lo| <= N 2^(b-1) 2^s < 2^62, |lo| <= 2^51
-  fq[FQ_SF * kFqCols + c] = ldexp(1.0, s);
+  // sum of |lo| <= N 2^(b-1) 2^s < 2^62, |lo| <= 2^51; s <= 1074 keeps the quantum 2^-s a (subnormal)
+  // double, and the scale goes in two factors once s passes 1000 (a column of values near 1e-300)
+  const int s = min(min(63 - eN, 52) - b, 1074);
+  const int s2 = s > 1000 ? s - 1000 : 0;
+  fq[FQ_SF * kFqCols + c] = ldexp(1.0, s - s2);
+  fq[FQ_SF2 * kFqCols + c] = ldexp(1.0, s2);
   fq[FQ_QF * kFqCols + c] = ldexp(1.0, -s);
   // (a margin below Qc / 2: a value may exceed its bound M by the rounding of the sum it came from)
   fq[FQ_BIG * kFqCols + c] = (!finite || M >= ldexp(1.0 - 0x1p-20, b - 1)) ? 1.0 : 0.0;

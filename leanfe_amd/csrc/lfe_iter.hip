@@ -1226,7 +1226,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   // dense count tables where the primary x secondary table holds >= ~0.15 rows per cell (both
   // cross terms on the matrix cores, lfe_dense.hip); else the segment / run layouts
   // the tables prepare_layout built on every row hold the kept rows when nothing was dropped
-  const bool dense = c->dn_pre_valid || dense_ok(c);
+  // (owner-sharded ranks: dense_ok alone, a decision every rank takes alike; dn_pre_valid is local)
+  const bool dense = !c->dense_off && ((c->dn_pre_valid && c->world == 1) || dense_ok(c));
   c->dense_cells = 0;
   if (dense) {
     c->hists_kept = false;
@@ -1236,7 +1237,11 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     LFE_TRY(build_layouts(c, Q));
   }
   LFE_TRY(ensure_f64(c, c->alpha_spare, c->alpha_spare_cap, (size_t)fq.G * p));
-  LFE_TRY(ensure_dred(c, 1));
+  LFE_TRY(ensure_dred(c, 2));
+  // the i8 digits' dynamic-range guard: its flag rides with the stop test's read-back (and, with
+  // several ranks, with every sweep's T_Q all-reduce, so all ranks see the same flag)
+  const bool guard = dense && c->dn8;
+  if (guard) LFE_TRY(range_flag_reset(c));
   const size_t lds_tp = sizeof(double) * ((size_t)fq.G + 1) * p;
   const size_t lds_tq = sizeof(double) * (((size_t)1 << c->L.s) + 1) * p;
   const void* ftp = NT == 1 ? reinterpret_cast<const void*>(&k_tp<1>)
@@ -1322,6 +1327,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   LFE_TRY(fin_check(c, Q, nullptr, nullptr, fq.alpha, false));
   int iterations = 0;
   double last = -1.0;
+  int flag_read = 0;  // the sweep whose check read the guard's flag
   for (int it = 1; it <= max_iter; ++it) {
     tp.alphaQ = fq.alpha;
     tp.zeroT = nullptr;  // K2 writes every run slot; k_tq_reduce writes T_Q
@@ -1379,7 +1385,10 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
                            m, fq.T);
       }
       LFE_HIP(hipGetLastError());
-      LFE_TRY(allreduce_sum_f64(c, fq.T, (size_t)fq.G * p));
+      if (guard)
+        LFE_TRY(allreduce_sum_f64_many(c, {{fq.T, (size_t)fq.G * p}, {c->rflag, 1}}));
+      else
+        LFE_TRY(allreduce_sum_f64(c, fq.T, (size_t)fq.G * p));
       if (!check && it == max_iter) break;
       LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check));
     }
@@ -1388,12 +1397,21 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       // or the previous was within 100x of tol: the check falls ~100x per sweep) - the Gram of
       // the tables and its Cholesky, so the GPU works through the host's decision and the
       // return to the caller; lfe_gram_resid then starts at the residual pass
-      LFE_TRY(d2h_async(c, c->dred, sizeof(double)));
+      if (guard)
+        LFE_HIP(hipMemcpyAsync(c->dred + 1, c->rflag, sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+      LFE_TRY(d2h_async(c, c->dred, sizeof(double) * (guard ? 2 : 1)));
       int spec = 0;
       c->tq_final = true;
       if (it == check_from || (last >= 0.0 && last < 100.0 * tol)) LFE_TRY(gram_spec_enqueue(c, &spec));
       c->tq_final = false;
-      LFE_TRY(d2h_wait(c, &last, sizeof(double)));
+      double rb[2] = {0.0, 0.0};
+      LFE_TRY(d2h_wait(c, rb, sizeof(double) * (guard ? 2 : 1)));
+      last = rb[0];
+      flag_read = it;
+      if (rb[1] != 0.0) {  // a tile's digits lost precision: lfe_demean redoes the solve without them
+        c->dense_coarse = true;
+        break;
+      }
       if (last < tol) {  // converged after sweep `it`: keep alpha_Q of this sweep
         c->gram_spec = spec != 0;
         break;
@@ -1401,6 +1419,11 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     }
     if (it == max_iter) break;
     std::swap(fq.alpha, c->alpha_spare);
+  }
+  if (guard && !c->dense_coarse && flag_read != iterations) {  // the loop ended without a check
+    double f = 0.0;
+    LFE_TRY(d2h_sync(c, &f, c->rflag, sizeof(double)));
+    c->dense_coarse = f != 0.0;
   }
   if (timing) {
     auto report = [&](const char* name, unsigned long long* d, int n) -> int {

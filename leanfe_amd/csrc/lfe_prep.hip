@@ -799,10 +799,12 @@ __global__ void k_kept_pack(const int32_t* __restrict__ is, int64_t n, int P, in
   d[0] = (double)(n - is[2 * kMaxFE]);
   d[1] = owner ? (double)is[2 * P] : 0.0;
   d[2] = owner ? (double)is[2 * P + 1] : 0.0;
+  d[3] = owner && is[kIscratchCmax + P] > 65535 ? 1.0 : 0.0;  // the dense paths' u16 counts (dense_ok)
 }
-__global__ void k_kept_unpack(const double* __restrict__ d, int32_t* __restrict__ is) {
+__global__ void k_kept_unpack(const double* __restrict__ d, int owner, int32_t* __restrict__ is) {
   if (threadIdx.x != 0) return;
   const int64_t k = (int64_t)d[0];
+  is[kIsCmaxOver] = owner ? (int32_t)d[3] : 0;
   is[kIsKept] = (int32_t)(uint32_t)(k & 0xffffffffll);
   is[kIsKept + 1] = (int32_t)(k >> 32);
   is[kIsKept + 2] = (int32_t)d[1];
@@ -1204,12 +1206,12 @@ int prepare_layout(lfe_ctx* c) {
     }
   }
   if (c->world > 1) {
-    LFE_TRY(ensure_dred(c, 3));
+    LFE_TRY(ensure_dred(c, 4));
     hipLaunchKernelGGL(k_kept_pack, dim3(1), dim3(64), 0, c->stream, c->iscratch, n, L.P, c->owner_on ? 1 : 0,
                        c->dred);
     LFE_HIP(hipGetLastError());
-    LFE_TRY(allreduce_sum_f64(c, c->dred, c->owner_on ? 3 : 1));
-    hipLaunchKernelGGL(k_kept_unpack, dim3(1), dim3(64), 0, c->stream, c->dred, c->iscratch);
+    LFE_TRY(allreduce_sum_f64(c, c->dred, c->owner_on ? 4 : 1));
+    hipLaunchKernelGGL(k_kept_unpack, dim3(1), dim3(64), 0, c->stream, c->dred, c->owner_on ? 1 : 0, c->iscratch);
     LFE_HIP(hipGetLastError());
   }
   int32_t h[kIscratchInts];  // dims / card per FE, dropped rows, kept sums, largest kept counts
@@ -1246,6 +1248,7 @@ int prepare_layout(lfe_ctx* c) {
   }
   c->n_kept = (int64_t)kept[0];
   c->n_kept_local = n - h[2 * kMaxFE];
+  c->cmax_over_ranks = c->world > 1 && c->owner_on ? h[kIsCmaxOver] : 0;
   return LFE_OK;
 }
 

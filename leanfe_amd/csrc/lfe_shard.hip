@@ -165,8 +165,7 @@ int reshard_owner(lfe_ctx* c, int fe, int32_t* lo_out, int32_t* hi_out) {
       short_mem = 1;
   }
   (void)hipGetLastError();  // a failed allocation is decided below, with the other ranks
-  if (const char* e = getenv("LFE_TEST_RESHARD_SHORT_RANK"))  // tests: one rank short of memory
-    if (atoi(e) == rank) short_mem = 1;
+  if (c->test_hooks & LFE_TEST_SHORT_MEMORY) short_mem = 1;  // tests: this rank short of memory
   {
     int32_t* dflag = W.ocnt;  // [world * world] is free again after the counts above
     LFE_TRY(h2d_small(c, dflag, &short_mem, sizeof(int32_t)));

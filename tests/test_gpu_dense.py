@@ -250,3 +250,38 @@ def test_dense_wide_fits(vcov, p_k, monkeypatch):
     _check(rows, o)
     np.testing.assert_allclose(dense[0], rows[0], rtol=1e-11, atol=0)
     np.testing.assert_allclose(dense[1], rows[1], rtol=1e-11, atol=0)
+
+
+def test_two_fe_column_group_sums_form_their_own_raw_gram(monkeypatch):
+    """a two-FE fit whose secondary table does not fit LDS (p = 14, G_Q = 2,000)
+    takes the column-group sums, which form no raw Gram tile; the Gram must not reuse a tile left
+    by an earlier fit on the same Engine (here a G_Q = 600 fit, whose sums do write one).  Both
+    fits against the oracle, the second also against the sums without column groups
+    (LFE_SUMS_CG=0) and repeated on the same Engine."""
+    from leanfe_amd import leanfe_hip, synth
+    from leanfe_amd._lib import Engine
+
+    k = 13
+    xs = [f"x{j + 1}" for j in range(k)]
+    first = synth.panel(600_000, k, [3_000, 600], seed=92)
+    wide = synth.panel(1_000_000, k, [6_000, 2_000], seed=93)
+
+    def fit(data, eng):
+        r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], strategy="alt_proj", vcov="HC1",
+                       quiet=True, engine=eng)
+        return (np.array([r.coefs[x] for x in xs]), np.array([r.std_errors[x] for x in xs]), r.iterations, r.n_obs,
+                r.df_resid)
+
+    o_first, o_wide = _oracle(first, xs), _oracle(wide, xs)
+    with Engine(0) as eng:
+        a = fit(first, eng)
+        b = fit(wide, eng)
+        b2 = fit(wide, eng)
+        monkeypatch.setenv("LFE_SUMS_CG", "0")
+        b_flat = fit(wide, eng)
+    _check(a, o_first)
+    _check(b, o_wide)
+    _check(b_flat, o_wide)
+    np.testing.assert_array_equal(b[0], b2[0])
+    np.testing.assert_array_equal(b[1], b2[1])
+    np.testing.assert_allclose(b[0], b_flat[0], rtol=1e-12, atol=0)

@@ -416,7 +416,7 @@ def test_emulated_contiguous_blocks_reshard_to_owners(world, n, k, levels, vcov,
 
 def test_reshard_memory_refusal_is_decided_by_every_rank(monkeypatch):
     """a re-shard refusal on one rank (here: rank 1 "short of device memory" for the
-    staging copy, LFE_TEST_RESHARD_SHORT_RANK) must be an all-rank decision taken before any row
+    staging copy, the LFE_TEST_SHORT_MEMORY hook) must be an all-rank decision taken before any row
     moves - every rank returns LFE_ENOMEM, keeps its contiguous block and the fit goes on with the
     row-block schedule, equal to the oracle and bit-identical across ranks (no rank is left inside a
     collective the others skipped)."""
@@ -428,7 +428,6 @@ def test_reshard_memory_refusal_is_decided_by_every_rank(monkeypatch):
     full = dict(synth.panel(n, k, levels, seed=31))
     xs = [f"x{j + 1}" for j in range(k)]
     monkeypatch.setattr(dist, "agree_levels", lambda eng, lv: [max(a, b) for a, b in zip(lv, levels)])
-    monkeypatch.setenv("LFE_TEST_RESHARD_SHORT_RANK", "1")
     group = EmuGroup(world)
     out, errs = {}, {}
 
@@ -438,6 +437,8 @@ def test_reshard_memory_refusal_is_decided_by_every_rank(monkeypatch):
             eng = Engine(0)
             eng.set_emu(group, rank)
             eng.dist_group = ("emulated",)
+            if rank == 1:
+                eng.test_hooks(1)  # LFE_TEST_SHORT_MEMORY
             shard = {c: np.asarray(v)[lo:hi] for c, v in full.items()}
             r = leanfe_hip(shard, y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], vcov="HC1", strategy="alt_proj",
                            quiet=True, engine=eng)
@@ -594,3 +595,68 @@ def test_emulated_owner_sharded_pair_tables(world, n, k, levels, vcov, cl, monke
             np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=0)
             np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
             np.testing.assert_array_equal(res["beta"], out[0]["first"]["beta"])
+
+
+@pytest.mark.parametrize("levels", [(20_000, 500), (6_000, 900, 150)])
+def test_unbalanced_owner_shards_take_the_same_sweeps(levels):
+    """the dense-path decision (two FEs: count tables vs row layouts; three FEs:
+    pair tables vs general sweeps) is taken from the whole panel's kept rows and largest primary
+    level (summed with the kept-row total), not each rank's own: here rank 0 holds 7/8 of the rows
+    and would take the tables alone while rank 1's shard is too sparse for them.  No LFE_DENSE
+    override: both ranks must take the same path, equal the oracle and agree bit for bit."""
+    from leanfe_amd._lib import EmuGroup, Engine
+    from leanfe_amd.dist import owner_range
+    from oracle import altproj
+
+    world, k = 2, 3
+    n = 4_000_000 if len(levels) == 2 else 3_000_000
+    rng = np.random.default_rng(44)
+    G0 = levels[0]
+    heavy = rng.random(n) < 0.875
+    fe1 = np.where(heavy, rng.integers(0, G0 // 2, n), rng.integers(G0 // 2, G0, n)).astype(np.int32)
+    codes = [fe1] + [rng.integers(0, g, n).astype(np.int32) for g in levels[1:]]
+    x = rng.standard_normal((n, k))
+    y = x @ np.array([1.0, -0.5, 0.25]) + sum(rng.standard_normal(g)[c] for g, c in zip(levels, codes)) + \
+        rng.standard_normal(n)
+    data = {"y": y, **{f"x{j + 1}": x[:, j].copy() for j in range(k)},
+            **{f"fe{f + 1}": c for f, c in enumerate(codes)}}
+    group = EmuGroup(world)
+    out, errs = {}, {}
+
+    def worker(rank):
+        try:
+            lo, hi = owner_range(G0, rank, world)
+            sel = (fe1 >= lo) & (fe1 < hi)
+            eng = Engine(0)
+            eng.set_emu(group, rank)
+            eng.load([y[sel]] + [x[sel, j].copy() for j in range(k)], [c[sel] for c in codes], list(levels))
+            eng.set_owner(0, lo, hi)
+            res = _solve(eng, "HC1", None)
+            res["cells"] = eng.dense_cells()
+            res["rows"] = int(sel.sum())
+            out[rank] = res
+            eng.close()
+        except BaseException as e:  # noqa: BLE001
+            errs[rank] = e
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+    if errs:
+        raise next(iter(errs.values()))
+    assert out[0]["rows"] > 5 * out[1]["rows"]
+    assert (out[0]["cells"] > 0) == (out[1]["cells"] > 0)
+    assert out[0]["cells"] > 0  # the whole panel is dense enough for the tables
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    o = altproj.fit(data, "y", xs, fes, vcov="HC1")
+    for r in range(world):
+        res = out[r]
+        assert res["iterations"] == o["iterations"] and res["n_obs"] == o["n_obs"]
+        np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=0)
+        np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(res["beta"], out[0]["beta"])
+        np.testing.assert_array_equal(res["se"], out[0]["se"])

@@ -277,3 +277,60 @@ def test_float_order_keys_preserve_np_unique_order():
     uv, iv = np.unique(v, return_inverse=True)
     assert uk.size == uv.size
     np.testing.assert_array_equal(ik.ravel(), iv.ravel())
+
+
+# ---------------------------------------------------------------- stream discipline (source check)
+# Round 4 found a race in the emulated collectives: a null-stream hipMemcpy is not ordered against
+# a context's non-blocking stream, so a kernel read an all-to-all block before it landed.
+# Every device copy, fill, kernel launch and RCCL call of the engine therefore goes on the context's
+# own stream (the work-item upload on its side stream, joined by events); synchronous null-stream
+# copies are allowed only in the opt-in timing diagnostics that read their stamps after a sync.
+
+_STREAM_CALLS = re.compile(r"\b(hipMemcpyAsync|hipMemsetAsync|hipMemcpy|hipMemset|hipLaunchKernelGGL|hipLaunchKernel|"
+                           r"ncclAllReduce|ncclSend|ncclRecv|ncclBroadcast|ncclAllGather|ncclReduceScatter)\s*\(")
+_DIAG_SYNC_OK = {"lfe_dense.hip": 5, "lfe_iter.hip": 1}  # LFE_DN8_TIMING / LFE_SWEEP_TIMING stamps
+
+
+def _call_args(src, i):
+    depth, cur, out = 0, "", []
+    for ch in src[i:]:
+        if ch == "(":
+            depth += 1
+            if depth == 1:
+                continue
+        elif ch == ")":
+            depth -= 1
+            if depth == 0:
+                out.append(cur.strip())
+                return out
+        if ch == "," and depth == 1:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    raise AssertionError("unbalanced call")
+
+
+def test_every_device_operation_is_issued_on_the_context_stream():
+    import glob
+
+    sync_calls = {}
+    checked = 0
+    for path in sorted(glob.glob(os.path.join(ROOT, "leanfe_amd", "csrc", "*.hip"))):
+        src = open(path).read()
+        name = os.path.basename(path)
+        for m in _STREAM_CALLS.finditer(src):
+            fn = m.group(1)
+            args = _call_args(src, m.end() - 1)
+            line = src.count("\n", 0, m.start()) + 1
+            if fn in ("hipMemcpy", "hipMemset"):
+                sync_calls[name] = sync_calls.get(name, 0) + 1
+                continue
+            stream = args[4] if fn == "hipLaunchKernelGGL" else args[-1]
+            if fn == "hipLaunchKernelGGL" and stream == "s":  # the one helper that takes its stream
+                continue
+            ok = {"c->stream"} | ({"c->up_stream"} if fn == "hipMemcpyAsync" else set())
+            assert stream in ok, f"{name}:{line}: {fn} on '{stream}', not the context stream"
+            checked += 1
+    assert checked > 250
+    assert sync_calls == _DIAG_SYNC_OK, sync_calls

@@ -13,7 +13,7 @@ timeout -k 10 300 python bench.py --no-cpu --no-h2d --steps 20 --warmup 5 > $out
 tail -1 $out/headline.log >> $out/lines.jsonl
 echo "headline ok"
 for p in "${list[@]}"; do
-  timeout -k 10 300 python bench.py --no-cpu --no-h2d --steps 10 --warmup 3 --preset $p > $out/$p.log 2>&1 \
+  timeout -k 10 300 python bench.py --no-h2d --steps 10 --warmup 3 --preset $p > $out/$p.log 2>&1 \
     || { tail -5 $out/$p.log; exit 1; }
   tail -1 $out/$p.log >> $out/lines.jsonl
   echo "$p ok"
