@@ -50,12 +50,15 @@ void lfe_ctx_destroy(lfe_ctx* ctx);
 int lfe_comm_unique_id(void* out128);
 int lfe_ctx_set_comm(lfe_ctx* ctx, const void* unique_id128, int rank, int world);
 
-/* Testing the multi-rank paths on one GPU: an in-process emulated group of `world`
- * contexts (each driven by its own host thread) whose all-reduces go through host
- * memory behind a barrier, in the same order as with RCCL. */
+/* An in-process group of `world` contexts (each driven by its own host thread) whose
+ * collectives go through host memory behind a barrier, in the same order as with RCCL: the
+ * multi-rank paths tested on one GPU, and a fit of more rows than one context holds (< 2^31
+ * rows per context) as several contexts on one device.  lfe_emu_abort (a member failed): every
+ * collective waiting in the group, and every later one, returns LFE_ESTATE. */
 typedef struct lfe_emu lfe_emu;
 int lfe_emu_create(int world, lfe_emu** out);
 void lfe_emu_destroy(lfe_emu* emu);
+void lfe_emu_abort(lfe_emu* emu);
 int lfe_ctx_set_emu(lfe_ctx* ctx, lfe_emu* emu, int rank);
 
 /* Upload one row shard.  cols[0] = y, cols[1..p-1] = x (then instruments),
@@ -271,6 +274,11 @@ int lfe_stream_cluster_meats(lfe_ctx* ctx, double* meats_out, int64_t* G_out);
 /* Benchmark / test helpers: lfe_synth_load's panel with only the codes resident, and one chunk
  * of its columns generated on the device and streamed through the current pass. */
 int lfe_synth_load_codes(lfe_ctx* ctx, int64_t n, int k, int n_fe, const int32_t* n_levels, uint64_t seed);
+/* The same for rows [row0, row0 + n) of the panel (lfe_stream_synth_rows then generates rows
+ * row0 + r): one context of several on one device, each under 2^31 rows, joined in a group
+ * (a fit of more rows than one context holds). */
+int lfe_synth_load_codes_at(lfe_ctx* ctx, int64_t n, int64_t row0, int k, int n_fe, const int32_t* n_levels,
+                            uint64_t seed);
 int lfe_stream_synth_rows(lfe_ctx* ctx, int64_t row0, int64_t rows, int k, const int32_t* n_levels,
                           const double* beta, uint64_t seed);
 

@@ -35,6 +35,7 @@ SIGNATURES = {
     "lfe_ctx_set_comm": (C.c_int, [_vp, _vp, C.c_int, C.c_int]),
     "lfe_emu_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
     "lfe_emu_destroy": (None, [_vp]),
+    "lfe_emu_abort": (None, [_vp]),
     "lfe_ctx_set_emu": (C.c_int, [_vp, _vp, C.c_int]),
     "lfe_load": (C.c_int, [_vp, C.c_int64, C.c_int, C.POINTER(_vp), C.c_int, C.POINTER(_vp), _i32p, _vp, C.c_int]),
     "lfe_load_begin": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, _i32p, C.c_int]),
@@ -63,6 +64,7 @@ SIGNATURES = {
     "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
     "lfe_dense_cells": (C.c_int, [_vp, _i64p]),
     "lfe_ctx_test_hooks": (C.c_int, [_vp, C.c_int]),
+    "lfe_synth_load_codes_at": (C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int, C.c_int, _i32p, C.c_uint64]),
     "lfe_dense_cell_bytes": (C.c_int, [_vp, C.POINTER(C.c_int32)]),
     "lfe_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.POINTER(_vp), _i32p, _dp, C.c_int]),
     "lfe_stream_clusters": (C.c_int, [_vp, C.c_int, _i32p]),
@@ -481,9 +483,12 @@ class Engine:
         _check(self._lib.lfe_stream_end(self._h, out.ctypes.data_as(C.POINTER(C.c_double))))
         return out
 
-    def synth_load_codes(self, n: int, k: int, levels: list[int], seed: int = 12345) -> None:
+    def synth_load_codes(self, n: int, k: int, levels: list[int], seed: int = 12345, row0: int = 0) -> None:
+        """Codes of rows [row0, row0 + n) of the synthetic panel (lfe_synth_load_codes_at); the
+        columns come later, generated chunk by chunk (stream_synth_pass)."""
         lv = (C.c_int32 * len(levels))(*[int(g) for g in levels])
-        _check(self._lib.lfe_synth_load_codes(self._h, int(n), int(k), len(levels), lv, C.c_uint64(seed)))
+        _check(self._lib.lfe_synth_load_codes_at(self._h, int(n), int(row0), int(k), len(levels), lv,
+                                                 C.c_uint64(seed)))
         self.p, self.F, self.n = int(k) + 1, len(levels), int(n)
         self.owner = None
 
@@ -560,15 +565,35 @@ def version() -> str:
 
 
 class EmuGroup:
-    """In-process emulated communicator of `world` contexts (lfe_emu_create): each
-    context must be driven by its own thread; all-reduces meet at a host barrier."""
+    """In-process group of `world` contexts (lfe_emu_create): each context is driven by its own
+    thread and the engine's collectives meet at a host barrier.  Used by the tests' emulated ranks
+    and by a fit of more rows than one context holds (< 2^31 per context: several contexts on one
+    device, hip_impl._out_of_core_split).  ``exchange`` is the host-side all-gather those threads
+    use for the level counts and factor categories they must agree on."""
 
     def __init__(self, world: int):
+        import threading
+
         self._lib = load_library()
         h = _vp()
         _check(self._lib.lfe_emu_create(int(world), C.byref(h)))
         self.handle = h
         self.world = world
+        self._barrier = threading.Barrier(int(world))
+        self._slots = [None] * int(world)
+
+    def abort(self) -> None:
+        """A member failed: the others' waiting and later collectives fail instead of waiting."""
+        self._lib.lfe_emu_abort(self.handle)
+        self._barrier.abort()
+
+    def exchange(self, rank: int, obj):
+        """Every member's ``obj``, in rank order (all members call it, each from its thread)."""
+        self._slots[rank] = obj
+        self._barrier.wait()
+        out = list(self._slots)
+        self._barrier.wait()  # every member has read the slots before they are reused
+        return out
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -195,16 +195,19 @@ struct lfe_emu {
   // all-to-all: every rank publishes its device send buffer and per-peer blocks
   std::vector<const char*> a2a_send;
   std::vector<std::vector<size_t>> a2a_off, a2a_bytes;
-  void barrier() {
+  bool aborted = false;  // lfe_emu_abort: a member failed; every waiting and later barrier fails
+  bool barrier() {
     std::unique_lock<std::mutex> lk(m);
+    if (aborted) return false;
     const int64_t gen = generation;
     if (++arrived == world) {
       arrived = 0;
       ++generation;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return generation != gen; });
+      cv.wait(lk, [&] { return generation != gen || aborted; });
     }
+    return !aborted;
   }
 };
 
@@ -223,7 +226,7 @@ static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
   // before a host-to-device copy lands)
   LFE_HIP(hipMemcpyAsync(e->slots[c->rank].data(), dev, bytes, hipMemcpyDeviceToHost, c->stream));
   LFE_HIP(hipStreamSynchronize(c->stream));
-  e->barrier();
+  if (!e->barrier()) return fail(LFE_ESTATE, "group aborted by a member");
   if (c->rank == 0) {  // fixed rank order: deterministic
     e->result = e->slots[0];
     for (int r = 1; r < e->world; ++r)
@@ -240,10 +243,10 @@ static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
         }
       }
   }
-  e->barrier();
+  if (!e->barrier()) return fail(LFE_ESTATE, "group aborted by a member");
   LFE_HIP(hipMemcpyAsync(dev, e->result.data(), bytes, hipMemcpyHostToDevice, c->stream));
   LFE_HIP(hipStreamSynchronize(c->stream));
-  e->barrier();  // every rank has its copy before the result buffer is reused
+  if (!e->barrier()) return fail(LFE_ESTATE, "group aborted by a member");  // copies done before reuse
   return LFE_OK;
 }
 
@@ -270,7 +273,7 @@ int alltoallv_bytes(lfe_ctx* c, const char* send, const size_t* send_off, const 
       e->a2a_off[c->rank].assign(send_off, send_off + W);
       e->a2a_bytes[c->rank].assign(send_bytes, send_bytes + W);
     }
-    e->barrier();
+    if (!e->barrier()) return fail(LFE_ESTATE, "group aborted by a member");
     for (int q = 0; q < W; ++q) {
       const size_t b = e->a2a_bytes[q][c->rank];
       if (b != recv_bytes[q]) return fail(LFE_EINVAL, "alltoallv: peer block size mismatch");
@@ -280,7 +283,7 @@ int alltoallv_bytes(lfe_ctx* c, const char* send, const size_t* send_off, const 
     // the copies complete before the peers go on (a plain device-to-device hipMemcpy may return
     // before its copy is done, and runs on the null stream, unordered with this context's stream)
     LFE_HIP(hipStreamSynchronize(c->stream));
-    e->barrier();  // every peer has read this rank's buffer
+    if (!e->barrier()) return fail(LFE_ESTATE, "group aborted by a member");  // peers read this buffer
     return LFE_OK;
   }
   LFE_NCCL(ncclGroupStart());
@@ -705,6 +708,13 @@ int lfe_emu_create(int world, lfe_emu** out) {
 
 void lfe_emu_destroy(lfe_emu* e) { delete e; }
 
+void lfe_emu_abort(lfe_emu* e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> lk(e->m);
+  e->aborted = true;
+  e->cv.notify_all();
+}
+
 int lfe_ctx_set_emu(lfe_ctx* c, lfe_emu* e, int rank) {
   LFE_CTX(c);
   if (!e || rank < 0 || rank >= e->world) return fail(LFE_EINVAL, "bad emulated group / rank");
@@ -857,14 +867,21 @@ int lfe_stream_rows(lfe_ctx* c, int64_t row0, int64_t rows, const double* const*
 
 // benchmark / test helpers: the synthetic panel of lfe_synth_load with the codes resident and
 // the columns generated chunk by chunk on the device (no host copy of data larger than HBM)
-int lfe_synth_load_codes(lfe_ctx* c, int64_t n, int k, int n_fe, const int32_t* n_levels, uint64_t seed) {
+int lfe_synth_load_codes_at(lfe_ctx* c, int64_t n, int64_t row0, int k, int n_fe, const int32_t* n_levels,
+                            uint64_t seed) {
   LFE_CTX(c);
   if (n_fe < 1 || n_fe > kMaxFE || !n_levels) return fail(LFE_EINVAL, "streamed X needs 1 to 8 fixed effects");
   if (k < 1 || k + 1 > kMaxCols) return fail(LFE_EINVAL, "k out of range");
+  if (row0 < 0) return fail(LFE_EINVAL, "row0 must be >= 0");
   LFE_TRY(alloc_data(c, n, k + 1, n_fe, n_levels, false, true));
-  LFE_TRY(synth_codes(c, n_levels, seed));
+  LFE_TRY(synth_codes(c, n_levels, seed, row0));
+  c->synth_row0 = row0;
   c->loaded = true;
   return LFE_OK;
+}
+
+int lfe_synth_load_codes(lfe_ctx* c, int64_t n, int k, int n_fe, const int32_t* n_levels, uint64_t seed) {
+  return lfe_synth_load_codes_at(c, n, 0, k, n_fe, n_levels, seed);
 }
 
 int lfe_stream_synth_rows(lfe_ctx* c, int64_t row0, int64_t rows, int k, const int32_t* n_levels,
@@ -877,7 +894,7 @@ int lfe_stream_synth_rows(lfe_ctx* c, int64_t row0, int64_t rows, int k, const i
   if (rows == 0) return LFE_OK;
   const int64_t cld = (rows + 63) / 64 * 64;
   LFE_TRY(ensure_f64(c, w.x, w.x_cap, (size_t)c->p * cld));
-  LFE_TRY(synth_chunk(c, k, n_levels, beta, seed, row0, rows, w.x, cld));
+  LFE_TRY(synth_chunk(c, k, n_levels, beta, seed, c->synth_row0 + row0, rows, w.x, cld));
   LFE_TRY(stream_chunk(c, cld, row0, rows));
   return LFE_OK;
 }

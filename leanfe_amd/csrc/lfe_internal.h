@@ -375,7 +375,8 @@ struct lfe_ctx {
   int owner_fe = -1;
   int32_t owner_lo = 0, owner_hi = 0;
   bool owner_on = false;
-  int test_hooks = 0;  // lfe_ctx_test_hooks (LFE_TEST_* bits; tests only, 0 in production)
+  int test_hooks = 0;
+  int64_t synth_row0 = 0;  // lfe_synth_load_codes_at: the synthetic panel's global index of row 0  // lfe_ctx_test_hooks (LFE_TEST_* bits; tests only, 0 in production)
   // deterministic T_Q: per-(bucket, q) run sums reduced in bucket order (no cross-bucket atomics)
   double* tq_runs = nullptr;     // [nb * G_Q][p]
   size_t tq_runs_cap = 0;
@@ -539,7 +540,7 @@ int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* fl
 // --- synthetic panel (lfe_synth.hip) ---
 int synth_chunk(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed, int64_t row0,
                 int64_t rows, double* X, int64_t ld);
-int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed);
+int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed, int64_t row0);
 int launch_synth(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed,
                  int64_t row_offset);
 // owner-sharded synthetic shard: count the rows of [0, n_total) whose code of FE f is in [lo, hi)

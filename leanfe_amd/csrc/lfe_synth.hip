@@ -185,7 +185,7 @@ int synth_chunk(lfe_ctx* c, int k, const int32_t* levels, const double* beta, ui
   return LFE_OK;
 }
 
-int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed) {
+int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed, int64_t row0) {
   SynthArgs a{};
   a.F = c->F;
   a.k = 0;
@@ -195,7 +195,7 @@ int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed) {
   }
   if (c->n)
     hipLaunchKernelGGL(k_synth_rows, dim3(grid_for(c->n, kBlock, 256 * 16)), dim3(kBlock), 0, c->stream, a,
-                       static_cast<double*>(nullptr), c->ld, c->n, seed, (int64_t)0, nullptr);
+                       static_cast<double*>(nullptr), c->ld, c->n, seed, row0, nullptr);
   LFE_HIP(hipGetLastError());
   LFE_HIP(hipStreamSynchronize(c->stream));
   return LFE_OK;

@@ -82,12 +82,35 @@ def agree_levels(engine, levels: list[int]) -> list[int]:
     every rank."""
     if not is_sharded(engine) or not levels:
         return list(levels)
+    if engine.dist_group[0] == "local":  # contexts of one process (EmuGroup): a host all-gather
+        _, group, rank = engine.dist_group
+        return [max(v) for v in zip(*group.exchange(rank, [int(g) for g in levels]))]
     import torch
     import torch.distributed as dist
 
     t = torch.tensor([int(g) for g in levels], dtype=torch.int64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=engine.dist_group[0])
     return [int(g) for g in t.tolist()]
+
+
+def agree_categories(engine, cats):
+    """The sorted union over the ranks of ``engine``'s group of each rank's categories of a factor
+    column (a row shard may miss some): every rank then expands ``i(var)`` / ``var:i(f)`` into the
+    same dummy columns, in the same order (polars_impl.py:27-115 on the whole column)."""
+    import numpy as np
+
+    cats = np.unique(np.asarray(cats))
+    if not is_sharded(engine):
+        return cats
+    if engine.dist_group[0] == "local":
+        _, group, rank = engine.dist_group
+        return np.unique(np.concatenate(group.exchange(rank, cats)))
+    import torch.distributed as dist
+
+    group = engine.dist_group[0]
+    parts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(parts, cats.tolist(), group=group)
+    return np.unique(np.concatenate([np.asarray(p_, dtype=cats.dtype) for p_ in parts]))
 
 
 class HostGroup:

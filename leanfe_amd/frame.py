@@ -50,16 +50,38 @@ def parquet_rows(path: str) -> int:
     return int(pq.ParquetFile(path).metadata.num_rows)
 
 
-def stream_parquet(path: str, names: list[str], batch_rows: int = 1 << 22):
+def stream_parquet(path: str, names: list[str], batch_rows: int = 1 << 22, row_range=None):
     """Yield (row0, {name: ndarray}) batches of a Parquet file's columns, in file order
     (the streaming counterpart of ``pl.scan_parquet``, polars_impl.py:341-343): one
-    batch is decoded while the previous one is uploaded."""
+    batch is decoded while the previous one is uploaded.  ``row_range`` (lo, hi): only
+    those rows, from the row groups that hold them, with row0 counted from lo."""
     import pyarrow.parquet as pq
+    pf = pq.ParquetFile(path)
+    groups, skip, lo, hi = None, 0, 0, None
+    if row_range is not None:
+        lo, hi = (int(x) for x in row_range)
+        groups, start = [], 0
+        for g in range(pf.metadata.num_row_groups):
+            end = start + pf.metadata.row_group(g).num_rows
+            if end > lo and start < hi:
+                if not groups:
+                    skip = lo - start
+                groups.append(g)
+            start = end
     row0 = 0
-    for rb in pq.ParquetFile(path).iter_batches(batch_size=int(batch_rows), columns=list(names)):
-        out = {c: _arrow_to_numpy(rb.column(c)) for c in names}
+    for rb in pf.iter_batches(batch_size=int(batch_rows), columns=list(names), row_groups=groups):
+        a, b = 0, rb.num_rows
+        if row_range is not None:
+            a = min(skip, b)
+            skip -= a
+            b = min(b, a + (hi - lo) - row0)
+            if b <= a:
+                if row0 >= hi - lo:
+                    break
+                continue
+        out = {c: _arrow_to_numpy(rb.column(c).slice(a, b - a)) for c in names}
         yield row0, out
-        row0 += rb.num_rows
+        row0 += b - a
 
 
 def _arrow_to_numpy(col) -> np.ndarray:
@@ -211,35 +233,62 @@ def _coerce_ref(ref, categories):
     return ref
 
 
-def expand_interactions(cols: dict[str, np.ndarray], interactions) -> list[str]:
+class Expansion:
+    """The dummy columns a formula's ``var:i(factor)`` and ``i(var)`` terms expand into
+    (polars_impl.py:27-115), planned once from the whole factor columns and applied to any row
+    range, so that a streamed (out-of-core) fit expands each chunk as it arrives, as the
+    reference expands its scanned LazyFrame lazily (polars_impl.py:342-365).
+
+    ``terms``: (name, var or None, factor, category) in the reference's column order (the
+    interactions' columns, then the factors'); ``var`` None is a plain dummy."""
+
+    def __init__(self, factors: dict[str, np.ndarray], interactions, factor_vars, unique=np.unique):
+        self.terms = []
+        for var, factor, ref in interactions:
+            for cat in _categories(unique(factors[factor]), ref, factor):
+                self.terms.append((f"{var}_{cat}", var, factor, cat))
+        for var, ref in factor_vars:
+            for cat in _categories(unique(factors[var]), ref, var):
+                self.terms.append((f"{var}_{cat}", None, var, cat))
+
+    @property
+    def names(self) -> list[str]:
+        return [t[0] for t in self.terms]
+
+    @property
+    def numeric_sources(self) -> list[str]:
+        """The numeric columns the interaction terms multiply (streamed with the chunks)."""
+        return list(dict.fromkeys(t[1] for t in self.terms if t[1] is not None))
+
+    def columns(self, factors: dict[str, np.ndarray], values: dict[str, np.ndarray], rows: slice | None = None):
+        """The expanded columns for one row range: ``factors`` hold the whole factor columns
+        (sliced by ``rows``), ``values`` the interactions' numeric columns of that range."""
+        sl = rows if rows is not None else slice(None)
+        out = []
+        for _, var, factor, cat in self.terms:
+            hit = np.asarray(factors[factor])[sl] == cat
+            out.append(np.asarray(values[var], dtype=np.float64) * hit if var is not None else hit.astype(np.float64))
+        return out
+
+
+def _categories(cats, ref, name):
+    ref_cat = _coerce_ref(ref, cats)
+    if ref_cat not in cats:
+        raise ValueError(f"Reference category '{ref}' not found in {name}. Available: {list(cats)}")
+    return [cat for cat in cats if cat != ref_cat]
+
+
+def expand_interactions(cols: dict[str, np.ndarray], interactions, unique=np.unique) -> list[str]:
     """``var:i(factor)`` -> var * (factor == cat) for cat != ref (polars_impl.py:72-115)."""
-    names = []
-    for var, factor, ref in interactions:
-        cats = np.unique(cols[factor])
-        ref_cat = _coerce_ref(ref, cats)
-        if ref_cat not in cats:
-            raise ValueError(f"Reference category '{ref}' not found in {factor}. Available: {list(cats)}")
-        for cat in cats:
-            if cat == ref_cat:
-                continue
-            name = f"{var}_{cat}"
-            cols[name] = np.asarray(cols[var], dtype=np.float64) * (cols[factor] == cat)
-            names.append(name)
-    return names
+    plan = Expansion(cols, interactions, [], unique)
+    for name, col in zip(plan.names, plan.columns(cols, cols)):
+        cols[name] = col
+    return plan.names
 
 
-def expand_factors(cols: dict[str, np.ndarray], factor_vars) -> list[str]:
+def expand_factors(cols: dict[str, np.ndarray], factor_vars, unique=np.unique) -> list[str]:
     """``i(var)`` -> dummies (var == cat) for cat != ref (polars_impl.py:27-69)."""
-    names = []
-    for var, ref in factor_vars:
-        cats = np.unique(cols[var])
-        ref_cat = _coerce_ref(ref, cats)
-        if ref_cat not in cats:
-            raise ValueError(f"Reference category '{ref}' not found in {var}. Available: {list(cats)}")
-        for cat in cats:
-            if cat == ref_cat:
-                continue
-            name = f"{var}_{cat}"
-            cols[name] = (cols[var] == cat).astype(np.float64)
-            names.append(name)
-    return names
+    plan = Expansion(cols, [], factor_vars, unique)
+    for name, col in zip(plan.names, plan.columns(cols, cols)):
+        cols[name] = col
+    return plan.names

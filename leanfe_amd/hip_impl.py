@@ -46,7 +46,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     in ``chunk_rows`` row chunks through the group sums, (if needed) the design Gram and the
     residual pass.  Any number of FEs and regressors, weights, IV, IID / HC1 /
     one-way and multi-way clustered SEs, one process or a sharded engine; factor and interaction
-    terms must be expanded into columns first."""
+    terms are expanded chunk by chunk as the columns stream (frame.Expansion)."""
     t_start = time.perf_counter()
     say = (lambda *a: None) if quiet else print
     if formula is not None:
@@ -76,27 +76,40 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     # a Parquet path streams: the FE / cluster / weight columns are read first (for the codes),
     # then [y] + x + instruments are decoded batch by batch while earlier batches upload
     # (pl.scan_parquet's role, polars_impl.py:341-343)
-    stream = (isinstance(data, str) and not factor_vars and not interactions and sample_frac is None
+    if out_of_core is None:
+        out_of_core = os.environ.get("LEANFE_HIP_OUT_OF_CORE", "0") == "1"
+    expand = bool(factor_vars or interactions)
+    # (a resident fit expands factor / interaction terms on whole columns; an out-of-core fit per chunk)
+    stream = (isinstance(data, str) and (out_of_core or not expand) and sample_frac is None
               and os.environ.get("LEANFE_HIP_STREAM", "1") != "0")
-    num_cols = [y_col] + x_cols + instruments  # the columns leanfe demeans (polars_impl.py:486)
+    factor_src = [var for var, _ in factor_vars] + [fac for _, fac, _ in interactions]
     if stream:
-        small = list(dict.fromkeys(fe_cols + list(cluster_cols or []) + ([weights] if weights else [])))
+        small = list(dict.fromkeys(fe_cols + list(cluster_cols or []) + ([weights] if weights else []) + factor_src))
         cols = frame.get_columns(data, small) if small else {}
         n_rows = frame.parquet_rows(data)
     else:
         cols = frame.get_columns(data, needed)
 
-    if interactions:
-        x_cols = x_cols + frame.expand_interactions(cols, interactions)
-    if sample_frac is not None:
-        n0 = len(cols[y_col])
-        idx = np.sort(np.random.default_rng(42).choice(n0, size=int(round(n0 * sample_frac)), replace=False))
-        cols = {c: np.asarray(a)[idx] for c, a in cols.items()}
-    if factor_vars:
-        x_cols = x_cols + frame.expand_factors(cols, factor_vars)
+    plan, x_base = None, list(x_cols)
+    sharded = engine is not None and dist.is_sharded(engine)
+    # a row shard's categories are agreed over the ranks (every rank expands the same columns)
+    unique = (lambda v: dist.agree_categories(engine, v)) if sharded else np.unique
+    if out_of_core and expand and sample_frac is None:
+        # planned on the whole factor columns, applied to each streamed chunk (polars_impl.py:342-365)
+        plan = frame.Expansion(cols, interactions, factor_vars, unique)
+        x_cols = x_cols + plan.names
+    else:
+        if interactions:
+            x_cols = x_cols + frame.expand_interactions(cols, interactions, unique)
+        if sample_frac is not None:
+            n0 = len(cols[y_col])
+            idx = np.sort(np.random.default_rng(42).choice(n0, size=int(round(n0 * sample_frac)), replace=False))
+            cols = {c: np.asarray(a)[idx] for c, a in cols.items()}
+        if factor_vars:
+            x_cols = x_cols + frame.expand_factors(cols, factor_vars, unique)
+    num_cols = [y_col] + x_cols + instruments  # the columns leanfe demeans (polars_impl.py:486)
 
     own_engine = engine is None
-    sharded = engine is not None and dist.is_sharded(engine)
     eng = engine if engine is not None else Engine(_default_device() if device is None else device)
     try:
         # FE codes (polars_impl.py:118-139); sparse integer ids are factorized on the GPU
@@ -106,18 +119,21 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             codes.append(c)
             levels.append(g)
         levels = dist.agree_levels(eng, levels)
-        if out_of_core is None:
-            out_of_core = os.environ.get("LEANFE_HIP_OUT_OF_CORE", "0") == "1"
         if out_of_core:
-            if not fe_cols or factor_vars or interactions or strategy not in ("auto", "alt_proj", "demean"):
-                raise ValueError("out_of_core fits take one or more FEs, no factor / interaction terms, and "
-                                 "strategy 'alt_proj' (or 'demean' for one FE)")
+            if not fe_cols or strategy not in ("auto", "alt_proj", "demean"):
+                raise ValueError("out_of_core fits take one or more FEs and strategy 'alt_proj' (or 'demean' for "
+                                 "one FE)")
             source = data if stream else cols
             n_rows_oc = n_rows if stream else len(cols[y_col])
             w_oc = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
-            return _out_of_core_fit(eng, source, cols, n_rows_oc, y_col, x_cols, instruments, fe_cols, codes, levels,
-                                    w_oc, cluster_cols, v, vcov, ssc, demean_tol, max_iter, int(chunk_rows),
-                                    formula, t_start, say, sharded)
+            args = (source, cols, n_rows_oc, y_col, x_cols, instruments, fe_cols, codes, levels, w_oc, cluster_cols,
+                    v, vcov, ssc, demean_tol, max_iter, int(chunk_rows), formula, t_start, say)
+            if not sharded and n_rows_oc > context_rows():
+                # more rows than one context holds: contexts of < 2^31 rows on this device, joined in
+                # one in-process group (the same collectives as row shards on several GPUs)
+                dev = eng.device if own_engine else getattr(eng, "device", _default_device())
+                return _out_of_core_split(dev, args, plan, x_base)
+            return _out_of_core_fit(eng, *args, sharded, plan, x_base)
         w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
         # polars_impl.py:180: an all-ones instrument stops 2SLS from adding an intercept to Z.
         # Demeaned instruments cannot be all ones; without FEs they are the raw columns.
@@ -272,9 +288,66 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                         rss=rss, tss=tss, backend="hip", timings=timings)
 
 
+def context_rows() -> int:
+    """Rows one engine context holds (its row indices are int32; LEANFE_HIP_CONTEXT_ROWS lowers
+    it, e.g. for tests of the multi-context split at small sizes)."""
+    cap = (1 << 31) - 64
+    return max(1, min(cap, int(os.environ.get("LEANFE_HIP_CONTEXT_ROWS", cap))))
+
+
+def _out_of_core_split(device, args, plan, x_base) -> LeanFEResult:
+    """An out-of-core fit of more rows than one context holds: the rows are cut
+    into S = ceil(n / context_rows()) contiguous blocks, each a context on the same device driven by
+    its own thread and joined in an in-process group (EmuGroup), so that the fit runs the row-shard
+    schedule of several GPUs - all-reduced group sums, cross terms, Gram and SE statistics, cluster
+    scores to owner contexts - and every context returns the same global result.  FE codes are
+    global already; cluster columns are factorized here over all rows."""
+    import threading
+
+    from ._lib import EmuGroup
+
+    (source, cols, n_rows, y_col, x_cols, instruments, fe_cols, codes, levels, w, cluster_cols, v, vcov, ssc,
+     demean_tol, max_iter, chunk_rows, formula, t_start, say) = args
+    S = -(-n_rows // context_rows())
+    say(f"{n_rows:_} rows: {S} engine contexts on device {device}")
+    group = EmuGroup(S)
+    cl = {c: frame.factorize(cols[c])[0] for c in (cluster_cols or [])}
+    out, errs = [None] * S, []
+
+    def work(r):
+        lo, hi = dist.shard_range(n_rows, r, S)
+        eng = None
+        try:
+            eng = Engine(device)
+            eng.set_emu(group, r)
+            eng.dist_group = ("local", group, r)
+            sub = {c: np.asarray(a)[lo:hi] for c, a in cols.items()}
+            sub.update({c: a[lo:hi] for c, a in cl.items()})
+            src = source if isinstance(source, str) else sub
+            out[r] = _out_of_core_fit(eng, src, sub, hi - lo, y_col, x_cols, instruments, fe_cols,
+                                      [c[lo:hi] for c in codes], levels, None if w is None else w[lo:hi],
+                                      cluster_cols, v, vcov, ssc, demean_tol, max_iter, chunk_rows, formula, t_start,
+                                      say if r == 0 else (lambda *a_: None), True, plan, x_base, (lo, hi))
+        except BaseException as e:  # noqa: BLE001 - the others must not wait for this member
+            errs.append(e)
+            group.abort()
+        finally:
+            if eng is not None:
+                eng.close()
+
+    threads = [threading.Thread(target=work, args=(r,)) for r in range(S)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errs:
+        raise errs[0]
+    return out[0]
+
+
 def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_cols, codes, levels, w, cluster_cols,
                      v, vcov, ssc, demean_tol, max_iter, chunk_rows, formula, t_start, say,
-                     sharded=False) -> LeanFEResult:
+                     sharded=False, plan=None, x_base=None, row_range=None) -> LeanFEResult:
     """Out-of-core X (data larger than HBM): the FE codes (and weights, cluster codes) and their
     layouts stay on the GPU, the columns [y] + x (+ instruments) are streamed from host memory (or a
     Parquet file, re-read per pass) in row chunks through pass 1 (group sums S_f, W_f,
@@ -284,20 +357,32 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
     RSS, the HC1 meat and the cluster scores, :229, std_errors.py:183-602).  Same estimator, same
     stop rule and iterations as the resident fit.  A sharded engine streams this rank's rows; the
     group sums, Gram tiles and SE statistics are all-reduced, and the per-cluster score sums go to
-    their owner ranks (lfe_stream.hip), so cluster columns must hold global codes."""
+    their owner ranks (lfe_stream.hip), so cluster columns must hold global codes (``row_range``: this
+    context's rows of a Parquet source, _out_of_core_split).  ``plan``
+    (frame.Expansion): the factor / interaction columns of x_cols (after ``x_base``) are formed
+    per chunk from the whole factor columns in ``cols`` and the chunk's numeric columns."""
     from leanfe_amd._lib import NeedsStreamPass
 
     num_cols = [y_col] + list(x_cols) + list(instruments)
     p, k, mz = len(num_cols), len(x_cols), len(instruments)
     say("Using FWL/alternating projections strategy (out-of-core columns)...")
+    base = [y_col] + list(x_cols if plan is None else x_base)
+    read = list(dict.fromkeys(base + (plan.numeric_sources if plan else []) + list(instruments)))
+
+    def assemble(b, rows):
+        out = [np.asarray(b[c], dtype=np.float64) for c in base]
+        if plan is not None:
+            out += plan.columns(cols, b, rows)
+        return out + [np.asarray(b[z], dtype=np.float64) for z in instruments]
 
     def chunks():
         if isinstance(source, str):
-            for row0, b in frame.stream_parquet(source, num_cols, batch_rows=chunk_rows):
-                yield row0, [b[c] for c in num_cols]
+            for row0, b in frame.stream_parquet(source, read, batch_rows=chunk_rows, row_range=row_range):
+                yield row0, assemble(b, slice(row0, row0 + len(b[y_col])))
         else:
             for r0 in range(0, n_rows, chunk_rows):
-                yield r0, [np.asarray(source[c][r0:r0 + chunk_rows], dtype=np.float64) for c in num_cols]
+                b = {c: source[c][r0:r0 + chunk_rows] for c in read}
+                yield r0, assemble(b, slice(r0, r0 + len(b[y_col])))
 
     t0 = time.perf_counter()
     eng.load_codes(codes, levels, p, weights=w)  # a sharded engine: this rank's rows (global codes)

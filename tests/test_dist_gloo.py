@@ -70,6 +70,23 @@ def _entry(rank, port, q, fn, args):
 # plumbing
 # ---------------------------------------------------------------------------
 
+def _agree_categories_worker(rank):
+    from leanfe_amd import dist as ldist
+
+    class _Eng:  # what agree_categories needs of an attached engine: its torch group
+        dist_group = (None,)
+
+    local = np.array([2001, 2003, 2007]) if rank == 0 else np.array([2003, 2010])
+    return ldist.agree_categories(_Eng(), local).tolist()
+
+
+def test_factor_categories_agreed_across_row_shards():
+    """i(var) on a row shard: every rank expands the union of the ranks' categories (a shard may
+    miss some), so all ranks load the same columns (hip_impl: dist.agree_categories)."""
+    out = _run(_agree_categories_worker)
+    assert out[0] == out[1] == [2001, 2003, 2007, 2010]
+
+
 def test_shard_range_partitions_rows():
     for n in (0, 1, 7, 10, 1001):
         for world in (1, 2, 3, 8):

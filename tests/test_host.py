@@ -334,3 +334,24 @@ def test_every_device_operation_is_issued_on_the_context_stream():
             checked += 1
     assert checked > 250
     assert sync_calls == _DIAG_SYNC_OK, sync_calls
+
+
+def test_expansion_plan_applied_per_chunk_equals_whole_columns():
+    """frame.Expansion (the out-of-core path's lazy i(var) / var:i(f) expansion): the columns it
+    forms chunk by chunk are the whole-column expansion (polars_impl.py:27-115), names and order
+    included, for string and integer factors and a chosen reference category."""
+    rng = np.random.default_rng(3)
+    n = 10_007
+    cols = {"year": rng.integers(2000, 2012, n), "region": rng.choice(np.array(["N", "S", "E", "W"]), n),
+            "treat": rng.standard_normal(n)}
+    inter, facs = [("treat", "region", "S")], [("year", 2005)]
+    whole = dict(cols)
+    names = frame.expand_interactions(whole, inter) + frame.expand_factors(whole, facs)
+    plan = frame.Expansion(cols, inter, facs)
+    assert plan.names == names and plan.numeric_sources == ["treat"]
+    assert "region_S" not in [nm.split("treat_")[-1] for nm in names] and "year_2005" not in names
+    for r0 in range(0, n, 3_000):
+        sl = slice(r0, min(n, r0 + 3_000))
+        chunk = plan.columns(cols, {"treat": cols["treat"][sl]}, sl)
+        for name, col in zip(names, chunk):
+            np.testing.assert_array_equal(col, whole[name][sl])

@@ -1,12 +1,16 @@
 """Out-of-core X at a size whose resident layout does not fit one MI355X.
 
     python tools/oocore_run.py --rows 2100000000 --k 10 --levels 100000,1000 --chunk 50000000
+    python tools/oocore_run.py --rows 3000000000 --contexts 2 --chunk 50000000 --chunk2 70000000
 
 The synthetic panel of bench.py (counter-based, seed 12345) with only the FE codes resident;
 the columns are generated chunk by chunk on the device and streamed through pass 1 (group sums
 + raw Gram), the codes-only sweeps, the Gram from the tables and pass 2 (residual + HC1 meat).
 Checks printed with the timing: the fit is the same under a second chunking (--chunk2), and
 beta lies within a few SEs of the generating coefficients.  One JSON line on stdout.
+``--contexts S``: the rows in S contexts of < 2^31 rows each on the device (rows [row0, row0 + n_r)
+of the panel per context, lfe_synth_load_codes_at), joined in one in-process group (EmuGroup), as
+hip_impl._out_of_core_split runs a fit of more rows than one context holds.
 """
 from __future__ import annotations
 
@@ -22,11 +26,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def fit(eng, n, k, L, beta, chunk, seed):
+def fit(eng, n, k, L, beta, chunk, seed, row0=0):
     from leanfe_amd import inference
     t = {}
     t0 = time.perf_counter()
-    eng.synth_load_codes(n, k, L, seed=seed)
+    eng.synth_load_codes(n, k, L, seed=seed, row0=row0)
     eng.sync()
     t["codes_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
@@ -52,6 +56,39 @@ def fit(eng, n, k, L, beta, chunk, seed):
     return dict(beta=bf[1:], se=se, iterations=it, n_obs=n_obs, df_resid=df, rss=float(out[1]), t=t)
 
 
+def fit_contexts(S, rows, k, L, beta, chunk, seed):
+    """The fit on S contexts of one device (one thread each, one in-process group): rank 0's result."""
+    import threading
+
+    from leanfe_amd import dist
+    from leanfe_amd._lib import EmuGroup, Engine
+    if S == 1:
+        with Engine(0) as eng:
+            return fit(eng, rows, k, L, beta, chunk, seed)
+    group, out, errs = EmuGroup(S), [None] * S, []
+
+    def work(r):
+        lo, hi = dist.shard_range(rows, r, S)
+        try:
+            with Engine(0) as eng:
+                eng.set_emu(group, r)
+                out[r] = fit(eng, hi - lo, k, L, beta, chunk, seed, row0=lo)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            group.abort()
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(S)]
+    for t_ in ts:
+        t_.start()
+    for t_ in ts:
+        t_.join()
+    if errs:
+        raise errs[0]
+    for r in range(1, S):  # every context returns the same global fit
+        assert np.array_equal(out[r]["beta"], out[0]["beta"])
+    return out[0]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=2_100_000_000)
@@ -60,29 +97,27 @@ def main():
     ap.add_argument("--chunk", type=int, default=50_000_000)
     ap.add_argument("--chunk2", type=int, default=0, help="second chunking for the invariance check (0: off)")
     ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--contexts", type=int, default=1, help="contexts of < 2^31 rows on the device")
     a = ap.parse_args()
     from leanfe_amd import synth
-    from leanfe_amd._lib import Engine
     L = [int(x) for x in a.levels.split(",")]
     beta = synth.betas(a.k)
-    with Engine(0) as eng:
-        r = fit(eng, a.rows, a.k, L, beta, a.chunk, a.seed)
-        free = total = None
-        try:
-            import torch
-            free, total = torch.cuda.mem_get_info(0)
-        except Exception:  # noqa: BLE001 - torch is plumbing only; the figure is optional
-            pass
+    r = fit_contexts(a.contexts, a.rows, a.k, L, beta, a.chunk, a.seed)
+    free = total = None
+    try:
+        import torch
+        free, total = torch.cuda.mem_get_info(0)
+    except Exception:  # noqa: BLE001 - torch is plumbing only; the figure is optional
+        pass
     line = dict(kind="out-of-core X (codes resident, columns streamed in chunks generated on the device)",
-                rows=a.rows, k=a.k, levels=L, chunk_rows=a.chunk, iterations=r["iterations"], n_obs=r["n_obs"],
+                rows=a.rows, contexts=a.contexts, k=a.k, levels=L, chunk_rows=a.chunk, iterations=r["iterations"], n_obs=r["n_obs"],
                 x_bytes=a.rows * (a.k + 1) * 8, resident_layout_bytes_estimate=a.rows * (2 * 8 * (a.k + 1) + 30),
                 hbm_total=total, hbm_free_after=free, times=r["t"],
                 total_s=sum(r["t"].values()), mrows_s=a.rows / sum(r["t"].values()) / 1e6,
                 beta=[float(x) for x in r["beta"]], se=[float(x) for x in r["se"]],
                 max_abs_t_vs_generating_beta=float(np.max(np.abs((r["beta"] - beta) / r["se"]))))
     if a.chunk2:
-        with Engine(0) as eng:
-            r2 = fit(eng, a.rows, a.k, L, beta, a.chunk2, a.seed)
+        r2 = fit_contexts(a.contexts, a.rows, a.k, L, beta, a.chunk2, a.seed)
         line["chunk2"] = a.chunk2
         line["chunking_max_rel_beta"] = float(np.max(np.abs(r2["beta"] - r["beta"]) / np.abs(r["beta"])))
         line["chunking_max_rel_se"] = float(np.max(np.abs(r2["se"] - r["se"]) / np.abs(r["se"])))
