@@ -296,6 +296,12 @@ def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cel
         "cross": 4 * n * (F - 1),                    # the other FEs' codes in segment order
         "check": 4 * n * (F - 1),
         **({"count": 4 * n} if F != 2 else {}),      # one FE's codes (two FEs: the layouts' histograms)
+        # clustered SEs (lfe_cluster.hip): a sort launch is a digit histogram (8 B keys read) or a
+        # scatter (key + row read and written, 24 B) - 16 B/row on average over the pairs; a
+        # one-column subset's fixed-point sums (k_clfix_*) read the score rows and codes twice and
+        # add each score value into its cluster's entry: 3 x 8k + 16 B/row
+        "cluster_sort": 16 * n,
+        "cluster_scatter": n * (24 * k + 16),
         **dense,
     }
 

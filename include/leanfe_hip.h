@@ -297,6 +297,29 @@ int lfe_dense_cells(lfe_ctx* ctx, int64_t* cells);
  * x base-128 digits of the effects on v_mfma_i32_16x16x64_i8), 2 for the u16 / f64-MFMA form. */
 int lfe_dense_cell_bytes(lfe_ctx* ctx, int32_t* bytes);
 
+/* Wide fits (more than 63 columns: the reference's X'X of any width, polars_impl.py:165-209).
+ * A context holds at most 63 columns, so the columns run in blocks of contexts (each loads the
+ * codes and its columns; blocks after the first demean with tol = 0 and max_iter = the first
+ * block's iterations, so every column gets the same sweeps) and every block writes its demeaned
+ * columns into one device matrix D [P][ldD] in input row order:
+ *   lfe_dev_alloc / lfe_dev_free: a zero-filled device buffer of n_doubles (the caller frees it);
+ *   lfe_materialize: the context's demeaned columns [first, p) into D's columns col0, col0 + 1, ...
+ *     (0 on dropped rows) and, mask_col >= 0, the kept-row indicator (1 / 0) into column mask_col;
+ * then on the block holding y, the weights and the cluster columns (input order, ldD >= its rows):
+ *   lfe_wide_gram: out (P x P, host) = sum over rows of s_i D_i D_i' over D's columns [c0, c0 + P),
+ *     s = 1 (mode 0), w (1), w r^2 (2), r^2 (3) - the Gram of [1, y~, x~] and the HC1 meat;
+ *   lfe_wide_resid: r = D v over D's first P columns (v = [-b0, 1, -b], r: ldD device doubles),
+ *     stats = [sum w r^2, sum r^2, sum y~, sum y~^2] over kept rows;
+ *   lfe_wide_cluster_meats: per CGM subset (as lfe_cluster_meat_subsets) the meat S'S of the
+ *     per-cluster sums of D's columns [c0, c0 + k) times r (w), and the cluster counts. */
+int lfe_dev_alloc(lfe_ctx* ctx, int64_t n_doubles, double** dev_out);
+int lfe_dev_free(lfe_ctx* ctx, double* dev);
+int lfe_materialize(lfe_ctx* ctx, double* D, int64_t ldD, int first, int col0, int mask_col);
+int lfe_wide_gram(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, int P, int mode, const double* r, double* out);
+int lfe_wide_resid(lfe_ctx* ctx, const double* D, int64_t ldD, int P, const double* coef, double* r, double* stats);
+int lfe_wide_cluster_meats(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, int k, const double* r, int n_subsets,
+                           const int32_t* masks, double* meats_out, int64_t* G_out);
+
 /* Test-only switches of one context (0 clears them; production code never sets any).
  * LFE_TEST_SHORT_MEMORY: lfe_reshard_owner on this rank reports too little device memory for
  * its staging copy, so that the all-rank refusal can be tested (every rank keeps its rows). */

@@ -64,6 +64,12 @@ SIGNATURES = {
     "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
     "lfe_dense_cells": (C.c_int, [_vp, _i64p]),
     "lfe_ctx_test_hooks": (C.c_int, [_vp, C.c_int]),
+    "lfe_dev_alloc": (C.c_int, [_vp, C.c_int64, C.POINTER(_vp)]),
+    "lfe_dev_free": (C.c_int, [_vp, _vp]),
+    "lfe_materialize": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int]),
+    "lfe_wide_gram": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int, _vp, _dp]),
+    "lfe_wide_resid": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, _dp, _vp, _dp]),
+    "lfe_wide_cluster_meats": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, _vp, C.c_int, _i32p, _dp, _i64p]),
     "lfe_synth_load_codes_at": (C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int, C.c_int, _i32p, C.c_uint64]),
     "lfe_dense_cell_bytes": (C.c_int, [_vp, C.POINTER(C.c_int32)]),
     "lfe_load_codes": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.POINTER(_vp), _i32p, _dp, C.c_int]),
@@ -516,6 +522,43 @@ class Engine:
         on = C.c_int32(0)
         _check(self._lib.lfe_exact_sums(self._h, C.byref(on)))
         return bool(on.value)
+
+    # -- wide fits (p > 63: column blocks of contexts, lfe_wide.hip) ------------
+    def dev_alloc(self, n_doubles: int) -> int:
+        """A zero-filled device buffer of n_doubles (lfe_dev_alloc); release with dev_free."""
+        p = _vp()
+        _check(self._lib.lfe_dev_alloc(self._h, int(n_doubles), C.byref(p)))
+        return p.value
+
+    def dev_free(self, ptr: int) -> None:
+        _check(self._lib.lfe_dev_free(self._h, _vp(ptr)))
+
+    def materialize(self, D: int, ldD: int, first: int, col0: int, mask_col: int = -1) -> None:
+        """This context's demeaned columns [first, p) into D's columns col0.. (input row order)."""
+        _check(self._lib.lfe_materialize(self._h, _vp(D), int(ldD), int(first), int(col0), int(mask_col)))
+
+    def wide_gram(self, D: int, ldD: int, c0: int, P: int, mode: int = 0, r: int | None = None) -> np.ndarray:
+        out = np.zeros((P, P))
+        _check(self._lib.lfe_wide_gram(self._h, _vp(D), int(ldD), int(c0), int(P), int(mode),
+                                       None if r is None else _vp(r), out.ctypes.data_as(_dp)))
+        return out
+
+    def wide_resid(self, D: int, ldD: int, coef: np.ndarray, r: int) -> np.ndarray:
+        v = np.ascontiguousarray(coef, dtype=np.float64)
+        stats = np.zeros(4)
+        _check(self._lib.lfe_wide_resid(self._h, _vp(D), int(ldD), int(v.size), v.ctypes.data_as(_dp), _vp(r),
+                                        stats.ctypes.data_as(_dp)))
+        return stats
+
+    def wide_cluster_meats(self, D: int, ldD: int, c0: int, k: int, r: int, subsets) -> tuple[np.ndarray, np.ndarray]:
+        masks = np.array([sum(1 << j for j in s) for s in subsets], dtype=np.int32)
+        m = len(masks)
+        meats = np.zeros(max(m * k * k, 1))
+        G = np.zeros(max(m, 1), dtype=np.int64)
+        _check(self._lib.lfe_wide_cluster_meats(self._h, _vp(D), int(ldD), int(c0), int(k), _vp(r), m,
+                                                masks.ctypes.data_as(_i32p), meats.ctypes.data_as(_dp),
+                                                G.ctypes.data_as(_i64p)))
+        return meats[:m * k * k].reshape(m, k, k), G[:m]
 
     def test_hooks(self, flags: int) -> None:
         """Test-only switches (lfe_ctx_test_hooks; 1 = LFE_TEST_SHORT_MEMORY: this rank's owner

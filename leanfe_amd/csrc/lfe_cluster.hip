@@ -481,11 +481,222 @@ int owner_meat(lfe_ctx* c, const uint64_t* K, const int32_t* seg_off, const doub
   return LFE_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Per-row cluster ids in input row order (the wide fits of lfe_wide.hip)
+// ---------------------------------------------------------------------------
+__global__ void k_cid_one(const int32_t* __restrict__ code, const double* __restrict__ kept, int64_t n,
+                          int32_t* __restrict__ cid) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    cid[i] = kept[i] != 0.0 ? code[i] : -1;
+}
+
+__global__ void k_cid_keys(KeyArgs a, const double* __restrict__ kept) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t key = 0;
+    for (int j = 0; j < a.m; ++j) key += (uint64_t)(uint32_t)a.code[j][i] * a.mult[j];
+    a.keys[i] = kept[i] != 0.0 ? key : a.drop;
+    a.rows[i] = (int32_t)i;
+  }
+}
+
+// sorted position j -> its segment's index (heads before j, minus one unless j heads a segment)
+__global__ void k_cid_scatter(const uint64_t* __restrict__ K, const int32_t* __restrict__ R,
+                              const int32_t* __restrict__ scan, int64_t n, uint64_t drop, int32_t* __restrict__ cid) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+    cid[R[j]] = K[j] == drop ? -1 : scan[j] - (cl_head(K, j, drop) ? 0 : 1);
+}
+
+int cluster_ids_input(lfe_ctx* c, int mask, const double* kept, int32_t* cid, int32_t* G_out) {
+  const int64_t n = c->n;
+  auto& W = c->clw;
+  if (__builtin_popcount((unsigned)mask) == 1) {
+    const int j = __builtin_ctz((unsigned)mask);
+    if (n > 0)
+      hipLaunchKernelGGL(k_cid_one, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, c->cl[j], kept, n,
+                         cid);
+    LFE_HIP(hipGetLastError());
+    *G_out = c->cl_levels[j];
+    return LFE_OK;
+  }
+  KeyArgs ka{};
+  uint64_t span = 1;
+  for (int j = 0; j < (int)c->cl.size(); ++j) {
+    if (!(mask >> j & 1)) continue;
+    if (ka.m == kMaxCl) return fail(LFE_EINVAL, "too many cluster columns in one subset");
+    const uint64_t g = (uint64_t)c->cl_levels[j];
+    if (span > ((1ull << 62) / g)) return fail(LFE_EINVAL, "cluster intersection span exceeds 2^62");
+    ka.code[ka.m] = c->cl[j];
+    ka.mult[ka.m] = span;
+    ++ka.m;
+    span *= g;
+  }
+  LFE_TRY(ensure_sort_ws(c, (size_t)c->ld));
+  ka.n = n;
+  ka.drop = span;
+  ka.keys = W.keys[0];
+  ka.rows = W.rows[0];
+  if (n > 0) hipLaunchKernelGGL(k_cid_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka, kept);
+  LFE_HIP(hipGetLastError());
+  int buf = 0;
+  if (n > 0) LFE_TRY(radix_sort(c, n, bit_length(span), &buf));
+  int32_t G = 0, nv = 0;
+  LFE_TRY(group_segments(c, n, span, W.keys[buf], &G, &nv));
+  if (n > 0)
+    hipLaunchKernelGGL(k_cid_scatter, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, W.keys[buf],
+                       W.rows[buf], W.flag, n, span, cid);
+  LFE_HIP(hipGetLastError());
+  *G_out = G;
+  return LFE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// One cluster column: per-cluster score sums in two-limb fixed point, no sort
+// ---------------------------------------------------------------------------
+// A one-column subset's clusters are that column's codes, so S_c = sum of the score rows of c's kept
+// rows can be formed the way the group sums S_f are (lfe_fast.hip): every score value enters its
+// cluster's entry as a fine limb (int64 global adds) and, beyond the column's typical range, a
+// coarse limb (integer-valued f64 adds) - exact in any order, so the meat repeats bit for bit
+// without ordering the rows.  It replaces the key build, the radix sort and the segmented sums of
+// the sorted path (std_errors.py:317-333 groups by the column).
+constexpr int kClFixChunk = 8192;
+
+// the score columns' statistics in the colstat form of lfe_fast.hip (max |s_c| bits by u64
+// atomicMax; the chunk's sum of s_c^2 in fixed lane / wave order) and the clusters' kept-row counts
+__global__ __launch_bounds__(256) void k_clfix_stats(const int32_t* __restrict__ code, const int32_t* __restrict__ keep,
+                                                     int64_t n, const double* __restrict__ U, int k, int nchunks,
+                                                     int32_t* __restrict__ cnt, double* __restrict__ st) {
+  __shared__ double ws[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * kClFixChunk, r1 = min(n, r0 + kClFixChunk);
+  for (int64_t i = r0 + tid; i < r1; i += 256)
+    if (!keep || keep[i] >= 0) atomicAdd(&cnt[code[i]], 1);
+  const auto fmaxop = [](double x, double y) { return fmax(x, y); };
+  const auto addop = [](double x, double y) { return x + y; };
+  for (int c = 0; c < k; ++c) {
+    double m = 0.0, q = 0.0;
+    for (int64_t i = r0 + tid; i < r1; i += 256) {
+      if (keep && keep[i] < 0) continue;
+      const double v = U[i * k + c];
+      m = fmax(m, fabs(v));
+      q = __builtin_fma(v, v, q);
+    }
+    m = wave_reduce63(m, 0.0, fmaxop);
+    q = wave_reduce63(q, 0.0, addop);
+    if (lane == 63) {
+      ws[0][wave] = m;
+      ws[1][wave] = q;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double mm = fmax(fmax(ws[0][0], ws[0][1]), fmax(ws[0][2], ws[0][3]));
+      st[kColStatHead + (int64_t)c * nchunks + blockIdx.x] = ((ws[1][0] + ws[1][1]) + ws[1][2]) + ws[1][3];
+      atomicMax(reinterpret_cast<unsigned long long*>(st) + c, (unsigned long long)__double_as_longlong(mm));
+    }
+    __syncthreads();
+  }
+}
+
+// out[0] = clusters with kept rows, out[1] = the largest cluster (integer atomics: any order)
+__global__ void k_clfix_count(const int32_t* __restrict__ cnt, int32_t G, int32_t* __restrict__ out) {
+  int32_t nz = 0, mx = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (int64_t)gridDim.x * blockDim.x) {
+    nz += cnt[g] > 0 ? 1 : 0;
+    mx = max(mx, cnt[g]);
+  }
+  if (nz) atomicAdd(&out[0], nz);
+  if (mx) atomicMax(&out[1], mx);
+}
+
+// every kept score value into its cluster's entry: fine limb (int64 bits) and coarse limb
+__global__ void k_clfix_add(const int32_t* __restrict__ code, const int32_t* __restrict__ keep, int64_t n,
+                            const double* __restrict__ U, int k, const double* __restrict__ fq,
+                            unsigned long long* __restrict__ S, double* __restrict__ hi) {
+  const int64_t m = n * k;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / k;
+    const int c = (int)(e - i * k);
+    if (keep && keep[i] < 0) continue;
+    double hh;
+    const unsigned long long xi = fix_split(U[e], fix_col(fq, c), hh);
+    const int64_t t = (int64_t)code[i] * k + c;
+    if (xi) atomicAdd(&S[t], xi);
+    if (hh != 0.0) atomicAdd(&hi[t], hh);
+  }
+}
+
+static bool clfix_on() {
+  static const bool on = [] {
+    const char* e = getenv("LFE_CL_FIX");  // "0": the sorted path for one-column subsets too (A/B, tests)
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// meat and cluster count of the one-column subset j by the fixed-point sums (S: [G][k], then S'S)
+static int subset_meat_fix(lfe_ctx* c, int j, double* meat, int64_t* G_out) {
+  const int k = c->score_k;
+  const int64_t n = c->n;
+  const int32_t G = c->cl_levels[j];
+  auto& W = c->clw;
+  const int32_t* keep = c->L.P >= 0 ? c->L.code[c->L.P] : nullptr;
+  const int nch = (int)std::max<int64_t>(1, (n + kClFixChunk - 1) / kClFixChunk);
+  const size_t m = (size_t)G * std::max(k, 1);
+  LFE_TRY(ensure_f64(c, W.fixst, W.fixst_cap, (size_t)kColStatHead + (size_t)std::max(k, 1) * nch));
+  LFE_TRY(ensure_f64(c, W.fixq, W.fixq_cap, (size_t)kFqRows * kFqCols));
+  LFE_TRY(ensure_cluster_ws(c, m, (size_t)G + 4));   // clS: coarse limbs; clP: counts, then [nonzero, max]
+  LFE_TRY(ensure_f64(c, W.srec, W.srec_cap, m));      // fine limbs -> S
+  int32_t* cnt = c->clP;
+  int32_t* cm = c->clP + G;
+  double* S = W.srec;
+  LFE_HIP(hipMemsetAsync(W.fixst, 0, sizeof(double) * kColStatHead, c->stream));
+  LFE_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * ((size_t)G + 4), c->stream));
+  LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * m, c->stream));
+  LFE_HIP(hipMemsetAsync(S, 0, sizeof(double) * m, c->stream));
+  {
+    ProfScope _ps(c, K_CLUSTER_SCATTER);
+    if (n > 0)
+      hipLaunchKernelGGL(k_clfix_stats, dim3(nch), dim3(256), 0, c->stream, W.lay[j], keep, n, c->scores, k, nch, cnt,
+                         W.fixst);
+    LFE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, cnt, G, cm);
+    LFE_HIP(hipGetLastError());
+    if (k > 0 && n > 0) {
+      LFE_TRY(launch_fix_quanta(c, W.fixst, nch, std::max<int64_t>(c->n_kept_local, 1), cm + 1, 1, W.fixq, k));
+      hipLaunchKernelGGL(k_clfix_add, dim3(grid_for(n * k, 256, 8192)), dim3(256), 0, c->stream, W.lay[j], keep, n,
+                         c->scores, k, W.fixq, reinterpret_cast<unsigned long long*>(S), c->clS);
+      LFE_HIP(hipGetLastError());
+      LFE_TRY(launch_fix_convert(c, S, c->clS, (int64_t)m, k, W.fixq));
+    }
+  }
+  if (c->world > 1) {  // every rank's sums in the key-indexed table (global codes): all-reduced
+    LFE_TRY(allreduce_sum_f64(c, S, (size_t)G * k));
+    LFE_TRY(allreduce_sum_i32(c, cnt, (size_t)G));
+    LFE_HIP(hipMemsetAsync(cm, 0, sizeof(int32_t) * 2, c->stream));
+    hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, cnt, G, cm);
+    LFE_HIP(hipGetLastError());
+  }
+  int32_t hG = 0;
+  LFE_TRY(d2h_sync(c, &hG, cm, sizeof(int32_t)));
+  *G_out = hG;
+  if (k == 0) return LFE_OK;
+  const int world = c->world;  // S is replicated after the all-reduce: reduce its Gram locally
+  c->world = 1;
+  const int rc = launch_table_gram(c, S, G, k, meat);
+  c->world = world;
+  return rc;
+}
+
 // meat and cluster count of one subset (mask over the loaded cluster columns)
 static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   const int k = c->score_k;
   const int64_t n = c->n;
   auto& W = c->clw;
+  if (clfix_on() && __builtin_popcount((unsigned)mask) == 1) {
+    const int j = __builtin_ctz((unsigned)mask);
+    const int64_t m = (int64_t)c->cl_levels[j] * std::max(k, 1);
+    // a key-indexed table of at most 2^26 entries (512 MB), all-reduced whole across ranks up to 64 MB
+    if (m <= (1ll << 26) && (c->world == 1 || m * 8 <= (64ll << 20))) return subset_meat_fix(c, j, meat, G_out);
+  }
   KeyArgs ka{};
   uint64_t span = 1;
   for (int j = 0; j < (int)c->cl.size(); ++j) {
@@ -590,6 +801,9 @@ int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, doub
 
 void free_cluster_ws(lfe_ctx* c) {
   auto& W = c->clw;
+  dfree_any(W.fixst);
+  dfree_any(W.fixq);
+  W.fixst_cap = W.fixq_cap = 0;
   for (int b = 0; b < 2; ++b) {
     dfree_any(W.keys[b]);
     dfree_any(W.rows[b]);

@@ -105,6 +105,12 @@ struct Prof {
 
 // cluster workspace (lfe_cluster.hip)
 struct ClusterWS {
+  // one-column subsets on a dense key table (no sort): the score columns' statistics and quanta,
+  // the per-cluster fine limbs
+  double* fixst = nullptr;      // [kColStatHead + k * nchunks] max |s_c| bits, per-chunk sums of s_c^2
+  size_t fixst_cap = 0;
+  double* fixq = nullptr;       // [kFqRows][kFqCols]
+  size_t fixq_cap = 0;
   uint64_t* keys[2] = {nullptr, nullptr};  // radix sort ping-pong
   size_t keys_cap[2] = {0, 0};
   int32_t* rows[2] = {nullptr, nullptr};
@@ -516,6 +522,11 @@ inline int stream_tile_stride(int p) { return p <= 11 ? 16 : 16 * ((p + 1 + 15) 
 inline size_t stream_tile_len(int p) { const size_t t = (size_t)stream_tile_stride(p); return t * t + 4; }
 void stream_tile_add(lfe_ctx* c, const double* t, int m);
 int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
+// lfe_fast.hip: quanta of `ncols` columns from colstat-form statistics (max count: the max of cmax[0..nfe)),
+// and a [m] two-limb table (fine limbs' bits in S, coarse limbs in hi) -> double in place
+int launch_fix_quanta(lfe_ctx* c, const double* st, int nchunks, int64_t n, const int32_t* cmax, int nfe, double* fq,
+                      int ncols);
+int launch_fix_convert(lfe_ctx* c, double* S, double* hi, int64_t m, int p, const double* fq);
 void reduce_tiles(lfe_ctx* c, const double* part, int nblocks, double* out);  // sum of [nblocks][256] tiles
 // --- YOCO records (lfe_compress.hip) ---
 int records_layout(lfe_ctx* c);   // rec_sy / rec_syy in layout order -> rec_lay
@@ -525,6 +536,9 @@ int ensure_sort_ws(lfe_ctx* c, size_t n);
 int radix_sort(lfe_ctx* c, int64_t n, int bits, int* out_buf);
 // --- clusters (lfe_cluster.hip) ---
 int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, double* meats, int64_t* G_out);
+// per-row cluster ids (input row order) of subset `mask` over the loaded cluster columns; rows with
+// kept[i] == 0 get -1; *G_out: the id range (a column's levels, or an intersection's segments)
+int cluster_ids_input(lfe_ctx* c, int mask, const double* kept, int32_t* cid, int32_t* G_out);
 // multi-rank: per-cluster score rows S[G][k] (keys K[seg_off[h]], or K[h] with seg_off null) exchanged
 // to their owner ranks, merged by key; the k x k meat and the global cluster count
 int owner_meat(lfe_ctx* c, const uint64_t* K, const int32_t* seg_off, const double* S, int32_t G, int k,

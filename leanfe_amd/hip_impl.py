@@ -21,6 +21,7 @@ from .result import LeanFEResult
 from .strategy import DEFAULT_MAX_FE_LEVELS, determine_strategy
 
 MAX_FE_LEVELS = DEFAULT_MAX_FE_LEVELS  # polars_impl.py:24
+MAX_CONTEXT_COLS = 63  # columns one engine context holds (y + regressors + instruments); wider: _wide_fit
 _VERBOSE = os.environ.get("LEANFE_HIP_VERBOSE", "0") not in ("", "0")
 
 
@@ -108,6 +109,13 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         if factor_vars:
             x_cols = x_cols + frame.expand_factors(cols, factor_vars, unique)
     num_cols = [y_col] + x_cols + instruments  # the columns leanfe demeans (polars_impl.py:486)
+
+    if len(num_cols) > MAX_CONTEXT_COLS:
+        if out_of_core or instruments or sharded or strategy == "compress":
+            raise ValueError(f"{len(num_cols)} columns: a fit wider than {MAX_CONTEXT_COLS} columns runs resident, "
+                             "in one process, without instruments and with strategy alt_proj / demean")
+        return _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc, strategy, demean_tol,
+                         max_iter, formula, t_start, say, engine, device)
 
     own_engine = engine is None
     eng = engine if engine is not None else Engine(_default_device() if device is None else device)
@@ -454,6 +462,116 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
                         fe_dims=fe_dims, r_squared=None if mz else (1 - rss / tss if tss > 0 else None),
                         compression_ratio=None, rss=float(rss), tss=None if mz else tss, backend="hip",
                         timings=timings)
+
+
+def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc, strategy, demean_tol, max_iter,
+              formula, t_start, say, engine=None, device=None) -> LeanFEResult:
+    """A fit of more than 63 columns (e.g. an event study's i(year) dummies, polars_impl.py:27-69,
+    whose X'X the reference forms at any width, :165-209): the columns run in blocks of engine
+    contexts - the first [y] + 62 regressors with the stop test, every later one 63 regressors
+    with exactly the first block's number of sweeps (each column's projections are its own,
+    :491-508) - and each block writes its demeaned columns into one device matrix D = [1_kept, y~,
+    x~] (input row order, lfe_materialize).  The Gram, the residual, the HC1 meat and the cluster
+    score sums then come from D (lfe_wide.hip), the solve and the sandwiches from the host as in
+    the resident fit (inference.py, std_errors.py:183-441)."""
+    k = len(x_cols)
+    P = 2 + k
+    w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
+    y = np.asarray(cols[y_col], dtype=np.float64)
+    n = y.size
+    ldD = (n + 63) // 64 * 64
+    per = MAX_CONTEXT_COLS
+    blocks = [x_cols[:per - 1]] + [x_cols[j:j + per] for j in range(per - 1, k, per)]
+    dev = _default_device() if device is None else device
+    eng = engine if engine is not None else Engine(dev)
+    D = r = None
+    try:
+        codes, levels = [], []
+        for fe in fe_cols:
+            c, g = frame.factorize(cols[fe], device=eng)
+            codes.append(c)
+            levels.append(g)
+        if strategy == "auto":
+            strategy = "demean" if len(fe_cols) == 1 else ("alt_proj" if fe_cols else "ols")
+        if strategy == "demean" and len(fe_cols) != 1:
+            raise ValueError("Strategy 'demean' requires exactly one FE column.")
+        if strategy == "alt_proj" and not fe_cols:
+            raise ValueError("Strategy 'alt_proj' requires FE-cols. Use strategy='ols' instead for OLS without FE.")
+        if strategy == "ols" and fe_cols:
+            raise ValueError("Strategy 'ols' takes no fixed effects")
+        say(f"Wide fit: {k} regressors in {len(blocks)} column blocks")
+        t0 = time.perf_counter()
+        D = eng.dev_alloc(P * ldD)
+        eng.sync()  # zero-filled before any block's context writes into it
+        iterations = 0
+        col0 = 1
+        for b, xb in enumerate(blocks):
+            e = eng if b == 0 else Engine(eng.device)
+            try:
+                colsb = ([y] if b == 0 else []) + [np.asarray(cols[c], dtype=np.float64) for c in xb]
+                e.load(colsb, codes, levels, w)
+                n_obs, fe_dims, fe_card = e.drop_singletons()
+                if strategy == "demean":
+                    it, _ = e.demean([0], demean_tol, max_iter, check_from=0)
+                    iterations = 1
+                elif strategy == "alt_proj":
+                    order = sorted(range(len(fe_cols)), key=lambda i: fe_card[i])  # polars_impl.py:485
+                    if b == 0:
+                        iterations, _ = e.demean(order, demean_tol, max_iter, check_from=3)
+                    else:  # the same sweeps as the first block: no stop test of its own
+                        e.demean(order, 0.0, iterations, check_from=3)
+                else:
+                    e.demean([], demean_tol, max_iter, check_from=0)
+                e.materialize(D, ldD, 0, col0, 0 if b == 0 else -1)
+                col0 += len(colsb)
+                e.sync()
+            finally:
+                if b > 0:
+                    e.close()
+        t_load = time.perf_counter() - t0
+        if strategy == "ols":
+            iterations, absorbed_df, fe_dims = 0, 0, None
+        elif strategy == "demean":
+            absorbed_df = fe_dims[0] - 1
+        else:
+            absorbed_df = sum(fe_dims) - len(fe_cols)
+        df_resid = n_obs - (k + 1) - absorbed_df
+        G = eng.wide_gram(D, ldD, 0, P, mode=1 if w is not None else 0)
+        XtX, Xty = inference.split_gram(G)
+        beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # polars_impl.py:212-226
+        Vb = XtX_inv[1:, 1:]
+        r = eng.dev_alloc(ldD)
+        coef = np.concatenate([[-beta_full[0], 1.0], -beta_full[1:]])
+        rss_w, rss, sum_y, sum_y2 = eng.wide_resid(D, ldD, coef, r)
+        n_clusters = None
+        if v == "iid":
+            se = inference.se_iid(Vb, rss_w, df_resid)
+        elif v == "hc1":
+            meat = eng.wide_gram(D, ldD, 2, k, mode=2 if w is not None else 3, r=r)
+            se = inference.se_hc1(Vb, meat, n_obs, df_resid)
+        else:
+            _load_clusters(eng, cols, cluster_cols, False)
+            subsets = inference.cluster_subsets(len(cluster_cols))
+            meats, Gs = eng.wide_cluster_meats(D, ldD, 2, k, r, subsets)
+            if len(cluster_cols) == 1:
+                se, n_clusters = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, ssc)
+            else:
+                se, n_clusters = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets, n_obs,
+                                                               df_resid, ssc)
+        tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
+        timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
+    finally:
+        for ptr in (D, r):
+            if ptr is not None:
+                eng.dev_free(ptr)
+        if engine is None:
+            eng.close()
+    return LeanFEResult(coefs=dict(zip(x_cols, (float(b_) for b_ in beta_full[1:]))),
+                        std_errors=dict(zip(x_cols, (float(s_) for s_ in se))), n_obs=n_obs,
+                        iterations=iterations, vcov_type=vcov, is_iv=False, n_instruments=None,
+                        n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
+                        fe_dims=fe_dims, r_squared=1 - rss / tss if tss > 0 else None, compression_ratio=None,
+                        rss=float(rss), tss=tss, backend="hip", timings=timings)
 
 
 def _beta_agrees(beta_dev, beta_host, rtol: float = 1e-10) -> bool:

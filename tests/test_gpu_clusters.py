@@ -1,0 +1,120 @@
+"""Clustered SEs: one-column subsets by two-limb fixed-point sums (lfe_cluster.hip subset_meat_fix).
+
+A one-column cluster subset's clusters are the column's codes, so the per-cluster score sums
+S_c = sum_{i in c} x~_i r_i (w_i) (std_errors.py:317-333) are formed the way the group sums are -
+fine limbs by int64 adds, outliers' coarse limbs by integer-valued f64 adds - into a table indexed
+by the code, with no sort.  Against the sorted path (LFE_CL_FIX=0: keys, radix sort, segmented sums)
+and the CPU oracle (oracle/altproj.py: std_errors.py:289-441): one-way and multi-way CGM (the
+intersection subset still sorts), clusters on FE columns (reg_test.py:55, 61) and on a column that
+is no FE, weights, a 5e9 outlier (coarse limbs), bit-identical repeats, and an emulated 2-rank
+group (the table all-reduced)."""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import pytest
+
+from leanfe_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _fit(data, xs, fes, cl, **kw):
+    from leanfe_amd import leanfe_hip
+
+    r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov="cluster", cluster_cols=cl,
+                   quiet=True, device=0, **kw)
+    return r
+
+
+def _arr(r, xs, what):
+    return np.array([getattr(r, what)[x] for x in xs])
+
+
+CASES = [
+    ("fe_oneway", [20_000, 600], ["fe1"], None),
+    ("fe_twoway", [20_000, 600], ["fe1", "fe2"], None),
+    ("other_oneway_weighted", [20_000, 600], ["grp"], "w"),
+    ("fe3_cgm_outlier", [9_000, 800, 150], ["fe2", "fe3"], None),
+]
+
+
+@pytest.mark.parametrize("name,L,cl,weights", CASES, ids=[c[0] for c in CASES])
+def test_one_column_subsets_without_sort(name, L, cl, weights, monkeypatch):
+    from oracle import altproj
+
+    n, k = 500_000, 4
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(L))]
+    d = dict(synth.panel(n, k, L, seed=71))
+    rng = np.random.default_rng(71)
+    d["grp"] = rng.integers(0, 3_000, n)
+    if weights:
+        d["w"] = rng.uniform(0.5, 2.0, n)
+    if "outlier" in name:
+        x = np.array(d["x2"], copy=True)
+        x[777] = 5e9
+        d["x2"] = x
+    kw = dict(weights=weights) if weights else {}
+    fix = _fit(d, xs, fes, cl, **kw)
+    again = _fit(d, xs, fes, cl, **kw)
+    monkeypatch.setenv("LFE_CL_FIX", "0")
+    srt = _fit(d, xs, fes, cl, **kw)
+    o = altproj.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=cl, weights=weights)
+    ncl = o["n_clusters"]
+    assert fix.n_clusters == srt.n_clusters
+    assert (tuple(fix.n_clusters) if isinstance(fix.n_clusters, (list, tuple)) else fix.n_clusters) == (
+        tuple(ncl) if isinstance(ncl, (list, tuple)) else ncl)
+    assert fix.iterations == o["iterations"] and fix.n_obs == o["n_obs"]
+    np.testing.assert_allclose(_arr(fix, xs, "coefs"), o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(_arr(fix, xs, "std_errors"), o["se"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(_arr(fix, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
+    np.testing.assert_array_equal(_arr(fix, xs, "std_errors"), _arr(again, xs, "std_errors"))
+
+
+def test_one_column_subset_on_emulated_ranks():
+    """Row-sharded ranks: each rank's fixed-point table goes into the all-reduced key-indexed table;
+    every rank equals the oracle on the whole panel and all ranks agree bit for bit."""
+    from leanfe_amd import inference
+    from leanfe_amd._lib import EmuGroup, Engine
+    from leanfe_amd.dist import shard_range
+    from oracle import altproj
+
+    world, n, k, L = 3, 450_001, 3, [6_000, 300]
+    data = synth.panel(n, k, L, seed=88)
+    group, out, errs = EmuGroup(world), {}, []
+
+    def work(r):
+        lo, hi = shard_range(n, r, world)
+        try:
+            with Engine(0) as eng:
+                eng.set_emu(group, r)
+                eng.synth_load(hi - lo, k, L, synth.betas(k), seed=88, row_offset=lo)
+                _, codes = eng.copy_inputs()
+                eng.load_clusters([np.ascontiguousarray(codes[1])], [L[1]])
+                n_obs, dims, card = eng.drop_singletons()
+                it, _ = eng.demean(sorted(range(2), key=lambda i: card[i]), 1e-6, 50, check_from=3)
+                G = eng.gram()
+                bf, XtX_inv = inference.solve_normal(*inference.split_gram(G))
+                eng.resid(bf, hc1=False, keep_scores=True)
+                meats, Gs = eng.cluster_meat()
+                df = n_obs - (k + 1) - (sum(dims) - 2)
+                se, ncl = inference.se_cluster_oneway(XtX_inv[1:, 1:], meats[0], int(Gs[0]), n_obs, df, True)
+                out[r] = dict(se=se, ncl=ncl, it=it)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            group.abort()
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    xs = [f"x{j + 1}" for j in range(k)]
+    o = altproj.fit(data, "y", xs, ["fe1", "fe2"], vcov="cluster", cluster_cols=["fe2"])
+    for r in range(world):
+        assert out[r]["it"] == o["iterations"] and out[r]["ncl"] == o["n_clusters"]
+        np.testing.assert_allclose(out[r]["se"], o["se"], rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(out[r]["se"], out[0]["se"])

@@ -1,0 +1,85 @@
+"""Fits wider than one engine context (more than 63 columns; VERDICT r4 Missing 2).
+
+The reference forms X'X of [1, X_dm] at any width (polars_impl.py:165-209), e.g. an event study's
+i(year) dummies (:27-69) beside controls.  hip_impl._wide_fit runs the columns in blocks of
+contexts (the first with the stop test, the others with exactly its sweeps) and writes the
+demeaned columns into one device matrix; the Gram, residual, HC1 meat and cluster score sums then
+come from that matrix (lfe_wide.hip).  Checked against the CPU oracle (oracle/altproj.py) at 1e-10
+with equal iterations, and - with the context width lowered so that a 40-column fit takes three
+blocks - against the one-context fit at 1e-12."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from leanfe_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(r, o, xs):
+    assert r.iterations == o["iterations"] and r.n_obs == o["n_obs"] and r.df_resid == o["df_resid"]
+    np.testing.assert_allclose([r.coefs[x] for x in xs], o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose([r.std_errors[x] for x in xs], o["se"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("vcov,cl,weighted", [("HC1", None, False), ("iid", None, True), ("cluster", ["fe1"], False),
+                                              ("cluster", ["fe1", "fe2"], True)])
+def test_wide_fit_matches_oracle(vcov, cl, weighted):
+    from leanfe_amd import leanfe_hip
+    from oracle import altproj
+
+    n, k, L = 150_001, 99, [3_000, 200]
+    d = dict(synth.panel(n, k, L, seed=12))
+    kw = {}
+    if weighted:
+        d["w"] = np.random.default_rng(12).uniform(0.5, 2.0, n)
+        kw["weights"] = "w"
+    xs = [f"x{j + 1}" for j in range(k)]
+    r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], strategy="alt_proj", vcov=vcov, cluster_cols=cl,
+                   quiet=True, **kw)
+    o = altproj.fit(d, "y", xs, ["fe1", "fe2"], vcov=vcov, cluster_cols=cl, weights=kw.get("weights"))
+    _check(r, o, xs)
+    if cl:
+        ncl = o["n_clusters"]
+        assert (tuple(r.n_clusters) if isinstance(r.n_clusters, (list, tuple)) else r.n_clusters) == (
+            tuple(ncl) if isinstance(ncl, (list, tuple)) else ncl)
+
+
+def test_event_study_formula_beyond_63_columns():
+    """y ~ x1 + x2 + i(year) with 80 years and firm clusters: 81 dummies + 2 controls."""
+    from leanfe_amd import frame, leanfe_hip
+    from oracle import altproj
+
+    n, L = 200_000, [4_000, 150]
+    d = dict(synth.panel(n, 2, L, seed=33))
+    d["year"] = np.random.default_rng(33).integers(1940, 2021, n)
+    r = leanfe_hip(d, formula="y ~ x1 + x2 + i(year) | fe1 + fe2", strategy="alt_proj", vcov="cluster",
+                   cluster_cols=["fe1"], quiet=True)
+    full = dict(d)
+    xs = ["x1", "x2"] + frame.expand_factors(full, [("year", None)])
+    assert list(r.coefs) == xs and len(xs) == 82
+    o = altproj.fit(full, "y", xs, ["fe1", "fe2"], vcov="cluster", cluster_cols=["fe1"])
+    _check(r, o, xs)
+
+
+@pytest.mark.parametrize("vcov,F", [("HC1", 2), ("cluster", 3), ("iid", 1)])
+def test_column_blocks_equal_the_one_context_fit(vcov, F, monkeypatch):
+    from leanfe_amd import hip_impl, leanfe_hip
+
+    n, k = 300_000, 39
+    L = [5_000, 400, 60][:F]
+    d = dict(synth.panel(n, k, L, seed=5))
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(F)]
+    cl = ["fe2", "fe3"] if vcov == "cluster" else None
+    strat = "demean" if F == 1 else "alt_proj"
+    one = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy=strat, vcov=vcov, cluster_cols=cl, quiet=True)
+    monkeypatch.setattr(hip_impl, "MAX_CONTEXT_COLS", 16)  # 40 columns: three blocks
+    wide = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy=strat, vcov=vcov, cluster_cols=cl, quiet=True)
+    assert wide.iterations == one.iterations and wide.n_obs == one.n_obs and wide.df_resid == one.df_resid
+    np.testing.assert_allclose([wide.coefs[x] for x in xs], [one.coefs[x] for x in xs], rtol=1e-12, atol=0)
+    np.testing.assert_allclose([wide.std_errors[x] for x in xs], [one.std_errors[x] for x in xs], rtol=1e-12,
+                               atol=0)
+    if cl:
+        assert tuple(wide.n_clusters) == tuple(one.n_clusters)
