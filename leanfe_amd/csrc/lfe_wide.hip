@@ -88,6 +88,7 @@ __device__ __forceinline__ void tile_of_pair(int pair, int nt, int& ti, int& tj)
   tj = ti + pair;
 }
 
+template <bool ROWQ>  // ROWQ: rs == 1, a lane's 4 rows of a column are one 32-byte load
 __global__ __launch_bounds__(256) void k_wide_syrk(SyrkArgs a) {
   const int pair = blockIdx.x / a.nsplit, split = blockIdx.x - pair * a.nsplit;
   int ti, tj;
@@ -111,16 +112,38 @@ __global__ __launch_bounds__(256) void k_wide_syrk(SyrkArgs a) {
   for (int jb = 0; jb < 4; ++jb) acc[jb] = d4{0.0, 0.0, 0.0, 0.0};
   for (int64_t rb = r0 + 4 * kq; rb < r1; rb += 16) {
     double av[4], bv[4][4];
+    if (ROWQ) {  // rows past n are zero in A (its padding) and get scale 0
+      const d4 x = *reinterpret_cast<const d4*>(pa + rb);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int64_t i = rb + s;
-      const bool in = i < a.n;
-      double sc = 1.0;
-      if (a.mode == 1 || a.mode == 2) sc = (a.w && in) ? a.w[i] : 1.0;
-      if (a.mode >= 2 && in) sc *= a.r[i] * a.r[i];
-      av[s] = (in && va) ? pa[i * a.rs] * sc : 0.0;
+      for (int jb = 0; jb < 4; ++jb) {
+        const d4 y = *reinterpret_cast<const d4*>(pb[jb] + rb);
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb) bv[jb][s] = (in && vb[jb]) ? pb[jb][i * a.rs] : 0.0;
+        for (int s = 0; s < 4; ++s) bv[jb][s] = vb[jb] ? y[s] : 0.0;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) av[s] = va ? x[s] : 0.0;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int64_t i = rb + s;
+        const bool in = i < a.n;
+        av[s] = (in && va) ? pa[i * a.rs] : 0.0;
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) bv[jb][s] = (in && vb[jb]) ? pb[jb][i * a.rs] : 0.0;
+      }
+    }
+    if (a.mode) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int64_t i = rb + s;
+        const bool in = i < a.n;
+        double sc = 0.0;
+        if (in) {
+          sc = (a.mode == 1 || a.mode == 2) && a.w ? a.w[i] : 1.0;
+          if (a.mode >= 2) sc *= a.r[i] * a.r[i];
+        }
+        av[s] *= sc;
+      }
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -174,7 +197,11 @@ int wide_syrk(lfe_ctx* c, const double* A, int64_t cs, int64_t rs, int64_t n, in
     a.partial = part;
     {
       ProfScope _ps(c, K_GRAM_DESIGN);
-      hipLaunchKernelGGL(k_wide_syrk, dim3((unsigned)(npairs * nsplit)), dim3(256), 0, c->stream, a);
+      // the 32-byte row quads need rows up to the next multiple of 16 inside A's padded columns
+      if (rs == 1 && cs >= (n + 15) / 16 * 16 && cs % 4 == 0)
+        hipLaunchKernelGGL(k_wide_syrk<true>, dim3((unsigned)(npairs * nsplit)), dim3(256), 0, c->stream, a);
+      else
+        hipLaunchKernelGGL(k_wide_syrk<false>, dim3((unsigned)(npairs * nsplit)), dim3(256), 0, c->stream, a);
       hipLaunchKernelGGL(k_wide_reduce, dim3(grid_for((int64_t)npairs * kWT * kWT)), dim3(kBlock), 0, c->stream, part,
                          npairs, nsplit, tiles);
     }

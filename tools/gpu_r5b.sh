@@ -10,10 +10,8 @@ rc=$?; echo "stream pytest rc=$rc"; tail -2 gpurun_out/pytest_r5a.log
 timeout -k 10 800 python -m pytest tests/test_gpu_wide.py tests/test_gpu_clusters.py tests/test_gpu_dense.py tests/test_gpu_determinism.py tests/test_gpu_configs.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r5b.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_r5b.log
 [ $rc -eq 0 ] || exit $rc
-for v in 0 1 0 1; do
-  LFE_SUMS_ROWS=$v timeout -k 10 300 python bench.py --no-cpu --no-h2d > gpurun_out/b_rows$v.json 2>gpurun_out/b_rows$v.err || exit 1
-  python -c "import json;d=json.load(open('gpurun_out/b_rows$v.json'));print('rows=$v', d['ms_per_step'], d['kernels_ms']['group_sums'], d['kernels_ms']['part_scatter'])"
-done
 timeout -k 10 400 python tools/oocore_run.py --rows 3000000000 --contexts 2 --chunk 50000000 --chunk2 70000000 \
   > gpurun_out/oocore_3000m.json 2> gpurun_out/oocore_3000m.err
 rc=$?; echo "oocore rc=$rc"; tail -c 2500 gpurun_out/oocore_3000m.json; tail -5 gpurun_out/oocore_3000m.err
+[ $rc -eq 0 ] || exit $rc
+bash tools/gpu_r5c.sh
