@@ -305,6 +305,9 @@ int lfe_dense_cell_bytes(lfe_ctx* ctx, int32_t* bytes);
  *   lfe_dev_alloc / lfe_dev_free: a zero-filled device buffer of n_doubles (the caller frees it);
  *   lfe_materialize: the context's demeaned columns [first, p) into D's columns col0, col0 + 1, ...
  *     (0 on dropped rows) and, mask_col >= 0, the kept-row indicator (1 / 0) into column mask_col;
+ *   lfe_stream_materialize: the same for a streamed (codes-only) context - it opens pass 5, whose
+ *     chunks (lfe_stream_rows / lfe_stream_synth_rows, all p columns) write x~ into D's rows
+ *     row0.. from column col0; lfe_stream_end (out may be null) closes it;
  * then on the block holding y, the weights and the cluster columns (input order, ldD >= its rows):
  *   lfe_wide_gram: out (P x P, host) = sum over rows of s_i D_i D_i' over D's columns [c0, c0 + P),
  *     s = 1 (mode 0), w (1), w r^2 (2), r^2 (3) - the Gram of [1, y~, x~] and the HC1 meat;
@@ -315,6 +318,7 @@ int lfe_dense_cell_bytes(lfe_ctx* ctx, int32_t* bytes);
 int lfe_dev_alloc(lfe_ctx* ctx, int64_t n_doubles, double** dev_out);
 int lfe_dev_free(lfe_ctx* ctx, double* dev);
 int lfe_materialize(lfe_ctx* ctx, double* D, int64_t ldD, int first, int col0, int mask_col);
+int lfe_stream_materialize(lfe_ctx* ctx, double* D, int64_t ldD, int col0, int mask_col);
 int lfe_wide_gram(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, int P, int mode, const double* r, double* out);
 int lfe_wide_resid(lfe_ctx* ctx, const double* D, int64_t ldD, int P, const double* coef, double* r, double* stats);
 int lfe_wide_cluster_meats(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, int k, const double* r, int n_subsets,

@@ -67,6 +67,7 @@ SIGNATURES = {
     "lfe_dev_alloc": (C.c_int, [_vp, C.c_int64, C.POINTER(_vp)]),
     "lfe_dev_free": (C.c_int, [_vp, _vp]),
     "lfe_materialize": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int]),
+    "lfe_stream_materialize": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int]),
     "lfe_wide_gram": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int, _vp, _dp]),
     "lfe_wide_resid": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, _dp, _vp, _dp]),
     "lfe_wide_cluster_meats": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, _vp, C.c_int, _i32p, _dp, _i64p]),
@@ -536,6 +537,13 @@ class Engine:
     def materialize(self, D: int, ldD: int, first: int, col0: int, mask_col: int = -1) -> None:
         """This context's demeaned columns [first, p) into D's columns col0.. (input row order)."""
         _check(self._lib.lfe_materialize(self._h, _vp(D), int(ldD), int(first), int(col0), int(mask_col)))
+
+    def stream_materialize(self, D: int, ldD: int, col0: int, chunks, mask_col: int = -1) -> None:
+        """A streamed context's demeaned columns, chunk by chunk, into D's columns col0.. (pass 5)."""
+        _check(self._lib.lfe_stream_materialize(self._h, _vp(D), int(ldD), int(col0), int(mask_col)))
+        for row0, cols in chunks:
+            self.stream_rows(row0, cols)
+        _check(self._lib.lfe_stream_end(self._h, None))
 
     def wide_gram(self, D: int, ldD: int, c0: int, P: int, mode: int = 0, r: int | None = None) -> np.ndarray:
         out = np.zeros((P, P))

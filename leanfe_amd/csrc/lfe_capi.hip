@@ -834,6 +834,8 @@ static int stream_chunk(lfe_ctx* c, int64_t cld, int64_t row0, int64_t rows) {
   PhaseTimer t(c, w.pass == 1 ? PH_PREP : w.pass == 3 ? PH_GRAM : PH_RESID);
   if (w.pass == 1) {
     LFE_TRY(stream_sums_chunk(c, w.x, cld, row0, rows, w.rows_done == 0));
+  } else if (w.pass == 5) {
+    LFE_TRY(stream_materialize_chunk(c, w.x, cld, row0, rows));
   } else {
     const bool resid = w.pass == 2 || w.pass == 4;
     const bool scored = resid && !w.cid.empty();
@@ -907,6 +909,10 @@ int lfe_stream_end(lfe_ctx* c, double* out) {
   w.pass = 0;
   if (w.rows_done != c->n) return fail(LFE_EINVAL, "the streamed chunks did not cover the loaded rows");
   const int p = c->p, k = p - 1;
+  if (pass == 5) {  // lfe_stream_materialize: nothing to reduce
+    w.mD = nullptr;
+    return LFE_OK;
+  }
   if (pass == 1) {
     LFE_TRY(ensure_f64(c, c->raw_tile, c->raw_tile_cap, 256));
     if (c->n > 0) LFE_HIP(hipMemcpyAsync(c->raw_tile, w.tile, sizeof(double) * 256, hipMemcpyDeviceToDevice, c->stream));

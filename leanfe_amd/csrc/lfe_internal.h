@@ -419,6 +419,10 @@ struct lfe_ctx {
     double* toff = nullptr;  // [4 kMaxFE] 8-byte slots: table ends (int64), S / W / Sy pointers per FE
     size_t toff_cap = 0;
     int icpt = 0;            // pass 4: the IV residual over u = [1, x~, z~]
+    // pass 5 (lfe_stream_materialize): the chunks' demeaned columns into a caller's matrix
+    double* mD = nullptr;    // [cols][mld], input row order (0 on dropped rows)
+    int64_t mld = 0;
+    int mcol0 = 0, mmask = -1;  // first target column; kept-row indicator column (-1: none)
     // clustered SEs (lfe_stream_clusters): every subset's dense cluster id per input row, and the
     // per-cluster score sums the residual passes add in chunk order
     std::vector<int32_t> masks;
@@ -514,6 +518,7 @@ void free_stream_clusters(lfe_ctx* c);
 // records in c->clS (lfe_cluster.hip)
 int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R, const double* table,
                  int k, int32_t* G_out);  // weighted streamed fits: w's max / rms into fixq column p
+int stream_materialize_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows);  // lfe_wide.hip
 int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t ld, int64_t row0, int64_t rows,
                       double* scores);
 // streamed tile stride for p data columns: the p <= 11 row-per-lane passes use the 16 x 16 tile of

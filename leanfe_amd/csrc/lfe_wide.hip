@@ -63,6 +63,58 @@ __global__ void k_materialize(LayoutArgs la, const double* __restrict__ X, int64
   }
 }
 
+// streamed X (pass 5): a chunk's x~ = x - sum_f alpha_f[g_f] (the keep test of the streamed passes,
+// lfe_gram.hip k_stream_rows) into D's rows row0.. (the chunk is in input order already)
+struct StreamMatArgs {
+  const double* X;
+  int64_t ld, rows;
+  int p, F;
+  const int32_t* code[kMaxFE];
+  const int32_t* cnt_pre[kMaxFE];
+  const double* alpha[kMaxFE];
+  double* D;
+  int64_t ldD;
+  int col0, mask_col;
+};
+
+__global__ void k_stream_materialize(StreamMatArgs a) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.rows; i += (int64_t)gridDim.x * blockDim.x) {
+    bool keep = true;
+    for (int f = 0; f < a.F; ++f) keep = keep && a.cnt_pre[f][a.code[f][i]] > 1;
+    if (a.mask_col >= 0) a.D[(int64_t)a.mask_col * a.ldD + i] = keep ? 1.0 : 0.0;
+    for (int c = 0; c < a.p; ++c) {
+      double v = 0.0;
+      if (keep) {
+        v = a.X[(int64_t)c * a.ld + i];
+        for (int f = 0; f < a.F; ++f) v -= a.alpha[f][(int64_t)a.code[f][i] * a.p + c];
+      }
+      a.D[(int64_t)(a.col0 + c) * a.ldD + i] = v;
+    }
+  }
+}
+
+int stream_materialize_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows) {
+  const auto& w = c->sw;
+  StreamMatArgs a{};
+  a.X = X;
+  a.ld = ld;
+  a.rows = rows;
+  a.p = c->p;
+  a.F = c->F;
+  for (int f = 0; f < c->F; ++f) {
+    a.code[f] = c->fe[f].code + row0;
+    a.cnt_pre[f] = c->fe[f].cnt_pre;
+    a.alpha[f] = c->fe[f].alpha;
+  }
+  a.D = w.mD + row0;
+  a.ldD = w.mld;
+  a.col0 = w.mcol0;
+  a.mask_col = w.mmask;
+  if (rows > 0) hipLaunchKernelGGL(k_stream_materialize, dim3(grid_for(rows)), dim3(kBlock), 0, c->stream, a);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
 // ---------------------------------------------------------------------------
 // A' diag(s) A over the rows, tiles of 64 x 64
 // ---------------------------------------------------------------------------
@@ -394,6 +446,22 @@ int lfe_materialize(lfe_ctx* c, double* D, int64_t ldD, int first, int col0, int
     hipLaunchKernelGGL(k_materialize, dim3(grid_for(c->n)), dim3(kBlock), 0, c->stream, layout_args(c), c->L.X, c->ld,
                        c->n, c->L.orig, D, ldD, first, col0, mask_col);
   LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+int lfe_stream_materialize(lfe_ctx* c, double* D, int64_t ldD, int col0, int mask_col) {
+  LFE_WCTX(c);
+  auto& w = c->sw;
+  if (!w.on) return fail(LFE_ESTATE, "lfe_stream_materialize: the context holds resident columns (lfe_materialize)");
+  if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
+  if (w.pass != 0) return fail(LFE_ESTATE, "a streamed pass is open (lfe_stream_end first)");
+  if (!D || ldD < c->n || col0 < 0) return fail(LFE_EINVAL, "bad arguments");
+  w.mD = D;
+  w.mld = ldD;
+  w.mcol0 = col0;
+  w.mmask = mask_col;
+  w.pass = 5;
+  w.rows_done = 0;
   return LFE_OK;
 }
 

@@ -111,11 +111,23 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     num_cols = [y_col] + x_cols + instruments  # the columns leanfe demeans (polars_impl.py:486)
 
     if len(num_cols) > MAX_CONTEXT_COLS:
-        if out_of_core or instruments or sharded or strategy == "compress":
-            raise ValueError(f"{len(num_cols)} columns: a fit wider than {MAX_CONTEXT_COLS} columns runs resident, "
-                             "in one process, without instruments and with strategy alt_proj / demean")
+        if instruments or sharded or strategy == "compress":
+            raise ValueError(f"{len(num_cols)} columns: a fit wider than {MAX_CONTEXT_COLS} columns runs in one "
+                             "process, without instruments and with strategy alt_proj / demean")
+        ooc = None
+        if out_of_core:
+            if not fe_cols or strategy not in ("auto", "alt_proj", "demean"):
+                raise ValueError("out_of_core fits take one or more FEs and strategy 'alt_proj' (or 'demean' for "
+                                 "one FE)")
+            src = data if stream else cols
+            n_oc = n_rows if stream else len(cols[y_col])
+            if n_oc > context_rows():
+                raise ValueError(f"{len(num_cols)} columns: a wide out-of-core fit takes at most {context_rows()} rows")
+            ooc = dict(source=src, n_rows=n_oc, chunk_rows=int(chunk_rows), plan=plan, x_base=x_base)
+        elif stream:  # a Parquet path read resident: the numeric columns too
+            cols.update(frame.get_columns(data, [c for c in num_cols if c not in cols]))
         return _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc, strategy, demean_tol,
-                         max_iter, formula, t_start, say, engine, device)
+                         max_iter, formula, t_start, say, engine, device, ooc)
 
     own_engine = engine is None
     eng = engine if engine is not None else Engine(_default_device() if device is None else device)
@@ -353,6 +365,30 @@ def _out_of_core_split(device, args, plan, x_base) -> LeanFEResult:
     return out[0]
 
 
+def _stream_chunks(source, cols, n_rows, chunk_rows, y_col, x_cols, instruments, plan, x_base, row_range=None,
+                   select=None):
+    """(row0, columns) per row chunk of an out-of-core source (a Parquet path, re-read per pass, or
+    in-memory arrays): [y] + x_cols + instruments, the factor / interaction columns of x_cols (after
+    ``x_base``) formed from the chunk by ``plan``; ``select``: only these indices of that list."""
+    base = [y_col] + list(x_cols if plan is None else x_base)
+    read = list(dict.fromkeys(base + (plan.numeric_sources if plan else []) + list(instruments)))
+
+    def assemble(b, rows):
+        out = [np.asarray(b[c], dtype=np.float64) for c in base]
+        if plan is not None:
+            out += plan.columns(cols, b, rows)
+        out += [np.asarray(b[z], dtype=np.float64) for z in instruments]
+        return out if select is None else [out[i] for i in select]
+
+    if isinstance(source, str):
+        for row0, b in frame.stream_parquet(source, read, batch_rows=chunk_rows, row_range=row_range):
+            yield row0, assemble(b, slice(row0, row0 + len(b[y_col])))
+    else:
+        for r0 in range(0, n_rows, chunk_rows):
+            b = {c: source[c][r0:r0 + chunk_rows] for c in read}
+            yield r0, assemble(b, slice(r0, r0 + len(b[y_col])))
+
+
 def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_cols, codes, levels, w, cluster_cols,
                      v, vcov, ssc, demean_tol, max_iter, chunk_rows, formula, t_start, say,
                      sharded=False, plan=None, x_base=None, row_range=None) -> LeanFEResult:
@@ -374,23 +410,9 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
     num_cols = [y_col] + list(x_cols) + list(instruments)
     p, k, mz = len(num_cols), len(x_cols), len(instruments)
     say("Using FWL/alternating projections strategy (out-of-core columns)...")
-    base = [y_col] + list(x_cols if plan is None else x_base)
-    read = list(dict.fromkeys(base + (plan.numeric_sources if plan else []) + list(instruments)))
-
-    def assemble(b, rows):
-        out = [np.asarray(b[c], dtype=np.float64) for c in base]
-        if plan is not None:
-            out += plan.columns(cols, b, rows)
-        return out + [np.asarray(b[z], dtype=np.float64) for z in instruments]
 
     def chunks():
-        if isinstance(source, str):
-            for row0, b in frame.stream_parquet(source, read, batch_rows=chunk_rows, row_range=row_range):
-                yield row0, assemble(b, slice(row0, row0 + len(b[y_col])))
-        else:
-            for r0 in range(0, n_rows, chunk_rows):
-                b = {c: source[c][r0:r0 + chunk_rows] for c in read}
-                yield r0, assemble(b, slice(r0, r0 + len(b[y_col])))
+        return _stream_chunks(source, cols, n_rows, chunk_rows, y_col, x_cols, instruments, plan, x_base, row_range)
 
     t0 = time.perf_counter()
     eng.load_codes(codes, levels, p, weights=w)  # a sharded engine: this rank's rows (global codes)
@@ -465,7 +487,7 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
 
 
 def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc, strategy, demean_tol, max_iter,
-              formula, t_start, say, engine=None, device=None) -> LeanFEResult:
+              formula, t_start, say, engine=None, device=None, ooc=None) -> LeanFEResult:
     """A fit of more than 63 columns (e.g. an event study's i(year) dummies, polars_impl.py:27-69,
     whose X'X the reference forms at any width, :165-209): the columns run in blocks of engine
     contexts - the first [y] + 62 regressors with the stop test, every later one 63 regressors
@@ -473,14 +495,17 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
     :491-508) - and each block writes its demeaned columns into one device matrix D = [1_kept, y~,
     x~] (input row order, lfe_materialize).  The Gram, the residual, the HC1 meat and the cluster
     score sums then come from D (lfe_wide.hip), the solve and the sandwiches from the host as in
-    the resident fit (inference.py, std_errors.py:183-441)."""
+    the resident fit (inference.py, std_errors.py:183-441).  ``ooc`` (out-of-core source: the
+    arguments of _stream_chunks): every block is a streamed context - group sums from one pass over
+    its columns, codes-only sweeps, then a second pass writes its x~ into D (lfe_stream_materialize) -
+    so the columns are never resident twice; D itself (P n doubles) stays on the device."""
     k = len(x_cols)
     P = 2 + k
     w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
-    y = np.asarray(cols[y_col], dtype=np.float64)
-    n = y.size
+    y = None if ooc is not None else np.asarray(cols[y_col], dtype=np.float64)
+    n = ooc["n_rows"] if ooc is not None else y.size
     ldD = (n + 63) // 64 * 64
-    per = MAX_CONTEXT_COLS
+    per = MAX_CONTEXT_COLS - (1 if ooc is not None and w is not None else 0)  # streamed weighted sums: p <= 62
     blocks = [x_cols[:per - 1]] + [x_cols[j:j + per] for j in range(per - 1, k, per)]
     dev = _default_device() if device is None else device
     eng = engine if engine is not None else Engine(dev)
@@ -508,9 +533,23 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
         for b, xb in enumerate(blocks):
             e = eng if b == 0 else Engine(eng.device)
             try:
-                colsb = ([y] if b == 0 else []) + [np.asarray(cols[c], dtype=np.float64) for c in xb]
-                e.load(colsb, codes, levels, w)
+                pb = len(xb) + (1 if b == 0 else 0)
+                if ooc is None:
+                    colsb = ([y] if b == 0 else []) + [np.asarray(cols[c], dtype=np.float64) for c in xb]
+                    e.load(colsb, codes, levels, w)
+                else:
+                    # the block's indices in [y] + x_cols: block 0 holds y and x[0:62], block b the next 63
+                    lo = 0 if b == 0 else col0 - 1
+                    sel = list(range(lo, lo + pb))
+
+                    def chunks(sel=sel):
+                        return _stream_chunks(ooc["source"], cols, n, ooc["chunk_rows"], y_col, x_cols, [],
+                                              ooc["plan"], ooc["x_base"], select=sel)
+
+                    e.load_codes(codes, levels, pb, weights=w)
                 n_obs, fe_dims, fe_card = e.drop_singletons()
+                if ooc is not None:
+                    e.stream_pass(1, chunks())
                 if strategy == "demean":
                     it, _ = e.demean([0], demean_tol, max_iter, check_from=0)
                     iterations = 1
@@ -522,8 +561,11 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
                         e.demean(order, 0.0, iterations, check_from=3)
                 else:
                     e.demean([], demean_tol, max_iter, check_from=0)
-                e.materialize(D, ldD, 0, col0, 0 if b == 0 else -1)
-                col0 += len(colsb)
+                if ooc is None:
+                    e.materialize(D, ldD, 0, col0, 0 if b == 0 else -1)
+                else:
+                    e.stream_materialize(D, ldD, col0, chunks(), 0 if b == 0 else -1)
+                col0 += pb
                 e.sync()
             finally:
                 if b > 0:

@@ -83,3 +83,51 @@ def test_column_blocks_equal_the_one_context_fit(vcov, F, monkeypatch):
                                atol=0)
     if cl:
         assert tuple(wide.n_clusters) == tuple(one.n_clusters)
+
+
+@pytest.mark.parametrize("vcov,cl,weighted", [("HC1", None, False), ("cluster", ["fe1", "fe2"], True)])
+def test_streamed_wide_fit(vcov, cl, weighted):
+    """k = 80 out of core: every block is a streamed context (group sums from one pass, codes-only
+    sweeps, lfe_stream_materialize into D); against the resident wide fit and the oracle."""
+    from leanfe_amd import leanfe_hip
+    from oracle import altproj
+
+    n, k, L = 120_001, 80, [2_500, 150]
+    d = dict(synth.panel(n, k, L, seed=21))
+    kw = {}
+    if weighted:
+        d["w"] = np.random.default_rng(21).uniform(0.5, 2.0, n)
+        kw["weights"] = "w"
+    xs = [f"x{j + 1}" for j in range(k)]
+    args = dict(y_col="y", x_cols=xs, fe_cols=["fe1", "fe2"], strategy="alt_proj", vcov=vcov, cluster_cols=cl,
+                quiet=True, **kw)
+    oc = leanfe_hip(d, out_of_core=True, chunk_rows=50_000, **args)
+    res = leanfe_hip(d, **args)
+    o = altproj.fit(d, "y", xs, ["fe1", "fe2"], vcov=vcov, cluster_cols=cl, weights=kw.get("weights"))
+    _check(oc, o, xs)
+    assert oc.iterations == res.iterations and oc.n_obs == res.n_obs
+    np.testing.assert_allclose([oc.coefs[x] for x in xs], [res.coefs[x] for x in xs], rtol=1e-11, atol=0)
+    np.testing.assert_allclose([oc.std_errors[x] for x in xs], [res.std_errors[x] for x in xs], rtol=1e-11, atol=0)
+
+
+def test_streamed_wide_event_study_from_parquet(tmp_path):
+    """A Parquet source, out of core, y ~ x1 + x2 + i(year) with 70 years: the dummies are formed
+    chunk by chunk from the streamed rows (frame.Expansion) for both blocks."""
+    pa = pytest.importorskip("pyarrow")
+    import pyarrow.parquet as pq
+
+    from leanfe_amd import frame, leanfe_hip
+    from oracle import altproj
+
+    n, L = 150_000, [3_000, 120]
+    d = dict(synth.panel(n, 2, L, seed=34))
+    d["year"] = np.random.default_rng(34).integers(1950, 2020, n)
+    path = str(tmp_path / "wide.parquet")
+    pq.write_table(pa.table({c: np.asarray(v) for c, v in d.items()}), path, row_group_size=40_000)
+    r = leanfe_hip(path, formula="y ~ x1 + x2 + i(year) | fe1 + fe2", strategy="alt_proj", vcov="HC1", quiet=True,
+                   out_of_core=True, chunk_rows=40_000)
+    full = dict(d)
+    xs = ["x1", "x2"] + frame.expand_factors(full, [("year", None)])
+    assert list(r.coefs) == xs and len(xs) == 71
+    o = altproj.fit(full, "y", xs, ["fe1", "fe2"], vcov="HC1")
+    _check(r, o, xs)

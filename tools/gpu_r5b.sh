@@ -1,15 +1,17 @@
 #!/bin/bash
-# round 5: row-per-lane group sums - parity subset, then A/B against the MFMA lane form
+# round 5: parity of the new paths (streamed factors / contexts, wide fits, sort-free cluster sums,
+# row-per-lane group sums), the 3e9-row run, then the A/B of gpu_r5c.sh.  Test failures (rc 1) do
+# not stop the script; anything else (timeout, abort, fault) does.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_stream.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 600 python -m pytest tests/test_gpu_stream.py -q --timeout 300 --timeout-method thread -p no:cacheprovider \
   -k "factor or split or contexts" > gpurun_out/pytest_r5a.log 2>&1
 rc=$?; echo "stream pytest rc=$rc"; tail -2 gpurun_out/pytest_r5a.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 800 python -m pytest tests/test_gpu_wide.py tests/test_gpu_clusters.py tests/test_gpu_dense.py tests/test_gpu_determinism.py tests/test_gpu_configs.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r5b.log 2>&1
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 900 python -m pytest tests/test_gpu_wide.py tests/test_gpu_clusters.py tests/test_gpu_dense.py tests/test_gpu_determinism.py tests/test_gpu_configs.py -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r5b.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_r5b.log
-[ $rc -eq 0 ] || exit $rc
+[ $rc -le 1 ] || exit $rc
 timeout -k 10 400 python tools/oocore_run.py --rows 3000000000 --contexts 2 --chunk 50000000 --chunk2 70000000 \
   > gpurun_out/oocore_3000m.json 2> gpurun_out/oocore_3000m.err
 rc=$?; echo "oocore rc=$rc"; tail -c 2500 gpurun_out/oocore_3000m.json; tail -5 gpurun_out/oocore_3000m.err
