@@ -330,10 +330,11 @@ __global__ void k_wide_stats(const double* __restrict__ partial, int nblk, doubl
 // cluster score sums over per-row cluster ids: two-limb fixed point (lfe_cluster.hip's form)
 // ---------------------------------------------------------------------------
 constexpr int kWcChunk = 8192;
+constexpr int kWcCols = 64;  // score columns per fixed-point pass (the statistics head and quanta table width)
 struct WideScoreArgs {
   const double* D;
   int64_t ldD, n;
-  int c0, k;           // score columns: D's [c0, c0 + k) times e = r (w)
+  int c0, k;           // score columns: D's [c0, c0 + k) times e = r (w) (one pass: k <= kWcCols)
   const double* r;
   const double* w;
   const int32_t* cid;  // cluster id of every row (-1: not in any cluster)
@@ -349,8 +350,9 @@ __global__ __launch_bounds__(256) void k_wc_stats(WideScoreArgs a, int nchunks, 
   __shared__ double ws[2][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t i0 = (int64_t)blockIdx.x * kWcChunk, i1 = min(a.n, i0 + kWcChunk);
-  for (int64_t i = i0 + tid; i < i1; i += 256)
-    if (a.cid[i] >= 0) atomicAdd(&cnt[a.cid[i]], 1);
+  if (cnt)  // the first column pass counts the rows per cluster
+    for (int64_t i = i0 + tid; i < i1; i += 256)
+      if (a.cid[i] >= 0) atomicAdd(&cnt[a.cid[i]], 1);
   const auto fmaxop = [](double x, double y) { return fmax(x, y); };
   const auto addop = [](double x, double y) { return x + y; };
   for (int c = 0; c < a.k; ++c) {
@@ -516,6 +518,8 @@ int lfe_wide_cluster_meats(lfe_ctx* c, const double* D, int64_t ldD, int c0, int
     if (masks[s] <= 0 || masks[s] >= (1 << m)) return fail(LFE_EINVAL, "subset mask must select loaded cluster columns");
   const int64_t n = c->n;
   int32_t* cid = nullptr;
+  double* full = nullptr;  // k > kWcCols: the [G][k] table assembled from the column passes
+  size_t full_cap = 0;
   LFE_TRY(walloc(&cid, (size_t)std::max<int64_t>(n, 1)));
   int rc = LFE_OK;
   for (int s = 0; s < n_subsets && rc == LFE_OK; ++s) {
@@ -524,47 +528,67 @@ int lfe_wide_cluster_meats(lfe_ctx* c, const double* D, int64_t ldD, int c0, int
     if (rc != LFE_OK) break;
     auto& W = c->clw;
     const int nch = (int)std::max<int64_t>(1, (n + kWcChunk - 1) / kWcChunk);
-    const size_t tab = (size_t)std::max(G, 1) * k;
-    rc = ensure_f64(c, W.fixst, W.fixst_cap, (size_t)kColStatHead + (size_t)k * nch);
+    const int kg_max = std::min(k, kWcCols);
+    const size_t tab = (size_t)std::max(G, 1) * kg_max;
+    rc = ensure_f64(c, W.fixst, W.fixst_cap, (size_t)kColStatHead + (size_t)kg_max * nch);
     if (rc == LFE_OK) rc = ensure_f64(c, W.fixq, W.fixq_cap, (size_t)kFqRows * kFqCols);
     if (rc == LFE_OK) rc = ensure_cluster_ws(c, tab, (size_t)G + 4);
     if (rc == LFE_OK) rc = ensure_f64(c, W.srec, W.srec_cap, tab);
+    if (rc == LFE_OK && k > kWcCols && (size_t)std::max(G, 1) * k > full_cap) {
+      (void)hipStreamSynchronize(c->stream);  // an earlier subset's table may still be read
+      dfree_any(full);
+      full = nullptr;
+      full_cap = (size_t)std::max(G, 1) * k;
+      rc = walloc(&full, full_cap);
+    }
     if (rc != LFE_OK) break;
     int32_t* cnt = c->clP;
     int32_t* cm = c->clP + G;
-    hipMemsetAsync(W.fixst, 0, sizeof(double) * kColStatHead, c->stream);
     hipMemsetAsync(cnt, 0, sizeof(int32_t) * ((size_t)G + 4), c->stream);
-    hipMemsetAsync(c->clS, 0, sizeof(double) * tab, c->stream);
-    hipMemsetAsync(W.srec, 0, sizeof(double) * tab, c->stream);
-    WideScoreArgs a{D, ldD, n, c0, k, r, c->w, cid};
-    {
-      ProfScope _ps(c, K_CLUSTER_SCATTER);
-      if (n > 0) hipLaunchKernelGGL(k_wc_stats, dim3(nch), dim3(256), 0, c->stream, a, nch, cnt, W.fixst);
-      hipLaunchKernelGGL(k_wc_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, cnt, G, cm);
+    // columns in passes of <= 64 (one quanta table each); a wider table is assembled in `full`
+    for (int cb = 0; cb < k && rc == LFE_OK; cb += kWcCols) {
+      const int kg = std::min(kWcCols, k - cb);
+      hipMemsetAsync(W.fixst, 0, sizeof(double) * kColStatHead, c->stream);
+      hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream);
+      hipMemsetAsync(W.srec, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream);
+      WideScoreArgs a{D, ldD, n, c0 + cb, kg, r, c->w, cid};
+      {
+        ProfScope _ps(c, K_CLUSTER_SCATTER);
+        if (n > 0)
+          hipLaunchKernelGGL(k_wc_stats, dim3(nch), dim3(256), 0, c->stream, a, nch, cb == 0 ? cnt : nullptr, W.fixst);
+        if (cb == 0) hipLaunchKernelGGL(k_wc_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, cnt, G, cm);
+      }
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        set_error(std::string("wide cluster sums: ") + hipGetErrorString(e));
+        rc = LFE_EHIP;
+        break;
+      }
+      rc = launch_fix_quanta(c, W.fixst, nch, std::max<int64_t>(n, 1), cm + 1, 1, W.fixq, kg);
+      if (rc != LFE_OK) break;
+      if (n > 0) {
+        ProfScope _ps(c, K_CLUSTER_SCATTER);
+        hipLaunchKernelGGL(k_wc_add, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, a, W.fixq,
+                           reinterpret_cast<unsigned long long*>(W.srec), c->clS);
+      }
+      rc = launch_fix_convert(c, W.srec, c->clS, (int64_t)G * kg, kg, W.fixq);
+      if (rc == LFE_OK && full && G > 0) {  // [G][kg] -> columns cb.. of the [G][k] table
+        const hipError_t e2 = hipMemcpy2DAsync(full + cb, sizeof(double) * k, W.srec, sizeof(double) * kg,
+                                               sizeof(double) * kg, (size_t)G, hipMemcpyDeviceToDevice, c->stream);
+        if (e2 != hipSuccess) rc = fail(LFE_EHIP, "wide cluster sums: hipMemcpy2DAsync");
+      }
     }
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-      set_error(std::string("wide cluster sums: ") + hipGetErrorString(e));
-      rc = LFE_EHIP;
-      break;
-    }
-    rc = launch_fix_quanta(c, W.fixst, nch, std::max<int64_t>(n, 1), cm + 1, 1, W.fixq, k);
     if (rc != LFE_OK) break;
-    if (n > 0) {
-      ProfScope _ps(c, K_CLUSTER_SCATTER);
-      hipLaunchKernelGGL(k_wc_add, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, a, W.fixq,
-                         reinterpret_cast<unsigned long long*>(W.srec), c->clS);
-    }
-    rc = launch_fix_convert(c, W.srec, c->clS, (int64_t)G * k, k, W.fixq);
     int32_t hG = 0;
-    if (rc == LFE_OK) rc = d2h_sync(c, &hG, cm, sizeof(int32_t));
+    rc = d2h_sync(c, &hG, cm, sizeof(int32_t));
     if (rc != LFE_OK) break;
     G_out[s] = hG;
     // S' S of the row-major [G][k] table: element (row g, column j) at S[j + g k]
-    rc = wide_syrk(c, W.srec, 1, k, G, k, 0, nullptr, nullptr, meats_out + (size_t)s * k * k);
+    rc = wide_syrk(c, full ? full : W.srec, 1, k, G, k, 0, nullptr, nullptr, meats_out + (size_t)s * k * k);
   }
   (void)hipStreamSynchronize(c->stream);
   dfree_any(cid);
+  dfree_any(full);
   return rc;
 }
 

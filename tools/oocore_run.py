@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 def fit(eng, n, k, L, beta, chunk, seed, row0=0):
     from leanfe_amd import inference
+    from leanfe_amd._lib import NeedsStreamPass
     t = {}
     t0 = time.perf_counter()
     eng.synth_load_codes(n, k, L, seed=seed, row0=row0)
@@ -43,7 +44,10 @@ def fit(eng, n, k, L, beta, chunk, seed, row0=0):
     t["pass1_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     it, _ = eng.demean(sorted(range(2), key=lambda i: card[i]), 1e-6, 50, check_from=3)
-    G = eng.gram()
+    try:
+        G = eng.gram()
+    except NeedsStreamPass:  # several contexts (ranks' raw tiles have their own shifts): the design-Gram pass
+        G = eng.stream_synth_pass(3, k, L, beta, chunk_rows=chunk, seed=seed)[:(k + 2) ** 2].reshape(k + 2, k + 2)
     t["demean_gram_s"] = time.perf_counter() - t0
     XtX, Xty = inference.split_gram(G)
     bf, XtX_inv = inference.solve_normal(XtX, Xty)
