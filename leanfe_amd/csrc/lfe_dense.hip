@@ -1050,7 +1050,6 @@ __device__ __forceinline__ void dn8_wave_stream(const Dn8Args& a, const int8_t* 
 
 // K1, persistent: the digit tiles of alpha_Q formed in LDS by every workgroup, then workgroup i takes
 // output blocks [i T / grid, (i + 1) T / grid) of the T = nbe x B/16 primary blocks, wave w every 16th
-template <bool PRE>  // PRE: the digit tiles come from k_dn8_digits (a.dq / a.eq)
 __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
   extern __shared__ __attribute__((aligned(16))) int8_t fr[];  // [ntile][8 kb][8 d][1 KB]
   __shared__ double red[1024 + 16];
@@ -1065,24 +1064,14 @@ __global__ __launch_bounds__(1024) void k_dn8_k1s(Dn8Args a) {
   const int ntile = (a.nkb + 7) / 8;
   for (int t = 0; t < ntile; ++t) {
     if (t) __syncthreads();
-    auto mid = [&]() {
-      if (t == 0) dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
-    };
-    if (PRE) {  // the tile's digits formed once (k_dn8_digits): a 64 KB copy from L2 instead
-      const int4* s4 = reinterpret_cast<const int4*>(a.dq + (int64_t)t * kDn8TileBytes);
-      int4* d4p = reinterpret_cast<int4*>(fr + (size_t)t * kDn8TileBytes);
-      int4 tmp[kDn8TileBytes / 16 / 1024];
-#pragma unroll
-      for (int u = 0; u < kDn8TileBytes / 16 / 1024; ++u) tmp[u] = s4[u * 1024 + tid];
-      mid();
-#pragma unroll
-      for (int u = 0; u < kDn8TileBytes / 16 / 1024; ++u) d4p[u * 1024 + tid] = tmp[u];
-      if (tid < 16) sc[16 * t + tid] = a.eq[t * 16 + tid];
-    } else {
-      dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.lda, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p, a.lda,
-                            fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red, mid, nullptr,
-                            blockIdx.x == 0 ? a.rflag : nullptr);  // every workgroup forms the same digits
-    }
+    // every workgroup forms the same digits (measured faster than one k_dn8_digits pass whose
+    // 64 KB tiles every workgroup copies: 0.448 vs 0.474 ms per config-1 solve, round 5)
+    dn8_tile_digits<1024>(a.alpha + (int64_t)t * kDn8Tile * a.lda, min(kDn8Tile, a.G_Q - t * kDn8Tile), a.p, a.lda,
+                          fr + (size_t)t * kDn8TileBytes, sc + 16 * t, red,
+                          [&]() {
+                            if (t == 0) dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
+                          },
+                          nullptr, blockIdx.x == 0 ? a.rflag : nullptr);
   }
   if (ntile == 0) dn8_ring_fill(a, R, 0, i0 + wave, W, i1, lane);
   __syncthreads();
@@ -1423,10 +1412,8 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
     a.zero_check = zero_check;
     if (nkb <= kDn8MaxKb && !dn8_tiled()) {  // persistent streaming form (LFE_DN8_TILED=1: A/B)
       const size_t lds = (size_t)ntile * kDn8TileBytes;
-      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k1s<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k1s<false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k1s), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
       const int64_t total = (int64_t)std::max(c->nbe, 1) * a.nrb;
       const int grid = (int)std::min<int64_t>(c->n_cu, (total + 15) / 16);
       if (dn8_timing()) {
@@ -1438,18 +1425,6 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
       }
       // wide fits: one pass per 16-column group (each projects its own columns of alpha_P)
       const int p = c->p;
-      // the digit tiles formed once by k_dn8_digits and copied by every workgroup (LFE_DN8_PRE=0:
-      // each workgroup digitizes alpha_Q itself): ~2 us of copy in place of a ~16 us prologue
-      static const bool pre = [] {
-        const char* e = getenv("LFE_DN8_PRE");
-        return !(e && e[0] == '0');
-      }();
-      if (pre) {
-        LFE_TRY(ensure_i8(c, c->dn8_dq, c->dn8_dq_cap, (size_t)ntile * kDn8TileBytes));
-        LFE_TRY(ensure_f64(c, c->dn8_eq, c->dn8_eq_cap, (size_t)ntile * 16));
-        LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_digits),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, kDn8TileBytes));
-      }
       for (int c0 = 0; c0 < p; c0 += 16) {
         Dn8Args g = a;
         g.p = std::min(16, p - c0);
@@ -1457,16 +1432,7 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
         g.S_P = a.S_P + c0;
         g.alphaP = a.alphaP + c0;
         if (c0) g.zero_check = nullptr;
-        if (pre) {
-          hipLaunchKernelGGL(k_dn8_digits, dim3(ntile), dim3(256), kDn8TileBytes, c->stream, g.alpha, a.G_Q, g.p,
-                             a.lda, c->dn8_dq, c->dn8_eq, a.rflag);
-          g.dq = c->dn8_dq;
-          g.eq = c->dn8_eq;
-        } else {
-          g.dq = nullptr;
-        }
-        if (pre) hipLaunchKernelGGL(k_dn8_k1s<true>, dim3(grid), dim3(1024), lds, c->stream, g);
-        else hipLaunchKernelGGL(k_dn8_k1s<false>, dim3(grid), dim3(1024), lds, c->stream, g);
+        hipLaunchKernelGGL(k_dn8_k1s, dim3(grid), dim3(1024), lds, c->stream, g);
         LFE_HIP(hipGetLastError());
       }
       if (a.dbg) return dn8_timing_report(c, "K1", grid);

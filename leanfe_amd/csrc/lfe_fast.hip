@@ -424,148 +424,6 @@ __global__ __launch_bounds__(TH) void k_sums2_raw(Sums4Args a) {
   else sums2_raw_body<TH, NACC, GU, false>(a, lds, rred);
 }
 
-// The same sums in the residual pass's row-per-lane form (lfe_gram.hip k_resid_rows): a lane owns
-// one row, so each column is read with contiguous loads across the wave (the MFMA lane layout
-// above gives a 16-byte load 64 bytes from each of 16 columns, and its loads ran at 5.2 TB/s
-// against the residual pass's 6.2), the fine limbs go into the same LDS tables by LDS atomics, and
-// the raw Gram of [z, 1] (z = x - shift) accumulates on VALU FMAs: the upper triangle of z z'
-// (PM (PM + 1) / 2 sums), the column sums and the row count, reduced per wave over DPP lane moves
-// and written in the [16][16] tile order of the MFMA form (slot 15 = intercept), so the epilogue
-// and the Gram from the tables are unchanged.  PM >= p (every sum stays in registers up to 11).
-constexpr int kSumRowThreads = 512;
-
-template <int PM, bool BIG>
-__device__ __forceinline__ void sums2_rows_body(const Sums4Args& a, double* __restrict__ lds,
-                                                double* __restrict__ rred) {
-  constexpr int NM = PM * (PM + 1) / 2;  // z z' upper triangle
-  constexpr int NS = NM + PM + 1;        // + column sums + row count
-  constexpr int NW = kSumRowThreads / 64;
-  typedef unsigned long long u64;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int p = a.la.p, P = a.la.P, Q = a.qf[0], s = a.la.s;
-  const int qoff = a.tab_off[Q];
-  double* const qtab = lds + qoff;
-  const int32_t* __restrict__ hP = a.la.code[P];
-  const int32_t* __restrict__ hQ = a.la.code[Q];
-  const double* __restrict__ X = a.X;
-  const int64_t ld = a.ld;
-  double acc[NS];
-#pragma unroll
-  for (int e = 0; e < NS; ++e) acc[e] = 0.0;
-  double* const hiP = a.hi[P];
-  double* const hiQ = a.hi[Q];
-  for (int j = tid; j < a.G[Q] * p; j += kSumRowThreads) lds[qoff + j] = 0.0;
-  for (int j = tid; j < a.B * p; j += kSumRowThreads) lds[j] = 0.0;
-  auto flush = [&](int b) {
-    const int lo = b << s;
-    for (int j = tid; j < a.B * p; j += kSumRowThreads) {
-      const int g = lo + j / p;
-      const u64 val = reinterpret_cast<const u64*>(lds)[j];
-      if (val != 0ull && g < a.G_P) atomicAdd(reinterpret_cast<u64*>(&a.S[P][(int64_t)g * p + (j % p)]), val);
-      lds[j] = 0.0;
-    }
-  };
-  const BlockRows br = block_rows(a.la.items, a.la.n_items, lane);
-  int cur = -1;
-  for (int item = br.first; item < a.la.n_items; ++item) {
-    int4 it = a.la.items[item];
-    if (it.y >= br.hi) break;
-    it.y = max(it.y, br.lo);
-    it.z = min(it.z, br.hi);
-    if (it.x != cur) {
-      __syncthreads();
-      if (cur >= 0) flush(cur);
-      __syncthreads();
-      cur = it.x;
-    }
-    const int lo = it.x << s;
-    for (int rb = it.y + wave * 64; rb < it.z; rb += NW * 64) {
-      const int r = rb + lane;
-      const bool in = r < it.z;
-      const int h = in ? hP[r] : -1;
-      const int q = in ? hQ[r] : 0;
-      double z[PM];
-#pragma unroll
-      for (int c = 0; c < PM; ++c) z[c] = (in && c < p) ? X[(int64_t)c * ld + r] : 0.0;
-      if (h < 0) continue;  // a dropped row, or past the item
-      u64* const sp = reinterpret_cast<u64*>(lds + (h - lo) * p);
-      u64* const qp = reinterpret_cast<u64*>(qtab + q * p);
-#pragma unroll
-      for (int c = 0; c < PM; ++c) {
-        if (c >= p) break;  // integer adds commute
-        const FixCol fc = fix_col(a.fixq, c);
-        u64 xi;
-        if (BIG) {
-          double hh;
-          xi = fix_split(z[c], fc, hh);
-          if (hh != 0.0) {  // an outlier (or a non-finite value): its coarse limb
-            atomicAdd(&hiP[(int64_t)h * p + c], hh);
-            atomicAdd(&hiQ[(int64_t)q * p + c], hh);
-          }
-        } else {
-          xi = (u64)__double_as_longlong(__builtin_fma(z[c] * fc.sf2, fc.sf, kFixMagic)) - kFixMagicBits;
-        }
-        atomicAdd(sp + c, xi);
-        atomicAdd(qp + c, xi);
-        z[c] -= X[(int64_t)c * ld];  // the shift: the layout's first row (uniform, from L1 / L2)
-      }
-      int e = 0;
-#pragma unroll
-      for (int i = 0; i < PM; ++i)
-#pragma unroll
-        for (int j = i; j < PM; ++j, ++e) acc[e] = __builtin_fma(z[i], z[j], acc[e]);
-#pragma unroll
-      for (int c = 0; c < PM; ++c) acc[NM + c] += z[c];
-      acc[NM + PM] += 1.0;
-    }
-  }
-  __syncthreads();
-  if (cur >= 0) flush(cur);
-  {  // the block's secondary table goes out whole (k_qpart_reduce sums the blocks in order)
-    const int64_t m = (int64_t)a.G[Q] * p;
-    double* dst = a.qpart + (int64_t)blockIdx.x * m;
-    for (int j = tid; j < m; j += kSumRowThreads) dst[j] = lds[qoff + j];
-  }
-  // raw tile: wave sums over DPP lane moves (fixed order), then the waves in order
-  const auto addop = [](double x, double y) { return x + y; };
-#pragma unroll
-  for (int e = 0; e < NS; ++e) {
-    const double v = wave_reduce63(acc[e], 0.0, addop);
-    if (lane == 63) rred[wave * NS + e] = v;
-  }
-  __syncthreads();
-  for (int t = tid; t < 256; t += kSumRowThreads) {
-    const int i = t >> 4, j = t & 15;
-    int e = -1;
-    if (i < PM && j < PM) {
-      const int lo2 = i < j ? i : j, hi2 = i < j ? j : i;
-      e = lo2 * PM - lo2 * (lo2 - 1) / 2 + (hi2 - lo2);
-    } else if (i < PM && j == 15) {
-      e = NM + i;
-    } else if (i == 15 && j < PM) {
-      e = NM + j;
-    } else if (i == 15 && j == 15) {
-      e = NM + PM;
-    }
-    double v = 0.0;
-    if (e >= 0)
-      for (int w = 0; w < NW; ++w) v += rred[w * NS + e];
-    a.raw_part[(int64_t)blockIdx.x * 256 + t] = v;
-  }
-}
-
-template <int PM>
-__global__ __launch_bounds__(kSumRowThreads) void k_sums2_rows(Sums4Args a) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  constexpr int NS = PM * (PM + 1) / 2 + PM + 1;
-  __shared__ double rred[(kSumRowThreads / 64) * NS];
-  bool any = false;
-  for (int j = 0; j < a.la.p; ++j) any = any || a.fixq[FQ_BIG * kFqCols + j] != 0.0;
-  if (any) sums2_rows_body<PM, true>(a, lds, rred);
-  else sums2_rows_body<PM, false>(a, lds, rred);
-}
-
 // ---------------------------------------------------------------------------
 // two-limb fixed-point group sums (lfe_internal.h): quanta from the column statistics
 // ---------------------------------------------------------------------------
@@ -1015,17 +873,6 @@ int sums4(lfe_ctx* c) {
     fn = two   ? reinterpret_cast<const void*>(&k_sums2_raw<1024, 4, 1>)
          : raw ? reinterpret_cast<const void*>(&k_sums4<1, 2, 1, 1024, true>)
                : SUMS4_FN(1, 2, 1, 1024);
-    // the row-per-lane form (k_sums2_rows) up to 12 columns (LFE_SUMS_ROWS=0: the MFMA lane form)
-    static const bool rows_on = [] {
-      const char* e = getenv("LFE_SUMS_ROWS");
-      return !(e && e[0] == '0');
-    }();
-    if (two && rows_on && p <= 11) {
-      threads = kSumRowThreads;
-      fn = p <= 4 ? reinterpret_cast<const void*>(&k_sums2_rows<4>)
-           : p <= 8 ? reinterpret_cast<const void*>(&k_sums2_rows<8>)
-                    : reinterpret_cast<const void*>(&k_sums2_rows<11>);
-    }
   } else if (a.nq <= 1) {
     fn = NT == 2 ? SUMS4_FN(1, 2, 2, kSumThreads) : NT == 3 ? SUMS4_FN(1, 2, 3, kSumThreads)
                                                     : SUMS4_FN(1, 2, 4, kSumThreads);

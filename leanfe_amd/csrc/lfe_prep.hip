@@ -14,7 +14,6 @@
 // ballots, so the layout is a pure function of the codes and the geometry.
 #include "lfe_internal.h"
 
-#include <cstdio>
 
 #include <algorithm>
 #include <cstdlib>
@@ -947,8 +946,6 @@ static int launch_part_scatter(lfe_ctx* c, int cols, int orig) {
   const bool o32 = (uint64_t)c->ld * 8 <= 0xffffffffull;
 #define PART_FN(PER, NTH) (o32 ? &k_part_scatter<PER, NTH, true> : &k_part_scatter<PER, NTH, false>)
   Fn fn = g.nth == 1024 ? (g.per == 16 ? PART_FN(16, 1024) : g.per == 8 ? PART_FN(8, 1024) : PART_FN(4, 1024))
-        : g.per == 36   ? PART_FN(36, 512)
-        : g.per == 32   ? PART_FN(32, 512)
         : g.per == 16   ? PART_FN(16, 512)
                         : PART_FN(8, 512);
 #undef PART_FN
@@ -1071,20 +1068,7 @@ int prepare_layout(lfe_ctx* c) {
     const int nth = part_lds(1024) <= 150 * 1024 ? 1024 : 512;
     if (cw == 16384 && nth != 1024) cw = 8192;
     if (part_lds(nth) > 150 * 1024) cw = 4096;
-    int per = (int)(cw / nth);
-    if (const char* e = getenv("LFE_PART_GEOM")) {  // A/B only: "512,36" (18432-row chunks on 8 waves)
-      int t = 0, q = 0;
-      if (sscanf(e, "%d,%d", &t, &q) == 2 && t == 512 && (q == 32 || q == 36) && n >= (int64_t)t * q) {
-        const int64_t cw2 = (int64_t)t * q;
-        const size_t lds2 = sizeof(double) * cw2 + sizeof(uint16_t) * (((size_t)(t / 64) * nb + 1) & ~(size_t)1) +
-                            sizeof(int32_t) * (2 * (size_t)nb + 1);
-        if (lds2 <= 156 * 1024) {
-          cw = cw2;
-          per = q;
-        }
-      }
-    }
-    const int nth_eff = (int)(cw / per);
+    const int per = (int)(cw / nth);
     const int nw = (int)((n + cw - 1) / cw);
     // column statistics of the exact group sums, written by the scatter (max |x| by atomicMax)
     LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nw * c->p));
@@ -1103,8 +1087,8 @@ int prepare_layout(lfe_ctx* c) {
     int32_t* dbstart = c->pcounts + m;
     LFE_TRY(exclusive_scan_g(c, c->pcounts, m, nullptr, 0, dbstart, nw, nb));
     LFE_TRY(d2h_async(c, dbstart, sizeof(int32_t) * nb));
-    const size_t lds = std::min<size_t>(std::max(part_lds(nth_eff), kLdsMin), 160 * 1024);
-    L.part = PartGeom{nth_eff, per, nw, lds};
+    const size_t lds = std::min<size_t>(std::max(part_lds(nth), kLdsMin), 160 * 1024);
+    L.part = PartGeom{nth, per, nw, lds};
     // the input row index of each layout row is written only when a caller needs it
     // (ensure_layout_orig: cluster, records and demeaned-column export paths)
     // loaded cluster columns (clustered SEs follow this solve) move with the codes: no later

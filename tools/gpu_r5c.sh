@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 5: A/B on one box - group-sums form, partition geometry, K1 digit source - on the headline,
-# config 1 and the 8-rank owner shard
+# A/B on one box: the headline, config 1 and the 8-rank owner shard, with optional env overrides
+# (AB_ENV="NAME=VALUE ..." for the variant runs), two repetitions each
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
@@ -12,12 +12,11 @@ run() {  # label, bench args (quoted), env...
 }
 for rep in 1 2; do
   run base$rep ""
-  run mfma$rep "" LFE_SUMS_ROWS=0
-  run g36_$rep "" LFE_PART_GEOM=512,36
-  run g32_$rep "" LFE_PART_GEOM=512,32
-  run k1own$rep "" LFE_DN8_PRE=0
   run c1_$rep "--config 1"
-  run c1own$rep "--config 1" LFE_DN8_PRE=0
   run e8_$rep "--emulate-rank 0/8"
-  run e8own$rep "--emulate-rank 0/8" LFE_DN8_PRE=0
+  if [ -n "${AB_ENV:-}" ]; then
+    run var$rep "" $AB_ENV
+    run c1var$rep "--config 1" $AB_ENV
+    run e8var$rep "--emulate-rank 0/8" $AB_ENV
+  fi
 done
