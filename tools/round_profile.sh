@@ -8,8 +8,9 @@ mkdir -p gpurun_out
 python -m leanfe_amd.build > gpurun_out/build.log 2>&1 || { echo build failed; exit 1; }
 python -c "from oracle.altproj_c import build; build()" || exit 1
 step() { local rc=$1 name=$2; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
-timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest.log 2>&1
-step $? pytest; tail -2 gpurun_out/pytest.log
+timeout -k 10 840 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread \
+  > gpurun_out/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest.log; [ $rc -le 1 ] || exit $rc  # failures: still profile
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 step $? bench; tail -c 2500 gpurun_out/bench.log
 export TMPDIR=/tmp
