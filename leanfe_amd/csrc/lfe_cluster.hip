@@ -561,38 +561,38 @@ int cluster_ids_input(lfe_ctx* c, int mask, const double* kept, int32_t* cid, in
 constexpr int kClFixChunk = 8192;
 
 // the score columns' statistics in the colstat form of lfe_fast.hip (max |s_c| bits by u64
-// atomicMax; the chunk's sum of s_c^2 in fixed lane / wave order) and the clusters' kept-row counts
+// atomicMax; the chunk's sum of s_c^2 in fixed order) and the clusters' kept-row counts.  Thread t
+// reads column t % k of rows t / k, t / k + R, ... (R = 256 / k rows per step): the row-major score
+// rows are read in contiguous runs, each thread's sums in row order, then the R partials of a
+// column in thread order.
 __global__ __launch_bounds__(256) void k_clfix_stats(const int32_t* __restrict__ code, const int32_t* __restrict__ keep,
                                                      int64_t n, const double* __restrict__ U, int k, int nchunks,
                                                      int32_t* __restrict__ cnt, double* __restrict__ st) {
-  __shared__ double ws[2][4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ double wm[256], wq[256];
+  const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * kClFixChunk, r1 = min(n, r0 + kClFixChunk);
   for (int64_t i = r0 + tid; i < r1; i += 256)
     if (!keep || keep[i] >= 0) atomicAdd(&cnt[code[i]], 1);
-  const auto fmaxop = [](double x, double y) { return fmax(x, y); };
-  const auto addop = [](double x, double y) { return x + y; };
-  for (int c = 0; c < k; ++c) {
-    double m = 0.0, q = 0.0;
-    for (int64_t i = r0 + tid; i < r1; i += 256) {
+  const int R = 256 / k, c = tid % k, ro = tid / k;
+  double m = 0.0, q = 0.0;
+  if (ro < R)
+    for (int64_t i = r0 + ro; i < r1; i += R) {
       if (keep && keep[i] < 0) continue;
       const double v = U[i * k + c];
       m = fmax(m, fabs(v));
       q = __builtin_fma(v, v, q);
     }
-    m = wave_reduce63(m, 0.0, fmaxop);
-    q = wave_reduce63(q, 0.0, addop);
-    if (lane == 63) {
-      ws[0][wave] = m;
-      ws[1][wave] = q;
+  wm[tid] = m;
+  wq[tid] = q;
+  __syncthreads();
+  if (tid < k) {
+    double M = 0.0, Q = 0.0;
+    for (int j = 0; j < R; ++j) {
+      M = fmax(M, wm[tid + j * k]);
+      Q += wq[tid + j * k];
     }
-    __syncthreads();
-    if (tid == 0) {
-      const double mm = fmax(fmax(ws[0][0], ws[0][1]), fmax(ws[0][2], ws[0][3]));
-      st[kColStatHead + (int64_t)c * nchunks + blockIdx.x] = ((ws[1][0] + ws[1][1]) + ws[1][2]) + ws[1][3];
-      atomicMax(reinterpret_cast<unsigned long long*>(st) + c, (unsigned long long)__double_as_longlong(mm));
-    }
-    __syncthreads();
+    st[kColStatHead + (int64_t)tid * nchunks + blockIdx.x] = Q;
+    atomicMax(reinterpret_cast<unsigned long long*>(st) + tid, (unsigned long long)__double_as_longlong(M));
   }
 }
 
@@ -607,21 +607,73 @@ __global__ void k_clfix_count(const int32_t* __restrict__ cnt, int32_t G, int32_
   if (mx) atomicMax(&out[1], mx);
 }
 
-// every kept score value into its cluster's entry: fine limb (int64 bits) and coarse limb
-__global__ void k_clfix_add(const int32_t* __restrict__ code, const int32_t* __restrict__ keep, int64_t n,
-                            const double* __restrict__ U, int k, const double* __restrict__ fq,
-                            unsigned long long* __restrict__ S, double* __restrict__ hi) {
-  const int64_t m = n * k;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = e / k;
-    const int c = (int)(e - i * k);
-    if (keep && keep[i] < 0) continue;
-    double hh;
-    const unsigned long long xi = fix_split(U[e], fix_col(fq, c), hh);
-    const int64_t t = (int64_t)code[i] * k + c;
-    if (xi) atomicAdd(&S[t], xi);
-    if (hh != 0.0) atomicAdd(&hi[t], hh);
+// every kept score value into its cluster's entry, fine limbs first into an LDS window of the
+// table: the whole [G][k] table (a small G), or - the cluster column being the layout's primary FE -
+// the [B][k] slice of the work item's bucket (items run bucket by bucket, like the group sums of
+// lfe_fast.hip).  A window goes out by int64 global adds of its nonzero entries when the bucket
+// changes and at the end; coarse limbs (outliers) go to the global f64 table directly.
+constexpr int kClFixThreads = 1024;
+constexpr size_t kClFixLds = 96 * 1024;
+struct ClFixAdd {
+  const int32_t* code;  // cluster codes (layout order)
+  const int32_t* keep;  // the primary FE's codes (< 0: dropped row), or null
+  const double* U;      // [n][k] score rows (layout order)
+  const double* fq;
+  const int4* items;
+  unsigned long long* S;  // [G][k] fine limbs
+  double* hi;             // [G][k] coarse limbs
+  int n_items, k, s, win, G;
+  int bucketed;
+};
+
+__global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
+  typedef unsigned long long u64;
+  extern __shared__ u64 t[];  // [win][k]
+  const int tid = threadIdx.x, k = a.k;
+  const int wk = a.win * k;
+  for (int j = tid; j < wk; j += kClFixThreads) t[j] = 0ull;
+  const int i0 = (int)((int64_t)a.n_items * blockIdx.x / gridDim.x);
+  const int i1 = (int)((int64_t)a.n_items * (blockIdx.x + 1) / gridDim.x);
+  int cur = -1;
+  auto flush = [&](int lo) {
+    for (int j = tid; j < wk; j += kClFixThreads) {
+      const u64 v = t[j];
+      if (v != 0ull && lo + j / k < a.G) atomicAdd(&a.S[(int64_t)lo * k + j], v);
+      t[j] = 0ull;
+    }
+  };
+  for (int item = i0; item < i1; ++item) {
+    const int4 it = a.items[item];
+    const int lo = a.bucketed ? it.x << a.s : 0;
+    if (lo != cur) {
+      __syncthreads();
+      if (cur >= 0) flush(cur);
+      __syncthreads();
+      cur = lo;
+    }
+    const int64_t m = (int64_t)(it.z - it.y) * k;
+    for (int64_t e = tid; e < m; e += kClFixThreads) {
+      const int64_t i = it.y + e / k;
+      const int cc = (int)(e % k);
+      if (a.keep && a.keep[i] < 0) continue;
+      const int g = a.code[i];
+      double hh;
+      const u64 xi = fix_split(a.U[i * k + cc], fix_col(a.fq, cc), hh);
+      if (xi) atomicAdd(&t[(g - lo) * k + cc], xi);
+      if (hh != 0.0) atomicAdd(&a.hi[(int64_t)g * k + cc], hh);
+    }
   }
+  __syncthreads();
+  if (cur >= 0) flush(cur);
+}
+
+// flag[0] = 1 when some kept row's cluster code differs from its primary FE code
+__global__ void k_cl_same(const int32_t* __restrict__ a, const int32_t* __restrict__ p, int64_t n,
+                          int32_t* __restrict__ flag) {
+  bool diff = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    diff = diff || (p[i] >= 0 && a[i] != p[i]);
+  if (__any(diff) && (threadIdx.x & 63) == 0) flag[0] = 1;
 }
 
 static bool clfix_on() {
@@ -632,8 +684,9 @@ static bool clfix_on() {
   return on;
 }
 
-// meat and cluster count of the one-column subset j by the fixed-point sums (S: [G][k], then S'S)
-static int subset_meat_fix(lfe_ctx* c, int j, double* meat, int64_t* G_out) {
+// meat and cluster count of the one-column subset j by the fixed-point sums (S: [G][k], then S'S);
+// win / bucketed: the LDS window of k_clfix_add
+static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* meat, int64_t* G_out) {
   const int k = c->score_k;
   const int64_t n = c->n;
   const int32_t G = c->cl_levels[j];
@@ -655,15 +708,32 @@ static int subset_meat_fix(lfe_ctx* c, int j, double* meat, int64_t* G_out) {
   {
     ProfScope _ps(c, K_CLUSTER_SCATTER);
     if (n > 0)
-      hipLaunchKernelGGL(k_clfix_stats, dim3(nch), dim3(256), 0, c->stream, W.lay[j], keep, n, c->scores, k, nch, cnt,
-                         W.fixst);
+      hipLaunchKernelGGL(k_clfix_stats, dim3(nch), dim3(256), 0, c->stream, W.lay[j], keep, n, c->scores, std::max(k, 1),
+                         nch, cnt, W.fixst);
     LFE_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, cnt, G, cm);
     LFE_HIP(hipGetLastError());
     if (k > 0 && n > 0) {
       LFE_TRY(launch_fix_quanta(c, W.fixst, nch, std::max<int64_t>(c->n_kept_local, 1), cm + 1, 1, W.fixq, k));
-      hipLaunchKernelGGL(k_clfix_add, dim3(grid_for(n * k, 256, 8192)), dim3(256), 0, c->stream, W.lay[j], keep, n,
-                         c->scores, k, W.fixq, reinterpret_cast<unsigned long long*>(S), c->clS);
+      ClFixAdd a{};
+      a.code = W.lay[j];
+      a.keep = keep;
+      a.U = c->scores;
+      a.fq = W.fixq;
+      a.items = reinterpret_cast<const int4*>(c->items_d);
+      a.S = reinterpret_cast<unsigned long long*>(S);
+      a.hi = c->clS;
+      a.n_items = c->L.n_items;
+      a.k = k;
+      a.s = c->L.s;
+      a.win = win;
+      a.G = G;
+      a.bucketed = bucketed ? 1 : 0;
+      const size_t lds = sizeof(unsigned long long) * (size_t)win * k;
+      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_clfix_add),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 8)));
+      const int grid = std::max(1, std::min(c->L.n_items, 2 * c->n_cu));
+      hipLaunchKernelGGL(k_clfix_add, dim3(grid), dim3(kClFixThreads), lds, c->stream, a);
       LFE_HIP(hipGetLastError());
       LFE_TRY(launch_fix_convert(c, S, c->clS, (int64_t)m, k, W.fixq));
     }
@@ -686,16 +756,48 @@ static int subset_meat_fix(lfe_ctx* c, int j, double* meat, int64_t* G_out) {
   return rc;
 }
 
+// is loaded cluster column j the layout's primary FE on every kept row (its bucket slices then
+// hold every cluster of a work item)?
+static int cluster_is_primary(lfe_ctx* c, int j, bool* same) {
+  *same = false;
+  const auto& L = c->L;
+  if (!L.permuted || L.P < 0 || c->cl_levels[j] != c->fe[L.P].G) return LFE_OK;
+  LFE_TRY(ensure_iscratch(c, kIscratchInts + 1));  // (prepare_layout's size: the counts stay)
+  int32_t* flag = c->iscratch + kIsClSame;
+  LFE_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), c->stream));
+  if (c->n > 0)
+    hipLaunchKernelGGL(k_cl_same, dim3(grid_for(c->n, 256, 2048)), dim3(256), 0, c->stream, c->clw.lay[j],
+                       L.code[L.P], c->n, flag);
+  LFE_HIP(hipGetLastError());
+  int32_t h = 1;
+  LFE_TRY(d2h_sync(c, &h, flag, sizeof(int32_t)));
+  *same = h == 0;
+  return LFE_OK;
+}
+
 // meat and cluster count of one subset (mask over the loaded cluster columns)
 static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   const int k = c->score_k;
   const int64_t n = c->n;
   auto& W = c->clw;
-  if (clfix_on() && __builtin_popcount((unsigned)mask) == 1) {
+  if (clfix_on() && __builtin_popcount((unsigned)mask) == 1 && k >= 1 && k <= 63 && c->L.n_items > 0) {
+    // one column: the sort-free sums when its table window fits in LDS - the whole table (few
+    // clusters), or the bucket slice when the column is the primary FE; all-reduced whole across
+    // ranks up to 64 MB.  Otherwise the sorted path below (global atomics per score value were
+    // measured slower than the sort: 4.7 vs 2.5 ms on config 4's 1e5-level column, round 5)
     const int j = __builtin_ctz((unsigned)mask);
-    const int64_t m = (int64_t)c->cl_levels[j] * std::max(k, 1);
-    // a key-indexed table of at most 2^26 entries (512 MB), all-reduced whole across ranks up to 64 MB
-    if (m <= (1ll << 26) && (c->world == 1 || m * 8 <= (64ll << 20))) return subset_meat_fix(c, j, meat, G_out);
+    const int64_t G = c->cl_levels[j];
+    if (c->world == 1 || G * k * 8 <= (64ll << 20)) {
+      int win = 0;
+      bool bucketed = false;
+      if ((size_t)G * k * 8 <= kClFixLds) {
+        win = (int)G;
+      } else if (((size_t)8 << c->L.s) * k <= kClFixLds) {
+        LFE_TRY(cluster_is_primary(c, j, &bucketed));
+        if (bucketed) win = 1 << c->L.s;
+      }
+      if (win > 0) return subset_meat_fix(c, j, win, bucketed, meat, G_out);
+    }
   }
   KeyArgs ka{};
   uint64_t span = 1;
