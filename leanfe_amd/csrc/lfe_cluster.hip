@@ -631,6 +631,8 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
   extern __shared__ u64 t[];  // [win][k]
   const int tid = threadIdx.x, k = a.k;
   const int wk = a.win * k;
+  const int R = kClFixThreads / k, cc = tid % k, ro = tid / k;
+  const FixCol fc = fix_col(a.fq, cc);
   for (int j = tid; j < wk; j += kClFixThreads) t[j] = 0ull;
   const int i0 = (int)((int64_t)a.n_items * blockIdx.x / gridDim.x);
   const int i1 = (int)((int64_t)a.n_items * (blockIdx.x + 1) / gridDim.x);
@@ -651,17 +653,15 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
       __syncthreads();
       cur = lo;
     }
-    const int64_t m = (int64_t)(it.z - it.y) * k;
-    for (int64_t e = tid; e < m; e += kClFixThreads) {
-      const int64_t i = it.y + e / k;
-      const int cc = (int)(e % k);
-      if (a.keep && a.keep[i] < 0) continue;
-      const int g = a.code[i];
-      double hh;
-      const u64 xi = fix_split(a.U[i * k + cc], fix_col(a.fq, cc), hh);
-      if (xi) atomicAdd(&t[(g - lo) * k + cc], xi);
-      if (hh != 0.0) atomicAdd(&a.hi[(int64_t)g * k + cc], hh);
-    }
+    if (ro < R)  // thread (row ro, column cc): R rows of k contiguous values per step
+      for (int i = it.y + ro; i < it.z; i += R) {
+        if (a.keep && a.keep[i] < 0) continue;
+        const int g = a.code[i];
+        double hh;
+        const u64 xi = fix_split(a.U[(int64_t)i * k + cc], fc, hh);
+        if (xi) atomicAdd(&t[(g - lo) * k + cc], xi);
+        if (hh != 0.0) atomicAdd(&a.hi[(int64_t)g * k + cc], hh);
+      }
   }
   __syncthreads();
   if (cur >= 0) flush(cur);
