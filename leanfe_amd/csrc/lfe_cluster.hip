@@ -571,8 +571,9 @@ __global__ __launch_bounds__(256) void k_clfix_stats(const int32_t* __restrict__
   __shared__ double wm[256], wq[256];
   const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * kClFixChunk, r1 = min(n, r0 + kClFixChunk);
-  for (int64_t i = r0 + tid; i < r1; i += 256)
-    if (!keep || keep[i] >= 0) atomicAdd(&cnt[code[i]], 1);
+  if (cnt)
+    for (int64_t i = r0 + tid; i < r1; i += 256)
+      if (!keep || keep[i] >= 0) atomicAdd(&cnt[code[i]], 1);
   const int R = 256 / k, c = tid % k, ro = tid / k;
   double m = 0.0, q = 0.0;
   if (ro < R)
@@ -594,6 +595,20 @@ __global__ __launch_bounds__(256) void k_clfix_stats(const int32_t* __restrict__
     st[kColStatHead + (int64_t)tid * nchunks + blockIdx.x] = Q;
     atomicMax(reinterpret_cast<unsigned long long*>(st) + tid, (unsigned long long)__double_as_longlong(M));
   }
+}
+
+// kept rows per cluster of a small table: per-workgroup LDS counts, then one global add per
+// nonzero count (integer adds: any order)
+__global__ __launch_bounds__(1024) void k_clfix_hist(const int32_t* __restrict__ code, const int32_t* __restrict__ keep,
+                                                     int64_t n, int32_t G, int32_t* __restrict__ cnt) {
+  extern __shared__ int32_t h[];
+  for (int j = threadIdx.x; j < G; j += 1024) h[j] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 1024)
+    if (!keep || keep[i] >= 0) atomicAdd(&h[code[i]], 1);
+  __syncthreads();
+  for (int j = threadIdx.x; j < G; j += 1024)
+    if (h[j]) atomicAdd(&cnt[j], h[j]);
 }
 
 // out[0] = clusters with kept rows, out[1] = the largest cluster (integer atomics: any order)
@@ -707,9 +722,21 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
   LFE_HIP(hipMemsetAsync(S, 0, sizeof(double) * m, c->stream));
   {
     ProfScope _ps(c, K_CLUSTER_SCATTER);
+    // kept rows per cluster: the primary FE's kept counts (bucketed: the column repeats it), an LDS
+    // histogram (a small table), else global adds in the statistics pass
+    int32_t* cnt_in_stats = nullptr;
+    if (bucketed) {
+      LFE_HIP(hipMemcpyAsync(cnt, c->fe[c->L.P].cnt, sizeof(int32_t) * G, hipMemcpyDeviceToDevice, c->stream));
+    } else if ((size_t)G * 4 <= kClFixLds) {
+      if (n > 0)
+        hipLaunchKernelGGL(k_clfix_hist, dim3(std::max(1, std::min<int>(2 * c->n_cu, (int)((n + 8191) / 8192)))),
+                           dim3(1024), sizeof(int32_t) * G, c->stream, W.lay[j], keep, n, G, cnt);
+    } else {
+      cnt_in_stats = cnt;
+    }
     if (n > 0)
       hipLaunchKernelGGL(k_clfix_stats, dim3(nch), dim3(256), 0, c->stream, W.lay[j], keep, n, c->scores, std::max(k, 1),
-                         nch, cnt, W.fixst);
+                         nch, cnt_in_stats, W.fixst);
     LFE_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, cnt, G, cm);
     LFE_HIP(hipGetLastError());
@@ -756,22 +783,9 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
   return rc;
 }
 
-// is loaded cluster column j the layout's primary FE on every kept row (its bucket slices then
-// hold every cluster of a work item)?
-static int cluster_is_primary(lfe_ctx* c, int j, bool* same) {
-  *same = false;
-  const auto& L = c->L;
-  if (!L.permuted || L.P < 0 || c->cl_levels[j] != c->fe[L.P].G) return LFE_OK;
-  LFE_TRY(ensure_iscratch(c, kIscratchInts + 1));  // (prepare_layout's size: the counts stay)
-  int32_t* flag = c->iscratch + kIsClSame;
-  LFE_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), c->stream));
-  if (c->n > 0)
-    hipLaunchKernelGGL(k_cl_same, dim3(grid_for(c->n, 256, 2048)), dim3(256), 0, c->stream, c->clw.lay[j],
-                       L.code[L.P], c->n, flag);
+int launch_codes_differ(lfe_ctx* c, const int32_t* a, const int32_t* b, int64_t n, int32_t* flag) {
+  if (n > 0) hipLaunchKernelGGL(k_cl_same, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, a, b, n, flag);
   LFE_HIP(hipGetLastError());
-  int32_t h = 1;
-  LFE_TRY(d2h_sync(c, &h, flag, sizeof(int32_t)));
-  *same = h == 0;
   return LFE_OK;
 }
 
@@ -792,9 +806,10 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
       bool bucketed = false;
       if ((size_t)G * k * 8 <= kClFixLds) {
         win = (int)G;
-      } else if (((size_t)8 << c->L.s) * k <= kClFixLds) {
-        LFE_TRY(cluster_is_primary(c, j, &bucketed));
-        if (bucketed) win = 1 << c->L.s;
+      } else if (c->world == 1 && c->L.permuted && c->L.P >= 0 && j < (int)c->cl_fe.size() && c->cl_fe[j] == c->L.P &&
+                 ((size_t)8 << c->L.s) * k <= kClFixLds) {
+        bucketed = true;  // the column repeats the primary FE (lfe_load_clusters compared them)
+        win = 1 << c->L.s;
       }
       if (win > 0) return subset_meat_fix(c, j, win, bucketed, meat, G_out);
     }

@@ -287,6 +287,7 @@ struct lfe_ctx {
   // clusters (input row order)
   std::vector<int32_t*> cl;
   std::vector<int32_t> cl_levels;
+  std::vector<int> cl_fe;  // per cluster column: the FE column it repeats (equal codes), or -1
   lfe::ClusterWS clw;
   // pinned host staging (small transfers avoid the runtime's pageable path)
   char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
@@ -519,6 +520,7 @@ void free_stream_clusters(lfe_ctx* c);
 // records in c->clS (lfe_cluster.hip)
 int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R, const double* table,
                  int k, int32_t* G_out);  // weighted streamed fits: w's max / rms into fixq column p
+int launch_codes_differ(lfe_ctx* c, const int32_t* a, const int32_t* b, int64_t n, int32_t* flag);  // lfe_cluster.hip
 int stream_materialize_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows);  // lfe_wide.hip
 int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t ld, int64_t row0, int64_t rows,
                       double* scores);
