@@ -576,13 +576,16 @@ __global__ __launch_bounds__(256) void k_clfix_stats(const int32_t* __restrict__
       if (!keep || keep[i] >= 0) atomicAdd(&cnt[code[i]], 1);
   const int R = 256 / k, c = tid % k, ro = tid / k;
   double m = 0.0, q = 0.0;
-  if (ro < R)
+  if (ro < R) {
+    // branch-free (a dropped row adds 0 to both), four rows in flight per thread
+#pragma unroll 4
     for (int64_t i = r0 + ro; i < r1; i += R) {
-      if (keep && keep[i] < 0) continue;
-      const double v = U[i * k + c];
+      const double u = U[i * k + c];
+      const double v = (!keep || keep[i] >= 0) ? u : 0.0;
       m = fmax(m, fabs(v));
       q = __builtin_fma(v, v, q);
     }
+  }
   wm[tid] = m;
   wq[tid] = q;
   __syncthreads();
@@ -668,15 +671,28 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
       __syncthreads();
       cur = lo;
     }
-    if (ro < R)  // thread (row ro, column cc): R rows of k contiguous values per step
-      for (int i = it.y + ro; i < it.z; i += R) {
-        if (a.keep && a.keep[i] < 0) continue;
+    if (ro < R) {  // thread (row ro, column cc): R rows of k contiguous values per step, two in flight
+      int i = it.y + ro;
+      for (; i + R < it.z; i += 2 * R) {
+        const int i2 = i + R;
+        const bool k1 = !a.keep || a.keep[i] >= 0, k2 = !a.keep || a.keep[i2] >= 0;
+        const int g1 = a.code[i], g2 = a.code[i2];
+        const double u1 = a.U[(int64_t)i * k + cc], u2 = a.U[(int64_t)i2 * k + cc];
+        double h1, h2;
+        const u64 x1 = fix_split(u1, fc, h1), x2 = fix_split(u2, fc, h2);
+        if (k1 && x1) atomicAdd(&t[(g1 - lo) * k + cc], x1);
+        if (k2 && x2) atomicAdd(&t[(g2 - lo) * k + cc], x2);
+        if (k1 && h1 != 0.0) atomicAdd(&a.hi[(int64_t)g1 * k + cc], h1);
+        if (k2 && h2 != 0.0) atomicAdd(&a.hi[(int64_t)g2 * k + cc], h2);
+      }
+      if (i < it.z && (!a.keep || a.keep[i] >= 0)) {
         const int g = a.code[i];
         double hh;
         const u64 xi = fix_split(a.U[(int64_t)i * k + cc], fc, hh);
         if (xi) atomicAdd(&t[(g - lo) * k + cc], xi);
         if (hh != 0.0) atomicAdd(&a.hi[(int64_t)g * k + cc], hh);
       }
+    }
   }
   __syncthreads();
   if (cur >= 0) flush(cur);
