@@ -297,12 +297,13 @@ def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cel
         "check": 4 * n * (F - 1),
         **({"count": 4 * n} if F != 2 else {}),      # one FE's codes (two FEs: the layouts' histograms)
         # clustered SEs (lfe_cluster.hip): a sort launch is a digit histogram (8 B keys read) or a
-        # scatter (key + row read and written, 24 B) - 16 B/row on average over the pairs; a
-        # one-column subset's fixed-point sums (k_clfix_stats, k_clfix_add) read the score rows, the
-        # cluster codes and the keep flags twice: 2 x (8k + 8) B/row (a sorted subset's segmented
-        # sums read the score rows once through the sorted row index: fewer bytes, not counted)
+        # scatter (key + row read and written, 24 B) - 16 B/row on average over the pairs; a sorted
+        # subset's segmented sums read the sorted keys, segment flags and row index and gather the
+        # score rows through it (8k + 16 B/row); a one-column subset's sort-free fixed-point sums
+        # (k_clfix_stats, k_clfix_add) read the score rows, cluster codes and keep flags twice
         "cluster_sort": 16 * n,
-        "cluster_scatter": n * (16 * k + 16),
+        "cluster_scatter": n * (8 * k + 16),
+        "cluster_fix": n * (16 * k + 16),
         **dense,
     }
 

@@ -351,7 +351,7 @@ const char* const kKernelNames[K_NUM_KERNELS] = {
     "part_hist", "scan", "part_scatter", "count", "mark", "group_sums", "cross", "check", "finalize",
     "check_max", "gram_design", "gram_resid", "gram_table", "reduce_partials", "cluster_scatter", "misc", "synth",
     "tp", "tq", "seg_build", "cluster_sort", "gram_tables", "layout_hist", "layout_base", "layout_scatter",
-    "tq_reduce", "fix_sums"};
+    "tq_reduce", "fix_sums", "cluster_fix"};
 
 static hipEvent_t prof_event(lfe_ctx* c) {
   if (!c->prof.pool.empty()) {

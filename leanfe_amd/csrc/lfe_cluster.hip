@@ -737,7 +737,7 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
   LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * m, c->stream));
   LFE_HIP(hipMemsetAsync(S, 0, sizeof(double) * m, c->stream));
   {
-    ProfScope _ps(c, K_CLUSTER_SCATTER);
+    ProfScope _ps(c, K_CLUSTER_FIX);
     // kept rows per cluster: the primary FE's kept counts (bucketed: the column repeats it), an LDS
     // histogram (a small table), else global adds in the statistics pass
     int32_t* cnt_in_stats = nullptr;

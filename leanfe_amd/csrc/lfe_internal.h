@@ -90,7 +90,7 @@ enum KernelId {
   K_PART_HIST = 0, K_SCAN, K_PART_SCATTER, K_COUNT, K_MARK, K_GROUP_SUMS, K_CROSS, K_CHECK, K_FINALIZE,
   K_CHECK_MAX, K_GRAM_DESIGN, K_GRAM_RESID, K_GRAM_TABLE, K_REDUCE, K_CLUSTER_SCATTER, K_MISC, K_SYNTH,
   K_TP, K_TQ, K_SEG_BUILD, K_CLUSTER_SORT, K_GRAM_TABLES, K_LAYOUT_HIST, K_LAYOUT_BASE, K_LAYOUT_SCATTER,
-  K_TQ_REDUCE, K_FIX_SUMS, K_NUM_KERNELS
+  K_TQ_REDUCE, K_FIX_SUMS, K_CLUSTER_FIX, K_NUM_KERNELS
 };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 
