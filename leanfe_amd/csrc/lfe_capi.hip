@@ -437,6 +437,7 @@ static void free_data(lfe_ctx* c) {
   for (auto& p : c->cl) dfree(p);
   c->cl.clear();
   c->cl_levels.clear();
+  c->cl_fe.clear();
   free_cluster_ws(c);
   dfree(c->rec_sy);
   dfree(c->rec_syy);
