@@ -328,6 +328,12 @@ int lfe_wide_cluster_meats(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, i
  * LFE_TEST_SHORT_MEMORY: lfe_reshard_owner on this rank reports too little device memory for
  * its staging copy, so that the all-rank refusal can be tested (every rank keeps its rows). */
 #define LFE_TEST_SHORT_MEMORY 1
+/* LFE_TEST_CLUSTER_SORTED: one-column cluster subsets take the sorted path (keys, radix sort,
+ * segmented sums) instead of the sort-free fixed-point sums.
+ * LFE_TEST_CLUSTER_STATS: the sort-free sums take their quanta from a statistics pass over the
+ * score rows instead of the residual pass's meat. */
+#define LFE_TEST_CLUSTER_SORTED 2
+#define LFE_TEST_CLUSTER_STATS 4
 int lfe_ctx_test_hooks(lfe_ctx* ctx, int flags);
 
 /* Wait for all work queued on the context's stream. */

@@ -22,6 +22,9 @@
 // and the cluster counts are all-reduced.
 #include "lfe_internal.h"
 
+#include <cmath>
+#include <cstring>
+
 #include <algorithm>
 
 namespace lfe {
@@ -642,6 +645,11 @@ struct ClFixAdd {
   double* hi;             // [G][k] coarse limbs
   int n_items, k, s, win, G;
   int bucketed;
+  // quanta from the residual pass's meat (no statistics pass): every value may carry a coarse
+  // limb, and one whose coarse limb could make a cluster's f64 sum inexact raises *oflag (the
+  // caller then redoes the subset with the statistics pass)
+  const int32_t* cmax;  // [1]: the largest cluster's kept rows
+  int32_t* oflag;       // null: quanta from the statistics pass
 };
 
 __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
@@ -650,7 +658,13 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
   const int tid = threadIdx.x, k = a.k;
   const int wk = a.win * k;
   const int R = kClFixThreads / k, cc = tid % k, ro = tid / k;
-  const FixCol fc = fix_col(a.fq, cc);
+  FixCol fc = fix_col(a.fq, cc);
+  double hlim = 0.0;
+  if (a.oflag) {
+    fc.big = true;
+    hlim = 0x1p51 / (double)max(*a.cmax, 1) - 1.0;  // N (|h| + 1) < 2^51: exact f64 sums of h
+  }
+  bool over = false;
   for (int j = tid; j < wk; j += kClFixThreads) t[j] = 0ull;
   const int i0 = (int)((int64_t)a.n_items * blockIdx.x / gridDim.x);
   const int i1 = (int)((int64_t)a.n_items * (blockIdx.x + 1) / gridDim.x);
@@ -684,6 +698,7 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
         if (k2 && x2) atomicAdd(&t[(g2 - lo) * k + cc], x2);
         if (k1 && h1 != 0.0) atomicAdd(&a.hi[(int64_t)g1 * k + cc], h1);
         if (k2 && h2 != 0.0) atomicAdd(&a.hi[(int64_t)g2 * k + cc], h2);
+        over = over || (k1 && !(fabs(h1) <= hlim)) || (k2 && !(fabs(h2) <= hlim));
       }
       if (i < it.z && (!a.keep || a.keep[i] >= 0)) {
         const int g = a.code[i];
@@ -691,11 +706,13 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
         const u64 xi = fix_split(a.U[(int64_t)i * k + cc], fc, hh);
         if (xi) atomicAdd(&t[(g - lo) * k + cc], xi);
         if (hh != 0.0) atomicAdd(&a.hi[(int64_t)g * k + cc], hh);
+        over = over || !(fabs(hh) <= hlim);
       }
     }
   }
   __syncthreads();
   if (cur >= 0) flush(cur);
+  if (a.oflag && __any(over) && (tid & 63) == 0) a.oflag[0] = 1;
 }
 
 // flag[0] = 1 when some kept row's cluster code differs from its primary FE code
@@ -717,7 +734,8 @@ static bool clfix_on() {
 
 // meat and cluster count of the one-column subset j by the fixed-point sums (S: [G][k], then S'S);
 // win / bucketed: the LDS window of k_clfix_add
-static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* meat, int64_t* G_out) {
+static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* meat, int64_t* G_out,
+                           bool stats_pass = false) {
   const int k = c->score_k;
   const int64_t n = c->n;
   const int32_t G = c->cl_levels[j];
@@ -750,14 +768,33 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
     } else {
       cnt_in_stats = cnt;
     }
-    if (n > 0)
+    // quanta: from the residual pass's meat (one process: Σ_i s_ic^2 ≈ its diagonal, deterministic;
+    // max |s| taken as 64 rms, every value checked against the coarse sums' bound in the adds) or
+    // from a statistics pass over the score rows
+    const bool from_meat = !stats_pass && !cnt_in_stats && c->world == 1 &&
+                           c->score_meat.size() == (size_t)k * k && k > 0;
+    if (from_meat) {
+      std::vector<double> hs((size_t)kColStatHead + k, 0.0);
+      const double nk = (double)std::max<int64_t>(c->n_kept, 1);
+      for (int e = 0; e < k; ++e) {
+        const double d = std::max(c->score_meat[(size_t)e * k + e], 0.0);
+        const double M = std::isfinite(d) ? 64.0 * std::sqrt(d / nk) : d;
+        uint64_t bits;
+        std::memcpy(&bits, &M, sizeof(bits));
+        std::memcpy(&hs[e], &bits, sizeof(bits));
+        hs[kColStatHead + e] = d;  // one chunk
+      }
+      LFE_TRY(h2d_small(c, W.fixst, hs.data(), sizeof(double) * hs.size()));
+    } else if (n > 0) {
       hipLaunchKernelGGL(k_clfix_stats, dim3(nch), dim3(256), 0, c->stream, W.lay[j], keep, n, c->scores, std::max(k, 1),
                          nch, cnt_in_stats, W.fixst);
+    }
     LFE_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, cnt, G, cm);
     LFE_HIP(hipGetLastError());
     if (k > 0 && n > 0) {
-      LFE_TRY(launch_fix_quanta(c, W.fixst, nch, std::max<int64_t>(c->n_kept_local, 1), cm + 1, 1, W.fixq, k));
+      LFE_TRY(launch_fix_quanta(c, W.fixst, from_meat ? 1 : nch,
+                                std::max<int64_t>(from_meat ? c->n_kept : c->n_kept_local, 1), cm + 1, 1, W.fixq, k));
       ClFixAdd a{};
       a.code = W.lay[j];
       a.keep = keep;
@@ -772,6 +809,8 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
       a.win = win;
       a.G = G;
       a.bucketed = bucketed ? 1 : 0;
+      a.cmax = cm + 1;
+      a.oflag = from_meat ? cm + 2 : nullptr;
       const size_t lds = sizeof(unsigned long long) * (size_t)win * k;
       LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_clfix_add),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 8)));
@@ -788,9 +827,11 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
     hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, cnt, G, cm);
     LFE_HIP(hipGetLastError());
   }
-  int32_t hG = 0;
-  LFE_TRY(d2h_sync(c, &hG, cm, sizeof(int32_t)));
-  *G_out = hG;
+  int32_t hc[3] = {0, 0, 0};
+  LFE_TRY(d2h_sync(c, hc, cm, sizeof(hc)));
+  if (hc[2] != 0)  // a value past the assumed range: the quanta from the statistics pass instead
+    return subset_meat_fix(c, j, win, bucketed, meat, G_out, true);
+  *G_out = hc[0];
   if (k == 0) return LFE_OK;
   const int world = c->world;  // S is replicated after the all-reduce: reduce its Gram locally
   c->world = 1;
@@ -810,7 +851,8 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   const int k = c->score_k;
   const int64_t n = c->n;
   auto& W = c->clw;
-  if (clfix_on() && __builtin_popcount((unsigned)mask) == 1 && k >= 1 && k <= 63 && c->L.n_items > 0) {
+  if (clfix_on() && !(c->test_hooks & LFE_TEST_CLUSTER_SORTED) && __builtin_popcount((unsigned)mask) == 1 && k >= 1 &&
+      k <= 63 && c->L.n_items > 0) {
     // one column: the sort-free sums when its table window fits in LDS - the whole table (few
     // clusters), or the bucket slice when the column is the primary FE; all-reduced whole across
     // ranks up to 64 MB.  Otherwise the sorted path below (global atomics per score value were
@@ -827,7 +869,13 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
         bucketed = true;  // the column repeats the primary FE (lfe_load_clusters compared them)
         win = 1 << c->L.s;
       }
-      if (win > 0) return subset_meat_fix(c, j, win, bucketed, meat, G_out);
+      static const bool stats_env = [] {  // "1": quanta from the statistics pass (A/B, tests)
+        const char* e = getenv("LFE_CL_STATS");
+        return e && e[0] == '1';
+      }();
+      if (win > 0)
+        return subset_meat_fix(c, j, win, bucketed, meat, G_out,
+                               stats_env || (c->test_hooks & LFE_TEST_CLUSTER_STATS) != 0);
     }
   }
   KeyArgs ka{};

@@ -3,7 +3,7 @@
 A one-column cluster subset's clusters are the column's codes, so the per-cluster score sums
 S_c = sum_{i in c} x~_i r_i (w_i) (std_errors.py:317-333) are formed the way the group sums are -
 fine limbs by int64 adds, outliers' coarse limbs by integer-valued f64 adds - into a table indexed
-by the code, with no sort.  Against the sorted path (LFE_CL_FIX=0: keys, radix sort, segmented sums)
+by the code, with no sort.  Against the sorted path (the LFE_TEST_CLUSTER_SORTED hook: keys, radix sort, segmented sums)
 and the CPU oracle (oracle/altproj.py: std_errors.py:289-441): one-way and multi-way CGM (the
 intersection subset still sorts), clusters on FE columns (reg_test.py:55, 61) and on a column that
 is no FE, weights, a 5e9 outlier (coarse limbs), bit-identical repeats, and an emulated 2-rank
@@ -20,12 +20,23 @@ from leanfe_amd import synth
 pytestmark = pytest.mark.gpu
 
 
-def _fit(data, xs, fes, cl, **kw):
-    from leanfe_amd import leanfe_hip
+SORTED, STATS = 2, 4  # LFE_TEST_CLUSTER_SORTED, LFE_TEST_CLUSTER_STATS (include/leanfe_hip.h)
 
-    r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov="cluster", cluster_cols=cl,
-                   quiet=True, device=0, **kw)
-    return r
+
+def _fit(data, xs, fes, cl, hooks=0, **kw):
+    """The fit on its own engine with the given test hooks: 0 = the sort-free sums with quanta from
+    the residual pass's meat, STATS = from a statistics pass, SORTED = the sorted path."""
+    from leanfe_amd import leanfe_hip
+    from leanfe_amd._lib import Engine
+
+    with Engine(0) as eng:
+        if hooks:
+            eng.test_hooks(hooks)
+        eng.profile(True)
+        r = leanfe_hip(data, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov="cluster",
+                       cluster_cols=cl, quiet=True, engine=eng, **kw)
+        r.kernels = set(eng.kernel_stats())  # which cluster paths ran ("cluster_fix": the sort-free sums)
+        return r
 
 
 def _arr(r, xs, what):
@@ -41,7 +52,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("name,L,cl,weights", CASES, ids=[c[0] for c in CASES])
-def test_one_column_subsets_without_sort(name, L, cl, weights, monkeypatch):
+def test_one_column_subsets_without_sort(name, L, cl, weights):
     from oracle import altproj
 
     n, k = 500_000, 4
@@ -59,8 +70,8 @@ def test_one_column_subsets_without_sort(name, L, cl, weights, monkeypatch):
     kw = dict(weights=weights) if weights else {}
     fix = _fit(d, xs, fes, cl, **kw)
     again = _fit(d, xs, fes, cl, **kw)
-    monkeypatch.setenv("LFE_CL_FIX", "0")
-    srt = _fit(d, xs, fes, cl, **kw)
+    st = _fit(d, xs, fes, cl, hooks=STATS, **kw)
+    srt = _fit(d, xs, fes, cl, hooks=SORTED, **kw)
     o = altproj.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=cl, weights=weights)
     ncl = o["n_clusters"]
     assert fix.n_clusters == srt.n_clusters
@@ -70,6 +81,9 @@ def test_one_column_subsets_without_sort(name, L, cl, weights, monkeypatch):
     np.testing.assert_allclose(_arr(fix, xs, "coefs"), o["beta"], rtol=1e-10, atol=0)
     np.testing.assert_allclose(_arr(fix, xs, "std_errors"), o["se"], rtol=1e-10, atol=0)
     np.testing.assert_allclose(_arr(fix, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
+    np.testing.assert_allclose(_arr(st, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
+    # the comparisons are between different computations: the sort-free sums ran in fix and st only
+    assert "cluster_fix" in fix.kernels and "cluster_fix" in st.kernels and "cluster_fix" not in srt.kernels
     np.testing.assert_array_equal(_arr(fix, xs, "std_errors"), _arr(again, xs, "std_errors"))
 
 
