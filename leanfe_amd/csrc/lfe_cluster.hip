@@ -617,6 +617,20 @@ __global__ __launch_bounds__(1024) void k_clfix_hist(const int32_t* __restrict__
     if (h[j]) atomicAdd(&cnt[j], h[j]);
 }
 
+// the statistics head from the residual pass's meat, passed by value (no host-to-device copy to
+// wait for): max |s_c| bits (an assumed bound) and one chunk's sum of s_c^2 per column
+struct ClMeatStats {
+  double M[64];
+  double d[64];
+  int k;
+};
+__global__ void k_clfix_meat_stats(ClMeatStats a, double* __restrict__ st) {
+  for (int e = threadIdx.x; e < a.k; e += blockDim.x) {
+    st[e] = a.M[e];  // as u64 bits: the same bits as a double >= 0
+    st[kColStatHead + e] = a.d[e];
+  }
+}
+
 // out[0] = clusters with kept rows, out[1] = the largest cluster (integer atomics: any order)
 __global__ void k_clfix_count(const int32_t* __restrict__ cnt, int32_t G, int32_t* __restrict__ out) {
   int32_t nz = 0, mx = 0;
@@ -772,19 +786,19 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
     // max |s| taken as 64 rms, every value checked against the coarse sums' bound in the adds) or
     // from a statistics pass over the score rows
     const bool from_meat = !stats_pass && !cnt_in_stats && c->world == 1 &&
-                           c->score_meat.size() == (size_t)k * k && k > 0;
+                           c->score_meat.size() == (size_t)k * k && k > 0 && k <= 64;
     if (from_meat) {
-      std::vector<double> hs((size_t)kColStatHead + k, 0.0);
+      // max |s_c| assumed 8 rms (the typical range of the fine limb; a larger value takes a coarse
+      // limb, one past the coarse sums' bound raises the overflow flag)
+      ClMeatStats ms{};
+      ms.k = k;
       const double nk = (double)std::max<int64_t>(c->n_kept, 1);
       for (int e = 0; e < k; ++e) {
         const double d = std::max(c->score_meat[(size_t)e * k + e], 0.0);
-        const double M = std::isfinite(d) ? 64.0 * std::sqrt(d / nk) : d;
-        uint64_t bits;
-        std::memcpy(&bits, &M, sizeof(bits));
-        std::memcpy(&hs[e], &bits, sizeof(bits));
-        hs[kColStatHead + e] = d;  // one chunk
+        ms.M[e] = std::isfinite(d) ? 8.0 * std::sqrt(d / nk) : d;
+        ms.d[e] = d;
       }
-      LFE_TRY(h2d_small(c, W.fixst, hs.data(), sizeof(double) * hs.size()));
+      hipLaunchKernelGGL(k_clfix_meat_stats, dim3(1), dim3(64), 0, c->stream, ms, W.fixst);
     } else if (n > 0) {
       hipLaunchKernelGGL(k_clfix_stats, dim3(nch), dim3(256), 0, c->stream, W.lay[j], keep, n, c->scores, std::max(k, 1),
                          nch, cnt_in_stats, W.fixst);
