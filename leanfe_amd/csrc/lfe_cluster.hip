@@ -631,6 +631,11 @@ __global__ void k_clfix_meat_stats(ClMeatStats a, double* __restrict__ st) {
   }
 }
 
+// every column may carry coarse limbs (the adds split them, the conversion adds them back)
+__global__ void k_fq_all_big(double* __restrict__ fq, int k) {
+  for (int e = threadIdx.x; e < k; e += blockDim.x) fq[FQ_BIG * kFqCols + e] = 1.0;
+}
+
 // out[0] = clusters with kept rows, out[1] = the largest cluster (integer atomics: any order)
 __global__ void k_clfix_count(const int32_t* __restrict__ cnt, int32_t G, int32_t* __restrict__ out) {
   int32_t nz = 0, mx = 0;
@@ -672,12 +677,9 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
   const int tid = threadIdx.x, k = a.k;
   const int wk = a.win * k;
   const int R = kClFixThreads / k, cc = tid % k, ro = tid / k;
-  FixCol fc = fix_col(a.fq, cc);
-  double hlim = 0.0;
-  if (a.oflag) {
-    fc.big = true;
-    hlim = 0x1p51 / (double)max(*a.cmax, 1) - 1.0;  // N (|h| + 1) < 2^51: exact f64 sums of h
-  }
+  const FixCol fc = fix_col(a.fq, cc);
+  // (meat quanta: every column flagged big) N (|h| + 1) < 2^51 keeps the f64 sums of h exact
+  const double hlim = a.oflag ? 0x1p51 / (double)max(*a.cmax, 1) - 1.0 : 0x1p1023;
   bool over = false;
   for (int j = tid; j < wk; j += kClFixThreads) t[j] = 0ull;
   const int i0 = (int)((int64_t)a.n_items * blockIdx.x / gridDim.x);
@@ -809,6 +811,7 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
     if (k > 0 && n > 0) {
       LFE_TRY(launch_fix_quanta(c, W.fixst, from_meat ? 1 : nch,
                                 std::max<int64_t>(from_meat ? c->n_kept : c->n_kept_local, 1), cm + 1, 1, W.fixq, k));
+      if (from_meat) hipLaunchKernelGGL(k_fq_all_big, dim3(1), dim3(64), 0, c->stream, W.fixq, k);
       ClFixAdd a{};
       a.code = W.lay[j];
       a.keep = keep;
