@@ -787,7 +787,8 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
     // quanta: from the residual pass's meat (one process: Σ_i s_ic^2 ≈ its diagonal, deterministic;
     // max |s| taken as 64 rms, every value checked against the coarse sums' bound in the adds) or
     // from a statistics pass over the score rows
-    const bool from_meat = !stats_pass && !cnt_in_stats && c->world == 1 &&
+    // (score_meat_ok: the meat is exactly sum s s' - one process, no weights, no records)
+    const bool from_meat = !stats_pass && !cnt_in_stats && c->world == 1 && c->score_meat_ok &&
                            c->score_meat.size() == (size_t)k * k && k > 0 && k <= 64;
     if (from_meat) {
       // max |s_c| assumed 8 rms (the typical range of the fine limb; a larger value takes a coarse
