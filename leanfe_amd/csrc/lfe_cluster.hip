@@ -791,14 +791,14 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
     const bool from_meat = !stats_pass && !cnt_in_stats && c->world == 1 && c->score_meat_ok &&
                            c->score_meat.size() == (size_t)k * k && k > 0 && k <= 64;
     if (from_meat) {
-      // max |s_c| assumed 8 rms (the typical range of the fine limb; a larger value takes a coarse
+      // max |s_c| assumed 16 rms (the typical range of the fine limb; a larger value takes a coarse
       // limb, one past the coarse sums' bound raises the overflow flag)
       ClMeatStats ms{};
       ms.k = k;
       const double nk = (double)std::max<int64_t>(c->n_kept, 1);
       for (int e = 0; e < k; ++e) {
         const double d = std::max(c->score_meat[(size_t)e * k + e], 0.0);
-        ms.M[e] = std::isfinite(d) ? 8.0 * std::sqrt(d / nk) : d;
+        ms.M[e] = std::isfinite(d) ? 16.0 * std::sqrt(d / nk) : d;
         ms.d[e] = d;
       }
       hipLaunchKernelGGL(k_clfix_meat_stats, dim3(1), dim3(64), 0, c->stream, ms, W.fixst);
