@@ -671,6 +671,7 @@ struct ClFixAdd {
   int32_t* oflag;       // null: quanta from the statistics pass
 };
 
+template <bool CHECK>  // CHECK: meat quanta (a.oflag set), every coarse limb checked against the bound
 __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
   typedef unsigned long long u64;
   extern __shared__ u64 t[];  // [win][k]
@@ -679,7 +680,7 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
   const int R = kClFixThreads / k, cc = tid % k, ro = tid / k;
   const FixCol fc = fix_col(a.fq, cc);
   // (meat quanta: every column flagged big) N (|h| + 1) < 2^51 keeps the f64 sums of h exact
-  const double hlim = a.oflag ? 0x1p51 / (double)max(*a.cmax, 1) - 1.0 : 0x1p1023;
+  const double hlim = CHECK ? 0x1p51 / (double)max(*a.cmax, 1) - 1.0 : 0.0;
   bool over = false;
   for (int j = tid; j < wk; j += kClFixThreads) t[j] = 0ull;
   const int i0 = (int)((int64_t)a.n_items * blockIdx.x / gridDim.x);
@@ -714,7 +715,7 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
         if (k2 && x2) atomicAdd(&t[(g2 - lo) * k + cc], x2);
         if (k1 && h1 != 0.0) atomicAdd(&a.hi[(int64_t)g1 * k + cc], h1);
         if (k2 && h2 != 0.0) atomicAdd(&a.hi[(int64_t)g2 * k + cc], h2);
-        over = over || (k1 && !(fabs(h1) <= hlim)) || (k2 && !(fabs(h2) <= hlim));
+        if (CHECK) over = over || (k1 && !(fabs(h1) <= hlim)) || (k2 && !(fabs(h2) <= hlim));
       }
       if (i < it.z && (!a.keep || a.keep[i] >= 0)) {
         const int g = a.code[i];
@@ -722,13 +723,13 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
         const u64 xi = fix_split(a.U[(int64_t)i * k + cc], fc, hh);
         if (xi) atomicAdd(&t[(g - lo) * k + cc], xi);
         if (hh != 0.0) atomicAdd(&a.hi[(int64_t)g * k + cc], hh);
-        over = over || !(fabs(hh) <= hlim);
+        if (CHECK) over = over || !(fabs(hh) <= hlim);
       }
     }
   }
   __syncthreads();
   if (cur >= 0) flush(cur);
-  if (a.oflag && __any(over) && (tid & 63) == 0) a.oflag[0] = 1;
+  if (CHECK && __any(over) && (tid & 63) == 0) a.oflag[0] = 1;
 }
 
 // flag[0] = 1 when some kept row's cluster code differs from its primary FE code
@@ -830,10 +831,12 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
       a.cmax = cm + 1;
       a.oflag = from_meat ? cm + 2 : nullptr;
       const size_t lds = sizeof(unsigned long long) * (size_t)win * k;
-      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_clfix_add),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 8)));
+      const void* fn = from_meat ? reinterpret_cast<const void*>(&k_clfix_add<true>)
+                                 : reinterpret_cast<const void*>(&k_clfix_add<false>);
+      LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 8)));
       const int grid = std::max(1, std::min(c->L.n_items, 2 * c->n_cu));
-      hipLaunchKernelGGL(k_clfix_add, dim3(grid), dim3(kClFixThreads), lds, c->stream, a);
+      if (from_meat) hipLaunchKernelGGL(k_clfix_add<true>, dim3(grid), dim3(kClFixThreads), lds, c->stream, a);
+      else hipLaunchKernelGGL(k_clfix_add<false>, dim3(grid), dim3(kClFixThreads), lds, c->stream, a);
       LFE_HIP(hipGetLastError());
       LFE_TRY(launch_fix_convert(c, S, c->clS, (int64_t)m, k, W.fixq));
     }
