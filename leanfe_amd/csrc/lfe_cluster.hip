@@ -715,7 +715,7 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
         if (k2 && x2) atomicAdd(&t[(g2 - lo) * k + cc], x2);
         if (k1 && h1 != 0.0) atomicAdd(&a.hi[(int64_t)g1 * k + cc], h1);
         if (k2 && h2 != 0.0) atomicAdd(&a.hi[(int64_t)g2 * k + cc], h2);
-        if (CHECK) over = over || (k1 && !(fabs(h1) <= hlim)) || (k2 && !(fabs(h2) <= hlim));
+        if (CHECK) over |= (k1 & !(fabs(h1) <= hlim)) | (k2 & !(fabs(h2) <= hlim));  // branch-free
       }
       if (i < it.z && (!a.keep || a.keep[i] >= 0)) {
         const int g = a.code[i];
@@ -723,7 +723,7 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
         const u64 xi = fix_split(a.U[(int64_t)i * k + cc], fc, hh);
         if (xi) atomicAdd(&t[(g - lo) * k + cc], xi);
         if (hh != 0.0) atomicAdd(&a.hi[(int64_t)g * k + cc], hh);
-        if (CHECK) over = over || !(fabs(hh) <= hlim);
+        if (CHECK) over |= !(fabs(hh) <= hlim);
       }
     }
   }
