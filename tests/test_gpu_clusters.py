@@ -132,3 +132,20 @@ def test_one_column_subset_on_emulated_ranks():
         assert out[r]["it"] == o["iterations"] and out[r]["ncl"] == o["n_clusters"]
         np.testing.assert_allclose(out[r]["se"], o["se"], rtol=1e-10, atol=0)
         np.testing.assert_array_equal(out[r]["se"], out[0]["se"])
+
+
+def test_non_finite_scores_take_the_statistics_pass():
+    """A NaN score value raises the meat-quanta path's bound flag (its coarse limb is not finite), so
+    the subset is redone with quanta from the statistics pass: NaN propagates into the same SEs as
+    on the sorted path, and the finite SEs stay finite (std_errors.py:317-333 on NaN data)."""
+    n, k, L = 200_000, 3, [5_000, 300]
+    xs = [f"x{j + 1}" for j in range(k)]
+    d = dict(synth.panel(n, k, L, seed=91))
+    x = np.array(d["x2"], copy=True)
+    x[1234] = np.nan
+    d["x2"] = x
+    fix = _fit(d, xs, ["fe1", "fe2"], ["fe2"])
+    srt = _fit(d, xs, ["fe1", "fe2"], ["fe2"], hooks=SORTED)
+    a, b = _arr(fix, xs, "std_errors"), _arr(srt, xs, "std_errors")
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    assert "cluster_fix" in fix.kernels
