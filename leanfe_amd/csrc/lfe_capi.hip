@@ -1145,6 +1145,7 @@ int lfe_drop_singletons(lfe_ctx* c, int64_t* n_kept, int32_t* fe_dims_out, int32
   c->prepared = true;
   c->demeaned = false;
   c->scores_valid = false;
+  c->clfused = false;
   return LFE_OK;
 }
 

@@ -861,6 +861,95 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
   return rc;
 }
 
+// ---------------------------------------------------------------------------
+// One-way cluster on the primary FE, summed in the residual pass (lfe_gram.hip k_resid_rows<.., true>)
+// ---------------------------------------------------------------------------
+// Quanta before the pass, from its Gram tile and beta (both on the device): rms of the score column
+// x~_j r taken as rms(x~_j) rms(r), with sum r^2 = v' T v (v = [-b0, 1, -b]) in fixed order; the
+// fine limb's range is 16 rms, every column may carry coarse limbs, and one past the exact-sum bound
+// raises the flag (the subset is then redone from score rows).  Deterministic: a fixed function of
+// the tile.
+__global__ void k_clfused_quanta(const double* __restrict__ tile, const double* __restrict__ beta, int p, int64_t n,
+                                 const int32_t* __restrict__ cmax, double* __restrict__ fq) {
+  __shared__ double rss;
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i <= p; ++i) {
+      const double vi = i == 0 ? -beta[0] : i == 1 ? 1.0 : -beta[i - 1];
+      double u = 0.0;
+      for (int j = 0; j <= p; ++j) {
+        const double vj = j == 0 ? -beta[0] : j == 1 ? 1.0 : -beta[j - 1];
+        u += tile[i * 16 + j] * vj;
+      }
+      t += vi * u;
+    }
+    rss = t > 0.0 ? t : 0.0;
+  }
+  __syncthreads();
+  const double nn = n > 0 ? (double)n : 1.0;
+  const double N = (double)max(*cmax, 1);
+  for (int e = threadIdx.x; e < p - 1; e += blockDim.x) {
+    const double g = tile[(e + 2) * 16 + (e + 2)];
+    const double rms = sqrt((g > 0.0 ? g : 0.0) / nn) * sqrt(rss / nn);
+    fix_quanta_col(16.0 * rms, rms, N, fq, e);
+    fq[FQ_BIG * kFqCols + e] = 1.0;
+  }
+}
+
+bool cluster_fused_ok(const lfe_ctx* c) {
+  static const bool env_on = [] {  // "LFE_CL_FUSED=0": score rows and the separate sums (A/B)
+    const char* e = getenv("LFE_CL_FUSED");
+    const char* s = getenv("LFE_CL_STATS");
+    return !(e && e[0] == '0') && !(s && s[0] == '1');
+  }();
+  const int k = c->p - 1;
+  return env_on && clfix_on() && !(c->test_hooks & (LFE_TEST_CLUSTER_SORTED | LFE_TEST_CLUSTER_STATS)) &&
+         c->world == 1 && c->cl.size() == 1 && c->cl_fe.size() == 1 && c->L.P >= 0 && c->cl_fe[0] == c->L.P &&
+         c->L.permuted && !c->w && !c->records && k >= 1 && k <= 63;
+}
+
+int cluster_fused_prepare(lfe_ctx* c) {
+  const int k = c->p - 1, G = c->fe[c->L.P].G;
+  auto& W = c->clw;
+  LFE_TRY(ensure_cluster_ws(c, (size_t)G * k, (size_t)G + 4));  // clS: coarse limbs; clP: counts, [G, max, flag]
+  LFE_TRY(ensure_f64(c, W.srec, W.srec_cap, (size_t)G * k));      // fine limbs
+  LFE_TRY(ensure_f64(c, W.fixq, W.fixq_cap, (size_t)kFqRows * kFqCols));
+  int32_t* cm = c->clP + G;
+  LFE_HIP(hipMemcpyAsync(c->clP, c->fe[c->L.P].cnt, sizeof(int32_t) * G, hipMemcpyDeviceToDevice, c->stream));
+  LFE_HIP(hipMemsetAsync(cm, 0, sizeof(int32_t) * 4, c->stream));
+  hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, c->clP, G, cm);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+int cluster_fused_reset(lfe_ctx* c, const double* tile, const double* beta) {
+  const int k = c->p - 1, G = c->fe[c->L.P].G;
+  auto& W = c->clw;
+  LFE_HIP(hipMemsetAsync(W.srec, 0, sizeof(double) * (size_t)G * k, c->stream));
+  LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)G * k, c->stream));
+  LFE_HIP(hipMemsetAsync(c->clP + G + 2, 0, sizeof(int32_t), c->stream));
+  hipLaunchKernelGGL(k_clfused_quanta, dim3(1), dim3(64), 0, c->stream, tile, beta, c->p,
+                     std::max<int64_t>(c->n_kept, 1), c->clP + G + 1, W.fixq);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
+// the fused pass's sums -> meat (S'S) and cluster count; 1: its bound flag is up (redo from score rows)
+static int cluster_fused_finish(lfe_ctx* c, double* meat, int64_t* G_out, int* redo) {
+  const int k = c->score_k, G = c->fe[c->L.P].G;
+  auto& W = c->clw;
+  int32_t hc[3] = {0, 0, 0};
+  LFE_TRY(d2h_sync(c, hc, c->clP + G, sizeof(hc)));
+  *redo = hc[2] != 0;
+  if (*redo) return LFE_OK;
+  {
+    ProfScope _ps(c, K_CLUSTER_FIX);
+    LFE_TRY(launch_fix_convert(c, W.srec, c->clS, (int64_t)G * k, k, W.fixq));
+  }
+  *G_out = hc[0];
+  return launch_table_gram(c, W.srec, G, k, meat);
+}
+
 int launch_codes_differ(lfe_ctx* c, const int32_t* a, const int32_t* b, int64_t n, int32_t* flag) {
   if (n > 0) hipLaunchKernelGGL(k_cl_same, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, a, b, n, flag);
   LFE_HIP(hipGetLastError());
@@ -869,6 +958,16 @@ int launch_codes_differ(lfe_ctx* c, const int32_t* a, const int32_t* b, int64_t 
 
 // meat and cluster count of one subset (mask over the loaded cluster columns)
 static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
+  if (c->clfused) {  // the residual pass summed the one cluster column (the primary FE)
+    int redo = 0;
+    if (mask == 1) {
+      LFE_TRY(cluster_fused_finish(c, meat, G_out, &redo));
+      if (!redo) return LFE_OK;
+    }
+    // another subset, or a value past the fused quanta's bound: the pass again, writing score rows
+    double st[4];
+    LFE_TRY(launch_resid(c, c->clfused_beta.data(), st, nullptr, 1, 0));
+  }
   const int k = c->score_k;
   const int64_t n = c->n;
   auto& W = c->clw;

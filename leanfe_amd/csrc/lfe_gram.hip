@@ -49,6 +49,14 @@ struct GramArgs {
   int nq;               // number of non-primary FEs
   int qf[kMaxFE];       // their FE indices
   int G_Q;              // levels of qf[0] (its alpha table staged in LDS when it fits)
+  // k_resid_rows<.., CL = true>: the one-way cluster sums on the primary FE formed in the residual
+  // pass itself - every score value's fine limb into the bucket's LDS window of the [G_P][k]
+  // table, coarse limbs into clHi, a coarse limb past the exact-sum bound raises *clFlag
+  unsigned long long* clS;
+  double* clHi;
+  const double* clFq;
+  const int32_t* clCmax;
+  int32_t* clFlag;
 };
 
 template <int NT>
@@ -434,26 +442,45 @@ __global__ __launch_bounds__(TH, (NT == 2 && GU == 1 && TH == 256 && FQ == 1) ? 
 // statistics per block as k_gram<RESID>.
 constexpr int kResThreads = 512;
 
-template <int PM, int UR>
+// CL: the one-way cluster sums on the primary FE (GramArgs.cl*): alpha_Q comes from global memory
+// (L2) and the LDS holds the slice and the bucket's [B][k] window of fine limbs instead; the
+// window goes out by int64 global adds when the bucket changes and at the end (no score rows).
+template <int PM, int UR, bool CL>
 __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* __restrict__ partial, int64_t pstride) {
   constexpr int KM = PM - 1;              // regressor columns held
   constexpr int NM = KM * (KM + 1) / 2;   // meat upper triangle
   constexpr int NW = kResThreads / 64;
   typedef double d2 __attribute__((ext_vector_type(2)));
+  typedef unsigned long long u64;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double* slice = lds;                    // [B][PM] alpha_P slice of the current bucket
-  double* aqL = lds + a.B * PM;           // [G_Q][PM] alpha_Q
+  double* aqL = lds + a.B * PM;           // [G_Q][PM] alpha_Q (!CL)
+  u64* win = reinterpret_cast<u64*>(lds + a.B * PM);  // [B][p - 1] cluster fine limbs (CL)
   __shared__ double red[NW][NM + 4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int p = a.la.p, P = a.la.P;
   const int Q = a.qf[0];
   const double* aQg = a.la.alpha[Q];
+  const int kc = p - 1;  // CL: score columns
   // the pad columns [p, PM) of both tables once, then the rows (the slice rows are restaged per
   // bucket below; their pads stay 0)
-  for (int j = tid; j < (a.B + a.G_Q) * PM; j += kResThreads)
+  for (int j = tid; j < (CL ? a.B : a.B + a.G_Q) * PM; j += kResThreads)
     if (j % PM >= p) lds[j] = 0.0;
-  stage_lds<kResThreads>(aqL, aQg, a.G_Q * p, tid, p, PM);
+  if (CL) {
+    for (int j = tid; j < a.B * kc; j += kResThreads) win[j] = 0ull;
+  } else {
+    stage_lds<kResThreads>(aqL, aQg, a.G_Q * p, tid, p, PM);
+  }
+  const double hlim = CL ? 0x1p51 / (double)max(*a.clCmax, 1) - 1.0 : 0.0;
+  bool over = false;
+  auto flush = [&](int lo) {  // (between barriers) the window's nonzero limbs out, the window zeroed
+    for (int j = tid; j < a.B * kc; j += kResThreads) {
+      const u64 v = win[j];
+      if (v != 0ull && lo + j / kc < a.G_P) atomicAdd(&a.clS[(int64_t)lo * kc + j], v);
+      win[j] = 0ull;
+    }
+  };
   double beta[PM];
 #pragma unroll
   for (int cc = 0; cc < PM; ++cc) beta[cc] = cc < p ? a.beta[cc] : 0.0;
@@ -473,6 +500,7 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
     const int lo = it.x << a.la.s;
     if (it.x != staged) {
       __syncthreads();
+      if (CL && staged >= 0) flush(staged << a.la.s);
       {  // rows past G_P: data columns cleared (their codes never occur)
         const int nr = max(0, min(a.B, a.G_P - lo));
         stage_lds<kResThreads>(slice, a.la.alpha[P] + (int64_t)lo * p, nr * p, tid, p, PM);
@@ -509,13 +537,23 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
       for (int u = 0; u < UR; ++u) {
         const bool valid = hq[u] >= 0;
         const d2* sp = reinterpret_cast<const d2*>(slice + (valid ? hq[u] - lo : 0) * PM);
-        const d2* qp = reinterpret_cast<const d2*>(aqL + qq[u] * PM);
         double xt[PM];
+        if (CL) {  // alpha_Q rows from global memory (an L2-resident table, unpadded rows)
+          const double* qg = aQg + (int64_t)qq[u] * p;
 #pragma unroll
-        for (int c2 = 0; c2 < PM / 2; ++c2) {
-          const d2 s2 = sp[c2], q2 = qp[c2];
-          xt[2 * c2] = x[u][2 * c2] - s2.x - q2.x;
-          xt[2 * c2 + 1] = x[u][2 * c2 + 1] - s2.y - q2.y;
+          for (int c2 = 0; c2 < PM / 2; ++c2) {
+            const d2 s2 = sp[c2];
+            xt[2 * c2] = x[u][2 * c2] - s2.x - (2 * c2 < p ? qg[2 * c2] : 0.0);
+            xt[2 * c2 + 1] = x[u][2 * c2 + 1] - s2.y - (2 * c2 + 1 < p ? qg[2 * c2 + 1] : 0.0);
+          }
+        } else {
+          const d2* qp = reinterpret_cast<const d2*>(aqL + qq[u] * PM);
+#pragma unroll
+          for (int c2 = 0; c2 < PM / 2; ++c2) {
+            const d2 s2 = sp[c2], q2 = qp[c2];
+            xt[2 * c2] = x[u][2 * c2] - s2.x - q2.x;
+            xt[2 * c2 + 1] = x[u][2 * c2 + 1] - s2.y - q2.y;
+          }
         }
         // r = y~ - beta0 - sum_j beta_j x~_j (polars_impl.py:229)
         double res = xt[0] - beta[0];
@@ -541,8 +579,25 @@ __global__ __launch_bounds__(kResThreads) void k_resid_rows(GramArgs a, double* 
           for (int j = 0; j < KM; ++j)
             if (j + 1 < p) a.scores[(int64_t)r * (p - 1) + j] = wv[j];
         }
+        if (CL) {  // the score row into the cluster's window entries (lfe_cluster.hip's two limbs)
+          const int hl = (hq[u] - lo) * kc;
+#pragma unroll
+          for (int j = 0; j < KM; ++j) {
+            if (j + 1 >= p) break;
+            double hh;
+            const u64 xi = fix_split(wv[j], fix_col(a.clFq, j), hh);
+            if (xi) atomicAdd(&win[hl + j], xi);
+            if (hh != 0.0) atomicAdd(&a.clHi[(int64_t)hq[u] * kc + j], hh);
+            over |= !(fabs(hh) <= hlim);
+          }
+        }
       }
     }
+  }
+  if (CL) {
+    __syncthreads();
+    if (staged >= 0) flush(staged << a.la.s);
+    if (__any(over) && lane == 0) *a.clFlag = 1;
   }
   // block reduction: wave sums over DPP lane moves (VALU, fixed order; xor shuffles of the
   // NM + 4 sums cost ds_bpermute latency at the kernel's tail), then the NW wave rows in LDS
@@ -1584,13 +1639,17 @@ int launch_gram(lfe_ctx* c, double* host_gram) {
 // row-per-lane residual pass (k_resid_rows): two FEs, unweighted, p <= 12, both
 // alpha tables (padded to PM doubles per row) in LDS; leaves the reduced [16][16]
 // tile + 4 statistics (260 doubles, all ranks) in out_dev
-static int resid_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
+static int resid_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev, bool cl = false) {
   const int p = c->p;
   const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
-  const size_t dyn = sizeof(double) * ((size_t)a.B + a.G_Q) * PM;
-  const void* fn = PM == 4   ? reinterpret_cast<const void*>(&k_resid_rows<4, 2>)
-                   : PM == 8 ? reinterpret_cast<const void*>(&k_resid_rows<8, 2>)
-                             : reinterpret_cast<const void*>(&k_resid_rows<12, 2>);
+  const size_t dyn = cl ? sizeof(double) * (size_t)a.B * (PM + (p - 1))
+                        : sizeof(double) * ((size_t)a.B + a.G_Q) * PM;
+  const void* fn = cl ? (PM == 4   ? reinterpret_cast<const void*>(&k_resid_rows<4, 2, true>)
+                         : PM == 8 ? reinterpret_cast<const void*>(&k_resid_rows<8, 2, true>)
+                                   : reinterpret_cast<const void*>(&k_resid_rows<12, 2, true>))
+                      : (PM == 4   ? reinterpret_cast<const void*>(&k_resid_rows<4, 2, false>)
+                         : PM == 8 ? reinterpret_cast<const void*>(&k_resid_rows<8, 2, false>)
+                                   : reinterpret_cast<const void*>(&k_resid_rows<12, 2, false>));
   if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
   const int nblocks = row_blocks(c, resident_blocks(c, fn, kResThreads, dyn));
   const int64_t pstride = 256 + 4;
@@ -2019,6 +2078,11 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
   c->gram_spec = false;
   if (!(resid_rows_ok(c, a) && c->p <= 11)) return 1;
   const int p = c->p, k = p - 1;
+  // a one-way cluster on the primary FE: its sums in this pass (no score rows written)
+  const bool cl = keep_scores && cluster_fused_ok(c) &&
+                  (size_t)a.B * (12 + k) * 8 + 5120 <= 160 * 1024;
+  c->clfused = false;
+  if (cl) LFE_TRY(cluster_fused_prepare(c));
   // dred: [0, 256) design tile | [256, 516) residual tile + stats | 516 ok | [520, 532) beta | 532 tables guard
   LFE_TRY(ensure_dred(c, 544));
   std::vector<double> h(533);
@@ -2041,8 +2105,17 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
     ar.qf[0] = 1 - a.la.P;
     ar.G_Q = c->fe[ar.qf[0]].G;
     ar.beta = buf == c->dred ? c->dbeta : c->dspec + 520;
-    ar.scores = keep_scores ? c->scores : nullptr;
-    LFE_TRY(resid_rows_enqueue(c, ar, buf + 256));
+    ar.scores = keep_scores && !cl ? c->scores : nullptr;
+    if (cl) {  // quanta from this pass's Gram tile and beta (on the device), the sums zeroed
+      LFE_TRY(cluster_fused_reset(c, buf, ar.beta));
+      const int G = c->fe[c->L.P].G;
+      ar.clS = reinterpret_cast<unsigned long long*>(c->clw.srec);
+      ar.clHi = c->clS;
+      ar.clFq = c->clw.fixq;
+      ar.clCmax = c->clP + G + 1;
+      ar.clFlag = c->clP + G + 2;
+    }
+    LFE_TRY(resid_rows_enqueue(c, ar, buf + 256, cl));
     LFE_TRY(d2h_sync(c, h.data(), buf, sizeof(double) * 533));
     if (pass == 1 || h[532] == 1.0) break;  // guard failed: the explicit design pass
   }
@@ -2059,10 +2132,13 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
   c->score_k = k;
   c->score_meat = meat;  // the row kernel's meat is sum s s' (unweighted two-FE case)
   c->score_meat_ok = keep_scores && c->world == 1;
+  c->clfused = cl;
+  if (cl) c->clfused_beta.assign(beta_full, beta_full + p);
   return LFE_OK;
 }
 
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores, int icpt) {
+  c->clfused = false;  // this pass writes the score rows
   GramArgs a = base_args(c);
   LFE_TRY(h2d_small(c, c->dbeta, beta_full, sizeof(double) * c->p));
   a.beta = c->dbeta;

@@ -288,6 +288,10 @@ struct lfe_ctx {
   std::vector<int32_t*> cl;
   std::vector<int32_t> cl_levels;
   std::vector<int> cl_fe;  // per cluster column: the FE column it repeats (equal codes), or -1
+  // the one cluster column is the primary FE: its sums came out of the residual pass (no score rows;
+  // lfe_gram.hip k_resid_rows<.., true>, finished by lfe_cluster.hip)
+  bool clfused = false;
+  std::vector<double> clfused_beta;  // beta_full of that pass (to redo it with score rows)
   lfe::ClusterWS clw;
   // pinned host staging (small transfers avoid the runtime's pageable path)
   char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
@@ -520,6 +524,10 @@ void free_stream_clusters(lfe_ctx* c);
 // records in c->clS (lfe_cluster.hip)
 int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R, const double* table,
                  int k, int32_t* G_out);  // weighted streamed fits: w's max / rms into fixq column p
+bool cluster_fused_ok(const lfe_ctx* c);                       // lfe_cluster.hip
+int cluster_fused_prepare(lfe_ctx* c);                         // buffers and counts, before the pass
+int cluster_fused_reset(lfe_ctx* c, const double* tile, const double* beta);  // zeroed sums + quanta
+int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores, int icpt);
 int launch_codes_differ(lfe_ctx* c, const int32_t* a, const int32_t* b, int64_t n, int32_t* flag);  // lfe_cluster.hip
 int stream_materialize_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows);  // lfe_wide.hip
 int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t ld, int64_t row0, int64_t rows,

@@ -134,18 +134,43 @@ def test_one_column_subset_on_emulated_ranks():
         np.testing.assert_array_equal(out[r]["se"], out[0]["se"])
 
 
-def test_non_finite_scores_take_the_statistics_pass():
-    """A NaN score value raises the meat-quanta path's bound flag (its coarse limb is not finite), so
-    the subset is redone with quanta from the statistics pass: NaN propagates into the same SEs as
-    on the sorted path, and the finite SEs stay finite (std_errors.py:317-333 on NaN data)."""
+@pytest.mark.parametrize("cl", [["fe2"], ["fe1"]])
+def test_non_finite_scores_take_the_statistics_pass(cl):
+    """A NaN score value raises the bound flag of the quanta that need no statistics pass (its coarse
+    limb is not finite): the one-way sums on the primary FE formed in the residual pass (fe1) redo
+    the pass with score rows, the sort-free sums (fe2) redo the subset with a statistics pass; NaN
+    propagates into the same SEs as on the sorted path (std_errors.py:317-333 on NaN data)."""
     n, k, L = 200_000, 3, [5_000, 300]
     xs = [f"x{j + 1}" for j in range(k)]
     d = dict(synth.panel(n, k, L, seed=91))
     x = np.array(d["x2"], copy=True)
     x[1234] = np.nan
     d["x2"] = x
-    fix = _fit(d, xs, ["fe1", "fe2"], ["fe2"])
-    srt = _fit(d, xs, ["fe1", "fe2"], ["fe2"], hooks=SORTED)
+    fix = _fit(d, xs, ["fe1", "fe2"], cl)
+    srt = _fit(d, xs, ["fe1", "fe2"], cl, hooks=SORTED)
     a, b = _arr(fix, xs, "std_errors"), _arr(srt, xs, "std_errors")
     np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
     assert "cluster_fix" in fix.kernels
+
+
+@pytest.mark.parametrize("k,L", [(4, [20_000, 600]), (10, [30_000, 1_000])])
+def test_one_way_cluster_on_the_primary_fe_in_the_residual_pass(k, L):
+    """A one-way cluster on the primary FE (reg_test.py:55): its sums come out of the residual pass
+    (k_resid_rows<.., true>: no score rows), against the separate sort-free sums (statistics hook),
+    the sorted path and the oracle; bit-identical repeats."""
+    from oracle import altproj
+
+    n = 600_000
+    xs = [f"x{j + 1}" for j in range(k)]
+    d = dict(synth.panel(n, k, L, seed=57))
+    fused = _fit(d, xs, ["fe1", "fe2"], ["fe1"])
+    again = _fit(d, xs, ["fe1", "fe2"], ["fe1"])
+    st = _fit(d, xs, ["fe1", "fe2"], ["fe1"], hooks=STATS)
+    srt = _fit(d, xs, ["fe1", "fe2"], ["fe1"], hooks=SORTED)
+    o = altproj.fit(d, "y", xs, ["fe1", "fe2"], vcov="cluster", cluster_cols=["fe1"])
+    assert fused.n_clusters == o["n_clusters"] == srt.n_clusters
+    assert fused.iterations == o["iterations"]
+    np.testing.assert_allclose(_arr(fused, xs, "std_errors"), o["se"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(_arr(fused, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
+    np.testing.assert_allclose(_arr(st, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
+    np.testing.assert_array_equal(_arr(fused, xs, "std_errors"), _arr(again, xs, "std_errors"))
