@@ -153,8 +153,8 @@ def test_non_finite_scores_take_the_statistics_pass(cl):
     assert "cluster_fix" in fix.kernels
 
 
-@pytest.mark.parametrize("k,L", [(4, [20_000, 600]), (10, [30_000, 1_000])])
-def test_one_way_cluster_on_the_primary_fe_in_the_residual_pass(k, L):
+@pytest.mark.parametrize("k,L,singletons", [(4, [20_000, 600], 0), (10, [30_000, 1_000], 0), (6, [25_000, 800], 40)])
+def test_one_way_cluster_on_the_primary_fe_in_the_residual_pass(k, L, singletons):
     """A one-way cluster on the primary FE (reg_test.py:55): its sums come out of the residual pass
     (k_resid_rows<.., true>: no score rows), against the separate sort-free sums (statistics hook),
     the sorted path and the oracle; bit-identical repeats."""
@@ -163,13 +163,17 @@ def test_one_way_cluster_on_the_primary_fe_in_the_residual_pass(k, L):
     n = 600_000
     xs = [f"x{j + 1}" for j in range(k)]
     d = dict(synth.panel(n, k, L, seed=57))
+    if singletons:  # rows alone in their primary level: dropped (polars_impl.py:477-482), still keyed
+        f1 = np.array(d["fe1"], copy=True)
+        f1[:singletons] = L[0] + np.arange(singletons)
+        d["fe1"] = f1
     fused = _fit(d, xs, ["fe1", "fe2"], ["fe1"])
     again = _fit(d, xs, ["fe1", "fe2"], ["fe1"])
     st = _fit(d, xs, ["fe1", "fe2"], ["fe1"], hooks=STATS)
     srt = _fit(d, xs, ["fe1", "fe2"], ["fe1"], hooks=SORTED)
     o = altproj.fit(d, "y", xs, ["fe1", "fe2"], vcov="cluster", cluster_cols=["fe1"])
     assert fused.n_clusters == o["n_clusters"] == srt.n_clusters
-    assert fused.iterations == o["iterations"]
+    assert fused.iterations == o["iterations"] and fused.n_obs == o["n_obs"] == n - singletons
     np.testing.assert_allclose(_arr(fused, xs, "std_errors"), o["se"], rtol=1e-10, atol=0)
     np.testing.assert_allclose(_arr(fused, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
     np.testing.assert_allclose(_arr(st, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
