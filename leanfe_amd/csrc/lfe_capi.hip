@@ -1096,7 +1096,7 @@ int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const i
   c->cl_levels.assign(cl_levels, cl_levels + m);
   const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
   // [0]: a code out of range; [1 + j kMaxFE + f]: column j differs from FE f (of the same level count)
-  LFE_TRY(ensure_iscratch(c, std::max<size_t>(kIscratchInts + 1, 1 + (size_t)m * kMaxFE)));
+  LFE_TRY(ensure_iscratch(c, std::max<size_t>(kIscratchInts, 1 + (size_t)m * kMaxFE)));
   LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t) * (1 + (size_t)m * kMaxFE), c->stream));
   int rc = LFE_OK;
   for (int j = 0; j < m && rc == LFE_OK; ++j) {

@@ -732,7 +732,7 @@ __global__ __launch_bounds__(kClFixThreads) void k_clfix_add(ClFixAdd a) {
   if (CHECK && __any(over) && (tid & 63) == 0) a.oflag[0] = 1;
 }
 
-// flag[0] = 1 when some kept row's cluster code differs from its primary FE code
+// flag[0] = 1 when some row's code in a differs from its code in p (rows with p < 0 are skipped)
 __global__ void k_cl_same(const int32_t* __restrict__ a, const int32_t* __restrict__ p, int64_t n,
                           int32_t* __restrict__ flag) {
   bool diff = false;

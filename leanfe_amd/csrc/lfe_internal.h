@@ -24,7 +24,6 @@ constexpr int kIscratchCmax = 2 * kMaxFE + 8;
 constexpr int kIsDnPre = 2 * kMaxFE + 6;  // iscratch: a primary level of > 65535 rows in the pre-filter table build
 constexpr int kIsCmaxOver = 2 * kMaxFE + 7;  // iscratch: ranks whose primary FE keeps a level of > 65535 rows (owner)
 constexpr int kIscratchInts = kIscratchCmax + kMaxFE;
-constexpr int kIsClSame = kIscratchInts;  // iscratch: a cluster column differs from the primary FE (lfe_cluster.hip)
 constexpr int kBlock = 256;      // threads per workgroup for simple streaming kernels
 constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
 constexpr int kLdsBudget = 64 * 1024;  // bytes of LDS tables per sweep workgroup (2 WG per CU)
