@@ -1095,9 +1095,11 @@ int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const i
   c->cl.assign(m, nullptr);
   c->cl_levels.assign(cl_levels, cl_levels + m);
   const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-  // [0]: a code out of range; [1 + j kMaxFE + f]: column j differs from FE f (of the same level count)
-  LFE_TRY(ensure_iscratch(c, std::max<size_t>(kIscratchInts, 1 + (size_t)m * kMaxFE)));
-  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t) * (1 + (size_t)m * kMaxFE), c->stream));
+  // [0]: a code out of range; [kIsClFlags + j kMaxFE + f]: column j differs from FE f (of the same
+  // level count) - past the drop's counts, which a later demean still reads
+  LFE_TRY(ensure_iscratch(c, kIscratchAll));
+  LFE_HIP(hipMemsetAsync(c->iscratch, 0, sizeof(int32_t), c->stream));
+  LFE_HIP(hipMemsetAsync(c->iscratch + kIsClFlags, 0, sizeof(int32_t) * (size_t)m * kMaxFE, c->stream));
   int rc = LFE_OK;
   for (int j = 0; j < m && rc == LFE_OK; ++j) {
     rc = dalloc(&c->cl[j], (size_t)c->ld);
@@ -1118,15 +1120,15 @@ int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const i
   for (int j = 0; j < m && c->n > 0; ++j)
     for (int f = 0; f < c->F; ++f)
       if (c->fe[f].G == cl_levels[j]) LFE_TRY(launch_codes_differ(c, c->cl[j], c->fe[f].code, c->n,
-                                                                  c->iscratch + 1 + j * kMaxFE + f));
-  std::vector<int32_t> h(1 + (size_t)m * kMaxFE, 0);
+                                                                  c->iscratch + kIsClFlags + j * kMaxFE + f));
+  std::vector<int32_t> h(kIsClFlags + (size_t)m * kMaxFE, 0);
   LFE_HIP(hipMemcpyAsync(h.data(), c->iscratch, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, c->stream));
   LFE_HIP(hipStreamSynchronize(c->stream));
   if (h[0]) return fail(LFE_EINVAL, "cluster codes must be dense int32 in [0, n_levels)");
   c->cl_fe.assign(m, -1);
   for (int j = 0; j < m && c->n > 0; ++j)
     for (int f = 0; f < c->F && c->cl_fe[j] < 0; ++f)
-      if (c->fe[f].G == cl_levels[j] && h[1 + j * kMaxFE + f] == 0) c->cl_fe[j] = f;
+      if (c->fe[f].G == cl_levels[j] && h[kIsClFlags + j * kMaxFE + f] == 0) c->cl_fe[j] = f;
   return LFE_OK;
 }
 

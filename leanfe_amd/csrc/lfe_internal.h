@@ -24,6 +24,10 @@ constexpr int kIscratchCmax = 2 * kMaxFE + 8;
 constexpr int kIsDnPre = 2 * kMaxFE + 6;  // iscratch: a primary level of > 65535 rows in the pre-filter table build
 constexpr int kIsCmaxOver = 2 * kMaxFE + 7;  // iscratch: ranks whose primary FE keeps a level of > 65535 rows (owner)
 constexpr int kIscratchInts = kIscratchCmax + kMaxFE;
+// iscratch's allocation: the counts above, then lfe_load_clusters' per (cluster column, FE) flags
+// (allocated whole at the first use, so that loading clusters after the drop keeps the counts)
+constexpr int kIsClFlags = kIscratchInts;
+constexpr int kIscratchAll = kIsClFlags + 30 * kMaxFE;
 constexpr int kBlock = 256;      // threads per workgroup for simple streaming kernels
 constexpr int kSweepThreads = 512;   // sweep kernels (8 waves)
 constexpr int kLdsBudget = 64 * 1024;  // bytes of LDS tables per sweep workgroup (2 WG per CU)

@@ -998,7 +998,7 @@ int prepare_layout(lfe_ctx* c) {
   // all-reduce - in the two-FE sweeps and in the general sweeps (any F, weights) alike
   c->owner_on = c->world > 1 && c->owner_fe >= 0 && c->owner_fe == L.P && !c->records;
   // every count / drop / group-sum table and the scratch counters zeroed in one launch
-  LFE_TRY(ensure_iscratch(c, kIscratchInts));
+  LFE_TRY(ensure_iscratch(c, kIscratchAll));
   {
     std::vector<std::pair<void*, size_t>> z;
     for (int f = 0; f < c->F; ++f) {

@@ -177,14 +177,16 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             eng.load([Y] + Xc, codes, levels, w)
             n_initial = Y.size
         cl_loaded = None
+        if v == "cluster" and strategy != "compress":
+            # cluster columns load before the singleton drop: the partition moves them with the rows
+            # (no gathers into the layout later), an owner re-shard moves them too, and a one-way
+            # cluster on the primary FE is then summed inside the residual pass (lfe_gram.hip)
+            cl_loaded = _load_clusters(eng, cols, cluster_cols, sharded)
         if (sharded and len(fe_cols) >= 2 and strategy in ("auto", "alt_proj")
                 and os.environ.get("LEANFE_HIP_RESHARD", "1") != "0"):
             # contiguous row blocks -> owner-sharded rows (lfe_reshard_owner): every rank then holds
             # all rows of a range of the primary FE's (most levels) levels, and a projection
-            # all-reduces only the other FEs' tables - two FEs or more, weighted or not.  Cluster
-            # columns load first, so that they move with their rows.
-            if v == "cluster":
-                cl_loaded = _load_clusters(eng, cols, cluster_cols, sharded)
+            # all-reduces only the other FEs' tables - two FEs or more, weighted or not
             try:
                 eng.reshard_owner(max(range(len(fe_cols)), key=lambda f: levels[f]))
             except (ValueError, MemoryError):
