@@ -1,7 +1,8 @@
 #!/bin/bash
-# round 5 measurement set (beside round_profile.sh): preset lines (with CPU baselines), config lines
-# 1-5 and the 8-rank owner shard, then rocprofv3 kernel stats of config 1, config 4, the shard and
-# the clustered presets.  Any failure stops the script.
+# Measurement set beside round_profile.sh: preset lines (with CPU baselines), config lines 1-5 and
+# the 8-rank owner shard, then rocprofv3 kernel stats of config 1, config 4, the shard and the
+# clustered presets (profiles/rNN/presets_bench.jsonl, configs_bench.jsonl, *_kernel_stats.csv).
+# Any failure stops the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 out=gpurun_out/r5e
