@@ -5,7 +5,7 @@
 # Any failure stops the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-out=gpurun_out/r5e
+out=gpurun_out/lines
 mkdir -p $out
 : > $out/configs.jsonl
 bash tools/bench_presets.sh || exit $?
