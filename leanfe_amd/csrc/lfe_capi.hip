@@ -131,37 +131,28 @@ int ensure_u64(lfe_ctx*, uint64_t*& p, size_t& cap, size_t elems) { return ensur
 int ensure_i8(lfe_ctx*, int8_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 int ensure_u8(lfe_ctx*, uint8_t*& p, size_t& cap, size_t elems) { return ensure(p, cap, elems); }
 
-struct ZeroArgs {
-  uint32_t* p[32];
-  int64_t end[32];  // running word offsets: range j covers [end[j - 1], end[j])
-  int n;
-};
-
-// every range over the whole grid in turn, its 16-byte-aligned body in 16-byte stores
 __global__ void k_zero_ranges(ZeroArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
-  for (int j = 0; j < a.n; ++j) {
-    uint32_t* p = a.p[j];
-    const int64_t len = a.end[j] - (j ? a.end[j - 1] : 0);
-    const int64_t head = min(len, (int64_t)(((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4));
-    const int64_t nb = (len - head) / 4;
-    uint4* q = reinterpret_cast<uint4*>(p + head);
-    for (int64_t e = t; e < head; e += nt) p[e] = 0u;
-    for (int64_t e = t; e < nb; e += nt) q[e] = uint4{0u, 0u, 0u, 0u};
-    for (int64_t e = head + 4 * nb + t; e < len; e += nt) p[e] = 0u;
+  zero_ranges_part(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+}
+
+int build_zero_args(const std::vector<std::pair<void*, size_t>>& ranges, ZeroArgs* a, int64_t* words) {
+  *a = ZeroArgs{};
+  int64_t off = 0;
+  for (const auto& r : ranges) {
+    if (!r.first || r.second == 0) continue;
+    if (a->n == 32) return fail(LFE_EINVAL, "zero_ranges: at most 32 ranges");
+    a->p[a->n] = static_cast<uint32_t*>(r.first);
+    off += (int64_t)(r.second / 4);
+    a->end[a->n++] = off;
   }
+  if (words) *words = off;
+  return LFE_OK;
 }
 
 int zero_ranges(lfe_ctx* c, const std::vector<std::pair<void*, size_t>>& ranges) {
   ZeroArgs a{};
   int64_t off = 0;
-  for (const auto& r : ranges) {
-    if (!r.first || r.second == 0) continue;
-    if (a.n == 32) return fail(LFE_EINVAL, "zero_ranges: at most 32 ranges");
-    a.p[a.n] = static_cast<uint32_t*>(r.first);
-    off += (int64_t)(r.second / 4);
-    a.end[a.n++] = off;
-  }
+  LFE_TRY(build_zero_args(ranges, &a, &off));
   if (a.n == 0) return LFE_OK;
   hipLaunchKernelGGL(k_zero_ranges, dim3(grid_for((off + 3) / 4, 256, 1024)), dim3(256), 0, c->stream, a);
   LFE_HIP(hipGetLastError());

@@ -612,6 +612,27 @@ int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
 int exclusive_scan2(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2);
 // zero up to 32 device ranges (byte counts multiples of 4) in one launch instead of a memset each
 int zero_ranges(lfe_ctx* c, const std::vector<std::pair<void*, size_t>>& ranges);
+// the same ranges as kernel arguments, for a kernel that zeroes them beside its own work
+// (lfe_prep.hip k_part_hist): range j covers words [end[j - 1], end[j]) of the concatenation
+struct ZeroArgs {
+  uint32_t* p[32];
+  int64_t end[32];
+  int n;
+};
+int build_zero_args(const std::vector<std::pair<void*, size_t>>& ranges, ZeroArgs* a, int64_t* words);
+// thread t of nt: every range in turn, its 16-byte-aligned body in 16-byte stores
+__device__ inline void zero_ranges_part(const ZeroArgs& a, int64_t t, int64_t nt) {
+  for (int j = 0; j < a.n; ++j) {
+    uint32_t* p = a.p[j];
+    const int64_t len = a.end[j] - (j ? a.end[j - 1] : 0);
+    const int64_t head = min(len, (int64_t)(((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4));
+    const int64_t nb = (len - head) / 4;
+    uint4* q = reinterpret_cast<uint4*>(p + head);
+    for (int64_t e = t; e < head; e += nt) p[e] = 0u;
+    for (int64_t e = t; e < nb; e += nt) q[e] = uint4{0u, 0u, 0u, 0u};
+    for (int64_t e = head + 4 * nb + t; e < len; e += nt) p[e] = 0u;
+  }
+}
 // device -> host copy of a small result through pinned staging, synchronizing the stream
 int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes);
 // device -> host copy into the pinned staging region without waiting; d2h_wait finishes it

@@ -92,10 +92,12 @@ __global__ void k_hist_global(const int32_t* __restrict__ code, int64_t n, int32
 }
 
 // per-chunk bucket histogram, chunk = rows [w*cw, (w+1)*cw) -> counts[bucket][chunk]
+// (z: the drop's tables and counters zeroed by the same grid, one launch fewer; n == 0 ranges: none)
 __global__ __launch_bounds__(256) void k_part_hist(const int32_t* __restrict__ code, int64_t n, int s, int nb,
-                                                   int64_t cw, int nw, int32_t* __restrict__ counts) {
+                                                   int64_t cw, int nw, int32_t* __restrict__ counts, ZeroArgs z) {
   extern __shared__ int32_t h[];
   const int w = blockIdx.x;
+  zero_ranges_part(z, (int64_t)w * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
   for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)w * cw, r1 = min(n, r0 + cw);
@@ -999,6 +1001,7 @@ int prepare_layout(lfe_ctx* c) {
   c->owner_on = c->world > 1 && c->owner_fe >= 0 && c->owner_fe == L.P && !c->records;
   // every count / drop / group-sum table and the scratch counters zeroed in one launch
   LFE_TRY(ensure_iscratch(c, kIscratchAll));
+  ZeroArgs zpart{};  // zeroed by k_part_hist instead (the two-FE fast layout)
   {
     std::vector<std::pair<void*, size_t>> z;
     for (int f = 0; f < c->F; ++f) {
@@ -1011,7 +1014,14 @@ int prepare_layout(lfe_ctx* c) {
     // shard (an owner shard's other levels, levels whose rows were all dropped stay 0)
     if (L.P >= 0) z.push_back({c->fe[L.P].alpha, sizeof(double) * (size_t)c->fe[L.P].G * c->p});
     z.push_back({c->iscratch, sizeof(int32_t) * kIscratchInts});
-    LFE_TRY(zero_ranges(c, z));
+    if (L.permuted && item_counts && n > 0) {
+      // nothing reads these before the partition histogram: it zeroes them (colstat's head too)
+      LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead));
+      z.push_back({c->colstat, sizeof(double) * kColStatHead});
+      LFE_TRY(build_zero_args(z, &zpart, nullptr));
+    } else {
+      LFE_TRY(zero_ranges(c, z));
+    }
     c->sums_zeroed = true;
   }
   // pre-filter counts of every FE (on input codes, except P when bucketed)
@@ -1071,15 +1081,29 @@ int prepare_layout(lfe_ctx* c) {
     const int per = (int)(cw / nth);
     const int nw = (int)((n + cw - 1) / cw);
     // column statistics of the exact group sums, written by the scatter (max |x| by atomicMax)
-    LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nw * c->p));
-    LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
+    if (zpart.n == 0 || c->colstat_cap < (size_t)kColStatHead + (size_t)nw * c->p) {
+      // (a larger colstat moves: its head zeroed here, and the ranges' copy of the old pointer
+      // dropped - the ranges are zeroed now by their own launch)
+      LFE_TRY(ensure_f64(c, c->colstat, c->colstat_cap, (size_t)kColStatHead + (size_t)nw * c->p));
+      if (zpart.n > 0) {
+        std::vector<std::pair<void*, size_t>> z2;
+        for (int j = 0; j < zpart.n; ++j) {
+          const int64_t len = zpart.end[j] - (j ? zpart.end[j - 1] : 0);
+          z2.push_back({zpart.p[j], (size_t)len * 4});
+        }
+        z2.pop_back();  // the old colstat head
+        LFE_TRY(zero_ranges(c, z2));
+        zpart = ZeroArgs{};
+      }
+      LFE_HIP(hipMemsetAsync(c->colstat, 0, sizeof(double) * kColStatHead, c->stream));
+    }
     c->colstat_chunks = nw;
     const int64_t m = (int64_t)nb * nw;
     LFE_TRY(ensure_pcounts(c, (size_t)m + nb + 1, 0));
     {
       ProfScope _ps(c, K_PART_HIST);
       hipLaunchKernelGGL(k_part_hist, dim3(nw), dim3(256), sizeof(int32_t) * nb, c->stream, c->fe[L.P].code, n, L.s,
-                         nb, cw, nw, c->pcounts);
+                         nb, cw, nw, c->pcounts, zpart);
     }
     LFE_HIP(hipGetLastError());
     // bucket starts depend on the scan only (gathered by its last kernel): fetch them now and
