@@ -111,9 +111,9 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     num_cols = [y_col] + x_cols + instruments  # the columns leanfe demeans (polars_impl.py:486)
 
     if len(num_cols) > MAX_CONTEXT_COLS:
-        if instruments or sharded or strategy == "compress":
+        if sharded or strategy == "compress":
             raise ValueError(f"{len(num_cols)} columns: a fit wider than {MAX_CONTEXT_COLS} columns runs in one "
-                             "process, without instruments and with strategy alt_proj / demean")
+                             "process, with strategy alt_proj / demean")
         ooc = None
         if out_of_core:
             if not fe_cols or strategy not in ("auto", "alt_proj", "demean"):
@@ -127,7 +127,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         elif stream:  # a Parquet path read resident: the numeric columns too
             cols.update(frame.get_columns(data, [c for c in num_cols if c not in cols]))
         return _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc, strategy, demean_tol,
-                         max_iter, formula, t_start, say, engine, device, ooc)
+                         max_iter, formula, t_start, say, engine, device, ooc, instruments)
 
     own_engine = engine is None
     eng = engine if engine is not None else Engine(_default_device() if device is None else device)
@@ -489,7 +489,7 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
 
 
 def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc, strategy, demean_tol, max_iter,
-              formula, t_start, say, engine=None, device=None, ooc=None) -> LeanFEResult:
+              formula, t_start, say, engine=None, device=None, ooc=None, instruments=()) -> LeanFEResult:
     """A fit of more than 63 columns (e.g. an event study's i(year) dummies, polars_impl.py:27-69,
     whose X'X the reference forms at any width, :165-209): the columns run in blocks of engine
     contexts - the first [y] + 62 regressors with the stop test, every later one 63 regressors
@@ -500,15 +500,22 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
     the resident fit (inference.py, std_errors.py:183-441).  ``ooc`` (out-of-core source: the
     arguments of _stream_chunks): every block is a streamed context - group sums from one pass over
     its columns, codes-only sweeps, then a second pass writes its x~ into D (lfe_stream_materialize) -
-    so the columns are never resident twice; D itself (P n doubles) stays on the device."""
-    k = len(x_cols)
-    P = 2 + k
+    so the columns are never resident twice; D itself (P n doubles) stays on the device.
+    ``instruments`` (IV / 2SLS, common.py:188-287): D = [1_kept, y~, x~, z~]; 2SLS from D's Gram
+    (inference.IVSystem), the residual over u = [1, x~, z~] and its meats over u (D's column 1
+    dropped), mapped to the X_hat space as in the resident fit (std_errors.py:448-602)."""
+    instruments = list(instruments)
+    k, mz = len(x_cols), len(instruments)
+    if mz and not fe_cols:
+        raise ValueError("a wide IV fit takes one or more FEs (demeaned instruments are never all ones)")
+    dcols = list(x_cols) + instruments  # D's columns after [1, y~]
+    P = 2 + len(dcols)
     w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
     y = None if ooc is not None else np.asarray(cols[y_col], dtype=np.float64)
     n = ooc["n_rows"] if ooc is not None else y.size
     ldD = (n + 63) // 64 * 64
     per = MAX_CONTEXT_COLS - (1 if ooc is not None and w is not None else 0)  # streamed weighted sums: p <= 62
-    blocks = [x_cols[:per - 1]] + [x_cols[j:j + per] for j in range(per - 1, k, per)]
+    blocks = [dcols[:per - 1]] + [dcols[j:j + per] for j in range(per - 1, len(dcols), per)]
     dev = _default_device() if device is None else device
     eng = engine if engine is not None else Engine(dev)
     D = r = None
@@ -526,7 +533,7 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
             raise ValueError("Strategy 'alt_proj' requires FE-cols. Use strategy='ols' instead for OLS without FE.")
         if strategy == "ols" and fe_cols:
             raise ValueError("Strategy 'ols' takes no fixed effects")
-        say(f"Wide fit: {k} regressors in {len(blocks)} column blocks")
+        say(f"Wide fit: {k} regressors{f' and {mz} instruments' if mz else ''} in {len(blocks)} column blocks")
         t0 = time.perf_counter()
         D = eng.dev_alloc(P * ldD)
         eng.sync()  # zero-filled before any block's context writes into it
@@ -545,7 +552,7 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
                     sel = list(range(lo, lo + pb))
 
                     def chunks(sel=sel):
-                        return _stream_chunks(ooc["source"], cols, n, ooc["chunk_rows"], y_col, x_cols, [],
+                        return _stream_chunks(ooc["source"], cols, n, ooc["chunk_rows"], y_col, x_cols, instruments,
                                               ooc["plan"], ooc["x_base"], select=sel)
 
                     e.load_codes(codes, levels, pb, weights=w)
@@ -581,27 +588,40 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
             absorbed_df = sum(fe_dims) - len(fe_cols)
         df_resid = n_obs - (k + 1) - absorbed_df
         G = eng.wide_gram(D, ldD, 0, P, mode=1 if w is not None else 0)
-        XtX, Xty = inference.split_gram(G)
-        beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # polars_impl.py:212-226
-        Vb = XtX_inv[1:, 1:]
+        if mz:  # 2SLS from the Gram of [1, y~, x~, z~] (common.py:188-287)
+            iv = inference.IVSystem(G, k, mz, z_has_ones=False)
+            beta_full, Vb, to_meat = iv.beta_full, iv.XtX_inv, iv.xhat_meat
+            coef = np.concatenate([[-iv.coef[0], 1.0], -iv.coef[1:]])  # r = y~ - u coef, u = [1, x~, z~]
+            keep = [0] + list(range(2, P))  # u's columns in D (y~ dropped from the meats)
+            c0, km = 0, P
+        else:
+            XtX, Xty = inference.split_gram(G)
+            beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # polars_impl.py:212-226
+            Vb, to_meat = XtX_inv[1:, 1:], (lambda M: M)
+            coef = np.concatenate([[-beta_full[0], 1.0], -beta_full[1:]])
+            keep = None
+            c0, km = 2, k
+        sub = (lambda M: M) if keep is None else (lambda M: M[np.ix_(keep, keep)])
         r = eng.dev_alloc(ldD)
-        coef = np.concatenate([[-beta_full[0], 1.0], -beta_full[1:]])
         rss_w, rss, sum_y, sum_y2 = eng.wide_resid(D, ldD, coef, r)
         n_clusters = None
         if v == "iid":
             se = inference.se_iid(Vb, rss_w, df_resid)
         elif v == "hc1":
-            meat = eng.wide_gram(D, ldD, 2, k, mode=2 if w is not None else 3, r=r)
-            se = inference.se_hc1(Vb, meat, n_obs, df_resid)
+            meat = eng.wide_gram(D, ldD, c0, km, mode=2 if w is not None else 3, r=r)
+            se = inference.se_hc1(Vb, to_meat(sub(meat)), n_obs, df_resid)
         else:
             _load_clusters(eng, cols, cluster_cols, False)
             subsets = inference.cluster_subsets(len(cluster_cols))
-            meats, Gs = eng.wide_cluster_meats(D, ldD, 2, k, r, subsets)
+            meats, Gs = eng.wide_cluster_meats(D, ldD, c0, km, r, subsets)
+            meats = [to_meat(sub(M)) for M in meats]
             if len(cluster_cols) == 1:
                 se, n_clusters = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, ssc)
             else:
                 se, n_clusters = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets, n_obs,
                                                                df_resid, ssc)
+        if mz:  # the intercept's row of the IV covariance (polars_impl.py:238 slices it off)
+            se = se[1:]
         tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
         timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
     finally:
@@ -612,10 +632,11 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
             eng.close()
     return LeanFEResult(coefs=dict(zip(x_cols, (float(b_) for b_ in beta_full[1:]))),
                         std_errors=dict(zip(x_cols, (float(s_) for s_ in se))), n_obs=n_obs,
-                        iterations=iterations, vcov_type=vcov, is_iv=False, n_instruments=None,
+                        iterations=iterations, vcov_type=vcov, is_iv=bool(mz), n_instruments=mz or None,
                         n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
-                        fe_dims=fe_dims, r_squared=1 - rss / tss if tss > 0 else None, compression_ratio=None,
-                        rss=float(rss), tss=tss, backend="hip", timings=timings)
+                        fe_dims=fe_dims, r_squared=None if mz else (1 - rss / tss if tss > 0 else None),
+                        compression_ratio=None, rss=float(rss), tss=None if mz else tss, backend="hip",
+                        timings=timings)
 
 
 def _beta_agrees(beta_dev, beta_host, rtol: float = 1e-10) -> bool:

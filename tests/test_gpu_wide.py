@@ -131,3 +131,56 @@ def test_streamed_wide_event_study_from_parquet(tmp_path):
     assert list(r.coefs) == xs and len(xs) == 71
     o = altproj.fit(full, "y", xs, ["fe1", "fe2"], vcov="HC1")
     _check(r, o, xs)
+
+
+def _iv_panel(seed, n, L, k):
+    """k regressors (x1 endogenous), k instruments: z1 plus the exogenous x2..xk (2SLS,
+    common.py:188-287)."""
+    d = dict(synth.panel(n, k, list(L), seed=seed))
+    rng = np.random.default_rng(seed)
+    u = rng.normal(0, 1, n)
+    d["z1"] = rng.normal(0, 1, n) + 0.3 * d["x2"]
+    d["x1"] = d["x1"] + 0.8 * d["z1"] + 0.6 * u
+    d["y"] = d["y"] + 0.6 * d["x1"] + u
+    d["cl1"] = rng.integers(0, 97, n)
+    return d, ["z1"] + [f"x{j + 1}" for j in range(1, k)]
+
+
+@pytest.mark.parametrize("vcov,cl,weighted", [("HC1", None, False), ("cluster", ["cl1", "fe2"], True), ("iid", None, False)])
+def test_wide_iv_fit_matches_oracle(vcov, cl, weighted):
+    """IV beyond 63 columns: [y] + 40 regressors + 40 instruments = 81 columns in two blocks; 2SLS
+    from the device matrix's Gram, meats over u = [1, x~, z~] (std_errors.py:448-602)."""
+    from leanfe_amd import leanfe_hip
+    from oracle import altproj
+
+    k, L = 40, [2_000, 150]
+    d, inst = _iv_panel(44, 120_001, L, k)
+    kw = {}
+    if weighted:
+        d["w"] = np.random.default_rng(45).uniform(0.5, 2.0, d["y"].size)
+        kw["weights"] = "w"
+    xs = [f"x{j + 1}" for j in range(k)]
+    f = f"y ~ {' + '.join(xs)} | fe1 + fe2 | {' + '.join(inst)}"
+    r = leanfe_hip(d, formula=f, strategy="alt_proj", vcov=vcov, cluster_cols=cl, quiet=True, **kw)
+    assert r.is_iv and r.n_instruments == k
+    o = altproj.fit(d, "y", xs, ["fe1", "fe2"], vcov=vcov, cluster_cols=cl, weights=kw.get("weights"),
+                    instruments=inst)
+    _check(r, o, xs)
+
+
+@pytest.mark.parametrize("vcov", ["HC1", "cluster"])
+def test_wide_iv_blocks_equal_the_one_context_iv_fit(vcov, monkeypatch):
+    from leanfe_amd import hip_impl, leanfe_hip
+
+    k = 5
+    d, inst = _iv_panel(46, 250_000, [6_000, 200], k)
+    xs = [f"x{j + 1}" for j in range(k)]
+    f = f"y ~ {' + '.join(xs)} | fe1 + fe2 | {' + '.join(inst)}"
+    cl = ["cl1"] if vcov == "cluster" else None
+    one = leanfe_hip(d, formula=f, strategy="alt_proj", vcov=vcov, cluster_cols=cl, quiet=True)
+    monkeypatch.setattr(hip_impl, "MAX_CONTEXT_COLS", 5)  # 11 columns: three blocks
+    wide = leanfe_hip(d, formula=f, strategy="alt_proj", vcov=vcov, cluster_cols=cl, quiet=True)
+    assert wide.iterations == one.iterations and wide.n_obs == one.n_obs and wide.is_iv
+    np.testing.assert_allclose([wide.coefs[x] for x in xs], [one.coefs[x] for x in xs], rtol=1e-12, atol=0)
+    np.testing.assert_allclose([wide.std_errors[x] for x in xs], [one.std_errors[x] for x in xs], rtol=1e-12,
+                               atol=0)
