@@ -184,3 +184,21 @@ def test_wide_iv_blocks_equal_the_one_context_iv_fit(vcov, monkeypatch):
     np.testing.assert_allclose([wide.coefs[x] for x in xs], [one.coefs[x] for x in xs], rtol=1e-12, atol=0)
     np.testing.assert_allclose([wide.std_errors[x] for x in xs], [one.std_errors[x] for x in xs], rtol=1e-12,
                                atol=0)
+
+
+def test_streamed_wide_iv_fit():
+    """Out of core and wide with instruments: the streamed blocks carry [y] + x + z chunk by chunk
+    (hip_impl._stream_chunks), against the resident wide IV fit and the oracle."""
+    from leanfe_amd import leanfe_hip
+    from oracle import altproj
+
+    k, L = 35, [1_500, 100]
+    d, inst = _iv_panel(47, 90_001, L, k)
+    xs = [f"x{j + 1}" for j in range(k)]
+    f = f"y ~ {' + '.join(xs)} | fe1 + fe2 | {' + '.join(inst)}"
+    res = leanfe_hip(d, formula=f, strategy="alt_proj", vcov="HC1", quiet=True)
+    oc = leanfe_hip(d, formula=f, strategy="alt_proj", vcov="HC1", quiet=True, out_of_core=True, chunk_rows=40_000)
+    o = altproj.fit(d, "y", xs, ["fe1", "fe2"], vcov="HC1", instruments=inst)
+    _check(oc, o, xs)
+    np.testing.assert_allclose([oc.coefs[x] for x in xs], [res.coefs[x] for x in xs], rtol=1e-11, atol=0)
+    np.testing.assert_allclose([oc.std_errors[x] for x in xs], [res.std_errors[x] for x in xs], rtol=1e-11, atol=0)
