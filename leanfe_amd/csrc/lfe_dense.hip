@@ -1126,6 +1126,16 @@ __global__ __launch_bounds__(512, 4) void k_dn8_k2s_batch(Dn8Batch b) {
   dn8_k2s_body(b.a[j], b.np[j], (int)blockIdx.x - b.start[j]);
 }
 
+// K1's fewest output blocks per workgroup (LFE_DN8_K1_MIN: A/B)
+static int64_t dn8_k1_min_blocks() {
+  static const int64_t v = [] {
+    const char* e = getenv("LFE_DN8_K1_MIN");
+    const long long x = e ? atoll(e) : 4;
+    return (int64_t)(x >= 1 ? x : 4);
+  }();
+  return v;
+}
+
 // LFE_DN8_TIMING=1 (diagnostic): per-workgroup phase times of the last K1 / K2 launch to stderr
 static bool dn8_timing() {
   static const bool on = [] {
@@ -1415,7 +1425,11 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
       LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k1s), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
       const int64_t total = (int64_t)std::max(c->nbe, 1) * a.nrb;
-      const int grid = (int)std::min<int64_t>(c->n_cu, (total + 15) / 16);
+      // every CU a workgroup down to 4 output blocks each: an owner shard's few buckets (the 8-rank
+      // shard: 800 blocks) ran on 50 workgroups at 16 blocks each, its stream phase 11.5 us after a
+      // 12.7 us digit prologue that more workgroups do not lengthen (LFE_DN8_TIMING)
+      const int64_t per_wg = dn8_k1_min_blocks();
+      const int grid = (int)std::min<int64_t>(c->n_cu, (total + per_wg - 1) / per_wg);
       if (dn8_timing()) {
         if (!g_dn8_dbg) {
           LFE_HIP(hipMalloc(reinterpret_cast<void**>(&g_dn8_dbg), sizeof(unsigned long long) * 7 * 65536));
