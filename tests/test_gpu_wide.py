@@ -202,3 +202,24 @@ def test_streamed_wide_iv_fit():
     _check(oc, o, xs)
     np.testing.assert_allclose([oc.coefs[x] for x in xs], [res.coefs[x] for x in xs], rtol=1e-11, atol=0)
     np.testing.assert_allclose([oc.std_errors[x] for x in xs], [res.std_errors[x] for x in xs], rtol=1e-11, atol=0)
+
+
+def test_wide_fit_three_fes_with_singletons():
+    """Three FEs, rows alone in their level (dropped before the sweeps, polars_impl.py:477-482),
+    weights and a one-way cluster on the second FE, 70 regressors in two blocks."""
+    from leanfe_amd import leanfe_hip
+    from oracle import altproj
+
+    n, k, L = 100_003, 70, [2_500, 300, 40]
+    d = dict(synth.panel(n, k, L, seed=61))
+    f1 = np.array(d["fe1"], copy=True)
+    f1[:25] = L[0] + np.arange(25)  # 25 singleton levels
+    d["fe1"] = f1
+    d["w"] = np.random.default_rng(61).uniform(0.5, 2.0, n)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = ["fe1", "fe2", "fe3"]
+    r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="alt_proj", vcov="cluster", cluster_cols=["fe2"],
+                   weights="w", quiet=True)
+    o = altproj.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=["fe2"], weights="w")
+    assert r.n_obs == n - 25 and r.n_clusters == o["n_clusters"]
+    _check(r, o, xs)
