@@ -429,6 +429,12 @@ static void free_data(lfe_ctx* c) {
   c->cl.clear();
   c->cl_levels.clear();
   c->cl_fe.clear();
+  c->clfused = false;
+  dfree(c->clf_S);
+  dfree(c->clf_hi);
+  dfree(c->clf_cnt);
+  dfree(c->clf_fq);
+  c->clf_S_cap = c->clf_hi_cap = c->clf_cnt_cap = c->clf_fq_cap = 0;
   free_cluster_ws(c);
   dfree(c->rec_sy);
   dfree(c->rec_syy);

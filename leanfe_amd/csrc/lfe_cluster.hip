@@ -896,40 +896,44 @@ __global__ void k_clfused_quanta(const double* __restrict__ tile, const double* 
   }
 }
 
-bool cluster_fused_ok(const lfe_ctx* c) {
+// the cluster column whose one-way sums the residual pass can form (it repeats the primary FE),
+// or -1
+int cluster_fused_col(const lfe_ctx* c) {
   static const bool env_on = [] {  // "LFE_CL_FUSED=0": score rows and the separate sums (A/B)
     const char* e = getenv("LFE_CL_FUSED");
     const char* s = getenv("LFE_CL_STATS");
     return !(e && e[0] == '0') && !(s && s[0] == '1');
   }();
   const int k = c->p - 1;
-  return env_on && clfix_on() && !(c->test_hooks & (LFE_TEST_CLUSTER_SORTED | LFE_TEST_CLUSTER_STATS)) &&
-         c->world == 1 && c->cl.size() == 1 && c->cl_fe.size() == 1 && c->L.P >= 0 && c->cl_fe[0] == c->L.P &&
-         c->L.permuted && !c->w && !c->records && k >= 1 && k <= 63;
+  if (!(env_on && clfix_on() && !(c->test_hooks & (LFE_TEST_CLUSTER_SORTED | LFE_TEST_CLUSTER_STATS)) &&
+        c->world == 1 && c->L.P >= 0 && c->L.permuted && !c->w && !c->records && k >= 1 && k <= 63))
+    return -1;
+  for (int j = 0; j < (int)c->cl_fe.size() && j < (int)c->cl.size(); ++j)
+    if (c->cl_fe[j] == c->L.P) return j;
+  return -1;
 }
 
 int cluster_fused_prepare(lfe_ctx* c) {
   const int k = c->p - 1, G = c->fe[c->L.P].G;
-  auto& W = c->clw;
-  LFE_TRY(ensure_cluster_ws(c, (size_t)G * k, (size_t)G + 4));  // clS: coarse limbs; clP: counts, [G, max, flag]
-  LFE_TRY(ensure_f64(c, W.srec, W.srec_cap, (size_t)G * k));      // fine limbs
-  LFE_TRY(ensure_f64(c, W.fixq, W.fixq_cap, (size_t)kFqRows * kFqCols));
-  int32_t* cm = c->clP + G;
-  LFE_HIP(hipMemcpyAsync(c->clP, c->fe[c->L.P].cnt, sizeof(int32_t) * G, hipMemcpyDeviceToDevice, c->stream));
+  LFE_TRY(ensure_f64(c, c->clf_S, c->clf_S_cap, (size_t)G * k));      // fine limbs
+  LFE_TRY(ensure_f64(c, c->clf_hi, c->clf_hi_cap, (size_t)G * k));    // coarse limbs
+  LFE_TRY(ensure_i32(c, c->clf_cnt, c->clf_cnt_cap, (size_t)G + 4));  // counts, then [G, max, flag]
+  LFE_TRY(ensure_f64(c, c->clf_fq, c->clf_fq_cap, (size_t)kFqRows * kFqCols));
+  int32_t* cm = c->clf_cnt + G;
+  LFE_HIP(hipMemcpyAsync(c->clf_cnt, c->fe[c->L.P].cnt, sizeof(int32_t) * G, hipMemcpyDeviceToDevice, c->stream));
   LFE_HIP(hipMemsetAsync(cm, 0, sizeof(int32_t) * 4, c->stream));
-  hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, c->clP, G, cm);
+  hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, c->clf_cnt, G, cm);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
 }
 
 int cluster_fused_reset(lfe_ctx* c, const double* tile, const double* beta) {
   const int k = c->p - 1, G = c->fe[c->L.P].G;
-  auto& W = c->clw;
-  LFE_HIP(hipMemsetAsync(W.srec, 0, sizeof(double) * (size_t)G * k, c->stream));
-  LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)G * k, c->stream));
-  LFE_HIP(hipMemsetAsync(c->clP + G + 2, 0, sizeof(int32_t), c->stream));
+  LFE_HIP(hipMemsetAsync(c->clf_S, 0, sizeof(double) * (size_t)G * k, c->stream));
+  LFE_HIP(hipMemsetAsync(c->clf_hi, 0, sizeof(double) * (size_t)G * k, c->stream));
+  LFE_HIP(hipMemsetAsync(c->clf_cnt + G + 2, 0, sizeof(int32_t), c->stream));
   hipLaunchKernelGGL(k_clfused_quanta, dim3(1), dim3(64), 0, c->stream, tile, beta, c->p,
-                     std::max<int64_t>(c->n_kept, 1), c->clP + G + 1, W.fixq);
+                     std::max<int64_t>(c->n_kept, 1), c->clf_cnt + G + 1, c->clf_fq);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
 }
@@ -937,17 +941,26 @@ int cluster_fused_reset(lfe_ctx* c, const double* tile, const double* beta) {
 // the fused pass's sums -> meat (S'S) and cluster count; 1: its bound flag is up (redo from score rows)
 static int cluster_fused_finish(lfe_ctx* c, double* meat, int64_t* G_out, int* redo) {
   const int k = c->score_k, G = c->fe[c->L.P].G;
-  auto& W = c->clw;
+  *redo = 0;
+  if (c->clfused_done) {  // asked again after the same pass
+    std::copy(c->clfused_meat.begin(), c->clfused_meat.end(), meat);
+    *G_out = c->clfused_G;
+    return LFE_OK;
+  }
   int32_t hc[3] = {0, 0, 0};
-  LFE_TRY(d2h_sync(c, hc, c->clP + G, sizeof(hc)));
+  LFE_TRY(d2h_sync(c, hc, c->clf_cnt + G, sizeof(hc)));
   *redo = hc[2] != 0;
   if (*redo) return LFE_OK;
   {
     ProfScope _ps(c, K_CLUSTER_FIX);
-    LFE_TRY(launch_fix_convert(c, W.srec, c->clS, (int64_t)G * k, k, W.fixq));
+    LFE_TRY(launch_fix_convert(c, c->clf_S, c->clf_hi, (int64_t)G * k, k, c->clf_fq));
   }
   *G_out = hc[0];
-  return launch_table_gram(c, W.srec, G, k, meat);
+  LFE_TRY(launch_table_gram(c, c->clf_S, G, k, meat));
+  c->clfused_meat.assign(meat, meat + (size_t)k * k);
+  c->clfused_G = hc[0];
+  c->clfused_done = true;
+  return LFE_OK;
 }
 
 int launch_codes_differ(lfe_ctx* c, const int32_t* a, const int32_t* b, int64_t n, int32_t* flag) {
@@ -958,15 +971,18 @@ int launch_codes_differ(lfe_ctx* c, const int32_t* a, const int32_t* b, int64_t 
 
 // meat and cluster count of one subset (mask over the loaded cluster columns)
 static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
-  if (c->clfused) {  // the residual pass summed the one cluster column (the primary FE)
+  if (c->clfused) {  // the residual pass summed the cluster column that repeats the primary FE
     int redo = 0;
-    if (mask == 1) {
+    if (mask == 1 << c->clfused_j) {
       LFE_TRY(cluster_fused_finish(c, meat, G_out, &redo));
       if (!redo) return LFE_OK;
     }
-    // another subset, or a value past the fused quanta's bound: the pass again, writing score rows
-    double st[4];
-    LFE_TRY(launch_resid(c, c->clfused_beta.data(), st, nullptr, 1, 0));
+    // a subset the pass did not sum (from its score rows, if it wrote them), or a value past the
+    // fused quanta's bound: the pass again, writing score rows
+    if (redo || !c->clfused_scores) {
+      double st[4];
+      LFE_TRY(launch_resid(c, c->clfused_beta.data(), st, nullptr, 1, 0));
+    }
   }
   const int k = c->score_k;
   const int64_t n = c->n;

@@ -2079,8 +2079,9 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
   if (!(resid_rows_ok(c, a) && c->p <= 11)) return 1;
   const int p = c->p, k = p - 1;
   // a one-way cluster on the primary FE: its sums in this pass (no score rows written)
-  const bool cl = keep_scores && cluster_fused_ok(c) &&
-                  (size_t)a.B * (12 + k) * 8 + 5120 <= 160 * 1024;
+  const int clj = keep_scores ? cluster_fused_col(c) : -1;
+  const bool cl = clj >= 0 && (size_t)a.B * (12 + k) * 8 + 5120 <= 160 * 1024;
+  const bool cl_scores = cl && c->cl.size() > 1;  // the other subsets read score rows
   c->clfused = false;
   if (cl) LFE_TRY(cluster_fused_prepare(c));
   // dred: [0, 256) design tile | [256, 516) residual tile + stats | 516 ok | [520, 532) beta | 532 tables guard
@@ -2105,15 +2106,15 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
     ar.qf[0] = 1 - a.la.P;
     ar.G_Q = c->fe[ar.qf[0]].G;
     ar.beta = buf == c->dred ? c->dbeta : c->dspec + 520;
-    ar.scores = keep_scores && !cl ? c->scores : nullptr;
+    ar.scores = keep_scores && (!cl || cl_scores) ? c->scores : nullptr;
     if (cl) {  // quanta from this pass's Gram tile and beta (on the device), the sums zeroed
       LFE_TRY(cluster_fused_reset(c, buf, ar.beta));
       const int G = c->fe[c->L.P].G;
-      ar.clS = reinterpret_cast<unsigned long long*>(c->clw.srec);
-      ar.clHi = c->clS;
-      ar.clFq = c->clw.fixq;
-      ar.clCmax = c->clP + G + 1;
-      ar.clFlag = c->clP + G + 2;
+      ar.clS = reinterpret_cast<unsigned long long*>(c->clf_S);
+      ar.clHi = c->clf_hi;
+      ar.clFq = c->clf_fq;
+      ar.clCmax = c->clf_cnt + G + 1;
+      ar.clFlag = c->clf_cnt + G + 2;
     }
     LFE_TRY(resid_rows_enqueue(c, ar, buf + 256, cl));
     LFE_TRY(d2h_sync(c, h.data(), buf, sizeof(double) * 533));
@@ -2133,6 +2134,9 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
   c->score_meat = meat;  // the row kernel's meat is sum s s' (unweighted two-FE case)
   c->score_meat_ok = keep_scores && c->world == 1;
   c->clfused = cl;
+  c->clfused_done = false;
+  c->clfused_j = clj;
+  c->clfused_scores = cl_scores;
   if (cl) c->clfused_beta.assign(beta_full, beta_full + p);
   return LFE_OK;
 }

@@ -294,7 +294,19 @@ struct lfe_ctx {
   // the one cluster column is the primary FE: its sums came out of the residual pass (no score rows;
   // lfe_gram.hip k_resid_rows<.., true>, finished by lfe_cluster.hip)
   bool clfused = false;
+  int clfused_j = -1;            // that cluster column
+  bool clfused_scores = false;   // the pass wrote the score rows too (other subsets need them)
   std::vector<double> clfused_beta;  // beta_full of that pass (to redo it with score rows)
+  bool clfused_done = false;         // its meat formed (the sums are converted in place: kept here)
+  std::vector<double> clfused_meat;
+  int64_t clfused_G = 0;
+  // its sums (kept apart from the other subsets' work buffers): fine limbs, coarse limbs, counts
+  // with [G, max, flag] after them, quanta
+  double* clf_S = nullptr;
+  double* clf_hi = nullptr;
+  int32_t* clf_cnt = nullptr;
+  double* clf_fq = nullptr;
+  size_t clf_S_cap = 0, clf_hi_cap = 0, clf_cnt_cap = 0, clf_fq_cap = 0;
   lfe::ClusterWS clw;
   // pinned host staging (small transfers avoid the runtime's pageable path)
   char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
@@ -527,7 +539,7 @@ void free_stream_clusters(lfe_ctx* c);
 // records in c->clS (lfe_cluster.hip)
 int group_sorted(lfe_ctx* c, int64_t n, uint64_t drop, const uint64_t* K, const int32_t* R, const double* table,
                  int k, int32_t* G_out);  // weighted streamed fits: w's max / rms into fixq column p
-bool cluster_fused_ok(const lfe_ctx* c);                       // lfe_cluster.hip
+int cluster_fused_col(const lfe_ctx* c);                       // lfe_cluster.hip (-1: none)
 int cluster_fused_prepare(lfe_ctx* c);                         // buffers and counts, before the pass
 int cluster_fused_reset(lfe_ctx* c, const double* tile, const double* beta);  // zeroed sums + quanta
 int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1, int keep_scores, int icpt);
