@@ -2079,9 +2079,11 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
   if (!(resid_rows_ok(c, a) && c->p <= 11)) return 1;
   const int p = c->p, k = p - 1;
   // a one-way cluster on the primary FE: its sums in this pass (no score rows written)
-  const int clj = keep_scores ? cluster_fused_col(c) : -1;
+  // (one cluster column: with more, the other subsets need the score rows, and the pass that both
+  // writes them and sums was slower than the separate sums - HDFE_CLUSTER2 4.00-4.04 vs 3.98 ms)
+  const int clj = keep_scores && c->cl.size() == 1 ? cluster_fused_col(c) : -1;
   const bool cl = clj >= 0 && (size_t)a.B * (12 + k) * 8 + 5120 <= 160 * 1024;
-  const bool cl_scores = cl && c->cl.size() > 1;  // the other subsets read score rows
+  const bool cl_scores = false;
   c->clfused = false;
   if (cl) LFE_TRY(cluster_fused_prepare(c));
   // dred: [0, 256) design tile | [256, 516) residual tile + stats | 516 ok | [520, 532) beta | 532 tables guard

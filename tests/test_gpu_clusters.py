@@ -46,7 +46,7 @@ def _arr(r, xs, what):
 CASES = [
     ("fe_oneway", [20_000, 600], ["fe1"], None),
     ("fe_twoway", [20_000, 600], ["fe1", "fe2"], None),
-    ("fe_twoway_primary_second", [20_000, 600], ["fe2", "fe1"], None),  # the fused column is j = 1
+    ("fe_twoway_primary_second", [20_000, 600], ["fe2", "fe1"], None),  # the primary FE second
     ("other_oneway_weighted", [20_000, 600], ["grp"], "w"),
     ("fe3_cgm_outlier", [9_000, 800, 150], ["fe2", "fe3"], None),
 ]
