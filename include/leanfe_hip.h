@@ -334,6 +334,9 @@ int lfe_wide_cluster_meats(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, i
  * score rows instead of the residual pass's meat. */
 #define LFE_TEST_CLUSTER_SORTED 2
 #define LFE_TEST_CLUSTER_STATS 4
+/* LFE_TEST_SEG_SCATTER: the row sweeps' segment layouts are built by the block scatter
+ * (k_seg_scatter2) instead of the sorted build. */
+#define LFE_TEST_SEG_SCATTER 8
 int lfe_ctx_test_hooks(lfe_ctx* ctx, int flags);
 
 /* Wait for all work queued on the context's stream. */

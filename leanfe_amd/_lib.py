@@ -572,7 +572,8 @@ class Engine:
         """Test-only switches (lfe_ctx_test_hooks; 1 = LFE_TEST_SHORT_MEMORY: this rank's owner
         re-shard reports too little device memory; 2 = LFE_TEST_CLUSTER_SORTED: one-column cluster
         subsets take the sorted path; 4 = LFE_TEST_CLUSTER_STATS: the sort-free cluster sums take
-        their quanta from a statistics pass)."""
+        their quanta from a statistics pass; 8 = LFE_TEST_SEG_SCATTER: the row sweeps' segment
+        layouts are built by the block scatter instead of the sorted build)."""
         _check(self._lib.lfe_ctx_test_hooks(self._h, int(flags)))
 
     def dense_cells(self) -> int:

@@ -1309,7 +1309,7 @@ int lfe_exact_sums(lfe_ctx* c, int* on) {
 
 int lfe_ctx_test_hooks(lfe_ctx* c, int flags) {
   LFE_CTX(c);
-  if (flags & ~(LFE_TEST_SHORT_MEMORY | LFE_TEST_CLUSTER_SORTED | LFE_TEST_CLUSTER_STATS))
+  if (flags & ~(LFE_TEST_SHORT_MEMORY | LFE_TEST_CLUSTER_SORTED | LFE_TEST_CLUSTER_STATS | LFE_TEST_SEG_SCATTER))
     return fail(LFE_EINVAL, "unknown test hook");
   c->test_hooks = flags;
   return LFE_OK;

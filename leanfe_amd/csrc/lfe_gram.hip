@@ -160,6 +160,7 @@ __global__ __launch_bounds__(TH, (NT == 2 && GU == 1 && TH == 256 && FQ == 1) ? 
     GramArgs a, double* __restrict__ partial, int64_t pstride) {
   using Sh = GramShape<NT>;
   constexpr int NW = TH / 64;
+  constexpr bool PF = NT == 1 && !QL && FQ == 2;  // (the generic FQ 7 variant measured slower with it)
   __shared__ double red[Sh::LEN];
   __shared__ double stat_red[NW][4];
   extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
@@ -256,7 +257,20 @@ __global__ __launch_bounds__(TH, (NT == 2 && GU == 1 && TH == 256 && FQ == 1) ? 
         }
       }
     };
+    // PF: the X columns of a batch are loaded one iteration ahead too (the wave then waits on the
+    // L2 gathers only, not on an HBM round trip per batch)
+    d4 xn[GU][NT];
+    auto load_x = [&](int gb) {
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int gi = gb + u;
+        const int r = gi * 16 + kq * 4;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) xn[u][I] = gi < g1 ? ld4(xb[I] + r) : d4{0.0, 0.0, 0.0, 0.0};
+      }
+    };
     load_codes(g0 + wave * GU);
+    if (PF) load_x(g0 + wave * GU);
     for (int gb = g0 + wave * GU; gb < g1; gb += step) {
       d4 xv[GU][NT], wv[GU], yr[GU], s1[GU], s2[GU];
       bool valid[GU][4];
@@ -265,7 +279,7 @@ __global__ __launch_bounds__(TH, (NT == 2 && GU == 1 && TH == 256 && FQ == 1) ? 
         const int gi = gb + u;
         const int r = gi * 16 + kq * 4;
 #pragma unroll
-        for (int I = 0; I < NT; ++I) xv[u][I] = gi < g1 ? ld4(xb[I] + r) : d4{0.0, 0.0, 0.0, 0.0};
+        for (int I = 0; I < NT; ++I) xv[u][I] = PF ? xn[u][I] : gi < g1 ? ld4(xb[I] + r) : d4{0.0, 0.0, 0.0, 0.0};
         if (WT) wv[u] = gi < g1 ? ld4(a.w + r) : d4{0.0, 0.0, 0.0, 0.0};
         if (MODE == GRAM_RESID && WT && a.yoco) {  // record mean of y (raw column 0), _sum_y, _sum_y_sq
           yr[u] = gi < g1 ? ld4(a.X + r) : d4{0.0, 0.0, 0.0, 0.0};
@@ -305,6 +319,7 @@ __global__ __launch_bounds__(TH, (NT == 2 && GU == 1 && TH == 256 && FQ == 1) ? 
 #pragma unroll
         for (int s = 0; s < 4; ++s) hv[u][s] = hq[u][s];
       load_codes(gb + step);  // next batch
+      if (PF) load_x(gb + step);
       if (P >= 0) {
         // separate LDS / global paths: a generic pointer over both address
         // spaces trips a gfx950 codegen error (flat address-space check)
@@ -797,12 +812,23 @@ constexpr int kGramGU = 2;
 constexpr int kGramThreadsQL = 1024;  // alpha_Q in LDS: one 110 KB workgroup per CU, 16 waves
 
 template <int MODE, int NT>
-static const void* gram_kernel(bool general, bool weighted, bool ql) {
+static const void* gram_kernel(bool general, bool weighted, bool ql, bool nq2 = false) {
   if (MODE == GRAM_TABLE) return reinterpret_cast<const void*>(&k_gram_table<NT>);
   constexpr int M = MODE == GRAM_TABLE ? GRAM_DESIGN : MODE;
-  if (general)
+  if (general) {
+    // three FEs at p <= 16: two 16-row groups per wave iteration with X loaded a batch ahead
+    // (config 4: residual 3.76 -> 3.47 ms, design 2.39 -> 2.29 ms; round 5).  LFE_GRAM_GEN=0: the
+    // generic variant (A/B)
+    static const int gen = [] {
+      const char* e = getenv("LFE_GRAM_GEN");
+      return e ? atoi(e) : 2;
+    }();
+    if (gen == 2 && nq2 && NT == 1)
+      return weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, 2, 2, true, false, kGramThreads>)
+                      : reinterpret_cast<const void*>(&k_gram<M, NT, 2, 2, false, false, kGramThreads>);
     return weighted ? reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, true, false, kGramThreads>)
                     : reinterpret_cast<const void*>(&k_gram<M, NT, kMaxFE - 1, 1, false, false, kGramThreads>);
+  }
   if (ql && NT == 1) {
     // 16 waves per CU need <= 128 VGPRs: GU 2
     return weighted ? reinterpret_cast<const void*>(&k_gram<M, 1, 1, 2, true, true, kGramThreadsQL>)
@@ -847,7 +873,7 @@ static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
       dyn += qbytes;
       threads = kGramThreadsQL;
     }
-    fn = gram_kernel<MODE, NT>(a.nq > 1, a.w != nullptr, ql);
+    fn = gram_kernel<MODE, NT>(a.nq > 1, a.w != nullptr, ql, a.nq == 2);
     if (dyn > 64 * 1024)  // dynamic LDS above 64 KB must be opted in
       LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
     nblocks = row_blocks(c, resident_blocks(c, fn, threads, dyn));

@@ -565,6 +565,7 @@ int records_layout(lfe_ctx* c);   // rec_sy / rec_syy in layout order -> rec_lay
 int bit_length(uint64_t v);
 int ensure_sort_ws(lfe_ctx* c, size_t n);
 int radix_sort(lfe_ctx* c, int64_t n, int bits, int* out_buf);
+int radix_pass(lfe_ctx* c, int64_t n, int shift, int cur, int kid);
 // --- clusters (lfe_cluster.hip) ---
 int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, double* meats, int64_t* G_out);
 // per-row cluster ids (input row order) of subset `mask` over the loaded cluster columns; rows with

@@ -167,27 +167,34 @@ int ensure_sort_ws(lfe_ctx* c, size_t n) {
   return LFE_OK;
 }
 
+// one stable pass of the workspace's (keys, rows) [0, n) from buffer cur to 1 - cur by the 8-bit
+// digit at `shift`
+int radix_pass(lfe_ctx* c, int64_t n, int shift, int cur, int kid) {
+  auto& W = c->clw;
+  if (n <= 0) return LFE_OK;
+  const int nblk = (int)((n + kRsItems - 1) / kRsItems);
+  LFE_TRY(ensure_i32(c, W.counts, W.counts_cap, (size_t)kRsBins * std::max(nblk, 1)));
+  {
+    ProfScope _ps(c, kid);
+    hipLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], n, shift, nblk, W.counts);
+  }
+  LFE_HIP(hipGetLastError());
+  LFE_TRY(exclusive_scan(c, W.counts, (int64_t)kRsBins * nblk));
+  {
+    ProfScope _ps(c, kid);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], W.rows[cur],
+                       W.keys[1 - cur], W.rows[1 - cur], n, shift, nblk, W.counts);
+  }
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
 // sort (keys, rows) [0, n) of the workspace by the low `bits` bits; *out_buf = the
 // buffer (0/1) holding the result
 int radix_sort(lfe_ctx* c, int64_t n, int bits, int* out_buf) {
-  auto& W = c->clw;
-  const int nblk = (int)((n + kRsItems - 1) / kRsItems);
-  LFE_TRY(ensure_i32(c, W.counts, W.counts_cap, (size_t)kRsBins * std::max(nblk, 1)));
   int cur = 0;
   for (int shift = 0; shift < bits && n > 0; shift += kRsBits) {
-    {
-      ProfScope _ps(c, K_CLUSTER_SORT);
-      hipLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], n, shift, nblk,
-                         W.counts);
-    }
-    LFE_HIP(hipGetLastError());
-    LFE_TRY(exclusive_scan(c, W.counts, (int64_t)kRsBins * nblk));
-    {
-      ProfScope _ps(c, K_CLUSTER_SORT);
-      hipLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(kRsThreads), 0, c->stream, W.keys[cur], W.rows[cur],
-                         W.keys[1 - cur], W.rows[1 - cur], n, shift, nblk, W.counts);
-    }
-    LFE_HIP(hipGetLastError());
+    LFE_TRY(radix_pass(c, n, shift, cur, K_CLUSTER_SORT));
     cur = 1 - cur;
   }
   *out_buf = cur;

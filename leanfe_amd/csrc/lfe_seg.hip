@@ -174,6 +174,142 @@ __global__ __launch_bounds__(kSegBlkThreads) void k_seg_scatter2(SegScatter2Args
   }
 }
 
+// Sorted build (unweighted, two or three FEs), one FE f at a time: k_seg_keys writes every row's
+// key (g_f in the low word - bit 31 marks a dropped row - and the first other FE's code in the high
+// word) and the second other FE's code as the row slot; stable radix passes order them by the bits
+// of g_f above the lowest `shift` (coarse buckets of at most 2^9 codes; none for the primary FE, whose
+// layout order already is by buckets of 2^s codes); k_seg_rank then sorts each block of 8192 rows by
+// code in LDS, reserves each code's slots with one returning global add and stores the block's rows
+// code run by code run.  (k_seg_scatter2 instead takes a returning global add per row for an FE too
+// wide for its LDS bins - config 4's 1e5-level FE - and stores runs of a few rows per code.
+// Measured on config 4: the layouts' build 6.46 ms, of which the 1e5-level FE 3.0 ms, the 1e4-level
+// FE 2.0 ms, the primary 1.7 ms; round 5.)
+__global__ void k_seg_keys(const int32_t* __restrict__ keep, const int32_t* __restrict__ code,
+                           const int32_t* __restrict__ oa, const int32_t* __restrict__ ob, int64_t n,
+                           uint64_t* __restrict__ keys, int32_t* __restrict__ rows) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = keep[i] >= 0 ? (uint32_t)code[i] : 0x80000000u;
+    keys[i] = ((uint64_t)(uint32_t)oa[i] << 32) | g;
+    rows[i] = ob ? ob[i] : 0;
+  }
+}
+
+constexpr int kRankThreads = 1024;
+constexpr int kRankPer = 8;
+constexpr int kRankRows = kRankThreads * kRankPer;  // rows per block
+constexpr int kRankBins = 4096;                     // code range of a block ranked in LDS
+
+struct SegRankArgs {
+  const uint64_t* keys;  // ordered by the coarse bucket of g_f
+  const int32_t* rows;
+  int64_t n, ld;
+  int32_t* cur;  // FE f's cursors (from seg_off)
+  int32_t* oc;   // FE f's other codes [no][ld]
+  int no;
+};
+
+__global__ __launch_bounds__(kRankThreads) void k_seg_rank(SegRankArgs a) {
+  __shared__ int32_t st[kRankBins];  // counts, then the codes' starts in the block's sorted rows
+  __shared__ int32_t gb[kRankBins];  // the codes' first global slots
+  __shared__ int2 stage[kRankRows];  // the block's other codes, sorted by g_f
+  __shared__ int32_t wsum[kRankThreads / 64];
+  __shared__ int32_t smin, smax;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * kRankRows;
+  if (tid == 0) {
+    smin = 0x7fffffff;
+    smax = -1;
+  }
+  uint64_t key[kRankPer];
+  int32_t ob[kRankPer];
+  int32_t mn = 0x7fffffff, mx = -1;
+#pragma unroll
+  for (int s = 0; s < kRankPer; ++s) {
+    const int64_t i = r0 + s * kRankThreads + tid;
+    key[s] = i < a.n ? a.keys[i] : 0x80000000ull;
+    ob[s] = i < a.n ? a.rows[i] : 0;
+    const uint32_t g = (uint32_t)key[s];
+    if (!(g & 0x80000000u)) {
+      mn = min(mn, (int32_t)g);
+      mx = max(mx, (int32_t)g);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = min(mn, __shfl_xor(mn, off, 64));
+    mx = max(mx, __shfl_xor(mx, off, 64));
+  }
+  __syncthreads();
+  if (lane == 0) {
+    atomicMin(&smin, mn);
+    atomicMax(&smax, mx);
+  }
+  __syncthreads();
+  const int32_t lo = smin, w = smax >= smin ? smax - smin + 1 : 0;
+  if (w > kRankBins) {  // block-uniform: codes too spread for the LDS bins - one global add per row
+#pragma unroll
+    for (int s = 0; s < kRankPer; ++s) {
+      const uint32_t g = (uint32_t)key[s];
+      if (g & 0x80000000u) continue;
+      const int64_t pos = atomicAdd(&a.cur[g], 1);
+      a.oc[pos] = (int32_t)(key[s] >> 32);
+      if (a.no > 1) a.oc[a.ld + pos] = ob[s];
+    }
+    return;
+  }
+  for (int j = tid; j < w; j += kRankThreads) st[j] = 0;
+  __syncthreads();
+  int rk[kRankPer];
+#pragma unroll
+  for (int s = 0; s < kRankPer; ++s) {
+    const uint32_t g = (uint32_t)key[s];
+    rk[s] = (g & 0x80000000u) ? -1 : atomicAdd(&st[(int32_t)g - lo], 1);
+  }
+  __syncthreads();
+  // each code's slots (one returning global add), then the exclusive scan of the counts: thread t
+  // takes codes 4t .. 4t + 3
+  int v[4], sum = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = 4 * tid + q;
+    v[q] = j < w ? st[j] : 0;
+    if (v[q] > 0) gb[j] = atomicAdd(&a.cur[lo + j], v[q]);
+    sum += v[q];
+  }
+  int x = sum;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int before = 0;
+  for (int w2 = 0; w2 < wave; ++w2) before += wsum[w2];
+  int run = before + x - sum;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = 4 * tid + q;
+    if (j < w) st[j] = run;
+    run += v[q];
+  }
+  int kept = 0;
+  for (int w2 = 0; w2 < kRankThreads / 64; ++w2) kept += wsum[w2];
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < kRankPer; ++s)
+    if (rk[s] >= 0) stage[st[(int32_t)(uint32_t)key[s] - lo] + rk[s]] = int2{(int32_t)(key[s] >> 32), ob[s]};
+  __syncthreads();
+  // consecutive threads store consecutive rows of a code's run
+  for (int q = tid; q < kept; q += kRankThreads) {
+    int j = 0;  // the last code whose start is <= q (empty codes share the next one's start)
+    for (int step = kRankBins / 2; step > 0; step >>= 1)
+      if (j + step < w && st[j + step] <= q) j += step;
+    const int64_t pos = (int64_t)gb[j] + (q - st[j]);
+    const int2 e = stage[q];
+    a.oc[pos] = e.x;
+    if (a.no > 1) a.oc[a.ld + pos] = e.y;
+  }
+}
+
 // ufirst[u] = the segment holding row u * kSegUnit
 __global__ void k_seg_units(const int32_t* __restrict__ seg_off, int32_t G, int32_t* __restrict__ ufirst) {
   for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
@@ -726,9 +862,59 @@ int seg_build(lfe_ctx* c) {
     a.oc[f] = fe.oc;
     a.ws[f] = weighted ? fe.ws : nullptr;
   }
+  static const int sorted_env = [] {  // "0": k_seg_scatter2 for every fit (A/B)
+    const char* e = getenv("LFE_SEG_SORTED");
+    return e ? atoi(e) : 1;
+  }();
+  // the sorted build: unweighted, two or three FEs, its workspace (24 bytes a row) at most 6 GB
+  const bool sorted = sorted_env != 0 && !(c->test_hooks & LFE_TEST_SEG_SCATTER) && !weighted && (c->F == 2 || c->F == 3) && n > 0 &&
+                      c->ld <= (int64_t)1 << 28 && getenv("LFE_SEG_SCATTER_ROWS") == nullptr;
+  if (sorted) {
+    LFE_TRY(ensure_sort_ws(c, (size_t)c->ld));
+    auto& W = c->clw;
+    for (int f = 0; f < c->F; ++f) {
+      const int32_t* other[2] = {nullptr, nullptr};
+      int j = 0;
+      for (int f2 = 0; f2 < c->F; ++f2)
+        if (f2 != f) other[j++] = L.code[f2];
+      {
+        ProfScope _ps(c, K_SEG_BUILD);
+        hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a.keep, L.code[f],
+                           other[0], other[1], n, W.keys[0], W.rows[0]);
+      }
+      LFE_HIP(hipGetLastError());
+      // coarse buckets of at most 2^9 codes: the primary FE's layout buckets (2^s codes), else the
+      // radix passes over the code's bits above the lowest `shift` (8 bits a pass)
+      int cur = 0;
+      if (!(f == L.P && L.permuted && L.s <= 9)) {
+        const int bits = bit_length((uint64_t)std::max(c->fe[f].G - 1, 0));
+        const int passes = bits > 9 ? (bits - 9 + 7) / 8 : 0;
+        for (int q = 0; q < passes; ++q) {
+          LFE_TRY(radix_pass(c, n, bits - 8 * (passes - q), cur, K_SEG_BUILD));
+          cur = 1 - cur;
+        }
+      }
+      SegRankArgs r{};
+      r.keys = W.keys[cur];
+      r.rows = W.rows[cur];
+      r.n = n;
+      r.ld = c->ld;
+      r.cur = c->fe[f].seg_cur;
+      r.oc = c->fe[f].oc;
+      r.no = c->F - 1;
+      {
+        ProfScope _ps(c, K_SEG_BUILD);
+        hipLaunchKernelGGL(k_seg_rank, dim3((unsigned)((n + kRankRows - 1) / kRankRows)), dim3(kRankThreads), 0,
+                           c->stream, r);
+      }
+      LFE_HIP(hipGetLastError());
+    }
+  }
   {
     ProfScope _ps(c, K_SEG_BUILD);
-    if (n > 0 && getenv("LFE_SEG_SCATTER_ROWS") == nullptr) {  // (env: the per-row kernel, A/B only)
+    if (sorted) {
+      // (built above)
+    } else if (n > 0 && getenv("LFE_SEG_SCATTER_ROWS") == nullptr) {  // (env: the per-row kernel, A/B only)
       SegScatter2Args a2{};
       a2.s = a;
       for (int f = 0; f < c->F; ++f) a2.G[f] = c->fe[f].G;

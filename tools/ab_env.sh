@@ -1,20 +1,25 @@
 #!/bin/bash
-# Same-box A/B of an environment knob on bench lines:  tools/ab_env.sh VAR "v1 v2 ..." "bench args" [rounds]
-# prints ms/step and the per-kernel ms of the dense / sweep passes for every (round, value)
+# A/B of env variants on one box: AB_CASES="label:bench args|..." (e.g. "c4:--config 4|m1:--preset
+# mega_cluster1"), AB_VARS="label:NAME=VALUE ...|..." (the first variant is usually "base:"), two
+# repetitions; prints ms per step and the named kernel groups (AB_KERNELS, space separated)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-var=$1; vals=$2; args=$3; rounds=${4:-2}
-mkdir -p gpurun_out
-for r in $(seq 1 $rounds); do
-  for v in $vals; do
-    env $var=$v timeout -k 10 300 python bench.py --no-cpu --no-h2d $args > gpurun_out/ab_env.log 2>&1 || { tail -5 gpurun_out/ab_env.log; exit 1; }
-    tail -1 gpurun_out/ab_env.log > gpurun_out/ab_env.json
-    python - "$var=$v $args" <<'PY'
-import json, sys
-d = json.load(open("gpurun_out/ab_env.json"))
-k = d["kernels_ms"]
-top = sorted(k.items(), key=lambda kv: -kv[1][0])[:7]
-print(sys.argv[1], d["ms_per_step"], "it", d["config"]["iterations"], " ".join(f"{n}:{v[0]:.3f}" for n, v in top), flush=True)
-PY
+mkdir -p gpurun_out/ab
+: > gpurun_out/ab/lines.txt
+IFS='|' read -r -a cases <<< "${AB_CASES}"
+IFS='|' read -r -a vars <<< "${AB_VARS}"
+for rep in 1 2; do
+  for cs in "${cases[@]}"; do
+    cl=${cs%%:*}; args=${cs#*:}
+    for vs in "${vars[@]}"; do
+      vl=${vs%%:*}; ev=${vs#*:}
+      f=gpurun_out/ab/${cl}_${vl}_$rep
+      env $ev timeout -k 10 300 python bench.py --no-cpu --no-h2d --steps ${AB_STEPS:-10} --warmup 3 $args > $f.json 2> $f.err \
+        || { tail -3 $f.err; exit 1; }
+      python -c "
+import json,sys
+d=json.loads(open('$f.json').read().strip().splitlines()[-1]);k=d.get('kernels_ms',{})
+print('$cl', '$vl', d['ms_per_step'], {n:k[n][0] for n in '${AB_KERNELS:-}'.split() if n in k})" | tee -a gpurun_out/ab/lines.txt
+    done
   done
 done
