@@ -421,6 +421,7 @@ static void free_data(lfe_ctx* c) {
     dfree(fe.seg_off);
     dfree(fe.seg_cur);
     dfree(fe.oc);
+    dfree(fe.perm);
     dfree(fe.ws);
     dfree(fe.ufirst);
   }

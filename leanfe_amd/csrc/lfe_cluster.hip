@@ -861,6 +861,54 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
   return rc;
 }
 
+// meat and cluster count of the one-column subset whose column repeats FE f, by the FE's segment
+// layout (the general sweeps' sorted build orders the kept rows by the code and keeps the row
+// permutation): two-limb sums of the score rows per segment (seg_score_sums), quanta from a
+// statistics pass over the score rows - no keys, no radix sort, no segment heads (config 4's 1e5-
+// and 1e4-level columns; one process)
+static int subset_meat_seg(lfe_ctx* c, int f, double* meat, int64_t* G_out) {
+  const int k = c->score_k;
+  const int64_t n = c->n;
+  const int32_t G = c->fe[f].G;
+  auto& W = c->clw;
+  const int32_t* keep = c->L.P >= 0 ? c->L.code[c->L.P] : nullptr;
+  const int nch = (int)std::max<int64_t>(1, (n + kClFixChunk - 1) / kClFixChunk);
+  const size_t m = (size_t)G * k;
+  LFE_TRY(ensure_f64(c, W.fixq, W.fixq_cap, (size_t)kFqRows * kFqCols));
+  LFE_TRY(ensure_cluster_ws(c, m, 4));            // clS: coarse limbs; clP: [nonzero, max]
+  LFE_TRY(ensure_f64(c, W.srec, W.srec_cap, m));  // fine limbs -> S
+  int32_t* cm = c->clP;
+  double* S = W.srec;
+  // the score rows' statistics: once per launch_cluster_subsets call (its subsets share the rows)
+  const bool stats = !W.segst_ok;
+  if (stats) {
+    LFE_TRY(ensure_f64(c, W.segst, W.segst_cap, (size_t)kColStatHead + (size_t)k * nch));
+    LFE_HIP(hipMemsetAsync(W.segst, 0, sizeof(double) * kColStatHead, c->stream));
+    W.segst_ok = true;
+  }
+  LFE_HIP(hipMemsetAsync(cm, 0, sizeof(int32_t) * 4, c->stream));
+  LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * m, c->stream));
+  LFE_HIP(hipMemsetAsync(S, 0, sizeof(double) * m, c->stream));
+  {
+    ProfScope _ps(c, K_CLUSTER_FIX);
+    hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, c->fe[f].cnt, G, cm);
+    if (stats && n > 0)
+      hipLaunchKernelGGL(k_clfix_stats, dim3(nch), dim3(256), 0, c->stream, keep, keep, n, c->scores, k, nch, nullptr,
+                         W.segst);
+    LFE_HIP(hipGetLastError());
+    LFE_TRY(launch_fix_quanta(c, W.segst, nch, std::max<int64_t>(c->n_kept_local, 1), cm + 1, 1, W.fixq, k));
+  }
+  LFE_TRY(seg_score_sums(c, f, c->scores, k, W.fixq, S, c->clS, K_CLUSTER_FIX));
+  {
+    ProfScope _ps(c, K_CLUSTER_FIX);
+    LFE_TRY(launch_fix_convert(c, S, c->clS, (int64_t)m, k, W.fixq));
+  }
+  int32_t hc[2] = {0, 0};
+  LFE_TRY(d2h_sync(c, hc, cm, sizeof(hc)));
+  *G_out = hc[0];
+  return launch_table_gram(c, S, G, k, meat);
+}
+
 // ---------------------------------------------------------------------------
 // One-way cluster on the primary FE, summed in the residual pass (lfe_gram.hip k_resid_rows<.., true>)
 // ---------------------------------------------------------------------------
@@ -1013,6 +1061,10 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
         return subset_meat_fix(c, j, win, bucketed, meat, G_out,
                                stats_env || (c->test_hooks & LFE_TEST_CLUSTER_STATS) != 0);
     }
+    // a column that repeats an FE of the general sweeps: that FE's segment layout
+    const int f = j < (int)c->cl_fe.size() ? c->cl_fe[j] : -1;
+    if (c->world == 1 && f >= 0 && f < c->F && c->seg_ready && c->fe[f].perm_ok && c->fe[f].G == G)
+      return subset_meat_seg(c, f, meat, G_out);
   }
   KeyArgs ka{};
   uint64_t span = 1;
@@ -1111,6 +1163,7 @@ int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, doub
     }
     W.lay_valid = true;
   }
+  W.segst_ok = false;  // (subset_meat_seg: the score rows' statistics, formed by the first subset)
   for (int s = 0; s < n_subsets; ++s)
     LFE_TRY(subset_meat(c, masks[s], meats + (size_t)s * k * k, G_out + s));
   return LFE_OK;
@@ -1120,7 +1173,9 @@ void free_cluster_ws(lfe_ctx* c) {
   auto& W = c->clw;
   dfree_any(W.fixst);
   dfree_any(W.fixq);
-  W.fixst_cap = W.fixq_cap = 0;
+  dfree_any(W.segst);
+  W.fixst_cap = W.fixq_cap = W.segst_cap = 0;
+  W.segst_ok = false;
   for (int b = 0; b < 2; ++b) {
     dfree_any(W.keys[b]);
     dfree_any(W.rows[b]);

@@ -81,6 +81,9 @@ struct FeState {
   size_t seg_cur_cap = 0;
   int32_t* oc = nullptr;       // [F - 1][ld] the other FEs' codes, segment order
   size_t oc_cap = 0;
+  int32_t* perm = nullptr;     // [ld] the layout row of every segment position (sorted build)
+  size_t perm_cap = 0;
+  bool perm_ok = false;        // perm holds the current segment order
   double* ws = nullptr;        // [ld] weights, segment order (weighted fits)
   size_t ws_cap = 0;
   int32_t* ufirst = nullptr;   // [units] segment holding each work unit's first row
@@ -115,6 +118,9 @@ struct ClusterWS {
   size_t fixst_cap = 0;
   double* fixq = nullptr;       // [kFqRows][kFqCols]
   size_t fixq_cap = 0;
+  double* segst = nullptr;      // subsets on an FE's segments: the score rows' statistics (fixst form)
+  size_t segst_cap = 0;
+  bool segst_ok = false;        // segst holds this launch_cluster_subsets call's statistics
   uint64_t* keys[2] = {nullptr, nullptr};  // radix sort ping-pong
   size_t keys_cap[2] = {0, 0};
   int32_t* rows[2] = {nullptr, nullptr};
@@ -577,6 +583,9 @@ int owner_meat(lfe_ctx* c, const uint64_t* K, const int32_t* seg_off, const doub
                uint64_t span, double* meat, int64_t* G_out);
 void free_cluster_ws(lfe_ctx* c);
 // --- segmented gather-sums (lfe_seg.hip) ---
+// cluster score sums over FE f's segments (the sorted build's permutation), two-limb (lfe_seg.hip)
+int seg_score_sums(lfe_ctx* c, int f, const double* table, int cols, const double* xq, double* S, double* Shi,
+                   int kid);
 int seg_gather_sum(lfe_ctx* c, const int32_t* seg_off, int32_t G, int32_t* ufirst, int64_t n_pos,
                    const int32_t* rows, const double* table, int stride, int cols, double* out, int kid);
 int seg_units_needed(int64_t n_pos);

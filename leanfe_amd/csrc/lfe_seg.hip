@@ -184,13 +184,26 @@ __global__ __launch_bounds__(kSegBlkThreads) void k_seg_scatter2(SegScatter2Args
 // wide for its LDS bins - config 4's 1e5-level FE - and stores runs of a few rows per code.
 // Measured on config 4: the layouts' build 6.46 ms, of which the 1e5-level FE 3.0 ms, the 1e4-level
 // FE 2.0 ms, the primary 1.7 ms; round 5.)
-__global__ void k_seg_keys(const int32_t* __restrict__ keep, const int32_t* __restrict__ code,
-                           const int32_t* __restrict__ oa, const int32_t* __restrict__ ob, int64_t n,
-                           uint64_t* __restrict__ keys, int32_t* __restrict__ rows) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t g = keep[i] >= 0 ? (uint32_t)code[i] : 0x80000000u;
-    keys[i] = ((uint64_t)(uint32_t)oa[i] << 32) | g;
-    rows[i] = ob ? ob[i] : 0;
+// key = g_f | a << bf | b << (bf + ba) (a, b: the other FEs' codes, bit 63: a dropped row), row
+// slot = the layout row (the segment order's row permutation, for the cluster sums)
+struct SegKeyArgs {
+  const int32_t* keep;
+  const int32_t* code;
+  const int32_t* oa;
+  const int32_t* ob;  // null: two FEs
+  int64_t n;
+  int bf, ba;
+  uint64_t* keys;
+  int32_t* rows;
+};
+__global__ void k_seg_keys(SegKeyArgs a) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t k = (uint64_t)(uint32_t)a.code[i] & ((1ull << a.bf) - 1);
+    k |= (uint64_t)(uint32_t)a.oa[i] << a.bf;
+    if (a.ob) k |= (uint64_t)(uint32_t)a.ob[i] << (a.bf + a.ba);
+    if (a.keep[i] < 0) k |= 1ull << 63;
+    a.keys[i] = k;
+    a.rows[i] = (int32_t)i;
   }
 }
 
@@ -203,35 +216,38 @@ struct SegRankArgs {
   const uint64_t* keys;  // ordered by the coarse bucket of g_f
   const int32_t* rows;
   int64_t n, ld;
-  int32_t* cur;  // FE f's cursors (from seg_off)
-  int32_t* oc;   // FE f's other codes [no][ld]
+  int bf, ba, bb;
+  int32_t* cur;   // FE f's cursors (from seg_off)
+  int32_t* oc;    // FE f's other codes [no][ld]
+  int32_t* perm;  // FE f's layout row of every position
   int no;
 };
 
 __global__ __launch_bounds__(kRankThreads) void k_seg_rank(SegRankArgs a) {
   __shared__ int32_t st[kRankBins];  // counts, then the codes' starts in the block's sorted rows
   __shared__ int32_t gb[kRankBins];  // the codes' first global slots
-  __shared__ int2 stage[kRankRows];  // the block's other codes, sorted by g_f
+  __shared__ int3 stage[kRankRows];  // the block's (other codes, layout row), sorted by g_f
   __shared__ int32_t wsum[kRankThreads / 64];
   __shared__ int32_t smin, smax;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * kRankRows;
+  const uint64_t mf = (1ull << a.bf) - 1, ma = (1ull << a.ba) - 1, mb = (1ull << a.bb) - 1;
   if (tid == 0) {
     smin = 0x7fffffff;
     smax = -1;
   }
   uint64_t key[kRankPer];
-  int32_t ob[kRankPer];
+  int32_t row[kRankPer];
   int32_t mn = 0x7fffffff, mx = -1;
 #pragma unroll
   for (int s = 0; s < kRankPer; ++s) {
     const int64_t i = r0 + s * kRankThreads + tid;
-    key[s] = i < a.n ? a.keys[i] : 0x80000000ull;
-    ob[s] = i < a.n ? a.rows[i] : 0;
-    const uint32_t g = (uint32_t)key[s];
-    if (!(g & 0x80000000u)) {
-      mn = min(mn, (int32_t)g);
-      mx = max(mx, (int32_t)g);
+    key[s] = i < a.n ? a.keys[i] : 1ull << 63;
+    row[s] = i < a.n ? a.rows[i] : 0;
+    if (!(key[s] >> 63)) {
+      const int32_t g = (int32_t)(key[s] & mf);
+      mn = min(mn, g);
+      mx = max(mx, g);
     }
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -245,25 +261,22 @@ __global__ __launch_bounds__(kRankThreads) void k_seg_rank(SegRankArgs a) {
   }
   __syncthreads();
   const int32_t lo = smin, w = smax >= smin ? smax - smin + 1 : 0;
+  auto put = [&](int64_t pos, uint64_t k, int32_t r) {
+    a.oc[pos] = (int32_t)((k >> a.bf) & ma);
+    if (a.no > 1) a.oc[a.ld + pos] = (int32_t)((k >> (a.bf + a.ba)) & mb);
+    a.perm[pos] = r;
+  };
   if (w > kRankBins) {  // block-uniform: codes too spread for the LDS bins - one global add per row
 #pragma unroll
-    for (int s = 0; s < kRankPer; ++s) {
-      const uint32_t g = (uint32_t)key[s];
-      if (g & 0x80000000u) continue;
-      const int64_t pos = atomicAdd(&a.cur[g], 1);
-      a.oc[pos] = (int32_t)(key[s] >> 32);
-      if (a.no > 1) a.oc[a.ld + pos] = ob[s];
-    }
+    for (int s = 0; s < kRankPer; ++s)
+      if (!(key[s] >> 63)) put(atomicAdd(&a.cur[(int32_t)(key[s] & mf)], 1), key[s], row[s]);
     return;
   }
   for (int j = tid; j < w; j += kRankThreads) st[j] = 0;
   __syncthreads();
   int rk[kRankPer];
 #pragma unroll
-  for (int s = 0; s < kRankPer; ++s) {
-    const uint32_t g = (uint32_t)key[s];
-    rk[s] = (g & 0x80000000u) ? -1 : atomicAdd(&st[(int32_t)g - lo], 1);
-  }
+  for (int s = 0; s < kRankPer; ++s) rk[s] = (key[s] >> 63) ? -1 : atomicAdd(&st[(int32_t)(key[s] & mf) - lo], 1);
   __syncthreads();
   // each code's slots (one returning global add), then the exclusive scan of the counts: thread t
   // takes codes 4t .. 4t + 3
@@ -296,7 +309,11 @@ __global__ __launch_bounds__(kRankThreads) void k_seg_rank(SegRankArgs a) {
   __syncthreads();
 #pragma unroll
   for (int s = 0; s < kRankPer; ++s)
-    if (rk[s] >= 0) stage[st[(int32_t)(uint32_t)key[s] - lo] + rk[s]] = int2{(int32_t)(key[s] >> 32), ob[s]};
+    if (rk[s] >= 0) {
+      const uint64_t k = key[s];
+      stage[st[(int32_t)(k & mf) - lo] + rk[s]] =
+          int3{(int32_t)((k >> a.bf) & ma), (int32_t)((k >> (a.bf + a.ba)) & mb), row[s]};
+    }
   __syncthreads();
   // consecutive threads store consecutive rows of a code's run
   for (int q = tid; q < kept; q += kRankThreads) {
@@ -304,9 +321,10 @@ __global__ __launch_bounds__(kRankThreads) void k_seg_rank(SegRankArgs a) {
     for (int step = kRankBins / 2; step > 0; step >>= 1)
       if (j + step < w && st[j + step] <= q) j += step;
     const int64_t pos = (int64_t)gb[j] + (q - st[j]);
-    const int2 e = stage[q];
+    const int3 e = stage[q];
     a.oc[pos] = e.x;
     if (a.no > 1) a.oc[a.ld + pos] = e.y;
+    a.perm[pos] = e.z;
   }
 }
 
@@ -867,30 +885,49 @@ int seg_build(lfe_ctx* c) {
     return e ? atoi(e) : 1;
   }();
   // the sorted build: unweighted, two or three FEs, its workspace (24 bytes a row) at most 6 GB
-  const bool sorted = sorted_env != 0 && !(c->test_hooks & LFE_TEST_SEG_SCATTER) && !weighted && (c->F == 2 || c->F == 3) && n > 0 &&
+  const bool sorted0 = sorted_env != 0 && !(c->test_hooks & LFE_TEST_SEG_SCATTER) && !weighted && (c->F == 2 || c->F == 3) && n > 0 &&
                       c->ld <= (int64_t)1 << 28 && getenv("LFE_SEG_SCATTER_ROWS") == nullptr;
+  int bits[kMaxFE] = {}, bsum = 0;  // code bits of every FE (at least 1): the packed keys need <= 63
+  for (int f = 0; f < c->F; ++f) {
+    bits[f] = std::max(1, bit_length((uint64_t)std::max(c->fe[f].G - 1, 0)));
+    bsum += bits[f];
+  }
+  const bool sorted = sorted0 && bsum <= 63;
+  for (auto& fe : c->fe) fe.perm_ok = false;
   if (sorted) {
     LFE_TRY(ensure_sort_ws(c, (size_t)c->ld));
+    for (auto& fe : c->fe) LFE_TRY(ensure_i32(c, fe.perm, fe.perm_cap, (size_t)c->ld));
     auto& W = c->clw;
     for (int f = 0; f < c->F; ++f) {
       const int32_t* other[2] = {nullptr, nullptr};
-      int j = 0;
+      int of[2] = {0, 0}, j = 0;
       for (int f2 = 0; f2 < c->F; ++f2)
-        if (f2 != f) other[j++] = L.code[f2];
+        if (f2 != f) {
+          of[j] = f2;
+          other[j++] = L.code[f2];
+        }
+      SegKeyArgs ka{};
+      ka.keep = a.keep;
+      ka.code = L.code[f];
+      ka.oa = other[0];
+      ka.ob = other[1];
+      ka.n = n;
+      ka.bf = bits[f];
+      ka.ba = bits[of[0]];
+      ka.keys = W.keys[0];
+      ka.rows = W.rows[0];
       {
         ProfScope _ps(c, K_SEG_BUILD);
-        hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a.keep, L.code[f],
-                           other[0], other[1], n, W.keys[0], W.rows[0]);
+        hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka);
       }
       LFE_HIP(hipGetLastError());
       // coarse buckets of at most 2^9 codes: the primary FE's layout buckets (2^s codes), else the
       // radix passes over the code's bits above the lowest `shift` (8 bits a pass)
       int cur = 0;
       if (!(f == L.P && L.permuted && L.s <= 9)) {
-        const int bits = bit_length((uint64_t)std::max(c->fe[f].G - 1, 0));
-        const int passes = bits > 9 ? (bits - 9 + 7) / 8 : 0;
+        const int passes = bits[f] > 9 ? (bits[f] - 9 + 7) / 8 : 0;
         for (int q = 0; q < passes; ++q) {
-          LFE_TRY(radix_pass(c, n, bits - 8 * (passes - q), cur, K_SEG_BUILD));
+          LFE_TRY(radix_pass(c, n, bits[f] - 8 * (passes - q), cur, K_SEG_BUILD));
           cur = 1 - cur;
         }
       }
@@ -899,8 +936,12 @@ int seg_build(lfe_ctx* c) {
       r.rows = W.rows[cur];
       r.n = n;
       r.ld = c->ld;
+      r.bf = bits[f];
+      r.ba = bits[of[0]];
+      r.bb = c->F > 2 ? bits[of[1]] : 0;
       r.cur = c->fe[f].seg_cur;
       r.oc = c->fe[f].oc;
+      r.perm = c->fe[f].perm;
       r.no = c->F - 1;
       {
         ProfScope _ps(c, K_SEG_BUILD);
@@ -908,6 +949,7 @@ int seg_build(lfe_ctx* c) {
                            c->stream, r);
       }
       LFE_HIP(hipGetLastError());
+      c->fe[f].perm_ok = true;
     }
   }
   {
@@ -1049,6 +1091,40 @@ int seg_gather_sum(lfe_ctx* c, const int32_t* seg_off, int32_t G, int32_t* ufirs
   }
   LFE_HIP(hipGetLastError());
   return launch_seg_chain(c, seg_off, ufirst, G, n_units, cols, out);
+}
+
+// Cluster score sums of a column that repeats FE f (lfe_cluster.hip): S[g][0, cols) = the sum over
+// f's segment g of table[perm[q]][0, cols) (row stride cols), two-limb with quanta xq - fine limbs
+// as int64 bits in S, coarse limbs in Shi, both zeroed by the caller - so exact whatever the order
+// of a segment's rows (the sorted build ranks them by LDS atomics).  Needs the sorted build's perm.
+int seg_score_sums(lfe_ctx* c, int f, const double* table, int cols, const double* xq, double* S, double* Shi,
+                   int kid) {
+  auto& fe = c->fe[f];
+  if (!c->seg_ready || !fe.perm_ok || cols < 1 || cols > 64) {
+    set_error("seg_score_sums: no segment permutation for this FE");
+    return LFE_ESTATE;
+  }
+  SegCrossArgs a{};
+  a.seg_off = fe.seg_off;
+  a.ufirst = fe.ufirst;
+  a.n_units = n_units_of(c);
+  a.oc[0] = fe.perm;
+  a.alpha[0] = table;
+  a.p = cols;
+  a.pc = cols;
+  a.G = fe.G;
+  a.T = S;
+  a.xq = xq;
+  a.Thi = Shi;
+  if (a.n_units > 0 && fe.G > 0) {
+    CrossFn fn = cross_fn((cols + 15) / 16, 1, false);
+    const int waves_per_block = kSegThreads / 64;
+    ProfScope _ps(c, kid);
+    hipLaunchKernelGGL(fn, dim3((a.n_units + waves_per_block - 1) / waves_per_block), dim3(kSegThreads), 0, c->stream,
+                       a);
+  }
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
 }
 
 int seg_units_needed(int64_t n_pos) { return (int)std::max<int64_t>((n_pos + kSegUnit - 1) / kSegUnit, 1); }
