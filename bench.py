@@ -259,7 +259,7 @@ def load_shard(eng, a, rank: int, world: int, shard: str) -> dict:
 # ---------------------------------------------------------------------------
 
 def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cells: int = 0,
-                      cell_bytes: int = 2) -> dict:
+                      cell_bytes: int = 2, levels: list | None = None) -> dict:
     """HBM bytes each kernel must move per launch, n rows of the shard,
     p = 1 + k f64 data columns, F int32 code columns.  Kernels absent here move only group
     tables or scalars (latency-bound) and count as 0 in the step total.  The general sweeps'
@@ -268,8 +268,18 @@ def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cel
     two-FE cross terms (``dense_cells`` > 0, lfe_dense.hip) the table build reads both codes and
     writes two count tables of ``cell_bytes`` per cell (1: the exact i8 form, 2: u16), and each
     cross-term pass reads one of them; with three or more FEs on pair tables (lfe_dense3.hip) the
-    projections read the tables instead of gathering rows."""
+    projections read the tables instead of gathering rows.  With ``levels`` (unweighted, two or
+    three FEs on the general sweeps) the segment layouts come from the sorted build (lfe_seg.hip):
+    per FE a key pass, radix passes over the code bits above 9 (none for the primary) and a rank
+    pass, so its bytes per launch are that build's total over its launches."""
     k = p - 1
+    seg = n * (4 * F + 4 * F * (F - 1))  # codes -> every FE's other codes, segment order (block scatter)
+    if levels and F in (2, 3) and not dense_cells:
+        prim = max(range(F), key=lambda f: levels[f])
+        passes = sum(0 if f == prim else max(0, -(-(max(1, (levels[f] - 1).bit_length()) - 9) // 8))
+                     for f in range(F))
+        total = n * (F * (4 * (F + 1) + 12) + 32 * passes + F * (12 + 4 * (F - 1) + 4))
+        seg = total / (2 * F + 2 * passes + 1)
     cb = cell_bytes
     dense = {"layout_scatter": 8 * n + 2 * cb * dense_cells, "tp": cb * dense_cells, "tq": cb * dense_cells,
              "layout_base": 0} if dense_cells else {}
@@ -292,7 +302,7 @@ def algorithmic_bytes(n: int, p: int, F: int, clustered: bool = False, dense_cel
         "tq": 2 * n,                                 # run_h: the cross term of the secondary FE
         "gram_design": n * (8 * p + 4 * F),          # X + codes
         "gram_resid": n * (8 * p + 4 * F + (8 * k if clustered else 0)),  # X + codes (+ score rows)
-        "seg_build": n * (4 * F + 4 * F * (F - 1)),  # codes -> every FE's other codes, segment order
+        "seg_build": seg,
         "cross": 4 * n * (F - 1),                    # the other FEs' codes in segment order
         "check": 4 * n * (F - 1),
         **({"count": 4 * n} if F != 2 else {}),      # one FE's codes (two FEs: the layouts' histograms)
@@ -456,7 +466,8 @@ def main(argv=None):
     p, F = a.k + 1, len(a.levels)
     cells = eng.dense_cells()
     cbytes = eng.dense_cell_bytes() if cells else 0
-    ab = algorithmic_bytes(geo["local"], p, F, clustered=bool(a.cl), dense_cells=cells, cell_bytes=cbytes or 2)
+    ab = algorithmic_bytes(geo["local"], p, F, clustered=bool(a.cl), dense_cells=cells, cell_bytes=cbytes or 2,
+                           levels=list(a.levels))
     # dominant kernel = most device time in the timed region (rank 0's shard)
     dom = max(kstats.items(), key=lambda kv: kv[1][0]) if kstats else ("none", (0.0, 1))
     dom_name, (dom_ms, dom_launches) = dom

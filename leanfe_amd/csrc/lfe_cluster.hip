@@ -890,17 +890,14 @@ static int subset_meat_seg(lfe_ctx* c, int f, double* meat, int64_t* G_out) {
   LFE_HIP(hipMemsetAsync(c->clS, 0, sizeof(double) * m, c->stream));
   LFE_HIP(hipMemsetAsync(S, 0, sizeof(double) * m, c->stream));
   {
-    ProfScope _ps(c, K_CLUSTER_FIX);
+    ProfScope _ps(c, K_CLUSTER_FIX);  // one scope: statistics (first subset), sums, conversion
     hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, c->fe[f].cnt, G, cm);
     if (stats && n > 0)
       hipLaunchKernelGGL(k_clfix_stats, dim3(nch), dim3(256), 0, c->stream, keep, keep, n, c->scores, k, nch, nullptr,
                          W.segst);
     LFE_HIP(hipGetLastError());
     LFE_TRY(launch_fix_quanta(c, W.segst, nch, std::max<int64_t>(c->n_kept_local, 1), cm + 1, 1, W.fixq, k));
-  }
-  LFE_TRY(seg_score_sums(c, f, c->scores, k, W.fixq, S, c->clS, K_CLUSTER_FIX));
-  {
-    ProfScope _ps(c, K_CLUSTER_FIX);
+    LFE_TRY(seg_score_sums(c, f, c->scores, k, W.fixq, S, c->clS, -1));
     LFE_TRY(launch_fix_convert(c, S, c->clS, (int64_t)m, k, W.fixq));
   }
   int32_t hc[2] = {0, 0};

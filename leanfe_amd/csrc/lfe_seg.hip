@@ -1097,6 +1097,7 @@ int seg_gather_sum(lfe_ctx* c, const int32_t* seg_off, int32_t G, int32_t* ufirs
 // f's segment g of table[perm[q]][0, cols) (row stride cols), two-limb with quanta xq - fine limbs
 // as int64 bits in S, coarse limbs in Shi, both zeroed by the caller - so exact whatever the order
 // of a segment's rows (the sorted build ranks them by LDS atomics).  Needs the sorted build's perm.
+// kid < 0: no timing scope of its own (the caller's is open)
 int seg_score_sums(lfe_ctx* c, int f, const double* table, int cols, const double* xq, double* S, double* Shi,
                    int kid) {
   auto& fe = c->fe[f];
@@ -1119,9 +1120,14 @@ int seg_score_sums(lfe_ctx* c, int f, const double* table, int cols, const doubl
   if (a.n_units > 0 && fe.G > 0) {
     CrossFn fn = cross_fn((cols + 15) / 16, 1, false);
     const int waves_per_block = kSegThreads / 64;
-    ProfScope _ps(c, kid);
-    hipLaunchKernelGGL(fn, dim3((a.n_units + waves_per_block - 1) / waves_per_block), dim3(kSegThreads), 0, c->stream,
-                       a);
+    if (kid >= 0) {
+      ProfScope _ps(c, kid);
+      hipLaunchKernelGGL(fn, dim3((a.n_units + waves_per_block - 1) / waves_per_block), dim3(kSegThreads), 0, c->stream,
+                         a);
+    } else {  // (inside the caller's scope)
+      hipLaunchKernelGGL(fn, dim3((a.n_units + waves_per_block - 1) / waves_per_block), dim3(kSegThreads), 0, c->stream,
+                         a);
+    }
   }
   LFE_HIP(hipGetLastError());
   return LFE_OK;
