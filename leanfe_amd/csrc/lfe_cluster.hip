@@ -50,12 +50,19 @@ struct KeyArgs {
   uint64_t drop;                // key of dropped rows (= span)
   uint64_t* keys;
   int32_t* rows;
+  // pj >= 0: column pj repeats the layout's primary FE (rows in order of its buckets of 2^ps codes):
+  // its code g enters as (g mod 2^ps) mult[pj] + (g >> ps) << pshift, so the sort needs only the
+  // bits below pshift (equal low parts keep the bucket order: equal keys stay contiguous)
+  int pj, ps, pshift;
 };
 
 __global__ void k_cl_keys(KeyArgs a) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t key = 0;
-    for (int j = 0; j < a.m; ++j) key += (uint64_t)(uint32_t)a.code[j][i] * a.mult[j];
+    for (int j = 0; j < a.m; ++j) {
+      const uint64_t g = (uint32_t)a.code[j][i];
+      key += j == a.pj ? (g & ((1ull << a.ps) - 1)) * a.mult[j] + ((g >> a.ps) << a.pshift) : g * a.mult[j];
+    }
     a.keys[i] = (a.keep && a.keep[i] < 0) ? a.drop : key;
     a.rows[i] = (int32_t)i;
   }
@@ -1080,13 +1087,60 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   ka.drop = span;
   ka.keys = W.keys[0];
   ka.rows = W.rows[0];
+  ka.pj = -1;
+  int sort_bits = bit_length(span);
+  // one process, a column that repeats the primary FE: the layout's bucket order already sorts the
+  // key's top part (HDFE_CLUSTER2, MEGA_CLUSTER2: 4 -> 3 radix passes).  Dropped rows take the low
+  // part past every kept row's, so they end the sorted order as one run.
+  if (c->world == 1 && c->L.permuted && c->L.P >= 0 && ka.m >= 2 && !(c->test_hooks & LFE_TEST_CLUSTER_SORTED)) {
+    int jp = -1, kj = 0;
+    for (int j = 0; j < (int)c->cl.size(); ++j) {
+      if (!(mask >> j & 1)) continue;
+      if (jp < 0 && j < (int)c->cl_fe.size() && c->cl_fe[j] == c->L.P && c->cl_levels[j] == c->fe[c->L.P].G) jp = kj;
+      ++kj;
+    }
+    if (jp >= 0) {
+      uint64_t other = 1;  // product of the other columns' levels
+      kj = 0;
+      for (int j = 0; j < (int)c->cl.size(); ++j) {
+        if (!(mask >> j & 1)) continue;
+        if (kj != jp) other *= (uint64_t)c->cl_levels[j];
+        ++kj;
+      }
+      const int s = c->L.s;
+      const uint64_t lmax = (other << s);  // low parts < lmax; dropped rows: exactly lmax
+      const int lbits = bit_length(lmax);
+      const uint64_t nb = (uint64_t)c->L.nb;
+      if ((lbits + 7) / 8 < (sort_bits + 7) / 8 && lbits + bit_length(nb) <= 62) {
+        // mixed radix of the other columns as before (their multipliers skip the primary's), the
+        // primary's low bits above them
+        uint64_t mul = 1;
+        kj = 0;
+        for (int j = 0; j < (int)c->cl.size(); ++j) {
+          if (!(mask >> j & 1)) continue;
+          if (kj != jp) {
+            ka.mult[kj] = mul;
+            mul *= (uint64_t)c->cl_levels[j];
+          }
+          ++kj;
+        }
+        ka.mult[jp] = other;
+        ka.pj = jp;
+        ka.ps = s;
+        ka.pshift = lbits;
+        ka.drop = lmax;
+        sort_bits = lbits;
+      }
+    }
+  }
+  const uint64_t drop = ka.drop;
   if (n > 0) hipLaunchKernelGGL(k_cl_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka);
   LFE_HIP(hipGetLastError());
 
   int buf = 0;
-  if (n > 0) LFE_TRY(radix_sort(c, n, bit_length(span), &buf));
+  if (n > 0) LFE_TRY(radix_sort(c, n, sort_bits, &buf));
   int32_t G = 0, nv = 0;
-  LFE_TRY(group_segments(c, n, span, W.keys[buf], &G, &nv));
+  LFE_TRY(group_segments(c, n, drop, W.keys[buf], &G, &nv));
   // one process, unweighted, mostly singletons (mean cluster size below 2): D + the multi-row
   // clusters' corrections, without gathering every row
   if (c->world == 1 && k > 0 && c->score_meat_ok && (int)c->score_meat.size() == k * k && G > 0 &&
@@ -1094,7 +1148,7 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
     *G_out = G;
     return singleton_meat(c, W.rows[buf], G, k, meat);
   }
-  if (k > 0) LFE_TRY(group_sums(c, n, span, W.keys[buf], W.rows[buf], c->scores, k, G, nv));
+  if (k > 0) LFE_TRY(group_sums(c, n, drop, W.keys[buf], W.rows[buf], c->scores, k, G, nv));
 
   // multi-rank, few clusters: a key-indexed table, all-reduced (smaller than the exchange)
   const char* own_env = getenv("LFE_CL_OWNER_MIN_SPAN");  // tests: force the owner-partitioned form
