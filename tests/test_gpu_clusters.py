@@ -179,3 +179,35 @@ def test_one_way_cluster_on_the_primary_fe_in_the_residual_pass(k, L, singletons
     np.testing.assert_allclose(_arr(fused, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
     np.testing.assert_allclose(_arr(st, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
     np.testing.assert_array_equal(_arr(fused, xs, "std_errors"), _arr(again, xs, "std_errors"))
+
+
+INTERSECTIONS = [
+    # (levels, cluster columns): the primary FE (most levels) first, second, and in a three-way subset;
+    # 120K rows on 40K primary levels leave many singletons (dropped rows inside the buckets)
+    ([40_000, 700], ["fe1", "fe2"]),
+    ([40_000, 700], ["fe2", "fe1"]),
+    ([40_000, 700, 90], ["fe3", "fe1", "fe2"]),
+]
+
+
+@pytest.mark.parametrize("L,cl", INTERSECTIONS, ids=["primary_first", "primary_second", "three_way"])
+def test_intersections_on_the_primary_fe_sort_below_its_buckets(L, cl):
+    """An intersection subset with a column that repeats the layout's primary FE sorts only the key
+    bits below that FE's buckets (the layout's bucket order sorts the rest; dropped rows end the
+    order as one run): equal to the full sort (the LFE_TEST_CLUSTER_SORTED hook) at 1e-12 with equal
+    cluster counts, to the oracle at 1e-10, and bit for bit on a repeat."""
+    from oracle import altproj
+
+    n, k = 120_000, 3
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(L))]
+    d = dict(synth.panel(n, k, L, seed=57))
+    r = _fit(d, xs, fes, cl)
+    again = _fit(d, xs, fes, cl)
+    srt = _fit(d, xs, fes, cl, hooks=SORTED)
+    o = altproj.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=cl)
+    assert r.n_obs == o["n_obs"] < n  # singletons dropped
+    assert tuple(r.n_clusters) == tuple(srt.n_clusters) == tuple(o["n_clusters"])
+    np.testing.assert_allclose(_arr(r, xs, "std_errors"), o["se"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(_arr(r, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
+    np.testing.assert_array_equal(_arr(r, xs, "std_errors"), _arr(again, xs, "std_errors"))
