@@ -68,21 +68,6 @@ __global__ void k_cl_keys(KeyArgs a) {
   }
 }
 
-// keys in FE a's segment order (the general sweeps' sorted build): g_a (the segment, found by a
-// binary search of seg_off; empty segments share the next one's start) above the other column's
-// code b, row slot = the layout row
-__global__ void k_cl_seg_keys(const int32_t* __restrict__ seg_off, int32_t G, int top, const int32_t* __restrict__ ocb,
-                              const int32_t* __restrict__ perm, int bits_b, int64_t npos, uint64_t* __restrict__ keys,
-                              int32_t* __restrict__ rows) {
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npos; q += (int64_t)gridDim.x * blockDim.x) {
-    int g = 0;
-    for (int step = top; step > 0; step >>= 1)
-      if (g + step < G && seg_off[g + step] <= q) g += step;
-    keys[q] = ((uint64_t)g << bits_b) | (uint32_t)ocb[q];
-    rows[q] = perm[q];
-  }
-}
-
 __device__ __forceinline__ bool cl_head(const uint64_t* K, int64_t i, uint64_t drop) {
   return K[i] != drop && (i == 0 || K[i] != K[i - 1]);
 }
@@ -1104,47 +1089,10 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   ka.rows = W.rows[0];
   ka.pj = -1;
   int sort_bits = bit_length(span);
-  int64_t n_sort = n;  // positions sorted
-  bool seg_keys = false;
-  // two columns that repeat two FEs of the general sweeps: the keys in the segment order of the one
-  // with more levels (already sorted by its code), so the sort needs only the other column's bits
-  // and no dropped rows enter it (config 4's fe2 x fe3: 31 -> 14 bits)
-  if (c->world == 1 && ka.m == 2 && c->seg_ready && !(c->test_hooks & LFE_TEST_CLUSTER_SORTED)) {
-    int js[2], kk = 0;
-    for (int j = 0; j < (int)c->cl.size() && kk < 2; ++j)
-      if (mask >> j & 1) js[kk++] = j;
-    auto fe_of = [&](int j) {
-      const int f = j < (int)c->cl_fe.size() ? c->cl_fe[j] : -1;
-      return (f >= 0 && f < c->F && c->fe[f].G == c->cl_levels[j]) ? f : -1;
-    };
-    int fa = fe_of(js[0]), fb = fe_of(js[1]);
-    if (fa >= 0 && fb >= 0 && fa != fb) {
-      if (c->fe[fa].G < c->fe[fb].G) std::swap(fa, fb);
-      const int bits_b = std::max(1, bit_length((uint64_t)c->fe[fb].G - 1));
-      const int bits_a = bit_length((uint64_t)c->fe[fa].G);
-      if (c->fe[fa].perm_ok && (bits_b + 7) / 8 < (sort_bits + 7) / 8 && bits_a + bits_b <= 62) {
-        int jb = 0;  // fb's slot among fa's other codes
-        for (int f2 = 0; f2 < fb; ++f2)
-          if (f2 != fa) ++jb;
-        n_sort = c->n_kept_local;
-        int top = 1;
-        while (2 * top <= c->fe[fa].G) top *= 2;
-        if (n_sort > 0)
-          hipLaunchKernelGGL(k_cl_seg_keys, dim3(grid_for(n_sort, kBlock, 8192)), dim3(kBlock), 0, c->stream,
-                             c->fe[fa].seg_off, c->fe[fa].G, top, c->fe[fa].oc + (size_t)jb * c->ld, c->fe[fa].perm,
-                             bits_b, n_sort, W.keys[0], W.rows[0]);
-        LFE_HIP(hipGetLastError());
-        ka.drop = (uint64_t)c->fe[fa].G << bits_b;  // no key takes it (no dropped rows here)
-        sort_bits = bits_b;
-        seg_keys = true;
-      }
-    }
-  }
   // one process, a column that repeats the primary FE: the layout's bucket order already sorts the
   // key's top part (HDFE_CLUSTER2, MEGA_CLUSTER2: 4 -> 3 radix passes).  Dropped rows take the low
   // part past every kept row's, so they end the sorted order as one run.
-  if (!seg_keys && c->world == 1 && c->L.permuted && c->L.P >= 0 && ka.m >= 2 &&
-      !(c->test_hooks & LFE_TEST_CLUSTER_SORTED)) {
+  if (c->world == 1 && c->L.permuted && c->L.P >= 0 && ka.m >= 2 && !(c->test_hooks & LFE_TEST_CLUSTER_SORTED)) {
     int jp = -1, kj = 0;
     for (int j = 0; j < (int)c->cl.size(); ++j) {
       if (!(mask >> j & 1)) continue;
@@ -1186,13 +1134,13 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
     }
   }
   const uint64_t drop = ka.drop;
-  if (n > 0 && !seg_keys) hipLaunchKernelGGL(k_cl_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka);
+  if (n > 0) hipLaunchKernelGGL(k_cl_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, ka);
   LFE_HIP(hipGetLastError());
 
   int buf = 0;
-  if (n_sort > 0) LFE_TRY(radix_sort(c, n_sort, sort_bits, &buf));
+  if (n > 0) LFE_TRY(radix_sort(c, n, sort_bits, &buf));
   int32_t G = 0, nv = 0;
-  LFE_TRY(group_segments(c, n_sort, drop, W.keys[buf], &G, &nv));
+  LFE_TRY(group_segments(c, n, drop, W.keys[buf], &G, &nv));
   // one process, unweighted, mostly singletons (mean cluster size below 2): D + the multi-row
   // clusters' corrections, without gathering every row
   if (c->world == 1 && k > 0 && c->score_meat_ok && (int)c->score_meat.size() == k * k && G > 0 &&
@@ -1200,7 +1148,7 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
     *G_out = G;
     return singleton_meat(c, W.rows[buf], G, k, meat);
   }
-  if (k > 0) LFE_TRY(group_sums(c, n_sort, drop, W.keys[buf], W.rows[buf], c->scores, k, G, nv));
+  if (k > 0) LFE_TRY(group_sums(c, n, drop, W.keys[buf], W.rows[buf], c->scores, k, G, nv));
 
   // multi-rank, few clusters: a key-indexed table, all-reduced (smaller than the exchange)
   const char* own_env = getenv("LFE_CL_OWNER_MIN_SPAN");  // tests: force the owner-partitioned form
