@@ -1109,7 +1109,9 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
       }
       const int s = c->L.s;
       const uint64_t lmax = (other << s);  // low parts < lmax; dropped rows: exactly lmax
-      const int lbits = bit_length(lmax);
+      // whole 8-bit digits: the sort's last digit must not reach into the bucket part (else a kept
+      // row's low bucket bits would order it after the dropped rows)
+      const int lbits = (bit_length(lmax) + 7) / 8 * 8;
       const uint64_t nb = (uint64_t)c->L.nb;
       if ((lbits + 7) / 8 < (sort_bits + 7) / 8 && lbits + bit_length(nb) <= 62) {
         // mixed radix of the other columns as before (their multipliers skip the primary's), the

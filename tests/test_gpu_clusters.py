@@ -182,16 +182,19 @@ def test_one_way_cluster_on_the_primary_fe_in_the_residual_pass(k, L, singletons
 
 
 INTERSECTIONS = [
-    # (levels, cluster columns): the primary FE (most levels) first, second, and in a three-way subset;
-    # 120K rows on 40K primary levels leave many singletons (dropped rows inside the buckets)
-    ([40_000, 700], ["fe1", "fe2"]),
-    ([40_000, 700], ["fe2", "fe1"]),
-    ([40_000, 700, 90], ["fe3", "fe1", "fe2"]),
+    # (levels, cluster columns, weighted): the primary FE (most levels) first, second, and in a
+    # three-way subset; 120K rows on 40K primary levels leave many singletons (dropped rows inside
+    # the buckets); weighted fits sum every subset's clusters from the sorted rows (no singleton form)
+    ([40_000, 700], ["fe1", "fe2"], False),
+    ([40_000, 700], ["fe2", "fe1"], False),
+    ([40_000, 700, 90], ["fe3", "fe1", "fe2"], False),
+    ([40_000, 700, 90], ["fe3", "fe1", "fe2"], True),
 ]
 
 
-@pytest.mark.parametrize("L,cl", INTERSECTIONS, ids=["primary_first", "primary_second", "three_way"])
-def test_intersections_on_the_primary_fe_sort_below_its_buckets(L, cl):
+@pytest.mark.parametrize("L,cl,weighted", INTERSECTIONS,
+                         ids=["primary_first", "primary_second", "three_way", "three_way_weighted"])
+def test_intersections_on_the_primary_fe_sort_below_its_buckets(L, cl, weighted):
     """An intersection subset with a column that repeats the layout's primary FE sorts only the key
     bits below that FE's buckets (the layout's bucket order sorts the rest; dropped rows end the
     order as one run): equal to the full sort (the LFE_TEST_CLUSTER_SORTED hook) at 1e-12 with equal
@@ -202,10 +205,14 @@ def test_intersections_on_the_primary_fe_sort_below_its_buckets(L, cl):
     xs = [f"x{j + 1}" for j in range(k)]
     fes = [f"fe{f + 1}" for f in range(len(L))]
     d = dict(synth.panel(n, k, L, seed=57))
-    r = _fit(d, xs, fes, cl)
-    again = _fit(d, xs, fes, cl)
-    srt = _fit(d, xs, fes, cl, hooks=SORTED)
-    o = altproj.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=cl)
+    kw = {}
+    if weighted:
+        d["w"] = np.random.default_rng(5).uniform(0.5, 2.0, n)
+        kw = dict(weights="w")
+    r = _fit(d, xs, fes, cl, **kw)
+    again = _fit(d, xs, fes, cl, **kw)
+    srt = _fit(d, xs, fes, cl, hooks=SORTED, **kw)
+    o = altproj.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=cl, weights=kw.get("weights"))
     assert r.n_obs == o["n_obs"] < n  # singletons dropped
     assert tuple(r.n_clusters) == tuple(srt.n_clusters) == tuple(o["n_clusters"])
     np.testing.assert_allclose(_arr(r, xs, "std_errors"), o["se"], rtol=1e-10, atol=0)
