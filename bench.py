@@ -91,6 +91,8 @@ def parse(argv=None):
     ap.add_argument("--no-h2d", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="diagnostic: no per-kernel events (no roofline)")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="A/B only: an engine test knob (lfe_test_set_knob); the engine reads no environment")
     ap.add_argument("--print-rank-env", action="store_true",
                     help="diagnostic: each rank prints its rank / world / device and exits (no GPU call)")
     a = ap.parse_args(argv)
@@ -324,14 +326,17 @@ def gather_bytes(n: int, p: int, F: int) -> dict:
     return {"cross": n * (F - 1) * 128, "check": n * (F - 1) * 8}
 
 
-def pmc_traffic(kernel: str, a) -> tuple[float | None, str | None]:
+def pmc_traffic(kernel: str, a, local_rows: int) -> tuple[float | None, str | None]:
     """HBM bytes per launch of ``kernel`` from the newest rocprofv3 PMC summary for this exact
     configuration (tools/pmc.sh + tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
-    correction of MI355X_MICROARCH.md), else None."""
+    correction of MI355X_MICROARCH.md), else None.  Matched on the rows of the shard this process
+    solved (an --emulate-rank shard is not the whole panel the PMC pass may have measured)."""
     import glob
     import re
 
-    cfg = {"rows": a.rows, "k": a.k, "levels": list(a.levels), "vcov": a.vcov}
+    if a.knob:
+        return None, None  # an A/B variant: the PMC passes measured the production path
+    cfg = {"rows": local_rows, "k": a.k, "levels": list(a.levels), "vcov": a.vcov}
     rounds = glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "pmc_traffic.json"))
     rounds.sort(key=lambda p: int(re.search(r"r(\d+)", os.path.basename(os.path.dirname(p))).group(1)), reverse=True)
     for path in rounds:
@@ -403,8 +408,12 @@ def main(argv=None):
 
     import numpy as np
 
-    from leanfe_amd._lib import Engine
+    from leanfe_amd._lib import Engine, set_knob
     from leanfe_amd.dist import HostGroup
+
+    for kv in a.knob:
+        name, _, val = kv.partition("=")
+        set_knob(name, val)
 
     d = HostGroup()
     if d.world != a.gpus:
@@ -475,7 +484,7 @@ def main(argv=None):
     roofline = None
     if ab.get(dom_name):
         achieved = ab[dom_name] / per_launch_s / 1e9
-        traffic, tsrc = pmc_traffic(dom_name, a)
+        traffic, tsrc = pmc_traffic(dom_name, a, geo["local"])
         roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                     "bytes_per_launch": ab[dom_name], "avg_launch_ms": round(per_launch_s * 1e3, 4)}
@@ -552,6 +561,8 @@ def main(argv=None):
             "gen_s": round(gen_s, 3),
             "beta_dev_vs_host": res["beta_dev_vs_host"],
         }
+        if a.knob:
+            line["knobs"] = list(a.knob)
         if a.verbose:
             line["beta"] = [float(x) for x in res["beta"]]
             line["se"] = [float(x) for x in res["se"]]

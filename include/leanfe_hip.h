@@ -339,6 +339,16 @@ int lfe_wide_cluster_meats(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, i
 #define LFE_TEST_SEG_SCATTER 8
 int lfe_ctx_test_hooks(lfe_ctx* ctx, int flags);
 
+/* Test / A-B knobs (no reference counterpart; tests and bench.py --knob only).  A process-wide
+ * name -> value table: the engine never reads the environment, so only this call can move it off
+ * its production kernel paths.  value NULL removes the knob; name "*" with value NULL removes all.
+ * Names: LFE_DENSE ("0" never / "1" whenever the count tables fit), LFE_DN8 ("0": f64 dense passes),
+ * LFE_DN_C8 / LFE_DN_C4 (table build counter width), LFE_SUMS_CG, LFE_TAB3, LFE_CL_FIX, LFE_CL_FUSED,
+ * LFE_CL_STATS, LFE_CL_OWNER_MIN_SPAN, LFE_ROW_HASH_BITS / LFE_STR_HASH_BITS (short hashes force
+ * collisions), LFE_K1_UNIT, LFE_SEG_SORTED, LFE_GRAM_GEN, ... (the A/B sizes are listed in DESIGN.md).
+ * The diagnostics LFE_DN8_TIMING / LFE_SWEEP_TIMING print per-workgroup phase times to stderr. */
+int lfe_test_set_knob(const char* name, const char* value);
+
 /* Wait for all work queued on the context's stream. */
 int lfe_sync(lfe_ctx* ctx);
 

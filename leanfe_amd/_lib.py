@@ -64,6 +64,7 @@ SIGNATURES = {
     "lfe_exact_sums": (C.c_int, [_vp, _i32p]),
     "lfe_dense_cells": (C.c_int, [_vp, _i64p]),
     "lfe_ctx_test_hooks": (C.c_int, [_vp, C.c_int]),
+    "lfe_test_set_knob": (C.c_int, [C.c_char_p, C.c_char_p]),
     "lfe_dev_alloc": (C.c_int, [_vp, C.c_int64, C.POINTER(_vp)]),
     "lfe_dev_free": (C.c_int, [_vp, _vp]),
     "lfe_materialize": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int]),
@@ -121,6 +122,17 @@ def load_library(path: str | None = None) -> C.CDLL:
         if path is None:
             _lib = lib
         return lib
+
+
+def set_knob(name: str, value: str | None) -> None:
+    """Set (or with None remove) an engine test / A-B knob (lfe_test_set_knob).  The engine reads no
+    environment variables; tests and ``bench.py --knob NAME=VALUE`` use this instead."""
+    lib = load_library()
+    _check(lib.lfe_test_set_knob(name.encode(), None if value is None else str(value).encode()))
+
+
+def clear_knobs() -> None:
+    _check(load_library().lfe_test_set_knob(b"*", None))
 
 
 def _check(rc: int) -> None:

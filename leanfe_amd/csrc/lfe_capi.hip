@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <map>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -11,6 +12,22 @@
 #include "lfe_internal.h"
 
 namespace lfe {
+
+static std::mutex g_knob_mu;
+static std::map<std::string, std::string> g_knobs;
+
+const char* knob(const char* name) {
+  thread_local std::string ring[8];
+  thread_local int slot = 0;
+  std::lock_guard<std::mutex> lk(g_knob_mu);
+  if (g_knobs.empty()) return nullptr;
+  const auto it = g_knobs.find(name);
+  if (it == g_knobs.end()) return nullptr;
+  std::string& out = ring[slot];
+  slot = (slot + 1) & 7;
+  out = it->second;
+  return out.c_str();
+}
 
 static thread_local std::string g_err;
 
@@ -1090,6 +1107,10 @@ int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const i
     if (cl_levels[j] < 1) return fail(LFE_EINVAL, "cluster n_levels must be >= 1");
   for (auto& p : c->cl) dfree(p);
   free_cluster_ws(c);
+  // the residual pass's one-way sums (and the meat cached from them) belong to the old columns;
+  // c->clfused stays, so a subset of the new columns reruns that pass writing score rows
+  c->clfused_done = false;
+  c->clfused_j = -1;
   c->cl.assign(m, nullptr);
   c->cl_levels.assign(cl_levels, cl_levels + m);
   const hipMemcpyKind kind = where == LFE_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
@@ -1306,6 +1327,18 @@ int lfe_exact_sums(lfe_ctx* c, int* on) {
   LFE_CTX(c);
   if (!on) return fail(LFE_EINVAL, "null pointer");
   return exact_sums_on(c, on);
+}
+
+int lfe_test_set_knob(const char* name, const char* value) {
+  if (!name || !name[0]) return fail(LFE_EINVAL, "knob name is empty");
+  std::lock_guard<std::mutex> lk(g_knob_mu);
+  if (value)
+    g_knobs[name] = value;
+  else if (name[0] == '*' && !name[1])
+    g_knobs.clear();
+  else
+    g_knobs.erase(name);
+  return LFE_OK;
 }
 
 int lfe_ctx_test_hooks(lfe_ctx* c, int flags) {

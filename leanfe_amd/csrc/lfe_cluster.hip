@@ -749,8 +749,8 @@ __global__ void k_cl_same(const int32_t* __restrict__ a, const int32_t* __restri
 }
 
 static bool clfix_on() {
-  static const bool on = [] {
-    const char* e = getenv("LFE_CL_FIX");  // "0": the sorted path for one-column subsets too (A/B, tests)
+  const bool on = [] {
+    const char* e = knob("LFE_CL_FIX");  // "0": the sorted path for one-column subsets too (A/B, tests)
     return !(e && e[0] == '0');
   }();
   return on;
@@ -922,7 +922,7 @@ static int subset_meat_seg(lfe_ctx* c, int f, double* meat, int64_t* G_out) {
 // raises the flag (the subset is then redone from score rows).  Deterministic: a fixed function of
 // the tile.
 __global__ void k_clfused_quanta(const double* __restrict__ tile, const double* __restrict__ beta, int p, int64_t n,
-                                 const int32_t* __restrict__ cmax, double* __restrict__ fq) {
+                                 int32_t* __restrict__ cmax, double* __restrict__ fq) {
   __shared__ double rss;
   if (threadIdx.x == 0) {
     double t = 0.0;
@@ -936,6 +936,11 @@ __global__ void k_clfused_quanta(const double* __restrict__ tile, const double* 
       t += vi * u;
     }
     rss = t > 0.0 ? t : 0.0;
+    // a near-perfect fit: v'Tv has cancelled, so rms(r) says nothing about the scores' scale -
+    // raise the bound flag (cmax[1]) and the subset is summed from score rows with the
+    // statistics-pass quanta instead
+    const double yy = tile[1 * 16 + 1];
+    if (!(rss > 0x1p-40 * yy)) cmax[1] = 1;
   }
   __syncthreads();
   const double nn = n > 0 ? (double)n : 1.0;
@@ -951,9 +956,9 @@ __global__ void k_clfused_quanta(const double* __restrict__ tile, const double* 
 // the cluster column whose one-way sums the residual pass can form (it repeats the primary FE),
 // or -1
 int cluster_fused_col(const lfe_ctx* c) {
-  static const bool env_on = [] {  // "LFE_CL_FUSED=0": score rows and the separate sums (A/B)
-    const char* e = getenv("LFE_CL_FUSED");
-    const char* s = getenv("LFE_CL_STATS");
+  const bool env_on = [] {  // "LFE_CL_FUSED=0": score rows and the separate sums (A/B)
+    const char* e = knob("LFE_CL_FUSED");
+    const char* s = knob("LFE_CL_STATS");
     return !(e && e[0] == '0') && !(s && s[0] == '1');
   }();
   const int k = c->p - 1;
@@ -1025,7 +1030,7 @@ int launch_codes_differ(lfe_ctx* c, const int32_t* a, const int32_t* b, int64_t 
 static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   if (c->clfused) {  // the residual pass summed the cluster column that repeats the primary FE
     int redo = 0;
-    if (mask == 1 << c->clfused_j) {
+    if (c->clfused_j >= 0 && mask == 1 << c->clfused_j) {
       LFE_TRY(cluster_fused_finish(c, meat, G_out, &redo));
       if (!redo) return LFE_OK;
     }
@@ -1057,8 +1062,8 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
         bucketed = true;  // the column repeats the primary FE (lfe_load_clusters compared them)
         win = 1 << c->L.s;
       }
-      static const bool stats_env = [] {  // "1": quanta from the statistics pass (A/B, tests)
-        const char* e = getenv("LFE_CL_STATS");
+      const bool stats_env = [] {  // "1": quanta from the statistics pass (A/B, tests)
+        const char* e = knob("LFE_CL_STATS");
         return e && e[0] == '1';
       }();
       if (win > 0)
@@ -1146,14 +1151,14 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   // one process, unweighted, mostly singletons (mean cluster size below 2): D + the multi-row
   // clusters' corrections, without gathering every row
   if (c->world == 1 && k > 0 && c->score_meat_ok && (int)c->score_meat.size() == k * k && G > 0 &&
-      2 * (int64_t)G > (int64_t)nv && getenv("LFE_CL_NO_SINGLETON") == nullptr) {
+      2 * (int64_t)G > (int64_t)nv && knob("LFE_CL_NO_SINGLETON") == nullptr) {
     *G_out = G;
     return singleton_meat(c, W.rows[buf], G, k, meat);
   }
   if (k > 0) LFE_TRY(group_sums(c, n, drop, W.keys[buf], W.rows[buf], c->scores, k, G, nv));
 
   // multi-rank, few clusters: a key-indexed table, all-reduced (smaller than the exchange)
-  const char* own_env = getenv("LFE_CL_OWNER_MIN_SPAN");  // tests: force the owner-partitioned form
+  const char* own_env = knob("LFE_CL_OWNER_MIN_SPAN");  // tests: force the owner-partitioned form
   const uint64_t owner_min = own_env ? (uint64_t)atoll(own_env) : ((64ull << 20) / (8ull * std::max(k, 1)));
   if (c->world > 1 && span < owner_min && span < (1ull << 31)) {
     const int32_t C = (int32_t)span;

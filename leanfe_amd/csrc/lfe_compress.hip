@@ -222,7 +222,7 @@ int lfe_compress(lfe_ctx* c, int64_t* n_records_out) {
   a.p = p;
   for (int f = 0; f < F; ++f) a.icol[a.ni++] = c->fe[f].code;
   for (int j = 0; j < m; ++j) a.icol[a.ni++] = c->cl[j];
-  const char* hb_env = getenv("LFE_ROW_HASH_BITS");  // tests: a short hash forces collisions
+  const char* hb_env = knob("LFE_ROW_HASH_BITS");  // tests: a short hash forces collisions
   const int hb = hb_env ? atoi(hb_env) : 64;
   a.hash_bits = hb >= 4 && hb <= 64 ? hb : 64;
 

@@ -1128,8 +1128,8 @@ __global__ __launch_bounds__(512, 4) void k_dn8_k2s_batch(Dn8Batch b) {
 
 // K1's fewest output blocks per workgroup (LFE_DN8_K1_MIN: A/B)
 static int64_t dn8_k1_min_blocks() {
-  static const int64_t v = [] {
-    const char* e = getenv("LFE_DN8_K1_MIN");
+  const int64_t v = [] {
+    const char* e = knob("LFE_DN8_K1_MIN");
     const long long x = e ? atoll(e) : 4;
     return (int64_t)(x >= 1 ? x : 4);
   }();
@@ -1138,8 +1138,8 @@ static int64_t dn8_k1_min_blocks() {
 
 // LFE_DN8_TIMING=1 (diagnostic): per-workgroup phase times of the last K1 / K2 launch to stderr
 static bool dn8_timing() {
-  static const bool on = [] {
-    const char* e = getenv("LFE_DN8_TIMING");
+  const bool on = [] {
+    const char* e = knob("LFE_DN8_TIMING");
     return e && e[0] == '1';
   }();
   return on;
@@ -1201,12 +1201,12 @@ int64_t dense_table_cells(const lfe_ctx* c) {
 // the exact i8 passes: the counters of a 64-group chunk of GQ64 columns fit the build's LDS, the
 // bucket is whole 64-row k blocks (LFE_DN8=0: the f64 passes, for A/B)
 static bool dn8_tiled() {  // A/B: the tiled forms of the i8 passes
-  const char* e = getenv("LFE_DN8_TILED");
+  const char* e = knob("LFE_DN8_TILED");
   return e && e[0] == '1';
 }
 
 static bool dn8_ok(const lfe_ctx* c) {
-  const char* e = getenv("LFE_DN8");
+  const char* e = knob("LFE_DN8");
   if (e && e[0] == '0') return false;
   const int64_t B = 1ll << c->L.s;
   if (!(B % 64 == 0 && (size_t)kDnHC * dn_gq64(c) * 2 <= 150 * 1024)) return false;
@@ -1221,9 +1221,9 @@ static bool dn8_ok(const lfe_ctx* c);
 // panel without drops (the cmax bound is checked on the device) - LFE_DN_PRE=0 turns it off
 bool dense_pre_ok(const lfe_ctx* c) {
   if (c->dense_off) return false;
-  const char* e = getenv("LFE_DENSE");
+  const char* e = knob("LFE_DENSE");
   if (e && e[0] == '0') return false;
-  const char* pe = getenv("LFE_DN_PRE");
+  const char* pe = knob("LFE_DN_PRE");
   if (pe && pe[0] == '0') return false;
   const int P = c->L.P, Q = 1 - P;
   (void)P;
@@ -1236,7 +1236,7 @@ bool dense_pre_ok(const lfe_ctx* c) {
 
 bool dense_ok(const lfe_ctx* c) {
   if (c->dense_off) return false;  // the digits' range guard fired (lfe_demean)
-  const char* e = getenv("LFE_DENSE");  // "0": never (A/B); "1": whenever it fits
+  const char* e = knob("LFE_DENSE");  // "0": never (A/B); "1": whenever it fits
   if (e && e[0] == '0') return false;
   const int P = c->L.P, Q = 1 - P, p = c->p;
   if (!(c->world == 1 || c->owner_on) || c->nbe < 1) return false;
@@ -1308,13 +1308,13 @@ int dense_build(lfe_ctx* c, bool pre) {
   // owner shard's 25 buckets 0.068 vs 0.055
   const bool c8_fits = (size_t)2 * kDnHC * GQW <= 150 * 1024 && B % (2 * kDnHC) == 0;
   bool c8 = c8_fits && (int64_t)c->nbe * (B / (2 * kDnHC)) >= c->n_cu;
-  if (const char* e = getenv("LFE_DN_C8")) c8 = c8_fits && e[0] == '1';  // tests: force either form
+  if (const char* e = knob("LFE_DN_C8")) c8 = c8_fits && e[0] == '1';  // tests: force either form
   // 256-group chunks on 4-bit counters (the i8 tables; half the code reads of the 8-bit form) where
   // cells average under 2 rows (a 16-row cell is then rare) and the chunks still fill the CUs
   const bool c4_fits = c8_fits && c->dn8 && B % (4 * kDnHC) == 0;
   bool c4 = c4_fits && (int64_t)c->nbe * (B / (4 * kDnHC)) >= c->n_cu &&
             (double)c->n < 2.0 * (double)std::max(c->nbe, 1) * B * GQ64;
-  if (const char* e = getenv("LFE_DN_C4")) c4 = c4_fits && e[0] == '1';  // A/B, tests
+  if (const char* e = knob("LFE_DN_C4")) c4 = c4_fits && e[0] == '1';  // A/B, tests
   a.nch = B / (c4 ? 4 * kDnHC : c8 ? 2 * kDnHC : kDnHC);
   a.NA = c->dn_na;
   a.NB = c->dn_nb;
@@ -1334,7 +1334,7 @@ int dense_build(lfe_ctx* c, bool pre) {
 static int dn_parts(const lfe_ctx* c, int blocks, int wpc) {
   int kp = 1;
   int64_t rounds = 1;
-  if (const char* e = getenv("LFE_DN_ROUNDS")) rounds = std::max(1ll, atoll(e));  // A/B only
+  if (const char* e = knob("LFE_DN_ROUNDS")) rounds = std::max(1ll, atoll(e));  // A/B only
   while (kp < kDnWaves && (int64_t)blocks * kp < rounds * c->n_cu * wpc) kp *= 2;
   return kp;
 }
@@ -1379,7 +1379,7 @@ int range_flag_reset(lfe_ctx* c) {
 // 196 buckets x 3 parts = 588 > 512), at least 8 output blocks each
 static int k2_parts(const lfe_ctx* c, int nbe, int nrb) {
   int np = (int)std::max<int64_t>(1, (2 * (int64_t)c->n_cu) / std::max(nbe, 1));
-  if (const char* e = getenv("LFE_K2_NP")) np = std::max(1, atoi(e));  // A/B only
+  if (const char* e = knob("LFE_K2_NP")) np = std::max(1, atoi(e));  // A/B only
   return std::min(np, std::max(1, nrb / 8));
 }
 

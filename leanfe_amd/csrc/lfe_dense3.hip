@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void k_d3_ycheck(const double* __restrict__ S,
 bool dense3_ok(const lfe_ctx* c, const std::vector<int>& order, int check_from) {
   (void)order;
   if (c->dense_off) return false;  // the digits' range guard fired (lfe_demean)
-  const char* e = getenv("LFE_DENSE");  // "0": never (A/B); "1": whenever it fits
+  const char* e = knob("LFE_DENSE");  // "0": never (A/B); "1": whenever it fits
   if (e && e[0] == '0') return false;
   const bool force = e && e[0] == '1';
   const int F = c->F;
@@ -478,8 +478,8 @@ static int d3_cross(lfe_ctx* c, int f, bool y_only, int* ns_out) {
     slot += tiles_of(c->fe[b].G);
   }
   // every partner and column group of the projection in one launch (LFE_D3_BATCH=0: one each, A/B)
-  static const bool batch = [] {
-    const char* e = getenv("LFE_D3_BATCH");
+  const bool batch = [] {
+    const char* e = knob("LFE_D3_BATCH");
     return !(e && e[0] == '0');
   }();
   if (batch) {

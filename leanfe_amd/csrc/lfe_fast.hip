@@ -800,7 +800,7 @@ __global__ __launch_bounds__(kCgThreads) void k_sums_cg(SumsCgArgs a) {
 static int sums_cg_nc(const lfe_ctx* c) {
   const int P = c->L.P;
   if (c->F < 2 || c->F > kCgMaxF || P < 0) return 0;
-  const char* e = getenv("LFE_SUMS_CG");  // "0": off (A/B)
+  const char* e = knob("LFE_SUMS_CG");  // "0": off (A/B)
   if (e && e[0] == '0') return 0;
   int64_t per_col = (int64_t)1 << c->L.s;
   for (int f = 0; f < c->F; ++f)

@@ -819,8 +819,8 @@ static const void* gram_kernel(bool general, bool weighted, bool ql, bool nq2 = 
     // three FEs at p <= 16: two 16-row groups per wave iteration with X loaded a batch ahead
     // (config 4: residual 3.76 -> 3.47 ms, design 2.39 -> 2.29 ms; round 5).  LFE_GRAM_GEN=0: the
     // generic variant (A/B)
-    static const int gen = [] {
-      const char* e = getenv("LFE_GRAM_GEN");
+    const int gen = [] {
+      const char* e = knob("LFE_GRAM_GEN");
       return e ? atoi(e) : 2;
     }();
     if (gen == 2 && nq2 && NT == 1)
@@ -838,8 +838,8 @@ static const void* gram_kernel(bool general, bool weighted, bool ql, bool nq2 = 
                               : reinterpret_cast<const void*>(&k_gram<M, NT, 1, GU, false, false, kGramThreads>))
   // wide fits: one 16-row group per wave iteration (GU 2 holds 232 registers at NT = 2: two waves
   // per SIMD) unless LFE_GRAM_GU=2 (A/B)
-  static const int gu_wide = [] {
-    const char* e = getenv("LFE_GRAM_GU");
+  const int gu_wide = [] {
+    const char* e = knob("LFE_GRAM_GU");
     return e ? atoi(e) : 1;
   }();
   if (NT >= 2 && gu_wide == 1) return GRAM_FN(1);
@@ -1146,8 +1146,8 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, do
       src = msum;
       ns = 1;
     }
-    static const bool split = [] {  // diagnostic: the Cholesky as its own launch (rocprof A/B)
-      const char* e = getenv("LFE_CHOL_SPLIT");
+    const bool split = [] {  // diagnostic: the Cholesky as its own launch (rocprof A/B)
+      const char* e = knob("LFE_CHOL_SPLIT");
       return e && e[0] == '1';
     }();
     hipLaunchKernelGGL(kfinal, dim3(1), dim3(1024), 0, c->stream, src, ns, c->raw_tile, p, out_dev, flag_dev,
@@ -1547,7 +1547,7 @@ __global__ __launch_bounds__(256) void k_raw_perm(const double* __restrict__ rt,
 }
 
 static bool tables3_ok(const lfe_ctx* c) {
-  const char* e = getenv("LFE_TAB3");  // "0": the design pass (A/B)
+  const char* e = knob("LFE_TAB3");  // "0": the design pass (A/B)
   if (e && e[0] == '0') return false;
   if (!(c->world == 1 && !c->L.w && !c->records && !c->sw.on && c->p <= kT3MaxP && c->L.P >= 0 && c->L.n_items > 0))
     return false;

@@ -38,6 +38,12 @@ constexpr size_t kPinSmall = 192 * 1024; // pinned staging total (D2H + small H2
 
 void set_error(const std::string& msg);
 
+// Test / A-B knobs: a process-wide name -> value table that only lfe_test_set_knob writes (tests,
+// bench --knob).  The engine never reads the environment, so a stray variable cannot change which
+// kernels run; with no knob set every path is the production one.  nullptr = not set.  The value
+// is a copy in a small per-thread ring: read it at once (e[0], atoi), do not keep the pointer.
+const char* knob(const char* name);
+
 #define LFE_HIP(expr)                                                                    \
   do {                                                                                   \
     hipError_t _e = (expr);                                                              \

@@ -609,7 +609,7 @@ static int build_layouts(lfe_ctx* c, int Q) {
   // shard) 0.107 -> 0.090 (512), 1M (config 1) 0.121 -> 0.080 (512).  LFE_K1_UNIT: a fixed size.
   const int64_t waves = (int64_t)c->n_cu * 16;  // K1: one 1024-thread workgroup per CU
   int64_t U = std::max<int64_t>(256, ((c->n_kept_local + waves - 1) / waves + 15) / 16 * 16);
-  if (const char* e = getenv("LFE_K1_UNIT")) U = std::max<int64_t>(16, atoll(e) / 16 * 16);
+  if (const char* e = knob("LFE_K1_UNIT")) U = std::max<int64_t>(16, atoll(e) / 16 * 16);
   const int32_t H = L.nb * B;
   c->n_units = (int)std::max<int64_t>(1, (c->n_kept_local + U - 1) / U);
   LFE_TRY(ensure_i32(c, c->seg_units, c->seg_units_cap, (size_t)4 * c->n_units));
@@ -1291,7 +1291,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
      // proportionally fewer rows
     const int64_t per_bucket = c->n_kept_local / nbe;
     int64_t min_rows = std::max<int64_t>(2048, (int64_t)8192 * p / 11);
-    if (const char* e = getenv("LFE_K2_MINROWS")) min_rows = std::max<int64_t>(256, atoll(e));  // A/B only
+    if (const char* e = knob("LFE_K2_MINROWS")) min_rows = std::max<int64_t>(256, atoll(e));  // A/B only
     tq.split = (int)std::max<int64_t>(1, std::min<int64_t>(tq.split, per_bucket / min_rows));
     // ... but no fewer workgroups than CUs while each keeps >= 8K rows (6.25M rows over 196
     // buckets: 196 -> 392 workgroups)
@@ -1316,7 +1316,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     }
   }
   // LFE_SWEEP_TIMING (diagnostic): per-workgroup wall clock of the last K1 / K2 launch to stderr
-  const bool timing = !dense && getenv("LFE_SWEEP_TIMING") != nullptr;
+  const bool timing = !dense && knob("LFE_SWEEP_TIMING") != nullptr;
   const int tp_grid = c->n_cu, tq_grid_wg = std::max(tq.nbe, 1) * tq.split;
   if (timing) {
     LFE_HIP(hipMalloc(&tp.dbg, sizeof(unsigned long long) * 2 * tp_grid));

@@ -494,7 +494,7 @@ int lfe_factorize_strings(lfe_ctx* c, int64_t n, const int64_t* offsets, const u
   a.off = static_cast<const int64_t*>(boff.p);
   a.data = static_cast<const uint8_t*>(bdata.p);
   a.n = n;
-  const char* hb_env = getenv("LFE_STR_HASH_BITS");  // tests: a short hash forces collisions
+  const char* hb_env = knob("LFE_STR_HASH_BITS");  // tests: a short hash forces collisions
   const int hb = hb_env ? atoi(hb_env) : 64;
   a.hash_bits = hb >= 4 && hb <= 64 ? hb : 64;
   LFE_HIP(hipMemcpyAsync(boff.p, offsets, sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, c->stream));
@@ -569,7 +569,7 @@ int lfe_count_distinct_rows(lfe_ctx* c, int n_x, int64_t* n_distinct_out) {
   a.p = n_x < 0 ? c->p : 1 + n_x;  // key: x columns 1..n_x (instruments after them are not keyed)
   a.F = c->F;
   for (int f = 0; f < c->F; ++f) a.code[f] = c->fe[f].code;
-  const char* hb_env = getenv("LFE_ROW_HASH_BITS");  // tests: a short hash forces collisions
+  const char* hb_env = knob("LFE_ROW_HASH_BITS");  // tests: a short hash forces collisions
   const int hb = hb_env ? atoi(hb_env) : 64;
   a.hash_bits = hb >= 4 && hb <= 64 ? hb : 64;
   hipLaunchKernelGGL(k_row_hash, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, c->stream, a, W.keys[0], W.rows[0]);

@@ -1069,7 +1069,7 @@ int prepare_layout(lfe_ctx* c) {
       for (int64_t w = 8192; w >= 4096; w /= 2)
         if (fill(w) > fill(cw) + 0.1) cw = w;
     }
-    if (const char* e = getenv("LFE_PART_CW")) cw = atoll(e);  // A/B only
+    if (const char* e = knob("LFE_PART_CW")) cw = atoll(e);  // A/B only
     auto part_lds = [&](int nth) {  // stage, 16-bit per-wave cursors, deltas and totals
       return sizeof(double) * cw + sizeof(uint16_t) * (((size_t)(nth / 64) * nb + 1) & ~(size_t)1) +
              sizeof(int32_t) * (2 * (size_t)nb + 1);

@@ -880,13 +880,13 @@ int seg_build(lfe_ctx* c) {
     a.oc[f] = fe.oc;
     a.ws[f] = weighted ? fe.ws : nullptr;
   }
-  static const int sorted_env = [] {  // "0": k_seg_scatter2 for every fit (A/B)
-    const char* e = getenv("LFE_SEG_SORTED");
+  const int sorted_env = [] {  // "0": k_seg_scatter2 for every fit (A/B)
+    const char* e = knob("LFE_SEG_SORTED");
     return e ? atoi(e) : 1;
   }();
   // the sorted build: unweighted, two or three FEs, its workspace (24 bytes a row) at most 6 GB
   const bool sorted0 = sorted_env != 0 && !(c->test_hooks & LFE_TEST_SEG_SCATTER) && !weighted && (c->F == 2 || c->F == 3) && n > 0 &&
-                      c->ld <= (int64_t)1 << 28 && getenv("LFE_SEG_SCATTER_ROWS") == nullptr;
+                      c->ld <= (int64_t)1 << 28 && knob("LFE_SEG_SCATTER_ROWS") == nullptr;
   int bits[kMaxFE] = {}, bsum = 0;  // code bits of every FE (at least 1): the packed keys need <= 63
   for (int f = 0; f < c->F; ++f) {
     bits[f] = std::max(1, bit_length((uint64_t)std::max(c->fe[f].G - 1, 0)));
@@ -956,7 +956,7 @@ int seg_build(lfe_ctx* c) {
     ProfScope _ps(c, K_SEG_BUILD);
     if (sorted) {
       // (built above)
-    } else if (n > 0 && getenv("LFE_SEG_SCATTER_ROWS") == nullptr) {  // (env: the per-row kernel, A/B only)
+    } else if (n > 0 && knob("LFE_SEG_SCATTER_ROWS") == nullptr) {  // (env: the per-row kernel, A/B only)
       SegScatter2Args a2{};
       a2.s = a;
       for (int f = 0; f < c->F; ++f) a2.G[f] = c->fe[f].G;

@@ -522,6 +522,12 @@ int lfe_wide_cluster_meats(lfe_ctx* c, const double* D, int64_t ldD, int c0, int
   size_t full_cap = 0;
   LFE_TRY(walloc(&cid, (size_t)std::max<int64_t>(n, 1)));
   int rc = LFE_OK;
+  auto hip_ok = [&rc](hipError_t e, const char* what) {  // the fills below: errors into rc, as the rest
+    if (e != hipSuccess && rc == LFE_OK) {
+      set_error(std::string(what) + ": " + hipGetErrorString(e));
+      rc = e == hipErrorOutOfMemory ? LFE_ENOMEM : LFE_EHIP;
+    }
+  };
   for (int s = 0; s < n_subsets && rc == LFE_OK; ++s) {
     int32_t G = 0;
     rc = cluster_ids_input(c, masks[s], D, cid, &G);  // D's column 0: the kept rows
@@ -544,13 +550,14 @@ int lfe_wide_cluster_meats(lfe_ctx* c, const double* D, int64_t ldD, int c0, int
     if (rc != LFE_OK) break;
     int32_t* cnt = c->clP;
     int32_t* cm = c->clP + G;
-    hipMemsetAsync(cnt, 0, sizeof(int32_t) * ((size_t)G + 4), c->stream);
+    hip_ok(hipMemsetAsync(cnt, 0, sizeof(int32_t) * ((size_t)G + 4), c->stream), "hipMemsetAsync(counts)");
     // columns in passes of <= 64 (one quanta table each); a wider table is assembled in `full`
     for (int cb = 0; cb < k && rc == LFE_OK; cb += kWcCols) {
       const int kg = std::min(kWcCols, k - cb);
-      hipMemsetAsync(W.fixst, 0, sizeof(double) * kColStatHead, c->stream);
-      hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream);
-      hipMemsetAsync(W.srec, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream);
+      hip_ok(hipMemsetAsync(W.fixst, 0, sizeof(double) * kColStatHead, c->stream), "hipMemsetAsync(fixst)");
+      hip_ok(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream), "hipMemsetAsync(clS)");
+      hip_ok(hipMemsetAsync(W.srec, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream), "hipMemsetAsync(srec)");
+      if (rc != LFE_OK) break;
       WideScoreArgs a{D, ldD, n, c0 + cb, kg, r, c->w, cid};
       {
         ProfScope _ps(c, K_CLUSTER_SCATTER);

@@ -260,12 +260,14 @@ class Expansion:
         """The numeric columns the interaction terms multiply (streamed with the chunks)."""
         return list(dict.fromkeys(t[1] for t in self.terms if t[1] is not None))
 
-    def columns(self, factors: dict[str, np.ndarray], values: dict[str, np.ndarray], rows: slice | None = None):
+    def columns(self, factors: dict[str, np.ndarray], values: dict[str, np.ndarray], rows: slice | None = None,
+                which: list[int] | None = None):
         """The expanded columns for one row range: ``factors`` hold the whole factor columns
-        (sliced by ``rows``), ``values`` the interactions' numeric columns of that range."""
+        (sliced by ``rows``), ``values`` the interactions' numeric columns of that range;
+        ``which``: only these terms (indices into ``terms``)."""
         sl = rows if rows is not None else slice(None)
         out = []
-        for _, var, factor, cat in self.terms:
+        for _, var, factor, cat in (self.terms if which is None else [self.terms[i] for i in which]):
             hit = np.asarray(factors[factor])[sl] == cat
             out.append(np.asarray(values[var], dtype=np.float64) * hit if var is not None else hit.astype(np.float64))
         return out

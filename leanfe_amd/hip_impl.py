@@ -22,7 +22,14 @@ from .strategy import DEFAULT_MAX_FE_LEVELS, determine_strategy
 
 MAX_FE_LEVELS = DEFAULT_MAX_FE_LEVELS  # polars_impl.py:24
 MAX_CONTEXT_COLS = 63  # columns one engine context holds (y + regressors + instruments); wider: _wide_fit
-_VERBOSE = os.environ.get("LEANFE_HIP_VERBOSE", "0") not in ("", "0")
+_VERBOSE = os.environ.get("LEANFE_HIP_VERBOSE", "0") not in ("", "0")  # log lines only
+# Path switches for tests and A/B runs (the process environment selects no path):
+#   out_of_core   default of leanfe_hip(out_of_core=None)
+#   stream        a Parquet path streams into the engine batch by batch (False: read whole first)
+#   stream_batch  rows per streamed Parquet batch
+#   reshard       sharded two-FE fits move contiguous row blocks to owner ranks (lfe_reshard_owner)
+#   context_rows  rows per engine context (None: 2^31 - 64, the int32 row-index cap)
+KNOBS = {"out_of_core": False, "stream": True, "stream_batch": 1 << 22, "reshard": True, "context_rows": None}
 
 
 def _default_device() -> int:
@@ -78,11 +85,11 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     # then [y] + x + instruments are decoded batch by batch while earlier batches upload
     # (pl.scan_parquet's role, polars_impl.py:341-343)
     if out_of_core is None:
-        out_of_core = os.environ.get("LEANFE_HIP_OUT_OF_CORE", "0") == "1"
+        out_of_core = bool(KNOBS["out_of_core"])
     expand = bool(factor_vars or interactions)
     # (a resident fit expands factor / interaction terms on whole columns; an out-of-core fit per chunk)
     stream = (isinstance(data, str) and (out_of_core or not expand) and sample_frac is None
-              and os.environ.get("LEANFE_HIP_STREAM", "1") != "0")
+              and KNOBS["stream"])
     factor_src = [var for var, _ in factor_vars] + [fac for _, fac, _ in interactions]
     if stream:
         small = list(dict.fromkeys(fe_cols + list(cluster_cols or []) + ([weights] if weights else []) + factor_src))
@@ -161,7 +168,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
         t0 = time.perf_counter()
         if stream:
             eng.load_begin(n_rows, len(num_cols), levels, weighted=w is not None)
-            batch = int(os.environ.get("LEANFE_HIP_STREAM_BATCH", 1 << 22))
+            batch = int(KNOBS["stream_batch"])
             for row0, b in frame.stream_parquet(data, num_cols, batch_rows=batch):
                 sl = slice(row0, row0 + len(b[y_col]))
                 eng.load_rows(row0, [b[c] for c in num_cols], [c[sl] for c in codes], None if w is None else w[sl])
@@ -183,7 +190,7 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
             # cluster on the primary FE is then summed inside the residual pass (lfe_gram.hip)
             cl_loaded = _load_clusters(eng, cols, cluster_cols, sharded)
         if (sharded and len(fe_cols) >= 2 and strategy in ("auto", "alt_proj")
-                and os.environ.get("LEANFE_HIP_RESHARD", "1") != "0"):
+                and KNOBS["reshard"]):
             # contiguous row blocks -> owner-sharded rows (lfe_reshard_owner): every rank then holds
             # all rows of a range of the primary FE's (most levels) levels, and a projection
             # all-reduces only the other FEs' tables - two FEs or more, weighted or not
@@ -311,10 +318,11 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
 
 
 def context_rows() -> int:
-    """Rows one engine context holds (its row indices are int32; LEANFE_HIP_CONTEXT_ROWS lowers
+    """Rows one engine context holds (its row indices are int32; KNOBS["context_rows"] lowers
     it, e.g. for tests of the multi-context split at small sizes)."""
     cap = (1 << 31) - 64
-    return max(1, min(cap, int(os.environ.get("LEANFE_HIP_CONTEXT_ROWS", cap))))
+    want = KNOBS["context_rows"]
+    return max(1, min(cap, int(want if want is not None else cap)))
 
 
 def _out_of_core_split(device, args, plan, x_base) -> LeanFEResult:
@@ -371,24 +379,33 @@ def _stream_chunks(source, cols, n_rows, chunk_rows, y_col, x_cols, instruments,
                    select=None):
     """(row0, columns) per row chunk of an out-of-core source (a Parquet path, re-read per pass, or
     in-memory arrays): [y] + x_cols + instruments, the factor / interaction columns of x_cols (after
-    ``x_base``) formed from the chunk by ``plan``; ``select``: only these indices of that list."""
+    ``x_base``) formed from the chunk by ``plan``; ``select``: only these indices of that list, and
+    only the source columns they need are read (a wide fit's column block)."""
     base = [y_col] + list(x_cols if plan is None else x_base)
-    read = list(dict.fromkeys(base + (plan.numeric_sources if plan else []) + list(instruments)))
+    nb, nt = len(base), (len(plan.terms) if plan is not None else 0)
+    sel = list(range(nb + nt + len(instruments))) if select is None else list(select)
+    sb = [i for i in sel if i < nb]
+    st = [i - nb for i in sel if nb <= i < nb + nt]
+    sz = [i - nb - nt for i in sel if i >= nb + nt]
+    need = [base[i] for i in sb] + [plan.terms[t][1] for t in st if plan.terms[t][1] is not None] + \
+        [instruments[j] for j in sz]
+    read = list(dict.fromkeys(need or [y_col]))
+    pos = {i: j for j, i in enumerate(sb + [nb + t for t in st] + [nb + nt + z for z in sz])}
 
     def assemble(b, rows):
-        out = [np.asarray(b[c], dtype=np.float64) for c in base]
-        if plan is not None:
-            out += plan.columns(cols, b, rows)
-        out += [np.asarray(b[z], dtype=np.float64) for z in instruments]
-        return out if select is None else [out[i] for i in select]
+        out = [np.asarray(b[base[i]], dtype=np.float64) for i in sb]
+        if st:
+            out += plan.columns(cols, b, rows, which=st)
+        out += [np.asarray(b[instruments[j]], dtype=np.float64) for j in sz]
+        return [out[pos[i]] for i in sel]
 
     if isinstance(source, str):
         for row0, b in frame.stream_parquet(source, read, batch_rows=chunk_rows, row_range=row_range):
-            yield row0, assemble(b, slice(row0, row0 + len(b[y_col])))
+            yield row0, assemble(b, slice(row0, row0 + len(b[read[0]])))
     else:
         for r0 in range(0, n_rows, chunk_rows):
             b = {c: source[c][r0:r0 + chunk_rows] for c in read}
-            yield r0, assemble(b, slice(r0, r0 + len(b[y_col])))
+            yield r0, assemble(b, slice(r0, r0 + len(b[read[0]])))
 
 
 def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_cols, codes, levels, w, cluster_cols,

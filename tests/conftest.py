@@ -22,3 +22,31 @@ def gpu_available() -> bool:
         return hip.hipGetDeviceCount(ctypes.byref(n)) == 0 and n.value > 0
     except Exception:
         return False
+
+
+class Knobs:
+    """The engine's test / A-B knobs (lfe_test_set_knob), with monkeypatch's setenv / delenv shape.
+    The engine reads no environment variables: a test that wants a non-default kernel path sets a
+    knob, and every knob it set is removed at teardown."""
+
+    def __init__(self):
+        self.names = set()
+
+    def setenv(self, name: str, value) -> None:
+        from leanfe_amd._lib import set_knob
+        set_knob(name, str(value))
+        self.names.add(name)
+
+    def delenv(self, name: str, raising: bool = False) -> None:
+        from leanfe_amd._lib import set_knob
+        set_knob(name, None)
+        self.names.discard(name)
+
+
+@pytest.fixture
+def knob():
+    k = Knobs()
+    yield k
+    if k.names:
+        from leanfe_amd._lib import clear_knobs
+        clear_knobs()

@@ -218,3 +218,38 @@ def test_intersections_on_the_primary_fe_sort_below_its_buckets(L, cl, weighted)
     np.testing.assert_allclose(_arr(r, xs, "std_errors"), o["se"], rtol=1e-10, atol=0)
     np.testing.assert_allclose(_arr(r, xs, "std_errors"), _arr(srt, xs, "std_errors"), rtol=1e-12, atol=0)
     np.testing.assert_array_equal(_arr(r, xs, "std_errors"), _arr(again, xs, "std_errors"))
+
+
+def test_clusters_loaded_after_the_fused_pass():
+    """ADVICE r5: the residual pass summed a one-way cluster on the primary FE (no score rows);
+    cluster columns loaded afterwards (Engine.load_clusters is public) must get their own meat - the
+    pass is rerun writing score rows - never the one cached for the old column.  Against the sorted
+    path (LFE_TEST_CLUSTER_SORTED) on the same engine calls."""
+    from leanfe_amd._lib import Engine
+
+    n, k, L = 300_000, 3, [8_000, 300]
+
+    def run(hooks):
+        with Engine(0) as eng:
+            if hooks:
+                eng.test_hooks(hooks)
+            eng.synth_load(n, k, L, synth.betas(k), seed=44)
+            _, codes = eng.copy_inputs()
+            eng.load_clusters([np.ascontiguousarray(codes[0])], [L[0]])
+            _, _, card = eng.drop_singletons()
+            eng.demean(sorted(range(2), key=lambda i: card[i]), 1e-6, 50, check_from=3)
+            assert eng.gram_resid(keep_scores=True) is not None
+            m1, g1 = eng.cluster_meat()
+            again = eng.cluster_meat()  # the cached meat of the same pass
+            np.testing.assert_array_equal(again[0], m1)
+            eng.load_clusters([np.ascontiguousarray(codes[1])], [L[1]])
+            m2, g2 = eng.cluster_meat()
+            eng.load_clusters([np.ascontiguousarray(codes[0]), np.ascontiguousarray(codes[1])], L)
+            m3, g3 = eng.cluster_meat_subsets([(0,), (1,), (0, 1)])
+            return (m1, g1), (m2, g2), (m3, g3)
+
+    fused, srt = run(0), run(SORTED)
+    assert int(fused[0][1][0]) == L[0] and int(fused[1][1][0]) == L[1]
+    for (a, ga), (b, gb) in zip(fused, srt):
+        np.testing.assert_array_equal(ga, gb)
+        assert np.abs(a - b).max() <= 1e-12 * np.abs(b).max()

@@ -52,7 +52,7 @@ def _check(res, o):
 
 
 @pytest.mark.parametrize("vcov", ["HC1", "iid"])
-def test_dense_and_row_paths_match_oracle_and_each_other(vcov, monkeypatch):
+def test_dense_and_row_paths_match_oracle_and_each_other(vcov, knob):
     from leanfe_amd import synth
 
     k = 5
@@ -60,9 +60,9 @@ def test_dense_and_row_paths_match_oracle_and_each_other(vcov, monkeypatch):
     # 0.6 rows per cell: the default picks the dense path
     data = synth.panel(1_200_000, k, [4_000, 500], seed=2024)
     o = _oracle(data, xs, vcov)
-    monkeypatch.setenv("LFE_DENSE", "0")
+    knob.setenv("LFE_DENSE", "0")
     rows = _fit(data, xs, vcov)
-    monkeypatch.delenv("LFE_DENSE")
+    knob.delenv("LFE_DENSE")
     dense = _fit(data, xs, vcov)
     _check(rows, o)
     _check(dense, o)
@@ -72,7 +72,7 @@ def test_dense_and_row_paths_match_oracle_and_each_other(vcov, monkeypatch):
     np.testing.assert_array_equal(dense[1], again[1])
 
 
-def test_dense_with_singletons_and_ragged_bucket(monkeypatch):
+def test_dense_with_singletons_and_ragged_bucket(knob):
     """Singleton rows dropped before the table is built (40 primary levels with one row each); a
     primary FE whose last bucket is partial (G_P = 3,041) and a secondary FE that is not a multiple
     of 16 levels (G_Q = 77)."""
@@ -84,11 +84,11 @@ def test_dense_with_singletons_and_ragged_bucket(monkeypatch):
     fe1 = np.array(data["fe1"], copy=True)
     fe1[:40] = np.arange(40) + 3_001  # 40 new levels of one row each: singletons, dropped
     data = dict(data, fe1=fe1)
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     _check(_fit(data, xs), _oracle(data, xs))
 
 
-def test_dense_counts_beyond_8_bits(monkeypatch):
+def test_dense_counts_beyond_8_bits(knob):
     """(h, q) pairs with ~50K rows: on the 8-bit counters of the build (forced with LFE_DN_C8=1: at
     1,000 primary levels the build would otherwise pick 16-bit chunks, since 8-bit ones would leave
     CUs idle) these pairs overflow, and the chunk is counted again on 16-bit counters.  A wrapped
@@ -108,22 +108,22 @@ def test_dense_counts_beyond_8_bits(monkeypatch):
     data = {"y": y, "fe1": fe1, "fe2": fe2, **{f"x{j + 1}": x[:, j].copy() for j in range(k)}}
     xs = ["x1", "x2", "x3"]
     o = _oracle(data, xs)
-    monkeypatch.setenv("LFE_DENSE", "1")
-    monkeypatch.setenv("LFE_DN_C8", "1")
+    knob.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DN_C8", "1")
     dense8 = _fit(data, xs)
     _check(dense8, o)
-    monkeypatch.setenv("LFE_DN_C8", "0")
+    knob.setenv("LFE_DN_C8", "0")
     dense16 = _fit(data, xs)
     np.testing.assert_array_equal(dense8[0], dense16[0])
     np.testing.assert_array_equal(dense8[1], dense16[1])
-    monkeypatch.delenv("LFE_DN_C8")
-    monkeypatch.setenv("LFE_DENSE", "0")
+    knob.delenv("LFE_DN_C8")
+    knob.setenv("LFE_DENSE", "0")
     rows = _fit(data, xs)
     _check(rows, o)
     np.testing.assert_allclose(dense8[0], rows[0], rtol=1e-13, atol=0)
 
 
-def test_dense_owner_shard_matches_whole_panel(monkeypatch):
+def test_dense_owner_shard_matches_whole_panel(knob):
     """Rank 7 of 8 of the strong-scaled headline schedule solved alone (bench --emulate-rank): its
     few buckets take the dense path and the owner shard matches the oracle on the same rows."""
     import bench
@@ -132,7 +132,7 @@ def test_dense_owner_shard_matches_whole_panel(monkeypatch):
     from oracle import altproj
 
     n, k, L = 2_000_000, 4, [40_000, 300]
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     with Engine(0) as eng:
         eng.synth_load_owned(n, k, L, synth.betas(k), 0, 35_000, 40_000, seed=31)
         got = bench.solve_step(eng, "iid")
@@ -148,7 +148,7 @@ def test_dense_owner_shard_matches_whole_panel(monkeypatch):
 
 
 @pytest.mark.parametrize("vcov,p_k", [("HC1", 10), ("iid", 3), ("HC1", 15)])
-def test_dense_i8_digits_match_f64_mfma_and_oracle(vcov, p_k, monkeypatch):
+def test_dense_i8_digits_match_f64_mfma_and_oracle(vcov, p_k, knob):
     """The i8 passes (default) against the f64-MFMA passes (LFE_DN8=0) and the oracle: equal
     integers, beta / SE at 1e-10 of the oracle and 1e-12 of each other, bit-identical repeats;
     k = 15 fills all 16 MFMA columns (p = 16)."""
@@ -157,10 +157,10 @@ def test_dense_i8_digits_match_f64_mfma_and_oracle(vcov, p_k, monkeypatch):
     xs = [f"x{j + 1}" for j in range(p_k)]
     data = synth.panel(900_000, p_k, [3_000, 600], seed=77)
     o = _oracle(data, xs, vcov)
-    monkeypatch.setenv("LFE_DENSE", "1")
-    monkeypatch.setenv("LFE_DN8", "0")
+    knob.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DN8", "0")
     f64 = _fit(data, xs, vcov)
-    monkeypatch.delenv("LFE_DN8")
+    knob.delenv("LFE_DN8")
     i8 = _fit(data, xs, vcov)
     _check(f64, o)
     _check(i8, o)
@@ -171,7 +171,7 @@ def test_dense_i8_digits_match_f64_mfma_and_oracle(vcov, p_k, monkeypatch):
     np.testing.assert_array_equal(i8[1], again[1])
 
 
-def test_dense_i8_flagged_blocks_mixed_with_exact_blocks(monkeypatch):
+def test_dense_i8_flagged_blocks_mixed_with_exact_blocks(knob):
     """A few (h, q) pairs with 128-400 rows among ordinary cells: their 16 x 64 blocks are flagged
     (zero in the i8 tables, u16 counts summed in f64) while every other block runs on the i8
     MFMAs - both orientations (K1 and K2 blocks) - against the oracle and the f64 passes."""
@@ -191,15 +191,15 @@ def test_dense_i8_flagged_blocks_mixed_with_exact_blocks(monkeypatch):
     data = {"y": y, "fe1": fe1, "fe2": fe2, **{f"x{j + 1}": x[:, j].copy() for j in range(k)}}
     xs = [f"x{j + 1}" for j in range(k)]
     o = _oracle(data, xs)
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     i8 = _fit(data, xs)
     _check(i8, o)
-    monkeypatch.setenv("LFE_DN8", "0")
+    knob.setenv("LFE_DN8", "0")
     f64 = _fit(data, xs)
     np.testing.assert_allclose(i8[0], f64[0], rtol=1e-12, atol=0)
 
 
-def test_dense_four_bit_counters(monkeypatch):
+def test_dense_four_bit_counters(knob):
     """The 256-group chunks on 4-bit counters (LFE_DN_C4=1): a sparse panel's tables are the same
     bits as the 8-bit build's, and a panel with cells of 16+ rows (two ~50K-row pairs and many
     2-16-row ones) recounts those chunks on 8- and 16-bit counters and still matches the oracle."""
@@ -207,10 +207,10 @@ def test_dense_four_bit_counters(monkeypatch):
 
     xs = ["x1", "x2", "x3"]
     data = synth.panel(1_000_000, 3, [4_096, 1_000], seed=13)
-    monkeypatch.setenv("LFE_DENSE", "1")
-    monkeypatch.setenv("LFE_DN_C4", "1")
+    knob.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DN_C4", "1")
     c4 = _fit(data, xs)
-    monkeypatch.setenv("LFE_DN_C4", "0")
+    knob.setenv("LFE_DN_C4", "0")
     c8 = _fit(data, xs)
     np.testing.assert_array_equal(c4[0], c8[0])
     np.testing.assert_array_equal(c4[1], c8[1])
@@ -226,12 +226,12 @@ def test_dense_four_bit_counters(monkeypatch):
     y = x @ np.array([1.0, -0.5, 0.25]) + rng.standard_normal(1_024)[fe1] + rng.standard_normal(40)[fe2] + \
         rng.standard_normal(n)
     heavy_data = {"y": y, "fe1": fe1, "fe2": fe2, **{f"x{j + 1}": x[:, j].copy() for j in range(3)}}
-    monkeypatch.setenv("LFE_DN_C4", "1")
+    knob.setenv("LFE_DN_C4", "1")
     _check(_fit(heavy_data, xs), _oracle(heavy_data, xs))
 
 
 @pytest.mark.parametrize("vcov,p_k", [("HC1", 14), ("iid", 20), ("HC1", 20)])
-def test_dense_wide_fits(vcov, p_k, monkeypatch):
+def test_dense_wide_fits(vcov, p_k, knob):
     """Two FEs at p = 15 and 21: the dense passes in 16-column groups (the row layouts' LDS tables
     do not fit), the column-group group sums and the Gram from the group tables (raw MFMA pass +
     table terms) against the oracle and the general sweeps (LFE_DENSE=0), bit-identical repeats."""
@@ -245,14 +245,14 @@ def test_dense_wide_fits(vcov, p_k, monkeypatch):
     again = _fit(data, xs, vcov)
     np.testing.assert_array_equal(dense[0], again[0])
     np.testing.assert_array_equal(dense[1], again[1])
-    monkeypatch.setenv("LFE_DENSE", "0")
+    knob.setenv("LFE_DENSE", "0")
     rows = _fit(data, xs, vcov)
     _check(rows, o)
     np.testing.assert_allclose(dense[0], rows[0], rtol=1e-11, atol=0)
     np.testing.assert_allclose(dense[1], rows[1], rtol=1e-11, atol=0)
 
 
-def test_two_fe_column_group_sums_form_their_own_raw_gram(monkeypatch):
+def test_two_fe_column_group_sums_form_their_own_raw_gram(knob):
     """a two-FE fit whose secondary table does not fit LDS (p = 14, G_Q = 2,000)
     takes the column-group sums, which form no raw Gram tile; the Gram must not reuse a tile left
     by an earlier fit on the same Engine (here a G_Q = 600 fit, whose sums do write one).  Both
@@ -277,7 +277,7 @@ def test_two_fe_column_group_sums_form_their_own_raw_gram(monkeypatch):
         a = fit(first, eng)
         b = fit(wide, eng)
         b2 = fit(wide, eng)
-        monkeypatch.setenv("LFE_SUMS_CG", "0")
+        knob.setenv("LFE_SUMS_CG", "0")
         b_flat = fit(wide, eng)
     _check(a, o_first)
     _check(b, o_wide)

@@ -66,7 +66,7 @@ def _dense_cells(data, xs, fes):
 
 
 @pytest.mark.parametrize("vcov", ["HC1", "iid"])
-def test_pair_tables_match_oracle_and_row_sweeps(vcov, monkeypatch):
+def test_pair_tables_match_oracle_and_row_sweeps(vcov, knob):
     from leanfe_amd import synth
 
     k = 5
@@ -74,9 +74,9 @@ def test_pair_tables_match_oracle_and_row_sweeps(vcov, monkeypatch):
     fes = ["fe1", "fe2", "fe3"]
     data = synth.panel(1_500_000, k, [3_000, 800, 200], seed=303)
     o = _oracle(data, xs, fes, vcov)
-    monkeypatch.setenv("LFE_DENSE", "0")
+    knob.setenv("LFE_DENSE", "0")
     rows = _fit(data, xs, fes, vcov)
-    monkeypatch.delenv("LFE_DENSE")
+    knob.delenv("LFE_DENSE")
     dense = _fit(data, xs, fes, vcov)
     _check(rows, o)
     _check(dense, o)
@@ -87,7 +87,7 @@ def test_pair_tables_match_oracle_and_row_sweeps(vcov, monkeypatch):
     np.testing.assert_array_equal(dense[1], again[1])
 
 
-def test_pair_tables_wide_four_fes_singletons_ragged(monkeypatch):
+def test_pair_tables_wide_four_fes_singletons_ragged(knob):
     """k = 20 (p = 21: two 16-column groups per table), four FEs with level counts off every 64 /
     512 boundary, 30 singleton levels dropped before the tables are built, one-way clustered SEs."""
     from leanfe_amd import synth
@@ -99,11 +99,11 @@ def test_pair_tables_wide_four_fes_singletons_ragged(monkeypatch):
     fe1 = np.array(data["fe1"], copy=True)
     fe1[:30] = np.arange(30) + 2_777
     data = dict(data, fe1=fe1)
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     _check(_fit(data, xs, fes, "cluster", ["fe3"]), _oracle(data, xs, fes, "cluster", ["fe3"]))
 
 
-def test_pair_tables_heavy_cells(monkeypatch):
+def test_pair_tables_heavy_cells(knob):
     """Cells with 128-400 rows (flagged 16 x 64 blocks, their u16 counts summed in f64) and one
     with ~40K rows (its 64-level chunk counted again on 16-bit counters), in every orientation."""
     rng = np.random.default_rng(21)
@@ -123,10 +123,10 @@ def test_pair_tables_heavy_cells(monkeypatch):
     xs = ["x1", "x2", "x3"]
     fes = ["fe1", "fe2", "fe3"]
     o = _oracle(data, xs, fes)
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     dense = _fit(data, xs, fes)
     _check(dense, o)
-    monkeypatch.setenv("LFE_DENSE", "0")
+    knob.setenv("LFE_DENSE", "0")
     rows = _fit(data, xs, fes)
     np.testing.assert_allclose(dense[0], rows[0], rtol=1e-12, atol=0)
 
@@ -145,7 +145,7 @@ def test_pair_tables_taken_where_expected(monkeypatch):
 
 
 @pytest.mark.parametrize("vcov", ["iid", "HC1"])
-def test_tables_gram_matches_design_pass(vcov, monkeypatch):
+def test_tables_gram_matches_design_pass(vcov, knob):
     from leanfe_amd import synth
 
     k = 14
@@ -154,7 +154,7 @@ def test_tables_gram_matches_design_pass(vcov, monkeypatch):
     data = synth.panel(800_000, k, [2_000, 400, 100], seed=41)
     o = _oracle(data, xs, fes, vcov)
     tab = _fit(data, xs, fes, vcov)
-    monkeypatch.setenv("LFE_TAB3", "0")
+    knob.setenv("LFE_TAB3", "0")
     design = _fit(data, xs, fes, vcov)
     _check(tab, o)
     _check(design, o)

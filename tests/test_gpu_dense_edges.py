@@ -117,7 +117,7 @@ def _demeaned_columns_match(data, cols_names, fes, levels):
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_two_fe_digits_at_numeric_edges(case, monkeypatch):
+def test_two_fe_digits_at_numeric_edges(case, knob):
     from leanfe_amd._lib import Engine
     from oracle import altproj
 
@@ -126,15 +126,15 @@ def test_two_fe_digits_at_numeric_edges(case, monkeypatch):
     fes = ["fe1", "fe2"]
     data = _panel(case, 900_000, levels, k, seed=606)
     o = altproj.fit(data, "y", xs, fes, vcov="HC1")
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     with Engine(0) as eng:
         i8 = _fit(data, xs, fes, eng)
         again = _fit(data, xs, fes, eng)
-        monkeypatch.setenv("LFE_DN8", "0")
+        knob.setenv("LFE_DN8", "0")
         f64 = _fit(data, xs, fes, eng)
         assert f64["cells"] > 0 and f64["bytes"] == 2  # the f64 passes have no guard
-        monkeypatch.delenv("LFE_DN8")
-        monkeypatch.setenv("LFE_DENSE", "0")
+        knob.delenv("LFE_DN8")
+        knob.setenv("LFE_DENSE", "0")
         rows = _fit(data, xs, fes, eng)
     _check(i8, o)
     _check(f64, o)
@@ -146,12 +146,12 @@ def test_two_fe_digits_at_numeric_edges(case, monkeypatch):
         assert i8["cells"] > 0 and i8["bytes"] == 1  # the exact i8 passes ran
         _close(i8, f64, 1e-12)
     if case == "nan_x":
-        monkeypatch.setenv("LFE_DENSE", "1")
+        knob.setenv("LFE_DENSE", "1")
         _demeaned_columns_match(data, ["y"] + xs, fes, levels)
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_pair_table_digits_at_numeric_edges(case, monkeypatch):
+def test_pair_table_digits_at_numeric_edges(case, knob):
     from leanfe_amd._lib import Engine
     from oracle import altproj
 
@@ -160,11 +160,11 @@ def test_pair_table_digits_at_numeric_edges(case, monkeypatch):
     fes = ["fe1", "fe2", "fe3"]
     data = _panel(case, 1_200_000, levels, k, seed=707)
     o = altproj.fit(data, "y", xs, fes, vcov="HC1")
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     with Engine(0) as eng:
         dense = _fit(data, xs, fes, eng)
         again = _fit(data, xs, fes, eng)
-        monkeypatch.setenv("LFE_DENSE", "0")
+        knob.setenv("LFE_DENSE", "0")
         rows = _fit(data, xs, fes, eng)
         assert rows["cells"] == 0
     _check(dense, o)
@@ -186,11 +186,11 @@ def test_pair_table_digits_at_numeric_edges(case, monkeypatch):
     else:
         _close(dense, rows, 1e-12)
     if case == "nan_x":
-        monkeypatch.setenv("LFE_DENSE", "1")
+        knob.setenv("LFE_DENSE", "1")
         _demeaned_columns_match(data, ["y"] + xs, fes, levels)
 
 
-def test_tiny_effects_digitize_exactly(monkeypatch):
+def test_tiny_effects_digitize_exactly(knob):
     """A column whose effects all lie near 1e-300 (below 2^-969, where the digit scale 2^(54 - e)
     alone overflows to inf and 0 * inf made NaN digits): the scale goes in two exact
     power-of-two factors, so the tiny column demeans as the oracle does (compared after scaling
@@ -203,7 +203,7 @@ def test_tiny_effects_digitize_exactly(monkeypatch):
     data = _panel("none", 900_000, levels, 2, seed=808)
     cols = [np.asarray(data["y"]) * 1e-300, np.asarray(data["x1"]), np.asarray(data["x2"]) * 1e-310]
     codes = [np.ascontiguousarray(data[f], dtype=np.int32) for f in fes]
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     with Engine(0) as eng:
         eng.load(cols, codes, levels)
         _, _, card = eng.drop_singletons()

@@ -57,7 +57,7 @@ def test_same_panel_twice_is_bit_identical(n, L):
 
 
 @pytest.mark.parametrize("units", ["256", "4096", "100000"])
-def test_sweep_work_units_do_not_change_bits(units, monkeypatch):
+def test_sweep_work_units_do_not_change_bits(units, knob):
     """K1 (lfe_iter.hip k_tp) sums every segment in batches aligned to absolute 16-group
     boundaries, so its results do not depend on how the segments are split into work units (the
     unit size follows the shard size and the CU count)."""
@@ -68,7 +68,7 @@ def test_sweep_work_units_do_not_change_bits(units, monkeypatch):
     with Engine(0) as eng:
         eng.synth_load(n, k, L, synth.betas(k), seed=91)
         ref = _solve(eng)
-        monkeypatch.setenv("LFE_K1_UNIT", units)
+        knob.setenv("LFE_K1_UNIT", units)
         other = _solve(eng)
     _same(ref, other)
 

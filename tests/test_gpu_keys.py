@@ -56,7 +56,7 @@ def _host_distinct(cols, codes):
 
 
 @pytest.mark.parametrize("hash_bits", [64, 10])
-def test_count_distinct_rows_exact(eng, hash_bits):
+def test_count_distinct_rows_exact(eng, hash_bits, knob):
     rng = np.random.default_rng(9)
     n = 400_000
     y = rng.standard_normal(n)                     # y is not part of the key
@@ -66,11 +66,11 @@ def test_count_distinct_rows_exact(eng, hash_bits):
     fe1 = rng.integers(0, 40, n).astype(np.int32)
     fe2 = rng.integers(0, 7, n).astype(np.int32)
     eng.load([y, x1, x2, x3], [fe1, fe2], [40, 7])
-    os.environ["LFE_ROW_HASH_BITS"] = str(hash_bits)  # 10 bits: thousands of collisions -> exact recount
+    knob.setenv("LFE_ROW_HASH_BITS", str(hash_bits))  # 10 bits: thousands of collisions -> exact recount
     try:
         got = eng.count_distinct_rows()
     finally:
-        os.environ.pop("LFE_ROW_HASH_BITS", None)
+        knob.delenv("LFE_ROW_HASH_BITS")
     assert got == _host_distinct([x1, x2, x3], [fe1, fe2])
 
 
@@ -152,23 +152,23 @@ def _words(rng, n, n_distinct):
 
 
 @pytest.mark.parametrize("hash_bits", [64, 8])
-def test_factorize_strings_exact_grouping(eng, hash_bits):
+def test_factorize_strings_exact_grouping(eng, hash_bits, knob):
     """String FE ids (_cats_to_int's String -> Categorical cast, polars_impl.py:118-139) are
     grouped on the device exactly as np.unique groups them; 8-bit hashes force thousands of
     collisions through the exact split (k_str_exact)."""
     from leanfe_amd import frame
     rng = np.random.default_rng(31)
     v = _words(rng, 200_000 if hash_bits == 64 else 30_000, 3000)
-    os.environ["LFE_STR_HASH_BITS"] = str(hash_bits)
+    knob.setenv("LFE_STR_HASH_BITS", str(hash_bits))
     try:
         codes, G = frame.factorize(v, device=eng)
     finally:
-        os.environ.pop("LFE_STR_HASH_BITS", None)
+        knob.delenv("LFE_STR_HASH_BITS")
     uniq, inv = np.unique(v.astype(str), return_inverse=True)
     _same_partition(codes, G, inv.ravel(), uniq.size)
 
 
-def test_factorize_strings_frequent_value_beside_collisions(eng):
+def test_factorize_strings_frequent_value_beside_collisions(eng, knob):
     """A very frequent string whose hash run holds only that string is not walked by the exact
     split, even when other runs collide (20-bit hashes over 20K strings: ~200 colliding pairs);
     the grouping is exact (k_str_exact walked every run head serially)."""
@@ -179,13 +179,13 @@ def test_factorize_strings_frequent_value_beside_collisions(eng):
     pool = _words(rng, 20_000, 20_000)
     v = np.concatenate([np.array(["the frequent value"] * 1_000_000, dtype=object), pool[rng.integers(0, pool.size, 500_000)]])
     v = v[rng.permutation(v.size)]
-    os.environ["LFE_STR_HASH_BITS"] = "20"
+    knob.setenv("LFE_STR_HASH_BITS", "20")
     try:
         t0 = time.perf_counter()
         codes, G = frame.factorize(v, device=eng)
         dt = time.perf_counter() - t0
     finally:
-        os.environ.pop("LFE_STR_HASH_BITS", None)
+        knob.delenv("LFE_STR_HASH_BITS")
     uniq, inv = np.unique(v.astype(str), return_inverse=True)
     _same_partition(codes, G, inv.ravel(), uniq.size)
     assert dt < 10.0, dt

@@ -100,13 +100,13 @@ def _run_group(world, n, k, levels, vcov, cluster_fe, seed):
     (3, 250_001, 5, (30000, 120), "cluster", (0, 1), True),    # 3 ranks; fe1 x fe2: ~1.4 rows per cluster
     (3, 250_001, 5, (30000, 120), "cluster", (0, 1), False),   # same through the key-indexed table
 ])
-def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe, owner, monkeypatch):
+def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe, owner, knob):
     from oracle import altproj
 
     if owner:
-        monkeypatch.setenv("LFE_CL_OWNER_MIN_SPAN", "0")
+        knob.setenv("LFE_CL_OWNER_MIN_SPAN", "0")
     else:
-        monkeypatch.setenv("LFE_CL_OWNER_MIN_SPAN", str(1 << 40))
+        knob.setenv("LFE_CL_OWNER_MIN_SPAN", str(1 << 40))
     seed = 11
     out = _run_group(world, n, k, list(levels), vcov, cluster_fe, seed)
     full = synth.panel(n, k, list(levels), seed=seed)
@@ -135,11 +135,11 @@ def test_emulated_ranks_match_oracle(world, n, k, levels, vcov, cluster_fe, owne
     (2, 200_000, 3, (3000, 200, 9), 1),          # F = 3 sweeps + key-indexed score table
     (3, 250_001, 5, (30000, 120), (0, 1)),       # two-way CGM through the key-indexed table
 ])
-def test_emulated_key_indexed_clusters_repeat_bit_identically(world, n, k, levels, cluster_fe, monkeypatch):
+def test_emulated_key_indexed_clusters_repeat_bit_identically(world, n, k, levels, cluster_fe, knob):
     """The multi-rank key-indexed cluster table is filled from each rank's sorted cluster sums
     (one store per cluster, k_cl_dense_put) instead of per-row f64 atomics: two solves give the
     same bits on every rank."""
-    monkeypatch.setenv("LFE_CL_OWNER_MIN_SPAN", str(1 << 40))
+    knob.setenv("LFE_CL_OWNER_MIN_SPAN", str(1 << 40))
     a = _run_group(world, n, k, list(levels), "cluster", cluster_fe, 17)
     b = _run_group(world, n, k, list(levels), "cluster", cluster_fe, 17)
     for r in range(world):
@@ -576,13 +576,13 @@ def test_owner_shard_solves_in_its_share_of_time(rank):
     (4, 600_000, 14, (20_000, 4_000, 1_000), "iid", None),  # MEGA-shaped, p = 15
     (3, 500_000, 4, (3_000, 500, 120), "cluster", [1, 2]),
 ])
-def test_emulated_owner_sharded_pair_tables(world, n, k, levels, vcov, cl, monkeypatch):
+def test_emulated_owner_sharded_pair_tables(world, n, k, levels, vcov, cl, knob):
     """The pair-table sweeps (lfe_dense3.hip, forced with LFE_DENSE=1) on owner shards: each rank's
     tables count its own rows, the primary FE's cross term stays local and the others' are
     all-reduced; every rank equals the oracle and repeats bit for bit."""
     from oracle import altproj
 
-    monkeypatch.setenv("LFE_DENSE", "1")
+    knob.setenv("LFE_DENSE", "1")
     seed = 19
     out = _run_owned_cl(world, n, k, list(levels), vcov, cl, seed)
     full = dict(synth.panel(n, k, list(levels), seed=seed))

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from golden_util import load, names, ncl
-from leanfe_amd import synth
+from leanfe_amd import hip_impl, synth
 from oracle import altproj, yoco
 
 pytestmark = pytest.mark.gpu
@@ -285,7 +285,7 @@ def test_yoco_nearly_nested_fes_converge_to_the_exact_lsdv():
     assert r.iterations < 100_000
 
 
-def test_yoco_auto_selects_compress_and_hash_collisions_are_exact(monkeypatch):
+def test_yoco_auto_selects_compress_and_hash_collisions_are_exact(knob):
     """strategy='auto' picks 'compress' for low-cardinality FEs with discrete x
     (compress.py:96-184), and an 8-bit row hash (forced collisions) still groups exactly."""
     from leanfe_amd import leanfe_hip
@@ -295,7 +295,7 @@ def test_yoco_auto_selects_compress_and_hash_collisions_are_exact(monkeypatch):
     r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="auto", vcov="HC1", quiet=True)
     assert r.n_compressed == o["n_compressed"]
     _assert_yoco(r, o, xs)
-    monkeypatch.setenv("LFE_ROW_HASH_BITS", "8")
+    knob.setenv("LFE_ROW_HASH_BITS", "8")
     d = _yoco_panel(56, 20_000, (30, 10), 2)
     o = yoco.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=["cl1"])
     r = leanfe_hip(d, y_col="y", x_cols=xs, fe_cols=fes, strategy="compress", vcov="cluster", cluster_cols=["cl1"],
@@ -341,7 +341,7 @@ def test_parquet_path_streams_and_matches_in_memory(tmp_path, monkeypatch, vcov,
     d["z1"] = d["x1"] + rng.normal(0, 1, d["y"].size)
     path = str(tmp_path / "panel.parquet")
     pq.write_table(pa.table(d), path, row_group_size=70_000)
-    monkeypatch.setenv("LEANFE_HIP_STREAM_BATCH", "65536")
+    monkeypatch.setitem(hip_impl.KNOBS, "stream_batch", 65536)
     formula = "y ~ x1 + x2 + x3 | fe1 + fe2" + (" | z1 + x2 + x3" if inst else "")
     kw = dict(formula=formula, strategy="alt_proj", vcov=vcov, cluster_cols=["cl"] if vcov == "cluster" else None,
               weights="w" if weights else None, quiet=True)

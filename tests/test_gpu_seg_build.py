@@ -49,10 +49,10 @@ CASES = [
 
 
 @pytest.mark.parametrize("name,n,L,vcov,cl", CASES, ids=[c[0] for c in CASES])
-def test_sorted_build_matches_scatter_and_oracle(monkeypatch, name, n, L, vcov, cl):
+def test_sorted_build_matches_scatter_and_oracle(knob, name, n, L, vcov, cl):
     from oracle import altproj
 
-    monkeypatch.setenv("LFE_DENSE", "0")  # the row sweeps (lfe_seg.hip), not the count tables
+    knob.setenv("LFE_DENSE", "0")  # the row sweeps (lfe_seg.hip), not the count tables
     k = 3
     xs = [f"x{j + 1}" for j in range(k)]
     fes = [f"fe{f + 1}" for f in range(len(L))]

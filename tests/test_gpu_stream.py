@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from leanfe_amd import synth
+from leanfe_amd import hip_impl, synth
 from oracle import altproj
 
 pytestmark = pytest.mark.gpu
@@ -263,7 +263,7 @@ def test_streamed_factor_and_interaction_terms_equal_the_resident_fit(source, tm
 def test_out_of_core_fit_split_into_contexts(case, monkeypatch, tmp_path):
     """VERDICT r4 Missing 1: one context holds < 2^31 rows (int32 row indices), so a longer
     out-of-core fit runs as several contexts on one device joined in an in-process group - the
-    row-shard schedule of several GPUs (hip_impl._out_of_core_split).  LEANFE_HIP_CONTEXT_ROWS
+    row-shard schedule of several GPUs (hip_impl._out_of_core_split).  hip_impl.KNOBS["context_rows"]
     lowers the per-context cap so that 700K rows take 3 contexts; the fit equals the oracle and the
     one-context streamed fit (equal integers, beta / SE to rounding)."""
     import pyarrow as pa
@@ -292,7 +292,7 @@ def test_out_of_core_fit_split_into_contexts(case, monkeypatch, tmp_path):
         kw = dict(formula="y ~ x1 + x2 + x3 + i(year) | fe1 + fe2", strategy="alt_proj", vcov="HC1", quiet=True,
                   out_of_core=True, chunk_rows=90_000)
     one = leanfe_hip(data, **kw)
-    monkeypatch.setenv("LEANFE_HIP_CONTEXT_ROWS", "250000")
+    monkeypatch.setitem(hip_impl.KNOBS, "context_rows", 250_000)
     split = leanfe_hip(data, **kw)
     names = list(one.coefs)
     assert split.iterations == one.iterations and split.n_obs == one.n_obs and split.df_resid == one.df_resid

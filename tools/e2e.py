@@ -18,7 +18,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from leanfe_amd import leanfe_hip, synth  # noqa: E402
+from leanfe_amd import hip_impl, leanfe_hip, synth  # noqa: E402
 
 
 def main():
@@ -58,7 +58,7 @@ def main():
         t_write = time.perf_counter() - t0
         del data
         for mode in ("1", "0"):  # streamed (lfe_load_rows per batch) / read whole, then lfe_load
-            os.environ["LEANFE_HIP_STREAM"] = mode
+            hip_impl.KNOBS["stream"] = mode == "1"
             walls = []
             for _ in range(a.repeat):
                 t0 = time.perf_counter()

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Tuning sweep on one box: bench.py once per value of an engine tuning variable.
+# Tuning sweep on one box: bench.py once per value of an engine tuning knob (bench --knob).
 #   VAR=SOME_ENV VALUES="1 2 4" KEYS="tq,tp" bash tools/tune_env.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for v in ${VALUES}; do
-  env ${VAR}=${v} timeout -k 10 120 python bench.py --no-cpu --steps ${STEPS:-10} --warmup 5 > gpurun_out/tune_${v}.log 2>&1
+  timeout -k 10 120 python bench.py --no-cpu --steps ${STEPS:-10} --warmup 5 --knob ${VAR}=${v} > gpurun_out/tune_${v}.log 2>&1
   rc=$?
   [ $rc -eq 0 ] || { echo "${VAR}=${v} rc=$rc"; tail -3 gpurun_out/tune_${v}.log; exit $rc; }
   python - "$v" "${KEYS:-}" <<'PY'
