@@ -550,13 +550,13 @@ int lfe_wide_cluster_meats(lfe_ctx* c, const double* D, int64_t ldD, int c0, int
     if (rc != LFE_OK) break;
     int32_t* cnt = c->clP;
     int32_t* cm = c->clP + G;
-    hip_ok(hipMemsetAsync(cnt, 0, sizeof(int32_t) * ((size_t)G + 4), c->stream), "hipMemsetAsync(counts)");
+    hip_ok(hipMemsetAsync(cnt, 0, sizeof(int32_t) * ((size_t)G + 4), c->stream), "memset of the counts");
     // columns in passes of <= 64 (one quanta table each); a wider table is assembled in `full`
     for (int cb = 0; cb < k && rc == LFE_OK; cb += kWcCols) {
       const int kg = std::min(kWcCols, k - cb);
-      hip_ok(hipMemsetAsync(W.fixst, 0, sizeof(double) * kColStatHead, c->stream), "hipMemsetAsync(fixst)");
-      hip_ok(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream), "hipMemsetAsync(clS)");
-      hip_ok(hipMemsetAsync(W.srec, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream), "hipMemsetAsync(srec)");
+      hip_ok(hipMemsetAsync(W.fixst, 0, sizeof(double) * kColStatHead, c->stream), "memset of fixst");
+      hip_ok(hipMemsetAsync(c->clS, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream), "memset of clS");
+      hip_ok(hipMemsetAsync(W.srec, 0, sizeof(double) * (size_t)std::max(G, 1) * kg, c->stream), "memset of srec");
       if (rc != LFE_OK) break;
       WideScoreArgs a{D, ldD, n, c0 + cb, kg, r, c->w, cid};
       {
