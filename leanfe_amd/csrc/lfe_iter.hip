@@ -1142,8 +1142,11 @@ __global__ __launch_bounds__(256) void k_tq_reduce_fin(const double* __restrict_
                                                        double* __restrict__ T, const double* __restrict__ S,
                                                        const int32_t* __restrict__ cnt, int p,
                                                        const double* __restrict__ cur, double* __restrict__ out,
-                                                       unsigned long long* __restrict__ check) {
+                                                       unsigned long long* __restrict__ check,
+                                                       const double* __restrict__ flag_in, double* __restrict__ flag_out) {
   __shared__ double part[kTqRedS][kTqRedE];
+  // the digits' guard flag beside the stop test, for the same read-back (no separate copy)
+  if (flag_in && blockIdx.x == 0 && threadIdx.x == 0) *flag_out = *flag_in;
   const int ei = threadIdx.x % kTqRedE, sl = threadIdx.x / kTqRedE;
   const int64_t e = (int64_t)blockIdx.x * kTqRedE + ei;
   part[sl][ei] = tq_red_slice(runs, nb, m, e, sl);
@@ -1157,7 +1160,9 @@ __global__ __launch_bounds__(256) void k_tq_reduce_fin(const double* __restrict_
 // (= |mean_g(y~)| after the sweep); NaN propagates (a NaN panel never converges).
 __global__ void k_fin_check(const double* __restrict__ S, const double* __restrict__ T,
                             const int32_t* __restrict__ cnt, int32_t G, int p, const double* __restrict__ cur,
-                            double* __restrict__ out, unsigned long long* __restrict__ check) {
+                            double* __restrict__ out, unsigned long long* __restrict__ check,
+                            const double* __restrict__ flag_in = nullptr, double* __restrict__ flag_out = nullptr) {
+  if (flag_in && blockIdx.x == 0 && threadIdx.x == 0) *flag_out = *flag_in;
   double m = 0.0;
   const int64_t total = (int64_t)G * p;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -1178,11 +1183,13 @@ __global__ void k_fin_check(const double* __restrict__ S, const double* __restri
   if ((threadIdx.x & 63) == 0) atomicMax(check, (unsigned long long)__double_as_longlong(fabs(m)));
 }
 
-static int fin_check(lfe_ctx* c, int f, const double* T, const double* cur, double* out, bool check) {
+static int fin_check(lfe_ctx* c, int f, const double* T, const double* cur, double* out, bool check,
+                     const double* flag_in = nullptr) {
   auto& fe = c->fe[f];
   ProfScope _ps(c, K_FINALIZE);
   hipLaunchKernelGGL(k_fin_check, dim3(grid_for((int64_t)fe.G * c->p)), dim3(kBlock), 0, c->stream, fe.S, T, fe.cnt,
-                     fe.G, c->p, cur, out, check ? reinterpret_cast<unsigned long long*>(c->dred) : nullptr);
+                     fe.G, c->p, cur, out, check ? reinterpret_cast<unsigned long long*>(c->dred) : nullptr,
+                     check ? flag_in : nullptr, c->dred + 1);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
 }
@@ -1374,7 +1381,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
         ProfScope _ps(c, K_TQ_REDUCE);
         hipLaunchKernelGGL(k_tq_reduce_fin, dim3(tq_grid), dim3(kTqRedE * kTqRedS), 0, c->stream, c->tq_runs,
                            c->nbe, m, fq.T, fq.S, fq.cnt, p, fq.alpha, c->alpha_spare,
-                           check ? reinterpret_cast<unsigned long long*>(c->dred) : nullptr);
+                           check ? reinterpret_cast<unsigned long long*>(c->dred) : nullptr,
+                           check && guard ? c->rflag : nullptr, c->dred + 1);
       }
       LFE_HIP(hipGetLastError());
       if (!check && it == max_iter) break;
@@ -1390,15 +1398,14 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       else
         LFE_TRY(allreduce_sum_f64(c, fq.T, (size_t)fq.G * p));
       if (!check && it == max_iter) break;
-      LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check));
+      LFE_TRY(fin_check(c, Q, fq.T, fq.alpha, c->alpha_spare, check, guard ? c->rflag : nullptr));
     }
     if (check) {
       // the check's read-back first, then - when this check is likely the last (the first one,
       // or the previous was within 100x of tol: the check falls ~100x per sweep) - the Gram of
       // the tables and its Cholesky, so the GPU works through the host's decision and the
       // return to the caller; lfe_gram_resid then starts at the residual pass
-      if (guard)
-        LFE_HIP(hipMemcpyAsync(c->dred + 1, c->rflag, sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+      // (the guard's flag was copied beside the check by the reduce / projection kernel)
       LFE_TRY(d2h_async(c, c->dred, sizeof(double) * (guard ? 2 : 1)));
       int spec = 0;
       c->tq_final = true;

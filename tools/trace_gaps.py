@@ -17,8 +17,9 @@ def main():
     rows.sort()
     # the bench's steps start with k_part_hist; take the last one
     starts = [i for i, r in enumerate(rows) if "k_part_hist" in r[2]]
-    i0 = starts[-1]
-    seg = rows[i0:]
+    # a whole step from one k_part_hist to the next (the host's work between steps included), else
+    # the last step to the end of the trace
+    seg = rows[starts[-2]:starts[-1] + 1] if len(starts) >= 2 else rows[starts[-1]:]
     t0 = seg[0][0]
     prev_end = t0
     busy = gap = 0
