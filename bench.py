@@ -191,49 +191,30 @@ def device_sync(eng):
 
 
 def solve_step(eng, vcov: str, n_cl: int = 0) -> dict:
-    """One regression on the loaded shard, as ``leanfe_hip`` runs it (hip_impl.py:230-250, the same
+    """One regression on the loaded shard, as ``leanfe_hip`` runs it (hip_impl.py, the same
     fallbacks: a second residual pass when r'r cancels in the Gram or the device Cholesky's beta
-    drifted from the host solve)."""
+    drifted from the host solve): one lfe_fit call - drop, projections, Gram + device solve +
+    residual pass, host solve and IID / HC1 SEs - then, clustered, the meats and the CGM sandwich."""
     from leanfe_amd import inference
-    from leanfe_amd.hip_impl import _beta_agrees
 
-    n_obs, dims, card = eng.drop_singletons()
-    order = sorted(range(len(card)), key=lambda i: card[i])  # polars_impl.py:485
-    iterations, _ = eng.demean(order, 1e-6, 50, check_from=3)
     v = vcov.lower()
-    gram_only = v == "iid"  # IID without weights: residual statistics from the Gram
-    fused = None if gram_only else eng.gram_resid(hc1=v == "hc1", keep_scores=v == "cluster")
-    G = fused[0] if fused is not None else eng.gram()
-    XtX, Xty = inference.split_gram(G)
-    beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # host, polars_impl.py:212-226
-    k = XtX.shape[0] - 1
-    df_resid = n_obs - (k + 1) - (sum(dims) - len(dims))
-    Vb = XtX_inv[1:, 1:]
-    dbeta = 0.0
-    stats, meat = (inference.stats_from_gram(G, beta_full), None) if gram_only else (None, None)
-    if stats is not None:
-        pass
-    elif fused is not None and _beta_agrees(fused[1], beta_full):
-        stats, meat = fused[2], fused[3]
-        # the residual pass used the device Cholesky's beta: record its distance to the host solve
-        dbeta = float(abs(fused[1] - beta_full).max() / max(abs(beta_full).max(), 1e-300))
-    else:
-        stats, meat = eng.resid(beta_full, hc1=v == "hc1", keep_scores=v == "cluster")
+    r = eng.fit(v)
+    n_obs, df_resid = r["n_obs"], r["df_resid"]
     ncl = None
-    if v == "iid":
-        se = inference.se_iid(Vb, stats[0], df_resid)
-    elif v == "hc1":
-        se = inference.se_hc1(Vb, meat, n_obs, df_resid)
-    elif n_cl == 1:
-        meats, Gs = eng.cluster_meat()
-        se, ncl = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, True)
-    else:
-        subsets = inference.cluster_subsets(n_cl)
-        meats, Gs = eng.cluster_meat_subsets(subsets)  # intersections formed on the device
-        se, ncl = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets, n_obs, df_resid,
-                                                True)
-    return dict(n_obs=n_obs, iterations=iterations, beta=beta_full[1:], se=se, df_resid=df_resid,
-                fe_dims=list(dims), n_clusters=ncl, rss=float(stats[1]), beta_dev_vs_host=dbeta)
+    se = r["se"]
+    if v == "cluster":
+        Vb = r["xtx_inv"][1:, 1:]
+        if n_cl == 1:
+            meats, Gs = eng.cluster_meat()
+            se, ncl = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), n_obs, df_resid, True)
+        else:
+            subsets = inference.cluster_subsets(n_cl)
+            meats, Gs = eng.cluster_meat_subsets(subsets)  # intersections formed on the device
+            se, ncl = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets, n_obs, df_resid,
+                                                    True)
+    return dict(n_obs=n_obs, iterations=r["iterations"], beta=r["beta_full"][1:], se=se, df_resid=df_resid,
+                fe_dims=list(r["fe_dims"]), n_clusters=ncl, rss=float(r["stats"][1]),
+                beta_dev_vs_host=r["beta_dev_vs_host"])
 
 
 def load_shard(eng, a, rank: int, world: int, shard: str) -> dict:

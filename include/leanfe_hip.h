@@ -188,6 +188,26 @@ int lfe_resid_iv(lfe_ctx* ctx, const double* coef, double* stats_out, double* me
 int lfe_gram_resid(lfe_ctx* ctx, double* gram_out, double* beta_full_out, double* stats_out, double* hc1_meat,
                    int keep_scores);
 
+/* One whole regression on the loaded shard in one call (no return to the caller between the
+ * steps): [flags & LFE_FIT_DROP: lfe_drop_singletons], lfe_demean with the FEs ordered by
+ * pre-filter cardinality (polars_impl.py:485), the Gram with the fused device solve + residual
+ * pass (lfe_gram_resid; lfe_gram alone for IID), the host solve (:211-220: Cholesky, LU when X'X
+ * is not positive definite) and the SEs: IID (std_errors.py:196-210) from the Gram's residual
+ * statistics unless r'r cancels there, HC1 (:275-282).  vcov LFE_FIT_SCORES keeps the score rows
+ * for lfe_cluster_meat*: se_out is then 0 and the caller forms the CGM sandwich.  Unweighted,
+ * resident, no instruments (every column after y is a regressor): else LFE_EINVAL.
+ * Outputs: ints_out[4 + 2F] = {n_obs, iterations, df_resid, fused pass used, fe_dims[F],
+ * fe_card[F]}; gram_out (p+1)^2 as lfe_gram; beta_full_out[p]; xtx_inv_out p x p; stats_out[4]
+ * as lfe_resid; meat_out k x k (HC1, k = p-1); se_out[k]; diag_out[2] (may be NULL) = {last stop
+ * test, |beta_device - beta_host| / max|beta_host|}. */
+#define LFE_FIT_IID 0
+#define LFE_FIT_HC1 1
+#define LFE_FIT_SCORES 2
+#define LFE_FIT_DROP 1
+int lfe_fit(lfe_ctx* ctx, int flags, double tol, int max_iter, int check_from, int vcov, int64_t* ints_out,
+            double* gram_out, double* beta_full_out, double* xtx_inv_out, double* stats_out, double* meat_out,
+            double* se_out, double* diag_out);
+
 /* For each loaded cluster array j: S_c = sum_{i in c} u_i r_i (w_i);
  * meats_out[j] = S'S (k x k), G_out[j] = number of clusters present among the
  * kept rows (std_errors.py:317-336, compress.py:929-942 — the W_C'(X.e) SpMM).

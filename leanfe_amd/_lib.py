@@ -53,6 +53,8 @@ SIGNATURES = {
     "lfe_resid": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int]),
     "lfe_resid_iv": (C.c_int, [_vp, _dp, _dp, _dp, C.c_int]),
     "lfe_gram_resid": (C.c_int, [_vp, _dp, _dp, _dp, _dp, C.c_int]),
+    "lfe_fit": (C.c_int, [_vp, C.c_int, C.c_double, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                          _vp]),
     "lfe_cluster_meat": (C.c_int, [_vp, _dp, _i64p]),
     "lfe_cluster_meat_subsets": (C.c_int, [_vp, C.c_int, _vp, _dp, _i64p]),
     "lfe_factorize_ids": (C.c_int, [_vp, C.c_int64, _vp, _vp, C.POINTER(C.c_int32)]),
@@ -409,6 +411,32 @@ class Engine:
         if keep_scores:
             self._score_k = k
         return G, b, stats, (meat[:k, :k] if hc1 else None)
+
+    FIT_VCOV = {"iid": 0, "hc1": 1, "cluster": 2}
+
+    def fit(self, vcov: str, tol: float = 1e-6, max_iter: int = 50, check_from: int = 3, drop: bool = True) -> dict:
+        """One whole regression in one C call (lfe_fit): [singleton drop], projections with the FEs
+        ordered by cardinality, Gram + device solve + residual pass, host solve and the IID / HC1
+        SEs; 'cluster' keeps the score rows for cluster_meat* (se is then None).  Unweighted,
+        resident, no instruments."""
+        v = self.FIT_VCOV[vcov.lower()]
+        F, p = self.F, self.p
+        k, D = p - 1, p + 1
+        ints = np.zeros(4 + 2 * F, dtype=np.int64)
+        buf = np.zeros(D * D + p + p * p + 4 + k * k + k + 2)
+        o = np.cumsum([0, D * D, p, p * p, 4, k * k, k])
+        b = buf.ctypes.data
+        _check(self._lib.lfe_fit(self._h, 1 if drop else 0, float(tol), int(max_iter), int(check_from), v,
+                                 ints.ctypes.data, b, b + 8 * int(o[1]), b + 8 * int(o[2]), b + 8 * int(o[3]),
+                                 b + 8 * int(o[4]), b + 8 * int(o[5]), b + 8 * int(o[6])))
+        if v == 2:
+            self._score_k = k
+        return dict(n_obs=int(ints[0]), iterations=int(ints[1]), df_resid=int(ints[2]), fused=bool(ints[3]),
+                    fe_dims=tuple(int(x) for x in ints[4:4 + F]), fe_card=tuple(int(x) for x in ints[4 + F:]),
+                    gram=buf[:o[1]].reshape(D, D), beta_full=buf[o[1]:o[2]], xtx_inv=buf[o[2]:o[3]].reshape(p, p),
+                    stats=buf[o[3]:o[4]], meat=buf[o[4]:o[5]].reshape(k, k) if v == 1 else None,
+                    se=buf[o[5]:o[6]] if v != 2 else None, last_check=float(buf[o[6]]),
+                    beta_dev_vs_host=float(buf[o[6] + 1]))
 
     def cluster_meat(self) -> tuple[np.ndarray, np.ndarray]:
         k = getattr(self, "_score_k", self.p - 1)

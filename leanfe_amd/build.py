@@ -30,7 +30,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["lfe_capi.hip", "lfe_prep.hip", "lfe_sweep.hip", "lfe_fast.hip", "lfe_iter.hip", "lfe_dense.hip", "lfe_dense3.hip", "lfe_seg.hip", "lfe_gram.hip", "lfe_cluster.hip", "lfe_keys.hip", "lfe_compress.hip", "lfe_synth.hip", "lfe_shard.hip", "lfe_stream.hip", "lfe_wide.hip"]
+SOURCES = ["lfe_capi.hip", "lfe_prep.hip", "lfe_sweep.hip", "lfe_fast.hip", "lfe_iter.hip", "lfe_dense.hip", "lfe_dense3.hip", "lfe_seg.hip", "lfe_gram.hip", "lfe_cluster.hip", "lfe_keys.hip", "lfe_compress.hip", "lfe_synth.hip", "lfe_shard.hip", "lfe_stream.hip", "lfe_wide.hip", "lfe_fit.hip"]
 HEADERS = ["lfe_internal.h", os.path.join("..", "..", "include", "leanfe_hip.h")]
 
 CFLAGS = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",

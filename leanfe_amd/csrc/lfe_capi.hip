@@ -641,11 +641,14 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->hpin_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->side_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->up_ev0, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->up_ev1, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->hpin), kPinSmall, hipHostMallocDefault) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess) {
+      hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&c->gsync), kGsyncSlots * sizeof(unsigned int)) != hipSuccess ||
+      hipMemsetAsync(c->gsync, 0, kGsyncSlots * sizeof(unsigned int), c->stream) != hipSuccess) {
     delete c;
     return fail(LFE_EHIP, "stream/event/buffer creation failed");
   }
@@ -667,6 +670,8 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   free_data(c);
   dfree(c->scratch);
   dfree(c->dred);
+  if (c->gsync) (void)hipFree(c->gsync);
+  c->gsync = nullptr;
   dfree(c->iscratch);
   dfree(c->pcounts);
   dfree(c->psums);
@@ -686,6 +691,7 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   for (auto& e : c->load_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->aux_ev) (void)hipEventDestroy(c->aux_ev);
+  if (c->side_ev) (void)hipEventDestroy(c->side_ev);
   if (c->up_ev0) (void)hipEventDestroy(c->up_ev0);
   if (c->up_ev1) (void)hipEventDestroy(c->up_ev1);
   if (c->up_stream) (void)hipStreamDestroy(c->up_stream);

@@ -1021,8 +1021,21 @@ struct TabArgs {
   int q_on;                // 0: skip the secondary groups (owner-sharded ranks other than 0)
 };
 
+// the final step of the tables Gram (k_tables_final_chol): partials -> tile, guard flag, Cholesky
+struct TabFinal {
+  const double* raw;
+  double* tile;
+  double* flag;
+  double* beta;
+  double* beta_copy;
+  double* ok;
+  unsigned int* done;  // non-null: the last block of k_tables_gram runs the final step itself
+};
+template <int PM, int NTH>
+__device__ void tables_final_body(const double* __restrict__ partial, int nblk, int p, const TabFinal& f);
+
 template <int PM>
-__global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restrict__ partial) {
+__global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restrict__ partial, TabFinal fin) {
   constexpr int NG = PM * (PM + 1) / 2;
   constexpr int NA = NG + PM;
   __shared__ double red[4][NA];
@@ -1073,6 +1086,8 @@ __global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restri
   // entry-major [NA][blocks]: the final kernel's lanes then read consecutive blocks of one entry
   for (int e = threadIdx.x; e < NA; e += blockDim.x)
     partial[(int64_t)e * gridDim.x + blockIdx.x] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+  // one launch for the partials and the final tile + Cholesky: the last block to finish sums them
+  if (fin.done && last_block_done(fin.done)) tables_final_body<PM, 256>(partial, gridDim.x, p, fin);
 }
 
 // out[e] = sum over the row e of an entry-major [rows][nblk] partial table, blocks in order
@@ -1133,6 +1148,10 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, do
   ProfScope _ps(c, K_GRAM_TABLES);
   double* part = c->scratch;
   double* msum = c->scratch + (size_t)nblk * NA;
+  const bool split = [] {  // diagnostic: the Cholesky as its own launch (rocprof A/B)
+    const char* e = knob("LFE_CHOL_SPLIT");
+    return e && e[0] == '1';
+  }();
   auto final_from = [&](auto kfinal) -> int {
     // one block sums the block partials in a fixed order, forms the tile and (beta) solves it.
     // Owner-sharded rows: one workgroup per entry sums the partials first, then the sums over
@@ -1146,28 +1165,27 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, do
       src = msum;
       ns = 1;
     }
-    const bool split = [] {  // diagnostic: the Cholesky as its own launch (rocprof A/B)
-      const char* e = knob("LFE_CHOL_SPLIT");
-      return e && e[0] == '1';
-    }();
     hipLaunchKernelGGL(kfinal, dim3(1), dim3(1024), 0, c->stream, src, ns, c->raw_tile, p, out_dev, flag_dev,
                        split ? nullptr : beta, beta_copy, ok);
     if (split && beta)
       hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, out_dev, p, beta, beta_copy, ok);
     return LFE_OK;
   };
+  // one rank (the usual case): the last block of k_tables_gram forms the tile and solves it
+  const bool fuse = !c->owner_on && !split;
+  const TabFinal fin{c->raw_tile, out_dev, flag_dev, beta, beta_copy, ok, fuse ? c->gsync + GS_TABLES_GRAM : nullptr};
   switch (PM) {
     case 4:
-      hipLaunchKernelGGL(k_tables_gram<4>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      LFE_TRY(final_from(k_tables_final_chol<4>));
+      hipLaunchKernelGGL(k_tables_gram<4>, dim3(nblk), dim3(256), 0, c->stream, t, part, fin);
+      if (!fuse) LFE_TRY(final_from(k_tables_final_chol<4>));
       break;
     case 8:
-      hipLaunchKernelGGL(k_tables_gram<8>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      LFE_TRY(final_from(k_tables_final_chol<8>));
+      hipLaunchKernelGGL(k_tables_gram<8>, dim3(nblk), dim3(256), 0, c->stream, t, part, fin);
+      if (!fuse) LFE_TRY(final_from(k_tables_final_chol<8>));
       break;
     default:
-      hipLaunchKernelGGL(k_tables_gram<12>, dim3(nblk), dim3(256), 0, c->stream, t, part);
-      LFE_TRY(final_from(k_tables_final_chol<12>));
+      hipLaunchKernelGGL(k_tables_gram<12>, dim3(nblk), dim3(256), 0, c->stream, t, part, fin);
+      if (!fuse) LFE_TRY(final_from(k_tables_final_chol<12>));
       break;
   }
   LFE_HIP(hipGetLastError());
@@ -1284,39 +1302,38 @@ __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __r
   if (threadIdx.x < 64) chol_solve_wave(tile, p, beta, beta_copy, ok, L);
 }
 
-// The design tile from the raw tile + the table partials (16 waves sum the block partials of one
+// The design tile from the raw tile + the table partials (the waves sum the block partials of one
 // entry each, lanes over blocks in a fixed order); *flag = 1 when the cancellation guard holds;
-// with beta, the Cholesky solve of the tile too, in the same launch
-template <int PM>
-__global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __restrict__ partial, int nblk,
-                                                            const double* __restrict__ raw, int p,
-                                                            double* __restrict__ tile, double* __restrict__ flag,
-                                                            double* __restrict__ beta, double* __restrict__ beta_copy,
-                                                            double* __restrict__ ok) {
+// with beta, the Cholesky solve of the tile too, in the same launch.  NTH threads (>= 256): the
+// one-block finisher (1024) or the last block of k_tables_gram (256)
+template <int PM, int NTH>
+__device__ void tables_final_body(const double* __restrict__ partial, int nblk, int p, const TabFinal& f) {
   constexpr int NG = PM * (PM + 1) / 2;
   constexpr int NA = NG + PM;
+  constexpr int NW = NTH / 64;
   __shared__ double m[NA];
   __shared__ double tl[256];
   __shared__ int bad;
   __shared__ double L[kCholM][kCholM + 1];
+  const double* raw = f.raw;
   if (threadIdx.x == 0) bad = 0;
   {
-    // wave w sums entries w, w + 16, ..; lane l the blocks l, l + 64, .. (<= 256 blocks) in that
+    // wave w sums entries w, w + NW, ..; lane l the blocks l, l + 64, .. (<= 256 blocks) in that
     // order: every load issued before the first add
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const auto addop = [](double x, double y) { return x + y; };
-    constexpr int EU = (NA + 15) / 16;
+    constexpr int EU = (NA + NW - 1) / NW;
     double v[EU][4];
 #pragma unroll
     for (int u = 0; u < EU; ++u)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int e = wave + 16 * u, q = lane + 64 * rr;
+        const int e = wave + NW * u, q = lane + 64 * rr;
         v[u][rr] = (e < NA && q < nblk) ? partial[(int64_t)e * nblk + q] : 0.0;
       }
 #pragma unroll
     for (int u = 0; u < EU; ++u) {
-      const int e = wave + 16 * u;
+      const int e = wave + NW * u;
       double s = 0.0;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
@@ -1342,12 +1359,22 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
         if (i == j && !(v > 0.0 && raw[i * 16 + i] <= kTabKappa * v)) atomicAdd(&bad, 1);
       }
     }
-    tile[t] = v;
+    f.tile[t] = v;
     tl[t] = v;
   }
   __syncthreads();
-  if (threadIdx.x == 0) *flag = bad ? 0.0 : 1.0;
-  if (beta && threadIdx.x < 64) chol_solve_wave(tl, p, beta, beta_copy, ok, L);
+  if (threadIdx.x == 0) *f.flag = bad ? 0.0 : 1.0;
+  if (f.beta && threadIdx.x < 64) chol_solve_wave(tl, p, f.beta, f.beta_copy, f.ok, L);
+}
+
+template <int PM>
+__global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __restrict__ partial, int nblk,
+                                                            const double* __restrict__ raw, int p,
+                                                            double* __restrict__ tile, double* __restrict__ flag,
+                                                            double* __restrict__ beta, double* __restrict__ beta_copy,
+                                                            double* __restrict__ ok) {
+  const TabFinal f{raw, tile, flag, beta, beta_copy, ok, nullptr};
+  tables_final_body<PM, 1024>(partial, nblk, p, f);
 }
 
 // ---------------------------------------------------------------------------

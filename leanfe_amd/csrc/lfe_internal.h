@@ -324,6 +324,7 @@ struct lfe_ctx {
   char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
   hipEvent_t hpin_ev = nullptr;    // last H2D from the staging region
   hipEvent_t aux_ev = nullptr;     // completion of an asynchronous D2H into the staging region
+  hipEvent_t side_ev = nullptr;    // main-stream point a side-stream D2H waits for (prepare_layout's bucket starts)
   // the layout's work-item upload runs on its own stream while the partition scatter runs:
   // up_ev0 (main stream, before the scatter: earlier readers of items_d are done), up_ev1 (upload done)
   hipStream_t up_stream = nullptr;
@@ -381,6 +382,7 @@ struct lfe_ctx {
   double* scratch = nullptr;     // device partials
   size_t scratch_elems = 0;
   double* dred = nullptr;        // device reduced output (small)
+  unsigned int* gsync = nullptr; // [kGsyncSlots] grid-completion counters (last_block_done), zero between launches
   size_t dred_elems = 0;
   int32_t* iscratch = nullptr;   // device int scratch
   size_t iscratch_elems = 0;
@@ -782,6 +784,28 @@ __device__ __forceinline__ double row16_reduce15(double v, double idv, Op op) {
   v = op(v, dpp64<0x118, 0xF>(v, idv));
   return v;
 }
+// Grid completion of a fused reduction (one launch instead of a kernel and a one-block finisher):
+// every workgroup calls it once, with all its threads, after its global writes; it returns true in
+// exactly one workgroup - the last to arrive - which then sees every other workgroup's writes
+// (agent-scope release before the count, acquire after it).  *counter is 0 at launch and 0 again
+// when the last workgroup leaves, so a slot serves one launch at a time on its context's stream.
+constexpr int kGsyncSlots = 16;
+enum GsyncSlot { GS_TABLES_GRAM = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4 };
+__device__ __forceinline__ bool last_block_done(unsigned int* counter) {
+  __shared__ unsigned int amlast;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned int total = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned int t = atomicAdd(counter, 1u);
+    amlast = t == total - 1 ? 1u : 0u;
+    if (amlast) atomicExch(counter, 0u);
+  }
+  __syncthreads();
+  if (amlast) __threadfence();
+  return amlast != 0;
+}
+
 template <class Op>
 __device__ __forceinline__ double wave_reduce63(double v, double idv, Op op) {
   v = row16_reduce15(v, idv, op);

@@ -246,6 +246,12 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
                 raise ValueError("Strategy 'alt_proj' requires FE-cols. "
                                  "Use strategy='ols' instead for OLS without FE.")
             say("Using FWL/alternating projections strategy...")
+            if weights is None and not instruments:
+                # projections, Gram, solve, residual pass and the IID / HC1 SEs in one engine call
+                # (lfe_fit: the same steps as below without a return to Python between them)
+                fit = eng.fit(v, demean_tol, max_iter, check_from=3, drop=False)
+                return _fit_result(eng, fit, cols, x_cols, fe_cols, fe_dims, cluster_cols, v, vcov, sharded, ssc,
+                                   cl_loaded, formula, est_comp_ratio, t_load, t_start)
             order = sorted(range(len(fe_cols)), key=lambda i: fe_card[i])  # polars_impl.py:485
             iterations, _ = eng.demean(order, demean_tol, max_iter, check_from=3)
             absorbed_df = sum(fe_dims) - len(fe_cols)
@@ -312,6 +318,32 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
     return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta))),
                         std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
                         iterations=iterations, vcov_type=vcov, is_iv=False, n_instruments=None,
+                        n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
+                        fe_dims=fe_dims, r_squared=r_squared, compression_ratio=est_comp_ratio,
+                        rss=rss, tss=tss, backend="hip", timings=timings)
+
+
+def _fit_result(eng, fit, cols, x_cols, fe_cols, fe_dims, cluster_cols, v, vcov, sharded, ssc, cl_loaded, formula,
+                est_comp_ratio, t_load, t_start) -> LeanFEResult:
+    """LeanFEResult of an lfe_fit call (Engine.fit): IID / HC1 SEs come with it, clustered ones from
+    the kept score rows (std_errors.py:289-441)."""
+    n_obs, df_resid = fit["n_obs"], fit["df_resid"]
+    beta = fit["beta_full"][1:]
+    rss_w, rss, sum_y, sum_y2 = fit["stats"]
+    n_clusters = None
+    if v == "cluster":
+        se, n_clusters = _cluster_se(eng, cols, cluster_cols, sharded, fit["xtx_inv"][1:, 1:], lambda M: M, n_obs,
+                                     df_resid, ssc, cl_loaded)
+    else:
+        se = fit["se"]
+    tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
+    r_squared = 1 - rss / tss if tss > 0 else None
+    timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
+    if _VERBOSE:
+        print(f"[leanfe_amd] iterations={fit['iterations']} device ms: {timings}")
+    return LeanFEResult(coefs=dict(zip(x_cols, (float(b) for b in beta))),
+                        std_errors=dict(zip(x_cols, (float(s) for s in se))), n_obs=n_obs,
+                        iterations=fit["iterations"], vcov_type=vcov, is_iv=False, n_instruments=None,
                         n_clusters=n_clusters, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
                         fe_dims=fe_dims, r_squared=r_squared, compression_ratio=est_comp_ratio,
                         rss=rss, tss=tss, backend="hip", timings=timings)
