@@ -1219,6 +1219,7 @@ int lfe_demean(lfe_ctx* c, const int* fe_order, double tol, int max_iter, int ch
           LFE_TRY(demean_generic(c, order, tol, max_iter, check_from, &iterations, &last));
         }
       }
+      c->q_first = nullptr;  // (demean_fast consumed it, or another path ran)
       if (!c->dense_coarse || c->dense_off) break;
       c->dense_off = true;
     }

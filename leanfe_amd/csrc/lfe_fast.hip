@@ -555,7 +555,9 @@ int launch_fix_convert(lfe_ctx* c, double* S, double* hi, int64_t m, int p, cons
 // consecutive entries x 16 block slices per workgroup
 __device__ __forceinline__ void qpart_reduce_block(const double* __restrict__ part, int nblk, int64_t m,
                                                    const double* __restrict__ fq, int p, double* __restrict__ S,
-                                                   double* __restrict__ hi, int blk) {
+                                                   double* __restrict__ hi, int blk,
+                                                   double* __restrict__ alpha = nullptr,
+                                                   const int32_t* __restrict__ cnt = nullptr) {
   __shared__ unsigned long long pi[16][16];
   const int ei = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int64_t e = (int64_t)blk * 16 + ei;
@@ -568,7 +570,12 @@ __device__ __forceinline__ void qpart_reduce_block(const double* __restrict__ pa
   unsigned long long r = 0;
   for (int k = 0; k < 16; ++k) r += pi[k][ei];
   const int c = (int)(e % p);
-  S[e] = fix_value(r, take_hi(hi, e, fq, c), fq, c);
+  const double v = fix_value(r, take_hi(hi, e, fq, c), fq, c);
+  S[e] = v;
+  if (alpha) {  // the first projection of the sweeps (k_fin_check with T = 0): alpha_Q = S_Q / n_Q
+    const int32_t n = cnt[e / p];
+    alpha[e] = n > 0 ? (v - 0.0) / (double)n : 0.0;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_qpart_reduce(const double* __restrict__ part, int nblk, int64_t m,
@@ -599,11 +606,14 @@ struct Sums2Epi {
   int64_t ld;
   int has_rows, rank;
   double* raw_shift;
+  double* alphaQ;        // non-null (one rank): the sweeps' first projection alpha_Q = S_Q / n_Q here
+  const int32_t* cntQ;
+  double* zero2;         // non-null: two doubles zeroed (the i8 digits' guard flag)
 };
 __global__ __launch_bounds__(256) void k_sums2_epilogue(Sums2Epi a) {
   int b = blockIdx.x;
   if (b < a.nbq) {
-    qpart_reduce_block(a.qpart, a.nblk, a.mq, a.fq, a.p, a.SQ, a.hiQ, b);
+    qpart_reduce_block(a.qpart, a.nblk, a.mq, a.fq, a.p, a.SQ, a.hiQ, b, a.alphaQ, a.cntQ);
     return;
   }
   b -= a.nbq;
@@ -629,6 +639,7 @@ __global__ __launch_bounds__(256) void k_sums2_epilogue(Sums2Epi a) {
     return;
   }
   const int j = threadIdx.x;  // the raw shift (k_raw_shift)
+  if (a.zero2 && j < 2) a.zero2[j] = 0.0;
   if (j >= 16) return;
   const double own = (j < a.p && a.has_rows) ? a.X[(int64_t)j * a.ld] : 0.0;
   a.raw_shift[16 + j] = own;
@@ -1014,6 +1025,13 @@ int sums4(lfe_ctx* c) {
     e.has_rows = c->L.n_items > 0 ? 1 : 0;
     e.rank = c->rank;
     e.raw_shift = c->raw_shift;
+    if (c->world == 1) {  // (several ranks all-reduce S_Q after this launch)
+      LFE_TRY(ensure_f64(c, c->rflag, c->rflag_cap, 2));
+      e.alphaQ = c->fe[a.qf[0]].alpha;
+      e.cntQ = c->fe[a.qf[0]].cnt;
+      e.zero2 = c->rflag;
+      c->q_first = e.alphaQ;
+    }
     hipLaunchKernelGGL(k_sums2_epilogue, dim3((unsigned)(e.nbq + e.nbp + 256 + 1)), dim3(256), 0, c->stream, e);
     LFE_HIP(hipGetLastError());
     c->raw_ready = true;

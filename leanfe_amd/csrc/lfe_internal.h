@@ -244,6 +244,7 @@ struct lfe_ctx {
   // effects held most of its values 2^16 below its largest; lfe_demean then redoes the solve
   // without the dense cross terms (dense_off), and dense_coarse records that it did
   double* rflag = nullptr;
+  const double* q_first = nullptr;  // the two-FE sums' epilogue wrote alpha_Q = S_Q / n_Q there (and zeroed rflag)
   size_t rflag_cap = 0;
   bool dense_off = false;
   bool dense_coarse = false;

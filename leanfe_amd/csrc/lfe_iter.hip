@@ -1248,7 +1248,11 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   // the i8 digits' dynamic-range guard: its flag rides with the stop test's read-back (and, with
   // several ranks, with every sweep's T_Q all-reduce, so all ranks see the same flag)
   const bool guard = dense && c->dn8;
-  if (guard) LFE_TRY(range_flag_reset(c));
+  // the sums' epilogue already formed the first projection alpha_Q = S_Q / n_Q and zeroed the
+  // guard's flag (one rank; consumed once: a redo without the dense passes projects again)
+  const bool first_done = c->q_first != nullptr && c->q_first == fq.alpha;
+  c->q_first = nullptr;
+  if (guard && !first_done) LFE_TRY(range_flag_reset(c));
   const size_t lds_tp = sizeof(double) * ((size_t)fq.G + 1) * p;
   const size_t lds_tq = sizeof(double) * (((size_t)1 << c->L.s) + 1) * p;
   const void* ftp = NT == 1 ? reinterpret_cast<const void*>(&k_tp<1>)
@@ -1331,7 +1335,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
   }
   // sweep 1's Q projection: alpha_P = 0 -> alpha_Q = S_Q / n_Q (alpha_P is first written by K1,
   // which covers every primary group)
-  LFE_TRY(fin_check(c, Q, nullptr, nullptr, fq.alpha, false));
+  if (!first_done) LFE_TRY(fin_check(c, Q, nullptr, nullptr, fq.alpha, false));
   int iterations = 0;
   double last = -1.0;
   int flag_read = 0;  // the sweep whose check read the guard's flag

@@ -973,6 +973,7 @@ int prepare_layout(lfe_ctx* c) {
   auto& L = c->L;
   const int64_t n = c->n;
   c->sums_ready = false;
+  c->q_first = nullptr;
   c->seg_ready = false;
   c->colstat_chunks = 0;  // the partition (or sums4's k_col_stats) writes them again
   c->gram_spec = false;

@@ -10,7 +10,8 @@ mkdir -p $out
 : > $out/configs.jsonl
 bash tools/bench_presets.sh || exit $?
 for c in 1 2 3 4 5; do
-  timeout -k 10 300 python bench.py --no-h2d --no-cpu --steps 10 --warmup 3 --config $c > $out/config$c.log 2>&1 \
+  # every config line with its CPU baseline (config 5: the first 5e7 rows of its 5e8-row panel)
+  timeout -k 10 300 python bench.py --no-h2d --cpu-rows 50000000 --steps 10 --warmup 3 --config $c > $out/config$c.log 2>&1 \
     || { tail -5 $out/config$c.log; exit 1; }
   tail -1 $out/config$c.log >> $out/configs.jsonl; echo "config $c ok"
 done
