@@ -508,7 +508,10 @@ static void free_data(lfe_ctx* c) {
   c->tq_runs_cap = 0;
   dfree(c->colstat);
   dfree(c->fixq);
-  c->colstat_cap = c->fixq_cap = 0;
+  dfree(c->colq);
+  c->colstat_cap = c->fixq_cap = c->colq_cap = 0;
+  c->fixq_ready = c->any_ready = false;
+  c->q_first = nullptr;
   c->colstat_chunks = 0;
   c->owner_fe = -1;
   c->owner_on = false;

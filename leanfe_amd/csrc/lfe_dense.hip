@@ -70,6 +70,10 @@ struct DnBuildArgs {
   int32_t* cntQ;
   int32_t* flag;
   int G_P, G_Q;
+  // one rank: the singleton test of k_any_singleton folded in - a primary count of 1 where it is
+  // written, the secondary counts (summed by atomics over the workgroups) by the last workgroup
+  int32_t* any;
+  unsigned int* done;
 };
 
 // pre-filter mode: row sums of the chunk's counters = the primary counts of its groups (each group is
@@ -84,6 +88,7 @@ __device__ void dn_counts(const DnBuildArgs& a, const CT* cnt, int hlo, int HW) 
     if (lane == 0 && hlo + r < a.G_P) {
       a.cntP[hlo + r] = s;
       if (s > 65535) atomicOr(a.flag, 1);
+      if (s == 1 && a.any) atomicAdd(a.any, 1);
     }
   }
   for (int q = threadIdx.x; q < a.G_Q; q += blockDim.x) {
@@ -306,6 +311,7 @@ __device__ void dn_counts4(const DnBuildArgs& a, const uint32_t* cw, int hlo, in
     if (lane == 0 && hlo + r < a.G_P) {
       a.cntP[hlo + r] = s;
       if (s > 65535) atomicOr(a.flag, 1);
+      if (s == 1 && a.any) atomicAdd(a.any, 1);
     }
   }
   for (int q = threadIdx.x; q < a.G_Q; q += blockDim.x) {
@@ -376,8 +382,20 @@ __device__ void dn_chunk8(const DnBuildArgs& a, uint32_t* cw, int bi, int hlo, i
 // (~0.5 rows per cell): HC = 256 groups on 4-bit counters (the codes read B / 256 times), a chunk
 // with a 16-row cell counted again as two 128-group chunks.  The workgroups of a bucket share an
 // XCD (block i -> XCD i % 8), so its codes are read from one L2.
+__device__ void dn_build_body(const DnBuildArgs& a, uint32_t* cw);
+
 __global__ __launch_bounds__(1024) void k_dn_build(DnBuildArgs a) {
   extern __shared__ uint32_t cw[];  // [HC][GQ16] 8-bit or [HC / 2][GQ16] 16-bit counters
+  dn_build_body(a, cw);
+  if (a.done && last_block_done(a.done)) {  // every secondary count is final: any of them 1?
+    int found = 0;
+    for (int q = threadIdx.x; q < a.G_Q; q += blockDim.x)
+      found |= __hip_atomic_load(&a.cntQ[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
+    if (__any(found) && (threadIdx.x & 63) == 0) atomicAdd(a.any, 1);
+  }
+}
+
+__device__ void dn_build_body(const DnBuildArgs& a, uint32_t* cw) {
   const int i = blockIdx.x, x = i & 7, r = i >> 3;
   const int chunk = r % a.nch, bi = (r / a.nch) * 8 + x;
   if (bi >= a.nbe) return;
@@ -1277,6 +1295,11 @@ int dense_build(lfe_ctx* c, bool pre) {
     a.cntP = c->fe[L.P].cnt_pre;
     a.cntQ = c->fe[Q].cnt_pre;
     a.flag = c->iscratch + kIsDnPre;
+    if (c->world == 1) {  // (several ranks: the counts are summed afterwards, k_any_singleton tests them)
+      a.any = c->iscratch + kIsAny;
+      a.done = c->gsync + GS_DN_BUILD;
+      c->any_ready = true;
+    }
   }
   if (c->dn8) {
     const int nbe = std::max(c->nbe, 1);

@@ -933,11 +933,12 @@ int sums4(lfe_ctx* c) {
       LFE_HIP(hipGetLastError());
       c->colstat_chunks = nch;
     }
-    if (!wexact) {
+    if (!wexact && !c->fixq_ready) {  // (else k_finish_counts formed them from the same statistics)
       hipLaunchKernelGGL(k_fix_quanta, dim3(p), dim3(256), 0, c->stream, c->colstat, c->colstat_chunks, c->n,
                          c->iscratch + kIscratchCmax, c->F, c->fixq);
       LFE_HIP(hipGetLastError());
     }
+    c->fixq_ready = false;
     a.fixq = c->fixq;
   }
   c->exact_sums = true;

@@ -23,6 +23,7 @@ constexpr int kColStatHead = 64; // colstat: max |x_c| bits of every column befo
 constexpr int kIscratchCmax = 2 * kMaxFE + 8;
 constexpr int kIsDnPre = 2 * kMaxFE + 6;  // iscratch: a primary level of > 65535 rows in the pre-filter table build
 constexpr int kIsCmaxOver = 2 * kMaxFE + 7;  // iscratch: ranks whose primary FE keeps a level of > 65535 rows (owner)
+constexpr int kIsAny = 2 * kMaxFE + 1;   // iscratch: groups with a pre-filter count of 1 (0: nothing to mark)
 constexpr int kIscratchInts = kIscratchCmax + kMaxFE;
 // iscratch's allocation: the counts above, then lfe_load_clusters' per (cluster column, FE) flags
 // (allocated whole at the first use, so that loading clusters after the drop keeps the counts)
@@ -244,6 +245,8 @@ struct lfe_ctx {
   // effects held most of its values 2^16 below its largest; lfe_demean then redoes the solve
   // without the dense cross terms (dense_off), and dense_coarse records that it did
   double* rflag = nullptr;
+  bool any_ready = false;    // this solve's pre-filter count kernel also counted the singleton groups
+  bool fixq_ready = false;   // k_finish_counts formed the group sums' quanta (lfe_fast.hip sums4)
   const double* q_first = nullptr;  // the two-FE sums' epilogue wrote alpha_Q = S_Q / n_Q there (and zeroed rflag)
   size_t rflag_cap = 0;
   bool dense_off = false;
@@ -429,6 +432,8 @@ struct lfe_ctx {
   size_t colstat_cap = 0;
   int colstat_chunks = 0;        // chunks of per-chunk sums of squares written for this layout
   double* fixq = nullptr;        // [kFqRows][kFqCols] quanta of the group sums (fix_quanta_col)
+  double* colq = nullptr;        // [kMaxCols + 1] column sums of squares (k_finish_counts' quanta)
+  size_t colq_cap = 0;
   size_t fixq_cap = 0;
   bool exact_sums = false;       // the group sums of this layout were formed (always two-limb fixed point)
   // speculative Gram tile + Cholesky of the converged tables (gram_spec_enqueue), valid until the

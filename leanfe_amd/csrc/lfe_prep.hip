@@ -671,28 +671,42 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
 // its bucket's items (cnt1[item][h - lo]); secondary level q sums a 1/256 slice of all items
 // both in one launch: blocks [0, nbp) the primary FE (one group per thread), then the secondary
 // levels in 256 item slices (block nbp + y * nqx + x: levels 256 x.., slice y)
+// any / done (one rank): the singleton test of k_any_singleton folded in - a primary count of 1 as
+// it is written, the secondary counts (summed by atomics) by the last workgroup
 __global__ void k_cnt_from_items(const int32_t* __restrict__ cnt1, const int32_t* __restrict__ cnt2,
                                  const int32_t* __restrict__ bitems, int s, int32_t G_P, int32_t* __restrict__ cntP,
-                                 int n_items, int32_t G_Q, int32_t* __restrict__ cntQ, int nbp, int nqx) {
+                                 int n_items, int32_t G_Q, int32_t* __restrict__ cntQ, int nbp, int nqx,
+                                 int32_t* __restrict__ any, unsigned int* __restrict__ done) {
+  int found = 0;
   if ((int)blockIdx.x < nbp) {
     const int B = 1 << s;
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= G_P) return;
-    const int b = h >> s, j = h & (B - 1);
-    int32_t t = 0;
+    if (h < G_P) {
+      const int b = h >> s, j = h & (B - 1);
+      int32_t t = 0;
 #pragma unroll 4
-    for (int i = bitems[b]; i < bitems[b + 1]; ++i) t += cnt1[(int64_t)i * B + j];
-    cntP[h] = t;
-    return;
+      for (int i = bitems[b]; i < bitems[b + 1]; ++i) t += cnt1[(int64_t)i * B + j];
+      cntP[h] = t;
+      found = t == 1;
+    }
+  } else {
+    const int lin = blockIdx.x - nbp, x = lin % nqx, y = lin / nqx;
+    const int q = x * blockDim.x + threadIdx.x;
+    if (q < G_Q) {
+      const int i0 = (int)((int64_t)y * n_items / 256), i1 = (int)((int64_t)(y + 1) * n_items / 256);
+      int32_t t = 0;
+#pragma unroll 4
+      for (int i = i0; i < i1; ++i) t += cnt2[(int64_t)i * G_Q + q];
+      if (t) atomicAdd(&cntQ[q], t);
+    }
   }
-  const int lin = blockIdx.x - nbp, x = lin % nqx, y = lin / nqx;
-  const int q = x * blockDim.x + threadIdx.x;
-  if (q >= G_Q) return;
-  const int i0 = (int)((int64_t)y * n_items / 256), i1 = (int)((int64_t)(y + 1) * n_items / 256);
-  int32_t t = 0;
-#pragma unroll 4
-  for (int i = i0; i < i1; ++i) t += cnt2[(int64_t)i * G_Q + q];
-  if (t) atomicAdd(&cntQ[q], t);
+  if (!done) return;
+  if (__any(found) && (threadIdx.x & 63) == 0) atomicAdd(any, 1);
+  if (!last_block_done(done)) return;
+  found = 0;
+  for (int q = threadIdx.x; q < G_Q; q += blockDim.x)
+    found |= __hip_atomic_load(&cntQ[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
+  if (__any(found) && (threadIdx.x & 63) == 0) atomicAdd(any, 1);
 }
 
 // primary-FE counts: per work item an LDS slice of 2^s bins
@@ -769,28 +783,62 @@ struct FinishCountsArgs {
   int32_t G[kMaxFE];
   int32_t* out;  // [2 F]: (levels kept, levels present) per FE
   int32_t* cmax;  // [F]: largest kept count per FE (the exact group sums' bound, lfe_fast.hip)
+  // the group sums' quanta in the same launch (k_fix_quanta of lfe_fast.hip): the workgroups of row
+  // blockIdx.y == F sum the partition's per-chunk squares of one column each, and the last
+  // workgroup of the grid forms every column's quanta from them and the kept counts' maximum
+  const double* st;  // the partition's column statistics (null: no quanta here)
+  int nchunks, p;
+  int64_t n;
+  double* colq;      // [p] the columns' sums of squares
+  double* fq;
+  unsigned int* done;
 };
 
-__global__ void k_finish_counts(FinishCountsArgs a) {
+__global__ void k_finish_counts(FinishCountsArgs a, int F) {
   const int f = blockIdx.y;
-  const int32_t G = a.G[f];
-  int la = 0, lb = 0, mx = 0;
-  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
-    const int32_t pre = a.pre[f][g], c = pre - a.drops[f][g];
-    a.cnt[f][g] = c;
-    la += c > 0;
-    lb += pre > 0;
-    mx = max(mx, c);
+  if (f < F) {
+    const int32_t G = a.G[f];
+    int la = 0, lb = 0, mx = 0;
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+      const int32_t pre = a.pre[f][g], c = pre - a.drops[f][g];
+      a.cnt[f][g] = c;
+      la += c > 0;
+      lb += pre > 0;
+      mx = max(mx, c);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      la += __shfl_down(la, off, 64);
+      lb += __shfl_down(lb, off, 64);
+      mx = max(mx, __shfl_down(mx, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      if (la) atomicAdd(&a.out[2 * f], la);
+      if (lb) atomicAdd(&a.out[2 * f + 1], lb);
+      if (mx) atomicMax(&a.cmax[f], mx);
+    }
+  } else {
+    // column c's sum of the per-chunk squares, in k_fix_quanta's order (256 threads, DPP wave sums,
+    // the four waves in order)
+    __shared__ double ws[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int c = blockIdx.x; c < a.p; c += gridDim.x) {
+      const double* sq = a.st + kColStatHead + (int64_t)c * a.nchunks;
+      double q = 0.0;
+      for (int ch = tid; ch < a.nchunks; ch += 256) q += sq[ch];
+      q = wave_reduce63(q, 0.0, [](double x, double y) { return x + y; });
+      if (lane == 63) ws[wave] = q;
+      __syncthreads();
+      if (tid == 0) a.colq[c] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+      __syncthreads();
+    }
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    la += __shfl_down(la, off, 64);
-    lb += __shfl_down(lb, off, 64);
-    mx = max(mx, __shfl_down(mx, off, 64));
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (la) atomicAdd(&a.out[2 * f], la);
-    if (lb) atomicAdd(&a.out[2 * f + 1], lb);
-    if (mx) atomicMax(&a.cmax[f], mx);
+  if (!a.done || !last_block_done(a.done)) return;
+  int N = 1;
+  for (int g = 0; g < F; ++g) N = max(N, __hip_atomic_load(&a.cmax[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (int c = threadIdx.x; c < a.p; c += blockDim.x) {
+    const double M = __longlong_as_double(reinterpret_cast<const long long*>(a.st)[c]);
+    const double rms = a.n > 0 ? sqrt(a.colq[c] / (double)a.n) : 0.0;
+    fix_quanta_col(M, rms, (double)N, a.fq, c);
   }
 }
 
@@ -974,6 +1022,8 @@ int prepare_layout(lfe_ctx* c) {
   const int64_t n = c->n;
   c->sums_ready = false;
   c->q_first = nullptr;
+  c->any_ready = false;
+  c->fixq_ready = false;
   c->seg_ready = false;
   c->colstat_chunks = 0;  // the partition (or sums4's k_col_stats) writes them again
   c->gram_spec = false;
@@ -1171,8 +1221,11 @@ int prepare_layout(lfe_ctx* c) {
     const int32_t* c1 = c->seg_aux;
     const int32_t* c2 = c->seg_aux + (size_t)L.n_items * B;
     const int nbp = (c->fe[L.P].G + 255) / 256, nqx = (c->fe[Q].G + 255) / 256;
+    const bool one = c->world == 1;  // (several ranks sum the counts afterwards: k_any_singleton then)
     hipLaunchKernelGGL(k_cnt_from_items, dim3(nbp + nqx * 256), dim3(256), 0, c->stream, c1, c2, c->bitems_d, L.s,
-                       c->fe[L.P].G, c->fe[L.P].cnt_pre, L.n_items, c->fe[Q].G, c->fe[Q].cnt_pre, nbp, nqx);
+                       c->fe[L.P].G, c->fe[L.P].cnt_pre, L.n_items, c->fe[Q].G, c->fe[Q].cnt_pre, nbp, nqx,
+                       c->iscratch + kIsAny, one ? c->gsync + GS_CNT_ITEMS : nullptr);
+    c->any_ready = one;
     LFE_HIP(hipGetLastError());
   } else if (L.permuted) {
     ProfScope _ps(c, K_COUNT);
@@ -1203,8 +1256,9 @@ int prepare_layout(lfe_ctx* c) {
       a.G[f] = c->fe[f].G;
       gmax = std::max(gmax, c->fe[f].G);
     }
-    hipLaunchKernelGGL(k_any_singleton, dim3(grid_for(gmax, kBlock, 256)), dim3(kBlock), 0, c->stream, a,
-                       ndropped + 1);
+    if (!c->any_ready)  // (else the count kernel above counted the singleton groups)
+      hipLaunchKernelGGL(k_any_singleton, dim3(grid_for(gmax, kBlock, 256)), dim3(kBlock), 0, c->stream, a,
+                         ndropped + 1);
     LFE_HIP(hipGetLastError());
     // YOCO records keep every record: compress has no singleton drop (compress.py:1049-1175);
     // a record alone in its level is fitted exactly by its own dummy
@@ -1231,9 +1285,25 @@ int prepare_layout(lfe_ctx* c) {
     }
     fa.out = c->iscratch;
     fa.cmax = c->iscratch + kIscratchCmax;
+    // the unweighted group sums' quanta from the partition's column statistics in this launch too
+    // (sums4 then launches no k_fix_quanta)
+    c->fixq_ready = false;
+    if (!c->w && !c->sw.on && L.permuted && c->colstat_chunks > 0 && n > 0) {
+      LFE_TRY(ensure_f64(c, c->fixq, c->fixq_cap, (size_t)kFqRows * kFqCols));
+      LFE_TRY(ensure_f64(c, c->colq, c->colq_cap, (size_t)kMaxCols + 1));
+      fa.st = c->colstat;
+      fa.nchunks = c->colstat_chunks;
+      fa.p = c->p;
+      fa.n = n;
+      fa.colq = c->colq;
+      fa.fq = c->fixq;
+      fa.done = c->gsync + GS_FINISH;
+      c->fixq_ready = true;
+    }
     if (c->F > 0) {
       // few blocks: thousands of same-address adds would serialize
-      hipLaunchKernelGGL(k_finish_counts, dim3(grid_for(gmax, kBlock, 32), c->F), dim3(kBlock), 0, c->stream, fa);
+      hipLaunchKernelGGL(k_finish_counts, dim3(grid_for(gmax, kBlock, 32), c->F + (fa.done ? 1 : 0)), dim3(kBlock), 0,
+                         c->stream, fa, c->F);
       LFE_HIP(hipGetLastError());
     }
   }
