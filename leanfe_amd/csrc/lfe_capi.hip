@@ -674,6 +674,8 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   dfree(c->scratch);
   dfree(c->dred);
   if (c->gsync) (void)hipFree(c->gsync);
+  if (c->scan_status) (void)hipFree(c->scan_status);
+  c->scan_status = nullptr;
   c->gsync = nullptr;
   dfree(c->iscratch);
   dfree(c->pcounts);

@@ -386,6 +386,8 @@ struct lfe_ctx {
   double* scratch = nullptr;     // device partials
   size_t scratch_elems = 0;
   double* dred = nullptr;        // device reduced output (small)
+  unsigned long long* scan_status = nullptr;  // k_scan_fused: per-block sums tagged with the launch's epoch
+  unsigned int scan_epoch = 0;
   unsigned int* gsync = nullptr; // [kGsyncSlots] grid-completion counters (last_block_done), zero between launches
   size_t dred_elems = 0;
   int32_t* iscratch = nullptr;   // device int scratch
@@ -796,7 +798,7 @@ __device__ __forceinline__ double row16_reduce15(double v, double idv, Op op) {
 // (agent-scope release before the count, acquire after it).  *counter is 0 at launch and 0 again
 // when the last workgroup leaves, so a slot serves one launch at a time on its context's stream.
 constexpr int kGsyncSlots = 16;
-enum GsyncSlot { GS_TABLES_GRAM = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4 };
+enum GsyncSlot { GS_TABLES_GRAM = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4, GS_SCAN = 5 };
 __device__ __forceinline__ bool last_block_done(unsigned int* counter) {
   __shared__ unsigned int amlast;
   __syncthreads();

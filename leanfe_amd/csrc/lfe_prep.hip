@@ -310,6 +310,64 @@ __global__ __launch_bounds__(1024) void k_scan_one(ScanPair sp, int32_t* __restr
   }
 }
 
+// Up to kScanFewBlocks blocks in one launch: a block takes the next ticket (the dispatch order, so
+// it waits only on blocks that are running), scans its 2048 elements, publishes its sum tagged with
+// the launch's epoch, then adds the published sums of the blocks before it in its array (integer
+// adds: any order) - k_scan_blocks + k_scan_add_few without the kernel boundary.  status needs no
+// zeroing between launches: a word of another epoch reads as not yet published.
+__global__ __launch_bounds__(256) void k_scan_fused(ScanPair sp, unsigned long long* __restrict__ status,
+                                                    unsigned int* __restrict__ ticket, unsigned int epoch, int nblocks,
+                                                    int32_t* __restrict__ gout, int64_t gstride, int gn) {
+  __shared__ int32_t tmp[8];
+  __shared__ int32_t total;
+  __shared__ int id_s;
+  __shared__ int32_t ws[4];
+  if (threadIdx.x == 0) {
+    const unsigned int t = atomicAdd(ticket, 1u);
+    if (t == (unsigned int)nblocks - 1) atomicExch(ticket, 0u);  // the last ticket: reset for the next launch
+    id_s = (int)t;
+  }
+  __syncthreads();
+  const int id = id_s;
+  int64_t blk = id, m;
+  const int64_t first = blk < sp.nb1 ? 0 : sp.nb1;  // this array's first block
+  int32_t* __restrict__ a = sp.arr(blk, m);
+  const int64_t base = blk * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+  int32_t v[kScanPer];
+  scan_load8(a, base, m, v);
+  int32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) s += v[k];
+  int32_t off = block_excl_scan(s, tmp, &total);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&status[id], ((unsigned long long)epoch << 32) | (unsigned int)total, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  int32_t part = 0;
+  for (int64_t j = first + threadIdx.x; j < (int64_t)id; j += 256) {
+    unsigned long long w;
+    int spin = 0;  // bounded: a lost publication would give a wrong scan, never a hung queue
+    do {
+      w = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    } while ((unsigned int)(w >> 32) != epoch && ++spin < (1 << 22));
+    part += (int32_t)(unsigned int)w;
+  }
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_down(part, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = part;
+  __syncthreads();
+  off += (ws[0] + ws[1]) + (ws[2] + ws[3]);
+  int32_t o8[kScanPer];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    o8[k] = off;
+    off += v[k];
+  }
+  scan_store8(a, base, m, o8);
+  if (gout && id < sp.nb1)
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k)
+      if (base + k < m && (base + k) % gstride == 0 && (base + k) / gstride < gn) gout[(base + k) / gstride] = o8[k];
+}
+
 static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2, int32_t* gout,
                             int64_t gstride, int gn) {
   const int64_t nb1 = (m1 + kScanBlock - 1) / kScanBlock, nb2 = a2 ? (m2 + kScanBlock - 1) / kScanBlock : 0;
@@ -322,6 +380,18 @@ static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, in
   }
   const ScanPair sp{a1, m1, nb1, a2, m2};
   ProfScope _ps(c, K_SCAN);
+  if (nblocks <= kScanFewBlocks) {  // one launch
+    if (!c->scan_status) {
+      LFE_HIP(hipMalloc(reinterpret_cast<void**>(&c->scan_status), sizeof(unsigned long long) * kScanFewBlocks));
+      LFE_HIP(hipMemsetAsync(c->scan_status, 0, sizeof(unsigned long long) * kScanFewBlocks, c->stream));
+      c->scan_epoch = 0;
+    }
+    if (++c->scan_epoch == 0) c->scan_epoch = 1;  // (0 is the zeroed buffer's tag)
+    hipLaunchKernelGGL(k_scan_fused, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->scan_status,
+                       c->gsync + GS_SCAN, c->scan_epoch, (int)nblocks, gout, gstride, gn);
+    LFE_HIP(hipGetLastError());
+    return LFE_OK;
+  }
   if (m1 + (a2 ? m2 : 0) <= kScanOneMax) {  // one launch instead of two
     hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(1024), 0, c->stream, sp, gout, gstride, gn);
     LFE_HIP(hipGetLastError());
