@@ -29,6 +29,21 @@ const char* knob(const char* name) {
   return out.c_str();
 }
 
+static std::mutex g_lds_mu;
+static std::map<std::pair<int, const void*>, int> g_lds_set;
+
+hipError_t set_max_lds(const void* fn, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(g_lds_mu);
+  int& have = g_lds_set[{dev, fn}];
+  if (bytes <= have) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) have = bytes;
+  return e;
+}
+
 static thread_local std::string g_err;
 
 void set_error(const std::string& msg) { g_err = msg; }

@@ -840,7 +840,7 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
       const size_t lds = sizeof(unsigned long long) * (size_t)win * k;
       const void* fn = from_meat ? reinterpret_cast<const void*>(&k_clfix_add<true>)
                                  : reinterpret_cast<const void*>(&k_clfix_add<false>);
-      LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 8)));
+      LFE_HIP(set_max_lds(fn, (int)std::max<size_t>(lds, 8)));
       const int grid = std::max(1, std::min(c->L.n_items, 2 * c->n_cu));
       if (from_meat) hipLaunchKernelGGL(k_clfix_add<true>, dim3(grid), dim3(kClFixThreads), lds, c->stream, a);
       else hipLaunchKernelGGL(k_clfix_add<false>, dim3(grid), dim3(kClFixThreads), lds, c->stream, a);

@@ -1342,8 +1342,7 @@ int dense_build(lfe_ctx* c, bool pre) {
   a.NA = c->dn_na;
   a.NB = c->dn_nb;
   const size_t lds = sizeof(uint16_t) * kDnHC * GQW;  // both forms
-  LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn_build), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds));
+  LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_dn_build), (int)lds));
   const int grid = (c->nbe + 7) / 8 * 8 * a.nch;
   ProfScope _ps(c, K_LAYOUT_SCATTER);
   hipLaunchKernelGGL(k_dn_build, dim3(grid), dim3(1024), lds, c->stream, a);
@@ -1412,7 +1411,7 @@ static int dn8_launch(lfe_ctx* c, const Dn8Args& a, int waves, int grid) {
   const void* f1 = reinterpret_cast<const void*>(&k_dn8_pass<K2, 1>);
   const void* f2 = reinterpret_cast<const void*>(&k_dn8_pass<K2, 2>);
   const bool two = a.rbw == 2 * waves;
-  LFE_HIP(hipFuncSetAttribute(two ? f2 : f1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  LFE_HIP(set_max_lds(two ? f2 : f1, (int)lds));
   if (two) hipLaunchKernelGGL((k_dn8_pass<K2, 2>), dim3(grid), dim3(64 * waves), lds, c->stream, a);
   else hipLaunchKernelGGL((k_dn8_pass<K2, 1>), dim3(grid), dim3(64 * waves), lds, c->stream, a);
   LFE_HIP(hipGetLastError());
@@ -1445,8 +1444,7 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
     a.zero_check = zero_check;
     if (nkb <= kDn8MaxKb && !dn8_tiled()) {  // persistent streaming form (LFE_DN8_TILED=1: A/B)
       const size_t lds = (size_t)ntile * kDn8TileBytes;
-      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k1s), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
+      LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_dn8_k1s), (int)lds));
       const int64_t total = (int64_t)std::max(c->nbe, 1) * a.nrb;
       // every CU a workgroup down to 4 output blocks each: an owner shard's few buckets (the 8-rank
       // shard: 800 blocks) ran on 50 workgroups at 16 blocks each, its stream phase 11.5 us after a
@@ -1478,8 +1476,7 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
     // tiled form: alpha_Q's digit tiles formed once per pass by k_dn8_digits
     LFE_TRY(ensure_i8(c, c->dn8_dq, c->dn8_dq_cap, (size_t)ntile * kDn8TileBytes));
     LFE_TRY(ensure_f64(c, c->dn8_eq, c->dn8_eq_cap, (size_t)ntile * 16));
-    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_digits), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kDn8TileBytes));
+    LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_dn8_digits), kDn8TileBytes));
     hipLaunchKernelGGL(k_dn8_digits, dim3(ntile), dim3(256), kDn8TileBytes, c->stream, alphaQ, a.G_Q, a.p, a.p,
                        c->dn8_dq, c->dn8_eq, a.rflag);
     LFE_HIP(hipGetLastError());
@@ -1498,8 +1495,7 @@ int dense_tp(lfe_ctx* c, const double* alphaQ, double* zero_check) {
   a.KP = dn_parts(c, c->nbe * ((nrb + kDnR - 1) / kDnR), 16);  // alpha_Q in LDS: one workgroup per CU
   const int upw = kDnWaves / a.KP * kDnR, wgpb = (nrb + upw - 1) / upw;
   const size_t lds = sizeof(double) * a.GQ16 * a.p;
-  LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn_pass<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_dn_pass<false>), (int)lds));
   hipLaunchKernelGGL(k_dn_pass<false>, dim3(c->nbe * wgpb), dim3(kDnThreads), lds, c->stream, a);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
@@ -1518,8 +1514,7 @@ int dense_tq(lfe_ctx* c, double* runs) {
     a.alpha = c->fe[c->L.P].alpha;
     a.runs = runs;
     if (a.nkb <= 8 && !dn8_tiled()) {  // streaming form: two workgroups per bucket and CU
-      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k2s), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  kDn8TileBytes));
+      LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_dn8_k2s), kDn8TileBytes));
       const int nbe = std::max(c->nbe, 1);
       const int np = k2_parts(c, nbe, a.nrb);
       if (dn8_timing()) {
@@ -1553,8 +1548,7 @@ int dense_tq(lfe_ctx* c, double* runs) {
   a.KP = dn_parts(c, c->nbe * ((nrb + kDnR - 1) / kDnR), 32);  // a 45 KB slice: two workgroups per CU
   const int upw = kDnWaves / a.KP * kDnR, wgpb = (nrb + upw - 1) / upw;
   const size_t lds = sizeof(double) * a.B * a.p;
-  LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn_pass<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_dn_pass<true>), (int)lds));
   hipLaunchKernelGGL(k_dn_pass<true>, dim3(c->nbe * wgpb), dim3(kDnThreads), lds, c->stream, a);
   LFE_HIP(hipGetLastError());
   return LFE_OK;
@@ -1589,8 +1583,7 @@ int dn8_pair_pass(lfe_ctx* c, const PairPass& pp) { return dn8_pair_passes(c, &p
 int dn8_pair_passes(lfe_ctx* c, const PairPass* pp, int n) {
   static bool attr = false;
   if (!attr) {
-    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dn8_k2s_batch),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kDn8TileBytes));
+    LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_dn8_k2s_batch), kDn8TileBytes));
     attr = true;
   }
   for (int j0 = 0; j0 < n; j0 += kDn8Batch) {

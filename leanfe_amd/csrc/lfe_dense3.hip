@@ -375,8 +375,7 @@ static int d3_build(lfe_ctx* c) {
   LFE_TRY(ensure_dev(d.part, d.part_cap, (size_t)std::max<int64_t>(c->n_kept_local, 1)));
   d.table_bytes = 0;
   const size_t lds = (size_t)kD3Chunk * kD3W;  // 8-bit counters (16-bit: half the columns)
-  LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_d3_build), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds));
+  LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_d3_build), (int)lds));
   // every unordered pair is counted from the partition of its FE with more levels (more chunks):
   // one partition (histogram, scan, scatter) per such FE and up to kD3Slots partners
   std::vector<std::vector<int>> partners(F);

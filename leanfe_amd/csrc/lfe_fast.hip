@@ -894,7 +894,7 @@ int sums4(lfe_ctx* c) {
                    : SUMS4_FN(7, 1, 4, kSumThreads);
   }
 #undef SUMS4_FN
-  LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds, 1)));
+  LFE_HIP(set_max_lds(fn, (int)std::max<size_t>(lds, 1)));
   const int nblocks = row_blocks(c, resident_blocks(c, fn, threads, lds));
   if (raw) {
     LFE_TRY(ensure_f64(c, c->raw_part, c->raw_part_cap, (size_t)nblocks * 256));
@@ -977,8 +977,7 @@ int sums4(lfe_ctx* c) {
     // one workgroup per CU in all (LDS), the row parts spread over the column groups
     g.nparts = std::max(1, std::min(c->L.n_items * 4, (c->n_cu + g.ncg - 1) / g.ncg));
     const size_t lds_cg = sizeof(unsigned long long) * off_w;
-    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sums_cg), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds_cg));
+    LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_sums_cg), (int)lds_cg));
     ProfScope _ps(c, K_GROUP_SUMS);
     hipLaunchKernelGGL(k_sums_cg, dim3((g.nparts + 7) / 8 * 8 * g.ncg), dim3(kCgThreads), lds_cg, c->stream, g);
   } else {
@@ -994,8 +993,7 @@ int sums4(lfe_ctx* c) {
     const int nb = std::max(1, (2 * c->n_cu + p - 1) / p);  // ~2 blocks per CU over the p columns
     LFE_TRY(ensure_f64(c, c->colsum_part, c->colsum_part_cap, (size_t)p * nb * G));
     const size_t lds = sizeof(unsigned long long) * G;
-    LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col_sums), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)std::max<size_t>(lds, 1)));
+    LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_col_sums), (int)std::max<size_t>(lds, 1)));
     auto* part = reinterpret_cast<unsigned long long*>(c->colsum_part);
     hipLaunchKernelGGL(k_col_sums, dim3(nb, p), dim3(1024), lds, c->stream, c->L.code[f],
                        P >= 0 ? c->L.code[P] : nullptr, c->L.X, c->ld, c->L.w, c->n, G, p, c->fixq, c->fe[f].hi, part);

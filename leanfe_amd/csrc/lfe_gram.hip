@@ -875,7 +875,7 @@ static int run_gram(lfe_ctx* c, GramArgs a, double* host_out, int extra) {
     }
     fn = gram_kernel<MODE, NT>(a.nq > 1, a.w != nullptr, ql, a.nq == 2);
     if (dyn > 64 * 1024)  // dynamic LDS above 64 KB must be opted in
-      LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+      LFE_HIP(set_max_lds(fn, (int)dyn));
     nblocks = row_blocks(c, resident_blocks(c, fn, threads, dyn));
   }
   const int64_t pstride = Sh::LEN + 4;
@@ -976,7 +976,7 @@ static int design_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev) {
   const void* fn = PM == 4   ? reinterpret_cast<const void*>(&k_design_rows<4, 2>)
                    : PM == 8 ? reinterpret_cast<const void*>(&k_design_rows<8, 2>)
                              : reinterpret_cast<const void*>(&k_design_rows<11, 1>);
-  if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+  if (dyn > 64 * 1024) LFE_HIP(set_max_lds(fn, (int)dyn));
   const int nblocks = row_blocks(c, resident_blocks(c, fn, kResThreads, dyn));
   const int64_t pstride = 256 + 4;
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
@@ -1019,7 +1019,15 @@ struct TabArgs {
   int p;
   const double* shift;     // [16] the raw tile's shift c
   int q_on;                // 0: skip the secondary groups (owner-sharded ranks other than 0)
+  // speculative Gram (gram_spec_enqueue): run only when the stop test just computed on the device
+  // (u64 bits of the check's max) is below tol - an unconverged sweep pays an empty launch
+  const unsigned long long* gate;
+  double gate_tol;
 };
+
+__device__ __forceinline__ bool gate_closed(const unsigned long long* gate, double tol) {
+  return gate && !(__longlong_as_double((long long)*gate) < tol);
+}
 
 // the final step of the tables Gram (k_tables_final_chol): partials -> tile, guard flag, Cholesky
 struct TabFinal {
@@ -1039,6 +1047,7 @@ __global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restri
   constexpr int NG = PM * (PM + 1) / 2;
   constexpr int NA = NG + PM;
   __shared__ double red[4][NA];
+  if (gate_closed(t.gate, t.gate_tol)) return;
   const int p = t.p;
   double sh[PM];
 #pragma unroll
@@ -1115,7 +1124,8 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
                                                             const double* __restrict__ raw, int p,
                                                             double* __restrict__ tile, double* __restrict__ flag,
                                                             double* __restrict__ beta, double* __restrict__ beta_copy,
-                                                            double* __restrict__ ok);
+                                                            double* __restrict__ ok, const unsigned long long* gate,
+                                                            double gate_tol);
 
 __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __restrict__ beta,
                              double* __restrict__ beta_copy, double* __restrict__ ok);
@@ -1123,7 +1133,8 @@ __global__ void k_chol_solve(const double* __restrict__ tile, int p, double* __r
 // design tile into out_dev[0, 256) and the guard flag into *flag_dev, from the group tables; with
 // beta, also the Cholesky solve of the tile (beta, beta_copy, ok as k_chol_solve)
 static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, double* beta = nullptr,
-                               double* beta_copy = nullptr, double* ok = nullptr) {
+                               double* beta_copy = nullptr, double* ok = nullptr,
+                               const unsigned long long* gate = nullptr, double gate_tol = 0.0) {
   const int P = c->L.P, Q = 1 - P, p = c->p;
   TabArgs t{};
   t.alpha[0] = c->fe[P].alpha;
@@ -1141,6 +1152,8 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, do
   // secondary tables are global (counted on rank 0 only); the sums are all-reduced before the
   // final tile.  Otherwise every rank holds the same global tables.
   t.q_on = (!c->owner_on || c->rank == 0) ? 1 : 0;
+  t.gate = gate;
+  t.gate_tol = gate_tol;
   const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
   const int NA = PM * (PM + 1) / 2 + PM;
   const int nblk = grid_for((int64_t)t.G[0] + t.G[1], 256, 256);  // the final sums the partials by waves
@@ -1166,13 +1179,15 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, do
       ns = 1;
     }
     hipLaunchKernelGGL(kfinal, dim3(1), dim3(1024), 0, c->stream, src, ns, c->raw_tile, p, out_dev, flag_dev,
-                       split ? nullptr : beta, beta_copy, ok);
+                       split ? nullptr : beta, beta_copy, ok, gate, gate_tol);
     if (split && beta)
       hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, out_dev, p, beta, beta_copy, ok);
     return LFE_OK;
   };
   // one rank (the usual case): the last block of k_tables_gram forms the tile and solves it
-  const bool fuse = !c->owner_on && !split;
+  // (the fused form - the last block of k_tables_gram summing the partials on 256 threads - measured
+  // 43 us against 14 + 14 us for the two launches at the 8-rank shard: kept apart)
+  const bool fuse = false;
   const TabFinal fin{c->raw_tile, out_dev, flag_dev, beta, beta_copy, ok, fuse ? c->gsync + GS_TABLES_GRAM : nullptr};
   switch (PM) {
     case 4:
@@ -1372,7 +1387,9 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
                                                             const double* __restrict__ raw, int p,
                                                             double* __restrict__ tile, double* __restrict__ flag,
                                                             double* __restrict__ beta, double* __restrict__ beta_copy,
-                                                            double* __restrict__ ok) {
+                                                            double* __restrict__ ok, const unsigned long long* gate,
+                                                            double gate_tol) {
+  if (gate_closed(gate, gate_tol)) return;
   const TabFinal f{raw, tile, flag, beta, beta_copy, ok, nullptr};
   tables_final_body<PM, 1024>(partial, nblk, p, f);
 }
@@ -1703,7 +1720,7 @@ static int resid_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev, bool cl =
                       : (PM == 4   ? reinterpret_cast<const void*>(&k_resid_rows<4, 2, false>)
                          : PM == 8 ? reinterpret_cast<const void*>(&k_resid_rows<8, 2, false>)
                                    : reinterpret_cast<const void*>(&k_resid_rows<12, 2, false>));
-  if (dyn > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+  if (dyn > 64 * 1024) LFE_HIP(set_max_lds(fn, (int)dyn));
   const int nblocks = row_blocks(c, resident_blocks(c, fn, kResThreads, dyn));
   const int64_t pstride = 256 + 4;
   LFE_TRY(ensure_scratch(c, (size_t)nblocks * pstride));
@@ -2114,13 +2131,14 @@ int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t l
 
 // Gram, device solve and residual pass with one host round trip (row-kernel case:
 // two FEs, unweighted, p <= 11).  Returns 1 (nothing done) when unavailable.
-int gram_spec_enqueue(lfe_ctx* c, int* queued) {
+int gram_spec_enqueue(lfe_ctx* c, int* queued, const unsigned long long* gate, double tol) {
   *queued = 0;
   c->gram_spec = false;
   GramArgs a = base_args(c);
   if (!(resid_rows_ok(c, a) && c->p <= 11 && tables_gram_ok(c))) return LFE_OK;
   LFE_TRY(ensure_f64(c, c->dspec, c->dspec_elems, 544));
-  LFE_TRY(tables_gram_enqueue(c, c->dspec, c->dspec + 532, c->dspec + 520, c->dspec + 520, c->dspec + 516));
+  LFE_TRY(tables_gram_enqueue(c, c->dspec, c->dspec + 532, c->dspec + 520, c->dspec + 520, c->dspec + 516, gate,
+                              tol));
   *queued = 1;
   return LFE_OK;
 }

@@ -45,6 +45,11 @@ void set_error(const std::string& msg);
 // is a copy in a small per-thread ring: read it at once (e[0], atoi), do not keep the pointer.
 const char* knob(const char* name);
 
+// hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) once per (device, kernel) and size: the
+// limit only grows, and the call (~µs of host time on the launch path) is skipped when it is already
+// high enough
+hipError_t set_max_lds(const void* fn, int bytes);
+
 #define LFE_HIP(expr)                                                                    \
   do {                                                                                   \
     hipError_t _e = (expr);                                                              \
@@ -548,7 +553,7 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
 int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* stats, double* hc1, int keep_scores);
 // speculative Gram-from-tables + device Cholesky, enqueued behind a convergence check's read-back
 // so that the GPU keeps working while the host decides (lfe_gram.hip); *queued = 1 if enqueued
-int gram_spec_enqueue(lfe_ctx* c, int* queued);
+int gram_spec_enqueue(lfe_ctx* c, int* queued, const unsigned long long* gate = nullptr, double tol = 0.0);
 // out-of-core X (lfe_fast.hip / lfe_gram.hip): one streamed chunk ([p][ld] on the device)
 int stream_sums_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t row0, int64_t rows, bool first);
 int stream_weight_stats(lfe_ctx* c);

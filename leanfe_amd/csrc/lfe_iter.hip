@@ -526,7 +526,7 @@ static int local_sort(lfe_ctx* c, int Q, int K, int32_t* itemcnt, int32_t*& off,
   const int per = ls_per();
   const size_t lds = ls_scatter_lds(K, per);
   const void* fn = reinterpret_cast<const void*>(&k_ls_scatter<KEYQ, VT, kLsPer>);
-  if (lds > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (lds > 64 * 1024) LFE_HIP(set_max_lds(fn, (int)lds));
   {
     ProfScope _ps(c, K_LAYOUT_SCATTER);
     hipLaunchKernelGGL((k_ls_scatter<KEYQ, VT, kLsPer>), dim3(c->n_xgrid), dim3(kLsThreads), lds, c->stream,
@@ -592,7 +592,7 @@ static int build_layouts(lfe_ctx* c, int Q) {
     a.seg_q = c->seg_q;
     a.run_h = c->run_h;
     const void* fn = reinterpret_cast<const void*>(&k_ls_scatter2<kLsPer>);
-    if (lds2 > 64 * 1024) LFE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+    if (lds2 > 64 * 1024) LFE_HIP(set_max_lds(fn, (int)lds2));
     {
       ProfScope _ps(c, K_LAYOUT_SCATTER);
       void* args[] = {&a};
@@ -1264,8 +1264,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
                     : NT == 3 ? reinterpret_cast<const void*>(&k_tq<3>)
                               : reinterpret_cast<const void*>(&k_tq<4>);
   if (!dense) {  // the row passes' LDS tables (a wide fit runs the dense passes only)
-    LFE_HIP(hipFuncSetAttribute(ftp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds_tp, 1)));
-    LFE_HIP(hipFuncSetAttribute(ftq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max<size_t>(lds_tq, 1)));
+    LFE_HIP(set_max_lds(ftp, (int)std::max<size_t>(lds_tp, 1)));
+    LFE_HIP(set_max_lds(ftq, (int)std::max<size_t>(lds_tq, 1)));
   }
   TpArgs tp{};
   tp.seg_off = c->seg_off;
@@ -1413,7 +1413,10 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       LFE_TRY(d2h_async(c, c->dred, sizeof(double) * (guard ? 2 : 1)));
       int spec = 0;
       c->tq_final = true;
-      if (it == check_from || (last >= 0.0 && last < 100.0 * tol)) LFE_TRY(gram_spec_enqueue(c, &spec));
+      // at every check, gated on the device by the check itself: an unconverged sweep pays two empty
+      // launches (the old host-side guess - the first check, or the previous within 100x of tol -
+      // ran the whole tables Gram at two of config 1's three checks for nothing: ~15 us each)
+      LFE_TRY(gram_spec_enqueue(c, &spec, reinterpret_cast<const unsigned long long*>(c->dred), tol));
       c->tq_final = false;
       double rb[2] = {0.0, 0.0};
       LFE_TRY(d2h_wait(c, rb, sizeof(double) * (guard ? 2 : 1)));

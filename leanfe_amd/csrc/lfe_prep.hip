@@ -1069,8 +1069,7 @@ static int launch_part_scatter(lfe_ctx* c, int cols, int orig) {
         : g.per == 16   ? PART_FN(16, 512)
                         : PART_FN(8, 512);
 #undef PART_FN
-  LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)g.lds));
+  LFE_HIP(set_max_lds(reinterpret_cast<const void*>(fn), (int)g.lds));
   {
     ProfScope _ps(c, cols ? K_PART_SCATTER : K_MISC);
     hipLaunchKernelGGL(fn, dim3(pgrid), dim3(g.nth), g.lds, c->stream, a);
@@ -1158,8 +1157,7 @@ int prepare_layout(lfe_ctx* c) {
       // about two blocks per CU over all ranges, and at least ~64K rows per block
       const int bx = (int)std::max<int64_t>(1, std::min<int64_t>((2 * (int64_t)c->n_cu + nr - 1) / nr, n / 65536 + 1));
       const size_t lds = sizeof(int32_t) * kHistRange;
-      LFE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist_lds_range),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      LFE_HIP(set_max_lds(reinterpret_cast<const void*>(&k_hist_lds_range), (int)lds));
       hipLaunchKernelGGL(k_hist_lds_range, dim3(bx, nr), dim3(1024), lds, c->stream, fe.code, n, fe.G, fe.cnt_pre);
     } else
       hipLaunchKernelGGL(k_hist_global, dim3(grid_for(n)), dim3(kBlock), 0, c->stream, fe.code, n, fe.cnt_pre);
