@@ -236,11 +236,11 @@ struct lfe_emu {
 
 namespace lfe {
 
-enum EmuOp { EMU_SUM_F64, EMU_SUM_I32, EMU_MAX_F64, EMU_MAX_U64 };
+enum EmuOp { EMU_SUM_F64, EMU_SUM_I32, EMU_MAX_F64, EMU_MAX_U64, EMU_MAX_I32 };
 
 static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
   lfe_emu* e = c->emu;
-  const size_t esz = op == EMU_SUM_I32 ? sizeof(int32_t) : sizeof(double);
+  const size_t esz = (op == EMU_SUM_I32 || op == EMU_MAX_I32) ? sizeof(int32_t) : sizeof(double);
   const size_t bytes = count * esz;
   LFE_HIP(hipStreamSynchronize(c->stream));
   e->slots[c->rank].resize(bytes);
@@ -256,6 +256,9 @@ static int emu_allreduce(lfe_ctx* c, void* dev, size_t count, EmuOp op) {
       for (size_t i = 0; i < count; ++i) {
         if (op == EMU_SUM_I32) {
           reinterpret_cast<int32_t*>(e->result.data())[i] += reinterpret_cast<const int32_t*>(e->slots[r].data())[i];
+        } else if (op == EMU_MAX_I32) {
+          int32_t& acc = reinterpret_cast<int32_t*>(e->result.data())[i];
+          acc = std::max(acc, reinterpret_cast<const int32_t*>(e->slots[r].data())[i]);
         } else if (op == EMU_MAX_U64) {
           uint64_t& acc = reinterpret_cast<uint64_t*>(e->result.data())[i];
           acc = std::max(acc, reinterpret_cast<const uint64_t*>(e->slots[r].data())[i]);
@@ -348,6 +351,13 @@ int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count) {
   if (c->world <= 1 || count == 0) return LFE_OK;
   if (c->emu) return emu_allreduce(c, dev, count, EMU_SUM_I32);
   LFE_NCCL(ncclAllReduce(dev, dev, count, ncclInt32, ncclSum, c->comm, c->stream));
+  return LFE_OK;
+}
+
+int allreduce_max_i32(lfe_ctx* c, int32_t* dev, size_t count) {
+  if (c->world <= 1 || count == 0) return LFE_OK;
+  if (c->emu) return emu_allreduce(c, dev, count, EMU_MAX_I32);
+  LFE_NCCL(ncclAllReduce(dev, dev, count, ncclInt32, ncclMax, c->comm, c->stream));
   return LFE_OK;
 }
 
@@ -1166,6 +1176,10 @@ int lfe_load_clusters(lfe_ctx* c, int m, const int32_t* const* cl_codes, const i
     for (int f = 0; f < c->F; ++f)
       if (c->fe[f].G == cl_levels[j]) LFE_TRY(launch_codes_differ(c, c->cl[j], c->fe[f].code, c->n,
                                                                   c->iscratch + kIsClFlags + j * kMaxFE + f));
+  // several ranks: a bad code anywhere fails every rank, and a column repeats an FE only if it does
+  // on every rank's rows (the owner-local cluster forms are then a decision all ranks take alike)
+  LFE_TRY(allreduce_sum_i32(c, c->iscratch, 1));
+  LFE_TRY(allreduce_sum_i32(c, c->iscratch + kIsClFlags, (size_t)m * kMaxFE));
   std::vector<int32_t> h(kIsClFlags + (size_t)m * kMaxFE, 0);
   LFE_HIP(hipMemcpyAsync(h.data(), c->iscratch, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, c->stream));
   LFE_HIP(hipStreamSynchronize(c->stream));

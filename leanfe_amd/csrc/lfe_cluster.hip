@@ -758,8 +758,38 @@ static bool clfix_on() {
 
 // meat and cluster count of the one-column subset j by the fixed-point sums (S: [G][k], then S'S);
 // win / bucketed: the LDS window of k_clfix_add
+// Owner-sharded ranks hold every row of a range of the primary FE's levels: a subset with a cluster
+// column that repeats that FE (lfe_load_clusters compared them, every rank agreeing) has each of its
+// clusters on one rank, so its sums - sort-free or sorted, bucket keys included - need no exchange:
+// every rank forms S'S of its own clusters and the k x k meat and the cluster count are summed over
+// ranks.  Returns that column, or -1.
+static int owner_col(const lfe_ctx* c, int mask) {
+  if (!(c->world > 1 && c->owner_on && c->L.P >= 0 && c->L.permuted)) return -1;
+  for (int j = 0; j < (int)c->cl.size(); ++j)
+    if ((mask >> j & 1) && j < (int)c->cl_fe.size() && c->cl_fe[j] == c->L.P &&
+        c->cl_levels[j] == c->fe[c->L.P].G)
+      return j;
+  return -1;
+}
+
+// an integer summed over ranks (exact in f64 below 2^53)
+static int sum_over_ranks(lfe_ctx* c, int64_t v, int64_t* out) {
+  if (c->world <= 1) {
+    *out = v;
+    return LFE_OK;
+  }
+  LFE_TRY(ensure_f64(c, c->clw.rsum, c->clw.rsum_cap, 2));
+  const double d = (double)v;
+  LFE_TRY(h2d_small(c, c->clw.rsum, &d, sizeof(double)));
+  LFE_TRY(allreduce_sum_f64(c, c->clw.rsum, 1));
+  double h = 0.0;
+  LFE_TRY(d2h_sync(c, &h, c->clw.rsum, sizeof(double)));
+  *out = (int64_t)h;
+  return LFE_OK;
+}
+
 static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* meat, int64_t* G_out,
-                           bool stats_pass = false) {
+                           bool stats_pass = false, bool owner_local = false) {
   const int k = c->score_k;
   const int64_t n = c->n;
   const int32_t G = c->cl_levels[j];
@@ -848,7 +878,10 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
       LFE_TRY(launch_fix_convert(c, S, c->clS, (int64_t)m, k, W.fixq));
     }
   }
-  if (c->world > 1) {  // every rank's sums in the key-indexed table (global codes): all-reduced
+  if (owner_local) {  // each cluster on one rank: the counts of present clusters summed
+    LFE_TRY(allreduce_sum_i32(c, cm, 1));
+    LFE_TRY(allreduce_max_i32(c, cm + 2, 1));
+  } else if (c->world > 1) {  // every rank's sums in the key-indexed table (global codes): all-reduced
     LFE_TRY(allreduce_sum_f64(c, S, (size_t)G * k));
     LFE_TRY(allreduce_sum_i32(c, cnt, (size_t)G));
     LFE_HIP(hipMemsetAsync(cm, 0, sizeof(int32_t) * 2, c->stream));
@@ -858,11 +891,13 @@ static int subset_meat_fix(lfe_ctx* c, int j, int win, bool bucketed, double* me
   int32_t hc[3] = {0, 0, 0};
   LFE_TRY(d2h_sync(c, hc, cm, sizeof(hc)));
   if (hc[2] != 0)  // a value past the assumed range: the quanta from the statistics pass instead
-    return subset_meat_fix(c, j, win, bucketed, meat, G_out, true);
+    return subset_meat_fix(c, j, win, bucketed, meat, G_out, true, owner_local);
   *G_out = hc[0];
   if (k == 0) return LFE_OK;
-  const int world = c->world;  // S is replicated after the all-reduce: reduce its Gram locally
-  c->world = 1;
+  // S is replicated after the all-reduce: reduce its Gram locally; owner-local: each rank's S'S of
+  // its own clusters, summed over ranks by the Gram's reduction
+  const int world = c->world;
+  if (!owner_local) c->world = 1;
   const int rc = launch_table_gram(c, S, G, k, meat);
   c->world = world;
   return rc;
@@ -963,7 +998,7 @@ int cluster_fused_col(const lfe_ctx* c) {
   }();
   const int k = c->p - 1;
   if (!(env_on && clfix_on() && !(c->test_hooks & (LFE_TEST_CLUSTER_SORTED | LFE_TEST_CLUSTER_STATS)) &&
-        c->world == 1 && c->L.P >= 0 && c->L.permuted && !c->w && !c->records && k >= 1 && k <= 63))
+        (c->world == 1 || c->owner_on) && c->L.P >= 0 && c->L.permuted && !c->w && !c->records && k >= 1 && k <= 63))
     return -1;
   for (int j = 0; j < (int)c->cl_fe.size() && j < (int)c->cl.size(); ++j)
     if (c->cl_fe[j] == c->L.P) return j;
@@ -981,6 +1016,8 @@ int cluster_fused_prepare(lfe_ctx* c) {
   LFE_HIP(hipMemsetAsync(cm, 0, sizeof(int32_t) * 4, c->stream));
   hipLaunchKernelGGL(k_clfix_count, dim3(grid_for(G, 256, 1024)), dim3(256), 0, c->stream, c->clf_cnt, G, cm);
   LFE_HIP(hipGetLastError());
+  // owner-sharded ranks: the largest cluster over all ranks, so every rank takes the same quanta
+  LFE_TRY(allreduce_max_i32(c, cm + 1, 1));
   return LFE_OK;
 }
 
@@ -1005,6 +1042,9 @@ static int cluster_fused_finish(lfe_ctx* c, double* meat, int64_t* G_out, int* r
     return LFE_OK;
   }
   int32_t hc[3] = {0, 0, 0};
+  // owner-sharded ranks: clusters present and the bound flag over all ranks (the redo is everyone's)
+  LFE_TRY(allreduce_sum_i32(c, c->clf_cnt + G, 1));
+  LFE_TRY(allreduce_max_i32(c, c->clf_cnt + G + 2, 1));
   LFE_TRY(d2h_sync(c, hc, c->clf_cnt + G, sizeof(hc)));
   *redo = hc[2] != 0;
   if (*redo) return LFE_OK;
@@ -1052,13 +1092,14 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
     // measured slower than the sort: 4.7 vs 2.5 ms on config 4's 1e5-level column, round 5)
     const int j = __builtin_ctz((unsigned)mask);
     const int64_t G = c->cl_levels[j];
-    if (c->world == 1 || G * k * 8 <= (64ll << 20)) {
+    const bool own = owner_col(c, mask) == j;
+    if (c->world == 1 || own || G * k * 8 <= (64ll << 20)) {
       int win = 0;
       bool bucketed = false;
       if ((size_t)G * k * 8 <= kClFixLds) {
         win = (int)G;
-      } else if (c->world == 1 && c->L.permuted && c->L.P >= 0 && j < (int)c->cl_fe.size() && c->cl_fe[j] == c->L.P &&
-                 ((size_t)8 << c->L.s) * k <= kClFixLds) {
+      } else if ((c->world == 1 || own) && c->L.permuted && c->L.P >= 0 && j < (int)c->cl_fe.size() &&
+                 c->cl_fe[j] == c->L.P && ((size_t)8 << c->L.s) * k <= kClFixLds) {
         bucketed = true;  // the column repeats the primary FE (lfe_load_clusters compared them)
         win = 1 << c->L.s;
       }
@@ -1068,7 +1109,7 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
       }();
       if (win > 0)
         return subset_meat_fix(c, j, win, bucketed, meat, G_out,
-                               stats_env || (c->test_hooks & LFE_TEST_CLUSTER_STATS) != 0);
+                               stats_env || (c->test_hooks & LFE_TEST_CLUSTER_STATS) != 0, own);
     }
     // a column that repeats an FE of the general sweeps: that FE's segment layout
     const int f = j < (int)c->cl_fe.size() ? c->cl_fe[j] : -1;
@@ -1097,7 +1138,8 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   // one process, a column that repeats the primary FE: the layout's bucket order already sorts the
   // key's top part (HDFE_CLUSTER2, MEGA_CLUSTER2: 4 -> 3 radix passes).  Dropped rows take the low
   // part past every kept row's, so they end the sorted order as one run.
-  if (c->world == 1 && c->L.permuted && c->L.P >= 0 && ka.m >= 2 && !(c->test_hooks & LFE_TEST_CLUSTER_SORTED)) {
+  const bool own = owner_col(c, mask) >= 0;  // every cluster of the subset on one rank
+  if ((c->world == 1 || own) && c->L.permuted && c->L.P >= 0 && ka.m >= 2 && !(c->test_hooks & LFE_TEST_CLUSTER_SORTED)) {
     int jp = -1, kj = 0;
     for (int j = 0; j < (int)c->cl.size(); ++j) {
       if (!(mask >> j & 1)) continue;
@@ -1156,6 +1198,11 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
     return singleton_meat(c, W.rows[buf], G, k, meat);
   }
   if (k > 0) LFE_TRY(group_sums(c, n, drop, W.keys[buf], W.rows[buf], c->scores, k, G, nv));
+  if (own) {  // owner-local: this rank's clusters are whole; the meat and the count summed over ranks
+    LFE_TRY(sum_over_ranks(c, G, G_out));
+    if (k == 0) return LFE_OK;
+    return launch_table_gram(c, c->clS, G, k, meat);
+  }
 
   // multi-rank, few clusters: a key-indexed table, all-reduced (smaller than the exchange)
   const char* own_env = knob("LFE_CL_OWNER_MIN_SPAN");  // tests: force the owner-partitioned form
@@ -1230,6 +1277,8 @@ int launch_cluster_subsets(lfe_ctx* c, int n_subsets, const int32_t* masks, doub
 void free_cluster_ws(lfe_ctx* c) {
   auto& W = c->clw;
   dfree_any(W.fixst);
+  dfree_any(W.rsum);
+  W.rsum_cap = 0;
   dfree_any(W.fixq);
   dfree_any(W.segst);
   W.fixst_cap = W.fixq_cap = W.segst_cap = 0;

@@ -151,6 +151,8 @@ struct ClusterWS {
   size_t skey_cap = 0;
   double* srec = nullptr;       // [G_local][k] send records
   size_t srec_cap = 0;
+  double* rsum = nullptr;       // one double summed over ranks (sum_over_ranks)
+  size_t rsum_cap = 0;
   uint64_t* rkey = nullptr;     // received keys
   size_t rkey_cap = 0;
   double* rrec = nullptr;       // received records
@@ -703,6 +705,7 @@ int allreduce_sum_f64_many(lfe_ctx* c, const std::vector<std::pair<double*, size
 int allreduce_sum_i32(lfe_ctx* c, int32_t* dev, size_t count);
 int allreduce_max_f64(lfe_ctx* c, double* dev, size_t count);
 int allreduce_max_u64(lfe_ctx* c, uint64_t* dev, size_t count);
+int allreduce_max_i32(lfe_ctx* c, int32_t* dev, size_t count);
 int alltoallv_bytes(lfe_ctx* c, const char* send, const size_t* send_off, const size_t* send_bytes, char* recv,
                     const size_t* recv_off, const size_t* recv_bytes);
 void prof_begin(lfe_ctx* c, int kid);

@@ -660,3 +660,81 @@ def test_unbalanced_owner_shards_take_the_same_sweeps(levels):
         np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
         np.testing.assert_array_equal(res["beta"], out[0]["beta"])
         np.testing.assert_array_equal(res["se"], out[0]["se"])
+
+
+@pytest.mark.parametrize("world,n,k,levels,cl", [
+    (4, 1_500_000, 4, (10_000, 2_000), (0,)),          # HDFE_CLUSTER1's shape: sums in the residual pass
+    (4, 1_500_000, 4, (10_000, 2_000), (0, 1)),        # HDFE_CLUSTER2's: owner-local bucket keys for fe1 x fe2
+    (8, 1_500_000, 4, (10_000, 2_000), (0, 1)),
+    (4, 1_000_000, 5, (40_000, 4_000, 400), (1, 2)),   # config 4's: fe2 x fe3 holds no owner column
+    (8, 1_000_000, 5, (40_000, 4_000, 400), (1, 2)),
+], ids=["hdfe_cl1_w4", "hdfe_cl2_w4", "hdfe_cl2_w8", "config4_w4", "config4_w8"])
+def test_emulated_owner_shards_cluster_forms(world, n, k, levels, cl):
+    """Owner-sharded ranks (every row of a range of the primary FE's levels on one rank: the
+    strong-scaled headline schedule, dist.owner_range) with clustered SEs (std_errors.py:289-441):
+    a subset holding the cluster column that repeats the primary FE has each cluster on one rank, so
+    the round-5 forms run per rank - the one-way sums inside the residual pass, the bucket-key
+    intersections - with only the k x k meat and the cluster count summed over ranks; other subsets
+    keep the all-reduced table or the owner exchange.  Every rank equals the oracle on the whole panel
+    (1e-10, equal integers) and all ranks and a second run agree bit for bit."""
+    from leanfe_amd import dist
+    from leanfe_amd._lib import EmuGroup, Engine
+    from oracle import altproj
+
+    seed = 61
+    P = max(range(len(levels)), key=lambda f: levels[f])
+
+    def run():
+        group = EmuGroup(world)
+        out, errs = {}, {}
+
+        def worker(rank):
+            try:
+                lo, hi = dist.owner_range(levels[P], rank, world)
+                eng = Engine(0)
+                eng.set_emu(group, rank)
+                eng.synth_load_owned(n, k, list(levels), synth.betas(k), P, lo, hi, seed=seed)
+                _, codes = eng.copy_inputs()
+                eng.load_clusters([np.ascontiguousarray(codes[f]) for f in cl], [levels[f] for f in cl])
+                r = eng.fit("cluster")
+                Vb = r["xtx_inv"][1:, 1:]
+                if len(cl) == 1:
+                    meats, Gs = eng.cluster_meat()
+                    se, ncl = inference.se_cluster_oneway(Vb, meats[0], int(Gs[0]), r["n_obs"], r["df_resid"], True)
+                else:
+                    subsets = inference.cluster_subsets(len(cl))
+                    meats, Gs = eng.cluster_meat_subsets(subsets)
+                    se, ncl = inference.se_cluster_multiway(Vb, list(meats), [int(g) for g in Gs], subsets,
+                                                            r["n_obs"], r["df_resid"], True)
+                out[rank] = dict(beta=r["beta_full"][1:], se=se, ncl=ncl, it=r["iterations"], n_obs=r["n_obs"])
+                eng.close()
+            except BaseException as e:  # noqa: BLE001
+                errs[rank] = e
+                group.abort()
+
+        threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=300)
+        assert not any(t.is_alive() for t in threads), "emulated group deadlocked"
+        if errs:
+            raise next(iter(errs.values()))
+        return out
+
+    a, b = run(), run()
+    full = synth.panel(n, k, list(levels), seed=seed)
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = [f"fe{f + 1}" for f in range(len(levels))]
+    o = altproj.fit(full, "y", xs, fes, vcov="cluster", cluster_cols=[fes[f] for f in cl])
+    ncl = o["n_clusters"]
+    for r in range(world):
+        res = a[r]
+        assert res["it"] == o["iterations"] and res["n_obs"] == o["n_obs"]
+        got = res["ncl"] if len(cl) > 1 else [res["ncl"]]
+        assert list(got) == (list(ncl) if isinstance(ncl, (list, tuple)) else [ncl])
+        np.testing.assert_allclose(res["beta"], o["beta"], rtol=1e-10, atol=0)
+        np.testing.assert_allclose(res["se"], o["se"], rtol=1e-10, atol=0)
+        for other in (a[0], b[r]):
+            np.testing.assert_array_equal(res["beta"], other["beta"])
+            np.testing.assert_array_equal(res["se"], other["se"])
