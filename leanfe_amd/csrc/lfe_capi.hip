@@ -113,6 +113,24 @@ int d2h_async(lfe_ctx* c, const void* src_dev, size_t bytes) {
   return LFE_OK;
 }
 
+// the values a kernel published with host_msg_publish under sequence number seq; a bounded spin (the
+// stream is synchronized after ~2 s without the message, which then must be there)
+int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals) {
+  for (long spin = 0;; ++spin) {
+    if (__atomic_load_n(&c->hmsg[0], __ATOMIC_ACQUIRE) == seq) break;
+    if (spin == (1l << 26)) {
+      LFE_HIP(hipStreamSynchronize(c->stream));
+      if (__atomic_load_n(&c->hmsg[0], __ATOMIC_ACQUIRE) != seq) return fail(LFE_EHIP, "device message lost");
+      break;
+    }
+  }
+  for (int i = 0; i < nvals; ++i) {
+    const unsigned long long b = __atomic_load_n(&c->hmsg[1 + i], __ATOMIC_RELAXED);
+    memcpy(&vals[i], &b, sizeof(double));
+  }
+  return LFE_OK;
+}
+
 int d2h_wait(lfe_ctx* c, void* dst, size_t bytes) {
   LFE_HIP(hipEventSynchronize(c->aux_ev));  // work enqueued after the copy keeps running
   memcpy(dst, c->hpin, bytes);
@@ -674,12 +692,15 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
       hipEventCreateWithFlags(&c->up_ev0, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->up_ev1, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->hpin), kPinSmall, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->hmsg), 4096, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dmsg), c->hmsg, 0) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->gsync), kGsyncSlots * sizeof(unsigned int)) != hipSuccess ||
       hipMemsetAsync(c->gsync, 0, kGsyncSlots * sizeof(unsigned int), c->stream) != hipSuccess) {
     delete c;
     return fail(LFE_EHIP, "stream/event/buffer creation failed");
   }
+  memset(c->hmsg, 0, 4096);
   for (auto& pair : c->tm.ev)
     for (auto& e : pair)
       if (hipEventCreate(&e) != hipSuccess) {
@@ -716,6 +737,7 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   dfree(c->alpha_spare);
   dfree(c->dbeta);
   if (c->hpin) (void)hipHostFree(c->hpin);
+  if (c->hmsg) (void)hipHostFree(c->hmsg);
   if (c->hpin_items) (void)hipHostFree(c->hpin_items);
   if (c->hpin_ev) (void)hipEventDestroy(c->hpin_ev);
   for (auto& e : c->load_ev)

@@ -333,6 +333,11 @@ struct lfe_ctx {
   lfe::ClusterWS clw;
   // pinned host staging (small transfers avoid the runtime's pageable path)
   char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
+  // mapped, coherent host memory the device writes small results into (no copy kernel, no event):
+  // msg[0] = sequence number, msg[1..] = values; the host spins on the sequence (host_msg_wait)
+  unsigned long long* hmsg = nullptr;   // host view
+  unsigned long long* dmsg = nullptr;   // device view
+  unsigned long long msg_seq = 0;
   hipEvent_t hpin_ev = nullptr;    // last H2D from the staging region
   hipEvent_t aux_ev = nullptr;     // completion of an asynchronous D2H into the staging region
   hipEvent_t side_ev = nullptr;    // main-stream point a side-stream D2H waits for (prepare_layout's bucket starts)
@@ -683,6 +688,7 @@ int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes);
 // device -> host copy into the pinned staging region without waiting; d2h_wait finishes it
 int d2h_async(lfe_ctx* c, const void* src_dev, size_t bytes);
 int d2h_wait(lfe_ctx* c, void* dst, size_t bytes);
+int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals);
 // host -> device copy of a small argument through pinned staging (asynchronous)
 int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes);
 // pinned upload buffer of at least `bytes` (work items)
@@ -805,8 +811,17 @@ __device__ __forceinline__ double row16_reduce15(double v, double idv, Op op) {
 // exactly one workgroup - the last to arrive - which then sees every other workgroup's writes
 // (agent-scope release before the count, acquire after it).  *counter is 0 at launch and 0 again
 // when the last workgroup leaves, so a slot serves one launch at a time on its context's stream.
+// the last workgroup of a launch publishes nv values to the host message (lfe_ctx::dmsg): values
+// first, then the sequence number with a system-scope release (the host spins on it)
+__device__ __forceinline__ void host_msg_publish(unsigned long long* msg, unsigned long long seq, const double* v, int nv) {
+  for (int i = 0; i < nv; ++i)
+    __hip_atomic_store(&msg[1 + i], (unsigned long long)__double_as_longlong(v[i]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&msg[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 constexpr int kGsyncSlots = 16;
-enum GsyncSlot { GS_TABLES_GRAM = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4, GS_SCAN = 5 };
+enum GsyncSlot { GS_TABLES_GRAM = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4, GS_SCAN = 5, GS_TQ_REDUCE = 6 };
 __device__ __forceinline__ bool last_block_done(unsigned int* counter) {
   __shared__ unsigned int amlast;
   __syncthreads();

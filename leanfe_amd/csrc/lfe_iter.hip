@@ -1143,7 +1143,9 @@ __global__ __launch_bounds__(256) void k_tq_reduce_fin(const double* __restrict_
                                                        const int32_t* __restrict__ cnt, int p,
                                                        const double* __restrict__ cur, double* __restrict__ out,
                                                        unsigned long long* __restrict__ check,
-                                                       const double* __restrict__ flag_in, double* __restrict__ flag_out) {
+                                                       const double* __restrict__ flag_in, double* __restrict__ flag_out,
+                                                       unsigned int* __restrict__ done,
+                                                       unsigned long long* __restrict__ msg, unsigned long long seq) {
   __shared__ double part[kTqRedS][kTqRedE];
   // the digits' guard flag beside the stop test, for the same read-back (no separate copy)
   if (flag_in && blockIdx.x == 0 && threadIdx.x == 0) *flag_out = *flag_in;
@@ -1154,6 +1156,14 @@ __global__ __launch_bounds__(256) void k_tq_reduce_fin(const double* __restrict_
   double mx = 0.0;
   if (sl == 0 && e < m) mx = tq_red_fin(tq_red_total(part, ei), e, T, S, cnt, p, cur, out, check != nullptr);
   if (check && threadIdx.x < 64) tq_red_check(mx, threadIdx.x, check);
+  // the stop test (and the guard's flag) straight into mapped host memory by the last workgroup:
+  // no copy kernel and no event between the sweep and the host's decision
+  if (msg && last_block_done(done) && threadIdx.x == 0) {
+    double v[2];
+    v[0] = __longlong_as_double((long long)__hip_atomic_load(check, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    v[1] = flag_in ? __hip_atomic_load(flag_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    host_msg_publish(msg, seq, v, 2);
+  }
 }
 
 // alpha_new = (S - T) / cnt; check = max_g |alpha_new[g][0] - alpha_cur[g][0]| over groups present
@@ -1380,13 +1390,16 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     const bool check = it >= check_from;
     const int64_t m = (int64_t)fq.G * p;
     const unsigned tq_grid = (unsigned)((m + kTqRedE - 1) / kTqRedE);
+    unsigned long long seq = 0;  // the stop test published to mapped host memory (one rank)
     if (c->world == 1) {  // T_Q and the next Q projection in one launch
+      if (check) seq = ++c->msg_seq;
       {
         ProfScope _ps(c, K_TQ_REDUCE);
         hipLaunchKernelGGL(k_tq_reduce_fin, dim3(tq_grid), dim3(kTqRedE * kTqRedS), 0, c->stream, c->tq_runs,
                            c->nbe, m, fq.T, fq.S, fq.cnt, p, fq.alpha, c->alpha_spare,
                            check ? reinterpret_cast<unsigned long long*>(c->dred) : nullptr,
-                           check && guard ? c->rflag : nullptr, c->dred + 1);
+                           check && guard ? c->rflag : nullptr, c->dred + 1, c->gsync + GS_TQ_REDUCE,
+                           check ? c->dmsg : nullptr, seq);
       }
       LFE_HIP(hipGetLastError());
       if (!check && it == max_iter) break;
@@ -1410,7 +1423,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       // the tables and its Cholesky, so the GPU works through the host's decision and the
       // return to the caller; lfe_gram_resid then starts at the residual pass
       // (the guard's flag was copied beside the check by the reduce / projection kernel)
-      LFE_TRY(d2h_async(c, c->dred, sizeof(double) * (guard ? 2 : 1)));
+      if (!seq) LFE_TRY(d2h_async(c, c->dred, sizeof(double) * (guard ? 2 : 1)));
       int spec = 0;
       c->tq_final = true;
       // at every check, gated on the device by the check itself: an unconverged sweep pays two empty
@@ -1419,7 +1432,8 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
       LFE_TRY(gram_spec_enqueue(c, &spec, reinterpret_cast<const unsigned long long*>(c->dred), tol));
       c->tq_final = false;
       double rb[2] = {0.0, 0.0};
-      LFE_TRY(d2h_wait(c, rb, sizeof(double) * (guard ? 2 : 1)));
+      if (seq) LFE_TRY(host_msg_wait(c, seq, rb, 2));
+      else LFE_TRY(d2h_wait(c, rb, sizeof(double) * (guard ? 2 : 1)));
       last = rb[0];
       flag_read = it;
       if (rb[1] != 0.0) {  // a tile's digits lost precision: lfe_demean redoes the solve without them
