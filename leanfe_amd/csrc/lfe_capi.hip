@@ -7,6 +7,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "lfe_internal.h"
@@ -166,10 +167,22 @@ int ensure_pinned_items(lfe_ctx* c, size_t bytes) {
   return LFE_OK;
 }
 
+// the occupancy query costs several µs of host time on the launch path: cached per (device, kernel,
+// block size, dynamic LDS)
 int resident_blocks(lfe_ctx* c, const void* fn, int threads, size_t dyn_lds) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, const void*, int, size_t>, int> cache;
+  const auto key = std::make_tuple(c->device, fn, threads, dyn_lds);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second * c->n_cu;
+  }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, dyn_lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = per_cu;
   return per_cu * c->n_cu;
 }
 
@@ -692,7 +705,7 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
       hipEventCreateWithFlags(&c->up_ev0, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->up_ev1, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->hpin), kPinSmall, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&c->hmsg), 4096, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->hmsg), kHostMsgBytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dmsg), c->hmsg, 0) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->dbeta), 64 * sizeof(double)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->gsync), kGsyncSlots * sizeof(unsigned int)) != hipSuccess ||
@@ -700,7 +713,7 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
     delete c;
     return fail(LFE_EHIP, "stream/event/buffer creation failed");
   }
-  memset(c->hmsg, 0, 4096);
+  memset(c->hmsg, 0, kHostMsgBytes);
   for (auto& pair : c->tm.ev)
     for (auto& e : pair)
       if (hipEventCreate(&e) != hipSuccess) {

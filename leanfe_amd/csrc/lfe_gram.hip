@@ -768,6 +768,37 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const double* __restric
   if (threadIdx.x == 0) out[e] = red[0];
 }
 
+// k_reduce_partials whose last workgroup then publishes src[0, count) (the whole result block the
+// host reads: spec tile, beta, guard and this residual tile) into mapped host memory (one rank)
+__global__ __launch_bounds__(256) void k_reduce_partials_msg(const double* __restrict__ partial, int nblocks,
+                                                             int64_t pstride, double* __restrict__ out,
+                                                             unsigned int* __restrict__ done, const double* src,
+                                                             int count, unsigned long long* __restrict__ msg,
+                                                             unsigned long long seq) {
+  __shared__ double red[256];
+  const int e = blockIdx.x;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += 256) s += partial[(int64_t)b * pstride + e];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[e] = red[0];
+  if (!last_block_done(done)) return;
+  for (int i = threadIdx.x; i < count; i += 256)
+    __hip_atomic_store(&msg[1 + i],
+                       (unsigned long long)__double_as_longlong(__hip_atomic_load(&src[i], __ATOMIC_RELAXED,
+                                                                                  __HIP_MEMORY_SCOPE_AGENT)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(&msg[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void k_validate(const int32_t* __restrict__ code, int64_t n, int32_t lo, int32_t hi,
                            int32_t* __restrict__ flag) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1709,7 +1740,8 @@ int launch_gram(lfe_ctx* c, double* host_gram) {
 // row-per-lane residual pass (k_resid_rows): two FEs, unweighted, p <= 12, both
 // alpha tables (padded to PM doubles per row) in LDS; leaves the reduced [16][16]
 // tile + 4 statistics (260 doubles, all ranks) in out_dev
-static int resid_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev, bool cl = false) {
+static int resid_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev, bool cl = false,
+                              const double* msg_src = nullptr, int msg_count = 0, unsigned long long msg_seq = 0) {
   const int p = c->p;
   const int PM = p <= 4 ? 4 : p <= 8 ? 8 : 12;
   const size_t dyn = cl ? sizeof(double) * (size_t)a.B * (PM + (p - 1))
@@ -1733,8 +1765,12 @@ static int resid_rows_enqueue(lfe_ctx* c, GramArgs a, double* out_dev, bool cl =
   LFE_HIP(hipGetLastError());
   {
     ProfScope _ps(c, K_REDUCE);
-    hipLaunchKernelGGL(k_reduce_partials, dim3(pstride), dim3(256), 0, c->stream, c->scratch, nblocks, pstride,
-                       out_dev);
+    if (msg_src)  // one rank: the result block straight to mapped host memory
+      hipLaunchKernelGGL(k_reduce_partials_msg, dim3(pstride), dim3(256), 0, c->stream, c->scratch, nblocks, pstride,
+                         out_dev, c->gsync + GS_RESID, msg_src, msg_count, c->dmsg, msg_seq);
+    else
+      hipLaunchKernelGGL(k_reduce_partials, dim3(pstride), dim3(256), 0, c->stream, c->scratch, nblocks, pstride,
+                         out_dev);
   }
   LFE_HIP(hipGetLastError());
   return allreduce_sum_f64(c, out_dev, (size_t)pstride);
@@ -2189,8 +2225,10 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
       ar.clCmax = c->clf_cnt + G + 1;
       ar.clFlag = c->clf_cnt + G + 2;
     }
-    LFE_TRY(resid_rows_enqueue(c, ar, buf + 256, cl));
-    LFE_TRY(d2h_sync(c, h.data(), buf, sizeof(double) * 533));
+    const unsigned long long seq = c->world == 1 ? ++c->msg_seq : 0;
+    LFE_TRY(resid_rows_enqueue(c, ar, buf + 256, cl, seq ? buf : nullptr, 533, seq));
+    if (seq) LFE_TRY(host_msg_wait(c, seq, h.data(), 533));
+    else LFE_TRY(d2h_sync(c, h.data(), buf, sizeof(double) * 533));
     if (pass == 1 || h[532] == 1.0) break;  // guard failed: the explicit design pass
   }
   if (h[516] != 1.0) return 1;  // not positive definite: the caller takes the two-call path
