@@ -376,8 +376,11 @@ int lfe_sync(lfe_ctx* ctx);
 int lfe_shard_rows(lfe_ctx* ctx, int64_t* n_out);
 
 /* Per-phase device times (ms) of the last lfe_* calls, measured with HIP
- * events on the context's stream: [prep, demean, gram, resid, cluster, last_kernel]. */
+ * events on the context's stream: [prep, demean, gram, resid, cluster, last_kernel].
+ * Only while lfe_phase_timing(ctx, 1) is on (else zeros): every event record costs host time
+ * on the launch path. */
 int lfe_timings(lfe_ctx* ctx, double* out6);
+int lfe_phase_timing(lfe_ctx* ctx, int enable);
 
 /* Per-kernel HIP-event timing on the context's stream.  lfe_profile(ctx, 1)
  * resets and enables it (each launch is bracketed by an event pair; adds no

@@ -87,6 +87,7 @@ SIGNATURES = {
     "lfe_sync": (C.c_int, [_vp]),
     "lfe_shard_rows": (C.c_int, [_vp, _i64p]),
     "lfe_timings": (C.c_int, [_vp, _dp]),
+    "lfe_phase_timing": (C.c_int, [_vp, C.c_int]),
     "lfe_profile": (C.c_int, [_vp, C.c_int]),
     "lfe_kernel_stats": (C.c_int, [_vp, C.c_int, C.c_char_p, _dp, _i64p, _i32p]),
     "lfe_last_error": (C.c_char_p, []),
@@ -631,6 +632,10 @@ class Engine:
         return int(v.value)
     def profile(self, enable: bool = True) -> None:
         _check(self._lib.lfe_profile(self._h, 1 if enable else 0))
+
+    def phase_timing(self, enable: bool = True) -> None:
+        """Per-phase device times for timings() (off by default: event records cost host time)."""
+        _check(self._lib.lfe_phase_timing(self._h, 1 if enable else 0))
 
     def kernel_stats(self) -> dict:
         """{kernel name: (total ms, launches)} since the last profile(True)."""

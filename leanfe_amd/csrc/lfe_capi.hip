@@ -632,8 +632,12 @@ enum { PH_PREP, PH_DEMEAN, PH_GRAM, PH_RESID, PH_CLUSTER };
 struct PhaseTimer {
   lfe_ctx* c;
   int ph;
-  PhaseTimer(lfe_ctx* c_, int ph_) : c(c_), ph(ph_) { (void)hipEventRecord(c->tm.ev[ph][0], c->stream); }
+  // (opt-in, lfe_phase_timing: an event record costs several µs of host time, on the launch path)
+  PhaseTimer(lfe_ctx* c_, int ph_) : c(c_), ph(ph_) {
+    if (c->tm.on) (void)hipEventRecord(c->tm.ev[ph][0], c->stream);
+  }
   ~PhaseTimer() {
+    if (!c->tm.on) return;
     (void)hipEventRecord(c->tm.ev[ph][1], c->stream);
     c->tm.pending |= 1u << ph;
     c->tm.last_phase = ph;
@@ -700,7 +704,6 @@ int lfe_ctx_create(lfe_ctx** out, int device) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->hpin_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->side_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->up_ev0, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->up_ev1, hipEventDisableTiming) != hipSuccess ||
@@ -756,7 +759,6 @@ void lfe_ctx_destroy(lfe_ctx* c) {
   for (auto& e : c->load_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->aux_ev) (void)hipEventDestroy(c->aux_ev);
-  if (c->side_ev) (void)hipEventDestroy(c->side_ev);
   if (c->up_ev0) (void)hipEventDestroy(c->up_ev0);
   if (c->up_ev1) (void)hipEventDestroy(c->up_ev1);
   if (c->up_stream) (void)hipStreamDestroy(c->up_stream);
@@ -1453,6 +1455,12 @@ int lfe_profile(lfe_ctx* c, int enable) {
     c->prof.count[k] = 0;
   }
   c->prof.on = enable != 0;
+  return LFE_OK;
+}
+
+int lfe_phase_timing(lfe_ctx* c, int enable) {
+  if (!c) return fail(LFE_EINVAL, "null context");
+  c->tm.on = enable != 0;
   return LFE_OK;
 }
 

@@ -185,6 +185,7 @@ struct Timings {
   hipEvent_t ev[5][2] = {};
   unsigned pending = 0;  // phases whose events are not read yet
   int last_phase = -1;
+  bool on = false;       // lfe_phase_timing
 };
 
 // Row layout used by every pass after the singleton drop: rows grouped by
@@ -340,7 +341,6 @@ struct lfe_ctx {
   unsigned long long msg_seq = 0;
   hipEvent_t hpin_ev = nullptr;    // last H2D from the staging region
   hipEvent_t aux_ev = nullptr;     // completion of an asynchronous D2H into the staging region
-  hipEvent_t side_ev = nullptr;    // main-stream point a side-stream D2H waits for (prepare_layout's bucket starts)
   // the layout's work-item upload runs on its own stream while the partition scatter runs:
   // up_ev0 (main stream, before the scatter: earlier readers of items_d are done), up_ev1 (upload done)
   hipStream_t up_stream = nullptr;

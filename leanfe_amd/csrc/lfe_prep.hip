@@ -1230,8 +1230,9 @@ int prepare_layout(lfe_ctx* c) {
     int32_t* dbstart = c->pcounts + m;
     LFE_TRY(exclusive_scan_g(c, c->pcounts, m, nullptr, 0, dbstart, nw, nb));
     // (read on the side stream below, after the scatter is enqueued: no copy enqueue between the
-    // scan and the scatter on the main stream, whose GPU time it was)
-    LFE_HIP(hipEventRecord(c->side_ev, c->stream));
+    // scan and the scatter on the main stream, whose GPU time it was).  One event after the scan
+    // serves both side-stream jobs: the bucket starts are final, and items_d is free (build_items)
+    LFE_HIP(hipEventRecord(c->up_ev0, c->stream));
     const size_t lds = std::min<size_t>(std::max(part_lds(nth), kLdsMin), 160 * 1024);
     L.part = PartGeom{nth, per, nw, lds};
     // the input row index of each layout row is written only when a caller needs it
@@ -1246,9 +1247,8 @@ int prepare_layout(lfe_ctx* c) {
       W.lay_cap.resize(m, 0);
       for (int j = 0; j < m; ++j) LFE_TRY(ensure_i32(c, W.lay[j], W.lay_cap[j], (size_t)c->ld));
     }
-    LFE_HIP(hipEventRecord(c->up_ev0, c->stream));  // items_d is free from here (build_items)
     LFE_TRY(launch_part_scatter(c, /*cols=*/c->sw.on ? 2 : 1, /*orig=*/0));
-    LFE_HIP(hipStreamWaitEvent(c->up_stream, c->side_ev, 0));  // the scan is done
+    LFE_HIP(hipStreamWaitEvent(c->up_stream, c->up_ev0, 0));  // the scan is done
     LFE_HIP(hipMemcpyAsync(c->hpin, dbstart, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->up_stream));
     LFE_HIP(hipEventRecord(c->aux_ev, c->up_stream));
     W.lay_valid = W.lay_move;

@@ -29,7 +29,10 @@ _VERBOSE = os.environ.get("LEANFE_HIP_VERBOSE", "0") not in ("", "0")  # log lin
 #   stream_batch  rows per streamed Parquet batch
 #   reshard       sharded two-FE fits move contiguous row blocks to owner ranks (lfe_reshard_owner)
 #   context_rows  rows per engine context (None: 2^31 - 64, the int32 row-index cap)
-KNOBS = {"out_of_core": False, "stream": True, "stream_batch": 1 << 22, "reshard": True, "context_rows": None}
+#   phase_timing  the engine's per-phase device times in LeanFEResult.timings (HIP events: host time
+#                 on the launch path; also on with LEANFE_HIP_VERBOSE)
+KNOBS = {"out_of_core": False, "stream": True, "stream_batch": 1 << 22, "reshard": True, "context_rows": None,
+         "phase_timing": False}
 
 
 def _default_device() -> int:
@@ -138,6 +141,8 @@ def leanfe_hip(data, demean_tol: float = 1e-6, y_col: str | None = None, x_cols:
 
     own_engine = engine is None
     eng = engine if engine is not None else Engine(_default_device() if device is None else device)
+    if KNOBS["phase_timing"] or _VERBOSE:
+        eng.phase_timing(True)
     try:
         # FE codes (polars_impl.py:118-139); sparse integer ids are factorized on the GPU
         codes, levels = [], []

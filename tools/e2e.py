@@ -20,6 +20,8 @@ sys.path.insert(0, ROOT)
 
 from leanfe_amd import hip_impl, leanfe_hip, synth  # noqa: E402
 
+hip_impl.KNOBS["phase_timing"] = True  # the per-phase device times in the printed lines
+
 
 def main():
     ap = argparse.ArgumentParser()
