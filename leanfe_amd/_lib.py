@@ -415,29 +415,49 @@ class Engine:
 
     FIT_VCOV = {"iid": 0, "hc1": 1, "cluster": 2}
 
-    def fit(self, vcov: str, tol: float = 1e-6, max_iter: int = 50, check_from: int = 3, drop: bool = True) -> dict:
-        """One whole regression in one C call (lfe_fit): [singleton drop], projections with the FEs
-        ordered by cardinality, Gram + device solve + residual pass, host solve and the IID / HC1
-        SEs; 'cluster' keeps the score rows for cluster_meat* (se is then None).  Unweighted,
-        resident, no instruments."""
-        v = self.FIT_VCOV[vcov.lower()]
+    def _fit_bufs(self, v: int, drop: bool, tol: float, max_iter: int, check_from: int):
+        """Output buffers and the ctypes argument tuple of lfe_fit, built once per shape and options
+        (the call sits between two solves on the GPU's critical path: ~20 us of argument conversion
+        and allocation per call otherwise)."""
+        if self._h is None:
+            raise RuntimeError("engine is closed")
+        key = (self._h, self.F, self.p, v, drop, tol, max_iter, check_from)
+        cache = self.__dict__.setdefault("_fit_cache", {})
+        hit = cache.get(key)
+        if hit is not None:
+            return hit
         F, p = self.F, self.p
         k, D = p - 1, p + 1
         ints = np.zeros(4 + 2 * F, dtype=np.int64)
         buf = np.zeros(D * D + p + p * p + 4 + k * k + k + 2)
-        o = np.cumsum([0, D * D, p, p * p, 4, k * k, k])
+        o = [int(x) for x in np.cumsum([0, D * D, p, p * p, 4, k * k, k])]
         b = buf.ctypes.data
-        _check(self._lib.lfe_fit(self._h, 1 if drop else 0, float(tol), int(max_iter), int(check_from), v,
-                                 ints.ctypes.data, b, b + 8 * int(o[1]), b + 8 * int(o[2]), b + 8 * int(o[3]),
-                                 b + 8 * int(o[4]), b + 8 * int(o[5]), b + 8 * int(o[6])))
+        args = (C.c_void_p(self._h), C.c_int(1 if drop else 0), C.c_double(tol), C.c_int(max_iter),
+                C.c_int(check_from), C.c_int(v), C.c_void_p(ints.ctypes.data),
+                *[C.c_void_p(b + 8 * o[i]) for i in range(7)])
+        fn = self._lib.lfe_fit
+        hit = cache[key] = (fn, args, ints, buf, o)
+        return hit
+
+    def fit(self, vcov: str, tol: float = 1e-6, max_iter: int = 50, check_from: int = 3, drop: bool = True) -> dict:
+        """One whole regression in one C call (lfe_fit): [singleton drop], projections with the FEs
+        ordered by cardinality, Gram + device solve + residual pass, host solve and the IID / HC1
+        SEs; 'cluster' keeps the score rows for cluster_meat* (se is then None).  Unweighted,
+        resident, no instruments.  The returned arrays are copies."""
+        v = self.FIT_VCOV[vcov.lower()]
+        fn, args, ints, buf, o = self._fit_bufs(v, drop, float(tol), int(max_iter), int(check_from))
+        _check(fn(*args))
+        F, p = self.F, self.p
+        k, D = p - 1, p + 1
         if v == 2:
             self._score_k = k
+        out = buf.copy()
         return dict(n_obs=int(ints[0]), iterations=int(ints[1]), df_resid=int(ints[2]), fused=bool(ints[3]),
-                    fe_dims=tuple(int(x) for x in ints[4:4 + F]), fe_card=tuple(int(x) for x in ints[4 + F:]),
-                    gram=buf[:o[1]].reshape(D, D), beta_full=buf[o[1]:o[2]], xtx_inv=buf[o[2]:o[3]].reshape(p, p),
-                    stats=buf[o[3]:o[4]], meat=buf[o[4]:o[5]].reshape(k, k) if v == 1 else None,
-                    se=buf[o[5]:o[6]] if v != 2 else None, last_check=float(buf[o[6]]),
-                    beta_dev_vs_host=float(buf[o[6] + 1]))
+                    fe_dims=tuple(ints[4:4 + F].tolist()), fe_card=tuple(ints[4 + F:].tolist()),
+                    gram=out[:o[1]].reshape(D, D), beta_full=out[o[1]:o[2]], xtx_inv=out[o[2]:o[3]].reshape(p, p),
+                    stats=out[o[3]:o[4]], meat=out[o[4]:o[5]].reshape(k, k) if v == 1 else None,
+                    se=out[o[5]:o[6]] if v != 2 else None, last_check=float(out[o[6]]),
+                    beta_dev_vs_host=float(out[o[6] + 1]))
 
     def cluster_meat(self) -> tuple[np.ndarray, np.ndarray]:
         k = getattr(self, "_score_k", self.p - 1)

@@ -132,6 +132,17 @@ int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals) {
   return LFE_OK;
 }
 
+int host_msg_wait_i32(lfe_ctx* c, unsigned long long seq, int32_t* vals, int n) {
+  std::vector<double> w((size_t)(n + 1) / 2);
+  LFE_TRY(host_msg_wait(c, seq, w.data(), (int)w.size()));
+  for (int i = 0; i < n; ++i) {
+    unsigned long long b;
+    memcpy(&b, &w[(size_t)i / 2], sizeof(b));
+    vals[i] = (int32_t)(uint32_t)(i % 2 ? b >> 32 : b & 0xffffffffull);
+  }
+  return LFE_OK;
+}
+
 int d2h_wait(lfe_ctx* c, void* dst, size_t bytes) {
   LFE_HIP(hipEventSynchronize(c->aux_ev));  // work enqueued after the copy keeps running
   memcpy(dst, c->hpin, bytes);

@@ -689,6 +689,7 @@ int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes);
 int d2h_async(lfe_ctx* c, const void* src_dev, size_t bytes);
 int d2h_wait(lfe_ctx* c, void* dst, size_t bytes);
 int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals);
+int host_msg_wait_i32(lfe_ctx* c, unsigned long long seq, int32_t* vals, int n);
 // host -> device copy of a small argument through pinned staging (asynchronous)
 int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes);
 // pinned upload buffer of at least `bytes` (work items)
@@ -817,6 +818,19 @@ __device__ __forceinline__ void host_msg_publish(unsigned long long* msg, unsign
   for (int i = 0; i < nv; ++i)
     __hip_atomic_store(&msg[1 + i], (unsigned long long)__double_as_longlong(v[i]), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&msg[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ... and n int32 values (agent-scope loads of what other workgroups wrote), two per message word
+__device__ __forceinline__ void host_msg_publish_i32(unsigned long long* msg, unsigned long long seq,
+                                                     const int32_t* v, int n) {
+  for (int i = 0; i < n; i += 2) {
+    const unsigned int lo = (unsigned int)__hip_atomic_load(&v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int hi =
+        i + 1 < n ? (unsigned int)__hip_atomic_load(&v[i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    __hip_atomic_store(&msg[1 + i / 2], ((unsigned long long)hi << 32) | lo, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __hip_atomic_store(&msg[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

@@ -862,6 +862,11 @@ struct FinishCountsArgs {
   double* colq;      // [p] the columns' sums of squares
   double* fq;
   unsigned int* done;
+  // one rank: the last workgroup publishes the count scratch (iscratch[0, kIscratchInts)) to the
+  // host message - no copy kernel and no event between the drop and the group sums
+  const int32_t* is;
+  unsigned long long* msg;
+  unsigned long long seq;
 };
 
 __global__ void k_finish_counts(FinishCountsArgs a, int F) {
@@ -903,13 +908,16 @@ __global__ void k_finish_counts(FinishCountsArgs a, int F) {
     }
   }
   if (!a.done || !last_block_done(a.done)) return;
-  int N = 1;
-  for (int g = 0; g < F; ++g) N = max(N, __hip_atomic_load(&a.cmax[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  for (int c = threadIdx.x; c < a.p; c += blockDim.x) {
-    const double M = __longlong_as_double(reinterpret_cast<const long long*>(a.st)[c]);
-    const double rms = a.n > 0 ? sqrt(a.colq[c] / (double)a.n) : 0.0;
-    fix_quanta_col(M, rms, (double)N, a.fq, c);
+  if (a.st) {
+    int N = 1;
+    for (int g = 0; g < F; ++g) N = max(N, __hip_atomic_load(&a.cmax[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int c = threadIdx.x; c < a.p; c += blockDim.x) {
+      const double M = __longlong_as_double(reinterpret_cast<const long long*>(a.st)[c]);
+      const double rms = a.n > 0 ? sqrt(a.colq[c] / (double)a.n) : 0.0;
+      fix_quanta_col(M, rms, (double)N, a.fq, c);
+    }
   }
+  if (a.msg && threadIdx.x == 0) host_msg_publish_i32(a.msg, a.seq, a.is, kIscratchInts);
 }
 
 // multi-rank: the kept rows and (owner-sharded) the primary FE's level counts summed over ranks
@@ -1305,6 +1313,7 @@ int prepare_layout(lfe_ctx* c) {
   for (int f = 0; f < c->F; ++f)
     if (!(c->owner_on && f == L.P)) LFE_TRY(allreduce_sum_i32(c, c->fe[f].cnt_pre, c->fe[f].G));
 
+  unsigned long long is_seq = 0;  // the counts published to the host message (k_finish_counts)
   // ---- single-pass singleton drop: mark, then kept counts = pre - drops ----
   int32_t* ndropped = c->iscratch + 2 * kMaxFE;
   if (c->F > 0) {
@@ -1368,9 +1377,15 @@ int prepare_layout(lfe_ctx* c) {
       fa.done = c->gsync + GS_FINISH;
       c->fixq_ready = true;
     }
+    if (c->world == 1) {  // the counts to the host by the last workgroup
+      fa.is = c->iscratch;
+      fa.msg = c->dmsg;
+      fa.seq = is_seq = ++c->msg_seq;
+      fa.done = c->gsync + GS_FINISH;
+    }
     if (c->F > 0) {
       // few blocks: thousands of same-address adds would serialize
-      hipLaunchKernelGGL(k_finish_counts, dim3(grid_for(gmax, kBlock, 32), c->F + (fa.done ? 1 : 0)), dim3(kBlock), 0,
+      hipLaunchKernelGGL(k_finish_counts, dim3(grid_for(gmax, kBlock, 32), c->F + (fa.st ? 1 : 0)), dim3(kBlock), 0,
                          c->stream, fa, c->F);
       LFE_HIP(hipGetLastError());
     }
@@ -1385,14 +1400,15 @@ int prepare_layout(lfe_ctx* c) {
     LFE_HIP(hipGetLastError());
   }
   int32_t h[kIscratchInts];  // dims / card per FE, dropped rows, kept sums, largest kept counts
-  LFE_TRY(d2h_async(c, c->iscratch, sizeof(h)));
+  if (!is_seq) LFE_TRY(d2h_async(c, c->iscratch, sizeof(h)));
   // the constant group sums S_f do not depend on the FE order: enqueue them now so the
   // GPU keeps working while the host reads the counts and returns (lfe_demean skips them)
   if (c->F > 0 && c->n > 0 && !c->sw.on) {  // streamed X: the sums come from lfe_stream pass 1
     LFE_TRY(sweep_group_sums(c));
     c->sums_ready = true;
   }
-  LFE_TRY(d2h_wait(c, h, sizeof(h)));
+  if (is_seq) LFE_TRY(host_msg_wait_i32(c, is_seq, h, kIscratchInts));
+  else LFE_TRY(d2h_wait(c, h, sizeof(h)));
   for (int f = 0; f < c->F; ++f) {
     c->fe[f].dims = h[2 * f];
     c->fe[f].card = h[2 * f + 1];
