@@ -421,7 +421,8 @@ class Engine:
         and allocation per call otherwise)."""
         if self._h is None:
             raise RuntimeError("engine is closed")
-        key = (self._h, self.F, self.p, v, drop, tol, max_iter, check_from)
+        h = self._h.value if isinstance(self._h, C.c_void_p) else self._h
+        key = (h, self.F, self.p, v, drop, tol, max_iter, check_from)
         cache = self.__dict__.setdefault("_fit_cache", {})
         hit = cache.get(key)
         if hit is not None:
@@ -432,7 +433,7 @@ class Engine:
         buf = np.zeros(D * D + p + p * p + 4 + k * k + k + 2)
         o = [int(x) for x in np.cumsum([0, D * D, p, p * p, 4, k * k, k])]
         b = buf.ctypes.data
-        args = (C.c_void_p(self._h), C.c_int(1 if drop else 0), C.c_double(tol), C.c_int(max_iter),
+        args = (C.c_void_p(h), C.c_int(1 if drop else 0), C.c_double(tol), C.c_int(max_iter),
                 C.c_int(check_from), C.c_int(v), C.c_void_p(ints.ctypes.data),
                 *[C.c_void_p(b + 8 * o[i]) for i in range(7)])
         fn = self._lib.lfe_fit
