@@ -835,8 +835,8 @@ __device__ __forceinline__ void host_msg_publish_i32(unsigned long long* msg, un
 }
 
 constexpr int kGsyncSlots = 16;
-constexpr size_t kHostMsgBytes = 8192;  // lfe_ctx::hmsg: the sequence word and up to 1023 values
-enum GsyncSlot { GS_TABLES_GRAM = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4, GS_SCAN = 5, GS_TQ_REDUCE = 6 };
+constexpr size_t kHostMsgBytes = 16384;  // lfe_ctx::hmsg: the sequence word and up to 2047 values
+enum GsyncSlot { GS_TABLES_GRAM = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4, GS_SCAN = 5, GS_TQ_REDUCE = 6, GS_SCAN_DONE = 7 };
 __device__ __forceinline__ bool last_block_done(unsigned int* counter) {
   __shared__ unsigned int amlast;
   __syncthreads();

@@ -317,7 +317,9 @@ __global__ __launch_bounds__(1024) void k_scan_one(ScanPair sp, int32_t* __restr
 // zeroing between launches: a word of another epoch reads as not yet published.
 __global__ __launch_bounds__(256) void k_scan_fused(ScanPair sp, unsigned long long* __restrict__ status,
                                                     unsigned int* __restrict__ ticket, unsigned int epoch, int nblocks,
-                                                    int32_t* __restrict__ gout, int64_t gstride, int gn) {
+                                                    int32_t* __restrict__ gout, int64_t gstride, int gn,
+                                                    unsigned int* __restrict__ done, unsigned long long* __restrict__ msg,
+                                                    unsigned long long seq) {
   __shared__ int32_t tmp[8];
   __shared__ int32_t total;
   __shared__ int id_s;
@@ -366,10 +368,12 @@ __global__ __launch_bounds__(256) void k_scan_fused(ScanPair sp, unsigned long l
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k)
       if (base + k < m && (base + k) % gstride == 0 && (base + k) / gstride < gn) gout[(base + k) / gstride] = o8[k];
+  // the gathered values (the partition's bucket starts) to the host message by the last block
+  if (msg && last_block_done(done) && threadIdx.x == 0) host_msg_publish_i32(msg, seq, gout, gn);
 }
 
 static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2, int32_t* gout,
-                            int64_t gstride, int gn) {
+                            int64_t gstride, int gn, unsigned long long* gout_seq = nullptr) {
   const int64_t nb1 = (m1 + kScanBlock - 1) / kScanBlock, nb2 = a2 ? (m2 + kScanBlock - 1) / kScanBlock : 0;
   const int64_t nblocks = nb1 + nb2;
   if (nblocks == 0) return LFE_OK;
@@ -387,8 +391,12 @@ static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, in
       c->scan_epoch = 0;
     }
     if (++c->scan_epoch == 0) c->scan_epoch = 1;  // (0 is the zeroed buffer's tag)
+    // gout_seq: the gathered values to the host message (one rank, fits the message)
+    const bool msg = gout_seq && gout && c->world == 1 && (size_t)(gn + 1) / 2 + 1 <= kHostMsgBytes / 8;
+    if (msg) *gout_seq = ++c->msg_seq;
     hipLaunchKernelGGL(k_scan_fused, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->scan_status,
-                       c->gsync + GS_SCAN, c->scan_epoch, (int)nblocks, gout, gstride, gn);
+                       c->gsync + GS_SCAN, c->scan_epoch, (int)nblocks, gout, gstride, gn, c->gsync + GS_SCAN_DONE,
+                       msg ? c->dmsg : nullptr, msg ? *gout_seq : 0ull);
     LFE_HIP(hipGetLastError());
     return LFE_OK;
   }
@@ -1018,14 +1026,10 @@ static int build_items(lfe_ctx* c, bool side) {
   memcpy(c->hpin_items + ib, bfirst.data(), bb);
   memcpy(c->hpin_items + ib + bb, xg.data(), xb);
   memcpy(c->hpin_items + ib + bb + xb, bl.data(), lb);
-  if (side) {
-    LFE_HIP(hipStreamWaitEvent(c->up_stream, c->up_ev0, 0));
-    LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb + lb, hipMemcpyHostToDevice, c->up_stream));
-    LFE_HIP(hipEventRecord(c->up_ev1, c->up_stream));
-    LFE_HIP(hipStreamWaitEvent(c->stream, c->up_ev1, 0));
-  } else {
-    LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb + lb, hipMemcpyHostToDevice, c->stream));
-  }
+  // on the main stream, behind the partition scatter (a few KB: the copy that follows the scatter
+  // costs less than the cross-stream wait that let it overlap, ~10 us of barrier at small shards)
+  (void)side;
+  LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb + lb, hipMemcpyHostToDevice, c->stream));
   return LFE_OK;
 }
 
@@ -1236,11 +1240,11 @@ int prepare_layout(lfe_ctx* c) {
     // bucket starts depend on the scan only (gathered by its last kernel): fetch them now and
     // build the work items on the host while the GPU runs the scatter
     int32_t* dbstart = c->pcounts + m;
-    LFE_TRY(exclusive_scan_g(c, c->pcounts, m, nullptr, 0, dbstart, nw, nb));
-    // (read on the side stream below, after the scatter is enqueued: no copy enqueue between the
-    // scan and the scatter on the main stream, whose GPU time it was).  One event after the scan
-    // serves both side-stream jobs: the bucket starts are final, and items_d is free (build_items)
-    LFE_HIP(hipEventRecord(c->up_ev0, c->stream));
+    unsigned long long bseq = 0;  // the scan's last block publishes the bucket starts (one rank)
+    LFE_TRY(exclusive_scan_g(c, c->pcounts, m, nullptr, 0, dbstart, nw, nb, &bseq));
+    // (else read on the side stream below, after the scatter is enqueued: no copy enqueue between
+    // the scan and the scatter on the main stream, whose GPU time it was)
+    if (!bseq) LFE_HIP(hipEventRecord(c->up_ev0, c->stream));
     const size_t lds = std::min<size_t>(std::max(part_lds(nth), kLdsMin), 160 * 1024);
     L.part = PartGeom{nth, per, nw, lds};
     // the input row index of each layout row is written only when a caller needs it
@@ -1256,15 +1260,18 @@ int prepare_layout(lfe_ctx* c) {
       for (int j = 0; j < m; ++j) LFE_TRY(ensure_i32(c, W.lay[j], W.lay_cap[j], (size_t)c->ld));
     }
     LFE_TRY(launch_part_scatter(c, /*cols=*/c->sw.on ? 2 : 1, /*orig=*/0));
-    LFE_HIP(hipStreamWaitEvent(c->up_stream, c->up_ev0, 0));  // the scan is done
-    LFE_HIP(hipMemcpyAsync(c->hpin, dbstart, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->up_stream));
-    LFE_HIP(hipEventRecord(c->aux_ev, c->up_stream));
+    if (!bseq) {
+      LFE_HIP(hipStreamWaitEvent(c->up_stream, c->up_ev0, 0));  // the scan is done
+      LFE_HIP(hipMemcpyAsync(c->hpin, dbstart, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->up_stream));
+      LFE_HIP(hipEventRecord(c->aux_ev, c->up_stream));
+    }
     W.lay_valid = W.lay_move;
     W.lay_move = false;
     L.orig_pending = true;
     LFE_HIP(hipGetLastError());
     L.bstart.assign(nb + 1, 0);
-    LFE_TRY(d2h_wait(c, L.bstart.data(), sizeof(int32_t) * nb));
+    if (bseq) LFE_TRY(host_msg_wait_i32(c, bseq, L.bstart.data(), nb));
+    else LFE_TRY(d2h_wait(c, L.bstart.data(), sizeof(int32_t) * nb));
     L.bstart[nb] = (int32_t)n;
     L.X = c->sw.on ? nullptr : c->Xp;
     L.w = c->w ? c->wp : nullptr;
