@@ -132,6 +132,12 @@ int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals) {
   return LFE_OK;
 }
 
+bool host_msg_on(const lfe_ctx* c) {
+  if (c->world != 1) return false;
+  const char* e = knob("LFE_HOST_MSG");
+  return !(e && e[0] == '0');
+}
+
 int host_msg_wait_i32(lfe_ctx* c, unsigned long long seq, int32_t* vals, int n) {
   std::vector<double> w((size_t)(n + 1) / 2);
   LFE_TRY(host_msg_wait(c, seq, w.data(), (int)w.size()));

@@ -2225,7 +2225,7 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
       ar.clCmax = c->clf_cnt + G + 1;
       ar.clFlag = c->clf_cnt + G + 2;
     }
-    const unsigned long long seq = c->world == 1 ? ++c->msg_seq : 0;
+    const unsigned long long seq = host_msg_on(c) ? ++c->msg_seq : 0;
     LFE_TRY(resid_rows_enqueue(c, ar, buf + 256, cl, seq ? buf : nullptr, 533, seq));
     if (seq) LFE_TRY(host_msg_wait(c, seq, h.data(), 533));
     else LFE_TRY(d2h_sync(c, h.data(), buf, sizeof(double) * 533));

@@ -689,6 +689,8 @@ int d2h_sync(lfe_ctx* c, void* dst, const void* src_dev, size_t bytes);
 int d2h_async(lfe_ctx* c, const void* src_dev, size_t bytes);
 int d2h_wait(lfe_ctx* c, void* dst, size_t bytes);
 int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals);
+// small device results go to the host through the mapped message (one rank; knob LFE_HOST_MSG=0: copies)
+bool host_msg_on(const lfe_ctx* c);
 int host_msg_wait_i32(lfe_ctx* c, unsigned long long seq, int32_t* vals, int n);
 // host -> device copy of a small argument through pinned staging (asynchronous)
 int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes);

@@ -392,7 +392,7 @@ static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, in
     }
     if (++c->scan_epoch == 0) c->scan_epoch = 1;  // (0 is the zeroed buffer's tag)
     // gout_seq: the gathered values to the host message (one rank, fits the message)
-    const bool msg = gout_seq && gout && c->world == 1 && (size_t)(gn + 1) / 2 + 1 <= kHostMsgBytes / 8;
+    const bool msg = gout_seq && gout && host_msg_on(c) && (size_t)(gn + 1) / 2 + 1 <= kHostMsgBytes / 8;
     if (msg) *gout_seq = ++c->msg_seq;
     hipLaunchKernelGGL(k_scan_fused, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->scan_status,
                        c->gsync + GS_SCAN, c->scan_epoch, (int)nblocks, gout, gstride, gn, c->gsync + GS_SCAN_DONE,
@@ -1384,7 +1384,7 @@ int prepare_layout(lfe_ctx* c) {
       fa.done = c->gsync + GS_FINISH;
       c->fixq_ready = true;
     }
-    if (c->world == 1) {  // the counts to the host by the last workgroup
+    if (host_msg_on(c)) {  // the counts to the host by the last workgroup
       fa.is = c->iscratch;
       fa.msg = c->dmsg;
       fa.seq = is_seq = ++c->msg_seq;
