@@ -114,19 +114,32 @@ int d2h_async(lfe_ctx* c, const void* src_dev, size_t bytes) {
   return LFE_OK;
 }
 
-// the values a kernel published with host_msg_publish under sequence number seq; a bounded spin (the
-// stream is synchronized after ~2 s without the message, which then must be there)
-int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals) {
-  for (long spin = 0;; ++spin) {
-    if (__atomic_load_n(&c->hmsg[0], __ATOMIC_ACQUIRE) == seq) break;
-    if (spin == (1l << 26)) {
-      LFE_HIP(hipStreamSynchronize(c->stream));
-      if (__atomic_load_n(&c->hmsg[0], __ATOMIC_ACQUIRE) != seq) return fail(LFE_EHIP, "device message lost");
-      break;
+// the n tagged words a kernel published under sequence number seq; a bounded spin per word (the
+// stream is synchronized after ~2 s without it, which then must be there)
+static int host_msg_words(lfe_ctx* c, unsigned long long seq, unsigned int* out, int n) {
+  const unsigned long long tag = seq & 0xffffffffull;
+  if ((size_t)n > kHostMsgBytes / 8) return fail(LFE_EINVAL, "host message too long");
+  for (int i = 0; i < n; ++i) {
+    unsigned long long w = __atomic_load_n(&c->hmsg[i], __ATOMIC_ACQUIRE);
+    for (long spin = 0; (w >> 32) != tag; ++spin) {
+      if (spin == (1l << 26)) {
+        LFE_HIP(hipStreamSynchronize(c->stream));
+        w = __atomic_load_n(&c->hmsg[i], __ATOMIC_ACQUIRE);
+        if ((w >> 32) != tag) return fail(LFE_EHIP, "device message lost");
+        break;
+      }
+      w = __atomic_load_n(&c->hmsg[i], __ATOMIC_ACQUIRE);
     }
+    out[i] = (unsigned int)w;
   }
+  return LFE_OK;
+}
+
+int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals) {
+  std::vector<unsigned int> w((size_t)2 * nvals);
+  LFE_TRY(host_msg_words(c, seq, w.data(), 2 * nvals));
   for (int i = 0; i < nvals; ++i) {
-    const unsigned long long b = __atomic_load_n(&c->hmsg[1 + i], __ATOMIC_RELAXED);
+    const unsigned long long b = (unsigned long long)w[2 * i] | ((unsigned long long)w[2 * i + 1] << 32);
     memcpy(&vals[i], &b, sizeof(double));
   }
   return LFE_OK;
@@ -139,13 +152,9 @@ bool host_msg_on(const lfe_ctx* c) {
 }
 
 int host_msg_wait_i32(lfe_ctx* c, unsigned long long seq, int32_t* vals, int n) {
-  std::vector<double> w((size_t)(n + 1) / 2);
-  LFE_TRY(host_msg_wait(c, seq, w.data(), (int)w.size()));
-  for (int i = 0; i < n; ++i) {
-    unsigned long long b;
-    memcpy(&b, &w[(size_t)i / 2], sizeof(b));
-    vals[i] = (int32_t)(uint32_t)(i % 2 ? b >> 32 : b & 0xffffffffull);
-  }
+  std::vector<unsigned int> w((size_t)n);
+  LFE_TRY(host_msg_words(c, seq, w.data(), n));
+  for (int i = 0; i < n; ++i) vals[i] = (int32_t)w[i];
   return LFE_OK;
 }
 

@@ -787,15 +787,11 @@ __global__ __launch_bounds__(256) void k_reduce_partials_msg(const double* __res
   }
   if (threadIdx.x == 0) out[e] = red[0];
   if (!last_block_done(done)) return;
-  for (int i = threadIdx.x; i < count; i += 256)
-    __hip_atomic_store(&msg[1 + i],
-                       (unsigned long long)__double_as_longlong(__hip_atomic_load(&src[i], __ATOMIC_RELAXED,
-                                                                                  __HIP_MEMORY_SCOPE_AGENT)),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    __hip_atomic_store(&msg[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int i = threadIdx.x; i < count; i += 256) {
+    const unsigned long long b =
+        (unsigned long long)__double_as_longlong(__hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    host_msg_word(msg, 2 * i, seq, (unsigned int)b);
+    host_msg_word(msg, 2 * i + 1, seq, (unsigned int)(b >> 32));
   }
 }
 
@@ -2225,7 +2221,7 @@ int launch_gram_resid(lfe_ctx* c, double* host_gram, double* beta_full, double* 
       ar.clCmax = c->clf_cnt + G + 1;
       ar.clFlag = c->clf_cnt + G + 2;
     }
-    const unsigned long long seq = host_msg_on(c) ? ++c->msg_seq : 0;
+    const unsigned long long seq = host_msg_on(c) ? next_msg_seq(c) : 0;
     LFE_TRY(resid_rows_enqueue(c, ar, buf + 256, cl, seq ? buf : nullptr, 533, seq));
     if (seq) LFE_TRY(host_msg_wait(c, seq, h.data(), 533));
     else LFE_TRY(d2h_sync(c, h.data(), buf, sizeof(double) * 533));

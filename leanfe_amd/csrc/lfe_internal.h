@@ -691,6 +691,11 @@ int d2h_wait(lfe_ctx* c, void* dst, size_t bytes);
 int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals);
 // small device results go to the host through the mapped message (one rank; knob LFE_HOST_MSG=0: copies)
 bool host_msg_on(const lfe_ctx* c);
+// the next message's sequence number (its 32-bit tag is never 0: the zeroed buffer's)
+inline unsigned long long next_msg_seq(lfe_ctx* c) {
+  if (((++c->msg_seq) & 0xffffffffull) == 0) ++c->msg_seq;
+  return c->msg_seq;
+}
 int host_msg_wait_i32(lfe_ctx* c, unsigned long long seq, int32_t* vals, int n);
 // host -> device copy of a small argument through pinned staging (asynchronous)
 int h2d_small(lfe_ctx* c, void* dst_dev, const void* src, size_t bytes);
@@ -814,30 +819,29 @@ __device__ __forceinline__ double row16_reduce15(double v, double idv, Op op) {
 // exactly one workgroup - the last to arrive - which then sees every other workgroup's writes
 // (agent-scope release before the count, acquire after it).  *counter is 0 at launch and 0 again
 // when the last workgroup leaves, so a slot serves one launch at a time on its context's stream.
-// the last workgroup of a launch publishes nv values to the host message (lfe_ctx::dmsg): values
-// first, then the sequence number with a system-scope release (the host spins on it)
-__device__ __forceinline__ void host_msg_publish(unsigned long long* msg, unsigned long long seq, const double* v, int nv) {
-  for (int i = 0; i < nv; ++i)
-    __hip_atomic_store(&msg[1 + i], (unsigned long long)__double_as_longlong(v[i]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&msg[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// Host messages (lfe_ctx::dmsg, mapped coherent host memory): every word carries the low 32 bits of
+// the message's sequence number above 32 payload bits, so the host checks each word by itself and
+// the device needs no release fence (a system-scope release writes the whole L2 back): relaxed
+// system-scope stores only.  A double takes two words (low, high half).
+__device__ __forceinline__ void host_msg_word(unsigned long long* msg, int i, unsigned long long seq, unsigned int v) {
+  __hip_atomic_store(&msg[i], ((seq & 0xffffffffull) << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-
-// ... and n int32 values (agent-scope loads of what other workgroups wrote), two per message word
+__device__ __forceinline__ void host_msg_publish(unsigned long long* msg, unsigned long long seq, const double* v, int nv) {
+  for (int i = 0; i < nv; ++i) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v[i]);
+    host_msg_word(msg, 2 * i, seq, (unsigned int)b);
+    host_msg_word(msg, 2 * i + 1, seq, (unsigned int)(b >> 32));
+  }
+}
+// ... n int32 values (agent-scope loads of what other workgroups wrote), one word each
 __device__ __forceinline__ void host_msg_publish_i32(unsigned long long* msg, unsigned long long seq,
                                                      const int32_t* v, int n) {
-  for (int i = 0; i < n; i += 2) {
-    const unsigned int lo = (unsigned int)__hip_atomic_load(&v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int hi =
-        i + 1 < n ? (unsigned int)__hip_atomic_load(&v[i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    __hip_atomic_store(&msg[1 + i / 2], ((unsigned long long)hi << 32) | lo, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  __hip_atomic_store(&msg[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int i = 0; i < n; ++i)
+    host_msg_word(msg, i, seq, (unsigned int)__hip_atomic_load(&v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 constexpr int kGsyncSlots = 16;
-constexpr size_t kHostMsgBytes = 16384;  // lfe_ctx::hmsg: the sequence word and up to 2047 values
+constexpr size_t kHostMsgBytes = 16384;  // lfe_ctx::hmsg: 2048 tagged words (1024 doubles)
 enum GsyncSlot { GS_TABLES_GRAM = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4, GS_SCAN = 5, GS_TQ_REDUCE = 6, GS_SCAN_DONE = 7 };
 __device__ __forceinline__ bool last_block_done(unsigned int* counter) {
   __shared__ unsigned int amlast;

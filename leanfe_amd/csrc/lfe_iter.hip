@@ -1392,7 +1392,7 @@ int demean_fast(lfe_ctx* c, double tol, int max_iter, int check_from, int* itera
     const unsigned tq_grid = (unsigned)((m + kTqRedE - 1) / kTqRedE);
     unsigned long long seq = 0;  // the stop test published to mapped host memory (one rank)
     if (c->world == 1) {  // T_Q and the next Q projection in one launch
-      if (check && host_msg_on(c)) seq = ++c->msg_seq;
+      if (check && host_msg_on(c)) seq = next_msg_seq(c);
       {
         ProfScope _ps(c, K_TQ_REDUCE);
         hipLaunchKernelGGL(k_tq_reduce_fin, dim3(tq_grid), dim3(kTqRedE * kTqRedS), 0, c->stream, c->tq_runs,

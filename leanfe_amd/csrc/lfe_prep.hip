@@ -392,8 +392,8 @@ static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, in
     }
     if (++c->scan_epoch == 0) c->scan_epoch = 1;  // (0 is the zeroed buffer's tag)
     // gout_seq: the gathered values to the host message (one rank, fits the message)
-    const bool msg = gout_seq && gout && host_msg_on(c) && (size_t)(gn + 1) / 2 + 1 <= kHostMsgBytes / 8;
-    if (msg) *gout_seq = ++c->msg_seq;
+    const bool msg = gout_seq && gout && host_msg_on(c) && (size_t)gn <= kHostMsgBytes / 8;
+    if (msg) *gout_seq = next_msg_seq(c);
     hipLaunchKernelGGL(k_scan_fused, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->scan_status,
                        c->gsync + GS_SCAN, c->scan_epoch, (int)nblocks, gout, gstride, gn, c->gsync + GS_SCAN_DONE,
                        msg ? c->dmsg : nullptr, msg ? *gout_seq : 0ull);
@@ -1387,7 +1387,7 @@ int prepare_layout(lfe_ctx* c) {
     if (host_msg_on(c)) {  // the counts to the host by the last workgroup
       fa.is = c->iscratch;
       fa.msg = c->dmsg;
-      fa.seq = is_seq = ++c->msg_seq;
+      fa.seq = is_seq = next_msg_seq(c);
       fa.done = c->gsync + GS_FINISH;
     }
     if (c->F > 0) {
