@@ -339,6 +339,21 @@ int lfe_dev_alloc(lfe_ctx* ctx, int64_t n_doubles, double** dev_out);
 int lfe_dev_free(lfe_ctx* ctx, double* dev);
 int lfe_materialize(lfe_ctx* ctx, double* D, int64_t ldD, int first, int col0, int mask_col);
 int lfe_stream_materialize(lfe_ctx* ctx, double* D, int64_t ldD, int col0, int mask_col);
+/* Chunked wide fits (no resident D: the P n doubles of D cap a one-GPU fit near 3.5e8 rows at
+ * k = 100): the same for the rows [row0, row0 + rows) only, into D rows 0 .. rows - 1 (one chunk
+ * buffer for every column block); then lfe_wide_gram_rows / lfe_wide_resid_rows over that chunk
+ * (weights offset by row0), whose Grams, meats and statistics the caller adds in chunk order. */
+int lfe_stream_materialize_rows(lfe_ctx* ctx, double* D, int64_t ldD, int col0, int mask_col, int64_t row0,
+                                int64_t rows);
+int lfe_wide_gram_rows(lfe_ctx* ctx, const double* D, int64_t ldD, int64_t row0, int64_t rows, int c0, int P,
+                       int mode, const double* r, double* out);
+int lfe_wide_resid_rows(lfe_ctx* ctx, const double* D, int64_t ldD, int64_t row0, int64_t rows, int P,
+                        const double* coef, double* r, double* stats);
+/* A column block [c_lo, c_lo + p) of the K-regressor synthetic panel (column 0 = y, j = x_j; the
+ * generator of lfe_synth_load for any K, beta[K]) generated on the device for rows [row0, + rows)
+ * and streamed through the current pass (benchmarks and tests of wide streamed fits). */
+int lfe_stream_synth_cols(lfe_ctx* ctx, int64_t row0, int64_t rows, int K, int c_lo, const int32_t* n_levels,
+                          const double* beta, uint64_t seed);
 int lfe_wide_gram(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, int P, int mode, const double* r, double* out);
 int lfe_wide_resid(lfe_ctx* ctx, const double* D, int64_t ldD, int P, const double* coef, double* r, double* stats);
 int lfe_wide_cluster_meats(lfe_ctx* ctx, const double* D, int64_t ldD, int c0, int k, const double* r, int n_subsets,

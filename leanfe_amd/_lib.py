@@ -71,6 +71,10 @@ SIGNATURES = {
     "lfe_dev_free": (C.c_int, [_vp, _vp]),
     "lfe_materialize": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int]),
     "lfe_stream_materialize": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int]),
+    "lfe_stream_materialize_rows": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int64, C.c_int64]),
+    "lfe_wide_gram_rows": (C.c_int, [_vp, _vp, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _vp, _dp]),
+    "lfe_wide_resid_rows": (C.c_int, [_vp, _vp, C.c_int64, C.c_int64, C.c_int64, C.c_int, _dp, _vp, _dp]),
+    "lfe_stream_synth_cols": (C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int, C.c_int, _i32p, _dp, C.c_uint64]),
     "lfe_wide_gram": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int, _vp, _dp]),
     "lfe_wide_resid": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, _dp, _vp, _dp]),
     "lfe_wide_cluster_meats": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, _vp, C.c_int, _i32p, _dp, _i64p]),
@@ -606,6 +610,42 @@ class Engine:
         for row0, cols in chunks:
             self.stream_rows(row0, cols)
         _check(self._lib.lfe_stream_end(self._h, None))
+
+    def stream_materialize_rows(self, D: int, ldD: int, col0: int, row0: int, cols, mask_col: int = -1) -> None:
+        """Rows [row0, row0 + len) of a streamed context's demeaned columns into D rows 0.. (one chunk of
+        a chunked wide fit); ``cols``: the chunk's columns (host arrays) or ("synth", K, c_lo, levels,
+        beta, seed) to generate them on the device."""
+        if isinstance(cols, tuple) and cols and cols[0] == "synth":
+            _, rows, K, c_lo, levels, beta, seed = cols
+        else:
+            rows = len(cols[0])
+        _check(self._lib.lfe_stream_materialize_rows(self._h, _vp(D), int(ldD), int(col0), int(mask_col), int(row0),
+                                                     int(rows)))
+        if isinstance(cols, tuple) and cols and cols[0] == "synth":
+            self.stream_synth_cols(row0, rows, K, c_lo, levels, beta, seed)
+        else:
+            self.stream_rows(row0, cols)
+        _check(self._lib.lfe_stream_end(self._h, None))
+
+    def stream_synth_cols(self, row0: int, rows: int, K: int, c_lo: int, levels, beta, seed: int) -> None:
+        lv = (C.c_int32 * max(len(levels), 1))(*[int(g) for g in levels])
+        b = np.ascontiguousarray(beta, dtype=np.float64)
+        _check(self._lib.lfe_stream_synth_cols(self._h, int(row0), int(rows), int(K), int(c_lo), lv,
+                                               b.ctypes.data_as(_dp), C.c_uint64(seed)))
+
+    def wide_gram_rows(self, D: int, ldD: int, row0: int, rows: int, c0: int, P: int, mode: int = 0,
+                       r: int | None = None) -> np.ndarray:
+        out = np.zeros((P, P))
+        _check(self._lib.lfe_wide_gram_rows(self._h, _vp(D), int(ldD), int(row0), int(rows), int(c0), int(P), int(mode),
+                                            None if r is None else _vp(r), out.ctypes.data_as(_dp)))
+        return out
+
+    def wide_resid_rows(self, D: int, ldD: int, row0: int, rows: int, coef: np.ndarray, r: int) -> np.ndarray:
+        v = np.ascontiguousarray(coef, dtype=np.float64)
+        stats = np.zeros(4)
+        _check(self._lib.lfe_wide_resid_rows(self._h, _vp(D), int(ldD), int(row0), int(rows), int(v.size),
+                                             v.ctypes.data_as(_dp), _vp(r), stats.ctypes.data_as(_dp)))
+        return stats
 
     def wide_gram(self, D: int, ldD: int, c0: int, P: int, mode: int = 0, r: int | None = None) -> np.ndarray:
         out = np.zeros((P, P))

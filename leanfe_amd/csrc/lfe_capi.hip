@@ -1016,16 +1016,35 @@ int lfe_stream_synth_rows(lfe_ctx* c, int64_t row0, int64_t rows, int k, const i
   return LFE_OK;
 }
 
+int lfe_stream_synth_cols(lfe_ctx* c, int64_t row0, int64_t rows, int K, int c_lo, const int32_t* n_levels,
+                          const double* beta, uint64_t seed) {
+  LFE_CTX(c);
+  auto& w = c->sw;
+  if (!w.on || w.pass == 0) return fail(LFE_ESTATE, "lfe_stream_begin first");
+  if (K < 0 || c_lo < 0 || c_lo + c->p > K + 1 || !n_levels || (K > 0 && !beta))
+    return fail(LFE_EINVAL, "the column block must lie in [0, K]");
+  if (row0 < 0 || rows < 0 || row0 + rows > c->n) return fail(LFE_EINVAL, "rows outside the loaded codes");
+  if (rows == 0) return LFE_OK;
+  const int64_t cld = (rows + 63) / 64 * 64;
+  LFE_TRY(ensure_f64(c, w.x, w.x_cap, (size_t)c->p * cld));
+  LFE_TRY(synth_cols_chunk(c, K, c_lo, n_levels, beta, seed, c->synth_row0 + row0, rows, w.x, cld));
+  LFE_TRY(stream_chunk(c, cld, row0, rows));
+  return LFE_OK;
+}
+
 int lfe_stream_end(lfe_ctx* c, double* out) {
   LFE_CTX(c);
   auto& w = c->sw;
   if (!w.on || w.pass == 0) return fail(LFE_ESTATE, "lfe_stream_begin first");
   const int pass = w.pass;
   w.pass = 0;
-  if (w.rows_done != c->n) return fail(LFE_EINVAL, "the streamed chunks did not cover the loaded rows");
+  const int64_t want = pass == 5 && w.mrows >= 0 ? w.mrows : c->n;  // (a row range of lfe_stream_materialize_rows)
+  if (w.rows_done != want) return fail(LFE_EINVAL, "the streamed chunks did not cover the loaded rows");
   const int p = c->p, k = p - 1;
   if (pass == 5) {  // lfe_stream_materialize: nothing to reduce
     w.mD = nullptr;
+    w.mbase = 0;
+    w.mrows = -1;
     return LFE_OK;
   }
   if (pass == 1) {

@@ -477,6 +477,7 @@ struct lfe_ctx {
     // pass 5 (lfe_stream_materialize): the chunks' demeaned columns into a caller's matrix
     double* mD = nullptr;    // [cols][mld], input row order (0 on dropped rows)
     int64_t mld = 0;
+    int64_t mbase = 0, mrows = -1;  // lfe_stream_materialize_rows: D row = row - mbase over mrows rows (-1: all)
     int mcol0 = 0, mmask = -1;  // first target column; kept-row indicator column (-1: none)
     // clustered SEs (lfe_stream_clusters): every subset's dense cluster id per input row, and the
     // per-cluster score sums the residual passes add in chunk order
@@ -621,6 +622,8 @@ int launch_copy_demeaned(lfe_ctx* c, double* dev_out);
 int launch_validate_codes(const int32_t* code, int64_t n, int32_t G, int32_t* flag, hipStream_t s);
 
 // --- synthetic panel (lfe_synth.hip) ---
+int synth_cols_chunk(lfe_ctx* c, int K, int c_lo, const int32_t* levels, const double* beta, uint64_t seed,
+                     int64_t row0, int64_t rows, double* X, int64_t ld);
 int synth_chunk(lfe_ctx* c, int k, const int32_t* levels, const double* beta, uint64_t seed, int64_t row0,
                 int64_t rows, double* X, int64_t ld);
 int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed, int64_t row0);

@@ -185,6 +185,72 @@ int synth_chunk(lfe_ctx* c, int k, const int32_t* levels, const double* beta, ui
   return LFE_OK;
 }
 
+// Columns [c_lo, c_lo + pc) of the K-regressor panel (global column 0 = y, j >= 1 = x_j) for global
+// rows row0 + r: a wide fit's column block (k_synth_rows for K > 62; y needs every x of the row, so
+// a block holding y evaluates all K, in k_synth_rows' order).  beta: K device doubles.
+__global__ void k_synth_cols(SynthArgs a, int K, int c_lo, int pc, const double* __restrict__ beta,
+                             double* __restrict__ X, int64_t ld, int64_t n, uint64_t seed, int64_t row0) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = (uint64_t)(row0 + r);
+    int32_t g[kMaxFE];
+    for (int f = 0; f < a.F; ++f) g[f] = synth_code(i, f, a.L[f], seed);
+    const double a0 = a.F > 0 ? a.eff[0][g[0]] : 0.0;
+    if (c_lo == 0) {
+      double y = 0.0;
+      for (int j = 0; j < K; ++j) {
+        const double x = nrm(i, 200 + j, seed) + 0.5 * a0;
+        if (1 + j < pc) X[(int64_t)(1 + j) * ld + r] = x;
+        const double t = beta[j] * x;
+        y = (j == 0) ? t : y + t;
+      }
+      for (int f = 0; f < a.F; ++f) y = y + a.eff[f][g[f]];
+      y = y + nrm(i, 300, seed);
+      X[r] = y;
+    } else {
+      for (int c = 0; c < pc; ++c) {
+        const int j = c_lo + c - 1;  // x_{j+1}
+        X[(int64_t)c * ld + r] = nrm(i, 200 + (uint64_t)j, seed) + 0.5 * a0;
+      }
+    }
+  }
+}
+
+int synth_cols_chunk(lfe_ctx* c, int K, int c_lo, const int32_t* levels, const double* beta, uint64_t seed,
+                     int64_t row0, int64_t rows, double* X, int64_t ld) {
+  SynthArgs a{};
+  a.F = c->F;
+  a.k = 0;
+  std::vector<double*> eff(c->F, nullptr);
+  double* dbeta = nullptr;
+  double scale = 1.0;
+  int rc = LFE_OK;
+  for (int f = 0; f < c->F && rc == LFE_OK; ++f) {
+    a.L[f] = levels[f];
+    if (hipMalloc(&eff[f], sizeof(double) * (size_t)levels[f]) != hipSuccess) {
+      rc = LFE_ENOMEM;
+      break;
+    }
+    hipLaunchKernelGGL(k_synth_effects, dim3(grid_for(levels[f])), dim3(kBlock), 0, c->stream, eff[f], levels[f], f,
+                       scale, seed);
+    a.eff[f] = eff[f];
+    scale *= 0.5;
+  }
+  if (rc == LFE_OK && hipMalloc(&dbeta, sizeof(double) * (size_t)std::max(K, 1)) != hipSuccess) rc = LFE_ENOMEM;
+  if (rc == LFE_OK && K > 0 &&
+      hipMemcpyAsync(dbeta, beta, sizeof(double) * (size_t)K, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    rc = LFE_EHIP;
+  if (rc == LFE_OK && rows)
+    hipLaunchKernelGGL(k_synth_cols, dim3(grid_for(rows, kBlock, 256 * 16)), dim3(kBlock), 0, c->stream, a, K, c_lo,
+                       c->p, dbeta, X, ld, rows, seed, row0);
+  if (rc == LFE_OK && hipGetLastError() != hipSuccess) rc = LFE_EHIP;
+  (void)hipStreamSynchronize(c->stream);
+  for (auto* e : eff)
+    if (e) (void)hipFree(e);
+  if (dbeta) (void)hipFree(dbeta);
+  if (rc != LFE_OK) set_error("synthetic column block: allocation or launch failed");
+  return rc;
+}
+
 int synth_codes(lfe_ctx* c, const int32_t* levels, uint64_t seed, int64_t row0) {
   SynthArgs a{};
   a.F = c->F;

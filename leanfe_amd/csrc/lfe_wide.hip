@@ -106,7 +106,9 @@ int stream_materialize_chunk(lfe_ctx* c, const double* X, int64_t ld, int64_t ro
     a.cnt_pre[f] = c->fe[f].cnt_pre;
     a.alpha[f] = c->fe[f].alpha;
   }
-  a.D = w.mD + row0;
+  if (row0 < w.mbase || (w.mrows >= 0 && row0 + rows > w.mbase + w.mrows) || row0 - w.mbase + rows > w.mld)
+    return fail(LFE_EINVAL, "rows outside the materialized range");
+  a.D = w.mD + (row0 - w.mbase);
   a.ldD = w.mld;
   a.col0 = w.mcol0;
   a.mask_col = w.mmask;
@@ -451,6 +453,25 @@ int lfe_materialize(lfe_ctx* c, double* D, int64_t ldD, int first, int col0, int
   return LFE_OK;
 }
 
+int lfe_stream_materialize_rows(lfe_ctx* c, double* D, int64_t ldD, int col0, int mask_col, int64_t row0,
+                                int64_t rows) {
+  LFE_WCTX(c);
+  auto& w = c->sw;
+  if (!w.on) return fail(LFE_ESTATE, "lfe_stream_materialize_rows: the context holds resident columns");
+  if (!c->demeaned) return fail(LFE_ESTATE, "lfe_demean first");
+  if (w.pass != 0) return fail(LFE_ESTATE, "a streamed pass is open (lfe_stream_end first)");
+  if (!D || row0 < 0 || rows < 0 || row0 + rows > c->n || ldD < rows || col0 < 0) return fail(LFE_EINVAL, "bad arguments");
+  w.mD = D;
+  w.mld = ldD;
+  w.mcol0 = col0;
+  w.mmask = mask_col;
+  w.mbase = row0;
+  w.mrows = rows;
+  w.pass = 5;
+  w.rows_done = 0;
+  return LFE_OK;
+}
+
 int lfe_stream_materialize(lfe_ctx* c, double* D, int64_t ldD, int col0, int mask_col) {
   LFE_WCTX(c);
   auto& w = c->sw;
@@ -462,32 +483,49 @@ int lfe_stream_materialize(lfe_ctx* c, double* D, int64_t ldD, int col0, int mas
   w.mld = ldD;
   w.mcol0 = col0;
   w.mmask = mask_col;
+  w.mbase = 0;
+  w.mrows = -1;
   w.pass = 5;
   w.rows_done = 0;
   return LFE_OK;
 }
 
-int lfe_wide_gram(lfe_ctx* c, const double* D, int64_t ldD, int c0, int P, int mode, const double* r, double* out) {
+int lfe_wide_gram_rows(lfe_ctx* c, const double* D, int64_t ldD, int64_t row0, int64_t rows, int c0, int P, int mode,
+                       const double* r, double* out) {
   LFE_WCTX(c);
-  if (!D || !out || P < 1 || c0 < 0 || ldD < c->n || mode < 0 || mode > 3 || (mode >= 2 && !r))
+  if (!D || !out || P < 1 || c0 < 0 || row0 < 0 || rows < 0 || row0 + rows > c->n || ldD < rows || mode < 0 ||
+      mode > 3 || (mode >= 2 && !r))
     return fail(LFE_EINVAL, "bad arguments");
   if (c->world > 1) return fail(LFE_EINVAL, "wide fits run in one process");
-  return wide_syrk(c, D + (int64_t)c0 * ldD, ldD, 1, c->n, P, mode, c->w, r, out);
+  return wide_syrk(c, D + (int64_t)c0 * ldD, ldD, 1, rows, P, mode, c->w ? c->w + row0 : nullptr, r, out);
+}
+
+int lfe_wide_gram(lfe_ctx* c, const double* D, int64_t ldD, int c0, int P, int mode, const double* r, double* out) {
+  if (!c) return fail(LFE_EINVAL, "null context");
+  return lfe_wide_gram_rows(c, D, ldD, 0, c->n, c0, P, mode, r, out);
 }
 
 int lfe_wide_resid(lfe_ctx* c, const double* D, int64_t ldD, int P, const double* coef, double* r, double* stats) {
+  if (!c) return fail(LFE_EINVAL, "null context");
+  return lfe_wide_resid_rows(c, D, ldD, 0, c->n, P, coef, r, stats);
+}
+
+int lfe_wide_resid_rows(lfe_ctx* c, const double* D, int64_t ldD, int64_t row0, int64_t rows, int P,
+                        const double* coef, double* r, double* stats) {
   LFE_WCTX(c);
-  if (!D || !coef || !r || !stats || P < 2 || P > kWrMaxP || ldD < c->n) return fail(LFE_EINVAL, "bad arguments");
+  if (!D || !coef || !r || !stats || P < 2 || P > kWrMaxP || row0 < 0 || rows < 0 || row0 + rows > c->n || ldD < rows)
+    return fail(LFE_EINVAL, "bad arguments");
+  const double* wr = c->w ? c->w + row0 : nullptr;
   double* v = nullptr;
   double* part = nullptr;
-  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>((c->n + 255) / 256, 4 * (int64_t)c->n_cu));
+  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 255) / 256, 4 * (int64_t)c->n_cu));
   LFE_TRY(walloc(&v, (size_t)P + 4));
   int rc = walloc(&part, (size_t)nblk * 4 + 4);
   if (rc == LFE_OK) {
     hipError_t e = hipMemcpyAsync(v, coef, sizeof(double) * P, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) {
       ProfScope _ps(c, K_GRAM_RESID);
-      hipLaunchKernelGGL(k_wide_resid, dim3(nblk), dim3(256), sizeof(double) * P, c->stream, D, ldD, c->n, P, v, c->w,
+      hipLaunchKernelGGL(k_wide_resid, dim3(nblk), dim3(256), sizeof(double) * P, c->stream, D, ldD, rows, P, v, wr,
                          r, part);
       hipLaunchKernelGGL(k_wide_stats, dim3(1), dim3(64), 0, c->stream, part, nblk, part + (size_t)nblk * 4);
       e = hipGetLastError();

@@ -31,8 +31,9 @@ _VERBOSE = os.environ.get("LEANFE_HIP_VERBOSE", "0") not in ("", "0")  # log lin
 #   context_rows  rows per engine context (None: 2^31 - 64, the int32 row-index cap)
 #   phase_timing  the engine's per-phase device times in LeanFEResult.timings (HIP events: host time
 #                 on the launch path; also on with LEANFE_HIP_VERBOSE)
+#   wide_chunked  streamed wide IID / HC1 fits in row chunks without a resident D (False: D resident)
 KNOBS = {"out_of_core": False, "stream": True, "stream_batch": 1 << 22, "reshard": True, "context_rows": None,
-         "phase_timing": False}
+         "phase_timing": False, "wide_chunked": True}
 
 
 def _default_device() -> int:
@@ -542,6 +543,148 @@ def _out_of_core_fit(eng, source, cols, n_rows, y_col, x_cols, instruments, fe_c
                         timings=timings)
 
 
+def _wide_fit_chunked(cols, y_col, x_cols, fe_cols, weights, v, vcov, strategy, demean_tol, max_iter, formula, t_start,
+                      say, engine, device, ooc, instruments) -> LeanFEResult:
+    """A streamed wide fit (IID / HC1) without a resident D: every column block stays an engine
+    context (codes, layouts and its effect tables: ~22 B a row each), and the source is read twice
+    more in row chunks - each chunk's [1_kept, y~, x~, z~] formed for all blocks into one chunk
+    buffer (lfe_stream_materialize_rows), whose Gram (pass A) or residual, statistics and HC1 meat
+    (pass B) are added in chunk order (lfe_wide_gram_rows, lfe_wide_resid_rows).  So the P n doubles
+    of D and the context's 2^31-row cap on D's rows are gone: device memory is the blocks' codes plus
+    P x chunk doubles (polars_impl.py:165-209 at any width; duckdb_impl.py:272-300 forms X'X out of
+    core in one aggregation the same way)."""
+    instruments = list(instruments)
+    k, mz = len(x_cols), len(instruments)
+    if mz and not fe_cols:
+        raise ValueError("a wide IV fit takes one or more FEs (demeaned instruments are never all ones)")
+    dcols = list(x_cols) + instruments
+    P = 2 + len(dcols)
+    w = None if weights is None else np.asarray(cols[weights], dtype=np.float64)
+    n = ooc["n_rows"]
+    chunk = max(64, int(ooc["chunk_rows"]) // 64 * 64)
+    per = MAX_CONTEXT_COLS - (1 if w is not None else 0)
+    blocks = [dcols[:per - 1]] + [dcols[j:j + per] for j in range(per - 1, len(dcols), per)]
+    dev = _default_device() if device is None else device
+    eng = engine if engine is not None else Engine(dev)
+    engines = [eng]
+    Dc = r = None
+
+    def chunks(select=None):  # the source re-read in row chunks of `chunk` rows
+        return _stream_chunks(ooc["source"], cols, n, chunk, y_col, x_cols, instruments, ooc["plan"], ooc["x_base"],
+                              select=select)
+
+    try:
+        codes, levels = [], []
+        for fe in fe_cols:
+            c, g = frame.factorize(cols[fe], device=eng)
+            codes.append(c)
+            levels.append(g)
+        if strategy == "auto":
+            strategy = "demean" if len(fe_cols) == 1 else ("alt_proj" if fe_cols else "ols")
+        if strategy == "demean" and len(fe_cols) != 1:
+            raise ValueError("Strategy 'demean' requires exactly one FE column.")
+        if strategy == "alt_proj" and not fe_cols:
+            raise ValueError("Strategy 'alt_proj' requires FE-cols. Use strategy='ols' instead for OLS without FE.")
+        if strategy == "ols" and fe_cols:
+            raise ValueError("Strategy 'ols' takes no fixed effects")
+        say(f"Wide fit: {k} regressors{f' and {mz} instruments' if mz else ''} in {len(blocks)} column blocks, "
+            f"chunks of {chunk:_} rows (no resident D)")
+        t0 = time.perf_counter()
+        iterations = 0
+        spans = []  # each block's columns within [y] + dcols
+        lo = 0
+        for b, xb in enumerate(blocks):
+            e = eng if b == 0 else Engine(eng.device)
+            if b > 0:
+                engines.append(e)
+            pb = len(xb) + (1 if b == 0 else 0)
+            spans.append((lo, pb))
+            e.load_codes(codes, levels, pb, weights=w)
+            n_obs, fe_dims, fe_card = e.drop_singletons()
+            e.stream_pass(1, chunks(list(range(lo, lo + pb))))
+            if strategy == "demean":
+                e.demean([0], demean_tol, max_iter, check_from=0)
+                iterations = 1
+            elif strategy == "alt_proj":
+                order = sorted(range(len(fe_cols)), key=lambda i: fe_card[i])  # polars_impl.py:485
+                if b == 0:
+                    iterations, _ = e.demean(order, demean_tol, max_iter, check_from=3)
+                else:  # the same sweeps as the first block: no stop test of its own
+                    e.demean(order, 0.0, iterations, check_from=3)
+            else:
+                e.demean([], demean_tol, max_iter, check_from=0)
+            lo += pb
+        if strategy == "ols":
+            iterations, absorbed_df, fe_dims = 0, 0, None
+        elif strategy == "demean":
+            absorbed_df = fe_dims[0] - 1
+        else:
+            absorbed_df = sum(fe_dims) - len(fe_cols)
+        df_resid = n_obs - (k + 1) - absorbed_df
+        Dc = eng.dev_alloc(P * chunk)
+        r = eng.dev_alloc(chunk)
+        eng.sync()
+
+        def fill(row0, colsall):  # the chunk's [1_kept, y~, x~, z~] from every block
+            col0 = 1
+            for b, (lo_b, pb) in enumerate(spans):
+                engines[b].stream_materialize_rows(Dc, chunk, col0, row0, colsall[lo_b:lo_b + pb], 0 if b == 0 else -1)
+                col0 += pb
+            return len(colsall[0])
+
+        mode_g = 1 if w is not None else 0
+        G = np.zeros((P, P))
+        for row0, colsall in chunks():  # pass A: the Gram, chunk by chunk
+            rows = fill(row0, colsall)
+            G += eng.wide_gram_rows(Dc, chunk, row0, rows, 0, P, mode=mode_g)
+        t_load = time.perf_counter() - t0
+        if mz:  # 2SLS from the Gram of [1, y~, x~, z~] (common.py:188-287)
+            iv = inference.IVSystem(G, k, mz, z_has_ones=False)
+            beta_full, Vb, to_meat = iv.beta_full, iv.XtX_inv, iv.xhat_meat
+            coef = np.concatenate([[-iv.coef[0], 1.0], -iv.coef[1:]])
+            keep = [0] + list(range(2, P))
+            c0, km = 0, P
+        else:
+            XtX, Xty = inference.split_gram(G)
+            beta_full, XtX_inv = inference.solve_normal(XtX, Xty)  # polars_impl.py:212-226
+            Vb, to_meat = XtX_inv[1:, 1:], (lambda M: M)
+            coef = np.concatenate([[-beta_full[0], 1.0], -beta_full[1:]])
+            keep = None
+            c0, km = 2, k
+        sub = (lambda M: M) if keep is None else (lambda M: M[np.ix_(keep, keep)])
+        stats = np.zeros(4)
+        meat = np.zeros((km, km))
+        for row0, colsall in chunks():  # pass B: residuals, statistics, the HC1 meat
+            rows = fill(row0, colsall)
+            stats += eng.wide_resid_rows(Dc, chunk, row0, rows, coef, r)
+            if v == "hc1":
+                meat += eng.wide_gram_rows(Dc, chunk, row0, rows, c0, km, mode=2 if w is not None else 3, r=r)
+        rss_w, rss, sum_y, sum_y2 = stats
+        if v == "iid":
+            se = inference.se_iid(Vb, rss_w, df_resid)
+        else:
+            se = inference.se_hc1(Vb, to_meat(sub(meat)), n_obs, df_resid)
+        if mz:
+            se = se[1:]
+        tss = sum_y2 - sum_y * sum_y / n_obs if n_obs else 0.0
+        timings = dict(eng.timings(), load_s=t_load, total_s=time.perf_counter() - t_start)
+    finally:
+        for ptr in (Dc, r):
+            if ptr is not None:
+                eng.dev_free(ptr)
+        for e in engines[1:]:
+            e.close()
+        if engine is None:
+            eng.close()
+    return LeanFEResult(coefs=dict(zip(x_cols, (float(b_) for b_ in beta_full[1:]))),
+                        std_errors=dict(zip(x_cols, (float(s_) for s_ in se))), n_obs=n_obs,
+                        iterations=iterations, vcov_type=vcov, is_iv=bool(mz), n_instruments=mz or None,
+                        n_clusters=None, df_resid=df_resid, formula=formula, fe_cols=fe_cols,
+                        fe_dims=fe_dims, r_squared=None if mz else (1 - rss / tss if tss > 0 else None),
+                        compression_ratio=None, rss=float(rss), tss=None if mz else tss, backend="hip",
+                        timings=timings)
+
+
 def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc, strategy, demean_tol, max_iter,
               formula, t_start, say, engine=None, device=None, ooc=None, instruments=()) -> LeanFEResult:
     """A fit of more than 63 columns (e.g. an event study's i(year) dummies, polars_impl.py:27-69,
@@ -558,6 +701,9 @@ def _wide_fit(cols, y_col, x_cols, fe_cols, weights, cluster_cols, v, vcov, ssc,
     ``instruments`` (IV / 2SLS, common.py:188-287): D = [1_kept, y~, x~, z~]; 2SLS from D's Gram
     (inference.IVSystem), the residual over u = [1, x~, z~] and its meats over u (D's column 1
     dropped), mapped to the X_hat space as in the resident fit (std_errors.py:448-602)."""
+    if ooc is not None and v in ("iid", "hc1") and KNOBS["wide_chunked"]:
+        return _wide_fit_chunked(cols, y_col, x_cols, fe_cols, weights, v, vcov, strategy, demean_tol, max_iter,
+                                 formula, t_start, say, engine, device, ooc, instruments)
     instruments = list(instruments)
     k, mz = len(x_cols), len(instruments)
     if mz and not fe_cols:
