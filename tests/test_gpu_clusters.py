@@ -253,3 +253,36 @@ def test_clusters_loaded_after_the_fused_pass():
     for (a, ga), (b, gb) in zip(fused, srt):
         np.testing.assert_array_equal(ga, gb)
         assert np.abs(a - b).max() <= 1e-12 * np.abs(b).max()
+
+
+@pytest.mark.parametrize("k", [3, 14, 20])
+def test_mostly_singleton_intersection_multi_row_corrections(k, knob):
+    """A two-way CGM whose intersection is mostly singletons (mean cluster size < 2, as config 4's
+    fe2 x fe3 and MEGA_CLUSTER2's fe1 x fe2): meat = D + sum over clusters of two or more rows of
+    (S_c S_c' - sum_i s_i s_i').  k <= 16 forms the corrections in one pass over those clusters' rows
+    (k_multi_meat); k = 20, and LFE_CL_MULTI_GATHER, gather the rows and Gram the tables;
+    LFE_CL_NO_SINGLETON sums every cluster.  All three at 1e-12, the oracle at 1e-10 with equal cluster
+    counts, bit-identical repeats."""
+    from oracle import altproj
+
+    n, L = 400_000, [2_000, 400, 50]  # 800K cells: ~60 % of the rows singletons, the rest in 2+ row clusters
+    xs = [f"x{j + 1}" for j in range(k)]
+    fes = ["fe1", "fe2", "fe3"]
+    d = dict(synth.panel(n, k, L, seed=83))
+    cl = ["fe1", "fe2"]
+    a = _fit(d, xs, fes, cl)
+    again = _fit(d, xs, fes, cl)
+    knob.setenv("LFE_CL_MULTI_GATHER", "1")
+    g = _fit(d, xs, fes, cl)
+    knob.delenv("LFE_CL_MULTI_GATHER")
+    knob.setenv("LFE_CL_NO_SINGLETON", "1")
+    full = _fit(d, xs, fes, cl)
+    o = altproj.fit(d, "y", xs, fes, vcov="cluster", cluster_cols=cl)
+    assert tuple(a.n_clusters) == tuple(o["n_clusters"]) == tuple(full.n_clusters)
+    inter = np.unique(np.asarray(d["fe1"], np.int64) * L[1] + np.asarray(d["fe2"]))
+    assert 2 * inter.size > n and inter.size < n  # the intersection: mostly singletons, some multi-row clusters
+    np.testing.assert_array_equal(_arr(a, xs, "std_errors"), _arr(again, xs, "std_errors"))
+    for other in (g, full):
+        np.testing.assert_allclose(_arr(a, xs, "std_errors"), _arr(other, xs, "std_errors"), rtol=1e-12, atol=0)
+    np.testing.assert_allclose(_arr(a, xs, "coefs"), o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(_arr(a, xs, "std_errors"), o["se"], rtol=1e-10, atol=0)

@@ -253,3 +253,32 @@ def test_streamed_wide_fit_without_resident_design_matrix(vcov, weighted, monkey
         assert other.iterations == a.iterations and other.n_obs == a.n_obs
         np.testing.assert_allclose([a.coefs[x] for x in xs], [other.coefs[x] for x in xs], rtol=tol, atol=0)
         np.testing.assert_allclose([a.std_errors[x] for x in xs], [other.std_errors[x] for x in xs], rtol=tol, atol=0)
+
+
+def test_device_generated_wide_fit_matches_the_oracle():
+    """tools/wide_oocore_run.py's chunked wide fit (K = 100 columns generated per chunk on the device,
+    no resident D; run at 1e9 rows into profiles/r06) at 150K rows: the oracle on the same panel
+    (synth.panel, the host restatement of the device generator) at 1e-10 with equal integers, and a
+    second chunking at 1e-13."""
+    import importlib.util
+    import os
+
+    from oracle import altproj
+
+    spec = importlib.util.spec_from_file_location(
+        "wide_oocore_run", os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "wide_oocore_run.py"))
+    tool = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tool)
+    n, K, L = 150_000, 100, [3_000, 120]
+    beta = synth.betas(K)
+    a = tool.wide_fit(n, K, L, beta, 40_000, seed=41)
+    b = tool.wide_fit(n, K, L, beta, 64_000 + 64 * 7, seed=41)
+    d = dict(synth.panel(n, K, L, seed=41))
+    xs = [f"x{j + 1}" for j in range(K)]
+    o = altproj.fit(d, "y", xs, ["fe1", "fe2"], vcov="HC1")
+    assert a["blocks"] == 2 and a["iterations"] == o["iterations"] and a["n_obs"] == o["n_obs"]
+    np.testing.assert_allclose(a["beta"], o["beta"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(a["se"], o["se"], rtol=1e-10, atol=0)
+    assert (b["iterations"], b["n_obs"], b["df_resid"]) == (a["iterations"], a["n_obs"], a["df_resid"])
+    np.testing.assert_allclose(b["beta"], a["beta"], rtol=1e-13, atol=0)
+    np.testing.assert_allclose(b["se"], a["se"], rtol=1e-13, atol=0)
