@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void k_wide_syrk(SyrkArgs a) {
   for (int jb = 0; jb < 4; ++jb) acc[jb] = d4{0.0, 0.0, 0.0, 0.0};
   for (int64_t rb = r0 + 4 * kq; rb < r1; rb += 16) {
     double av[4], bv[4][4];
-    if (ROWQ) {  // rows past n are zero in A (its padding) and get scale 0
+    if (ROWQ) {  // rows past n (A's padding, or a previous chunk's rows in a chunk buffer) count 0
       const d4 x = *reinterpret_cast<const d4*>(pa + rb);
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void k_wide_syrk(SyrkArgs a) {
         for (int s = 0; s < 4; ++s) bv[jb][s] = vb[jb] ? y[s] : 0.0;
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) av[s] = va ? x[s] : 0.0;
+      for (int s = 0; s < 4; ++s) av[s] = (va && rb + s < a.n) ? x[s] : 0.0;
     } else {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
