@@ -279,7 +279,8 @@ int lfe_copy_inputs(lfe_ctx* ctx, double* const* cols_out, int32_t* const* codes
  * sums go to their owner ranks by cluster key (cluster codes must then be global).
  * cols = p column pointers of `rows` doubles each (kind LFE_HOST / LFE_DEVICE).
  * lfe_stream_end's `out`: pass 2: stats[4] then the (p-1)^2 meat; pass 4: stats[4] then the p^2
- * meat; pass 3: the (p+1)^2 Gram; pass 1: unused. */
+ * meat; pass 3: the (p+1)^2 Gram; pass 1 and 5 (materialize): unused - pass 5 returns with D written
+ * (the context's stream synchronized: another context's stream reads D next). */
 int lfe_load_codes(lfe_ctx* ctx, int64_t n, int p, int F, const int32_t* const* fe_codes,
                    const int32_t* n_levels, const double* weights_or_null, int kind);
 int lfe_stream_begin(lfe_ctx* ctx, int pass, const double* beta_full);

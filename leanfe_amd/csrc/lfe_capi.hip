@@ -1041,10 +1041,11 @@ int lfe_stream_end(lfe_ctx* c, double* out) {
   const int64_t want = pass == 5 && w.mrows >= 0 ? w.mrows : c->n;  // (a row range of lfe_stream_materialize_rows)
   if (w.rows_done != want) return fail(LFE_EINVAL, "the streamed chunks did not cover the loaded rows");
   const int p = c->p, k = p - 1;
-  if (pass == 5) {  // lfe_stream_materialize: nothing to reduce
-    w.mD = nullptr;
+  if (pass == 5) {  // lfe_stream_materialize: nothing to reduce; D is written when this returns (other
+    w.mD = nullptr;  // contexts' streams read it next: the column blocks of a wide fit)
     w.mbase = 0;
     w.mrows = -1;
+    LFE_HIP(hipStreamSynchronize(c->stream));
     return LFE_OK;
   }
   if (pass == 1) {
