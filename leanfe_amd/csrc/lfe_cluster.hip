@@ -326,119 +326,30 @@ __global__ void k_multi_sums(const int32_t* __restrict__ seg2, int32_t G2, const
   }
 }
 
-// k_multi_compact with the end offset: seg2[G2] = N2 (both read on the device, no round trip)
-__global__ void k_multi_compact_end(const int32_t* __restrict__ seg_off, int32_t G, const int32_t* __restrict__ pos2,
-                                    const int32_t* __restrict__ idx2, const int32_t* __restrict__ R,
-                                    int32_t* __restrict__ seg2, int32_t* __restrict__ r2) {
-  for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < G; h += (int64_t)gridDim.x * blockDim.x) {
-    if (h == 0) seg2[idx2[G]] = pos2[G];
-    const int32_t a = seg_off[h], len = seg_off[h + 1] - a;
-    if (len < 2) continue;
-    const int32_t q = pos2[h];
-    seg2[idx2[h]] = q;
-    for (int32_t j = 0; j < len; ++j) r2[q + j] = R[a + j];
-  }
-}
-
-// The multi-row clusters' corrections sum_c (S_c S_c' - sum_{i in c} s_i s_i') in one pass over their
-// rows (no gathered copy t2, no per-cluster table s2, no Grams of them): a 16-lane group is a worker
-// with a contiguous run of clusters (G2 read on the device), lane j holds score column j; it walks
-// its rows r2 in batches of 16 (the next batch's row indices in flight), the cluster ends from a
-// 16-entry register window of seg2, and per cluster adds d_j = S_c S_j - sum_i s_ic s_ij to its
-// accumulators (cluster order).  A workgroup's 16 workers are summed in fixed order into part[b],
-// k_reduce_partials sums the workgroups in block order: the same bits on every run.  k <= 16.
-constexpr int kMultiThreads = 256;
-constexpr int kMultiWorkers = kMultiThreads / 16;
-
-__global__ __launch_bounds__(kMultiThreads) void k_multi_meat(const int32_t* __restrict__ seg2,
-                                                              const int32_t* __restrict__ G2p,
-                                                              const int32_t* __restrict__ r2,
-                                                              const double* __restrict__ U, int k,
-                                                              double* __restrict__ part) {
-  __shared__ double red[kMultiWorkers][256];
-  const int lane = threadIdx.x & 63, gb = lane & 48, c = lane & 15, wl = threadIdx.x >> 4;
-  const int64_t G2 = *G2p;
-  const int64_t nwk = (int64_t)gridDim.x * kMultiWorkers;
-  const int64_t per = (G2 + nwk - 1) / nwk;
-  const int64_t h0 = min(G2, ((int64_t)blockIdx.x * kMultiWorkers + wl) * per), h1 = min(G2, h0 + per);
-  double acc[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.0;
-  if (h0 < h1) {
-    int64_t h = h0, wb = h0;
-    int32_t win = wb + 1 + c <= h1 ? seg2[wb + 1 + c] : INT32_MAX;  // ends of clusters wb .. wb + 15
-    int32_t cend = __shfl(win, gb, 64);
-    const int32_t qend = seg2[h1];
-    int32_t q = seg2[h0];
-    int32_t rr = q + c < qend ? r2[q + c] : 0;
-    double S = 0.0, d[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) d[j] = 0.0;
-    auto close = [&]() {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const double sj = __shfl(S, gb + j, 64);
-        if (j < k) acc[j] += d[j] + S * sj;
-        d[j] = 0.0;
-      }
-      S = 0.0;
-    };
-    for (; q < qend; q += 16) {
-      const int nb = min(16, qend - q);
-      double v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int ri = __shfl(rr, gb + i, 64);
-        v[i] = (i < nb && c < k) ? U[(int64_t)ri * k + c] : 0.0;
-      }
-      rr = q + 16 + c < qend ? r2[q + 16 + c] : 0;  // the next batch's rows
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (i < nb) {
-          if (q + i == cend) {  // cluster h ends before this row (every cluster holds two or more rows)
-            close();
-            ++h;
-            if (h - wb == 16) {
-              wb = h;
-              win = wb + 1 + c <= h1 ? seg2[wb + 1 + c] : INT32_MAX;
-            }
-            cend = __shfl(win, gb + (int)(h - wb), 64);
-          }
-          S += v[i];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const double vj = __shfl(v[i], gb + j, 64);
-            if (j < k) d[j] -= v[i] * vj;
-          }
-        }
-      }
+// s2[h] = the sum of cluster h's score rows U[r2[q]], q in [seg2[h], seg2[h+1]), in row order: a
+// 16-lane group per cluster, lane j column j (k <= 16); two rows' loads in flight per step
+__global__ __launch_bounds__(256) void k_multi_sums16(const int32_t* __restrict__ seg2, int32_t G2,
+                                                      const int32_t* __restrict__ r2, const double* __restrict__ U,
+                                                      int k, double* __restrict__ s2) {
+  const int c = threadIdx.x & 15;
+  const int cc = c < k ? c : 0;
+  for (int64_t h = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; h < G2;
+       h += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+    const int32_t a = seg2[h], b = seg2[h + 1];
+    double s = 0.0;
+    int32_t q = a;
+    for (; q + 1 < b; q += 2) {
+      const int32_t i0 = r2[q], i1 = r2[q + 1];
+      const double v0 = U[(int64_t)i0 * k + cc], v1 = U[(int64_t)i1 * k + cc];
+      s += v0;
+      s += v1;
     }
-    close();
+    if (q < b) s += U[(int64_t)r2[q] * k + cc];
+    if (c < k) s2[h * k + c] = s;
   }
-#pragma unroll
-  for (int j = 0; j < 16; ++j) red[wl][c * 16 + j] = acc[j];
-  __syncthreads();
-  double s = 0.0;
-  for (int w = 0; w < kMultiWorkers; ++w) s += red[w][threadIdx.x];
-  part[(int64_t)blockIdx.x * 256 + threadIdx.x] = s;
 }
 
-// part[b][256] summed over the workgroups b: a workgroup per entry, fixed-order tree
-__global__ __launch_bounds__(256) void k_multi_reduce(const double* __restrict__ part, int nwg, double* __restrict__ out) {
-  __shared__ double red[256];
-  const int e = blockIdx.x;
-  double s = 0.0;
-  for (int b = threadIdx.x; b < nwg; b += 256) s += part[(int64_t)b * 256 + e];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[e] = red[0];
-}
-
-static int singleton_meat(lfe_ctx* c, const int32_t* R, int32_t G, int64_t n, int k, double* meat) {
+static int singleton_meat(lfe_ctx* c, const int32_t* R, int32_t G, int k, double* meat) {
   auto& W = c->clw;
   LFE_TRY(ensure_i32(c, W.off2, W.off2_cap, (size_t)G + 1));
   LFE_TRY(ensure_i32(c, W.idx2, W.idx2_cap, (size_t)G + 1));
@@ -451,29 +362,6 @@ static int singleton_meat(lfe_ctx* c, const int32_t* R, int32_t G, int64_t n, in
   }
   LFE_HIP(hipGetLastError());
   LFE_TRY(exclusive_scan2(c, W.off2, (int64_t)G + 1, W.idx2, (int64_t)G + 1));
-  if (k <= 16 && knob("LFE_CL_MULTI_GATHER") == nullptr) {
-    // one pass over the multi-row clusters' rows; sized by G (no read of N2, G2 on the host)
-    const int nwg = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ((int64_t)G / 4 + 16 * 32 - 1) / (16 * 32)));
-    LFE_TRY(ensure_i32(c, W.seg2, W.seg2_cap, (size_t)G + 1));
-    LFE_TRY(ensure_i32(c, W.r2, W.r2_cap, (size_t)std::max<int64_t>(1, n)));
-    LFE_TRY(ensure_f64(c, W.t2, W.t2_cap, (size_t)nwg * 256 + 256));
-    double* part = W.t2;
-    double* red = W.t2 + (size_t)nwg * 256;
-    {
-      ProfScope _ps(c, K_CLUSTER_SCATTER);
-      hipLaunchKernelGGL(k_multi_compact_end, dim3(grid_for(G, kBlock, 8192)), dim3(kBlock), 0, c->stream, W.seg_off,
-                         G, W.off2, W.idx2, R, W.seg2, W.r2);
-      hipLaunchKernelGGL(k_multi_meat, dim3(nwg), dim3(kMultiThreads), 0, c->stream, W.seg2, W.idx2 + G, W.r2,
-                         c->scores, k, part);
-      hipLaunchKernelGGL(k_multi_reduce, dim3(256), dim3(256), 0, c->stream, part, nwg, red);
-    }
-    LFE_HIP(hipGetLastError());
-    double M[256];
-    LFE_TRY(d2h_sync(c, M, red, sizeof(M)));
-    for (int a = 0; a < k; ++a)
-      for (int b = 0; b < k; ++b) meat[a * k + b] = c->score_meat[a * k + b] + M[a * 16 + b];
-    return LFE_OK;
-  }
   int32_t n2[2] = {0, 0};
   LFE_TRY(d2h_sync(c, &n2[0], W.off2 + G, sizeof(int32_t)));
   LFE_TRY(d2h_sync(c, &n2[1], W.idx2 + G, sizeof(int32_t)));
@@ -482,21 +370,30 @@ static int singleton_meat(lfe_ctx* c, const int32_t* R, int32_t G, int64_t n, in
   if (G2 > 0) {
     LFE_TRY(ensure_i32(c, W.seg2, W.seg2_cap, (size_t)G2 + 1));
     LFE_TRY(ensure_i32(c, W.r2, W.r2_cap, (size_t)N2));
-    LFE_TRY(ensure_f64(c, W.t2, W.t2_cap, (size_t)N2 * k));
+    // k <= 16: the clusters' sums by a 16-lane group each, straight from the score rows, and the rows'
+    // Gram through the row index (no gathered copy t2); LFE_CL_MULTI_GATHER: the gathered copy
+    const bool direct = k <= 16 && knob("LFE_CL_MULTI_GATHER") == nullptr;
+    if (!direct) LFE_TRY(ensure_f64(c, W.t2, W.t2_cap, (size_t)N2 * k));
     LFE_TRY(ensure_f64(c, W.s2, W.s2_cap, (size_t)G2 * k));
     LFE_TRY(h2d_small(c, W.seg2 + G2, &N2, sizeof(int32_t)));
     {
       ProfScope _ps(c, K_CLUSTER_SCATTER);
       hipLaunchKernelGGL(k_multi_compact, dim3(grid_for(G, kBlock, 8192)), dim3(kBlock), 0, c->stream, W.seg_off, G,
                          W.off2, W.idx2, R, W.seg2, W.r2);
-      hipLaunchKernelGGL(k_multi_rows, dim3(grid_for((int64_t)N2 * k, kBlock, 8192)), dim3(kBlock), 0, c->stream,
-                         W.r2, (int64_t)N2, c->scores, k, W.t2);
-      hipLaunchKernelGGL(k_multi_sums, dim3(grid_for((int64_t)G2 * k, kBlock, 8192)), dim3(kBlock), 0, c->stream,
-                         W.seg2, G2, W.t2, k, W.s2);
+      if (direct) {
+        hipLaunchKernelGGL(k_multi_sums16, dim3(grid_for((int64_t)G2 * 16, 256, 8192)), dim3(256), 0, c->stream,
+                           W.seg2, G2, W.r2, c->scores, k, W.s2);
+      } else {
+        hipLaunchKernelGGL(k_multi_rows, dim3(grid_for((int64_t)N2 * k, kBlock, 8192)), dim3(kBlock), 0, c->stream,
+                           W.r2, (int64_t)N2, c->scores, k, W.t2);
+        hipLaunchKernelGGL(k_multi_sums, dim3(grid_for((int64_t)G2 * k, kBlock, 8192)), dim3(kBlock), 0, c->stream,
+                           W.seg2, G2, W.t2, k, W.s2);
+      }
     }
     LFE_HIP(hipGetLastError());
     LFE_TRY(launch_table_gram(c, W.s2, G2, k, A.data()));
-    LFE_TRY(launch_table_gram(c, W.t2, N2, k, B.data()));
+    if (direct) LFE_TRY(launch_table_gram(c, c->scores, N2, k, B.data(), W.r2));
+    else LFE_TRY(launch_table_gram(c, W.t2, N2, k, B.data()));
   }
   for (int e = 0; e < k * k; ++e) meat[e] = c->score_meat[e] + (A[e] - B[e]);
   return LFE_OK;
@@ -1330,7 +1227,7 @@ static int subset_meat(lfe_ctx* c, int mask, double* meat, int64_t* G_out) {
   if (c->world == 1 && k > 0 && c->score_meat_ok && (int)c->score_meat.size() == k * k && G > 0 &&
       2 * (int64_t)G > (int64_t)nv && knob("LFE_CL_NO_SINGLETON") == nullptr) {
     *G_out = G;
-    return singleton_meat(c, W.rows[buf], G, n, k, meat);
+    return singleton_meat(c, W.rows[buf], G, k, meat);
   }
   if (k > 0) LFE_TRY(group_sums(c, n, drop, W.keys[buf], W.rows[buf], c->scores, k, G, nv));
   if (own) {  // owner-local: this rank's clusters are whole; the meat and the count summed over ranks

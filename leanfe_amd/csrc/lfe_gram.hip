@@ -41,6 +41,7 @@ struct GramArgs {
   const double* rsy;    // yoco: [ld] _sum_y, layout order
   const double* rsyy;   // yoco: [ld] _sum_y_sq, layout order
   const double* table;  // GRAM_TABLE: row-major [rows][tcols]
+  const int32_t* tidx;  // GRAM_TABLE: optional row index (row q of the Gram = table row tidx[q])
   int64_t rows;         // GRAM_TABLE
   int tcols;
   int B;                // 1 << s
@@ -137,7 +138,8 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_table(GramArgs a, double*
 #pragma unroll
       for (int I = 0; I < NT; ++I) {
         const int col = 16 * I + c;
-        z[s][I] = (r < a.rows && col < a.tcols) ? a.table[r * a.tcols + col] : 0.0;
+        const int64_t tr = a.tidx && r < a.rows ? (int64_t)a.tidx[r] : r;
+        z[s][I] = (r < a.rows && col < a.tcols) ? a.table[tr * a.tcols + col] : 0.0;
       }
     }
     mfma_rows<NT>(z, acc);
@@ -2292,9 +2294,10 @@ int launch_resid(lfe_ctx* c, const double* beta_full, double* stats, double* hc1
 
 // meat = table' table of a row-major [rows][k] score table (summed over ranks
 // unless the caller sets world = 1 for a replicated table)
-int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat) {
+int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat, const int32_t* idx) {
   GramArgs a{};
   a.table = table;
+  a.tidx = idx;
   a.rows = rows;
   a.tcols = k;
   return gram_dispatch<GRAM_TABLE>(c, a, k, 0, k, meat, nullptr, 0);

@@ -587,7 +587,8 @@ int stream_rows_chunk(lfe_ctx* c, int mode, int icpt, const double* X, int64_t l
 inline int stream_tile_stride(int p) { return p <= 11 ? 16 : 16 * ((p + 1 + 15) / 16); }
 inline size_t stream_tile_len(int p) { const size_t t = (size_t)stream_tile_stride(p); return t * t + 4; }
 void stream_tile_add(lfe_ctx* c, const double* t, int m);
-int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat);
+int launch_table_gram(lfe_ctx* c, const double* table, int64_t rows, int k, double* meat,
+                      const int32_t* idx = nullptr);  // idx: row q of the Gram = table row idx[q]
 // lfe_fast.hip: quanta of `ncols` columns from colstat-form statistics (max count: the max of cmax[0..nfe)),
 // and a [m] two-limb table (fine limbs' bits in S, coarse limbs in hi) -> double in place
 int launch_fix_quanta(lfe_ctx* c, const double* st, int nchunks, int64_t n, const int32_t* cmax, int nfe, double* fq,
