@@ -145,10 +145,13 @@ int host_msg_wait(lfe_ctx* c, unsigned long long seq, double* vals, int nvals) {
   return LFE_OK;
 }
 
+// off by default: with a kernel storing into the mapped host words the 8-rank shard solved in
+// 1.10 vs 0.91 ms and config 3 in 4.78-4.83 vs 4.62-4.63 ms, config 1 0.385-0.391 vs 0.390-0.403
+// (same box, profiles/r06/ab_hostmsg.txt); LFE_HOST_MSG=1 turns them on
 bool host_msg_on(const lfe_ctx* c) {
   if (c->world != 1) return false;
   const char* e = knob("LFE_HOST_MSG");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 int host_msg_wait_i32(lfe_ctx* c, unsigned long long seq, int32_t* vals, int n) {

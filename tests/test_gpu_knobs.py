@@ -25,7 +25,7 @@ ENV_VALUES = {
     "LFE_PART_CW": "4096", "LFE_SUMS_CG": "0", "LFE_TAB3": "0", "LFE_GRAM_GEN": "0", "LFE_GRAM_GU": "2",
     "LFE_CHOL_SPLIT": "1", "LFE_SEG_SORTED": "0", "LFE_SEG_SCATTER_ROWS": "1", "LFE_D3_BATCH": "0",
     "LFE_CL_FIX": "0", "LFE_CL_FUSED": "0", "LFE_CL_STATS": "1", "LFE_CL_NO_SINGLETON": "1",
-    "LFE_CL_OWNER_MIN_SPAN": "0", "LFE_CL_MULTI_GATHER": "1", "LFE_ROW_HASH_BITS": "8", "LFE_STR_HASH_BITS": "8", "LFE_HOST_MSG": "0",
+    "LFE_CL_OWNER_MIN_SPAN": "0", "LFE_CL_MULTI_GATHER": "1", "LFE_ROW_HASH_BITS": "8", "LFE_STR_HASH_BITS": "8", "LFE_HOST_MSG": "1",
 }
 
 
@@ -77,3 +77,18 @@ def test_environment_variables_do_not_change_the_bits(cfg, monkeypatch, knob):
     assert (moved_cells == 0) == bool(cells)
     assert moved["iterations"] == base["iterations"]
     np.testing.assert_allclose(moved["beta"], base["beta"], rtol=1e-10, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cfg", [1, 3])
+def test_host_messages_give_the_same_bits(cfg, knob):
+    """LFE_HOST_MSG=1 (off by default: measured slower, profiles/r06/ab_hostmsg.txt): the drop counts,
+    bucket starts, stop tests and the residual pass's result block reach the host through mapped host
+    words the kernels store, instead of copies - the same values, so the same bits."""
+    base, cells = _solve(cfg)
+    knob.setenv("LFE_HOST_MSG", "1")
+    msg, msg_cells = _solve(cfg)
+    assert (msg["iterations"], msg["n_obs"], msg_cells) == (base["iterations"], base["n_obs"], cells)
+    np.testing.assert_array_equal(msg["beta"], base["beta"])
+    np.testing.assert_array_equal(msg["se"], base["se"])
