@@ -346,6 +346,7 @@ struct lfe_ctx {
   hipStream_t up_stream = nullptr;
   hipEvent_t up_ev0 = nullptr, up_ev1 = nullptr;
   char* hpin_items = nullptr;      // work-item upload staging
+  char* hpin_items_dev = nullptr;  // its device address (mapped, coherent)
   size_t hpin_items_cap = 0;
   double* scores = nullptr;  // row-major [ld][score_k] score rows u r (w), layout order (p * ld allocated)
   double* dbeta = nullptr;   // [64] beta_full staging

@@ -429,6 +429,12 @@ int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m) { return exclusive_scan2(c
 // partition scatter
 // ---------------------------------------------------------------------------
 
+// the work items from the mapped staging (host memory, coherent) into the device buffer
+__global__ __launch_bounds__(256) void k_copy_staged(const int4* __restrict__ src, int4* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
 // LDS-staged scatter.  A workgroup owns a chunk of kPartThreads*PER rows
 // (wave w: PER*64 consecutive rows).  It ranks its rows by bucket in LDS, then
 // moves every column through an LDS stage in bucket order, so consecutive
@@ -1027,9 +1033,14 @@ static int build_items(lfe_ctx* c, bool side) {
   memcpy(c->hpin_items + ib + bb, xg.data(), xb);
   memcpy(c->hpin_items + ib + bb + xb, bl.data(), lb);
   // on the main stream, behind the partition scatter (a few KB: the copy that follows the scatter
-  // costs less than the cross-stream wait that let it overlap, ~10 us of barrier at small shards)
+  // costs less than the cross-stream wait that let it overlap, ~10 us of barrier at small shards),
+  // by a kernel reading the mapped staging (an SDMA copy there left the GPU idle ~15-20 us)
   (void)side;
-  LFE_HIP(hipMemcpyAsync(c->items_d, c->hpin_items, ib + bb + xb + lb, hipMemcpyHostToDevice, c->stream));
+  const int64_t words = (int64_t)((ib + bb + xb + lb + 15) / 16);
+  hipLaunchKernelGGL(k_copy_staged, dim3((unsigned)std::min<int64_t>(64, (words + 255) / 256)), dim3(256), 0,
+                     c->stream, reinterpret_cast<const int4*>(c->hpin_items_dev), reinterpret_cast<int4*>(c->items_d),
+                     words);
+  LFE_HIP(hipGetLastError());
   return LFE_OK;
 }
 
@@ -1243,8 +1254,18 @@ int prepare_layout(lfe_ctx* c) {
     unsigned long long bseq = 0;  // the scan's last block publishes the bucket starts (one rank)
     LFE_TRY(exclusive_scan_g(c, c->pcounts, m, nullptr, 0, dbstart, nw, nb, &bseq));
     // (else read on the side stream below, after the scatter is enqueued: no copy enqueue between
-    // the scan and the scatter on the main stream, whose GPU time it was)
-    if (!bseq) LFE_HIP(hipEventRecord(c->up_ev0, c->stream));
+    // the scan and the scatter on the main stream, whose GPU time it was - unless the scatter is
+    // short: the side stream's wait for the scan took ~20 us at 1M rows, longer than the host then
+    // needs to build the items, so up to 16M rows the copy goes on the main stream before the
+    // scatter; same-box A/B, profiles/r06/ab_bstart.txt: 1-10M rows equal or slightly faster)
+    const char* kb = knob("LFE_BSTART_MAIN_ROWS");
+    const bool bs_main = !bseq && n <= (kb ? std::atoll(kb) : (int64_t)(16 << 20));
+    if (bs_main) {
+      LFE_HIP(hipMemcpyAsync(c->hpin, dbstart, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->stream));
+      LFE_HIP(hipEventRecord(c->aux_ev, c->stream));
+    } else if (!bseq) {
+      LFE_HIP(hipEventRecord(c->up_ev0, c->stream));
+    }
     const size_t lds = std::min<size_t>(std::max(part_lds(nth), kLdsMin), 160 * 1024);
     L.part = PartGeom{nth, per, nw, lds};
     // the input row index of each layout row is written only when a caller needs it
@@ -1260,7 +1281,7 @@ int prepare_layout(lfe_ctx* c) {
       for (int j = 0; j < m; ++j) LFE_TRY(ensure_i32(c, W.lay[j], W.lay_cap[j], (size_t)c->ld));
     }
     LFE_TRY(launch_part_scatter(c, /*cols=*/c->sw.on ? 2 : 1, /*orig=*/0));
-    if (!bseq) {
+    if (!bseq && !bs_main) {
       LFE_HIP(hipStreamWaitEvent(c->up_stream, c->up_ev0, 0));  // the scan is done
       LFE_HIP(hipMemcpyAsync(c->hpin, dbstart, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, c->up_stream));
       LFE_HIP(hipEventRecord(c->aux_ev, c->up_stream));
