@@ -333,7 +333,9 @@ struct lfe_ctx {
   size_t clf_S_cap = 0, clf_hi_cap = 0, clf_cnt_cap = 0, clf_fq_cap = 0;
   lfe::ClusterWS clw;
   // pinned host staging (small transfers avoid the runtime's pageable path)
-  char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results, then H2D staging
+  char* hpin = nullptr;            // kPinSmall bytes: [0, kPinD2H) D2H results
+  char* hup = nullptr;             // kPinSmall - kPinD2H bytes of small-upload staging (mapped, coherent)
+  char* hup_dev = nullptr;         // its device address
   // mapped, coherent host memory the device writes small results into (no copy kernel, no event):
   // msg[0] = sequence number, msg[1..] = values; the host spins on the sequence (host_msg_wait)
   unsigned long long* hmsg = nullptr;   // host view

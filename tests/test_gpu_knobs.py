@@ -25,7 +25,7 @@ ENV_VALUES = {
     "LFE_PART_CW": "4096", "LFE_SUMS_CG": "0", "LFE_TAB3": "0", "LFE_GRAM_GEN": "0", "LFE_GRAM_GU": "2",
     "LFE_CHOL_SPLIT": "1", "LFE_SEG_SORTED": "0", "LFE_SEG_SCATTER_ROWS": "1", "LFE_D3_BATCH": "0",
     "LFE_CL_FIX": "0", "LFE_CL_FUSED": "0", "LFE_CL_STATS": "1", "LFE_CL_NO_SINGLETON": "1",
-    "LFE_CL_OWNER_MIN_SPAN": "0", "LFE_CL_MULTI_GATHER": "1", "LFE_ROW_HASH_BITS": "8", "LFE_STR_HASH_BITS": "8", "LFE_HOST_MSG": "1", "LFE_BSTART_MAIN_ROWS": "0",
+    "LFE_CL_OWNER_MIN_SPAN": "0", "LFE_CL_MULTI_GATHER": "1", "LFE_ROW_HASH_BITS": "8", "LFE_STR_HASH_BITS": "8", "LFE_HOST_MSG": "1", "LFE_BSTART_MAIN_ROWS": "0", "LFE_H2D_SDMA": "1",
 }
 
 
