@@ -385,6 +385,11 @@ int lfe_ctx_test_hooks(lfe_ctx* ctx, int flags);
  * The diagnostics LFE_DN8_TIMING / LFE_SWEEP_TIMING print per-workgroup phase times to stderr. */
 int lfe_test_set_knob(const char* name, const char* value);
 
+/* Host helper (no reference counterpart; frame.factorize's dense-code test, polars_impl.py:118-139
+ * casts FE columns to integer codes): min and max of n signed integers of `width` bytes (1, 2, 4
+ * or 8) in one pass over up to 8 host threads. */
+int lfe_int_range(const void* values, int64_t n, int width, int64_t* min_out, int64_t* max_out);
+
 /* Wait for all work queued on the context's stream. */
 int lfe_sync(lfe_ctx* ctx);
 

@@ -67,6 +67,7 @@ SIGNATURES = {
     "lfe_dense_cells": (C.c_int, [_vp, _i64p]),
     "lfe_ctx_test_hooks": (C.c_int, [_vp, C.c_int]),
     "lfe_test_set_knob": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "lfe_int_range": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "lfe_dev_alloc": (C.c_int, [_vp, C.c_int64, C.POINTER(_vp)]),
     "lfe_dev_free": (C.c_int, [_vp, _vp]),
     "lfe_materialize": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int]),
@@ -129,6 +130,15 @@ def load_library(path: str | None = None) -> C.CDLL:
         if path is None:
             _lib = lib
         return lib
+
+
+def int_range(values: np.ndarray) -> tuple[int, int]:
+    """(min, max) of a signed integer array in one multi-threaded pass (lfe_int_range, host only)."""
+    v = np.ascontiguousarray(values)
+    lo, hi = C.c_int64(), C.c_int64()
+    _check(load_library().lfe_int_range(v.ctypes.data_as(C.c_void_p), v.size, v.dtype.itemsize, C.byref(lo),
+                                        C.byref(hi)))
+    return int(lo.value), int(hi.value)
 
 
 def set_knob(name: str, value: str | None) -> None:

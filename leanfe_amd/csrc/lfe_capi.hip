@@ -7,6 +7,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -1476,6 +1477,56 @@ int lfe_exact_sums(lfe_ctx* c, int* on) {
   LFE_CTX(c);
   if (!on) return fail(LFE_EINVAL, "null pointer");
   return exact_sums_on(c, on);
+}
+
+// host: (min, max) of an integer column in one pass over up to 8 threads (the dense-code test of
+// frame.factorize; NumPy's two single-threaded reductions took 14 ms per 50M-row column)
+// one slice: min / max reductions the compiler vectorizes; compiled for AVX2 and for the baseline
+#define LFE_RANGE_SLICE(NAME, ATTR)                                                            \
+  template <typename T>                                                                        \
+  ATTR static void NAME(const T* __restrict__ v, int64_t a, int64_t b, int64_t* lo, int64_t* hi) { \
+    T l = v[a], h = v[a];                                                                      \
+    _Pragma("clang loop vectorize(enable) interleave(enable)")                                 \
+    for (int64_t j = a; j < b; ++j) {                                                          \
+      l = std::min(l, v[j]);                                                                   \
+      h = std::max(h, v[j]);                                                                   \
+    }                                                                                          \
+    *lo = l;                                                                                   \
+    *hi = h;                                                                                   \
+  }
+extern "C++" {
+LFE_RANGE_SLICE(range_slice_avx2, __attribute__((target("avx2"))))
+LFE_RANGE_SLICE(range_slice_base, )
+
+template <typename T>
+static void int_range_t(const T* v, int64_t n, int64_t* mn, int64_t* mx) {
+  const int64_t t = std::max<int64_t>(1, std::min<int64_t>(8, n >> 22));
+  const bool avx2 = __builtin_cpu_supports("avx2");
+  std::vector<int64_t> lo((size_t)t), hi((size_t)t);
+  auto work = [&](int64_t i) {
+    const int64_t a = n * i / t, b = n * (i + 1) / t;
+    if (avx2) range_slice_avx2(v, a, b, &lo[(size_t)i], &hi[(size_t)i]);
+    else range_slice_base(v, a, b, &lo[(size_t)i], &hi[(size_t)i]);
+  };
+  std::vector<std::thread> th;
+  for (int64_t i = 1; i < t; ++i) th.emplace_back(work, i);
+  work(0);
+  for (auto& x : th) x.join();
+  *mn = *std::min_element(lo.begin(), lo.end());
+  *mx = *std::max_element(hi.begin(), hi.end());
+}
+}
+
+int lfe_int_range(const void* values, int64_t n, int width, int64_t* min_out, int64_t* max_out) {
+  if (!min_out || !max_out || n < 1 || !values) return fail(LFE_EINVAL, "lfe_int_range: bad arguments");
+  switch (width) {
+    case 1: int_range_t(static_cast<const int8_t*>(values), n, min_out, max_out); break;
+    case 2: int_range_t(static_cast<const int16_t*>(values), n, min_out, max_out); break;
+    case 4: int_range_t(static_cast<const int32_t*>(values), n, min_out, max_out); break;
+    case 8: int_range_t(static_cast<const int64_t*>(values), n, min_out, max_out); break;
+    default: return fail(LFE_EINVAL, "lfe_int_range: width must be 1, 2, 4 or 8 (signed)");
+  }
+  return LFE_OK;
 }
 
 int lfe_test_set_knob(const char* name, const char* value) {

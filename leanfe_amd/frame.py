@@ -98,6 +98,19 @@ def _polars_to_numpy(s) -> np.ndarray:
     return s.to_numpy()
 
 
+def int_range(v: np.ndarray) -> tuple[int, int]:
+    """(min, max) of an integer array: past 4M signed values one pass over host threads in the
+    engine library (lfe_int_range: NumPy's two single-threaded reductions took 14 ms per 50M-row
+    code column of a 146 ms end-to-end fit, profiles/r06/e2e_profile.txt)."""
+    if v.size >= (1 << 22) and v.dtype.kind == "i":
+        try:
+            from leanfe_amd._lib import int_range as lib_range
+            return lib_range(v)
+        except OSError:  # the library is not built (host-only use): NumPy
+            pass
+    return int(v.min()), int(v.max())
+
+
 def factorize(values, global_codes: bool = False, device=None) -> tuple[np.ndarray, int]:
     """Dense int32 group codes and the number of code values.
 
@@ -123,14 +136,14 @@ def factorize(values, global_codes: bool = False, device=None) -> tuple[np.ndarr
             return np.zeros(0, dtype=np.int32), 1
         if not (np.issubdtype(v.dtype, np.integer) or v.dtype == np.bool_):
             raise ValueError("sharded fits need global non-negative integer FE / cluster codes")
-        vmin, vmax = int(v.min()), int(v.max())
+        vmin, vmax = int_range(v)
         if vmin < 0 or vmax >= 2 ** 31 - 1:
             raise ValueError("sharded fits need global integer codes in [0, 2^31 - 1)")
         return v.astype(np.int32, copy=False), vmax + 1
     if n == 0:
         return np.zeros(0, dtype=np.int32), 1
     if np.issubdtype(v.dtype, np.integer) or v.dtype == np.bool_:
-        vmin, vmax = int(v.min()), int(v.max())
+        vmin, vmax = int_range(v) if v.dtype != np.bool_ else (int(v.min()), int(v.max()))
         if vmin >= 0 and vmax < max(4 * n, 1 << 20) and vmax < 2 ** 31 - 1:
             return v.astype(np.int32, copy=False), vmax + 1
         if device is not None and n < 2 ** 31 - 1 and (v.dtype != np.uint64 or vmax < 2 ** 63):

@@ -355,3 +355,20 @@ def test_expansion_plan_applied_per_chunk_equals_whole_columns():
         chunk = plan.columns(cols, {"treat": cols["treat"][sl]}, sl)
         for name, col in zip(names, chunk):
             np.testing.assert_array_equal(col, whole[name][sl])
+
+
+def test_int_range_matches_numpy():
+    """lfe_int_range (frame.factorize's dense-code test on host threads) = NumPy's min / max for
+    every signed width, extremes and odd lengths included (host code: no GPU)."""
+    from leanfe_amd import frame
+    from leanfe_amd._lib import int_range
+
+    rng = np.random.default_rng(5)
+    for dt in (np.int8, np.int16, np.int32, np.int64):
+        info = np.iinfo(dt)
+        for n in (1, 7, 1_000_003, 5_000_001):
+            v = rng.integers(info.min, info.max, n, dtype=dt, endpoint=True)
+            assert int_range(v) == (int(v.min()), int(v.max()))
+        v = np.zeros(4_200_000, dtype=dt)
+        v[-1], v[0] = info.max, info.min
+        assert int_range(v) == (int(info.min), int(info.max)) == frame.int_range(v)
