@@ -1066,13 +1066,10 @@ struct TabFinal {
   double* beta;
   double* beta_copy;
   double* ok;
-  unsigned int* done;  // non-null: the last block of k_tables_gram runs the final step itself
 };
-template <int PM, int NTH>
-__device__ void tables_final_body(const double* __restrict__ partial, int nblk, int p, const TabFinal& f);
 
 template <int PM>
-__global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restrict__ partial, TabFinal fin) {
+__global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restrict__ partial) {
   constexpr int NG = PM * (PM + 1) / 2;
   constexpr int NA = NG + PM;
   __shared__ double red[4][NA];
@@ -1124,8 +1121,6 @@ __global__ __launch_bounds__(256) void k_tables_gram(TabArgs t, double* __restri
   // entry-major [NA][blocks]: the final kernel's lanes then read consecutive blocks of one entry
   for (int e = threadIdx.x; e < NA; e += blockDim.x)
     partial[(int64_t)e * gridDim.x + blockIdx.x] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
-  // one launch for the partials and the final tile + Cholesky: the last block to finish sums them
-  if (fin.done && last_block_done(fin.done)) tables_final_body<PM, 256>(partial, gridDim.x, p, fin);
 }
 
 // out[e] = sum over the row e of an entry-major [rows][nblk] partial table, blocks in order
@@ -1213,23 +1208,20 @@ static int tables_gram_enqueue(lfe_ctx* c, double* out_dev, double* flag_dev, do
       hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(64), 0, c->stream, out_dev, p, beta, beta_copy, ok);
     return LFE_OK;
   };
-  // one rank (the usual case): the last block of k_tables_gram forms the tile and solves it
-  // (the fused form - the last block of k_tables_gram summing the partials on 256 threads - measured
-  // 43 us against 14 + 14 us for the two launches at the 8-rank shard: kept apart)
-  const bool fuse = false;
-  const TabFinal fin{c->raw_tile, out_dev, flag_dev, beta, beta_copy, ok, fuse ? c->gsync + GS_TABLES_GRAM : nullptr};
+  // (a fused form - the last block of k_tables_gram summing the partials and solving on 256 threads -
+  // measured 43 us against 14 + 14 us for the two launches at the 8-rank shard: kept apart)
   switch (PM) {
     case 4:
-      hipLaunchKernelGGL(k_tables_gram<4>, dim3(nblk), dim3(256), 0, c->stream, t, part, fin);
-      if (!fuse) LFE_TRY(final_from(k_tables_final_chol<4>));
+      hipLaunchKernelGGL(k_tables_gram<4>, dim3(nblk), dim3(256), 0, c->stream, t, part);
+      LFE_TRY(final_from(k_tables_final_chol<4>));
       break;
     case 8:
-      hipLaunchKernelGGL(k_tables_gram<8>, dim3(nblk), dim3(256), 0, c->stream, t, part, fin);
-      if (!fuse) LFE_TRY(final_from(k_tables_final_chol<8>));
+      hipLaunchKernelGGL(k_tables_gram<8>, dim3(nblk), dim3(256), 0, c->stream, t, part);
+      LFE_TRY(final_from(k_tables_final_chol<8>));
       break;
     default:
-      hipLaunchKernelGGL(k_tables_gram<12>, dim3(nblk), dim3(256), 0, c->stream, t, part, fin);
-      if (!fuse) LFE_TRY(final_from(k_tables_final_chol<12>));
+      hipLaunchKernelGGL(k_tables_gram<12>, dim3(nblk), dim3(256), 0, c->stream, t, part);
+      LFE_TRY(final_from(k_tables_final_chol<12>));
       break;
   }
   LFE_HIP(hipGetLastError());
@@ -1419,7 +1411,7 @@ __global__ __launch_bounds__(1024) void k_tables_final_chol(const double* __rest
                                                             double* __restrict__ ok, const unsigned long long* gate,
                                                             double gate_tol) {
   if (gate_closed(gate, gate_tol)) return;
-  const TabFinal f{raw, tile, flag, beta, beta_copy, ok, nullptr};
+  const TabFinal f{raw, tile, flag, beta, beta_copy, ok};
   tables_final_body<PM, 1024>(partial, nblk, p, f);
 }
 
