@@ -447,20 +447,29 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
         iacc[I] = 0;
       }
     };
-    for (int gs0 = lo; gs0 < hi && !done; gs0 += 16 * UNR) {
-      // codes of UNR 16-row groups, then all their gathers
+    // the codes of a batch of UNR 16-row groups are loaded one batch ahead (ping-pong register sets,
+    // no copies): a batch then waits on its gathers only, not on a code load before them
+    auto load_codes = [&](int gs0, int4 (&cv)[UNR][NO]) {
+#pragma unroll
+      for (int U = 0; U < UNR; ++U) {
+        const int rb = min(gs0 + 16 * U, hi - 1) & ~15;  // a group past the unit reloads a valid one
+#pragma unroll
+        for (int j = 0; j < NO; ++j) cv[U][j] = *reinterpret_cast<const int4*>(a.oc[j] + rb + 4 * kq);
+      }
+    };
+    auto batch = [&](int gs0, const int4 (&cv)[UNR][NO]) {
       int cd[UNR][NO][4];
 #pragma unroll
       for (int U = 0; U < UNR; ++U) {
         const int rb = gs0 + 16 * U + 4 * kq;
+        const bool gin = gs0 + 16 * U < hi;
 #pragma unroll
         for (int j = 0; j < NO; ++j) {
-          int4 v = int4{0, 0, 0, 0};
-          if (gs0 + 16 * U < hi) v = *reinterpret_cast<const int4*>(a.oc[j] + rb);
-          cd[U][j][0] = rb + 0 < hi ? v.x : 0;
-          cd[U][j][1] = rb + 1 < hi ? v.y : 0;
-          cd[U][j][2] = rb + 2 < hi ? v.z : 0;
-          cd[U][j][3] = rb + 3 < hi ? v.w : 0;
+          const int4 v = cv[U][j];
+          cd[U][j][0] = gin && rb + 0 < hi ? v.x : 0;
+          cd[U][j][1] = gin && rb + 1 < hi ? v.y : 0;
+          cd[U][j][2] = gin && rb + 2 < hi ? v.z : 0;
+          cd[U][j][3] = gin && rb + 3 < hi ? v.w : 0;
         }
       }
       double val[UNR][4][NT];
@@ -528,6 +537,17 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
           if (r0 >= ge) break;
         }
       }
+    };
+    int4 cva[UNR][NO], cvb[UNR][NO];
+    load_codes(lo, cva);
+    for (int gs0 = lo; gs0 < hi && !done;) {
+      load_codes(gs0 + 16 * UNR, cvb);
+      batch(gs0, cva);
+      gs0 += 16 * UNR;
+      if (gs0 >= hi || done) break;
+      load_codes(gs0 + 16 * UNR, cva);
+      batch(gs0, cvb);
+      gs0 += 16 * UNR;
     }
     // segment h continues past the unit: partial sum
     if (!done && h < G && r0 < hi && r1 > hi) finalize(part ? 1 : 2);
