@@ -447,67 +447,64 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
         iacc[I] = 0;
       }
     };
-    // the codes of a batch of UNR 16-row groups are loaded one batch ahead (ping-pong register sets,
-    // no copies): a batch then waits on its gathers only, not on a code load before them
-    auto load_codes = [&](int gs0, int4 (&cv)[UNR][NO]) {
+    // pipeline: a batch's codes are loaded two batches ahead and its gathers one batch ahead (ping-pong
+    // register sets, no copies): the batch being summed waits on nothing
+    constexpr int UG = UNR > 1 ? UNR / 2 : 1;  // groups per batch
+    auto load_codes = [&](int gs0, int4 (&cv)[UG][NO]) {
 #pragma unroll
-      for (int U = 0; U < UNR; ++U) {
+      for (int U = 0; U < UG; ++U) {
         const int rb = min(gs0 + 16 * U, hi - 1) & ~15;  // a group past the unit reloads a valid one
 #pragma unroll
         for (int j = 0; j < NO; ++j) cv[U][j] = *reinterpret_cast<const int4*>(a.oc[j] + rb + 4 * kq);
       }
     };
-    auto batch = [&](int gs0, const int4 (&cv)[UNR][NO]) {
-      int cd[UNR][NO][4];
+    auto gather = [&](int gs0, const int4 (&cv)[UG][NO], double (&gv)[UG][NO][4][NT]) {
 #pragma unroll
-      for (int U = 0; U < UNR; ++U) {
+      for (int U = 0; U < UG; ++U) {
         const int rb = gs0 + 16 * U + 4 * kq;
         const bool gin = gs0 + 16 * U < hi;
 #pragma unroll
         for (int j = 0; j < NO; ++j) {
           const int4 v = cv[U][j];
-          cd[U][j][0] = gin && rb + 0 < hi ? v.x : 0;
-          cd[U][j][1] = gin && rb + 1 < hi ? v.y : 0;
-          cd[U][j][2] = gin && rb + 2 < hi ? v.z : 0;
-          cd[U][j][3] = gin && rb + 3 < hi ? v.w : 0;
-        }
-      }
-      double val[UNR][4][NT];
+          const int cd[4] = {gin && rb + 0 < hi ? v.x : 0, gin && rb + 1 < hi ? v.y : 0,
+                             gin && rb + 2 < hi ? v.z : 0, gin && rb + 3 < hi ? v.w : 0};
 #pragma unroll
-      for (int U = 0; U < UNR; ++U)
+          for (int s = 0; s < 4; ++s) {
+            const double* al = a.alpha[j] + (uint64_t)(uint32_t)cd[s] * (uint32_t)p;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-#pragma unroll
-          for (int I = 0; I < NT; ++I) val[U][s][I] = 0.0;
-#pragma unroll
-          for (int j = 0; j < NO; ++j) {
-            const double* al = a.alpha[j] + (uint64_t)(uint32_t)cd[U][j][s] * (uint32_t)p;
-#pragma unroll
-            for (int I = 0; I < NT; ++I) val[U][s][I] += al[cl[I]];
+            for (int I = 0; I < NT; ++I) gv[U][j][s][I] = al[cl[I]];
           }
         }
+      }
+    };
+    auto batch = [&](int gs0, const double (&gv)[UG][NO][4][NT]) {
 #pragma unroll
-      for (int U = 0; U < UNR; ++U) {
+      for (int U = 0; U < UG; ++U) {
         const int gs = gs0 + 16 * U, ge = gs + 16;
         if (gs >= hi || done) break;
         const int rb = gs + 4 * kq;
+        double val[4][NT];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           double ws = rb + s < hi ? 1.0 : 0.0;
           if (WT) ws = rb + s < hi ? a.ws[rb + s] : 0.0;
 #pragma unroll
-          for (int I = 0; I < NT; ++I) val[U][s][I] *= ws;
+          for (int I = 0; I < NT; ++I) {
+            double t = gv[U][0][s][I];
+#pragma unroll
+            for (int j = 1; j < NO; ++j) t += gv[U][j][s][I];
+            val[s][I] = t * ws;
+          }
         }
         while (true) {
           if (r0 <= gs && r1 >= ge) {  // the whole group lies in segment h
             if (ex) {
 #pragma unroll
               for (int I = 0; I < NT; ++I)
-                iacc[I] += (fx(val[U][0][I], I) + fx(val[U][1][I], I)) + (fx(val[U][2][I], I) + fx(val[U][3][I], I));
+                iacc[I] += (fx(val[0][I], I) + fx(val[1][I], I)) + (fx(val[2][I], I) + fx(val[3][I], I));
             } else {
 #pragma unroll
-              for (int I = 0; I < NT; ++I)
-                acc[I] += (val[U][0][I] + val[U][1][I]) + (val[U][2][I] + val[U][3][I]);
+              for (int I = 0; I < NT; ++I) acc[I] += (val[0][I] + val[1][I]) + (val[2][I] + val[3][I]);
             }
           } else {
 #pragma unroll
@@ -516,8 +513,8 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
               const bool in = row >= r0 && row < r1;
 #pragma unroll
               for (int I = 0; I < NT; ++I) {
-                if (ex) iacc[I] += in ? fx(val[U][s][I], I) : 0ll;
-                else acc[I] += in ? val[U][s][I] : 0.0;
+                if (ex) iacc[I] += in ? fx(val[s][I], I) : 0ll;
+                else acc[I] += in ? val[s][I] : 0.0;
               }
             }
           }
@@ -538,16 +535,22 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_cross(SegCrossArgs a) {
         }
       }
     };
-    int4 cva[UNR][NO], cvb[UNR][NO];
+    constexpr int B = 16 * UG;  // rows per batch
+    int4 cva[UG][NO], cvb[UG][NO];
+    double gva[UG][NO][4][NT], gvb[UG][NO][4][NT];
     load_codes(lo, cva);
+    load_codes(lo + B, cvb);
+    gather(lo, cva, gva);
     for (int gs0 = lo; gs0 < hi && !done;) {
-      load_codes(gs0 + 16 * UNR, cvb);
-      batch(gs0, cva);
-      gs0 += 16 * UNR;
+      load_codes(gs0 + 2 * B, cva);  // batch + 2
+      gather(gs0 + B, cvb, gvb);     // batch + 1
+      batch(gs0, gva);
+      gs0 += B;
       if (gs0 >= hi || done) break;
-      load_codes(gs0 + 16 * UNR, cva);
-      batch(gs0, cvb);
-      gs0 += 16 * UNR;
+      load_codes(gs0 + 2 * B, cvb);
+      gather(gs0 + B, cva, gva);
+      batch(gs0, gvb);
+      gs0 += B;
     }
     // segment h continues past the unit: partial sum
     if (!done && h < G && r0 < hi && r1 > hi) finalize(part ? 1 : 2);
