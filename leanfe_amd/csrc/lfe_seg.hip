@@ -768,6 +768,8 @@ __global__ void k_check_max(const double* __restrict__ Sy, int sy_stride, const 
 // consecutive positions per step.
 struct SegCheckArgs {
   const int32_t* seg_off;  // [G + 1]
+  const int32_t* ufirst;   // [n_units] the segment holding each unit's first position
+  int n_units;
   int32_t G;
   const int32_t* oc[kMaxFE - 1];
   const double* ay[kMaxFE - 1];
@@ -781,53 +783,54 @@ __global__ __launch_bounds__(256) void k_seg_check(SegCheckArgs a) {
   const int lane = threadIdx.x & 63;
   const int32_t kept = a.seg_off[a.G];
   const FixCol fc = fix_col(a.xq, 0);
-  const int64_t nwaves = (int64_t)gridDim.x * 4;
-  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 256; base < kept; base += nwaves * 256) {
-    // the segment holding position base (binary search, wave-uniform)
-    int lo = 0, hi = a.G - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (a.seg_off[mid] <= base) lo = mid;
-      else hi = mid - 1;
-    }
-    int h = lo;
-    double y[4];
+  const int nwaves = gridDim.x * 4;
+  // a wave walks whole units of kSegUnit positions from the unit's first segment (ufirst), carrying
+  // the segment from step to step (a binary search over seg_off per 256 positions cost ~20 dependent
+  // loads each at 1e6 segments)
+  for (int uu = blockIdx.x * 4 + (threadIdx.x >> 6); uu < a.n_units; uu += nwaves) {
+    const int64_t u0 = (int64_t)uu * kSegUnit;
+    if (u0 >= kept) break;
+    const int64_t u1 = min((int64_t)kept, u0 + kSegUnit);
+    int h = __builtin_amdgcn_readfirstlane(a.ufirst[uu]);
+    for (int64_t base = u0; base < u1; base += 256) {
+      double y[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // every gather of the step in flight together
-      const int64_t q = base + u * 64 + lane;
-      double v = 0.0;
-      if (q < kept)
-        for (int j = 0; j < a.no; ++j) v += a.ay[j][a.oc[j][q]];
-      y[u] = v;
-    }
+      for (int u = 0; u < 4; ++u) {  // every gather of the step in flight together
+        const int64_t q = base + u * 64 + lane;
+        double v = 0.0;
+        if (q < kept)
+          for (int j = 0; j < a.no; ++j) v += a.ay[j][a.oc[j][q]];
+        y[u] = v;
+      }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t q = base + u * 64 + lane;
-      const bool in = q < kept;
-      int hl = h;  // this lane's segment: h, or a few after it
-      if (in)
-        while (a.seg_off[hl + 1] <= q) ++hl;
-      double hh = 0.0;
-      long long lo_i = in ? (long long)fix_split(y[u], fc, hh) : 0ll;
-      if (!in) hl = 0x7fffffff;
-      // segmented inclusive scan over the lanes (segment ids do not decrease)
+      for (int u = 0; u < 4; ++u) {
+        const int64_t q = base + u * 64 + lane;
+        const bool in = q < kept;
+        int hl = h;  // this lane's segment: h, or a few after it
+        if (in)
+          while (a.seg_off[hl + 1] <= q) ++hl;
+        double hh = 0.0;
+        long long lo_i = in ? (long long)fix_split(y[u], fc, hh) : 0ll;
+        if (!in) hl = 0x7fffffff;
+        // segmented inclusive scan over the lanes (segment ids do not decrease)
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int oh = __shfl_up(hl, off, 64);
-        const long long ol = __shfl_up(lo_i, off, 64);
-        const double oH = __shfl_up(hh, off, 64);
-        if (lane >= off && oh == hl) {
-          lo_i += ol;
-          hh += oH;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int oh = __shfl_up(hl, off, 64);
+          const long long ol = __shfl_up(lo_i, off, 64);
+          const double oH = __shfl_up(hh, off, 64);
+          if (lane >= off && oh == hl) {
+            lo_i += ol;
+            hh += oH;
+          }
         }
+        const int nh = __shfl_down(hl, 1, 64);
+        if (in && (lane == 63 || nh != hl)) {  // the last lane of its run
+          atomicAdd(&a.R[hl], (unsigned long long)lo_i);
+          if (hh != 0.0) atomicAdd(&a.Rhi[hl], hh);
+        }
+        h = __shfl(hl, 63, 64);  // the next 64 positions start in the last lane's segment (or later)
+        if (h == 0x7fffffff) h = a.G - 1;
       }
-      const int nh = __shfl_down(hl, 1, 64);
-      if (in && (lane == 63 || nh != hl)) {  // the last lane of its run
-        atomicAdd(&a.R[hl], (unsigned long long)lo_i);
-        if (hh != 0.0) atomicAdd(&a.Rhi[hl], hh);
-      }
-      h = __shfl(hl, 63, 64);  // the next 64 positions start in the last lane's segment (or later)
-      if (h == 0x7fffffff) h = a.G - 1;
     }
   }
 }
@@ -1047,6 +1050,8 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
   if (y_only && !wt) {  // the unweighted check term: one row per lane (k_seg_check)
     SegCheckArgs k{};
     k.seg_off = fe.seg_off;
+    k.ufirst = a.ufirst;
+    k.n_units = a.n_units;
     k.G = fe.G;
     for (int j2 = 0; j2 < c->F - 1; ++j2) {
       k.oc[j2] = a.oc[j2];
@@ -1057,10 +1062,9 @@ static int seg_cross(lfe_ctx* c, int f, bool y_only, int kid) {
     k.R = reinterpret_cast<unsigned long long*>(out);
     k.Rhi = fe.hi;
     const int64_t n_kept = c->n;  // an upper bound on the kept positions (the kernel reads seg_off[G])
-    if (n_kept > 0 && fe.G > 0) {
+    if (n_kept > 0 && fe.G > 0 && a.n_units > 0) {
       ProfScope _ps(c, kid);
-      hipLaunchKernelGGL(k_seg_check, dim3(grid_for((n_kept + 255) / 256 * 64, 256, 4096)), dim3(256), 0, c->stream,
-                         k);
+      hipLaunchKernelGGL(k_seg_check, dim3((unsigned)((a.n_units + 3) / 4)), dim3(256), 0, c->stream, k);
     }
     LFE_HIP(hipGetLastError());
   } else if (a.n_units > 0) {
