@@ -370,9 +370,11 @@ static int singleton_meat(lfe_ctx* c, const int32_t* R, int32_t G, int k, double
   if (G2 > 0) {
     LFE_TRY(ensure_i32(c, W.seg2, W.seg2_cap, (size_t)G2 + 1));
     LFE_TRY(ensure_i32(c, W.r2, W.r2_cap, (size_t)N2));
-    // k <= 16: the clusters' sums by a 16-lane group each, straight from the score rows, and the rows'
-    // Gram through the row index (no gathered copy t2); LFE_CL_MULTI_GATHER: the gathered copy
-    const bool direct = k <= 16 && knob("LFE_CL_MULTI_GATHER") == nullptr;
+    // 8 <= k <= 16: the clusters' sums by a 16-lane group each, straight from the score rows, and the
+    // rows' Gram through the row index (no gathered copy t2: MEGA_CLUSTER2 25.9 -> 25.3 ms); narrower
+    // rows keep the copy (k = 4, HDFE_CLUSTER2: the indexed Gram's 32-byte gathers cost 0.13 ms more
+    // than copy + Gram); LFE_CL_MULTI_GATHER: the copy always
+    const bool direct = k >= 8 && k <= 16 && knob("LFE_CL_MULTI_GATHER") == nullptr;
     if (!direct) LFE_TRY(ensure_f64(c, W.t2, W.t2_cap, (size_t)N2 * k));
     LFE_TRY(ensure_f64(c, W.s2, W.s2_cap, (size_t)G2 * k));
     LFE_TRY(h2d_small(c, W.seg2 + G2, &N2, sizeof(int32_t)));

@@ -849,7 +849,7 @@ __device__ __forceinline__ void host_msg_publish_i32(unsigned long long* msg, un
 
 constexpr int kGsyncSlots = 16;
 constexpr size_t kHostMsgBytes = 16384;  // lfe_ctx::hmsg: 2048 tagged words (1024 doubles)
-enum GsyncSlot { GS_SPARE = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_CNT_ITEMS = 4, GS_SCAN = 5, GS_TQ_REDUCE = 6, GS_SCAN_DONE = 7 };
+enum GsyncSlot { GS_SPARE = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_SPARE1 = 4, GS_SCAN = 5, GS_TQ_REDUCE = 6, GS_SCAN_DONE = 7 };
 __device__ __forceinline__ bool last_block_done(unsigned int* counter) {
   __shared__ unsigned int amlast;
   __syncthreads();

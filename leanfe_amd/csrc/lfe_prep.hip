@@ -274,43 +274,9 @@ __global__ __launch_bounds__(256) void k_scan_add_few(ScanPair sp, const int32_t
     }
 }
 
-// small scans in one launch: one 1024-thread block walks a1 then a2 in 8192-element rounds
-// (eight per thread, carried from round to round), with out[b] = a1[b * gstride] from registers
-constexpr int64_t kScanOneMax = 16384;
-__global__ __launch_bounds__(1024) void k_scan_one(ScanPair sp, int32_t* __restrict__ gout, int64_t gstride, int gn) {
-  __shared__ int32_t tmp[16];
-  __shared__ int32_t total;
-  for (int arr = 0; arr < 2; ++arr) {
-    int32_t* a = arr ? sp.a2 : sp.a1;
-    const int64_t m = arr ? sp.m2 : sp.m1;
-    if (!a) continue;
-    int32_t carry = 0;
-    for (int64_t r0 = 0; r0 < m; r0 += 1024 * kScanPer) {
-      const int64_t base = r0 + (int64_t)threadIdx.x * kScanPer;
-      int32_t v[kScanPer];
-      scan_load8(a, base, m, v);
-      int32_t t = 0;
-#pragma unroll
-      for (int k = 0; k < kScanPer; ++k) t += v[k];
-      int32_t off = block_excl_scan(t, tmp, &total) + carry;
-      int32_t o[kScanPer];
-#pragma unroll
-      for (int k = 0; k < kScanPer; ++k) {
-        o[k] = off;
-        off += v[k];
-      }
-      scan_store8(a, base, m, o);
-      if (gout && arr == 0)
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k)
-          if (base + k < m && (base + k) % gstride == 0 && (base + k) / gstride < gn) gout[(base + k) / gstride] = o[k];
-      carry += total;
-      __syncthreads();  // total is rewritten by the next round
-    }
-  }
-}
+constexpr int64_t kScanFusedMax = 96;  // blocks of the one-launch ticketed scan (k_scan_fused)
 
-// Up to kScanFewBlocks blocks in one launch: a block takes the next ticket (the dispatch order, so
+// Up to kScanFusedMax blocks in one launch: a block takes the next ticket (the dispatch order, so
 // it waits only on blocks that are running), scans its 2048 elements, publishes its sum tagged with
 // the launch's epoch, then adds the published sums of the blocks before it in its array (integer
 // adds: any order) - k_scan_blocks + k_scan_add_few without the kernel boundary.  status needs no
@@ -384,7 +350,10 @@ static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, in
   }
   const ScanPair sp{a1, m1, nb1, a2, m2};
   ProfScope _ps(c, K_SCAN);
-  if (nblocks <= kScanFewBlocks) {  // one launch
+  // one launch for few blocks: every block reads the published sums of all blocks before it, so the
+  // reads grow with the square of the blocks (292 blocks, the headline's partition scan: 28 us against
+  // 13 us for k_scan_blocks + k_scan_add_few; 37 blocks, the 8-rank shard's: 11 against 14 us)
+  if (nblocks <= kScanFusedMax) {
     if (!c->scan_status) {
       LFE_HIP(hipMalloc(reinterpret_cast<void**>(&c->scan_status), sizeof(unsigned long long) * kScanFewBlocks));
       LFE_HIP(hipMemsetAsync(c->scan_status, 0, sizeof(unsigned long long) * kScanFewBlocks, c->stream));
@@ -397,11 +366,6 @@ static int exclusive_scan_g(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, in
     hipLaunchKernelGGL(k_scan_fused, dim3((unsigned)nblocks), dim3(256), 0, c->stream, sp, c->scan_status,
                        c->gsync + GS_SCAN, c->scan_epoch, (int)nblocks, gout, gstride, gn, c->gsync + GS_SCAN_DONE,
                        msg ? c->dmsg : nullptr, msg ? *gout_seq : 0ull);
-    LFE_HIP(hipGetLastError());
-    return LFE_OK;
-  }
-  if (m1 + (a2 ? m2 : 0) <= kScanOneMax) {  // one launch instead of two
-    hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(1024), 0, c->stream, sp, gout, gstride, gn);
     LFE_HIP(hipGetLastError());
     return LFE_OK;
   }
@@ -760,7 +724,7 @@ __global__ __launch_bounds__(NTH) void k_part_scatter(ScatterArgs a) {
 __global__ void k_cnt_from_items(const int32_t* __restrict__ cnt1, const int32_t* __restrict__ cnt2,
                                  const int32_t* __restrict__ bitems, int s, int32_t G_P, int32_t* __restrict__ cntP,
                                  int n_items, int32_t G_Q, int32_t* __restrict__ cntQ, int nbp, int nqx,
-                                 int32_t* __restrict__ any, unsigned int* __restrict__ done) {
+                                 int32_t* __restrict__ any) {
   int found = 0;
   if ((int)blockIdx.x < nbp) {
     const int B = 1 << s;
@@ -784,12 +748,16 @@ __global__ void k_cnt_from_items(const int32_t* __restrict__ cnt1, const int32_t
       if (t) atomicAdd(&cntQ[q], t);
     }
   }
-  if (!done) return;
-  if (__any(found) && (threadIdx.x & 63) == 0) atomicAdd(any, 1);
-  if (!last_block_done(done)) return;
-  found = 0;
-  for (int q = threadIdx.x; q < G_Q; q += blockDim.x)
-    found |= __hip_atomic_load(&cntQ[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
+  // the primary FE's singleton levels counted here (its counts are final per thread); the secondary
+  // FE's, whose counts the blocks add up, by k_any_eq1 after the launch.  (Folding that check into
+  // the last block to finish cost every block a fence and a counter add: +9 to +44 us at 1-15M rows.)
+  if (any && __any(found) && (threadIdx.x & 63) == 0) atomicAdd(any, 1);
+}
+
+// any level with a count of one -> *any += 1 (per wave)
+__global__ void k_any_eq1(const int32_t* __restrict__ cnt, int32_t G, int32_t* __restrict__ any) {
+  int found = 0;
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) found |= cnt[g] == 1;
   if (__any(found) && (threadIdx.x & 63) == 0) atomicAdd(any, 1);
 }
 
@@ -1328,7 +1296,10 @@ int prepare_layout(lfe_ctx* c) {
     const bool one = c->world == 1;  // (several ranks sum the counts afterwards: k_any_singleton then)
     hipLaunchKernelGGL(k_cnt_from_items, dim3(nbp + nqx * 256), dim3(256), 0, c->stream, c1, c2, c->bitems_d, L.s,
                        c->fe[L.P].G, c->fe[L.P].cnt_pre, L.n_items, c->fe[Q].G, c->fe[Q].cnt_pre, nbp, nqx,
-                       c->iscratch + kIsAny, one ? c->gsync + GS_CNT_ITEMS : nullptr);
+                       one ? c->iscratch + kIsAny : nullptr);
+    if (one)
+      hipLaunchKernelGGL(k_any_eq1, dim3((unsigned)std::min(64, (c->fe[Q].G + 255) / 256)), dim3(256), 0, c->stream,
+                         c->fe[Q].cnt_pre, c->fe[Q].G, c->iscratch + kIsAny);
     c->any_ready = one;
     LFE_HIP(hipGetLastError());
   } else if (L.permuted) {

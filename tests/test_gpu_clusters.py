@@ -255,14 +255,14 @@ def test_clusters_loaded_after_the_fused_pass():
         assert np.abs(a - b).max() <= 1e-12 * np.abs(b).max()
 
 
-@pytest.mark.parametrize("k", [3, 14, 20])
+@pytest.mark.parametrize("k", [3, 10, 14, 20])
 def test_mostly_singleton_intersection_multi_row_corrections(k, knob):
     """A two-way CGM whose intersection is mostly singletons (mean cluster size < 2, as config 4's
     fe2 x fe3 and MEGA_CLUSTER2's fe1 x fe2): meat = D + sum over clusters of two or more rows of
-    (S_c S_c' - sum_i s_i s_i').  k <= 16 forms the corrections in one pass over those clusters' rows
-    (k_multi_sums16 and the Gram through the row index); k = 20, and LFE_CL_MULTI_GATHER, gather the rows and Gram the tables;
-    LFE_CL_NO_SINGLETON sums every cluster.  All three at 1e-12, the oracle at 1e-10 with equal cluster
-    counts, bit-identical repeats."""
+    (S_c S_c' - sum_i s_i s_i').  8 <= k <= 16 sums each cluster's rows straight from the score rows
+    (k_multi_sums16) and forms the rows' Gram through the row index; k = 3, k = 20 and
+    LFE_CL_MULTI_GATHER gather the rows into a copy first; LFE_CL_NO_SINGLETON sums every cluster.
+    All at 1e-12 of each other, the oracle at 1e-10 with equal cluster counts, bit-identical repeats."""
     from oracle import altproj
 
     n, L = 400_000, [2_000, 400, 50]  # 800K cells: ~60 % of the rows singletons, the rest in 2+ row clusters
