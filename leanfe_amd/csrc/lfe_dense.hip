@@ -71,9 +71,8 @@ struct DnBuildArgs {
   int32_t* flag;
   int G_P, G_Q;
   // one rank: the singleton test of k_any_singleton folded in - a primary count of 1 where it is
-  // written, the secondary counts (summed by atomics over the workgroups) by the last workgroup
+  // written; the secondary counts (summed by atomics over the workgroups) by launch_any_eq1 after
   int32_t* any;
-  unsigned int* done;
 };
 
 // pre-filter mode: row sums of the chunk's counters = the primary counts of its groups (each group is
@@ -387,12 +386,6 @@ __device__ void dn_build_body(const DnBuildArgs& a, uint32_t* cw);
 __global__ __launch_bounds__(1024) void k_dn_build(DnBuildArgs a) {
   extern __shared__ uint32_t cw[];  // [HC][GQ16] 8-bit or [HC / 2][GQ16] 16-bit counters
   dn_build_body(a, cw);
-  if (a.done && last_block_done(a.done)) {  // every secondary count is final: any of them 1?
-    int found = 0;
-    for (int q = threadIdx.x; q < a.G_Q; q += blockDim.x)
-      found |= __hip_atomic_load(&a.cntQ[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
-    if (__any(found) && (threadIdx.x & 63) == 0) atomicAdd(a.any, 1);
-  }
 }
 
 __device__ void dn_build_body(const DnBuildArgs& a, uint32_t* cw) {
@@ -1297,7 +1290,6 @@ int dense_build(lfe_ctx* c, bool pre) {
     a.flag = c->iscratch + kIsDnPre;
     if (c->world == 1) {  // (several ranks: the counts are summed afterwards, k_any_singleton tests them)
       a.any = c->iscratch + kIsAny;
-      a.done = c->gsync + GS_DN_BUILD;
       c->any_ready = true;
     }
   }
@@ -1347,6 +1339,9 @@ int dense_build(lfe_ctx* c, bool pre) {
   ProfScope _ps(c, K_LAYOUT_SCATTER);
   hipLaunchKernelGGL(k_dn_build, dim3(grid), dim3(1024), lds, c->stream, a);
   LFE_HIP(hipGetLastError());
+  // the secondary FE's singleton levels once its counts are final (its own small kernel: a test in
+  // the build's last workgroup cost every workgroup a fence and a counter add, +13 us at 50M rows)
+  if (a.any) LFE_TRY(launch_any_eq1(c, a.cntQ, a.G_Q, a.any));
   return LFE_OK;
 }
 

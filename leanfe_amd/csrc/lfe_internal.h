@@ -667,6 +667,8 @@ inline void dfree_any(T*& p) {
 int exclusive_scan(lfe_ctx* c, int32_t* a, int64_t m);
 // two independent exclusive scans in one set of launches (a2 may be null)
 int exclusive_scan2(lfe_ctx* c, int32_t* a1, int64_t m1, int32_t* a2, int64_t m2);
+// *any += 1 (per wave) if some level of cnt[0, G) has a count of one (a singleton test)
+int launch_any_eq1(lfe_ctx* c, const int32_t* cnt, int32_t G, int32_t* any);
 // zero up to 32 device ranges (byte counts multiples of 4) in one launch instead of a memset each
 int zero_ranges(lfe_ctx* c, const std::vector<std::pair<void*, size_t>>& ranges);
 // the same ranges as kernel arguments, for a kernel that zeroes them beside its own work
@@ -849,7 +851,7 @@ __device__ __forceinline__ void host_msg_publish_i32(unsigned long long* msg, un
 
 constexpr int kGsyncSlots = 16;
 constexpr size_t kHostMsgBytes = 16384;  // lfe_ctx::hmsg: 2048 tagged words (1024 doubles)
-enum GsyncSlot { GS_SPARE = 0, GS_RESID = 1, GS_FINISH = 2, GS_DN_BUILD = 3, GS_SPARE1 = 4, GS_SCAN = 5, GS_TQ_REDUCE = 6, GS_SCAN_DONE = 7 };
+enum GsyncSlot { GS_SPARE = 0, GS_RESID = 1, GS_FINISH = 2, GS_SPARE2 = 3, GS_SPARE1 = 4, GS_SCAN = 5, GS_TQ_REDUCE = 6, GS_SCAN_DONE = 7 };
 __device__ __forceinline__ bool last_block_done(unsigned int* counter) {
   __shared__ unsigned int amlast;
   __syncthreads();

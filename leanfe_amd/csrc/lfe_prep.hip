@@ -761,6 +761,13 @@ __global__ void k_any_eq1(const int32_t* __restrict__ cnt, int32_t G, int32_t* _
   if (__any(found) && (threadIdx.x & 63) == 0) atomicAdd(any, 1);
 }
 
+int launch_any_eq1(lfe_ctx* c, const int32_t* cnt, int32_t G, int32_t* any) {
+  if (G > 0)
+    hipLaunchKernelGGL(k_any_eq1, dim3((unsigned)std::min(64, (G + 255) / 256)), dim3(256), 0, c->stream, cnt, G, any);
+  LFE_HIP(hipGetLastError());
+  return LFE_OK;
+}
+
 // primary-FE counts: per work item an LDS slice of 2^s bins
 __global__ __launch_bounds__(256) void k_count_items(const int4* __restrict__ items, const int32_t* __restrict__ code,
                                                      int s, int32_t G, int32_t* __restrict__ cnt) {
@@ -1297,9 +1304,7 @@ int prepare_layout(lfe_ctx* c) {
     hipLaunchKernelGGL(k_cnt_from_items, dim3(nbp + nqx * 256), dim3(256), 0, c->stream, c1, c2, c->bitems_d, L.s,
                        c->fe[L.P].G, c->fe[L.P].cnt_pre, L.n_items, c->fe[Q].G, c->fe[Q].cnt_pre, nbp, nqx,
                        one ? c->iscratch + kIsAny : nullptr);
-    if (one)
-      hipLaunchKernelGGL(k_any_eq1, dim3((unsigned)std::min(64, (c->fe[Q].G + 255) / 256)), dim3(256), 0, c->stream,
-                         c->fe[Q].cnt_pre, c->fe[Q].G, c->iscratch + kIsAny);
+    if (one) LFE_TRY(launch_any_eq1(c, c->fe[Q].cnt_pre, c->fe[Q].G, c->iscratch + kIsAny));
     c->any_ready = one;
     LFE_HIP(hipGetLastError());
   } else if (L.permuted) {
